@@ -1,0 +1,166 @@
+"""ctypes binding of libaqchip.so (include/aqc_hip.h).
+
+The HIP library is the only compute path: if it is missing or no GPU is visible, every
+backend call raises ``AqcError`` -- there is no CPU fallback.
+"""
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libaqchip.so")
+
+OP_DTYPE = np.dtype(
+    [("nq", "<i4"), ("q0", "<i4"), ("q1", "<i4"), ("flags", "<i4"), ("m", "<f8", (32,))], align=True
+)
+assert OP_DTYPE.itemsize == 272
+
+# every symbol declared in include/aqc_hip.h
+EXPORTS = (
+    "aqc_last_error", "aqc_version", "aqc_init", "aqc_finalize", "aqc_timing_enable",
+    "aqc_timing_query", "aqc_timing_reset",
+    "aqc_sv_create", "aqc_sv_destroy", "aqc_sv_reset", "aqc_sv_copy", "aqc_sv_apply",
+    "aqc_sv_amp0", "aqc_sv_z_all", "aqc_sv_get", "aqc_sv_set",
+    "aqc_mps_create", "aqc_mps_destroy", "aqc_mps_set_truncation", "aqc_mps_set_vidal",
+    "aqc_mps_get_vidal", "aqc_mps_get_dims", "aqc_mps_copy", "aqc_mps_apply",
+    "aqc_mps_apply_batch", "aqc_mps_sort", "aqc_mps_sort_batch", "aqc_mps_overlap_zero",
+    "aqc_mps_overlap_zero_batch", "aqc_mps_dot", "aqc_mps_z_all", "aqc_mps_amps_hw1",
+    "aqc_pair_grads", "aqc_pair_grads_batch", "aqc_argmax_scaled", "aqc_mps_jacobi_stats",
+    "aqc_mps_set_jacobi_tol",
+)
+
+
+class AqcError(RuntimeError):
+    pass
+
+
+_lock = threading.Lock()
+_lib = None
+_initialised_device = None
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_D = ctypes.c_double
+_DP = ctypes.POINTER(ctypes.c_double)
+_IP = ctypes.POINTER(ctypes.c_int)
+
+_SIGS = {
+    "aqc_last_error": ([], ctypes.c_char_p),
+    "aqc_version": ([], _I),
+    "aqc_init": ([_I], _I),
+    "aqc_finalize": ([], _I),
+    "aqc_timing_enable": ([_I], _I),
+    "aqc_timing_query": ([ctypes.c_char_p, _DP, ctypes.POINTER(ctypes.c_int64), _DP, _DP], _I),
+    "aqc_timing_reset": ([], _I),
+    "aqc_sv_create": ([_I, ctypes.POINTER(_P)], _I),
+    "aqc_sv_destroy": ([_P], _I),
+    "aqc_sv_reset": ([_P], _I),
+    "aqc_sv_copy": ([_P, _P], _I),
+    "aqc_sv_apply": ([_P, _P, _I], _I),
+    "aqc_sv_amp0": ([_P, _DP, _DP], _I),
+    "aqc_sv_z_all": ([_P, _DP], _I),
+    "aqc_sv_get": ([_P, _P], _I),
+    "aqc_sv_set": ([_P, _P], _I),
+    "aqc_mps_create": ([_I, _I, _D, _I, ctypes.POINTER(_P)], _I),
+    "aqc_mps_destroy": ([_P], _I),
+    "aqc_mps_set_truncation": ([_P, _D, _I], _I),
+    "aqc_mps_set_vidal": ([_P, _P, _P, _P], _I),
+    "aqc_mps_get_vidal": ([_P, _P, _P, _P], _I),
+    "aqc_mps_get_dims": ([_P, _P], _I),
+    "aqc_mps_copy": ([_P, _P], _I),
+    "aqc_mps_apply": ([_P, _P, _I], _I),
+    "aqc_mps_apply_batch": ([_P, _I, _P, _P], _I),
+    "aqc_mps_sort": ([_P], _I),
+    "aqc_mps_sort_batch": ([_P, _I], _I),
+    "aqc_mps_overlap_zero": ([_P, _DP, _DP], _I),
+    "aqc_mps_overlap_zero_batch": ([_P, _I, _P], _I),
+    "aqc_mps_dot": ([_P, _P, _DP, _DP], _I),
+    "aqc_mps_z_all": ([_P, _P], _I),
+    "aqc_mps_amps_hw1": ([_P, _P], _I),
+    "aqc_pair_grads": ([_P, _P, _P, _I, _P, _P, _P, _I, _P, _I], _I),
+    "aqc_pair_grads_batch": ([_P, _I, _P, _P, _I, _P, _P, _P, _I, _P, _I], _I),
+    "aqc_argmax_scaled": ([_P, _P, _I, _I, _IP], _I),
+    "aqc_mps_jacobi_stats": ([_P, _IP], _I),
+    "aqc_mps_set_jacobi_tol": ([_D], _I),
+}
+
+
+def load(path=LIB_PATH):
+    """Load libaqchip.so (does not touch the GPU)."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(path):
+            raise AqcError(
+                f"HIP library not found at {path}; build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+            )
+        lib = ctypes.CDLL(path)
+        for name, (args, res) in _SIGS.items():
+            f = getattr(lib, name)
+            f.argtypes = args
+            f.restype = res
+        _lib = lib
+        return lib
+
+
+def check(rc):
+    if rc != 0:
+        msg = load().aqc_last_error().decode(errors="replace")
+        raise AqcError(f"libaqchip error {rc}: {msg}")
+
+
+def device_index():
+    """Device for this process: LOCAL_RANK when launched one process per GPU."""
+    return int(os.environ.get("AQC_DEVICE", os.environ.get("LOCAL_RANK", "0")))
+
+
+def lib():
+    """The loaded library with this process's device selected (raises without a GPU)."""
+    global _initialised_device
+    l = load()
+    dev = device_index()
+    if _initialised_device != dev:
+        check(l.aqc_init(dev))
+        _initialised_device = dev
+    return l
+
+
+def ptr(a):
+    return ctypes.c_void_p(a.ctypes.data) if a is not None else None
+
+
+def dptr(a):
+    return a.ctypes.data_as(_DP)
+
+
+def ops_array(ops):
+    """[(matrix (2x2 or 4x4 complex), qubits tuple)] -> contiguous aqc_op_t array."""
+    arr = np.zeros(len(ops), dtype=OP_DTYPE)
+    for i, (m, qubits) in enumerate(ops):
+        m = np.asarray(m, dtype=np.complex128)
+        k = len(qubits)
+        arr[i]["nq"] = k
+        arr[i]["q0"] = qubits[0]
+        arr[i]["q1"] = qubits[1] if k == 2 else 0
+        flat = m.reshape(-1)
+        arr[i]["m"][: 2 * flat.size : 2] = flat.real
+        arr[i]["m"][1 : 2 * flat.size : 2] = flat.imag
+    return arr
+
+
+def timing_enable(on=True):
+    check(load().aqc_timing_enable(1 if on else 0))
+
+
+def timing_reset():
+    check(load().aqc_timing_reset())
+
+
+def timing_query(name):
+    ms, b, f = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+    n = ctypes.c_int64()
+    check(load().aqc_timing_query(name.encode(), ctypes.byref(ms), ctypes.byref(n), ctypes.byref(b), ctypes.byref(f)))
+    return {"ms": ms.value, "launches": n.value, "bytes": b.value, "flops": f.value}

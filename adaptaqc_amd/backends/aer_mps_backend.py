@@ -1,0 +1,115 @@
+"""MPS backend on MI355X: drop-in for adaptaqc/backends/aer_mps_backend.py:27-93.
+
+``compiler.full_circuit[0]`` is the ``set_matrix_product_state`` op holding the cached MPS
+(approximate_compiler.py:180-204); it is uploaded once per payload and every evaluation
+replays the remaining gates on a device copy with Aer's MPS semantics, then measures on the
+device (overlap chain, environments) -- no host round trip of the tensors.
+"""
+import logging
+from types import SimpleNamespace
+
+import numpy as np
+
+from ..circuit import device_ops
+from ..device import DeviceMPS
+from ..mps_operations import chi_cap_for, zero_aer_mps
+from .aqc_backend import AQCBackend
+
+logger = logging.getLogger(__name__)
+
+
+class MPSSimulator:
+    """Holds the options the reference reads from ``backend.simulator.options``."""
+
+    def __init__(self, mps_truncation_threshold=1e-16, max_chi=None, mps_log_data=False):
+        self.options = SimpleNamespace(
+            method="matrix_product_state",
+            matrix_product_state_truncation_threshold=mps_truncation_threshold,
+            matrix_product_state_max_bond_dimension=max_chi,
+            mps_log_data=mps_log_data,
+        )
+
+    def __repr__(self):
+        o = self.options
+        return (f"MPSSimulator(threshold={o.matrix_product_state_truncation_threshold}, "
+                f"max_chi={o.matrix_product_state_max_bond_dimension})")
+
+
+def mps_sim_with_args(mps_truncation_threshold=1e-16, max_chi=None, mps_log_data=False):
+    """Reference aer_mps_backend.py:27-42 (same arguments, HIP engine)."""
+    logger.info(f"Using HIP MPS engine with truncation {mps_truncation_threshold}")
+    return MPSSimulator(mps_truncation_threshold, max_chi, mps_log_data)
+
+
+class AerMPSBackend(AQCBackend):
+    def __init__(self, simulator=None):
+        self.simulator = simulator if simulator is not None else mps_sim_with_args()
+        self._base = None  # (payload id, DeviceMPS)
+        self._work = None
+
+    def __getstate__(self):
+        d = dict(self.__dict__)
+        d["_base"] = None
+        d["_work"] = None
+        return d
+
+    def _options(self):
+        o = self.simulator.options
+        return o.matrix_product_state_truncation_threshold, o.matrix_product_state_max_bond_dimension
+
+    def device_state(self, circuit):
+        """Replay ``circuit`` on the device; returns the (sorted) work DeviceMPS."""
+        thr, max_chi = self._options()
+        n = circuit.num_qubits
+        start = 0
+        payload = None
+        if len(circuit.data) and circuit.data[0].operation.name == "set_matrix_product_state":
+            payload = circuit.data[0].operation.params[0]
+            start = 1
+        key = id(payload) if payload is not None else ("zero", n)
+        lmax = max(np.asarray(a).shape[1] for a, _ in payload[0]) if payload is not None else 1
+        cap = chi_cap_for(n, max_chi, lmax)
+        if self._base is None or self._base[0] != key or self._base[2] is not payload or self._base[1].chi_cap != cap:
+            base = DeviceMPS(n, cap, thr, max_chi)
+            base.load_aer(payload if payload is not None else zero_aer_mps(n))
+            self._base = (key, base, payload)
+            self._work = DeviceMPS(n, cap, thr, max_chi)
+        work = self._work
+        work.set_truncation(thr, max_chi)
+        work.copy_from(self._base[1])
+        work.apply(device_ops(circuit, start))
+        work.sort()
+        return work
+
+    def evaluate_global_cost(self, compiler):
+        psi = self.device_state(compiler.full_circuit)
+        global_cost = 1 - np.absolute(psi.overlap_zero()) ** 2
+        if not compiler.soften_global_cost:
+            return global_cost
+        previous_cost = compiler.global_cost_history[-1] if len(compiler.global_cost_history) > 0 else 1
+        alpha = abs(previous_cost - compiler.adapt_config.sufficient_cost)
+        return global_cost - alpha * sum(self.evaluate_hamming_weight_one_overlaps(psi))
+
+    def evaluate_local_cost(self, compiler):
+        evals = self.measure_qubit_expectation_values(compiler)
+        return 0.5 * (1 - np.mean(evals))
+
+    def evaluate_circuit(self, compiler):
+        """Preprocessed MPS (list of (2, chi_l, chi_r) arrays), as the reference returns."""
+        return self.device_state(compiler.full_circuit).preprocessed()
+
+    def measure_qubit_expectation_values(self, compiler):
+        psi = self.device_state(compiler.full_circuit)
+        return [float(x) for x in psi.z_all()]
+
+    def evaluate_hamming_weight_one_overlaps(self, mps):
+        if isinstance(mps, DeviceMPS):
+            amps = mps.amps_hw1()
+        else:
+            from ..mps_operations import _as_device
+
+            amps = _as_device(mps, True).amps_hw1()
+        return [float(abs(a) ** 2) for a in amps]
+
+
+HipMPSBackend = AerMPSBackend

@@ -1,0 +1,296 @@
+"""Minimal quantum-circuit IR standing in for the parts of ``qiskit.QuantumCircuit`` that the
+hot path touches (qiskit is not a dependency here).
+
+Mirrors the attribute shapes the reference code reads: ``circuit.data[i].operation.name /
+.params / .label``, ``circuit.data[i].qubits``, ``num_qubits``, ``copy()``, ``inverse()``,
+``compose(other, qubits)`` and ``set_matrix_product_state(mps)``
+(approximate_compiler.py:180-204).  Qubits are plain integers (little-endian: qubit 0 is the
+least significant bit of a statevector index).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import gates as G
+
+ONE_Q = set(G.CONST_1Q) | {"rx", "ry", "rz", "p", "u1", "u", "u3", "u2"}
+TWO_Q = set(G.TWO_QUBIT) | {"crx", "cry", "crz", "cp", "cu1", "rzz"}
+_SELF_INVERSE = {"id", "x", "y", "z", "h", "cx", "cy", "cz", "swap", "ccx"}
+_INVERSE_NAME = {"s": "sdg", "sdg": "s", "t": "tdg", "tdg": "t", "sx": "sxdg", "sxdg": "sx"}
+_PARAM_NEGATE = {"rx", "ry", "rz", "p", "u1", "crx", "cry", "crz", "cp", "cu1", "rzz"}
+
+
+class Operation:
+    """A named gate (``qiskit.circuit.Gate`` stand-in)."""
+
+    __slots__ = ("name", "params", "label", "num_qubits")
+
+    def __init__(self, name, num_qubits, params=(), label=None):
+        self.name = name
+        self.num_qubits = num_qubits
+        self.params = list(params)
+        self.label = label
+
+    def copy(self):
+        return Operation(self.name, self.num_qubits, list(self.params), self.label)
+
+    def to_matrix(self):
+        if self.name == "unitary":
+            return np.asarray(self.params[0], dtype=complex)
+        if self.num_qubits == 1:
+            return G.one_qubit(self.name, self.params)
+        if self.num_qubits == 2:
+            return G.two_qubit(self.name, self.params)
+        raise ValueError(f"no matrix for {self.name}")
+
+    def inverse(self):
+        if self.name in _SELF_INVERSE:
+            return self.copy()
+        if self.name in _INVERSE_NAME:
+            return Operation(_INVERSE_NAME[self.name], self.num_qubits, (), self.label)
+        if self.name in _PARAM_NEGATE:
+            return Operation(self.name, self.num_qubits, [-p for p in self.params], self.label)
+        if self.name in ("u", "u3"):
+            t, ph, lam = self.params
+            return Operation(self.name, 1, [-t, -lam, -ph], self.label)
+        if self.name == "u2":
+            ph, lam = self.params
+            return Operation("u3", 1, [-np.pi / 2, -lam, -ph], self.label)
+        if self.name == "unitary":
+            return Operation("unitary", self.num_qubits, [np.conj(np.asarray(self.params[0])).T], self.label)
+        raise ValueError(f"cannot invert {self.name}")
+
+    def _key(self):
+        ps = []
+        for p in self.params:
+            if isinstance(p, np.ndarray):
+                ps.append(("arr", p.shape, p.tobytes()))
+            elif isinstance(p, tuple) and self.name == "set_matrix_product_state":
+                ps.append(("mps", id(p)))
+            else:
+                ps.append(float(p) if np.isscalar(p) else p)
+        return (self.name, tuple(ps))
+
+    def __eq__(self, other):
+        return isinstance(other, Operation) and self._key() == other._key()
+
+    def __repr__(self):
+        return f"Operation({self.name!r}, params={self.params})"
+
+
+class CircuitInstruction:
+    __slots__ = ("operation", "qubits", "clbits")
+
+    def __init__(self, operation, qubits, clbits=()):
+        self.operation = operation
+        self.qubits = tuple(int(q) for q in qubits)
+        self.clbits = tuple(clbits)
+
+    def copy(self):
+        return CircuitInstruction(self.operation.copy(), self.qubits, self.clbits)
+
+    def __eq__(self, other):
+        return (
+            isinstance(other, CircuitInstruction)
+            and self.qubits == other.qubits
+            and self.operation == other.operation
+        )
+
+    def __iter__(self):  # legacy (instr, qargs, cargs) unpacking
+        return iter((self.operation, self.qubits, self.clbits))
+
+
+class QuantumCircuit:
+    def __init__(self, num_qubits: int):
+        self.num_qubits = int(num_qubits)
+        self.data: list[CircuitInstruction] = []
+
+    # -- construction ------------------------------------------------------------------
+    def append(self, operation, qubits):
+        qubits = tuple(int(q) for q in (qubits if np.iterable(qubits) else [qubits]))
+        for q in qubits:
+            if not 0 <= q < self.num_qubits:
+                raise IndexError(f"qubit {q} out of range for {self.num_qubits}-qubit circuit")
+        if len(set(qubits)) != len(qubits):
+            raise ValueError("duplicate qubit arguments")
+        self.data.append(CircuitInstruction(operation, qubits))
+        return self
+
+    def _g1(self, name, qubit, params=(), label=None):
+        for q in (qubit if np.iterable(qubit) else [qubit]):
+            self.append(Operation(name, 1, params, label), [q])
+        return self
+
+    def rx(self, theta, q):
+        return self._g1("rx", q, [theta])
+
+    def ry(self, theta, q):
+        return self._g1("ry", q, [theta])
+
+    def rz(self, theta, q):
+        return self._g1("rz", q, [theta])
+
+    def p(self, lam, q):
+        return self._g1("p", q, [lam])
+
+    def u(self, theta, phi, lam, q):
+        return self._g1("u", q, [theta, phi, lam])
+
+    def x(self, q):
+        return self._g1("x", q)
+
+    def y(self, q):
+        return self._g1("y", q)
+
+    def z(self, q):
+        return self._g1("z", q)
+
+    def h(self, q):
+        return self._g1("h", q)
+
+    def s(self, q):
+        return self._g1("s", q)
+
+    def sdg(self, q):
+        return self._g1("sdg", q)
+
+    def t(self, q):
+        return self._g1("t", q)
+
+    def tdg(self, q):
+        return self._g1("tdg", q)
+
+    def sx(self, q):
+        return self._g1("sx", q)
+
+    def id(self, q):
+        return self._g1("id", q)
+
+    def cx(self, c, t):
+        return self.append(Operation("cx", 2), [c, t])
+
+    def cy(self, c, t):
+        return self.append(Operation("cy", 2), [c, t])
+
+    def cz(self, c, t):
+        return self.append(Operation("cz", 2), [c, t])
+
+    def swap(self, a, b):
+        return self.append(Operation("swap", 2), [a, b])
+
+    def crz(self, theta, c, t):
+        return self.append(Operation("crz", 2, [theta]), [c, t])
+
+    def rzz(self, theta, a, b):
+        return self.append(Operation("rzz", 2, [theta]), [a, b])
+
+    def ccx(self, a, b, c):
+        return self.append(Operation("ccx", 3), [a, b, c])
+
+    def unitary(self, matrix, qubits, label=None):
+        qubits = list(qubits) if np.iterable(qubits) else [qubits]
+        m = np.asarray(matrix, dtype=complex)
+        if m.shape != (2 ** len(qubits),) * 2:
+            raise ValueError("unitary shape does not match qubit count")
+        return self.append(Operation("unitary", len(qubits), [m], label), qubits)
+
+    def set_matrix_product_state(self, mps):
+        """Embed an Aer-format MPS (list[(G0, G1)], list[lambda]) as the initial state."""
+        gam, lam = mps
+        if len(gam) != self.num_qubits:
+            raise ValueError("MPS size does not match the circuit")
+        op = Operation("set_matrix_product_state", self.num_qubits, [mps])
+        self.data.append(CircuitInstruction(op, range(self.num_qubits)))
+        return self
+
+    def barrier(self, *args):
+        return self
+
+    # -- container protocol ------------------------------------------------------------
+    def __len__(self):
+        return len(self.data)
+
+    def __iter__(self):
+        return iter(self.data)
+
+    def __getitem__(self, i):
+        return self.data[i]
+
+    def __eq__(self, other):
+        return (
+            isinstance(other, QuantumCircuit)
+            and self.num_qubits == other.num_qubits
+            and len(self.data) == len(other.data)
+            and all(a == b for a, b in zip(self.data, other.data))
+        )
+
+    def __repr__(self):
+        body = ", ".join(f"{i.operation.name}{list(i.qubits)}" for i in self.data[:12])
+        more = "" if len(self.data) <= 12 else f", ... (+{len(self.data) - 12})"
+        return f"QuantumCircuit({self.num_qubits}: {body}{more})"
+
+    def copy(self):
+        qc = QuantumCircuit(self.num_qubits)
+        qc.data = [i.copy() for i in self.data]
+        return qc
+
+    def inverse(self):
+        qc = QuantumCircuit(self.num_qubits)
+        for ins in reversed(self.data):
+            if ins.operation.name == "set_matrix_product_state":
+                raise ValueError("cannot invert a circuit holding an MPS state")
+            qc.data.append(CircuitInstruction(ins.operation.inverse(), ins.qubits))
+        return qc
+
+    def compose(self, other, qubits=None):
+        """Return self followed by ``other`` mapped onto ``qubits`` (qiskit semantics)."""
+        qc = self.copy()
+        mapping = list(range(other.num_qubits)) if qubits is None else list(qubits)
+        for ins in other.data:
+            qc.data.append(CircuitInstruction(ins.operation.copy(), [mapping[q] for q in ins.qubits]))
+        return qc
+
+    def count_ops(self):
+        out = {}
+        for ins in self.data:
+            out[ins.operation.name] = out.get(ins.operation.name, 0) + 1
+        return out
+
+    def depth(self, filter_function=None):
+        level = [0] * self.num_qubits
+        for ins in self.data:
+            if filter_function is not None and not filter_function(ins):
+                continue
+            d = max(level[q] for q in ins.qubits) + 1
+            for q in ins.qubits:
+                level[q] = d
+        return max(level) if level else 0
+
+
+def decompose(ins: CircuitInstruction):
+    """Yield (matrix, qubits) 1-/2-qubit pieces of an instruction (unroll_to_basis_gates)."""
+    op, q = ins.operation, ins.qubits
+    name = op.name
+    if name in ("barrier", "measure", "id"):
+        return
+    if name == "ccx":
+        a, b, c = q
+        seq = [("h", (c,)), ("cx", (b, c)), ("tdg", (c,)), ("cx", (a, c)), ("t", (c,)), ("cx", (b, c)),
+               ("tdg", (c,)), ("cx", (a, c)), ("t", (b,)), ("t", (c,)), ("h", (c,)), ("cx", (a, b)),
+               ("t", (a,)), ("tdg", (b,)), ("cx", (a, b))]
+        for nm, qq in seq:
+            yield (G.one_qubit(nm) if len(qq) == 1 else G.two_qubit(nm)), qq
+        return
+    if op.num_qubits > 2:
+        raise ValueError(f"gate {name} on {op.num_qubits} qubits is not supported")
+    yield op.to_matrix(), q
+
+
+def device_ops(circuit: QuantumCircuit, start: int = 0):
+    """Flatten gates from ``circuit.data[start:]`` into (matrix, qubits) pairs."""
+    out = []
+    for ins in circuit.data[start:]:
+        if ins.operation.name == "set_matrix_product_state":
+            raise ValueError("set_matrix_product_state must be the first instruction")
+        out.extend(decompose(ins))
+    return out

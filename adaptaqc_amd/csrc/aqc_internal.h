@@ -1,0 +1,79 @@
+// Internal helpers shared by the libaqchip translation units (gfx950 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <string>
+#include <vector>
+
+#include "../../include/aqc_hip.h"
+
+namespace aqc {
+
+void set_error(const std::string& msg);
+
+#define AQC_HIP_CHECK(expr)                                                              \
+  do {                                                                                   \
+    hipError_t _e = (expr);                                                              \
+    if (_e != hipSuccess) {                                                              \
+      ::aqc::set_error(std::string(#expr) + ": " + hipGetErrorString(_e));               \
+      return AQC_ERR_HIP;                                                                \
+    }                                                                                    \
+  } while (0)
+
+#define AQC_CHECK_LAUNCH()                                                               \
+  do {                                                                                   \
+    hipError_t _e = hipGetLastError();                                                   \
+    if (_e != hipSuccess) {                                                              \
+      ::aqc::set_error(std::string("kernel launch: ") + hipGetErrorString(_e));          \
+      return AQC_ERR_HIP;                                                                \
+    }                                                                                    \
+  } while (0)
+
+#define AQC_REQUIRE(cond, msg)                                                           \
+  do {                                                                                   \
+    if (!(cond)) {                                                                       \
+      ::aqc::set_error(msg);                                                             \
+      return AQC_ERR_ARG;                                                                \
+    }                                                                                    \
+  } while (0)
+
+// ---- complex double helpers ----------------------------------------------------------
+typedef double2 cplx;
+
+__host__ __device__ __forceinline__ cplx cmk(double r, double i) { return make_double2(r, i); }
+__host__ __device__ __forceinline__ cplx cadd(cplx a, cplx b) { return cmk(a.x + b.x, a.y + b.y); }
+__host__ __device__ __forceinline__ cplx csub(cplx a, cplx b) { return cmk(a.x - b.x, a.y - b.y); }
+__host__ __device__ __forceinline__ cplx cmul(cplx a, cplx b) {
+  return cmk(fma(a.x, b.x, -a.y * b.y), fma(a.x, b.y, a.y * b.x));
+}
+// a * conj(b)
+__host__ __device__ __forceinline__ cplx cmulc(cplx a, cplx b) {
+  return cmk(fma(a.x, b.x, a.y * b.y), fma(a.y, b.x, -a.x * b.y));
+}
+// conj(a) * b
+__host__ __device__ __forceinline__ cplx cconjmul(cplx a, cplx b) {
+  return cmk(fma(a.x, b.x, a.y * b.y), fma(a.x, b.y, -a.y * b.x));
+}
+// acc += a*b
+__host__ __device__ __forceinline__ cplx cfma(cplx a, cplx b, cplx acc) {
+  return cmk(fma(a.x, b.x, fma(-a.y, b.y, acc.x)), fma(a.x, b.y, fma(a.y, b.x, acc.y)));
+}
+// acc += conj(a)*b
+__host__ __device__ __forceinline__ cplx cfmac(cplx a, cplx b, cplx acc) {
+  return cmk(fma(a.x, b.x, fma(a.y, b.y, acc.x)), fma(a.x, b.y, fma(-a.y, b.x, acc.y)));
+}
+__host__ __device__ __forceinline__ cplx cscale(cplx a, double s) { return cmk(a.x * s, a.y * s); }
+__host__ __device__ __forceinline__ cplx cconj(cplx a) { return cmk(a.x, -a.y); }
+__host__ __device__ __forceinline__ double cnorm2(cplx a) { return fma(a.x, a.x, a.y * a.y); }
+
+// ---- kernel timing (HIP events on the launching stream) ------------------------------
+struct KernelTimer {
+  // Begin/End bracket one launch on `stream` when timing is enabled.
+  static void begin(hipStream_t stream, const char* family, double bytes, double flops);
+  static void end(hipStream_t stream);
+};
+
+}  // namespace aqc

@@ -1,0 +1,417 @@
+// Candidate sweep: replaces adaptaqc/utils/gradients.py:23-124 (general_grad_of_pairs).
+//
+// The reference builds, for every coupling-map pair (c, t) and every generator G_k, the MPS of
+// G_k^dag|s> through Aer and takes a whole-psi dot.  With a product starting state |s> every
+// such overlap factorises through a 4-vector per pair:
+//   T_ab[sa, sb] = <s_{not a,b}, sa sb | psi>,   <s|O|psi> = sum (s_c (x) s_t)^dag O T_ct,
+// so one sweep over psi yields every pair's overlaps:
+//   M_i = sum_s conj(s_i[s]) A_i[s]            (k_sweep_M)
+//   l_b = M_0 .. M_{b-1},  r_b = M_b .. M_{n-1}  (k_sweep_lr)
+//   w_b[s] = A_b[s] r_{b+1},  v_a[s] = l_a A_a[s] (k_sweep_w)
+//   for each a: T_ab = v . w_b, v <- v M_b      (k_sweep_chain, one workgroup per a)
+//   g_p = sqrt(sum_k deg_k (-Im(<s|G_k|psi> <psi|U0^dag|s>))^2)  (k_sweep_grad)
+// Work per state: sum_a (n-a) vector-matrix products, O(n^2 chi^2), instead of the reference's
+// O(n^2 * n_gen) MPS builds and O(n^3 chi^2 n_gen) dot work.
+#include <algorithm>
+#include <cstring>
+
+#include "mps_internal.h"
+
+using aqc::cplx;
+
+namespace {
+
+constexpr int kT = 256;
+
+struct SweepJob {
+  const cplx* gam;
+  const double* lam;
+  const int* dims;
+  int n;
+  int cap;
+  cplx* M;      // n * cap * cap
+  cplx* lv;     // (n+1) * cap
+  cplx* rv;     // (n+1) * cap
+  cplx* w;      // n * 2 * cap
+  cplx* v0;     // n * 2 * cap
+  cplx* T;      // n * n * 4
+  double* out;  // npairs
+};
+
+struct SweepConst {
+  int npairs;
+  int ngen;
+  const int* pairs;      // 2 * npairs
+  const cplx* svec;      // n * 2
+  const cplx* u0;        // 16
+  const cplx* gens;      // ngen * 16
+  const double* degs;    // ngen
+};
+
+__device__ __forceinline__ cplx site_a(const SweepJob& j, int i, int s, int l, int r) {
+  const size_t ss = (size_t)2 * j.cap * j.cap;
+  return aqc::cscale(j.gam[(size_t)i * ss + (size_t)s * j.cap * j.cap + (size_t)l * j.cap + r],
+                     j.lam[(size_t)(i + 1) * j.cap + r]);
+}
+
+// blockIdx.x: site, blockIdx.y: job
+__global__ __launch_bounds__(kT) void k_sweep_M(const SweepJob* __restrict__ jobs, const cplx* __restrict__ svec) {
+  const SweepJob& j = jobs[blockIdx.y];
+  const int i = blockIdx.x;
+  const int cl = j.dims[i], cr = j.dims[i + 1];
+  const cplx s0 = aqc::cconj(svec[2 * i]), s1 = aqc::cconj(svec[2 * i + 1]);
+  cplx* Mi = j.M + (size_t)i * j.cap * j.cap;
+  for (int e = threadIdx.x; e < cl * cr; e += kT) {
+    const int l = e / cr, r = e % cr;
+    Mi[(size_t)l * j.cap + r] = aqc::cfma(s1, site_a(j, i, 1, l, r), aqc::cmul(s0, site_a(j, i, 0, l, r)));
+  }
+}
+
+// blockIdx.x: job, blockIdx.y: 0 left / 1 right
+__global__ __launch_bounds__(kT) void k_sweep_lr(const SweepJob* __restrict__ jobs) {
+  const SweepJob& j = jobs[blockIdx.x];
+  const int cap = j.cap, n = j.n;
+  const int tid = threadIdx.x;
+  if (blockIdx.y == 0) {
+    if (tid == 0) j.lv[0] = aqc::cmk(1, 0);
+    __syncthreads();
+    for (int i = 0; i < n; ++i) {
+      const int cl = j.dims[i], cr = j.dims[i + 1];
+      const cplx* Mi = j.M + (size_t)i * cap * cap;
+      for (int r = tid; r < cr; r += kT) {
+        cplx acc = aqc::cmk(0, 0);
+        for (int l = 0; l < cl; ++l) acc = aqc::cfma(j.lv[(size_t)i * cap + l], Mi[(size_t)l * cap + r], acc);
+        j.lv[(size_t)(i + 1) * cap + r] = acc;
+      }
+      __syncthreads();
+    }
+  } else {
+    if (tid == 0) j.rv[(size_t)n * cap] = aqc::cmk(1, 0);
+    __syncthreads();
+    for (int i = n - 1; i >= 0; --i) {
+      const int cl = j.dims[i], cr = j.dims[i + 1];
+      const cplx* Mi = j.M + (size_t)i * cap * cap;
+      for (int l = tid; l < cl; l += kT) {
+        cplx acc = aqc::cmk(0, 0);
+        for (int r = 0; r < cr; ++r) acc = aqc::cfma(Mi[(size_t)l * cap + r], j.rv[(size_t)(i + 1) * cap + r], acc);
+        j.rv[(size_t)i * cap + l] = acc;
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// blockIdx.x: site, blockIdx.y: job.  w_b[s][l] = sum_r A_b[s][l][r] rv[b+1][r];
+// v0_a[s][r] = sum_l lv[a][l] A_a[s][l][r].
+__global__ __launch_bounds__(kT) void k_sweep_w(const SweepJob* __restrict__ jobs) {
+  const SweepJob& j = jobs[blockIdx.y];
+  const int i = blockIdx.x, cap = j.cap;
+  const int cl = j.dims[i], cr = j.dims[i + 1];
+  for (int e = threadIdx.x; e < 2 * cl; e += kT) {
+    const int s = e / cl, l = e % cl;
+    cplx acc = aqc::cmk(0, 0);
+    for (int r = 0; r < cr; ++r) acc = aqc::cfma(site_a(j, i, s, l, r), j.rv[(size_t)(i + 1) * cap + r], acc);
+    j.w[((size_t)i * 2 + s) * cap + l] = acc;
+  }
+  for (int e = threadIdx.x; e < 2 * cr; e += kT) {
+    const int s = e / cr, r = e % cr;
+    cplx acc = aqc::cmk(0, 0);
+    for (int l = 0; l < cl; ++l) acc = aqc::cfma(j.lv[(size_t)i * cap + l], site_a(j, i, s, l, r), acc);
+    j.v0[((size_t)i * 2 + s) * cap + r] = acc;
+  }
+}
+
+// One workgroup per (a, job): propagate the two row vectors v[sa] through M_b, emitting T_ab.
+__global__ __launch_bounds__(kT) void k_sweep_chain(const SweepJob* __restrict__ jobs, const int* __restrict__ alist) {
+  const SweepJob& j = jobs[blockIdx.y];
+  const int a = alist[blockIdx.x];
+  const int n = j.n, cap = j.cap;
+  if (a >= n - 1) return;
+  __shared__ cplx v[2][2][256];
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6, lane = tid & 63;
+  const int d0 = j.dims[a + 1];
+  for (int e = tid; e < 2 * d0; e += kT) v[0][e / d0][e % d0] = j.v0[((size_t)a * 2 + e / d0) * cap + e % d0];
+  __syncthreads();
+  int cur = 0;
+  for (int b = a + 1; b < n; ++b) {
+    const int db = j.dims[b], dn = j.dims[b + 1];
+    // T_ab[sa][sb] = sum_k v[sa][k] w_b[sb][k] : wave w -> (sa, sb) = (w >> 1, w & 1)
+    {
+      const int sa = wave >> 1, sb = wave & 1;
+      const cplx* wb = j.w + ((size_t)b * 2 + sb) * cap;
+      cplx acc = aqc::cmk(0, 0);
+      for (int k = lane; k < db; k += 64) acc = aqc::cfma(v[cur][sa][k], wb[k], acc);
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) {
+        acc.x += __shfl_xor(acc.x, off);
+        acc.y += __shfl_xor(acc.y, off);
+      }
+      if (lane == 0) j.T[((size_t)a * n + b) * 4 + wave] = acc;
+    }
+    if (b == n - 1) break;
+    // v[s] <- v[s] M_b
+    const cplx* Mb = j.M + (size_t)b * cap * cap;
+    for (int e = tid; e < 2 * dn; e += kT) {
+      const int s = e / dn, r = e % dn;
+      cplx acc = aqc::cmk(0, 0);
+      for (int k = 0; k < db; ++k) acc = aqc::cfma(v[cur][s][k], Mb[(size_t)k * cap + r], acc);
+      v[cur ^ 1][s][r] = acc;
+    }
+    __syncthreads();
+    cur ^= 1;
+  }
+}
+
+// One thread per pair.
+__global__ void k_sweep_grad(const SweepJob* __restrict__ jobs, SweepConst c) {
+  const SweepJob& j = jobs[blockIdx.y];
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= c.npairs) return;
+  const int qc = c.pairs[2 * p], qt = c.pairs[2 * p + 1];
+  const int a = qc < qt ? qc : qt, b = qc < qt ? qt : qc;
+  const cplx* tab = j.T + ((size_t)a * j.n + b) * 4;  // [sa][sb]
+  cplx vec[4];  // little-endian over (c, t): index 2*st + sc
+#pragma unroll
+  for (int sa = 0; sa < 2; ++sa)
+#pragma unroll
+    for (int sb = 0; sb < 2; ++sb) {
+      const int sc = qc == a ? sa : sb, st = qc == a ? sb : sa;
+      vec[2 * st + sc] = tab[2 * sa + sb];
+    }
+  cplx s4[4];
+#pragma unroll
+  for (int x = 0; x < 4; ++x) s4[x] = aqc::cconj(aqc::cmul(c.svec[2 * qt + (x >> 1)], c.svec[2 * qc + (x & 1)]));
+  auto bra_op_ket = [&](const cplx* O) {
+    cplx acc = aqc::cmk(0, 0);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      cplx ov = aqc::cmk(0, 0);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) ov = aqc::cfma(O[4 * r + k], vec[k], ov);
+      acc = aqc::cfma(s4[r], ov, acc);
+    }
+    return acc;
+  };
+  const cplx z = aqc::cconj(bra_op_ket(c.u0));  // <psi|U0^dag|s>
+  double g = 0.0;
+  for (int k = 0; k < c.ngen; ++k) {
+    const cplx ov = bra_op_ket(c.gens + 16 * k);  // <s|G_k|psi>
+    const double gg = -aqc::cmul(ov, z).y;
+    g += gg * gg * c.degs[k];
+  }
+  j.out[(size_t)blockIdx.y * 0 + p] = sqrt(g);
+}
+
+__global__ void k_argmax(const double* s, const double* prio, int count, int* best) {
+  __shared__ double bv[256];
+  __shared__ int bi[256];
+  double v = -1.0 / 0.0;
+  int idx = 0x7fffffff;
+  for (int i = threadIdx.x; i < count; i += blockDim.x) {
+    const double x = s[i] * prio[i];
+    if (x > v || (x == v && i < idx) || (x != x && v == v)) {  // NaN wins like np.argmax
+      v = x;
+      idx = i;
+    }
+  }
+  bv[threadIdx.x] = v;
+  bi[threadIdx.x] = idx;
+  __syncthreads();
+  for (int st = blockDim.x / 2; st > 0; st >>= 1) {
+    if (threadIdx.x < st) {
+      const double o = bv[threadIdx.x + st];
+      const int oi = bi[threadIdx.x + st];
+      const double m = bv[threadIdx.x];
+      const int mi = bi[threadIdx.x];
+      const bool on = o != o, mn = m != m;
+      bool take;
+      if (on || mn) take = on && (!mn || oi < mi);
+      else take = (o > m) || (o == m && oi < mi);
+      if (take) {
+        bv[threadIdx.x] = o;
+        bi[threadIdx.x] = oi;
+      }
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *best = bi[0];
+}
+
+struct GradBuffers {
+  void* dev = nullptr;
+  size_t cap = 0;
+};
+
+GradBuffers& gbuf() {
+  static GradBuffers g[64];
+  int dev = 0;
+  hipGetDevice(&dev);
+  return g[dev];
+}
+
+int ensure_gw(aqc_mps_t h) {
+  const size_t cap = h->d.cap, n = h->d.n;
+  const size_t need = (n * cap * cap + 2 * (n + 1) * cap + 4 * n * cap + n * n * 4) * sizeof(cplx);
+  if (h->gw_bytes >= need) return AQC_OK;
+  if (h->gw) hipFree(h->gw);
+  AQC_HIP_CHECK(hipMalloc(&h->gw, need));
+  h->gw_bytes = need;
+  return AQC_OK;
+}
+
+SweepJob make_job(aqc_mps_t h, double* out) {
+  SweepJob j;
+  const size_t cap = h->d.cap, n = h->d.n;
+  j.gam = h->d.gam;
+  j.lam = h->d.lam;
+  j.dims = h->d.dims;
+  j.n = (int)n;
+  j.cap = (int)cap;
+  cplx* p = h->gw;
+  j.M = p;
+  p += n * cap * cap;
+  j.lv = p;
+  p += (n + 1) * cap;
+  j.rv = p;
+  p += (n + 1) * cap;
+  j.w = p;
+  p += 2 * n * cap;
+  j.v0 = p;
+  p += 2 * n * cap;
+  j.T = p;
+  j.out = out;
+  return j;
+}
+
+}  // namespace
+
+extern "C" {
+
+int aqc_pair_grads_batch(aqc_mps_t* psis, int ns, const double* svec, const int* pairs, int npairs,
+                         const double* u0, const double* gens, const double* degs, int ngen, double* out,
+                         int out_is_device) {
+  AQC_REQUIRE(psis && ns > 0 && svec && pairs && u0 && out && npairs >= 0 && ngen >= 0,
+              "aqc_pair_grads_batch: bad arguments");
+  AQC_REQUIRE(ngen == 0 || (gens && degs), "aqc_pair_grads_batch: null generators");
+  const int n = psis[0]->d.n;
+  for (int s = 0; s < ns; ++s) AQC_REQUIRE(psis[s] && psis[s]->d.n == n, "aqc_pair_grads_batch: all states need n qubits");
+  for (int p = 0; p < npairs; ++p) {
+    const int a = pairs[2 * p], b = pairs[2 * p + 1];
+    AQC_REQUIRE(a >= 0 && a < n && b >= 0 && b < n && a != b, "aqc_pair_grads_batch: bad pair");
+  }
+  int rc = aqc_mps_sort_batch(psis, ns);
+  if (rc != AQC_OK) return rc;
+  for (int s = 0; s < ns; ++s) {
+    rc = ensure_gw(psis[s]);
+    if (rc != AQC_OK) return rc;
+  }
+  hipStream_t st = aqc::mps_stream();
+  // constants + jobs + (host-out) result buffer in one device allocation
+  const size_t jb = ns * sizeof(SweepJob);
+  // chains are needed only for the first qubits present in `pairs` (pair sharding across ranks)
+  std::vector<int> alist;
+  {
+    std::vector<char> need(n, 0);
+    for (int p = 0; p < npairs; ++p) need[std::min(pairs[2 * p], pairs[2 * p + 1])] = 1;
+    for (int a = 0; a < n - 1; ++a)
+      if (need[a]) alist.push_back(a);
+  }
+  const size_t cb = (alist.size() + 4) * sizeof(int) + 2 * npairs * sizeof(int) + 2 * n * sizeof(cplx) + 16 * sizeof(cplx) +
+                    16 * (size_t)ngen * sizeof(cplx) + ngen * sizeof(double) + 256;
+  const size_t ob = out_is_device ? 0 : (size_t)ns * npairs * sizeof(double);
+  GradBuffers& gb = gbuf();
+  AQC_HIP_CHECK(hipStreamSynchronize(st));
+  const size_t need = jb + cb + ob + 1024;
+  if (need > gb.cap) {
+    if (gb.dev) hipFree(gb.dev);
+    gb.cap = std::max(need, 2 * gb.cap);
+    AQC_HIP_CHECK(hipMalloc(&gb.dev, gb.cap));
+  }
+  char* base = (char*)gb.dev;
+  SweepJob* djobs = (SweepJob*)base;
+  char* cptr = base + ((jb + 255) / 256) * 256;
+  int* dpairs = (int*)cptr;
+  cplx* dsvec = (cplx*)(cptr + ((2 * npairs * sizeof(int) + 15) / 16) * 16);
+  cplx* du0 = dsvec + 2 * n;
+  cplx* dgens = du0 + 16;
+  double* ddegs = (double*)(dgens + 16 * (size_t)ngen);
+  int* dalist = (int*)(ddegs + ngen);
+  double* dout = out_is_device ? out : (double*)(((uintptr_t)(dalist + alist.size() + 4) + 255) & ~(uintptr_t)255);
+  std::vector<SweepJob> jobs(ns);
+  for (int s = 0; s < ns; ++s) jobs[s] = make_job(psis[s], dout + (size_t)s * npairs);
+  AQC_HIP_CHECK(hipMemcpy(djobs, jobs.data(), jb, hipMemcpyHostToDevice));
+  if (npairs) AQC_HIP_CHECK(hipMemcpy(dpairs, pairs, 2 * npairs * sizeof(int), hipMemcpyHostToDevice));
+  AQC_HIP_CHECK(hipMemcpy(dsvec, svec, 2 * n * sizeof(cplx), hipMemcpyHostToDevice));
+  AQC_HIP_CHECK(hipMemcpy(du0, u0, 16 * sizeof(cplx), hipMemcpyHostToDevice));
+  if (!alist.empty()) AQC_HIP_CHECK(hipMemcpy(dalist, alist.data(), alist.size() * sizeof(int), hipMemcpyHostToDevice));
+  if (ngen) {
+    AQC_HIP_CHECK(hipMemcpy(dgens, gens, 16 * (size_t)ngen * sizeof(cplx), hipMemcpyHostToDevice));
+    AQC_HIP_CHECK(hipMemcpy(ddegs, degs, ngen * sizeof(double), hipMemcpyHostToDevice));
+  }
+  const int cap = psis[0]->d.cap;
+  hipLaunchKernelGGL(k_sweep_M, dim3(n, ns), dim3(kT), 0, st, djobs, dsvec);
+  AQC_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_sweep_lr, dim3(ns, 2), dim3(kT), 0, st, djobs);
+  AQC_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_sweep_w, dim3(n, ns), dim3(kT), 0, st, djobs);
+  AQC_CHECK_LAUNCH();
+  {
+    // algorithmic work of the chain: sum_a (n-a-1) steps of a 2 x chi x chi complex vec-mat
+    const double c = cap;
+    double steps = 0.0;
+    for (int a : alist) steps += (double)(n - 1 - a);
+    if (!alist.empty()) {
+      aqc::KernelTimer::begin(st, "grad_chain", ns * steps * c * c * 16.0, ns * steps * 2.0 * c * c * 8.0);
+      hipLaunchKernelGGL(k_sweep_chain, dim3((unsigned)alist.size(), ns), dim3(kT), 0, st, djobs, dalist);
+      aqc::KernelTimer::end(st);
+      AQC_CHECK_LAUNCH();
+    }
+  }
+  if (npairs) {
+    SweepConst c;
+    c.npairs = npairs;
+    c.ngen = ngen;
+    c.pairs = dpairs;
+    c.svec = dsvec;
+    c.u0 = du0;
+    c.gens = dgens;
+    c.degs = ddegs;
+    hipLaunchKernelGGL(k_sweep_grad, dim3((npairs + 127) / 128, ns), dim3(128), 0, st, djobs, c);
+    AQC_CHECK_LAUNCH();
+  }
+  if (!out_is_device && npairs) {
+    AQC_HIP_CHECK(hipMemcpyAsync(out, dout, (size_t)ns * npairs * sizeof(double), hipMemcpyDeviceToHost, st));
+  }
+  AQC_HIP_CHECK(hipStreamSynchronize(st));
+  return AQC_OK;
+}
+
+int aqc_pair_grads(aqc_mps_t psi, const double* svec, const int* pairs, int npairs, const double* u0,
+                   const double* gens, const double* degs, int ngen, double* out, int out_is_device) {
+  return aqc_pair_grads_batch(&psi, 1, svec, pairs, npairs, u0, gens, degs, ngen, out, out_is_device);
+}
+
+int aqc_argmax_scaled(const double* scores, const double* prio, int count, int scores_is_device, int* best) {
+  AQC_REQUIRE(scores && prio && best && count > 0, "aqc_argmax_scaled: bad arguments");
+  hipStream_t st = aqc::mps_stream();
+  double* ds = nullptr;
+  double* dp = nullptr;
+  int* db = nullptr;
+  AQC_HIP_CHECK(hipMalloc(&dp, count * sizeof(double) + sizeof(int) * 4));
+  db = (int*)(dp + count);
+  if (!scores_is_device) {
+    AQC_HIP_CHECK(hipMalloc(&ds, count * sizeof(double)));
+    AQC_HIP_CHECK(hipMemcpy(ds, scores, count * sizeof(double), hipMemcpyHostToDevice));
+  }
+  AQC_HIP_CHECK(hipMemcpy(dp, prio, count * sizeof(double), hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(k_argmax, dim3(1), dim3(256), 0, st, scores_is_device ? scores : ds, dp, count, db);
+  AQC_CHECK_LAUNCH();
+  AQC_HIP_CHECK(hipMemcpyAsync(best, db, sizeof(int), hipMemcpyDeviceToHost, st));
+  AQC_HIP_CHECK(hipStreamSynchronize(st));
+  hipFree(dp);
+  if (ds) hipFree(ds);
+  return AQC_OK;
+}
+
+}  // extern "C"

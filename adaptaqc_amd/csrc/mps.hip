@@ -1,0 +1,1450 @@
+// MPS engine: replaces qiskit-aer's matrix_product_state simulator as driven by
+// adaptaqc/backends/aer_mps_backend.py:27-93 and the aqc_research.mps_operations measurements.
+//
+// Gate application follows Aer's algorithm (see oracle/mps.py for the restatement):
+//   * 1-qubit gates act on the Gamma of the qubit's current site (here deferred and folded into
+//     the next two-site update on that qubit, which is exact: truncation commutes with a local
+//     unitary on either side of the cut);
+//   * 2-qubit gates use "swap-left" routing with a lazily kept qubit permutation (host side);
+//   * every two-site update = contract theta (k_theta), one-sided Jacobi SVD (k_jacobi),
+//     reduce_zeros truncation + renormalisation (k_rank), and the lambda-divided split into the
+//     two new Gammas (k_split_copy, k_split_gemm).
+// Independent states advance in lock-step: one launch of each kernel serves one two-site
+// update of every state in the batch (blockIdx.y / blockIdx.x = job).
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <mutex>
+
+#include "mps_internal.h"
+
+using aqc::cplx;
+
+namespace aqc {
+
+hipStream_t mps_stream() {
+  static std::mutex mu;
+  static hipStream_t s[64] = {nullptr};
+  int dev = 0;
+  hipGetDevice(&dev);
+  std::lock_guard<std::mutex> lk(mu);
+  if (!s[dev]) hipStreamCreateWithFlags(&s[dev], hipStreamNonBlocking);
+  return s[dev];
+}
+
+}  // namespace aqc
+
+namespace {
+
+constexpr int kT = 256;
+constexpr double kChop = 1e-16;
+constexpr int kPanelCplx = 8192;  // 128 KiB of LDS for Jacobi panels
+constexpr int kMaxSweeps = 60;
+// rotation threshold: |a^H b| > tol_factor * L * eps * |a| |b|  (L = column length)
+double g_jacobi_tol_factor = 1.0;
+
+struct OneSiteJob {
+  cplx* g;
+  const int* dims;  // &dims[p]
+  int cap;
+  int pad;
+  cplx u[4];
+};
+
+struct TwoSiteJob {
+  cplx* gp;
+  cplx* gq;
+  const double* ll;
+  double* lm;
+  const double* lr;
+  int* dims;  // &dims[p] : dims[0] = chi_l, dims[1] = chi_m, dims[2] = chi_r
+  cplx* theta;
+  cplx* work;
+  double* sig;
+  int* perm;
+  int* flags;
+  int cap;
+  int max_chi;
+  double thr;
+  double jtol;  // Jacobi rotation threshold factor
+  double pad2;
+  cplx G[16];  // row = 2*s1'+s2' (out), col = 2*s1+s2 (in)
+};
+
+// ------------------------------------------------------------------------------------------
+__global__ void k_mps_zero(cplx* gam, double* lam, int* dims, int n, int cap) {
+  const size_t ss = (size_t)2 * cap * cap;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    gam[(size_t)i * ss] = aqc::cmk(1.0, 0.0);
+  }
+  for (int b = blockIdx.x * blockDim.x + threadIdx.x; b <= n; b += gridDim.x * blockDim.x) {
+    lam[(size_t)b * cap] = 1.0;
+    dims[b] = 1;
+  }
+}
+
+__global__ __launch_bounds__(kT) void k_1q(const OneSiteJob* __restrict__ jobs) {
+  const OneSiteJob& j = jobs[blockIdx.y];
+  const int cl = j.dims[0], cr = j.dims[1];
+  const int cap = j.cap;
+  const size_t half = (size_t)cap * cap;
+  for (int e = blockIdx.x * kT + threadIdx.x; e < cl * cr; e += gridDim.x * kT) {
+    const int l = e / cr, r = e % cr;
+    const size_t o = (size_t)l * cap + r;
+    cplx a0 = j.g[o], a1 = j.g[half + o];
+    j.g[o] = aqc::cfma(j.u[1], a1, aqc::cmul(j.u[0], a0));
+    j.g[half + o] = aqc::cfma(j.u[3], a1, aqc::cmul(j.u[2], a0));
+  }
+}
+
+// theta[(s2*chr + r)*M + s1*chl + l] = sum_in G[out][in] * P_in[l][r],
+// P_{s1' s2'}[l][r] = sum_m ll[l] Gp[s1'][l][m] lm[m] Gq[s2'][m][r] lr[r].
+__global__ __launch_bounds__(kT) void k_theta(const TwoSiteJob* __restrict__ jobs) {
+  const TwoSiteJob& j = jobs[blockIdx.y];
+  const int chl = j.dims[0], chm = j.dims[1], chr = j.dims[2];
+  const int cap = j.cap;
+  const int tiles_r = (cap + 15) / 16;
+  const int l0 = (blockIdx.x / tiles_r) * 16, r0 = (blockIdx.x % tiles_r) * 16;
+  if (l0 >= chl || r0 >= chr) return;
+  __shared__ cplx As[2][16][17];
+  __shared__ cplx Bs[2][16][17];
+  const int ty = threadIdx.x / 16, tx = threadIdx.x % 16;
+  const int l = l0 + ty, r = r0 + tx;
+  const size_t half = (size_t)cap * cap;
+  cplx acc[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) acc[i] = aqc::cmk(0, 0);
+  const double lll = l < chl ? j.ll[l] : 0.0;
+  const double lrr = r < chr ? j.lr[r] : 0.0;
+  for (int m0 = 0; m0 < chm; m0 += 16) {
+    const int ma = m0 + tx, mb = m0 + ty;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      cplx a = aqc::cmk(0, 0), b = aqc::cmk(0, 0);
+      if (l < chl && ma < chm) a = aqc::cscale(j.gp[s * half + (size_t)l * cap + ma], lll * j.lm[ma]);
+      if (mb < chm && r < chr) b = aqc::cscale(j.gq[s * half + (size_t)mb * cap + r], lrr);
+      As[s][ty][tx] = a;
+      Bs[s][ty][tx] = b;
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int mm = 0; mm < 16; ++mm) {
+      const cplx a0 = As[0][ty][mm], a1 = As[1][ty][mm];
+      const cplx b0 = Bs[0][mm][tx], b1 = Bs[1][mm][tx];
+      acc[0] = aqc::cfma(a0, b0, acc[0]);
+      acc[1] = aqc::cfma(a0, b1, acc[1]);
+      acc[2] = aqc::cfma(a1, b0, acc[2]);
+      acc[3] = aqc::cfma(a1, b1, acc[3]);
+    }
+    __syncthreads();
+  }
+  if (l < chl && r < chr) {
+    const int M = 2 * chl;
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+      cplx v = aqc::cmul(j.G[o * 4 + 0], acc[0]);
+      v = aqc::cfma(j.G[o * 4 + 1], acc[1], v);
+      v = aqc::cfma(j.G[o * 4 + 2], acc[2], v);
+      v = aqc::cfma(j.G[o * 4 + 3], acc[3], v);
+      const int s1 = o >> 1, s2 = o & 1;
+      j.theta[(size_t)(s2 * chr + r) * M + s1 * chl + l] = v;
+    }
+  }
+}
+
+// ---- one-sided Jacobi ------------------------------------------------------------------
+// Columns of the working matrix W (L rows, C columns, column-major, ld = L) are orthogonalised
+// by complex plane rotations.  Columns are processed in LDS panels: blocks of b columns,
+// one cyclic sweep = every block's internal pairs (round robin) + every cross pair of every
+// block pair; with C <= panel capacity the whole matrix stays in LDS across sweeps.
+// LPP lanes cooperate on one column pair; each lane holds its MAXR rows of both columns in
+// registers for the round (rows interleaved by LPP -> conflict-free 16-B LDS accesses), so a
+// round is one LDS read + one LDS write per element, with every load of the round in flight.
+constexpr int kJT = 512;  // Jacobi workgroup: 8 waves, 2 per SIMD
+
+__device__ __forceinline__ int rr_elem(int pos, int r, int c) {
+  // round-robin tournament on c (even) players: position 0 fixed, others rotate.
+  if (pos == 0) return 0;
+  return ((pos - 1 + r) % (c - 1)) + 1;
+}
+
+// Rotate the pairs of one round.  pair_of(p) -> (ja, jb) column slots in the panel (-1 = skip).
+template <int LPP, int MAXR, typename PairFn>
+__device__ __forceinline__ void jacobi_round(cplx* panel, int ld, int L, int npairs, double tol, double floor2,
+                                             PairFn pair_of, int* rot_count) {
+  const int tid = threadIdx.x;
+  const int grp = tid / LPP, lane = tid % LPP;
+  constexpr int kGroups = kJT / LPP;
+  for (int pbase = 0; pbase < npairs; pbase += kGroups) {
+    const int p = pbase + grp;
+    int ja = -1, jb = -1;
+    if (p < npairs) pair_of(p, ja, jb);
+    const bool active = (ja >= 0 && jb >= 0);
+    cplx ra[MAXR], rb[MAXR];
+    double al = 0, be = 0;
+    cplx ga = aqc::cmk(0, 0);
+    if (active) {
+      const cplx* ca = panel + ja * ld;
+      const cplx* cb = panel + jb * ld;
+#pragma unroll
+      for (int i = 0; i < MAXR; ++i) {
+        const int r = lane + i * LPP;
+        ra[i] = r < L ? ca[r] : aqc::cmk(0, 0);
+        rb[i] = r < L ? cb[r] : aqc::cmk(0, 0);
+      }
+#pragma unroll
+      for (int i = 0; i < MAXR; ++i) {
+        al += aqc::cnorm2(ra[i]);
+        be += aqc::cnorm2(rb[i]);
+        ga = aqc::cfmac(ra[i], rb[i], ga);
+      }
+    }
+#pragma unroll
+    for (int off = 1; off < LPP; off <<= 1) {
+      al += __shfl_xor(al, off, LPP);
+      be += __shfl_xor(be, off, LPP);
+      ga.x += __shfl_xor(ga.x, off, LPP);
+      ga.y += __shfl_xor(ga.y, off, LPP);
+    }
+    if (active) {
+      const double g = sqrt(aqc::cnorm2(ga));
+      // Columns below floor2 (squared norm) are rounding noise of exactly-zero singular values:
+      // their direction is random, so relative orthogonality can never be reached; they are
+      // far below the CHOP cut (s^2 <= 1e-16) and are left alone.
+      if (g > tol * sqrt(al * be) && al > floor2 && be > floor2) {
+        const double zeta = (be - al) / (2.0 * g);
+        const double t = (zeta >= 0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
+        const double c = 1.0 / sqrt(1.0 + t * t);
+        const double s = c * t;
+        const double ig = 1.0 / g;
+        const cplx se = aqc::cmk(ga.x * ig * s, ga.y * ig * s);    // s e
+        const cplx sec = aqc::cmk(ga.x * ig * s, -ga.y * ig * s);  // s conj(e)
+        cplx* ca = panel + ja * ld;
+        cplx* cb = panel + jb * ld;
+#pragma unroll
+        for (int i = 0; i < MAXR; ++i) {
+          const int r = lane + i * LPP;
+          // a' = c a - s conj(e) b ; b' = s e a + c b
+          const cplx a = ra[i], b = rb[i];
+          if (r < L) {
+            ca[r] = aqc::csub(aqc::cscale(a, c), aqc::cmul(sec, b));
+            cb[r] = aqc::cfma(se, a, aqc::cscale(b, c));
+          }
+        }
+        if (lane == 0) atomicAdd(rot_count, 1);
+      }
+    }
+  }
+}
+
+template <int LPP, int MAXR>
+__global__ __launch_bounds__(kJT) void k_jacobi(const TwoSiteJob* __restrict__ jobs) {
+  const TwoSiteJob& j = jobs[blockIdx.x];
+  __shared__ cplx panel[kPanelCplx];
+  __shared__ int rot;
+  __shared__ double fred[kJT];
+  const int chl = j.dims[0], chr = j.dims[2];
+  const int M = 2 * chl, N = 2 * chr;
+  const bool tr = M < N;
+  const int L = tr ? N : M;
+  const int C = tr ? M : N;
+  const int tid = threadIdx.x;
+  cplx* W = j.work;
+  // W <- theta (or theta^H), column-major with ld = L; squared Frobenius norm on the way
+  double f = 0.0;
+  for (int idx = tid; idx < L * C; idx += kJT) {
+    const int col = idx / L, row = idx % L;
+    const cplx v = tr ? aqc::cconj(j.theta[(size_t)row * M + col]) : j.theta[(size_t)col * M + row];
+    W[idx] = v;
+    f += aqc::cnorm2(v);
+  }
+  fred[tid] = f;
+  __syncthreads();
+  for (int s = kJT / 2; s > 0; s >>= 1) {
+    if (tid < s) fred[tid] += fred[tid + s];
+    __syncthreads();
+  }
+  // absolute noise floor for squared column norms, relative to ||W||_F^2
+  const double floor2 = fred[0] * 1e-24;
+  const double tol = j.jtol * (double)L * 2.220446049250313e-16;
+  const int ld = L + 1;
+  int sweeps = 0;
+  if (C >= 2) {
+    const int cap_cols = kPanelCplx / ld;
+    if (C <= cap_cols) {
+      // whole matrix resident in LDS
+      for (int idx = tid; idx < L * C; idx += kJT) panel[(idx / L) * ld + idx % L] = W[idx];
+      __syncthreads();
+      const int ce = C + (C & 1);
+      for (sweeps = 0; sweeps < kMaxSweeps; ++sweeps) {
+        if (tid == 0) rot = 0;
+        __syncthreads();
+        for (int r = 0; r < ce - 1; ++r) {
+          jacobi_round<LPP, MAXR>(panel, ld, L, ce / 2, tol, floor2,
+                                  [&](int p, int& a, int& b) {
+                                    a = rr_elem(p, r, ce);
+                                    b = rr_elem(ce - 1 - p, r, ce);
+                                    if (a >= C || b >= C) a = b = -1;
+                                  },
+                                  &rot);
+          __syncthreads();
+        }
+        if (rot == 0) break;
+        __syncthreads();
+      }
+      for (int idx = tid; idx < L * C; idx += kJT) W[idx] = panel[(idx / L) * ld + idx % L];
+      __syncthreads();
+    } else {
+      const int b = cap_cols / 2;
+      const int nb = (C + b - 1) / b;
+      const int be = b + (b & 1);
+      for (sweeps = 0; sweeps < kMaxSweeps; ++sweeps) {
+        if (tid == 0) rot = 0;
+        __syncthreads();
+        // intra-block visits
+        for (int I = 0; I < nb; ++I) {
+          const int c0 = I * b, cn = min(b, C - c0);
+          for (int idx = tid; idx < L * cn; idx += kJT)
+            panel[(idx / L) * ld + idx % L] = W[(size_t)c0 * L + idx];
+          __syncthreads();
+          for (int r = 0; r < be - 1; ++r) {
+            jacobi_round<LPP, MAXR>(panel, ld, L, be / 2, tol, floor2,
+                                    [&](int p, int& a, int& bb) {
+                                      a = rr_elem(p, r, be);
+                                      bb = rr_elem(be - 1 - p, r, be);
+                                      if (a >= cn || bb >= cn) a = bb = -1;
+                                    },
+                                    &rot);
+            __syncthreads();
+          }
+          for (int idx = tid; idx < L * cn; idx += kJT)
+            W[(size_t)c0 * L + idx] = panel[(idx / L) * ld + idx % L];
+          __syncthreads();
+        }
+        // cross-block visits
+        for (int I = 0; I < nb; ++I) {
+          for (int J = I + 1; J < nb; ++J) {
+            const int cI = I * b, nI = min(b, C - cI);
+            const int cJ = J * b, nJ = min(b, C - cJ);
+            for (int idx = tid; idx < L * nI; idx += kJT) panel[(idx / L) * ld + idx % L] = W[(size_t)cI * L + idx];
+            for (int idx = tid; idx < L * nJ; idx += kJT)
+              panel[(b + idx / L) * ld + idx % L] = W[(size_t)cJ * L + idx];
+            __syncthreads();
+            for (int r = 0; r < b; ++r) {
+              jacobi_round<LPP, MAXR>(panel, ld, L, b, tol, floor2,
+                                      [&](int p, int& a, int& bb) {
+                                        const int q = (p + r) % b;
+                                        a = p < nI ? p : -1;
+                                        bb = q < nJ ? b + q : -1;
+                                      },
+                                      &rot);
+              __syncthreads();
+            }
+            for (int idx = tid; idx < L * nI; idx += kJT) W[(size_t)cI * L + idx] = panel[(idx / L) * ld + idx % L];
+            for (int idx = tid; idx < L * nJ; idx += kJT)
+              W[(size_t)cJ * L + idx] = panel[(b + idx / L) * ld + idx % L];
+            __syncthreads();
+          }
+        }
+        if (rot == 0) break;
+        __syncthreads();
+      }
+    }
+  }
+  // column norms: LPP lanes per column, coalesced
+  {
+    const int grp = tid / LPP, lane = tid % LPP;
+    for (int col = grp; col < C; col += kJT / LPP) {
+      double s = 0;
+      for (int row = lane; row < L; row += LPP) s += aqc::cnorm2(W[(size_t)col * L + row]);
+#pragma unroll
+      for (int off = 1; off < LPP; off <<= 1) s += __shfl_xor(s, off, LPP);
+      if (lane == 0) j.sig[col] = sqrt(s);
+    }
+  }
+  if (tid == 0) {
+    if (sweeps >= kMaxSweeps) atomicOr(&j.flags[1], 1);
+    atomicMax(&j.flags[2], sweeps + 1);
+  }
+}
+
+// Sort singular values, apply reduce_zeros, write lambda_m / dims[1] / perm / sorted sig.
+__global__ __launch_bounds__(kT) void k_rank(const TwoSiteJob* __restrict__ jobs) {
+  const TwoSiteJob& j = jobs[blockIdx.x];
+  __shared__ double sv[512];
+  __shared__ int si[512];
+  __shared__ int kk_s;
+  __shared__ double norm_s;
+  const int chl = j.dims[0], chr = j.dims[2];
+  const int M = 2 * chl, N = 2 * chr;
+  const int C = M < N ? M : N;
+  int P = 1;
+  while (P < C) P <<= 1;
+  const int tid = threadIdx.x;
+  for (int i = tid; i < P; i += kT) {
+    sv[i] = i < C ? j.sig[i] : -1.0;
+    si[i] = i;
+  }
+  __syncthreads();
+  // bitonic sort, descending by value, ascending index on ties
+  for (int k = 2; k <= P; k <<= 1) {
+    for (int s = k >> 1; s > 0; s >>= 1) {
+      for (int i = tid; i < P; i += kT) {
+        const int ixj = i ^ s;
+        if (ixj > i) {
+          const bool desc = (i & k) == 0;
+          const double a = sv[i], b = sv[ixj];
+          const bool a_first = (a > b) || (a == b && si[i] < si[ixj]);
+          if (a_first != desc) {
+            sv[i] = b;
+            sv[ixj] = a;
+            const int t = si[i];
+            si[i] = si[ixj];
+            si[ixj] = t;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  if (tid == 0) {
+    int k = 0;
+    for (int i = 0; i < C; ++i)
+      if (sv[i] * sv[i] > kChop) ++k;
+    if (k < 1) k = 1;
+    if (j.max_chi > 0 && k > j.max_chi) k = j.max_chi;
+    if (k > j.cap) {
+      k = j.cap;
+      atomicOr(&j.flags[0], 1);
+    }
+    double tail = 0.0;
+    while (k > 1 && tail + sv[k - 1] * sv[k - 1] < j.thr) {
+      tail += sv[k - 1] * sv[k - 1];
+      --k;
+    }
+    double nn = 0.0;
+    for (int i = 0; i < k; ++i) nn += sv[i] * sv[i];
+    kk_s = k;
+    norm_s = sqrt(nn);
+    j.dims[1] = k;
+  }
+  __syncthreads();
+  const int k = kk_s;
+  for (int i = tid; i < k; i += kT) {
+    j.lm[i] = sv[i] / norm_s;
+    j.perm[i] = si[i];
+    j.sig[i + 512] = sv[i];  // sorted copy lives past the raw norms
+  }
+}
+
+// Orthogonalised side: copy (scaled) columns of W into the Gamma they define.
+__global__ __launch_bounds__(kT) void k_split_copy(const TwoSiteJob* __restrict__ jobs) {
+  const TwoSiteJob& j = jobs[blockIdx.y];
+  const int chl = j.dims[0], k = j.dims[1], chr = j.dims[2];
+  const int M = 2 * chl, N = 2 * chr;
+  const bool tr = M < N;
+  const int L = tr ? N : M;
+  const int cap = j.cap;
+  const size_t half = (size_t)cap * cap;
+  const double* ss = j.sig + 512;
+  if (!tr) {
+    // Gp'[s1][l][kk] = W[perm kk][s1*chl + l] / sig_kk / ll[l]
+    for (int e = blockIdx.x * kT + threadIdx.x; e < 2 * chl * k; e += gridDim.x * kT) {
+      const int kk = e % k, rr = e / k;
+      const int s1 = rr / chl, l = rr % chl;
+      const double d = ss[kk] * j.ll[l];
+      const cplx w = j.work[(size_t)j.perm[kk] * L + rr];
+      j.gp[s1 * half + (size_t)l * cap + kk] = d != 0.0 ? aqc::cscale(w, 1.0 / d) : aqc::cmk(0, 0);
+    }
+  } else {
+    // Gq'[s2][kk][r] = conj(W[perm kk][s2*chr + r]) / sig_kk / lr[r]
+    for (int e = blockIdx.x * kT + threadIdx.x; e < 2 * chr * k; e += gridDim.x * kT) {
+      const int cc = e % N, kk = e / N;
+      const int s2 = cc / chr, r = cc % chr;
+      const double d = ss[kk] * j.lr[r];
+      const cplx w = aqc::cconj(j.work[(size_t)j.perm[kk] * L + cc]);
+      j.gq[s2 * half + (size_t)kk * cap + r] = d != 0.0 ? aqc::cscale(w, 1.0 / d) : aqc::cmk(0, 0);
+    }
+  }
+}
+
+// Other side by one GEMM against the original theta:
+//   !tr: Vh[kk][c] = sum_R conj(W_j[R]) theta[R][c] / sig^2 -> Gq'[s2][kk][r] = Vh / lr[r]
+//    tr: U[R][kk]  = sum_c theta[R][c] W_j[c] / sig^2      -> Gp'[s1][l][kk] = U / ll[l]
+__global__ __launch_bounds__(kT) void k_split_gemm(const TwoSiteJob* __restrict__ jobs) {
+  const TwoSiteJob& j = jobs[blockIdx.y];
+  const int chl = j.dims[0], k = j.dims[1], chr = j.dims[2];
+  const int M = 2 * chl, N = 2 * chr;
+  const bool tr = M < N;
+  const int L = tr ? N : M;
+  const int cap = j.cap;
+  const size_t half = (size_t)cap * cap;
+  const double* ss = j.sig + 512;
+  // output tile: rows = kk (16), cols = c (16) for !tr ; rows = R (16), cols = kk (16) for tr
+  const int rows = tr ? M : k, cols = tr ? k : N;
+  const int tiles_c = (2 * cap + 15) / 16;
+  const int r0 = (blockIdx.x / tiles_c) * 16, c0 = (blockIdx.x % tiles_c) * 16;
+  if (r0 >= rows || c0 >= cols) return;
+  __shared__ cplx As[16][17];
+  __shared__ cplx Bs[16][17];
+  const int ty = threadIdx.x / 16, tx = threadIdx.x % 16;
+  const int ro = r0 + ty, co = c0 + tx;
+  cplx acc = aqc::cmk(0, 0);
+  const int K = L;  // inner dimension: M for !tr, N for tr
+  for (int k0 = 0; k0 < K; k0 += 16) {
+    // A[ro][kin], B[kin][co]
+    {
+      const int ar = r0 + ty, ak = k0 + tx;
+      cplx a = aqc::cmk(0, 0);
+      if (ar < rows && ak < K) {
+        if (!tr) a = aqc::cconj(j.work[(size_t)j.perm[ar] * L + ak]);  // conj(W_j[R])
+        else a = j.theta[(size_t)ak * M + ar];                         // theta[R][c]
+      }
+      As[ty][tx] = a;
+      const int bk = k0 + ty, bc = c0 + tx;
+      cplx b = aqc::cmk(0, 0);
+      if (bk < K && bc < cols) {
+        if (!tr) b = j.theta[(size_t)bc * M + bk];                 // theta[R][c]
+        else b = j.work[(size_t)j.perm[bc] * L + bk];               // W_j[c]
+      }
+      Bs[ty][tx] = b;
+    }
+    __syncthreads();
+#pragma unroll 8
+    for (int kk = 0; kk < 16; ++kk) acc = aqc::cfma(As[ty][kk], Bs[kk][tx], acc);
+    __syncthreads();
+  }
+  if (ro < rows && co < cols) {
+    if (!tr) {
+      const int kk = ro, cc = co;
+      const int s2 = cc / chr, r = cc % chr;
+      const double d = ss[kk] * ss[kk] * j.lr[r];
+      j.gq[s2 * half + (size_t)kk * cap + r] = d != 0.0 ? aqc::cscale(acc, 1.0 / d) : aqc::cmk(0, 0);
+    } else {
+      const int R = ro, kk = co;
+      const int s1 = R / chl, l = R % chl;
+      const double d = ss[kk] * ss[kk] * j.ll[l];
+      j.gp[s1 * half + (size_t)l * cap + kk] = d != 0.0 ? aqc::cscale(acc, 1.0 / d) : aqc::cmk(0, 0);
+    }
+  }
+}
+
+// ---- measurements -------------------------------------------------------------------------
+struct MeasJob {
+  const cplx* gam;
+  const double* lam;
+  const int* dims;
+  int n;
+  int cap;
+  cplx* out;
+  cplx* vec;   // zero-chain scratch (2*(n+1)*cap)
+  cplx* env;   // env scratch
+  cplx* tmp;   // 2*cap*cap
+};
+
+__device__ __forceinline__ cplx site_a(const cplx* gam, const double* lam, int cap, int i, int s, int l,
+                                        int r) {
+  // A_i[s][l][r] = Gamma_i[s][l][r] * lambda_{i+1}[r]  (aqc_research _preprocess_mps)
+  const size_t ss = (size_t)2 * cap * cap;
+  return aqc::cscale(gam[(size_t)i * ss + (size_t)s * cap * cap + (size_t)l * cap + r],
+                     lam[(size_t)(i + 1) * cap + r]);
+}
+
+// <0...0|psi>: v <- v A_i[0] from the left.  One workgroup per state.
+__global__ __launch_bounds__(kT) void k_overlap_zero(const MeasJob* __restrict__ jobs) {
+  const MeasJob& j = jobs[blockIdx.x];
+  __shared__ cplx v[2][256];
+  __shared__ cplx part[4][256];
+  const int tid = threadIdx.x;
+  if (tid == 0) v[0][0] = aqc::cmk(1.0, 0.0);
+  __syncthreads();
+  int cur = 0;
+  const int q = tid >> 6, lane = tid & 63;
+  for (int i = 0; i < j.n; ++i) {
+    const int cl = j.dims[i], cr = j.dims[i + 1];
+    for (int r0 = 0; r0 < cr; r0 += 64) {
+      const int r = r0 + lane;
+      cplx acc = aqc::cmk(0, 0);
+      if (r < cr)
+        for (int l = q; l < cl; l += 4) acc = aqc::cfma(v[cur][l], site_a(j.gam, j.lam, j.cap, i, 0, l, r), acc);
+      part[q][lane + 0] = acc;
+      __syncthreads();
+      if (q == 0 && r < cr)
+        v[cur ^ 1][r] = aqc::cadd(aqc::cadd(part[0][lane], part[1][lane]), aqc::cadd(part[2][lane], part[3][lane]));
+      __syncthreads();
+    }
+    cur ^= 1;
+  }
+  if (tid == 0) j.out[0] = v[cur][0];
+}
+
+// Zero chains: vec[b] (left, bond b) = <0..0| A_0..A_{b-1};  vec[(n+1)+b] (right) = A_b..A_{n-1}|0..0>.
+// blockIdx.y = 0 -> left chain, 1 -> right chain.
+__global__ __launch_bounds__(kT) void k_zero_chains(const MeasJob* __restrict__ jobs) {
+  const MeasJob& j = jobs[blockIdx.x];
+  const int tid = threadIdx.x;
+  const int cap = j.cap, n = j.n;
+  cplx* L = j.vec;
+  cplx* R = j.vec + (size_t)(n + 1) * cap;
+  if (blockIdx.y == 0) {
+    if (tid == 0) L[0] = aqc::cmk(1.0, 0.0);
+    __syncthreads();
+    for (int i = 0; i < n; ++i) {
+      const int cl = j.dims[i], cr = j.dims[i + 1];
+      for (int r = tid; r < cr; r += kT) {
+        cplx acc = aqc::cmk(0, 0);
+        for (int l = 0; l < cl; ++l) acc = aqc::cfma(L[(size_t)i * cap + l], site_a(j.gam, j.lam, cap, i, 0, l, r), acc);
+        L[(size_t)(i + 1) * cap + r] = acc;
+      }
+      __syncthreads();
+    }
+  } else {
+    if (tid == 0) R[(size_t)n * cap] = aqc::cmk(1.0, 0.0);
+    __syncthreads();
+    for (int i = n - 1; i >= 0; --i) {
+      const int cl = j.dims[i], cr = j.dims[i + 1];
+      for (int l = tid; l < cl; l += kT) {
+        cplx acc = aqc::cmk(0, 0);
+        for (int r = 0; r < cr; ++r) acc = aqc::cfma(site_a(j.gam, j.lam, cap, i, 0, l, r), R[(size_t)(i + 1) * cap + r], acc);
+        R[(size_t)i * cap + l] = acc;
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// amp_i = <e_i|psi> = L[i] A_i[1] R[i+1].  blockIdx.x = site, blockIdx.y = job.
+__global__ __launch_bounds__(kT) void k_hw1(const MeasJob* __restrict__ jobs) {
+  const MeasJob& j = jobs[blockIdx.y];
+  const int i = blockIdx.x;
+  const int cap = j.cap, n = j.n;
+  if (i >= n) return;
+  const cplx* L = j.vec + (size_t)i * cap;
+  const cplx* R = j.vec + (size_t)(n + 1) * cap + (size_t)(i + 1) * cap;
+  const int cl = j.dims[i], cr = j.dims[i + 1];
+  __shared__ double red[2][kT];
+  cplx acc = aqc::cmk(0, 0);
+  for (int e = threadIdx.x; e < cl * cr; e += kT) {
+    const int l = e / cr, r = e % cr;
+    acc = aqc::cfma(aqc::cmul(L[l], site_a(j.gam, j.lam, cap, i, 1, l, r)), R[r], acc);
+  }
+  red[0][threadIdx.x] = acc.x;
+  red[1][threadIdx.x] = acc.y;
+  __syncthreads();
+  for (int s = kT / 2; s > 0; s >>= 1) {
+    if (threadIdx.x < s) {
+      red[0][threadIdx.x] += red[0][threadIdx.x + s];
+      red[1][threadIdx.x] += red[1][threadIdx.x + s];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) j.out[i] = aqc::cmk(red[0][0], red[1][0]);
+}
+
+// Transfer-matrix environments of <a|b> (one workgroup per chain):
+//   left : E_{i+1}[ra][rb] = sum_s sum_{la,lb} conj(A_i[s][la][ra]) E_i[la][lb] B_i[s][lb][rb]
+//   right: E_i[la][lb]     = sum_s sum_{ra,rb} conj(A_i[s][la][ra]) B_i[s][lb][rb] E_{i+1}[ra][rb]
+// With keep_all, every bond's environment is stored (env + b*cap*cap), else only the final one.
+struct EnvJob {
+  const cplx* ga;
+  const double* la;
+  const int* da;
+  const cplx* gb;
+  const double* lb;
+  const int* db;
+  int n;
+  int cap;
+  cplx* env;  // (n+1) * cap * cap if keep_all, else 2 * cap*cap ping-pong
+  cplx* tmp;  // 2 * cap * cap
+  int keep_all;
+  int right;
+  cplx* out;
+};
+
+__global__ __launch_bounds__(kT) void k_env(const EnvJob* __restrict__ jobs) {
+  const EnvJob& j = jobs[blockIdx.x];
+  const int tid = threadIdx.x;
+  const int cap = j.cap, n = j.n;
+  const size_t cc = (size_t)cap * cap;
+  auto envp = [&](int b) -> cplx* { return j.keep_all ? j.env + (size_t)b * cc : j.env + (size_t)(b & 1) * cc; };
+  if (!j.right) {
+    if (tid == 0) envp(0)[0] = aqc::cmk(1.0, 0.0);
+    __syncthreads();
+    for (int i = 0; i < n; ++i) {
+      const int la = j.da[i], ra = j.da[i + 1], lb = j.db[i], rb = j.db[i + 1];
+      const cplx* E = envp(i);
+      cplx* En = envp(i + 1);
+      // X[s][la][rb] = sum_lb E[la][lb] B[s][lb][rb]   (X in tmp, ld = cap)
+      for (int e = tid; e < 2 * la * rb; e += kT) {
+        const int s = e / (la * rb), rem = e % (la * rb), a = rem / rb, c = rem % rb;
+        cplx acc = aqc::cmk(0, 0);
+        for (int b = 0; b < lb; ++b) acc = aqc::cfma(E[(size_t)a * cap + b], site_a(j.gb, j.lb, cap, i, s, b, c), acc);
+        j.tmp[(size_t)s * cc + (size_t)a * cap + c] = acc;
+      }
+      __syncthreads();
+      for (int e = tid; e < ra * rb; e += kT) {
+        const int a = e / rb, c = e % rb;
+        cplx acc = aqc::cmk(0, 0);
+        for (int s = 0; s < 2; ++s)
+          for (int x = 0; x < la; ++x)
+            acc = aqc::cfmac(site_a(j.ga, j.la, cap, i, s, x, a), j.tmp[(size_t)s * cc + (size_t)x * cap + c], acc);
+        En[(size_t)a * cap + c] = acc;
+      }
+      __syncthreads();
+    }
+    if (tid == 0 && j.out) j.out[0] = envp(n)[0];
+  } else {
+    if (tid == 0) envp(n)[0] = aqc::cmk(1.0, 0.0);
+    __syncthreads();
+    for (int i = n - 1; i >= 0; --i) {
+      const int la = j.da[i], ra = j.da[i + 1], lb = j.db[i], rb = j.db[i + 1];
+      const cplx* E = envp(i + 1);
+      cplx* En = envp(i);
+      // Y[s][lb][ra] = sum_rb B[s][lb][rb] E[ra][rb]
+      for (int e = tid; e < 2 * lb * ra; e += kT) {
+        const int s = e / (lb * ra), rem = e % (lb * ra), b = rem / ra, a = rem % ra;
+        cplx acc = aqc::cmk(0, 0);
+        for (int c = 0; c < rb; ++c) acc = aqc::cfma(site_a(j.gb, j.lb, cap, i, s, b, c), E[(size_t)a * cap + c], acc);
+        j.tmp[(size_t)s * cc + (size_t)b * cap + a] = acc;
+      }
+      __syncthreads();
+      for (int e = tid; e < la * lb; e += kT) {
+        const int a = e / lb, b = e % lb;
+        cplx acc = aqc::cmk(0, 0);
+        for (int s = 0; s < 2; ++s)
+          for (int x = 0; x < ra; ++x)
+            acc = aqc::cfmac(site_a(j.ga, j.la, cap, i, s, a, x), j.tmp[(size_t)s * cc + (size_t)b * cap + x], acc);
+        En[(size_t)a * cap + b] = acc;
+      }
+      __syncthreads();
+    }
+    if (tid == 0 && j.out) j.out[0] = envp(0)[0];
+  }
+}
+
+// <Z_i> = sum_s z_s sum conj(A[s][l][r]) L[l][l'] A[s][l'][r'] R[r][r'].  blockIdx.x = site.
+__global__ __launch_bounds__(kT) void k_zexp(const cplx* gam, const double* lam, const int* dims, int n, int cap,
+                                             const cplx* Lenv, const cplx* Renv, cplx* out) {
+  const int i = blockIdx.x;
+  const size_t cc = (size_t)cap * cap;
+  const cplx* Lm = Lenv + (size_t)i * cc;
+  const cplx* Rm = Renv + (size_t)(i + 1) * cc;
+  const int cl = dims[i], cr = dims[i + 1];
+  __shared__ double red[kT];
+  double acc = 0.0;
+  // sum over (s, l, r): conj(A[s][l][r]) * (sum_{l'} L[l][l'] * (sum_{r'} A[s][l'][r'] R[r][r']))
+  for (int e = threadIdx.x; e < 2 * cl * cr; e += kT) {
+    const int s = e / (cl * cr), rem = e % (cl * cr), l = rem / cr, r = rem % cr;
+    cplx t = aqc::cmk(0, 0);
+    for (int lp = 0; lp < cl; ++lp) {
+      cplx u = aqc::cmk(0, 0);
+      for (int rp = 0; rp < cr; ++rp) u = aqc::cfma(site_a(gam, lam, cap, i, s, lp, rp), Rm[(size_t)r * cap + rp], u);
+      t = aqc::cfma(Lm[(size_t)l * cap + lp], u, t);
+    }
+    const cplx v = aqc::cconjmul(site_a(gam, lam, cap, i, s, l, r), t);
+    acc += (s == 0 ? 1.0 : -1.0) * v.x;
+  }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int s = kT / 2; s > 0; s >>= 1) {
+    if (threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[i] = aqc::cmk(red[0], 0.0);
+}
+
+// ---- host-side scheduling ---------------------------------------------------------------
+struct DevOp {
+  int kind;  // 1: one-site, 2: two-site (p, p+1)
+  int p;
+  cplx m[16];
+};
+
+inline cplx hc(double r, double i) { return aqc::cmk(r, i); }
+
+void mat2_mul(const cplx* a, const cplx* b, cplx* out) {  // out = a b (2x2)
+  cplx t[4];
+  for (int r = 0; r < 2; ++r)
+    for (int c = 0; c < 2; ++c)
+      t[r * 2 + c] = aqc::cfma(a[r * 2 + 1], b[2 + c], aqc::cmul(a[r * 2], b[c]));
+  std::memcpy(out, t, sizeof(t));
+}
+
+struct Scheduler {
+  int n;
+  std::vector<int>& order;
+  std::vector<int>& loc;
+  std::vector<cplx> pend;     // 4 per qubit
+  std::vector<char> has;
+  std::vector<DevOp>& out;
+
+  Scheduler(int n_, std::vector<int>& o, std::vector<int>& l, std::vector<DevOp>& dst)
+      : n(n_), order(o), loc(l), pend(4 * n_), has(n_, 0), out(dst) {}
+
+  void swap_sites(int p) {
+    DevOp d;
+    std::memset(&d, 0, sizeof(d));
+    d.kind = 2;
+    d.p = p;
+    // SWAP in site order: out (s1', s2') = in (s2, s1)
+    for (int o = 0; o < 4; ++o) {
+      const int s1 = o >> 1, s2 = o & 1;
+      const int in = 2 * s2 + s1;
+      d.m[o * 4 + in] = hc(1, 0);
+    }
+    out.push_back(d);
+    const int qa = order[p], qb = order[p + 1];
+    order[p] = qb;
+    order[p + 1] = qa;
+    loc[qa] = p + 1;
+    loc[qb] = p;
+  }
+
+  void one(int q, const double* m) {
+    cplx u[4];
+    for (int e = 0; e < 4; ++e) u[e] = hc(m[2 * e], m[2 * e + 1]);
+    if (!has[q]) {
+      std::memcpy(&pend[4 * q], u, sizeof(u));
+      has[q] = 1;
+    } else {
+      mat2_mul(u, &pend[4 * q], &pend[4 * q]);
+    }
+  }
+
+  void two(int qa, int qb, const double* m) {
+    const int pa = loc[qa], pb = loc[qb];
+    const int low = std::min(pa, pb), high = std::max(pa, pb);
+    for (int i = high; i > low + 1; --i) swap_sites(i - 1);  // change_position(high, low+1)
+    cplx M4[16];
+    for (int e = 0; e < 16; ++e) M4[e] = hc(m[2 * e], m[2 * e + 1]);
+    // fold pending one-qubit gates: M' = M . kron(P_b, P_a)   (index 2*b1 + b0, b0 <-> qa)
+    cplx Pa[4] = {hc(1, 0), hc(0, 0), hc(0, 0), hc(1, 0)}, Pb[4] = {hc(1, 0), hc(0, 0), hc(0, 0), hc(1, 0)};
+    if (has[qa]) std::memcpy(Pa, &pend[4 * qa], sizeof(Pa));
+    if (has[qb]) std::memcpy(Pb, &pend[4 * qb], sizeof(Pb));
+    has[qa] = has[qb] = 0;
+    cplx K[16];
+    for (int r = 0; r < 4; ++r)
+      for (int c = 0; c < 4; ++c) K[r * 4 + c] = aqc::cmul(Pb[(r >> 1) * 2 + (c >> 1)], Pa[(r & 1) * 2 + (c & 1)]);
+    cplx Mf[16];
+    for (int r = 0; r < 4; ++r)
+      for (int c = 0; c < 4; ++c) {
+        cplx acc = hc(0, 0);
+        for (int t = 0; t < 4; ++t) acc = aqc::cfma(M4[r * 4 + t], K[t * 4 + c], acc);
+        Mf[r * 4 + c] = acc;
+      }
+    // to site order: G[(2 s1' + s2')][(2 s1 + s2)]
+    const bool a_low = loc[qa] == low;
+    DevOp d;
+    std::memset(&d, 0, sizeof(d));
+    d.kind = 2;
+    d.p = low;
+    for (int so = 0; so < 4; ++so)
+      for (int si = 0; si < 4; ++si) {
+        const int s1o = so >> 1, s2o = so & 1, s1i = si >> 1, s2i = si & 1;
+        int ro, ci;
+        if (a_low) {  // b0 = s1 (qa), b1 = s2 (qb)
+          ro = 2 * s2o + s1o;
+          ci = 2 * s2i + s1i;
+        } else {  // b0 = s2 (qa), b1 = s1 (qb)
+          ro = 2 * s1o + s2o;
+          ci = 2 * s1i + s2i;
+        }
+        d.m[so * 4 + si] = Mf[ro * 4 + ci];
+      }
+    out.push_back(d);
+  }
+
+  void flush() {
+    for (int q = 0; q < n; ++q) {
+      if (!has[q]) continue;
+      DevOp d;
+      std::memset(&d, 0, sizeof(d));
+      d.kind = 1;
+      d.p = loc[q];
+      std::memcpy(d.m, &pend[4 * q], 4 * sizeof(cplx));
+      out.push_back(d);
+      has[q] = 0;
+    }
+  }
+
+  void sort() {
+    for (int left = 0; left < n; ++left) {
+      const int pos = loc[left];
+      for (int j = pos; j > left; --j) swap_sites(j - 1);
+    }
+  }
+};
+
+int validate_ops(aqc_mps_t h, const aqc_op_t* ops, int nops) {
+  for (int i = 0; i < nops; ++i) {
+    const aqc_op_t& o = ops[i];
+    AQC_REQUIRE(o.nq == 1 || o.nq == 2, "aqc_mps_apply: only 1- and 2-qubit ops are supported");
+    AQC_REQUIRE(o.q0 >= 0 && o.q0 < h->d.n, "aqc_mps_apply: qubit index out of range");
+    if (o.nq == 2) AQC_REQUIRE(o.q1 >= 0 && o.q1 < h->d.n && o.q1 != o.q0, "aqc_mps_apply: bad second qubit");
+  }
+  return AQC_OK;
+}
+
+void schedule(aqc_mps_t h, const aqc_op_t* ops, int nops, bool sort_after, std::vector<DevOp>& out) {
+  Scheduler s(h->d.n, h->order, h->loc, out);
+  for (int i = 0; i < nops; ++i) {
+    if (ops[i].nq == 1) s.one(ops[i].q0, ops[i].m);
+    else s.two(ops[i].q0, ops[i].q1, ops[i].m);
+  }
+  s.flush();
+  if (sort_after) s.sort();
+}
+
+// Device staging buffers for job arrays (grown on demand, reused across calls).
+struct Staging {
+  void* dev = nullptr;
+  size_t cap = 0;
+  void* host = nullptr;
+  size_t hcap = 0;
+};
+
+int ensure_staging(Staging& st, size_t bytes) {
+  if (bytes > st.cap) {
+    if (st.dev) hipFree(st.dev);
+    st.cap = std::max(bytes, st.cap * 2);
+    AQC_HIP_CHECK(hipMalloc(&st.dev, st.cap));
+  }
+  if (bytes > st.hcap) {
+    if (st.host) hipHostFree(st.host);
+    st.hcap = std::max(bytes, st.hcap * 2);
+    AQC_HIP_CHECK(hipHostMalloc(&st.host, st.hcap, hipHostMallocDefault));
+  }
+  return AQC_OK;
+}
+
+Staging& staging() {
+  static Staging s[64];
+  int dev = 0;
+  hipGetDevice(&dev);
+  return s[dev];
+}
+
+TwoSiteJob make_two(aqc_mps_t h, const DevOp& op) {
+  TwoSiteJob j;
+  std::memset(&j, 0, sizeof(j));
+  const int p = op.p;
+  j.gp = h->d.site(p);
+  j.gq = h->d.site(p + 1);
+  j.ll = h->d.bond(p);
+  j.lm = h->d.bond(p + 1);
+  j.lr = h->d.bond(p + 2);
+  j.dims = h->d.dims + p;
+  j.theta = h->d.theta;
+  j.work = h->d.work;
+  j.sig = h->d.sig;
+  j.perm = h->d.perm;
+  j.flags = h->d.flags;
+  j.cap = h->d.cap;
+  j.max_chi = h->max_chi;
+  j.thr = h->thr;
+  j.jtol = g_jacobi_tol_factor;
+  std::memcpy(j.G, op.m, sizeof(j.G));
+  return j;
+}
+
+OneSiteJob make_one(aqc_mps_t h, const DevOp& op) {
+  OneSiteJob j;
+  std::memset(&j, 0, sizeof(j));
+  j.g = h->d.site(op.p);
+  j.dims = h->d.dims + op.p;
+  j.cap = h->d.cap;
+  std::memcpy(j.u, op.m, sizeof(j.u));
+  return j;
+}
+
+// Run per-state device-op lists in lock-step waves on the MPS stream.
+int run_waves(aqc_mps_t* hs, int ns, std::vector<std::vector<DevOp>>& lists) {
+  hipStream_t st = aqc::mps_stream();
+  size_t maxlen = 0;
+  for (auto& l : lists) maxlen = std::max(maxlen, l.size());
+  if (maxlen == 0) return AQC_OK;
+  // pre-build every wave's jobs into one staging buffer
+  std::vector<TwoSiteJob> two;
+  std::vector<OneSiteJob> one;
+  std::vector<std::pair<size_t, size_t>> two_rng(maxlen), one_rng(maxlen);
+  int cap_max = 0;
+  for (int s = 0; s < ns; ++s) cap_max = std::max(cap_max, hs[s]->d.cap);
+  for (size_t w = 0; w < maxlen; ++w) {
+    size_t t0 = two.size(), o0 = one.size();
+    for (int s = 0; s < ns; ++s) {
+      if (w >= lists[s].size()) continue;
+      const DevOp& op = lists[s][w];
+      if (op.kind == 2) two.push_back(make_two(hs[s], op));
+      else one.push_back(make_one(hs[s], op));
+    }
+    two_rng[w] = {t0, two.size() - t0};
+    one_rng[w] = {o0, one.size() - o0};
+  }
+  const size_t tb = two.size() * sizeof(TwoSiteJob), ob = one.size() * sizeof(OneSiteJob);
+  Staging& sg = staging();
+  AQC_HIP_CHECK(hipStreamSynchronize(st));  // staging buffers may still feed earlier launches
+  int rc = ensure_staging(sg, tb + ob + 256);
+  if (rc != AQC_OK) return rc;
+  std::memcpy(sg.host, two.data(), tb);
+  std::memcpy((char*)sg.host + tb, one.data(), ob);
+  AQC_HIP_CHECK(hipMemcpyAsync(sg.dev, sg.host, tb + ob, hipMemcpyHostToDevice, st));
+  const TwoSiteJob* dtwo = (const TwoSiteJob*)sg.dev;
+  const OneSiteJob* done = (const OneSiteJob*)((char*)sg.dev + tb);
+  const int tiles = ((cap_max + 15) / 16) * ((cap_max + 15) / 16);
+  const int tiles_split = ((2 * cap_max + 15) / 16) * ((2 * cap_max + 15) / 16);
+  for (size_t w = 0; w < maxlen; ++w) {
+    if (one_rng[w].second) {
+      const int nj = (int)one_rng[w].second;
+      hipLaunchKernelGGL(k_1q, dim3((cap_max * cap_max + kT - 1) / kT, nj), dim3(kT), 0, st,
+                         done + one_rng[w].first);
+      AQC_CHECK_LAUNCH();
+    }
+    if (two_rng[w].second) {
+      const int nj = (int)two_rng[w].second;
+      const TwoSiteJob* jp = dtwo + two_rng[w].first;
+      const double c = cap_max;
+      aqc::KernelTimer::begin(st, "mps_theta", nj * (6.0 * c * c * 16 + 4.0 * c * c * 16), nj * 4.0 * c * c * c * 8);
+      hipLaunchKernelGGL(k_theta, dim3(tiles, nj), dim3(kT), 0, st, jp);
+      aqc::KernelTimer::end(st);
+      AQC_CHECK_LAUNCH();
+      aqc::KernelTimer::begin(st, "mps_svd", nj * 2.0 * (4.0 * c * c * 16), 0.0);
+      // rows per lane from the largest possible column length (2 * cap)
+      if (2 * cap_max <= 64) hipLaunchKernelGGL((k_jacobi<16, 4>), dim3(nj), dim3(kJT), 0, st, jp);
+      else if (2 * cap_max <= 128) hipLaunchKernelGGL((k_jacobi<16, 8>), dim3(nj), dim3(kJT), 0, st, jp);
+      else if (2 * cap_max <= 256) hipLaunchKernelGGL((k_jacobi<16, 16>), dim3(nj), dim3(kJT), 0, st, jp);
+      else hipLaunchKernelGGL((k_jacobi<32, 16>), dim3(nj), dim3(kJT), 0, st, jp);
+      aqc::KernelTimer::end(st);
+      AQC_CHECK_LAUNCH();
+      hipLaunchKernelGGL(k_rank, dim3(nj), dim3(kT), 0, st, jp);
+      AQC_CHECK_LAUNCH();
+      hipLaunchKernelGGL(k_split_copy, dim3(std::max(1, (4 * cap_max * cap_max + kT - 1) / kT), nj), dim3(kT), 0, st, jp);
+      AQC_CHECK_LAUNCH();
+      aqc::KernelTimer::begin(st, "mps_split", 0.0, nj * 2.0 * c * c * 2.0 * c * 8);
+      hipLaunchKernelGGL(k_split_gemm, dim3(tiles_split, nj), dim3(kT), 0, st, jp);
+      aqc::KernelTimer::end(st);
+      AQC_CHECK_LAUNCH();
+    }
+  }
+  return AQC_OK;
+}
+
+int check_flags(aqc_mps_t h) {
+  int f[3] = {0, 0, 0};
+  AQC_HIP_CHECK(hipMemcpyAsync(f, h->d.flags, sizeof(f), hipMemcpyDeviceToHost, aqc::mps_stream()));
+  AQC_HIP_CHECK(hipStreamSynchronize(aqc::mps_stream()));
+  if (f[0]) {
+    aqc::set_error("MPS bond capacity (chi_cap) exceeded: increase chi_cap or set max_chi");
+    int z[3] = {0, 0, 0};
+    hipMemcpy(h->d.flags, z, sizeof(z), hipMemcpyHostToDevice);
+    return AQC_ERR_STATE;
+  }
+  if (f[1]) {
+    aqc::set_error("one-sided Jacobi SVD did not converge");
+    int z[3] = {0, 0, 0};
+    hipMemcpy(h->d.flags, z, sizeof(z), hipMemcpyHostToDevice);
+    return AQC_ERR_STATE;
+  }
+  return AQC_OK;
+}
+
+bool is_sorted_order(aqc_mps_t h) {
+  for (int i = 0; i < h->d.n; ++i)
+    if (h->order[i] != i) return false;
+  return true;
+}
+
+int do_sort(aqc_mps_t* hs, int ns) {
+  std::vector<std::vector<DevOp>> lists(ns);
+  for (int s = 0; s < ns; ++s) {
+    Scheduler sc(hs[s]->d.n, hs[s]->order, hs[s]->loc, lists[s]);
+    sc.sort();
+  }
+  return run_waves(hs, ns, lists);
+}
+
+MeasJob make_meas(aqc_mps_t h, cplx* out) {
+  MeasJob m;
+  m.gam = h->d.gam;
+  m.lam = h->d.lam;
+  m.dims = h->d.dims;
+  m.n = h->d.n;
+  m.cap = h->d.cap;
+  m.out = out;
+  m.vec = h->d.vec;
+  m.env = h->d.env;
+  m.tmp = h->d.tmp;
+  return m;
+}
+
+template <typename T>
+int upload_jobs(const std::vector<T>& jobs, const T** dptr) {
+  Staging& sg = staging();
+  hipStream_t st = aqc::mps_stream();
+  AQC_HIP_CHECK(hipStreamSynchronize(st));
+  const size_t b = jobs.size() * sizeof(T);
+  int rc = ensure_staging(sg, b + 64);
+  if (rc != AQC_OK) return rc;
+  std::memcpy(sg.host, jobs.data(), b);
+  AQC_HIP_CHECK(hipMemcpyAsync(sg.dev, sg.host, b, hipMemcpyHostToDevice, st));
+  *dptr = (const T*)sg.dev;
+  return AQC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int aqc_mps_create(int n, int chi_cap, double threshold, int max_chi, aqc_mps_t* out) {
+  AQC_REQUIRE(out, "aqc_mps_create: null out");
+  AQC_REQUIRE(n >= 1 && n <= 4096, "aqc_mps_create: bad n");
+  AQC_REQUIRE(chi_cap >= 1 && chi_cap <= 256, "aqc_mps_create: chi_cap must be in [1, 256]");
+  auto* h = new aqc_mps_s();
+  h->d.n = n;
+  h->d.cap = chi_cap;
+  h->thr = threshold;
+  h->max_chi = max_chi;
+  h->order.resize(n);
+  h->loc.resize(n);
+  for (int i = 0; i < n; ++i) h->order[i] = h->loc[i] = i;
+  const size_t cap = chi_cap;
+  const size_t g = (size_t)n * 2 * cap * cap;
+  hipStream_t st = aqc::mps_stream();
+  AQC_HIP_CHECK(hipMalloc(&h->d.gam, g * sizeof(cplx)));
+  AQC_HIP_CHECK(hipMalloc(&h->d.lam, (size_t)(n + 1) * cap * sizeof(double)));
+  AQC_HIP_CHECK(hipMalloc(&h->d.dims, (size_t)(n + 1) * sizeof(int)));
+  AQC_HIP_CHECK(hipMalloc(&h->d.theta, 4 * cap * cap * sizeof(cplx)));
+  AQC_HIP_CHECK(hipMalloc(&h->d.work, 4 * cap * cap * sizeof(cplx)));
+  AQC_HIP_CHECK(hipMalloc(&h->d.sig, 1024 * sizeof(double)));
+  AQC_HIP_CHECK(hipMalloc(&h->d.perm, 512 * sizeof(int)));
+  AQC_HIP_CHECK(hipMalloc(&h->d.flags, 4 * sizeof(int)));
+  AQC_HIP_CHECK(hipMalloc(&h->d.vec, 2 * (size_t)(n + 1) * cap * sizeof(cplx)));
+  AQC_HIP_CHECK(hipMalloc(&h->d.tmp, 2 * cap * cap * sizeof(cplx)));
+  AQC_HIP_CHECK(hipMalloc(&h->d.scal, (size_t)(2 * n + 8) * sizeof(cplx)));
+  h->d.env = nullptr;  // allocated lazily for dot / z_all
+  AQC_HIP_CHECK(hipMemsetAsync(h->d.gam, 0, g * sizeof(cplx), st));
+  AQC_HIP_CHECK(hipMemsetAsync(h->d.lam, 0, (size_t)(n + 1) * cap * sizeof(double), st));
+  AQC_HIP_CHECK(hipMemsetAsync(h->d.flags, 0, 4 * sizeof(int), st));
+  hipLaunchKernelGGL(k_mps_zero, dim3(1 + n / 256), dim3(256), 0, st, h->d.gam, h->d.lam, h->d.dims, n, chi_cap);
+  AQC_CHECK_LAUNCH();
+  AQC_HIP_CHECK(hipStreamSynchronize(st));
+  *out = h;
+  return AQC_OK;
+}
+
+int aqc_mps_destroy(aqc_mps_t h) {
+  if (!h) return AQC_OK;
+  hipStreamSynchronize(aqc::mps_stream());
+  hipFree(h->d.gam);
+  hipFree(h->d.lam);
+  hipFree(h->d.dims);
+  hipFree(h->d.theta);
+  hipFree(h->d.work);
+  hipFree(h->d.sig);
+  hipFree(h->d.perm);
+  hipFree(h->d.flags);
+  hipFree(h->d.vec);
+  hipFree(h->d.tmp);
+  hipFree(h->d.scal);
+  if (h->d.env) hipFree(h->d.env);
+  if (h->gw) hipFree(h->gw);
+  delete h;
+  return AQC_OK;
+}
+
+int aqc_mps_jacobi_stats(aqc_mps_t h, int* max_sweeps) {
+  AQC_REQUIRE(h && max_sweeps, "aqc_mps_jacobi_stats: null argument");
+  hipStream_t st = aqc::mps_stream();
+  int f[3] = {0, 0, 0};
+  AQC_HIP_CHECK(hipMemcpyAsync(f, h->d.flags, sizeof(f), hipMemcpyDeviceToHost, st));
+  AQC_HIP_CHECK(hipStreamSynchronize(st));
+  *max_sweeps = f[2];
+  int z = 0;
+  AQC_HIP_CHECK(hipMemcpy(h->d.flags + 2, &z, sizeof(int), hipMemcpyHostToDevice));
+  return AQC_OK;
+}
+
+int aqc_mps_set_jacobi_tol(double factor) {
+  AQC_REQUIRE(factor > 0, "aqc_mps_set_jacobi_tol: factor must be positive");
+  g_jacobi_tol_factor = factor;
+  return AQC_OK;
+}
+
+int aqc_mps_set_truncation(aqc_mps_t h, double threshold, int max_chi) {
+  AQC_REQUIRE(h, "aqc_mps_set_truncation: null handle");
+  h->thr = threshold;
+  h->max_chi = max_chi;
+  return AQC_OK;
+}
+
+int aqc_mps_set_vidal(aqc_mps_t h, const int* dims, const double* gammas, const double* lambdas) {
+  AQC_REQUIRE(h && dims && gammas && lambdas, "aqc_mps_set_vidal: null argument");
+  const int n = h->d.n, cap = h->d.cap;
+  AQC_REQUIRE(dims[0] == 1 && dims[n] == 1, "aqc_mps_set_vidal: dims[0] and dims[n] must be 1");
+  for (int b = 0; b <= n; ++b) {
+    if (dims[b] < 1 || dims[b] > cap) {
+      aqc::set_error("aqc_mps_set_vidal: bond dimension exceeds chi_cap");
+      return AQC_ERR_ARG;
+    }
+  }
+  std::vector<cplx> g((size_t)n * 2 * cap * cap, aqc::cmk(0, 0));
+  std::vector<double> l((size_t)(n + 1) * cap, 0.0);
+  size_t off = 0;
+  for (int i = 0; i < n; ++i)
+    for (int s = 0; s < 2; ++s)
+      for (int a = 0; a < dims[i]; ++a)
+        for (int b = 0; b < dims[i + 1]; ++b, ++off)
+          g[(size_t)i * 2 * cap * cap + (size_t)s * cap * cap + (size_t)a * cap + b] =
+              aqc::cmk(gammas[2 * off], gammas[2 * off + 1]);
+  l[0] = 1.0;
+  l[(size_t)n * cap] = 1.0;
+  size_t lo = 0;
+  for (int b = 1; b < n; ++b)
+    for (int k = 0; k < dims[b]; ++k) l[(size_t)b * cap + k] = lambdas[lo++];
+  hipStream_t st = aqc::mps_stream();
+  AQC_HIP_CHECK(hipStreamSynchronize(st));
+  AQC_HIP_CHECK(hipMemcpy(h->d.gam, g.data(), g.size() * sizeof(cplx), hipMemcpyHostToDevice));
+  AQC_HIP_CHECK(hipMemcpy(h->d.lam, l.data(), l.size() * sizeof(double), hipMemcpyHostToDevice));
+  AQC_HIP_CHECK(hipMemcpy(h->d.dims, dims, (n + 1) * sizeof(int), hipMemcpyHostToDevice));
+  for (int i = 0; i < n; ++i) h->order[i] = h->loc[i] = i;
+  return AQC_OK;
+}
+
+int aqc_mps_get_dims(aqc_mps_t h, int* dims) {
+  AQC_REQUIRE(h && dims, "aqc_mps_get_dims: null argument");
+  hipStream_t st = aqc::mps_stream();
+  AQC_HIP_CHECK(hipMemcpyAsync(dims, h->d.dims, (h->d.n + 1) * sizeof(int), hipMemcpyDeviceToHost, st));
+  AQC_HIP_CHECK(hipStreamSynchronize(st));
+  return AQC_OK;
+}
+
+int aqc_mps_sort(aqc_mps_t h) {
+  AQC_REQUIRE(h, "aqc_mps_sort: null handle");
+  if (is_sorted_order(h)) return AQC_OK;
+  int rc = do_sort(&h, 1);
+  if (rc != AQC_OK) return rc;
+  return check_flags(h);
+}
+
+int aqc_mps_sort_batch(aqc_mps_t* hs, int ns) {
+  AQC_REQUIRE(hs && ns >= 0, "aqc_mps_sort_batch: bad arguments");
+  int rc = do_sort(hs, ns);
+  if (rc != AQC_OK) return rc;
+  for (int s = 0; s < ns; ++s) {
+    rc = check_flags(hs[s]);
+    if (rc != AQC_OK) return rc;
+  }
+  return AQC_OK;
+}
+
+int aqc_mps_get_vidal(aqc_mps_t h, int* dims, double* gammas, double* lambdas) {
+  AQC_REQUIRE(h && dims, "aqc_mps_get_vidal: null argument");
+  int rc = aqc_mps_sort(h);
+  if (rc != AQC_OK) return rc;
+  rc = aqc_mps_get_dims(h, dims);
+  if (rc != AQC_OK) return rc;
+  if (!gammas || !lambdas) return AQC_OK;
+  const int n = h->d.n, cap = h->d.cap;
+  std::vector<cplx> g((size_t)n * 2 * cap * cap);
+  std::vector<double> l((size_t)(n + 1) * cap);
+  AQC_HIP_CHECK(hipMemcpy(g.data(), h->d.gam, g.size() * sizeof(cplx), hipMemcpyDeviceToHost));
+  AQC_HIP_CHECK(hipMemcpy(l.data(), h->d.lam, l.size() * sizeof(double), hipMemcpyDeviceToHost));
+  size_t off = 0;
+  for (int i = 0; i < n; ++i)
+    for (int s = 0; s < 2; ++s)
+      for (int a = 0; a < dims[i]; ++a)
+        for (int b = 0; b < dims[i + 1]; ++b, ++off) {
+          const cplx v = g[(size_t)i * 2 * cap * cap + (size_t)s * cap * cap + (size_t)a * cap + b];
+          gammas[2 * off] = v.x;
+          gammas[2 * off + 1] = v.y;
+        }
+  size_t lo = 0;
+  for (int b = 1; b < n; ++b)
+    for (int k = 0; k < dims[b]; ++k) lambdas[lo++] = l[(size_t)b * cap + k];
+  return AQC_OK;
+}
+
+int aqc_mps_copy(aqc_mps_t dst, const aqc_mps_t src) {
+  AQC_REQUIRE(dst && src && dst->d.n == src->d.n && dst->d.cap == src->d.cap, "aqc_mps_copy: handle mismatch");
+  hipStream_t st = aqc::mps_stream();
+  const size_t cap = src->d.cap, n = src->d.n;
+  AQC_HIP_CHECK(hipMemcpyAsync(dst->d.gam, src->d.gam, n * 2 * cap * cap * sizeof(cplx), hipMemcpyDeviceToDevice, st));
+  AQC_HIP_CHECK(hipMemcpyAsync(dst->d.lam, src->d.lam, (n + 1) * cap * sizeof(double), hipMemcpyDeviceToDevice, st));
+  AQC_HIP_CHECK(hipMemcpyAsync(dst->d.dims, src->d.dims, (n + 1) * sizeof(int), hipMemcpyDeviceToDevice, st));
+  dst->order = src->order;
+  dst->loc = src->loc;
+  return AQC_OK;
+}
+
+int aqc_mps_apply_batch(aqc_mps_t* hs, int ns, const aqc_op_t* const* ops, const int* nops) {
+  AQC_REQUIRE(hs && ops && nops && ns >= 0, "aqc_mps_apply_batch: null argument");
+  std::vector<std::vector<DevOp>> lists(ns);
+  for (int s = 0; s < ns; ++s) {
+    AQC_REQUIRE(hs[s], "aqc_mps_apply_batch: null handle");
+    int rc = validate_ops(hs[s], ops[s], nops[s]);
+    if (rc != AQC_OK) return rc;
+  }
+  for (int s = 0; s < ns; ++s) schedule(hs[s], ops[s], nops[s], false, lists[s]);
+  int rc = run_waves(hs, ns, lists);
+  if (rc != AQC_OK) return rc;
+  for (int s = 0; s < ns; ++s) {
+    rc = check_flags(hs[s]);
+    if (rc != AQC_OK) return rc;
+  }
+  return AQC_OK;
+}
+
+int aqc_mps_apply(aqc_mps_t h, const aqc_op_t* ops, int nops) {
+  return aqc_mps_apply_batch(&h, 1, &ops, &nops);
+}
+
+int aqc_mps_overlap_zero_batch(aqc_mps_t* hs, int ns, double* out) {
+  AQC_REQUIRE(hs && out && ns >= 0, "aqc_mps_overlap_zero_batch: null argument");
+  if (ns == 0) return AQC_OK;
+  int rc = aqc_mps_sort_batch(hs, ns);
+  if (rc != AQC_OK) return rc;
+  std::vector<MeasJob> jobs(ns);
+  for (int s = 0; s < ns; ++s) jobs[s] = make_meas(hs[s], hs[s]->d.scal);
+  const MeasJob* dj = nullptr;
+  rc = upload_jobs(jobs, &dj);
+  if (rc != AQC_OK) return rc;
+  hipStream_t st = aqc::mps_stream();
+  double bytes = 0;
+  for (int s = 0; s < ns; ++s) bytes += (double)hs[s]->d.n * hs[s]->d.cap * hs[s]->d.cap * 16.0;
+  aqc::KernelTimer::begin(st, "mps_overlap0", bytes, bytes / 2.0);
+  hipLaunchKernelGGL(k_overlap_zero, dim3(ns), dim3(kT), 0, st, dj);
+  aqc::KernelTimer::end(st);
+  AQC_CHECK_LAUNCH();
+  for (int s = 0; s < ns; ++s) {
+    cplx v;
+    AQC_HIP_CHECK(hipMemcpyAsync(&v, hs[s]->d.scal, sizeof(cplx), hipMemcpyDeviceToHost, st));
+    AQC_HIP_CHECK(hipStreamSynchronize(st));
+    // mps_dot(psi, zero) = <psi|0..0> = conj(amplitude of |0..0>)
+    out[2 * s] = v.x;
+    out[2 * s + 1] = -v.y;
+  }
+  return AQC_OK;
+}
+
+int aqc_mps_overlap_zero(aqc_mps_t h, double* re, double* im) {
+  AQC_REQUIRE(re && im, "aqc_mps_overlap_zero: null argument");
+  double o[2];
+  int rc = aqc_mps_overlap_zero_batch(&h, 1, o);
+  *re = o[0];
+  *im = o[1];
+  return rc;
+}
+
+int aqc_mps_amps_hw1(aqc_mps_t h, double* out) {
+  AQC_REQUIRE(h && out, "aqc_mps_amps_hw1: null argument");
+  int rc = aqc_mps_sort(h);
+  if (rc != AQC_OK) return rc;
+  std::vector<MeasJob> jobs(1, make_meas(h, h->d.scal));
+  const MeasJob* dj = nullptr;
+  rc = upload_jobs(jobs, &dj);
+  if (rc != AQC_OK) return rc;
+  hipStream_t st = aqc::mps_stream();
+  hipLaunchKernelGGL(k_zero_chains, dim3(1, 2), dim3(kT), 0, st, dj);
+  AQC_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_hw1, dim3(h->d.n, 1), dim3(kT), 0, st, dj);
+  AQC_CHECK_LAUNCH();
+  AQC_HIP_CHECK(hipMemcpyAsync(out, h->d.scal, 2 * h->d.n * sizeof(double), hipMemcpyDeviceToHost, st));
+  AQC_HIP_CHECK(hipStreamSynchronize(st));
+  return AQC_OK;
+}
+
+static int ensure_env(aqc_mps_t h) {
+  if (h->d.env) return AQC_OK;
+  const size_t cap = h->d.cap;
+  AQC_HIP_CHECK(hipMalloc(&h->d.env, 2 * (size_t)(h->d.n + 1) * cap * cap * sizeof(cplx)));
+  return AQC_OK;
+}
+
+int aqc_mps_dot(aqc_mps_t a, aqc_mps_t b, double* re, double* im) {
+  AQC_REQUIRE(a && b && re && im && a->d.n == b->d.n, "aqc_mps_dot: bad arguments");
+  int rc = aqc_mps_sort(a);
+  if (rc != AQC_OK) return rc;
+  rc = aqc_mps_sort(b);
+  if (rc != AQC_OK) return rc;
+  rc = ensure_env(a);
+  if (rc != AQC_OK) return rc;
+  // env scratch sized for max(cap)
+  const int cap = std::max(a->d.cap, b->d.cap);
+  EnvJob j;
+  std::memset(&j, 0, sizeof(j));
+  if (a->d.cap != b->d.cap) {
+    aqc::set_error("aqc_mps_dot: both MPS must share chi_cap");
+    return AQC_ERR_ARG;
+  }
+  j.ga = a->d.gam;
+  j.la = a->d.lam;
+  j.da = a->d.dims;
+  j.gb = b->d.gam;
+  j.lb = b->d.lam;
+  j.db = b->d.dims;
+  j.n = a->d.n;
+  j.cap = cap;
+  j.env = a->d.env;
+  j.tmp = a->d.tmp;
+  j.keep_all = 0;
+  j.right = 0;
+  j.out = a->d.scal;
+  std::vector<EnvJob> jobs(1, j);
+  const EnvJob* dj = nullptr;
+  rc = upload_jobs(jobs, &dj);
+  if (rc != AQC_OK) return rc;
+  hipStream_t st = aqc::mps_stream();
+  hipLaunchKernelGGL(k_env, dim3(1), dim3(kT), 0, st, dj);
+  AQC_CHECK_LAUNCH();
+  cplx v;
+  AQC_HIP_CHECK(hipMemcpyAsync(&v, a->d.scal, sizeof(cplx), hipMemcpyDeviceToHost, st));
+  AQC_HIP_CHECK(hipStreamSynchronize(st));
+  *re = v.x;
+  *im = v.y;
+  return AQC_OK;
+}
+
+int aqc_mps_z_all(aqc_mps_t h, double* out) {
+  AQC_REQUIRE(h && out, "aqc_mps_z_all: null argument");
+  int rc = aqc_mps_sort(h);
+  if (rc != AQC_OK) return rc;
+  rc = ensure_env(h);
+  if (rc != AQC_OK) return rc;
+  const int n = h->d.n;
+  const size_t cc = (size_t)h->d.cap * h->d.cap;
+  cplx* Lenv = h->d.env;
+  cplx* Renv = h->d.env + (size_t)(n + 1) * cc;
+  // right chain needs its own tmp: use the theta workspace (4 cap^2 >= 2 cap^2)
+  EnvJob jl;
+  std::memset(&jl, 0, sizeof(jl));
+  jl.ga = jl.gb = h->d.gam;
+  jl.la = jl.lb = h->d.lam;
+  jl.da = jl.db = h->d.dims;
+  jl.n = n;
+  jl.cap = h->d.cap;
+  jl.env = Lenv;
+  jl.tmp = h->d.tmp;
+  jl.keep_all = 1;
+  jl.right = 0;
+  jl.out = nullptr;
+  EnvJob jr = jl;
+  jr.env = Renv;
+  jr.tmp = h->d.theta;
+  jr.right = 1;
+  std::vector<EnvJob> jobs = {jl, jr};
+  const EnvJob* dj = nullptr;
+  rc = upload_jobs(jobs, &dj);
+  if (rc != AQC_OK) return rc;
+  hipStream_t st = aqc::mps_stream();
+  hipLaunchKernelGGL(k_env, dim3(2), dim3(kT), 0, st, dj);
+  AQC_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_zexp, dim3(n), dim3(kT), 0, st, h->d.gam, h->d.lam, h->d.dims, n, h->d.cap, Lenv, Renv,
+                     h->d.scal);
+  AQC_CHECK_LAUNCH();
+  std::vector<cplx> z(n);
+  AQC_HIP_CHECK(hipMemcpyAsync(z.data(), h->d.scal, n * sizeof(cplx), hipMemcpyDeviceToHost, st));
+  AQC_HIP_CHECK(hipStreamSynchronize(st));
+  for (int i = 0; i < n; ++i) out[i] = z[i].x;
+  return AQC_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,435 @@
+// Statevector engine: replaces Aer's statevector_simulator as driven by
+// adaptaqc/backends/aer_sv_backend.py:37-59.
+//
+// Layout: 2^n interleaved complex128 amplitudes, little-endian (qubit q = bit q of the index).
+// Gates are fused on the host into "segments": a run of gates (reordered only across gates on
+// disjoint qubits) whose qubits fit in a K-bit tile.  One launch per segment: each workgroup
+// gathers the 2^K amplitudes of one tile (tile bits = segment qubits padded with the lowest
+// free bits, so global reads are contiguous runs), applies every gate of the segment in LDS,
+// and writes the tile back.  A segment therefore costs one HBM/MALL pass (32 * 2^n bytes)
+// regardless of how many gates it holds.
+#include <algorithm>
+#include <cstring>
+
+#include "aqc_internal.h"
+
+using aqc::cplx;
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kMaxTileBits = 12;
+
+struct SegGate {
+  int32_t nq;  // 1 or 2
+  int32_t t0;  // local bit of q0
+  int32_t t1;  // local bit of q1 (2q only)
+  int32_t pad;
+  cplx m[16];
+};
+
+struct SegHeader {
+  int32_t tilebits[kMaxTileBits];  // ascending global bit positions
+  int32_t gate_off;                // index into gate array
+  int32_t ngates;
+  int32_t pad[2];
+};
+
+__device__ __forceinline__ uint64_t insert_zero(uint64_t v, int b) {
+  uint64_t lo = v & ((1ull << b) - 1ull);
+  return ((v >> b) << (b + 1)) | lo;
+}
+
+template <int K>
+__global__ __launch_bounds__(kThreads) void k_sv_segment(cplx* __restrict__ state, int n,
+                                                         const SegHeader* __restrict__ hdr,
+                                                         const SegGate* __restrict__ gates) {
+  __shared__ cplx tile[1 << K];
+  __shared__ SegGate g_s;
+  constexpr int kPer = (1 << K) / kThreads > 0 ? (1 << K) / kThreads : 1;
+  const int tid = threadIdx.x;
+  int tb[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) tb[j] = hdr->tilebits[j];
+  // base index: blockIdx bits scattered into the non-tile positions
+  uint64_t base = blockIdx.x;
+#pragma unroll
+  for (int j = 0; j < K; ++j) base = insert_zero(base, tb[j]);
+  uint64_t gidx[kPer];
+#pragma unroll
+  for (int r = 0; r < kPer; ++r) {
+    int x = tid + r * kThreads;
+    uint64_t g = base;
+#pragma unroll
+    for (int j = 0; j < K; ++j) g |= (uint64_t)((x >> j) & 1) << tb[j];
+    gidx[r] = g;
+    if (x < (1 << K)) tile[x] = state[g];
+  }
+  const int ng = hdr->ngates;
+  const SegGate* gp = gates + hdr->gate_off;
+  for (int gi = 0; gi < ng; ++gi) {
+    __syncthreads();
+    if (tid < (int)(sizeof(SegGate) / 8)) {
+      reinterpret_cast<double*>(&g_s)[tid] = reinterpret_cast<const double*>(gp + gi)[tid];
+    }
+    __syncthreads();
+    if (g_s.nq == 1) {
+      const int t = g_s.t0;
+      const cplx m00 = g_s.m[0], m01 = g_s.m[1], m10 = g_s.m[2], m11 = g_s.m[3];
+      for (int p = tid; p < (1 << (K - 1)); p += kThreads) {
+        int i0 = (int)insert_zero((uint64_t)p, t);
+        int i1 = i0 | (1 << t);
+        cplx a0 = tile[i0], a1 = tile[i1];
+        tile[i0] = aqc::cfma(m01, a1, aqc::cmul(m00, a0));
+        tile[i1] = aqc::cfma(m11, a1, aqc::cmul(m10, a0));
+      }
+    } else if constexpr (K >= 2) {
+      const int t0 = g_s.t0, t1 = g_s.t1;
+      const int lo = t0 < t1 ? t0 : t1, hi = t0 < t1 ? t1 : t0;
+      for (int p = tid; p < (1 << (K - 2)); p += kThreads) {
+        int b = (int)insert_zero(insert_zero((uint64_t)p, lo), hi);
+        int idx[4];
+        cplx v[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          idx[s] = b | ((s & 1) << t0) | ((s >> 1) << t1);
+          v[s] = tile[idx[s]];
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          cplx acc = aqc::cmul(g_s.m[4 * r], v[0]);
+          acc = aqc::cfma(g_s.m[4 * r + 1], v[1], acc);
+          acc = aqc::cfma(g_s.m[4 * r + 2], v[2], acc);
+          acc = aqc::cfma(g_s.m[4 * r + 3], v[3], acc);
+          tile[idx[r]] = acc;
+        }
+      }
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < kPer; ++r) {
+    int x = tid + r * kThreads;
+    if (x < (1 << K)) state[gidx[r]] = tile[x];
+  }
+}
+
+// Per-workgroup partial probabilities: out[wg * (n+1) + i] = sum |a|^2 over amplitudes of this
+// workgroup with bit i set (i < n); out[wg*(n+1)+n] = total.
+constexpr int kZChunk = 16;  // amplitudes per thread
+__global__ __launch_bounds__(kThreads) void k_sv_zpartial(const cplx* __restrict__ state, int n,
+                                                          double* __restrict__ out) {
+  __shared__ double red[kThreads];
+  const int tid = threadIdx.x;
+  const uint64_t dim = 1ull << n;
+  const uint64_t base = (uint64_t)blockIdx.x * (kThreads * kZChunk);
+  double tot = 0.0;
+  double pj[kZChunk];
+#pragma unroll
+  for (int j = 0; j < kZChunk; ++j) {
+    uint64_t x = base + tid + (uint64_t)j * kThreads;
+    double p = 0.0;
+    if (x < dim) p = aqc::cnorm2(state[x]);
+    pj[j] = p;
+    tot += p;
+  }
+  // bits 8..11 vary with j (kThreads = 256 = 2^8)
+  double hi4[4];
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    double s = 0;
+#pragma unroll
+    for (int j = 0; j < kZChunk; ++j)
+      if ((j >> b) & 1) s += pj[j];
+    hi4[b] = s;
+  }
+  for (int i = 0; i <= n; ++i) {
+    double c;
+    if (i == n) {
+      c = tot;
+    } else if (i < 8) {
+      c = ((tid >> i) & 1) ? tot : 0.0;
+    } else if (i < 12) {
+      c = hi4[i - 8];
+    } else {
+      c = ((base >> i) & 1ull) ? tot : 0.0;
+    }
+    red[tid] = c;
+    __syncthreads();
+    for (int s = kThreads / 2; s > 0; s >>= 1) {
+      if (tid < s) red[tid] += red[tid + s];
+      __syncthreads();
+    }
+    if (tid == 0) out[(uint64_t)blockIdx.x * (n + 1) + i] = red[0];
+    __syncthreads();
+  }
+}
+
+__global__ void k_sv_zfinal(const double* __restrict__ part, int nwg, int n, double* __restrict__ z) {
+  const int i = threadIdx.x;
+  if (i > n) return;
+  double s = 0.0, t = 0.0;
+  for (int w = 0; w < nwg; ++w) {
+    s += part[(uint64_t)w * (n + 1) + i];
+    t += part[(uint64_t)w * (n + 1) + n];
+  }
+  if (i < n) z[i] = t - 2.0 * s;  // p0 - p1 with p0 = total - p1
+}
+
+__global__ void k_sv_reset(cplx* state, uint64_t dim) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i < dim; i += (uint64_t)gridDim.x * blockDim.x) state[i] = aqc::cmk(i == 0 ? 1.0 : 0.0, 0.0);
+}
+
+// ---- host-side segmentation -------------------------------------------------------------
+struct HostSeg {
+  std::vector<int> gates;  // indices into op list, in application order
+  uint64_t qmask = 0;
+};
+
+std::vector<HostSeg> build_segments(const aqc_op_t* ops, int nops, int K, int n) {
+  std::vector<HostSeg> segs;
+  std::vector<char> done(nops, 0);
+  int remaining = nops;
+  int first = 0;
+  while (remaining > 0) {
+    while (first < nops && done[first]) ++first;
+    HostSeg seg;
+    uint64_t blocked = 0;
+    for (int i = first; i < nops; ++i) {
+      if (done[i]) continue;
+      uint64_t gm = (1ull << ops[i].q0);
+      if (ops[i].nq == 2) gm |= (1ull << ops[i].q1);
+      if (gm & blocked) {
+        blocked |= gm;
+      } else {
+        uint64_t u = seg.qmask | gm;
+        if (__builtin_popcountll(u) <= K) {
+          seg.qmask = u;
+          seg.gates.push_back(i);
+          done[i] = 1;
+          --remaining;
+        } else {
+          blocked |= gm;
+        }
+      }
+      if (__builtin_popcountll(blocked) >= n) break;
+    }
+    segs.push_back(std::move(seg));
+  }
+  return segs;
+}
+
+}  // namespace
+
+struct aqc_sv_s {
+  int n = 0;
+  int K = 0;
+  cplx* state = nullptr;
+  hipStream_t stream = nullptr;
+  SegHeader* d_hdr = nullptr;
+  size_t hdr_cap = 0;
+  SegGate* d_gates = nullptr;
+  size_t gate_cap = 0;
+  double* d_zpart = nullptr;
+  double* d_z = nullptr;
+  int zwg = 0;
+  cplx* h_pinned = nullptr;
+};
+
+static int sv_launch_segment(aqc_sv_t h, const SegHeader* dh, const SegGate* dg, int nblocks) {
+  const double bytes = 32.0 * (double)(1ull << h->n);
+  aqc::KernelTimer::begin(h->stream, "sv_segment", bytes, 0.0);
+  switch (h->K) {
+#define AQC_SEG_CASE(KK)                                                                   \
+  case KK:                                                                                 \
+    hipLaunchKernelGGL(k_sv_segment<KK>, dim3(nblocks), dim3(kThreads), 0, h->stream,      \
+                       h->state, h->n, dh, dg);                                            \
+    break;
+    AQC_SEG_CASE(1)
+    AQC_SEG_CASE(2)
+    AQC_SEG_CASE(3)
+    AQC_SEG_CASE(4)
+    AQC_SEG_CASE(5)
+    AQC_SEG_CASE(6)
+    AQC_SEG_CASE(7)
+    AQC_SEG_CASE(8)
+    AQC_SEG_CASE(9)
+    AQC_SEG_CASE(10)
+    AQC_SEG_CASE(11)
+#undef AQC_SEG_CASE
+    default:
+      aqc::set_error("sv: unsupported tile size");
+      return AQC_ERR_UNSUPPORTED;
+  }
+  aqc::KernelTimer::end(h->stream);
+  AQC_CHECK_LAUNCH();
+  return AQC_OK;
+}
+
+extern "C" {
+
+int aqc_sv_create(int n, aqc_sv_t* out) {
+  AQC_REQUIRE(out != nullptr, "aqc_sv_create: null out");
+  AQC_REQUIRE(n >= 1 && n <= 34, "aqc_sv_create: n must be in [1, 34]");
+  auto* h = new aqc_sv_s();
+  h->n = n;
+  h->K = n < 10 ? n : 10;
+  const uint64_t dim = 1ull << n;
+  hipError_t e = hipMalloc(&h->state, dim * sizeof(cplx));
+  if (e != hipSuccess) {
+    delete h;
+    aqc::set_error(std::string("aqc_sv_create: hipMalloc state: ") + hipGetErrorString(e));
+    return AQC_ERR_NOMEM;
+  }
+  AQC_HIP_CHECK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+  h->zwg = (int)((dim + kThreads * kZChunk - 1) / (kThreads * kZChunk));
+  AQC_HIP_CHECK(hipMalloc(&h->d_zpart, sizeof(double) * (size_t)h->zwg * (n + 1)));
+  AQC_HIP_CHECK(hipMalloc(&h->d_z, sizeof(double) * (n + 1)));
+  AQC_HIP_CHECK(hipHostMalloc(&h->h_pinned, sizeof(cplx) * 64, hipHostMallocDefault));
+  *out = h;
+  return aqc_sv_reset(h);
+}
+
+int aqc_sv_destroy(aqc_sv_t h) {
+  if (!h) return AQC_OK;
+  if (h->stream) hipStreamSynchronize(h->stream);
+  hipFree(h->state);
+  hipFree(h->d_hdr);
+  hipFree(h->d_gates);
+  hipFree(h->d_zpart);
+  hipFree(h->d_z);
+  if (h->h_pinned) hipHostFree(h->h_pinned);
+  if (h->stream) hipStreamDestroy(h->stream);
+  delete h;
+  return AQC_OK;
+}
+
+int aqc_sv_reset(aqc_sv_t h) {
+  AQC_REQUIRE(h, "aqc_sv_reset: null handle");
+  const uint64_t dim = 1ull << h->n;
+  unsigned grid = (unsigned)std::min<uint64_t>((dim + 255) / 256, 65536);
+  hipLaunchKernelGGL(k_sv_reset, dim3(grid), dim3(256), 0, h->stream, h->state, dim);
+  AQC_CHECK_LAUNCH();
+  return AQC_OK;
+}
+
+int aqc_sv_copy(aqc_sv_t dst, const aqc_sv_t src) {
+  AQC_REQUIRE(dst && src && dst->n == src->n, "aqc_sv_copy: handle mismatch");
+  AQC_HIP_CHECK(hipStreamSynchronize(src->stream));
+  AQC_HIP_CHECK(hipMemcpyAsync(dst->state, src->state, sizeof(cplx) << dst->n,
+                               hipMemcpyDeviceToDevice, dst->stream));
+  return AQC_OK;
+}
+
+int aqc_sv_apply(aqc_sv_t h, const aqc_op_t* ops, int nops) {
+  AQC_REQUIRE(h, "aqc_sv_apply: null handle");
+  if (nops <= 0) return AQC_OK;
+  AQC_REQUIRE(ops, "aqc_sv_apply: null ops");
+  for (int i = 0; i < nops; ++i) {
+    const aqc_op_t& o = ops[i];
+    AQC_REQUIRE(o.nq == 1 || o.nq == 2, "aqc_sv_apply: only 1- and 2-qubit ops are supported");
+    AQC_REQUIRE(o.q0 >= 0 && o.q0 < h->n, "aqc_sv_apply: qubit index out of range");
+    if (o.nq == 2) {
+      AQC_REQUIRE(o.q1 >= 0 && o.q1 < h->n && o.q1 != o.q0, "aqc_sv_apply: bad second qubit");
+    }
+  }
+  const int K = h->K;
+  std::vector<HostSeg> segs = build_segments(ops, nops, K, h->n);
+  std::vector<SegHeader> hdr(segs.size());
+  std::vector<SegGate> gts;
+  gts.reserve(nops);
+  for (size_t s = 0; s < segs.size(); ++s) {
+    // tile bits: segment qubits + lowest free bits up to K
+    uint64_t mask = segs[s].qmask;
+    for (int b = 0; b < h->n && __builtin_popcountll(mask) < K; ++b) mask |= (1ull << b);
+    int pos[64];
+    int cnt = 0;
+    for (int b = 0; b < h->n; ++b)
+      if ((mask >> b) & 1ull) pos[cnt++] = b;
+    std::memset(&hdr[s], 0, sizeof(SegHeader));
+    int local_of[64];
+    for (int j = 0; j < cnt; ++j) {
+      hdr[s].tilebits[j] = pos[j];
+      local_of[pos[j]] = j;
+    }
+    hdr[s].gate_off = (int)gts.size();
+    hdr[s].ngates = (int)segs[s].gates.size();
+    for (int gi : segs[s].gates) {
+      const aqc_op_t& o = ops[gi];
+      SegGate g;
+      std::memset(&g, 0, sizeof(g));
+      g.nq = o.nq;
+      g.t0 = local_of[o.q0];
+      g.t1 = o.nq == 2 ? local_of[o.q1] : 0;
+      const int nel = o.nq == 1 ? 4 : 16;
+      for (int e = 0; e < nel; ++e) g.m[e] = aqc::cmk(o.m[2 * e], o.m[2 * e + 1]);
+      gts.push_back(g);
+    }
+  }
+  if (hdr.size() > h->hdr_cap) {
+    AQC_HIP_CHECK(hipStreamSynchronize(h->stream));
+    hipFree(h->d_hdr);
+    h->hdr_cap = hdr.size() * 2;
+    AQC_HIP_CHECK(hipMalloc(&h->d_hdr, sizeof(SegHeader) * h->hdr_cap));
+  }
+  if (gts.size() > h->gate_cap) {
+    AQC_HIP_CHECK(hipStreamSynchronize(h->stream));
+    hipFree(h->d_gates);
+    h->gate_cap = gts.size() * 2;
+    AQC_HIP_CHECK(hipMalloc(&h->d_gates, sizeof(SegGate) * h->gate_cap));
+  }
+  // The previous call's launches may still read these buffers: order the copy on the stream.
+  AQC_HIP_CHECK(hipMemcpyAsync(h->d_hdr, hdr.data(), sizeof(SegHeader) * hdr.size(),
+                               hipMemcpyHostToDevice, h->stream));
+  AQC_HIP_CHECK(hipMemcpyAsync(h->d_gates, gts.data(), sizeof(SegGate) * gts.size(),
+                               hipMemcpyHostToDevice, h->stream));
+  // hipMemcpyAsync from pageable memory is staged before returning, so hdr/gts may go out
+  // of scope; synchronising keeps that guarantee explicit.
+  AQC_HIP_CHECK(hipStreamSynchronize(h->stream));
+  const int nblocks = (int)(1ull << (h->n - K));
+  for (size_t s = 0; s < hdr.size(); ++s) {
+    int rc = sv_launch_segment(h, h->d_hdr + s, h->d_gates, nblocks);
+    if (rc != AQC_OK) return rc;
+  }
+  return AQC_OK;
+}
+
+int aqc_sv_amp0(aqc_sv_t h, double* re, double* im) {
+  AQC_REQUIRE(h && re && im, "aqc_sv_amp0: null argument");
+  AQC_HIP_CHECK(hipMemcpyAsync(h->h_pinned, h->state, sizeof(cplx), hipMemcpyDeviceToHost, h->stream));
+  AQC_HIP_CHECK(hipStreamSynchronize(h->stream));
+  *re = h->h_pinned[0].x;
+  *im = h->h_pinned[0].y;
+  return AQC_OK;
+}
+
+int aqc_sv_z_all(aqc_sv_t h, double* out) {
+  AQC_REQUIRE(h && out, "aqc_sv_z_all: null argument");
+  aqc::KernelTimer::begin(h->stream, "sv_zall", 16.0 * (double)(1ull << h->n), 0.0);
+  hipLaunchKernelGGL(k_sv_zpartial, dim3(h->zwg), dim3(kThreads), 0, h->stream, h->state, h->n,
+                     h->d_zpart);
+  aqc::KernelTimer::end(h->stream);
+  AQC_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_sv_zfinal, dim3(1), dim3(64), 0, h->stream, h->d_zpart, h->zwg, h->n, h->d_z);
+  AQC_CHECK_LAUNCH();
+  AQC_HIP_CHECK(hipMemcpyAsync(out, h->d_z, sizeof(double) * h->n, hipMemcpyDeviceToHost, h->stream));
+  AQC_HIP_CHECK(hipStreamSynchronize(h->stream));
+  return AQC_OK;
+}
+
+int aqc_sv_get(aqc_sv_t h, double* out) {
+  AQC_REQUIRE(h && out, "aqc_sv_get: null argument");
+  AQC_HIP_CHECK(hipMemcpyAsync(out, h->state, sizeof(cplx) << h->n, hipMemcpyDeviceToHost, h->stream));
+  AQC_HIP_CHECK(hipStreamSynchronize(h->stream));
+  return AQC_OK;
+}
+
+int aqc_sv_set(aqc_sv_t h, const double* in) {
+  AQC_REQUIRE(h && in, "aqc_sv_set: null argument");
+  AQC_HIP_CHECK(hipMemcpyAsync(h->state, in, sizeof(cplx) << h->n, hipMemcpyHostToDevice, h->stream));
+  AQC_HIP_CHECK(hipStreamSynchronize(h->stream));
+  return AQC_OK;
+}
+
+}  // extern "C"

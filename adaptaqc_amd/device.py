@@ -1,0 +1,219 @@
+"""Owning Python wrappers around libaqchip handles (device-resident statevector / MPS)."""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+
+
+class DeviceSV:
+    """2^n complex128 amplitudes resident in HBM (Aer statevector_simulator state)."""
+
+    def __init__(self, n):
+        self._l = _lib.lib()
+        self.n = int(n)
+        h = ctypes.c_void_p()
+        _lib.check(self._l.aqc_sv_create(self.n, ctypes.byref(h)))
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None) is not None and self.h.value:
+            self._l.aqc_sv_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def reset(self):
+        _lib.check(self._l.aqc_sv_reset(self.h))
+
+    def copy_from(self, other):
+        _lib.check(self._l.aqc_sv_copy(self.h, other.h))
+
+    def apply(self, ops):
+        if len(ops) == 0:
+            return
+        arr = ops if isinstance(ops, np.ndarray) else _lib.ops_array(ops)
+        _lib.check(self._l.aqc_sv_apply(self.h, _lib.ptr(arr), len(arr)))
+
+    def amp0(self):
+        re, im = ctypes.c_double(), ctypes.c_double()
+        _lib.check(self._l.aqc_sv_amp0(self.h, ctypes.byref(re), ctypes.byref(im)))
+        return complex(re.value, im.value)
+
+    def z_all(self):
+        out = np.zeros(self.n)
+        _lib.check(self._l.aqc_sv_z_all(self.h, _lib.dptr(out)))
+        return out
+
+    def get(self):
+        out = np.zeros(2 ** self.n, dtype=np.complex128)
+        _lib.check(self._l.aqc_sv_get(self.h, _lib.ptr(out)))
+        return out
+
+    def set(self, psi):
+        psi = np.ascontiguousarray(psi, dtype=np.complex128)
+        _lib.check(self._l.aqc_sv_set(self.h, _lib.ptr(psi)))
+
+
+class DeviceMPS:
+    """Vidal-form MPS resident in HBM with Aer MPS-simulator semantics."""
+
+    def __init__(self, n, chi_cap, threshold=1e-16, max_chi=None):
+        self._l = _lib.lib()
+        self.n = int(n)
+        self.chi_cap = int(chi_cap)
+        h = ctypes.c_void_p()
+        _lib.check(
+            self._l.aqc_mps_create(self.n, self.chi_cap, float(threshold), int(max_chi or 0), ctypes.byref(h))
+        )
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None) is not None and self.h.value:
+            self._l.aqc_mps_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+    # -- state transfer --------------------------------------------------------------
+    def set_truncation(self, threshold, max_chi):
+        _lib.check(self._l.aqc_mps_set_truncation(self.h, float(threshold), int(max_chi or 0)))
+
+    def load_aer(self, qiskit_mps):
+        gam, lam = qiskit_mps
+        if len(gam) != self.n:
+            raise ValueError("MPS length mismatch")
+        dims = [1]
+        for a, _ in gam:
+            dims.append(np.asarray(a).shape[1])
+        dims = np.asarray(dims, dtype=np.int32)
+        if dims.max() > self.chi_cap:
+            raise ValueError(f"MPS bond dimension {dims.max()} exceeds chi_cap {self.chi_cap}")
+        g = np.concatenate(
+            [np.stack([np.asarray(a, dtype=np.complex128), np.asarray(b, dtype=np.complex128)]).reshape(-1) for a, b in gam]
+        )
+        l = np.concatenate([np.asarray(x, dtype=np.float64).reshape(-1) for x in lam]) if len(lam) else np.zeros(1)
+        g = np.ascontiguousarray(g)
+        l = np.ascontiguousarray(l)
+        _lib.check(self._l.aqc_mps_set_vidal(self.h, _lib.ptr(dims), _lib.ptr(g), _lib.ptr(l)))
+
+    def dims(self):
+        d = np.zeros(self.n + 1, dtype=np.int32)
+        _lib.check(self._l.aqc_mps_get_dims(self.h, _lib.ptr(d)))
+        return d
+
+    def to_aer(self):
+        """save_matrix_product_state: sorted qubits, Aer format."""
+        d = np.zeros(self.n + 1, dtype=np.int32)
+        _lib.check(self._l.aqc_mps_get_vidal(self.h, _lib.ptr(d), None, None))
+        ng = int(sum(2 * d[i] * d[i + 1] for i in range(self.n)))
+        nl = int(sum(d[1:self.n]))
+        g = np.zeros(ng, dtype=np.complex128)
+        l = np.zeros(max(nl, 1), dtype=np.float64)
+        _lib.check(self._l.aqc_mps_get_vidal(self.h, _lib.ptr(d), _lib.ptr(g), _lib.ptr(l)))
+        gam, lam = [], []
+        off = 0
+        for i in range(self.n):
+            a, b = int(d[i]), int(d[i + 1])
+            t = g[off: off + 2 * a * b].reshape(2, a, b)
+            gam.append((t[0].copy(), t[1].copy()))
+            off += 2 * a * b
+        off = 0
+        for bnd in range(1, self.n):
+            k = int(d[bnd])
+            lam.append(l[off: off + k].copy())
+            off += k
+        return gam, lam
+
+    def preprocessed(self):
+        """aqc_research ``_preprocess_mps`` form: list of (2, chi_l, chi_r) arrays."""
+        gam, lam = self.to_aer()
+        out = []
+        for i, (a, b) in enumerate(gam):
+            t = np.stack([a, b])
+            if i < self.n - 1:
+                t = t * lam[i][None, None, :]
+            out.append(t)
+        return out
+
+    def copy_from(self, other):
+        _lib.check(self._l.aqc_mps_copy(self.h, other.h))
+
+    # -- gates and measurements ------------------------------------------------------
+    def apply(self, ops):
+        if len(ops) == 0:
+            return
+        arr = ops if isinstance(ops, np.ndarray) else _lib.ops_array(ops)
+        _lib.check(self._l.aqc_mps_apply(self.h, _lib.ptr(arr), len(arr)))
+
+    def sort(self):
+        _lib.check(self._l.aqc_mps_sort(self.h))
+
+    def overlap_zero(self):
+        """``mps_dot(psi, zero_mps)`` = <psi|0...0>."""
+        re, im = ctypes.c_double(), ctypes.c_double()
+        _lib.check(self._l.aqc_mps_overlap_zero(self.h, ctypes.byref(re), ctypes.byref(im)))
+        return complex(re.value, im.value)
+
+    def dot(self, other):
+        """<self|other> (conjugates self)."""
+        re, im = ctypes.c_double(), ctypes.c_double()
+        _lib.check(self._l.aqc_mps_dot(self.h, other.h, ctypes.byref(re), ctypes.byref(im)))
+        return complex(re.value, im.value)
+
+    def z_all(self):
+        out = np.zeros(self.n)
+        _lib.check(self._l.aqc_mps_z_all(self.h, _lib.ptr(out)))
+        return out
+
+    def amps_hw1(self):
+        out = np.zeros(2 * self.n)
+        _lib.check(self._l.aqc_mps_amps_hw1(self.h, _lib.ptr(out)))
+        return out[0::2] + 1j * out[1::2]
+
+
+def _handles(states):
+    arr = (ctypes.c_void_p * len(states))(*[s.h.value for s in states])
+    return arr
+
+
+def apply_batch(states, ops_lists):
+    """Apply per-state op lists in lock-step launches."""
+    if not states:
+        return
+    l = _lib.lib()
+    arrs = [o if isinstance(o, np.ndarray) else _lib.ops_array(o) for o in ops_lists]
+    ptrs = (ctypes.c_void_p * len(arrs))(*[a.ctypes.data if len(a) else 0 for a in arrs])
+    counts = np.asarray([len(a) for a in arrs], dtype=np.int32)
+    _lib.check(l.aqc_mps_apply_batch(_handles(states), len(states), ptrs, _lib.ptr(counts)))
+
+
+def overlap_zero_batch(states):
+    l = _lib.lib()
+    out = np.zeros(2 * len(states))
+    _lib.check(l.aqc_mps_overlap_zero_batch(_handles(states), len(states), _lib.ptr(out)))
+    return out[0::2] + 1j * out[1::2]
+
+
+def pair_grads_batch(states, svec, pairs, u0, gens, degs, out=None):
+    """Per-state gradient norms for every pair; ``out`` may be a device pointer (int)."""
+    l = _lib.lib()
+    svec = np.ascontiguousarray(np.asarray(svec, dtype=np.complex128).reshape(-1))
+    pairs = np.ascontiguousarray(np.asarray(pairs, dtype=np.int32).reshape(-1))
+    u0 = np.ascontiguousarray(np.asarray(u0, dtype=np.complex128).reshape(16))
+    gens = np.ascontiguousarray(np.asarray(gens, dtype=np.complex128).reshape(-1))
+    degs = np.ascontiguousarray(np.asarray(degs, dtype=np.float64).reshape(-1))
+    npairs = len(pairs) // 2
+    ngen = len(degs)
+    if out is None:
+        host = np.zeros((len(states), npairs))
+        outp, is_dev = _lib.ptr(host), 0
+    else:
+        host, outp, is_dev = None, ctypes.c_void_p(int(out)), 1
+    _lib.check(
+        l.aqc_pair_grads_batch(
+            _handles(states), len(states), _lib.ptr(svec), _lib.ptr(pairs), npairs, _lib.ptr(u0),
+            _lib.ptr(gens) if ngen else None, _lib.ptr(degs) if ngen else None, ngen, outp, is_dev,
+        )
+    )
+    return host

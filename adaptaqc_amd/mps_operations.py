@@ -1,0 +1,176 @@
+"""GPU implementations of the ``aqc_research.mps_operations`` helpers the reference calls.
+
+Call sites: aer_mps_backend.py:49-93, gradients.py:60-110, approximate_compiler.py:133-135,198,
+adapt_compiler.py:1129.  Every function computes on the device through libaqchip; host numpy
+is used only to marshal MPS tensors in and out (Aer format / preprocessed lists).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .circuit import QuantumCircuit, device_ops
+from .device import DeviceMPS
+
+MAX_CHI_CAP = 256
+
+
+def check_mps(obj) -> bool:
+    """True for an Aer-format MPS ``(list[(G0, G1)], list[lambda])`` (constants.py:17)."""
+    try:
+        gam, lam = obj
+        if not isinstance(gam, (list, tuple)) or not isinstance(lam, (list, tuple)):
+            return False
+        if len(lam) != len(gam) - 1:
+            return False
+        for g in gam:
+            if len(g) != 2 or np.asarray(g[0]).ndim != 2:
+                return False
+        return True
+    except (TypeError, ValueError):
+        return False
+
+
+def _preprocess_mps(qiskit_mps):
+    """Gamma_i diag(lambda_i) for i < n-1 -> list of (2, chi_l, chi_r) arrays."""
+    gam, lam = qiskit_mps
+    out = []
+    for i, (a, b) in enumerate(gam):
+        t = np.stack([np.asarray(a, dtype=complex), np.asarray(b, dtype=complex)])
+        if i < len(gam) - 1:
+            t = t * np.asarray(lam[i])[None, None, :]
+        out.append(t)
+    return out
+
+
+def chi_cap_for(n, max_chi, loaded_max=1):
+    cap = int(max_chi) if max_chi else min(MAX_CHI_CAP, 2 ** (n // 2))
+    cap = max(cap, int(loaded_max), 1)
+    if cap > MAX_CHI_CAP:
+        raise NotImplementedError(f"bond dimension {cap} exceeds the supported maximum {MAX_CHI_CAP}")
+    return cap
+
+
+def _sim_options(sim):
+    if sim is None:
+        return 1e-16, None
+    o = sim.options
+    return o.matrix_product_state_truncation_threshold, o.matrix_product_state_max_bond_dimension
+
+
+def device_mps_from_circuit(circuit: QuantumCircuit, sim=None, trunc_thr=None, out: DeviceMPS | None = None):
+    """Run ``circuit`` (optionally led by set_matrix_product_state) on the device MPS engine."""
+    thr, max_chi = _sim_options(sim)
+    if trunc_thr is not None:
+        thr = trunc_thr
+    n = circuit.num_qubits
+    start = 0
+    loaded = None
+    if len(circuit.data) and circuit.data[0].operation.name == "set_matrix_product_state":
+        loaded = circuit.data[0].operation.params[0]
+        start = 1
+    lmax = max(np.asarray(a).shape[1] for a, _ in loaded[0]) if loaded is not None else 1
+    cap = chi_cap_for(n, max_chi, lmax)
+    if out is None or out.n != n or out.chi_cap < cap:
+        out = DeviceMPS(n, cap, thr, max_chi)
+    else:
+        out.set_truncation(thr, max_chi)
+    if loaded is not None:
+        out.load_aer(loaded)
+    else:
+        out.load_aer(zero_aer_mps(n))
+    out.apply(device_ops(circuit, start))
+    out.sort()
+    return out
+
+
+def zero_aer_mps(n):
+    g = (np.array([[1.0 + 0j]]), np.array([[0.0 + 0j]]))
+    return [tuple(x.copy() for x in g) for _ in range(n)], [np.ones(1) for _ in range(n - 1)]
+
+
+def mps_from_circuit(circuit: QuantumCircuit, return_preprocessed=False, sim=None, trunc_thr=None,
+                     print_log_data=False):
+    """aqc_research ``mps_from_circuit``: Aer tuple, or the preprocessed list if requested."""
+    d = device_mps_from_circuit(circuit, sim, trunc_thr)
+    return d.preprocessed() if return_preprocessed else d.to_aer()
+
+
+def _as_device(mps, already_preprocessed, like: DeviceMPS | None = None):
+    if isinstance(mps, DeviceMPS):
+        return mps
+    if not already_preprocessed and check_mps(mps):
+        aer = mps
+    else:
+        # preprocessed list: load as Gammas with unit lambdas (A_i = Gamma_i * 1)
+        aer = ([(np.asarray(t[0]), np.asarray(t[1])) for t in mps], [np.ones(np.asarray(t).shape[2]) for t in mps[:-1]])
+    n = len(aer[0])
+    lmax = max(np.asarray(a).shape[1] for a, _ in aer[0])
+    cap = like.chi_cap if like is not None and like.chi_cap >= lmax else chi_cap_for(n, None, lmax)
+    d = DeviceMPS(n, cap)
+    d.load_aer(aer)
+    return d
+
+
+def _is_zero_state(mps, pre):
+    """Host MPS equal to |0...0> (every site a (2,1,1) tensor [1, 0])."""
+    if isinstance(mps, DeviceMPS):
+        return False
+    try:
+        sites = mps if pre else _preprocess_mps(mps)
+        return all(np.shape(t) == (2, 1, 1) and t[0, 0, 0] == 1 and t[1, 0, 0] == 0 for t in sites)
+    except (TypeError, ValueError, IndexError):
+        return False
+
+
+def _to_aer_like(mps, pre):
+    if isinstance(mps, DeviceMPS):
+        return mps.to_aer(), False
+    return mps, pre
+
+
+def mps_dot(a, b, already_preprocessed=False):
+    """<a|b>, conjugating ``a`` (pinned by test_gradients.py:39-73)."""
+    if _is_zero_state(b, already_preprocessed):
+        return _as_device(a, already_preprocessed).overlap_zero()
+    if _is_zero_state(a, already_preprocessed):
+        return np.conj(_as_device(b, already_preprocessed).overlap_zero())
+    da = _as_device(a, already_preprocessed)
+    db = _as_device(b, already_preprocessed)
+    if da.chi_cap != db.chi_cap:
+        big = max(da.chi_cap, db.chi_cap)
+        if da.chi_cap != big:
+            src, pre = _to_aer_like(a, already_preprocessed)
+            da = _as_device(src, pre, db)
+        else:
+            src, pre = _to_aer_like(b, already_preprocessed)
+            db = _as_device(src, pre, da)
+    return da.dot(db)
+
+
+def mps_expectation(mps, operator, qubit, already_preprocessed=False):
+    if operator != "Z":
+        raise NotImplementedError("only Z expectations are on the hot path")
+    return float(_as_device(mps, already_preprocessed).z_all()[qubit])
+
+
+def extract_amplitude(mps, index, already_preprocessed=False):
+    d = _as_device(mps, already_preprocessed)
+    n = d.n
+    if index == 0:
+        return np.conj(d.overlap_zero())
+    if index & (index - 1) == 0:
+        i = int(index).bit_length() - 1
+        return complex(d.amps_hw1()[i])
+    basis = zero_aer_mps(n)
+    for q in range(n):
+        if (index >> q) & 1:
+            basis[0][q] = (np.array([[0.0 + 0j]]), np.array([[1.0 + 0j]]))
+    bd = DeviceMPS(n, d.chi_cap)
+    bd.load_aer(basis)
+    return bd.dot(d)
+
+
+def mps_to_vector(mps, already_preprocessed=False):
+    """Dense statevector of a (small) MPS, evaluated amplitude by amplitude on the device."""
+    d = _as_device(mps, already_preprocessed)
+    return np.array([extract_amplitude(d, i) for i in range(2 ** d.n)])

@@ -1,0 +1,188 @@
+"""Candidate-pair gradients on MI355X: drop-in for adaptaqc/utils/gradients.py:23-224.
+
+``general_grad_of_pairs`` keeps the reference signature and return value (list of floats, one
+per coupling-map pair) but evaluates every pair's generator overlaps in one device sweep over
+|psi> (libaqchip ``aqc_pair_grads``) instead of 1 + Npairs * (Ngen + [U0 != I]) Aer runs.
+Starting circuits made of 1-qubit gates give the product state |s> the sweep needs; a starting
+circuit with entangling gates takes the per-(pair, generator) device MPS route instead.
+"""
+from typing import List, Tuple
+
+import numpy as np
+
+from .. import gates as G
+from ..circuit import QuantumCircuit
+from ..device import DeviceMPS, pair_grads_batch
+from ..mps_operations import device_mps_from_circuit
+from .utilityfunctions import get_distinct_items_and_degeneracies
+
+PARAMETERISED = ("rx", "ry", "rz")
+
+
+def circuit_unitary(qc: QuantumCircuit) -> np.ndarray:
+    """Unitary of a small circuit (little-endian over its qubits)."""
+    n = qc.num_qubits
+    u = np.eye(2 ** n, dtype=complex)
+    for ins in qc.data:
+        m = ins.operation.to_matrix()
+        full = _embed(m, ins.qubits, n)
+        u = full @ u
+    return u
+
+
+def _embed(m, qubits, n):
+    k = len(qubits)
+    dim = 2 ** n
+    out = np.zeros((dim, dim), dtype=complex)
+    for col in range(dim):
+        sub_in = 0
+        for i, q in enumerate(qubits):
+            sub_in |= ((col >> q) & 1) << i
+        rest = col
+        for q in qubits:
+            rest &= ~(1 << q)
+        for sub_out in range(2 ** k):
+            row = rest
+            for i, q in enumerate(qubits):
+                row |= ((sub_out >> i) & 1) << q
+            out[row, col] += m[sub_out, sub_in]
+    return out
+
+
+def product_state_vectors(n, starting_circuit):
+    """Per-qubit 2-vectors of |s> = starting_circuit|0..0>, or None if it entangles."""
+    s = np.zeros((n, 2), dtype=complex)
+    s[:, 0] = 1.0
+    if starting_circuit is None:
+        return s
+    for ins in starting_circuit.data:
+        if ins.operation.name in ("barrier", "id"):
+            continue
+        if len(ins.qubits) != 1:
+            return None
+        s[ins.qubits[0]] = ins.operation.to_matrix() @ s[ins.qubits[0]]
+    return s
+
+
+def general_grad_of_pairs(
+    circuit: QuantumCircuit,
+    inverse_zero_ansatz: QuantumCircuit,
+    generators: List[QuantumCircuit],
+    degeneracies: List[int],
+    coupling_map: List[Tuple],
+    starting_circuit=None,
+    backend=None,
+):
+    """Euclidean norm over the layer's generators of dC/dtheta at theta=0, for every pair.
+
+    g_ct = sqrt(sum_k deg_k * (-Im(<s|G_k|psi> <psi|U0^dag|s>))^2)  (gradients.py:23-124).
+    ``generators`` are the circuits of G_k^dag and ``inverse_zero_ansatz`` that of U0^dag, as
+    in the reference (adapt_compiler.py:213-216).
+    """
+    if backend is None:
+        from ..backends.python_default_backends import MPS_SIM as backend
+    psi = device_mps_from_circuit(circuit.copy(), sim=backend.simulator)
+    return grads_for_state(psi, circuit.num_qubits, inverse_zero_ansatz, generators, degeneracies,
+                           coupling_map, starting_circuit, backend)
+
+
+def layer_operators(inverse_zero_ansatz, generators):
+    u0 = circuit_unitary(inverse_zero_ansatz).conj().T
+    gmats = [circuit_unitary(g).conj().T for g in generators]
+    return u0, gmats
+
+
+def grads_for_state(psi: DeviceMPS, n, inverse_zero_ansatz, generators, degeneracies, coupling_map,
+                    starting_circuit=None, backend=None):
+    if len(coupling_map) == 0:
+        return []
+    u0, gmats = layer_operators(inverse_zero_ansatz, generators)
+    svec = product_state_vectors(n, starting_circuit)
+    if svec is not None:
+        gens = np.stack(gmats) if gmats else np.zeros((0, 4, 4), dtype=complex)
+        out = pair_grads_batch([psi], svec, coupling_map, u0, gens, np.asarray(degeneracies, dtype=float))
+        return [float(x) for x in out[0]]
+    return _grads_entangled_start(psi, n, inverse_zero_ansatz, generators, degeneracies, coupling_map,
+                                  starting_circuit, backend)
+
+
+def _grads_entangled_start(psi, n, inverse_zero_ansatz, generators, degeneracies, coupling_map,
+                           starting_circuit, backend):
+    """Reference structure (gradients.py:81-122) with every MPS build and dot on the device."""
+    sim = backend.simulator if backend is not None else None
+    resolves_to_id = np.allclose(circuit_unitary(inverse_zero_ansatz), np.eye(4))
+    if resolves_to_id:
+        s = device_mps_from_circuit(starting_circuit.copy(), sim=sim)
+        zero_overlap = psi.dot(s)
+    out = []
+    for control, target in coupling_map:
+        if not resolves_to_id:
+            st = device_mps_from_circuit(starting_circuit.compose(inverse_zero_ansatz, [control, target]), sim=sim)
+            zero_overlap = psi.dot(st)
+        g = 0.0
+        for gen, deg in zip(generators, degeneracies):
+            st = device_mps_from_circuit(starting_circuit.compose(gen, [control, target]), sim=sim)
+            ov = st.dot(psi)
+            gg = -1 * np.imag(ov * zero_overlap)
+            g += (gg ** 2) * deg
+        out.append(float(np.sqrt(g)))
+    return out
+
+
+def remove_unnecessary_2q_gates_from_circuit(circuit: QuantumCircuit):
+    """Cancel adjacent identical CX/CY/CZ pairs (circuit_operations_optimisation.py:167-204)."""
+    data = circuit.data
+    to_remove, dealt = [], []
+    for gi in range(len(data) - 1, -1, -1):
+        ins = data[gi]
+        if ins.operation.name not in ("cx", "cy", "cz") or gi in to_remove or gi in dealt:
+            continue
+        req = set(ins.qubits)
+        pi = gi - 1
+        while pi >= 0 and not (req & set(data[pi].qubits)):
+            pi -= 1
+        if pi < 0 or data[pi].operation.name != ins.operation.name:
+            continue
+        if pi in to_remove or pi in dealt:
+            continue
+        if data[pi].qubits == ins.qubits:
+            to_remove += [gi, pi]
+    for i in sorted(to_remove, reverse=True):
+        del data[i]
+
+
+def get_generators_and_degeneracies(ansatz: QuantumCircuit, rotoselect: bool = False, inverse: bool = False):
+    """gradients.py:127-170."""
+    gens = []
+    for i, ins in enumerate(ansatz.data):
+        if ins.operation.name in PARAMETERISED:
+            for op in (PARAMETERISED if rotoselect else (ins.operation.name,)):
+                g = get_generator(ansatz, i, op)
+                gens.append(g.inverse() if inverse else g)
+    return get_distinct_items_and_degeneracies(gens)
+
+
+def get_generator(ansatz: QuantumCircuit, index: int, op: str):
+    """gradients.py:173-224."""
+    if op not in PARAMETERISED:
+        raise ValueError("op must be one of rx, ry or rz")
+    gen = QuantumCircuit(2)
+    for i, ins in enumerate(ansatz.data):
+        name = ins.operation.name
+        if name not in ("rx", "ry", "rz", "cx"):
+            raise ValueError("Circuit must only contain rx, ry, rz and cx gates")
+        if i == index:
+            getattr(gen, {"rx": "x", "ry": "y", "rz": "z"}[op])(ins.qubits[0])
+        if name == "cx":
+            gen.cx(*ins.qubits)
+    remove_unnecessary_2q_gates_from_circuit(gen)
+    return gen
+
+
+__all__ = [
+    "general_grad_of_pairs",
+    "get_generators_and_degeneracies",
+    "get_generator",
+    "circuit_unitary",
+    "G",
+]

@@ -1,0 +1,132 @@
+/*
+ * aqc_hip.h -- C ABI of libaqchip.so, the MI355X (gfx950) engine behind the
+ * adaptaqc_amd backends.
+ *
+ * Every entry point replaces a specific reference call site (qiskit-community/adapt-aqc,
+ * paths relative to the reference root); the arithmetic those call sites delegated to
+ * qiskit-aer ~=0.16.0 and aqc_research.mps_operations runs here in hand-written HIP.
+ *
+ * Conventions
+ *   - return value: AQC_OK (0) or a negative AQC_ERR_*; aqc_last_error() gives a
+ *     thread-local message for the last failure.
+ *   - complex numbers are interleaved (re, im) doubles; matrices are row-major.
+ *   - gate matrices follow Qiskit: for an op on qubits (q0, q1) the row/column index is
+ *     2*b1 + b0 (b0 = bit of q0).
+ *   - handles own their device memory and one HIP stream; a handle is not re-entrant.
+ *   - *_batch entry points take arrays of handles and run them in lock-step launches
+ *     (one kernel launch serves every handle), so independent evaluations fill the GPU.
+ */
+#ifndef AQC_HIP_H
+#define AQC_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AQC_OK 0
+#define AQC_ERR_ARG (-1)
+#define AQC_ERR_HIP (-2)
+#define AQC_ERR_STATE (-3)
+#define AQC_ERR_UNSUPPORTED (-4)
+#define AQC_ERR_NOMEM (-5)
+
+/* One gate.  nq = 1: m[0..7] holds the 2x2 matrix; nq = 2: m[0..31] the 4x4 matrix. */
+typedef struct aqc_op {
+  int32_t nq;
+  int32_t q0;
+  int32_t q1;
+  int32_t flags; /* reserved, 0 */
+  double m[32];
+} aqc_op_t;
+
+typedef struct aqc_sv_s* aqc_sv_t;
+typedef struct aqc_mps_s* aqc_mps_t;
+
+/* ---- library -------------------------------------------------------------------- */
+const char* aqc_last_error(void);
+int aqc_version(void);
+/* Select the HIP device used by handles created afterwards (hipSetDevice). */
+int aqc_init(int device);
+int aqc_finalize(void);
+/* Kernel-time instrumentation: accumulate HIP-event time of the named kernel family
+ * ("sv_segment", "mps_svd", "grad_chain", ...) issued after the call. */
+int aqc_timing_enable(int on);
+int aqc_timing_query(const char* name, double* total_ms, int64_t* launches, double* bytes,
+                     double* flops);
+int aqc_timing_reset(void);
+
+/* ---- statevector: replaces aer_sv_backend.py:37-59 ---------------------------- */
+/* Allocate |0...0> on n qubits (Aer statevector_simulator state). */
+int aqc_sv_create(int n, aqc_sv_t* out);
+int aqc_sv_destroy(aqc_sv_t h);
+int aqc_sv_reset(aqc_sv_t h);
+int aqc_sv_copy(aqc_sv_t dst, const aqc_sv_t src);
+/* Apply ops in order (aer_sv_backend.py:42-47 simulator.run(full_circuit)).  Gates are
+ * fused on the host into qubit-local segments (<= 10-bit tiles) that run in LDS. */
+int aqc_sv_apply(aqc_sv_t h, const aqc_op_t* ops, int nops);
+/* sv[0] (aer_sv_backend.py:29). */
+int aqc_sv_amp0(aqc_sv_t h, double* re, double* im);
+/* <Z_i> = p0 - p1 for all i (aer_sv_backend.py:49-59), out[n]. */
+int aqc_sv_z_all(aqc_sv_t h, double* out);
+/* Host copies of the full state (2^n interleaved complex). */
+int aqc_sv_get(aqc_sv_t h, double* out);
+int aqc_sv_set(aqc_sv_t h, const double* in);
+
+/* ---- MPS: replaces aer_mps_backend.py:27-93 and aqc_research.mps_operations ----- */
+/* |0...0> on n qubits, bond capacity chi_cap; truncation as mps_sim_with_args
+ * (aer_mps_backend.py:27-42): threshold on the discarded tail sum of s^2, max_chi <= 0
+ * means unlimited (bounded by chi_cap). */
+int aqc_mps_create(int n, int chi_cap, double threshold, int max_chi, aqc_mps_t* out);
+int aqc_mps_destroy(aqc_mps_t h);
+int aqc_mps_set_truncation(aqc_mps_t h, double threshold, int max_chi);
+/* Load Aer-format Vidal MPS (set_matrix_product_state, approximate_compiler.py:180-204):
+ * dims[n+1] bond dims (dims[0] = dims[n] = 1); gammas: for site i, 2*dims[i]*dims[i+1]
+ * complex laid out [s][l][r]; lambdas: for bond i < n-1, dims[i+1] doubles. */
+int aqc_mps_set_vidal(aqc_mps_t h, const int* dims, const double* gammas, const double* lambdas);
+/* Export (save_matrix_product_state): sorts qubits first.  Pass NULL to query dims. */
+int aqc_mps_get_vidal(aqc_mps_t h, int* dims, double* gammas, double* lambdas);
+int aqc_mps_get_dims(aqc_mps_t h, int* dims);
+int aqc_mps_copy(aqc_mps_t dst, const aqc_mps_t src);
+/* Apply ops with Aer MPS semantics (swap-left routing, lazy qubit order, two-site SVD with
+ * reduce_zeros truncation) -- the replay inside mps_from_circuit (aer_mps_backend.py:76-78). */
+int aqc_mps_apply(aqc_mps_t h, const aqc_op_t* ops, int nops);
+int aqc_mps_apply_batch(aqc_mps_t* hs, int nstates, const aqc_op_t* const* ops, const int* nops);
+/* Diagnostics: largest Jacobi sweep count since the last call (then reset). */
+int aqc_mps_jacobi_stats(aqc_mps_t h, int* max_sweeps);
+/* Jacobi rotation threshold |a^H b| > factor * L * eps * |a||b| (default factor 1). */
+int aqc_mps_set_jacobi_tol(double factor);
+/* move_all_qubits_to_sorted_ordering (done implicitly by every measurement below). */
+int aqc_mps_sort(aqc_mps_t h);
+int aqc_mps_sort_batch(aqc_mps_t* hs, int nstates);
+/* mps_dot(psi, zero_mps) = <psi|0...0> (aer_mps_backend.py:49-57). */
+int aqc_mps_overlap_zero(aqc_mps_t h, double* re, double* im);
+int aqc_mps_overlap_zero_batch(aqc_mps_t* hs, int nstates, double* out /* 2*nstates */);
+/* mps_dot(a, b) = <a|b>, conjugating a. */
+int aqc_mps_dot(aqc_mps_t a, aqc_mps_t b, double* re, double* im);
+/* mps_expectation(psi, "Z", i) for all i (aer_mps_backend.py:80-86), out[n]. */
+int aqc_mps_z_all(aqc_mps_t h, double* out);
+/* extract_amplitude(psi, 2**i) for all i (aer_mps_backend.py:88-93), out[2n]. */
+int aqc_mps_amps_hw1(aqc_mps_t h, double* out);
+
+/* ---- candidate sweep: replaces gradients.py:23-124 ------------------------------ */
+/* For every pair (pairs[2p], pairs[2p+1]) = (control, target):
+ *   g_p = sqrt( sum_k degs[k] * ( -Im( <s|G_k|psi> <psi|U0^dag|s> ) )^2 )
+ * |s> is the product state with per-qubit 2-vectors svec[n][2] (complex); u0 and gens are
+ * 4x4 (little-endian over (control, target)) matrices of U0 and G_k (NOT their inverses).
+ * out: npairs doubles; out_is_device != 0 means `out` is a device pointer (for RCCL). */
+int aqc_pair_grads(aqc_mps_t psi, const double* svec, const int* pairs, int npairs,
+                   const double* u0, const double* gens, const double* degs, int ngen,
+                   double* out, int out_is_device);
+int aqc_pair_grads_batch(aqc_mps_t* psis, int nstates, const double* svec, const int* pairs,
+                         int npairs, const double* u0, const double* gens, const double* degs,
+                         int ngen, double* out /* nstates*npairs */, int out_is_device);
+/* np.argmax(scores * priorities) with lowest-index tie-break (adapt_compiler.py:832-837). */
+int aqc_argmax_scaled(const double* scores, const double* prio, int count, int scores_is_device,
+                      int* best);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* AQC_HIP_H */

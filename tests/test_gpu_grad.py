@@ -1,0 +1,169 @@
+"""Candidate-sweep parity on MI355X vs the oracle (gradients.py:23-124)."""
+import numpy as np
+import pytest
+
+from conftest import to_circuit
+from oracle import adapt_host
+from oracle import gradients as ogr
+from oracle import mps as M
+from oracle import sv as osv
+
+pytestmark = pytest.mark.gpu
+
+
+def _layer(kind):
+    from adaptaqc_amd.utils import ansatzes
+
+    return ansatzes.identity_resolvable() if kind == "identity_resolvable" else ansatzes.thinly_dressed_cnot()
+
+
+def _inputs(kind):
+    from adaptaqc_amd.utils.gradients import get_generators_and_degeneracies
+
+    layer = _layer(kind)
+    gens, deg = get_generators_and_degeneracies(layer, rotoselect=True, inverse=True)
+    return layer.inverse(), gens, deg
+
+
+@pytest.mark.parametrize("kind", ["identity_resolvable", "thinly_dressed"])
+def test_fixture_all_pairs(random_mps, goldens, kind):
+    """1225-pair sweep on the 50-qubit paper fixtures vs oracle goldens."""
+    from adaptaqc_amd.device import DeviceMPS
+    from adaptaqc_amd.utils.gradients import grads_for_state
+
+    cmap = [tuple(x) for x in goldens["cmap"]]
+    inv0, gens, deg = _inputs(kind)
+    for seed in (1, 2, 64, 100):
+        d = DeviceMPS(50, 4)
+        d.load_aer(random_mps[seed])
+        g = np.array(grads_for_state(d, 50, inv0, gens, deg, cmap))
+        ref = goldens[f"s{seed}_grad_{kind}"]
+        scale = np.max(np.abs(ref))
+        np.testing.assert_allclose(g, ref, rtol=0, atol=1e-9 * scale)
+
+
+def test_analytic_two_qubit_gradient():
+    """test_gradients.py:39-73: sqrt(Im(conj(a) b)^2 + Re(conj(a) c)^2), places=10."""
+    from adaptaqc_amd.circuit import QuantumCircuit
+    from adaptaqc_amd.utils.gradients import general_grad_of_pairs, get_generators_and_degeneracies
+
+    rng = np.random.default_rng(0)
+    qc = QuantumCircuit(2)
+    ops = []
+    for _ in range(5):
+        th = rng.uniform(-3, 3, 3)
+        qc.ry(th[0], 0)
+        qc.rz(th[1], 1)
+        qc.cx(1, 0)
+        qc.rx(th[2], 0)
+        ops += [("ry", (0,), (th[0],)), ("rz", (1,), (th[1],)), ("cx", (1, 0), ()), ("rx", (0,), (th[2],))]
+    s = osv.simulate(2, ops)
+    a, b, c = s[0], s[1], s[2]
+    expected = np.sqrt(np.imag(np.conj(a) * b) ** 2 + np.real(np.conj(a) * c) ** 2)
+    ans = QuantumCircuit(2)
+    ans.rx(0, 0)
+    ans.ry(0, 1)
+    gens, deg = get_generators_and_degeneracies(ans, rotoselect=False, inverse=True)
+    got = general_grad_of_pairs(qc, ans.inverse(), gens, deg, coupling_map=[(0, 1)])[0]
+    assert abs(got - expected) < 1e-10
+
+
+def test_no_ansatz_zero_gradient():
+    """test_gradients.py:14-37."""
+    from adaptaqc_amd.circuit import QuantumCircuit
+    from adaptaqc_amd.utils.gradients import general_grad_of_pairs, get_generators_and_degeneracies
+
+    rng = np.random.default_rng(2)
+    qc = QuantumCircuit(5)
+    for _ in range(5):
+        for q in range(5):
+            qc.rx(rng.uniform(-3, 3), q)
+        qc.cx(0, 3)
+        qc.cx(4, 1)
+    start = QuantumCircuit(5)
+    for q in range(5):
+        start.ry(rng.uniform(-3, 3), q)
+    ans = QuantumCircuit(2)
+    gens, deg = get_generators_and_degeneracies(ans)
+    g = general_grad_of_pairs(qc, ans, gens, deg, [(0, 1), (1, 2), (2, 3), (3, 4)], starting_circuit=start)
+    np.testing.assert_array_almost_equal(g, [0, 0, 0, 0])
+
+
+@pytest.mark.parametrize("kind", ["identity_resolvable", "thinly_dressed"])
+def test_product_start_random_state_vs_reference_structure(kind):
+    """12-qubit state near |s>, tenpy-like product starting circuit, full map."""
+    from adaptaqc_amd.utils.gradients import general_grad_of_pairs
+
+    rng = np.random.default_rng(21)
+    n = 12
+    ops = []
+    for layer in range(4):
+        for q in range(n):
+            ops.append(("ry", (q,), (0.3 * rng.standard_normal(),)))
+        for q in range(layer % 2, n - 1, 2):
+            ops.append(("cx", (q, q + 1), ()))
+    start_ops = [("ry", (q,), (0.2 * q,)) for q in range(n)] + [("rz", (q,), (0.1,)) for q in range(0, n, 3)]
+    cmap = adapt_host.coupling_map_full(n)
+    inv0, gens, deg = _inputs(kind)
+    got = general_grad_of_pairs(to_circuit(n, ops), inv0, gens, deg, cmap, starting_circuit=to_circuit(n, start_ops))
+    o_layer = [(i.operation.name, i.qubits, tuple(i.operation.params)) for i in _layer(kind).data]
+    o_gens, o_deg = ogr.get_generators_and_degeneracies(o_layer, True, True)
+    psi = M.run_circuit(n, ops).preprocessed()
+    ref = ogr.general_grad_of_pairs_ref(psi, n, ogr.inverse_ops(o_layer), o_gens, o_deg, cmap, start_ops)
+    np.testing.assert_allclose(got, ref, atol=1e-11)
+    assert np.max(ref) > 1e-3  # non-trivial gradients
+
+
+def test_entangled_starting_circuit_device_route():
+    from adaptaqc_amd.utils.gradients import general_grad_of_pairs
+
+    n = 6
+    rng = np.random.default_rng(4)
+    ops = [("ry", (q,), (rng.uniform(-1, 1),)) for q in range(n)] + [("cx", (0, 1), ()), ("cx", (2, 4), ())]
+    start = [("h", (0,), ()), ("cx", (0, 5), ()), ("ry", (3,), (0.4,))]
+    cmap = adapt_host.coupling_map_full(n)
+    inv0, gens, deg = _inputs("thinly_dressed")
+    got = general_grad_of_pairs(to_circuit(n, ops), inv0, gens, deg, cmap, starting_circuit=to_circuit(n, start))
+    o_layer = [(i.operation.name, i.qubits, tuple(i.operation.params)) for i in _layer("thinly_dressed").data]
+    o_gens, o_deg = ogr.get_generators_and_degeneracies(o_layer, True, True)
+    psi = M.run_circuit(n, ops).preprocessed()
+    ref = ogr.general_grad_of_pairs_ref(psi, n, ogr.inverse_ops(o_layer), o_gens, o_deg, cmap, start)
+    np.testing.assert_allclose(got, ref, atol=1e-11)
+
+
+def test_sharded_pairs_equal_full(random_mps):
+    """Per-rank pair subsets (first-qubit sharding) reproduce the full sweep bit for bit."""
+    from adaptaqc_amd.device import DeviceMPS, pair_grads_batch
+    from adaptaqc_amd.sharding import PairShard
+    from adaptaqc_amd.utils.gradients import layer_operators
+
+    n = 50
+    cmap = adapt_host.coupling_map_full(n)
+    inv0, gens, deg = _inputs("identity_resolvable")
+    u0, gm = layer_operators(inv0, gens)
+    svec = np.zeros((n, 2), complex)
+    svec[:, 0] = 1
+    d = DeviceMPS(n, 4)
+    d.load_aer(random_mps[35])
+    full = pair_grads_batch([d], svec, cmap, u0, np.stack(gm), deg)[0]
+    for world in (2, 3, 8):
+        got = np.zeros(len(cmap))
+        for r in range(world):
+            sh = PairShard(cmap, n, r, world)
+            part = pair_grads_batch([d], svec, sh.local_pairs, u0, np.stack(gm), deg)[0]
+            got[sh.local_index] = part
+        np.testing.assert_array_equal(got, full)
+
+
+def test_argmax_c_abi_tie_break():
+    import ctypes
+
+    from adaptaqc_amd import _lib
+
+    rng = np.random.default_rng(0)
+    for trial in range(20):
+        s = rng.integers(0, 4, 1225).astype(float)
+        p = rng.choice([-1.0, 0.5, 1.0], 1225)
+        best = ctypes.c_int()
+        _lib.check(_lib.lib().aqc_argmax_scaled(_lib.ptr(s), _lib.ptr(p), len(s), 0, ctypes.byref(best)))
+        assert best.value == int(np.argmax(s * p))

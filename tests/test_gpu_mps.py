@@ -1,0 +1,195 @@
+"""MPS engine parity on MI355X vs the oracle (1e-6 for truncated MPS; tighter where exact)."""
+import numpy as np
+import pytest
+
+from conftest import FakeCompiler, golden_ops, to_circuit
+from oracle import mps as M
+from oracle import sv as osv
+
+pytestmark = pytest.mark.gpu
+
+
+def _dev_from_aer(q, cap=None, thr=1e-16, max_chi=None):
+    from adaptaqc_amd.device import DeviceMPS
+
+    n = len(q[0])
+    lmax = max(np.asarray(a).shape[1] for a, _ in q[0])
+    d = DeviceMPS(n, cap or max(lmax, 4), thr, max_chi)
+    d.load_aer(q)
+    return d
+
+
+def test_fixture_measurements(random_mps, goldens):
+    """paper/random_mps fixtures: <psi|0>, <Z_i>, HW-1 amplitudes vs oracle goldens."""
+    for seed in (1, 2, 64, 100):
+        d = _dev_from_aer(random_mps[seed])
+        ov = d.overlap_zero()
+        ref = complex(goldens[f"s{seed}_ov0"])
+        assert abs(ov - ref) <= 1e-12 * max(1.0, abs(ref)) + 1e-30
+        np.testing.assert_allclose(d.z_all(), goldens[f"s{seed}_z"], atol=1e-10)
+        np.testing.assert_allclose(d.amps_hw1(), goldens[f"s{seed}_hw1"], atol=1e-14)
+
+
+def test_vidal_round_trip_unchanged(random_mps):
+    """test_utilityfunctions.py:317-338: Gamma/lambda unchanged through set/save."""
+    q = random_mps[17]
+    d = _dev_from_aer(q)
+    gam, lam = d.to_aer()
+    for (a, b), (a2, b2) in zip(q[0], gam):
+        np.testing.assert_allclose(a, a2)
+        np.testing.assert_allclose(b, b2)
+    for x, y in zip(q[1], lam):
+        np.testing.assert_allclose(x, y)
+
+
+@pytest.mark.parametrize("chi", [0, 4])
+def test_golden_circuits(goldens, chi):
+    """Seeded 8-qubit circuits with non-adjacent gates; chi=4 makes truncation bind."""
+    from adaptaqc_amd.circuit import device_ops
+    from adaptaqc_amd.device import DeviceMPS
+
+    for seed in range(3):
+        ops = golden_ops(goldens, seed)
+        d = DeviceMPS(8, 16, 1e-16, chi or None)
+        d.apply(device_ops(to_circuit(8, ops)))
+        assert abs(d.overlap_zero() - complex(goldens[f"circ{seed}_chi{chi}_ov0"])) < 1e-10
+        np.testing.assert_allclose(d.z_all(), goldens[f"circ{seed}_chi{chi}_z"], atol=1e-9)
+        np.testing.assert_array_equal(d.dims(), goldens[f"circ{seed}_chi{chi}_dims"])
+
+
+def test_mps_equals_statevector_without_truncation():
+    """SV == MPS when nothing is truncated (test_approximate_compiler.py:78-112 style)."""
+    from adaptaqc_amd.circuit import device_ops
+
+    rng = np.random.default_rng(7)
+    n = 10
+    ops = []
+    for layer in range(6):
+        for q in range(n):
+            ops.append((["rx", "ry", "rz"][rng.integers(3)], (q,), (rng.uniform(-np.pi, np.pi),)))
+        for _ in range(4):
+            a, b = rng.choice(n, 2, replace=False)
+            ops.append(("cx", (int(a), int(b)), ()))
+    psi = osv.simulate(n, ops)
+    from adaptaqc_amd.device import DeviceMPS
+
+    d = DeviceMPS(n, 32)
+    d.apply(device_ops(to_circuit(n, ops)))
+    pre = d.preprocessed()
+    vec = np.array([M.extract_amplitude(pre, i) for i in range(2 ** n)])
+    np.testing.assert_allclose(vec, psi, atol=1e-11)
+
+
+def test_backend_costs_sv_vs_mps():
+    """Global / local cost of SV and MPS backends agree (reference: 5 decimals; here 1e-10)."""
+    from adaptaqc_amd.backends import AerMPSBackend, AerSVBackend
+    from adaptaqc_amd.circuit import QuantumCircuit
+
+    rng = np.random.default_rng(3)
+    n = 6
+    qc = QuantumCircuit(n)
+    for _ in range(5):
+        for q in range(n):
+            qc.ry(rng.uniform(-1, 1), q)
+            qc.rz(rng.uniform(-1, 1), q)
+        for q in range(0, n - 1):
+            qc.cx(q, q + 1)
+    sv_comp = FakeCompiler(qc)
+    sv = AerSVBackend()
+    mps_b = AerMPSBackend()
+    mps_circ = QuantumCircuit(n)
+    from adaptaqc_amd.mps_operations import mps_from_circuit
+
+    mps_circ.set_matrix_product_state(mps_from_circuit(qc))
+    mps_comp = FakeCompiler(mps_circ)
+    assert abs(sv.evaluate_global_cost(sv_comp) - mps_b.evaluate_global_cost(mps_comp)) < 1e-10
+    assert abs(sv.evaluate_local_cost(sv_comp) - mps_b.evaluate_local_cost(mps_comp)) < 1e-10
+
+
+def test_soften_global_cost():
+    """aer_mps_backend.py:58-70: C - alpha * sum_i |<e_i|psi>|^2."""
+    from adaptaqc_amd.backends import AerMPSBackend
+    from adaptaqc_amd.circuit import QuantumCircuit
+    from adaptaqc_amd.mps_operations import mps_from_circuit
+
+    qc = QuantumCircuit(5)
+    for q in range(5):
+        qc.ry(0.3 + 0.1 * q, q)
+    qc.cx(0, 3)
+    circ = QuantumCircuit(5)
+    circ.set_matrix_product_state(mps_from_circuit(qc))
+    be = AerMPSBackend()
+    comp = FakeCompiler(circ, soften=True, history=[0.4], sufficient_cost=0.01)
+    psi = osv.simulate(5, [("ry", (q,), (0.3 + 0.1 * q,)) for q in range(5)] + [("cx", (0, 3), ())])
+    c = 1 - abs(psi[0]) ** 2
+    expect = c - abs(0.4 - 0.01) * sum(abs(psi[1 << i]) ** 2 for i in range(5))
+    assert abs(be.evaluate_global_cost(comp) - expect) < 1e-12
+
+
+def test_hadamard_and_zero_z():
+    """test_utilityfunctions.py:201-211."""
+    from adaptaqc_amd.backends import AerMPSBackend
+    from adaptaqc_amd.circuit import QuantumCircuit
+    from adaptaqc_amd.mps_operations import mps_from_circuit
+
+    be = AerMPSBackend()
+    for gates, expect in (("", [1, 1, 1, 1]), ("h", [0, 0, 0, 0])):
+        qc = QuantumCircuit(4)
+        if gates:
+            qc.h([0, 1, 2, 3])
+        circ = QuantumCircuit(4)
+        circ.set_matrix_product_state(mps_from_circuit(qc))
+        np.testing.assert_allclose(be.measure_qubit_expectation_values(FakeCompiler(circ)), expect, atol=1e-7)
+
+
+def test_chi64_fifty_qubits_vs_oracle():
+    """50 qubits, max_chi = 64 binding: device replay vs oracle replay of the same ops."""
+    from adaptaqc_amd.circuit import device_ops
+    from adaptaqc_amd.device import DeviceMPS
+
+    n, chi = 50, 64
+    rng = np.random.default_rng(11)
+    ops = []
+    for layer in range(14):
+        for q in range(n):
+            ops.append(("ry", (q,), (rng.uniform(-np.pi, np.pi),)))
+            ops.append(("rz", (q,), (rng.uniform(-np.pi, np.pi),)))
+        for q in range(layer % 2, n - 1, 2):
+            ops.append(("cx", (q, q + 1), ()))
+    ops += [("cx", (3, 9), ()), ("cx", (30, 22), ())]
+    ref = M.run_circuit(n, ops, 1e-16, chi)
+    d = DeviceMPS(n, chi, 1e-16, chi)
+    d.apply(device_ops(to_circuit(n, ops)))
+    dims = d.dims()
+    ref_dims = [1] + [x.shape[2] for x in ref.preprocessed()]
+    np.testing.assert_array_equal(dims, ref_dims)
+    pre_ref = ref.preprocessed()
+    ov_ref = M.mps_dot(pre_ref, M.zero_mps(n))
+    ov = d.overlap_zero()
+    assert abs(ov - ov_ref) <= 1e-6 * abs(ov_ref) + 1e-18
+    zr = np.array([M.mps_expectation_z(pre_ref, q) for q in range(0, n, 7)])
+    np.testing.assert_allclose(d.z_all()[0:n:7], zr, atol=1e-6)
+
+
+def test_batch_apply_matches_single():
+    from adaptaqc_amd.device import DeviceMPS, apply_batch, overlap_zero_batch
+    from adaptaqc_amd import _lib
+
+    rng = np.random.default_rng(5)
+    n = 12
+    states, lists = [], []
+    for s in range(4):
+        ops = []
+        for _ in range(20):
+            a, b = rng.choice(n, 2, replace=False)
+            th = rng.uniform(-3, 3, 2)
+            ops.append((np.array([[np.cos(th[0]), -np.sin(th[0])], [np.sin(th[0]), np.cos(th[0])]], complex), (int(a),)))
+            ops.append((np.kron(np.eye(2), np.eye(2))[[0, 1, 3, 2]] .astype(complex), (int(a), int(b))))
+        lists.append(_lib.ops_array(ops))
+        states.append(DeviceMPS(n, 16, 1e-16, 8))
+    apply_batch(states, lists)
+    ov = overlap_zero_batch(states)
+    for s in range(4):
+        d = DeviceMPS(n, 16, 1e-16, 8)
+        d.apply(lists[s])
+        assert abs(d.overlap_zero() - ov[s]) < 1e-13

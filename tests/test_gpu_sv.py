@@ -1,0 +1,124 @@
+"""Statevector parity on MI355X vs the oracle (tolerance 1e-10 on overlaps, per north_star)."""
+import numpy as np
+import pytest
+
+from conftest import FakeCompiler, golden_ops, to_circuit
+from oracle import sv as osv
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-10
+
+
+def brickwork(n, depth, seed):
+    rng = np.random.default_rng(seed)
+    ops = []
+    for layer in range(depth):
+        for q in range(n):
+            ops.append((["rx", "ry", "rz"][rng.integers(3)], (q,), (rng.uniform(-np.pi, np.pi),)))
+        for q in range(layer % 2, n - 1, 2):
+            ops.append(("cx", (q, q + 1), ()))
+    return ops
+
+
+def test_golden_circuits_statevector(goldens):
+    from adaptaqc_amd.circuit import device_ops
+    from adaptaqc_amd.device import DeviceSV
+
+    for seed in range(3):
+        ops = golden_ops(goldens, seed)
+        qc = to_circuit(8, ops)
+        d = DeviceSV(8)
+        d.apply(device_ops(qc))
+        np.testing.assert_allclose(d.get(), goldens[f"circ{seed}_sv"], atol=1e-12)
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_20_qubit_brickwork_global_cost_and_z(seed):
+    """Config 2: 20-qubit random circuit, overlap vs oracle within 1e-10."""
+    n = 20
+    ops = brickwork(n, 8, seed)
+    ops += [("cx", (0, 19), ()), ("cz", (13, 2), ()), ("swap", (5, 17), ())]
+    psi = osv.simulate(n, ops)
+    from adaptaqc_amd.backends import AerSVBackend
+
+    be = AerSVBackend()
+    comp = FakeCompiler(to_circuit(n, ops))
+    assert abs(be.evaluate_global_cost(comp) - osv.global_cost(psi)) < TOL
+    z = be.measure_qubit_expectation_values(comp)
+    np.testing.assert_allclose(z, osv.z_expectations(psi, n), atol=1e-10)
+    st = be.evaluate_circuit(comp)
+    assert abs(st[0] - psi[0]) < TOL
+    np.testing.assert_allclose(st.data, psi, atol=1e-12)
+
+
+def test_reference_cost_table():
+    """test_approximate_compiler.py:114-150 exact costs for |0000>, Neel, GHZ, |++++>."""
+    from adaptaqc_amd.backends import AerSVBackend
+    from adaptaqc_amd.circuit import QuantumCircuit
+
+    zero = QuantumCircuit(4)
+    neel = QuantumCircuit(4)
+    neel.x([0, 2])
+    ghz = QuantumCircuit(4)
+    ghz.h(0)
+    for i in range(3):
+        ghz.cx(0, i + 1)
+    had = QuantumCircuit(4)
+    had.h([0, 1, 2, 3])
+    be = AerSVBackend()
+    got = []
+    for c in (zero, neel, ghz, had):
+        comp = FakeCompiler(c)
+        got += [be.evaluate_global_cost(comp), be.evaluate_local_cost(comp)]
+    np.testing.assert_allclose(got, [0, 0, 1, 0.5, 0.5, 0.5, 15 / 16, 0.5], atol=1e-12)
+
+
+def test_sigma_z_x_h_known_answer():
+    """test_utilityfunctions.py:86-95: <Z> = [-1, 0, 1] for x(0), h(1)."""
+    from adaptaqc_amd.backends import AerSVBackend
+    from adaptaqc_amd.circuit import QuantumCircuit
+
+    qc = QuantumCircuit(3)
+    qc.x(0)
+    qc.h(1)
+    z = AerSVBackend().measure_qubit_expectation_values(FakeCompiler(qc))
+    np.testing.assert_array_almost_equal(z, [-1.0, 0.0, 1.0], decimal=15)
+
+
+def test_ccx_readme_circuit():
+    """examples/readme_example.py:14-19 circuit (ccx unrolled on the host)."""
+    from adaptaqc_amd.circuit import QuantumCircuit, device_ops
+    from adaptaqc_amd.device import DeviceSV
+
+    qc = QuantumCircuit(3)
+    qc.rx(1.23, 0)
+    qc.cx(0, 1)
+    qc.ry(2.5, 1)
+    qc.rx(-1.6, 2)
+    qc.ccx(2, 1, 0)
+    ops = [("rx", (0,), (1.23,)), ("cx", (0, 1), ()), ("ry", (1,), (2.5,)), ("rx", (2,), (-1.6,)), ("ccx", (2, 1, 0), ())]
+    d = DeviceSV(3)
+    d.apply(device_ops(qc))
+    np.testing.assert_allclose(d.get(), osv.simulate(3, ops), atol=1e-12)
+
+
+def test_soften_raises_on_sv():
+    from adaptaqc_amd.backends import AerSVBackend
+    from adaptaqc_amd.circuit import QuantumCircuit
+
+    with pytest.raises(NotImplementedError):
+        AerSVBackend().evaluate_global_cost(FakeCompiler(QuantumCircuit(2), soften=True))
+
+
+def test_small_and_segment_edge_sizes():
+    """n below, at and above the 10-bit tile; long gate lists spanning many segments."""
+    from adaptaqc_amd.circuit import device_ops
+    from adaptaqc_amd.device import DeviceSV
+
+    for n in (1, 2, 9, 10, 11, 14):
+        ops = brickwork(n, 5, n) if n > 1 else [("rx", (0,), (0.3,)), ("rz", (0,), (1.1,))]
+        if n >= 4:
+            ops += [("cx", (n - 1, 0), ()), ("cz", (1, n - 2), ())]
+        d = DeviceSV(n)
+        d.apply(device_ops(to_circuit(n, ops)))
+        np.testing.assert_allclose(d.get(), osv.simulate(n, ops), atol=1e-12, err_msg=f"n={n}")
