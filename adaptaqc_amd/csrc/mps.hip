@@ -267,7 +267,7 @@ __global__ __launch_bounds__(kJT) void k_jacobi(const TwoSiteJob* __restrict__ j
   // absolute noise floor for squared column norms, relative to ||W||_F^2
   const double floor2 = fred[0] * 1e-24;
   const double tol = j.jtol * (double)L * 2.220446049250313e-16;
-  const int ld = L + 1;
+  const int ld = (L + 15) & ~15;
   int sweeps = 0;
   if (C >= 2) {
     const int cap_cols = kPanelCplx / ld;

@@ -139,7 +139,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--states", type=int, default=64, help="states per rank")
+    ap.add_argument("--states", type=int, default=256, help="states per rank")
     ap.add_argument("--distinct", type=int, default=8, help="distinct random states generated")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
