@@ -1,0 +1,113 @@
+"""ApproximateCompiler (reference compilers/approximate_compiler.py:64-527), host side.
+
+Builds ``full_circuit = [target | ansatz | starting_circuit^-1]`` (:435-512), keeps the
+MPS target as a leading ``set_matrix_product_state`` instruction when the backend is the MPS
+backend (:165-217), and dispatches every cost evaluation to the backend (:514-527).
+"""
+import logging
+from abc import ABC, abstractmethod
+
+from ..backends.aer_mps_backend import AerMPSBackend
+from ..backends.python_default_backends import SV_SIM
+from ..circuit import QuantumCircuit
+from ..mps_operations import check_mps, mps_from_circuit, zero_aer_mps, _preprocess_mps
+from ..utils import circuit_operations as co
+from ..utils.cost_minimiser import CostMinimiser
+from ..utils.utilityfunctions import is_statevector_backend
+
+logger = logging.getLogger(__name__)
+
+
+class ApproximateCompiler(ABC):
+    full_circuit: QuantumCircuit
+
+    def __init__(self, target, backend, execute_kwargs=None, initial_state=None, qubit_subset=None,
+                 general_initial_state=False, starting_circuit=None, optimise_local_cost=False,
+                 soften_global_cost=False, itensor_chi=None, itensor_cutoff=None, rotosolve_fraction=1.0):
+        if initial_state is not None or general_initial_state:
+            raise NotImplementedError("initial_state / general_initial_state are outside the MI355X hot path")
+        self.target = target
+        self.original_circuit_classical_ops = None
+        self.backend = backend if backend is not None else SV_SIM
+        self.is_statevector_backend = is_statevector_backend(self.backend)
+        self.is_aer_mps_backend = isinstance(self.backend, AerMPSBackend)
+        if check_mps(self.target) and not self.is_aer_mps_backend:
+            raise Exception("Aer MPS backend must be used when target is an Aer MPS")
+        self.circuit_to_compile = self.prepare_circuit()
+        self.execute_kwargs = dict(execute_kwargs or {})
+        self.execute_kwargs.setdefault("shots", 1)
+        self.execute_kwargs.setdefault("optimization_level", 0)
+        self.backend_options = {"method": "automatic"}
+        self.initial_state_circuit = None
+        self.total_num_qubits = self.circuit_to_compile.num_qubits
+        self.qubit_subset_to_compile = qubit_subset if qubit_subset else list(range(self.total_num_qubits))
+        self.general_initial_state = False
+        self.starting_circuit = self.prepare_starting_circuit(starting_circuit)
+        # approximate_compiler.py:133-135 builds this through Aer; it is |0..0> in preprocessed form
+        self.zero_mps = _preprocess_mps(zero_aer_mps(self.total_num_qubits))
+        self.optimise_local_cost = optimise_local_cost
+        self.soften_global_cost = soften_global_cost
+        self.full_circuit, self.lhs_gate_count, self.rhs_gate_count = self._prepare_full_circuit()
+        if not 0 < rotosolve_fraction <= 1:
+            raise ValueError("rotosolve_fraction must be in the range (0,1]")
+        self.minimizer = CostMinimiser(self.evaluate_cost, self.variational_circuit_range, self.full_circuit,
+                                       rotosolve_fraction)
+        self.cost_evaluation_counter = 0
+        self.compiling_finished = False
+
+    def prepare_circuit(self):
+        if check_mps(self.target):
+            qc = QuantumCircuit(len(self.target[0]))
+            qc.set_matrix_product_state(self.target)
+            return qc
+        prepared = self.target.copy()
+        if self.is_aer_mps_backend:
+            logger.info("Pre-computing target circuit as MPS on the device")
+            target_mps = mps_from_circuit(prepared, sim=self.backend.simulator)
+            qc = QuantumCircuit(prepared.num_qubits)
+            qc.set_matrix_product_state(target_mps)
+            return qc
+        return prepared
+
+    def prepare_starting_circuit(self, starting_circuit):
+        if starting_circuit is None or isinstance(starting_circuit, QuantumCircuit):
+            return starting_circuit
+        if starting_circuit == "tenpy_product_state":
+            raise NotImplementedError("tenpy is not available; pass the product-state circuit explicitly")
+        raise ValueError("starting_circuit must be a QuantumCircuit, None, or string: 'tenpy_product_state'")
+
+    def variational_circuit_range(self, circuit=None):
+        if circuit is None:
+            circuit = self.full_circuit
+        return self.lhs_gate_count, len(circuit.data) - self.rhs_gate_count
+
+    def ansatz_range(self):
+        return self.lhs_gate_count, len(self.full_circuit.data)
+
+    @abstractmethod
+    def compile(self):
+        raise NotImplementedError
+
+    def _prepare_full_circuit(self):
+        qc = QuantumCircuit(self.total_num_qubits)
+        co.add_to_circuit(qc, self.circuit_to_compile, qubit_subset=self.qubit_subset_to_compile)
+        lhs = len(qc.data)
+        if self.starting_circuit is not None:
+            co.add_to_circuit(qc, self.starting_circuit.inverse())
+        return qc, lhs, len(qc.data) - lhs
+
+    def get_compiled_circuit(self):
+        compiled = co.circuit_by_inverting_circuit(
+            co.extract_inner_circuit(self.full_circuit, self.variational_circuit_range()))
+        if self.starting_circuit is not None:
+            co.add_to_circuit(compiled, self.starting_circuit, 0)
+        final = QuantumCircuit(self.circuit_to_compile.num_qubits)
+        co.add_to_circuit(final, compiled, qubit_subset={i: q for i, q in enumerate(self.qubit_subset_to_compile)})
+        return final
+
+    def evaluate_cost(self):
+        """approximate_compiler.py:514-527."""
+        self.cost_evaluation_counter += 1
+        if self.optimise_local_cost:
+            return self.backend.evaluate_local_cost(self)
+        return self.backend.evaluate_global_cost(self)

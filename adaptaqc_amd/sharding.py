@@ -60,8 +60,9 @@ def gather_scores(local_scores, shard: PairShard, group=None, nstates: int = 1):
     buf = torch.zeros((nstates, m), dtype=torch.float64, device=dev)
     buf[:, : local_scores.shape[1]] = local_scores
     if shard.world > 1:
-        gathered = torch.empty((shard.world, nstates, m), dtype=torch.float64, device=dev)
+        gathered = torch.empty((shard.world * nstates, m), dtype=torch.float64, device=dev)
         dist.all_gather_into_tensor(gathered, buf.contiguous(), group=group)
+        gathered = gathered.view(shard.world, nstates, m)
     else:
         gathered = buf.unsqueeze(0)
     full = torch.empty((nstates, len(shard.coupling_map)), dtype=torch.float64, device=dev)

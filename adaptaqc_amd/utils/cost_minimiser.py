@@ -1,0 +1,103 @@
+"""Rotoselect / Rotosolve sequential optimiser (reference utils/cost_minimiser.py:32-418).
+
+Host caller of the hot path: every ``cost_finder()`` call is one overlap evaluation on the
+device (3 per rotation gate for Rotosolve, 7 for Rotoselect).
+"""
+import logging
+import random
+
+import numpy as np
+
+from . import circuit_operations as co
+from .constants import ALG_ROTOSELECT, ALG_ROTOSOLVE
+from .utilityfunctions import has_stopped_improving, minimum_of_sinusoidal
+
+logger = logging.getLogger(__name__)
+ALG_SCIPY = "scipy"
+
+
+class CostMinimiser:
+    def __init__(self, cost_finder, variational_circuit_range, full_circuit, rotosolve_fraction=1.0):
+        self.cost_finder = cost_finder
+        self.variational_circuit_range = variational_circuit_range
+        self.full_circuit = full_circuit
+        self.rotosolve_fraction = rotosolve_fraction
+
+    def minimize_cost(self, algorithm_kind=ALG_ROTOSOLVE, algorithm_identifier=None, max_cycles=1000,
+                      stop_val=-np.inf, tol=1e-10, indexes_to_modify=None, alg_kwargs=None):
+        """cost_minimiser.py:52-106 (Rotosolve / Rotoselect) and :145-160 (SciPy)."""
+        alg_kwargs = alg_kwargs or {}
+        if algorithm_kind in (ALG_ROTOSOLVE, ALG_ROTOSELECT):
+            cost_history = []
+            cost = self.cost_finder()
+            cycles = 0
+            while cost > stop_val and cycles < max_cycles:
+                cost = self._reduce_cost(algorithm_kind == ALG_ROTOSELECT, indexes_to_modify)
+                cycles += 1
+                cost_history.append(cost)
+                if len(cost_history) > 3 and has_stopped_improving(cost_history[-3:], tol):
+                    break
+            return cost
+        if algorithm_kind == ALG_SCIPY:
+            from scipy.optimize import minimize
+
+            x0 = co.find_angles_in_circuit(self.full_circuit, self.variational_circuit_range())
+            res = minimize(fun=self._find_cost_with_angles, method=algorithm_identifier, x0=x0, tol=tol, **alg_kwargs)
+            co.update_angles_in_circuit(self.full_circuit, res["x"], self.variational_circuit_range())
+            return res["fun"]
+        if algorithm_kind in ("nlopt", "pybobyqa"):
+            raise ModuleNotFoundError(f"{algorithm_kind} is not installed in this environment")
+        raise ValueError(f"Invalid algorithm kind {algorithm_kind}")
+
+    def _find_cost_with_angles(self, angles, grad=None):
+        co.update_angles_in_circuit(self.full_circuit, angles, self.variational_circuit_range())
+        return self.cost_finder()
+
+    def _reduce_cost(self, change_1q_gate_kind=False, indexes_to_modify=None):
+        """cost_minimiser.py:267-316."""
+        cost = 1
+        vrange = self.variational_circuit_range()
+        if indexes_to_modify is None:
+            indexes_to_modify = vrange
+        else:
+            indexes_to_modify = (max(indexes_to_modify[0], vrange[0]), min(indexes_to_modify[1], vrange[1]))
+        if self.rotosolve_fraction < 1.0 and not change_1q_gate_kind:
+            cands = [i for i in range(*indexes_to_modify) if co.is_supported_1q_gate(self.full_circuit.data[i].operation)]
+            sample = sorted(random.sample(cands, int(np.ceil(self.rotosolve_fraction * len(cands)))))
+        else:
+            sample = list(range(*indexes_to_modify))
+        for index in sample:
+            old_gate = self.full_circuit.data[index].operation
+            if change_1q_gate_kind and co.is_supported_1q_gate(old_gate):
+                cost = self.replace_with_best_1q_gate(index)
+            elif co.is_supported_1q_gate(old_gate):
+                angle, cost = self.find_best_angle(index, old_gate.label)
+                co.replace_1q_gate(self.full_circuit, index, old_gate.label, angle)
+        return cost
+
+    def replace_with_best_1q_gate(self, gate_index):
+        """cost_minimiser.py:318-342: 1 + 3 x 2 = 7 cost evaluations."""
+        co.replace_1q_gate(self.full_circuit, gate_index, "rx", 0)
+        cost_identity = self.cost_finder()
+        best_name, best_angle, best_cost = None, None, 1
+        for name in co.SUPPORTED_1Q_GATES:
+            angle, cost = self.find_best_angle(gate_index, name, cost_identity)
+            if cost < best_cost:
+                best_name, best_angle, best_cost = name, angle, cost
+        co.replace_1q_gate(self.full_circuit, gate_index, best_name, best_angle)
+        return best_cost
+
+    def find_best_angle(self, gate_index, gate_name, cost_for_identity=None):
+        """cost_minimiser.py:344-368."""
+        instr = self.full_circuit.data[gate_index]
+        costs = []
+        angles = [0, np.pi / 2, -np.pi / 2]
+        if cost_for_identity is not None:
+            costs.append(cost_for_identity)
+            angles.remove(0)
+        for theta in angles:
+            co.replace_1q_gate(self.full_circuit, gate_index, gate_name, theta)
+            costs.append(self.cost_finder())
+        theta_min, cost_min = minimum_of_sinusoidal(costs[0], costs[1], costs[2])
+        self.full_circuit.data[gate_index] = instr
+        return theta_min, cost_min

@@ -1,0 +1,123 @@
+"""End-to-end compiler runs on the GPU backends (reference test_adapt_compiler.py style)."""
+import os
+import pickle
+
+import numpy as np
+import pytest
+
+from conftest import to_circuit
+from oracle import sv as osv
+
+pytestmark = pytest.mark.gpu
+
+
+def _random_state_circuit(n, depth, seed):
+    rng = np.random.default_rng(seed)
+    ops = []
+    for layer in range(depth):
+        for q in range(n):
+            ops.append((["rx", "ry", "rz"][rng.integers(3)], (q,), (rng.uniform(-np.pi, np.pi),)))
+        for q in range(layer % 2, n - 1, 2):
+            ops.append(("cx", (q, q + 1), ()))
+    return ops
+
+
+def test_readme_example_expectation_method():
+    """examples/readme_example.py circuit compiled on the SV backend (config 1 plumbing)."""
+    from adaptaqc_amd.circuit import QuantumCircuit
+    from adaptaqc_amd.compilers import AdaptCompiler, AdaptConfig
+
+    qc = QuantumCircuit(3)
+    qc.rx(1.23, 0)
+    qc.cx(0, 1)
+    qc.ry(2.5, 1)
+    qc.rx(-1.6, 2)
+    qc.ccx(2, 1, 0)
+    res = AdaptCompiler(qc, adapt_config=AdaptConfig(method="expectation")).compile()
+    assert res.overlap > 1 - 1e-2
+    assert res.exact_overlap > 1 - 1e-2
+    # independent check of the compiled circuit against the oracle
+    ops = [(i.operation.name, i.qubits, tuple(i.operation.params)) for i in res.circuit.data]
+    want = osv.simulate(3, [("rx", (0,), (1.23,)), ("cx", (0, 1), ()), ("ry", (1,), (2.5,)), ("rx", (2,), (-1.6,)),
+                            ("ccx", (2, 1, 0), ())])
+    got = osv.simulate(3, ops)
+    assert abs(np.vdot(want, got)) ** 2 > 1 - 1e-2
+
+
+def test_general_gradient_mps_compile():
+    """general_gradient pair selection (the paper setting) on the MPS backend."""
+    from adaptaqc_amd.backends import AerMPSBackend
+    from adaptaqc_amd.compilers import AdaptCompiler, AdaptConfig
+    from adaptaqc_amd.utils.ansatzes import identity_resolvable
+
+    ops = _random_state_circuit(4, 3, 5)
+    qc = to_circuit(4, ops)
+    comp = AdaptCompiler(qc, backend=AerMPSBackend(), adapt_config=AdaptConfig(method="general_gradient"),
+                         custom_layer_2q_gate=identity_resolvable())
+    res = comp.compile()
+    assert res.overlap > 1 - 1e-2
+    assert all(m == "general_gradient" for m in res.method_history)
+    psi = osv.simulate(4, ops)
+    got = osv.simulate(4, [(i.operation.name, i.qubits, tuple(i.operation.params)) for i in res.circuit.data])
+    assert abs(np.vdot(psi, got)) ** 2 > 1 - 1e-2
+
+
+@pytest.mark.parametrize("freq,maxmod,expect", [
+    (4, 3, [0, 0, 5, 10, 0, 0, 5, 10, 0, 0, 5, 10, 0]),
+    (4, 5, [5, 10, 15, 20, 5, 10, 15, 20, 5, 10, 15, 20, 5]),
+])
+def test_mps_absorption_counts(freq, maxmod, expect):
+    """test_adapt_compiler.py:673-718 on the device MPS backend."""
+    from adaptaqc_amd.backends import AerMPSBackend
+    from adaptaqc_amd.compilers import AdaptCompiler, AdaptConfig
+
+    qc = to_circuit(4, _random_state_circuit(4, 3, 1))
+    comp = AdaptCompiler(qc, backend=AerMPSBackend(),
+                         adapt_config=AdaptConfig(rotosolve_frequency=freq, max_layers_to_modify=maxmod, method="basic"))
+    got = []
+    for i in range(13):
+        comp._add_layer(i)
+        got.append(len(comp.full_circuit.data) - 1)
+    assert got == expect
+    # absorbed + live gates reproduce the same state as the reference circuit of all gates
+    from adaptaqc_amd.backends import AerSVBackend
+    from conftest import FakeCompiler
+
+    mps_cost = comp.backend.evaluate_global_cost(comp)
+    sv_cost = AerSVBackend().evaluate_global_cost(FakeCompiler(
+        to_circuit(4, _random_state_circuit(4, 3, 1)).compose(_strip_mps(comp.ref_circuit_as_gates))))
+    assert abs(mps_cost - sv_cost) < 1e-8
+
+
+def _strip_mps(circ):
+    c = circ.copy()
+    del c.data[0]
+    return c
+
+
+def test_sv_and_mps_compiler_costs_agree():
+    """test_approximate_compiler.py:78-112 (global and local cost, SV vs MPS)."""
+    from adaptaqc_amd.backends import AerMPSBackend, AerSVBackend
+    from adaptaqc_amd.compilers import AdaptCompiler
+
+    qc = to_circuit(4, _random_state_circuit(4, 4, 9))
+    for local in (False, True):
+        a = AdaptCompiler(qc, backend=AerSVBackend(), optimise_local_cost=local).evaluate_cost()
+        b = AdaptCompiler(qc, backend=AerMPSBackend(), optimise_local_cost=local).evaluate_cost()
+        assert abs(a - b) < 1e-10
+
+
+def test_checkpoint_resume(tmp_path):
+    """Checkpoints pickle the whole compiler incl. the GPU backend (adapt_compiler.py:484-506)."""
+    from adaptaqc_amd.backends import AerMPSBackend
+    from adaptaqc_amd.compilers import AdaptCompiler, AdaptConfig
+
+    qc = to_circuit(4, _random_state_circuit(4, 2, 3))
+    comp = AdaptCompiler(qc, backend=AerMPSBackend(), adapt_config=AdaptConfig(method="basic", max_layers=3))
+    comp.compile(checkpoint_every=1, checkpoint_dir=str(tmp_path))
+    with open(os.path.join(tmp_path, "1.pkl"), "rb") as f:
+        resumed = pickle.load(f)
+    assert resumed.resume_from_layer == 2
+    resumed.adapt_config.max_layers = 5
+    res = resumed.compile()
+    assert len(res.qubit_pair_history) >= 3
