@@ -38,10 +38,10 @@ namespace {
 
 constexpr int kT = 256;
 constexpr double kChop = 1e-16;
-constexpr int kPanelCplx = 8192;  // 128 KiB of LDS for Jacobi panels
 constexpr int kMaxSweeps = 60;
 // rotation threshold: |a^H b| > tol_factor * L * eps * |a| |b|  (L = column length)
 double g_jacobi_tol_factor = 1.0;
+int g_jacobi_variant = 2;
 
 struct OneSiteJob {
   cplx* g;
@@ -160,7 +160,6 @@ __global__ __launch_bounds__(kT) void k_theta(const TwoSiteJob* __restrict__ job
 // LPP lanes cooperate on one column pair; each lane holds its MAXR rows of both columns in
 // registers for the round (rows interleaved by LPP -> conflict-free 16-B LDS accesses), so a
 // round is one LDS read + one LDS write per element, with every load of the round in flight.
-constexpr int kJT = 512;  // Jacobi workgroup: 8 waves, 2 per SIMD
 
 __device__ __forceinline__ int rr_elem(int pos, int r, int c) {
   // round-robin tournament on c (even) players: position 0 fixed, others rotate.
@@ -169,12 +168,12 @@ __device__ __forceinline__ int rr_elem(int pos, int r, int c) {
 }
 
 // Rotate the pairs of one round.  pair_of(p) -> (ja, jb) column slots in the panel (-1 = skip).
-template <int LPP, int MAXR, typename PairFn>
+template <int LPP, int MAXR, int JT, typename PairFn>
 __device__ __forceinline__ void jacobi_round(cplx* panel, int ld, int L, int npairs, double tol, double floor2,
                                              PairFn pair_of, int* rot_count) {
   const int tid = threadIdx.x;
   const int grp = tid / LPP, lane = tid % LPP;
-  constexpr int kGroups = kJT / LPP;
+  constexpr int kGroups = JT / LPP;
   for (int pbase = 0; pbase < npairs; pbase += kGroups) {
     const int p = pbase + grp;
     int ja = -1, jb = -1;
@@ -237,8 +236,10 @@ __device__ __forceinline__ void jacobi_round(cplx* panel, int ld, int L, int npa
   }
 }
 
-template <int LPP, int MAXR>
-__global__ __launch_bounds__(kJT) void k_jacobi(const TwoSiteJob* __restrict__ jobs) {
+template <int LPP, int MAXR, int JT, int PANEL>
+__global__ __launch_bounds__(JT) void k_jacobi(const TwoSiteJob* __restrict__ jobs) {
+  constexpr int kJT = JT;
+  constexpr int kPanelCplx = PANEL;
   const TwoSiteJob& j = jobs[blockIdx.x];
   __shared__ cplx panel[kPanelCplx];
   __shared__ int rot;
@@ -280,7 +281,7 @@ __global__ __launch_bounds__(kJT) void k_jacobi(const TwoSiteJob* __restrict__ j
         if (tid == 0) rot = 0;
         __syncthreads();
         for (int r = 0; r < ce - 1; ++r) {
-          jacobi_round<LPP, MAXR>(panel, ld, L, ce / 2, tol, floor2,
+          jacobi_round<LPP, MAXR, JT>(panel, ld, L, ce / 2, tol, floor2,
                                   [&](int p, int& a, int& b) {
                                     a = rr_elem(p, r, ce);
                                     b = rr_elem(ce - 1 - p, r, ce);
@@ -308,7 +309,7 @@ __global__ __launch_bounds__(kJT) void k_jacobi(const TwoSiteJob* __restrict__ j
             panel[(idx / L) * ld + idx % L] = W[(size_t)c0 * L + idx];
           __syncthreads();
           for (int r = 0; r < be - 1; ++r) {
-            jacobi_round<LPP, MAXR>(panel, ld, L, be / 2, tol, floor2,
+            jacobi_round<LPP, MAXR, JT>(panel, ld, L, be / 2, tol, floor2,
                                     [&](int p, int& a, int& bb) {
                                       a = rr_elem(p, r, be);
                                       bb = rr_elem(be - 1 - p, r, be);
@@ -331,7 +332,7 @@ __global__ __launch_bounds__(kJT) void k_jacobi(const TwoSiteJob* __restrict__ j
               panel[(b + idx / L) * ld + idx % L] = W[(size_t)cJ * L + idx];
             __syncthreads();
             for (int r = 0; r < b; ++r) {
-              jacobi_round<LPP, MAXR>(panel, ld, L, b, tol, floor2,
+              jacobi_round<LPP, MAXR, JT>(panel, ld, L, b, tol, floor2,
                                       [&](int p, int& a, int& bb) {
                                         const int q = (p + r) % b;
                                         a = p < nI ? p : -1;
@@ -361,6 +362,173 @@ __global__ __launch_bounds__(kJT) void k_jacobi(const TwoSiteJob* __restrict__ j
       for (int off = 1; off < LPP; off <<= 1) s += __shfl_xor(s, off, LPP);
       if (lane == 0) j.sig[col] = sqrt(s);
     }
+  }
+  if (tid == 0) {
+    if (sweeps >= kMaxSweeps) atomicOr(&j.flags[1], 1);
+    atomicMax(&j.flags[2], sweeps + 1);
+  }
+}
+
+// ---- register-resident one-sided Jacobi (2*chi <= 128) ----------------------------------
+// Every column of W stays in VGPRs for the whole decomposition.  CP/2 groups of 16 lanes; group
+// g holds two columns ("S" and "M"), lane l holds rows l, l+16, ... (MAXR rows).  One sweep uses
+// recursive halving: level 0 pairs every S with every M (CP/2 rounds; after each round the M
+// columns shift by one group inside the sub-block), then each sub-block splits into its S half
+// and its M half (one swap exchange) and the same is done inside both halves, down to single
+// groups -- CP-1 rounds per sweep, every round a perfect matching, and only the M half of the
+// columns crosses LDS per round (the previous panel kernel moved every column twice).
+// Columns travel between groups, so each carries its id; it is written back to its own slot
+// (slots >= C hold zero padding columns that are never written).
+template <int CP, int MAXR>
+__global__ __launch_bounds__(CP * 8) void k_jacobi_reg(const TwoSiteJob* __restrict__ jobs) {
+  constexpr int kG = CP / 2;       // groups
+  constexpr int kThreads = kG * 16;
+  constexpr int ld = 16 * MAXR;    // exchange-buffer stride (compile time: no guards)
+  const TwoSiteJob& j = jobs[blockIdx.x];
+  extern __shared__ double2 xbuf[];  // kG * ld complex exchange buffer
+  __shared__ double fred[kThreads / 64];
+  __shared__ int xid[kG];
+  __shared__ int rot;
+  const int chl = j.dims[0], chr = j.dims[2];
+  const int M = 2 * chl, N = 2 * chr;
+  const bool tr = M < N;
+  const int L = tr ? N : M;
+  const int C = tr ? M : N;
+  const int tid = threadIdx.x;
+  const int g = tid >> 4, lane = tid & 15;
+  // plain doubles (real / imaginary planes) so the arrays stay in VGPRs
+  double sr[MAXR], si[MAXR], mr[MAXR], mi[MAXR];
+  int sid = g, mid = g + kG;  // column ids of S and M
+  double f = 0.0;
+#pragma unroll
+  for (int i = 0; i < MAXR; ++i) {
+    const int r = lane + 16 * i;
+    const int cs = g, cm = g + kG;
+    double2 a = make_double2(0, 0), b = make_double2(0, 0);
+    if (r < L && cs < C) a = tr ? aqc::cconj(j.theta[(size_t)r * M + cs]) : j.theta[(size_t)cs * M + r];
+    if (r < L && cm < C) b = tr ? aqc::cconj(j.theta[(size_t)r * M + cm]) : j.theta[(size_t)cm * M + r];
+    sr[i] = a.x;
+    si[i] = a.y;
+    mr[i] = b.x;
+    mi[i] = b.y;
+    f += a.x * a.x + a.y * a.y + b.x * b.x + b.y * b.y;
+  }
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) f += __shfl_xor(f, off);
+  if ((tid & 63) == 0) fred[tid >> 6] = f;
+  __syncthreads();
+  double fro = 0.0;
+#pragma unroll
+  for (int w = 0; w < kThreads / 64; ++w) fro += fred[w];
+  const double floor2 = fro * 1e-24;
+  const double tol = j.jtol * (double)L * 2.220446049250313e-16;
+  const double tol2 = tol * tol;
+  int sweeps = 0;
+  for (sweeps = 0; sweeps < kMaxSweeps; ++sweeps) {
+    if (tid == 0) rot = 0;
+    __syncthreads();
+    int my_rot = 0;
+    for (int m = kG; m >= 1; m >>= 1) {  // level: sub-blocks of m groups
+      const int li = g & (m - 1), base = g - li;
+      for (int r = 0; r < m; ++r) {
+        double al = 0, be = 0, gx = 0, gy = 0;
+#pragma unroll
+        for (int i = 0; i < MAXR; ++i) {
+          al = fma(sr[i], sr[i], fma(si[i], si[i], al));
+          be = fma(mr[i], mr[i], fma(mi[i], mi[i], be));
+          gx = fma(sr[i], mr[i], fma(si[i], mi[i], gx));   // conj(s) * m
+          gy = fma(sr[i], mi[i], fma(-si[i], mr[i], gy));
+        }
+#pragma unroll
+        for (int off = 1; off < 16; off <<= 1) {
+          al += __shfl_xor(al, off, 16);
+          be += __shfl_xor(be, off, 16);
+          gx += __shfl_xor(gx, off, 16);
+          gy += __shfl_xor(gy, off, 16);
+        }
+        const double g2 = gx * gx + gy * gy;
+        if (g2 > tol2 * al * be && al > floor2 && be > floor2) {
+          const double gg = sqrt(g2);
+          const double zeta = (be - al) / (2.0 * gg);
+          const double t = (zeta >= 0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
+          const double c = 1.0 / sqrt(1.0 + t * t);
+          const double sc = c * t / gg;
+          const double ex = gx * sc, ey = gy * sc;  // s e  (s conj(e) = (ex, -ey))
+#pragma unroll
+          for (int i = 0; i < MAXR; ++i) {
+            const double ar = sr[i], ai = si[i], br = mr[i], bi = mi[i];
+            // a' = c a - s conj(e) b ; b' = s e a + c b
+            sr[i] = fma(c, ar, -fma(ex, br, ey * bi));
+            si[i] = fma(c, ai, -fma(ex, bi, -ey * br));
+            mr[i] = fma(c, br, fma(ex, ar, -ey * ai));
+            mi[i] = fma(c, bi, fma(ex, ai, ey * ar));
+          }
+          my_rot = 1;
+        }
+        if (r == m - 1) break;
+        // shift M inside the sub-block: group li receives M of group (li + 1) % m
+#pragma unroll
+        for (int i = 0; i < MAXR; ++i) xbuf[g * ld + lane + 16 * i] = make_double2(mr[i], mi[i]);
+        if (lane == 0) xid[g] = mid;
+        __syncthreads();
+        const int src = base + ((li + 1) & (m - 1));
+#pragma unroll
+        for (int i = 0; i < MAXR; ++i) {
+          const double2 v = xbuf[src * ld + lane + 16 * i];
+          mr[i] = v.x;
+          mi[i] = v.y;
+        }
+        mid = xid[src];
+        __syncthreads();
+      }
+      if (m == 1) break;
+      // split the sub-block: group li < m/2 swaps its M with the S of group li + m/2
+      const int h = m >> 1;
+      const bool lowh = li < h;
+#pragma unroll
+      for (int i = 0; i < MAXR; ++i)
+        xbuf[g * ld + lane + 16 * i] = lowh ? make_double2(mr[i], mi[i]) : make_double2(sr[i], si[i]);
+      if (lane == 0) xid[g] = lowh ? mid : sid;
+      __syncthreads();
+      const int partner = lowh ? g + h : g - h;
+      const int pid = xid[partner];
+      mid = lowh ? pid : mid;
+      sid = lowh ? sid : pid;
+#pragma unroll
+      for (int i = 0; i < MAXR; ++i) {
+        const double2 v = xbuf[partner * ld + lane + 16 * i];
+        // low half: new M = S of the upper partner; high half: new S = M of the lower partner
+        mr[i] = lowh ? v.x : mr[i];
+        mi[i] = lowh ? v.y : mi[i];
+        sr[i] = lowh ? sr[i] : v.x;
+        si[i] = lowh ? si[i] : v.y;
+      }
+      __syncthreads();
+    }
+    if (my_rot && lane == 0) atomicAdd(&rot, 1);
+    __syncthreads();
+    if (rot == 0) break;
+    __syncthreads();
+  }
+  // write columns (any order: k_rank sorts by norm) and their norms
+  double2* W = j.work;
+  double ns = 0, nm = 0;
+#pragma unroll
+  for (int i = 0; i < MAXR; ++i) {
+    const int row = lane + 16 * i;
+    if (row < L && sid < C) W[(size_t)sid * L + row] = make_double2(sr[i], si[i]);
+    if (row < L && mid < C) W[(size_t)mid * L + row] = make_double2(mr[i], mi[i]);
+    ns = fma(sr[i], sr[i], fma(si[i], si[i], ns));
+    nm = fma(mr[i], mr[i], fma(mi[i], mi[i], nm));
+  }
+#pragma unroll
+  for (int off = 1; off < 16; off <<= 1) {
+    ns += __shfl_xor(ns, off, 16);
+    nm += __shfl_xor(nm, off, 16);
+  }
+  if (lane == 0) {
+    if (sid < C) j.sig[sid] = sqrt(ns);
+    if (mid < C) j.sig[mid] = sqrt(nm);
   }
   if (tid == 0) {
     if (sweeps >= kMaxSweeps) atomicOr(&j.flags[1], 1);
@@ -1008,11 +1176,28 @@ int run_waves(aqc_mps_t* hs, int ns, std::vector<std::vector<DevOp>>& lists) {
       aqc::KernelTimer::end(st);
       AQC_CHECK_LAUNCH();
       aqc::KernelTimer::begin(st, "mps_svd", nj * 2.0 * (4.0 * c * c * 16), 0.0);
-      // rows per lane from the largest possible column length (2 * cap)
-      if (2 * cap_max <= 64) hipLaunchKernelGGL((k_jacobi<16, 4>), dim3(nj), dim3(kJT), 0, st, jp);
-      else if (2 * cap_max <= 128) hipLaunchKernelGGL((k_jacobi<16, 8>), dim3(nj), dim3(kJT), 0, st, jp);
-      else if (2 * cap_max <= 256) hipLaunchKernelGGL((k_jacobi<16, 16>), dim3(nj), dim3(kJT), 0, st, jp);
-      else hipLaunchKernelGGL((k_jacobi<32, 16>), dim3(nj), dim3(kJT), 0, st, jp);
+      // rows per lane from the largest possible column length (2 * cap); variant 1 = half-size
+      // panel and workgroup so two decompositions share a CU
+      const bool half = g_jacobi_variant == 1;
+      if (g_jacobi_variant == 2 && 2 * cap_max <= 128) {
+        // register-resident kernel; column count padded to a power of two
+        if (2 * cap_max <= 32)
+          hipLaunchKernelGGL((k_jacobi_reg<32, 2>), dim3(nj), dim3(256), 16 * 32 * 16, st, jp);
+        else if (2 * cap_max <= 64)
+          hipLaunchKernelGGL((k_jacobi_reg<64, 4>), dim3(nj), dim3(512), 32 * 64 * 16, st, jp);
+        else
+          hipLaunchKernelGGL((k_jacobi_reg<128, 8>), dim3(nj), dim3(1024), 64 * 128 * 16, st, jp);
+      } else if (2 * cap_max <= 64) {
+        if (half) hipLaunchKernelGGL((k_jacobi<16, 4, 256, 4096>), dim3(nj), dim3(256), 0, st, jp);
+        else hipLaunchKernelGGL((k_jacobi<16, 4, 512, 8192>), dim3(nj), dim3(512), 0, st, jp);
+      } else if (2 * cap_max <= 128) {
+        if (half) hipLaunchKernelGGL((k_jacobi<16, 8, 256, 4096>), dim3(nj), dim3(256), 0, st, jp);
+        else hipLaunchKernelGGL((k_jacobi<16, 8, 512, 8192>), dim3(nj), dim3(512), 0, st, jp);
+      } else if (2 * cap_max <= 256) {
+        hipLaunchKernelGGL((k_jacobi<16, 16, 512, 8192>), dim3(nj), dim3(512), 0, st, jp);
+      } else {
+        hipLaunchKernelGGL((k_jacobi<32, 16, 512, 8192>), dim3(nj), dim3(512), 0, st, jp);
+      }
       aqc::KernelTimer::end(st);
       AQC_CHECK_LAUNCH();
       hipLaunchKernelGGL(k_rank, dim3(nj), dim3(kT), 0, st, jp);
@@ -1166,6 +1351,12 @@ int aqc_mps_jacobi_stats(aqc_mps_t h, int* max_sweeps) {
 int aqc_mps_set_jacobi_tol(double factor) {
   AQC_REQUIRE(factor > 0, "aqc_mps_set_jacobi_tol: factor must be positive");
   g_jacobi_tol_factor = factor;
+  return AQC_OK;
+}
+
+int aqc_mps_set_jacobi_variant(int variant) {
+  AQC_REQUIRE(variant >= 0 && variant <= 2, "aqc_mps_set_jacobi_variant: variant must be 0, 1 or 2");
+  g_jacobi_variant = variant;
   return AQC_OK;
 }
 

@@ -97,6 +97,9 @@ int aqc_mps_apply_batch(aqc_mps_t* hs, int nstates, const aqc_op_t* const* ops, 
 int aqc_mps_jacobi_stats(aqc_mps_t h, int* max_sweeps);
 /* Jacobi rotation threshold |a^H b| > factor * L * eps * |a||b| (default factor 1). */
 int aqc_mps_set_jacobi_tol(double factor);
+/* Jacobi kernel: 2 = register-resident columns for 2*chi <= 128 (default; larger chi uses 0),
+   0 = 512 threads / 128 KiB LDS panel, 1 = 256 threads / 64 KiB panel (2 per CU). */
+int aqc_mps_set_jacobi_variant(int variant);
 /* move_all_qubits_to_sorted_ordering (done implicitly by every measurement below). */
 int aqc_mps_sort(aqc_mps_t h);
 int aqc_mps_sort_batch(aqc_mps_t* hs, int nstates);

@@ -193,3 +193,38 @@ def test_batch_apply_matches_single():
         d = DeviceMPS(n, 16, 1e-16, 8)
         d.apply(lists[s])
         assert abs(d.overlap_zero() - ov[s]) < 1e-13
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2])
+def test_jacobi_variants_vs_oracle(goldens, variant):
+    """Every Jacobi kernel shape reproduces the oracle (small, ragged and full-width theta)."""
+    from adaptaqc_amd import _lib
+    from adaptaqc_amd.circuit import device_ops
+    from adaptaqc_amd.device import DeviceMPS
+
+    _lib.check(_lib.lib().aqc_mps_set_jacobi_variant(variant))
+    try:
+        for seed in range(3):
+            for chi in (0, 4):
+                d = DeviceMPS(8, 16, 1e-16, chi or None)
+                d.apply(device_ops(to_circuit(8, golden_ops(goldens, seed))))
+                assert abs(d.overlap_zero() - complex(goldens[f"circ{seed}_chi{chi}_ov0"])) < 1e-10
+                np.testing.assert_array_equal(d.dims(), goldens[f"circ{seed}_chi{chi}_dims"])
+        rng = np.random.default_rng(21)
+        for n, chi in ((12, 32), (16, 64)):
+            ops = []
+            for layer in range(8):
+                for q in range(n):
+                    ops.append(("ry", (q,), (rng.uniform(-np.pi, np.pi),)))
+                    ops.append(("rz", (q,), (rng.uniform(-np.pi, np.pi),)))
+                for q in range(layer % 2, n - 1, 2):
+                    ops.append(("cx", (q, q + 1), ()))
+            ops.append(("cx", (1, n - 2), ()))
+            ref = M.run_circuit(n, ops, 1e-16, chi)
+            d = DeviceMPS(n, chi, 1e-16, chi)
+            d.apply(device_ops(to_circuit(n, ops)))
+            np.testing.assert_array_equal(d.dims(), [1] + [x.shape[2] for x in ref.preprocessed()])
+            ov_ref = M.mps_dot(ref.preprocessed(), M.zero_mps(n))
+            assert abs(d.overlap_zero() - ov_ref) <= 1e-8 * abs(ov_ref) + 1e-18
+    finally:
+        _lib.check(_lib.lib().aqc_mps_set_jacobi_variant(2))
