@@ -41,7 +41,7 @@ constexpr double kChop = 1e-16;
 constexpr int kMaxSweeps = 60;
 // rotation threshold: |a^H b| > tol_factor * L * eps * |a| |b|  (L = column length)
 double g_jacobi_tol_factor = 1.0;
-int g_jacobi_variant = 2;
+int g_jacobi_variant = 3;  // 2 (pivoted-QR preconditioning) once its parity is green
 
 struct OneSiteJob {
   cplx* g;
@@ -67,7 +67,8 @@ struct TwoSiteJob {
   int max_chi;
   double thr;
   double jtol;  // Jacobi rotation threshold factor
-  double pad2;
+  int qr;       // 1: Jacobi ran on R^H of a pivoted QR -> W holds the other side (see k_jacobi_reg)
+  int dbg;      // diagnostics (aqc_svd_debug): 1 = stop after the QR phase, write X unpermuted
   cplx G[16];  // row = 2*s1'+s2' (out), col = 2*s1+s2 (in)
 };
 
@@ -230,7 +231,7 @@ __device__ __forceinline__ void jacobi_round(cplx* panel, int ld, int L, int npa
             cb[r] = aqc::cfma(se, a, aqc::cscale(b, c));
           }
         }
-        if (lane == 0) atomicAdd(rot_count, 1);
+        if (lane == 0 && g > 4.0 * tol * sqrt(al * be)) atomicAdd(rot_count, 1);  // above noise
       }
     }
   }
@@ -376,24 +377,85 @@ __global__ __launch_bounds__(JT) void k_jacobi(const TwoSiteJob* __restrict__ jo
 // columns shift by one group inside the sub-block), then each sub-block splits into its S half
 // and its M half (one swap exchange) and the same is done inside both halves, down to single
 // groups -- CP-1 rounds per sweep, every round a perfect matching, and only the M half of the
-// columns crosses LDS per round (the previous panel kernel moved every column twice).
-// Columns travel between groups, so each carries its id; it is written back to its own slot
-// (slots >= C hold zero padding columns that are never written).
+// columns crosses LDS per round.  Columns travel between groups, so each carries its id; it is
+// written back to its own slot (slots >= C hold zero padding columns that are never written).
+//
+// Preconditioning (j.qr, Drmac-Veselic): W P = Q R by Householder QR with column pivoting, done
+// in the same register layout, then the Jacobi runs on X = R^H.  The bench's two-site thetas
+// (swap-routed, graded lambdas) need 14-25 sweeps plain and 7-9 after QRP, and a batched launch
+// waits for its slowest decomposition.  X's orthogonalised columns are the singular vectors of
+// the *other* side times sigma (rows mapped back through the pivot order P), which k_split
+// handles by flipping its side test (tools/qrp_jacobi_proto.py is the numpy restatement).
+
+// sortable pivot key: non-negative double bits with the low byte replaced by (255 - id), so
+// that the 64-bit maximum is the largest trailing norm, ties to the lowest column id
+__device__ __forceinline__ unsigned long long pivot_key(double v, int id) {
+  return ((unsigned long long)__double_as_longlong(v) & ~255ull) | (unsigned long long)(255 - id);
+}
+
+// Householder step k on the pivot column x (this group's S or M): v (zlarfg convention, v_k = 1)
+// and tau go to LDS, x becomes R's column (beta on the diagonal, zeros below).
+template <int MAXR>
+__device__ __forceinline__ void qr_reflector(double (&xr)[MAXR], double (&xi)[MAXR], int k, int lane, double2* vb,
+                                             double2* tb) {
+  const int kr = k >> 4;
+  double ar = 0, ai = 0, s2 = 0;
+#pragma unroll
+  for (int i = 0; i < MAXR; ++i) {
+    const int row = lane + 16 * i;
+    if (i == kr) ar = xr[i], ai = xi[i];
+    const double w = row > k ? 1.0 : 0.0;
+    s2 = fma(w, fma(xr[i], xr[i], xi[i] * xi[i]), s2);
+  }
+  ar = __shfl(ar, k & 15, 16);
+  ai = __shfl(ai, k & 15, 16);
+  s2 = aqc::row_sum16(s2);
+  double beta, tr_, ti_, cr = 0, ci = 0;  // tau = (tr_, ti_), scale = 1 / (alpha - beta)
+  if (s2 == 0.0 && ai == 0.0) {
+    beta = ar, tr_ = 0.0, ti_ = 0.0;
+  } else {
+    const double nrm = sqrt(fma(ar, ar, fma(ai, ai, s2)));
+    beta = ar >= 0.0 ? -nrm : nrm;
+    tr_ = (beta - ar) / beta;
+    ti_ = -ai / beta;
+    const double dr = ar - beta, di = ai, id2 = 1.0 / fma(dr, dr, di * di);
+    cr = dr * id2, ci = -di * id2;
+  }
+#pragma unroll
+  for (int i = 0; i < MAXR; ++i) {
+    const int row = lane + 16 * i;
+    double2 v = make_double2(0, 0);
+    if (row > k) v = make_double2(xr[i] * cr - xi[i] * ci, xr[i] * ci + xi[i] * cr);
+    if (row == k) v = make_double2(1.0, 0.0);
+    vb[row] = v;
+    const double nr = row == k ? beta : (row > k ? 0.0 : xr[i]);
+    const double ni = row >= k ? 0.0 : xi[i];
+    xr[i] = nr, xi[i] = ni;
+  }
+  if (lane == 0) *tb = make_double2(tr_, ti_);
+}
+
 template <int CP, int MAXR>
 __global__ __launch_bounds__(CP * 8) void k_jacobi_reg(const TwoSiteJob* __restrict__ jobs) {
   constexpr int kG = CP / 2;       // groups
   constexpr int kThreads = kG * 16;
   constexpr int ld = 16 * MAXR;    // exchange-buffer stride (compile time: no guards)
+  constexpr int ldt = CP + 1;      // transpose-buffer stride (odd: conflict-free column writes)
   const TwoSiteJob& j = jobs[blockIdx.x];
-  extern __shared__ double2 xbuf[];  // kG * ld complex exchange buffer
+  extern __shared__ double2 xbuf[];  // max(kG * ld, kG * ldt) complex
   __shared__ double fred[kThreads / 64];
   __shared__ int xid[kG];
   __shared__ int rot;
+  __shared__ unsigned long long pkey[2];
+  __shared__ double2 vb[2][CP];
+  __shared__ double2 tb[2];
+  __shared__ int perm_s[CP];
   const int chl = j.dims[0], chr = j.dims[2];
   const int M = 2 * chl, N = 2 * chr;
   const bool tr = M < N;
   const int L = tr ? N : M;
   const int C = tr ? M : N;
+  const bool use_qr = j.qr != 0;
   const int tid = threadIdx.x;
   const int g = tid >> 4, lane = tid & 15;
   // plain doubles (real / imaginary planes) so the arrays stay in VGPRs
@@ -416,15 +478,99 @@ __global__ __launch_bounds__(CP * 8) void k_jacobi_reg(const TwoSiteJob* __restr
 #pragma unroll
   for (int off = 1; off < 64; off <<= 1) f += __shfl_xor(f, off);
   if ((tid & 63) == 0) fred[tid >> 6] = f;
+  if (tid == 0) pkey[0] = pkey[1] = 0ull;
   __syncthreads();
   double fro = 0.0;
 #pragma unroll
   for (int w = 0; w < kThreads / 64; ++w) fro += fred[w];
+  int Lj = L;  // row count of the matrix the Jacobi sees
+  if (use_qr) {
+    int ks = -1, km = -1;  // pivot step of S / M (-1: not pivoted yet)
+    for (int k = 0; k < C; ++k) {
+      const int b = k & 1;
+      // trailing squared norms (rows >= k) of the unpivoted columns
+      double ns = 0, nm = 0;
+#pragma unroll
+      for (int i = 0; i < MAXR; ++i) {
+        const double w = (lane + 16 * i) >= k ? 1.0 : 0.0;
+        ns = fma(w, fma(sr[i], sr[i], si[i] * si[i]), ns);
+        nm = fma(w, fma(mr[i], mr[i], mi[i] * mi[i]), nm);
+      }
+      ns = aqc::row_sum16(ns);
+      nm = aqc::row_sum16(nm);
+      const unsigned long long ka = (ks < 0 && sid < C) ? pivot_key(ns, sid) : 0ull;
+      const unsigned long long kb = (km < 0 && mid < C) ? pivot_key(nm, mid) : 0ull;
+      if (lane == 0) atomicMax(&pkey[b], ka > kb ? ka : kb);
+      __syncthreads();
+      const int p = 255 - (int)(pkey[b] & 255ull);
+      if (tid == 0) pkey[b ^ 1] = 0ull;
+      if (sid == p) {  // this group owns the pivot column: build the reflector
+        qr_reflector<MAXR>(sr, si, k, lane, vb[b], &tb[b]);
+        ks = k;
+      } else if (mid == p) {
+        qr_reflector<MAXR>(mr, mi, k, lane, vb[b], &tb[b]);
+        km = k;
+      }
+      if (tid == 0) perm_s[k] = p;
+      __syncthreads();
+      // c <- H^H c = c - conj(tau) v (v^H c) for every unpivoted column
+      const double2 tau = tb[b];
+      double wsr = 0, wsi = 0, wmr = 0, wmi = 0;
+#pragma unroll
+      for (int i = 0; i < MAXR; ++i) {  // v^H c (v re-read from LDS below: saves 4*MAXR VGPRs)
+        const double2 v = vb[b][lane + 16 * i];
+        wsr = fma(v.x, sr[i], fma(v.y, si[i], wsr));
+        wsi = fma(v.x, si[i], fma(-v.y, sr[i], wsi));
+        wmr = fma(v.x, mr[i], fma(v.y, mi[i], wmr));
+        wmi = fma(v.x, mi[i], fma(-v.y, mr[i], wmi));
+      }
+      wsr = aqc::row_sum16(wsr);
+      wsi = aqc::row_sum16(wsi);
+      wmr = aqc::row_sum16(wmr);
+      wmi = aqc::row_sum16(wmi);
+      // f = conj(tau) * w ; c -= v * f
+      const double as = ks < 0 ? 1.0 : 0.0, am = km < 0 ? 1.0 : 0.0;
+      const double fsr = as * (tau.x * wsr + tau.y * wsi), fsi = as * (tau.x * wsi - tau.y * wsr);
+      const double fmr = am * (tau.x * wmr + tau.y * wmi), fmi = am * (tau.x * wmi - tau.y * wmr);
+#pragma unroll
+      for (int i = 0; i < MAXR; ++i) {
+        const double2 v = vb[b][lane + 16 * i];
+        sr[i] -= v.x * fsr - v.y * fsi;
+        si[i] -= v.x * fsi + v.y * fsr;
+        mr[i] -= v.x * fmr - v.y * fmi;
+        mi[i] -= v.x * fmi + v.y * fmr;
+      }
+    }
+    // X = R^H: X[i][jx] = conj(R[jx][column pivoted at step i]); new S / M = X columns g, g + kG
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+#pragma unroll
+      for (int i = h * MAXR / 2; i < (h + 1) * MAXR / 2; ++i) {
+        const int jx = lane + 16 * i - h * kG;
+        if (ks >= 0) xbuf[jx * ldt + ks] = make_double2(sr[i], -si[i]);
+        if (km >= 0) xbuf[jx * ldt + km] = make_double2(mr[i], -mi[i]);
+      }
+      __syncthreads();
+      const int jx = g + h * kG;
+#pragma unroll
+      for (int i = 0; i < MAXR; ++i) {
+        const int row = lane + 16 * i;
+        double2 v = make_double2(0, 0);
+        if (row < C && jx < C) v = xbuf[g * ldt + row];
+        if (h == 0) sr[i] = v.x, si[i] = v.y;
+        else mr[i] = v.x, mi[i] = v.y;
+      }
+      __syncthreads();
+    }
+    Lj = C;
+  }
   const double floor2 = fro * 1e-24;
-  const double tol = j.jtol * (double)L * 2.220446049250313e-16;
+  const double tol = j.jtol * (double)Lj * 2.220446049250313e-16;
   const double tol2 = tol * tol;
+  const int max_sweeps = j.dbg == 1 ? 0 : kMaxSweeps;
+  const bool map_rows = use_qr && j.dbg != 1;
   int sweeps = 0;
-  for (sweeps = 0; sweeps < kMaxSweeps; ++sweeps) {
+  for (sweeps = 0; sweeps < max_sweeps; ++sweeps) {
     if (tid == 0) rot = 0;
     __syncthreads();
     int my_rot = 0;
@@ -439,15 +585,16 @@ __global__ __launch_bounds__(CP * 8) void k_jacobi_reg(const TwoSiteJob* __restr
           gx = fma(sr[i], mr[i], fma(si[i], mi[i], gx));   // conj(s) * m
           gy = fma(sr[i], mi[i], fma(-si[i], mr[i], gy));
         }
-#pragma unroll
-        for (int off = 1; off < 16; off <<= 1) {
-          al += __shfl_xor(al, off, 16);
-          be += __shfl_xor(be, off, 16);
-          gx += __shfl_xor(gx, off, 16);
-          gy += __shfl_xor(gy, off, 16);
-        }
+        al = aqc::row_sum16(al);
+        be = aqc::row_sum16(be);
+        gx = aqc::row_sum16(gx);
+        gy = aqc::row_sum16(gy);
         const double g2 = gx * gx + gy * gy;
-        if (g2 > tol2 * al * be && al > floor2 && be > floor2) {
+        const double ab = al * be;
+        if (g2 > tol2 * ab && al > floor2 && be > floor2) {
+          // only rotations above dot-product noise keep the sweep loop going: a pair of
+          // (near-)degenerate columns can otherwise flip-flop at |g| ~ tol forever
+          if (g2 > 16.0 * tol2 * ab) my_rot = 1;
           const double gg = sqrt(g2);
           const double zeta = (be - al) / (2.0 * gg);
           const double t = (zeta >= 0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
@@ -463,7 +610,6 @@ __global__ __launch_bounds__(CP * 8) void k_jacobi_reg(const TwoSiteJob* __restr
             mr[i] = fma(c, br, fma(ex, ar, -ey * ai));
             mi[i] = fma(c, bi, fma(ex, ai, ey * ar));
           }
-          my_rot = 1;
         }
         if (r == m - 1) break;
         // shift M inside the sub-block: group li receives M of group (li + 1) % m
@@ -510,22 +656,23 @@ __global__ __launch_bounds__(CP * 8) void k_jacobi_reg(const TwoSiteJob* __restr
     if (rot == 0) break;
     __syncthreads();
   }
-  // write columns (any order: k_rank sorts by norm) and their norms
+  // write columns to their own slots (with QR: rows mapped back through the pivot order) and
+  // their norms
   double2* W = j.work;
   double ns = 0, nm = 0;
 #pragma unroll
   for (int i = 0; i < MAXR; ++i) {
     const int row = lane + 16 * i;
-    if (row < L && sid < C) W[(size_t)sid * L + row] = make_double2(sr[i], si[i]);
-    if (row < L && mid < C) W[(size_t)mid * L + row] = make_double2(mr[i], mi[i]);
+    if (row < Lj) {
+      const int orow = map_rows ? perm_s[row] : row;
+      if (sid < C) W[(size_t)sid * Lj + orow] = make_double2(sr[i], si[i]);
+      if (mid < C) W[(size_t)mid * Lj + orow] = make_double2(mr[i], mi[i]);
+    }
     ns = fma(sr[i], sr[i], fma(si[i], si[i], ns));
     nm = fma(mr[i], mr[i], fma(mi[i], mi[i], nm));
   }
-#pragma unroll
-  for (int off = 1; off < 16; off <<= 1) {
-    ns += __shfl_xor(ns, off, 16);
-    nm += __shfl_xor(nm, off, 16);
-  }
+  ns = aqc::row_sum16(ns);
+  nm = aqc::row_sum16(nm);
   if (lane == 0) {
     if (sid < C) j.sig[sid] = sqrt(ns);
     if (mid < C) j.sig[mid] = sqrt(nm);
@@ -533,6 +680,9 @@ __global__ __launch_bounds__(CP * 8) void k_jacobi_reg(const TwoSiteJob* __restr
   if (tid == 0) {
     if (sweeps >= kMaxSweeps) atomicOr(&j.flags[1], 1);
     atomicMax(&j.flags[2], sweeps + 1);
+  }
+  if (j.dbg == 1 && use_qr) {  // diagnostics: pivot order after the W columns
+    for (int k = tid; k < C; k += kThreads) j.perm[k] = perm_s[k];
   }
 }
 
@@ -610,7 +760,8 @@ __global__ __launch_bounds__(kT) void k_split_copy(const TwoSiteJob* __restrict_
   const TwoSiteJob& j = jobs[blockIdx.y];
   const int chl = j.dims[0], k = j.dims[1], chr = j.dims[2];
   const int M = 2 * chl, N = 2 * chr;
-  const bool tr = M < N;
+  // tr: W's columns are V-side (length N); the QR-preconditioned Jacobi flips the side
+  const bool tr = (M < N) != (j.qr != 0);
   const int L = tr ? N : M;
   const int cap = j.cap;
   const size_t half = (size_t)cap * cap;
@@ -643,7 +794,7 @@ __global__ __launch_bounds__(kT) void k_split_gemm(const TwoSiteJob* __restrict_
   const TwoSiteJob& j = jobs[blockIdx.y];
   const int chl = j.dims[0], k = j.dims[1], chr = j.dims[2];
   const int M = 2 * chl, N = 2 * chr;
-  const bool tr = M < N;
+  const bool tr = (M < N) != (j.qr != 0);  // as in k_split_copy
   const int L = tr ? N : M;
   const int cap = j.cap;
   const size_t half = (size_t)cap * cap;
@@ -1137,13 +1288,19 @@ int run_waves(aqc_mps_t* hs, int ns, std::vector<std::vector<DevOp>>& lists) {
   std::vector<std::pair<size_t, size_t>> two_rng(maxlen), one_rng(maxlen);
   int cap_max = 0;
   for (int s = 0; s < ns; ++s) cap_max = std::max(cap_max, hs[s]->d.cap);
+  const bool reg = (g_jacobi_variant == 2 || g_jacobi_variant == 3) && 2 * cap_max <= 128;
+  const int use_qr = reg && g_jacobi_variant == 2 ? 1 : 0;
   for (size_t w = 0; w < maxlen; ++w) {
     size_t t0 = two.size(), o0 = one.size();
     for (int s = 0; s < ns; ++s) {
       if (w >= lists[s].size()) continue;
       const DevOp& op = lists[s][w];
-      if (op.kind == 2) two.push_back(make_two(hs[s], op));
-      else one.push_back(make_one(hs[s], op));
+      if (op.kind == 2) {
+        two.push_back(make_two(hs[s], op));
+        two.back().qr = use_qr;
+      } else {
+        one.push_back(make_one(hs[s], op));
+      }
     }
     two_rng[w] = {t0, two.size() - t0};
     one_rng[w] = {o0, one.size() - o0};
@@ -1179,14 +1336,15 @@ int run_waves(aqc_mps_t* hs, int ns, std::vector<std::vector<DevOp>>& lists) {
       // rows per lane from the largest possible column length (2 * cap); variant 1 = half-size
       // panel and workgroup so two decompositions share a CU
       const bool half = g_jacobi_variant == 1;
-      if (g_jacobi_variant == 2 && 2 * cap_max <= 128) {
-        // register-resident kernel; column count padded to a power of two
+      if (reg) {
+        // register-resident kernel; column count padded to a power of two.  Dynamic LDS holds
+        // the round exchange (kG x 16*MAXR) or the QR transpose (kG x (CP+1)), whichever is larger
         if (2 * cap_max <= 32)
-          hipLaunchKernelGGL((k_jacobi_reg<32, 2>), dim3(nj), dim3(256), 16 * 32 * 16, st, jp);
+          hipLaunchKernelGGL((k_jacobi_reg<32, 2>), dim3(nj), dim3(256), 16 * 33 * 16, st, jp);
         else if (2 * cap_max <= 64)
-          hipLaunchKernelGGL((k_jacobi_reg<64, 4>), dim3(nj), dim3(512), 32 * 64 * 16, st, jp);
+          hipLaunchKernelGGL((k_jacobi_reg<64, 4>), dim3(nj), dim3(512), 32 * 65 * 16, st, jp);
         else
-          hipLaunchKernelGGL((k_jacobi_reg<128, 8>), dim3(nj), dim3(1024), 64 * 128 * 16, st, jp);
+          hipLaunchKernelGGL((k_jacobi_reg<128, 8>), dim3(nj), dim3(1024), 64 * 129 * 16, st, jp);
       } else if (2 * cap_max <= 64) {
         if (half) hipLaunchKernelGGL((k_jacobi<16, 4, 256, 4096>), dim3(nj), dim3(256), 0, st, jp);
         else hipLaunchKernelGGL((k_jacobi<16, 4, 512, 8192>), dim3(nj), dim3(512), 0, st, jp);
@@ -1336,6 +1494,57 @@ int aqc_mps_destroy(aqc_mps_t h) {
   return AQC_OK;
 }
 
+int aqc_svd_debug(const double* theta, int m, int n, int variant, int stop_after_qr, double* w_out,
+                  double* sig_out, int* perm_out, int* sweeps) {
+  AQC_REQUIRE(theta && w_out && sig_out && sweeps, "aqc_svd_debug: null argument");
+  AQC_REQUIRE(m >= 1 && n >= 1 && m % 2 == 0 && n % 2 == 0 && m <= 128 && n <= 128,
+              "aqc_svd_debug: m, n must be even and <= 128");
+  AQC_REQUIRE(variant == 2 || variant == 3, "aqc_svd_debug: variant must be 2 or 3");
+  hipStream_t st = aqc::mps_stream();
+  const int cp = std::max(m, n) <= 32 ? 32 : (std::max(m, n) <= 64 ? 64 : 128);
+  const size_t mat = (size_t)128 * 128 * sizeof(cplx);
+  char* buf = nullptr;
+  AQC_HIP_CHECK(hipMalloc(&buf, 2 * mat + 1024 * sizeof(double) + 512 * sizeof(int) + 4 * sizeof(int) +
+                                    sizeof(TwoSiteJob)));
+  cplx* th = (cplx*)buf;
+  cplx* wk = (cplx*)(buf + mat);
+  double* sg = (double*)(buf + 2 * mat);
+  int* pm = (int*)(sg + 1024);
+  int* dm = pm + 512;  // dims[3] + flags share this tail
+  int* fl = dm + 4;
+  TwoSiteJob* dj = (TwoSiteJob*)(fl + 4);
+  TwoSiteJob j;
+  std::memset(&j, 0, sizeof(j));
+  j.dims = dm;
+  j.theta = th;
+  j.work = wk;
+  j.sig = sg;
+  j.perm = pm;
+  j.flags = fl;
+  j.jtol = g_jacobi_tol_factor;
+  j.qr = variant == 2 ? 1 : 0;
+  j.dbg = stop_after_qr ? 1 : 0;
+  int hd[8] = {m / 2, 0, n / 2, 0, 0, 0, 0, 0};  // dims, then zeroed flags
+  AQC_HIP_CHECK(hipMemcpyAsync(th, theta, (size_t)m * n * sizeof(cplx), hipMemcpyHostToDevice, st));
+  AQC_HIP_CHECK(hipMemcpyAsync(dm, hd, sizeof(hd), hipMemcpyHostToDevice, st));
+  AQC_HIP_CHECK(hipMemcpyAsync(dj, &j, sizeof(j), hipMemcpyHostToDevice, st));
+  AQC_HIP_CHECK(hipMemsetAsync(wk, 0, mat, st));
+  if (cp == 32) hipLaunchKernelGGL((k_jacobi_reg<32, 2>), dim3(1), dim3(256), 16 * 33 * 16, st, dj);
+  else if (cp == 64) hipLaunchKernelGGL((k_jacobi_reg<64, 4>), dim3(1), dim3(512), 32 * 65 * 16, st, dj);
+  else hipLaunchKernelGGL((k_jacobi_reg<128, 8>), dim3(1), dim3(1024), 64 * 129 * 16, st, dj);
+  AQC_CHECK_LAUNCH();
+  const int L = std::max(m, n), C = std::min(m, n);
+  const int Lw = j.qr ? C : L;
+  AQC_HIP_CHECK(hipMemcpyAsync(w_out, wk, (size_t)C * Lw * sizeof(cplx), hipMemcpyDeviceToHost, st));
+  AQC_HIP_CHECK(hipMemcpyAsync(sig_out, sg, (size_t)C * sizeof(double), hipMemcpyDeviceToHost, st));
+  if (perm_out) AQC_HIP_CHECK(hipMemcpyAsync(perm_out, pm, (size_t)C * sizeof(int), hipMemcpyDeviceToHost, st));
+  AQC_HIP_CHECK(hipMemcpyAsync(hd, fl, 4 * sizeof(int), hipMemcpyDeviceToHost, st));
+  AQC_HIP_CHECK(hipStreamSynchronize(st));
+  *sweeps = hd[2];
+  AQC_HIP_CHECK(hipFree(buf));
+  return AQC_OK;
+}
+
 int aqc_mps_jacobi_stats(aqc_mps_t h, int* max_sweeps) {
   AQC_REQUIRE(h && max_sweeps, "aqc_mps_jacobi_stats: null argument");
   hipStream_t st = aqc::mps_stream();
@@ -1355,7 +1564,7 @@ int aqc_mps_set_jacobi_tol(double factor) {
 }
 
 int aqc_mps_set_jacobi_variant(int variant) {
-  AQC_REQUIRE(variant >= 0 && variant <= 2, "aqc_mps_set_jacobi_variant: variant must be 0, 1 or 2");
+  AQC_REQUIRE(variant >= 0 && variant <= 3, "aqc_mps_set_jacobi_variant: variant must be 0..3");
   g_jacobi_variant = variant;
   return AQC_OK;
 }

@@ -97,9 +97,17 @@ int aqc_mps_apply_batch(aqc_mps_t* hs, int nstates, const aqc_op_t* const* ops, 
 int aqc_mps_jacobi_stats(aqc_mps_t h, int* max_sweeps);
 /* Jacobi rotation threshold |a^H b| > factor * L * eps * |a||b| (default factor 1). */
 int aqc_mps_set_jacobi_tol(double factor);
-/* Jacobi kernel: 2 = register-resident columns for 2*chi <= 128 (default; larger chi uses 0),
+/* Jacobi kernel: 2 = register-resident columns with pivoted-QR preconditioning for
+   2*chi <= 128 (default; larger chi uses 0), 3 = register-resident without QR,
    0 = 512 threads / 128 KiB LDS panel, 1 = 256 threads / 64 KiB panel (2 per CU). */
 int aqc_mps_set_jacobi_variant(int variant);
+/* Diagnostics: one register-resident Jacobi launch (variant 2 = with pivoted QR, 3 = without) on
+   theta (m x n column-major complex, m, n even <= 128, as the two-site update builds it).
+   w_out receives min(m,n) columns of length (variant 2: min(m,n), 3: max(m,n)); sig_out their
+   norms; perm_out (optional) the pivot order when stop_after_qr (then w_out holds X = R^H
+   unsorted).  For tests and tools only: allocates and frees device memory per call. */
+int aqc_svd_debug(const double* theta, int m, int n, int variant, int stop_after_qr, double* w_out,
+                  double* sig_out, int* perm_out, int* sweeps);
 /* move_all_qubits_to_sorted_ordering (done implicitly by every measurement below). */
 int aqc_mps_sort(aqc_mps_t h);
 int aqc_mps_sort_batch(aqc_mps_t* hs, int nstates);

@@ -195,7 +195,7 @@ def test_batch_apply_matches_single():
         assert abs(d.overlap_zero() - ov[s]) < 1e-13
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
 def test_jacobi_variants_vs_oracle(goldens, variant):
     """Every Jacobi kernel shape reproduces the oracle (small, ragged and full-width theta)."""
     from adaptaqc_amd import _lib
@@ -227,4 +227,4 @@ def test_jacobi_variants_vs_oracle(goldens, variant):
             ov_ref = M.mps_dot(ref.preprocessed(), M.zero_mps(n))
             assert abs(d.overlap_zero() - ov_ref) <= 1e-8 * abs(ov_ref) + 1e-18
     finally:
-        _lib.check(_lib.lib().aqc_mps_set_jacobi_variant(2))
+        _lib.check(_lib.lib().aqc_mps_set_jacobi_variant(3))

@@ -1,0 +1,88 @@
+"""The two-site SVD kernel on its own (aqc_svd_debug) against LAPACK / scipy on the same theta.
+
+Shapes follow the two-site update: theta is (2 chi_l) x (2 chi_r), column-major.  The QR phase is
+pinned to scipy's pivoted QR (zgeqp3: same reflector convention, pivot = largest trailing norm),
+the decomposition to numpy's SVD; tolerances are relative to sigma_max.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+import scipy.linalg as sla
+
+pytestmark = pytest.mark.gpu
+
+SHAPES = [(4, 4), (2, 8), (16, 8), (32, 32), (24, 64), (64, 64), (128, 64), (64, 128), (128, 128)]
+
+
+def _theta(m, n, seed, rank=None):
+    rng = np.random.default_rng(seed)
+    a = rng.standard_normal((m, n)) + 1j * rng.standard_normal((m, n))
+    a *= (0.8 ** np.arange(n))[None, :]  # graded columns, like lambda-weighted thetas
+    if rank is not None:
+        u, s, vh = np.linalg.svd(a, full_matrices=False)
+        s[rank:] = 0.0
+        a = (u * s) @ vh
+    return a / np.linalg.norm(a)
+
+
+def _run(theta, variant, stop_after_qr=False):
+    from adaptaqc_amd import _lib
+
+    m, n = theta.shape
+    c, l = min(m, n), max(m, n)
+    lw = c if variant == 2 else l
+    th = np.asfortranarray(theta.astype(np.complex128)).ravel(order="F").copy()
+    w = np.zeros(c * lw, np.complex128)
+    sig = np.zeros(c)
+    perm = np.zeros(c, np.int32)
+    sw = ctypes.c_int()
+    _lib.check(_lib.lib().aqc_svd_debug(th.ctypes.data, m, n, variant, int(stop_after_qr), w.ctypes.data,
+                                        sig.ctypes.data, perm.ctypes.data, ctypes.byref(sw)))
+    return w.reshape(c, lw).T, sig, perm, sw.value  # columns of W as columns
+
+
+@pytest.mark.parametrize("m,n", SHAPES)
+def test_jacobi_singular_values(m, n):
+    th = _theta(m, n, m * 1000 + n)
+    s_ref = np.linalg.svd(th, compute_uv=False)
+    for variant in (3, 2):
+        w, sig, _, sweeps = _run(th, variant)
+        np.testing.assert_allclose(np.sort(sig)[::-1], s_ref, atol=1e-13 * s_ref[0])
+        assert sweeps < 40
+
+
+@pytest.mark.parametrize("m,n", SHAPES)
+def test_qr_phase_matches_scipy(m, n):
+    th = _theta(m, n, m * 7 + n)
+    w_in = th.conj().T if m < n else th
+    q, r, p = sla.qr(w_in, pivoting=True, mode="economic")
+    x, _, perm, _ = _run(th, 2, stop_after_qr=True)
+    np.testing.assert_array_equal(perm, p)
+    np.testing.assert_allclose(x, r.conj().T, atol=1e-13)
+
+
+@pytest.mark.parametrize("m,n", SHAPES)
+def test_qr_jacobi_vectors(m, n):
+    """With QR the output columns are the other side's singular vectors times sigma."""
+    th = _theta(m, n, m * 31 + n)
+    w, sig, _, _ = _run(th, 2)
+    u, s, vh = np.linalg.svd(th, full_matrices=False)
+    order = np.argsort(-sig, kind="stable")
+    w, sig = w[:, order], sig[order]
+    k = int(np.sum(s > 1e-12 * s[0]))
+    if m >= n:  # W = theta: output = V sigma, so theta (W / sigma^2) = U
+        vcols = w[:, :k] / sig[:k]
+        np.testing.assert_allclose(np.abs(vcols.conj().T @ vh[:k].conj().T), np.eye(k), atol=1e-10)
+    else:       # W = theta^H: output = U sigma
+        ucols = w[:, :k] / sig[:k]
+        np.testing.assert_allclose(np.abs(ucols.conj().T @ u[:, :k]), np.eye(k), atol=1e-10)
+
+
+def test_rank_deficient_and_zero_columns():
+    for rank in (1, 3, 17):
+        th = _theta(64, 64, rank, rank=rank)
+        s_ref = np.linalg.svd(th, compute_uv=False)
+        for variant in (3, 2):
+            _, sig, _, _ = _run(th, variant)
+            np.testing.assert_allclose(np.sort(sig)[::-1], s_ref, atol=1e-13)
