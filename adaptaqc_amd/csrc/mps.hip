@@ -41,7 +41,7 @@ constexpr double kChop = 1e-16;
 constexpr int kMaxSweeps = 60;
 // rotation threshold: |a^H b| > tol_factor * L * eps * |a| |b|  (L = column length)
 double g_jacobi_tol_factor = 1.0;
-int g_jacobi_variant = 3;  // 2 (pivoted-QR preconditioning) once its parity is green
+int g_jacobi_variant = 2;
 
 struct OneSiteJob {
   cplx* g;
@@ -541,26 +541,37 @@ __global__ __launch_bounds__(CP * 8) void k_jacobi_reg(const TwoSiteJob* __restr
         mi[i] -= v.x * fmi + v.y * fmr;
       }
     }
-    // X = R^H: X[i][jx] = conj(R[jx][column pivoted at step i]); new S / M = X columns g, g + kG
+    // X = R^H: X[i][jx] = conj(R[jx][column pivoted at step i]); new S / M = X columns g, g + kG.
+    // LDS holds half of the matrix, and the register halves whose R rows already went to LDS are
+    // reused: half 0 sends R rows [0, kG) and lands X column g in (S-low, M-low); half 1 sends R
+    // rows [kG, 2kG) and lands X column g + kG in (S-high, M-high); one register swap finishes.
+    constexpr int H = MAXR / 2;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
 #pragma unroll
-      for (int i = h * MAXR / 2; i < (h + 1) * MAXR / 2; ++i) {
-        const int jx = lane + 16 * i - h * kG;
+      for (int i = h * H; i < (h + 1) * H; ++i) {
+        const int jx = lane + 16 * (i - h * H);
         if (ks >= 0) xbuf[jx * ldt + ks] = make_double2(sr[i], -si[i]);
         if (km >= 0) xbuf[jx * ldt + km] = make_double2(mr[i], -mi[i]);
       }
       __syncthreads();
-      const int jx = g + h * kG;
+      const bool real_col = g + h * kG < C;
 #pragma unroll
-      for (int i = 0; i < MAXR; ++i) {
-        const int row = lane + 16 * i;
-        double2 v = make_double2(0, 0);
-        if (row < C && jx < C) v = xbuf[g * ldt + row];
-        if (h == 0) sr[i] = v.x, si[i] = v.y;
-        else mr[i] = v.x, mi[i] = v.y;
+      for (int i = h * H; i < (h + 1) * H; ++i) {
+        const int ra = lane + 16 * (i - h * H), rb = ra + kG;  // X rows (pivot steps)
+        double2 va = make_double2(0, 0), vb2 = make_double2(0, 0);
+        if (real_col && ra < C) va = xbuf[g * ldt + ra];
+        if (real_col && rb < C) vb2 = xbuf[g * ldt + rb];
+        sr[i] = va.x, si[i] = va.y;
+        mr[i] = vb2.x, mi[i] = vb2.y;
       }
       __syncthreads();
+    }
+#pragma unroll
+    for (int i = 0; i < H; ++i) {  // M-low <-> S-high
+      const double tr0 = mr[i], ti0 = mi[i];
+      mr[i] = sr[i + H], mi[i] = si[i + H];
+      sr[i + H] = tr0, si[i + H] = ti0;
     }
     Lj = C;
   }
@@ -1504,7 +1515,7 @@ int aqc_svd_debug(const double* theta, int m, int n, int variant, int stop_after
   const int cp = std::max(m, n) <= 32 ? 32 : (std::max(m, n) <= 64 ? 64 : 128);
   const size_t mat = (size_t)128 * 128 * sizeof(cplx);
   char* buf = nullptr;
-  AQC_HIP_CHECK(hipMalloc(&buf, 2 * mat + 1024 * sizeof(double) + 512 * sizeof(int) + 4 * sizeof(int) +
+  AQC_HIP_CHECK(hipMalloc(&buf, 2 * mat + 1024 * sizeof(double) + 512 * sizeof(int) + 8 * sizeof(int) +
                                     sizeof(TwoSiteJob)));
   cplx* th = (cplx*)buf;
   cplx* wk = (cplx*)(buf + mat);

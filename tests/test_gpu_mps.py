@@ -227,4 +227,4 @@ def test_jacobi_variants_vs_oracle(goldens, variant):
             ov_ref = M.mps_dot(ref.preprocessed(), M.zero_mps(n))
             assert abs(d.overlap_zero() - ov_ref) <= 1e-8 * abs(ov_ref) + 1e-18
     finally:
-        _lib.check(_lib.lib().aqc_mps_set_jacobi_variant(3))
+        _lib.check(_lib.lib().aqc_mps_set_jacobi_variant(2))
