@@ -822,22 +822,25 @@ __global__ __launch_bounds__(kT) void k_split_gemm(const TwoSiteJob* __restrict_
   cplx acc = aqc::cmk(0, 0);
   const int K = L;  // inner dimension: M for !tr, N for tr
   for (int k0 = 0; k0 < K; k0 += 16) {
-    // A[ro][kin], B[kin][co]
+    // As[row][kin], Bs[kin][col]; consecutive lanes (tx) always walk the contiguous dimension
+    // of the source (W columns, column-major theta), transposing through the padded tiles
     {
-      const int ar = r0 + ty, ak = k0 + tx;
-      cplx a = aqc::cmk(0, 0);
-      if (ar < rows && ak < K) {
-        if (!tr) a = aqc::cconj(j.work[(size_t)j.perm[ar] * L + ak]);  // conj(W_j[R])
-        else a = j.theta[(size_t)ak * M + ar];                         // theta[R][c]
+      cplx a = aqc::cmk(0, 0), b = aqc::cmk(0, 0);
+      if (!tr) {
+        const int ar = r0 + ty, ak = k0 + tx;  // conj(W_j[R]): contiguous in R
+        if (ar < rows && ak < K) a = aqc::cconj(j.work[(size_t)j.perm[ar] * L + ak]);
+        As[ty][tx] = a;
+        const int bk = k0 + tx, bc = c0 + ty;  // theta[R][c]: contiguous in R
+        if (bk < K && bc < cols) b = j.theta[(size_t)bc * M + bk];
+        Bs[tx][ty] = b;
+      } else {
+        const int ar = r0 + tx, ak = k0 + ty;  // theta[R][c]: contiguous in R
+        if (ar < rows && ak < K) a = j.theta[(size_t)ak * M + ar];
+        As[tx][ty] = a;
+        const int bk = k0 + tx, bc = c0 + ty;  // W_j[c]: contiguous in c
+        if (bk < K && bc < cols) b = j.work[(size_t)j.perm[bc] * L + bk];
+        Bs[tx][ty] = b;
       }
-      As[ty][tx] = a;
-      const int bk = k0 + ty, bc = c0 + tx;
-      cplx b = aqc::cmk(0, 0);
-      if (bk < K && bc < cols) {
-        if (!tr) b = j.theta[(size_t)bc * M + bk];                 // theta[R][c]
-        else b = j.work[(size_t)j.perm[bc] * L + bk];               // W_j[c]
-      }
-      Bs[ty][tx] = b;
     }
     __syncthreads();
 #pragma unroll 8
@@ -1401,6 +1404,57 @@ int check_flags(aqc_mps_t h) {
   return AQC_OK;
 }
 
+// Flags of many states with one gather launch and one read-back (instead of one synchronous
+// copy per state); only states with a raised flag are then inspected and reset one by one.
+__global__ void k_gather_flags(int* const* __restrict__ flags, int ns, int* __restrict__ out) {
+  for (int s = blockIdx.x * blockDim.x + threadIdx.x; s < ns; s += gridDim.x * blockDim.x)
+    out[s] = flags[s][0] | flags[s][1];
+}
+
+int check_flags_batch(aqc_mps_t* hs, int ns) {
+  if (ns <= 0) return AQC_OK;
+  if (ns == 1) return check_flags(hs[0]);
+  struct FlagStage {
+    void* dev = nullptr;
+    size_t cap = 0;
+    int* host = nullptr;
+    size_t hcap = 0;
+  };
+  static FlagStage stages[64];
+  int dev = 0;
+  hipGetDevice(&dev);
+  FlagStage& fs = stages[dev];
+  const size_t bytes = (size_t)ns * (sizeof(int*) + sizeof(int));
+  if (bytes > fs.cap) {
+    if (fs.dev) hipFree(fs.dev);
+    fs.cap = std::max(bytes, 2 * fs.cap);
+    AQC_HIP_CHECK(hipMalloc(&fs.dev, fs.cap));
+  }
+  if (bytes > fs.hcap) {
+    if (fs.host) hipHostFree(fs.host);
+    fs.hcap = std::max(bytes, 2 * fs.hcap);
+    AQC_HIP_CHECK(hipHostMalloc((void**)&fs.host, fs.hcap, hipHostMallocDefault));
+  }
+  hipStream_t st = aqc::mps_stream();
+  int** hp = (int**)fs.host;
+  for (int s = 0; s < ns; ++s) hp[s] = hs[s]->d.flags;
+  int** dp = (int**)fs.dev;
+  int* dout = (int*)((char*)fs.dev + (size_t)ns * sizeof(int*));
+  AQC_HIP_CHECK(hipMemcpyAsync(dp, hp, (size_t)ns * sizeof(int*), hipMemcpyHostToDevice, st));
+  hipLaunchKernelGGL(k_gather_flags, dim3((ns + 255) / 256), dim3(256), 0, st, (int* const*)dp, ns, dout);
+  AQC_CHECK_LAUNCH();
+  int* hout = (int*)((char*)fs.host + (size_t)ns * sizeof(int*));
+  AQC_HIP_CHECK(hipMemcpyAsync(hout, dout, (size_t)ns * sizeof(int), hipMemcpyDeviceToHost, st));
+  AQC_HIP_CHECK(hipStreamSynchronize(st));
+  for (int s = 0; s < ns; ++s) {
+    if (hout[s]) {
+      int rc = check_flags(hs[s]);
+      if (rc != AQC_OK) return rc;
+    }
+  }
+  return AQC_OK;
+}
+
 bool is_sorted_order(aqc_mps_t h) {
   for (int i = 0; i < h->d.n; ++i)
     if (h->order[i] != i) return false;
@@ -1640,11 +1694,7 @@ int aqc_mps_sort_batch(aqc_mps_t* hs, int ns) {
   AQC_REQUIRE(hs && ns >= 0, "aqc_mps_sort_batch: bad arguments");
   int rc = do_sort(hs, ns);
   if (rc != AQC_OK) return rc;
-  for (int s = 0; s < ns; ++s) {
-    rc = check_flags(hs[s]);
-    if (rc != AQC_OK) return rc;
-  }
-  return AQC_OK;
+  return check_flags_batch(hs, ns);
 }
 
 int aqc_mps_get_vidal(aqc_mps_t h, int* dims, double* gammas, double* lambdas) {
@@ -1674,6 +1724,68 @@ int aqc_mps_get_vidal(aqc_mps_t h, int* dims, double* gammas, double* lambdas) {
   return AQC_OK;
 }
 
+// Batched reload of cached MPS (one launch instead of three copies per state): every state's
+// gamma, lambda and dims blocks are contiguous, copied as 16-byte words, grid (chunks, states).
+struct CopyJob {
+  const double2* sg;
+  double2* dg;
+  size_t ng;  // double2 words of gamma
+  const double* sl;
+  double* dl;
+  size_t nl;
+  const int* sd;
+  int* dd;
+  int nd;
+  int pad;
+};
+
+__global__ __launch_bounds__(kT) void k_copy_batch(const CopyJob* __restrict__ jobs) {
+  const CopyJob& j = jobs[blockIdx.y];
+  const size_t stride = (size_t)gridDim.x * kT;
+  for (size_t e = (size_t)blockIdx.x * kT + threadIdx.x; e < j.ng; e += stride) j.dg[e] = j.sg[e];
+  for (size_t e = (size_t)blockIdx.x * kT + threadIdx.x; e < j.nl; e += stride) j.dl[e] = j.sl[e];
+  for (size_t e = (size_t)blockIdx.x * kT + threadIdx.x; e < (size_t)j.nd; e += stride) j.dd[e] = j.sd[e];
+}
+
+int aqc_mps_copy_batch(aqc_mps_t* dst, const aqc_mps_t* src, int ns) {
+  AQC_REQUIRE(ns >= 0 && (ns == 0 || (dst && src)), "aqc_mps_copy_batch: null argument");
+  if (ns == 0) return AQC_OK;
+  std::vector<CopyJob> jobs(ns);
+  for (int s = 0; s < ns; ++s) {
+    AQC_REQUIRE(dst[s] && src[s] && dst[s]->d.n == src[s]->d.n && dst[s]->d.cap == src[s]->d.cap,
+                "aqc_mps_copy_batch: handle mismatch");
+    const size_t cap = src[s]->d.cap, n = src[s]->d.n;
+    CopyJob& j = jobs[s];
+    j.sg = src[s]->d.gam;
+    j.dg = dst[s]->d.gam;
+    j.ng = n * 2 * cap * cap;
+    j.sl = src[s]->d.lam;
+    j.dl = dst[s]->d.lam;
+    j.nl = (n + 1) * cap;
+    j.sd = src[s]->d.dims;
+    j.dd = dst[s]->d.dims;
+    j.nd = (int)n + 1;
+    j.pad = 0;
+    dst[s]->order = src[s]->order;
+    dst[s]->loc = src[s]->loc;
+  }
+  hipStream_t st = aqc::mps_stream();
+  Staging& sg = staging();
+  AQC_HIP_CHECK(hipStreamSynchronize(st));  // staging may still feed earlier launches
+  const size_t bytes = jobs.size() * sizeof(CopyJob);
+  int rc = ensure_staging(sg, bytes);
+  if (rc != AQC_OK) return rc;
+  std::memcpy(sg.host, jobs.data(), bytes);
+  AQC_HIP_CHECK(hipMemcpyAsync(sg.dev, sg.host, bytes, hipMemcpyHostToDevice, st));
+  const size_t words = jobs[0].ng;
+  const int chunks = (int)std::min<size_t>(64, (words + 8 * kT - 1) / (8 * kT));
+  aqc::KernelTimer::begin(st, "mps_copy", 2.0 * ns * (words * 16.0 + jobs[0].nl * 8.0), 0.0);
+  hipLaunchKernelGGL(k_copy_batch, dim3(std::max(chunks, 1), ns), dim3(kT), 0, st, (const CopyJob*)sg.dev);
+  aqc::KernelTimer::end(st);
+  AQC_CHECK_LAUNCH();
+  return AQC_OK;
+}
+
 int aqc_mps_copy(aqc_mps_t dst, const aqc_mps_t src) {
   AQC_REQUIRE(dst && src && dst->d.n == src->d.n && dst->d.cap == src->d.cap, "aqc_mps_copy: handle mismatch");
   hipStream_t st = aqc::mps_stream();
@@ -1697,11 +1809,7 @@ int aqc_mps_apply_batch(aqc_mps_t* hs, int ns, const aqc_op_t* const* ops, const
   for (int s = 0; s < ns; ++s) schedule(hs[s], ops[s], nops[s], false, lists[s]);
   int rc = run_waves(hs, ns, lists);
   if (rc != AQC_OK) return rc;
-  for (int s = 0; s < ns; ++s) {
-    rc = check_flags(hs[s]);
-    if (rc != AQC_OK) return rc;
-  }
-  return AQC_OK;
+  return check_flags_batch(hs, ns);
 }
 
 int aqc_mps_apply(aqc_mps_t h, const aqc_op_t* ops, int nops) {
@@ -1713,8 +1821,17 @@ int aqc_mps_overlap_zero_batch(aqc_mps_t* hs, int ns, double* out) {
   if (ns == 0) return AQC_OK;
   int rc = aqc_mps_sort_batch(hs, ns);
   if (rc != AQC_OK) return rc;
+  static cplx* dres[64] = {nullptr};
+  static int dres_n[64] = {0};
+  int dev = 0;
+  hipGetDevice(&dev);
+  if (dres_n[dev] < ns) {
+    if (dres[dev]) hipFree(dres[dev]);
+    dres_n[dev] = std::max(ns, 2 * dres_n[dev]);
+    AQC_HIP_CHECK(hipMalloc(&dres[dev], (size_t)dres_n[dev] * sizeof(cplx)));
+  }
   std::vector<MeasJob> jobs(ns);
-  for (int s = 0; s < ns; ++s) jobs[s] = make_meas(hs[s], hs[s]->d.scal);
+  for (int s = 0; s < ns; ++s) jobs[s] = make_meas(hs[s], dres[dev] + s);  // one contiguous result array
   const MeasJob* dj = nullptr;
   rc = upload_jobs(jobs, &dj);
   if (rc != AQC_OK) return rc;
@@ -1725,13 +1842,13 @@ int aqc_mps_overlap_zero_batch(aqc_mps_t* hs, int ns, double* out) {
   hipLaunchKernelGGL(k_overlap_zero, dim3(ns), dim3(kT), 0, st, dj);
   aqc::KernelTimer::end(st);
   AQC_CHECK_LAUNCH();
+  std::vector<cplx> v(ns);
+  AQC_HIP_CHECK(hipMemcpyAsync(v.data(), dres[dev], (size_t)ns * sizeof(cplx), hipMemcpyDeviceToHost, st));
+  AQC_HIP_CHECK(hipStreamSynchronize(st));
   for (int s = 0; s < ns; ++s) {
-    cplx v;
-    AQC_HIP_CHECK(hipMemcpyAsync(&v, hs[s]->d.scal, sizeof(cplx), hipMemcpyDeviceToHost, st));
-    AQC_HIP_CHECK(hipStreamSynchronize(st));
     // mps_dot(psi, zero) = <psi|0..0> = conj(amplitude of |0..0>)
-    out[2 * s] = v.x;
-    out[2 * s + 1] = -v.y;
+    out[2 * s] = v[s].x;
+    out[2 * s + 1] = -v[s].y;
   }
   return AQC_OK;
 }

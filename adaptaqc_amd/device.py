@@ -188,6 +188,15 @@ def apply_batch(states, ops_lists):
     _lib.check(l.aqc_mps_apply_batch(_handles(states), len(states), ptrs, _lib.ptr(counts)))
 
 
+def copy_batch(dst, src):
+    """dst[s] <- src[s] for every state in one launch (per-evaluation reload of a cached MPS)."""
+    if len(dst) != len(src):
+        raise ValueError("copy_batch: dst and src differ in length")
+    if not dst:
+        return
+    _lib.check(_lib.lib().aqc_mps_copy_batch(_handles(dst), _handles(src), len(dst)))
+
+
 def overlap_zero_batch(states):
     l = _lib.lib()
     out = np.zeros(2 * len(states))

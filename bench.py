@@ -157,7 +157,7 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     from adaptaqc_amd import _lib
-    from adaptaqc_amd.device import DeviceMPS, apply_batch, overlap_zero_batch, pair_grads_batch
+    from adaptaqc_amd.device import DeviceMPS, apply_batch, copy_batch, overlap_zero_batch, pair_grads_batch
     from adaptaqc_amd.sharding import PairShard, gather_scores
     from adaptaqc_amd.utils.constants import coupling_map_fully_entangled
 
@@ -177,6 +177,7 @@ def main():
         states.append(d)
     own = states[rank * B:(rank + 1) * B]
     work = [DeviceMPS(n, CHI, 1e-16, CHI) for _ in range(B * len(DISTANCES))]
+    reload_src = [own[k // len(DISTANCES)] for k in range(len(work))]
     rng = np.random.default_rng(7)
     layer_ops = []
     for s in range(B):
@@ -192,8 +193,7 @@ def main():
         full = gather_scores(local_scores[:, : len(shard.local_pairs)], shard, nstates=S)
         best = torch.argmax(full * torch.as_tensor(prio, device=full.device), dim=1)
         # (ii) overlap evals on own states
-        for k, w in enumerate(work):
-            w.copy_from(own[k // len(DISTANCES)])
+        copy_batch(work, reload_src)
         apply_batch(work, layer_ops)
         ov = overlap_zero_batch(work)
         costs = 1.0 - np.abs(ov) ** 2
@@ -230,7 +230,8 @@ def main():
     evals_per_step = S * (len(cmap) + len(DISTANCES))
     value = evals_per_step * args.steps / elapsed
 
-    fams = {f: _lib.timing_query(f) for f in ("mps_svd", "mps_theta", "mps_split", "grad_chain", "mps_overlap0")}
+    fams = {f: _lib.timing_query(f)
+            for f in ("mps_svd", "mps_theta", "mps_split", "grad_chain", "mps_overlap0", "mps_copy")}
     dom = max(fams, key=lambda f: fams[f]["ms"])
     fd = fams[dom]
     launches = max(fd["launches"], 1)

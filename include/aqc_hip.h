@@ -89,6 +89,11 @@ int aqc_mps_set_vidal(aqc_mps_t h, const int* dims, const double* gammas, const 
 int aqc_mps_get_vidal(aqc_mps_t h, int* dims, double* gammas, double* lambdas);
 int aqc_mps_get_dims(aqc_mps_t h, int* dims);
 int aqc_mps_copy(aqc_mps_t dst, const aqc_mps_t src);
+/* Batched aqc_mps_copy (dst[s] <- src[s], same n and capacity): one launch for every state --
+   the per-evaluation reload of the cached MPS (reference: every cost evaluation re-runs
+   full_circuit, whose first instruction is set_matrix_product_state, aer_mps_backend.py:76-78;
+   the instruction is built at approximate_compiler.py:181-184). */
+int aqc_mps_copy_batch(aqc_mps_t* dst, const aqc_mps_t* src, int nstates);
 /* Apply ops with Aer MPS semantics (swap-left routing, lazy qubit order, two-site SVD with
  * reduce_zeros truncation) -- the replay inside mps_from_circuit (aer_mps_backend.py:76-78). */
 int aqc_mps_apply(aqc_mps_t h, const aqc_op_t* ops, int nops);

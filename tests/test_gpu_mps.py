@@ -228,3 +228,18 @@ def test_jacobi_variants_vs_oracle(goldens, variant):
             assert abs(d.overlap_zero() - ov_ref) <= 1e-8 * abs(ov_ref) + 1e-18
     finally:
         _lib.check(_lib.lib().aqc_mps_set_jacobi_variant(2))
+
+
+def test_copy_batch_matches_single_copies(random_mps):
+    from adaptaqc_amd.device import DeviceMPS, copy_batch
+
+    srcs = [_dev_from_aer(random_mps[s], cap=16) for s in (1, 2, 64)]
+    dst = [DeviceMPS(len(random_mps[1][0]), 16) for _ in range(5)]
+    pick = [srcs[k % 3] for k in range(5)]
+    copy_batch(dst, pick)
+    for d, s in zip(dst, pick):
+        assert abs(d.overlap_zero() - s.overlap_zero()) == 0.0
+        np.testing.assert_array_equal(d.dims(), s.dims())
+        for (a, b), (a2, b2) in zip(d.to_aer()[0], s.to_aer()[0]):
+            np.testing.assert_array_equal(a, a2)
+            np.testing.assert_array_equal(b, b2)
