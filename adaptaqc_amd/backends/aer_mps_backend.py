@@ -102,6 +102,11 @@ class AerMPSBackend(AQCBackend):
         psi = self.device_state(compiler.full_circuit)
         return [float(x) for x in psi.z_all()]
 
+    def pair_rdms(self, compiler, pairs):
+        """4x4 RDMs of every pair from one device replay (adapt_compiler.py:960-961 builds the MPS
+        once, then aqc_research partial_trace per pair)."""
+        return self.device_state(compiler.full_circuit).pair_rdms(pairs)
+
     def evaluate_hamming_weight_one_overlaps(self, mps):
         if isinstance(mps, DeviceMPS):
             amps = mps.amps_hw1()

@@ -68,5 +68,10 @@ class AerSVBackend(AQCBackend):
     def measure_qubit_expectation_values(self, compiler):
         return [float(x) for x in self._run(compiler).z_all()]
 
+    def pair_rdms(self, compiler, pairs):
+        """4x4 RDMs of every pair on the compiled state: the ISL sweep's input (one simulation
+        for all pairs, where the reference re-runs the circuit per pair, adapt_compiler.py:965)."""
+        return self._run(compiler).pair_rdms(pairs)
+
 
 HipSVBackend = AerSVBackend

@@ -4,8 +4,8 @@ Restates the adaptive layer loop around the hot path: pair selection (general_gr
 the device, or basic / random / expectation / brickwall), Rotoselect on the new layer and
 Rotosolve on the last ``max_layers_to_modify`` layers (every cost evaluation on the device),
 and, for the MPS backend, absorption of old layers into the cached MPS
-(:662-706, :1097-1145).  The ISL method needs the pairwise entanglement sweep (SURVEY.md
-section 8(f) #1), which is not built yet and raises NotImplementedError.
+(:662-706, :1097-1145).  ISL (the default method) runs the pairwise entanglement sweep on the
+device (utils/entanglement_measures.py, csrc/ent.hip).
 """
 import logging
 import os
@@ -28,10 +28,9 @@ from ..approximate_compiler import ApproximateCompiler
 from .adapt_config import AdaptConfig
 from .adapt_result import AdaptResult
 from .pair_selection import reuse_priorities
+from ...utils.entanglement_measures import EM_TOMOGRAPHY_CONCURRENCE
 
 logger = logging.getLogger(__name__)
-
-EM_TOMOGRAPHY_CONCURRENCE = "EM_TOMOGRAPHY_CONCURRENCE"
 
 
 class AdaptCompiler(ApproximateCompiler):
@@ -290,8 +289,9 @@ class AdaptCompiler(ApproximateCompiler):
         if m == "expectation":
             return self._find_best_expectation_qubit_pair()
         if m == "ISL":
-            raise NotImplementedError("ISL needs the pairwise entanglement sweep (SURVEY.md 8(f) #1), not built yet; "
-                                      "use method='general_gradient' (MPS) or 'expectation'")
+            ems = self._get_all_qubit_pair_entanglement_measures()
+            self.entanglement_measures_history.append(ems)
+            return self._find_best_entanglement_qubit_pair(ems)
         if m == "general_gradient":
             gradients = self._get_all_qubit_pair_gradients()
             self.general_gradient_history.append(gradients)
@@ -331,6 +331,40 @@ class AdaptCompiler(ApproximateCompiler):
         circuit = co.extract_inner_circuit(self.full_circuit, rng)
         return gr.general_grad_of_pairs(circuit, self.inverse_zero_ansatz, self.generators, self.degeneracies,
                                         self.coupling_map, self.starting_circuit, self.backend)
+
+    def _get_all_qubit_pair_entanglement_measures(self):
+        """adapt_compiler.py:955-976: one device state, every pair's RDM and measure in batches."""
+        from ...utils.entanglement_measures import pair_entanglement_measures
+
+        self.circ_mps = None  # the reference keeps the host MPS here; the sweep stays on the device
+        return pair_entanglement_measures(self.entanglement_measure_method, self, self.coupling_map)
+
+    def _find_best_entanglement_qubit_pair(self, entanglement_measures):
+        """adapt_compiler.py:858-919: entanglement x reuse priority, bad-pair memory, threshold
+        fall-back to the expectation method."""
+        reuse = self._get_all_qubit_pair_reuse_priorities(self.adapt_config.reuse_exponent)
+        if len(self.entanglement_measures_history) >= 2 + int(self.initial_single_qubit_layer):
+            prev_index = self.coupling_map.index(self.qubit_pair_history[-1])
+            pre_em = self.entanglement_measures_history[-2][prev_index]
+            post_em = self.entanglement_measures_history[-1][prev_index]
+            if post_em >= pre_em:
+                logger.debug(f"Entanglement did not reduce for previous pair {self.coupling_map[prev_index]}. "
+                             f"Adding to bad qubit pairs list.")
+                self.bad_qubit_pairs.append(self.coupling_map[prev_index])
+            if len(self.bad_qubit_pairs) > self.adapt_config.bad_qubit_pair_memory:
+                del self.bad_qubit_pairs[0]
+        filtered = [em * r for em, r in zip(entanglement_measures, reuse)]
+        memory = self.adapt_config.bad_qubit_pair_memory
+        for qp in set(self.bad_qubit_pairs):
+            reps = len([x for x in self.qubit_pair_history[-1 * memory:] if x == qp])
+            if reps >= 1:
+                filtered[self.coupling_map.index(qp)] = -1
+        if max(filtered) <= self.adapt_config.entanglement_threshold:
+            logger.info("No local entanglement detected in non-bad qubit pairs")
+            return self._find_best_expectation_qubit_pair()
+        self.pair_selection_method_history.append("ISL")
+        self.e_val_history.append(None)
+        return self.coupling_map[int(np.argmax(filtered))]
 
     def _find_best_expectation_qubit_pair(self):
         prio = self._get_all_qubit_pair_reuse_priorities(self.adapt_config.reuse_exponent)

@@ -1,0 +1,65 @@
+// Workgroup-level complex GEMM for the small (chi x chi) contractions of the environment chains.
+//
+// C[i][j] = sum_k a(i, k) * b(k, j) over an m x n output, computed by one 256-thread workgroup
+// in 64 x 64 output blocks; k is staged through LDS in tiles of 16 (As[k][i], Bs[k][j], row
+// padding 65 so the column-wise fills and the broadcast reads stay conflict-light); each thread
+// owns a 4 x 4 register block (rows 4*ty.., cols 4*tx..).  Accessors a / b return zero outside
+// the valid range; store(i, j, v) is called for i < m, j < n.  Callers provide the LDS tiles.
+#pragma once
+
+#include "aqc_internal.h"
+
+namespace aqc {
+
+constexpr int kGemmThreads = 256;
+
+struct GemmLds {
+  cplx As[16][65];
+  cplx Bs[16][65];
+};
+
+template <typename FA, typename FB, typename FS>
+__device__ __forceinline__ void block_cgemm(int m, int n, int k, FA a, FB b, FS store, GemmLds& lds) {
+  const int tid = threadIdx.x, ty = tid >> 4, tx = tid & 15;
+  for (int bi = 0; bi < m; bi += 64) {
+    for (int bj = 0; bj < n; bj += 64) {
+      cplx acc[4][4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[r][c] = cmk(0, 0);
+      for (int k0 = 0; k0 < k; k0 += 16) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int e = tid + q * kGemmThreads;
+          const int kk = e >> 6, ii = e & 63;
+          lds.As[kk][ii] = (bi + ii < m && k0 + kk < k) ? a(bi + ii, k0 + kk) : cmk(0, 0);
+          lds.Bs[kk][ii] = (bj + ii < n && k0 + kk < k) ? b(k0 + kk, bj + ii) : cmk(0, 0);
+        }
+        __syncthreads();
+#pragma unroll 4
+        for (int kk = 0; kk < 16; ++kk) {
+          cplx av[4], bv[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) av[r] = lds.As[kk][4 * ty + r];
+#pragma unroll
+          for (int c = 0; c < 4; ++c) bv[c] = lds.Bs[kk][4 * tx + c];
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) acc[r][c] = cfma(av[r], bv[c], acc[r][c]);
+        }
+        __syncthreads();
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const int i = bi + 4 * ty + r, j = bj + 4 * tx + c;
+          if (i < m && j < n) store(i, j, acc[r][c]);
+        }
+    }
+  }
+}
+
+}  // namespace aqc

@@ -1,0 +1,489 @@
+// ISL entanglement sweep: two-qubit reduced density matrices for every coupling-map pair and the
+// 4x4 entanglement measures.  Replaces adaptaqc/compilers/adapt/adapt_compiler.py:955-976
+// (_get_all_qubit_pair_entanglement_measures), whose loop calls
+// entanglement_measures.py:39-98 (calculate_entanglement_measure) once per pair: a full SV
+// partial trace (:326-340) or aqc_research.mps_operations.partial_trace per pair, then
+// concurrence / EoF / negativity / log-negativity (:245-306) on the 4x4 result.
+//
+// MPS (preprocessed A_i = Gamma_i lambda_{i+1}, sorted qubits), no canonical form assumed:
+//   L_{i+1} = sum_s A_i^{s dag} L_i A_i^s          (bra x ket, L_0 = 1)      k_rdm_env
+//   R_i     = sum_s A_i^s R_{i+1} A_i^{s dag}      (ket x bra, R_n = 1)      k_rdm_env
+//   P_b[s][sb] = A_b^s R_{b+1} A_b^{sb dag}                                   k_rdm_P
+//   per first qubit a and bra/ket index pair (sb, s) of site a:               k_rdm_chain
+//     E = A_a^{sb dag} L_a A_a^s;  for b > a:  rho_ab[(s, s_b), (sb, sb_b)] = Tr(E P_b[s_b][sb_b]),
+//     E <- sum_t A_b^{t dag} E A_b^t
+// Work per state: sum_a (n-1-a) transfer steps of 3 matrices x 4 chi^3 complex MACs, against
+// the reference's n(n-1)/2 independent contractions.  Row index of a 4x4 RDM: 2*bit(b) + bit(a)
+// for a < b (qiskit partial_trace convention: remaining qubits ascending, little-endian).
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "aqc_gemm.h"
+#include "mps_internal.h"
+
+using aqc::cplx;
+
+namespace {
+
+constexpr int kT = aqc::kGemmThreads;
+
+struct RdmJob {
+  const cplx* gam;
+  const double* lam;
+  const int* dims;
+  int n;
+  int cap;
+  cplx* Lenv;   // (n+1) cap^2
+  cplx* Renv;   // (n+1) cap^2
+  cplx* tmpL;   // cap x 2cap
+  cplx* tmpR;   // 2cap x cap
+  cplx* P;      // n x 3 cap^2
+  cplx* U;      // n x 3 cap^2
+  cplx* chain;  // na x 3 x 4 cap^2
+  cplx* rho;    // n x n x 16
+};
+
+__device__ __forceinline__ cplx aval(const RdmJob& j, int i, int s, int l, int r) {
+  const size_t cc = (size_t)j.cap * j.cap;
+  return aqc::cscale(j.gam[(size_t)i * 2 * cc + (size_t)s * cc + (size_t)l * j.cap + r], j.lam[(size_t)(i + 1) * j.cap + r]);
+}
+
+// blockIdx.x: 0 left / 1 right environments, blockIdx.y: state
+__global__ __launch_bounds__(kT) void k_rdm_env(const RdmJob* __restrict__ jobs) {
+  const RdmJob& j = jobs[blockIdx.y];
+  __shared__ aqc::GemmLds lds;
+  const int n = j.n, cap = j.cap;
+  const size_t cc = (size_t)cap * cap;
+  if (blockIdx.x == 0) {
+    if (threadIdx.x == 0) j.Lenv[0] = aqc::cmk(1, 0);
+    __syncthreads();
+    for (int i = 0; i + 1 < n; ++i) {
+      const int cl = j.dims[i], cr = j.dims[i + 1];
+      const cplx* L = j.Lenv + (size_t)i * cc;
+      cplx* T = j.tmpL;  // T[l][t*cap + r] = (L A^t)[l][r]
+      aqc::block_cgemm(
+          cl, 2 * cap, cl, [&](int r, int k) { return L[(size_t)r * cap + k]; },
+          [&](int k, int c) { const int t = c / cap, r = c % cap; return r < cr ? aval(j, i, t, k, r) : aqc::cmk(0, 0); },
+          [&](int r, int c, cplx v) { T[(size_t)r * 2 * cap + c] = v; }, lds);
+      __syncthreads();
+      cplx* Ln = j.Lenv + (size_t)(i + 1) * cc;
+      aqc::block_cgemm(
+          cr, cr, 2 * cl,
+          [&](int r, int kk) { const int t = kk / cl, k = kk % cl; return aqc::cconj(aval(j, i, t, k, r)); },
+          [&](int kk, int c) { const int t = kk / cl, k = kk % cl; return T[(size_t)k * 2 * cap + t * cap + c]; },
+          [&](int r, int c, cplx v) { Ln[(size_t)r * cap + c] = v; }, lds);
+      __syncthreads();
+    }
+  } else {
+    if (threadIdx.x == 0) j.Renv[(size_t)n * cc] = aqc::cmk(1, 0);
+    __syncthreads();
+    for (int i = n - 1; i >= 1; --i) {
+      const int cl = j.dims[i], cr = j.dims[i + 1];
+      const cplx* R = j.Renv + (size_t)(i + 1) * cc;
+      cplx* T = j.tmpR;  // T[t*cap + l][r] = (A^t R)[l][r]
+      aqc::block_cgemm(
+          2 * cap, cr, cr,
+          [&](int rr, int k) { const int t = rr / cap, l = rr % cap; return l < cl ? aval(j, i, t, l, k) : aqc::cmk(0, 0); },
+          [&](int k, int c) { return R[(size_t)k * cap + c]; }, [&](int rr, int c, cplx v) { T[(size_t)rr * cap + c] = v; },
+          lds);
+      __syncthreads();
+      cplx* Rn = j.Renv + (size_t)i * cc;
+      aqc::block_cgemm(
+          cl, cl, 2 * cr,
+          [&](int l, int kk) { const int t = kk / cr, k = kk % cr; return T[(size_t)(t * cap + l) * cap + k]; },
+          [&](int kk, int c) { const int t = kk / cr, k = kk % cr; return aqc::cconj(aval(j, i, t, c, k)); },
+          [&](int l, int c, cplx v) { Rn[(size_t)l * cap + c] = v; }, lds);
+      __syncthreads();
+    }
+  }
+}
+
+// P_b[s][sb] = A_b^s R_{b+1} A_b^{sb dag}; m = 0: (0,0), 1: (0,1), 2: (1,1).  grid (n, 3, states)
+__global__ __launch_bounds__(kT) void k_rdm_P(const RdmJob* __restrict__ jobs) {
+  const RdmJob& j = jobs[blockIdx.z];
+  __shared__ aqc::GemmLds lds;
+  const int b = blockIdx.x, m = blockIdx.y;
+  if (b == 0) return;  // site 0 is never the second qubit of a pair
+  const int s = m == 2 ? 1 : 0, sb = m == 0 ? 0 : 1;
+  const int cap = j.cap;
+  const size_t cc = (size_t)cap * cap;
+  const int cl = j.dims[b], cr = j.dims[b + 1];
+  const cplx* R = j.Renv + (size_t)(b + 1) * cc;
+  cplx* U = j.U + ((size_t)b * 3 + m) * cc;
+  cplx* P = j.P + ((size_t)b * 3 + m) * cc;
+  aqc::block_cgemm(
+      cl, cr, cr, [&](int l, int k) { return aval(j, b, s, l, k); }, [&](int k, int c) { return R[(size_t)k * cap + c]; },
+      [&](int l, int c, cplx v) { U[(size_t)l * cap + c] = v; }, lds);
+  __syncthreads();
+  aqc::block_cgemm(
+      cl, cl, cr, [&](int l, int k) { return U[(size_t)l * cap + k]; },
+      [&](int k, int c) { return aqc::cconj(aval(j, b, sb, c, k)); }, [&](int l, int c, cplx v) { P[(size_t)l * cap + c] = v; },
+      lds);
+}
+
+// grid (3 bra/ket combos of site a, first qubits, states)
+__global__ __launch_bounds__(kT) void k_rdm_chain(const RdmJob* __restrict__ jobs, const int* __restrict__ alist) {
+  const RdmJob& j = jobs[blockIdx.z];
+  __shared__ aqc::GemmLds lds;
+  __shared__ double red[8][kT];
+  const int m = blockIdx.x, a = alist[blockIdx.y];
+  const int sb = m == 2 ? 1 : 0, s = m == 0 ? 0 : 1;  // E[sb][s]: bra index sb, ket index s
+  const int n = j.n, cap = j.cap, tid = threadIdx.x;
+  const size_t cc = (size_t)cap * cap;
+  cplx* base = j.chain + ((size_t)blockIdx.y * 3 + m) * 4 * cc;
+  cplx* Eb[2] = {base, base + cc};
+  cplx* T = base + 2 * cc;  // cap x 2cap
+  {
+    const int cl = j.dims[a], cr = j.dims[a + 1];
+    const cplx* L = j.Lenv + (size_t)a * cc;
+    aqc::block_cgemm(
+        cl, cr, cl, [&](int r, int k) { return L[(size_t)r * cap + k]; }, [&](int k, int c) { return aval(j, a, s, k, c); },
+        [&](int r, int c, cplx v) { T[(size_t)r * 2 * cap + c] = v; }, lds);
+    __syncthreads();
+    cplx* E = Eb[0];
+    aqc::block_cgemm(
+        cr, cr, cl, [&](int r, int k) { return aqc::cconj(aval(j, a, sb, k, r)); },
+        [&](int k, int c) { return T[(size_t)k * 2 * cap + c]; }, [&](int r, int c, cplx v) { E[(size_t)r * cap + c] = v; },
+        lds);
+    __syncthreads();
+  }
+  int cur = 0;
+  for (int b = a + 1; b < n; ++b) {
+    const int cl = j.dims[b], cr = j.dims[b + 1];
+    const cplx* E = Eb[cur];
+    // closing: v[s_b][sb_b] = sum_{ij} E[i][j] P_b[s_b][sb_b][j][i], with P[1][0] = P[0][1]^dag
+    const cplx* P00 = j.P + ((size_t)b * 3 + 0) * cc;
+    const cplx* P01 = j.P + ((size_t)b * 3 + 1) * cc;
+    const cplx* P11 = j.P + ((size_t)b * 3 + 2) * cc;
+    double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int e = tid; e < cl * cl; e += kT) {
+      const int i = e / cl, jj = e % cl;
+      const cplx ev = E[(size_t)i * cap + jj];
+      const cplx p00 = P00[(size_t)jj * cap + i], p01 = P01[(size_t)jj * cap + i], p11 = P11[(size_t)jj * cap + i];
+      const cplx p10 = aqc::cconj(P01[(size_t)i * cap + jj]);
+      const cplx v00 = aqc::cmul(ev, p00), v01 = aqc::cmul(ev, p01), v10 = aqc::cmul(ev, p10), v11 = aqc::cmul(ev, p11);
+      acc[0] += v00.x, acc[1] += v00.y, acc[2] += v01.x, acc[3] += v01.y;
+      acc[4] += v10.x, acc[5] += v10.y, acc[6] += v11.x, acc[7] += v11.y;
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) red[q][tid] = acc[q];
+    __syncthreads();
+    for (int h = kT / 2; h > 0; h >>= 1) {
+      if (tid < h)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) red[q][tid] += red[q][tid + h];
+      __syncthreads();
+    }
+    if (tid < 4) {
+      const int sbk = tid >> 1, sbb = tid & 1;  // ket / bra index of site b
+      const cplx v = aqc::cmk(red[2 * tid][0], red[2 * tid + 1][0]);
+      cplx* rho = j.rho + ((size_t)a * n + b) * 16;
+      rho[(2 * sbk + s) * 4 + (2 * sbb + sb)] = v;
+      if (m == 1) rho[(2 * sbb + sb) * 4 + (2 * sbk + s)] = aqc::cconj(v);  // the (sb=1, s=0) block
+    }
+    __syncthreads();
+    if (b + 1 >= n) break;
+    // transfer through site b: E' = sum_t A_b^{t dag} E A_b^t
+    aqc::block_cgemm(
+        cl, 2 * cap, cl, [&](int r, int k) { return E[(size_t)r * cap + k]; },
+        [&](int k, int c) { const int t = c / cap, r = c % cap; return r < cr ? aval(j, b, t, k, r) : aqc::cmk(0, 0); },
+        [&](int r, int c, cplx v) { T[(size_t)r * 2 * cap + c] = v; }, lds);
+    __syncthreads();
+    cplx* En = Eb[cur ^ 1];
+    aqc::block_cgemm(
+        cr, cr, 2 * cl,
+        [&](int r, int kk) { const int t = kk / cl, k = kk % cl; return aqc::cconj(aval(j, b, t, k, r)); },
+        [&](int kk, int c) { const int t = kk / cl, k = kk % cl; return T[(size_t)k * 2 * cap + t * cap + c]; },
+        [&](int r, int c, cplx v) { En[(size_t)r * cap + c] = v; }, lds);
+    __syncthreads();
+    cur ^= 1;
+  }
+}
+
+// requested pairs (c, t) -> rho of (min, max); grid over pairs x states
+__global__ void k_rdm_gather(const RdmJob* __restrict__ jobs, const int* __restrict__ pairs, int npairs,
+                             cplx* __restrict__ out) {
+  const RdmJob& j = jobs[blockIdx.y];
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < npairs * 16; e += gridDim.x * blockDim.x) {
+    const int p = e / 16, q = e % 16;
+    const int a = min(pairs[2 * p], pairs[2 * p + 1]), b = max(pairs[2 * p], pairs[2 * p + 1]);
+    out[((size_t)blockIdx.y * npairs + p) * 16 + q] = j.rho[((size_t)a * j.n + b) * 16 + q];
+  }
+}
+
+// ---- 4x4 entanglement measures -------------------------------------------------------------
+// Cyclic complex Jacobi on a 4x4 Hermitian matrix: eigenvalues in ev, eigenvectors (columns)
+// in V when want_v.
+__device__ void herm4_eig(cplx H[4][4], double ev[4], cplx V[4][4], bool want_v) {
+  if (want_v)
+    for (int r = 0; r < 4; ++r)
+      for (int c = 0; c < 4; ++c) V[r][c] = aqc::cmk(r == c ? 1.0 : 0.0, 0.0);
+  for (int sweep = 0; sweep < 30; ++sweep) {
+    double off = 0, dia = 0;
+    for (int p = 0; p < 4; ++p) {
+      dia += H[p][p].x * H[p][p].x;
+      for (int q = p + 1; q < 4; ++q) off += aqc::cnorm2(H[p][q]);
+    }
+    if (off <= 1e-34 * (dia + 1e-300)) break;
+    for (int p = 0; p < 3; ++p)
+      for (int q = p + 1; q < 4; ++q) {
+        const double g = sqrt(aqc::cnorm2(H[p][q]));
+        if (g == 0.0) continue;
+        const cplx e = aqc::cmk(H[p][q].x / g, H[p][q].y / g);  // phase of H[p][q]
+        const double tau = (H[q][q].x - H[p][p].x) / (2.0 * g);
+        const double t = (tau >= 0 ? 1.0 : -1.0) / (fabs(tau) + sqrt(1.0 + tau * tau));
+        const double c = 1.0 / sqrt(1.0 + t * t), sn = t * c;
+        // J = [[c, s], [-s conj(e), c conj(e)]] on (p, q): H <- J^H H J, V <- V J
+        const cplx ec = aqc::cconj(e);
+        for (int k = 0; k < 4; ++k) {  // columns
+          const cplx hp = H[k][p], hq = H[k][q];
+          H[k][p] = aqc::csub(aqc::cscale(hp, c), aqc::cscale(aqc::cmul(hq, ec), sn));
+          H[k][q] = aqc::cadd(aqc::cscale(hp, sn), aqc::cscale(aqc::cmul(hq, ec), c));
+        }
+        for (int k = 0; k < 4; ++k) {  // rows (conjugate transpose of the column update)
+          const cplx hp = H[p][k], hq = H[q][k];
+          H[p][k] = aqc::csub(aqc::cscale(hp, c), aqc::cscale(aqc::cmul(hq, e), sn));
+          H[q][k] = aqc::cadd(aqc::cscale(hp, sn), aqc::cscale(aqc::cmul(hq, e), c));
+        }
+        H[p][q] = aqc::cmk(0, 0);
+        H[q][p] = aqc::cmk(0, 0);
+        if (want_v)
+          for (int k = 0; k < 4; ++k) {
+            const cplx vp = V[k][p], vq = V[k][q];
+            V[k][p] = aqc::csub(aqc::cscale(vp, c), aqc::cscale(aqc::cmul(vq, ec), sn));
+            V[k][q] = aqc::cadd(aqc::cscale(vp, sn), aqc::cscale(aqc::cmul(vq, ec), c));
+          }
+      }
+  }
+  for (int p = 0; p < 4; ++p) ev[p] = H[p][p].x;
+}
+
+__device__ double concurrence4(const cplx rho[4][4]) {
+  // eig(rho rho~) = eig(S rho~ S), S = sqrt(rho) (Hermitian PSD): same non-zero spectrum, and the
+  // Hermitian form keeps the eigenvalues real (the reference's eig path returns 0 when they are not)
+  cplx H[4][4], V[4][4];
+  double d[4];
+  for (int r = 0; r < 4; ++r)
+    for (int c = 0; c < 4; ++c) H[r][c] = rho[r][c];
+  herm4_eig(H, d, V, true);
+  cplx S[4][4];
+  for (int r = 0; r < 4; ++r)
+    for (int c = 0; c < 4; ++c) {
+      cplx acc = aqc::cmk(0, 0);
+      for (int k = 0; k < 4; ++k)
+        acc = aqc::cfma(aqc::cscale(V[r][k], sqrt(fmax(d[k], 0.0))), aqc::cconj(V[c][k]), acc);
+      S[r][c] = acc;
+    }
+  const double y[4] = {-1.0, 1.0, 1.0, -1.0};  // sigma_y (x) sigma_y is anti-diagonal (-1, 1, 1, -1)
+  cplx Rt[4][4], X[4][4];
+  for (int r = 0; r < 4; ++r)
+    for (int c = 0; c < 4; ++c) Rt[r][c] = aqc::cscale(aqc::cconj(rho[3 - r][3 - c]), y[r] * y[c]);
+  for (int r = 0; r < 4; ++r)
+    for (int c = 0; c < 4; ++c) {
+      cplx acc = aqc::cmk(0, 0);
+      for (int k = 0; k < 4; ++k) acc = aqc::cfma(S[r][k], Rt[k][c], acc);
+      X[r][c] = acc;
+    }
+  for (int r = 0; r < 4; ++r)
+    for (int c = 0; c < 4; ++c) {
+      cplx acc = aqc::cmk(0, 0);
+      for (int k = 0; k < 4; ++k) acc = aqc::cfma(X[r][k], S[k][c], acc);
+      H[r][c] = acc;
+    }
+  for (int r = 0; r < 4; ++r) {  // symmetrise rounding
+    H[r][r].y = 0.0;
+    for (int c = r + 1; c < 4; ++c) {
+      const cplx m = aqc::cscale(aqc::cadd(H[r][c], aqc::cconj(H[c][r])), 0.5);
+      H[r][c] = m;
+      H[c][r] = aqc::cconj(m);
+    }
+  }
+  herm4_eig(H, d, V, false);
+  double l[4];
+  for (int k = 0; k < 4; ++k) l[k] = sqrt(fmax(d[k], 0.0));
+  for (int x = 0; x < 4; ++x)  // sort descending
+    for (int z = x + 1; z < 4; ++z)
+      if (l[z] > l[x]) {
+        const double t = l[x];
+        l[x] = l[z];
+        l[z] = t;
+      }
+  return fmax(0.0, l[0] - l[1] - l[2] - l[3]);
+}
+
+__device__ double trace_norm_pt(const cplx rho[4][4]) {
+  // partial transpose w.r.t. the first (high) subsystem (entanglement_measures.py:343-356);
+  // Hermitian, so its trace norm is the sum of |eigenvalues|
+  cplx H[4][4], V[4][4];
+  double d[4];
+  for (int ja = 0; ja < 2; ++ja)
+    for (int ka = 0; ka < 2; ++ka)
+      for (int jb = 0; jb < 2; ++jb)
+        for (int kb = 0; kb < 2; ++kb) H[ka * 2 + jb][ja * 2 + kb] = rho[ja * 2 + jb][ka * 2 + kb];
+  herm4_eig(H, d, V, false);
+  return fabs(d[0]) + fabs(d[1]) + fabs(d[2]) + fabs(d[3]);
+}
+
+// method: 0 concurrence, 1 EoF, 2 negativity, 3 log-negativity
+__global__ void k_ent_measure(const cplx* __restrict__ rdms, int count, int method, double* __restrict__ out) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= count) return;
+  cplx rho[4][4];
+  for (int r = 0; r < 4; ++r)
+    for (int c = 0; c < 4; ++c) rho[r][c] = rdms[(size_t)p * 16 + r * 4 + c];
+  double v = 0.0;
+  if (method == 0 || method == 1) {
+    const double c = concurrence4(rho);
+    if (method == 0) {
+      v = c;
+    } else if (c != 0.0) {
+      // entanglement_measures.py:263-275 (1 - c^2 clamped at 0: C rounds to 1 + O(eps) on Bell pairs)
+      const double x = 0.5 * (1.0 + sqrt(fmax(0.0, 1.0 - c * c)));
+      v = (x >= 1.0) ? 0.0 : -x * log2(x) - (1.0 - x) * log2(1.0 - x);
+    }
+  } else {
+    const double tn = trace_norm_pt(rho);
+    v = method == 2 ? (tn - 1.0) / 2.0 : log2(tn);
+  }
+  out[p] = v;
+}
+
+struct RdmBuffers {
+  void* dev = nullptr;
+  size_t cap = 0;
+};
+
+RdmBuffers& rbuf() {
+  static RdmBuffers b[64];
+  int dev = 0;
+  hipGetDevice(&dev);
+  return b[dev];
+}
+
+int ensure(RdmBuffers& b, size_t need) {
+  if (need > b.cap) {
+    if (b.dev) hipFree(b.dev);
+    b.cap = std::max(need, 2 * b.cap);
+    AQC_HIP_CHECK(hipMalloc(&b.dev, b.cap));
+  }
+  return AQC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int aqc_mps_pair_rdms_batch(aqc_mps_t* hs, int ns, const int* pairs, int npairs, double* out, int out_is_device) {
+  AQC_REQUIRE(hs && ns > 0 && pairs && out && npairs >= 0, "aqc_mps_pair_rdms_batch: bad arguments");
+  const int n = hs[0]->d.n, cap = hs[0]->d.cap;
+  for (int s = 0; s < ns; ++s)
+    AQC_REQUIRE(hs[s] && hs[s]->d.n == n && hs[s]->d.cap == cap, "aqc_mps_pair_rdms_batch: all states need the same n and capacity");
+  for (int p = 0; p < npairs; ++p) {
+    const int a = pairs[2 * p], b = pairs[2 * p + 1];
+    AQC_REQUIRE(a >= 0 && a < n && b >= 0 && b < n && a != b, "aqc_mps_pair_rdms_batch: bad pair");
+  }
+  if (npairs == 0) return AQC_OK;
+  int rc = aqc_mps_sort_batch(hs, ns);  // qubits back in site order, as measurements do
+  if (rc != AQC_OK) return rc;
+  std::vector<int> alist;
+  {
+    std::vector<char> need(n, 0);
+    for (int p = 0; p < npairs; ++p) need[std::min(pairs[2 * p], pairs[2 * p + 1])] = 1;
+    for (int a = 0; a < n - 1; ++a)
+      if (need[a]) alist.push_back(a);
+  }
+  const int na = (int)alist.size();
+  const size_t cc = (size_t)cap * cap;
+  const size_t per_state =
+      (2 * (size_t)(n + 1) * cc + 4 * cc + 6 * (size_t)n * cc + 12 * (size_t)na * cc + (size_t)n * n * 16) * sizeof(cplx);
+  const size_t jb = ((ns * sizeof(RdmJob) + 255) / 256) * 256;
+  const size_t pb = ((2 * npairs * sizeof(int) + na * sizeof(int) + 255) / 256) * 256;
+  const size_t ob = out_is_device ? 0 : (size_t)ns * npairs * 16 * sizeof(cplx);
+  hipStream_t st = aqc::mps_stream();
+  RdmBuffers& rb = rbuf();
+  AQC_HIP_CHECK(hipStreamSynchronize(st));
+  rc = ensure(rb, jb + pb + ob + ns * per_state + 1024);
+  if (rc != AQC_OK) return rc;
+  char* base = (char*)rb.dev;
+  RdmJob* djobs = (RdmJob*)base;
+  int* dpairs = (int*)(base + jb);
+  int* dalist = dpairs + 2 * npairs;
+  cplx* dout = out_is_device ? (cplx*)out : (cplx*)(base + jb + pb);
+  cplx* work = (cplx*)(base + jb + pb + ob);
+  std::vector<RdmJob> jobs(ns);
+  for (int s = 0; s < ns; ++s) {
+    RdmJob& j = jobs[s];
+    j.gam = hs[s]->d.gam;
+    j.lam = hs[s]->d.lam;
+    j.dims = hs[s]->d.dims;
+    j.n = n;
+    j.cap = cap;
+    cplx* p = work + (size_t)s * (per_state / sizeof(cplx));
+    j.Lenv = p;
+    p += (size_t)(n + 1) * cc;
+    j.Renv = p;
+    p += (size_t)(n + 1) * cc;
+    j.tmpL = p;
+    p += 2 * cc;
+    j.tmpR = p;
+    p += 2 * cc;
+    j.P = p;
+    p += 3 * (size_t)n * cc;
+    j.U = p;
+    p += 3 * (size_t)n * cc;
+    j.chain = p;
+    p += 12 * (size_t)na * cc;
+    j.rho = p;
+  }
+  AQC_HIP_CHECK(hipMemcpyAsync(djobs, jobs.data(), ns * sizeof(RdmJob), hipMemcpyHostToDevice, st));
+  AQC_HIP_CHECK(hipMemcpyAsync(dpairs, pairs, 2 * npairs * sizeof(int), hipMemcpyHostToDevice, st));
+  AQC_HIP_CHECK(hipMemcpyAsync(dalist, alist.data(), na * sizeof(int), hipMemcpyHostToDevice, st));
+  const double c3 = (double)cap * cap * cap;
+  aqc::KernelTimer::begin(st, "rdm_env", 0.0, ns * 2.0 * n * 4.0 * c3 * 8.0);
+  hipLaunchKernelGGL(k_rdm_env, dim3(2, ns), dim3(kT), 0, st, djobs);
+  aqc::KernelTimer::end(st);
+  AQC_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_rdm_P, dim3(n, 3, ns), dim3(kT), 0, st, djobs);
+  AQC_CHECK_LAUNCH();
+  double steps = 0.0;
+  for (int a : alist) steps += (double)(n - 1 - a);
+  aqc::KernelTimer::begin(st, "rdm_chain", 0.0, ns * steps * 3.0 * 4.0 * c3 * 8.0);
+  hipLaunchKernelGGL(k_rdm_chain, dim3(3, na, ns), dim3(kT), 0, st, djobs, dalist);
+  aqc::KernelTimer::end(st);
+  AQC_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_rdm_gather, dim3((npairs * 16 + 255) / 256, ns), dim3(256), 0, st, djobs, dpairs, npairs, dout);
+  AQC_CHECK_LAUNCH();
+  if (!out_is_device)
+    AQC_HIP_CHECK(hipMemcpyAsync(out, dout, (size_t)ns * npairs * 16 * sizeof(cplx), hipMemcpyDeviceToHost, st));
+  AQC_HIP_CHECK(hipStreamSynchronize(st));
+  return AQC_OK;
+}
+
+int aqc_mps_pair_rdms(aqc_mps_t h, const int* pairs, int npairs, double* out) {
+  return aqc_mps_pair_rdms_batch(&h, 1, pairs, npairs, out, 0);
+}
+
+int aqc_entanglement_measures(const double* rdms, int count, int method, double* out, int on_device) {
+  AQC_REQUIRE(rdms && out && count >= 0, "aqc_entanglement_measures: bad arguments");
+  AQC_REQUIRE(method >= 0 && method <= 3, "aqc_entanglement_measures: method must be 0..3");
+  if (count == 0) return AQC_OK;
+  hipStream_t st = aqc::mps_stream();
+  const cplx* drdm = (const cplx*)rdms;
+  double* dout = out;
+  void* tmp = nullptr;
+  if (!on_device) {
+    AQC_HIP_CHECK(hipMalloc(&tmp, (size_t)count * (16 * sizeof(cplx) + sizeof(double))));
+    AQC_HIP_CHECK(hipMemcpyAsync(tmp, rdms, (size_t)count * 16 * sizeof(cplx), hipMemcpyHostToDevice, st));
+    drdm = (const cplx*)tmp;
+    dout = (double*)((char*)tmp + (size_t)count * 16 * sizeof(cplx));
+  }
+  hipLaunchKernelGGL(k_ent_measure, dim3((count + 63) / 64), dim3(64), 0, st, drdm, count, method, dout);
+  AQC_CHECK_LAUNCH();
+  if (!on_device) AQC_HIP_CHECK(hipMemcpyAsync(out, dout, (size_t)count * sizeof(double), hipMemcpyDeviceToHost, st));
+  AQC_HIP_CHECK(hipStreamSynchronize(st));
+  if (tmp) hipFree(tmp);
+  return AQC_OK;
+}
+
+}  // extern "C"

@@ -222,6 +222,73 @@ std::vector<HostSeg> build_segments(const aqc_op_t* ops, int nops, int K, int n)
 
 }  // namespace
 
+// ---- two-qubit reduced density matrices (ISL, entanglement_measures.py:326-340) ------------
+// rho_ab[x][x'] = sum_rest psi[rest, x] conj(psi[rest, x']), x = 2*bit(hi) + bit(lo).  Each
+// workgroup reduces one chunk of the 2^(n-2) "rest" indices of one pair into the 16 real
+// numbers of the Hermitian 4x4 (upper triangle); a second pass sums the chunks (deterministic).
+__device__ __forceinline__ size_t insert_zero_bit(size_t x, int pos) {
+  return ((x >> pos) << (pos + 1)) | (x & ((size_t(1) << pos) - 1));
+}
+
+__global__ __launch_bounds__(kThreads) void k_sv_rdm_partial(const cplx* __restrict__ psi, int n,
+                                                            const int* __restrict__ pairs,
+                                                            double* __restrict__ partial) {
+  const int p = blockIdx.y, chunks = gridDim.x;
+  const int lo = min(pairs[2 * p], pairs[2 * p + 1]), hi = max(pairs[2 * p], pairs[2 * p + 1]);
+  const size_t rest = size_t(1) << (n - 2);
+  double acc[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) acc[q] = 0.0;
+  for (size_t r = (size_t)blockIdx.x * kThreads + threadIdx.x; r < rest; r += (size_t)chunks * kThreads) {
+    const size_t base = insert_zero_bit(insert_zero_bit(r, lo), hi);
+    cplx v[4];
+#pragma unroll
+    for (int x = 0; x < 4; ++x) v[x] = psi[base | ((size_t)(x & 1) << lo) | ((size_t)(x >> 1) << hi)];
+    int q = 0;
+#pragma unroll
+    for (int x = 0; x < 4; ++x) {
+      acc[q++] += aqc::cnorm2(v[x]);
+#pragma unroll
+      for (int y = x + 1; y < 4; ++y) {
+        const cplx m = aqc::cmul(v[x], aqc::cconj(v[y]));
+        acc[q++] += m.x;
+        acc[q++] += m.y;
+      }
+    }
+  }
+  __shared__ double red[16][kThreads];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) red[q][threadIdx.x] = acc[q];
+  __syncthreads();
+  for (int h = kThreads / 2; h > 0; h >>= 1) {
+    if ((int)threadIdx.x < h)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) red[q][threadIdx.x] += red[q][threadIdx.x + h];
+    __syncthreads();
+  }
+  if (threadIdx.x < 16) partial[((size_t)p * chunks + blockIdx.x) * 16 + threadIdx.x] = red[threadIdx.x][0];
+}
+
+__global__ void k_sv_rdm_final(const double* __restrict__ partial, int chunks, int npairs, cplx* __restrict__ out) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= npairs) return;
+  double s[16];
+  for (int q = 0; q < 16; ++q) s[q] = 0.0;
+  for (int c = 0; c < chunks; ++c)
+    for (int q = 0; q < 16; ++q) s[q] += partial[((size_t)p * chunks + c) * 16 + q];
+  cplx* rho = out + (size_t)p * 16;
+  int q = 0;
+  for (int x = 0; x < 4; ++x) {
+    rho[x * 4 + x] = aqc::cmk(s[q++], 0.0);
+    for (int y = x + 1; y < 4; ++y) {
+      const cplx m = aqc::cmk(s[q], s[q + 1]);
+      q += 2;
+      rho[x * 4 + y] = m;
+      rho[y * 4 + x] = aqc::cconj(m);
+    }
+  }
+}
+
 struct aqc_sv_s {
   int n = 0;
   int K = 0;
@@ -415,6 +482,40 @@ int aqc_sv_z_all(aqc_sv_t h, double* out) {
   AQC_CHECK_LAUNCH();
   AQC_HIP_CHECK(hipMemcpyAsync(out, h->d_z, sizeof(double) * h->n, hipMemcpyDeviceToHost, h->stream));
   AQC_HIP_CHECK(hipStreamSynchronize(h->stream));
+  return AQC_OK;
+}
+
+int aqc_sv_pair_rdms(aqc_sv_t h, const int* pairs, int npairs, double* out) {
+  AQC_REQUIRE(h && pairs && out && npairs >= 0, "aqc_sv_pair_rdms: bad arguments");
+  AQC_REQUIRE(h->n >= 2, "aqc_sv_pair_rdms: needs at least 2 qubits");
+  for (int p = 0; p < npairs; ++p) {
+    const int a = pairs[2 * p], b = pairs[2 * p + 1];
+    AQC_REQUIRE(a >= 0 && a < h->n && b >= 0 && b < h->n && a != b, "aqc_sv_pair_rdms: bad pair");
+  }
+  if (npairs == 0) return AQC_OK;
+  const size_t rest = size_t(1) << (h->n - 2);
+  // about 2048 workgroups in total, at least 4 rest indices per thread
+  const size_t per_pair = std::max<size_t>(1, std::min<size_t>(rest / (4 * kThreads), (2048 + npairs - 1) / npairs));
+  const int chunks = (int)per_pair;
+  char* buf = nullptr;
+  const size_t pb = ((size_t)2 * npairs * sizeof(int) + 255) / 256 * 256;
+  const size_t qb = (size_t)npairs * chunks * 16 * sizeof(double);
+  const size_t ob = (size_t)npairs * 16 * sizeof(cplx);
+  AQC_HIP_CHECK(hipMalloc(&buf, pb + qb + ob));
+  int* dpairs = (int*)buf;
+  double* dpart = (double*)(buf + pb);
+  cplx* dout = (cplx*)(buf + pb + qb);
+  AQC_HIP_CHECK(hipMemcpyAsync(dpairs, pairs, 2 * npairs * sizeof(int), hipMemcpyHostToDevice, h->stream));
+  aqc::KernelTimer::begin(h->stream, "sv_rdm", (double)npairs * 16.0 * (double)(1ull << h->n), 0.0);
+  hipLaunchKernelGGL(k_sv_rdm_partial, dim3(chunks, npairs), dim3(kThreads), 0, h->stream, h->state, h->n, dpairs,
+                     dpart);
+  aqc::KernelTimer::end(h->stream);
+  AQC_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_sv_rdm_final, dim3((npairs + 63) / 64), dim3(64), 0, h->stream, dpart, chunks, npairs, dout);
+  AQC_CHECK_LAUNCH();
+  AQC_HIP_CHECK(hipMemcpyAsync(out, dout, ob, hipMemcpyDeviceToHost, h->stream));
+  AQC_HIP_CHECK(hipStreamSynchronize(h->stream));
+  AQC_HIP_CHECK(hipFree(buf));
   return AQC_OK;
 }
 

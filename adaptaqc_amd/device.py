@@ -45,6 +45,14 @@ class DeviceSV:
         _lib.check(self._l.aqc_sv_z_all(self.h, _lib.dptr(out)))
         return out
 
+    def pair_rdms(self, pairs):
+        """4x4 reduced density matrices of qubit pairs (entanglement_measures.py:326-340)."""
+        pairs = np.ascontiguousarray(np.asarray(pairs, dtype=np.int32).reshape(-1))
+        out = np.zeros(len(pairs) // 2 * 16, dtype=np.complex128)
+        if len(pairs):
+            _lib.check(self._l.aqc_sv_pair_rdms(self.h, _lib.ptr(pairs), len(pairs) // 2, _lib.ptr(out)))
+        return out.reshape(-1, 4, 4)
+
     def get(self):
         out = np.zeros(2 ** self.n, dtype=np.complex128)
         _lib.check(self._l.aqc_sv_get(self.h, _lib.ptr(out)))
@@ -171,6 +179,14 @@ class DeviceMPS:
         _lib.check(self._l.aqc_mps_amps_hw1(self.h, _lib.ptr(out)))
         return out[0::2] + 1j * out[1::2]
 
+    def pair_rdms(self, pairs):
+        """4x4 RDMs of qubit pairs by environment chains (aqc_research partial_trace semantics)."""
+        pairs = np.ascontiguousarray(np.asarray(pairs, dtype=np.int32).reshape(-1))
+        out = np.zeros(len(pairs) // 2 * 16, dtype=np.complex128)
+        if len(pairs):
+            _lib.check(self._l.aqc_mps_pair_rdms(self.h, _lib.ptr(pairs), len(pairs) // 2, _lib.ptr(out)))
+        return out.reshape(-1, 4, 4)
+
 
 def _handles(states):
     arr = (ctypes.c_void_p * len(states))(*[s.h.value for s in states])
@@ -186,6 +202,19 @@ def apply_batch(states, ops_lists):
     ptrs = (ctypes.c_void_p * len(arrs))(*[a.ctypes.data if len(a) else 0 for a in arrs])
     counts = np.asarray([len(a) for a in arrs], dtype=np.int32)
     _lib.check(l.aqc_mps_apply_batch(_handles(states), len(states), ptrs, _lib.ptr(counts)))
+
+
+EM_METHOD_CODES = {"concurrence": 0, "eof": 1, "negativity": 2, "log_negativity": 3}
+
+
+def entanglement_measures(rdms, method):
+    """Entanglement measure of each 4x4 density matrix on the device (aqc_entanglement_measures)."""
+    code = EM_METHOD_CODES[method]
+    r = np.ascontiguousarray(np.asarray(rdms, dtype=np.complex128).reshape(-1, 16))
+    out = np.zeros(len(r))
+    if len(r):
+        _lib.check(_lib.lib().aqc_entanglement_measures(_lib.ptr(r), len(r), code, _lib.ptr(out), 0))
+    return out
 
 
 def copy_batch(dst, src):

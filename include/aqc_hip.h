@@ -106,6 +106,21 @@ int aqc_mps_set_jacobi_tol(double factor);
    2*chi <= 128 (default; larger chi uses 0), 3 = register-resident without QR,
    0 = 512 threads / 128 KiB LDS panel, 1 = 256 threads / 64 KiB panel (2 per CU). */
 int aqc_mps_set_jacobi_variant(int variant);
+/* ---- ISL entanglement sweep (adapt_compiler.py:955-976 -> entanglement_measures.py:39-98) ----
+   Two-qubit reduced density matrices for npairs pairs (pairs[2p], pairs[2p+1]), out = npairs x
+   4 x 4 complex (row-major), row index 2*bit(max) + bit(min) as qiskit's partial_trace orders
+   the remaining qubits.  SV: entanglement_measures.py:326-340.  MPS: the contraction of
+   aqc_research.mps_operations.partial_trace (sorts qubits first); the batch version writes
+   nstates x npairs x 16 complex, to device memory when out_is_device. */
+int aqc_sv_pair_rdms(aqc_sv_t h, const int* pairs, int npairs, double* out);
+int aqc_mps_pair_rdms(aqc_mps_t h, const int* pairs, int npairs, double* out);
+int aqc_mps_pair_rdms_batch(aqc_mps_t* hs, int nstates, const int* pairs, int npairs, double* out,
+                            int out_is_device);
+/* Measures of count 4x4 density matrices (entanglement_measures.py:245-306): method 0 =
+   concurrence (EM_TOMOGRAPHY_CONCURRENCE), 1 = entanglement of formation, 2 = negativity,
+   3 = log-negativity.  rdms / out in device memory when on_device. */
+int aqc_entanglement_measures(const double* rdms, int count, int method, double* out, int on_device);
+
 /* Diagnostics: one register-resident Jacobi launch (variant 2 = with pivoted QR, 3 = without) on
    theta (m x n column-major complex, m, n even <= 128, as the two-site update builds it).
    w_out receives min(m,n) columns of length (variant 2: min(m,n), 3: max(m,n)); sig_out their

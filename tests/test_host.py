@@ -189,3 +189,29 @@ def test_isinstance_switches():
 
     assert is_statevector_backend(HipSVBackend()) and not is_statevector_backend(HipMPSBackend())
     assert isinstance(HipMPSBackend(), AerMPSBackend) and issubclass(HipSVBackend, AerSVBackend)
+
+
+def test_isl_pair_selection_host_logic(monkeypatch):
+    """adapt_compiler.py:858-919 on synthetic histories: reuse priority, bad pairs, threshold."""
+    from adaptaqc_amd.backends import AerSVBackend
+    from adaptaqc_amd.circuit import QuantumCircuit
+    from adaptaqc_amd.compilers import AdaptCompiler, AdaptConfig
+
+    qc = QuantumCircuit(3)
+    qc.h(0)
+    comp = AdaptCompiler(qc, backend=AerSVBackend(), adapt_config=AdaptConfig(bad_qubit_pair_memory=2))
+    cmap = comp.coupling_map
+    monkeypatch.setattr(comp, "_find_best_expectation_qubit_pair", lambda: "expectation")
+    ems = [0.1 * (i + 1) for i in range(len(cmap))]
+    comp.entanglement_measures_history.append(ems)
+    assert comp._find_best_entanglement_qubit_pair(ems) == cmap[-1]
+    comp.qubit_pair_history.append(cmap[-1])
+    # entanglement of the chosen pair did not go down -> bad pair, masked while in memory
+    comp.entanglement_measures_history.append(list(ems))
+    pick = comp._find_best_entanglement_qubit_pair(ems)
+    assert cmap[-1] in comp.bad_qubit_pairs and pick != cmap[-1]
+    # everything below the threshold -> expectation fall-back
+    tiny = [1e-12] * len(cmap)
+    comp.entanglement_measures_history.append(tiny)
+    comp.qubit_pair_history.append(pick)
+    assert comp._find_best_entanglement_qubit_pair(tiny) == "expectation"

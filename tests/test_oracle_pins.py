@@ -185,3 +185,37 @@ def test_minimum_of_sinusoidal():
         f = lambda x: a * np.sin(x + b) + c
         th, val = H.minimum_of_sinusoidal(f(0), f(np.pi / 2), f(-np.pi / 2))
         assert abs(val - (c - abs(a))) < 1e-12 and abs(f(th) - val) < 1e-12
+
+
+def test_entanglement_oracle_known_answers():
+    """oracle/entanglement.py: MPS contraction == SV partial trace; Bell / Werner / product."""
+    from oracle import entanglement as OE
+    from oracle import mps as M
+    from oracle import sv as osv
+
+    rng = np.random.default_rng(3)
+    n = 6
+    ops = []
+    for layer in range(5):
+        for q in range(n):
+            ops.append((["rx", "ry", "rz"][rng.integers(3)], (q,), (rng.uniform(-3, 3),)))
+        for q in range(layer % 2, n - 1, 2):
+            ops.append(("cx", (q, q + 1), ()))
+    ops.append(("cx", (0, 4), ()))
+    psi = osv.simulate(n, ops)
+    pre = M.run_circuit(n, ops, 1e-16, None).preprocessed()
+    for a in range(n):
+        for b in range(a + 1, n):
+            np.testing.assert_allclose(OE.mps_rdm(pre, a, b), OE.partial_trace_sv(psi, a, b), atol=1e-13)
+    bell = np.array([1, 0, 0, 1]) / np.sqrt(2)
+    rho = np.outer(bell, bell.conj())
+    assert abs(OE.concurrence(rho) - 1) < 1e-12 and abs(OE.eof(rho) - 1) < 1e-12
+    assert abs(OE.negativity(rho) - 0.5) < 1e-12 and abs(OE.log_negativity(rho) - 1) < 1e-12
+    w = 0.8 * rho + 0.2 / 4 * np.eye(4)
+    assert abs(OE.concurrence(w) - 0.7) < 1e-12
+    prod = np.kron([1, 0], [np.cos(0.3), np.sin(0.3)])
+    assert OE.concurrence(np.outer(prod, prod)) == 0.0
+    # qubit ordering of the 2-qubit partial trace: x = 2*bit(hi) + bit(lo)
+    psi2 = np.zeros(8, complex)
+    psi2[0b100] = 1.0  # qubit 2 = 1
+    np.testing.assert_allclose(np.diag(OE.partial_trace_sv(psi2, 0, 2)).real, [0, 0, 1, 0])
