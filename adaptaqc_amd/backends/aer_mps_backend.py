@@ -57,8 +57,9 @@ class AerMPSBackend(AQCBackend):
         o = self.simulator.options
         return o.matrix_product_state_truncation_threshold, o.matrix_product_state_max_bond_dimension
 
-    def device_state(self, circuit):
-        """Replay ``circuit`` on the device; returns the (sorted) work DeviceMPS."""
+    def ensure_base(self, circuit):
+        """Device copy of the circuit's leading set_matrix_product_state payload (or |0..0>),
+        cached across evaluations; returns (base DeviceMPS, index of the first gate to replay)."""
         thr, max_chi = self._options()
         n = circuit.num_qubits
         start = 0
@@ -74,9 +75,22 @@ class AerMPSBackend(AQCBackend):
             base.load_aer(payload if payload is not None else zero_aer_mps(n))
             self._base = (key, base, payload)
             self._work = DeviceMPS(n, cap, thr, max_chi)
+        self._base[1].set_truncation(thr, max_chi)
+        return self._base[1], start
+
+    def new_state(self):
+        """An empty device MPS shaped like the cached base (for prefix / variant states)."""
+        base = self._base[1]
+        thr, max_chi = self._options()
+        return DeviceMPS(base.n, base.chi_cap, thr, max_chi)
+
+    def device_state(self, circuit):
+        """Replay ``circuit`` on the device; returns the (sorted) work DeviceMPS."""
+        thr, max_chi = self._options()
+        base, start = self.ensure_base(circuit)
         work = self._work
         work.set_truncation(thr, max_chi)
-        work.copy_from(self._base[1])
+        work.copy_from(base)
         work.apply(device_ops(circuit, start))
         work.sort()
         return work

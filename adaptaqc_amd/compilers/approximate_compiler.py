@@ -51,7 +51,7 @@ class ApproximateCompiler(ABC):
         if not 0 < rotosolve_fraction <= 1:
             raise ValueError("rotosolve_fraction must be in the range (0,1]")
         self.minimizer = CostMinimiser(self.evaluate_cost, self.variational_circuit_range, self.full_circuit,
-                                       rotosolve_fraction)
+                                       rotosolve_fraction, evaluator_factory=self._candidate_evaluator)
         self.cost_evaluation_counter = 0
         self.compiling_finished = False
 
@@ -104,6 +104,15 @@ class ApproximateCompiler(ABC):
         final = QuantumCircuit(self.circuit_to_compile.num_qubits)
         co.add_to_circuit(final, compiled, qubit_subset={i: q for i, q in enumerate(self.qubit_subset_to_compile)})
         return final
+
+    def _candidate_evaluator(self):
+        """Cached Rotoselect / Rotosolve candidates (utils/cached_rotations.py) unless disabled
+        with ``use_cached_rotations = False``; None selects the reference's generic path."""
+        if not getattr(self, "use_cached_rotations", True):
+            return None
+        from ..utils.cached_rotations import make_evaluator
+
+        return make_evaluator(self)
 
     def evaluate_cost(self):
         """approximate_compiler.py:514-527."""

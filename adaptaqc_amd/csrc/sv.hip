@@ -289,6 +289,45 @@ __global__ void k_sv_rdm_final(const double* __restrict__ partial, int chunks, i
   }
 }
 
+// ---- transition matrix for cached Rotoselect / Rotosolve -------------------------------------
+// T[a][b] = <chi| (|a><b|)_q |phi> = sum_rest conj(chi[rest, q=a]) phi[rest, q=b]: with phi the
+// prefix state and chi = S^dag|0> the undone suffix, <0|S V P|0> = sum_ab V[a][b] T[a][b] for
+// every single-qubit gate V at that position (cost_minimiser.py:344-368 evaluates 3 of them by
+// full simulations).  Partial sums per workgroup, deterministic final pass.
+__global__ __launch_bounds__(kThreads) void k_sv_transition_partial(const cplx* __restrict__ chi,
+                                                                   const cplx* __restrict__ phi, int n, int q,
+                                                                   double* __restrict__ partial) {
+  const size_t half = size_t(1) << (n - 1);
+  double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (size_t r = (size_t)blockIdx.x * kThreads + threadIdx.x; r < half; r += (size_t)gridDim.x * kThreads) {
+    const size_t i0 = insert_zero_bit(r, q), i1 = i0 | (size_t(1) << q);
+    const cplx c0 = chi[i0], c1 = chi[i1], p0 = phi[i0], p1 = phi[i1];
+    const cplx t00 = aqc::cconjmul(c0, p0), t01 = aqc::cconjmul(c0, p1), t10 = aqc::cconjmul(c1, p0),
+               t11 = aqc::cconjmul(c1, p1);
+    acc[0] += t00.x, acc[1] += t00.y, acc[2] += t01.x, acc[3] += t01.y;
+    acc[4] += t10.x, acc[5] += t10.y, acc[6] += t11.x, acc[7] += t11.y;
+  }
+  __shared__ double red[8][kThreads];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) red[k][threadIdx.x] = acc[k];
+  __syncthreads();
+  for (int h = kThreads / 2; h > 0; h >>= 1) {
+    if ((int)threadIdx.x < h)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) red[k][threadIdx.x] += red[k][threadIdx.x + h];
+    __syncthreads();
+  }
+  if (threadIdx.x < 8) partial[(size_t)blockIdx.x * 8 + threadIdx.x] = red[threadIdx.x][0];
+}
+
+__global__ void k_sv_transition_final(const double* __restrict__ partial, int chunks, double* __restrict__ out) {
+  const int k = threadIdx.x;
+  if (k >= 8) return;
+  double s = 0.0;
+  for (int c = 0; c < chunks; ++c) s += partial[(size_t)c * 8 + k];
+  out[k] = s;
+}
+
 struct aqc_sv_s {
   int n = 0;
   int K = 0;
@@ -302,7 +341,20 @@ struct aqc_sv_s {
   double* d_z = nullptr;
   int zwg = 0;
   cplx* h_pinned = nullptr;
+  char* d_scratch = nullptr;  // grow-only workspace of the reduction kernels (RDMs, transition)
+  size_t scratch_cap = 0;
 };
+
+static int sv_scratch(aqc_sv_t h, size_t bytes, char** out) {
+  if (bytes > h->scratch_cap) {
+    AQC_HIP_CHECK(hipStreamSynchronize(h->stream));
+    if (h->d_scratch) AQC_HIP_CHECK(hipFree(h->d_scratch));
+    h->scratch_cap = std::max(bytes, 2 * h->scratch_cap);
+    AQC_HIP_CHECK(hipMalloc(&h->d_scratch, h->scratch_cap));
+  }
+  *out = h->d_scratch;
+  return AQC_OK;
+}
 
 static int sv_launch_segment(aqc_sv_t h, const SegHeader* dh, const SegGate* dg, int nblocks) {
   const double bytes = 32.0 * (double)(1ull << h->n);
@@ -366,6 +418,7 @@ int aqc_sv_destroy(aqc_sv_t h) {
   hipFree(h->d_gates);
   hipFree(h->d_zpart);
   hipFree(h->d_z);
+  if (h->d_scratch) hipFree(h->d_scratch);
   if (h->h_pinned) hipHostFree(h->h_pinned);
   if (h->stream) hipStreamDestroy(h->stream);
   delete h;
@@ -501,7 +554,8 @@ int aqc_sv_pair_rdms(aqc_sv_t h, const int* pairs, int npairs, double* out) {
   const size_t pb = ((size_t)2 * npairs * sizeof(int) + 255) / 256 * 256;
   const size_t qb = (size_t)npairs * chunks * 16 * sizeof(double);
   const size_t ob = (size_t)npairs * 16 * sizeof(cplx);
-  AQC_HIP_CHECK(hipMalloc(&buf, pb + qb + ob));
+  int rc = sv_scratch(h, pb + qb + ob, &buf);
+  if (rc != AQC_OK) return rc;
   int* dpairs = (int*)buf;
   double* dpart = (double*)(buf + pb);
   cplx* dout = (cplx*)(buf + pb + qb);
@@ -515,7 +569,28 @@ int aqc_sv_pair_rdms(aqc_sv_t h, const int* pairs, int npairs, double* out) {
   AQC_CHECK_LAUNCH();
   AQC_HIP_CHECK(hipMemcpyAsync(out, dout, ob, hipMemcpyDeviceToHost, h->stream));
   AQC_HIP_CHECK(hipStreamSynchronize(h->stream));
-  AQC_HIP_CHECK(hipFree(buf));
+  return AQC_OK;
+}
+
+int aqc_sv_transition(aqc_sv_t bra, aqc_sv_t ket, int q, double* out) {
+  AQC_REQUIRE(bra && ket && out, "aqc_sv_transition: null argument");
+  AQC_REQUIRE(bra->n == ket->n && q >= 0 && q < bra->n, "aqc_sv_transition: bad qubit or size mismatch");
+  const int n = bra->n;
+  // ket and bra live on their own streams: order the reads after both states' pending work
+  AQC_HIP_CHECK(hipStreamSynchronize(bra->stream));
+  const size_t half = size_t(1) << (n - 1);
+  const int chunks = (int)std::max<size_t>(1, std::min<size_t>(1024, half / (4 * kThreads)));
+  char* raw = nullptr;
+  int rc = sv_scratch(ket, ((size_t)chunks * 8 + 8) * sizeof(double), &raw);
+  if (rc != AQC_OK) return rc;
+  double* buf = (double*)raw;
+  hipLaunchKernelGGL(k_sv_transition_partial, dim3(chunks), dim3(kThreads), 0, ket->stream, bra->state, ket->state, n,
+                     q, buf);
+  AQC_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_sv_transition_final, dim3(1), dim3(64), 0, ket->stream, buf, chunks, buf + (size_t)chunks * 8);
+  AQC_CHECK_LAUNCH();
+  AQC_HIP_CHECK(hipMemcpyAsync(out, buf + (size_t)chunks * 8, 8 * sizeof(double), hipMemcpyDeviceToHost, ket->stream));
+  AQC_HIP_CHECK(hipStreamSynchronize(ket->stream));
   return AQC_OK;
 }
 

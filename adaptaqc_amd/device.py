@@ -45,6 +45,12 @@ class DeviceSV:
         _lib.check(self._l.aqc_sv_z_all(self.h, _lib.dptr(out)))
         return out
 
+    def transition(self, ket, q):
+        """2x2 T[a][b] = <self| (|a><b|)_q |ket> (cached Rotoselect / Rotosolve)."""
+        out = np.zeros(4, dtype=np.complex128)
+        _lib.check(self._l.aqc_sv_transition(self.h, ket.h, int(q), _lib.ptr(out)))
+        return out.reshape(2, 2)
+
     def pair_rdms(self, pairs):
         """4x4 reduced density matrices of qubit pairs (entanglement_measures.py:326-340)."""
         pairs = np.ascontiguousarray(np.asarray(pairs, dtype=np.int32).reshape(-1))

@@ -1,7 +1,9 @@
 """Rotoselect / Rotosolve sequential optimiser (reference utils/cost_minimiser.py:32-418).
 
-Host caller of the hot path: every ``cost_finder()`` call is one overlap evaluation on the
-device (3 per rotation gate for Rotosolve, 7 for Rotoselect).
+Host caller of the hot path.  Generic path: every ``cost_finder()`` call is one overlap
+evaluation on the device (3 per rotation gate for Rotosolve, 7 for Rotoselect), as in the
+reference.  With an ``evaluator_factory`` (set by the compilers) the candidates of a gate come
+from one cached evaluation instead (utils/cached_rotations.py).
 """
 import logging
 import random
@@ -17,11 +19,15 @@ ALG_SCIPY = "scipy"
 
 
 class CostMinimiser:
-    def __init__(self, cost_finder, variational_circuit_range, full_circuit, rotosolve_fraction=1.0):
+    def __init__(self, cost_finder, variational_circuit_range, full_circuit, rotosolve_fraction=1.0,
+                 evaluator_factory=None):
         self.cost_finder = cost_finder
         self.variational_circuit_range = variational_circuit_range
         self.full_circuit = full_circuit
         self.rotosolve_fraction = rotosolve_fraction
+        # cached / batched candidate evaluation (utils/cached_rotations.py); None = the reference's
+        # one-simulation-per-candidate path
+        self.evaluator_factory = evaluator_factory
 
     def minimize_cost(self, algorithm_kind=ALG_ROTOSOLVE, algorithm_identifier=None, max_cycles=1000,
                       stop_val=-np.inf, tol=1e-10, indexes_to_modify=None, alg_kwargs=None):
@@ -66,6 +72,9 @@ class CostMinimiser:
             sample = sorted(random.sample(cands, int(np.ceil(self.rotosolve_fraction * len(cands)))))
         else:
             sample = list(range(*indexes_to_modify))
+        ev = self.evaluator_factory() if self.evaluator_factory is not None else None
+        if ev is not None:
+            return self._reduce_cost_cached(ev, change_1q_gate_kind, sample)
         for index in sample:
             old_gate = self.full_circuit.data[index].operation
             if change_1q_gate_kind and co.is_supported_1q_gate(old_gate):
@@ -73,6 +82,41 @@ class CostMinimiser:
             elif co.is_supported_1q_gate(old_gate):
                 angle, cost = self.find_best_angle(index, old_gate.label)
                 co.replace_1q_gate(self.full_circuit, index, old_gate.label, angle)
+        return cost
+
+    def _reduce_cost_cached(self, ev, change_1q_gate_kind, sample):
+        """_reduce_cost with every candidate of a gate from one cached evaluation: the same
+        candidates, sinusoid fits and selection rules as replace_with_best_1q_gate /
+        find_best_angle, in the same gate order."""
+        from .cached_rotations import rotation
+
+        cost = 1
+        for index in sample:
+            old_gate = self.full_circuit.data[index].operation
+            if not co.is_supported_1q_gate(old_gate):
+                continue
+            ev.goto(index)
+            if change_1q_gate_kind:
+                names = co.SUPPORTED_1Q_GATES
+                mats = [rotation("rx", 0.0)]
+                for name in names:
+                    mats += [rotation(name, np.pi / 2), rotation(name, -np.pi / 2)]
+                c = ev.costs(index, mats)
+                ev.count(1 + 2 * len(names))
+                co.replace_1q_gate(self.full_circuit, index, "rx", 0)
+                best_name, best_angle, best_cost = None, None, 1
+                for k, name in enumerate(names):
+                    angle, cst = minimum_of_sinusoidal(c[0], c[1 + 2 * k], c[2 + 2 * k])
+                    if cst < best_cost:
+                        best_name, best_angle, best_cost = name, angle, cst
+                co.replace_1q_gate(self.full_circuit, index, best_name, best_angle)
+                cost = best_cost
+            else:
+                name = old_gate.label
+                c = ev.costs(index, [rotation(name, 0.0), rotation(name, np.pi / 2), rotation(name, -np.pi / 2)])
+                ev.count(3)
+                angle, cost = minimum_of_sinusoidal(c[0], c[1], c[2])
+                co.replace_1q_gate(self.full_circuit, index, name, angle)
         return cost
 
     def replace_with_best_1q_gate(self, gate_index):

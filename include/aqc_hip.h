@@ -116,6 +116,10 @@ int aqc_sv_pair_rdms(aqc_sv_t h, const int* pairs, int npairs, double* out);
 int aqc_mps_pair_rdms(aqc_mps_t h, const int* pairs, int npairs, double* out);
 int aqc_mps_pair_rdms_batch(aqc_mps_t* hs, int nstates, const int* pairs, int npairs, double* out,
                             int out_is_device);
+/* Cached Rotoselect / Rotosolve (replaces the 3-7 full simulations per gate of
+   cost_minimiser.py:318-368): out = 2x2 complex T[a][b] = <bra| (|a><b|)_q |ket>, so that
+   <bra|V_q|ket> = sum_ab V[a][b] T[a][b] for any single-qubit V. */
+int aqc_sv_transition(aqc_sv_t bra, aqc_sv_t ket, int q, double* out);
 /* Measures of count 4x4 density matrices (entanglement_measures.py:245-306): method 0 =
    concurrence (EM_TOMOGRAPHY_CONCURRENCE), 1 = entanglement of formation, 2 = negativity,
    3 = log-negativity.  rdms / out in device memory when on_device. */

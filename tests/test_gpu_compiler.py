@@ -121,3 +121,69 @@ def test_checkpoint_resume(tmp_path):
     resumed.adapt_config.max_layers = 5
     res = resumed.compile()
     assert len(res.qubit_pair_history) >= 3
+
+
+def _insert_ansatz(comp, seed):
+    """Labelled rotations + CX inserted at the end of the variational range (where ADAPT layers go)."""
+    from adaptaqc_amd.circuit import Operation
+    from adaptaqc_amd.utils import circuit_operations as co
+
+    rng = np.random.default_rng(seed)
+    n = comp.full_circuit.num_qubits
+    pos = len(comp.full_circuit.data) - comp.rhs_gate_count
+    gates = []
+    for layer in range(3):
+        for q in range(n):
+            gates.append((co.create_1q_gate(["rx", "ry", "rz"][rng.integers(3)], rng.uniform(-2, 2)), [q]))
+        for q in range(layer % 2, n - 1, 2):
+            gates.append((Operation("cx", 2, []), [q, q + 1]))
+    gates.append((Operation("cx", 2, []), [0, n - 1]))
+    for q in range(n):
+        gates.append((co.create_1q_gate("ry", rng.uniform(-2, 2)), [q]))
+    for k, (g, qs) in enumerate(gates):
+        co.add_gate(comp.full_circuit, g, pos + k, qs)
+
+
+@pytest.mark.parametrize("backend_kind", ["sv", "mps"])
+@pytest.mark.parametrize("rotoselect", [False, True])
+def test_cached_rotations_match_generic(backend_kind, rotoselect):
+    """Cached candidates (utils/cached_rotations.py) reproduce the reference's one-simulation-
+    per-candidate sweep: same gates, angles (1e-9), costs (1e-10) and evaluation count."""
+    from adaptaqc_amd.backends import AerMPSBackend, AerSVBackend
+    from adaptaqc_amd.compilers import AdaptCompiler
+
+    results = []
+    for cached in (False, True):
+        backend = AerSVBackend() if backend_kind == "sv" else AerMPSBackend()
+        comp = AdaptCompiler(to_circuit(4, _random_state_circuit(4, 3, 21)), backend=backend)
+        comp.use_cached_rotations = cached
+        _insert_ansatz(comp, 5)
+        rng = comp.variational_circuit_range()
+        assert rng[1] - rng[0] > 10
+        start_count = comp.cost_evaluation_counter
+        cost = comp.minimizer._reduce_cost(rotoselect, rng)
+        gates = [(i.operation.name, tuple(i.qubits), tuple(i.operation.params)) for i in comp.full_circuit.data]
+        results.append((cost, gates, comp.cost_evaluation_counter - start_count, comp.evaluate_cost()))
+    (c0, g0, n0, e0), (c1, g1, n1, e1) = results
+    assert n0 == n1
+    assert abs(c0 - c1) < 1e-10 and abs(e0 - e1) < 1e-10
+    assert [x[:2] for x in g0] == [x[:2] for x in g1]
+    for a, b in zip(g0, g1):
+        if a[0] in ("rx", "ry", "rz"):
+            np.testing.assert_allclose(a[2], b[2], atol=1e-9)
+
+
+def test_compile_cached_vs_generic_same_result():
+    from adaptaqc_amd.compilers import AdaptCompiler, AdaptConfig
+
+    qc = to_circuit(4, _random_state_circuit(4, 2, 13))
+    out = []
+    for cached in (False, True):
+        comp = AdaptCompiler(qc, adapt_config=AdaptConfig(method="basic", max_layers=6))
+        comp.use_cached_rotations = cached
+        res = comp.compile()
+        out.append((res.overlap, [(i.operation.name, tuple(i.qubits)) for i in res.circuit.data],
+                    comp.cost_evaluation_counter))
+    assert abs(out[0][0] - out[1][0]) < 1e-8
+    assert out[0][1] == out[1][1]
+    assert out[0][2] == out[1][2]
