@@ -387,6 +387,35 @@ __global__ __launch_bounds__(JT) void k_jacobi(const TwoSiteJob* __restrict__ jo
 // the *other* side times sigma (rows mapped back through the pivot order P), which k_split
 // handles by flipping its side test (tools/qrp_jacobi_proto.py is the numpy restatement).
 
+// Rotation parameters of the pair (alpha, beta, gamma = gx + i gy): t = sgn(zeta) /
+// (|zeta| + sqrt(1 + zeta^2)), zeta = (beta - alpha) / (2|gamma|), c = 1/sqrt(1 + t^2) and
+// s e = c t gamma / |gamma|.  v_rsq_f64 / v_rcp_f64 seeds with two Newton steps each (full double
+// precision) instead of the IEEE sqrt / divide sequences: this chain is serial per round.
+__device__ __forceinline__ void jacobi_params(double al, double be, double gx, double gy, double g2, double& c,
+                                              double& ex, double& ey) {
+  double rg = __builtin_amdgcn_rsq(g2);  // 1 / |gamma|
+  rg = rg * fma(-0.5 * g2 * rg, rg, 1.5);
+  rg = rg * fma(-0.5 * g2 * rg, rg, 1.5);
+  const double zeta = 0.5 * (be - al) * rg;
+  const double q = fma(zeta, zeta, 1.0);
+  double rq = __builtin_amdgcn_rsq(q);
+  rq = rq * fma(-0.5 * q * rq, rq, 1.5);
+  rq = rq * fma(-0.5 * q * rq, rq, 1.5);
+  const double den = fabs(zeta) + q * rq;  // |zeta| + sqrt(1 + zeta^2)
+  double inv = __builtin_amdgcn_rcp(den);
+  inv = inv * fma(-den, inv, 2.0);
+  inv = inv * fma(-den, inv, 2.0);
+  const double t = zeta >= 0 ? inv : -inv;
+  const double p = fma(t, t, 1.0);
+  double cc = __builtin_amdgcn_rsq(p);
+  cc = cc * fma(-0.5 * p * cc, cc, 1.5);
+  cc = cc * fma(-0.5 * p * cc, cc, 1.5);
+  c = cc;
+  const double sc = cc * t * rg;
+  ex = gx * sc;
+  ey = gy * sc;
+}
+
 // sortable pivot key: non-negative double bits with the low byte replaced by (255 - id), so
 // that the 64-bit maximum is the largest trailing norm, ties to the lowest column id
 __device__ __forceinline__ unsigned long long pivot_key(double v, int id) {
@@ -580,6 +609,18 @@ __global__ __launch_bounds__(CP * 8) void k_jacobi_reg(const TwoSiteJob* __restr
   const double tol2 = tol * tol;
   const int max_sweeps = j.dbg == 1 ? 0 : kMaxSweeps;
   const bool map_rows = use_qr && j.dbg != 1;
+  // The M half of the columns moves into LDS slots (slot g <- this group's M) and stays there:
+  // S stays in VGPRs.  Round r of a level with sub-blocks of m groups pairs S_g with slot
+  // base + (li + r) mod m -- the parallel ordering's shift is addressing only -- and a slot is
+  // written back only when its column was rotated, which late sweeps rarely do.  Level split:
+  // the upper half swaps its S with slot g - h (the lower half's next partners).  One barrier
+  // per round.  (A register-resident M with a per-round LDS shift moved every M column through
+  // the ~79 B/clk LDS store path twice per round: 1.5x slower, tools/jacobi_lab.hip.)
+  __syncthreads();  // the QR transpose's last reads of xbuf are done
+#pragma unroll
+  for (int i = 0; i < MAXR; ++i) xbuf[g * ld + lane + 16 * i] = make_double2(mr[i], mi[i]);
+  if (lane == 0) xid[g] = mid;
+  __syncthreads();
   int sweeps = 0;
   for (sweeps = 0; sweeps < max_sweeps; ++sweeps) {
     if (tid == 0) rot = 0;
@@ -588,6 +629,13 @@ __global__ __launch_bounds__(CP * 8) void k_jacobi_reg(const TwoSiteJob* __restr
     for (int m = kG; m >= 1; m >>= 1) {  // level: sub-blocks of m groups
       const int li = g & (m - 1), base = g - li;
       for (int r = 0; r < m; ++r) {
+        double2* col = xbuf + (base + ((li + r) & (m - 1))) * ld;
+#pragma unroll
+        for (int i = 0; i < MAXR; ++i) {
+          const double2 v = col[lane + 16 * i];
+          mr[i] = v.x;
+          mi[i] = v.y;
+        }
         double al = 0, be = 0, gx = 0, gy = 0;
 #pragma unroll
         for (int i = 0; i < MAXR; ++i) {
@@ -606,59 +654,34 @@ __global__ __launch_bounds__(CP * 8) void k_jacobi_reg(const TwoSiteJob* __restr
           // only rotations above dot-product noise keep the sweep loop going: a pair of
           // (near-)degenerate columns can otherwise flip-flop at |g| ~ tol forever
           if (g2 > 16.0 * tol2 * ab) my_rot = 1;
-          const double gg = sqrt(g2);
-          const double zeta = (be - al) / (2.0 * gg);
-          const double t = (zeta >= 0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
-          const double c = 1.0 / sqrt(1.0 + t * t);
-          const double sc = c * t / gg;
-          const double ex = gx * sc, ey = gy * sc;  // s e  (s conj(e) = (ex, -ey))
+          double c, ex, ey;  // c and s e (s conj(e) = (ex, -ey))
+          jacobi_params(al, be, gx, gy, g2, c, ex, ey);
 #pragma unroll
           for (int i = 0; i < MAXR; ++i) {
             const double ar = sr[i], ai = si[i], br = mr[i], bi = mi[i];
             // a' = c a - s conj(e) b ; b' = s e a + c b
             sr[i] = fma(c, ar, -fma(ex, br, ey * bi));
             si[i] = fma(c, ai, -fma(ex, bi, -ey * br));
-            mr[i] = fma(c, br, fma(ex, ar, -ey * ai));
-            mi[i] = fma(c, bi, fma(ex, ai, ey * ar));
+            col[lane + 16 * i] = make_double2(fma(c, br, fma(ex, ar, -ey * ai)), fma(c, bi, fma(ex, ai, ey * ar)));
           }
         }
-        if (r == m - 1) break;
-        // shift M inside the sub-block: group li receives M of group (li + 1) % m
-#pragma unroll
-        for (int i = 0; i < MAXR; ++i) xbuf[g * ld + lane + 16 * i] = make_double2(mr[i], mi[i]);
-        if (lane == 0) xid[g] = mid;
-        __syncthreads();
-        const int src = base + ((li + 1) & (m - 1));
-#pragma unroll
-        for (int i = 0; i < MAXR; ++i) {
-          const double2 v = xbuf[src * ld + lane + 16 * i];
-          mr[i] = v.x;
-          mi[i] = v.y;
-        }
-        mid = xid[src];
         __syncthreads();
       }
       if (m == 1) break;
-      // split the sub-block: group li < m/2 swaps its M with the S of group li + m/2
       const int h = m >> 1;
-      const bool lowh = li < h;
+      if (li >= h) {  // upper half: S <-> slot g - h
+        double2* col = xbuf + (g - h) * ld;
 #pragma unroll
-      for (int i = 0; i < MAXR; ++i)
-        xbuf[g * ld + lane + 16 * i] = lowh ? make_double2(mr[i], mi[i]) : make_double2(sr[i], si[i]);
-      if (lane == 0) xid[g] = lowh ? mid : sid;
-      __syncthreads();
-      const int partner = lowh ? g + h : g - h;
-      const int pid = xid[partner];
-      mid = lowh ? pid : mid;
-      sid = lowh ? sid : pid;
-#pragma unroll
-      for (int i = 0; i < MAXR; ++i) {
-        const double2 v = xbuf[partner * ld + lane + 16 * i];
-        // low half: new M = S of the upper partner; high half: new S = M of the lower partner
-        mr[i] = lowh ? v.x : mr[i];
-        mi[i] = lowh ? v.y : mi[i];
-        sr[i] = lowh ? sr[i] : v.x;
-        si[i] = lowh ? si[i] : v.y;
+        for (int i = 0; i < MAXR; ++i) {
+          const double2 v = col[lane + 16 * i];
+          col[lane + 16 * i] = make_double2(sr[i], si[i]);
+          sr[i] = v.x;
+          si[i] = v.y;
+        }
+        const int pid = xid[g - h];
+        __builtin_amdgcn_wave_barrier();
+        if (lane == 0) xid[g - h] = sid;
+        sid = pid;
       }
       __syncthreads();
     }
@@ -668,25 +691,27 @@ __global__ __launch_bounds__(CP * 8) void k_jacobi_reg(const TwoSiteJob* __restr
     __syncthreads();
   }
   // write columns to their own slots (with QR: rows mapped back through the pivot order) and
-  // their norms
+  // their norms: S from VGPRs, slot g's column from LDS
   double2* W = j.work;
+  const int mid_out = xid[g];
   double ns = 0, nm = 0;
 #pragma unroll
   for (int i = 0; i < MAXR; ++i) {
     const int row = lane + 16 * i;
+    const double2 mv = xbuf[g * ld + row];
     if (row < Lj) {
       const int orow = map_rows ? perm_s[row] : row;
       if (sid < C) W[(size_t)sid * Lj + orow] = make_double2(sr[i], si[i]);
-      if (mid < C) W[(size_t)mid * Lj + orow] = make_double2(mr[i], mi[i]);
+      if (mid_out < C) W[(size_t)mid_out * Lj + orow] = mv;
     }
     ns = fma(sr[i], sr[i], fma(si[i], si[i], ns));
-    nm = fma(mr[i], mr[i], fma(mi[i], mi[i], nm));
+    nm = fma(mv.x, mv.x, fma(mv.y, mv.y, nm));
   }
   ns = aqc::row_sum16(ns);
   nm = aqc::row_sum16(nm);
   if (lane == 0) {
     if (sid < C) j.sig[sid] = sqrt(ns);
-    if (mid < C) j.sig[mid] = sqrt(nm);
+    if (mid_out < C) j.sig[mid_out] = sqrt(nm);
   }
   if (tid == 0) {
     if (sweeps >= kMaxSweeps) atomicOr(&j.flags[1], 1);

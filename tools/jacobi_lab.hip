@@ -107,7 +107,7 @@ __global__ __launch_bounds__(kThreads) void k_lab(const double2* __restrict__ A,
             gx += __shfl_xor(gx, off, 16);
             gy += __shfl_xor(gy, off, 16);
           }
-        } else {
+        } else {  // RED 1, 2
           al = dpp_sum16(al);
           be = dpp_sum16(be);
           gx = dpp_sum16(gx);
@@ -115,12 +115,37 @@ __global__ __launch_bounds__(kThreads) void k_lab(const double2* __restrict__ A,
         }
         const double g2 = gx * gx + gy * gy;
         if (g2 > tol2 * al * be && al > floor2 && be > floor2) {
-          const double gg = sqrt(g2);
-          const double zeta = (be - al) / (2.0 * gg);
-          const double t = (zeta >= 0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
-          const double c = 1.0 / sqrt(1.0 + t * t);
-          const double sc = c * t / gg;
-          const double ex = gx * sc, ey = gy * sc;
+          double c, ex, ey;
+          if constexpr (RED == 2) {
+            // rsq + Newton steps instead of IEEE sqrt / div sequences
+            double rg = __builtin_amdgcn_rsq(g2);            // ~1/|g|
+            rg = rg * fma(-0.5 * g2 * rg, rg, 1.5);
+            rg = rg * fma(-0.5 * g2 * rg, rg, 1.5);
+            const double zeta = 0.5 * (be - al) * rg;
+            const double q = fma(zeta, zeta, 1.0);
+            double rq = __builtin_amdgcn_rsq(q);
+            rq = rq * fma(-0.5 * q * rq, rq, 1.5);
+            rq = rq * fma(-0.5 * q * rq, rq, 1.5);
+            const double den = fabs(zeta) + q * rq;            // |zeta| + sqrt(1 + zeta^2)
+            double inv = __builtin_amdgcn_rcp(den);
+            inv = inv * fma(-den, inv, 2.0);
+            inv = inv * fma(-den, inv, 2.0);
+            const double t = zeta >= 0 ? inv : -inv;
+            const double p = fma(t, t, 1.0);
+            double cc = __builtin_amdgcn_rsq(p);
+            cc = cc * fma(-0.5 * p * cc, cc, 1.5);
+            cc = cc * fma(-0.5 * p * cc, cc, 1.5);
+            c = cc;
+            const double sc = cc * t * rg;
+            ex = gx * sc, ey = gy * sc;
+          } else {
+            const double gg = sqrt(g2);
+            const double zeta = (be - al) / (2.0 * gg);
+            const double t = (zeta >= 0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
+            c = 1.0 / sqrt(1.0 + t * t);
+            const double sc = c * t / gg;
+            ex = gx * sc, ey = gy * sc;
+          }
           if constexpr (ROT) {
 #pragma unroll
             for (int i = 0; i < MAXR; ++i) {
@@ -136,6 +161,16 @@ __global__ __launch_bounds__(kThreads) void k_lab(const double2* __restrict__ A,
           my_rot = 1;
         }
         if (r == m - 1) break;
+        if constexpr (XCH == 3) {
+#pragma unroll
+          for (int i = 0; i < MAXR; ++i) xbuf[g * ld + lane + 16 * i] = make_double2(mr[i], mi[i]);
+          const int src = base + ((li + 1) & (m - 1));
+#pragma unroll
+          for (int i = 0; i < MAXR; ++i) {
+            const double2 v = xbuf[src * ld + lane + 16 * i];
+            mr[i] = v.x, mi[i] = v.y;
+          }
+        }
         if constexpr (XCH == 0) {
 #pragma unroll
           for (int i = 0; i < MAXR; ++i) xbuf[g * ld + lane + 16 * i] = make_double2(mr[i], mi[i]);
@@ -510,6 +545,157 @@ __global__ __launch_bounds__(NW * 64) void k_bj(const double2* __restrict__ A, d
   if (tid == 0) sweeps_out[blockIdx.x] = sweeps + 1;
 }
 
+
+// ---- LDS-resident M variant: S columns in VGPRs, the M half in 64 LDS slots --------------------
+// Round r of a level with sub-blocks of m groups: group g (li = g - base) pairs S_g with slot
+// base + (li + r) mod m -- the "shift" is addressing only.  A slot is written back only when
+// its column was rotated (rare in late sweeps).  Level split: the upper half swaps its S with
+// slot g - h (that slot then holds an upper S for the lower half).  One barrier per round.
+template <int RED>
+__global__ __launch_bounds__(kThreads) void k_slot(const double2* __restrict__ A, double2* __restrict__ W,
+                                                  double* __restrict__ sig, int* __restrict__ sweeps_out,
+                                                  int fixed_sweeps) {
+  extern __shared__ double2 xbuf[];  // kG slots x ld
+  __shared__ double fred[kThreads / 64];
+  __shared__ int xid[kG];
+  __shared__ int rot;
+  const int L = CP, C = CP;
+  const double2* a = A + (size_t)blockIdx.x * L * C;
+  const int tid = threadIdx.x, g = tid >> 4, lane = tid & 15;
+  double sr[MAXR], si[MAXR];
+  int sid = g;
+  double f = 0;
+#pragma unroll
+  for (int i = 0; i < MAXR; ++i) {
+    const int r = lane + 16 * i;
+    const double2 x = a[(size_t)sid * L + r], y = a[(size_t)(g + kG) * L + r];
+    sr[i] = x.x, si[i] = x.y;
+    xbuf[g * ld + r] = y;
+    f += x.x * x.x + x.y * x.y + y.x * y.x + y.y * y.y;
+  }
+  if (lane == 0) xid[g] = g + kG;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) f += __shfl_xor(f, off);
+  if ((tid & 63) == 0) fred[tid >> 6] = f;
+  __syncthreads();
+  double fro = 0;
+  for (int w = 0; w < kThreads / 64; ++w) fro += fred[w];
+  const double floor2 = fro * 1e-24, tol = c_tolf * L * 2.220446049250313e-16, tol2 = tol * tol;
+  int sweeps;
+  for (sweeps = 0; sweeps < 40; ++sweeps) {
+    if (tid == 0) rot = 0;
+    __syncthreads();
+    int my_rot = 0;
+    for (int m = kG; m >= 1; m >>= 1) {
+      const int li = g & (m - 1), base = g - li;
+      for (int r = 0; r < m; ++r) {
+        const int slot = base + ((li + r) & (m - 1));
+        double2* col = xbuf + slot * ld;
+        double mr[MAXR], mi[MAXR];
+#pragma unroll
+        for (int i = 0; i < MAXR; ++i) {
+          const double2 v = col[lane + 16 * i];
+          mr[i] = v.x, mi[i] = v.y;
+        }
+        double al = 0, be = 0, gx = 0, gy = 0;
+#pragma unroll
+        for (int i = 0; i < MAXR; ++i) {
+          al = fma(sr[i], sr[i], fma(si[i], si[i], al));
+          be = fma(mr[i], mr[i], fma(mi[i], mi[i], be));
+          gx = fma(sr[i], mr[i], fma(si[i], mi[i], gx));
+          gy = fma(sr[i], mi[i], fma(-si[i], mr[i], gy));
+        }
+        al = dpp_sum16(al);
+        be = dpp_sum16(be);
+        gx = dpp_sum16(gx);
+        gy = dpp_sum16(gy);
+        const double g2 = gx * gx + gy * gy;
+        if (g2 > tol2 * al * be && al > floor2 && be > floor2) {
+          if (g2 > 16.0 * tol2 * al * be) my_rot = 1;
+          double c, ex, ey;
+          if constexpr (RED == 2) {
+            double rg = __builtin_amdgcn_rsq(g2);
+            rg = rg * fma(-0.5 * g2 * rg, rg, 1.5);
+            rg = rg * fma(-0.5 * g2 * rg, rg, 1.5);
+            const double zeta = 0.5 * (be - al) * rg;
+            const double q = fma(zeta, zeta, 1.0);
+            double rq = __builtin_amdgcn_rsq(q);
+            rq = rq * fma(-0.5 * q * rq, rq, 1.5);
+            rq = rq * fma(-0.5 * q * rq, rq, 1.5);
+            const double den = fabs(zeta) + q * rq;
+            double inv = __builtin_amdgcn_rcp(den);
+            inv = inv * fma(-den, inv, 2.0);
+            inv = inv * fma(-den, inv, 2.0);
+            const double t = zeta >= 0 ? inv : -inv;
+            const double p = fma(t, t, 1.0);
+            double cc = __builtin_amdgcn_rsq(p);
+            cc = cc * fma(-0.5 * p * cc, cc, 1.5);
+            cc = cc * fma(-0.5 * p * cc, cc, 1.5);
+            c = cc;
+            const double sc = cc * t * rg;
+            ex = gx * sc, ey = gy * sc;
+          } else {
+            const double gg = sqrt(g2);
+            const double zeta = (be - al) / (2.0 * gg);
+            const double t = (zeta >= 0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
+            c = 1.0 / sqrt(1.0 + t * t);
+            const double sc = c * t / gg;
+            ex = gx * sc, ey = gy * sc;
+          }
+#pragma unroll
+          for (int i = 0; i < MAXR; ++i) {
+            const double ar = sr[i], ai = si[i], br = mr[i], bi = mi[i];
+            sr[i] = fma(c, ar, -fma(ex, br, ey * bi));
+            si[i] = fma(c, ai, -fma(ex, bi, -ey * br));
+            col[lane + 16 * i] = make_double2(fma(c, br, fma(ex, ar, -ey * ai)), fma(c, bi, fma(ex, ai, ey * ar)));
+          }
+        }
+        __syncthreads();
+      }
+      if (m == 1) break;
+      const int h = m >> 1;
+      if (li >= h) {  // upper half: S <-> slot g - h
+        double2* col = xbuf + (g - h) * ld;
+#pragma unroll
+        for (int i = 0; i < MAXR; ++i) {
+          const double2 v = col[lane + 16 * i];
+          col[lane + 16 * i] = make_double2(sr[i], si[i]);
+          sr[i] = v.x, si[i] = v.y;
+        }
+        const int pid = xid[g - h];
+        __builtin_amdgcn_wave_barrier();
+        if (lane == 0) xid[g - h] = sid;
+        sid = pid;
+      }
+      __syncthreads();
+    }
+    if (my_rot && lane == 0) atomicAdd(&rot, 1);
+    __syncthreads();
+    const bool done = fixed_sweeps > 0 ? sweeps + 1 >= fixed_sweeps : rot == 0;
+    if (done) break;
+    __syncthreads();
+  }
+  double2* wo = W + (size_t)blockIdx.x * L * C;
+  const int mid = xid[g];
+  double ns = 0, nm = 0;
+#pragma unroll
+  for (int i = 0; i < MAXR; ++i) {
+    const int row = lane + 16 * i;
+    const double2 mv = xbuf[g * ld + row];
+    wo[(size_t)sid * L + row] = make_double2(sr[i], si[i]);
+    wo[(size_t)mid * L + row] = mv;
+    ns = fma(sr[i], sr[i], fma(si[i], si[i], ns));
+    nm = fma(mv.x, mv.x, fma(mv.y, mv.y, nm));
+  }
+  ns = dpp_sum16(ns);
+  nm = dpp_sum16(nm);
+  if (lane == 0) {
+    sig[blockIdx.x * C + sid] = sqrt(ns);
+    sig[blockIdx.x * C + mid] = sqrt(nm);
+  }
+  if (tid == 0) sweeps_out[blockIdx.x] = sweeps + 1;
+}
+
 struct Out {
   std::vector<double> sig;
   std::vector<double2> W;
@@ -586,6 +772,39 @@ static float run_bj(const char* name, const double2* dA, double2* dW, double* dS
   return best;
 }
 
+
+template <int RED>
+static float run_slot(const char* name, const double2* dA, double2* dW, double* dS, int* dSw, int B, int fixed, Out* o) {
+  auto k = k_slot<RED>;
+  const size_t lds = (size_t)kG * ld * 16;
+  CK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  hipLaunchKernelGGL(k, dim3(B), dim3(kThreads), lds, 0, dA, dW, dS, dSw, fixed);
+  CK(hipDeviceSynchronize());
+  float best = 1e30f;
+  for (int rep = 0; rep < 3; ++rep) {
+    CK(hipEventRecord(e0));
+    hipLaunchKernelGGL(k, dim3(B), dim3(kThreads), lds, 0, dA, dW, dS, dSw, fixed);
+    CK(hipEventRecord(e1));
+    CK(hipEventSynchronize(e1));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    best = std::min(best, ms);
+  }
+  o->sig.resize((size_t)B * CP);
+  o->sw.resize(B);
+  o->W.resize((size_t)B * CP * CP);
+  CK(hipMemcpy(o->sig.data(), dS, o->sig.size() * 8, hipMemcpyDeviceToHost));
+  CK(hipMemcpy(o->sw.data(), dSw, B * 4, hipMemcpyDeviceToHost));
+  CK(hipMemcpy(o->W.data(), dW, o->W.size() * 16, hipMemcpyDeviceToHost));
+  int swmax = *std::max_element(o->sw.begin(), o->sw.end());
+  printf("%-34s %8.3f ms  (%.3f CU-ms/SVD, sweeps max %d, %.2f us/round)\n", name, best, best * 256.0 / B, swmax,
+         1e3 * best / swmax / (CP - 1) / std::max(1, (B + 255) / 256));
+  return best;
+}
+
 // max relative difference of sorted singular values vs ref; max column non-orthogonality of block 0
 static void check(const Out& o, const Out& ref, int B) {
   double dmax = 0;
@@ -632,25 +851,15 @@ int main(int argc, char** argv) {
   CK(hipMemcpy(dA, h.data(), h.size() * 16, hipMemcpyHostToDevice));
   printf("blocks %d, fixed sweeps %d (0 = converge)\n", B, fixed);
   Out ref, o;
-  run<0, 0, true>("shfl + ring LDS (library)", dA, dW, dS, dSw, B, fixed, &ref);
-  run<1, 0, true>("dpp + ring LDS", dA, dW, dS, dSw, B, fixed, &o);
+  run<1, 0, true>("dpp + ring LDS (library)", dA, dW, dS, dSw, B, fixed, &ref);
+  run<2, 0, true>("dpp + fast params + ring LDS", dA, dW, dS, dSw, B, fixed, &o);
   check(o, ref, B);
-  run_bj<16, 2>("block: wave = 2x4 columns", dA, dW, dS, dSw, B, fixed, &o);
+  run_slot<1>("LDS-resident M slots", dA, dW, dS, dSw, B, fixed, &o);
   check(o, ref, B);
-  {
-    const double tf = 2.0;
-    CK(hipMemcpyToSymbol(HIP_SYMBOL(c_tolf), &tf, sizeof(double)));
-    run_bj<16, 2>("block, tol x2", dA, dW, dS, dSw, B, fixed, &o);
-    check(o, ref, B);
-    run<1, 0, true>("dpp + ring LDS, tol x2", dA, dW, dS, dSw, B, fixed, &o);
-    run_bj<16, 2, 1>("block, tol x2, permlane gather", dA, dW, dS, dSw, B, fixed, &o);
-    check(o, ref, B);
-    const double t1 = 1.0;
-    CK(hipMemcpyToSymbol(HIP_SYMBOL(c_tolf), &t1, sizeof(double)));
-  }
+  run_slot<2>("LDS-resident M + fast params", dA, dW, dS, dSw, B, fixed, &o);
+  check(o, ref, B);
   const int fs = fixed > 0 ? fixed : 14;
   run<1, 2, true>("dpp + no exchange [timing]", dA, dW, dS, dSw, B, fs, &o);
-  run<1, 1, false>("dpp + gray, no update [timing]", dA, dW, dS, dSw, B, fs, &o);
-  run<1, 2, false>("dpp only dots [timing]", dA, dW, dS, dSw, B, fs, &o);
+  run<2, 2, true>("dpp + fast params, no exch [timing]", dA, dW, dS, dSw, B, fs, &o);
   return 0;
 }
