@@ -474,7 +474,7 @@ __global__ __launch_bounds__(CP * 8) void k_jacobi_reg(const TwoSiteJob* __restr
   extern __shared__ double2 xbuf[];  // max(kG * ld, kG * ldt) complex
   __shared__ double fred[kThreads / 64];
   __shared__ int xid[kG];
-  __shared__ int rot;
+  __shared__ int rot, big;
   __shared__ unsigned long long pkey[2];
   __shared__ double2 vb[2][CP];
   __shared__ double2 tb[2];
@@ -621,11 +621,15 @@ __global__ __launch_bounds__(CP * 8) void k_jacobi_reg(const TwoSiteJob* __restr
   for (int i = 0; i < MAXR; ++i) xbuf[g * ld + lane + 16 * i] = make_double2(mr[i], mi[i]);
   if (lane == 0) xid[g] = mid;
   __syncthreads();
+  // Stop rule: a sweep whose counted rotations all had |t| < kTinyT leaves every cosine at
+  // O(t * cos) ~ 1e-16 after it (quadratic convergence), so the confirming sweep with no
+  // rotation at all is skipped.
+  constexpr double kTinyT = 1e-8;
   int sweeps = 0;
   for (sweeps = 0; sweeps < max_sweeps; ++sweeps) {
-    if (tid == 0) rot = 0;
+    if (tid == 0) rot = big = 0;
     __syncthreads();
-    int my_rot = 0;
+    int my_rot = 0, my_big = 0;
     for (int m = kG; m >= 1; m >>= 1) {  // level: sub-blocks of m groups
       const int li = g & (m - 1), base = g - li;
       for (int r = 0; r < m; ++r) {
@@ -653,9 +657,12 @@ __global__ __launch_bounds__(CP * 8) void k_jacobi_reg(const TwoSiteJob* __restr
         if (g2 > tol2 * ab && al > floor2 && be > floor2) {
           // only rotations above dot-product noise keep the sweep loop going: a pair of
           // (near-)degenerate columns can otherwise flip-flop at |g| ~ tol forever
-          if (g2 > 16.0 * tol2 * ab) my_rot = 1;
           double c, ex, ey;  // c and s e (s conj(e) = (ex, -ey))
           jacobi_params(al, be, gx, gy, g2, c, ex, ey);
+          if (g2 > 16.0 * tol2 * ab) {
+            my_rot = 1;
+            if (ex * ex + ey * ey > kTinyT * kTinyT * c * c) my_big = 1;  // |t| = |s| / c
+          }
 #pragma unroll
           for (int i = 0; i < MAXR; ++i) {
             const double ar = sr[i], ai = si[i], br = mr[i], bi = mi[i];
@@ -686,8 +693,9 @@ __global__ __launch_bounds__(CP * 8) void k_jacobi_reg(const TwoSiteJob* __restr
       __syncthreads();
     }
     if (my_rot && lane == 0) atomicAdd(&rot, 1);
+    if (my_big && lane == 0) atomicAdd(&big, 1);
     __syncthreads();
-    if (rot == 0) break;
+    if (rot == 0 || big == 0) break;
     __syncthreads();
   }
   // write columns to their own slots (with QR: rows mapped back through the pivot order) and
