@@ -18,7 +18,9 @@ struct GemmLds {
   cplx Bs[16][65];
 };
 
-template <typename FA, typename FB, typename FS>
+// A_KFAST / B_KFAST choose the tile-load order: consecutive threads walk k (use when the source
+// is contiguous along k) instead of the output dimension.
+template <bool A_KFAST = false, bool B_KFAST = false, typename FA, typename FB, typename FS>
 __device__ __forceinline__ void block_cgemm(int m, int n, int k, FA a, FB b, FS store, GemmLds& lds) {
   const int tid = threadIdx.x, ty = tid >> 4, tx = tid & 15;
   for (int bi = 0; bi < m; bi += 64) {
@@ -32,9 +34,10 @@ __device__ __forceinline__ void block_cgemm(int m, int n, int k, FA a, FB b, FS 
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int e = tid + q * kGemmThreads;
-          const int kk = e >> 6, ii = e & 63;
-          lds.As[kk][ii] = (bi + ii < m && k0 + kk < k) ? a(bi + ii, k0 + kk) : cmk(0, 0);
-          lds.Bs[kk][ii] = (bj + ii < n && k0 + kk < k) ? b(k0 + kk, bj + ii) : cmk(0, 0);
+          const int ka = A_KFAST ? (e & 15) : (e >> 6), ia = A_KFAST ? (e >> 4) : (e & 63);
+          const int kb = B_KFAST ? (e & 15) : (e >> 6), ib = B_KFAST ? (e >> 4) : (e & 63);
+          lds.As[ka][ia] = (bi + ia < m && k0 + ka < k) ? a(bi + ia, k0 + ka) : cmk(0, 0);
+          lds.Bs[kb][ib] = (bj + ib < n && k0 + kb < k) ? b(k0 + kb, bj + ib) : cmk(0, 0);
         }
         __syncthreads();
 #pragma unroll 4

@@ -16,6 +16,7 @@
 #include <cstring>
 #include <mutex>
 
+#include "aqc_gemm.h"
 #include "mps_internal.h"
 
 using aqc::cplx;
@@ -831,67 +832,49 @@ __global__ __launch_bounds__(kT) void k_split_copy(const TwoSiteJob* __restrict_
   }
 }
 
-// Other side by one GEMM against the original theta:
+// Other side by one GEMM against the original theta (64 x 64 output blocks per workgroup,
+// register-blocked, aqc_gemm.h):
 //   !tr: Vh[kk][c] = sum_R conj(W_j[R]) theta[R][c] / sig^2 -> Gq'[s2][kk][r] = Vh / lr[r]
 //    tr: U[R][kk]  = sum_c theta[R][c] W_j[c] / sig^2      -> Gp'[s1][l][kk] = U / ll[l]
-__global__ __launch_bounds__(kT) void k_split_gemm(const TwoSiteJob* __restrict__ jobs) {
+// (tr: W's columns are V-side; the QR-preconditioned Jacobi flips the side, see k_split_copy.)
+__global__ __launch_bounds__(aqc::kGemmThreads) void k_split_gemm(const TwoSiteJob* __restrict__ jobs) {
   const TwoSiteJob& j = jobs[blockIdx.y];
+  __shared__ aqc::GemmLds lds;
   const int chl = j.dims[0], k = j.dims[1], chr = j.dims[2];
   const int M = 2 * chl, N = 2 * chr;
-  const bool tr = (M < N) != (j.qr != 0);  // as in k_split_copy
+  const bool tr = (M < N) != (j.qr != 0);
   const int L = tr ? N : M;
   const int cap = j.cap;
   const size_t half = (size_t)cap * cap;
   const double* ss = j.sig + 512;
-  // output tile: rows = kk (16), cols = c (16) for !tr ; rows = R (16), cols = kk (16) for tr
   const int rows = tr ? M : k, cols = tr ? k : N;
-  const int tiles_c = (2 * cap + 15) / 16;
-  const int r0 = (blockIdx.x / tiles_c) * 16, c0 = (blockIdx.x % tiles_c) * 16;
+  const int bcols = (2 * cap + 63) / 64;
+  const int r0 = (blockIdx.x / bcols) * 64, c0 = (blockIdx.x % bcols) * 64;
   if (r0 >= rows || c0 >= cols) return;
-  __shared__ cplx As[16][17];
-  __shared__ cplx Bs[16][17];
-  const int ty = threadIdx.x / 16, tx = threadIdx.x % 16;
-  const int ro = r0 + ty, co = c0 + tx;
-  cplx acc = aqc::cmk(0, 0);
-  const int K = L;  // inner dimension: M for !tr, N for tr
-  for (int k0 = 0; k0 < K; k0 += 16) {
-    // As[row][kin], Bs[kin][col]; consecutive lanes (tx) always walk the contiguous dimension
-    // of the source (W columns, column-major theta), transposing through the padded tiles
-    {
-      cplx a = aqc::cmk(0, 0), b = aqc::cmk(0, 0);
-      if (!tr) {
-        const int ar = r0 + ty, ak = k0 + tx;  // conj(W_j[R]): contiguous in R
-        if (ar < rows && ak < K) a = aqc::cconj(j.work[(size_t)j.perm[ar] * L + ak]);
-        As[ty][tx] = a;
-        const int bk = k0 + tx, bc = c0 + ty;  // theta[R][c]: contiguous in R
-        if (bk < K && bc < cols) b = j.theta[(size_t)bc * M + bk];
-        Bs[tx][ty] = b;
-      } else {
-        const int ar = r0 + tx, ak = k0 + ty;  // theta[R][c]: contiguous in R
-        if (ar < rows && ak < K) a = j.theta[(size_t)ak * M + ar];
-        As[tx][ty] = a;
-        const int bk = k0 + tx, bc = c0 + ty;  // W_j[c]: contiguous in c
-        if (bk < K && bc < cols) b = j.work[(size_t)j.perm[bc] * L + bk];
-        Bs[tx][ty] = b;
-      }
-    }
-    __syncthreads();
-#pragma unroll 8
-    for (int kk = 0; kk < 16; ++kk) acc = aqc::cfma(As[ty][kk], Bs[kk][tx], acc);
-    __syncthreads();
-  }
-  if (ro < rows && co < cols) {
-    if (!tr) {
-      const int kk = ro, cc = co;
-      const int s2 = cc / chr, r = cc % chr;
-      const double d = ss[kk] * ss[kk] * j.lr[r];
-      j.gq[s2 * half + (size_t)kk * cap + r] = d != 0.0 ? aqc::cscale(acc, 1.0 / d) : aqc::cmk(0, 0);
-    } else {
-      const int R = ro, kk = co;
-      const int s1 = R / chl, l = R % chl;
-      const double d = ss[kk] * ss[kk] * j.ll[l];
-      j.gp[s1 * half + (size_t)l * cap + kk] = d != 0.0 ? aqc::cscale(acc, 1.0 / d) : aqc::cmk(0, 0);
-    }
+  const int mb = min(64, rows - r0), nb = min(64, cols - c0);
+  const cplx* W = j.work;
+  const int* perm = j.perm;
+  const cplx* th = j.theta;
+  if (!tr) {
+    aqc::block_cgemm<true, true>(
+        mb, nb, L, [&](int kk, int R) { return aqc::cconj(W[(size_t)perm[r0 + kk] * L + R]); },
+        [&](int R, int c) { return th[(size_t)(c0 + c) * M + R]; },
+        [&](int kk, int c, cplx v) {
+          const int kq = r0 + kk, cc = c0 + c, s2 = cc / chr, r = cc % chr;
+          const double d = ss[kq] * ss[kq] * j.lr[r];
+          j.gq[s2 * half + (size_t)kq * cap + r] = d != 0.0 ? aqc::cscale(v, 1.0 / d) : aqc::cmk(0, 0);
+        },
+        lds);
+  } else {
+    aqc::block_cgemm<false, true>(
+        mb, nb, L, [&](int R, int c) { return th[(size_t)c * M + r0 + R]; },
+        [&](int c, int kk) { return W[(size_t)perm[c0 + kk] * L + c]; },
+        [&](int R, int kk, cplx v) {
+          const int Rr = r0 + R, kq = c0 + kk, s1 = Rr / chl, l = Rr % chl;
+          const double d = ss[kq] * ss[kq] * j.ll[l];
+          j.gp[s1 * half + (size_t)l * cap + kq] = d != 0.0 ? aqc::cscale(v, 1.0 / d) : aqc::cmk(0, 0);
+        },
+        lds);
   }
 }
 
@@ -1363,7 +1346,7 @@ int run_waves(aqc_mps_t* hs, int ns, std::vector<std::vector<DevOp>>& lists) {
   const TwoSiteJob* dtwo = (const TwoSiteJob*)sg.dev;
   const OneSiteJob* done = (const OneSiteJob*)((char*)sg.dev + tb);
   const int tiles = ((cap_max + 15) / 16) * ((cap_max + 15) / 16);
-  const int tiles_split = ((2 * cap_max + 15) / 16) * ((2 * cap_max + 15) / 16);
+  const int blocks_split = ((2 * cap_max + 63) / 64) * ((2 * cap_max + 63) / 64);
   for (size_t w = 0; w < maxlen; ++w) {
     if (one_rng[w].second) {
       const int nj = (int)one_rng[w].second;
@@ -1410,7 +1393,7 @@ int run_waves(aqc_mps_t* hs, int ns, std::vector<std::vector<DevOp>>& lists) {
       hipLaunchKernelGGL(k_split_copy, dim3(std::max(1, (4 * cap_max * cap_max + kT - 1) / kT), nj), dim3(kT), 0, st, jp);
       AQC_CHECK_LAUNCH();
       aqc::KernelTimer::begin(st, "mps_split", 0.0, nj * 2.0 * c * c * 2.0 * c * 8);
-      hipLaunchKernelGGL(k_split_gemm, dim3(tiles_split, nj), dim3(kT), 0, st, jp);
+      hipLaunchKernelGGL(k_split_gemm, dim3(blocks_split, nj), dim3(aqc::kGemmThreads), 0, st, jp);
       aqc::KernelTimer::end(st);
       AQC_CHECK_LAUNCH();
     }
