@@ -1,0 +1,352 @@
+// Multi-workgroup block one-sided Jacobi SVD for the large two-site updates (2 chi > 128:
+// chi = 128 and the 100-qubit chi = 256 MPS preparation of BASELINE config 5).
+//
+// The single-workgroup kernels of mps.hip keep a whole 2chi x 2chi theta in one CU (VGPRs for
+// chi <= 64).  A 512 x 512 complex theta is 4 MB: it lives in HBM / L2 here, and the cyclic
+// one-sided Jacobi is spread over many CUs by column blocks (Hestenes block-Jacobi):
+//   * W (L rows x C columns, column-major, ld = L) is cut into nb blocks of kB = 16 columns;
+//   * one sweep = one "intra" launch (every block orthogonalises its own 16 columns, one
+//     workgroup per block, round-robin in LDS) + nb - 1 "cross" launches (round-robin tournament
+//     over the blocks: nb / 2 workgroups, each rotating every column of block I against every
+//     column of block J);
+//   * a cross visit keeps block I's 16 columns in VGPRs (one wave per column, lane l holds rows
+//     l + 64 i) and block J's 16 columns in LDS (128 KB at L = 512); round r pairs wave g with LDS
+//     slot (g + r) mod 16, so each round is a perfect matching and only the J half crosses LDS;
+//   * launch boundaries are the only inter-workgroup synchronisation (no grid barrier, no
+//     cross-XCD coherence assumptions).
+// Rotation rule, thresholds and stop test are those of k_jacobi_reg (mps.hip): relative
+// threshold L eps, squared-norm floor ||W||^2 1e-24, a sweep without rotations above 4x the
+// threshold -- or with only |t| < 1e-8 ones -- is the last.  Output: W's columns = U sigma,
+// sig = their norms (the k_jacobi contract consumed by k_rank / k_split_*, qr = 0).
+#include "mps_internal.h"
+
+namespace aqc {
+namespace {
+
+constexpr int kB = 16;        // columns per block
+constexpr int kMaxSweepsBJ = 40;
+constexpr double kTinyT = 1e-8;
+
+struct BJState {
+  double fro;   // ||W||_F^2
+  int rot;      // rotations above noise in this sweep
+  int big;      // rotations with |t| >= kTinyT in this sweep
+  int done;     // converged (later launches return at once)
+  int sweeps;   // sweeps run
+  int pad[2];
+};
+
+// Sum over the 64 lanes of a wave, result in every lane: DPP row sums, then rows 0..3 combined
+// through row_bcast15 / row_bcast31 into lane 63 and read back as a wave-uniform value.
+__device__ __forceinline__ double wave_sum(double v) {
+  v = row_sum16(v);
+  v += __builtin_amdgcn_update_dpp(0.0, v, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
+  v += __builtin_amdgcn_update_dpp(0.0, v, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), 63);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), 63);
+  return __hiloint2double(hi, lo);
+}
+
+__device__ __forceinline__ void job_shape(const TwoSiteJob& j, int& L, int& C, bool& tr) {
+  const int M = 2 * j.dims[0], N = 2 * j.dims[2];
+  tr = M < N;
+  L = tr ? N : M;
+  C = tr ? M : N;
+}
+
+// round-robin tournament on c (even) players: position 0 fixed, the others rotate
+__device__ __forceinline__ int rr(int pos, int r, int c) { return pos == 0 ? 0 : ((pos - 1 + r) % (c - 1)) + 1; }
+
+// W <- theta (or theta^H when M < N), ||W||_F^2 into st.fro.  grid (chunks, nj).
+__global__ __launch_bounds__(256) void k_bj_init(const TwoSiteJob* __restrict__ jobs, BJState* __restrict__ st) {
+  const TwoSiteJob& j = jobs[blockIdx.y];
+  int L, C;
+  bool tr;
+  job_shape(j, L, C, tr);
+  const int M = 2 * j.dims[0];
+  double f = 0.0;
+  for (int idx = blockIdx.x * 256 + threadIdx.x; idx < L * C; idx += gridDim.x * 256) {
+    const int col = idx / L, row = idx - col * L;
+    const cplx v = tr ? cconj(j.theta[(size_t)row * M + col]) : j.theta[(size_t)col * M + row];
+    j.work[idx] = v;
+    f = fma(v.x, v.x, fma(v.y, v.y, f));
+  }
+  __shared__ double red[4];
+  f = wave_sum(f);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = f;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(&st[blockIdx.y].fro, red[0] + red[1] + red[2] + red[3]);
+}
+
+// One pair rotation of columns (a: sr/si, b: mr/mi) -- MAXR rows per lane, 64 lanes.  Returns
+// whether the pair was rotated; rot / big collect the stop-test flags.
+template <int MAXR>
+__device__ __forceinline__ bool rotate_pair(double (&sr)[MAXR], double (&si)[MAXR], double (&mr)[MAXR],
+                                            double (&mi)[MAXR], double tol2, double floor2, int& rot, int& big) {
+  double al = 0, be = 0, gx = 0, gy = 0;
+#pragma unroll
+  for (int i = 0; i < MAXR; ++i) {
+    al = fma(sr[i], sr[i], fma(si[i], si[i], al));
+    be = fma(mr[i], mr[i], fma(mi[i], mi[i], be));
+    gx = fma(sr[i], mr[i], fma(si[i], mi[i], gx));  // conj(a) * b
+    gy = fma(sr[i], mi[i], fma(-si[i], mr[i], gy));
+  }
+  al = wave_sum(al);
+  be = wave_sum(be);
+  gx = wave_sum(gx);
+  gy = wave_sum(gy);
+  const double g2 = gx * gx + gy * gy;
+  const double ab = al * be;
+  if (!(g2 > tol2 * ab && al > floor2 && be > floor2)) return false;
+  double c, ex, ey;
+  jacobi_params(al, be, gx, gy, g2, c, ex, ey);
+  if (g2 > 16.0 * tol2 * ab) {
+    rot = 1;
+    if (ex * ex + ey * ey > kTinyT * kTinyT * c * c) big = 1;
+  }
+#pragma unroll
+  for (int i = 0; i < MAXR; ++i) {
+    const double ar = sr[i], ai = si[i], br = mr[i], bi = mi[i];
+    // a' = c a - s conj(e) b ; b' = s e a + c b
+    sr[i] = fma(c, ar, -fma(ex, br, ey * bi));
+    si[i] = fma(c, ai, -fma(ex, bi, -ey * br));
+    mr[i] = fma(c, br, fma(ex, ar, -ey * ai));
+    mi[i] = fma(c, bi, fma(ex, ai, ey * ar));
+  }
+  return true;
+}
+
+__device__ __forceinline__ double tol_sq(const TwoSiteJob& j, int L) {
+  const double tol = j.jtol * (double)L * 2.220446049250313e-16;
+  return tol * tol;
+}
+
+// Intra-block visits: one workgroup (8 waves) per block; the block's 16 columns in LDS, 15
+// round-robin rounds of 8 pairs.  grid (nb, nj).
+template <int MAXR>
+__global__ __launch_bounds__(512) void k_bj_intra(const TwoSiteJob* __restrict__ jobs, BJState* __restrict__ st) {
+  BJState& s = st[blockIdx.y];
+  if (s.done) return;
+  const TwoSiteJob& j = jobs[blockIdx.y];
+  int L, C;
+  bool tr;
+  job_shape(j, L, C, tr);
+  const int c0 = blockIdx.x * kB;
+  if (c0 >= C) return;
+  const int nc = min(kB, C - c0);
+  extern __shared__ double2 cols[];  // kB x (64 MAXR)
+  constexpr int ldl = 64 * MAXR;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  cplx* W = j.work + (size_t)c0 * L;
+  for (int k = w; k < kB; k += 8) {
+#pragma unroll
+    for (int i = 0; i < MAXR; ++i) {
+      const int row = lane + 64 * i;
+      cols[k * ldl + row] = (k < nc && row < L) ? W[(size_t)k * L + row] : make_double2(0, 0);
+    }
+  }
+  __syncthreads();
+  const double tol2 = tol_sq(j, L), floor2 = s.fro * 1e-24;
+  int rot = 0, big = 0;
+  for (int r = 0; r < kB - 1; ++r) {
+    const int a = rr(w, r, kB), b = rr(kB - 1 - w, r, kB);
+    double sr[MAXR], si[MAXR], mr[MAXR], mi[MAXR];
+#pragma unroll
+    for (int i = 0; i < MAXR; ++i) {
+      const double2 x = cols[a * ldl + lane + 64 * i], y = cols[b * ldl + lane + 64 * i];
+      sr[i] = x.x, si[i] = x.y, mr[i] = y.x, mi[i] = y.y;
+    }
+    if (rotate_pair<MAXR>(sr, si, mr, mi, tol2, floor2, rot, big)) {
+#pragma unroll
+      for (int i = 0; i < MAXR; ++i) {
+        cols[a * ldl + lane + 64 * i] = make_double2(sr[i], si[i]);
+        cols[b * ldl + lane + 64 * i] = make_double2(mr[i], mi[i]);
+      }
+    }
+    __syncthreads();
+  }
+  for (int k = w; k < nc; k += 8) {
+#pragma unroll
+    for (int i = 0; i < MAXR; ++i) {
+      const int row = lane + 64 * i;
+      if (row < L) W[(size_t)k * L + row] = cols[k * ldl + row];
+    }
+  }
+  if (lane == 0 && rot) atomicOr(&s.rot, 1);
+  if (lane == 0 && big) atomicOr(&s.big, 1);
+}
+
+// Cross visits of tournament round `round` over nb blocks: workgroup p rotates every column of
+// block I = rr(p) (VGPRs, one wave per column) against every column of block J = rr(nb-1-p) (LDS).
+// grid (nb / 2, nj), 16 waves.
+template <int MAXR>
+__global__ __launch_bounds__(1024) void k_bj_cross(const TwoSiteJob* __restrict__ jobs, BJState* __restrict__ st,
+                                                   int round, int nb) {
+  BJState& s = st[blockIdx.y];
+  if (s.done) return;
+  const TwoSiteJob& j = jobs[blockIdx.y];
+  int L, C;
+  bool tr;
+  job_shape(j, L, C, tr);
+  const int I = rr(blockIdx.x, round, nb), J = rr(nb - 1 - blockIdx.x, round, nb);
+  const int cI = I * kB, cJ = J * kB;
+  if (cI >= C || cJ >= C) return;
+  const int nI = min(kB, C - cI), nJ = min(kB, C - cJ);
+  extern __shared__ double2 cols[];  // kB x (64 MAXR): block J
+  constexpr int ldl = 64 * MAXR;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  cplx* WI = j.work + (size_t)cI * L;
+  cplx* WJ = j.work + (size_t)cJ * L;
+  double sr[MAXR], si[MAXR], mr[MAXR], mi[MAXR];
+#pragma unroll
+  for (int i = 0; i < MAXR; ++i) {
+    const int row = lane + 64 * i;
+    const bool ok = row < L;
+    const double2 a = (ok && w < nI) ? WI[(size_t)w * L + row] : make_double2(0, 0);
+    const double2 b = (ok && w < nJ) ? WJ[(size_t)w * L + row] : make_double2(0, 0);
+    sr[i] = a.x, si[i] = a.y;
+    cols[w * ldl + row] = b;
+  }
+  __syncthreads();
+  const double tol2 = tol_sq(j, L), floor2 = s.fro * 1e-24;
+  int rot = 0, big = 0;
+  for (int r = 0; r < kB; ++r) {
+    double2* col = cols + ((w + r) & (kB - 1)) * ldl;
+#pragma unroll
+    for (int i = 0; i < MAXR; ++i) {
+      const double2 v = col[lane + 64 * i];
+      mr[i] = v.x, mi[i] = v.y;
+    }
+    if (rotate_pair<MAXR>(sr, si, mr, mi, tol2, floor2, rot, big)) {
+#pragma unroll
+      for (int i = 0; i < MAXR; ++i) col[lane + 64 * i] = make_double2(mr[i], mi[i]);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < MAXR; ++i) {
+    const int row = lane + 64 * i;
+    if (row < L) {
+      if (w < nI) WI[(size_t)w * L + row] = make_double2(sr[i], si[i]);
+      if (w < nJ) WJ[(size_t)w * L + row] = cols[w * ldl + row];
+    }
+  }
+  if (lane == 0 && rot) atomicOr(&s.rot, 1);
+  if (lane == 0 && big) atomicOr(&s.big, 1);
+}
+
+// End of sweep: decide convergence, reset the sweep flags, count converged jobs.  grid (nj).
+__global__ void k_bj_sweep_end(BJState* __restrict__ st, int* __restrict__ ndone) {
+  if (threadIdx.x != 0) return;
+  BJState& s = st[blockIdx.x];
+  if (s.done) return;
+  s.sweeps += 1;
+  if (s.rot == 0 || s.big == 0 || s.sweeps >= kMaxSweepsBJ) {
+    s.done = 1;
+    atomicAdd(ndone, 1);
+  }
+  s.rot = 0;
+  s.big = 0;
+}
+
+// sig = column norms (one wave per column), flags.  grid (ceil(C / 16), nj), 16 waves.
+template <int MAXR>
+__global__ __launch_bounds__(1024) void k_bj_final(const TwoSiteJob* __restrict__ jobs, const BJState* __restrict__ st) {
+  const TwoSiteJob& j = jobs[blockIdx.y];
+  const BJState& s = st[blockIdx.y];
+  int L, C;
+  bool tr;
+  job_shape(j, L, C, tr);
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int col = blockIdx.x * kB + w;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (s.sweeps >= kMaxSweepsBJ) atomicOr(&j.flags[1], 1);
+    atomicMax(&j.flags[2], s.sweeps);
+  }
+  if (col >= C) return;
+  double n2 = 0;
+#pragma unroll
+  for (int i = 0; i < MAXR; ++i) {
+    const int row = lane + 64 * i;
+    if (row < L) {
+      const double2 v = j.work[(size_t)col * L + row];
+      n2 = fma(v.x, v.x, fma(v.y, v.y, n2));
+    }
+  }
+  n2 = wave_sum(n2);
+  if (lane == 0) j.sig[col] = sqrt(n2);
+}
+
+struct BJBuffers {
+  BJState* st = nullptr;
+  int* ndone = nullptr;  // device counter
+  int* host = nullptr;   // pinned read-back
+  int cap = 0;
+};
+
+BJBuffers& bj_buffers() {
+  static BJBuffers b;
+  return b;
+}
+
+template <int MAXR>
+int run_block_jacobi(const TwoSiteJob* jobs, int nj, int cap_max, hipStream_t stream) {
+  BJBuffers& b = bj_buffers();
+  if (b.cap < nj) {
+    AQC_HIP_CHECK(hipStreamSynchronize(stream));
+    if (b.st) hipFree(b.st);
+    if (b.ndone) hipFree(b.ndone);
+    if (b.host) hipHostFree(b.host);
+    b.st = nullptr, b.ndone = nullptr, b.host = nullptr, b.cap = 0;
+    AQC_HIP_CHECK(hipMalloc(&b.st, sizeof(BJState) * nj));
+    AQC_HIP_CHECK(hipMalloc(&b.ndone, sizeof(int)));
+    AQC_HIP_CHECK(hipHostMalloc(&b.host, sizeof(int)));
+    b.cap = nj;
+  }
+  AQC_HIP_CHECK(hipMemsetAsync(b.st, 0, sizeof(BJState) * nj, stream));
+  AQC_HIP_CHECK(hipMemsetAsync(b.ndone, 0, sizeof(int), stream));
+  const int L = 2 * cap_max;
+  int nb = (L + kB - 1) / kB;
+  nb += nb & 1;
+  const size_t lds = (size_t)kB * 64 * MAXR * sizeof(double2);
+  const int chunks = std::max(1, std::min(1024, L * L / 1024));
+  hipLaunchKernelGGL(k_bj_init, dim3(chunks, nj), dim3(256), 0, stream, jobs, b.st);
+  AQC_CHECK_LAUNCH();
+  for (int sweep = 0; sweep < kMaxSweepsBJ; ++sweep) {
+    hipLaunchKernelGGL((k_bj_intra<MAXR>), dim3(nb, nj), dim3(512), lds, stream, jobs, b.st);
+    AQC_CHECK_LAUNCH();
+    for (int r = 0; r < nb - 1; ++r) {
+      hipLaunchKernelGGL((k_bj_cross<MAXR>), dim3(nb / 2, nj), dim3(1024), lds, stream, jobs, b.st, r, nb);
+      AQC_CHECK_LAUNCH();
+    }
+    hipLaunchKernelGGL(k_bj_sweep_end, dim3(nj), dim3(64), 0, stream, b.st, b.ndone);
+    AQC_CHECK_LAUNCH();
+    if (sweep >= 2) {
+      AQC_HIP_CHECK(hipMemcpyAsync(b.host, b.ndone, sizeof(int), hipMemcpyDeviceToHost, stream));
+      AQC_HIP_CHECK(hipStreamSynchronize(stream));
+      if (*b.host >= nj) break;
+    }
+  }
+  hipLaunchKernelGGL((k_bj_final<MAXR>), dim3(nb, nj), dim3(1024), 0, stream, jobs, b.st);
+  AQC_CHECK_LAUNCH();
+  return AQC_OK;
+}
+
+}  // namespace
+
+int block_jacobi(const TwoSiteJob* jobs, int nj, int cap_max, hipStream_t st) {
+  static bool attr = false;
+  if (!attr) {
+    // 128 KB of dynamic LDS (block J's 16 columns of 512 rows)
+    AQC_HIP_CHECK(hipFuncSetAttribute((const void*)k_bj_intra<8>, hipFuncAttributeMaxDynamicSharedMemorySize, 131072));
+    AQC_HIP_CHECK(hipFuncSetAttribute((const void*)k_bj_cross<8>, hipFuncAttributeMaxDynamicSharedMemorySize, 131072));
+    AQC_HIP_CHECK(hipFuncSetAttribute((const void*)k_bj_intra<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 65536));
+    AQC_HIP_CHECK(hipFuncSetAttribute((const void*)k_bj_cross<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 65536));
+    attr = true;
+  }
+  AQC_REQUIRE(2 * cap_max <= 512, "block Jacobi supports 2 * chi_cap <= 512");
+  if (2 * cap_max <= 256) return run_block_jacobi<4>(jobs, nj, cap_max, st);
+  return run_block_jacobi<8>(jobs, nj, cap_max, st);
+}
+
+}  // namespace aqc

@@ -52,26 +52,7 @@ struct OneSiteJob {
   cplx u[4];
 };
 
-struct TwoSiteJob {
-  cplx* gp;
-  cplx* gq;
-  const double* ll;
-  double* lm;
-  const double* lr;
-  int* dims;  // &dims[p] : dims[0] = chi_l, dims[1] = chi_m, dims[2] = chi_r
-  cplx* theta;
-  cplx* work;
-  double* sig;
-  int* perm;
-  int* flags;
-  int cap;
-  int max_chi;
-  double thr;
-  double jtol;  // Jacobi rotation threshold factor
-  int qr;       // 1: Jacobi ran on R^H of a pivoted QR -> W holds the other side (see k_jacobi_reg)
-  int dbg;      // diagnostics (aqc_svd_debug): 1 = stop after the QR phase, write X unpermuted
-  cplx G[16];  // row = 2*s1'+s2' (out), col = 2*s1+s2 (in)
-};
+using aqc::TwoSiteJob;
 
 // ------------------------------------------------------------------------------------------
 __global__ void k_mps_zero(cplx* gam, double* lam, int* dims, int n, int cap) {
@@ -388,34 +369,7 @@ __global__ __launch_bounds__(JT) void k_jacobi(const TwoSiteJob* __restrict__ jo
 // the *other* side times sigma (rows mapped back through the pivot order P), which k_split
 // handles by flipping its side test (tools/qrp_jacobi_proto.py is the numpy restatement).
 
-// Rotation parameters of the pair (alpha, beta, gamma = gx + i gy): t = sgn(zeta) /
-// (|zeta| + sqrt(1 + zeta^2)), zeta = (beta - alpha) / (2|gamma|), c = 1/sqrt(1 + t^2) and
-// s e = c t gamma / |gamma|.  v_rsq_f64 / v_rcp_f64 seeds with two Newton steps each (full double
-// precision) instead of the IEEE sqrt / divide sequences: this chain is serial per round.
-__device__ __forceinline__ void jacobi_params(double al, double be, double gx, double gy, double g2, double& c,
-                                              double& ex, double& ey) {
-  double rg = __builtin_amdgcn_rsq(g2);  // 1 / |gamma|
-  rg = rg * fma(-0.5 * g2 * rg, rg, 1.5);
-  rg = rg * fma(-0.5 * g2 * rg, rg, 1.5);
-  const double zeta = 0.5 * (be - al) * rg;
-  const double q = fma(zeta, zeta, 1.0);
-  double rq = __builtin_amdgcn_rsq(q);
-  rq = rq * fma(-0.5 * q * rq, rq, 1.5);
-  rq = rq * fma(-0.5 * q * rq, rq, 1.5);
-  const double den = fabs(zeta) + q * rq;  // |zeta| + sqrt(1 + zeta^2)
-  double inv = __builtin_amdgcn_rcp(den);
-  inv = inv * fma(-den, inv, 2.0);
-  inv = inv * fma(-den, inv, 2.0);
-  const double t = zeta >= 0 ? inv : -inv;
-  const double p = fma(t, t, 1.0);
-  double cc = __builtin_amdgcn_rsq(p);
-  cc = cc * fma(-0.5 * p * cc, cc, 1.5);
-  cc = cc * fma(-0.5 * p * cc, cc, 1.5);
-  c = cc;
-  const double sc = cc * t * rg;
-  ex = gx * sc;
-  ey = gy * sc;
-}
+using aqc::jacobi_params;
 
 // sortable pivot key: non-negative double bits with the low byte replaced by (255 - id), so
 // that the 64-bit maximum is the largest trailing norm, ties to the lowest column id
@@ -1381,10 +1335,13 @@ int run_waves(aqc_mps_t* hs, int ns, std::vector<std::vector<DevOp>>& lists) {
       } else if (2 * cap_max <= 128) {
         if (half) hipLaunchKernelGGL((k_jacobi<16, 8, 256, 4096>), dim3(nj), dim3(256), 0, st, jp);
         else hipLaunchKernelGGL((k_jacobi<16, 8, 512, 8192>), dim3(nj), dim3(512), 0, st, jp);
-      } else if (2 * cap_max <= 256) {
-        hipLaunchKernelGGL((k_jacobi<16, 16, 512, 8192>), dim3(nj), dim3(512), 0, st, jp);
+      } else if (g_jacobi_variant == 4) {  // single-workgroup LDS-panel Jacobi (reference variant)
+        if (2 * cap_max <= 256) hipLaunchKernelGGL((k_jacobi<16, 16, 512, 8192>), dim3(nj), dim3(512), 0, st, jp);
+        else hipLaunchKernelGGL((k_jacobi<32, 16, 512, 8192>), dim3(nj), dim3(512), 0, st, jp);
       } else {
-        hipLaunchKernelGGL((k_jacobi<32, 16, 512, 8192>), dim3(nj), dim3(512), 0, st, jp);
+        // 2 chi > 128: multi-workgroup block Jacobi (bjacobi.hip), W in HBM / L2
+        const int brc = aqc::block_jacobi(jp, nj, cap_max, st);
+        if (brc != AQC_OK) return brc;
       }
       aqc::KernelTimer::end(st);
       AQC_CHECK_LAUNCH();
@@ -1645,7 +1602,7 @@ int aqc_mps_set_jacobi_tol(double factor) {
 }
 
 int aqc_mps_set_jacobi_variant(int variant) {
-  AQC_REQUIRE(variant >= 0 && variant <= 3, "aqc_mps_set_jacobi_variant: variant must be 0..3");
+  AQC_REQUIRE(variant >= 0 && variant <= 4, "aqc_mps_set_jacobi_variant: variant must be 0..4");
   g_jacobi_variant = variant;
   return AQC_OK;
 }

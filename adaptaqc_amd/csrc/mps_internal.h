@@ -37,6 +37,63 @@ struct MpsDev {
   double* bond(int b) const { return lam + (size_t)b * cap; }
 };
 
+// One two-site update of one state (k_theta -> SVD -> k_rank -> k_split_*), see mps.hip.
+struct TwoSiteJob {
+  cplx* gp;
+  cplx* gq;
+  const double* ll;
+  double* lm;
+  const double* lr;
+  int* dims;  // &dims[p] : dims[0] = chi_l, dims[1] = chi_m, dims[2] = chi_r
+  cplx* theta;
+  cplx* work;
+  double* sig;
+  int* perm;
+  int* flags;
+  int cap;
+  int max_chi;
+  double thr;
+  double jtol;  // Jacobi rotation threshold factor
+  int qr;       // 1: Jacobi ran on R^H of a pivoted QR -> W holds the other side (see k_jacobi_reg)
+  int dbg;      // diagnostics (aqc_svd_debug): 1 = stop after the QR phase, write X unpermuted
+  cplx G[16];  // row = 2*s1'+s2' (out), col = 2*s1+s2 (in)
+};
+
+// Rotation parameters of the pair (alpha, beta, gamma = gx + i gy): t = sgn(zeta) /
+// (|zeta| + sqrt(1 + zeta^2)), zeta = (beta - alpha) / (2|gamma|), c = 1/sqrt(1 + t^2) and
+// s e = c t gamma / |gamma|.  v_rsq_f64 / v_rcp_f64 seeds with two Newton steps each (full double
+// precision) instead of the IEEE sqrt / divide sequences: this chain is serial per round.
+__device__ __forceinline__ void jacobi_params(double al, double be, double gx, double gy, double g2, double& c,
+                                              double& ex, double& ey) {
+  double rg = __builtin_amdgcn_rsq(g2);  // 1 / |gamma|
+  rg = rg * fma(-0.5 * g2 * rg, rg, 1.5);
+  rg = rg * fma(-0.5 * g2 * rg, rg, 1.5);
+  const double zeta = 0.5 * (be - al) * rg;
+  const double q = fma(zeta, zeta, 1.0);
+  double rq = __builtin_amdgcn_rsq(q);
+  rq = rq * fma(-0.5 * q * rq, rq, 1.5);
+  rq = rq * fma(-0.5 * q * rq, rq, 1.5);
+  const double den = fabs(zeta) + q * rq;  // |zeta| + sqrt(1 + zeta^2)
+  double inv = __builtin_amdgcn_rcp(den);
+  inv = inv * fma(-den, inv, 2.0);
+  inv = inv * fma(-den, inv, 2.0);
+  const double t = zeta >= 0 ? inv : -inv;
+  const double p = fma(t, t, 1.0);
+  double cc = __builtin_amdgcn_rsq(p);
+  cc = cc * fma(-0.5 * p * cc, cc, 1.5);
+  cc = cc * fma(-0.5 * p * cc, cc, 1.5);
+  c = cc;
+  const double sc = cc * t * rg;
+  ex = gx * sc;
+  ey = gy * sc;
+}
+
+// Multi-workgroup block one-sided Jacobi SVD for 2 * chi > 128 (bjacobi.hip): factors the nj
+// two-site thetas of `jobs` (device array) into the k_jacobi output contract (W columns = U sigma,
+// sig = column norms, qr = 0).  Enqueued on `st`; synchronises the host once per sweep (from the
+// third on) to stop when every decomposition has converged.
+int block_jacobi(const TwoSiteJob* jobs, int nj, int cap_max, hipStream_t st);
+
 hipStream_t mps_stream();
 
 }  // namespace aqc

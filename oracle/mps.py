@@ -171,7 +171,7 @@ def mps_dot(a, b):
     """<a|b>, conjugating the FIRST argument (pinned by test_gradients.py:39-73)."""
     env = np.ones((1, 1), dtype=complex)
     for x, y in zip(a, b):
-        env = np.einsum("ij,sik,sjl->kl", env, np.conj(x), y)
+        env = np.einsum("ij,sik,sjl->kl", env, np.conj(x), y, optimize=True)
     return complex(env[0, 0])
 
 
@@ -181,7 +181,7 @@ def mps_expectation_z(mps, q):
     z = np.array([1.0, -1.0])
     for i, x in enumerate(mps):
         y = x * z[:, None, None] if i == q else x
-        env = np.einsum("ij,sik,sjl->kl", env, np.conj(x), y)
+        env = np.einsum("ij,sik,sjl->kl", env, np.conj(x), y, optimize=True)
     return float(np.real(env[0, 0]))
 
 

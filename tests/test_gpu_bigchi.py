@@ -1,0 +1,82 @@
+"""Large-bond MPS updates (2 chi > 128: multi-workgroup block Jacobi, bjacobi.hip) vs the oracle.
+
+BASELINE configs 4 and 5 run at chi = 128 and chi = 256; here the same kernels on states small
+enough for the numpy oracle (LAPACK SVDs): random Vidal MPS whose middle bonds sit at the cap,
+then adjacent, swap-routed and truncating two-site gates.  Tolerance: the truncated-MPS bar of
+BASELINE.json (1e-6), on the fidelity between the device and oracle states, on <Z_i>, and exact
+bond dimensions.
+"""
+import numpy as np
+import pytest
+
+from bench import random_vidal_mps
+from conftest import to_circuit
+from oracle import mps as M
+
+pytestmark = pytest.mark.gpu
+
+
+def _check(n, chi, ops, seed, variant=None):
+    from adaptaqc_amd import _lib
+    from adaptaqc_amd.circuit import device_ops
+    from adaptaqc_amd.device import DeviceMPS
+
+    aer = random_vidal_mps(n, chi, seed)
+    ref = M.run_circuit(n, ops, 1e-16, chi, mps=M.MPS.from_aer(aer))
+    if variant is not None:
+        _lib.check(_lib.lib().aqc_mps_set_jacobi_variant(variant))
+    try:
+        d = DeviceMPS(n, chi, 1e-16, chi)
+        d.load_aer(aer)
+        d.apply(device_ops(to_circuit(n, ops)))
+        dims = d.dims()
+    finally:
+        if variant is not None:
+            _lib.check(_lib.lib().aqc_mps_set_jacobi_variant(2))
+    pre_ref = ref.preprocessed()
+    np.testing.assert_array_equal(dims, [1] + [x.shape[2] for x in pre_ref])
+    pre = d.preprocessed()
+    fid = abs(M.mps_dot(pre_ref, pre))
+    nrm = abs(M.mps_dot(pre, pre))
+    assert abs(nrm - 1.0) < 1e-10
+    assert abs(fid - 1.0) < 1e-6, fid
+    qs = list(range(0, n, 3))
+    zr = np.array([M.mps_expectation_z(pre_ref, q) for q in qs])
+    np.testing.assert_allclose(d.z_all()[qs], zr, atol=1e-6)
+    return dims
+
+
+def _gates(n, rng, pairs):
+    ops = []
+    for a, b in pairs:
+        for q in (a, b):
+            ops.append(("ry", (q,), (rng.uniform(-np.pi, np.pi),)))
+            ops.append(("rz", (q,), (rng.uniform(-np.pi, np.pi),)))
+        ops.append(("cx", (a, b), ()))
+    return ops
+
+
+@pytest.mark.parametrize("n,chi", [(16, 128), (18, 256)])
+def test_block_jacobi_adjacent_and_routed(n, chi):
+    """Middle bonds at the cap: adjacent gates (truncation 2chi -> chi binds) and a routed gate."""
+    rng = np.random.default_rng(chi)
+    m = n // 2
+    ops = _gates(n, rng, [(m - 1, m), (m, m + 1), (m + 1, m - 2)])
+    dims = _check(n, chi, ops, seed=chi + 1)
+    assert dims.max() == chi
+
+
+def test_block_jacobi_ragged_bonds():
+    """Bonds below the cap and non-multiples of the 16-column block (chi_l != chi_r)."""
+    rng = np.random.default_rng(3)
+    n, chi = 16, 100  # bonds 64 | 100 100 100 | 64: 200-row thetas (12.5 blocks), 128 x 200 (transposed)
+    ops = _gates(n, rng, [(7, 8), (6, 7), (8, 9), (2, 3), (0, 1)])
+    _check(n, chi, ops, seed=9)
+
+
+def test_panel_and_block_jacobi_agree():
+    """The single-workgroup LDS-panel kernel (variant 4) and the block Jacobi give the same state."""
+    rng = np.random.default_rng(4)
+    n, chi = 16, 128
+    ops = _gates(n, rng, [(7, 8), (6, 7)])
+    _check(n, chi, ops, seed=5, variant=4)
