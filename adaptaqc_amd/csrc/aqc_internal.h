@@ -69,13 +69,22 @@ __host__ __device__ __forceinline__ cplx cscale(cplx a, double s) { return cmk(a
 __host__ __device__ __forceinline__ cplx cconj(cplx a) { return cmk(a.x, -a.y); }
 __host__ __device__ __forceinline__ double cnorm2(cplx a) { return fma(a.x, a.x, a.y * a.y); }
 
+// Lane permutation of a double within DPP rows (CTRL: quad_perm / row_ror), as two 32-bit
+// v_mov_b32_dpp with no "old" operand (every lane of these patterns reads a valid source).
+template <int CTRL>
+__device__ __forceinline__ double dpp_perm(double v) {
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xF, 0xF, true);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xF, 0xF, true);
+  return __hiloint2double(hi, lo);
+}
+
 // Sum over the 16 lanes of a DPP row, result in every lane of the row.  Pure VALU (DPP
 // quad_perm / row_ror), no LDS crossbar: ~2.5x cheaper than the ds_bpermute __shfl_xor path.
 __device__ __forceinline__ double row_sum16(double v) {
-  v += __builtin_amdgcn_update_dpp(0.0, v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
-  v += __builtin_amdgcn_update_dpp(0.0, v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
-  v += __builtin_amdgcn_update_dpp(0.0, v, 0x124, 0xF, 0xF, false);  // row_ror:4
-  v += __builtin_amdgcn_update_dpp(0.0, v, 0x128, 0xF, 0xF, false);  // row_ror:8
+  v += dpp_perm<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_perm<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_perm<0x124>(v);  // row_ror:4
+  v += dpp_perm<0x128>(v);  // row_ror:8
   return v;
 }
 

@@ -370,6 +370,7 @@ __global__ __launch_bounds__(JT) void k_jacobi(const TwoSiteJob* __restrict__ jo
 // handles by flipping its side test (tools/qrp_jacobi_proto.py is the numpy restatement).
 
 using aqc::jacobi_params;
+using aqc::jacobi_tc;
 
 // sortable pivot key: non-negative double bits with the low byte replaced by (255 - id), so
 // that the 64-bit maximum is the largest trailing norm, ties to the lowest column id
@@ -571,67 +572,136 @@ __global__ __launch_bounds__(CP * 8) void k_jacobi_reg(const TwoSiteJob* __restr
   // the upper half swaps its S with slot g - h (the lower half's next partners).  One barrier
   // per round.  (A register-resident M with a per-round LDS shift moved every M column through
   // the ~79 B/clk LDS store path twice per round: 1.5x slower, tools/jacobi_lab.hip.)
+  //
+  // Scaled columns with tracked norms (the round is VALU-bound): a column is d * v (v stored,
+  // d > 0, 1/d kept too) with its squared norm n tracked through the rotation identity
+  // n_a' = n_a - t|g|, n_b' = n_b + t|g| (exact at every sweep start, recomputed when a norm
+  // falls by more than 1e6: cancellation).  The rotation of the true columns
+  //   a' = c a - s conj(e) b,  b' = s e a + c b   (t = s / c, e = g / |g|)
+  // acts on the stored vectors as v_a' = v_a - mu v_b, v_b' = v_b + nu v_a with
+  //   mu = t conj(e) d_b / d_a,  nu = t e d_a / d_b,  d' = c d:
+  // 8 FMAs per row instead of 12, and only g = a^H b is reduced per round (2 sums, not 4).
+  __shared__ double xnrm[kG], xscl[kG], xisc[kG];
   __syncthreads();  // the QR transpose's last reads of xbuf are done
 #pragma unroll
   for (int i = 0; i < MAXR; ++i) xbuf[g * ld + lane + 16 * i] = make_double2(mr[i], mi[i]);
-  if (lane == 0) xid[g] = mid;
-  __syncthreads();
+  if (lane == 0) {
+    xid[g] = mid;
+    xscl[g] = 1.0;
+  }
   // Stop rule: a sweep whose counted rotations all had |t| < kTinyT leaves every cosine at
   // O(t * cos) ~ 1e-16 after it (quadratic convergence), so the confirming sweep with no
   // rotation at all is skipped.
   constexpr double kTinyT = 1e-8;
+  double sd = 1.0, sn = 0.0;  // S: scale and tracked squared norm (uniform in the group)
   int sweeps = 0;
   for (sweeps = 0; sweeps < max_sweeps; ++sweeps) {
-    if (tid == 0) rot = big = 0;
+    {  // sweep start: fold the scales into the vectors, exact norms
+      double2* own = xbuf + g * ld;
+      const double od = xscl[g];
+      double a = 0, b = 0;
+#pragma unroll
+      for (int i = 0; i < MAXR; ++i) {
+        sr[i] *= sd;
+        si[i] *= sd;
+        double2 v = own[lane + 16 * i];
+        v.x *= od;
+        v.y *= od;
+        own[lane + 16 * i] = v;
+        a = fma(sr[i], sr[i], fma(si[i], si[i], a));
+        b = fma(v.x, v.x, fma(v.y, v.y, b));
+      }
+      a = aqc::row_sum16(a);
+      b = aqc::row_sum16(b);
+      sd = 1.0;
+      sn = a;
+      __builtin_amdgcn_wave_barrier();
+      if (lane == 0) {
+        xscl[g] = 1.0;
+        xisc[g] = 1.0;
+        xnrm[g] = b;
+      }
+      if (tid == 0) rot = big = 0;
+    }
     __syncthreads();
+    double isd = 1.0;
     int my_rot = 0, my_big = 0;
     for (int m = kG; m >= 1; m >>= 1) {  // level: sub-blocks of m groups
       const int li = g & (m - 1), base = g - li;
       for (int r = 0; r < m; ++r) {
-        double2* col = xbuf + (base + ((li + r) & (m - 1))) * ld;
+        const int slot = base + ((li + r) & (m - 1));
+        double2* col = xbuf + slot * ld;
 #pragma unroll
         for (int i = 0; i < MAXR; ++i) {
           const double2 v = col[lane + 16 * i];
           mr[i] = v.x;
           mi[i] = v.y;
         }
-        double al = 0, be = 0, gx = 0, gy = 0;
+        const double mn = xnrm[slot], md = xscl[slot], imd = xisc[slot];
+        double gx = 0, gy = 0;
 #pragma unroll
         for (int i = 0; i < MAXR; ++i) {
-          al = fma(sr[i], sr[i], fma(si[i], si[i], al));
-          be = fma(mr[i], mr[i], fma(mi[i], mi[i], be));
           gx = fma(sr[i], mr[i], fma(si[i], mi[i], gx));   // conj(s) * m
           gy = fma(sr[i], mi[i], fma(-si[i], mr[i], gy));
         }
-        al = aqc::row_sum16(al);
-        be = aqc::row_sum16(be);
         gx = aqc::row_sum16(gx);
         gy = aqc::row_sum16(gy);
+        const double dd = sd * md;
+        gx *= dd;
+        gy *= dd;
         const double g2 = gx * gx + gy * gy;
-        const double ab = al * be;
-        if (g2 > tol2 * ab && al > floor2 && be > floor2) {
+        const double ab = sn * mn;
+        if (g2 > tol2 * ab && sn > floor2 && mn > floor2) {
           // only rotations above dot-product noise keep the sweep loop going: a pair of
           // (near-)degenerate columns can otherwise flip-flop at |g| ~ tol forever
-          double c, ex, ey;  // c and s e (s conj(e) = (ex, -ey))
-          jacobi_params(al, be, gx, gy, g2, c, ex, ey);
+          double t, c, p, rg;
+          jacobi_tc(sn, mn, g2, t, c, p, rg);
           if (g2 > 16.0 * tol2 * ab) {
             my_rot = 1;
-            if (ex * ex + ey * ey > kTinyT * kTinyT * c * c) my_big = 1;  // |t| = |s| / c
+            if (fabs(t) > kTinyT) my_big = 1;
           }
+          const double ra = md * isd, ira = sd * imd;  // d_b / d_a and its inverse
+          const double te = t * rg;
+          const double mux = te * gx * ra, muy = -te * gy * ra;   // mu = t conj(e) d_b / d_a
+          const double nux = te * gx * ira, nuy = te * gy * ira;  // nu = t e d_a / d_b
 #pragma unroll
           for (int i = 0; i < MAXR; ++i) {
             const double ar = sr[i], ai = si[i], br = mr[i], bi = mi[i];
-            // a' = c a - s conj(e) b ; b' = s e a + c b
-            sr[i] = fma(c, ar, -fma(ex, br, ey * bi));
-            si[i] = fma(c, ai, -fma(ex, bi, -ey * br));
-            col[lane + 16 * i] = make_double2(fma(c, br, fma(ex, ar, -ey * ai)), fma(c, bi, fma(ex, ai, ey * ar)));
+            sr[i] = fma(-mux, br, fma(muy, bi, ar));
+            si[i] = fma(-mux, bi, fma(-muy, br, ai));
+            col[lane + 16 * i] = make_double2(fma(nux, ar, fma(-nuy, ai, br)), fma(nux, ai, fma(nuy, ar, bi)));
+          }
+          const double ic = p * c;  // 1 / c
+          sd *= c;
+          isd *= ic;
+          const double md2 = md * c, imd2 = imd * ic;
+          const double tg = t * (g2 * rg);  // t |g|
+          double sn2 = sn - tg, mn2 = mn + tg;
+          if (sn2 < 1e-6 * sn || mn2 < 1e-6 * mn) {  // cancellation: recompute exactly
+            double a = 0, b = 0;
+            asm volatile("" ::: "memory");  // re-read M from LDS: keeps it out of VGPRs above
+#pragma unroll
+            for (int i = 0; i < MAXR; ++i) {  // (this lane's own LDS writes: in order)
+              const double2 v = col[lane + 16 * i];
+              a = fma(sr[i], sr[i], fma(si[i], si[i], a));
+              b = fma(v.x, v.x, fma(v.y, v.y, b));
+            }
+            sn2 = aqc::row_sum16(a) * sd * sd;
+            mn2 = aqc::row_sum16(b) * md2 * md2;
+          }
+          sn = sn2;
+          __builtin_amdgcn_wave_barrier();
+          if (lane == 0) {
+            xnrm[slot] = mn2;
+            xscl[slot] = md2;
+            xisc[slot] = imd2;
           }
         }
         __syncthreads();
       }
       if (m == 1) break;
       const int h = m >> 1;
-      if (li >= h) {  // upper half: S <-> slot g - h
+      if (li >= h) {  // upper half: S <-> slot g - h (vectors, id, norm, scales)
         double2* col = xbuf + (g - h) * ld;
 #pragma unroll
         for (int i = 0; i < MAXR; ++i) {
@@ -641,9 +711,18 @@ __global__ __launch_bounds__(CP * 8) void k_jacobi_reg(const TwoSiteJob* __restr
           si[i] = v.y;
         }
         const int pid = xid[g - h];
+        const double pn = xnrm[g - h], pd = xscl[g - h], pi = xisc[g - h];
         __builtin_amdgcn_wave_barrier();
-        if (lane == 0) xid[g - h] = sid;
+        if (lane == 0) {
+          xid[g - h] = sid;
+          xnrm[g - h] = sn;
+          xscl[g - h] = sd;
+          xisc[g - h] = isd;
+        }
         sid = pid;
+        sn = pn;
+        sd = pd;
+        isd = pi;
       }
       __syncthreads();
     }
@@ -654,20 +733,24 @@ __global__ __launch_bounds__(CP * 8) void k_jacobi_reg(const TwoSiteJob* __restr
     __syncthreads();
   }
   // write columns to their own slots (with QR: rows mapped back through the pivot order) and
-  // their norms: S from VGPRs, slot g's column from LDS
+  // their norms: S from VGPRs, slot g's column from LDS, both with their scales applied
   double2* W = j.work;
   const int mid_out = xid[g];
+  const double od = xscl[g];
   double ns = 0, nm = 0;
 #pragma unroll
   for (int i = 0; i < MAXR; ++i) {
     const int row = lane + 16 * i;
-    const double2 mv = xbuf[g * ld + row];
+    double2 mv = xbuf[g * ld + row];
+    mv.x *= od;
+    mv.y *= od;
+    const double ar = sr[i] * sd, ai = si[i] * sd;
     if (row < Lj) {
       const int orow = map_rows ? perm_s[row] : row;
-      if (sid < C) W[(size_t)sid * Lj + orow] = make_double2(sr[i], si[i]);
+      if (sid < C) W[(size_t)sid * Lj + orow] = make_double2(ar, ai);
       if (mid_out < C) W[(size_t)mid_out * Lj + orow] = mv;
     }
-    ns = fma(sr[i], sr[i], fma(si[i], si[i], ns));
+    ns = fma(ar, ar, fma(ai, ai, ns));
     nm = fma(mv.x, mv.x, fma(mv.y, mv.y, nm));
   }
   ns = aqc::row_sum16(ns);

@@ -88,6 +88,32 @@ __device__ __forceinline__ void jacobi_params(double al, double be, double gx, d
   ey = gy * sc;
 }
 
+// Jacobi rotation of the pair (alpha = |a|^2, beta = |b|^2, |g|^2 = |a^H b|^2): t = sgn(zeta) /
+// (|zeta| + sqrt(1 + zeta^2)), zeta = (beta - alpha) / (2|g|), c = 1 / sqrt(p), p = 1 + t^2,
+// rg = 1 / |g| (rsq / rcp seeds with two Newton steps each: full double precision).
+__device__ __forceinline__ void jacobi_tc(double al, double be, double g2, double& t, double& c, double& p,
+                                          double& rg) {
+  double r = __builtin_amdgcn_rsq(g2);
+  r = r * fma(-0.5 * g2 * r, r, 1.5);
+  r = r * fma(-0.5 * g2 * r, r, 1.5);
+  rg = r;
+  const double zeta = 0.5 * (be - al) * r;
+  const double q = fma(zeta, zeta, 1.0);
+  double rq = __builtin_amdgcn_rsq(q);
+  rq = rq * fma(-0.5 * q * rq, rq, 1.5);
+  rq = rq * fma(-0.5 * q * rq, rq, 1.5);
+  const double den = fabs(zeta) + q * rq;
+  double inv = __builtin_amdgcn_rcp(den);
+  inv = inv * fma(-den, inv, 2.0);
+  inv = inv * fma(-den, inv, 2.0);
+  t = zeta >= 0 ? inv : -inv;
+  p = fma(t, t, 1.0);
+  double cc = __builtin_amdgcn_rsq(p);
+  cc = cc * fma(-0.5 * p * cc, cc, 1.5);
+  cc = cc * fma(-0.5 * p * cc, cc, 1.5);
+  c = cc;
+}
+
 // Multi-workgroup block one-sided Jacobi SVD for 2 * chi > 128 (bjacobi.hip): factors the nj
 // two-site thetas of `jobs` (device array) into the k_jacobi output contract (W columns = U sigma,
 // sig = column norms, qr = 0).  Enqueued on `st`; synchronises the host once per sweep (from the

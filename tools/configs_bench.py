@@ -163,6 +163,9 @@ def config5(gates, reps):
         work.dims()  # synchronises
     el = time.perf_counter() - t0
     _lib.timing_enable(False)
+    import ctypes
+    sw = ctypes.c_int()
+    _lib.check(_lib.lib().aqc_mps_jacobi_stats(work.h, ctypes.byref(sw)))
     nom = 32.0 * chi ** 3 + bench.svd_nominal_flops(2 * chi, 2 * chi)
     svd = _lib.timing_query("mps_svd")
     th = _lib.timing_query("mps_theta")
@@ -173,7 +176,7 @@ def config5(gates, reps):
             "value": reps * gates / el, "unit": "gates/s", "ms_per_gate": per_gate_ms,
             "nominal_tflops": nom / (per_gate_ms * 1e-3) / 1e12, "dtype": "c128", "data": "synthetic random Vidal MPS",
             "config": {"workload": "config5: (rz ry rz)x(rz ry rz).CX on disjoint middle pairs, max_chi=256",
-                       "n_qubits": n, "chi": chi, "gates": gates,
+                       "n_qubits": n, "chi": chi, "gates": gates, "max_jacobi_sweeps": sw.value,
                        "dims_after": [int(x) for x in work.dims()[mid:mid + 2 * gates + 1]]},
             "breakdown_ms_per_gate": {"svd": svd["ms"] / (reps * gates), "theta": th["ms"] / (reps * gates),
                                       "split": sp["ms"] / (reps * gates)},

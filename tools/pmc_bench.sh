@@ -1,0 +1,15 @@
+#!/bin/bash
+# PMC passes over a short bench run (one rocprofv3 --pmc pass per counter group; gfx950 slot
+# limits: 8 SQ, 4 TCC (FETCH_SIZE uses 3, WRITE_SIZE 2), 2 GRBM).  Output: gpurun_out/pmc_<k>/.
+# Usage (GPU box): bash tools/pmc_bench.sh [bench args...]
+set -e
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+ARGS=${@:-"--steps 1 --warmup 0 --no-cpu-baseline"}
+pass() {
+  local k=$1; shift
+  timeout -s KILL 120 rocprofv3 --pmc "$@" -d gpurun_out/pmc_$k -o run -- python3 bench.py $ARGS > gpurun_out/pmc_$k.log 2>&1
+}
+pass sq1 SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS
+pass sq2 SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAIT_INST_LDS SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE
+pass fetch FETCH_SIZE
+pass write WRITE_SIZE
