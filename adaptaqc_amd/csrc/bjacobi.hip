@@ -47,6 +47,8 @@ __device__ __forceinline__ double wave_sum(double v) {
   return __hiloint2double(hi, lo);
 }
 
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+
 __device__ __forceinline__ void job_shape(const TwoSiteJob& j, int& L, int& C, bool& tr) {
   const int M = 2 * j.dims[0], N = 2 * j.dims[2];
   tr = M < N;
@@ -78,42 +80,77 @@ __global__ __launch_bounds__(256) void k_bj_init(const TwoSiteJob* __restrict__ 
   if (threadIdx.x == 0) atomicAdd(&st[blockIdx.y].fro, red[0] + red[1] + red[2] + red[3]);
 }
 
-// One pair rotation of columns (a: sr/si, b: mr/mi) -- MAXR rows per lane, 64 lanes.  Returns
-// whether the pair was rotated; rot / big collect the stop-test flags.
+// One pair rotation of scaled columns a = da * (sr, si), b = db * (mr, mi) with tracked squared
+// norms na, nb (the scheme of k_jacobi_reg, mps.hip: v_a' = v_a - mu v_b, v_b' = v_b + nu v_a,
+// d' = c d, n_a' = n_a - t|g|, n_b' = n_b + t|g|, exact recompute on a 1e6 drop).  MAXR rows per
+// lane, 64 lanes.  Returns whether the pair was rotated; rot / big collect the stop-test flags.
+// With bcol != nullptr the new b goes straight to that LDS column (row lane + 64 i) instead of
+// back into mr / mi, which keeps the cross kernel (16 waves, 128 VGPRs) free of spills.
 template <int MAXR>
 __device__ __forceinline__ bool rotate_pair(double (&sr)[MAXR], double (&si)[MAXR], double (&mr)[MAXR],
-                                            double (&mi)[MAXR], double tol2, double floor2, int& rot, int& big) {
-  double al = 0, be = 0, gx = 0, gy = 0;
+                                            double (&mi)[MAXR], double& na, double& da, double& ida, double& nb,
+                                            double& db, double& idb, double tol2, double floor2, int& rot, int& big,
+                                            double2* bcol = nullptr) {
+  double gx = 0, gy = 0;
 #pragma unroll
   for (int i = 0; i < MAXR; ++i) {
-    al = fma(sr[i], sr[i], fma(si[i], si[i], al));
-    be = fma(mr[i], mr[i], fma(mi[i], mi[i], be));
     gx = fma(sr[i], mr[i], fma(si[i], mi[i], gx));  // conj(a) * b
     gy = fma(sr[i], mi[i], fma(-si[i], mr[i], gy));
   }
-  al = wave_sum(al);
-  be = wave_sum(be);
-  gx = wave_sum(gx);
-  gy = wave_sum(gy);
+  const double dd = da * db;
+  gx = wave_sum(gx) * dd;
+  gy = wave_sum(gy) * dd;
   const double g2 = gx * gx + gy * gy;
-  const double ab = al * be;
-  if (!(g2 > tol2 * ab && al > floor2 && be > floor2)) return false;
-  double c, ex, ey;
-  jacobi_params(al, be, gx, gy, g2, c, ex, ey);
+  const double ab = na * nb;
+  if (!(g2 > tol2 * ab && na > floor2 && nb > floor2)) return false;
+  double t, c, p, rg;
+  jacobi_tc(na, nb, g2, t, c, p, rg);
   if (g2 > 16.0 * tol2 * ab) {
     rot = 1;
-    if (ex * ex + ey * ey > kTinyT * kTinyT * c * c) big = 1;
+    if (fabs(t) > kTinyT) big = 1;
   }
+  const double ra = db * ida, ira = da * idb, te = t * rg;
+  const double mux = te * gx * ra, muy = -te * gy * ra;
+  const double nux = te * gx * ira, nuy = te * gy * ira;
 #pragma unroll
   for (int i = 0; i < MAXR; ++i) {
     const double ar = sr[i], ai = si[i], br = mr[i], bi = mi[i];
-    // a' = c a - s conj(e) b ; b' = s e a + c b
-    sr[i] = fma(c, ar, -fma(ex, br, ey * bi));
-    si[i] = fma(c, ai, -fma(ex, bi, -ey * br));
-    mr[i] = fma(c, br, fma(ex, ar, -ey * ai));
-    mi[i] = fma(c, bi, fma(ex, ai, ey * ar));
+    sr[i] = fma(-mux, br, fma(muy, bi, ar));
+    si[i] = fma(-mux, bi, fma(-muy, br, ai));
+    const double nr = fma(nux, ar, fma(-nuy, ai, br)), ni = fma(nux, ai, fma(nuy, ar, bi));
+    if (bcol) {
+      bcol[lane_id() + 64 * i] = make_double2(nr, ni);
+    } else {
+      mr[i] = nr;
+      mi[i] = ni;
+    }
   }
+  const double ic = p * c;
+  da *= c, ida *= ic, db *= c, idb *= ic;
+  const double tg = t * (g2 * rg);
+  double na2 = na - tg, nb2 = nb + tg;
+  if (na2 < 1e-6 * na || nb2 < 1e-6 * nb) {
+    double x = 0, y = 0;
+    if (bcol) asm volatile("" ::: "memory");  // re-read b from LDS (own lanes' writes: in order)
+#pragma unroll
+    for (int i = 0; i < MAXR; ++i) {
+      x = fma(sr[i], sr[i], fma(si[i], si[i], x));
+      const double2 v = bcol ? bcol[lane_id() + 64 * i] : make_double2(mr[i], mi[i]);
+      y = fma(v.x, v.x, fma(v.y, v.y, y));
+    }
+    na2 = wave_sum(x) * da * da;
+    nb2 = wave_sum(y) * db * db;
+  }
+  na = na2, nb = nb2;
   return true;
+}
+
+template <int MAXR>
+__device__ __forceinline__ double col_norm2(const double (&r)[MAXR], const double (&i_)[MAXR]) {
+  double x = 0;
+#pragma unroll
+  for (int i = 0; i < MAXR; ++i) x = fma(r[i], r[i], fma(i_[i], i_[i], x));
+  return wave_sum(x);
 }
 
 __device__ __forceinline__ double tol_sq(const TwoSiteJob& j, int L) {
@@ -146,6 +183,18 @@ __global__ __launch_bounds__(512) void k_bj_intra(const TwoSiteJob* __restrict__
     }
   }
   __syncthreads();
+  __shared__ double cn[kB], cd[kB], cid[kB];  // tracked norms and scales of the 16 columns
+  for (int k = w; k < kB; k += 8) {
+    double x = 0;
+#pragma unroll
+    for (int i = 0; i < MAXR; ++i) {
+      const double2 v = cols[k * ldl + lane + 64 * i];
+      x = fma(v.x, v.x, fma(v.y, v.y, x));
+    }
+    x = wave_sum(x);
+    if (lane == 0) cn[k] = x, cd[k] = 1.0, cid[k] = 1.0;
+  }
+  __syncthreads();
   const double tol2 = tol_sq(j, L), floor2 = s.fro * 1e-24;
   int rot = 0, big = 0;
   for (int r = 0; r < kB - 1; ++r) {
@@ -156,12 +205,15 @@ __global__ __launch_bounds__(512) void k_bj_intra(const TwoSiteJob* __restrict__
       const double2 x = cols[a * ldl + lane + 64 * i], y = cols[b * ldl + lane + 64 * i];
       sr[i] = x.x, si[i] = x.y, mr[i] = y.x, mi[i] = y.y;
     }
-    if (rotate_pair<MAXR>(sr, si, mr, mi, tol2, floor2, rot, big)) {
+    double na = cn[a], da = cd[a], ida = cid[a], nb = cn[b], db = cd[b], idb = cid[b];
+    if (rotate_pair<MAXR>(sr, si, mr, mi, na, da, ida, nb, db, idb, tol2, floor2, rot, big)) {
 #pragma unroll
       for (int i = 0; i < MAXR; ++i) {
         cols[a * ldl + lane + 64 * i] = make_double2(sr[i], si[i]);
         cols[b * ldl + lane + 64 * i] = make_double2(mr[i], mi[i]);
       }
+      __builtin_amdgcn_wave_barrier();
+      if (lane == 0) cn[a] = na, cd[a] = da, cid[a] = ida, cn[b] = nb, cd[b] = db, cid[b] = idb;
     }
     __syncthreads();
   }
@@ -169,7 +221,10 @@ __global__ __launch_bounds__(512) void k_bj_intra(const TwoSiteJob* __restrict__
 #pragma unroll
     for (int i = 0; i < MAXR; ++i) {
       const int row = lane + 64 * i;
-      if (row < L) W[(size_t)k * L + row] = cols[k * ldl + row];
+      if (row < L) {
+        const double2 v = cols[k * ldl + row];
+        W[(size_t)k * L + row] = make_double2(v.x * cd[k], v.y * cd[k]);
+      }
     }
   }
   if (lane == 0 && rot) atomicOr(&s.rot, 1);
@@ -207,19 +262,33 @@ __global__ __launch_bounds__(1024) void k_bj_cross(const TwoSiteJob* __restrict_
     sr[i] = a.x, si[i] = a.y;
     cols[w * ldl + row] = b;
   }
+  __shared__ double cn[kB], cd[kB], cid[kB];  // tracked norms and scales of block J's columns
+  {
+    double x = 0;
+#pragma unroll
+    for (int i = 0; i < MAXR; ++i) {
+      const double2 v = cols[w * ldl + lane + 64 * i];
+      x = fma(v.x, v.x, fma(v.y, v.y, x));
+    }
+    x = wave_sum(x);
+    if (lane == 0) cn[w] = x, cd[w] = 1.0, cid[w] = 1.0;
+  }
+  double na = col_norm2<MAXR>(sr, si), da = 1.0, ida = 1.0;
   __syncthreads();
   const double tol2 = tol_sq(j, L), floor2 = s.fro * 1e-24;
   int rot = 0, big = 0;
   for (int r = 0; r < kB; ++r) {
-    double2* col = cols + ((w + r) & (kB - 1)) * ldl;
+    const int slot = (w + r) & (kB - 1);
+    double2* col = cols + slot * ldl;
 #pragma unroll
     for (int i = 0; i < MAXR; ++i) {
       const double2 v = col[lane + 64 * i];
       mr[i] = v.x, mi[i] = v.y;
     }
-    if (rotate_pair<MAXR>(sr, si, mr, mi, tol2, floor2, rot, big)) {
-#pragma unroll
-      for (int i = 0; i < MAXR; ++i) col[lane + 64 * i] = make_double2(mr[i], mi[i]);
+    double nb = cn[slot], db = cd[slot], idb = cid[slot];
+    if (rotate_pair<MAXR>(sr, si, mr, mi, na, da, ida, nb, db, idb, tol2, floor2, rot, big, col)) {
+      __builtin_amdgcn_wave_barrier();
+      if (lane == 0) cn[slot] = nb, cd[slot] = db, cid[slot] = idb;
     }
     __syncthreads();
   }
@@ -227,8 +296,11 @@ __global__ __launch_bounds__(1024) void k_bj_cross(const TwoSiteJob* __restrict_
   for (int i = 0; i < MAXR; ++i) {
     const int row = lane + 64 * i;
     if (row < L) {
-      if (w < nI) WI[(size_t)w * L + row] = make_double2(sr[i], si[i]);
-      if (w < nJ) WJ[(size_t)w * L + row] = cols[w * ldl + row];
+      if (w < nI) WI[(size_t)w * L + row] = make_double2(sr[i] * da, si[i] * da);
+      if (w < nJ) {
+        const double2 v = cols[w * ldl + row];
+        WJ[(size_t)w * L + row] = make_double2(v.x * cd[w], v.y * cd[w]);
+      }
     }
   }
   if (lane == 0 && rot) atomicOr(&s.rot, 1);

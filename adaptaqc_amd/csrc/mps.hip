@@ -399,11 +399,21 @@ __device__ __forceinline__ void qr_reflector(double (&xr)[MAXR], double (&xi)[MA
   if (s2 == 0.0 && ai == 0.0) {
     beta = ar, tr_ = 0.0, ti_ = 0.0;
   } else {
-    const double nrm = sqrt(fma(ar, ar, fma(ai, ai, s2)));
+    // rsq / rcp seeds + two Newton steps (full precision) instead of the IEEE sqrt / divide
+    // sequences: this chain runs on one group while the workgroup waits at the next barrier
+    const double x = fma(ar, ar, fma(ai, ai, s2));
+    double r = __builtin_amdgcn_rsq(x);
+    r = r * fma(-0.5 * x * r, r, 1.5);
+    r = r * fma(-0.5 * x * r, r, 1.5);
+    const double nrm = x * r;
     beta = ar >= 0.0 ? -nrm : nrm;
-    tr_ = (beta - ar) / beta;
-    ti_ = -ai / beta;
-    const double dr = ar - beta, di = ai, id2 = 1.0 / fma(dr, dr, di * di);
+    const double ib = ar >= 0.0 ? -r : r;  // 1 / beta
+    tr_ = (beta - ar) * ib;
+    ti_ = -ai * ib;
+    const double dr = ar - beta, di = ai, d2 = fma(dr, dr, di * di);
+    double id2 = __builtin_amdgcn_rcp(d2);
+    id2 = id2 * fma(-d2, id2, 2.0);
+    id2 = id2 * fma(-d2, id2, 2.0);
     cr = dr * id2, ci = -di * id2;
   }
 #pragma unroll

@@ -1,0 +1,67 @@
+"""Single-workgroup timing of the register Jacobi's phases (run under rocprofv3 --kernel-trace).
+
+    rocprofv3 --kernel-trace -d gpurun_out/svdph -o run -- python3 tools/svd_phase_timing.py [reps]
+    python3 tools/svd_phase_timing.py --report gpurun_out/svdph/run_results.db [reps]
+
+A swap-routed two-site theta of the bench's random chi = 64 state (sites 24, 25) is decomposed
+`reps` times with the QR phase only (aqc_svd_debug stop_after_qr = 1), then `reps` times in full;
+the report splits the k_jacobi_reg dispatches in launch order.
+"""
+import ctypes
+import os
+import sqlite3
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def swap_theta(seed=1000, site=24):
+    import bench
+
+    gam, lam = bench.random_vidal_mps(50, 64, seed)
+    G0 = np.stack(gam[site])
+    G1 = np.stack(gam[site + 1])
+    ll, lm, lr = lam[site - 1], lam[site], lam[site + 1]
+    # theta[s1, l, s2, r] = ll[l] G0[s1, l, m] lm[m] G1[s2, m, r] lr[r]
+    th = np.einsum("l,alm,m,bmr,r->albr", ll, G0, lm, G1, lr)
+    th = th.transpose(2, 1, 0, 3)  # SWAP: (s2, l, s1, r)
+    chl, chr_ = G0.shape[1], G1.shape[2]
+    return th.reshape(2 * chl, 2 * chr_)
+
+
+def run(reps):
+    from adaptaqc_amd import _lib
+
+    T = swap_theta()
+    m, n = T.shape
+    th = np.asfortranarray(T.astype(np.complex128)).ravel(order="F").view(np.float64).copy()
+    w = np.zeros(2 * m * n)
+    sig = np.zeros(max(m, n))
+    perm = np.zeros(max(m, n), dtype=np.int32)
+    sw = ctypes.c_int()
+    L = _lib.lib()
+    for qr_only in (1, 0):
+        for _ in range(reps):
+            _lib.check(L.aqc_svd_debug(_lib.ptr(th), m, n, 2, qr_only, _lib.ptr(w), _lib.ptr(sig),
+                                       _lib.ptr(perm), ctypes.byref(sw)))
+        print(f"stop_after_qr={qr_only}: sweeps={sw.value}", flush=True)
+    print("sigma[:4]", sig[:4], "min", sig[:min(m, n)].min())
+
+
+def report(db, reps):
+    c = sqlite3.connect(db)
+    rows = c.execute("select name, duration from kernels order by start").fetchall()
+    d = [du for nm, du in rows if "k_jacobi_reg" in nm]
+    qr, full = d[:reps], d[reps:2 * reps]
+    print(f"QR phase: {np.mean(qr) / 1e3:.1f} us; full: {np.mean(full) / 1e3:.1f} us "
+          f"(sweeps phase {np.mean(full) / 1e3 - np.mean(qr) / 1e3:.1f} us)")
+
+
+if __name__ == "__main__":
+    if sys.argv[1:2] == ["--report"]:
+        report(sys.argv[2], int(sys.argv[3]) if len(sys.argv) > 3 else 5)
+    else:
+        run(int(sys.argv[1]) if len(sys.argv) > 1 else 5)
