@@ -9,6 +9,7 @@
 // and writes the tile back.  A segment therefore costs one HBM/MALL pass (32 * 2^n bytes)
 // regardless of how many gates it holds.
 #include <algorithm>
+#include <array>
 #include <cstring>
 
 #include "aqc_internal.h"
@@ -45,7 +46,6 @@ __global__ __launch_bounds__(kThreads) void k_sv_segment(cplx* __restrict__ stat
                                                          const SegHeader* __restrict__ hdr,
                                                          const SegGate* __restrict__ gates) {
   __shared__ cplx tile[1 << K];
-  __shared__ SegGate g_s;
   constexpr int kPer = (1 << K) / kThreads > 0 ? (1 << K) / kThreads : 1;
   const int tid = threadIdx.x;
   int tb[K];
@@ -68,10 +68,8 @@ __global__ __launch_bounds__(kThreads) void k_sv_segment(cplx* __restrict__ stat
   const int ng = hdr->ngates;
   const SegGate* gp = gates + hdr->gate_off;
   for (int gi = 0; gi < ng; ++gi) {
-    __syncthreads();
-    if (tid < (int)(sizeof(SegGate) / 8)) {
-      reinterpret_cast<double*>(&g_s)[tid] = reinterpret_cast<const double*>(gp + gi)[tid];
-    }
+    // the gate is wave-uniform: read it with scalar loads (no LDS staging, one barrier per gate)
+    const SegGate& g_s = gp[gi];
     __syncthreads();
     if (g_s.nq == 1) {
       const int t = g_s.t0;
@@ -218,6 +216,117 @@ std::vector<HostSeg> build_segments(const aqc_op_t* ops, int nops, int K, int n)
     segs.push_back(std::move(seg));
   }
   return segs;
+}
+
+// ---- host-side gate fusion inside a segment -------------------------------------------------
+// Every 1-qubit gate is multiplied into the last fused op on its qubit (1- or 2-qubit), or into
+// the next 2-qubit gate on it when that gate comes first; consecutive 2-qubit gates on the same
+// pair become one 4x4.  Valid because the merged ops are adjacent on their qubits (everything in
+// between acts on other qubits and commutes).  Aer fuses too (fusion_enable at >= 14 qubits);
+// here every tile pass saves one LDS sweep and one barrier per absorbed gate.  Brickwork: 3 ops
+// per pair and layer become 1.
+typedef std::array<cplx, 16> Mat4;
+
+static Mat4 mat4_mul(const Mat4& a, const Mat4& b) {  // a b
+  Mat4 c;
+  for (int r = 0; r < 4; ++r)
+    for (int k = 0; k < 4; ++k) {
+      cplx acc = aqc::cmk(0, 0);
+      for (int j = 0; j < 4; ++j) acc = aqc::cfma(a[4 * r + j], b[4 * j + k], acc);
+      c[4 * r + k] = acc;
+    }
+  return c;
+}
+
+// 1-qubit u on bit `which` (0: the op's t0, 1: its t1) of a 4x4 (index 2 b1 + b0)
+static Mat4 embed1(const cplx* u, int which) {
+  Mat4 m;
+  for (int r = 0; r < 4; ++r)
+    for (int c = 0; c < 4; ++c) {
+      const int r0 = r & 1, r1 = r >> 1, c0 = c & 1, c1 = c >> 1;
+      cplx v = aqc::cmk(0, 0);
+      if (which == 0 && r1 == c1) v = u[2 * r0 + c0];
+      if (which == 1 && r0 == c0) v = u[2 * r1 + c1];
+      m[4 * r + c] = v;
+    }
+  return m;
+}
+
+static Mat4 swap_bits(const Mat4& a) {  // the same operator with t0 and t1 exchanged
+  Mat4 m;
+  auto sw = [](int x) { return ((x & 1) << 1) | (x >> 1); };
+  for (int r = 0; r < 4; ++r)
+    for (int c = 0; c < 4; ++c) m[4 * sw(r) + sw(c)] = a[4 * r + c];
+  return m;
+}
+
+std::vector<SegGate> fuse_segment(const aqc_op_t* ops, const std::vector<int>& idx, const int* local_of) {
+  struct F {
+    int nq, t0, t1;
+    Mat4 m;  // nq == 1: m[0..3] = 2x2
+    bool dead = false;
+  };
+  std::vector<F> f;
+  int last[64];
+  for (int q = 0; q < 64; ++q) last[q] = -1;
+  for (int gi : idx) {
+    const aqc_op_t& o = ops[gi];
+    cplx u[16];
+    const int nel = o.nq == 1 ? 4 : 16;
+    for (int e = 0; e < nel; ++e) u[e] = aqc::cmk(o.m[2 * e], o.m[2 * e + 1]);
+    if (o.nq == 1) {
+      const int q = local_of[o.q0];
+      const int k = last[q];
+      if (k >= 0 && f[k].nq == 1) {  // 2x2 product u * m
+        Mat4 c = f[k].m;
+        for (int r = 0; r < 2; ++r)
+          for (int cc = 0; cc < 2; ++cc) c[2 * r + cc] = aqc::cfma(u[2 * r + 1], f[k].m[2 + cc], aqc::cmul(u[2 * r], f[k].m[cc]));
+        f[k].m = c;
+      } else if (k >= 0) {
+        f[k].m = mat4_mul(embed1(u, f[k].t0 == q ? 0 : 1), f[k].m);
+      } else {
+        F n;
+        n.nq = 1, n.t0 = q, n.t1 = 0;
+        n.m = Mat4{};
+        for (int e = 0; e < 4; ++e) n.m[e] = u[e];
+        f.push_back(n);
+        last[q] = (int)f.size() - 1;
+      }
+      continue;
+    }
+    const int a = local_of[o.q0], b = local_of[o.q1];
+    Mat4 g;
+    for (int e = 0; e < 16; ++e) g[e] = u[e];
+    const int ka = last[a], kb = last[b];
+    if (ka >= 0 && ka == kb && f[ka].nq == 2) {  // same pair again
+      f[ka].m = mat4_mul(f[ka].t0 == a ? g : swap_bits(g), f[ka].m);
+      continue;
+    }
+    // absorb pending single-qubit ops on a / b (their last op, nothing after them on that qubit)
+    Mat4 m = g;
+    if (ka >= 0 && f[ka].nq == 1) {
+      m = mat4_mul(m, embed1(f[ka].m.data(), 0));
+      f[ka].dead = true;
+    }
+    if (kb >= 0 && f[kb].nq == 1) {
+      m = mat4_mul(m, embed1(f[kb].m.data(), 1));
+      f[kb].dead = true;
+    }
+    F n;
+    n.nq = 2, n.t0 = a, n.t1 = b, n.m = m;
+    f.push_back(n);
+    last[a] = last[b] = (int)f.size() - 1;
+  }
+  std::vector<SegGate> out;
+  for (const F& x : f) {
+    if (x.dead) continue;
+    SegGate g;
+    std::memset(&g, 0, sizeof(g));
+    g.nq = x.nq, g.t0 = x.t0, g.t1 = x.t1;
+    for (int e = 0; e < (x.nq == 1 ? 4 : 16); ++e) g.m[e] = x.m[e];
+    out.push_back(g);
+  }
+  return out;
 }
 
 }  // namespace
@@ -474,18 +583,9 @@ int aqc_sv_apply(aqc_sv_t h, const aqc_op_t* ops, int nops) {
       local_of[pos[j]] = j;
     }
     hdr[s].gate_off = (int)gts.size();
-    hdr[s].ngates = (int)segs[s].gates.size();
-    for (int gi : segs[s].gates) {
-      const aqc_op_t& o = ops[gi];
-      SegGate g;
-      std::memset(&g, 0, sizeof(g));
-      g.nq = o.nq;
-      g.t0 = local_of[o.q0];
-      g.t1 = o.nq == 2 ? local_of[o.q1] : 0;
-      const int nel = o.nq == 1 ? 4 : 16;
-      for (int e = 0; e < nel; ++e) g.m[e] = aqc::cmk(o.m[2 * e], o.m[2 * e + 1]);
-      gts.push_back(g);
-    }
+    const std::vector<SegGate> fused = fuse_segment(ops, segs[s].gates, local_of);
+    hdr[s].ngates = (int)fused.size();
+    gts.insert(gts.end(), fused.begin(), fused.end());
   }
   if (hdr.size() > h->hdr_cap) {
     AQC_HIP_CHECK(hipStreamSynchronize(h->stream));

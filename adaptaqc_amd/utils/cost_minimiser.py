@@ -17,6 +17,17 @@ from .utilityfunctions import has_stopped_improving, minimum_of_sinusoidal
 logger = logging.getLogger(__name__)
 ALG_SCIPY = "scipy"
 
+# Candidate axes whose fitted costs agree to within this (costs live in [0, 1]) are ties: the
+# first in SUPPORTED_1Q_GATES order wins, as for exact ties in the reference's strict `<`
+# (cost_minimiser.py:335-340).  Without it, exact ties (e.g. an identity-optimal rotation, where
+# every axis gives the same cost) are broken by last-bit rounding, which differs between the
+# full re-simulation and the cached transition-matrix path.
+_TIE = 1e-13
+
+
+def _improves(cost, best_cost, best_name):
+    return cost < best_cost and (best_name is None or cost < best_cost - _TIE)
+
 
 class CostMinimiser:
     def __init__(self, cost_finder, variational_circuit_range, full_circuit, rotosolve_fraction=1.0,
@@ -107,7 +118,7 @@ class CostMinimiser:
                 best_name, best_angle, best_cost = None, None, 1
                 for k, name in enumerate(names):
                     angle, cst = minimum_of_sinusoidal(c[0], c[1 + 2 * k], c[2 + 2 * k])
-                    if cst < best_cost:
+                    if _improves(cst, best_cost, best_name):
                         best_name, best_angle, best_cost = name, angle, cst
                 co.replace_1q_gate(self.full_circuit, index, best_name, best_angle)
                 cost = best_cost
@@ -126,7 +137,7 @@ class CostMinimiser:
         best_name, best_angle, best_cost = None, None, 1
         for name in co.SUPPORTED_1Q_GATES:
             angle, cost = self.find_best_angle(gate_index, name, cost_identity)
-            if cost < best_cost:
+            if _improves(cost, best_cost, best_name):
                 best_name, best_angle, best_cost = name, angle, cost
         co.replace_1q_gate(self.full_circuit, gate_index, best_name, best_angle)
         return best_cost

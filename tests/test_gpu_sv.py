@@ -122,3 +122,27 @@ def test_small_and_segment_edge_sizes():
         d = DeviceSV(n)
         d.apply(device_ops(to_circuit(n, ops)))
         np.testing.assert_allclose(d.get(), osv.simulate(n, ops), atol=1e-12, err_msg=f"n={n}")
+
+
+def test_gate_fusion_patterns():
+    """Host fusion (1q into 2q, repeated and reversed pairs, pending 1q on both sides) is exact."""
+    from adaptaqc_amd.circuit import device_ops
+    from adaptaqc_amd.device import DeviceSV
+
+    rng = np.random.default_rng(17)
+    for n in (3, 6, 12):
+        ops = []
+        for _ in range(120):
+            k = rng.integers(6)
+            a, b = (int(x) for x in rng.choice(n, 2, replace=False))
+            if k < 3:
+                ops.append((["rx", "ry", "rz"][k], (a,), (rng.uniform(-np.pi, np.pi),)))
+            elif k == 3:
+                ops.append(("cx", (a, b), ()))
+            elif k == 4:
+                ops += [("cx", (a, b), ()), ("cx", (b, a), ()), ("rz", (b,), (0.4,)), ("cz", (a, b), ())]
+            else:
+                ops += [("h", (a,), ()), ("swap", (a, b), ()), ("ry", (a,), (1.3,))]
+        d = DeviceSV(n)
+        d.apply(device_ops(to_circuit(n, ops)))
+        np.testing.assert_allclose(d.get(), osv.simulate(n, ops), atol=1e-12, err_msg=f"n={n}")
