@@ -475,9 +475,14 @@ __global__ __launch_bounds__(CP * 8) void k_jacobi_reg(const TwoSiteJob* __restr
   if ((tid & 63) == 0) fred[tid >> 6] = f;
   if (tid == 0) pkey[0] = pkey[1] = 0ull;
   __syncthreads();
-  double fro = 0.0;
+  // ||W||_F^2 is needed only after the QR: sum it now into fred[0] (one thread, ordered by the
+  // QR's first barrier) rather than keep 16 partials live -- they were spilled to scratch
+  if (tid == 0) {
+    double s = 0.0;
 #pragma unroll
-  for (int w = 0; w < kThreads / 64; ++w) fro += fred[w];
+    for (int w = 0; w < kThreads / 64; ++w) s += fred[w];
+    fred[0] = s;
+  }
   int Lj = L;  // row count of the matrix the Jacobi sees
   if (use_qr) {
     int ks = -1, km = -1;  // pivot step of S / M (-1: not pivoted yet)
@@ -570,7 +575,8 @@ __global__ __launch_bounds__(CP * 8) void k_jacobi_reg(const TwoSiteJob* __restr
     }
     Lj = C;
   }
-  const double floor2 = fro * 1e-24;
+  __syncthreads();
+  const double floor2 = fred[0] * 1e-24;
   const double tol = j.jtol * (double)Lj * 2.220446049250313e-16;
   const double tol2 = tol * tol;
   const int max_sweeps = j.dbg == 1 ? 0 : kMaxSweeps;

@@ -33,6 +33,7 @@ DISTANCES = (1, 2, 5, 25)
 LAYER_A = 12
 FP64_PEAK_TFLOPS = 78.6  # MI355X dense FP64 (vector = matrix), MI355X_MICROARCH.md / SURVEY 8(d)
 HBM_PEAK_GBS = 8000.0
+TRAFFIC_JSON = "r1_traffic.json"
 
 
 def random_vidal_mps(n, chi, seed):
@@ -247,6 +248,15 @@ def main():
                 "peak": HBM_PEAK_GBS, "unit": "GB/s"}
     roof["frac"] = roof["achieved"] / roof["peak"]
     roof["traffic"] = None
+    # HBM bytes per launch of the same kernel and launch mix from the committed PMC passes
+    # (tools/pmc_bench.sh: rocprofv3 FETCH_SIZE x 2 + WRITE_SIZE, MI355X_MICROARCH.md corrections)
+    tj = os.path.join(ROOT, "profiles", TRAFFIC_JSON)
+    if dom == "mps_svd" and os.path.exists(tj):
+        with open(tj) as fh:
+            tr = json.load(fh)
+        roof["traffic"] = tr["traffic_bytes_per_launch"]
+        roof["traffic_source"] = f"profiles/{TRAFFIC_JSON} ({tr['kernel']}, rocprofv3 PMC)"
+        roof["algorithmic_bytes_per_launch"] = fd["bytes"] / launches
     roof["avg_launch_ms"] = avg_ms
     roof["launches"] = fd["launches"]
 
