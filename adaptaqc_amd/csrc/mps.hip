@@ -1326,7 +1326,7 @@ Staging& staging() {
   return s[dev];
 }
 
-TwoSiteJob make_two(aqc_mps_t h, const DevOp& op) {
+TwoSiteJob make_two(aqc_mps_t h, const DevOp& op, int slot = 0) {
   TwoSiteJob j;
   std::memset(&j, 0, sizeof(j));
   const int p = op.p;
@@ -1336,10 +1336,18 @@ TwoSiteJob make_two(aqc_mps_t h, const DevOp& op) {
   j.lm = h->d.bond(p + 1);
   j.lr = h->d.bond(p + 2);
   j.dims = h->d.dims + p;
-  j.theta = h->d.theta;
-  j.work = h->d.work;
-  j.sig = h->d.sig;
-  j.perm = h->d.perm;
+  if (slot == 0) {
+    j.theta = h->d.theta;
+    j.work = h->d.work;
+    j.sig = h->d.sig;
+    j.perm = h->d.perm;
+  } else {
+    const aqc_mps_s::Slot& sl = h->slots[slot - 1];
+    j.theta = sl.theta;
+    j.work = sl.work;
+    j.sig = sl.sig;
+    j.perm = sl.perm;
+  }
   j.flags = h->d.flags;
   j.cap = h->d.cap;
   j.max_chi = h->max_chi;
@@ -1360,10 +1368,59 @@ OneSiteJob make_one(aqc_mps_t h, const DevOp& op) {
 }
 
 // Run per-state device-op lists in lock-step waves on the MPS stream.
+// Extra two-site workspace (theta, W, sigma, perm) of `h` for concurrent updates of one state;
+// slot 0 is the handle's own workspace.
+int ensure_slots(aqc_mps_t h, int nslots) {
+  const size_t cap = h->d.cap;
+  while ((int)h->slots.size() + 1 < nslots) {
+    aqc_mps_s::Slot sl;
+    AQC_HIP_CHECK(hipMalloc(&sl.theta, 4 * cap * cap * sizeof(cplx)));
+    AQC_HIP_CHECK(hipMalloc(&sl.work, 4 * cap * cap * sizeof(cplx)));
+    AQC_HIP_CHECK(hipMalloc(&sl.sig, 1024 * sizeof(double)));
+    AQC_HIP_CHECK(hipMalloc(&sl.perm, 512 * sizeof(int)));
+    h->slots.push_back(sl);
+  }
+  return AQC_OK;
+}
+
+// Level each state's device-op list: an op goes one level after the last op touching one of its
+// sites.  Two-site updates at p and q with |p - q| >= 2 touch disjoint sites and bonds (the update
+// at p reads lambda_p, lambda_{p+1}, lambda_{p+2} and writes Gamma_p, Gamma_{p+1}, lambda_{p+1}),
+// so they commute exactly -- truncation included -- and one brickwork layer becomes one wave.
+std::vector<std::vector<const DevOp*>> level_ops(const std::vector<DevOp>& ops, int n) {
+  std::vector<int> last(n + 1, -1);
+  std::vector<std::vector<const DevOp*>> lv;
+  for (const DevOp& op : ops) {
+    int l;
+    if (op.kind == 2) {
+      l = std::max(last[op.p], last[op.p + 1]) + 1;
+      last[op.p] = last[op.p + 1] = l;
+    } else {
+      l = last[op.p] + 1;
+      last[op.p] = l;
+    }
+    if ((int)lv.size() <= l) lv.resize(l + 1);
+    lv[l].push_back(&op);
+  }
+  return lv;
+}
+
 int run_waves(aqc_mps_t* hs, int ns, std::vector<std::vector<DevOp>>& lists) {
   hipStream_t st = aqc::mps_stream();
+  std::vector<std::vector<std::vector<const DevOp*>>> lv(ns);
   size_t maxlen = 0;
-  for (auto& l : lists) maxlen = std::max(maxlen, l.size());
+  for (int s = 0; s < ns; ++s) {
+    lv[s] = level_ops(lists[s], hs[s]->d.n);
+    maxlen = std::max(maxlen, lv[s].size());
+    int width = 1;
+    for (auto& w : lv[s]) {
+      int k = 0;
+      for (const DevOp* op : w) k += op->kind == 2;
+      width = std::max(width, k);
+    }
+    int rc = ensure_slots(hs[s], width);
+    if (rc != AQC_OK) return rc;
+  }
   if (maxlen == 0) return AQC_OK;
   // pre-build every wave's jobs into one staging buffer
   std::vector<TwoSiteJob> two;
@@ -1376,13 +1433,15 @@ int run_waves(aqc_mps_t* hs, int ns, std::vector<std::vector<DevOp>>& lists) {
   for (size_t w = 0; w < maxlen; ++w) {
     size_t t0 = two.size(), o0 = one.size();
     for (int s = 0; s < ns; ++s) {
-      if (w >= lists[s].size()) continue;
-      const DevOp& op = lists[s][w];
-      if (op.kind == 2) {
-        two.push_back(make_two(hs[s], op));
-        two.back().qr = use_qr;
-      } else {
-        one.push_back(make_one(hs[s], op));
+      if (w >= lv[s].size()) continue;
+      int slot = 0;
+      for (const DevOp* op : lv[s][w]) {
+        if (op->kind == 2) {
+          two.push_back(make_two(hs[s], *op, slot++));
+          two.back().qr = use_qr;
+        } else {
+          one.push_back(make_one(hs[s], *op));
+        }
       }
     }
     two_rng[w] = {t0, two.size() - t0};
@@ -1627,6 +1686,12 @@ int aqc_mps_destroy(aqc_mps_t h) {
   hipFree(h->d.scal);
   if (h->d.env) hipFree(h->d.env);
   if (h->gw) hipFree(h->gw);
+  for (auto& sl : h->slots) {
+    hipFree(sl.theta);
+    hipFree(sl.work);
+    hipFree(sl.sig);
+    hipFree(sl.perm);
+  }
   delete h;
   return AQC_OK;
 }

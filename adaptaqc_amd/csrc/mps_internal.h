@@ -133,4 +133,12 @@ struct aqc_mps_s {
   // scratch for the candidate sweep (grad.hip), allocated lazily
   aqc::cplx* gw = nullptr;
   size_t gw_bytes = 0;
+  // extra two-site workspaces for concurrent updates of disjoint bonds (mps.hip run_waves)
+  struct Slot {
+    aqc::cplx* theta = nullptr;
+    aqc::cplx* work = nullptr;
+    double* sig = nullptr;
+    int* perm = nullptr;
+  };
+  std::vector<Slot> slots;
 };
