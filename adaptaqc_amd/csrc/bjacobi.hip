@@ -59,25 +59,65 @@ __device__ __forceinline__ void job_shape(const TwoSiteJob& j, int& L, int& C, b
 // round-robin tournament on c (even) players: position 0 fixed, the others rotate
 __device__ __forceinline__ int rr(int pos, int r, int c) { return pos == 0 ? 0 : ((pos - 1 + r) % (c - 1)) + 1; }
 
-// W <- theta (or theta^H when M < N), ||W||_F^2 into st.fro.  grid (chunks, nj).
-__global__ __launch_bounds__(256) void k_bj_init(const TwoSiteJob* __restrict__ jobs, BJState* __restrict__ st) {
-  const TwoSiteJob& j = jobs[blockIdx.y];
+// W <- theta (or theta^H when M < N) with the columns in descending norm order, ||W||_F^2 into
+// st.fro.  One workgroup per job.  The column order of W is free (k_rank sorts the singular
+// values, k_split recovers the other side from theta), and a one-sided Jacobi started on
+// norm-sorted columns converges in fewer sweeps (de Rijk).  grid (nj), 1024 threads.
+__global__ __launch_bounds__(1024) void k_bj_init(const TwoSiteJob* __restrict__ jobs, BJState* __restrict__ st) {
+  const TwoSiteJob& j = jobs[blockIdx.x];
   int L, C;
   bool tr;
   job_shape(j, L, C, tr);
   const int M = 2 * j.dims[0];
+  __shared__ double key[512];
+  __shared__ int idx[512];
+  __shared__ double red[16];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  auto elem = [&](int row, int col) -> cplx {
+    return tr ? cconj(j.theta[(size_t)row * M + col]) : j.theta[(size_t)col * M + row];
+  };
   double f = 0.0;
-  for (int idx = blockIdx.x * 256 + threadIdx.x; idx < L * C; idx += gridDim.x * 256) {
-    const int col = idx / L, row = idx - col * L;
-    const cplx v = tr ? cconj(j.theta[(size_t)row * M + col]) : j.theta[(size_t)col * M + row];
-    j.work[idx] = v;
-    f = fma(v.x, v.x, fma(v.y, v.y, f));
+  for (int c = w; c < 512; c += 16) {  // column norms, one wave per column
+    double x = 0.0;
+    if (c < C)
+      for (int r = lane; r < L; r += 64) {
+        const cplx v = elem(r, c);
+        x = fma(v.x, v.x, fma(v.y, v.y, x));
+      }
+    x = wave_sum(x);
+    f += x;
+    if (lane == 0) key[c] = c < C ? x : -1.0, idx[c] = c;
   }
-  __shared__ double red[4];
-  f = wave_sum(f);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = f;
+  if (lane == 0) red[w] = f;
   __syncthreads();
-  if (threadIdx.x == 0) atomicAdd(&st[blockIdx.y].fro, red[0] + red[1] + red[2] + red[3]);
+  // bitonic sort of 512 (key, idx), descending key (padding keys -1 sink to the end)
+  for (int k = 2; k <= 512; k <<= 1) {
+    for (int jj = k >> 1; jj > 0; jj >>= 1) {
+      const int i = threadIdx.x;
+      if (i < 512) {
+        const int l = i ^ jj;
+        if (l > i) {
+          const bool desc = (i & k) == 0;
+          const double a = key[i], b = key[l];
+          if (desc ? (a < b) : (a > b)) {
+            key[i] = b, key[l] = a;
+            const int t = idx[i];
+            idx[i] = idx[l], idx[l] = t;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int c = w; c < C; c += 16) {
+    const int src = idx[c];
+    for (int r = lane; r < L; r += 64) j.work[(size_t)c * L + r] = elem(r, src);
+  }
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int q = 0; q < 16; ++q) t += red[q];
+    st[blockIdx.x].fro = t;
+  }
 }
 
 // One pair rotation of scaled columns a = da * (sr, si), b = db * (mr, mi) with tracked squared
@@ -381,8 +421,7 @@ int run_block_jacobi(const TwoSiteJob* jobs, int nj, int cap_max, hipStream_t st
   int nb = (L + kB - 1) / kB;
   nb += nb & 1;
   const size_t lds = (size_t)kB * 64 * MAXR * sizeof(double2);
-  const int chunks = std::max(1, std::min(1024, L * L / 1024));
-  hipLaunchKernelGGL(k_bj_init, dim3(chunks, nj), dim3(256), 0, stream, jobs, b.st);
+  hipLaunchKernelGGL(k_bj_init, dim3(nj), dim3(1024), 0, stream, jobs, b.st);
   AQC_CHECK_LAUNCH();
   for (int sweep = 0; sweep < kMaxSweepsBJ; ++sweep) {
     hipLaunchKernelGGL((k_bj_intra<MAXR>), dim3(nb, nj), dim3(512), lds, stream, jobs, b.st);
