@@ -36,12 +36,11 @@ HBM_PEAK_GBS = 8000.0
 TRAFFIC_JSON = "r1_traffic.json"
 
 
-def random_vidal_mps(n, chi, seed):
-    """Random normalised MPS in exact Vidal canonical form (Aer tuple)."""
-    rng = np.random.default_rng(seed)
-    dims = [min(2 ** k, 2 ** (n - k), chi) for k in range(n + 1)]
-    A = [(rng.standard_normal((2, dims[i], dims[i + 1])) + 1j * rng.standard_normal((2, dims[i], dims[i + 1])))
-         for i in range(n)]
+def vidal_from_tensors(A):
+    """Vidal canonical form (Aer tuple) of the MPS with site tensors A[i] of shape (2, l, r):
+    left-canonicalise by QR, then right-to-left SVDs give the lambdas; normalised."""
+    A = [np.asarray(a, dtype=complex).copy() for a in A]
+    n = len(A)
     for i in range(n - 1):  # left-canonicalise
         s, l, r = A[i].shape
         q, rr = np.linalg.qr(A[i].transpose(1, 0, 2).reshape(l * s, r))
@@ -65,6 +64,16 @@ def random_vidal_mps(n, chi, seed):
             g = g / lam[i + 1][None, None, :]
         gam.append((g[0].copy(), g[1].copy()))
     return gam, [lam[i] for i in range(1, n)]
+
+
+def random_vidal_mps(n, chi, seed):
+    """Random normalised MPS in exact Vidal canonical form (Aer tuple): bonds min(2^k, 2^(n-k), chi),
+    complex-normal tensors."""
+    rng = np.random.default_rng(seed)
+    dims = [min(2 ** k, 2 ** (n - k), chi) for k in range(n + 1)]
+    A = [(rng.standard_normal((2, dims[i], dims[i + 1])) + 1j * rng.standard_normal((2, dims[i], dims[i + 1])))
+         for i in range(n)]
+    return vidal_from_tensors(A)
 
 
 def thin_layer_ops(a, b, angles):

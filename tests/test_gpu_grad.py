@@ -167,3 +167,53 @@ def test_argmax_c_abi_tie_break():
         best = ctypes.c_int()
         _lib.check(_lib.lib().aqc_argmax_scaled(_lib.ptr(s), _lib.ptr(p), len(s), 0, ctypes.byref(best)))
         assert best.value == int(np.argmax(s * p))
+
+
+def _near_zero_state(n, chi, seed, alpha=0.6):
+    """|psi> ~ alpha |p> + |phi>: |p> a product of single-qubit states near |0> (angles 0.15),
+    phi random, normalised, with bonds min(2^k - 1, 2^(n-k) - 1, chi - 1) -- every bond of psi at
+    min(2^k, 2^(n-k), chi), and gradients far from zero (for a random chi = 128 state every overlap
+    with a |0..0>-like state is ~1e-8)."""
+    from bench import random_vidal_mps, vidal_from_tensors
+
+    rng = np.random.default_rng(seed)
+    dims = [1] + [min(2 ** k - 1, 2 ** (n - k) - 1, chi - 1) for k in range(1, n)] + [1]
+    A = [(rng.standard_normal((2, dims[i], dims[i + 1])) + 1j * rng.standard_normal((2, dims[i], dims[i + 1])))
+         for i in range(n)]
+    gam, lam = vidal_from_tensors(A)
+    phi = [np.stack(g) * (lam[i][None, None, :] if i < n - 1 else 1.0) for i, g in enumerate(gam)]
+    out = []
+    for i, t in enumerate(phi):  # block-diagonal sum with the |0> product chain
+        s, l, r = t.shape
+        li, ri = (1 if i == 0 else l + 1), (1 if i == n - 1 else r + 1)
+        x = np.zeros((2, li, ri), dtype=complex)
+        a, b = 0.15 * (1 + rng.random()), rng.uniform(-np.pi, np.pi)
+        x[:, 0, 0] = (alpha if i == 0 else 1.0) * np.array([np.cos(a), np.exp(1j * b) * np.sin(a)])
+        x[:, li - l:, ri - r:] = t
+        out.append(x)
+    return vidal_from_tensors(out)
+
+
+def test_config4_full_size_chi128_vs_oracle():
+    """Config 4 size: 50 qubits, chi = 128, identity_resolvable generators, |s> = |0..0>, all 1225
+    pairs vs the oracle's environment form (itself pinned to the reference structure)."""
+    import bench
+    from adaptaqc_amd.device import DeviceMPS, pair_grads_batch
+    from adaptaqc_amd.utils import ansatzes
+
+    n, chi = 50, 128
+    aer = _near_zero_state(n, chi, 3)
+    d = DeviceMPS(n, chi, 1e-16, chi)
+    d.load_aer(aer)
+    assert d.dims().max() == chi
+    cmap = adapt_host.coupling_map_full(n)
+    layer, gens, deg, u0, gm = bench.layer_inputs()
+    svec = np.zeros((n, 2), complex)
+    svec[:, 0] = 1.0
+    got = pair_grads_batch([d], svec, cmap, u0, gm, deg)[0]
+    o_layer = [(i.operation.name, i.qubits, tuple(i.operation.params)) for i in ansatzes.identity_resolvable().data]
+    o_gens, o_deg = ogr.get_generators_and_degeneracies(o_layer, True, True)
+    psi = M.MPS.from_aer(aer).preprocessed()
+    ref = ogr.general_grad_of_pairs_env(psi, n, ogr.inverse_ops(o_layer), o_gens, o_deg, cmap)
+    assert np.max(ref) > 1e-3
+    np.testing.assert_allclose(got, ref, atol=1e-10)
