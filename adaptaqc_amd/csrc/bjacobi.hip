@@ -143,13 +143,13 @@ __device__ __forceinline__ bool rotate_pair(double (&sr)[MAXR], double (&si)[MAX
   const double g2 = gx * gx + gy * gy;
   const double ab = na * nb;
   if (!(g2 > tol2 * ab && na > floor2 && nb > floor2)) return false;
-  double t, c, p, rg;
-  jacobi_tc(na, nb, g2, t, c, p, rg);
+  double te, c, p;  // te = t / |g|, p = 1 + t^2
+  jacobi_te(na, nb, g2, te, c, p);
   if (g2 > 16.0 * tol2 * ab) {
     rot = 1;
-    if (fabs(t) > kTinyT) big = 1;
+    if (p - 1.0 > kTinyT * kTinyT) big = 1;
   }
-  const double ra = db * ida, ira = da * idb, te = t * rg;
+  const double ra = db * ida, ira = da * idb;
   const double mux = te * gx * ra, muy = -te * gy * ra;
   const double nux = te * gx * ira, nuy = te * gy * ira;
 #pragma unroll
@@ -167,7 +167,7 @@ __device__ __forceinline__ bool rotate_pair(double (&sr)[MAXR], double (&si)[MAX
   }
   const double ic = p * c;
   da *= c, ida *= ic, db *= c, idb *= ic;
-  const double tg = t * (g2 * rg);
+  const double tg = te * g2;
   double na2 = na - tg, nb2 = nb + tg;
   if (na2 < 1e-6 * na || nb2 < 1e-6 * nb) {
     double x = 0, y = 0;

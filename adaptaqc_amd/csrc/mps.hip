@@ -370,7 +370,7 @@ __global__ __launch_bounds__(JT) void k_jacobi(const TwoSiteJob* __restrict__ jo
 // handles by flipping its side test (tools/qrp_jacobi_proto.py is the numpy restatement).
 
 using aqc::jacobi_params;
-using aqc::jacobi_tc;
+using aqc::jacobi_te;
 
 // sortable pivot key: non-negative double bits with the low byte replaced by (255 - id), so
 // that the 64-bit maximum is the largest trailing norm, ties to the lowest column id
@@ -670,14 +670,13 @@ __global__ __launch_bounds__(CP * 8) void k_jacobi_reg(const TwoSiteJob* __restr
         if (g2 > tol2 * ab && sn > floor2 && mn > floor2) {
           // only rotations above dot-product noise keep the sweep loop going: a pair of
           // (near-)degenerate columns can otherwise flip-flop at |g| ~ tol forever
-          double t, c, p, rg;
-          jacobi_tc(sn, mn, g2, t, c, p, rg);
+          double te, c, p;  // te = t / |g|, p = 1 + t^2
+          jacobi_te(sn, mn, g2, te, c, p);
           if (g2 > 16.0 * tol2 * ab) {
             my_rot = 1;
-            if (fabs(t) > kTinyT) my_big = 1;
+            if (p - 1.0 > kTinyT * kTinyT) my_big = 1;  // |t| > kTinyT
           }
           const double ra = md * isd, ira = sd * imd;  // d_b / d_a and its inverse
-          const double te = t * rg;
           const double mux = te * gx * ra, muy = -te * gy * ra;   // mu = t conj(e) d_b / d_a
           const double nux = te * gx * ira, nuy = te * gy * ira;  // nu = t e d_a / d_b
 #pragma unroll
@@ -691,7 +690,7 @@ __global__ __launch_bounds__(CP * 8) void k_jacobi_reg(const TwoSiteJob* __restr
           sd *= c;
           isd *= ic;
           const double md2 = md * c, imd2 = imd * ic;
-          const double tg = t * (g2 * rg);  // t |g|
+          const double tg = te * g2;  // t |g|
           double sn2 = sn - tg, mn2 = mn + tg;
           if (sn2 < 1e-6 * sn || mn2 < 1e-6 * mn) {  // cancellation: recompute exactly
             double a = 0, b = 0;

@@ -114,6 +114,26 @@ __device__ __forceinline__ void jacobi_tc(double al, double be, double g2, doubl
   c = cc;
 }
 
+// The same rotation without |g|: with h = (beta - alpha) / 2, t / |g| = sgn(h) / (|h| + sqrt(h^2 +
+// |g|^2)) =: te, so t e = te g, t |g| = te |g|^2 and p = 1 + t^2 = 1 + te^2 |g|^2.  One rsq and
+// one rcp, each with a single Newton step (their ~2^-23 seeds -> ~2^-46: the angle needs no more,
+// as long as c = 1 / sqrt(p) is exact for the t actually applied -- two Newton steps there).
+__device__ __forceinline__ void jacobi_te(double al, double be, double g2, double& te, double& c, double& p) {
+  const double h = 0.5 * (be - al);
+  const double q = fma(h, h, g2);
+  double rq = __builtin_amdgcn_rsq(q);
+  rq = rq * fma(-0.5 * q * rq, rq, 1.5);
+  const double den = fabs(h) + q * rq;
+  double inv = __builtin_amdgcn_rcp(den);
+  inv = inv * fma(-den, inv, 2.0);
+  te = h >= 0 ? inv : -inv;
+  p = fma(te * te, g2, 1.0);
+  double cc = __builtin_amdgcn_rsq(p);
+  cc = cc * fma(-0.5 * p * cc, cc, 1.5);
+  cc = cc * fma(-0.5 * p * cc, cc, 1.5);
+  c = cc;
+}
+
 // Multi-workgroup block one-sided Jacobi SVD for 2 * chi > 128 (bjacobi.hip): factors the nj
 // two-site thetas of `jobs` (device array) into the k_jacobi output contract (W columns = U sigma,
 // sig = column norms, qr = 0).  Enqueued on `st`; synchronises the host once per sweep (from the
