@@ -486,18 +486,39 @@ __global__ __launch_bounds__(CP * 8) void k_jacobi_reg(const TwoSiteJob* __restr
   int Lj = L;  // row count of the matrix the Jacobi sees
   if (use_qr) {
     int ks = -1, km = -1;  // pivot step of S / M (-1: not pivoted yet)
+    // Trailing squared norms (rows >= k) of S and M, downdated by the row leaving the trailing
+    // block at every step (n -= |x_{k-1}|^2, LAPACK xLAQP2's scheme) and recomputed exactly when
+    // they fall below sqrt(eps) of their last exact value (cancellation).
+    double ns = 0, nm = 0, nsr = 0, nmr = 0;
     for (int k = 0; k < C; ++k) {
       const int b = k & 1;
-      // trailing squared norms (rows >= k) of the unpivoted columns
-      double ns = 0, nm = 0;
+      bool exact = k == 0;
+      if (k > 0) {
+        const int kr = (k - 1) >> 4, kl = (k - 1) & 15;
+        double es = 0, em = 0;
 #pragma unroll
-      for (int i = 0; i < MAXR; ++i) {
-        const double w = (lane + 16 * i) >= k ? 1.0 : 0.0;
-        ns = fma(w, fma(sr[i], sr[i], si[i] * si[i]), ns);
-        nm = fma(w, fma(mr[i], mr[i], mi[i] * mi[i]), nm);
+        for (int i = 0; i < MAXR; ++i) {
+          if (i == kr) {
+            es = fma(sr[i], sr[i], si[i] * si[i]);
+            em = fma(mr[i], mr[i], mi[i] * mi[i]);
+          }
+        }
+        ns -= __shfl(es, kl, 16);
+        nm -= __shfl(em, kl, 16);
+        exact = ns <= 1.5e-8 * nsr || nm <= 1.5e-8 * nmr;
       }
-      ns = aqc::row_sum16(ns);
-      nm = aqc::row_sum16(nm);
+      if (exact) {
+        ns = 0, nm = 0;
+#pragma unroll
+        for (int i = 0; i < MAXR; ++i) {
+          const double w = (lane + 16 * i) >= k ? 1.0 : 0.0;
+          ns = fma(w, fma(sr[i], sr[i], si[i] * si[i]), ns);
+          nm = fma(w, fma(mr[i], mr[i], mi[i] * mi[i]), nm);
+        }
+        ns = aqc::row_sum16(ns);
+        nm = aqc::row_sum16(nm);
+        nsr = ns, nmr = nm;
+      }
       const unsigned long long ka = (ks < 0 && sid < C) ? pivot_key(ns, sid) : 0ull;
       const unsigned long long kb = (km < 0 && mid < C) ? pivot_key(nm, mid) : 0ull;
       if (lane == 0) atomicMax(&pkey[b], ka > kb ? ka : kb);
@@ -535,10 +556,10 @@ __global__ __launch_bounds__(CP * 8) void k_jacobi_reg(const TwoSiteJob* __restr
 #pragma unroll
       for (int i = 0; i < MAXR; ++i) {
         const double2 v = vb[b][lane + 16 * i];
-        sr[i] -= v.x * fsr - v.y * fsi;
-        si[i] -= v.x * fsi + v.y * fsr;
-        mr[i] -= v.x * fmr - v.y * fmi;
-        mi[i] -= v.x * fmi + v.y * fmr;
+        sr[i] = fma(-v.x, fsr, fma(v.y, fsi, sr[i]));  // 2 FMAs per component, not mul+fma+add
+        si[i] = fma(-v.x, fsi, fma(-v.y, fsr, si[i]));
+        mr[i] = fma(-v.x, fmr, fma(v.y, fmi, mr[i]));
+        mi[i] = fma(-v.x, fmi, fma(-v.y, fmr, mi[i]));
       }
     }
     // X = R^H: X[i][jx] = conj(R[jx][column pivoted at step i]); new S / M = X columns g, g + kG.
