@@ -21,7 +21,7 @@ struct GemmLds {
 // A_KFAST / B_KFAST choose the tile-load order: consecutive threads walk k (use when the source
 // is contiguous along k) instead of the output dimension.
 template <bool A_KFAST = false, bool B_KFAST = false, typename FA, typename FB, typename FS>
-__device__ __forceinline__ void block_cgemm(int m, int n, int k, FA a, FB b, FS store, GemmLds& lds) {
+__device__ __forceinline__ void block_cgemm_valu(int m, int n, int k, FA a, FB b, FS store, GemmLds& lds) {
   const int tid = threadIdx.x, ty = tid >> 4, tx = tid & 15;
   for (int bi = 0; bi < m; bi += 64) {
     for (int bj = 0; bj < n; bj += 64) {
@@ -61,6 +61,70 @@ __device__ __forceinline__ void block_cgemm(int m, int n, int k, FA a, FB b, FS 
           const int i = bi + 4 * ty + r, j = bj + 4 * tx + c;
           if (i < m && j < n) store(i, j, acc[r][c]);
         }
+    }
+  }
+}
+
+// The same contract on the FP64 matrix cores: each of the 4 waves owns a 32 x 32 quarter of the
+// 64 x 64 output block as 2 x 2 tiles of v_mfma_f64_16x16x4_f64 (A operand: lane l holds
+// A[l & 15][k = l >> 4], B: B[k = l >> 4][l & 15]; C/D: col = lane & 15, row = (lane >> 4) +
+// 4 * reg).  A complex product is four real MFMAs into two accumulators (Re += Ar Br + (-Ai) Bi,
+// Im += Ar Bi + Ai Br).  Per 16-deep k tile a wave reads 4 KB of operands from LDS for 64
+// MFMAs, against 32 KB for the register-blocked VALU form: the LDS port stops being the limit.
+typedef double __attribute__((ext_vector_type(4))) d4_t;
+
+template <bool A_KFAST = false, bool B_KFAST = false, typename FA, typename FB, typename FS>
+__device__ __forceinline__ void block_cgemm(int m, int n, int k, FA a, FB b, FS store, GemmLds& lds) {
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int wr = (wave >> 1) * 32, wc = (wave & 1) * 32;
+  const int li = lane & 15, lk = lane >> 4;
+  for (int bi = 0; bi < m; bi += 64) {
+    for (int bj = 0; bj < n; bj += 64) {
+      d4_t cr[2][2], ci[2][2];
+#pragma unroll
+      for (int r = 0; r < 2; ++r)
+#pragma unroll
+        for (int c = 0; c < 2; ++c) cr[r][c] = d4_t{0, 0, 0, 0}, ci[r][c] = d4_t{0, 0, 0, 0};
+      for (int k0 = 0; k0 < k; k0 += 16) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int e = tid + q * kGemmThreads;
+          const int ka = A_KFAST ? (e & 15) : (e >> 6), ia = A_KFAST ? (e >> 4) : (e & 63);
+          const int kb = B_KFAST ? (e & 15) : (e >> 6), ib = B_KFAST ? (e >> 4) : (e & 63);
+          lds.As[ka][ia] = (bi + ia < m && k0 + ka < k) ? a(bi + ia, k0 + ka) : cmk(0, 0);
+          lds.Bs[kb][ib] = (bj + ib < n && k0 + kb < k) ? b(k0 + kb, bj + ib) : cmk(0, 0);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+          const int kk = 4 * ks + lk;
+          cplx av[2], bv[2];
+#pragma unroll
+          for (int t = 0; t < 2; ++t) {
+            av[t] = lds.As[kk][wr + 16 * t + li];
+            bv[t] = lds.Bs[kk][wc + 16 * t + li];
+          }
+#pragma unroll
+          for (int r = 0; r < 2; ++r)
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+              cr[r][c] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[r].x, bv[c].x, cr[r][c], 0, 0, 0);
+              cr[r][c] = __builtin_amdgcn_mfma_f64_16x16x4f64(-av[r].y, bv[c].y, cr[r][c], 0, 0, 0);
+              ci[r][c] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[r].x, bv[c].y, ci[r][c], 0, 0, 0);
+              ci[r][c] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[r].y, bv[c].x, ci[r][c], 0, 0, 0);
+            }
+        }
+        __syncthreads();
+      }
+#pragma unroll
+      for (int r = 0; r < 2; ++r)
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int i = bi + wr + 16 * r + lk + 4 * q, jj = bj + wc + 16 * c + li;
+            if (i < m && jj < n) store(i, jj, cmk(cr[r][c][q], ci[r][c][q]));
+          }
     }
   }
 }
