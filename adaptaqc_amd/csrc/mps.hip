@@ -929,7 +929,7 @@ __global__ __launch_bounds__(aqc::kGemmThreads) void k_split_gemm(const TwoSiteJ
   const int* perm = j.perm;
   const cplx* th = j.theta;
   if (!tr) {
-    aqc::block_cgemm<true, true>(
+    aqc::block_cgemm<true, true, true>(
         mb, nb, L, [&](int kk, int R) { return aqc::cconj(W[(size_t)perm[r0 + kk] * L + R]); },
         [&](int R, int c) { return th[(size_t)(c0 + c) * M + R]; },
         [&](int kk, int c, cplx v) {
@@ -939,7 +939,7 @@ __global__ __launch_bounds__(aqc::kGemmThreads) void k_split_gemm(const TwoSiteJ
         },
         lds);
   } else {
-    aqc::block_cgemm<false, true>(
+    aqc::block_cgemm<false, true, true>(
         mb, nb, L, [&](int R, int c) { return th[(size_t)c * M + r0 + R]; },
         [&](int c, int kk) { return W[(size_t)perm[c0 + kk] * L + c]; },
         [&](int R, int kk, cplx v) {
