@@ -20,6 +20,7 @@ namespace {
 
 constexpr int kThreads = 256;
 constexpr int kMaxTileBits = 12;
+constexpr int kGateChunk = 48;  // gates staged in LDS per chunk (48 x 272 B = 12.75 KB)
 
 struct SegGate {
   int32_t nq;  // 1 or 2
@@ -67,39 +68,52 @@ __global__ __launch_bounds__(kThreads) void k_sv_segment(cplx* __restrict__ stat
   }
   const int ng = hdr->ngates;
   const SegGate* gp = gates + hdr->gate_off;
-  for (int gi = 0; gi < ng; ++gi) {
-    // the gate is wave-uniform: read it with scalar loads (no LDS staging, one barrier per gate)
-    const SegGate& g_s = gp[gi];
-    __syncthreads();
-    if (g_s.nq == 1) {
-      const int t = g_s.t0;
-      const cplx m00 = g_s.m[0], m01 = g_s.m[1], m10 = g_s.m[2], m11 = g_s.m[3];
-      for (int p = tid; p < (1 << (K - 1)); p += kThreads) {
-        int i0 = (int)insert_zero((uint64_t)p, t);
-        int i1 = i0 | (1 << t);
-        cplx a0 = tile[i0], a1 = tile[i1];
-        tile[i0] = aqc::cfma(m01, a1, aqc::cmul(m00, a0));
-        tile[i1] = aqc::cfma(m11, a1, aqc::cmul(m10, a0));
-      }
-    } else if constexpr (K >= 2) {
-      const int t0 = g_s.t0, t1 = g_s.t1;
-      const int lo = t0 < t1 ? t0 : t1, hi = t0 < t1 ? t1 : t0;
-      for (int p = tid; p < (1 << (K - 2)); p += kThreads) {
-        int b = (int)insert_zero(insert_zero((uint64_t)p, lo), hi);
-        int idx[4];
-        cplx v[4];
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          idx[s] = b | ((s & 1) << t0) | ((s >> 1) << t1);
-          v[s] = tile[idx[s]];
+  // The segment's gates are staged into LDS in chunks with vector loads, so a gate costs one
+  // barrier and LDS broadcast reads: read through the scalar cache, each gate was a chain of six
+  // dependent s_load round trips (kind, bits, four matrix rows) standing between two barriers.
+  __shared__ SegGate gl[kGateChunk];
+  for (int c0 = 0; c0 < ng; c0 += kGateChunk) {
+    const int nc = min(kGateChunk, ng - c0);
+    __syncthreads();  // the previous chunk's last gate has been applied
+    constexpr int kWords = (int)(sizeof(SegGate) / sizeof(double2));
+    for (int w = tid; w < nc * kWords; w += kThreads)
+      reinterpret_cast<double2*>(gl)[w] = reinterpret_cast<const double2*>(gp + c0)[w];
+    for (int gi = 0; gi < nc; ++gi) {
+      const SegGate& g_s = gl[gi];
+      __syncthreads();
+      if (g_s.nq == 1) {
+        const int t = g_s.t0;
+        const cplx m00 = g_s.m[0], m01 = g_s.m[1], m10 = g_s.m[2], m11 = g_s.m[3];
+        for (int p = tid; p < (1 << (K - 1)); p += kThreads) {
+          int i0 = (int)insert_zero((uint64_t)p, t);
+          int i1 = i0 | (1 << t);
+          cplx a0 = tile[i0], a1 = tile[i1];
+          tile[i0] = aqc::cfma(m01, a1, aqc::cmul(m00, a0));
+          tile[i1] = aqc::cfma(m11, a1, aqc::cmul(m10, a0));
         }
+      } else if constexpr (K >= 2) {
+        const int t0 = g_s.t0, t1 = g_s.t1;
+        const int lo = t0 < t1 ? t0 : t1, hi = t0 < t1 ? t1 : t0;
+        cplx m[16];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          cplx acc = aqc::cmul(g_s.m[4 * r], v[0]);
-          acc = aqc::cfma(g_s.m[4 * r + 1], v[1], acc);
-          acc = aqc::cfma(g_s.m[4 * r + 2], v[2], acc);
-          acc = aqc::cfma(g_s.m[4 * r + 3], v[3], acc);
-          tile[idx[r]] = acc;
+        for (int e = 0; e < 16; ++e) m[e] = g_s.m[e];
+        for (int p = tid; p < (1 << (K - 2)); p += kThreads) {
+          int b = (int)insert_zero(insert_zero((uint64_t)p, lo), hi);
+          int idx[4];
+          cplx v[4];
+#pragma unroll
+          for (int s = 0; s < 4; ++s) {
+            idx[s] = b | ((s & 1) << t0) | ((s >> 1) << t1);
+            v[s] = tile[idx[s]];
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            cplx acc = aqc::cmul(m[4 * r], v[0]);
+            acc = aqc::cfma(m[4 * r + 1], v[1], acc);
+            acc = aqc::cfma(m[4 * r + 2], v[2], acc);
+            acc = aqc::cfma(m[4 * r + 3], v[3], acc);
+            tile[idx[r]] = acc;
+          }
         }
       }
     }
