@@ -26,6 +26,9 @@ namespace {
 constexpr int kB = 16;        // columns per block
 constexpr int kMaxSweepsBJ = 40;
 constexpr double kTinyT = 1e-8;
+// Cross visits run the 16-round shift this many times (2 passes: 17 -> 16 sweeps but 21% slower
+// per gate at config 5: the visits are compute-, not W-traffic-bound).
+constexpr int kCrossPasses = 1;
 
 struct BJState {
   double fro;   // ||W||_F^2
@@ -36,15 +39,14 @@ struct BJState {
   int pad[2];
 };
 
-// Sum over the 64 lanes of a wave, result in every lane: DPP row sums, then rows 0..3 combined
-// through row_bcast15 / row_bcast31 into lane 63 and read back as a wave-uniform value.
+// Sum over the 64 lanes of a wave, result in every lane: DPP row sums, then a two-step
+// ds_bpermute butterfly across the rows (the row_bcast15/31 + readlane form stalled on the
+// VALU -> SGPR -> VALU hazards).
 __device__ __forceinline__ double wave_sum(double v) {
   v = row_sum16(v);
-  v += __builtin_amdgcn_update_dpp(0.0, v, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
-  v += __builtin_amdgcn_update_dpp(0.0, v, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
-  const int lo = __builtin_amdgcn_readlane(__double2loint(v), 63);
-  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), 63);
-  return __hiloint2double(hi, lo);
+  v += __shfl_xor(v, 16);
+  v += __shfl_xor(v, 32);
+  return v;
 }
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
@@ -317,7 +319,7 @@ __global__ __launch_bounds__(1024) void k_bj_cross(const TwoSiteJob* __restrict_
   __syncthreads();
   const double tol2 = tol_sq(j, L), floor2 = s.fro * 1e-24;
   int rot = 0, big = 0;
-  for (int r = 0; r < kB; ++r) {
+  for (int r = 0; r < kCrossPasses * kB; ++r) {
     const int slot = (w + r) & (kB - 1);
     double2* col = cols + slot * ldl;
 #pragma unroll
