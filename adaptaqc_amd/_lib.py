@@ -28,7 +28,7 @@ EXPORTS = (
     "aqc_mps_apply_batch", "aqc_mps_sort", "aqc_mps_sort_batch", "aqc_mps_overlap_zero",
     "aqc_mps_overlap_zero_batch", "aqc_mps_dot", "aqc_mps_z_all", "aqc_mps_amps_hw1",
     "aqc_pair_grads", "aqc_pair_grads_batch", "aqc_argmax_scaled", "aqc_mps_jacobi_stats",
-    "aqc_mps_set_jacobi_tol", "aqc_mps_set_jacobi_variant", "aqc_svd_debug",
+    "aqc_mps_set_jacobi_tol", "aqc_mps_set_jacobi_stop", "aqc_mps_set_jacobi_variant", "aqc_svd_debug",
     "aqc_sv_pair_rdms", "aqc_mps_pair_rdms", "aqc_mps_pair_rdms_batch", "aqc_entanglement_measures",
     "aqc_sv_transition",
 )
@@ -87,6 +87,7 @@ _SIGS = {
     "aqc_argmax_scaled": ([_P, _P, _I, _I, _IP], _I),
     "aqc_mps_jacobi_stats": ([_P, _IP], _I),
     "aqc_mps_set_jacobi_tol": ([_D], _I),
+    "aqc_mps_set_jacobi_stop": ([_D], _I),
     "aqc_mps_set_jacobi_variant": ([_I], _I),
     "aqc_svd_debug": ([_P, _I, _I, _I, _I, _P, _P, _P, _P], _I),
     "aqc_sv_pair_rdms": ([_P, _P, _I, _P], _I),

@@ -88,6 +88,27 @@ __device__ __forceinline__ double row_sum16(double v) {
   return v;
 }
 
+// Sums over aligned groups of 8 / 4 lanes: the quad steps, then row_half_mirror (lane i of a
+// half-row reads lane 7 - i) joins the two quads of a half-row.
+__device__ __forceinline__ double row_sum8(double v) {
+  v += dpp_perm<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_perm<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_perm<0x141>(v);  // row_half_mirror
+  return v;
+}
+__device__ __forceinline__ double row_sum4(double v) {
+  v += dpp_perm<0xB1>(v);
+  v += dpp_perm<0x4E>(v);
+  return v;
+}
+// Sum over an aligned group of LPG (4, 8 or 16) lanes, result in every lane of the group.
+template <int LPG>
+__device__ __forceinline__ double group_sum(double v) {
+  if constexpr (LPG == 4) return row_sum4(v);
+  else if constexpr (LPG == 8) return row_sum8(v);
+  else return row_sum16(v);
+}
+
 // ---- kernel timing (HIP events on the launching stream) ------------------------------
 struct KernelTimer {
   // Begin/End bracket one launch on `stream` when timing is enabled.

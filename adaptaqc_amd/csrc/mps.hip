@@ -42,6 +42,10 @@ constexpr double kChop = 1e-16;
 constexpr int kMaxSweeps = 60;
 // rotation threshold: |a^H b| > tol_factor * L * eps * |a| |b|  (L = column length)
 double g_jacobi_tol_factor = 1.0;
+// Sweep stop of the register Jacobi: after a sweep whose counted rotations all had |t| <= this,
+// the remaining off-diagonal is O(t^2) (quadratic convergence) and no further sweep is run.
+constexpr double kDefaultTinyT = 1e-8;
+double g_jacobi_tiny_t = kDefaultTinyT;
 int g_jacobi_variant = 2;
 
 struct OneSiteJob {
@@ -380,21 +384,21 @@ __device__ __forceinline__ unsigned long long pivot_key(double v, int id) {
 
 // Householder step k on the pivot column x (this group's S or M): v (zlarfg convention, v_k = 1)
 // and tau go to LDS, x becomes R's column (beta on the diagonal, zeros below).
-template <int MAXR>
+template <int MAXR, int LPG>
 __device__ __forceinline__ void qr_reflector(double (&xr)[MAXR], double (&xi)[MAXR], int k, int lane, double2* vb,
                                              double2* tb) {
-  const int kr = k >> 4;
-  double ar = 0, ai = 0, s2 = 0;
+  const int kr = k / LPG;
+  double ar = 0, ai = 0, s2p[2] = {0, 0};  // two partial sums: this chain is on the critical path
 #pragma unroll
   for (int i = 0; i < MAXR; ++i) {
-    const int row = lane + 16 * i;
+    const int row = lane + LPG * i;
     if (i == kr) ar = xr[i], ai = xi[i];
     const double w = row > k ? 1.0 : 0.0;
-    s2 = fma(w, fma(xr[i], xr[i], xi[i] * xi[i]), s2);
+    s2p[i & 1] = fma(w, fma(xr[i], xr[i], xi[i] * xi[i]), s2p[i & 1]);
   }
-  ar = __shfl(ar, k & 15, 16);
-  ai = __shfl(ai, k & 15, 16);
-  s2 = aqc::row_sum16(s2);
+  ar = __shfl(ar, k % LPG, LPG);
+  ai = __shfl(ai, k % LPG, LPG);
+  const double s2 = aqc::group_sum<LPG>(s2p[0] + s2p[1]);
   double beta, tr_, ti_, cr = 0, ci = 0;  // tau = (tr_, ti_), scale = 1 / (alpha - beta)
   if (s2 == 0.0 && ai == 0.0) {
     beta = ar, tr_ = 0.0, ti_ = 0.0;
@@ -418,7 +422,7 @@ __device__ __forceinline__ void qr_reflector(double (&xr)[MAXR], double (&xi)[MA
   }
 #pragma unroll
   for (int i = 0; i < MAXR; ++i) {
-    const int row = lane + 16 * i;
+    const int row = lane + LPG * i;
     double2 v = make_double2(0, 0);
     if (row > k) v = make_double2(xr[i] * cr - xi[i] * ci, xr[i] * ci + xi[i] * cr);
     if (row == k) v = make_double2(1.0, 0.0);
@@ -430,11 +434,17 @@ __device__ __forceinline__ void qr_reflector(double (&xr)[MAXR], double (&xi)[MA
   if (lane == 0) *tb = make_double2(tr_, ti_);
 }
 
-template <int CP, int MAXR>
-__global__ __launch_bounds__(CP * 8) void k_jacobi_reg(const TwoSiteJob* __restrict__ jobs) {
+// LPG = lanes per column group (16: 1024 threads at CP = 128, 8: 512 threads with 16 rows per
+// lane -- twice the VGPR budget, so no spills, and the per-pair rotation parameters and
+// reductions amortised over twice the rows; 4: 256 threads, 32 rows per lane).
+template <int CP, int MAXR, int LPG = 16>
+__global__ __launch_bounds__(CP / 2 * LPG) void k_jacobi_reg(const TwoSiteJob* __restrict__ jobs) {
+  static_assert(LPG * MAXR == CP, "LPG lanes x MAXR rows must cover the CP rows of a column");
   constexpr int kG = CP / 2;       // groups
-  constexpr int kThreads = kG * 16;
-  constexpr int ld = 16 * MAXR;    // exchange-buffer stride (compile time: no guards)
+  constexpr int kThreads = kG * LPG;
+  // exchange-buffer stride (compile time: no guards); narrow groups pad a slot by LPG complex so
+  // that consecutive slots alternate LDS bank halves (a ds_read_b128 lane group spans groups)
+  constexpr int ld = LPG * MAXR + (LPG < 16 ? LPG : 0);
   constexpr int ldt = CP + 1;      // transpose-buffer stride (odd: conflict-free column writes)
   const TwoSiteJob& j = jobs[blockIdx.x];
   extern __shared__ double2 xbuf[];  // max(kG * ld, kG * ldt) complex
@@ -452,14 +462,14 @@ __global__ __launch_bounds__(CP * 8) void k_jacobi_reg(const TwoSiteJob* __restr
   const int C = tr ? M : N;
   const bool use_qr = j.qr != 0;
   const int tid = threadIdx.x;
-  const int g = tid >> 4, lane = tid & 15;
+  const int g = tid / LPG, lane = tid % LPG;
   // plain doubles (real / imaginary planes) so the arrays stay in VGPRs
   double sr[MAXR], si[MAXR], mr[MAXR], mi[MAXR];
   int sid = g, mid = g + kG;  // column ids of S and M
   double f = 0.0;
 #pragma unroll
   for (int i = 0; i < MAXR; ++i) {
-    const int r = lane + 16 * i;
+    const int r = lane + LPG * i;
     const int cs = g, cm = g + kG;
     double2 a = make_double2(0, 0), b = make_double2(0, 0);
     if (r < L && cs < C) a = tr ? aqc::cconj(j.theta[(size_t)r * M + cs]) : j.theta[(size_t)cs * M + r];
@@ -494,29 +504,26 @@ __global__ __launch_bounds__(CP * 8) void k_jacobi_reg(const TwoSiteJob* __restr
       const int b = k & 1;
       bool exact = k == 0;
       if (k > 0) {
-        const int kr = (k - 1) >> 4, kl = (k - 1) & 15;
-        double es = 0, em = 0;
+        const int kr = (k - 1) / LPG, kl = (k - 1) % LPG;
+        double xsr = 0, xsi = 0, xmr = 0, xmi = 0;  // row k-1 (select first, square once)
 #pragma unroll
         for (int i = 0; i < MAXR; ++i) {
-          if (i == kr) {
-            es = fma(sr[i], sr[i], si[i] * si[i]);
-            em = fma(mr[i], mr[i], mi[i] * mi[i]);
-          }
+          if (i == kr) xsr = sr[i], xsi = si[i], xmr = mr[i], xmi = mi[i];
         }
-        ns -= __shfl(es, kl, 16);
-        nm -= __shfl(em, kl, 16);
+        ns -= __shfl(fma(xsr, xsr, xsi * xsi), kl, LPG);
+        nm -= __shfl(fma(xmr, xmr, xmi * xmi), kl, LPG);
         exact = ns <= 1.5e-8 * nsr || nm <= 1.5e-8 * nmr;
       }
       if (exact) {
         ns = 0, nm = 0;
 #pragma unroll
         for (int i = 0; i < MAXR; ++i) {
-          const double w = (lane + 16 * i) >= k ? 1.0 : 0.0;
+          const double w = (lane + LPG * i) >= k ? 1.0 : 0.0;
           ns = fma(w, fma(sr[i], sr[i], si[i] * si[i]), ns);
           nm = fma(w, fma(mr[i], mr[i], mi[i] * mi[i]), nm);
         }
-        ns = aqc::row_sum16(ns);
-        nm = aqc::row_sum16(nm);
+        ns = aqc::group_sum<LPG>(ns);
+        nm = aqc::group_sum<LPG>(nm);
         nsr = ns, nmr = nm;
       }
       const unsigned long long ka = (ks < 0 && sid < C) ? pivot_key(ns, sid) : 0ull;
@@ -526,10 +533,10 @@ __global__ __launch_bounds__(CP * 8) void k_jacobi_reg(const TwoSiteJob* __restr
       const int p = 255 - (int)(pkey[b] & 255ull);
       if (tid == 0) pkey[b ^ 1] = 0ull;
       if (sid == p) {  // this group owns the pivot column: build the reflector
-        qr_reflector<MAXR>(sr, si, k, lane, vb[b], &tb[b]);
+        qr_reflector<MAXR, LPG>(sr, si, k, lane, vb[b], &tb[b]);
         ks = k;
       } else if (mid == p) {
-        qr_reflector<MAXR>(mr, mi, k, lane, vb[b], &tb[b]);
+        qr_reflector<MAXR, LPG>(mr, mi, k, lane, vb[b], &tb[b]);
         km = k;
       }
       if (tid == 0) perm_s[k] = p;
@@ -539,23 +546,24 @@ __global__ __launch_bounds__(CP * 8) void k_jacobi_reg(const TwoSiteJob* __restr
       double wsr = 0, wsi = 0, wmr = 0, wmi = 0;
 #pragma unroll
       for (int i = 0; i < MAXR; ++i) {  // v^H c (v re-read from LDS below: saves 4*MAXR VGPRs)
-        const double2 v = vb[b][lane + 16 * i];
+        const double2 v = vb[b][lane + LPG * i];
         wsr = fma(v.x, sr[i], fma(v.y, si[i], wsr));
         wsi = fma(v.x, si[i], fma(-v.y, sr[i], wsi));
         wmr = fma(v.x, mr[i], fma(v.y, mi[i], wmr));
         wmi = fma(v.x, mi[i], fma(-v.y, mr[i], wmi));
       }
-      wsr = aqc::row_sum16(wsr);
-      wsi = aqc::row_sum16(wsi);
-      wmr = aqc::row_sum16(wmr);
-      wmi = aqc::row_sum16(wmi);
+      wsr = aqc::group_sum<LPG>(wsr);
+      wsi = aqc::group_sum<LPG>(wsi);
+      wmr = aqc::group_sum<LPG>(wmr);
+      wmi = aqc::group_sum<LPG>(wmi);
       // f = conj(tau) * w ; c -= v * f
       const double as = ks < 0 ? 1.0 : 0.0, am = km < 0 ? 1.0 : 0.0;
       const double fsr = as * (tau.x * wsr + tau.y * wsi), fsi = as * (tau.x * wsi - tau.y * wsr);
       const double fmr = am * (tau.x * wmr + tau.y * wmi), fmi = am * (tau.x * wmi - tau.y * wmr);
+      asm volatile("" ::: "memory");  // re-read v below instead of keeping 2*MAXR doubles live
 #pragma unroll
       for (int i = 0; i < MAXR; ++i) {
-        const double2 v = vb[b][lane + 16 * i];
+        const double2 v = vb[b][lane + LPG * i];
         sr[i] = fma(-v.x, fsr, fma(v.y, fsi, sr[i]));  // 2 FMAs per component, not mul+fma+add
         si[i] = fma(-v.x, fsi, fma(-v.y, fsr, si[i]));
         mr[i] = fma(-v.x, fmr, fma(v.y, fmi, mr[i]));
@@ -571,7 +579,7 @@ __global__ __launch_bounds__(CP * 8) void k_jacobi_reg(const TwoSiteJob* __restr
     for (int h = 0; h < 2; ++h) {
 #pragma unroll
       for (int i = h * H; i < (h + 1) * H; ++i) {
-        const int jx = lane + 16 * (i - h * H);
+        const int jx = lane + LPG * (i - h * H);
         if (ks >= 0) xbuf[jx * ldt + ks] = make_double2(sr[i], -si[i]);
         if (km >= 0) xbuf[jx * ldt + km] = make_double2(mr[i], -mi[i]);
       }
@@ -579,7 +587,7 @@ __global__ __launch_bounds__(CP * 8) void k_jacobi_reg(const TwoSiteJob* __restr
       const bool real_col = g + h * kG < C;
 #pragma unroll
       for (int i = h * H; i < (h + 1) * H; ++i) {
-        const int ra = lane + 16 * (i - h * H), rb = ra + kG;  // X rows (pivot steps)
+        const int ra = lane + LPG * (i - h * H), rb = ra + kG;  // X rows (pivot steps)
         double2 va = make_double2(0, 0), vb2 = make_double2(0, 0);
         if (real_col && ra < C) va = xbuf[g * ldt + ra];
         if (real_col && rb < C) vb2 = xbuf[g * ldt + rb];
@@ -621,15 +629,15 @@ __global__ __launch_bounds__(CP * 8) void k_jacobi_reg(const TwoSiteJob* __restr
   __shared__ double xnrm[kG], xscl[kG], xisc[kG];
   __syncthreads();  // the QR transpose's last reads of xbuf are done
 #pragma unroll
-  for (int i = 0; i < MAXR; ++i) xbuf[g * ld + lane + 16 * i] = make_double2(mr[i], mi[i]);
+  for (int i = 0; i < MAXR; ++i) xbuf[g * ld + lane + LPG * i] = make_double2(mr[i], mi[i]);
   if (lane == 0) {
     xid[g] = mid;
     xscl[g] = 1.0;
   }
-  // Stop rule: a sweep whose counted rotations all had |t| < kTinyT leaves every cosine at
-  // O(t * cos) ~ 1e-16 after it (quadratic convergence), so the confirming sweep with no
-  // rotation at all is skipped.
-  constexpr double kTinyT = 1e-8;
+  // Stop rule: a sweep whose counted rotations all had |t| <= j.jtiny (default 1e-8) leaves every
+  // off-diagonal at O(t^2) relative after it (quadratic convergence), so the confirming sweep
+  // with no rotation at all is skipped.
+  const double tiny2 = j.jtiny * j.jtiny;
   double sd = 1.0, sn = 0.0;  // S: scale and tracked squared norm (uniform in the group)
   int sweeps = 0;
   for (sweeps = 0; sweeps < max_sweeps; ++sweeps) {
@@ -641,15 +649,15 @@ __global__ __launch_bounds__(CP * 8) void k_jacobi_reg(const TwoSiteJob* __restr
       for (int i = 0; i < MAXR; ++i) {
         sr[i] *= sd;
         si[i] *= sd;
-        double2 v = own[lane + 16 * i];
+        double2 v = own[lane + LPG * i];
         v.x *= od;
         v.y *= od;
-        own[lane + 16 * i] = v;
+        own[lane + LPG * i] = v;
         a = fma(sr[i], sr[i], fma(si[i], si[i], a));
         b = fma(v.x, v.x, fma(v.y, v.y, b));
       }
-      a = aqc::row_sum16(a);
-      b = aqc::row_sum16(b);
+      a = aqc::group_sum<LPG>(a);
+      b = aqc::group_sum<LPG>(b);
       sd = 1.0;
       sn = a;
       __builtin_amdgcn_wave_barrier();
@@ -670,19 +678,27 @@ __global__ __launch_bounds__(CP * 8) void k_jacobi_reg(const TwoSiteJob* __restr
         double2* col = xbuf + slot * ld;
 #pragma unroll
         for (int i = 0; i < MAXR; ++i) {
-          const double2 v = col[lane + 16 * i];
+          const double2 v = col[lane + LPG * i];
           mr[i] = v.x;
           mi[i] = v.y;
         }
         const double mn = xnrm[slot], md = xscl[slot], imd = xisc[slot];
-        double gx = 0, gy = 0;
+        // NP partial sums: with 16+ rows per lane and 1-2 waves per SIMD a single chain would
+        // expose its FMA latency
+        constexpr int NP = MAXR >= 16 ? 2 : 1;
+        double gxp[NP], gyp[NP];
+#pragma unroll
+        for (int q = 0; q < NP; ++q) gxp[q] = gyp[q] = 0.0;
 #pragma unroll
         for (int i = 0; i < MAXR; ++i) {
-          gx = fma(sr[i], mr[i], fma(si[i], mi[i], gx));   // conj(s) * m
-          gy = fma(sr[i], mi[i], fma(-si[i], mr[i], gy));
+          gxp[i % NP] = fma(sr[i], mr[i], fma(si[i], mi[i], gxp[i % NP]));   // conj(s) * m
+          gyp[i % NP] = fma(sr[i], mi[i], fma(-si[i], mr[i], gyp[i % NP]));
         }
-        gx = aqc::row_sum16(gx);
-        gy = aqc::row_sum16(gy);
+        double gx = gxp[0], gy = gyp[0];
+#pragma unroll
+        for (int q = 1; q < NP; ++q) gx += gxp[q], gy += gyp[q];
+        gx = aqc::group_sum<LPG>(gx);
+        gy = aqc::group_sum<LPG>(gy);
         const double dd = sd * md;
         gx *= dd;
         gy *= dd;
@@ -695,7 +711,7 @@ __global__ __launch_bounds__(CP * 8) void k_jacobi_reg(const TwoSiteJob* __restr
           jacobi_te(sn, mn, g2, te, c, p);
           if (g2 > 16.0 * tol2 * ab) {
             my_rot = 1;
-            if (p - 1.0 > kTinyT * kTinyT) my_big = 1;  // |t| > kTinyT
+            if (p - 1.0 > tiny2) my_big = 1;  // |t| > jtiny
           }
           const double ra = md * isd, ira = sd * imd;  // d_b / d_a and its inverse
           const double mux = te * gx * ra, muy = -te * gy * ra;   // mu = t conj(e) d_b / d_a
@@ -705,7 +721,7 @@ __global__ __launch_bounds__(CP * 8) void k_jacobi_reg(const TwoSiteJob* __restr
             const double ar = sr[i], ai = si[i], br = mr[i], bi = mi[i];
             sr[i] = fma(-mux, br, fma(muy, bi, ar));
             si[i] = fma(-mux, bi, fma(-muy, br, ai));
-            col[lane + 16 * i] = make_double2(fma(nux, ar, fma(-nuy, ai, br)), fma(nux, ai, fma(nuy, ar, bi)));
+            col[lane + LPG * i] = make_double2(fma(nux, ar, fma(-nuy, ai, br)), fma(nux, ai, fma(nuy, ar, bi)));
           }
           const double ic = p * c;  // 1 / c
           sd *= c;
@@ -718,12 +734,12 @@ __global__ __launch_bounds__(CP * 8) void k_jacobi_reg(const TwoSiteJob* __restr
             asm volatile("" ::: "memory");  // re-read M from LDS: keeps it out of VGPRs above
 #pragma unroll
             for (int i = 0; i < MAXR; ++i) {  // (this lane's own LDS writes: in order)
-              const double2 v = col[lane + 16 * i];
+              const double2 v = col[lane + LPG * i];
               a = fma(sr[i], sr[i], fma(si[i], si[i], a));
               b = fma(v.x, v.x, fma(v.y, v.y, b));
             }
-            sn2 = aqc::row_sum16(a) * sd * sd;
-            mn2 = aqc::row_sum16(b) * md2 * md2;
+            sn2 = aqc::group_sum<LPG>(a) * sd * sd;
+            mn2 = aqc::group_sum<LPG>(b) * md2 * md2;
           }
           sn = sn2;
           __builtin_amdgcn_wave_barrier();
@@ -741,8 +757,8 @@ __global__ __launch_bounds__(CP * 8) void k_jacobi_reg(const TwoSiteJob* __restr
         double2* col = xbuf + (g - h) * ld;
 #pragma unroll
         for (int i = 0; i < MAXR; ++i) {
-          const double2 v = col[lane + 16 * i];
-          col[lane + 16 * i] = make_double2(sr[i], si[i]);
+          const double2 v = col[lane + LPG * i];
+          col[lane + LPG * i] = make_double2(sr[i], si[i]);
           sr[i] = v.x;
           si[i] = v.y;
         }
@@ -776,7 +792,7 @@ __global__ __launch_bounds__(CP * 8) void k_jacobi_reg(const TwoSiteJob* __restr
   double ns = 0, nm = 0;
 #pragma unroll
   for (int i = 0; i < MAXR; ++i) {
-    const int row = lane + 16 * i;
+    const int row = lane + LPG * i;
     double2 mv = xbuf[g * ld + row];
     mv.x *= od;
     mv.y *= od;
@@ -789,8 +805,8 @@ __global__ __launch_bounds__(CP * 8) void k_jacobi_reg(const TwoSiteJob* __restr
     ns = fma(ar, ar, fma(ai, ai, ns));
     nm = fma(mv.x, mv.x, fma(mv.y, mv.y, nm));
   }
-  ns = aqc::row_sum16(ns);
-  nm = aqc::row_sum16(nm);
+  ns = aqc::group_sum<LPG>(ns);
+  nm = aqc::group_sum<LPG>(nm);
   if (lane == 0) {
     if (sid < C) j.sig[sid] = sqrt(ns);
     if (mid_out < C) j.sig[mid_out] = sqrt(nm);
@@ -802,6 +818,17 @@ __global__ __launch_bounds__(CP * 8) void k_jacobi_reg(const TwoSiteJob* __restr
   if (j.dbg == 1 && use_qr) {  // diagnostics: pivot order after the W columns
     for (int k = tid; k < C; k += kThreads) j.perm[k] = perm_s[k];
   }
+}
+
+// 2 chi = 128 register Jacobi by variant: 5 = 8-lane groups (512 threads), 6 = 4-lane groups
+// (256 threads), otherwise 16-lane groups (1024 threads).  Dynamic LDS = kG x max(ld, CP + 1).
+void launch_jacobi_reg128(int variant, int nj, hipStream_t st, const TwoSiteJob* jp) {
+  if (variant == 5)
+    hipLaunchKernelGGL((k_jacobi_reg<128, 16, 8>), dim3(nj), dim3(512), 64 * 136 * 16, st, jp);
+  else if (variant == 6)
+    hipLaunchKernelGGL((k_jacobi_reg<128, 32, 4>), dim3(nj), dim3(256), 64 * 132 * 16, st, jp);
+  else
+    hipLaunchKernelGGL((k_jacobi_reg<128, 8>), dim3(nj), dim3(1024), 64 * 129 * 16, st, jp);
 }
 
 // Sort singular values, apply reduce_zeros, write lambda_m / dims[1] / perm / sorted sig.
@@ -1373,6 +1400,7 @@ TwoSiteJob make_two(aqc_mps_t h, const DevOp& op, int slot = 0) {
   j.max_chi = h->max_chi;
   j.thr = h->thr;
   j.jtol = g_jacobi_tol_factor;
+  j.jtiny = g_jacobi_tiny_t;
   std::memcpy(j.G, op.m, sizeof(j.G));
   return j;
 }
@@ -1448,8 +1476,8 @@ int run_waves(aqc_mps_t* hs, int ns, std::vector<std::vector<DevOp>>& lists) {
   std::vector<std::pair<size_t, size_t>> two_rng(maxlen), one_rng(maxlen);
   int cap_max = 0;
   for (int s = 0; s < ns; ++s) cap_max = std::max(cap_max, hs[s]->d.cap);
-  const bool reg = (g_jacobi_variant == 2 || g_jacobi_variant == 3) && 2 * cap_max <= 128;
-  const int use_qr = reg && g_jacobi_variant == 2 ? 1 : 0;
+  const bool reg = (g_jacobi_variant == 2 || g_jacobi_variant == 3 || g_jacobi_variant >= 5) && 2 * cap_max <= 128;
+  const int use_qr = reg && g_jacobi_variant != 3 ? 1 : 0;
   for (size_t w = 0; w < maxlen; ++w) {
     size_t t0 = two.size(), o0 = one.size();
     for (int s = 0; s < ns; ++s) {
@@ -1506,7 +1534,7 @@ int run_waves(aqc_mps_t* hs, int ns, std::vector<std::vector<DevOp>>& lists) {
         else if (2 * cap_max <= 64)
           hipLaunchKernelGGL((k_jacobi_reg<64, 4>), dim3(nj), dim3(512), 32 * 65 * 16, st, jp);
         else
-          hipLaunchKernelGGL((k_jacobi_reg<128, 8>), dim3(nj), dim3(1024), 64 * 129 * 16, st, jp);
+          launch_jacobi_reg128(g_jacobi_variant, nj, st, jp);
       } else if (2 * cap_max <= 64) {
         if (half) hipLaunchKernelGGL((k_jacobi<16, 4, 256, 4096>), dim3(nj), dim3(256), 0, st, jp);
         else hipLaunchKernelGGL((k_jacobi<16, 4, 512, 8192>), dim3(nj), dim3(512), 0, st, jp);
@@ -1721,7 +1749,8 @@ int aqc_svd_debug(const double* theta, int m, int n, int variant, int stop_after
   AQC_REQUIRE(theta && w_out && sig_out && sweeps, "aqc_svd_debug: null argument");
   AQC_REQUIRE(m >= 1 && n >= 1 && m % 2 == 0 && n % 2 == 0 && m <= 128 && n <= 128,
               "aqc_svd_debug: m, n must be even and <= 128");
-  AQC_REQUIRE(variant == 2 || variant == 3, "aqc_svd_debug: variant must be 2 or 3");
+  AQC_REQUIRE(variant == 2 || variant == 3 || variant == 5 || variant == 6,
+              "aqc_svd_debug: variant must be 2, 3, 5 or 6");
   hipStream_t st = aqc::mps_stream();
   const int cp = std::max(m, n) <= 32 ? 32 : (std::max(m, n) <= 64 ? 64 : 128);
   const size_t mat = (size_t)128 * 128 * sizeof(cplx);
@@ -1744,7 +1773,8 @@ int aqc_svd_debug(const double* theta, int m, int n, int variant, int stop_after
   j.perm = pm;
   j.flags = fl;
   j.jtol = g_jacobi_tol_factor;
-  j.qr = variant == 2 ? 1 : 0;
+  j.jtiny = g_jacobi_tiny_t;
+  j.qr = variant != 3 ? 1 : 0;
   j.dbg = stop_after_qr ? 1 : 0;
   int hd[8] = {m / 2, 0, n / 2, 0, 0, 0, 0, 0};  // dims, then zeroed flags
   AQC_HIP_CHECK(hipMemcpyAsync(th, theta, (size_t)m * n * sizeof(cplx), hipMemcpyHostToDevice, st));
@@ -1753,7 +1783,7 @@ int aqc_svd_debug(const double* theta, int m, int n, int variant, int stop_after
   AQC_HIP_CHECK(hipMemsetAsync(wk, 0, mat, st));
   if (cp == 32) hipLaunchKernelGGL((k_jacobi_reg<32, 2>), dim3(1), dim3(256), 16 * 33 * 16, st, dj);
   else if (cp == 64) hipLaunchKernelGGL((k_jacobi_reg<64, 4>), dim3(1), dim3(512), 32 * 65 * 16, st, dj);
-  else hipLaunchKernelGGL((k_jacobi_reg<128, 8>), dim3(1), dim3(1024), 64 * 129 * 16, st, dj);
+  else launch_jacobi_reg128(variant, 1, st, dj);
   AQC_CHECK_LAUNCH();
   const int L = std::max(m, n), C = std::min(m, n);
   const int Lw = j.qr ? C : L;
@@ -1785,8 +1815,14 @@ int aqc_mps_set_jacobi_tol(double factor) {
   return AQC_OK;
 }
 
+int aqc_mps_set_jacobi_stop(double tiny_t) {
+  AQC_REQUIRE(tiny_t < 1e-3, "aqc_mps_set_jacobi_stop: tiny_t must be < 1e-3 (<= 0 restores the default)");
+  g_jacobi_tiny_t = tiny_t > 0 ? tiny_t : kDefaultTinyT;
+  return AQC_OK;
+}
+
 int aqc_mps_set_jacobi_variant(int variant) {
-  AQC_REQUIRE(variant >= 0 && variant <= 4, "aqc_mps_set_jacobi_variant: variant must be 0..4");
+  AQC_REQUIRE(variant >= 0 && variant <= 6, "aqc_mps_set_jacobi_variant: variant must be 0..6");
   g_jacobi_variant = variant;
   return AQC_OK;
 }

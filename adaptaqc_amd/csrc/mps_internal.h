@@ -54,7 +54,8 @@ struct TwoSiteJob {
   int max_chi;
   double thr;
   double jtol;  // Jacobi rotation threshold factor
-  int qr;       // 1: Jacobi ran on R^H of a pivoted QR -> W holds the other side (see k_jacobi_reg)
+  double jtiny; // sweep stop: a sweep whose counted rotations all had |t| <= jtiny is the last
+  int qr;      // 1: Jacobi ran on R^H of a pivoted QR -> W holds the other side (see k_jacobi_reg)
   int dbg;      // diagnostics (aqc_svd_debug): 1 = stop after the QR phase, write X unpermuted
   cplx G[16];  // row = 2*s1'+s2' (out), col = 2*s1+s2 (in)
 };

@@ -195,7 +195,7 @@ def test_batch_apply_matches_single():
         assert abs(d.overlap_zero() - ov[s]) < 1e-13
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 5, 6])
 def test_jacobi_variants_vs_oracle(goldens, variant):
     """Every Jacobi kernel shape reproduces the oracle (small, ragged and full-width theta)."""
     from adaptaqc_amd import _lib
@@ -243,3 +243,39 @@ def test_copy_batch_matches_single_copies(random_mps):
         for (a, b), (a2, b2) in zip(d.to_aer()[0], s.to_aer()[0]):
             np.testing.assert_array_equal(a, a2)
             np.testing.assert_array_equal(b, b2)
+
+
+@pytest.mark.parametrize("variant", [2, 5])
+def test_jacobi_stop_rule_vs_oracle(variant):
+    """A looser sweep stop (last sweep's rotations all |t| <= 1e-6 or 1e-5) keeps a 16-qubit chi = 64
+    replay (max_chi binding, 2 chi = 128 thetas) within 1e-9 of the oracle's overlap."""
+    import ctypes
+
+    from adaptaqc_amd import _lib
+    from adaptaqc_amd.circuit import device_ops
+    from adaptaqc_amd.device import DeviceMPS
+
+    rng = np.random.default_rng(33)
+    n, chi = 16, 64
+    ops = []
+    for layer in range(10):
+        for q in range(n):
+            ops.append(("ry", (q,), (rng.uniform(-np.pi, np.pi),)))
+            ops.append(("rz", (q,), (rng.uniform(-np.pi, np.pi),)))
+        for q in range(layer % 2, n - 1, 2):
+            ops.append(("cx", (q, q + 1), ()))
+    ops.append(("cx", (2, n - 3), ()))
+    ref = M.run_circuit(n, ops, 1e-16, chi)
+    ov_ref = M.mps_dot(ref.preprocessed(), M.zero_mps(n))
+    L = _lib.lib()
+    _lib.check(L.aqc_mps_set_jacobi_variant(variant))
+    try:
+        for tiny in (1e-8, 1e-6, 1e-5):
+            _lib.check(L.aqc_mps_set_jacobi_stop(ctypes.c_double(tiny)))
+            d = DeviceMPS(n, chi, 1e-16, chi)
+            d.apply(device_ops(to_circuit(n, ops)))
+            np.testing.assert_array_equal(d.dims(), [1] + [x.shape[2] for x in ref.preprocessed()])
+            assert abs(d.overlap_zero() - ov_ref) <= 1e-9 * abs(ov_ref) + 1e-18, tiny
+    finally:
+        _lib.check(L.aqc_mps_set_jacobi_stop(ctypes.c_double(0.0)))
+        _lib.check(L.aqc_mps_set_jacobi_variant(2))

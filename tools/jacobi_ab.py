@@ -1,0 +1,61 @@
+"""A/B of the two-site SVD kernel configurations on the bench's overlap workload (lab tool; MI355X).
+
+    python tools/jacobi_ab.py [states] [variant:tiny ...]      e.g. 256 2:1e-8 5:1e-8 5:1e-6
+
+Per config: the bench's overlap evaluations (thinly-dressed layers at distances 1, 2, 5, 25 on
+`states` random 50-qubit chi = 64 states: Aer routing, SVD truncation at chi = 64, sort back) run
+twice; the second run's mps_svd time (HIP events on the MPS stream) and the largest sweep count
+of a sample of states are reported, and each config's overlaps <0|psi> are compared with the first's (relative).
+"""
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+from adaptaqc_amd import _lib  # noqa: E402
+from adaptaqc_amd.device import DeviceMPS, apply_batch, copy_batch, overlap_zero_batch  # noqa: E402
+
+B = int(sys.argv[1]) if len(sys.argv) > 1 else 256
+configs = [(int(c.split(":")[0]), float(c.split(":")[1])) for c in sys.argv[2:]] or [(2, 1e-8), (5, 1e-8)]
+L = _lib.lib()
+distinct = [bench.random_vidal_mps(50, bench.CHI, 1000 + k) for k in range(8)]
+states = []
+for s in range(B):
+    d = DeviceMPS(50, bench.CHI, 1e-16, bench.CHI)
+    d.load_aer(distinct[s % len(distinct)])
+    states.append(d)
+work = [DeviceMPS(50, bench.CHI, 1e-16, bench.CHI) for _ in range(B * len(bench.DISTANCES))]
+src = [states[k // len(bench.DISTANCES)] for k in range(len(work))]
+rng = np.random.default_rng(7)
+ops = [_lib.ops_array(bench.thin_layer_ops(bench.LAYER_A, bench.LAYER_A + d, rng.uniform(-np.pi, np.pi, 4)))
+       for _ in range(B) for d in bench.DISTANCES]
+ref = None
+try:
+    for variant, tiny in configs:
+        _lib.check(L.aqc_mps_set_jacobi_variant(variant))
+        _lib.check(L.aqc_mps_set_jacobi_stop(ctypes.c_double(tiny)))
+        for rep in range(2):
+            copy_batch(work, src)
+            _lib.timing_reset()
+            _lib.timing_enable(True)
+            apply_batch(work, ops)
+            ov = overlap_zero_batch(work)
+            _lib.timing_enable(False)
+        svd = _lib.timing_query("mps_svd")
+        sw = ctypes.c_int()
+        msw = 0
+        for w in work[:: max(1, len(work) // 64)]:
+            _lib.check(L.aqc_mps_jacobi_stats(w.h, ctypes.byref(sw)))
+            msw = max(msw, sw.value)
+        if ref is None:
+            ref = ov
+        print(f"variant {variant} tiny {tiny:.0e}: svd {svd['ms']:8.2f} ms over {svd['launches']} launches "
+              f"({svd['ms'] / max(svd['launches'], 1):.3f} ms/launch), max sweeps {msw}, "
+              f"max |<0|psi> - ref| / |ref| {np.max(np.abs(ov - ref) / np.abs(ref)):.2e}", flush=True)
+finally:
+    _lib.check(L.aqc_mps_set_jacobi_variant(2))
+    _lib.check(L.aqc_mps_set_jacobi_stop(ctypes.c_double(0.0)))

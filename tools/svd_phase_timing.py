@@ -1,11 +1,11 @@
 """Single-workgroup timing of the register Jacobi's phases (run under rocprofv3 --kernel-trace).
 
-    rocprofv3 --kernel-trace -d gpurun_out/svdph -o run -- python3 tools/svd_phase_timing.py [reps]
-    python3 tools/svd_phase_timing.py --report gpurun_out/svdph/run_results.db [reps]
+    rocprofv3 --kernel-trace -d gpurun_out/svdph -o run -- python3 tools/svd_phase_timing.py [reps] [variant ...]
+    python3 tools/svd_phase_timing.py --report gpurun_out/svdph/run_results.db [reps] [variant ...]
 
 A swap-routed two-site theta of the bench's random chi = 64 state (sites 24, 25) is decomposed
 `reps` times with the QR phase only (aqc_svd_debug stop_after_qr = 1), then `reps` times in full;
-the report splits the k_jacobi_reg dispatches in launch order.
+the report splits the k_jacobi_reg dispatches in launch order, per variant (default 2).
 """
 import ctypes
 import os
@@ -32,7 +32,7 @@ def swap_theta(seed=1000, site=24):
     return th.reshape(2 * chl, 2 * chr_)
 
 
-def run(reps):
+def run(reps, variants):
     from adaptaqc_amd import _lib
 
     T = swap_theta()
@@ -43,25 +43,27 @@ def run(reps):
     perm = np.zeros(max(m, n), dtype=np.int32)
     sw = ctypes.c_int()
     L = _lib.lib()
-    for qr_only in (1, 0):
-        for _ in range(reps):
-            _lib.check(L.aqc_svd_debug(_lib.ptr(th), m, n, 2, qr_only, _lib.ptr(w), _lib.ptr(sig),
-                                       _lib.ptr(perm), ctypes.byref(sw)))
-        print(f"stop_after_qr={qr_only}: sweeps={sw.value}", flush=True)
+    for v in variants:
+        for qr_only in (1, 0):
+            for _ in range(reps):
+                _lib.check(L.aqc_svd_debug(_lib.ptr(th), m, n, v, qr_only, _lib.ptr(w), _lib.ptr(sig),
+                                           _lib.ptr(perm), ctypes.byref(sw)))
+            print(f"variant {v} stop_after_qr={qr_only}: sweeps={sw.value}", flush=True)
     print("sigma[:4]", sig[:4], "min", sig[:min(m, n)].min())
 
 
-def report(db, reps):
+def report(db, reps, variants):
     c = sqlite3.connect(db)
     rows = c.execute("select name, duration from kernels order by start").fetchall()
     d = [du for nm, du in rows if "k_jacobi_reg" in nm]
-    qr, full = d[:reps], d[reps:2 * reps]
-    print(f"QR phase: {np.mean(qr) / 1e3:.1f} us; full: {np.mean(full) / 1e3:.1f} us "
-          f"(sweeps phase {np.mean(full) / 1e3 - np.mean(qr) / 1e3:.1f} us)")
+    for k, v in enumerate(variants):
+        qr, full = d[2 * k * reps:(2 * k + 1) * reps], d[(2 * k + 1) * reps:(2 * k + 2) * reps]
+        print(f"variant {v}: QR phase: {np.mean(qr) / 1e3:.1f} us; full: {np.mean(full) / 1e3:.1f} us "
+              f"(sweeps phase {np.mean(full) / 1e3 - np.mean(qr) / 1e3:.1f} us)")
 
 
 if __name__ == "__main__":
     if sys.argv[1:2] == ["--report"]:
-        report(sys.argv[2], int(sys.argv[3]) if len(sys.argv) > 3 else 5)
+        report(sys.argv[2], int(sys.argv[3]) if len(sys.argv) > 3 else 5, [int(v) for v in sys.argv[4:]] or [2])
     else:
-        run(int(sys.argv[1]) if len(sys.argv) > 1 else 5)
+        run(int(sys.argv[1]) if len(sys.argv) > 1 else 5, [int(v) for v in sys.argv[2:]] or [2])
