@@ -55,7 +55,7 @@ def run(reps, variants):
 def report(db, reps, variants):
     c = sqlite3.connect(db)
     rows = c.execute("select name, duration from kernels order by start").fetchall()
-    d = [du for nm, du in rows if "k_jacobi_reg" in nm]
+    d = [du for nm, du in rows if "k_jacobi_reg" in nm or "k_jacobi_b2" in nm]
     for k, v in enumerate(variants):
         qr, full = d[2 * k * reps:(2 * k + 1) * reps], d[(2 * k + 1) * reps:(2 * k + 2) * reps]
         print(f"variant {v}: QR phase: {np.mean(qr) / 1e3:.1f} us; full: {np.mean(full) / 1e3:.1f} us "
