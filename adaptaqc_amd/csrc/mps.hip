@@ -44,7 +44,7 @@ constexpr int kMaxSweeps = 60;
 double g_jacobi_tol_factor = 1.0;
 // Sweep stop of the register Jacobi: after a sweep whose counted rotations all had |t| <= this,
 // the remaining off-diagonal is O(t^2) (quadratic convergence) and no further sweep is run.
-constexpr double kDefaultTinyT = 1e-8;
+constexpr double kDefaultTinyT = 1e-6;
 double g_jacobi_tiny_t = kDefaultTinyT;
 int g_jacobi_variant = 2;
 
@@ -434,9 +434,8 @@ __device__ __forceinline__ void qr_reflector(double (&xr)[MAXR], double (&xi)[MA
   if (lane == 0) *tb = make_double2(tr_, ti_);
 }
 
-// LPG = lanes per column group (16: 1024 threads at CP = 128, 8: 512 threads with 16 rows per
-// lane -- twice the VGPR budget, so no spills, and the per-pair rotation parameters and
-// reductions amortised over twice the rows; 4: 256 threads, 32 rows per lane).
+// LPG = lanes per column group (16: 1024 threads at CP = 128; 8: 512 threads with 16 rows per
+// lane, the per-pair rotation parameters and reductions amortised over twice the rows).
 template <int CP, int MAXR, int LPG = 16>
 __global__ __launch_bounds__(CP / 2 * LPG) void k_jacobi_reg(const TwoSiteJob* __restrict__ jobs) {
   static_assert(LPG * MAXR == CP, "LPG lanes x MAXR rows must cover the CP rows of a column");
@@ -634,7 +633,7 @@ __global__ __launch_bounds__(CP / 2 * LPG) void k_jacobi_reg(const TwoSiteJob* _
     xid[g] = mid;
     xscl[g] = 1.0;
   }
-  // Stop rule: a sweep whose counted rotations all had |t| <= j.jtiny (default 1e-8) leaves every
+  // Stop rule: a sweep whose counted rotations all had |t| <= j.jtiny (default 1e-6) leaves every
   // off-diagonal at O(t^2) relative after it (quadratic convergence), so the confirming sweep
   // with no rotation at all is skipped.
   const double tiny2 = j.jtiny * j.jtiny;
@@ -820,448 +819,16 @@ __global__ __launch_bounds__(CP / 2 * LPG) void k_jacobi_reg(const TwoSiteJob* _
   }
 }
 
-// ---- block-pair register Jacobi (2 chi = 128, variant 7) ---------------------------------------
-// k_jacobi_reg<128, 8> with FOUR columns per 16-lane group (512 threads, 32 groups, 2 waves per
-// SIMD): S0, S1 stay in VGPRs and the group's LDS slot holds a pair M0, M1.  The recursive-halving
-// tournament runs over super-columns of two (32 S pairs against 32 slot pairs: 63 rounds) and a
-// round rotates all four cross pairs -- (S0,M0) (S1,M1), then (S0,M1) (S1,M0): two independent
-// rotations per step -- before the slot is written back.  Per column pair that halves the rounds,
-// barriers and LDS traffic of k_jacobi_reg (whose rounds stall on them with the VALU ~75% busy)
-// and gives every lane two independent dependency chains.  The (S0,S1) and (M0,M1) pairs run at
-// sweep start.  QR preconditioning, rotation rule, thresholds, stop test and output contract are
-// those of k_jacobi_reg.
-struct B2Col {  // scaled column: true column = d * stored vector, n = tracked squared norm
-  double n, d, id;
-};
-struct B2Coef {  // v_a' = v_a - mu v_b, v_b' = v_b + nu v_a, d' = c d, n_a' = n_a - tg, n_b' = n_b + tg
-  double mux, muy, nux, nuy, c, ic, tg;
-};
-
-template <int MAXR>
-__device__ __forceinline__ void b2_dot(const double (&ar)[MAXR], const double (&ai)[MAXR], const double (&br)[MAXR],
-                                       const double (&bi)[MAXR], double& gx, double& gy) {
-  double x = 0, y = 0;
-#pragma unroll
-  for (int i = 0; i < MAXR; ++i) {
-    x = fma(ar[i], br[i], fma(ai[i], bi[i], x));  // conj(a) * b
-    y = fma(ar[i], bi[i], fma(-ai[i], br[i], y));
-  }
-  gx = x, gy = y;
-}
-
-// Coefficients of the pair's rotation, or the identity when go is false (so two pairs can be
-// applied side by side without a branch each).
-__device__ __forceinline__ B2Coef b2_coef(const B2Col& a, const B2Col& b, double gx, double gy, bool go, double tol2,
-                                          double tiny2, int& rot, int& big) {
-  const double g2 = gx * gx + gy * gy;
-  double te, c, p;
-  jacobi_te(a.n, b.n, g2, te, c, p);
-  if (!go) te = 0.0, c = 1.0, p = 1.0;
-  if (go && g2 > 16.0 * tol2 * (a.n * b.n)) {
-    rot = 1;
-    if (p - 1.0 > tiny2) big = 1;
-  }
-  const double ra = b.d * a.id, ira = a.d * b.id;
-  return B2Coef{te * gx * ra, -te * gy * ra, te * gx * ira, te * gy * ira, c, p * c, te * g2};
-}
-
-template <int MAXR>
-__device__ __forceinline__ void b2_apply(double (&ar)[MAXR], double (&ai)[MAXR], double (&br)[MAXR],
-                                         double (&bi)[MAXR], const B2Coef& k) {
-#pragma unroll
-  for (int i = 0; i < MAXR; ++i) {
-    const double xr = ar[i], xi = ai[i], yr = br[i], yi = bi[i];
-    ar[i] = fma(-k.mux, yr, fma(k.muy, yi, xr));
-    ai[i] = fma(-k.mux, yi, fma(-k.muy, yr, xi));
-    br[i] = fma(k.nux, xr, fma(-k.nuy, xi, yr));
-    bi[i] = fma(k.nux, xi, fma(k.nuy, xr, yi));
-  }
-}
-
-template <int MAXR>
-__device__ __forceinline__ void b2_post(const double (&ar)[MAXR], const double (&ai)[MAXR], const double (&br)[MAXR],
-                                        const double (&bi)[MAXR], B2Col& a, B2Col& b, const B2Coef& k) {
-  a.d *= k.c, a.id *= k.ic, b.d *= k.c, b.id *= k.ic;
-  double na = a.n - k.tg, nb = b.n + k.tg;
-  if (na < 1e-6 * a.n || nb < 1e-6 * b.n) {  // cancellation: recompute exactly
-    double x = 0, y = 0;
-#pragma unroll
-    for (int i = 0; i < MAXR; ++i) {
-      x = fma(ar[i], ar[i], fma(ai[i], ai[i], x));
-      y = fma(br[i], br[i], fma(bi[i], bi[i], y));
-    }
-    na = aqc::row_sum16(x) * a.d * a.d;
-    nb = aqc::row_sum16(y) * b.d * b.d;
-  }
-  a.n = na, b.n = nb;
-}
-
-// Two independent pair rotations (A: a0-b0, B: a1-b1).  Returns which pairs rotated (bit 0: A,
-// bit 1: B).
-template <int MAXR>
-__device__ __forceinline__ int b2_two_pairs(double (&a0r)[MAXR], double (&a0i)[MAXR], double (&b0r)[MAXR],
-                                            double (&b0i)[MAXR], B2Col& a0, B2Col& b0, double (&a1r)[MAXR],
-                                            double (&a1i)[MAXR], double (&b1r)[MAXR], double (&b1i)[MAXR],
-                                            B2Col& a1, B2Col& b1, double tol2, double floor2, double tiny2,
-                                            int& rot, int& big) {
-  double gAx, gAy, gBx, gBy;
-  b2_dot<MAXR>(a0r, a0i, b0r, b0i, gAx, gAy);
-  b2_dot<MAXR>(a1r, a1i, b1r, b1i, gBx, gBy);
-  gAx = aqc::row_sum16(gAx) * (a0.d * b0.d);
-  gAy = aqc::row_sum16(gAy) * (a0.d * b0.d);
-  gBx = aqc::row_sum16(gBx) * (a1.d * b1.d);
-  gBy = aqc::row_sum16(gBy) * (a1.d * b1.d);
-  const bool goA = gAx * gAx + gAy * gAy > tol2 * (a0.n * b0.n) && a0.n > floor2 && b0.n > floor2;
-  const bool goB = gBx * gBx + gBy * gBy > tol2 * (a1.n * b1.n) && a1.n > floor2 && b1.n > floor2;
-  if (goA || goB) {
-    const B2Coef kA = b2_coef(a0, b0, gAx, gAy, goA, tol2, tiny2, rot, big);
-    const B2Coef kB = b2_coef(a1, b1, gBx, gBy, goB, tol2, tiny2, rot, big);
-    b2_apply<MAXR>(a0r, a0i, b0r, b0i, kA);
-    b2_apply<MAXR>(a1r, a1i, b1r, b1i, kB);
-    b2_post<MAXR>(a0r, a0i, b0r, b0i, a0, b0, kA);
-    b2_post<MAXR>(a1r, a1i, b1r, b1i, a1, b1, kB);
-  }
-  return (goA ? 1 : 0) | (goB ? 2 : 0);
-}
-
-__global__ __launch_bounds__(512) void k_jacobi_b2(const TwoSiteJob* __restrict__ jobs) {
-  constexpr int CP = 128, MAXR = 8, LPG = 16, kG = 32, kThreads = 512;
-  constexpr int ld = CP;        // slot column stride (complex); a slot = 2 columns
-  constexpr int ldt = CP + 1;   // transpose-buffer stride
-  const TwoSiteJob& j = jobs[blockIdx.x];
-  extern __shared__ double2 xbuf[];  // max(2 kG ld, (CP / 2) ldt) complex
-  __shared__ double fred[kThreads / 64];
-  __shared__ int xid[2 * kG];
-  __shared__ double xnrm[2 * kG], xscl[2 * kG], xisc[2 * kG];
-  __shared__ int rot, big;
-  __shared__ unsigned long long pkey[2];
-  __shared__ double2 vb[2][CP];
-  __shared__ double2 tb[2];
-  __shared__ int perm_s[CP];
-  const int chl = j.dims[0], chr = j.dims[2];
-  const int M = 2 * chl, N = 2 * chr;
-  const bool tr = M < N;
-  const int L = tr ? N : M;
-  const int C = tr ? M : N;
-  const bool use_qr = j.qr != 0;
-  const int tid = threadIdx.x;
-  const int g = tid / LPG, lane = tid % LPG;
-  // columns g, g + 32, g + 64, g + 96 of W: S0, S1, then the slot pair M0, M1
-  double xr[4][MAXR], xi[4][MAXR];
-  double f = 0.0;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int c = g + kG * q;
-#pragma unroll
-    for (int i = 0; i < MAXR; ++i) {
-      const int r = lane + LPG * i;
-      double2 a = make_double2(0, 0);
-      if (r < L && c < C) a = tr ? aqc::cconj(j.theta[(size_t)r * M + c]) : j.theta[(size_t)c * M + r];
-      xr[q][i] = a.x;
-      xi[q][i] = a.y;
-      f += a.x * a.x + a.y * a.y;
-    }
-  }
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) f += __shfl_xor(f, off);
-  if ((tid & 63) == 0) fred[tid >> 6] = f;
-  if (tid == 0) pkey[0] = pkey[1] = 0ull;
-  __syncthreads();
-  if (tid == 0) {
-    double s = 0.0;
-#pragma unroll
-    for (int w = 0; w < kThreads / 64; ++w) s += fred[w];
-    fred[0] = s;
-  }
-  int Lj = L;
-  if (use_qr) {
-    int kq[4] = {-1, -1, -1, -1};         // pivot step of each column (-1: not yet)
-    double nq[4] = {0, 0, 0, 0}, nref[4] = {0, 0, 0, 0};  // trailing norms, last exact values
-    for (int k = 0; k < C; ++k) {
-      const int b = k & 1;
-      bool exact = k == 0;
-      if (k > 0) {
-        const int kr = (k - 1) / LPG, kl = (k - 1) % LPG;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          double yr = 0, yi = 0;
-#pragma unroll
-          for (int i = 0; i < MAXR; ++i)
-            if (i == kr) yr = xr[q][i], yi = xi[q][i];
-          nq[q] -= __shfl(fma(yr, yr, yi * yi), kl, LPG);
-          exact = exact || nq[q] <= 1.5e-8 * nref[q];
-        }
-      }
-      if (exact) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          double s = 0;
-#pragma unroll
-          for (int i = 0; i < MAXR; ++i) {
-            const double w = (lane + LPG * i) >= k ? 1.0 : 0.0;
-            s = fma(w, fma(xr[q][i], xr[q][i], xi[q][i] * xi[q][i]), s);
-          }
-          nq[q] = nref[q] = aqc::row_sum16(s);
-        }
-      }
-      unsigned long long key = 0ull;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int c = g + kG * q;
-        const unsigned long long kk = (kq[q] < 0 && c < C) ? pivot_key(nq[q], c) : 0ull;
-        key = kk > key ? kk : key;
-      }
-      if (lane == 0) atomicMax(&pkey[b], key);
-      __syncthreads();
-      const int p = 255 - (int)(pkey[b] & 255ull);
-      if (tid == 0) pkey[b ^ 1] = 0ull;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        if (g + kG * q == p) {  // this group owns the pivot column: build the reflector
-          qr_reflector<MAXR, LPG>(xr[q], xi[q], k, lane, vb[b], &tb[b]);
-          kq[q] = k;
-        }
-      }
-      if (tid == 0) perm_s[k] = p;
-      __syncthreads();
-      const double2 tau = tb[b];
-      double wr[4] = {0, 0, 0, 0}, wi[4] = {0, 0, 0, 0};
-#pragma unroll
-      for (int i = 0; i < MAXR; ++i) {  // v^H c for the four columns
-        const double2 v = vb[b][lane + LPG * i];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          wr[q] = fma(v.x, xr[q][i], fma(v.y, xi[q][i], wr[q]));
-          wi[q] = fma(v.x, xi[q][i], fma(-v.y, xr[q][i], wi[q]));
-        }
-      }
-      double fr[4], fi[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const double a = kq[q] < 0 ? 1.0 : 0.0;
-        const double sr_ = aqc::row_sum16(wr[q]), si_ = aqc::row_sum16(wi[q]);
-        fr[q] = a * (tau.x * sr_ + tau.y * si_);
-        fi[q] = a * (tau.x * si_ - tau.y * sr_);
-      }
-      asm volatile("" ::: "memory");  // re-read v below instead of keeping it live
-#pragma unroll
-      for (int i = 0; i < MAXR; ++i) {
-        const double2 v = vb[b][lane + LPG * i];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          xr[q][i] = fma(-v.x, fr[q], fma(v.y, fi[q], xr[q][i]));
-          xi[q][i] = fma(-v.x, fi[q], fma(-v.y, fr[q], xi[q][i]));
-        }
-      }
-    }
-    // X = R^H through LDS, half of R's rows at a time: half h holds R rows [64h, 64h + 64) as
-    // xbuf[jx * ldt + pivot step]; X column 64h + jx is row jx there.  This group's X columns
-    // are g + 32 q (q = 0..3): q = 0, 1 from half 0 and q = 2, 3 from half 1.
-    double ur[4][MAXR], ui[4][MAXR];
-    constexpr int H = MAXR / 2;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-#pragma unroll
-        for (int i = h * H; i < (h + 1) * H; ++i) {
-          const int jx = lane + LPG * (i - h * H);
-          if (kq[q] >= 0) xbuf[jx * ldt + kq[q]] = make_double2(xr[q][i], -xi[q][i]);
-        }
-      }
-      __syncthreads();
-#pragma unroll
-      for (int c2 = 0; c2 < 2; ++c2) {
-        const int xc = g + kG * c2;  // local row of xbuf = X column 64h + xc
-        const bool real_col = 64 * h + xc < C;
-#pragma unroll
-        for (int i = 0; i < MAXR; ++i) {
-          const int r = lane + LPG * i;  // X row = pivot step
-          double2 v = make_double2(0, 0);
-          if (real_col && r < C) v = xbuf[xc * ldt + r];
-          ur[2 * h + c2][i] = v.x;
-          ui[2 * h + c2][i] = v.y;
-        }
-      }
-      __syncthreads();
-    }
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-#pragma unroll
-      for (int i = 0; i < MAXR; ++i) xr[q][i] = ur[q][i], xi[q][i] = ui[q][i];
-    Lj = C;
-  }
-  __syncthreads();
-  const double floor2 = fred[0] * 1e-24;
-  const double tol = j.jtol * (double)Lj * 2.220446049250313e-16;
-  const double tol2 = tol * tol;
-  const double tiny2 = j.jtiny * j.jtiny;
-  const int max_sweeps = j.dbg == 1 ? 0 : kMaxSweeps;
-  const bool map_rows = use_qr && j.dbg != 1;
-  // slot g <- (M0, M1) = columns g + 64, g + 96
-#pragma unroll
-  for (int i = 0; i < MAXR; ++i) {
-    xbuf[(2 * g) * ld + lane + LPG * i] = make_double2(xr[2][i], xi[2][i]);
-    xbuf[(2 * g + 1) * ld + lane + LPG * i] = make_double2(xr[3][i], xi[3][i]);
-  }
-  if (lane == 0) {
-    xid[2 * g] = g + 2 * kG;
-    xid[2 * g + 1] = g + 3 * kG;
-    xscl[2 * g] = xscl[2 * g + 1] = 1.0;
-  }
-  int sid0 = g, sid1 = g + kG;
-  B2Col s0{0.0, 1.0, 1.0}, s1{0.0, 1.0, 1.0};
-  int sweeps = 0;
-  for (sweeps = 0; sweeps < max_sweeps; ++sweeps) {
-    __syncthreads();
-    int my_rot = 0, my_big = 0;
-    {  // sweep start: fold the scales, exact norms, then the intra pairs (S0,S1) and own (M0,M1)
-      double2* own0 = xbuf + (2 * g) * ld;
-      double2* own1 = own0 + ld;
-      const double od0 = xscl[2 * g], od1 = xscl[2 * g + 1];
-      double a0 = 0, a1 = 0, b0 = 0, b1 = 0;
-#pragma unroll
-      for (int i = 0; i < MAXR; ++i) {
-        xr[0][i] *= s0.d, xi[0][i] *= s0.d;
-        xr[1][i] *= s1.d, xi[1][i] *= s1.d;
-        const double2 v0 = own0[lane + LPG * i], v1 = own1[lane + LPG * i];
-        xr[2][i] = v0.x * od0, xi[2][i] = v0.y * od0;
-        xr[3][i] = v1.x * od1, xi[3][i] = v1.y * od1;
-        a0 = fma(xr[0][i], xr[0][i], fma(xi[0][i], xi[0][i], a0));
-        a1 = fma(xr[1][i], xr[1][i], fma(xi[1][i], xi[1][i], a1));
-        b0 = fma(xr[2][i], xr[2][i], fma(xi[2][i], xi[2][i], b0));
-        b1 = fma(xr[3][i], xr[3][i], fma(xi[3][i], xi[3][i], b1));
-      }
-      s0 = B2Col{aqc::row_sum16(a0), 1.0, 1.0};
-      s1 = B2Col{aqc::row_sum16(a1), 1.0, 1.0};
-      B2Col m0{aqc::row_sum16(b0), 1.0, 1.0}, m1{aqc::row_sum16(b1), 1.0, 1.0};
-      b2_two_pairs<MAXR>(xr[0], xi[0], xr[1], xi[1], s0, s1, xr[2], xi[2], xr[3], xi[3], m0, m1, tol2, floor2,
-                         tiny2, my_rot, my_big);
-#pragma unroll
-      for (int i = 0; i < MAXR; ++i) {
-        own0[lane + LPG * i] = make_double2(xr[2][i], xi[2][i]);
-        own1[lane + LPG * i] = make_double2(xr[3][i], xi[3][i]);
-      }
-      __builtin_amdgcn_wave_barrier();
-      if (lane == 0) {
-        xnrm[2 * g] = m0.n, xscl[2 * g] = m0.d, xisc[2 * g] = m0.id;
-        xnrm[2 * g + 1] = m1.n, xscl[2 * g + 1] = m1.d, xisc[2 * g + 1] = m1.id;
-      }
-      if (tid == 0) rot = big = 0;
-    }
-    __syncthreads();
-    for (int m = kG; m >= 1; m >>= 1) {  // level: sub-blocks of m groups
-      const int li = g & (m - 1), base = g - li;
-      for (int r = 0; r < m; ++r) {
-        const int slot = base + ((li + r) & (m - 1));
-        double2* col0 = xbuf + (2 * slot) * ld;
-        double2* col1 = col0 + ld;
-#pragma unroll
-        for (int i = 0; i < MAXR; ++i) {
-          const double2 v0 = col0[lane + LPG * i], v1 = col1[lane + LPG * i];
-          xr[2][i] = v0.x, xi[2][i] = v0.y;
-          xr[3][i] = v1.x, xi[3][i] = v1.y;
-        }
-        B2Col m0{xnrm[2 * slot], xscl[2 * slot], xisc[2 * slot]};
-        B2Col m1{xnrm[2 * slot + 1], xscl[2 * slot + 1], xisc[2 * slot + 1]};
-        // step A: (S0, M0), (S1, M1); step B: (S0, M1), (S1, M0)
-        const int ra = b2_two_pairs<MAXR>(xr[0], xi[0], xr[2], xi[2], s0, m0, xr[1], xi[1], xr[3], xi[3], s1, m1,
-                                          tol2, floor2, tiny2, my_rot, my_big);
-        const int rb = b2_two_pairs<MAXR>(xr[0], xi[0], xr[3], xi[3], s0, m1, xr[1], xi[1], xr[2], xi[2], s1, m0,
-                                          tol2, floor2, tiny2, my_rot, my_big);
-        const bool d0 = (ra & 1) || (rb & 2), d1 = (ra & 2) || (rb & 1);
-        if (d0) {
-#pragma unroll
-          for (int i = 0; i < MAXR; ++i) col0[lane + LPG * i] = make_double2(xr[2][i], xi[2][i]);
-        }
-        if (d1) {
-#pragma unroll
-          for (int i = 0; i < MAXR; ++i) col1[lane + LPG * i] = make_double2(xr[3][i], xi[3][i]);
-        }
-        __builtin_amdgcn_wave_barrier();
-        if (lane == 0) {
-          if (d0) xnrm[2 * slot] = m0.n, xscl[2 * slot] = m0.d, xisc[2 * slot] = m0.id;
-          if (d1) xnrm[2 * slot + 1] = m1.n, xscl[2 * slot + 1] = m1.d, xisc[2 * slot + 1] = m1.id;
-        }
-        __syncthreads();
-      }
-      if (m == 1) break;
-      const int h = m >> 1;
-      if (li >= h) {  // upper half: (S0, S1) <-> slot g - h (vectors, ids, norms, scales)
-        double2* col0 = xbuf + (2 * (g - h)) * ld;
-        double2* col1 = col0 + ld;
-#pragma unroll
-        for (int i = 0; i < MAXR; ++i) {
-          const double2 v0 = col0[lane + LPG * i], v1 = col1[lane + LPG * i];
-          col0[lane + LPG * i] = make_double2(xr[0][i], xi[0][i]);
-          col1[lane + LPG * i] = make_double2(xr[1][i], xi[1][i]);
-          xr[0][i] = v0.x, xi[0][i] = v0.y;
-          xr[1][i] = v1.x, xi[1][i] = v1.y;
-        }
-        const int q = 2 * (g - h);
-        const int pid0 = xid[q], pid1 = xid[q + 1];
-        const B2Col p0{xnrm[q], xscl[q], xisc[q]}, p1{xnrm[q + 1], xscl[q + 1], xisc[q + 1]};
-        __builtin_amdgcn_wave_barrier();
-        if (lane == 0) {
-          xid[q] = sid0, xnrm[q] = s0.n, xscl[q] = s0.d, xisc[q] = s0.id;
-          xid[q + 1] = sid1, xnrm[q + 1] = s1.n, xscl[q + 1] = s1.d, xisc[q + 1] = s1.id;
-        }
-        sid0 = pid0, sid1 = pid1, s0 = p0, s1 = p1;
-      }
-      __syncthreads();
-    }
-    if (my_rot && lane == 0) atomicAdd(&rot, 1);
-    if (my_big && lane == 0) atomicAdd(&big, 1);
-    __syncthreads();
-    if (rot == 0 || big == 0) break;
-  }
-  __syncthreads();
-  // output: S0, S1 from VGPRs, slot g's pair from LDS, scales applied, rows mapped back through
-  // the pivot order
-  double2* W = j.work;
-  const int cid[4] = {sid0, sid1, xid[2 * g], xid[2 * g + 1]};
-  const double cs[4] = {s0.d, s1.d, xscl[2 * g], xscl[2 * g + 1]};
-  double nn[4] = {0, 0, 0, 0};
-#pragma unroll
-  for (int i = 0; i < MAXR; ++i) {
-    const int row = lane + LPG * i;
-    double2 v[4];
-    v[0] = make_double2(xr[0][i], xi[0][i]);
-    v[1] = make_double2(xr[1][i], xi[1][i]);
-    v[2] = xbuf[(2 * g) * ld + row];
-    v[3] = xbuf[(2 * g + 1) * ld + row];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      v[q].x *= cs[q];
-      v[q].y *= cs[q];
-      nn[q] = fma(v[q].x, v[q].x, fma(v[q].y, v[q].y, nn[q]));
-      if (row < Lj && cid[q] < C) W[(size_t)cid[q] * Lj + (map_rows ? perm_s[row] : row)] = v[q];
-    }
-  }
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    nn[q] = aqc::row_sum16(nn[q]);
-    if (lane == 0 && cid[q] < C) j.sig[cid[q]] = sqrt(nn[q]);
-  }
-  if (tid == 0) {
-    if (sweeps >= kMaxSweeps) atomicOr(&j.flags[1], 1);
-    atomicMax(&j.flags[2], sweeps + 1);
-  }
-  if (j.dbg == 1 && use_qr) {
-    for (int k = tid; k < C; k += kThreads) j.perm[k] = perm_s[k];
-  }
-}
-
-// 2 chi = 128 register Jacobi by variant: 5 = 8-lane groups (512 threads), 6 = 4-lane groups
-// (256 threads), 7 = block pairs (k_jacobi_b2, 512 threads), otherwise 16-lane groups (1024
-// threads).  Dynamic LDS = kG x max(ld, CP + 1) complex.
+// 2 chi = 128 register Jacobi by variant: 5 = 8-lane groups (512 threads), otherwise 16-lane
+// groups (1024 threads).  Dynamic LDS = kG x max(ld, CP + 1) complex.  Measured on the bench's
+// thetas (tools/jacobi_ab.py, tools/svd_phase_timing.py): 8-lane groups cut the round's VALU
+// instructions by 26% but, at two waves per SIMD, run the sweeps at the same speed and the QR
+// phase 20% slower; 4-lane groups (one wave per SIMD, AGPR spills) 1.9x slower; four columns
+// per group with two independent rotations per step (git history, "block-pair register
+// Jacobi") 11% slower.
 void launch_jacobi_reg128(int variant, int nj, hipStream_t st, const TwoSiteJob* jp) {
-  if (variant == 7)
-    hipLaunchKernelGGL(k_jacobi_b2, dim3(nj), dim3(512), 64 * 129 * 16, st, jp);
-  else if (variant == 5)
+  if (variant == 5)
     hipLaunchKernelGGL((k_jacobi_reg<128, 16, 8>), dim3(nj), dim3(512), 64 * 136 * 16, st, jp);
-  else if (variant == 6)
-    hipLaunchKernelGGL((k_jacobi_reg<128, 32, 4>), dim3(nj), dim3(256), 64 * 132 * 16, st, jp);
   else
     hipLaunchKernelGGL((k_jacobi_reg<128, 8>), dim3(nj), dim3(1024), 64 * 129 * 16, st, jp);
 }
@@ -1911,7 +1478,7 @@ int run_waves(aqc_mps_t* hs, int ns, std::vector<std::vector<DevOp>>& lists) {
   std::vector<std::pair<size_t, size_t>> two_rng(maxlen), one_rng(maxlen);
   int cap_max = 0;
   for (int s = 0; s < ns; ++s) cap_max = std::max(cap_max, hs[s]->d.cap);
-  const bool reg = (g_jacobi_variant == 2 || g_jacobi_variant == 3 || g_jacobi_variant >= 5) && 2 * cap_max <= 128;
+  const bool reg = (g_jacobi_variant == 2 || g_jacobi_variant == 3 || g_jacobi_variant == 5) && 2 * cap_max <= 128;
   const int use_qr = reg && g_jacobi_variant != 3 ? 1 : 0;
   for (size_t w = 0; w < maxlen; ++w) {
     size_t t0 = two.size(), o0 = one.size();
@@ -2184,8 +1751,8 @@ int aqc_svd_debug(const double* theta, int m, int n, int variant, int stop_after
   AQC_REQUIRE(theta && w_out && sig_out && sweeps, "aqc_svd_debug: null argument");
   AQC_REQUIRE(m >= 1 && n >= 1 && m % 2 == 0 && n % 2 == 0 && m <= 128 && n <= 128,
               "aqc_svd_debug: m, n must be even and <= 128");
-  AQC_REQUIRE(variant == 2 || variant == 3 || variant >= 5 && variant <= 7,
-              "aqc_svd_debug: variant must be 2, 3, 5, 6 or 7");
+  AQC_REQUIRE(variant == 2 || variant == 3 || variant == 5,
+              "aqc_svd_debug: variant must be 2, 3 or 5");
   hipStream_t st = aqc::mps_stream();
   const int cp = std::max(m, n) <= 32 ? 32 : (std::max(m, n) <= 64 ? 64 : 128);
   const size_t mat = (size_t)128 * 128 * sizeof(cplx);
@@ -2257,7 +1824,7 @@ int aqc_mps_set_jacobi_stop(double tiny_t) {
 }
 
 int aqc_mps_set_jacobi_variant(int variant) {
-  AQC_REQUIRE(variant >= 0 && variant <= 7, "aqc_mps_set_jacobi_variant: variant must be 0..7");
+  AQC_REQUIRE(variant >= 0 && variant <= 5, "aqc_mps_set_jacobi_variant: variant must be 0..5");
   g_jacobi_variant = variant;
   return AQC_OK;
 }

@@ -103,11 +103,12 @@ int aqc_mps_jacobi_stats(aqc_mps_t h, int* max_sweeps);
 /* Jacobi rotation threshold |a^H b| > factor * L * eps * |a||b| (default factor 1). */
 int aqc_mps_set_jacobi_tol(double factor);
 /* Jacobi sweep stop: after a sweep whose counted rotations all had |t| <= tiny_t the
-   decomposition ends (default 1e-8; tiny_t <= 0 restores it; must be < 1e-3). */
+   decomposition ends (default 1e-6: the off-diagonal left is O(1e-12) relative; tiny_t <= 0
+   restores it; must be < 1e-3). */
 int aqc_mps_set_jacobi_stop(double tiny_t);
 /* Jacobi kernel: 2 = register-resident columns with pivoted-QR preconditioning for
    2*chi <= 128 (default; larger chi uses 0), 3 = register-resident without QR,
-   5 / 6 = as 2 with 8- / 4-lane column groups at 2*chi = 128 (512 / 256 threads),
+   5 = as 2 with 8-lane column groups at 2*chi = 128 (512 threads),
    0 = 512 threads / 128 KiB LDS panel, 1 = 256 threads / 64 KiB panel (2 per CU). */
 int aqc_mps_set_jacobi_variant(int variant);
 /* ---- ISL entanglement sweep (adapt_compiler.py:955-976 -> entanglement_measures.py:39-98) ----

@@ -195,7 +195,7 @@ def test_batch_apply_matches_single():
         assert abs(d.overlap_zero() - ov[s]) < 1e-13
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 5, 6, 7])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 5])
 def test_jacobi_variants_vs_oracle(goldens, variant):
     """Every Jacobi kernel shape reproduces the oracle (small, ragged and full-width theta)."""
     from adaptaqc_amd import _lib
@@ -245,7 +245,7 @@ def test_copy_batch_matches_single_copies(random_mps):
             np.testing.assert_array_equal(b, b2)
 
 
-@pytest.mark.parametrize("variant", [2, 5, 7])
+@pytest.mark.parametrize("variant", [2, 5])
 def test_jacobi_stop_rule_vs_oracle(variant):
     """A looser sweep stop (last sweep's rotations all |t| <= 1e-6 or 1e-5) keeps a 16-qubit chi = 64
     replay (max_chi binding, 2 chi = 128 thetas) within 1e-9 of the oracle's overlap."""
