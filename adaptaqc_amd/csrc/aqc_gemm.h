@@ -76,9 +76,13 @@ typedef double __attribute__((ext_vector_type(4))) d4_t;
 // PREFETCH: fetch the next k tile into registers while the MFMAs run on the current one (pays
 // where the tile loads are the latency, e.g. the split's indirect column reads: 8.9 -> 7.6
 // ms/step; it costs the register-heavy ISL chain 20%).
+// tid_in >= 0: the caller's 256-thread sub-group rank (several sub-groups of a larger workgroup
+// each running their own block; every sub-group must then make the same calls with the same m, n,
+// k so the barriers pair up); active = false runs only those barriers (an idle sub-group).
 template <bool A_KFAST = false, bool B_KFAST = false, bool PREFETCH = false, typename FA, typename FB, typename FS>
-__device__ __forceinline__ void block_cgemm(int m, int n, int k, FA a, FB b, FS store, GemmLds& lds) {
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+__device__ __forceinline__ void block_cgemm(int m, int n, int k, FA a, FB b, FS store, GemmLds& lds, int tid_in = -1,
+                                            bool active = true) {
+  const int tid = tid_in >= 0 ? tid_in : (int)threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int wr = (wave >> 1) * 32, wc = (wave & 1) * 32;
   const int li = lane & 15, lk = lane >> 4;
   for (int bi = 0; bi < m; bi += 64) {
@@ -99,8 +103,11 @@ __device__ __forceinline__ void block_cgemm(int m, int n, int k, FA a, FB b, FS 
           pb[q] = (bj + ib < n && k0 + kb < k) ? b(k0 + kb, bj + ib) : cmk(0, 0);
         }
       };
-      if constexpr (PREFETCH) fetch(0);
+      if constexpr (PREFETCH) {
+        if (active) fetch(0);
+      }
       for (int k0 = 0; k0 < k; k0 += 16) {
+        if (active) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int e = tid + q * kGemmThreads;
@@ -114,10 +121,12 @@ __device__ __forceinline__ void block_cgemm(int m, int n, int k, FA a, FB b, FS 
             lds.Bs[kb][ib] = (bj + ib < n && k0 + kb < k) ? b(k0 + kb, bj + ib) : cmk(0, 0);
           }
         }
+        }
         __syncthreads();
         if constexpr (PREFETCH) {
-          if (k0 + 16 < k) fetch(k0 + 16);
+          if (active && k0 + 16 < k) fetch(k0 + 16);
         }
+        if (active) {
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks) {
           const int kk = 4 * ks + lk;
@@ -137,6 +146,7 @@ __device__ __forceinline__ void block_cgemm(int m, int n, int k, FA a, FB b, FS 
               ci[r][c] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[r].y, bv[c].x, ci[r][c], 0, 0, 0);
             }
         }
+        }
         __syncthreads();
       }
 #pragma unroll
@@ -146,7 +156,7 @@ __device__ __forceinline__ void block_cgemm(int m, int n, int k, FA a, FB b, FS 
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             const int i = bi + wr + 16 * r + lk + 4 * q, jj = bj + wc + 16 * c + li;
-            if (i < m && jj < n) store(i, jj, cmk(cr[r][c][q], ci[r][c][q]));
+            if (active && i < m && jj < n) store(i, jj, cmk(cr[r][c][q], ci[r][c][q]));
           }
     }
   }

@@ -47,6 +47,9 @@ double g_jacobi_tol_factor = 1.0;
 constexpr double kDefaultTinyT = 1e-6;
 double g_jacobi_tiny_t = kDefaultTinyT;
 int g_jacobi_variant = 2;
+// Fused per-state chain (k_chain) for batches of >= kChainMinStates states at 2 chi = 128.
+bool g_fused_chain = true;
+constexpr int kChainMinStates = 32;
 
 struct OneSiteJob {
   cplx* g;
@@ -436,8 +439,9 @@ __device__ __forceinline__ void qr_reflector(double (&xr)[MAXR], double (&xi)[MA
 
 // LPG = lanes per column group (16: 1024 threads at CP = 128; 8: 512 threads with 16 rows per
 // lane, the per-pair rotation parameters and reductions amortised over twice the rows).
+// (The body is a device function so that the fused per-state chain, k_chain, runs it too.)
 template <int CP, int MAXR, int LPG = 16>
-__global__ __launch_bounds__(CP / 2 * LPG) void k_jacobi_reg(const TwoSiteJob* __restrict__ jobs) {
+__device__ __forceinline__ void jacobi_reg_body(const TwoSiteJob& j) {
   static_assert(LPG * MAXR == CP, "LPG lanes x MAXR rows must cover the CP rows of a column");
   constexpr int kG = CP / 2;       // groups
   constexpr int kThreads = kG * LPG;
@@ -445,7 +449,6 @@ __global__ __launch_bounds__(CP / 2 * LPG) void k_jacobi_reg(const TwoSiteJob* _
   // that consecutive slots alternate LDS bank halves (a ds_read_b128 lane group spans groups)
   constexpr int ld = LPG * MAXR + (LPG < 16 ? LPG : 0);
   constexpr int ldt = CP + 1;      // transpose-buffer stride (odd: conflict-free column writes)
-  const TwoSiteJob& j = jobs[blockIdx.x];
   extern __shared__ double2 xbuf[];  // max(kG * ld, kG * ldt) complex
   __shared__ double fred[kThreads / 64];
   __shared__ int xid[kG];
@@ -493,6 +496,19 @@ __global__ __launch_bounds__(CP / 2 * LPG) void k_jacobi_reg(const TwoSiteJob* _
     fred[0] = s;
   }
   int Lj = L;  // row count of the matrix the Jacobi sees
+  // dbg == 2 (aqc_svd_debug mode 2): thread 0 accumulates shader-clock ticks of the QR step's
+  // phases -- [0] downdate + pivot key, [1] pivot barrier, [2] reflector + its barrier, [3] update
+  // (kept in LDS, not registers: the QR loop has no VGPRs to spare)
+  __shared__ unsigned long long qt[5];  // 4 phase totals, last tick
+  const bool qtime = j.dbg == 2 && tid == 0;
+  if (qtime) qt[0] = qt[1] = qt[2] = qt[3] = qt[4] = 0;
+  auto qtick = [&](int ph) {
+    if (qtime) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      if (ph >= 0) qt[ph] += t - qt[4];
+      qt[4] = t;
+    }
+  };
   if (use_qr) {
     int ks = -1, km = -1;  // pivot step of S / M (-1: not pivoted yet)
     // Trailing squared norms (rows >= k) of S and M, downdated by the row leaving the trailing
@@ -502,6 +518,7 @@ __global__ __launch_bounds__(CP / 2 * LPG) void k_jacobi_reg(const TwoSiteJob* _
     for (int k = 0; k < C; ++k) {
       const int b = k & 1;
       bool exact = k == 0;
+      qtick(k == 0 ? -1 : 3);
       if (k > 0) {
         const int kr = (k - 1) / LPG, kl = (k - 1) % LPG;
         double xsr = 0, xsi = 0, xmr = 0, xmi = 0;  // row k-1 (select first, square once)
@@ -528,8 +545,10 @@ __global__ __launch_bounds__(CP / 2 * LPG) void k_jacobi_reg(const TwoSiteJob* _
       const unsigned long long ka = (ks < 0 && sid < C) ? pivot_key(ns, sid) : 0ull;
       const unsigned long long kb = (km < 0 && mid < C) ? pivot_key(nm, mid) : 0ull;
       if (lane == 0) atomicMax(&pkey[b], ka > kb ? ka : kb);
+      qtick(0);
       __syncthreads();
       const int p = 255 - (int)(pkey[b] & 255ull);
+      qtick(1);
       if (tid == 0) pkey[b ^ 1] = 0ull;
       if (sid == p) {  // this group owns the pivot column: build the reflector
         qr_reflector<MAXR, LPG>(sr, si, k, lane, vb[b], &tb[b]);
@@ -540,6 +559,7 @@ __global__ __launch_bounds__(CP / 2 * LPG) void k_jacobi_reg(const TwoSiteJob* _
       }
       if (tid == 0) perm_s[k] = p;
       __syncthreads();
+      qtick(2);
       // c <- H^H c = c - conj(tau) v (v^H c) for every unpivoted column
       const double2 tau = tb[b];
       double wsr = 0, wsi = 0, wmr = 0, wmi = 0;
@@ -607,8 +627,9 @@ __global__ __launch_bounds__(CP / 2 * LPG) void k_jacobi_reg(const TwoSiteJob* _
   const double floor2 = fred[0] * 1e-24;
   const double tol = j.jtol * (double)Lj * 2.220446049250313e-16;
   const double tol2 = tol * tol;
-  const int max_sweeps = j.dbg == 1 ? 0 : kMaxSweeps;
-  const bool map_rows = use_qr && j.dbg != 1;
+  qtick(3);
+  const int max_sweeps = j.dbg >= 1 ? 0 : kMaxSweeps;
+  const bool map_rows = use_qr && j.dbg == 0;
   // The M half of the columns moves into LDS slots (slot g <- this group's M) and stays there:
   // S stays in VGPRs.  Round r of a level with sub-blocks of m groups pairs S_g with slot
   // base + (li + r) mod m -- the parallel ordering's shift is addressing only -- and a slot is
@@ -814,9 +835,17 @@ __global__ __launch_bounds__(CP / 2 * LPG) void k_jacobi_reg(const TwoSiteJob* _
     if (sweeps >= kMaxSweeps) atomicOr(&j.flags[1], 1);
     atomicMax(&j.flags[2], sweeps + 1);
   }
-  if (j.dbg == 1 && use_qr) {  // diagnostics: pivot order after the W columns
+  if (qtime) {
+    for (int ph = 0; ph < 4; ++ph) j.sig[ph] = (double)qt[ph];
+  }
+  if (j.dbg >= 1 && use_qr) {  // diagnostics: pivot order after the W columns
     for (int k = tid; k < C; k += kThreads) j.perm[k] = perm_s[k];
   }
+}
+
+template <int CP, int MAXR, int LPG = 16>
+__global__ __launch_bounds__(CP / 2 * LPG) void k_jacobi_reg(const TwoSiteJob* __restrict__ jobs) {
+  jacobi_reg_body<CP, MAXR, LPG>(jobs[blockIdx.x]);
 }
 
 // 2 chi = 128 register Jacobi by variant: 5 = 8-lane groups (512 threads), otherwise 16-lane
@@ -834,8 +863,8 @@ void launch_jacobi_reg128(int variant, int nj, hipStream_t st, const TwoSiteJob*
 }
 
 // Sort singular values, apply reduce_zeros, write lambda_m / dims[1] / perm / sorted sig.
-__global__ __launch_bounds__(kT) void k_rank(const TwoSiteJob* __restrict__ jobs) {
-  const TwoSiteJob& j = jobs[blockIdx.x];
+template <int NT>
+__device__ __forceinline__ void rank_body(const TwoSiteJob& j) {
   __shared__ double sv[512];
   __shared__ int si[512];
   __shared__ int kk_s;
@@ -846,7 +875,7 @@ __global__ __launch_bounds__(kT) void k_rank(const TwoSiteJob* __restrict__ jobs
   int P = 1;
   while (P < C) P <<= 1;
   const int tid = threadIdx.x;
-  for (int i = tid; i < P; i += kT) {
+  for (int i = tid; i < P; i += NT) {
     sv[i] = i < C ? j.sig[i] : -1.0;
     si[i] = i;
   }
@@ -854,7 +883,7 @@ __global__ __launch_bounds__(kT) void k_rank(const TwoSiteJob* __restrict__ jobs
   // bitonic sort, descending by value, ascending index on ties
   for (int k = 2; k <= P; k <<= 1) {
     for (int s = k >> 1; s > 0; s >>= 1) {
-      for (int i = tid; i < P; i += kT) {
+      for (int i = tid; i < P; i += NT) {
         const int ixj = i ^ s;
         if (ixj > i) {
           const bool desc = (i & k) == 0;
@@ -895,16 +924,18 @@ __global__ __launch_bounds__(kT) void k_rank(const TwoSiteJob* __restrict__ jobs
   }
   __syncthreads();
   const int k = kk_s;
-  for (int i = tid; i < k; i += kT) {
+  for (int i = tid; i < k; i += NT) {
     j.lm[i] = sv[i] / norm_s;
     j.perm[i] = si[i];
     j.sig[i + 512] = sv[i];  // sorted copy lives past the raw norms
   }
 }
 
+__global__ __launch_bounds__(kT) void k_rank(const TwoSiteJob* __restrict__ jobs) { rank_body<kT>(jobs[blockIdx.x]); }
+
 // Orthogonalised side: copy (scaled) columns of W into the Gamma they define.
-__global__ __launch_bounds__(kT) void k_split_copy(const TwoSiteJob* __restrict__ jobs) {
-  const TwoSiteJob& j = jobs[blockIdx.y];
+// Element e = start, start + stride, ... of the copy.
+__device__ __forceinline__ void split_copy_body(const TwoSiteJob& j, int start, int stride) {
   const int chl = j.dims[0], k = j.dims[1], chr = j.dims[2];
   const int M = 2 * chl, N = 2 * chr;
   // tr: W's columns are V-side (length N); the QR-preconditioned Jacobi flips the side
@@ -915,7 +946,7 @@ __global__ __launch_bounds__(kT) void k_split_copy(const TwoSiteJob* __restrict_
   const double* ss = j.sig + 512;
   if (!tr) {
     // Gp'[s1][l][kk] = W[perm kk][s1*chl + l] / sig_kk / ll[l]
-    for (int e = blockIdx.x * kT + threadIdx.x; e < 2 * chl * k; e += gridDim.x * kT) {
+    for (int e = start; e < 2 * chl * k; e += stride) {
       const int kk = e % k, rr = e / k;
       const int s1 = rr / chl, l = rr % chl;
       const double d = ss[kk] * j.ll[l];
@@ -924,7 +955,7 @@ __global__ __launch_bounds__(kT) void k_split_copy(const TwoSiteJob* __restrict_
     }
   } else {
     // Gq'[s2][kk][r] = conj(W[perm kk][s2*chr + r]) / sig_kk / lr[r]
-    for (int e = blockIdx.x * kT + threadIdx.x; e < 2 * chr * k; e += gridDim.x * kT) {
+    for (int e = start; e < 2 * chr * k; e += stride) {
       const int cc = e % N, kk = e / N;
       const int s2 = cc / chr, r = cc % chr;
       const double d = ss[kk] * j.lr[r];
@@ -934,14 +965,28 @@ __global__ __launch_bounds__(kT) void k_split_copy(const TwoSiteJob* __restrict_
   }
 }
 
+__global__ __launch_bounds__(kT) void k_split_copy(const TwoSiteJob* __restrict__ jobs) {
+  split_copy_body(jobs[blockIdx.y], blockIdx.x * kT + threadIdx.x, gridDim.x * kT);
+}
+
 // Other side by one GEMM against the original theta (64 x 64 output blocks per workgroup,
 // register-blocked, aqc_gemm.h):
 //   !tr: Vh[kk][c] = sum_R conj(W_j[R]) theta[R][c] / sig^2 -> Gq'[s2][kk][r] = Vh / lr[r]
 //    tr: U[R][kk]  = sum_c theta[R][c] W_j[c] / sig^2      -> Gp'[s1][l][kk] = U / ll[l]
 // (tr: W's columns are V-side; the QR-preconditioned Jacobi flips the side, see k_split_copy.)
-__global__ __launch_bounds__(aqc::kGemmThreads) void k_split_gemm(const TwoSiteJob* __restrict__ jobs) {
-  const TwoSiteJob& j = jobs[blockIdx.y];
-  __shared__ aqc::GemmLds lds;
+// Output block blk (64 x 64) of the split GEMM.  ltid >= 0: the caller's rank in a 256-thread
+// sub-group of the fused chain, where an empty block still runs block_cgemm's barriers (inactive)
+// so that the sub-groups' barriers pair up; the standalone kernel skips empty blocks instead.
+__device__ __forceinline__ bool split_block_active(const TwoSiteJob& j, int blk) {
+  const int chl = j.dims[0], k = j.dims[1], chr = j.dims[2];
+  const int M = 2 * chl, N = 2 * chr;
+  const bool tr = (M < N) != (j.qr != 0);
+  const int rows = tr ? M : k, cols = tr ? k : N;
+  const int bcols = (2 * j.cap + 63) / 64;
+  return (blk / bcols) * 64 < rows && (blk % bcols) * 64 < cols;
+}
+
+__device__ __forceinline__ void split_gemm_body(const TwoSiteJob& j, int blk, aqc::GemmLds& lds, int ltid) {
   const int chl = j.dims[0], k = j.dims[1], chr = j.dims[2];
   const int M = 2 * chl, N = 2 * chr;
   const bool tr = (M < N) != (j.qr != 0);
@@ -951,9 +996,9 @@ __global__ __launch_bounds__(aqc::kGemmThreads) void k_split_gemm(const TwoSiteJ
   const double* ss = j.sig + 512;
   const int rows = tr ? M : k, cols = tr ? k : N;
   const int bcols = (2 * cap + 63) / 64;
-  const int r0 = (blockIdx.x / bcols) * 64, c0 = (blockIdx.x % bcols) * 64;
-  if (r0 >= rows || c0 >= cols) return;
-  const int mb = min(64, rows - r0), nb = min(64, cols - c0);
+  const int r0 = (blk / bcols) * 64, c0 = (blk % bcols) * 64;
+  const bool active = r0 < rows && c0 < cols;
+  const int mb = active ? min(64, rows - r0) : 64, nb = active ? min(64, cols - c0) : 64;
   const cplx* W = j.work;
   const int* perm = j.perm;
   const cplx* th = j.theta;
@@ -966,7 +1011,7 @@ __global__ __launch_bounds__(aqc::kGemmThreads) void k_split_gemm(const TwoSiteJ
           const double d = ss[kq] * ss[kq] * j.lr[r];
           j.gq[s2 * half + (size_t)kq * cap + r] = d != 0.0 ? aqc::cscale(v, 1.0 / d) : aqc::cmk(0, 0);
         },
-        lds);
+        lds, ltid, active);
   } else {
     aqc::block_cgemm<false, true, true>(
         mb, nb, L, [&](int R, int c) { return th[(size_t)c * M + r0 + R]; },
@@ -976,8 +1021,131 @@ __global__ __launch_bounds__(aqc::kGemmThreads) void k_split_gemm(const TwoSiteJ
           const double d = ss[kq] * ss[kq] * j.ll[l];
           j.gp[s1 * half + (size_t)l * cap + kq] = d != 0.0 ? aqc::cscale(v, 1.0 / d) : aqc::cmk(0, 0);
         },
-        lds);
+        lds, ltid, active);
   }
+}
+
+__global__ __launch_bounds__(aqc::kGemmThreads) void k_split_gemm(const TwoSiteJob* __restrict__ jobs) {
+  const TwoSiteJob& j = jobs[blockIdx.y];
+  __shared__ aqc::GemmLds lds;
+  if (!split_block_active(j, blockIdx.x)) return;
+  split_gemm_body(j, blockIdx.x, lds, -1);
+}
+
+// ---- fused per-state chain (2 chi = 128) ----------------------------------------------------
+// One 1024-thread workgroup runs one state's whole list of device ops -- for a two-site update
+// theta (four 256-thread sub-groups, one P_{s1' s2'} each on the matrix cores, then the gate mix
+// in place), the register Jacobi, the rank / truncation and the split -- with no grid-wide step
+// between updates.  The lock-step batch (run_waves) pays, per update, the slowest decomposition
+// of the whole launch and five launches; here a state's time is the sum of its own updates.
+// theta of job j: sub-group sg computes P_{s1' s2'} (s1' = sg >> 1, s2' = sg & 1) into theta at
+// the position of output (s1', s2'); then every (l, r) mixes its four values through G in place
+// (k_theta's contract).
+__device__ __forceinline__ void theta_chain(const TwoSiteJob& j, aqc::GemmLds* lds) {
+  const int tid = threadIdx.x, sg = tid >> 8, lt = tid & 255;
+  const int chl = j.dims[0], chm = j.dims[1], chr = j.dims[2];
+  const int cap = j.cap, M = 2 * chl;
+  const size_t half = (size_t)cap * cap;
+  const int s1 = sg >> 1, s2 = sg & 1;
+  const cplx* gp = j.gp + s1 * half;
+  const cplx* gq = j.gq + s2 * half;
+  aqc::block_cgemm<true, false>(
+      chl, chr, chm, [&](int l, int m) { return aqc::cscale(gp[(size_t)l * cap + m], j.ll[l] * j.lm[m]); },
+      [&](int m, int r) { return aqc::cscale(gq[(size_t)m * cap + r], j.lr[r]); },
+      [&](int l, int r, cplx v) { j.theta[(size_t)(s2 * chr + r) * M + s1 * chl + l] = v; }, lds[sg], lt);
+  __syncthreads();
+  for (int e = tid; e < chl * chr; e += 1024) {
+    const int l = e / chr, r = e % chr;
+    cplx p[4];
+#pragma unroll
+    for (int in = 0; in < 4; ++in) p[in] = j.theta[(size_t)((in & 1) * chr + r) * M + (in >> 1) * chl + l];
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+      cplx v = aqc::cmul(j.G[o * 4 + 0], p[0]);
+      v = aqc::cfma(j.G[o * 4 + 1], p[1], v);
+      v = aqc::cfma(j.G[o * 4 + 2], p[2], v);
+      v = aqc::cfma(j.G[o * 4 + 3], p[3], v);
+      j.theta[(size_t)((o & 1) * chr + r) * M + (o >> 1) * chl + l] = v;
+    }
+  }
+}
+
+__device__ __forceinline__ void one_site_body(const OneSiteJob& j, int start, int stride) {
+  const int cl = j.dims[0], cr = j.dims[1];
+  const int cap = j.cap;
+  const size_t half = (size_t)cap * cap;
+  for (int e = start; e < cl * cr; e += stride) {
+    const int l = e / cr, r = e % cr;
+    const size_t o = (size_t)l * cap + r;
+    cplx a0 = j.g[o], a1 = j.g[half + o];
+    j.g[o] = aqc::cfma(j.u[1], a1, aqc::cmul(j.u[0], a0));
+    j.g[half + o] = aqc::cfma(j.u[3], a1, aqc::cmul(j.u[2], a0));
+  }
+}
+
+struct ChainJob {
+  const int* ops;  // >= 0: two-site job index; < 0: one-site job -(code + 1)
+  int nops;
+  int pad;
+};
+
+constexpr int kChainLds = 4 * (int)sizeof(aqc::GemmLds);  // >= the Jacobi's 64 x 129 complex
+// phase ticks summed over workgroups: theta, Jacobi, rank, split, one-site
+__device__ unsigned long long g_chain_ticks[5];
+
+// The phases are separate (non-inlined) functions: inlined into one loop body the compiler kept
+// values live across them and spilled hundreds of bytes per lane inside the Jacobi rounds.
+__device__ __noinline__ void chain_theta(const TwoSiteJob& j) {
+  extern __shared__ double2 xbuf[];
+  theta_chain(j, reinterpret_cast<aqc::GemmLds*>(xbuf));
+}
+__device__ __noinline__ void chain_jacobi(const TwoSiteJob& j) { jacobi_reg_body<128, 8, 16>(j); }
+__device__ __noinline__ void chain_rank(const TwoSiteJob& j) { rank_body<1024>(j); }
+__device__ __noinline__ void chain_split(const TwoSiteJob& j) {
+  extern __shared__ double2 xbuf[];
+  const int tid = threadIdx.x;
+  split_copy_body(j, tid, 1024);
+  split_gemm_body(j, tid >> 8, reinterpret_cast<aqc::GemmLds*>(xbuf)[tid >> 8], tid & 255);
+}
+
+__global__ __launch_bounds__(1024) void k_chain(const ChainJob* __restrict__ chains, const TwoSiteJob* __restrict__ two,
+                                                const OneSiteJob* __restrict__ one) {
+  const ChainJob& c = chains[blockIdx.x];
+  const int tid = threadIdx.x;
+  // shader-clock ticks of the phases (thread 0 of each workgroup; aqc_mps_chain_ticks)
+  unsigned long long tk[5] = {0, 0, 0, 0, 0}, t0 = 0;
+  auto tick = [&](int ph) {
+    if (tid == 0) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      if (ph >= 0) tk[ph] += t - t0;
+      t0 = t;
+    }
+  };
+  tick(-1);
+  for (int o = 0; o < c.nops; ++o) {
+    const int code = c.ops[o];
+    if (code < 0) {
+      one_site_body(one[-code - 1], tid, 1024);
+      __syncthreads();
+      tick(4);
+      continue;
+    }
+    const TwoSiteJob& j = two[code];
+    chain_theta(j);
+    __syncthreads();
+    tick(0);
+    chain_jacobi(j);
+    __syncthreads();
+    tick(1);
+    chain_rank(j);
+    __syncthreads();
+    tick(2);
+    chain_split(j);
+    __syncthreads();
+    tick(3);
+  }
+  if (tid == 0)
+    for (int ph = 0; ph < 5; ++ph) atomicAdd(&g_chain_ticks[ph], tk[ph]);
 }
 
 // ---- measurements -------------------------------------------------------------------------
@@ -1455,7 +1623,71 @@ std::vector<std::vector<const DevOp*>> level_ops(const std::vector<DevOp>& ops, 
   return lv;
 }
 
+// Batches at 2 chi = 128: every state's op list runs in one k_chain workgroup (longest lists
+// first, so that the short ones fill in behind them).
+int run_chains(aqc_mps_t* hs, int ns, std::vector<std::vector<DevOp>>& lists, int cap_max) {
+  hipStream_t st = aqc::mps_stream();
+  std::vector<TwoSiteJob> two;
+  std::vector<OneSiteJob> one;
+  std::vector<int> codes;
+  std::vector<std::pair<int, int>> rng(ns);
+  for (int s = 0; s < ns; ++s) {
+    const int start = (int)codes.size();
+    for (const DevOp& op : lists[s]) {
+      if (op.kind == 2) {
+        two.push_back(make_two(hs[s], op, 0));
+        two.back().qr = 1;
+        codes.push_back((int)two.size() - 1);
+      } else {
+        one.push_back(make_one(hs[s], op));
+        codes.push_back(-(int)one.size());
+      }
+    }
+    rng[s] = {start, (int)codes.size() - start};
+  }
+  if (codes.empty()) return AQC_OK;
+  std::vector<int> order(ns);
+  for (int s = 0; s < ns; ++s) order[s] = s;
+  std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return rng[a].second > rng[b].second; });
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  const size_t o_two = 0, o_one = al(o_two + two.size() * sizeof(TwoSiteJob));
+  const size_t o_codes = al(o_one + one.size() * sizeof(OneSiteJob));
+  const size_t o_chain = al(o_codes + codes.size() * sizeof(int));
+  const size_t total = o_chain + (size_t)ns * sizeof(ChainJob);
+  Staging& sg = staging();
+  AQC_HIP_CHECK(hipStreamSynchronize(st));  // staging buffers may still feed earlier launches
+  int rc = ensure_staging(sg, total);
+  if (rc != AQC_OK) return rc;
+  char* hb = (char*)sg.host;
+  char* db = (char*)sg.dev;
+  if (!two.empty()) std::memcpy(hb + o_two, two.data(), two.size() * sizeof(TwoSiteJob));
+  if (!one.empty()) std::memcpy(hb + o_one, one.data(), one.size() * sizeof(OneSiteJob));
+  std::memcpy(hb + o_codes, codes.data(), codes.size() * sizeof(int));
+  ChainJob* hc = (ChainJob*)(hb + o_chain);
+  for (int k = 0; k < ns; ++k) {
+    const int s = order[k];
+    hc[k].ops = (const int*)(db + o_codes) + rng[s].first;
+    hc[k].nops = rng[s].second;
+    hc[k].pad = 0;
+  }
+  AQC_HIP_CHECK(hipMemcpyAsync(sg.dev, sg.host, total, hipMemcpyHostToDevice, st));
+  const double c = cap_max, nj = (double)two.size();
+  // algorithmic: the two sites' Gammas in and out; nominal SVD + theta + split flops
+  aqc::KernelTimer::begin(st, "mps_chain", nj * 8.0 * c * c * 16, nj * (84.0 * 8.0 + 64.0) * c * c * c);
+  hipLaunchKernelGGL(k_chain, dim3(ns), dim3(1024), kChainLds, st, (const ChainJob*)(db + o_chain),
+                     (const TwoSiteJob*)(db + o_two), (const OneSiteJob*)(db + o_one));
+  aqc::KernelTimer::end(st);
+  AQC_CHECK_LAUNCH();
+  return AQC_OK;
+}
+
 int run_waves(aqc_mps_t* hs, int ns, std::vector<std::vector<DevOp>>& lists) {
+  {
+    int cap_max = 0;
+    for (int s = 0; s < ns; ++s) cap_max = std::max(cap_max, hs[s]->d.cap);
+    if (g_fused_chain && g_jacobi_variant == 2 && ns >= kChainMinStates && 2 * cap_max > 64 && 2 * cap_max <= 128)
+      return run_chains(hs, ns, lists, cap_max);
+  }
   hipStream_t st = aqc::mps_stream();
   std::vector<std::vector<std::vector<const DevOp*>>> lv(ns);
   size_t maxlen = 0;
@@ -1751,6 +1983,7 @@ int aqc_svd_debug(const double* theta, int m, int n, int variant, int stop_after
   AQC_REQUIRE(theta && w_out && sig_out && sweeps, "aqc_svd_debug: null argument");
   AQC_REQUIRE(m >= 1 && n >= 1 && m % 2 == 0 && n % 2 == 0 && m <= 128 && n <= 128,
               "aqc_svd_debug: m, n must be even and <= 128");
+  AQC_REQUIRE(stop_after_qr >= 0 && stop_after_qr <= 2, "aqc_svd_debug: stop_after_qr must be 0, 1 or 2");
   AQC_REQUIRE(variant == 2 || variant == 3 || variant == 5,
               "aqc_svd_debug: variant must be 2, 3 or 5");
   hipStream_t st = aqc::mps_stream();
@@ -1777,7 +2010,7 @@ int aqc_svd_debug(const double* theta, int m, int n, int variant, int stop_after
   j.jtol = g_jacobi_tol_factor;
   j.jtiny = g_jacobi_tiny_t;
   j.qr = variant != 3 ? 1 : 0;
-  j.dbg = stop_after_qr ? 1 : 0;
+  j.dbg = stop_after_qr;  // 1: stop after the QR phase; 2: also QR phase clock ticks in sig[0..3]
   int hd[8] = {m / 2, 0, n / 2, 0, 0, 0, 0, 0};  // dims, then zeroed flags
   AQC_HIP_CHECK(hipMemcpyAsync(th, theta, (size_t)m * n * sizeof(cplx), hipMemcpyHostToDevice, st));
   AQC_HIP_CHECK(hipMemcpyAsync(dm, hd, sizeof(hd), hipMemcpyHostToDevice, st));
@@ -1820,6 +2053,22 @@ int aqc_mps_set_jacobi_tol(double factor) {
 int aqc_mps_set_jacobi_stop(double tiny_t) {
   AQC_REQUIRE(tiny_t < 1e-3, "aqc_mps_set_jacobi_stop: tiny_t must be < 1e-3 (<= 0 restores the default)");
   g_jacobi_tiny_t = tiny_t > 0 ? tiny_t : kDefaultTinyT;
+  return AQC_OK;
+}
+
+int aqc_mps_chain_ticks(double* out) {
+  AQC_REQUIRE(out, "aqc_mps_chain_ticks: null argument");
+  unsigned long long t[5] = {0, 0, 0, 0, 0};
+  AQC_HIP_CHECK(hipStreamSynchronize(aqc::mps_stream()));
+  AQC_HIP_CHECK(hipMemcpyFromSymbol(t, HIP_SYMBOL(g_chain_ticks), sizeof(t)));
+  const unsigned long long z[5] = {0, 0, 0, 0, 0};
+  AQC_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_chain_ticks), z, sizeof(z)));
+  for (int i = 0; i < 5; ++i) out[i] = (double)t[i];
+  return AQC_OK;
+}
+
+int aqc_mps_set_fused_chain(int on) {
+  g_fused_chain = on != 0;
   return AQC_OK;
 }
 
@@ -1993,7 +2242,7 @@ int aqc_mps_copy(aqc_mps_t dst, const aqc_mps_t src) {
   return AQC_OK;
 }
 
-int aqc_mps_apply_batch(aqc_mps_t* hs, int ns, const aqc_op_t* const* ops, const int* nops) {
+int apply_batch_impl(aqc_mps_t* hs, int ns, const aqc_op_t* const* ops, const int* nops, bool sort_after) {
   AQC_REQUIRE(hs && ops && nops && ns >= 0, "aqc_mps_apply_batch: null argument");
   std::vector<std::vector<DevOp>> lists(ns);
   for (int s = 0; s < ns; ++s) {
@@ -2001,10 +2250,18 @@ int aqc_mps_apply_batch(aqc_mps_t* hs, int ns, const aqc_op_t* const* ops, const
     int rc = validate_ops(hs[s], ops[s], nops[s]);
     if (rc != AQC_OK) return rc;
   }
-  for (int s = 0; s < ns; ++s) schedule(hs[s], ops[s], nops[s], false, lists[s]);
+  for (int s = 0; s < ns; ++s) schedule(hs[s], ops[s], nops[s], sort_after, lists[s]);
   int rc = run_waves(hs, ns, lists);
   if (rc != AQC_OK) return rc;
   return check_flags_batch(hs, ns);
+}
+
+int aqc_mps_apply_batch(aqc_mps_t* hs, int ns, const aqc_op_t* const* ops, const int* nops) {
+  return apply_batch_impl(hs, ns, ops, nops, false);
+}
+
+int aqc_mps_apply_sort_batch(aqc_mps_t* hs, int ns, const aqc_op_t* const* ops, const int* nops) {
+  return apply_batch_impl(hs, ns, ops, nops, true);
 }
 
 int aqc_mps_apply(aqc_mps_t h, const aqc_op_t* ops, int nops) {

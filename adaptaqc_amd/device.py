@@ -199,15 +199,18 @@ def _handles(states):
     return arr
 
 
-def apply_batch(states, ops_lists):
-    """Apply per-state op lists in lock-step launches."""
+def apply_batch(states, ops_lists, sort=False):
+    """Apply per-state op lists (one batched launch sequence, or one fused chain per state); with
+    sort=True every state also returns to sorted qubit order in the same schedule (an evaluation's
+    replay + save)."""
     if not states:
         return
     l = _lib.lib()
     arrs = [o if isinstance(o, np.ndarray) else _lib.ops_array(o) for o in ops_lists]
     ptrs = (ctypes.c_void_p * len(arrs))(*[a.ctypes.data if len(a) else 0 for a in arrs])
     counts = np.asarray([len(a) for a in arrs], dtype=np.int32)
-    _lib.check(l.aqc_mps_apply_batch(_handles(states), len(states), ptrs, _lib.ptr(counts)))
+    fn = l.aqc_mps_apply_sort_batch if sort else l.aqc_mps_apply_batch
+    _lib.check(fn(_handles(states), len(states), ptrs, _lib.ptr(counts)))
 
 
 EM_METHOD_CODES = {"concurrence": 0, "eof": 1, "negativity": 2, "log_negativity": 3}

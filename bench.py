@@ -213,7 +213,7 @@ def main():
         best = torch.argmax(full * torch.as_tensor(prio, device=full.device), dim=1)
         # (ii) overlap evals on own states
         copy_batch(work, reload_src)
-        apply_batch(work, layer_ops)
+        apply_batch(work, layer_ops, sort=True)  # replay + save (sorted), as mps_from_circuit
         ov = overlap_zero_batch(work)
         costs = 1.0 - np.abs(ov) ** 2
         return best, costs
@@ -250,12 +250,20 @@ def main():
     value = evals_per_step * args.steps / elapsed
 
     fams = {f: _lib.timing_query(f)
-            for f in ("mps_svd", "mps_theta", "mps_split", "grad_chain", "mps_overlap0", "mps_copy")}
+            for f in ("mps_chain", "mps_svd", "mps_theta", "mps_split", "grad_chain", "mps_overlap0", "mps_copy")}
     dom = max(fams, key=lambda f: fams[f]["ms"])
     fd = fams[dom]
     launches = max(fd["launches"], 1)
     avg_ms = fd["ms"] / launches
-    if dom == "mps_svd":
+    if dom == "mps_chain":
+        # fused per-state chain (k_chain): per two-site update the nominal SVD flops of the
+        # 128 x 128 theta (84 n^3) + theta (32 chi^3) + split GEMM (32 chi^3), from the launch's
+        # KernelTimer record; one launch serves every state of the step
+        roof = {"kernel": "k_chain (fused two-site updates: theta, Jacobi SVD, split)", "bound": "mfma",
+                "achieved": fd["flops"] / launches / (avg_ms * 1e-3) / 1e12, "peak": FP64_PEAK_TFLOPS,
+                "unit": "TFLOP/s", "updates_per_launch": fd["flops"] / launches / ((84.0 * 8 + 64.0) * CHI ** 3),
+                "svd_share_of_flops": 84.0 * 8 / (84.0 * 8 + 64.0)}
+    elif dom == "mps_svd":
         # jobs per launch: the 4B two-site updates of one lock-step wave (all 128 x 128 at chi = 64)
         jobs = fd["bytes"] / (2.0 * 4 * CHI * CHI * 16)
         achieved_flop = jobs / launches * svd_nominal_flops(2 * CHI, 2 * CHI)
@@ -269,11 +277,14 @@ def main():
     # HBM bytes per launch of the same kernel and launch mix from the committed PMC passes
     # (tools/pmc_bench.sh: rocprofv3 FETCH_SIZE x 2 + WRITE_SIZE, MI355X_MICROARCH.md corrections)
     tj = os.path.join(ROOT, "profiles", TRAFFIC_JSON)
-    if dom == "mps_svd" and os.path.exists(tj):
+    want = {"mps_chain": "k_chain", "mps_svd": "k_jacobi_reg"}.get(dom)
+    if want and os.path.exists(tj):
         with open(tj) as fh:
             tr = json.load(fh)
-        roof["traffic"] = tr["traffic_bytes_per_launch"]
-        roof["traffic_source"] = f"profiles/{TRAFFIC_JSON} ({tr['kernel']}, rocprofv3 PMC)"
+        if tr["kernel"] == want:
+            roof["traffic"] = tr["traffic_bytes_per_launch"]
+            roof["traffic_source"] = f"profiles/{TRAFFIC_JSON} ({tr['kernel']}, rocprofv3 PMC)"
+    if want:
         roof["algorithmic_bytes_per_launch"] = fd["bytes"] / launches
     roof["avg_launch_ms"] = avg_ms
     roof["launches"] = fd["launches"]

@@ -98,6 +98,10 @@ int aqc_mps_copy_batch(aqc_mps_t* dst, const aqc_mps_t* src, int nstates);
  * reduce_zeros truncation) -- the replay inside mps_from_circuit (aer_mps_backend.py:76-78). */
 int aqc_mps_apply(aqc_mps_t h, const aqc_op_t* ops, int nops);
 int aqc_mps_apply_batch(aqc_mps_t* hs, int nstates, const aqc_op_t* const* ops, const int* nops);
+/* As aqc_mps_apply_batch, then move every state back to sorted qubit order in the same schedule
+   -- one evaluation's replay + save of mps_from_circuit (aer_mps_backend.py:76-78), so that a
+   state's swaps back run in the same fused chain as its gates. */
+int aqc_mps_apply_sort_batch(aqc_mps_t* hs, int nstates, const aqc_op_t* const* ops, const int* nops);
 /* Diagnostics: largest Jacobi sweep count since the last call (then reset). */
 int aqc_mps_jacobi_stats(aqc_mps_t h, int* max_sweeps);
 /* Jacobi rotation threshold |a^H b| > factor * L * eps * |a||b| (default factor 1). */
@@ -111,6 +115,13 @@ int aqc_mps_set_jacobi_stop(double tiny_t);
    5 = as 2 with 8-lane column groups at 2*chi = 128 (512 threads),
    0 = 512 threads / 128 KiB LDS panel, 1 = 256 threads / 64 KiB panel (2 per CU). */
 int aqc_mps_set_jacobi_variant(int variant);
+/* Batched applies of >= 32 states at 2*chi = 128 (variant 2) run every state's whole op list in
+   one fused workgroup (theta, Jacobi, truncation, split per update: no grid-wide step between
+   updates); on = 0 selects the lock-step launches per update.  Default on. */
+int aqc_mps_set_fused_chain(int on);
+/* Diagnostics: shader-clock ticks spent by the fused chain's workgroups (thread 0) in theta,
+   Jacobi, rank, split and one-site ops since the last call (then reset); out[5]. */
+int aqc_mps_chain_ticks(double* out);
 /* ---- ISL entanglement sweep (adapt_compiler.py:955-976 -> entanglement_measures.py:39-98) ----
    Two-qubit reduced density matrices for npairs pairs (pairs[2p], pairs[2p+1]), out = npairs x
    4 x 4 complex (row-major), row index 2*bit(max) + bit(min) as qiskit's partial_trace orders
@@ -130,11 +141,13 @@ int aqc_sv_transition(aqc_sv_t bra, aqc_sv_t ket, int q, double* out);
    3 = log-negativity.  rdms / out in device memory when on_device. */
 int aqc_entanglement_measures(const double* rdms, int count, int method, double* out, int on_device);
 
-/* Diagnostics: one register-resident Jacobi launch (variant 2 = with pivoted QR, 3 = without) on
-   theta (m x n column-major complex, m, n even <= 128, as the two-site update builds it).
-   w_out receives min(m,n) columns of length (variant 2: min(m,n), 3: max(m,n)); sig_out their
+/* Diagnostics: one register-resident Jacobi launch (variant 2 / 5 = with pivoted QR, 3 = without)
+   on theta (m x n column-major complex, m, n even <= 128, as the two-site update builds it).
+   w_out receives min(m,n) columns of length (variant 2 / 5: min(m,n), 3: max(m,n)); sig_out their
    norms; perm_out (optional) the pivot order when stop_after_qr (then w_out holds X = R^H
-   unsorted).  For tests and tools only: allocates and frees device memory per call. */
+   unsorted).  stop_after_qr = 2 also writes the QR phase's shader-clock ticks to sig_out[0..3]
+   (downdate + pivot key, pivot barrier, reflector + barrier, update; 128 x 128 only).  For tests
+   and tools only: allocates and frees device memory per call. */
 int aqc_svd_debug(const double* theta, int m, int n, int variant, int stop_after_qr, double* w_out,
                   double* sig_out, int* perm_out, int* sweeps);
 /* move_all_qubits_to_sorted_ordering (done implicitly by every measurement below). */

@@ -279,3 +279,45 @@ def test_jacobi_stop_rule_vs_oracle(variant):
     finally:
         _lib.check(L.aqc_mps_set_jacobi_stop(ctypes.c_double(0.0)))
         _lib.check(L.aqc_mps_set_jacobi_variant(2))
+
+
+@pytest.mark.parametrize("sort", [False, True])
+def test_fused_chain_matches_lockstep_and_oracle(sort):
+    """Batched applies at 2 chi = 128 run each state's op list in one fused workgroup (k_chain);
+    the result equals the lock-step launches' (1e-12) and the oracle's (1e-9) on 40 states of a
+    16-qubit chi = 64 brickwork + long-range gates (swap routing, max_chi binding)."""
+    from adaptaqc_amd import _lib
+    from adaptaqc_amd.circuit import device_ops
+    from adaptaqc_amd.device import DeviceMPS, apply_batch, overlap_zero_batch
+
+    n, chi, ns = 16, 64, 40
+    rng = np.random.default_rng(41)
+    circuits = []
+    for s in range(ns):
+        ops = []
+        for layer in range(6 + s % 5):
+            for q in range(n):
+                ops.append(("ry", (q,), (rng.uniform(-np.pi, np.pi),)))
+            for q in range(layer % 2, n - 1, 2):
+                ops.append(("cx", (q, q + 1), ()))
+        a = int(rng.integers(0, n - 1))
+        ops.append(("cx", (a, int(rng.integers(a + 1, n))), ()))
+        circuits.append(ops)
+    lists = [device_ops(to_circuit(n, ops)) for ops in circuits]
+    L = _lib.lib()
+    res = {}
+    try:
+        for fused in (1, 0):
+            _lib.check(L.aqc_mps_set_fused_chain(fused))
+            st = [DeviceMPS(n, chi, 1e-16, chi) for _ in range(ns)]
+            apply_batch(st, lists, sort=sort)
+            res[fused] = (overlap_zero_batch(st), [d.dims() for d in st])
+    finally:
+        _lib.check(L.aqc_mps_set_fused_chain(1))
+    np.testing.assert_allclose(res[1][0], res[0][0], rtol=1e-12, atol=1e-16)
+    for a, b in zip(res[1][1], res[0][1]):
+        np.testing.assert_array_equal(a, b)
+    for s in (0, 7, 39):
+        ref = M.run_circuit(n, circuits[s], 1e-16, chi)
+        ov_ref = M.mps_dot(ref.preprocessed(), M.zero_mps(n))
+        assert abs(res[1][0][s] - ov_ref) <= 1e-9 * abs(ov_ref) + 1e-18

@@ -15,5 +15,5 @@ pass sq2 SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAIT_INST_LDS SQ_INSTS_VALU
 pass fetch FETCH_SIZE
 pass write WRITE_SIZE
 python3 tools/pmc_summary.py gpurun_out/pmc_sq1 gpurun_out/pmc_sq2 gpurun_out/pmc_fetch gpurun_out/pmc_write > gpurun_out/pmc_summary.txt
-python3 tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write k_jacobi_reg > gpurun_out/traffic.json
+python3 tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write ${PMC_KERNEL:-k_chain} > gpurun_out/traffic.json
 rm -rf gpurun_out/pmc_sq1 gpurun_out/pmc_sq2 gpurun_out/pmc_fetch gpurun_out/pmc_write

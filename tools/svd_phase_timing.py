@@ -62,8 +62,33 @@ def report(db, reps, variants):
               f"(sweeps phase {np.mean(full) / 1e3 - np.mean(qr) / 1e3:.1f} us)")
 
 
+def ticks(variants):
+    """QR-step phase split from the kernel's shader-clock ticks (aqc_svd_debug mode 2)."""
+    from adaptaqc_amd import _lib
+
+    T = swap_theta()
+    m, n = T.shape
+    th = np.asfortranarray(T.astype(np.complex128)).ravel(order="F").view(np.float64).copy()
+    w = np.zeros(2 * m * n)
+    sig = np.zeros(max(m, n))
+    perm = np.zeros(max(m, n), dtype=np.int32)
+    sw = ctypes.c_int()
+    L = _lib.lib()
+    names = ("downdate + pivot key", "pivot barrier", "reflector + barrier", "update")
+    for v in variants:
+        for _ in range(3):
+            _lib.check(L.aqc_svd_debug(_lib.ptr(th), m, n, v, 2, _lib.ptr(w), _lib.ptr(sig), _lib.ptr(perm),
+                                       ctypes.byref(sw)))
+        steps = min(m, n)
+        tot = sig[:4].sum()
+        print(f"variant {v}: {tot / steps:.0f} ticks per QR step: " +
+              ", ".join(f"{nm} {sig[i] / steps:.0f}" for i, nm in enumerate(names)), flush=True)
+
+
 if __name__ == "__main__":
-    if sys.argv[1:2] == ["--report"]:
+    if sys.argv[1:2] == ["--ticks"]:
+        ticks([int(v) for v in sys.argv[2:]] or [2])
+    elif sys.argv[1:2] == ["--report"]:
         report(sys.argv[2], int(sys.argv[3]) if len(sys.argv) > 3 else 5, [int(v) for v in sys.argv[4:]] or [2])
     else:
         run(int(sys.argv[1]) if len(sys.argv) > 1 else 5, [int(v) for v in sys.argv[2:]] or [2])
