@@ -1112,18 +1112,21 @@ __global__ __launch_bounds__(1024) void k_chain(const ChainJob* __restrict__ cha
                                                 const OneSiteJob* __restrict__ one) {
   const ChainJob& c = chains[blockIdx.x];
   const int tid = threadIdx.x;
-  // shader-clock ticks of the phases (thread 0 of each workgroup; aqc_mps_chain_ticks)
-  unsigned long long tk[5] = {0, 0, 0, 0, 0}, t0 = 0;
+  // shader-clock ticks of the phases (thread 0 of each workgroup; aqc_mps_chain_ticks), kept in
+  // LDS so that no VGPR stays live across the phases
+  __shared__ unsigned long long tk[6];  // 5 phase totals, last tick
+  if (tid == 0) tk[0] = tk[1] = tk[2] = tk[3] = tk[4] = tk[5] = 0;
   auto tick = [&](int ph) {
     if (tid == 0) {
       const unsigned long long t = __builtin_amdgcn_s_memtime();
-      if (ph >= 0) tk[ph] += t - t0;
-      t0 = t;
+      if (ph >= 0) tk[ph] += t - tk[5];
+      tk[5] = t;
     }
   };
   tick(-1);
   for (int o = 0; o < c.nops; ++o) {
-    const int code = c.ops[o];
+    // wave-uniform (SGPR) op code, so the job's fields are scalar loads and hold no VGPRs
+    const int code = __builtin_amdgcn_readfirstlane(c.ops[o]);
     if (code < 0) {
       one_site_body(one[-code - 1], tid, 1024);
       __syncthreads();
