@@ -986,6 +986,9 @@ __device__ __forceinline__ bool split_block_active(const TwoSiteJob& j, int blk)
   return (blk / bcols) * 64 < rows && (blk % bcols) * 64 < cols;
 }
 
+// PF: register prefetch of the next k tile (the standalone kernel; the 1024-thread chain, at 128
+// VGPRs per lane, runs without it)
+template <bool PF = true>
 __device__ __forceinline__ void split_gemm_body(const TwoSiteJob& j, int blk, aqc::GemmLds& lds, int ltid) {
   const int chl = j.dims[0], k = j.dims[1], chr = j.dims[2];
   const int M = 2 * chl, N = 2 * chr;
@@ -1003,7 +1006,7 @@ __device__ __forceinline__ void split_gemm_body(const TwoSiteJob& j, int blk, aq
   const int* perm = j.perm;
   const cplx* th = j.theta;
   if (!tr) {
-    aqc::block_cgemm<true, true, true>(
+    aqc::block_cgemm<true, true, PF>(
         mb, nb, L, [&](int kk, int R) { return aqc::cconj(W[(size_t)perm[r0 + kk] * L + R]); },
         [&](int R, int c) { return th[(size_t)(c0 + c) * M + R]; },
         [&](int kk, int c, cplx v) {
@@ -1013,7 +1016,7 @@ __device__ __forceinline__ void split_gemm_body(const TwoSiteJob& j, int blk, aq
         },
         lds, ltid, active);
   } else {
-    aqc::block_cgemm<false, true, true>(
+    aqc::block_cgemm<false, true, PF>(
         mb, nb, L, [&](int R, int c) { return th[(size_t)c * M + r0 + R]; },
         [&](int c, int kk) { return W[(size_t)perm[c0 + kk] * L + c]; },
         [&](int R, int kk, cplx v) {
@@ -1095,9 +1098,67 @@ __device__ unsigned long long g_chain_ticks[5];
 
 // The phases are separate (non-inlined) functions: inlined into one loop body the compiler kept
 // values live across them and spilled hundreds of bytes per lane inside the Jacobi rounds.
+// theta in the chain: k_theta's register-light VALU tiles (16 x 16 outputs with all four P's and
+// the gate mix in registers: no second pass over theta), sub-group sg of 256 threads taking tiles
+// sg, sg + 4, ...; every sub-group runs the same number of tiles and k steps so that the barriers
+// pair up.  (The MFMA form, theta_chain, needs more than the chain's 128 VGPRs per lane and
+// spilled inside its k loop: 118 us per update.)
 __device__ __noinline__ void chain_theta(const TwoSiteJob& j) {
   extern __shared__ double2 xbuf[];
-  theta_chain(j, reinterpret_cast<aqc::GemmLds*>(xbuf));
+  const int tid = threadIdx.x, sg = tid >> 8, lt = tid & 255;
+  cplx (*As)[16][17] = reinterpret_cast<cplx (*)[16][17]>(xbuf + sg * (4 * 16 * 17));
+  cplx (*Bs)[16][17] = As + 2;
+  const int chl = j.dims[0], chm = j.dims[1], chr = j.dims[2];
+  const int cap = j.cap;
+  const int tiles_r = (cap + 15) / 16, ntiles = tiles_r * tiles_r;
+  const int ty = lt / 16, tx = lt % 16;
+  const size_t half = (size_t)cap * cap;
+  const int M = 2 * chl;
+  for (int t0 = 0; t0 < ntiles; t0 += 4) {
+    const int t = t0 + sg;
+    const int l0 = (t / tiles_r) * 16, r0 = (t % tiles_r) * 16;
+    const bool active = t < ntiles && l0 < chl && r0 < chr;
+    const int l = l0 + ty, r = r0 + tx;
+    cplx acc[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[i] = aqc::cmk(0, 0);
+    const double lll = active && l < chl ? j.ll[l] : 0.0;
+    const double lrr = active && r < chr ? j.lr[r] : 0.0;
+    for (int m0 = 0; m0 < chm; m0 += 16) {
+      const int ma = m0 + tx, mb = m0 + ty;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        cplx a = aqc::cmk(0, 0), b = aqc::cmk(0, 0);
+        if (active && l < chl && ma < chm) a = aqc::cscale(j.gp[s * half + (size_t)l * cap + ma], lll * j.lm[ma]);
+        if (active && mb < chm && r < chr) b = aqc::cscale(j.gq[s * half + (size_t)mb * cap + r], lrr);
+        As[s][ty][tx] = a;
+        Bs[s][ty][tx] = b;
+      }
+      __syncthreads();
+      if (active) {
+#pragma unroll 4
+        for (int mm = 0; mm < 16; ++mm) {
+          const cplx a0 = As[0][ty][mm], a1 = As[1][ty][mm];
+          const cplx b0 = Bs[0][mm][tx], b1 = Bs[1][mm][tx];
+          acc[0] = aqc::cfma(a0, b0, acc[0]);
+          acc[1] = aqc::cfma(a0, b1, acc[1]);
+          acc[2] = aqc::cfma(a1, b0, acc[2]);
+          acc[3] = aqc::cfma(a1, b1, acc[3]);
+        }
+      }
+      __syncthreads();
+    }
+    if (active && l < chl && r < chr) {
+#pragma unroll
+      for (int o = 0; o < 4; ++o) {
+        cplx v = aqc::cmul(j.G[o * 4 + 0], acc[0]);
+        v = aqc::cfma(j.G[o * 4 + 1], acc[1], v);
+        v = aqc::cfma(j.G[o * 4 + 2], acc[2], v);
+        v = aqc::cfma(j.G[o * 4 + 3], acc[3], v);
+        j.theta[(size_t)((o & 1) * chr + r) * M + (o >> 1) * chl + l] = v;
+      }
+    }
+  }
 }
 __device__ __noinline__ void chain_jacobi(const TwoSiteJob& j) { jacobi_reg_body<128, 8, 16>(j); }
 __device__ __noinline__ void chain_rank(const TwoSiteJob& j) { rank_body<1024>(j); }
@@ -1105,7 +1166,7 @@ __device__ __noinline__ void chain_split(const TwoSiteJob& j) {
   extern __shared__ double2 xbuf[];
   const int tid = threadIdx.x;
   split_copy_body(j, tid, 1024);
-  split_gemm_body(j, tid >> 8, reinterpret_cast<aqc::GemmLds*>(xbuf)[tid >> 8], tid & 255);
+  split_gemm_body<false>(j, tid >> 8, reinterpret_cast<aqc::GemmLds*>(xbuf)[tid >> 8], tid & 255);
 }
 
 __global__ __launch_bounds__(1024) void k_chain(const ChainJob* __restrict__ chains, const TwoSiteJob* __restrict__ two,
