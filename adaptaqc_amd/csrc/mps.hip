@@ -1041,38 +1041,6 @@ __global__ __launch_bounds__(aqc::kGemmThreads) void k_split_gemm(const TwoSiteJ
 // in place), the register Jacobi, the rank / truncation and the split -- with no grid-wide step
 // between updates.  The lock-step batch (run_waves) pays, per update, the slowest decomposition
 // of the whole launch and five launches; here a state's time is the sum of its own updates.
-// theta of job j: sub-group sg computes P_{s1' s2'} (s1' = sg >> 1, s2' = sg & 1) into theta at
-// the position of output (s1', s2'); then every (l, r) mixes its four values through G in place
-// (k_theta's contract).
-__device__ __forceinline__ void theta_chain(const TwoSiteJob& j, aqc::GemmLds* lds) {
-  const int tid = threadIdx.x, sg = tid >> 8, lt = tid & 255;
-  const int chl = j.dims[0], chm = j.dims[1], chr = j.dims[2];
-  const int cap = j.cap, M = 2 * chl;
-  const size_t half = (size_t)cap * cap;
-  const int s1 = sg >> 1, s2 = sg & 1;
-  const cplx* gp = j.gp + s1 * half;
-  const cplx* gq = j.gq + s2 * half;
-  aqc::block_cgemm<true, false>(
-      chl, chr, chm, [&](int l, int m) { return aqc::cscale(gp[(size_t)l * cap + m], j.ll[l] * j.lm[m]); },
-      [&](int m, int r) { return aqc::cscale(gq[(size_t)m * cap + r], j.lr[r]); },
-      [&](int l, int r, cplx v) { j.theta[(size_t)(s2 * chr + r) * M + s1 * chl + l] = v; }, lds[sg], lt);
-  __syncthreads();
-  for (int e = tid; e < chl * chr; e += 1024) {
-    const int l = e / chr, r = e % chr;
-    cplx p[4];
-#pragma unroll
-    for (int in = 0; in < 4; ++in) p[in] = j.theta[(size_t)((in & 1) * chr + r) * M + (in >> 1) * chl + l];
-#pragma unroll
-    for (int o = 0; o < 4; ++o) {
-      cplx v = aqc::cmul(j.G[o * 4 + 0], p[0]);
-      v = aqc::cfma(j.G[o * 4 + 1], p[1], v);
-      v = aqc::cfma(j.G[o * 4 + 2], p[2], v);
-      v = aqc::cfma(j.G[o * 4 + 3], p[3], v);
-      j.theta[(size_t)((o & 1) * chr + r) * M + (o >> 1) * chl + l] = v;
-    }
-  }
-}
-
 __device__ __forceinline__ void one_site_body(const OneSiteJob& j, int start, int stride) {
   const int cl = j.dims[0], cr = j.dims[1];
   const int cap = j.cap;
