@@ -1069,7 +1069,7 @@ __device__ unsigned long long g_chain_ticks[5];
 // theta in the chain: k_theta's register-light VALU tiles (16 x 16 outputs with all four P's and
 // the gate mix in registers: no second pass over theta), sub-group sg of 256 threads taking tiles
 // sg, sg + 4, ...; every sub-group runs the same number of tiles and k steps so that the barriers
-// pair up.  (The MFMA form, theta_chain, needs more than the chain's 128 VGPRs per lane and
+// pair up.  (An MFMA form on aqc::block_cgemm needs more than the chain's 128 VGPRs per lane and
 // spilled inside its k loop: 118 us per update.)
 __device__ __noinline__ void chain_theta(const TwoSiteJob& j) {
   extern __shared__ double2 xbuf[];
