@@ -16,7 +16,7 @@
 //     cross-XCD coherence assumptions).
 // Rotation rule, thresholds and stop test are those of k_jacobi_reg (mps.hip): relative
 // threshold L eps, squared-norm floor ||W||^2 1e-24, a sweep without rotations above 4x the
-// threshold -- or with only |t| < 1e-8 ones -- is the last.  Output: W's columns = U sigma,
+// threshold -- or with only |t| <= j.jtiny ones (default 1e-6) -- is the last.  Output: W's columns = U sigma,
 // sig = their norms (the k_jacobi contract consumed by k_rank / k_split_*, qr = 0).
 #include "mps_internal.h"
 
@@ -25,7 +25,6 @@ namespace {
 
 constexpr int kB = 16;        // columns per block
 constexpr int kMaxSweepsBJ = 40;
-constexpr double kTinyT = 1e-8;
 // Cross visits run the 16-round shift this many times (2 passes: 17 -> 16 sweeps but 21% slower
 // per gate at config 5: the visits are compute-, not W-traffic-bound).
 constexpr int kCrossPasses = 1;
@@ -33,7 +32,7 @@ constexpr int kCrossPasses = 1;
 struct BJState {
   double fro;   // ||W||_F^2
   int rot;      // rotations above noise in this sweep
-  int big;      // rotations with |t| >= kTinyT in this sweep
+  int big;      // rotations with |t| > jtiny in this sweep
   int done;     // converged (later launches return at once)
   int sweeps;   // sweeps run
   int pad[2];
@@ -131,7 +130,8 @@ __global__ __launch_bounds__(1024) void k_bj_init(const TwoSiteJob* __restrict__
 template <int MAXR>
 __device__ __forceinline__ bool rotate_pair(double (&sr)[MAXR], double (&si)[MAXR], double (&mr)[MAXR],
                                             double (&mi)[MAXR], double& na, double& da, double& ida, double& nb,
-                                            double& db, double& idb, double tol2, double floor2, int& rot, int& big,
+                                            double& db, double& idb, double tol2, double floor2, double tiny2,
+                                            int& rot, int& big,
                                             double2* bcol = nullptr) {
   double gx = 0, gy = 0;
 #pragma unroll
@@ -149,7 +149,7 @@ __device__ __forceinline__ bool rotate_pair(double (&sr)[MAXR], double (&si)[MAX
   jacobi_te(na, nb, g2, te, c, p);
   if (g2 > 16.0 * tol2 * ab) {
     rot = 1;
-    if (p - 1.0 > kTinyT * kTinyT) big = 1;
+    if (p - 1.0 > tiny2) big = 1;
   }
   const double ra = db * ida, ira = da * idb;
   const double mux = te * gx * ra, muy = -te * gy * ra;
@@ -248,7 +248,7 @@ __global__ __launch_bounds__(512) void k_bj_intra(const TwoSiteJob* __restrict__
       sr[i] = x.x, si[i] = x.y, mr[i] = y.x, mi[i] = y.y;
     }
     double na = cn[a], da = cd[a], ida = cid[a], nb = cn[b], db = cd[b], idb = cid[b];
-    if (rotate_pair<MAXR>(sr, si, mr, mi, na, da, ida, nb, db, idb, tol2, floor2, rot, big)) {
+    if (rotate_pair<MAXR>(sr, si, mr, mi, na, da, ida, nb, db, idb, tol2, floor2, j.jtiny * j.jtiny, rot, big)) {
 #pragma unroll
       for (int i = 0; i < MAXR; ++i) {
         cols[a * ldl + lane + 64 * i] = make_double2(sr[i], si[i]);
@@ -328,7 +328,7 @@ __global__ __launch_bounds__(1024) void k_bj_cross(const TwoSiteJob* __restrict_
       mr[i] = v.x, mi[i] = v.y;
     }
     double nb = cn[slot], db = cd[slot], idb = cid[slot];
-    if (rotate_pair<MAXR>(sr, si, mr, mi, na, da, ida, nb, db, idb, tol2, floor2, rot, big, col)) {
+    if (rotate_pair<MAXR>(sr, si, mr, mi, na, da, ida, nb, db, idb, tol2, floor2, j.jtiny * j.jtiny, rot, big, col)) {
       __builtin_amdgcn_wave_barrier();
       if (lane == 0) cn[slot] = nb, cd[slot] = db, cid[slot] = idb;
     }
