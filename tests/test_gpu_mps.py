@@ -302,6 +302,8 @@ def test_fused_chain_matches_lockstep_and_oracle(sort):
                 ops.append(("cx", (q, q + 1), ()))
         a = int(rng.integers(0, n - 1))
         ops.append(("cx", (a, int(rng.integers(a + 1, n))), ()))
+        for q in range(0, n, 3):  # trailing 1-qubit gates: standalone one-site ops in the chain
+            ops.append(("rx", (q,), (rng.uniform(-np.pi, np.pi),)))
         circuits.append(ops)
     lists = [device_ops(to_circuit(n, ops)) for ops in circuits]
     L = _lib.lib()
