@@ -67,57 +67,84 @@ __global__ __launch_bounds__(kT) void k_sweep_M(const SweepJob* __restrict__ job
   }
 }
 
-// blockIdx.x: job, blockIdx.y: 0 left / 1 right
+// blockIdx.x: job, blockIdx.y: 0 left / 1 right.  A chain of n dependent vector-matrix products:
+// the contraction index is split over the workgroup's four waves (wave q takes indices q, q + 4,
+// ...) with the running vector in LDS and the four partial sums added through LDS, so a step is a
+// quarter-length dependent FMA chain with its loads in flight instead of a full-length one on a
+// quarter of the threads.
 __global__ __launch_bounds__(kT) void k_sweep_lr(const SweepJob* __restrict__ jobs) {
   const SweepJob& j = jobs[blockIdx.x];
   const int cap = j.cap, n = j.n;
-  const int tid = threadIdx.x;
-  if (blockIdx.y == 0) {
-    if (tid == 0) j.lv[0] = aqc::cmk(1, 0);
-    __syncthreads();
-    for (int i = 0; i < n; ++i) {
-      const int cl = j.dims[i], cr = j.dims[i + 1];
-      const cplx* Mi = j.M + (size_t)i * cap * cap;
-      for (int r = tid; r < cr; r += kT) {
-        cplx acc = aqc::cmk(0, 0);
-        for (int l = 0; l < cl; ++l) acc = aqc::cfma(j.lv[(size_t)i * cap + l], Mi[(size_t)l * cap + r], acc);
-        j.lv[(size_t)(i + 1) * cap + r] = acc;
+  const int tid = threadIdx.x, q = tid >> 6, t = tid & 63;
+  constexpr int kMaxCap = 256;
+  __shared__ cplx vec[kMaxCap];
+  __shared__ cplx part[4][kMaxCap];
+  const bool left = blockIdx.y == 0;
+  cplx* out = left ? j.lv : j.rv;
+  if (tid == 0) {
+    vec[0] = aqc::cmk(1, 0);
+    out[(size_t)(left ? 0 : n) * cap] = aqc::cmk(1, 0);
+  }
+  __syncthreads();
+  for (int step = 0; step < n; ++step) {
+    const int i = left ? step : n - 1 - step;
+    const int cl = j.dims[i], cr = j.dims[i + 1];
+    const cplx* Mi = j.M + (size_t)i * cap * cap;
+    const int nout = left ? cr : cl, nin = left ? cl : cr;
+    for (int o = t; o < nout; o += 64) {
+      cplx acc = aqc::cmk(0, 0);
+#pragma unroll 4
+      for (int k = q; k < nin; k += 4) {
+        // left: out[r] = sum_l vec[l] M[l][r];  right: out[l] = sum_r M[l][r] vec[r]
+        const cplx m = left ? Mi[(size_t)k * cap + o] : Mi[(size_t)o * cap + k];
+        acc = aqc::cfma(vec[k], m, acc);
       }
-      __syncthreads();
+      part[q][o] = acc;
     }
-  } else {
-    if (tid == 0) j.rv[(size_t)n * cap] = aqc::cmk(1, 0);
     __syncthreads();
-    for (int i = n - 1; i >= 0; --i) {
-      const int cl = j.dims[i], cr = j.dims[i + 1];
-      const cplx* Mi = j.M + (size_t)i * cap * cap;
-      for (int l = tid; l < cl; l += kT) {
-        cplx acc = aqc::cmk(0, 0);
-        for (int r = 0; r < cr; ++r) acc = aqc::cfma(Mi[(size_t)l * cap + r], j.rv[(size_t)(i + 1) * cap + r], acc);
-        j.rv[(size_t)i * cap + l] = acc;
-      }
-      __syncthreads();
+    for (int o = tid; o < nout; o += kT) {
+      const cplx v = aqc::cadd(aqc::cadd(part[0][o], part[1][o]), aqc::cadd(part[2][o], part[3][o]));
+      vec[o] = v;
+      out[(size_t)(left ? i + 1 : i) * cap + o] = v;
     }
+    __syncthreads();
   }
 }
 
 // blockIdx.x: site, blockIdx.y: job.  w_b[s][l] = sum_r A_b[s][l][r] rv[b+1][r];
-// v0_a[s][r] = sum_l lv[a][l] A_a[s][l][r].
-__global__ __launch_bounds__(kT) void k_sweep_w(const SweepJob* __restrict__ jobs) {
+// v0_a[s][r] = sum_l lv[a][l] A_a[s][l][r], the latter only at chain starts (start[a]: the first
+// qubits of this rank's pair shard).  Each output's contraction is split into two contiguous
+// halves over the two halves of the workgroup (all 256 threads busy, half-length chains), summed
+// through LDS.
+__global__ __launch_bounds__(kT) void k_sweep_w(const SweepJob* __restrict__ jobs, const int* __restrict__ start) {
   const SweepJob& j = jobs[blockIdx.y];
   const int i = blockIdx.x, cap = j.cap;
   const int cl = j.dims[i], cr = j.dims[i + 1];
-  for (int e = threadIdx.x; e < 2 * cl; e += kT) {
-    const int s = e / cl, l = e % cl;
-    cplx acc = aqc::cmk(0, 0);
-    for (int r = 0; r < cr; ++r) acc = aqc::cfma(site_a(j, i, s, l, r), j.rv[(size_t)(i + 1) * cap + r], acc);
-    j.w[((size_t)i * 2 + s) * cap + l] = acc;
+  const int tid = threadIdx.x, hh = tid >> 7, t = tid & 127;
+  __shared__ cplx part[2][512];
+  {
+    const int r0 = hh * ((cr + 1) / 2), r1 = hh ? cr : (cr + 1) / 2;
+    for (int e = t; e < 2 * cl; e += 128) {
+      const int s = e / cl, l = e % cl;
+      cplx acc = aqc::cmk(0, 0);
+      for (int r = r0; r < r1; ++r) acc = aqc::cfma(site_a(j, i, s, l, r), j.rv[(size_t)(i + 1) * cap + r], acc);
+      part[hh][e] = acc;
+    }
+    __syncthreads();
+    for (int e = tid; e < 2 * cl; e += kT) j.w[((size_t)i * 2 + e / cl) * cap + e % cl] = aqc::cadd(part[0][e], part[1][e]);
   }
-  for (int e = threadIdx.x; e < 2 * cr; e += kT) {
-    const int s = e / cr, r = e % cr;
-    cplx acc = aqc::cmk(0, 0);
-    for (int l = 0; l < cl; ++l) acc = aqc::cfma(j.lv[(size_t)i * cap + l], site_a(j, i, s, l, r), acc);
-    j.v0[((size_t)i * 2 + s) * cap + r] = acc;
+  if (!start[i]) return;  // uniform in the workgroup
+  __syncthreads();
+  {
+    const int l0 = hh * ((cl + 1) / 2), l1 = hh ? cl : (cl + 1) / 2;
+    for (int e = t; e < 2 * cr; e += 128) {
+      const int s = e / cr, r = e % cr;
+      cplx acc = aqc::cmk(0, 0);
+      for (int l = l0; l < l1; ++l) acc = aqc::cfma(j.lv[(size_t)i * cap + l], site_a(j, i, s, l, r), acc);
+      part[hh][e] = acc;
+    }
+    __syncthreads();
+    for (int e = tid; e < 2 * cr; e += kT) j.v0[((size_t)i * 2 + e / cr) * cap + e % cr] = aqc::cadd(part[0][e], part[1][e]);
   }
 }
 
@@ -296,6 +323,9 @@ int aqc_pair_grads_batch(aqc_mps_t* psis, int ns, const double* svec, const int*
   AQC_REQUIRE(ngen == 0 || (gens && degs), "aqc_pair_grads_batch: null generators");
   const int n = psis[0]->d.n;
   for (int s = 0; s < ns; ++s) AQC_REQUIRE(psis[s] && psis[s]->d.n == n, "aqc_pair_grads_batch: all states need n qubits");
+  for (int s = 0; s < ns; ++s)
+    AQC_REQUIRE(psis[s]->d.cap <= 256 && psis[s]->d.cap == psis[0]->d.cap,
+                "aqc_pair_grads_batch: states need one bond capacity <= 256");
   for (int p = 0; p < npairs; ++p) {
     const int a = pairs[2 * p], b = pairs[2 * p + 1];
     AQC_REQUIRE(a >= 0 && a < n && b >= 0 && b < n && a != b, "aqc_pair_grads_batch: bad pair");
@@ -317,7 +347,7 @@ int aqc_pair_grads_batch(aqc_mps_t* psis, int ns, const double* svec, const int*
     for (int a = 0; a < n - 1; ++a)
       if (need[a]) alist.push_back(a);
   }
-  const size_t cb = (alist.size() + 4) * sizeof(int) + 2 * npairs * sizeof(int) + 2 * n * sizeof(cplx) + 16 * sizeof(cplx) +
+  const size_t cb = (alist.size() + 4 + n) * sizeof(int) + 2 * npairs * sizeof(int) + 2 * n * sizeof(cplx) + 16 * sizeof(cplx) +
                     16 * (size_t)ngen * sizeof(cplx) + ngen * sizeof(double) + 256;
   const size_t ob = out_is_device ? 0 : (size_t)ns * npairs * sizeof(double);
   GradBuffers& gb = gbuf();
@@ -337,7 +367,8 @@ int aqc_pair_grads_batch(aqc_mps_t* psis, int ns, const double* svec, const int*
   cplx* dgens = du0 + 16;
   double* ddegs = (double*)(dgens + 16 * (size_t)ngen);
   int* dalist = (int*)(ddegs + ngen);
-  double* dout = out_is_device ? out : (double*)(((uintptr_t)(dalist + alist.size() + 4) + 255) & ~(uintptr_t)255);
+  int* dstart = dalist + alist.size() + 4;  // n flags: chain start (v0 needed) at this qubit
+  double* dout = out_is_device ? out : (double*)(((uintptr_t)(dstart + n) + 255) & ~(uintptr_t)255);
   std::vector<SweepJob> jobs(ns);
   for (int s = 0; s < ns; ++s) jobs[s] = make_job(psis[s], dout + (size_t)s * npairs);
   AQC_HIP_CHECK(hipMemcpy(djobs, jobs.data(), jb, hipMemcpyHostToDevice));
@@ -345,6 +376,11 @@ int aqc_pair_grads_batch(aqc_mps_t* psis, int ns, const double* svec, const int*
   AQC_HIP_CHECK(hipMemcpy(dsvec, svec, 2 * n * sizeof(cplx), hipMemcpyHostToDevice));
   AQC_HIP_CHECK(hipMemcpy(du0, u0, 16 * sizeof(cplx), hipMemcpyHostToDevice));
   if (!alist.empty()) AQC_HIP_CHECK(hipMemcpy(dalist, alist.data(), alist.size() * sizeof(int), hipMemcpyHostToDevice));
+  {
+    std::vector<int> startf(n, 0);
+    for (int a : alist) startf[a] = 1;
+    AQC_HIP_CHECK(hipMemcpy(dstart, startf.data(), n * sizeof(int), hipMemcpyHostToDevice));
+  }
   if (ngen) {
     AQC_HIP_CHECK(hipMemcpy(dgens, gens, 16 * (size_t)ngen * sizeof(cplx), hipMemcpyHostToDevice));
     AQC_HIP_CHECK(hipMemcpy(ddegs, degs, ngen * sizeof(double), hipMemcpyHostToDevice));
@@ -354,7 +390,7 @@ int aqc_pair_grads_batch(aqc_mps_t* psis, int ns, const double* svec, const int*
   AQC_CHECK_LAUNCH();
   hipLaunchKernelGGL(k_sweep_lr, dim3(ns, 2), dim3(kT), 0, st, djobs);
   AQC_CHECK_LAUNCH();
-  hipLaunchKernelGGL(k_sweep_w, dim3(n, ns), dim3(kT), 0, st, djobs);
+  hipLaunchKernelGGL(k_sweep_w, dim3(n, ns), dim3(kT), 0, st, djobs, (const int*)dstart);
   AQC_CHECK_LAUNCH();
   {
     // algorithmic work of the chain: sum_a (n-a-1) steps of a 2 x chi x chi complex vec-mat
