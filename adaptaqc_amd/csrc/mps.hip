@@ -1575,6 +1575,38 @@ Staging& staging() {
   return s[dev];
 }
 
+// Job staging for the gate-application launches: a ring of buffer sets per device, each with an
+// event recorded after the launches that read it, so that building the next batch's jobs waits
+// only for the set's previous use (four calls back) instead of draining the stream -- the host
+// schedules while the GPU still runs the previous work.
+struct StagingSet {
+  Staging buf;
+  hipEvent_t done = nullptr;
+  bool pending = false;
+};
+
+StagingSet& staging_acquire() {
+  constexpr int kRing = 4;
+  static StagingSet sets[64][kRing];
+  static int next[64] = {0};
+  int dev = 0;
+  hipGetDevice(&dev);
+  StagingSet& ss = sets[dev][next[dev]];
+  next[dev] = (next[dev] + 1) % kRing;
+  if (ss.pending) {
+    hipEventSynchronize(ss.done);
+    ss.pending = false;
+  }
+  return ss;
+}
+
+int staging_release(StagingSet& ss, hipStream_t st) {
+  if (!ss.done) AQC_HIP_CHECK(hipEventCreateWithFlags(&ss.done, hipEventDisableTiming));
+  AQC_HIP_CHECK(hipEventRecord(ss.done, st));
+  ss.pending = true;
+  return AQC_OK;
+}
+
 TwoSiteJob make_two(aqc_mps_t h, const DevOp& op, int slot = 0) {
   TwoSiteJob j;
   std::memset(&j, 0, sizeof(j));
@@ -1686,8 +1718,8 @@ int run_chains(aqc_mps_t* hs, int ns, std::vector<std::vector<DevOp>>& lists, in
   const size_t o_codes = al(o_one + one.size() * sizeof(OneSiteJob));
   const size_t o_chain = al(o_codes + codes.size() * sizeof(int));
   const size_t total = o_chain + (size_t)ns * sizeof(ChainJob);
-  Staging& sg = staging();
-  AQC_HIP_CHECK(hipStreamSynchronize(st));  // staging buffers may still feed earlier launches
+  StagingSet& ss = staging_acquire();
+  Staging& sg = ss.buf;
   int rc = ensure_staging(sg, total);
   if (rc != AQC_OK) return rc;
   char* hb = (char*)sg.host;
@@ -1710,7 +1742,7 @@ int run_chains(aqc_mps_t* hs, int ns, std::vector<std::vector<DevOp>>& lists, in
                      (const TwoSiteJob*)(db + o_two), (const OneSiteJob*)(db + o_one));
   aqc::KernelTimer::end(st);
   AQC_CHECK_LAUNCH();
-  return AQC_OK;
+  return staging_release(ss, st);
 }
 
 int run_waves(aqc_mps_t* hs, int ns, std::vector<std::vector<DevOp>>& lists) {
@@ -1762,8 +1794,8 @@ int run_waves(aqc_mps_t* hs, int ns, std::vector<std::vector<DevOp>>& lists) {
     one_rng[w] = {o0, one.size() - o0};
   }
   const size_t tb = two.size() * sizeof(TwoSiteJob), ob = one.size() * sizeof(OneSiteJob);
-  Staging& sg = staging();
-  AQC_HIP_CHECK(hipStreamSynchronize(st));  // staging buffers may still feed earlier launches
+  StagingSet& ss = staging_acquire();
+  Staging& sg = ss.buf;
   int rc = ensure_staging(sg, tb + ob + 256);
   if (rc != AQC_OK) return rc;
   std::memcpy(sg.host, two.data(), tb);
@@ -1827,7 +1859,7 @@ int run_waves(aqc_mps_t* hs, int ns, std::vector<std::vector<DevOp>>& lists) {
       AQC_CHECK_LAUNCH();
     }
   }
-  return AQC_OK;
+  return staging_release(ss, st);
 }
 
 int check_flags(aqc_mps_t h) {
