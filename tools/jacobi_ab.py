@@ -1,6 +1,6 @@
 """A/B of the two-site SVD kernel configurations on the bench's overlap workload (lab tool; MI355X).
 
-    python tools/jacobi_ab.py [states] [variant:tiny[:fused] ...]      e.g. 256 2:1e-8 5:1e-8 2:1e-6:0
+    python tools/jacobi_ab.py [states] [variant:tiny[:fused[:tol_factor]] ...]   e.g. 256 2:1e-6 2:1e-6:0 2:1e-6:1:32
 
 Per config: the bench's overlap evaluations (thinly-dressed layers at distances 1, 2, 5, 25 on
 `states` random 50-qubit chi = 64 states: Aer routing, SVD truncation at chi = 64, sort back) run
@@ -21,8 +21,12 @@ from adaptaqc_amd import _lib  # noqa: E402
 from adaptaqc_amd.device import DeviceMPS, apply_batch, copy_batch, overlap_zero_batch  # noqa: E402
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 256
-configs = [(int(c.split(":")[0]), float(c.split(":")[1]), int(c.split(":")[2]) if c.count(":") > 1 else 1)
-           for c in sys.argv[2:]] or [(2, 1e-6, 1), (2, 1e-6, 0)]
+def _cfg(c):
+    f = c.split(":")
+    return (int(f[0]), float(f[1]), int(f[2]) if len(f) > 2 else 1, float(f[3]) if len(f) > 3 else 1.0)
+
+
+configs = [_cfg(c) for c in sys.argv[2:]] or [(2, 1e-6, 1, 1.0), (2, 1e-6, 0, 1.0)]
 L = _lib.lib()
 distinct = [bench.random_vidal_mps(50, bench.CHI, 1000 + k) for k in range(8)]
 states = []
@@ -37,7 +41,8 @@ ops = [_lib.ops_array(bench.thin_layer_ops(bench.LAYER_A, bench.LAYER_A + d, rng
        for _ in range(B) for d in bench.DISTANCES]
 ref = None
 try:
-    for variant, tiny, fused in configs:
+    for variant, tiny, fused, tolf in configs:
+        _lib.check(L.aqc_mps_set_jacobi_tol(ctypes.c_double(tolf)))
         _lib.check(L.aqc_mps_set_jacobi_variant(variant))
         _lib.check(L.aqc_mps_set_jacobi_stop(ctypes.c_double(tiny)))
         _lib.check(L.aqc_mps_set_fused_chain(fused))
@@ -67,7 +72,7 @@ try:
                                                     zip(("theta", "jacobi", "rank", "split"), tks[:4])), flush=True)
         if ref is None:
             ref = ov
-        print(f"variant {variant} tiny {tiny:.0e} fused {fused}: apply {wall * 1e3:8.2f} ms wall "
+        print(f"variant {variant} tiny {tiny:.0e} fused {fused} tol x{tolf:g}: apply {wall * 1e3:8.2f} ms wall "
               f"({wall2 * 1e3:8.2f} with the overlaps), "
               f"{'chain' if fused and variant == 2 else 'svd'} {svd['ms']:8.2f} ms over {svd['launches']} launches "
               f"({svd['ms'] / max(svd['launches'], 1):.3f} ms/launch), max sweeps {msw}, "
@@ -76,3 +81,4 @@ finally:
     _lib.check(L.aqc_mps_set_jacobi_variant(2))
     _lib.check(L.aqc_mps_set_jacobi_stop(ctypes.c_double(0.0)))
     _lib.check(L.aqc_mps_set_fused_chain(1))
+    _lib.check(L.aqc_mps_set_jacobi_tol(ctypes.c_double(1.0)))
