@@ -1,7 +1,11 @@
 """Benchmark: overlap + gradient evaluations / s, 50-qubit MPS chi = 64 (BASELINE.json config 3).
 
-One step, per rank, on a global batch of S = world * states_per_rank synthetic random 50-qubit
-MPS (Vidal form, bonds min(2^k, 2^(50-k), 64)), all resident in HBM:
+One step, per rank, on a global batch of S = world * states_per_rank synthetic 50-qubit chi = 64
+MPS (Vidal form, every bond at min(2^k, 2^(50-k), 64)), all resident in HBM.  The states are
+random chi = 64 MPS with a product component near |0..0> (``near_product_mps``), so that the
+gradients and overlaps are far from zero and every output of the step can be checked against the
+oracle (on a plain random chi = 64 state every overlap with |0..0> is ~1e-8 and the gradients are
+rounding noise).
   (i)  candidate sweep: gradient norm of the identity_resolvable layer (rotoselect generators,
        12 distinct, |s> = |0..0>) for all 1225 pairs of the full coupling map, pairs sharded
        across ranks by first qubit (each rank covers its shard for all S states), one RCCL
@@ -11,10 +15,17 @@ MPS (Vidal form, bonds min(2^k, 2^(50-k), 64)), all resident in HBM:
        with max_chi = 64 truncation, sort back at save) and take 1 - |<0|psi>|^2.
 value = (S * 1225 + S * 4) evaluations / step time (max over ranks): weak scaling.
 
-Also reported: the dominant kernel's roofline (HIP events on the MPS stream around every launch
-of the timed region) and a CPU baseline: the oracle's port of the reference algorithm
-(per-pair, per-generator MPS build + whole-psi dot; numpy LAPACK SVDs) timed on a bounded
-sample on rank 0 at N = 1.
+Also reported (outside the timed region):
+  * each evaluation kind timed on its own (gradient / overlap evals per second) and the rate at
+    the reference's own per-layer mix (1225 gradients + 113 Rotoselect overlap evaluations);
+  * ``parity_check``: one state's 1225 gradients and arg-max pair and four overlap evaluations
+    (one per distance, through the fused chain) against the oracle;
+  * ``latency``: one state alone -- one overlap evaluation per distance, and one Rotoselect gate
+    (``replace_with_best_1q_gate``'s 7 evaluations) on the cached-prefix path;
+  * the dominant kernel's roofline (HIP events on the MPS stream around every launch);
+  * CPU baselines: the oracle's port of the reference algorithm (per-pair, per-generator MPS
+    build + whole-psi dot; numpy LAPACK SVDs), one process per host core with single-threaded
+    BLAS, on a bounded sample, run on rank 0 at N = 1 before the GPU is touched.
 """
 import argparse
 import json
@@ -22,7 +33,8 @@ import os
 import sys
 import time
 
-import numpy as np
+os.environ.setdefault("OPENBLAS_NUM_THREADS", "1")  # CPU baseline workers: one core each
+import numpy as np  # noqa: E402
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
@@ -31,9 +43,10 @@ N_QUBITS = 50
 CHI = 64
 DISTANCES = (1, 2, 5, 25)
 LAYER_A = 12
+REF_OVERLAPS_PER_LAYER = 113  # Rotoselect evaluations per 4-rotation layer
 FP64_PEAK_TFLOPS = 78.6  # MI355X dense FP64 (vector = matrix), MI355X_MICROARCH.md / SURVEY 8(d)
 HBM_PEAK_GBS = 8000.0
-TRAFFIC_JSON = "r1_traffic.json"
+TRAFFIC_JSON = "r2_traffic.json"
 
 
 def vidal_from_tensors(A):
@@ -76,13 +89,49 @@ def random_vidal_mps(n, chi, seed):
     return vidal_from_tensors(A)
 
 
-def thin_layer_ops(a, b, angles):
-    """Thinly-dressed CNOT layer with rotoselect-style angles: rx, rx, cx, rx, rx."""
+def near_product_mps(n, chi, seed, alpha=0.6):
+    """|psi> ~ alpha |p> + |phi> in Vidal form: |p> a product of single-qubit states near |0>
+    (angles 0.15-0.3, random phases), |phi> random with bonds min(2^k - 1, 2^(n-k) - 1, chi - 1),
+    so that every bond of psi sits at min(2^k, 2^(n-k), chi) while the overlaps with |0..0>-like
+    states (and so the gradients) are far from zero."""
+    rng = np.random.default_rng(seed)
+    dims = [1] + [min(2 ** k - 1, 2 ** (n - k) - 1, chi - 1) for k in range(1, n)] + [1]
+    A = [(rng.standard_normal((2, dims[i], dims[i + 1])) + 1j * rng.standard_normal((2, dims[i], dims[i + 1])))
+         for i in range(n)]
+    gam, lam = vidal_from_tensors(A)
+    phi = [np.stack(g) * (lam[i][None, None, :] if i < n - 1 else 1.0) for i, g in enumerate(gam)]
+    out = []
+    for i, t in enumerate(phi):  # block-diagonal sum with the near-|0> product chain
+        s, l, r = t.shape
+        li, ri = (1 if i == 0 else l + 1), (1 if i == n - 1 else r + 1)
+        x = np.zeros((2, li, ri), dtype=complex)
+        a, b = 0.15 * (1 + rng.random()), rng.uniform(-np.pi, np.pi)
+        x[:, 0, 0] = (alpha if i == 0 else 1.0) * np.array([np.cos(a), np.exp(1j * b) * np.sin(a)])
+        x[:, li - l:, ri - r:] = t
+        out.append(x)
+    return vidal_from_tensors(out)
+
+
+def bench_states(n, chi, count, kind="near-product"):
+    gen = near_product_mps if kind == "near-product" else random_vidal_mps
+    return [gen(n, chi, 1000 + k) for k in range(count)]
+
+
+THIN_AXES = ("rx", "rx", "rx", "rx")
+
+
+def thin_layer_ops(a, b, angles, axes=THIN_AXES):
+    """Thinly-dressed CNOT layer with rotoselect-style angles (and axes): r, r, cx, r, r."""
     from adaptaqc_amd import gates as G
 
-    rx = lambda t: G.one_qubit("rx", [t])
-    return [(rx(angles[0]), (a,)), (rx(angles[1]), (b,)), (G.TWO_QUBIT["cx"], (a, b)),
-            (rx(angles[2]), (a,)), (rx(angles[3]), (b,))]
+    r = [G.one_qubit(axes[k], [angles[k]]) for k in range(4)]
+    return [(r[0], (a,)), (r[1], (b,)), (G.TWO_QUBIT["cx"], (a, b)), (r[2], (a,)), (r[3], (b,))]
+
+
+def thin_layer_oracle_ops(a, b, angles, axes=THIN_AXES):
+    """The same layer as oracle ops (name, qubits, params)."""
+    return [(axes[0], (a,), (float(angles[0]),)), (axes[1], (b,), (float(angles[1]),)), ("cx", (a, b), ()),
+            (axes[2], (a,), (float(angles[2]),)), (axes[3], (b,), (float(angles[3]),))]
 
 
 def layer_inputs():
@@ -95,64 +144,105 @@ def layer_inputs():
     return layer, gens, deg, u0, np.stack(gm)
 
 
+def oracle_layer():
+    """identity_resolvable (ansatzes.py:201-211) as oracle ops, its generators (rotoselect,
+    inverse) and inverse."""
+    from adaptaqc_amd.utils import ansatzes
+    from oracle import gradients as ogr
+
+    o_layer = [(i.operation.name, tuple(i.qubits), tuple(i.operation.params))
+               for i in ansatzes.identity_resolvable().data]
+    og, od = ogr.get_generators_and_degeneracies(o_layer, True, True)
+    return o_layer, og, od, ogr.inverse_ops(o_layer)
+
+
 def svd_nominal_flops(m, n):
     """LAPACK-style complex SVD with both singular-vector sets: 4 x (4m^2n + 8mn^2 + 9n^3), m >= n."""
     m, n = max(m, n), min(m, n)
     return 4.0 * (4 * m * m * n + 8 * m * n * n + 9 * n ** 3)
 
 
-def cpu_baseline(seed_states, layer, u0, gm, deg, budget_s=20.0):
-    """Oracle port of the reference path on a bounded sample (rank 0, N = 1)."""
+# ---------------------------------------------------------------------------------------------
+# CPU baseline (oracle port of the reference structure), one process per core
+# ---------------------------------------------------------------------------------------------
+def _cpu_worker(args):
+    from threadpoolctl import threadpool_limits
+
+    with threadpool_limits(limits=1):  # one core per worker, whatever OMP/OPENBLAS_NUM_THREADS say
+        return _cpu_worker_body(*args)
+
+
+def _cpu_worker_body(kind, wid, budget_s, layer_seed):
     from oracle import adapt_host, gradients as ogr, mps as M
 
-    qmps = seed_states[0]
+    q = near_product_mps(N_QUBITS, CHI, layer_seed)
+    st = M.MPS.from_aer(q)
     n = N_QUBITS
-    st = M.MPS.from_aer(qmps)
-    psi = st.preprocessed()
-    o_layer = [(i.operation.name, i.qubits, tuple(i.operation.params)) for i in layer.data]
-    og, od = ogr.get_generators_and_degeneracies(o_layer, True, True)
-    inv0 = ogr.inverse_ops(o_layer)
-    cmap = adapt_host.coupling_map_full(n)
-    rng = np.random.default_rng(0)
-    # (ii) overlap evals: replay the layer on the cached MPS + <0|psi> (reference: Aer replay)
     t0 = time.perf_counter()
-    n_ov = 0
-    for d in DISTANCES:
-        ops = [("rx", (LAYER_A,), (0.3,)), ("rx", (LAYER_A + d,), (0.7,)), ("cx", (LAYER_A, LAYER_A + d), ()),
-               ("rx", (LAYER_A,), (-0.2,)), ("rx", (LAYER_A + d,), (1.1,))]
-        out = M.run_circuit(n, ops, 1e-16, CHI, mps=st)
-        _ = 1 - abs(M.mps_dot(out.preprocessed(), M.zero_mps(n))) ** 2
-        n_ov += 1
-    t_ov = (time.perf_counter() - t0) / n_ov
-    # (i) gradient evals: reference structure on a sample of pairs
-    t0 = time.perf_counter()
-    n_gr = 0
-    order = rng.permutation(len(cmap))
-    while time.perf_counter() - t0 < budget_s and n_gr < len(cmap):
-        pair = cmap[order[n_gr]]
-        ogr.general_grad_of_pairs_ref(psi, n, inv0, og, od, [pair], (), 1e-16, CHI)
-        n_gr += 1
-    t_gr = (time.perf_counter() - t0) / max(n_gr, 1)
-    per_state = len(DISTANCES) * t_ov + len(cmap) * t_gr
-    return {
-        "value": (len(DISTANCES) + len(cmap)) / per_state,
-        "unit": "evals/s",
-        "cores": int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)),
-        "kind": "port",
-        "sample": (f"1 state: {len(DISTANCES)} overlap evals ({t_ov * 1e3:.1f} ms each) + {n_gr} of 1225 pair "
-                   f"gradients ({t_gr * 1e3:.1f} ms each, 12 generators) extrapolated to the step mix"),
-    }
+    count = 0
+    per_d = {}
+    if kind == "overlap":
+        rng = np.random.default_rng(100 + wid)
+        k = wid
+        while True:  # one evaluation per distance, round-robin from this worker's offset
+            d = DISTANCES[k % len(DISTANCES)]
+            ops = thin_layer_oracle_ops(LAYER_A, LAYER_A + d, rng.uniform(-np.pi, np.pi, 4))
+            t1 = time.perf_counter()
+            out = M.run_circuit(n, ops, 1e-16, CHI, mps=st)  # replay on the cached MPS + save
+            _ = 1 - abs(M.mps_dot(out.preprocessed(), M.zero_mps(n))) ** 2
+            per_d.setdefault(d, []).append(time.perf_counter() - t1)
+            count += 1
+            k += 1
+            if time.perf_counter() - t0 > budget_s and count >= len(DISTANCES):
+                break
+    else:
+        psi = st.preprocessed()
+        _, og, od, inv0 = oracle_layer()
+        cmap = adapt_host.coupling_map_full(n)
+        order = np.random.default_rng(wid).permutation(len(cmap))
+        while time.perf_counter() - t0 < budget_s or count == 0:
+            pair = cmap[order[count % len(cmap)]]
+            ogr.general_grad_of_pairs_ref(psi, n, inv0, og, od, [pair], (), 1e-16, CHI)
+            count += 1
+    return count, time.perf_counter() - t0, per_d
 
 
+def cpu_baselines(budget_s, workers):
+    """Gradient and overlap evaluations / s of the oracle port on `workers` processes (fork, before
+    any GPU call), BLAS single-threaded in each.  Returns per-kind rates and the step-mix rate."""
+    import multiprocessing as mp
+
+    ctx = mp.get_context("fork")
+    out = {}
+    with ctx.Pool(workers) as pool:
+        for kind in ("gradient", "overlap"):
+            res = pool.map(_cpu_worker, [(kind, w, budget_s, 1000) for w in range(workers)])
+            count = sum(c for c, _, _ in res)
+            wall = max(t for _, t, _ in res)
+            out[kind] = {"evals": count, "wall_s": wall, "evals_per_s": count / wall}
+            if kind == "overlap":  # one evaluation on one core, per distance (latency comparison)
+                per_d = {}
+                for _, _, pd in res:
+                    for d, ts in pd.items():
+                        per_d.setdefault(d, []).extend(ts)
+                out[kind]["eval_ms_by_distance"] = {str(d): 1e3 * float(np.median(ts)) for d, ts in sorted(per_d.items())}
+    return out
+
+
+# ---------------------------------------------------------------------------------------------
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--states", type=int, default=256, help="states per rank")
-    ap.add_argument("--distinct", type=int, default=8, help="distinct random states generated")
+    ap.add_argument("--distinct", type=int, default=8, help="distinct synthetic states generated")
+    ap.add_argument("--state-kind", default="near-product", choices=("near-product", "random"))
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-budget", type=float, default=20.0)
+    ap.add_argument("--cpu-budget", type=float, default=4.0, help="seconds per CPU-baseline leg")
+    ap.add_argument("--cpu-workers", type=int, default=0, help="0: min(16, OMP_NUM_THREADS or cores)")
+    ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--no-latency", action="store_true")
     ap.add_argument("--simulate-world", type=int, default=0,
                     help="projection only (1 process): rank 0's share of an N-GPU run -- pair shard of N, "
                          "sweep over N x states -- with the all-gather replaced by a local scatter")
@@ -162,6 +252,13 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     os.environ["AQC_DEVICE"] = str(local)
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.simulate_world:
+        workers = args.cpu_workers or min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)))
+        cpu = cpu_baselines(args.cpu_budget, workers)
+        cpu["workers"] = workers
+
     import torch
     import torch.distributed as dist
 
@@ -184,7 +281,7 @@ def main():
     svec = np.zeros((n, 2), complex)
     svec[:, 0] = 1.0
 
-    distinct = [random_vidal_mps(n, CHI, 1000 + k) for k in range(min(args.distinct, S))]
+    distinct = bench_states(n, CHI, min(args.distinct, S), args.state_kind)
     states = []
     for s in range(S):
         d = DeviceMPS(n, CHI, 1e-16, CHI)
@@ -194,14 +291,17 @@ def main():
     work = [DeviceMPS(n, CHI, 1e-16, CHI) for _ in range(B * len(DISTANCES))]
     reload_src = [own[k // len(DISTANCES)] for k in range(len(work))]
     rng = np.random.default_rng(7)
-    layer_ops = []
+    layer_angles, layer_ops = [], []
     for s in range(B):
         for d in DISTANCES:
-            layer_ops.append(_lib.ops_array(thin_layer_ops(LAYER_A, LAYER_A + d, rng.uniform(-np.pi, np.pi, 4))))
+            ang = rng.uniform(-np.pi, np.pi, 4)
+            layer_angles.append(ang)
+            layer_ops.append(_lib.ops_array(thin_layer_ops(LAYER_A, LAYER_A + d, ang)))
     prio = np.ones(len(cmap))
     local_scores = torch.zeros((S, max(len(shard.local_pairs), 1)), dtype=torch.float64, device="cuda")
+    prio_t = torch.as_tensor(prio, device="cuda")
 
-    def step():
+    def sweep():
         # (i) sharded candidate sweep + all-gather + arg-max
         if shard.local_pairs:
             pair_grads_batch(states, svec, shard.local_pairs, u0, gm, deg, out=local_scores.data_ptr())
@@ -210,37 +310,45 @@ def main():
             full[:, torch.as_tensor(shard.local_index, device="cuda")] = local_scores[:, : len(shard.local_pairs)]
         else:
             full = gather_scores(local_scores[:, : len(shard.local_pairs)], shard, nstates=S)
-        best = torch.argmax(full * torch.as_tensor(prio, device=full.device), dim=1)
-        # (ii) overlap evals on own states
+        return full, torch.argmax(full * prio_t, dim=1)
+
+    def overlaps():
+        # (ii) overlap evals on own states: reload the cached MPS, replay + save, <0|psi>
         copy_batch(work, reload_src)
-        apply_batch(work, layer_ops, sort=True)  # replay + save (sorted), as mps_from_circuit
-        ov = overlap_zero_batch(work)
-        costs = 1.0 - np.abs(ov) ** 2
-        return best, costs
+        apply_batch(work, layer_ops, sort=True)
+        return 1.0 - np.abs(overlap_zero_batch(work)) ** 2
+
+    def step():
+        full, best = sweep()
+        costs = overlaps()
+        return full, best, costs
+
+    def barrier():
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+
+    def timed(fn, k):
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(k):
+            r = fn()
+        barrier()
+        el = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([el], dtype=torch.float64, device="cuda")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        return el, r
 
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    barrier()
     _lib.timing_reset()
     _lib.timing_enable(True)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        best, costs = step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t1 = time.perf_counter()
+    elapsed, (full, best, costs) = timed(step, args.steps)
     _lib.timing_enable(False)
-    elapsed = t1 - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
         chk = best.to(torch.int64).clone()
         ref = chk.clone()
         dist.broadcast(ref, 0)
@@ -251,6 +359,16 @@ def main():
 
     fams = {f: _lib.timing_query(f)
             for f in ("mps_chain", "mps_svd", "mps_theta", "mps_split", "grad_chain", "mps_overlap0", "mps_copy")}
+
+    # each evaluation kind on its own (outside the headline timed region)
+    k_ph = max(2, args.steps // 2)
+    t_sw, _ = timed(sweep, k_ph)
+    t_ov, _ = timed(overlaps, k_ph)
+    grad_rate = S * len(cmap) * k_ph / t_sw
+    ov_rate = B * len(DISTANCES) * k_ph / t_ov * (shard_world if not sim else 1)
+    mix_g, mix_o = len(cmap), REF_OVERLAPS_PER_LAYER
+    ref_mix = (mix_g + mix_o) / (mix_g / grad_rate + mix_o / ov_rate)
+
     dom = max(fams, key=lambda f: fams[f]["ms"])
     fd = fams[dom]
     launches = max(fd["launches"], 1)
@@ -259,16 +377,17 @@ def main():
         # fused per-state chain (k_chain): per two-site update the nominal SVD flops of the
         # 128 x 128 theta (84 n^3) + theta (32 chi^3) + split GEMM (32 chi^3), from the launch's
         # KernelTimer record; one launch serves every state of the step
-        roof = {"kernel": "k_chain (fused two-site updates: theta, Jacobi SVD, split)", "bound": "mfma",
+        roof = {"kernel": "k_chain (fused two-site updates: theta, SVD, split)", "bound": "valu-fp64",
                 "achieved": fd["flops"] / launches / (avg_ms * 1e-3) / 1e12, "peak": FP64_PEAK_TFLOPS,
                 "unit": "TFLOP/s", "updates_per_launch": fd["flops"] / launches / ((84.0 * 8 + 64.0) * CHI ** 3),
-                "svd_share_of_flops": 84.0 * 8 / (84.0 * 8 + 64.0)}
+                "svd_share_of_flops": 84.0 * 8 / (84.0 * 8 + 64.0),
+                "peak_note": "FP64 VALU and FP64 MFMA share one 78.6 TFLOP/s ceiling on gfx950 "
+                             "(profiles/r2_fp64_pipes.txt)"}
     elif dom == "mps_svd":
-        # jobs per launch: the 4B two-site updates of one lock-step wave (all 128 x 128 at chi = 64)
         jobs = fd["bytes"] / (2.0 * 4 * CHI * CHI * 16)
         achieved_flop = jobs / launches * svd_nominal_flops(2 * CHI, 2 * CHI)
-        roof = {"kernel": "k_jacobi (two-site SVD)", "bound": "mfma", "achieved": achieved_flop / (avg_ms * 1e-3) / 1e12,
-                "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s"}
+        roof = {"kernel": "k_jacobi (two-site SVD)", "bound": "valu-fp64",
+                "achieved": achieved_flop / (avg_ms * 1e-3) / 1e12, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s"}
     else:
         roof = {"kernel": dom, "bound": "hbm", "achieved": fd["bytes"] / launches / (avg_ms * 1e-3) / 1e9,
                 "peak": HBM_PEAK_GBS, "unit": "GB/s"}
@@ -289,9 +408,12 @@ def main():
     roof["avg_launch_ms"] = avg_ms
     roof["launches"] = fd["launches"]
 
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(distinct, layer, u0, gm, deg, args.cpu_budget)
+    parity = None
+    if rank == 0 and not args.no_parity and not sim:
+        parity = parity_check(full, best, costs, distinct, layer_angles, shard_world, cmap, prio)
+    latency = None
+    if rank == 0 and world == 1 and not args.no_latency and not sim:
+        latency = latency_block(distinct[0], cpu)
 
     if rank == 0 and sim:
         print(json.dumps({"projection": f"rank 0 of a {sim}-GPU run on one GPU (no collective)",
@@ -299,6 +421,19 @@ def main():
                           "projected_value": evals_per_step * args.steps / elapsed,
                           "breakdown_ms": {f: round(v["ms"] / args.steps, 3) for f, v in fams.items()}}))
     elif rank == 0:
+        cpu_line = None
+        if cpu is not None:
+            g, o = cpu["gradient"]["evals_per_s"], cpu["overlap"]["evals_per_s"]
+            step_mix = (len(cmap) + len(DISTANCES)) / (len(cmap) / g + len(DISTANCES) / o)
+            cpu_line = {
+                "value": step_mix, "unit": "evals/s", "cores": cpu["workers"], "kind": "port",
+                "sample": (f"oracle port of the reference structure, {cpu['workers']} processes x 1 BLAS thread, "
+                           f"{args.cpu_budget:.0f} s per kind: {cpu['gradient']['evals']} pair gradients "
+                           f"(12 generators, per-pair MPS builds + dots) and {cpu['overlap']['evals']} overlap evals "
+                           f"(d = 1, 2, 5, 25 round-robin, numpy SVDs), combined at the step's 1225:4 mix"),
+                "gradient_evals_per_s": g, "overlap_evals_per_s": o,
+                "reference_mix_evals_per_s": (mix_g + mix_o) / (mix_g / g + mix_o / o),
+            }
         line = {
             "metric": "overlap+gradient evals/sec, 50-qubit MPS chi=64, 1/2/4/8 MI355X",
             "value": value,
@@ -311,7 +446,7 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "c128",
-            "data": "synthetic random Vidal MPS (seeded), random layer angles",
+            "data": f"synthetic {args.state_kind} chi=64 Vidal MPS (seeded), random layer angles",
             "config": {
                 "workload": "config3: 50-qubit chi=64 MPS; per state 1225-pair identity_resolvable gradient sweep "
                             "(sharded, RCCL all-gather, arg-max) + 4 thinly-dressed-layer overlap evals (d=1,2,5,25)",
@@ -319,15 +454,107 @@ def main():
                 "pairs": len(cmap), "generators": int(len(deg)), "parallelism": f"pairs sharded x{world}",
             },
             "breakdown_ms": {f: round(v["ms"] / args.steps, 3) for f, v in fams.items()},
-            "gradient_evals_per_s": S * len(cmap) * args.steps / elapsed,
-            "overlap_evals_per_s": S * len(DISTANCES) * args.steps / elapsed,
+            "by_kind": {
+                "gradient_evals_per_s": grad_rate, "overlap_evals_per_s": ov_rate,
+                "reference_mix_evals_per_s": ref_mix,
+                "reference_mix": f"{mix_g} gradients + {mix_o} overlap evals per state (one layer, SURVEY 3 S2)",
+                "vs_cpu": ({"gradient": grad_rate / cpu_line["gradient_evals_per_s"],
+                            "overlap": ov_rate / cpu_line["overlap_evals_per_s"],
+                            "reference_mix": ref_mix / cpu_line["reference_mix_evals_per_s"]} if cpu_line else None),
+            },
             "roofline": roof,
-            "cpu_baseline": cpu,
+            "cpu_baseline": cpu_line,
+            "parity_check": parity,
+            "latency": latency,
         }
         print(json.dumps(line))
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def parity_check(full, best, costs, distinct, layer_angles, world, cmap, prio):
+    """State 0 of the last step against the oracle (outside every timed region): its 1225 gradients
+    (environment form, pinned to the reference structure by the tests; 8 pairs also through the
+    reference structure) and arg-max pair, and its four overlap evaluations (fused chain)."""
+    from oracle import gradients as ogr, mps as M
+
+    n = N_QUBITS
+    q0 = distinct[0]
+    psi = M.MPS.from_aer(q0).preprocessed()
+    _, og, od, inv0 = oracle_layer()
+    want = np.array(ogr.general_grad_of_pairs_env(psi, n, inv0, og, od, cmap))
+    got = full[0].double().cpu().numpy()
+    idx = np.random.default_rng(3).choice(len(cmap), 8, replace=False)
+    want_ref = np.array(ogr.general_grad_of_pairs_ref(psi, n, inv0, og, od, [cmap[i] for i in idx], (), 1e-16, CHI))
+    st = M.MPS.from_aer(q0)
+    ov_err, cost_err = 0.0, 0.0
+    for k, d in enumerate(DISTANCES):  # state 0's work states are the first len(DISTANCES)
+        out = M.run_circuit(n, thin_layer_oracle_ops(LAYER_A, LAYER_A + d, layer_angles[k]), 1e-16, CHI, mps=st)
+        c_ref = 1 - abs(M.mps_dot(out.preprocessed(), M.zero_mps(n))) ** 2
+        cost_err = max(cost_err, abs(float(costs[k]) - c_ref))
+    best0 = int(best[0].item())
+    res = {
+        "state": "state 0 (seed 1000), last timed step",
+        "grad_max_abs_err_env": float(np.max(np.abs(got - want))),
+        "grad_max_abs_err_ref_structure_8_pairs": float(np.max(np.abs(got[idx] - want_ref))),
+        "grad_max": float(np.max(want)),
+        "argmax_pair": list(cmap[best0]),
+        "argmax_match": bool(best0 == int(np.argmax(want * prio))),
+        "overlap_cost_max_abs_err": cost_err,
+        "costs": [float(c) for c in costs[:len(DISTANCES)]],
+    }
+    res["ok"] = bool(res["grad_max_abs_err_env"] < 1e-9 and res["argmax_match"] and cost_err < 1e-6)
+    return res
+
+
+def latency_block(q0, cpu):
+    """One state alone: an overlap evaluation per distance (reload + replay + save + <0|psi>), and
+    one Rotoselect gate -- replace_with_best_1q_gate's 7 evaluations (cost_minimiser.py:318-342:
+    the current angle, then rx / ry / rz at +-pi/2) -- as one batch from the cached MPS; medians
+    over repeats, each against one evaluation of the CPU port on one core."""
+    from adaptaqc_amd import _lib
+    from adaptaqc_amd.device import DeviceMPS, copy_batch, apply_batch, overlap_zero_batch
+
+    n = N_QUBITS
+    src = DeviceMPS(n, CHI, 1e-16, CHI)
+    src.load_aer(q0)
+    rng = np.random.default_rng(11)
+    cpu_ms = (cpu or {}).get("overlap", {}).get("eval_ms_by_distance", {})
+
+    def run(ws, ops, reps=5):
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            copy_batch(ws, [src] * len(ws))
+            apply_batch(ws, ops, sort=True)
+            overlap_zero_batch(ws)
+            ts.append(time.perf_counter() - t0)
+        return 1e3 * float(np.median(ts[1:]))
+
+    out = {"overlap_eval_ms": {}, "cpu_port_eval_ms_1core": cpu_ms, "speedup_vs_cpu_1core": {}}
+    w = [DeviceMPS(n, CHI, 1e-16, CHI)]
+    for d in DISTANCES:
+        ops = [_lib.ops_array(thin_layer_ops(LAYER_A, LAYER_A + d, rng.uniform(-np.pi, np.pi, 4)))]
+        out["overlap_eval_ms"][str(d)] = run(w, ops)
+        if str(d) in cpu_ms:
+            out["speedup_vs_cpu_1core"][str(d)] = cpu_ms[str(d)] / out["overlap_eval_ms"][str(d)]
+    for d in (1, 5):
+        base = rng.uniform(-np.pi, np.pi, 4)
+        cands = [(tuple(THIN_AXES), base)]
+        for ax in ("rx", "ry", "rz"):
+            for th in (np.pi / 2, -np.pi / 2):
+                c = base.copy()
+                c[0] = th
+                cands.append(((ax,) + tuple(THIN_AXES[1:]), c))
+        ws = [DeviceMPS(n, CHI, 1e-16, CHI) for _ in cands]
+        ops = [_lib.ops_array(thin_layer_ops(LAYER_A, LAYER_A + d, ang, axes)) for axes, ang in cands]
+        t = run(ws, ops)
+        out[f"rotoselect_gate_7_evals_ms_d{d}"] = t
+        if str(d) in cpu_ms:
+            out[f"rotoselect_gate_speedup_vs_cpu_1core_d{d}"] = 7 * cpu_ms[str(d)] / t
+    out["note"] = "single state on one GPU; wall time of one evaluation (or one gate's 7 as one batch)"
+    return out
 
 
 if __name__ == "__main__":

@@ -170,28 +170,10 @@ def test_argmax_c_abi_tie_break():
 
 
 def _near_zero_state(n, chi, seed, alpha=0.6):
-    """|psi> ~ alpha |p> + |phi>: |p> a product of single-qubit states near |0> (angles 0.15),
-    phi random, normalised, with bonds min(2^k - 1, 2^(n-k) - 1, chi - 1) -- every bond of psi at
-    min(2^k, 2^(n-k), chi), and gradients far from zero (for a random chi = 128 state every overlap
-    with a |0..0>-like state is ~1e-8)."""
-    from bench import random_vidal_mps, vidal_from_tensors
+    """bench.near_product_mps: every bond at min(2^k, 2^(n-k), chi), gradients far from zero."""
+    from bench import near_product_mps
 
-    rng = np.random.default_rng(seed)
-    dims = [1] + [min(2 ** k - 1, 2 ** (n - k) - 1, chi - 1) for k in range(1, n)] + [1]
-    A = [(rng.standard_normal((2, dims[i], dims[i + 1])) + 1j * rng.standard_normal((2, dims[i], dims[i + 1])))
-         for i in range(n)]
-    gam, lam = vidal_from_tensors(A)
-    phi = [np.stack(g) * (lam[i][None, None, :] if i < n - 1 else 1.0) for i, g in enumerate(gam)]
-    out = []
-    for i, t in enumerate(phi):  # block-diagonal sum with the |0> product chain
-        s, l, r = t.shape
-        li, ri = (1 if i == 0 else l + 1), (1 if i == n - 1 else r + 1)
-        x = np.zeros((2, li, ri), dtype=complex)
-        a, b = 0.15 * (1 + rng.random()), rng.uniform(-np.pi, np.pi)
-        x[:, 0, 0] = (alpha if i == 0 else 1.0) * np.array([np.cos(a), np.exp(1j * b) * np.sin(a)])
-        x[:, li - l:, ri - r:] = t
-        out.append(x)
-    return vidal_from_tensors(out)
+    return near_product_mps(n, chi, seed, alpha)
 
 
 def test_config4_full_size_chi128_vs_oracle():
