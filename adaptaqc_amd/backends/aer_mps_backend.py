@@ -1,3 +1,17 @@
+# (C) Copyright IBM 2025.
+#
+# This code is licensed under the Apache License, Version 2.0. You may
+# obtain a copy of this license in the LICENSE.txt file in the root directory
+# of this source tree or at http://www.apache.org/licenses/LICENSE-2.0.
+#
+# Any modifications or derivative works of this code must retain this
+# copyright notice, and modified files need to carry a notice indicating
+# that they have been altered from the originals.
+#
+# Modified for adaptaqc_amd: this file restates the reference file named in its docstring
+# (qiskit-community/adapt-aqc) on top of the MI355X engine (libaqchip); it has been altered
+# from the original.
+
 """MPS backend on MI355X: drop-in for adaptaqc/backends/aer_mps_backend.py:27-93.
 
 ``compiler.full_circuit[0]`` is the ``set_matrix_product_state`` op holding the cached MPS
@@ -10,9 +24,9 @@ from types import SimpleNamespace
 
 import numpy as np
 
-from ..circuit import device_ops
+from ..circuit import device_ops, mps_payload
 from ..device import DeviceMPS
-from ..mps_operations import chi_cap_for, zero_aer_mps
+from ..mps_operations import apply_checked, chi_cap_for, zero_aer_mps
 from .aqc_backend import AQCBackend
 
 logger = logging.getLogger(__name__)
@@ -65,7 +79,7 @@ class AerMPSBackend(AQCBackend):
         start = 0
         payload = None
         if len(circuit.data) and circuit.data[0].operation.name == "set_matrix_product_state":
-            payload = circuit.data[0].operation.params[0]
+            payload = mps_payload(circuit.data[0].operation)
             start = 1
         key = id(payload) if payload is not None else ("zero", n)
         lmax = max(np.asarray(a).shape[1] for a, _ in payload[0]) if payload is not None else 1
@@ -91,7 +105,7 @@ class AerMPSBackend(AQCBackend):
         work = self._work
         work.set_truncation(thr, max_chi)
         work.copy_from(base)
-        work.apply(device_ops(circuit, start))
+        apply_checked(work, device_ops(circuit, start))
         work.sort()
         return work
 

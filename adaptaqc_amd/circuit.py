@@ -206,6 +206,10 @@ class QuantumCircuit:
     def barrier(self, *args):
         return self
 
+    def find_bit(self, q):
+        """qiskit's ``find_bit``: here qubits are their own indices."""
+        return BitLocation(int(q))
+
     # -- container protocol ------------------------------------------------------------
     def __len__(self):
         return len(self.data)
@@ -267,9 +271,59 @@ class QuantumCircuit:
         return max(level) if level else 0
 
 
-def decompose(ins: CircuitInstruction):
+class BitLocation:
+    """``QuantumCircuit.find_bit`` result (qiskit's BitLocations: ``.index``)."""
+
+    __slots__ = ("index",)
+
+    def __init__(self, index):
+        self.index = index
+
+
+def mps_payload(op):
+    """The Aer-format MPS ``(list[(G0, G1)], list[lambda])`` held by a set_matrix_product_state
+    instruction: ``params[0]`` here and in qiskit-aer's SetMatrixProductState; an instruction that
+    carries gammas and lambdas as two parameters is accepted too."""
+    ps = list(op.params)
+    if len(ps) == 2 and isinstance(ps[0], (list, tuple)) and len(ps[0]) and isinstance(ps[0][0], (list, tuple)):
+        return ps[0], ps[1]
+    return ps[0]
+
+
+def qubit_indices(circuit, ins):
+    """Integer qubit indices of an instruction: plain ints (this IR), or qiskit ``Qubit`` objects
+    resolved through ``circuit.find_bit`` (the reference's qiskit circuits)."""
+    out = []
+    for q in ins.qubits:
+        if isinstance(q, (int, np.integer)):
+            out.append(int(q))
+        else:
+            out.append(int(circuit.find_bit(q).index))
+    return tuple(out)
+
+
+def op_matrix(op):
+    """Matrix of a gate: this IR's Operation, or a qiskit-shaped gate (standard names through the
+    same gate tables, anything else through its own ``to_matrix()``)."""
+    if isinstance(op, Operation):
+        return op.to_matrix()
+    name = op.name
+    params = list(getattr(op, "params", ()))
+    try:
+        vals = [float(p) for p in params]
+        if op.num_qubits == 1 and (name in G.CONST_1Q or name in ONE_Q):
+            return G.one_qubit(name, vals)
+        if op.num_qubits == 2 and name in TWO_Q:
+            return G.two_qubit(name, vals)
+    except (TypeError, ValueError, KeyError):
+        pass
+    return np.asarray(op.to_matrix(), dtype=complex)
+
+
+def decompose(ins, qubits=None):
     """Yield (matrix, qubits) 1-/2-qubit pieces of an instruction (unroll_to_basis_gates)."""
-    op, q = ins.operation, ins.qubits
+    op = ins.operation
+    q = tuple(qubits) if qubits is not None else tuple(ins.qubits)
     name = op.name
     if name in ("barrier", "measure", "id"):
         return
@@ -283,14 +337,40 @@ def decompose(ins: CircuitInstruction):
         return
     if op.num_qubits > 2:
         raise ValueError(f"gate {name} on {op.num_qubits} qubits is not supported")
-    yield op.to_matrix(), q
+    yield op_matrix(op), q
 
 
-def device_ops(circuit: QuantumCircuit, start: int = 0):
-    """Flatten gates from ``circuit.data[start:]`` into (matrix, qubits) pairs."""
+def device_ops(circuit, start: int = 0):
+    """Flatten gates from ``circuit.data[start:]`` into (matrix, qubits) pairs.  ``circuit`` is
+    this IR's QuantumCircuit or a qiskit-shaped one (``data`` of instructions with ``operation``
+    and ``qubits``, ``find_bit``), so the backends drop into the reference's own compiler."""
     out = []
     for ins in circuit.data[start:]:
         if ins.operation.name == "set_matrix_product_state":
             raise ValueError("set_matrix_product_state must be the first instruction")
-        out.extend(decompose(ins))
+        if ins.operation.name in ("barrier", "measure", "id", "delay"):
+            continue
+        out.extend(decompose(ins, qubit_indices(circuit, ins)))
     return out
+
+
+_QASM_NAMES = {"rx", "ry", "rz", "p", "u1", "u", "u3", "u2", "x", "y", "z", "h", "s", "sdg", "t", "tdg", "sx",
+               "sxdg", "id", "cx", "cy", "cz", "swap", "crx", "cry", "crz", "cp", "cu1", "rzz", "ccx"}
+
+
+def qasm2_dumps(circuit) -> str:
+    """OpenQASM 2.0 text of a circuit (``qiskit.qasm2.dumps`` for the standard-gate circuits the
+    compiler builds; adapt_compiler.py:359-366 keeps one per layer in ``circuit_history``)."""
+    lines = ["OPENQASM 2.0;", 'include "qelib1.inc";', f"qreg q[{circuit.num_qubits}];"]
+    for ins in circuit.data:
+        op = ins.operation
+        if op.name == "barrier":
+            continue
+        if op.name not in _QASM_NAMES:
+            raise ValueError(f"qasm2_dumps: gate {op.name} has no OpenQASM 2 form here")
+        ps = ""
+        if op.params:
+            ps = "(" + ",".join(repr(float(p)) for p in op.params) + ")"
+        qs = ",".join(f"q[{q}]" for q in qubit_indices(circuit, ins))
+        lines.append(f"{op.name}{ps} {qs};")
+    return "\n".join(lines) + "\n"

@@ -1,3 +1,17 @@
+# (C) Copyright IBM 2025.
+#
+# This code is licensed under the Apache License, Version 2.0. You may
+# obtain a copy of this license in the LICENSE.txt file in the root directory
+# of this source tree or at http://www.apache.org/licenses/LICENSE-2.0.
+#
+# Any modifications or derivative works of this code must retain this
+# copyright notice, and modified files need to carry a notice indicating
+# that they have been altered from the originals.
+#
+# Modified for adaptaqc_amd: this file restates the reference file named in its docstring
+# (qiskit-community/adapt-aqc) on top of the MI355X engine (libaqchip); it has been altered
+# from the original.
+
 """AdaptCompiler host loop (reference compilers/adapt/adapt_compiler.py:48-1163).
 
 Restates the adaptive layer loop around the hot path: pair selection (general_gradient sweep on
@@ -16,7 +30,7 @@ from pathlib import Path
 import numpy as np
 
 from ...backends.python_default_backends import SV_SIM
-from ...circuit import QuantumCircuit
+from ...circuit import QuantumCircuit, qasm2_dumps
 from ...mps_operations import mps_from_circuit
 from ...utils import ansatzes as ans
 from ...utils import circuit_operations as co
@@ -145,6 +159,13 @@ class AdaptCompiler(ApproximateCompiler):
                 co.remove_unnecessary_gates_from_circuit(self.full_circuit, False, False, gate_range=self.g_range())
             ref = self.ref_circuit_as_gates if self.is_aer_mps_backend else self.full_circuit
             num_2q_gates, _ = co.find_num_gates(ref, gate_range=self.g_range(ref if self.is_aer_mps_backend else None))
+            if self.save_circuit_history:  # adapt_compiler.py:359-366 (MPS: without the MPS op)
+                if not self.is_aer_mps_backend:
+                    self.circuit_history.append(qasm2_dumps(self.full_circuit))
+                else:
+                    circuit_copy = self.full_circuit.copy()
+                    del circuit_copy.data[0]
+                    self.circuit_history.append(qasm2_dumps(circuit_copy))
             cinl = self.adapt_config.cost_improvement_num_layers
             cit = self.adapt_config.cost_improvement_tol
             if len(self.global_cost_history) >= cinl and has_stopped_improving(self.global_cost_history[-cinl:], cit):
@@ -172,12 +193,18 @@ class AdaptCompiler(ApproximateCompiler):
         final_global_cost = self.backend.evaluate_global_cost(self)
         self.soften_global_cost = soft
         self.global_cost_history.append(final_global_cost)
+        if checkpoint_every > 0:  # adapt_compiler.py:432-439: the finished state is checkpointed too
+            self.checkpoint(checkpoint_every, checkpoint_dir, delete_prev_chkpt, len(self.qubit_pair_history) - 1,
+                            start_time)
         compiled = self.get_compiled_circuit()
         num_2q_gates, num_1q_gates = co.find_num_gates(compiled)
         self.cnot_depth_history.append(multi_qubit_gate_depth(compiled))
         exact_overlap = "Not computable without SV backend"
         if self.is_statevector_backend:
             exact_overlap = co.calculate_overlap_between_circuits(self.circuit_to_compile, compiled)
+        if self.save_circuit_history and self.is_aer_mps_backend:
+            logger.warning("When using MPS backend, circuit history will not contain the "
+                           "set_matrix_product_state instruction at the start of the circuit")
         return AdaptResult(
             circuit=compiled, overlap=1 - final_global_cost, exact_overlap=exact_overlap, num_1q_gates=num_1q_gates,
             num_2q_gates=num_2q_gates, cnot_depth_history=self.cnot_depth_history,

@@ -14,6 +14,7 @@
 // O(n^2 * n_gen) MPS builds and O(n^3 chi^2 n_gen) dot work.
 #include <algorithm>
 #include <cstring>
+#include <mutex>
 
 #include "mps_internal.h"
 
@@ -22,6 +23,9 @@ using aqc::cplx;
 namespace {
 
 constexpr int kT = 256;
+// k_sweep_lr splits each contraction over kT / 64 = 4 waves (part[4]) and k_sweep_w over two
+// halves of kT / 2 = 128 threads (part[2]): both index their partial sums from this block size
+static_assert(kT == 256, "k_sweep_lr / k_sweep_w assume 4 waves of 64 lanes per workgroup");
 
 struct SweepJob {
   const cplx* gam;
@@ -227,7 +231,7 @@ __global__ void k_sweep_grad(const SweepJob* __restrict__ jobs, SweepConst c) {
     const double gg = -aqc::cmul(ov, z).y;
     g += gg * gg * c.degs[k];
   }
-  j.out[(size_t)blockIdx.y * 0 + p] = sqrt(g);
+  j.out[p] = sqrt(g);  // out is per job (make_job)
 }
 
 __global__ void k_argmax(const double* s, const double* prio, int count, int* best) {
@@ -265,16 +269,51 @@ __global__ void k_argmax(const double* s, const double* prio, int count, int* be
   if (threadIdx.x == 0) *best = bi[0];
 }
 
+// Per-device staging for the sweep's jobs and constants: a ring of two (pinned host, device)
+// buffer pairs, each guarded by an event recorded after the launches that read it, so a call
+// packs its constants into one pinned buffer and issues ONE asynchronous copy instead of draining
+// the stream and issuing blocking hipMemcpys.
 struct GradBuffers {
   void* dev = nullptr;
   size_t cap = 0;
+  char* host = nullptr;
+  size_t hcap = 0;
+  hipEvent_t done = nullptr;
+  bool pending = false;
 };
 
-GradBuffers& gbuf() {
-  static GradBuffers g[64];
+struct GradRing {
+  std::mutex mu;
+  GradBuffers b[2];
+  int next = 0;
+};
+
+GradRing& gring() {
+  static GradRing g[64];
   int dev = 0;
   hipGetDevice(&dev);
   return g[dev];
+}
+
+int grad_buffers(GradBuffers& gb, size_t need) {
+  if (gb.pending) {
+    AQC_HIP_CHECK(hipEventSynchronize(gb.done));
+    gb.pending = false;
+  }
+  if (need > gb.cap) {
+    if (gb.dev) hipFree(gb.dev);
+    gb.dev = nullptr;
+    gb.cap = std::max(need, 2 * gb.cap);
+    AQC_HIP_CHECK(hipMalloc(&gb.dev, gb.cap));
+  }
+  if (need > gb.hcap) {
+    if (gb.host) hipHostFree(gb.host);
+    gb.host = nullptr;
+    gb.hcap = std::max(need, 2 * gb.hcap);
+    AQC_HIP_CHECK(hipHostMalloc((void**)&gb.host, gb.hcap, hipHostMallocDefault));
+  }
+  if (!gb.done) AQC_HIP_CHECK(hipEventCreateWithFlags(&gb.done, hipEventDisableTiming));
+  return AQC_OK;
 }
 
 int ensure_gw(aqc_mps_t h) {
@@ -337,7 +376,7 @@ int aqc_pair_grads_batch(aqc_mps_t* psis, int ns, const double* svec, const int*
     if (rc != AQC_OK) return rc;
   }
   hipStream_t st = aqc::mps_stream();
-  // constants + jobs + (host-out) result buffer in one device allocation
+  // constants + jobs + (host-out) result buffer: one pinned image, one asynchronous copy
   const size_t jb = ns * sizeof(SweepJob);
   // chains are needed only for the first qubits present in `pairs` (pair sharding across ranks)
   std::vector<int> alist;
@@ -347,44 +386,51 @@ int aqc_pair_grads_batch(aqc_mps_t* psis, int ns, const double* svec, const int*
     for (int a = 0; a < n - 1; ++a)
       if (need[a]) alist.push_back(a);
   }
-  const size_t cb = (alist.size() + 4 + n) * sizeof(int) + 2 * npairs * sizeof(int) + 2 * n * sizeof(cplx) + 16 * sizeof(cplx) +
-                    16 * (size_t)ngen * sizeof(cplx) + ngen * sizeof(double) + 256;
-  const size_t ob = out_is_device ? 0 : (size_t)ns * npairs * sizeof(double);
-  GradBuffers& gb = gbuf();
-  AQC_HIP_CHECK(hipStreamSynchronize(st));
-  const size_t need = jb + cb + ob + 1024;
-  if (need > gb.cap) {
-    if (gb.dev) hipFree(gb.dev);
-    gb.cap = std::max(need, 2 * gb.cap);
-    AQC_HIP_CHECK(hipMalloc(&gb.dev, gb.cap));
-  }
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  const size_t o_jobs = 0;
+  const size_t o_pairs = al(o_jobs + jb);
+  const size_t o_svec = al(o_pairs + 2 * (size_t)npairs * sizeof(int));
+  const size_t o_u0 = o_svec + 2 * (size_t)n * sizeof(cplx);
+  const size_t o_gens = o_u0 + 16 * sizeof(cplx);
+  const size_t o_degs = o_gens + 16 * (size_t)ngen * sizeof(cplx);
+  const size_t o_alist = al(o_degs + (size_t)ngen * sizeof(double));
+  const size_t o_start = al(o_alist + (alist.size() + 4) * sizeof(int));
+  const size_t o_out = al(o_start + (size_t)n * sizeof(int));
+  const size_t image = o_out;  // bytes copied host -> device
+  const size_t need = o_out + (out_is_device ? 0 : (size_t)ns * npairs * sizeof(double)) + 256;
+  GradRing& ring = gring();
+  std::lock_guard<std::mutex> lk(ring.mu);
+  GradBuffers& gb = ring.b[ring.next];
+  ring.next ^= 1;
+  rc = grad_buffers(gb, need);
+  if (rc != AQC_OK) return rc;
   char* base = (char*)gb.dev;
-  SweepJob* djobs = (SweepJob*)base;
-  char* cptr = base + ((jb + 255) / 256) * 256;
-  int* dpairs = (int*)cptr;
-  cplx* dsvec = (cplx*)(cptr + ((2 * npairs * sizeof(int) + 15) / 16) * 16);
-  cplx* du0 = dsvec + 2 * n;
-  cplx* dgens = du0 + 16;
-  double* ddegs = (double*)(dgens + 16 * (size_t)ngen);
-  int* dalist = (int*)(ddegs + ngen);
-  int* dstart = dalist + alist.size() + 4;  // n flags: chain start (v0 needed) at this qubit
-  double* dout = out_is_device ? out : (double*)(((uintptr_t)(dstart + n) + 255) & ~(uintptr_t)255);
-  std::vector<SweepJob> jobs(ns);
-  for (int s = 0; s < ns; ++s) jobs[s] = make_job(psis[s], dout + (size_t)s * npairs);
-  AQC_HIP_CHECK(hipMemcpy(djobs, jobs.data(), jb, hipMemcpyHostToDevice));
-  if (npairs) AQC_HIP_CHECK(hipMemcpy(dpairs, pairs, 2 * npairs * sizeof(int), hipMemcpyHostToDevice));
-  AQC_HIP_CHECK(hipMemcpy(dsvec, svec, 2 * n * sizeof(cplx), hipMemcpyHostToDevice));
-  AQC_HIP_CHECK(hipMemcpy(du0, u0, 16 * sizeof(cplx), hipMemcpyHostToDevice));
-  if (!alist.empty()) AQC_HIP_CHECK(hipMemcpy(dalist, alist.data(), alist.size() * sizeof(int), hipMemcpyHostToDevice));
+  char* hbase = gb.host;
+  SweepJob* djobs = (SweepJob*)(base + o_jobs);
+  int* dpairs = (int*)(base + o_pairs);
+  cplx* dsvec = (cplx*)(base + o_svec);
+  cplx* du0 = (cplx*)(base + o_u0);
+  cplx* dgens = (cplx*)(base + o_gens);
+  double* ddegs = (double*)(base + o_degs);
+  int* dalist = (int*)(base + o_alist);
+  int* dstart = (int*)(base + o_start);  // n flags: chain start (v0 needed) at this qubit
+  double* dout = out_is_device ? out : (double*)(base + o_out);
   {
-    std::vector<int> startf(n, 0);
-    for (int a : alist) startf[a] = 1;
-    AQC_HIP_CHECK(hipMemcpy(dstart, startf.data(), n * sizeof(int), hipMemcpyHostToDevice));
+    SweepJob* hj = (SweepJob*)(hbase + o_jobs);
+    for (int s = 0; s < ns; ++s) hj[s] = make_job(psis[s], dout + (size_t)s * npairs);
+    if (npairs) std::memcpy(hbase + o_pairs, pairs, 2 * (size_t)npairs * sizeof(int));
+    std::memcpy(hbase + o_svec, svec, 2 * (size_t)n * sizeof(cplx));
+    std::memcpy(hbase + o_u0, u0, 16 * sizeof(cplx));
+    if (ngen) {
+      std::memcpy(hbase + o_gens, gens, 16 * (size_t)ngen * sizeof(cplx));
+      std::memcpy(hbase + o_degs, degs, (size_t)ngen * sizeof(double));
+    }
+    if (!alist.empty()) std::memcpy(hbase + o_alist, alist.data(), alist.size() * sizeof(int));
+    int* hstart = (int*)(hbase + o_start);
+    for (int a = 0; a < n; ++a) hstart[a] = 0;
+    for (int a : alist) hstart[a] = 1;
   }
-  if (ngen) {
-    AQC_HIP_CHECK(hipMemcpy(dgens, gens, 16 * (size_t)ngen * sizeof(cplx), hipMemcpyHostToDevice));
-    AQC_HIP_CHECK(hipMemcpy(ddegs, degs, ngen * sizeof(double), hipMemcpyHostToDevice));
-  }
+  AQC_HIP_CHECK(hipMemcpyAsync(base, hbase, image, hipMemcpyHostToDevice, st));
   const int cap = psis[0]->d.cap;
   hipLaunchKernelGGL(k_sweep_M, dim3(n, ns), dim3(kT), 0, st, djobs, dsvec);
   AQC_CHECK_LAUNCH();
@@ -416,9 +462,13 @@ int aqc_pair_grads_batch(aqc_mps_t* psis, int ns, const double* svec, const int*
     hipLaunchKernelGGL(k_sweep_grad, dim3((npairs + 127) / 128, ns), dim3(128), 0, st, djobs, c);
     AQC_CHECK_LAUNCH();
   }
+  AQC_HIP_CHECK(hipEventRecord(gb.done, st));
+  gb.pending = true;
   if (!out_is_device && npairs) {
     AQC_HIP_CHECK(hipMemcpyAsync(out, dout, (size_t)ns * npairs * sizeof(double), hipMemcpyDeviceToHost, st));
   }
+  // the result (host, or device memory that the caller reads on its own stream, e.g. the
+  // all-gather's) is complete on return: one wait at the end, none before the launches
   AQC_HIP_CHECK(hipStreamSynchronize(st));
   return AQC_OK;
 }
@@ -431,22 +481,41 @@ int aqc_pair_grads(aqc_mps_t psi, const double* svec, const int* pairs, int npai
 int aqc_argmax_scaled(const double* scores, const double* prio, int count, int scores_is_device, int* best) {
   AQC_REQUIRE(scores && prio && best && count > 0, "aqc_argmax_scaled: bad arguments");
   hipStream_t st = aqc::mps_stream();
-  double* ds = nullptr;
-  double* dp = nullptr;
-  int* db = nullptr;
-  AQC_HIP_CHECK(hipMalloc(&dp, count * sizeof(double) + sizeof(int) * 4));
-  db = (int*)(dp + count);
-  if (!scores_is_device) {
-    AQC_HIP_CHECK(hipMalloc(&ds, count * sizeof(double)));
-    AQC_HIP_CHECK(hipMemcpy(ds, scores, count * sizeof(double), hipMemcpyHostToDevice));
+  // cached per-device (pinned host, device) pair: no allocation per call, one copy each way
+  struct ArgmaxBuf {
+    std::mutex mu;
+    double* dev = nullptr;
+    double* host = nullptr;
+    size_t cap = 0;  // doubles
+  };
+  static ArgmaxBuf bufs[64];
+  int devi = 0;
+  hipGetDevice(&devi);
+  ArgmaxBuf& ab = bufs[devi];
+  std::lock_guard<std::mutex> lk(ab.mu);
+  const size_t need = 2 * (size_t)count + 4;
+  if (need > ab.cap) {
+    if (ab.dev) hipFree(ab.dev);
+    if (ab.host) hipHostFree(ab.host);
+    ab.dev = nullptr;
+    ab.host = nullptr;
+    ab.cap = std::max(need, 2 * ab.cap);
+    AQC_HIP_CHECK(hipMalloc(&ab.dev, ab.cap * sizeof(double)));
+    AQC_HIP_CHECK(hipHostMalloc((void**)&ab.host, ab.cap * sizeof(double), hipHostMallocDefault));
   }
-  AQC_HIP_CHECK(hipMemcpy(dp, prio, count * sizeof(double), hipMemcpyHostToDevice));
+  double* dp = ab.dev;
+  double* ds = ab.dev + count;
+  int* db = (int*)(ab.dev + 2 * (size_t)count);
+  std::memcpy(ab.host, prio, count * sizeof(double));
+  if (!scores_is_device) std::memcpy(ab.host + count, scores, count * sizeof(double));
+  AQC_HIP_CHECK(hipMemcpyAsync(dp, ab.host, (scores_is_device ? 1 : 2) * (size_t)count * sizeof(double),
+                               hipMemcpyHostToDevice, st));
   hipLaunchKernelGGL(k_argmax, dim3(1), dim3(256), 0, st, scores_is_device ? scores : ds, dp, count, db);
   AQC_CHECK_LAUNCH();
-  AQC_HIP_CHECK(hipMemcpyAsync(best, db, sizeof(int), hipMemcpyDeviceToHost, st));
+  int* hb = (int*)(ab.host + 2 * (size_t)count);
+  AQC_HIP_CHECK(hipMemcpyAsync(hb, db, sizeof(int), hipMemcpyDeviceToHost, st));
   AQC_HIP_CHECK(hipStreamSynchronize(st));
-  hipFree(dp);
-  if (ds) hipFree(ds);
+  *best = *hb;
   return AQC_OK;
 }
 

@@ -1585,27 +1585,56 @@ struct StagingSet {
   bool pending = false;
 };
 
-StagingSet& staging_acquire() {
-  constexpr int kRing = 4;
-  static StagingSet sets[64][kRing];
-  static int next[64] = {0};
-  int dev = 0;
-  hipGetDevice(&dev);
-  StagingSet& ss = sets[dev][next[dev]];
-  next[dev] = (next[dev] + 1) % kRing;
-  if (ss.pending) {
-    hipEventSynchronize(ss.done);
-    ss.pending = false;
+// A lease on the next set of this device's ring.  It holds the device's staging mutex for its
+// lifetime (several host threads may drive one device) and records the set's event on the stream
+// on EVERY exit path -- an early error return included -- so the set is never handed out again
+// while kernels queued before the error may still read it.
+class StagingLease {
+ public:
+  explicit StagingLease(hipStream_t st) : st_(st), lk_(mutex_for(device())) {
+    constexpr int kRing = 4;
+    static StagingSet sets[64][kRing];
+    static int next[64] = {0};
+    const int dev = device();
+    ss_ = &sets[dev][next[dev]];
+    next[dev] = (next[dev] + 1) % kRing;
+    if (ss_->pending) {
+      const hipError_t e = hipEventSynchronize(ss_->done);
+      if (e != hipSuccess) {
+        aqc::set_error(std::string("staging event wait: ") + hipGetErrorString(e));
+        rc_ = AQC_ERR_HIP;
+      }
+      ss_->pending = false;
+    }
   }
-  return ss;
-}
+  ~StagingLease() {
+    if (!ss_->done && hipEventCreateWithFlags(&ss_->done, hipEventDisableTiming) != hipSuccess) {
+      hipStreamSynchronize(st_);  // no event: drain instead, so the next user finds the set idle
+      return;
+    }
+    if (hipEventRecord(ss_->done, st_) == hipSuccess) ss_->pending = true;
+    else hipStreamSynchronize(st_);
+  }
+  StagingLease(const StagingLease&) = delete;
+  StagingLease& operator=(const StagingLease&) = delete;
+  Staging& buf() { return ss_->buf; }
+  int rc() const { return rc_; }
 
-int staging_release(StagingSet& ss, hipStream_t st) {
-  if (!ss.done) AQC_HIP_CHECK(hipEventCreateWithFlags(&ss.done, hipEventDisableTiming));
-  AQC_HIP_CHECK(hipEventRecord(ss.done, st));
-  ss.pending = true;
-  return AQC_OK;
-}
+ private:
+  static int device() {
+    int dev = 0;
+    hipGetDevice(&dev);
+    return dev;
+  }
+  static std::mutex& mutex_for(int dev) {
+    static std::mutex m[64];
+    return m[dev];
+  }
+  hipStream_t st_;
+  std::unique_lock<std::mutex> lk_;
+  StagingSet* ss_ = nullptr;
+  int rc_ = AQC_OK;
+};
 
 TwoSiteJob make_two(aqc_mps_t h, const DevOp& op, int slot = 0) {
   TwoSiteJob j;
@@ -1718,8 +1747,9 @@ int run_chains(aqc_mps_t* hs, int ns, std::vector<std::vector<DevOp>>& lists, in
   const size_t o_codes = al(o_one + one.size() * sizeof(OneSiteJob));
   const size_t o_chain = al(o_codes + codes.size() * sizeof(int));
   const size_t total = o_chain + (size_t)ns * sizeof(ChainJob);
-  StagingSet& ss = staging_acquire();
-  Staging& sg = ss.buf;
+  StagingLease lease(st);
+  if (lease.rc() != AQC_OK) return lease.rc();
+  Staging& sg = lease.buf();
   int rc = ensure_staging(sg, total);
   if (rc != AQC_OK) return rc;
   char* hb = (char*)sg.host;
@@ -1742,7 +1772,7 @@ int run_chains(aqc_mps_t* hs, int ns, std::vector<std::vector<DevOp>>& lists, in
                      (const TwoSiteJob*)(db + o_two), (const OneSiteJob*)(db + o_one));
   aqc::KernelTimer::end(st);
   AQC_CHECK_LAUNCH();
-  return staging_release(ss, st);
+  return AQC_OK;  // the lease records the set's event
 }
 
 int run_waves(aqc_mps_t* hs, int ns, std::vector<std::vector<DevOp>>& lists) {
@@ -1794,8 +1824,9 @@ int run_waves(aqc_mps_t* hs, int ns, std::vector<std::vector<DevOp>>& lists) {
     one_rng[w] = {o0, one.size() - o0};
   }
   const size_t tb = two.size() * sizeof(TwoSiteJob), ob = one.size() * sizeof(OneSiteJob);
-  StagingSet& ss = staging_acquire();
-  Staging& sg = ss.buf;
+  StagingLease lease(st);
+  if (lease.rc() != AQC_OK) return lease.rc();
+  Staging& sg = lease.buf();
   int rc = ensure_staging(sg, tb + ob + 256);
   if (rc != AQC_OK) return rc;
   std::memcpy(sg.host, two.data(), tb);
@@ -1859,7 +1890,7 @@ int run_waves(aqc_mps_t* hs, int ns, std::vector<std::vector<DevOp>>& lists) {
       AQC_CHECK_LAUNCH();
     }
   }
-  return staging_release(ss, st);
+  return AQC_OK;  // the lease records the set's event
 }
 
 int check_flags(aqc_mps_t h) {

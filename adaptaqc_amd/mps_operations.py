@@ -8,7 +8,7 @@ from __future__ import annotations
 
 import numpy as np
 
-from .circuit import QuantumCircuit, device_ops
+from .circuit import QuantumCircuit, device_ops, mps_payload
 from .device import DeviceMPS
 
 MAX_CHI_CAP = 256
@@ -50,6 +50,22 @@ def chi_cap_for(n, max_chi, loaded_max=1):
     return cap
 
 
+def apply_checked(state: DeviceMPS, ops):
+    """state.apply(ops), re-raising a bond-capacity overflow with the remedy: an unbounded run
+    (max_chi None, the reference default) is capped at MAX_CHI_CAP on the device, where Aer's MPS
+    would keep growing."""
+    from ._lib import AqcError
+
+    try:
+        state.apply(ops)
+    except AqcError as e:
+        if "capacity" in str(e):
+            raise AqcError(f"{e} -- this MPS needs a bond dimension above chi_cap = {state.chi_cap} (the device "
+                           f"engine supports at most {MAX_CHI_CAP}); set max_chi (mps_sim_with_args(max_chi=...)) "
+                           f"to truncate as Aer's matrix_product_state_max_bond_dimension does") from e
+        raise
+
+
 def _sim_options(sim):
     if sim is None:
         return 1e-16, None
@@ -66,7 +82,7 @@ def device_mps_from_circuit(circuit: QuantumCircuit, sim=None, trunc_thr=None, o
     start = 0
     loaded = None
     if len(circuit.data) and circuit.data[0].operation.name == "set_matrix_product_state":
-        loaded = circuit.data[0].operation.params[0]
+        loaded = mps_payload(circuit.data[0].operation)
         start = 1
     lmax = max(np.asarray(a).shape[1] for a, _ in loaded[0]) if loaded is not None else 1
     cap = chi_cap_for(n, max_chi, lmax)
@@ -78,7 +94,7 @@ def device_mps_from_circuit(circuit: QuantumCircuit, sim=None, trunc_thr=None, o
         out.load_aer(loaded)
     else:
         out.load_aer(zero_aer_mps(n))
-    out.apply(device_ops(circuit, start))
+    apply_checked(out, device_ops(circuit, start))
     out.sort()
     return out
 

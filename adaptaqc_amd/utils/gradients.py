@@ -1,3 +1,17 @@
+# (C) Copyright IBM 2025.
+#
+# This code is licensed under the Apache License, Version 2.0. You may
+# obtain a copy of this license in the LICENSE.txt file in the root directory
+# of this source tree or at http://www.apache.org/licenses/LICENSE-2.0.
+#
+# Any modifications or derivative works of this code must retain this
+# copyright notice, and modified files need to carry a notice indicating
+# that they have been altered from the originals.
+#
+# Modified for adaptaqc_amd: this file restates the reference file named in its docstring
+# (qiskit-community/adapt-aqc) on top of the MI355X engine (libaqchip); it has been altered
+# from the original.
+
 """Candidate-pair gradients on MI355X: drop-in for adaptaqc/utils/gradients.py:23-224.
 
 ``general_grad_of_pairs`` keeps the reference signature and return value (list of floats, one
@@ -11,7 +25,7 @@ from typing import List, Tuple
 import numpy as np
 
 from .. import gates as G
-from ..circuit import QuantumCircuit
+from ..circuit import QuantumCircuit, op_matrix, qubit_indices
 from ..device import DeviceMPS, pair_grads_batch
 from ..mps_operations import device_mps_from_circuit
 from .utilityfunctions import get_distinct_items_and_degeneracies
@@ -24,8 +38,9 @@ def circuit_unitary(qc: QuantumCircuit) -> np.ndarray:
     n = qc.num_qubits
     u = np.eye(2 ** n, dtype=complex)
     for ins in qc.data:
-        m = ins.operation.to_matrix()
-        full = _embed(m, ins.qubits, n)
+        if ins.operation.name in ("barrier", "id"):
+            continue
+        full = _embed(op_matrix(ins.operation), qubit_indices(qc, ins), n)
         u = full @ u
     return u
 
@@ -60,7 +75,8 @@ def product_state_vectors(n, starting_circuit):
             continue
         if len(ins.qubits) != 1:
             return None
-        s[ins.qubits[0]] = ins.operation.to_matrix() @ s[ins.qubits[0]]
+        q = qubit_indices(starting_circuit, ins)[0]
+        s[q] = op_matrix(ins.operation) @ s[q]
     return s
 
 

@@ -113,8 +113,14 @@ def test_checkpoint_resume(tmp_path):
     from adaptaqc_amd.compilers import AdaptCompiler, AdaptConfig
 
     qc = to_circuit(4, _random_state_circuit(4, 2, 3))
-    comp = AdaptCompiler(qc, backend=AerMPSBackend(), adapt_config=AdaptConfig(method="basic", max_layers=3))
-    comp.compile(checkpoint_every=1, checkpoint_dir=str(tmp_path))
+    comp = AdaptCompiler(qc, backend=AerMPSBackend(), adapt_config=AdaptConfig(method="basic", max_layers=3),
+                         save_circuit_history=True)
+    first = comp.compile(checkpoint_every=1, checkpoint_dir=str(tmp_path))
+    # one QASM circuit per layer, without the MPS op (adapt_compiler.py:359-366)
+    assert len(first.circuit_history) == len(first.qubit_pair_history) >= 1
+    assert all(h.startswith("OPENQASM 2.0;") and "set_matrix_product_state" not in h for h in first.circuit_history)
+    # the finished state is checkpointed as well (adapt_compiler.py:432-439)
+    assert os.path.exists(os.path.join(tmp_path, f"{len(first.qubit_pair_history) - 1}.pkl"))
     with open(os.path.join(tmp_path, "1.pkl"), "rb") as f:
         resumed = pickle.load(f)
     assert resumed.resume_from_layer == 2
