@@ -87,8 +87,26 @@ class ApproximateCompiler(ABC):
         if starting_circuit is None or isinstance(starting_circuit, QuantumCircuit):
             return starting_circuit
         if starting_circuit == "tenpy_product_state":
-            raise NotImplementedError("tenpy is not available; pass the product-state circuit explicitly")
+            return self.product_state_circuit()
         raise ValueError("starting_circuit must be a QuantumCircuit, None, or string: 'tenpy_product_state'")
+
+    def product_state_circuit(self, min_sweeps=10, max_sweeps=50, tol=1e-12):
+        """approximate_compiler.py:222-242: the best chi = 1 approximation of the target (the
+        reference compresses with tenpy's variational method, chi_max 1, 10-50 sweeps), as one
+        single-qubit unitary per qubit in rx / ry / rz (tenpy_chi_1_mps_to_circuit,
+        utilityfunctions.py:333-358).  Here the compression runs on the device
+        (aqc_mps_product_fit: alternating two-site updates); parity with tenpy is unpinned."""
+        from ..mps_operations import device_mps_from_circuit
+
+        if self.is_aer_mps_backend:
+            thr = self.backend.simulator.options.matrix_product_state_truncation_threshold
+        else:
+            thr = 1e-8
+        psi = device_mps_from_circuit(self.circuit_to_compile.copy(), trunc_thr=thr)
+        svec, fid, sweeps = psi.product_fit(None, min_sweeps, max_sweeps, tol)
+        self.starting_state_fidelity = fid
+        logger.info(f"Product-state starting circuit: fidelity {fid:.6f} after {sweeps} sweeps")
+        return product_state_to_circuit(svec)
 
     def variational_circuit_range(self, circuit=None):
         if circuit is None:
@@ -134,3 +152,18 @@ class ApproximateCompiler(ABC):
         if self.optimise_local_cost:
             return self.backend.evaluate_local_cost(self)
         return self.backend.evaluate_global_cost(self)
+
+
+def product_state_to_circuit(svec):
+    """One single-qubit unitary per qubit with column 0 = the qubit's state (U = [[a, conj(b)],
+    [b, -conj(a)]], utilityfunctions.py:341-352), written in rz / ry / rz (the reference
+    transpiles to the basis rx, ry, rz; any such form prepares the same state up to phase)."""
+    n = len(svec)
+    qc = QuantumCircuit(n)
+    for q, (a, b) in enumerate(svec):
+        u = [[a, b.conjugate()], [b, -a.conjugate()]]
+        theta, phi, lam = co.zyz_angles(u)
+        for name, ang in (("rz", lam), ("ry", theta), ("rz", phi)):
+            if abs(ang) > 1e-14:
+                qc.append(co.create_1q_gate(name, float(ang)), [q])
+    return qc

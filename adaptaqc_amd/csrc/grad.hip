@@ -15,6 +15,7 @@
 #include <algorithm>
 #include <cstring>
 #include <mutex>
+#include <vector>
 
 #include "mps_internal.h"
 
@@ -269,6 +270,226 @@ __global__ void k_argmax(const double* s, const double* prio, int count, int* be
   if (threadIdx.x == 0) *best = bi[0];
 }
 
+// ---- chi = 1 variational compression (tenpy_product_state, approximate_compiler.py:222-242) ----
+// The best product-state approximation |s> = (x) s_i of psi by alternating two-site updates: with
+// every other site fixed, <s|psi> = sum_ab conj(s_i[a]) conj(s_{i+1}[b]) F[a][b], F[a][b] =
+// l_i A_i[a] A_{i+1}[b] r_{i+2}, is maximised by the top singular pair of the 2 x 2 F (s_i = u_1,
+// s_{i+1} = conj(v_1), |<s|psi>| = sigma_1).  One sweep = a left-to-right pass (right
+// environments r from the current s, left ones carried along) and a right-to-left pass.  One
+// workgroup per state; the chains are O(n chi^2) and sequential.
+struct FitJob {
+  const cplx* gam;
+  const double* lam;
+  const int* dims;
+  int n;
+  int cap;
+  cplx* svec;   // n x 2 (in: initial guess unless guess_from_gamma, out: result)
+  cplx* Lv;     // (n + 1) x cap left environments
+  cplx* Rv;     // (n + 1) x cap right environments
+  double* out;  // [0] fidelity |<s|psi>|^2, [1] sweeps, [2] fidelity after each sweep (max_sweeps)
+  int guess_from_gamma;
+  int min_sweeps;
+  int max_sweeps;
+  double tol;
+};
+
+__device__ __forceinline__ cplx fit_a(const FitJob& j, int i, int s, int l, int r) {
+  const size_t ss = (size_t)2 * j.cap * j.cap;
+  return aqc::cscale(j.gam[(size_t)i * ss + (size_t)s * j.cap * j.cap + (size_t)l * j.cap + r],
+                     j.lam[(size_t)(i + 1) * j.cap + r]);
+}
+
+// top singular pair of the 2 x 2 complex F (row a, column b): F v = sigma u
+__device__ void top_pair_2x2(const cplx F[4], cplx u[2], cplx v[2], double& sigma) {
+  const double h00 = F[0].x * F[0].x + F[0].y * F[0].y + F[2].x * F[2].x + F[2].y * F[2].y;
+  const double h11 = F[1].x * F[1].x + F[1].y * F[1].y + F[3].x * F[3].x + F[3].y * F[3].y;
+  const cplx h01 = aqc::cadd(aqc::cmul(aqc::cconj(F[0]), F[1]), aqc::cmul(aqc::cconj(F[2]), F[3]));
+  const double hm = 0.5 * (h00 + h11), hd = 0.5 * (h00 - h11);
+  const double lam = hm + sqrt(hd * hd + h01.x * h01.x + h01.y * h01.y);
+  cplx v0, v1;
+  if (h00 >= h11) {
+    v0 = aqc::cmk(lam - h11, 0.0);
+    v1 = aqc::cconj(h01);
+  } else {
+    v0 = h01;
+    v1 = aqc::cmk(lam - h00, 0.0);
+  }
+  double nv = sqrt(v0.x * v0.x + v0.y * v0.y + v1.x * v1.x + v1.y * v1.y);
+  if (!(nv > 0.0)) {
+    v0 = aqc::cmk(1, 0);
+    v1 = aqc::cmk(0, 0);
+    nv = 1.0;
+  }
+  v[0] = aqc::cscale(v0, 1.0 / nv);
+  v[1] = aqc::cscale(v1, 1.0 / nv);
+  const cplx a0 = aqc::cfma(F[1], v[1], aqc::cmul(F[0], v[0]));
+  const cplx a1 = aqc::cfma(F[3], v[1], aqc::cmul(F[2], v[0]));
+  sigma = sqrt(a0.x * a0.x + a0.y * a0.y + a1.x * a1.x + a1.y * a1.y);
+  if (sigma > 0.0) {
+    u[0] = aqc::cscale(a0, 1.0 / sigma);
+    u[1] = aqc::cscale(a1, 1.0 / sigma);
+  } else {
+    u[0] = aqc::cmk(1, 0);
+    u[1] = aqc::cmk(0, 0);
+  }
+}
+
+__global__ __launch_bounds__(kT) void k_product_fit(const FitJob* __restrict__ jobs) {
+  const FitJob& j = jobs[blockIdx.x];
+  const int n = j.n, cap = j.cap, tid = threadIdx.x;
+  __shared__ cplx vec[256];       // running l (left-to-right) or r (right-to-left)
+  __shared__ cplx uw[2][2][256];  // u[s][m], w[s][m]
+  __shared__ cplx part[4][kT / 64];
+  __shared__ cplx sv[2][2];       // the updated pair
+  __shared__ double fid_s;
+  if (j.guess_from_gamma && tid == 0) {
+    // chi = 1 truncation of the canonical form: keep the largest Schmidt value on every bond
+    for (int i = 0; i < n; ++i) {
+      const size_t ss = (size_t)2 * cap * cap;
+      cplx a = j.gam[(size_t)i * ss], b = j.gam[(size_t)i * ss + (size_t)cap * cap];
+      const double nn = sqrt(a.x * a.x + a.y * a.y + b.x * b.x + b.y * b.y);
+      if (nn > 0.0) {
+        a = aqc::cscale(a, 1.0 / nn);
+        b = aqc::cscale(b, 1.0 / nn);
+      } else {
+        a = aqc::cmk(1, 0);
+        b = aqc::cmk(0, 0);
+      }
+      j.svec[2 * i] = a;
+      j.svec[2 * i + 1] = b;
+    }
+  }
+  __syncthreads();
+  // r_k = M_k r_{k+1} for k = n-1 .. lo (M_k = sum_s conj(s_k[s]) A_k[s]); l_{k+1} = l_k M_k for k < hi
+  auto right_envs = [&]() {
+    if (tid == 0) j.Rv[(size_t)n * cap] = aqc::cmk(1, 0);
+    __syncthreads();
+    for (int k = n - 1; k >= 0; --k) {
+      const int cl = j.dims[k], cr = j.dims[k + 1];
+      const cplx c0 = aqc::cconj(j.svec[2 * k]), c1 = aqc::cconj(j.svec[2 * k + 1]);
+      const cplx* rn = j.Rv + (size_t)(k + 1) * cap;
+      for (int l = tid; l < cl; l += kT) {
+        cplx a0 = aqc::cmk(0, 0), a1 = aqc::cmk(0, 0);
+        for (int r = 0; r < cr; ++r) {
+          a0 = aqc::cfma(fit_a(j, k, 0, l, r), rn[r], a0);
+          a1 = aqc::cfma(fit_a(j, k, 1, l, r), rn[r], a1);
+        }
+        j.Rv[(size_t)k * cap + l] = aqc::cfma(c1, a1, aqc::cmul(c0, a0));
+      }
+      __syncthreads();
+    }
+  };
+  auto left_envs = [&]() {
+    if (tid == 0) j.Lv[0] = aqc::cmk(1, 0);
+    __syncthreads();
+    for (int k = 0; k < n; ++k) {
+      const int cl = j.dims[k], cr = j.dims[k + 1];
+      const cplx c0 = aqc::cconj(j.svec[2 * k]), c1 = aqc::cconj(j.svec[2 * k + 1]);
+      const cplx* lp = j.Lv + (size_t)k * cap;
+      for (int r = tid; r < cr; r += kT) {
+        cplx a0 = aqc::cmk(0, 0), a1 = aqc::cmk(0, 0);
+        for (int l = 0; l < cl; ++l) {
+          a0 = aqc::cfma(lp[l], fit_a(j, k, 0, l, r), a0);
+          a1 = aqc::cfma(lp[l], fit_a(j, k, 1, l, r), a1);
+        }
+        j.Lv[(size_t)(k + 1) * cap + r] = aqc::cfma(c1, a1, aqc::cmul(c0, a0));
+      }
+      __syncthreads();
+    }
+  };
+  // u[s][m] = sum_l lv[l] A_i[s][l][m], w[s][m] = sum_r A_{i+1}[s][m][r] rv[r]; F; update of (i, i+1)
+  auto update = [&](int i, const cplx* lv, const cplx* rv) {
+    const int cl = j.dims[i], cm = j.dims[i + 1], cr = j.dims[i + 2];
+    for (int e = tid; e < 2 * cm; e += kT) {
+      const int s = e / cm, m = e % cm;
+      cplx a = aqc::cmk(0, 0), b = aqc::cmk(0, 0);
+      for (int l = 0; l < cl; ++l) a = aqc::cfma(lv[l], fit_a(j, i, s, l, m), a);
+      for (int r = 0; r < cr; ++r) b = aqc::cfma(fit_a(j, i + 1, s, m, r), rv[r], b);
+      uw[0][s][m] = a;
+      uw[1][s][m] = b;
+    }
+    __syncthreads();
+    // F[a][b] = sum_m u[a][m] w[b][m]: wave q -> entry q
+    {
+      const int q = tid >> 6, lane = tid & 63;
+      const int a = q >> 1, b = q & 1;
+      cplx acc = aqc::cmk(0, 0);
+      for (int m = lane; m < cm; m += 64) acc = aqc::cfma(uw[0][a][m], uw[1][b][m], acc);
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) {
+        acc.x += __shfl_xor(acc.x, off);
+        acc.y += __shfl_xor(acc.y, off);
+      }
+      if (lane == 0) part[q][0] = acc;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      const cplx F[4] = {part[0][0], part[1][0], part[2][0], part[3][0]};
+      cplx u[2], v[2];
+      double sg;
+      top_pair_2x2(F, u, v, sg);
+      sv[0][0] = u[0];
+      sv[0][1] = u[1];
+      sv[1][0] = aqc::cconj(v[0]);
+      sv[1][1] = aqc::cconj(v[1]);
+      j.svec[2 * i] = sv[0][0];
+      j.svec[2 * i + 1] = sv[0][1];
+      j.svec[2 * (i + 1)] = sv[1][0];
+      j.svec[2 * (i + 1) + 1] = sv[1][1];
+      fid_s = sg * sg;
+    }
+    __syncthreads();
+  };
+  double prev = -1.0;
+  int sweep = 0;
+  if (n == 1) {  // a single site: s = psi itself
+    if (tid == 0) {
+      cplx a = fit_a(j, 0, 0, 0, 0), b = fit_a(j, 0, 1, 0, 0);
+      const double nn = sqrt(a.x * a.x + a.y * a.y + b.x * b.x + b.y * b.y);
+      j.svec[0] = aqc::cscale(a, 1.0 / nn);
+      j.svec[1] = aqc::cscale(b, 1.0 / nn);
+      j.out[0] = nn * nn;
+      j.out[1] = 0;
+    }
+    return;
+  }
+  for (sweep = 0; sweep < j.max_sweeps; ++sweep) {
+    // left to right
+    right_envs();
+    if (tid == 0) vec[0] = aqc::cmk(1, 0);
+    __syncthreads();
+    for (int i = 0; i < n - 1; ++i) {
+      update(i, vec, j.Rv + (size_t)(i + 2) * cap);
+      const int cm = j.dims[i + 1];
+      for (int m = tid; m < cm; m += kT)
+        vec[m] = aqc::cfma(aqc::cconj(sv[0][1]), uw[0][1][m], aqc::cmul(aqc::cconj(sv[0][0]), uw[0][0][m]));
+      __syncthreads();
+    }
+    // right to left
+    left_envs();
+    if (tid == 0) vec[0] = aqc::cmk(1, 0);
+    __syncthreads();
+    for (int i = n - 2; i >= 0; --i) {
+      update(i, j.Lv + (size_t)i * cap, vec);
+      const int cm = j.dims[i + 1];
+      for (int m = tid; m < cm; m += kT)
+        vec[m] = aqc::cfma(aqc::cconj(sv[1][1]), uw[1][1][m], aqc::cmul(aqc::cconj(sv[1][0]), uw[1][0][m]));
+      __syncthreads();
+    }
+    const double f = fid_s;
+    if (tid == 0) j.out[2 + sweep] = f;
+    if (sweep + 1 >= j.min_sweeps && prev >= 0.0 && fabs(f - prev) <= j.tol * f) {
+      ++sweep;
+      break;
+    }
+    prev = f;
+  }
+  if (tid == 0) {
+    j.out[0] = fid_s;
+    j.out[1] = (double)sweep;
+  }
+}
+
 // Per-device staging for the sweep's jobs and constants: a ring of two (pinned host, device)
 // buffer pairs, each guarded by an event recorded after the launches that read it, so a call
 // packs its constants into one pinned buffer and issues ONE asynchronous copy instead of draining
@@ -476,6 +697,68 @@ int aqc_pair_grads_batch(aqc_mps_t* psis, int ns, const double* svec, const int*
 int aqc_pair_grads(aqc_mps_t psi, const double* svec, const int* pairs, int npairs, const double* u0,
                    const double* gens, const double* degs, int ngen, double* out, int out_is_device) {
   return aqc_pair_grads_batch(&psi, 1, svec, pairs, npairs, u0, gens, degs, ngen, out, out_is_device);
+}
+
+int aqc_mps_product_fit(aqc_mps_t psi, double* svec, int guess_from_gamma, int min_sweeps, int max_sweeps,
+                        double tol, double* fidelity, int* sweeps) {
+  AQC_REQUIRE(psi && svec && max_sweeps >= 1 && min_sweeps >= 0 && tol >= 0.0, "aqc_mps_product_fit: bad arguments");
+  AQC_REQUIRE(psi->d.cap <= 256, "aqc_mps_product_fit: bond capacity above 256");
+  int rc = aqc_mps_sort(psi);  // the fit runs in qubit order
+  if (rc != AQC_OK) return rc;
+  rc = ensure_gw(psi);
+  if (rc != AQC_OK) return rc;
+  const int n = psi->d.n, cap = psi->d.cap;
+  hipStream_t st = aqc::mps_stream();
+  // device scratch: the sweep workspace (gw) holds n cap^2 >= 2 (n + 1) cap complex for the
+  // environments; svec, the job and the outputs in a small allocation of their own
+  cplx* Lv = psi->gw;
+  cplx* Rv = Lv + (size_t)(n + 1) * cap;
+  const size_t ob = (2 + (size_t)max_sweeps) * sizeof(double);
+  const size_t bytes = 2 * (size_t)n * sizeof(cplx) + sizeof(FitJob) + ob + 512;
+  char* d = nullptr;
+  AQC_HIP_CHECK(hipMalloc(&d, bytes));
+  cplx* dsv = (cplx*)d;
+  FitJob* dj = (FitJob*)(d + ((2 * (size_t)n * sizeof(cplx) + 255) & ~(size_t)255));
+  double* dout = (double*)((char*)dj + ((sizeof(FitJob) + 255) & ~(size_t)255));
+  FitJob j;
+  j.gam = psi->d.gam;
+  j.lam = psi->d.lam;
+  j.dims = psi->d.dims;
+  j.n = n;
+  j.cap = cap;
+  j.svec = dsv;
+  j.Lv = Lv;
+  j.Rv = Rv;
+  j.out = dout;
+  j.guess_from_gamma = guess_from_gamma ? 1 : 0;
+  j.min_sweeps = min_sweeps;
+  j.max_sweeps = max_sweeps;
+  j.tol = tol;
+  int err = AQC_OK;
+  std::vector<double> hout(2 + max_sweeps, 0.0);
+  do {
+    if (hipMemcpyAsync(dsv, svec, 2 * (size_t)n * sizeof(cplx), hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipMemcpyAsync(dj, &j, sizeof(FitJob), hipMemcpyHostToDevice, st) != hipSuccess) {
+      err = AQC_ERR_HIP;
+      break;
+    }
+    hipLaunchKernelGGL(k_product_fit, dim3(1), dim3(kT), 0, st, (const FitJob*)dj);
+    if (hipGetLastError() != hipSuccess ||
+        hipMemcpyAsync(svec, dsv, 2 * (size_t)n * sizeof(cplx), hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipMemcpyAsync(hout.data(), dout, ob, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess) {
+      err = AQC_ERR_HIP;
+      break;
+    }
+  } while (false);
+  hipFree(d);
+  if (err != AQC_OK) {
+    aqc::set_error("aqc_mps_product_fit: HIP failure");
+    return err;
+  }
+  if (fidelity) *fidelity = hout[0];
+  if (sweeps) *sweeps = (int)hout[1];
+  return AQC_OK;
 }
 
 int aqc_argmax_scaled(const double* scores, const double* prio, int count, int scores_is_device, int* best) {

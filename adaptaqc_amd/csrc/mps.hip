@@ -848,6 +848,10 @@ __global__ __launch_bounds__(CP / 2 * LPG) void k_jacobi_reg(const TwoSiteJob* _
   jacobi_reg_body<CP, MAXR, LPG>(jobs[blockIdx.x]);
 }
 
+#include "jacobi32.h"
+// sweep stop of the FP32 preconditioning stage (mixed-precision SVD)
+float g_jacobi32_tiny = 1e-3f;
+
 // 2 chi = 128 register Jacobi by variant: 5 = 8-lane groups (512 threads), otherwise 16-lane
 // groups (1024 threads).  Dynamic LDS = kG x max(ld, CP + 1) complex.  Measured on the bench's
 // thetas (tools/jacobi_ab.py, tools/svd_phase_timing.py): 8-lane groups cut the round's VALU
@@ -2079,8 +2083,10 @@ int aqc_svd_debug(const double* theta, int m, int n, int variant, int stop_after
   AQC_REQUIRE(m >= 1 && n >= 1 && m % 2 == 0 && n % 2 == 0 && m <= 128 && n <= 128,
               "aqc_svd_debug: m, n must be even and <= 128");
   AQC_REQUIRE(stop_after_qr >= 0 && stop_after_qr <= 2, "aqc_svd_debug: stop_after_qr must be 0, 1 or 2");
-  AQC_REQUIRE(variant == 2 || variant == 3 || variant == 5,
-              "aqc_svd_debug: variant must be 2, 3 or 5");
+  AQC_REQUIRE(variant == 2 || variant == 3 || variant == 5 || variant == 6,
+              "aqc_svd_debug: variant must be 2, 3, 5 or 6");
+  AQC_REQUIRE(variant != 6 || (std::max(m, n) > 64 && stop_after_qr == 0),
+              "aqc_svd_debug: variant 6 (FP32) needs 64 < max(m, n) <= 128 and no QR stop");
   hipStream_t st = aqc::mps_stream();
   const int cp = std::max(m, n) <= 32 ? 32 : (std::max(m, n) <= 64 ? 64 : 128);
   const size_t mat = (size_t)128 * 128 * sizeof(cplx);
@@ -2113,6 +2119,8 @@ int aqc_svd_debug(const double* theta, int m, int n, int variant, int stop_after
   AQC_HIP_CHECK(hipMemsetAsync(wk, 0, mat, st));
   if (cp == 32) hipLaunchKernelGGL((k_jacobi_reg<32, 2>), dim3(1), dim3(256), 16 * 33 * 16, st, dj);
   else if (cp == 64) hipLaunchKernelGGL((k_jacobi_reg<64, 4>), dim3(1), dim3(512), 32 * 65 * 16, st, dj);
+  else if (variant == 6)
+    hipLaunchKernelGGL((k_jacobi32<128, 8, 16>), dim3(1), dim3(1024), 64 * 129 * 16, st, dj, g_jacobi32_tiny);
   else launch_jacobi_reg128(variant, 1, st, dj);
   AQC_CHECK_LAUNCH();
   const int L = std::max(m, n), C = std::min(m, n);
@@ -2142,6 +2150,12 @@ int aqc_mps_jacobi_stats(aqc_mps_t h, int* max_sweeps) {
 int aqc_mps_set_jacobi_tol(double factor) {
   AQC_REQUIRE(factor > 0, "aqc_mps_set_jacobi_tol: factor must be positive");
   g_jacobi_tol_factor = factor;
+  return AQC_OK;
+}
+
+int aqc_mps_set_jacobi32_stop(double tiny_t) {
+  AQC_REQUIRE(tiny_t > 0.0 && tiny_t < 0.1, "aqc_mps_set_jacobi32_stop: need 0 < tiny_t < 0.1");
+  g_jacobi32_tiny = (float)tiny_t;
   return AQC_OK;
 }
 

@@ -185,6 +185,18 @@ class DeviceMPS:
         _lib.check(self._l.aqc_mps_amps_hw1(self.h, _lib.ptr(out)))
         return out[0::2] + 1j * out[1::2]
 
+    def product_fit(self, svec=None, min_sweeps=10, max_sweeps=50, tol=1e-12):
+        """Best product-state approximation (aqc_mps_product_fit): returns (svec (n, 2), fidelity,
+        sweeps).  svec None starts from the chi = 1 truncation of the canonical form."""
+        guess = svec is None
+        s = np.zeros((self.n, 2), dtype=np.complex128) if guess else np.array(svec, dtype=np.complex128)
+        s = np.ascontiguousarray(s.reshape(self.n, 2))
+        fid = ctypes.c_double()
+        sw = ctypes.c_int()
+        _lib.check(self._l.aqc_mps_product_fit(self.h, _lib.ptr(s), int(guess), int(min_sweeps), int(max_sweeps),
+                                               float(tol), ctypes.byref(fid), ctypes.byref(sw)))
+        return s, fid.value, sw.value
+
     def pair_rdms(self, pairs):
         """4x4 RDMs of qubit pairs by environment chains (aqc_research partial_trace semantics)."""
         pairs = np.ascontiguousarray(np.asarray(pairs, dtype=np.int32).reshape(-1))

@@ -110,6 +110,8 @@ int aqc_mps_set_jacobi_tol(double factor);
    decomposition ends (default 1e-6: the off-diagonal left is O(1e-12) relative; tiny_t <= 0
    restores it; must be < 1e-3). */
 int aqc_mps_set_jacobi_stop(double tiny_t);
+/* Sweep stop of the FP32 preconditioning stage of the mixed-precision two-site SVD (default 1e-3). */
+int aqc_mps_set_jacobi32_stop(double tiny_t);
 /* Jacobi kernel: 2 = register-resident columns with pivoted-QR preconditioning for
    2*chi <= 128 (default; larger chi uses 0), 3 = register-resident without QR,
    5 = as 2 with 8-lane column groups at 2*chi = 128 (512 threads),
@@ -142,7 +144,8 @@ int aqc_sv_transition(aqc_sv_t bra, aqc_sv_t ket, int q, double* out);
 int aqc_entanglement_measures(const double* rdms, int count, int method, double* out, int on_device);
 
 /* Diagnostics: one register-resident Jacobi launch (variant 2 / 5 = with pivoted QR, 3 = without)
-   on theta (m x n column-major complex, m, n even <= 128, as the two-site update builds it).
+   on theta (m x n column-major complex, m, n even <= 128, as the two-site update builds it);
+   variant 6 = the FP32 register Jacobi (pivoted QR + sweeps in single precision, 64 < max(m, n)).
    w_out receives min(m,n) columns of length (variant 2 / 5: min(m,n), 3: max(m,n)); sig_out their
    norms; perm_out (optional) the pivot order when stop_after_qr (then w_out holds X = R^H
    unsorted).  stop_after_qr = 2 also writes the QR phase's shader-clock ticks to sig_out[0..3]
@@ -175,6 +178,17 @@ int aqc_pair_grads(aqc_mps_t psi, const double* svec, const int* pairs, int npai
 int aqc_pair_grads_batch(aqc_mps_t* psis, int nstates, const double* svec, const int* pairs,
                          int npairs, const double* u0, const double* gens, const double* degs,
                          int ngen, double* out /* nstates*npairs */, int out_is_device);
+/* Best product-state (chi = 1) approximation of psi: the starting circuit
+ * starting_circuit="tenpy_product_state" (approximate_compiler.py:222-242, which compresses with
+ * tenpy's variational method: trunc_params chi_max = 1, min_sweeps 10, max_sweeps 50).  Alternating
+ * two-site updates maximise |<s|psi>| (each pair's optimum is the top singular pair of its 2 x 2
+ * environment tensor); a sweep is a left-to-right and a right-to-left pass; the fit stops after
+ * min_sweeps once a sweep changes the fidelity by <= tol (relative), or after max_sweeps.
+ * svec: n x 2 complex per-qubit vectors (in: initial guess unless guess_from_gamma != 0, which
+ * starts from the chi = 1 truncation of the canonical form; out: the fit).  fidelity = |<s|psi>|^2
+ * (psi normalised). */
+int aqc_mps_product_fit(aqc_mps_t psi, double* svec, int guess_from_gamma, int min_sweeps, int max_sweeps,
+                        double tol, double* fidelity, int* sweeps);
 /* np.argmax(scores * priorities) with lowest-index tie-break (adapt_compiler.py:832-837). */
 int aqc_argmax_scaled(const double* scores, const double* prio, int count, int scores_is_device,
                       int* best);

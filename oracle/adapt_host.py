@@ -5,8 +5,9 @@
 * reuse priorities and arg-max pair selection (compilers/adapt/adapt_compiler.py:832-837,
   984-1065);
 * layer-absorption counting (adapt_compiler.py:691-706);
-* ``minimum_of_sinusoidal`` (utils/utilityfunctions.py:34-57) and
-  ``has_stopped_improving`` (:272-278).
+* ``minimum_of_sinusoidal`` (utils/utilityfunctions.py:34-57),
+  ``has_stopped_improving`` (:272-278) and the Rotoselect / Rotosolve call sequence
+  (utils/cost_minimiser.py:52-106, 267-368: candidates, order, strict `<`).
 """
 import numpy as np
 
@@ -102,3 +103,85 @@ def has_stopped_improving(hist, rel_tol=1e-2):
         return fit[0] / np.absolute(np.mean(hist)) > -1 * rel_tol
     except np.linalg.LinAlgError:
         return False
+
+
+# --------------------------------------------------------------------------------------------
+# Rotoselect / Rotosolve call sequence (utils/cost_minimiser.py:52-106, 267-368)
+#
+# ``ops`` is a mutable list of [name, qubits, params(list), label]; ``cost_fn(ops)`` evaluates the
+# whole circuit (the reference's ``cost_finder``); ``log`` receives one entry per evaluation:
+# (gate index, gate name, angle) of the gate being varied, in call order.
+# --------------------------------------------------------------------------------------------
+SUPPORTED_1Q = ("rx", "ry", "rz")  # circuit_operations SUPPORTED_1Q_GATES order
+
+
+def _set_gate(ops, i, name, angle):
+    """co.replace_1q_gate (circuit_operations_basic.py:70-99): same qubit, new kind and angle,
+    label = the kind (create_1q_gate, :20-34); a None kind leaves the gate as it is."""
+    if name is None:
+        return
+    ops[i] = [name, ops[i][1], [float(angle)], name]
+
+
+def find_best_angle(ops, i, name, cost_fn, log, cost_for_identity=None):
+    """cost_minimiser.py:344-368: costs at 0, pi/2, -pi/2 (0 skipped when given), closed-form
+    sinusoid minimum; the gate is restored afterwards."""
+    orig = list(ops[i])
+    costs = []
+    angles = [0, np.pi / 2, -np.pi / 2]
+    if cost_for_identity is not None:
+        costs.append(cost_for_identity)
+        angles.remove(0)
+    for th in angles:
+        _set_gate(ops, i, name, th)
+        log.append((i, name, float(th)))
+        costs.append(cost_fn(ops))
+    th_min, c_min = minimum_of_sinusoidal(costs[0], costs[1], costs[2])
+    ops[i] = orig
+    return th_min, c_min
+
+
+def replace_with_best_1q_gate(ops, i, cost_fn, log):
+    """cost_minimiser.py:318-342: rx(0) once, then each axis at +-pi/2; strict `<` keeps the
+    first axis on exact ties."""
+    _set_gate(ops, i, "rx", 0)
+    log.append((i, "rx", 0.0))
+    c_id = cost_fn(ops)
+    best_name, best_angle, best_cost = None, None, 1
+    for name in SUPPORTED_1Q:
+        ang, c = find_best_angle(ops, i, name, cost_fn, log, c_id)
+        if c < best_cost:
+            best_name, best_angle, best_cost = name, ang, c
+    _set_gate(ops, i, best_name, best_angle)
+    return best_cost
+
+
+def reduce_cost(ops, cost_fn, change_kind, index_range, log):
+    """cost_minimiser.py:267-316 (rotosolve_fraction = 1): every supported 1-qubit gate in the
+    range, in circuit order."""
+    cost = 1
+    for i in range(*index_range):
+        if ops[i][0] not in SUPPORTED_1Q:
+            continue
+        if change_kind:
+            cost = replace_with_best_1q_gate(ops, i, cost_fn, log)
+        else:
+            ang, cost = find_best_angle(ops, i, ops[i][3], cost_fn, log)
+            _set_gate(ops, i, ops[i][3], ang)
+    return cost
+
+
+def minimize_cost(ops, cost_fn, rotoselect, index_range, log, max_cycles=1000, stop_val=-np.inf, tol=1e-10):
+    """cost_minimiser.py:52-106: one evaluation, then cycles of reduce_cost until stop_val, the
+    cycle cap, or has_stopped_improving over the last 3 cycles (after more than 3)."""
+    hist = []
+    log.append(("initial",))
+    cost = cost_fn(ops)
+    cycles = 0
+    while cost > stop_val and cycles < max_cycles:
+        cost = reduce_cost(ops, cost_fn, rotoselect, index_range, log)
+        cycles += 1
+        hist.append(cost)
+        if len(hist) > 3 and has_stopped_improving(hist[-3:], tol):
+            break
+    return cost

@@ -193,3 +193,79 @@ def test_compile_cached_vs_generic_same_result():
     assert abs(out[0][0] - out[1][0]) < 1e-8
     assert out[0][1] == out[1][1]
     assert out[0][2] == out[1][2]
+
+
+@pytest.mark.parametrize("backend_kind", ["sv", "mps"])
+@pytest.mark.parametrize("rotoselect", [True, False])
+def test_cached_rotations_vs_oracle_sequence(backend_kind, rotoselect):
+    """The cached path against the oracle's restatement of _reduce_cost / replace_with_best_1q_gate
+    / find_best_angle (oracle/adapt_host.py): per gate the same candidate gates in the same order
+    (rx(0), then rx, ry, rz at +-pi/2 for Rotoselect; 0, +-pi/2 of the gate's kind for Rotosolve),
+    the same costs (1e-10, the oracle's statevector) and the same final gates and angles."""
+    from adaptaqc_amd.backends import AerMPSBackend, AerSVBackend
+    from adaptaqc_amd.compilers import AdaptCompiler
+    from adaptaqc_amd.utils.cached_rotations import rotation
+    from oracle import adapt_host
+
+    n = 4
+    backend = AerSVBackend() if backend_kind == "sv" else AerMPSBackend()
+    comp = AdaptCompiler(to_circuit(n, _random_state_circuit(n, 3, 21)), backend=backend)
+    _insert_ansatz(comp, 5)
+    rng = comp.variational_circuit_range()
+    # the oracle sees the whole circuit the cost is taken on: target (expanded), ansatz, start^-1
+    if backend_kind == "sv":
+        prefix_ops = []
+        body = comp.full_circuit
+        lo = 0
+    else:  # MPS: full_circuit[0] is the target MPS; expand it back to the target's gates
+        prefix_ops = _random_state_circuit(n, 3, 21)
+        body = comp.full_circuit
+        lo = 1
+    ops0 = [[op[0], tuple(op[1]), list(op[2]), None] for op in prefix_ops]
+    off = len(ops0) - lo
+    for ins in body.data[lo:]:
+        ops0.append([ins.operation.name, tuple(ins.qubits), list(ins.operation.params), ins.operation.label])
+    orng = (rng[0] + off, rng[1] + off)
+
+    def cost_fn(o):
+        return 1.0 - abs(osv.simulate(n, [(x[0], x[1], tuple(x[2])) for x in o])[0]) ** 2
+
+    calls = []
+    orig = [list(x[:2]) + [list(x[2]), x[3]] for x in ops0]
+    adapt_host.reduce_cost(ops0, cost_fn, rotoselect, orng, calls)
+    recorded = []
+    factory = comp.minimizer.evaluator_factory
+
+    def wrapped():
+        ev = factory()
+        orig = ev.costs
+
+        def costs(index, mats):
+            out = orig(index, mats)
+            recorded.append((index, [np.asarray(m) for m in mats], list(out)))
+            return out
+
+        ev.costs = costs
+        return ev
+
+    comp.minimizer.evaluator_factory = wrapped
+    count0 = comp.cost_evaluation_counter
+    comp.minimizer._reduce_cost(rotoselect, rng)
+    per_gate = 7 if rotoselect else 3
+    assert comp.cost_evaluation_counter - count0 == len(calls) == per_gate * len(recorded)
+    for g, (index, mats, costs) in enumerate(recorded):
+        want = calls[per_gate * g: per_gate * (g + 1)]
+        assert all(w[0] - off == index for w in want)
+        for m, w, c in zip(mats, want, costs):
+            np.testing.assert_allclose(m, rotation(w[1], w[2]), atol=1e-15)
+            # the candidate circuit as the reference evaluates it: gates before it already at their
+            # optimised values, gates after it still at their original ones
+            i = w[0]
+            trial = ops0[:i] + [[w[1], ops0[i][1], [w[2]], w[1]]] + orig[i + 1:]
+            assert abs(c - cost_fn(trial)) < 1e-10
+    got = [(i.operation.name, float(i.operation.params[0])) for i in comp.full_circuit.data[rng[0]:rng[1]]
+           if i.operation.name in ("rx", "ry", "rz")]
+    want = [(o[0], float(o[2][0])) for o in ops0[orng[0]:orng[1]] if o[0] in ("rx", "ry", "rz")]
+    assert [x[0] for x in got] == [x[0] for x in want]
+    np.testing.assert_allclose([x[1] for x in got], [x[1] for x in want], atol=1e-9)
+

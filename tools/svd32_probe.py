@@ -1,0 +1,61 @@
+"""FP32 register Jacobi (aqc_svd_debug variant 6) vs the FP64 one (variant 2) on the bench's
+swap-routed two-site thetas: singular values against numpy, sweep counts.  Run under
+``rocprofv3 --kernel-trace --stats`` for the kernel times (k_jacobi32 vs k_jacobi_reg).
+
+    python3 tools/svd32_probe.py [reps] [tiny32 ...]
+"""
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+
+def swap_theta(aer, site=24):
+    gam, lam = aer
+    G0 = np.stack(gam[site])
+    G1 = np.stack(gam[site + 1])
+    ll, lm, lr = lam[site - 1], lam[site], lam[site + 1]
+    th = np.einsum("l,alm,m,bmr,r->albr", ll, G0, lm, G1, lr)
+    th = th.transpose(2, 1, 0, 3)  # SWAP: (s2, l, s1, r)
+    return th.reshape(2 * G0.shape[1], 2 * G1.shape[2])
+
+
+def main():
+    from adaptaqc_amd import _lib
+
+    reps = int(sys.argv[1]) if len(sys.argv) > 1 else 5
+    tinies = [float(x) for x in sys.argv[2:]] or [1e-3]
+    L = _lib.lib()
+    for kind in ("near-product", "random"):
+        aer = bench.bench_states(50, 64, 1, kind)[0]
+        T = swap_theta(aer)
+        m, n = T.shape
+        ref = np.linalg.svd(T, compute_uv=False)
+        th = np.asfortranarray(T.astype(np.complex128)).ravel(order="F").view(np.float64).copy()
+        w = np.zeros(2 * m * n)
+        sig = np.zeros(max(m, n))
+        sw = ctypes.c_int()
+        for v, tiny in [(2, None)] + [(6, t) for t in tinies]:
+            if tiny is not None:
+                _lib.check(L.aqc_mps_set_jacobi32_stop(ctypes.c_double(tiny)))
+            for _ in range(reps):
+                _lib.check(L.aqc_svd_debug(_lib.ptr(th), m, n, v, 0, _lib.ptr(w), _lib.ptr(sig), None,
+                                           ctypes.byref(sw)))
+            got = np.sort(sig[:min(m, n)])[::-1]
+            err = np.max(np.abs(got - ref)) / ref[0]
+            # the columns: right singular vectors x sigma (variant 2 / 6 contract); check V^H V
+            W = w.view(np.complex128).reshape(min(m, n), -1)
+            nn = np.linalg.norm(W, axis=1)
+            V = W / nn[:, None]
+            orth = np.max(np.abs(V.conj() @ V.T - np.eye(len(V))))
+            print(f"{kind:12s} variant {v} tiny {tiny}: sweeps {sw.value:2d}  max|sigma - ref|/sigma_1 {err:.2e}  "
+                  f"max|V^H V - I| {orth:.2e}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
