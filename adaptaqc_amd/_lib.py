@@ -30,7 +30,7 @@ EXPORTS = (
     "aqc_pair_grads", "aqc_pair_grads_batch", "aqc_argmax_scaled", "aqc_mps_jacobi_stats",
     "aqc_mps_set_jacobi_tol", "aqc_mps_set_jacobi_stop", "aqc_mps_set_jacobi_variant", "aqc_mps_set_fused_chain", "aqc_mps_chain_ticks", "aqc_svd_debug",
     "aqc_sv_pair_rdms", "aqc_mps_pair_rdms", "aqc_mps_pair_rdms_batch", "aqc_entanglement_measures",
-    "aqc_sv_transition", "aqc_mps_product_fit", "aqc_mps_set_jacobi32_stop",
+    "aqc_sv_transition", "aqc_mps_product_fit", "aqc_mps_set_jacobi32_stop", "aqc_mps_set_svd_path", "aqc_svd_gram_ticks",
 )
 
 
@@ -100,6 +100,8 @@ _SIGS = {
     "aqc_sv_transition": ([_P, _P, _I, _P], _I),
     "aqc_mps_product_fit": ([_P, _P, _I, _I, _I, _D, _DP, _IP], _I),
     "aqc_mps_set_jacobi32_stop": ([_D], _I),
+    "aqc_mps_set_svd_path": ([_I, _I], _I),
+    "aqc_svd_gram_ticks": ([_P], _I),
 }
 
 

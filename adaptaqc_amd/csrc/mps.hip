@@ -50,6 +50,9 @@ int g_jacobi_variant = 2;
 // Fused per-state chain (k_chain) for batches of >= kChainMinStates states at 2 chi = 128.
 bool g_fused_chain = true;
 constexpr int kChainMinStates = 32;
+// dynamic LDS of the 1024-thread two-site kernels: four 64 x 64 GEMM tiles (>= the register
+// Jacobi's 64 x 129 complex exchange buffer)
+constexpr int kChainLdsBytes = 4 * (int)sizeof(aqc::GemmLds);
 
 struct OneSiteJob {
   cplx* g;
@@ -851,6 +854,10 @@ __global__ __launch_bounds__(CP / 2 * LPG) void k_jacobi_reg(const TwoSiteJob* _
 #include "jacobi32.h"
 // sweep stop of the FP32 preconditioning stage (mixed-precision SVD)
 float g_jacobi32_tiny = 1e-3f;
+#include "svd_gram.h"
+// two-site SVDs at 2 chi = 128 try the Gram / tridiagonal path first (aqc_mps_set_svd_path)
+int g_svd_gram = 1;
+int g_debug_max_chi = 64;  // aqc_svd_debug's max_chi (the Gram path keeps K = min(C, max_chi))
 
 // 2 chi = 128 register Jacobi by variant: 5 = 8-lane groups (512 threads), otherwise 16-lane
 // groups (1024 threads).  Dynamic LDS = kG x max(ld, CP + 1) complex.  Measured on the bench's
@@ -860,6 +867,10 @@ float g_jacobi32_tiny = 1e-3f;
 // per group with two independent rotations per step (git history, "block-pair register
 // Jacobi") 11% slower.
 void launch_jacobi_reg128(int variant, int nj, hipStream_t st, const TwoSiteJob* jp) {
+  if (variant == 2 && g_svd_gram) {  // Gram path, the register Jacobi as the in-kernel fallback
+    hipLaunchKernelGGL(k_svd_gram, dim3(nj), dim3(1024), kChainLdsBytes, st, jp);
+    return;
+  }
   if (variant == 5)
     hipLaunchKernelGGL((k_jacobi_reg<128, 16, 8>), dim3(nj), dim3(512), 64 * 136 * 16, st, jp);
   else
@@ -1064,7 +1075,7 @@ struct ChainJob {
   int pad;
 };
 
-constexpr int kChainLds = 4 * (int)sizeof(aqc::GemmLds);  // >= the Jacobi's 64 x 129 complex
+constexpr int kChainLds = kChainLdsBytes;  // >= the Jacobi's 64 x 129 complex
 // phase ticks summed over workgroups: theta, Jacobi, rank, split, one-site
 __device__ unsigned long long g_chain_ticks[5];
 
@@ -1132,7 +1143,13 @@ __device__ __noinline__ void chain_theta(const TwoSiteJob& j) {
     }
   }
 }
-__device__ __noinline__ void chain_jacobi(const TwoSiteJob& j) { jacobi_reg_body<128, 8, 16>(j); }
+__device__ __noinline__ void chain_jacobi(const TwoSiteJob& j) {
+  if (j.gram) {
+    if (gram_svd_body(j)) return;
+    __syncthreads();
+  }
+  jacobi_reg_body<128, 8, 16>(j);
+}
 __device__ __noinline__ void chain_rank(const TwoSiteJob& j) { rank_body<1024>(j); }
 __device__ __noinline__ void chain_split(const TwoSiteJob& j) {
   extern __shared__ double2 xbuf[];
@@ -1668,6 +1685,7 @@ TwoSiteJob make_two(aqc_mps_t h, const DevOp& op, int slot = 0) {
   j.thr = h->thr;
   j.jtol = g_jacobi_tol_factor;
   j.jtiny = g_jacobi_tiny_t;
+  j.gram = g_svd_gram;
   std::memcpy(j.G, op.m, sizeof(j.G));
   return j;
 }
@@ -2083,8 +2101,10 @@ int aqc_svd_debug(const double* theta, int m, int n, int variant, int stop_after
   AQC_REQUIRE(m >= 1 && n >= 1 && m % 2 == 0 && n % 2 == 0 && m <= 128 && n <= 128,
               "aqc_svd_debug: m, n must be even and <= 128");
   AQC_REQUIRE(stop_after_qr >= 0 && stop_after_qr <= 2, "aqc_svd_debug: stop_after_qr must be 0, 1 or 2");
-  AQC_REQUIRE(variant == 2 || variant == 3 || variant == 5 || variant == 6,
-              "aqc_svd_debug: variant must be 2, 3, 5 or 6");
+  AQC_REQUIRE(variant == 2 || variant == 3 || variant == 5 || variant == 6 || variant == 7,
+              "aqc_svd_debug: variant must be 2, 3, 5, 6 or 7");
+  AQC_REQUIRE(variant != 7 || (std::max(m, n) > 64 && stop_after_qr == 0),
+              "aqc_svd_debug: variant 7 (Gram) needs 64 < max(m, n) <= 128 and no QR stop");
   AQC_REQUIRE(variant != 6 || (std::max(m, n) > 64 && stop_after_qr == 0),
               "aqc_svd_debug: variant 6 (FP32) needs 64 < max(m, n) <= 128 and no QR stop");
   hipStream_t st = aqc::mps_stream();
@@ -2111,7 +2131,10 @@ int aqc_svd_debug(const double* theta, int m, int n, int variant, int stop_after
   j.jtol = g_jacobi_tol_factor;
   j.jtiny = g_jacobi_tiny_t;
   j.qr = variant != 3 ? 1 : 0;
-  j.dbg = stop_after_qr;  // 1: stop after the QR phase; 2: also QR phase clock ticks in sig[0..3]
+  j.dbg = stop_after_qr;
+  j.cap = 64;                     // the work buffer holds 128 x 128
+  j.max_chi = g_debug_max_chi;    // Gram path: K = min(C, max_chi)
+  j.gram = variant == 7;  // 1: stop after the QR phase; 2: also QR phase clock ticks in sig[0..3]
   int hd[8] = {m / 2, 0, n / 2, 0, 0, 0, 0, 0};  // dims, then zeroed flags
   AQC_HIP_CHECK(hipMemcpyAsync(th, theta, (size_t)m * n * sizeof(cplx), hipMemcpyHostToDevice, st));
   AQC_HIP_CHECK(hipMemcpyAsync(dm, hd, sizeof(hd), hipMemcpyHostToDevice, st));
@@ -2121,6 +2144,10 @@ int aqc_svd_debug(const double* theta, int m, int n, int variant, int stop_after
   else if (cp == 64) hipLaunchKernelGGL((k_jacobi_reg<64, 4>), dim3(1), dim3(512), 32 * 65 * 16, st, dj);
   else if (variant == 6)
     hipLaunchKernelGGL((k_jacobi32<128, 8, 16>), dim3(1), dim3(1024), 64 * 129 * 16, st, dj, g_jacobi32_tiny);
+  else if (variant == 7)
+    hipLaunchKernelGGL(k_svd_gram, dim3(1), dim3(1024), kChainLdsBytes, st, dj);
+  else if (variant == 2)  // the register Jacobi itself (not the Gram path in front of it)
+    hipLaunchKernelGGL((k_jacobi_reg<128, 8>), dim3(1), dim3(1024), 64 * 129 * 16, st, dj);
   else launch_jacobi_reg128(variant, 1, st, dj);
   AQC_CHECK_LAUNCH();
   const int L = std::max(m, n), C = std::min(m, n);
@@ -2150,6 +2177,23 @@ int aqc_mps_jacobi_stats(aqc_mps_t h, int* max_sweeps) {
 int aqc_mps_set_jacobi_tol(double factor) {
   AQC_REQUIRE(factor > 0, "aqc_mps_set_jacobi_tol: factor must be positive");
   g_jacobi_tol_factor = factor;
+  return AQC_OK;
+}
+
+int aqc_svd_gram_ticks(double* out) {
+  AQC_REQUIRE(out, "aqc_svd_gram_ticks: null argument");
+  unsigned long long t[8];
+  AQC_HIP_CHECK(hipMemcpyFromSymbol(t, HIP_SYMBOL(g_gram_ticks), sizeof(t)));
+  for (int i = 0; i < 8; ++i) out[i] = (double)t[i];
+  unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  AQC_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_gram_ticks), z, sizeof(z)));
+  return AQC_OK;
+}
+
+int aqc_mps_set_svd_path(int gram, int debug_max_chi) {
+  AQC_REQUIRE(gram == 0 || gram == 1, "aqc_mps_set_svd_path: gram must be 0 or 1");
+  g_svd_gram = gram;
+  g_debug_max_chi = debug_max_chi;
   return AQC_OK;
 }
 

@@ -57,6 +57,8 @@ struct TwoSiteJob {
   double jtiny; // sweep stop: a sweep whose counted rotations all had |t| <= jtiny is the last
   int qr;      // 1: Jacobi ran on R^H of a pivoted QR -> W holds the other side (see k_jacobi_reg)
   int dbg;      // diagnostics (aqc_svd_debug): 1 = stop after the QR phase, write X unpermuted
+  int gram;     // 1: try the Gram / tridiagonal SVD first (svd_gram.h), the Jacobi as fallback
+  int pad_;
   cplx G[16];  // row = 2*s1'+s2' (out), col = 2*s1+s2 (in)
 };
 

@@ -1,0 +1,435 @@
+// Two-site SVD through the Gram matrix, its tridiagonal form and inverse iteration -- the fast
+// path of the 2 chi = 128 two-site update when the truncation keeps K <= 64 singular triplets.
+//
+// X = theta' (L x C, or its conjugate transpose so that L >= C):
+//   S1  G = X^H X                                  block GEMM on the FP64 matrix cores (aqc_gemm.h)
+//   S2  G into registers: thread t holds row t/8, columns t%8 + 8i (i < 16)
+//   S3  Householder tridiagonalisation G = Q T Q^H (LAPACK zhetd2, lower): two barriers per column,
+//       double-buffered LDS vectors, the reflectors packed into the work buffer
+//   S4  the top K eigenvalues of the real symmetric tridiagonal T by 17-section: 16 lanes per
+//       eigenvalue each evaluate one Sturm count, one ballot picks the subinterval (8 rounds)
+//   S5  inverse iteration (unpivoted LDL^T of T - lambda I, three solves) per eigenvector, Gram-
+//       Schmidt inside clusters (gaps below 1e-7 ||T||), sigma^2 = z^T T z
+//   S6  back-transformation V = Q Z (one barrier per reflector), output W = V Sigma
+// The output follows the QR-preconditioned register Jacobi's contract (TwoSiteJob::qr = 1): work
+// column c (length C, rows in X's column order) = right singular vector c of X times sigma_c, sig[c]
+// = sigma_c (0 for c >= K), so rank / split are unchanged.
+//
+// Accuracy: forming G squares the condition number, so eigenpairs are accurate to eps ||G|| in
+// absolute terms: singular values to eps sigma_1^2 / sigma_i and the kept subspace to eps sigma_1^2
+// / (sigma_K^2 - sigma_{K+1}^2) -- 1e-14 on the bench's thetas (tools/gram_svd_proto.py), as
+// accurate as the Jacobi.  Small singular values are not resolved: the path declines (returns
+// false, the caller runs the Jacobi) unless lambda_K > 1e-9 lambda_1, i.e. unless every kept
+// value is far above the noise floor and above the reduce_zeros CHOP (1e-16), so the truncation
+// decisions (kept count, tail sum, renormalisation) are the Jacobi's.  It also declines K > 64.
+//
+// Included into mps.hip's anonymous namespace.
+#pragma once
+
+constexpr int kGramMaxK = 64;
+constexpr double kGramRelFloor = 1e-9;
+// shader-clock ticks of the phases (thread 0), summed over calls: S1, S2+S3, S4, S5, S6, output
+__device__ unsigned long long g_gram_ticks[8];
+
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  return v;
+}
+
+// Sum over the 64 lanes, result uniform: DPP row sums, then the four rows through readlane (no
+// LDS crossbar; every lane must be active).
+__device__ __forceinline__ double wave_sum_dpp(double v) {
+  v = aqc::row_sum16(v);
+  double s = 0.0;
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) {
+    const int lo = __builtin_amdgcn_readlane(__double2loint(v), 16 * rr);
+    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), 16 * rr);
+    s += __hiloint2double(hi, lo);
+  }
+  return s;
+}
+
+__device__ __forceinline__ double rcp_nr1(double x) {  // one Newton step: ~2^-46
+  const double r = __builtin_amdgcn_rcp(x);
+  return r * fma(-x, r, 2.0);
+}
+
+__device__ __forceinline__ double rcp_nr(double x) {
+  double r = __builtin_amdgcn_rcp(x);
+  r = r * fma(-x, r, 2.0);
+  r = r * fma(-x, r, 2.0);
+  return r;
+}
+
+// Gram-path SVD of one 2 chi x 2 chi theta'; 1024 threads; `xbuf` = the workgroup's dynamic LDS
+// (>= 4 GemmLds).  Returns false (work untouched beyond scratch, caller runs the Jacobi) when the
+// fast path does not apply.  Uniform in the workgroup.
+__device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
+  extern __shared__ double2 xbuf[];
+  __shared__ double s_d[128], s_e[128], s_e2[128], s_lam[kGramMaxK], s_sig2[kGramMaxK];
+  __shared__ cplx s_tau[128];
+  __shared__ double s_lo, s_hi, s_tn;
+  __shared__ double2 s_de[128];
+  const int chl = j.dims[0], chr = j.dims[2];
+  const int M = 2 * chl, N = 2 * chr;
+  const bool tr = M < N;
+  const int L = tr ? N : M, C = tr ? M : N;
+  int K = C;
+  if (j.max_chi > 0 && j.max_chi < K) K = j.max_chi;
+  // (j.work must hold the 128 x 128 Gram matrix: capacity 64)
+  if (K > kGramMaxK || C < 4 || C > 128 || L > 128 || j.cap < 64) return false;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const cplx* th = j.theta;
+  cplx* Gbuf = j.work;  // 128 x 128, row stride 128
+  unsigned long long t_last = tid == 0 ? __builtin_amdgcn_s_memtime() : 0ull;
+  auto tick = [&](int ph) {
+    if (tid == 0) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      atomicAdd(&g_gram_ticks[ph], t - t_last);
+      t_last = t;
+    }
+  };
+  // ---- S1: G = X^H X (four 256-thread sub-groups, one 64 x 64 block each) ----
+  {
+    aqc::GemmLds* lds = reinterpret_cast<aqc::GemmLds*>(xbuf);
+    const int sg = tid >> 8, lt = tid & 255;
+    const int bi = (sg >> 1) * 64, bj = (sg & 1) * 64;
+    const bool act = bi < C && bj < C;
+    const int mb = act ? min(64, C - bi) : 64, nb = act ? min(64, C - bj) : 64;
+    auto store = [&](int i, int jj, cplx v) { Gbuf[(size_t)(bi + i) * 128 + bj + jj] = v; };
+    if (!tr) {  // X[k][c] = theta[c * M + k]
+      aqc::block_cgemm<true, true, false>(
+          mb, nb, L, [&](int i, int k) { return aqc::cconj(th[(size_t)(bi + i) * M + k]); },
+          [&](int k, int jj) { return th[(size_t)(bj + jj) * M + k]; }, store, lds[sg], lt, act);
+    } else {  // X[k][c] = conj(theta[k * M + c])
+      aqc::block_cgemm<false, false, false>(
+          mb, nb, L, [&](int i, int k) { return th[(size_t)k * M + bi + i]; },
+          [&](int k, int jj) { return aqc::cconj(th[(size_t)k * M + bj + jj]); }, store, lds[sg], lt, act);
+    }
+  }
+  __syncthreads();
+  tick(0);
+  // ---- S2: G into registers ----
+  const int r0 = tid >> 3, q0 = tid & 7;
+  const int r = r0, q = q0;
+  cplx g[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int c = q + 8 * i;
+    g[i] = (r < C && c < C) ? Gbuf[(size_t)r * 128 + c] : aqc::cmk(0, 0);
+  }
+  __syncthreads();  // every G load is done before the reflectors overwrite the buffer
+  // ---- S3: tridiagonalisation (zhetd2, lower) ----
+  cplx* xv = xbuf;                               // [2][128]  column k below the diagonal
+  cplx* pv = xbuf + 256;                         // [2][128]  p = tau G v
+  double* npart = reinterpret_cast<double*>(xbuf + 512);  // [2][16]
+  cplx* kpart = xbuf + 528;                      // [2][16]
+  cplx* hh = j.work;                             // reflector k at hh[k (2C - k - 1) / 2 + (row - k - 1)]
+  for (int k = 0; k < C - 1; ++k) {
+    const int b = k & 1;
+    const int ik = k >> 3, qk = k & 7;
+    // q and r laundered through an empty asm each step: otherwise the compiler hoists the 16
+    // columns' loop-invariant index / address values out of the k loop and spills them
+    int q = q0, r = r0;
+    asm volatile("" : "+v"(q), "+v"(r));
+    // waves whose rows are all <= k and column blocks with all columns <= k sit the step out
+    // (uniform branches): the trailing block shrinks, so the work is a third of the full sweep
+    const bool wact = wave * 8 + 7 > k;
+    cplx x = aqc::cmk(0, 0);
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      if (i == ik) x = g[i];
+    double nrm = 0.0;
+    if (q == qk && r > k && r < C) {
+      xv[b * 128 + r] = x;
+      if (r >= k + 2) nrm = aqc::cnorm2(x);
+    }
+    if (q == qk && r == k) s_d[k] = x.x;
+    if (wact) nrm = wave_sum_dpp(nrm);
+    if (lane == 0) npart[b * 16 + wave] = nrm;
+    __syncthreads();
+    tick(6);
+    // reflector scalars, redundantly in every thread (zlarfg)
+    double xn2 = 0.0;
+#pragma unroll
+    for (int w = 0; w < 16; ++w) xn2 += npart[b * 16 + w];
+    const cplx alpha = xv[b * 128 + k + 1];
+    double beta;
+    cplx tau, scl;
+    if (xn2 == 0.0 && alpha.y == 0.0) {
+      beta = alpha.x;
+      tau = aqc::cmk(0, 0);
+      scl = aqc::cmk(0, 0);
+    } else {
+      const double nn = sqrt(fma(alpha.x, alpha.x, fma(alpha.y, alpha.y, xn2)));
+      beta = alpha.x >= 0.0 ? -nn : nn;
+      tau = aqc::cmk((beta - alpha.x) / beta, -alpha.y / beta);
+      const double dr = alpha.x - beta, di = alpha.y, id2 = 1.0 / fma(dr, dr, di * di);
+      scl = aqc::cmk(dr * id2, -di * id2);  // 1 / (alpha - beta)
+    }
+    // v_c, branch-free: 1 at k + 1, x_c / (alpha - beta) below it, 0 at and above the diagonal
+    // (stale LDS entries are read and masked, never branched around)
+    auto vcol = [&](int c) {
+      const cplx xs = aqc::cmul(xv[b * 128 + (c & 127)], scl);
+      const bool below = c > k + 1 && c < C;
+      cplx v = aqc::cmk(below ? xs.x : 0.0, below ? xs.y : 0.0);
+      if (c == k + 1) v = aqc::cmk(1, 0);
+      return v;
+    };
+    const bool rowact = r > k && r < C;
+    const cplx vr = vcol(r);
+    cplx kp = aqc::cmk(0, 0);
+    if (wact) {
+      cplx acc = aqc::cmk(0, 0);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        if (8 * i + 7 > k) acc = aqc::cfma(g[i], vcol(q + 8 * i), acc);  // uniform skip; v_c = 0 for c <= k
+        if ((i & 3) == 3) asm volatile("" ::: "memory");  // keep the LDS reads in groups of 4
+      }
+      acc.x = aqc::row_sum8(acc.x);
+      acc.y = aqc::row_sum8(acc.y);
+      const cplx p = aqc::cmul(tau, acc);
+      if (q == 0 && rowact) {
+        pv[b * 128 + r] = p;
+        hh[(size_t)k * (2 * C - k - 1) / 2 + (r - k - 1)] = vr;
+      }
+      const cplx kk = aqc::cmul(aqc::cconj(p), vr);
+      kp.x = wave_sum_dpp(q == 0 && rowact ? kk.x : 0.0);
+      kp.y = wave_sum_dpp(q == 0 && rowact ? kk.y : 0.0);
+    }
+    if (lane == 0) kpart[b * 16 + wave] = kp;
+    if (tid == 0) {
+      s_tau[k] = tau;
+      s_e[k] = beta;
+    }
+    __syncthreads();
+    tick(7);
+    if (wact) {
+      cplx kt = aqc::cmk(0, 0);
+#pragma unroll
+      for (int w = 0; w < 16; ++w) kt = aqc::cadd(kt, kpart[b * 16 + w]);
+      const cplx a2 = aqc::cscale(aqc::cmul(tau, kt), -0.5);
+      // w_r (0 for rows at or above k: vr = 0 there too), so rows <= k get a zero update
+      const cplx wr0 = aqc::cfma(a2, vr, pv[b * 128 + r]);
+      const cplx wr = aqc::cmk(rowact ? wr0.x : 0.0, rowact ? wr0.y : 0.0);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        if (8 * i + 7 > k) {  // uniform
+          const int c = q + 8 * i;
+          const cplx vc = vcol(c);
+          const cplx wc0 = aqc::cfma(a2, vc, pv[b * 128 + c]);
+          const bool colact = c > k && c < C;
+          const cplx wc = aqc::cmk(colact ? wc0.x : 0.0, colact ? wc0.y : 0.0);
+          // g -= v_r conj(w_c) + w_r conj(v_c)  (zero outside the trailing block)
+          g[i] = aqc::csub(g[i], aqc::cadd(aqc::cmulc(vr, wc), aqc::cmulc(wr, vc)));
+        }
+        if ((i & 1) == 1) asm volatile("" ::: "memory");  // LDS reads in groups of 2: no spills
+      }
+    }
+  }
+  {
+    const int il = (C - 1) >> 3, ql = (C - 1) & 7;
+    cplx x = aqc::cmk(0, 0);
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      if (i == il) x = g[i];
+    if (q == ql && r == C - 1) s_d[C - 1] = x.x;
+  }
+  __syncthreads();
+  tick(1);
+  // ---- S4: top-K eigenvalues of T by 17-section ----
+  if (tid == 0) {
+    double lo = 1e300, hi = -1e300, tn = 0.0, e2m = 0.0;
+    for (int i = 0; i < C; ++i) {
+      const double el = i > 0 ? fabs(s_e[i - 1]) : 0.0, er = i < C - 1 ? fabs(s_e[i]) : 0.0;
+      lo = fmin(lo, s_d[i] - el - er);
+      hi = fmax(hi, s_d[i] + el + er);
+      tn = fmax(tn, fabs(s_d[i]) + el + er);
+      if (i < C - 1) {
+        s_e2[i] = s_e[i] * s_e[i];
+        e2m = fmax(e2m, s_e2[i]);
+      }
+    }
+    for (int i = 0; i < C; ++i) s_de[i] = make_double2(s_d[i], i > 0 ? s_e2[i - 1] : 0.0);
+    const double span = fmax(hi - lo, 1e-300);
+    s_lo = lo - 1e-12 * span;
+    s_hi = hi + 1e-12 * span;
+    s_tn = tn;
+  }
+  __syncthreads();
+  {
+    const int eid = tid >> 4, sub = tid & 15;
+    const int a = C - 1 - eid;  // ascending index of the eid-th largest eigenvalue
+    const double pivmin = 1e-290;
+    double lo = s_lo, hi = s_hi;
+    for (int round = 0; round < 8; ++round) {
+      const double x = lo + (hi - lo) * (double)(sub + 1) * (1.0 / 17.0);
+      double qv = s_de[0].x - x;
+      if (fabs(qv) < pivmin) qv = -pivmin;
+      int cnt = qv < 0.0;
+#pragma unroll 4
+      for (int i = 1; i < C; ++i) {
+        const double2 de = s_de[i];  // (d_i, e_{i-1}^2)
+        qv = (de.x - x) - de.y * rcp_nr1(qv);
+        if (fabs(qv) < pivmin) qv = -pivmin;
+        cnt += qv < 0.0;
+      }
+      const unsigned long long bal = __ballot(cnt >= a + 1);
+      const unsigned int gm = (unsigned int)(bal >> (lane & ~15)) & 0xFFFFu;
+      const int f = gm ? __builtin_ctz(gm) : 16;
+      const double nhi = f < 16 ? lo + (hi - lo) * (double)(f + 1) * (1.0 / 17.0) : hi;
+      const double nlo = f > 0 ? lo + (hi - lo) * (double)f * (1.0 / 17.0) : lo;
+      lo = nlo;
+      hi = nhi;
+    }
+    if (eid < K && sub == 0) s_lam[eid] = 0.5 * (lo + hi);
+  }
+  __syncthreads();
+  tick(2);
+  if (!(s_lam[0] > 0.0) || !(s_lam[K - 1] > kGramRelFloor * s_lam[0])) return false;  // uniform
+  // ---- S5: inverse iteration, Gram-Schmidt in clusters, Rayleigh quotients ----
+  double* zb = reinterpret_cast<double*>(xbuf);  // zb[row * 64 + i]
+  double* Db = zb + 128 * 64;                    // 1 / D_row of vector i at Db[row * 64 + i]
+  if (tid < K) {
+    const int i = tid;
+    const double lam = s_lam[i];
+    const double piv = 2.220446049250313e-16 * s_tn;
+    for (int row = 0; row < C; ++row) {  // deterministic start vector, in [-1, 1)
+      unsigned int h = (unsigned int)(row * 2654435761u) ^ (unsigned int)((i + 1) * 40503u);
+      h ^= h >> 13;
+      h *= 0x5bd1e995u;
+      h ^= h >> 15;
+      zb[row * 64 + i] = (double)(h & 0xFFFFFu) * (2.0 / 1048576.0) - 1.0;
+    }
+    for (int it = 0; it < 3; ++it) {
+      // L D L^T = T - lam I (no pivoting; tiny pivots -> +-eps ||T||); forward solve in place
+      double rdp = 0.0, yp = 0.0;
+      for (int row = 0; row < C; ++row) {
+        double dj = s_d[row] - lam;
+        double y = zb[row * 64 + i];
+        if (row > 0) {
+          dj -= s_e2[row - 1] * rdp;
+          y -= s_e[row - 1] * rdp * yp;
+        }
+        if (fabs(dj) < piv) dj = dj >= 0.0 ? piv : -piv;
+        const double rd = rcp_nr(dj);
+        zb[row * 64 + i] = y;
+        Db[row * 64 + i] = rd;
+        rdp = rd;
+        yp = y;
+      }
+      double zn = zb[(C - 1) * 64 + i] * Db[(C - 1) * 64 + i];
+      zb[(C - 1) * 64 + i] = zn;
+      double n2 = zn * zn;
+      for (int row = C - 2; row >= 0; --row) {
+        zn = (zb[row * 64 + i] - s_e[row] * zn) * Db[row * 64 + i];
+        zb[row * 64 + i] = zn;
+        n2 = fma(zn, zn, n2);
+      }
+      const double sc = __builtin_amdgcn_rsq(n2);
+      const double scn = sc * fma(-0.5 * n2 * sc, sc, 1.5);
+      for (int row = 0; row < C; ++row) zb[row * 64 + i] *= scn;
+    }
+  }
+  __syncthreads();
+  if (wave == 0) {  // Gram-Schmidt inside clusters (uniform loop over wave 0)
+    // clusters: gaps below 1e-7 ||T|| (dstein's 1e-3 is far more conservative than three
+    // inverse-iteration steps need: at gaps above ~1e-10 the vectors come out orthogonal to
+    // 1e-14 on their own, tools/gram_svd_proto.py)
+    const double ortol = 1e-7 * s_tn;
+    int start = 0;
+    for (int i = 1; i < K; ++i) {
+      if (s_lam[i - 1] - s_lam[i] >= ortol) {
+        start = i;
+        continue;
+      }
+      for (int jj = start; jj < i; ++jj) {
+        double dp = 0.0;
+        for (int row = lane; row < C; row += 64) dp = fma(zb[row * 64 + i], zb[row * 64 + jj], dp);
+        dp = wave_sum_d(dp);
+        for (int row = lane; row < C; row += 64) zb[row * 64 + i] = fma(-dp, zb[row * 64 + jj], zb[row * 64 + i]);
+      }
+      double n2 = 0.0;
+      for (int row = lane; row < C; row += 64) n2 = fma(zb[row * 64 + i], zb[row * 64 + i], n2);
+      n2 = wave_sum_d(n2);
+      const double sc = 1.0 / sqrt(n2);
+      for (int row = lane; row < C; row += 64) zb[row * 64 + i] *= sc;
+    }
+  }
+  __syncthreads();
+  if (tid < K) {
+    const int i = tid;
+    double s2 = 0.0;
+    for (int row = 0; row < C; ++row) {
+      const double z = zb[row * 64 + i];
+      s2 = fma(s_d[row] * z, z, s2);
+      if (row < C - 1) s2 = fma(2.0 * s_e[row] * z, zb[(row + 1) * 64 + i], s2);
+    }
+    s_sig2[i] = s2 > 0.0 ? s2 : 0.0;
+  }
+  __syncthreads();
+  tick(3);
+  // ---- S6: V = Q Z (rows (t >> 6) + 16 m, column t & 63) ----
+  const int jc = lane, rb = wave;
+  cplx V[8];
+#pragma unroll
+  for (int m = 0; m < 8; ++m) {
+    const int row = rb + 16 * m;
+    V[m] = aqc::cmk((jc < K && row < C) ? zb[row * 64 + jc] : 0.0, 0.0);
+  }
+  __syncthreads();  // zb / Db are dead from here: the partial sums reuse the LDS
+  cplx* sp = xbuf + 4096;  // [2][16][64]
+  cplx vn[8];  // the next reflector's entries for this thread's rows (prefetched a step ahead)
+  auto load_v = [&](int k, cplx (&dst)[8]) {
+    const cplx* v = hh + (size_t)k * (2 * C - k - 1) / 2;
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      const int row = rb + 16 * m;
+      dst[m] = (row > k && row < C) ? v[row - k - 1] : aqc::cmk(0, 0);
+    }
+  };
+  if (C >= 2) load_v(C - 2, vn);
+  for (int k = C - 2; k >= 0; --k) {
+    const int b = k & 1;
+    const cplx tk = s_tau[k];
+    cplx vr[8];
+#pragma unroll
+    for (int m = 0; m < 8; ++m) vr[m] = vn[m];
+    if (k > 0) load_v(k - 1, vn);
+    cplx part = aqc::cmk(0, 0);
+#pragma unroll
+    for (int m = 0; m < 8; ++m) part = aqc::cfmac(vr[m], V[m], part);  // conj(v) . V
+    sp[(b * 16 + wave) * 64 + jc] = part;
+    __syncthreads();
+    cplx s = aqc::cmk(0, 0);
+#pragma unroll
+    for (int w = 0; w < 16; ++w) s = aqc::cadd(s, sp[(b * 16 + w) * 64 + jc]);
+    const cplx ts = aqc::cmul(tk, s);
+#pragma unroll
+    for (int m = 0; m < 8; ++m) V[m] = aqc::csub(V[m], aqc::cmul(vr[m], ts));
+  }
+  __syncthreads();  // the reflectors are dead: W overwrites them
+  tick(4);
+  if (jc < K) {
+    const double sg = sqrt(s_sig2[jc]);
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      const int row = rb + 16 * m;
+      if (row < C) j.work[(size_t)jc * C + row] = aqc::cscale(V[m], sg);
+    }
+  }
+  for (int c = tid; c < C; c += 1024) j.sig[c] = c < K ? sqrt(s_sig2[c]) : 0.0;
+  if (tid == 0) atomicMax(&j.flags[2], 1);
+  tick(5);
+  return true;
+}
+
+__global__ __launch_bounds__(1024) void k_svd_gram(const TwoSiteJob* __restrict__ jobs) {
+  const TwoSiteJob& j = jobs[blockIdx.x];
+  if (!j.gram || !gram_svd_body(j)) {
+    __syncthreads();
+    jacobi_reg_body<128, 8, 16>(j);
+  }
+}

@@ -110,6 +110,14 @@ int aqc_mps_set_jacobi_tol(double factor);
    decomposition ends (default 1e-6: the off-diagonal left is O(1e-12) relative; tiny_t <= 0
    restores it; must be < 1e-3). */
 int aqc_mps_set_jacobi_stop(double tiny_t);
+/* Two-site SVD at 2 chi = 128: gram = 1 (default) tries the Gram / tridiagonal path first (G = X^H X
+   on the matrix cores, Householder tridiagonalisation, multisection, inverse iteration; taken when
+   the kept count K = min(2 chi, max_chi) <= 64 and lambda_K > 1e-9 lambda_1, else the register
+   Jacobi runs), gram = 0 the register Jacobi only.  debug_max_chi: max_chi of aqc_svd_debug. */
+int aqc_mps_set_svd_path(int gram, int debug_max_chi);
+/* Diagnostics: shader-clock ticks of the Gram path's phases (Gram GEMM, tridiagonalisation,
+   eigenvalues, eigenvectors, back-transformation, output) since the last call (then reset); out[8]. */
+int aqc_svd_gram_ticks(double* out);
 /* Sweep stop of the FP32 preconditioning stage of the mixed-precision two-site SVD (default 1e-3). */
 int aqc_mps_set_jacobi32_stop(double tiny_t);
 /* Jacobi kernel: 2 = register-resident columns with pivoted-QR preconditioning for
@@ -145,7 +153,8 @@ int aqc_entanglement_measures(const double* rdms, int count, int method, double*
 
 /* Diagnostics: one register-resident Jacobi launch (variant 2 / 5 = with pivoted QR, 3 = without)
    on theta (m x n column-major complex, m, n even <= 128, as the two-site update builds it);
-   variant 6 = the FP32 register Jacobi (pivoted QR + sweeps in single precision, 64 < max(m, n)).
+   variant 6 = the FP32 register Jacobi (pivoted QR + sweeps in single precision, 64 < max(m, n)),
+   variant 7 = the Gram / tridiagonal path (Jacobi fallback inside the kernel; same output contract).
    w_out receives min(m,n) columns of length (variant 2 / 5: min(m,n), 3: max(m,n)); sig_out their
    norms; perm_out (optional) the pivot order when stop_after_qr (then w_out holds X = R^H
    unsorted).  stop_after_qr = 2 also writes the QR phase's shader-clock ticks to sig_out[0..3]

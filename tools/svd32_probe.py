@@ -28,6 +28,8 @@ def swap_theta(aer, site=24):
 def main():
     from adaptaqc_amd import _lib
 
+    if os.environ.get("AQC_LIB"):  # experiment builds
+        _lib.load(os.environ["AQC_LIB"])
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 5
     tinies = [float(x) for x in sys.argv[2:]] or [1e-3]
     L = _lib.lib()
@@ -40,19 +42,32 @@ def main():
         w = np.zeros(2 * m * n)
         sig = np.zeros(max(m, n))
         sw = ctypes.c_int()
-        for v, tiny in [(2, None)] + [(6, t) for t in tinies]:
+        for v, tiny in [(2, None), (7, None)] + [(6, t) for t in tinies]:
             if tiny is not None:
                 _lib.check(L.aqc_mps_set_jacobi32_stop(ctypes.c_double(tiny)))
             for _ in range(reps):
                 _lib.check(L.aqc_svd_debug(_lib.ptr(th), m, n, v, 0, _lib.ptr(w), _lib.ptr(sig), None,
                                            ctypes.byref(sw)))
             got = np.sort(sig[:min(m, n)])[::-1]
-            err = np.max(np.abs(got - ref)) / ref[0]
+            kk = 64 if v == 7 else min(m, n)  # the Gram path returns the top 64
+            err = np.max(np.abs(got[:kk] - ref[:kk])) / ref[0]
             # the columns: right singular vectors x sigma (variant 2 / 6 contract); check V^H V
-            W = w.view(np.complex128).reshape(min(m, n), -1)
+            W = w.view(np.complex128).reshape(min(m, n), -1)[: (64 if v == 7 else min(m, n))]
             nn = np.linalg.norm(W, axis=1)
             V = W / nn[:, None]
             orth = np.max(np.abs(V.conj() @ V.T - np.eye(len(V))))
+            if v in (2, 7):  # kept subspace (top 64) against numpy
+                _, _, vh = np.linalg.svd(T)
+                Vt = vh[:64].conj().T
+                idx = np.argsort(-sig[:min(m, n)])[:64]
+                Vk = (w.view(np.complex128).reshape(min(m, n), -1)[idx] / np.sort(sig[:min(m, n)])[::-1][:64, None]).T
+                sub = np.linalg.norm(Vk @ Vk.conj().T - Vt @ Vt.conj().T, 2)
+                print(f"   kept-subspace distance {sub:.2e}")
+            if v == 7:
+                tk = np.zeros(8)
+                _lib.check(L.aqc_svd_gram_ticks(_lib.ptr(tk)))
+                print("   gram phase ticks per call (S1 gram, S3 tridiag [C part], S4 eig, S5 vec, S6 back, out, S3 A, S3 B):",
+                      (tk[:8] / reps).astype(int).tolist())
             print(f"{kind:12s} variant {v} tiny {tiny}: sweeps {sw.value:2d}  max|sigma - ref|/sigma_1 {err:.2e}  "
                   f"max|V^H V - I| {orth:.2e}", flush=True)
 
