@@ -10,7 +10,7 @@
 //       eigenvalue each evaluate one Sturm count, one ballot picks the subinterval (8 rounds)
 //   S5  inverse iteration (unpivoted LDL^T of T - lambda I, three solves) per eigenvector, Gram-
 //       Schmidt inside clusters (gaps below 1e-7 ||T||), sigma^2 = z^T T z
-//   S6  back-transformation V = Q Z (one barrier per reflector), output W = V Sigma
+//   S6  back-transformation V = Q Z (each wave owns four columns: no barriers), output W = V Sigma
 // The output follows the QR-preconditioned register Jacobi's contract (TwoSiteJob::qr = 1): work
 // column c (length C, rows in X's column order) = right singular vector c of X times sigma_c, sig[c]
 // = sigma_c (0 for c >= K), so rank / split are unchanged.
@@ -163,10 +163,17 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
       tau = aqc::cmk(0, 0);
       scl = aqc::cmk(0, 0);
     } else {
-      const double nn = sqrt(fma(alpha.x, alpha.x, fma(alpha.y, alpha.y, xn2)));
+      // rsq / rcp seeds with Newton steps (full precision) instead of the IEEE sqrt / divide
+      // sequences: this chain runs between the step's two barriers
+      const double x2 = fma(alpha.x, alpha.x, fma(alpha.y, alpha.y, xn2));
+      double rs = __builtin_amdgcn_rsq(x2);
+      rs = rs * fma(-0.5 * x2 * rs, rs, 1.5);
+      rs = rs * fma(-0.5 * x2 * rs, rs, 1.5);
+      const double nn = x2 * rs;
       beta = alpha.x >= 0.0 ? -nn : nn;
-      tau = aqc::cmk((beta - alpha.x) / beta, -alpha.y / beta);
-      const double dr = alpha.x - beta, di = alpha.y, id2 = 1.0 / fma(dr, dr, di * di);
+      const double ib = alpha.x >= 0.0 ? -rs : rs;  // 1 / beta
+      tau = aqc::cmk((beta - alpha.x) * ib, -alpha.y * ib);
+      const double dr = alpha.x - beta, di = alpha.y, id2 = rcp_nr(fma(dr, dr, di * di));
       scl = aqc::cmk(dr * id2, -di * id2);  // 1 / (alpha - beta)
     }
     // v_c, branch-free: 1 at k + 1, x_c / (alpha - beta) below it, 0 at and above the diagonal
@@ -371,44 +378,81 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
   }
   __syncthreads();
   tick(3);
-  // ---- S6: V = Q Z (rows (t >> 6) + 16 m, column t & 63) ----
-  const int jc = lane, rb = wave;
+  // ---- S6: V = Q Z.  Wave w owns columns 4w .. 4w + 3 whole: lane l holds column 4w + (l & 3),
+  // rows (l >> 2) + 16 m (m < 8), so every reflector's dot products reduce inside the wave (DPP
+  // row rotations + two cross-row shuffles) -- no LDS, no barrier, each wave runs on its own ----
+  const int jc = 4 * wave + (lane & 3), rb = lane >> 2;
   cplx V[8];
 #pragma unroll
   for (int m = 0; m < 8; ++m) {
     const int row = rb + 16 * m;
     V[m] = aqc::cmk((jc < K && row < C) ? zb[row * 64 + jc] : 0.0, 0.0);
   }
-  __syncthreads();  // zb / Db are dead from here: the partial sums reuse the LDS
-  cplx* sp = xbuf + 4096;  // [2][16][64]
-  cplx vn[8];  // the next reflector's entries for this thread's rows (prefetched a step ahead)
+  // the packed reflectors (<= 8128 complex = 127 KiB) move into the LDS once: every wave reads
+  // every reflector, and LDS reads are a few hundred cycles closer than L2 ones
+  __syncthreads();  // V's initial values are read from zb: the LDS can be overwritten now
+  const int nhh = (C - 1) * C / 2;
+  cplx* hl = xbuf;
+  for (int e = tid; e < nhh; e += 1024) hl[e] = hh[e];
+  __syncthreads();
   auto load_v = [&](int k, cplx (&dst)[8]) {
-    const cplx* v = hh + (size_t)k * (2 * C - k - 1) / 2;
+    const cplx* v = hl + (size_t)k * (2 * C - k - 1) / 2;
 #pragma unroll
     for (int m = 0; m < 8; ++m) {
       const int row = rb + 16 * m;
       dst[m] = (row > k && row < C) ? v[row - k - 1] : aqc::cmk(0, 0);
     }
   };
-  if (C >= 2) load_v(C - 2, vn);
-  for (int k = C - 2; k >= 0; --k) {
-    const int b = k & 1;
-    const cplx tk = s_tau[k];
-    cplx vr[8];
+  // sum over the 16 lanes sharing (l & 3): rotations by 4 and 8 inside a DPP row, then rows
+  auto col_sum = [&](double v) {
+    v += aqc::dpp_perm<0x124>(v);  // row_ror:4
+    v += aqc::dpp_perm<0x128>(v);  // row_ror:8
+    v += __shfl_xor(v, 16);
+    v += __shfl_xor(v, 32);
+    return v;
+  };
+  if (wave * 4 < K) {  // uniform per wave
+    // Two reflectors per pass (compact WY): with u_1 = v_k, u_2 = v_{k-1} (application order),
+    // s_i = u_i^H V from the pass's V and c = u_2^H u_1,
+    //   s'_1 = s_1,  s'_2 = s_2 - tau_1 c s'_1,  V <- V - tau_1 u_1 s'_1 - tau_2 u_2 s'_2,
+    // so the three reductions of a pass run side by side (four reflectors per pass spill: the
+    // 32 complex of u need more than the 128 VGPRs a 1024-thread workgroup allows).
+    int k = C - 2;
+    for (; k >= 1; k -= 2) {
+      cplx u1[8], u2[8];
+      load_v(k, u1);
+      load_v(k - 1, u2);
+      cplx s1 = aqc::cmk(0, 0), s2 = aqc::cmk(0, 0), c21 = aqc::cmk(0, 0);
 #pragma unroll
-    for (int m = 0; m < 8; ++m) vr[m] = vn[m];
-    if (k > 0) load_v(k - 1, vn);
-    cplx part = aqc::cmk(0, 0);
+      for (int m = 0; m < 8; ++m) {
+        s1 = aqc::cfmac(u1[m], V[m], s1);
+        s2 = aqc::cfmac(u2[m], V[m], s2);
+        c21 = aqc::cfmac(u2[m], u1[m], c21);
+      }
+      s1.x = col_sum(s1.x);
+      s1.y = col_sum(s1.y);
+      s2.x = col_sum(s2.x);
+      s2.y = col_sum(s2.y);
+      c21.x = col_sum(c21.x);
+      c21.y = col_sum(c21.y);
+      const cplx t1 = aqc::cmul(s_tau[k], s1);
+      const cplx t2 = aqc::cmul(s_tau[k - 1], aqc::csub(s2, aqc::cmul(c21, t1)));
 #pragma unroll
-    for (int m = 0; m < 8; ++m) part = aqc::cfmac(vr[m], V[m], part);  // conj(v) . V
-    sp[(b * 16 + wave) * 64 + jc] = part;
-    __syncthreads();
-    cplx s = aqc::cmk(0, 0);
+      for (int m = 0; m < 8; ++m) V[m] = aqc::csub(V[m], aqc::cfma(u2[m], t2, aqc::cmul(u1[m], t1)));
+    }
+    for (; k >= 0; --k) {  // the last reflector of an odd count
+      const cplx tk = s_tau[k];
+      cplx vr[8];
+      load_v(k, vr);
+      cplx part = aqc::cmk(0, 0);
 #pragma unroll
-    for (int w = 0; w < 16; ++w) s = aqc::cadd(s, sp[(b * 16 + w) * 64 + jc]);
-    const cplx ts = aqc::cmul(tk, s);
+      for (int m = 0; m < 8; ++m) part = aqc::cfmac(vr[m], V[m], part);  // conj(v) . V
+      part.x = col_sum(part.x);
+      part.y = col_sum(part.y);
+      const cplx ts = aqc::cmul(tk, part);
 #pragma unroll
-    for (int m = 0; m < 8; ++m) V[m] = aqc::csub(V[m], aqc::cmul(vr[m], ts));
+      for (int m = 0; m < 8; ++m) V[m] = aqc::csub(V[m], aqc::cmul(vr[m], ts));
+    }
   }
   __syncthreads();  // the reflectors are dead: W overwrites them
   tick(4);
