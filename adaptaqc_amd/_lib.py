@@ -10,7 +10,8 @@ import threading
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libaqchip.so")
+# AQC_LIB names an alternative build (experiment libraries built in-tree next to this one)
+LIB_PATH = os.environ.get("AQC_LIB") or os.path.join(_HERE, "libaqchip.so")
 
 OP_DTYPE = np.dtype(
     [("nq", "<i4"), ("q0", "<i4"), ("q1", "<i4"), ("flags", "<i4"), ("m", "<f8", (32,))], align=True

@@ -162,4 +162,77 @@ __device__ __forceinline__ void block_cgemm(int m, int n, int k, FA a, FB b, FS 
   }
 }
 
+// One 64 x 64 output block (rows bi.., cols bj..) of block_cgemm's product left in the wave's
+// accumulators: cr / ci[r][c][q] hold C[bi + wr + 16 r + lk + 4 q][bj + wc + 16 c + li] (the
+// Gram SVD moves them through the LDS itself).  block_cgemm keeps its own copy of the loop: built
+// on this function, the chain's split spilled 160 VGPRs.
+template <bool A_KFAST = false, bool B_KFAST = false, bool PREFETCH = false, typename FA, typename FB>
+__device__ __forceinline__ void block_cgemm_tile(int m, int n, int k, int bi, int bj, FA a, FB b, GemmLds& lds,
+                                                 int tid, bool active, d4_t (&cr)[2][2], d4_t (&ci)[2][2]) {
+  const int wave = tid >> 6, lane = tid & 63;
+  const int wr = (wave >> 1) * 32, wc = (wave & 1) * 32;
+  const int li = lane & 15, lk = lane >> 4;
+#pragma unroll
+  for (int r = 0; r < 2; ++r)
+#pragma unroll
+    for (int c = 0; c < 2; ++c) cr[r][c] = d4_t{0, 0, 0, 0}, ci[r][c] = d4_t{0, 0, 0, 0};
+  cplx pa[PREFETCH ? 4 : 1], pb[PREFETCH ? 4 : 1];
+  auto fetch = [&](int k0) {
+#pragma unroll
+    for (int q = 0; q < (PREFETCH ? 4 : 0); ++q) {
+      const int e = tid + q * kGemmThreads;
+      const int ka = A_KFAST ? (e & 15) : (e >> 6), ia = A_KFAST ? (e >> 4) : (e & 63);
+      const int kb = B_KFAST ? (e & 15) : (e >> 6), ib = B_KFAST ? (e >> 4) : (e & 63);
+      pa[q] = (bi + ia < m && k0 + ka < k) ? a(bi + ia, k0 + ka) : cmk(0, 0);
+      pb[q] = (bj + ib < n && k0 + kb < k) ? b(k0 + kb, bj + ib) : cmk(0, 0);
+    }
+  };
+  if constexpr (PREFETCH) {
+    if (active) fetch(0);
+  }
+  for (int k0 = 0; k0 < k; k0 += 16) {
+    if (active) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int e = tid + q * kGemmThreads;
+        const int ka = A_KFAST ? (e & 15) : (e >> 6), ia = A_KFAST ? (e >> 4) : (e & 63);
+        const int kb = B_KFAST ? (e & 15) : (e >> 6), ib = B_KFAST ? (e >> 4) : (e & 63);
+        if constexpr (PREFETCH) {
+          lds.As[ka][ia] = pa[q];
+          lds.Bs[kb][ib] = pb[q];
+        } else {
+          lds.As[ka][ia] = (bi + ia < m && k0 + ka < k) ? a(bi + ia, k0 + ka) : cmk(0, 0);
+          lds.Bs[kb][ib] = (bj + ib < n && k0 + kb < k) ? b(k0 + kb, bj + ib) : cmk(0, 0);
+        }
+      }
+    }
+    __syncthreads();
+    if constexpr (PREFETCH) {
+      if (active && k0 + 16 < k) fetch(k0 + 16);
+    }
+    if (active) {
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const int kk = 4 * ks + lk;
+        cplx av[2], bv[2];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          av[t] = lds.As[kk][wr + 16 * t + li];
+          bv[t] = lds.Bs[kk][wc + 16 * t + li];
+        }
+#pragma unroll
+        for (int r = 0; r < 2; ++r)
+#pragma unroll
+          for (int c = 0; c < 2; ++c) {
+            cr[r][c] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[r].x, bv[c].x, cr[r][c], 0, 0, 0);
+            cr[r][c] = __builtin_amdgcn_mfma_f64_16x16x4f64(-av[r].y, bv[c].y, cr[r][c], 0, 0, 0);
+            ci[r][c] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[r].x, bv[c].y, ci[r][c], 0, 0, 0);
+            ci[r][c] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[r].y, bv[c].x, ci[r][c], 0, 0, 0);
+          }
+      }
+    }
+    __syncthreads();
+  }
+}
+
 }  // namespace aqc

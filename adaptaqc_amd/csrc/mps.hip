@@ -37,6 +37,14 @@ hipStream_t mps_stream() {
 
 namespace {
 
+// threadIdx.x read through an empty asm: values a phase derives from it cannot be hoisted out of
+// the chain loop in k_chain (where they would stay live across every other phase)
+__device__ __forceinline__ int fresh_tid() {
+  int t = threadIdx.x;
+  asm volatile("" : "+v"(t));
+  return t;
+}
+
 constexpr int kT = 256;
 constexpr double kChop = 1e-16;
 constexpr int kMaxSweeps = 60;
@@ -164,7 +172,7 @@ __device__ __forceinline__ int rr_elem(int pos, int r, int c) {
 template <int LPP, int MAXR, int JT, typename PairFn>
 __device__ __forceinline__ void jacobi_round(cplx* panel, int ld, int L, int npairs, double tol, double floor2,
                                              PairFn pair_of, int* rot_count) {
-  const int tid = threadIdx.x;
+  const int tid = fresh_tid();
   const int grp = tid / LPP, lane = tid % LPP;
   constexpr int kGroups = JT / LPP;
   for (int pbase = 0; pbase < npairs; pbase += kGroups) {
@@ -242,7 +250,7 @@ __global__ __launch_bounds__(JT) void k_jacobi(const TwoSiteJob* __restrict__ jo
   const bool tr = M < N;
   const int L = tr ? N : M;
   const int C = tr ? M : N;
-  const int tid = threadIdx.x;
+  const int tid = fresh_tid();
   cplx* W = j.work;
   // W <- theta (or theta^H), column-major with ld = L; squared Frobenius norm on the way
   double f = 0.0;
@@ -466,7 +474,7 @@ __device__ __forceinline__ void jacobi_reg_body(const TwoSiteJob& j) {
   const int L = tr ? N : M;
   const int C = tr ? M : N;
   const bool use_qr = j.qr != 0;
-  const int tid = threadIdx.x;
+  const int tid = fresh_tid();
   const int g = tid / LPG, lane = tid % LPG;
   // plain doubles (real / imaginary planes) so the arrays stay in VGPRs
   double sr[MAXR], si[MAXR], mr[MAXR], mi[MAXR];
@@ -889,7 +897,7 @@ __device__ __forceinline__ void rank_body(const TwoSiteJob& j) {
   const int C = M < N ? M : N;
   int P = 1;
   while (P < C) P <<= 1;
-  const int tid = threadIdx.x;
+  const int tid = fresh_tid();
   for (int i = tid; i < P; i += NT) {
     sv[i] = i < C ? j.sig[i] : -1.0;
     si[i] = i;
@@ -1086,9 +1094,9 @@ __device__ unsigned long long g_chain_ticks[5];
 // sg, sg + 4, ...; every sub-group runs the same number of tiles and k steps so that the barriers
 // pair up.  (An MFMA form on aqc::block_cgemm needs more than the chain's 128 VGPRs per lane and
 // spilled inside its k loop: 118 us per update.)
-__device__ __noinline__ void chain_theta(const TwoSiteJob& j) {
+__device__ __forceinline__ void chain_theta(const TwoSiteJob& j) {
   extern __shared__ double2 xbuf[];
-  const int tid = threadIdx.x, sg = tid >> 8, lt = tid & 255;
+  const int tid = fresh_tid(), sg = tid >> 8, lt = tid & 255;
   cplx (*As)[16][17] = reinterpret_cast<cplx (*)[16][17]>(xbuf + sg * (4 * 16 * 17));
   cplx (*Bs)[16][17] = As + 2;
   const int chl = j.dims[0], chm = j.dims[1], chr = j.dims[2];
@@ -1143,17 +1151,20 @@ __device__ __noinline__ void chain_theta(const TwoSiteJob& j) {
     }
   }
 }
-__device__ __noinline__ void chain_jacobi(const TwoSiteJob& j) {
+// the register Jacobi is the chain's fallback (Gram path off or refused): a real call, so that
+// its register allocation stays out of k_chain's
+__device__ __noinline__ void chain_jacobi_fallback(const TwoSiteJob& j) { jacobi_reg_body<128, 8, 16>(j); }
+__device__ __forceinline__ void chain_jacobi(const TwoSiteJob& j) {
   if (j.gram) {
     if (gram_svd_body(j)) return;
     __syncthreads();
   }
-  jacobi_reg_body<128, 8, 16>(j);
+  chain_jacobi_fallback(j);
 }
-__device__ __noinline__ void chain_rank(const TwoSiteJob& j) { rank_body<1024>(j); }
-__device__ __noinline__ void chain_split(const TwoSiteJob& j) {
+__device__ __forceinline__ void chain_rank(const TwoSiteJob& j) { rank_body<1024>(j); }
+__device__ __forceinline__ void chain_split(const TwoSiteJob& j) {
   extern __shared__ double2 xbuf[];
-  const int tid = threadIdx.x;
+  const int tid = fresh_tid();
   split_copy_body(j, tid, 1024);
   split_gemm_body<false>(j, tid >> 8, reinterpret_cast<aqc::GemmLds*>(xbuf)[tid >> 8], tid & 255);
 }
@@ -1161,7 +1172,7 @@ __device__ __noinline__ void chain_split(const TwoSiteJob& j) {
 __global__ __launch_bounds__(1024) void k_chain(const ChainJob* __restrict__ chains, const TwoSiteJob* __restrict__ two,
                                                 const OneSiteJob* __restrict__ one) {
   const ChainJob& c = chains[blockIdx.x];
-  const int tid = threadIdx.x;
+  const int tid = fresh_tid();
   // shader-clock ticks of the phases (thread 0 of each workgroup; aqc_mps_chain_ticks), kept in
   // LDS so that no VGPR stays live across the phases
   __shared__ unsigned long long tk[6];  // 5 phase totals, last tick
@@ -1227,7 +1238,7 @@ __global__ __launch_bounds__(kT) void k_overlap_zero(const MeasJob* __restrict__
   const MeasJob& j = jobs[blockIdx.x];
   __shared__ cplx v[2][256];
   __shared__ cplx part[4][256];
-  const int tid = threadIdx.x;
+  const int tid = fresh_tid();
   if (tid == 0) v[0][0] = aqc::cmk(1.0, 0.0);
   __syncthreads();
   int cur = 0;
@@ -1254,7 +1265,7 @@ __global__ __launch_bounds__(kT) void k_overlap_zero(const MeasJob* __restrict__
 // blockIdx.y = 0 -> left chain, 1 -> right chain.
 __global__ __launch_bounds__(kT) void k_zero_chains(const MeasJob* __restrict__ jobs) {
   const MeasJob& j = jobs[blockIdx.x];
-  const int tid = threadIdx.x;
+  const int tid = fresh_tid();
   const int cap = j.cap, n = j.n;
   cplx* L = j.vec;
   cplx* R = j.vec + (size_t)(n + 1) * cap;
@@ -1335,7 +1346,7 @@ struct EnvJob {
 
 __global__ __launch_bounds__(kT) void k_env(const EnvJob* __restrict__ jobs) {
   const EnvJob& j = jobs[blockIdx.x];
-  const int tid = threadIdx.x;
+  const int tid = fresh_tid();
   const int cap = j.cap, n = j.n;
   const size_t cc = (size_t)cap * cap;
   auto envp = [&](int b) -> cplx* { return j.keep_all ? j.env + (size_t)b * cc : j.env + (size_t)(b & 1) * cc; };

@@ -78,11 +78,10 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
   const int L = tr ? N : M, C = tr ? M : N;
   int K = C;
   if (j.max_chi > 0 && j.max_chi < K) K = j.max_chi;
-  // (j.work must hold the 128 x 128 Gram matrix: capacity 64)
+  // (j.work holds the packed reflectors, <= 8128 complex: capacity 64)
   if (K > kGramMaxK || C < 4 || C > 128 || L > 128 || j.cap < 64) return false;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = fresh_tid(), lane = tid & 63, wave = tid >> 6;
   const cplx* th = j.theta;
-  cplx* Gbuf = j.work;  // 128 x 128, row stride 128
   unsigned long long t_last = tid == 0 ? __builtin_amdgcn_s_memtime() : 0ull;
   auto tick = [&](int ph) {
     if (tid == 0) {
@@ -91,36 +90,65 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
       t_last = t;
     }
   };
-  // ---- S1: G = X^H X (four 256-thread sub-groups, one 64 x 64 block each) ----
+  // ---- S1: G = X^H X (256-thread sub-groups on the matrix cores, one 64 x 64 block each; G is
+  // Hermitian, so the block below the diagonal is not computed) ----
+  const int r0 = tid >> 3, q0 = tid & 7;
+  const int r = r0, q = q0;
+  cplx g[16];
   {
     aqc::GemmLds* lds = reinterpret_cast<aqc::GemmLds*>(xbuf);
     const int sg = tid >> 8, lt = tid & 255;
     const int bi = (sg >> 1) * 64, bj = (sg & 1) * 64;
-    const bool act = bi < C && bj < C;
-    const int mb = act ? min(64, C - bi) : 64, nb = act ? min(64, C - bj) : 64;
-    auto store = [&](int i, int jj, cplx v) { Gbuf[(size_t)(bi + i) * 128 + bj + jj] = v; };
+    const bool act = bi < C && bj < C && bi <= bj;
+    aqc::d4_t cr[2][2], ci[2][2];
     if (!tr) {  // X[k][c] = theta[c * M + k]
-      aqc::block_cgemm<true, true, false>(
-          mb, nb, L, [&](int i, int k) { return aqc::cconj(th[(size_t)(bi + i) * M + k]); },
-          [&](int k, int jj) { return th[(size_t)(bj + jj) * M + k]; }, store, lds[sg], lt, act);
+      aqc::block_cgemm_tile<true, true, false>(
+          C, C, L, bi, bj, [&](int i, int k) { return aqc::cconj(th[(size_t)i * M + k]); },
+          [&](int k, int jj) { return th[(size_t)jj * M + k]; }, lds[sg], lt, act, cr, ci);
     } else {  // X[k][c] = conj(theta[k * M + c])
-      aqc::block_cgemm<false, false, false>(
-          mb, nb, L, [&](int i, int k) { return th[(size_t)k * M + bi + i]; },
-          [&](int k, int jj) { return aqc::cconj(th[(size_t)k * M + bj + jj]); }, store, lds[sg], lt, act);
+      aqc::block_cgemm_tile<false, false, false>(
+          C, C, L, bi, bj, [&](int i, int k) { return th[(size_t)k * M + i]; },
+          [&](int k, int jj) { return aqc::cconj(th[(size_t)k * M + jj]); }, lds[sg], lt, act, cr, ci);
     }
-  }
-  __syncthreads();
-  tick(0);
-  // ---- S2: G into registers ----
-  const int r0 = tid >> 3, q0 = tid & 7;
-  const int r = r0, q = q0;
-  cplx g[16];
+    // ---- S2: the upper triangle through the LDS (the block barrier at the end of the tile freed
+    // it) into the tridiagonalisation's register layout: thread (r, q) holds row r, columns
+    // q + 8 i.  LDS: block (0, 1) square (row stride 65) then the packed upper triangles of the
+    // diagonal blocks (column-major, entry (a, b), a <= b, at b (b + 1) / 2 + a): 8320 complex ----
+    cplx* gsq = xbuf;
+    cplx* gtri = xbuf + 64 * 65;
+    auto up_index = [](int a, int b) {  // G[a][b], a <= b
+      if (b < 64) return 64 * 65 + b * (b + 1) / 2 + a;
+      if (a >= 64) return 64 * 65 + 2080 + (b - 64) * (b - 63) / 2 + (a - 64);
+      return a * 65 + (b - 64);
+    };
+    (void)gtri;
+    if (act) {
+      const int wv = lt >> 6, ln = lt & 63;
+      const int wr = (wv >> 1) * 32, wc = (wv & 1) * 32, li = ln & 15, lk = ln >> 4;
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int c = q + 8 * i;
-    g[i] = (r < C && c < C) ? Gbuf[(size_t)r * 128 + c] : aqc::cmk(0, 0);
+      for (int rr = 0; rr < 2; ++rr)
+#pragma unroll
+        for (int cc = 0; cc < 2; ++cc)
+#pragma unroll
+          for (int qq = 0; qq < 4; ++qq) {
+            const int a = bi + wr + 16 * rr + lk + 4 * qq, b = bj + wc + 16 * cc + li;
+            if (a <= b) gsq[up_index(a, b)] = aqc::cmk(cr[rr][cc][qq], ci[rr][cc][qq]);
+          }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int c = q + 8 * i;
+      cplx v = aqc::cmk(0, 0);
+      if (r < C && c < C) {
+        v = gsq[c >= r ? up_index(r, c) : up_index(c, r)];
+        if (c < r) v.y = -v.y;
+      }
+      g[i] = v;
+    }
+    __syncthreads();  // the reflectors' scratch reuses the LDS
   }
-  __syncthreads();  // every G load is done before the reflectors overwrite the buffer
+  tick(0);
   // ---- S3: tridiagonalisation (zhetd2, lower) ----
   cplx* xv = xbuf;                               // [2][128]  column k below the diagonal
   cplx* pv = xbuf + 256;                         // [2][128]  p = tau G v
