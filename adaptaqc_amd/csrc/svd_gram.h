@@ -51,6 +51,20 @@ __device__ __forceinline__ double wave_sum_dpp(double v) {
   return s;
 }
 
+// g[i] for a wave-uniform i (a scalar switch, no per-lane selects)
+__device__ __forceinline__ cplx pick16(const cplx (&g)[16], int i) {
+  switch (i) {
+#define AQC_PICK(n) \
+  case n:           \
+    return g[n];
+    AQC_PICK(0) AQC_PICK(1) AQC_PICK(2) AQC_PICK(3) AQC_PICK(4) AQC_PICK(5) AQC_PICK(6) AQC_PICK(7)
+    AQC_PICK(8) AQC_PICK(9) AQC_PICK(10) AQC_PICK(11) AQC_PICK(12) AQC_PICK(13) AQC_PICK(14)
+#undef AQC_PICK
+    default:
+      return g[15];
+  }
+}
+
 __device__ __forceinline__ double rcp_nr1(double x) {  // one Newton step: ~2^-46
   const double r = __builtin_amdgcn_rcp(x);
   return r * fma(-x, r, 2.0);
@@ -87,6 +101,15 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
     if (tid == 0) {
       const unsigned long long t = __builtin_amdgcn_s_memtime();
       atomicAdd(&g_gram_ticks[ph], t - t_last);
+      t_last = t;
+    }
+  };
+  // the tridiagonalisation's two per-step phases add up in registers (one atomic each at the end)
+  unsigned long long t_a = 0, t_b = 0;
+  auto tick_step = [&](unsigned long long& acc) {
+    if (tid == 0) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      acc += t - t_last;
       t_last = t;
     }
   };
@@ -150,14 +173,18 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
   }
   tick(0);
   // ---- S3: tridiagonalisation (zhetd2, lower) ----
-  cplx* xv = xbuf;                               // [2][128]  column k below the diagonal
-  cplx* pv = xbuf + 256;                         // [2][128]  p = tau G v
-  double* npart = reinterpret_cast<double*>(xbuf + 512);  // [2][16]
-  cplx* kpart = xbuf + 528;                      // [2][16]
-  cplx* hh = j.work;                             // reflector k at hh[k (2C - k - 1) / 2 + (row - k - 1)]
+  // LDS (double-buffered by step parity b): xv = column k below the diagonal (0 at and above it),
+  // vb = the reflector v (0 at and above the diagonal, 1 at k + 1), pv = p = tau G v (0 at and
+  // above the diagonal), so the trailing-block update needs no masks
+  cplx* xv = xbuf;                                        // [2][128]
+  cplx* pv = xbuf + 256;                                  // [2][128]
+  cplx* vb = xbuf + 512;                                  // [2][128]
+  double* npart = reinterpret_cast<double*>(xbuf + 768);  // [2][16]
+  cplx* kpart = xbuf + 784;                               // [2][16]
+  cplx* hh = j.work;  // reflector k at hh[k (2C - k - 1) / 2 + (row - k - 1)]
   for (int k = 0; k < C - 1; ++k) {
     const int b = k & 1;
-    const int ik = k >> 3, qk = k & 7;
+    const int ik = k >> 3, qk = k & 7, ik1 = (k + 1) >> 3;
     // q and r laundered through an empty asm each step: otherwise the compiler hoists the 16
     // columns' loop-invariant index / address values out of the k loop and spills them
     int q = q0, r = r0;
@@ -165,20 +192,18 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
     // waves whose rows are all <= k and column blocks with all columns <= k sit the step out
     // (uniform branches): the trailing block shrinks, so the work is a third of the full sweep
     const bool wact = wave * 8 + 7 > k;
-    cplx x = aqc::cmk(0, 0);
-#pragma unroll
-    for (int i = 0; i < 16; ++i)
-      if (i == ik) x = g[i];
+    cplx x = pick16(g, ik);
     double nrm = 0.0;
-    if (q == qk && r > k && r < C) {
-      xv[b * 128 + r] = x;
+    if (q == qk) {
+      const bool below = r > k;
+      xv[b * 128 + r] = aqc::cmk(below ? x.x : 0.0, below ? x.y : 0.0);
       if (r >= k + 2) nrm = aqc::cnorm2(x);
+      if (r == k) s_d[k] = x.x;
     }
-    if (q == qk && r == k) s_d[k] = x.x;
     if (wact) nrm = wave_sum_dpp(nrm);
     if (lane == 0) npart[b * 16 + wave] = nrm;
     __syncthreads();
-    tick(6);
+    tick_step(t_a);
     // reflector scalars, redundantly in every thread (zlarfg)
     double xn2 = 0.0;
 #pragma unroll
@@ -204,35 +229,47 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
       const double dr = alpha.x - beta, di = alpha.y, id2 = rcp_nr(fma(dr, dr, di * di));
       scl = aqc::cmk(dr * id2, -di * id2);  // 1 / (alpha - beta)
     }
-    // v_c, branch-free: 1 at k + 1, x_c / (alpha - beta) below it, 0 at and above the diagonal
-    // (stale LDS entries are read and masked, never branched around)
-    auto vcol = [&](int c) {
-      const cplx xs = aqc::cmul(xv[b * 128 + (c & 127)], scl);
-      const bool below = c > k + 1 && c < C;
-      cplx v = aqc::cmk(below ? xs.x : 0.0, below ? xs.y : 0.0);
-      if (c == k + 1) v = aqc::cmk(1, 0);
-      return v;
-    };
+    // v = scl x' with x' = x except x'_{k+1} = alpha - beta, so G v = scl (G x'): the product
+    // reads the column straight from the LDS and patches the one entry k + 1
     const bool rowact = r > k && r < C;
-    const cplx vr = vcol(r);
+    cplx vr = aqc::cmul(xv[b * 128 + r], scl);
+    if (!(r > k + 1)) vr = aqc::cmk(r == k + 1 ? 1.0 : 0.0, 0.0);
     cplx kp = aqc::cmk(0, 0);
     if (wact) {
       cplx acc = aqc::cmk(0, 0);
+      // column blocks in groups of 4 (one uniform branch per group, so each group's LDS reads
+      // issue together); x'_c = 0 for c <= k, so a partly finished group adds zeros
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        if (8 * i + 7 > k) acc = aqc::cfma(g[i], vcol(q + 8 * i), acc);  // uniform skip; v_c = 0 for c <= k
-        if ((i & 3) == 3) asm volatile("" ::: "memory");  // keep the LDS reads in groups of 4
+      for (int gi = 0; gi < 4; ++gi) {
+        if (32 * gi + 31 > k) {
+#pragma unroll
+          for (int ii = 0; ii < 4; ++ii) {
+            const int i = 4 * gi + ii;
+            acc = aqc::cfma(g[i], xv[b * 128 + q + 8 * i], acc);
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      // x' differs from the stored column only at k + 1: alpha -> alpha - beta
+      if (q == ((k + 1) & 7)) {
+        const cplx gk1 = pick16(g, ik1);
+        acc.x = fma(-beta, gk1.x, acc.x);
+        acc.y = fma(-beta, gk1.y, acc.y);
       }
       acc.x = aqc::row_sum8(acc.x);
       acc.y = aqc::row_sum8(acc.y);
-      const cplx p = aqc::cmul(tau, acc);
-      if (q == 0 && rowact) {
+      cplx p = aqc::cmul(aqc::cmul(tau, scl), acc);
+      if (!rowact) p = aqc::cmk(0, 0);
+      if (q == 0) {
         pv[b * 128 + r] = p;
-        hh[(size_t)k * (2 * C - k - 1) / 2 + (r - k - 1)] = vr;
+        vb[b * 128 + r] = vr;
+        if (rowact) hh[(size_t)k * (2 * C - k - 1) / 2 + (r - k - 1)] = vr;
       }
       const cplx kk = aqc::cmul(aqc::cconj(p), vr);
-      kp.x = wave_sum_dpp(q == 0 && rowact ? kk.x : 0.0);
-      kp.y = wave_sum_dpp(q == 0 && rowact ? kk.y : 0.0);
+      kp.x = wave_sum_dpp(q == 0 ? kk.x : 0.0);
+      kp.y = wave_sum_dpp(q == 0 ? kk.y : 0.0);
+      // the row's own p stays in registers for w_r below
+      x = p;
     }
     if (lane == 0) kpart[b * 16 + wave] = kp;
     if (tid == 0) {
@@ -240,27 +277,31 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
       s_e[k] = beta;
     }
     __syncthreads();
-    tick(7);
+    tick_step(t_b);
     if (wact) {
       cplx kt = aqc::cmk(0, 0);
 #pragma unroll
       for (int w = 0; w < 16; ++w) kt = aqc::cadd(kt, kpart[b * 16 + w]);
       const cplx a2 = aqc::cscale(aqc::cmul(tau, kt), -0.5);
-      // w_r (0 for rows at or above k: vr = 0 there too), so rows <= k get a zero update
-      const cplx wr0 = aqc::cfma(a2, vr, pv[b * 128 + r]);
-      const cplx wr = aqc::cmk(rowact ? wr0.x : 0.0, rowact ? wr0.y : 0.0);
+      // w_r = a2 v_r + p_r (0 for rows at or above k, where v_r and p_r are 0)
+      const cplx wr = aqc::cfma(a2, vr, x);
+      const double nvx = -vr.x, nvy = -vr.y, nwx = -wr.x, nwy = -wr.y;
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        if (8 * i + 7 > k) {  // uniform
-          const int c = q + 8 * i;
-          const cplx vc = vcol(c);
-          const cplx wc0 = aqc::cfma(a2, vc, pv[b * 128 + c]);
-          const bool colact = c > k && c < C;
-          const cplx wc = aqc::cmk(colact ? wc0.x : 0.0, colact ? wc0.y : 0.0);
-          // g -= v_r conj(w_c) + w_r conj(v_c)  (zero outside the trailing block)
-          g[i] = aqc::csub(g[i], aqc::cadd(aqc::cmulc(vr, wc), aqc::cmulc(wr, vc)));
+      for (int gi = 0; gi < 4; ++gi) {
+        if (32 * gi + 31 > k) {  // uniform; v_c = p_c = 0 for c <= k
+#pragma unroll
+          for (int ii = 0; ii < 4; ++ii) {
+            const int i = 4 * gi + ii;
+            const int c = q + 8 * i;
+            const cplx vc = vb[b * 128 + c];
+            const cplx wc = aqc::cfma(a2, vc, pv[b * 128 + c]);
+            // g -= v_r conj(w_c) + w_r conj(v_c)  (zero outside the trailing block)
+            g[i].x = fma(nvx, wc.x, fma(nvy, wc.y, fma(nwx, vc.x, fma(nwy, vc.y, g[i].x))));
+            g[i].y = fma(nvy, wc.x, fma(vr.x, wc.y, fma(nwy, vc.x, fma(wr.x, vc.y, g[i].y))));
+            if (ii == 1) __builtin_amdgcn_sched_barrier(0);  // LDS reads in pairs: no spills
+          }
         }
-        if ((i & 1) == 1) asm volatile("" ::: "memory");  // LDS reads in groups of 2: no spills
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
   }
@@ -273,6 +314,10 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
     if (q == ql && r == C - 1) s_d[C - 1] = x.x;
   }
   __syncthreads();
+  if (tid == 0) {
+    atomicAdd(&g_gram_ticks[6], t_a);
+    atomicAdd(&g_gram_ticks[7], t_b);
+  }
   tick(1);
   // ---- S4: top-K eigenvalues of T by 17-section ----
   if (tid == 0) {
