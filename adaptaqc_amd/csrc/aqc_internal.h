@@ -78,6 +78,35 @@ __device__ __forceinline__ double dpp_perm(double v) {
   return __hiloint2double(hi, lo);
 }
 
+// Loads through a pointer known to address global memory.  Pointers read out of job structs
+// are generic, so the compiler emits FLAT loads, which also count on LGKM_CNT: every LDS wait
+// (and every barrier) then drains them too, and a prefetch issued ahead of a barrier stalls
+// there.  GLOBAL loads count on VM_CNT only.
+// (through double pointers: a cast of the HIP vector type's pointer is lost again in its copy
+// constructor, which takes a generic reference)
+typedef __attribute__((address_space(1))) double gdouble;
+__device__ __forceinline__ cplx ldg(const cplx* p) {
+  const gdouble* q = (const gdouble*)(const double*)p;
+  return cmk(q[0], q[1]);
+}
+__device__ __forceinline__ double ldg(const double* p) { return *(const gdouble*)p; }
+__device__ __forceinline__ void stg(cplx* p, cplx v) {
+  gdouble* q = (gdouble*)(double*)p;
+  q[0] = v.x;
+  q[1] = v.y;
+}
+
+// Raw buffer loads: a uniform (SGPR) resource + one 32-bit lane offset + a uniform SGPR offset,
+// so a run of loads at uniform strides holds one VGPR of addressing instead of a 64-bit address
+// each.  Offsets past `bytes` (lane offset + instruction offset) read as zero.  0x00020000 is the
+// gfx9 data-format word of the resource.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ cplx buf_ld(__amdgpu_buffer_rsrc_t r, unsigned lane_off, unsigned uni_off) {
+  return __builtin_bit_cast(cplx, __builtin_amdgcn_raw_buffer_load_b128(r, lane_off, uni_off, 0));
+}
+
 // Sum over the 16 lanes of a DPP row, result in every lane of the row.  Pure VALU (DPP
 // quad_perm / row_ror), no LDS crossbar: ~2.5x cheaper than the ds_bpermute __shfl_xor path.
 __device__ __forceinline__ double row_sum16(double v) {

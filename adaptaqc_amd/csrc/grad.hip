@@ -17,6 +17,7 @@
 #include <mutex>
 #include <vector>
 
+#include "aqc_gemm.h"
 #include "mps_internal.h"
 
 using aqc::cplx;
@@ -24,9 +25,8 @@ using aqc::cplx;
 namespace {
 
 constexpr int kT = 256;
-// k_sweep_lr splits each contraction over kT / 64 = 4 waves (part[4]) and k_sweep_w over two
-// halves of kT / 2 = 128 threads (part[2]): both index their partial sums from this block size
-static_assert(kT == 256, "k_sweep_lr / k_sweep_w assume 4 waves of 64 lanes per workgroup");
+// k_sweep_w splits each contraction over two halves of kT / 2 = 128 threads (part[2])
+static_assert(kT == 256, "k_sweep_w assumes 4 waves of 64 lanes per workgroup");
 
 struct SweepJob {
   const cplx* gam;
@@ -66,53 +66,242 @@ __global__ __launch_bounds__(kT) void k_sweep_M(const SweepJob* __restrict__ job
   const int cl = j.dims[i], cr = j.dims[i + 1];
   const cplx s0 = aqc::cconj(svec[2 * i]), s1 = aqc::cconj(svec[2 * i + 1]);
   cplx* Mi = j.M + (size_t)i * j.cap * j.cap;
-  for (int e = threadIdx.x; e < cl * cr; e += kT) {
-    const int l = e / cr, r = e % cr;
-    Mi[(size_t)l * j.cap + r] = aqc::cfma(s1, site_a(j, i, 1, l, r), aqc::cmul(s0, site_a(j, i, 0, l, r)));
+  // the whole cap x cap block, zeros outside chi_l x chi_r: the chains read it without masks
+  for (int e = threadIdx.x; e < j.cap * j.cap; e += kT) {
+    const int l = e / j.cap, r = e % j.cap;
+    Mi[e] = (l < cl && r < cr) ? aqc::cfma(s1, site_a(j, i, 1, l, r), aqc::cmul(s0, site_a(j, i, 0, l, r)))
+                               : aqc::cmk(0, 0);
   }
 }
 
-// blockIdx.x: job, blockIdx.y: 0 left / 1 right.  A chain of n dependent vector-matrix products:
-// the contraction index is split over the workgroup's four waves (wave q takes indices q, q + 4,
-// ...) with the running vector in LDS and the four partial sums added through LDS, so a step is a
-// quarter-length dependent FMA chain with its loads in flight instead of a full-length one on a
-// quarter of the threads.
-__global__ __launch_bounds__(kT) void k_sweep_lr(const SweepJob* __restrict__ jobs) {
+// blockIdx.x: job, blockIdx.y: 0 left / 1 right.  A chain of n dependent vector-matrix products
+// (l_{i+1} = l_i M_i, r_i = M_i r_{i+1}) in one 1024-thread workgroup: thread t owns output
+// o = t >> 3 (+ 128 per pass) and the contraction indices k = (t & 7) + 8 kk, so each group of 8
+// lanes reads 8 consecutive complex of one matrix row (128-byte segments for both orientations)
+// and sums through DPP (row_sum8); the running vector sits in LDS, double-buffered, one barrier
+// per step.  The matrices do not depend on the vector: with cap <= 128 the next step's 16 values
+// per thread are loaded while the current step computes, so the chain runs at the matrices'
+// streaming rate instead of one memory latency per step.
+__device__ __forceinline__ void lds_barrier() {
+  // LDS-only barrier: the workgroup fence of __syncthreads would also drain the prefetch loads
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// CAP: 64, 128 or 256 >= the bond capacity; EXACT: the capacity equals CAP (mask-free loads,
+// compile-time strides), otherwise out-of-block elements are clamped and zeroed.
+template <int CAP, bool EXACT>
+__global__ __launch_bounds__(1024) void k_sweep_lr(const SweepJob* __restrict__ jobs) {
+  static_assert(CAP == 64 || CAP == 128 || CAP == 256, "k_sweep_lr: capacity 64, 128 or 256");
+  constexpr int NP = CAP > 128 ? 2 : 1;   // output passes of 128
+  constexpr int NC = CAP > 128 ? 2 : 1;   // k chunks of 128 (8 lanes x NK)
+  constexpr int NK = CAP < 128 ? 8 : 16;  // elements per thread per chunk
+  constexpr bool PF = CAP <= 128;         // register prefetch of the next step
   const SweepJob& j = jobs[blockIdx.x];
-  const int cap = j.cap, n = j.n;
-  const int tid = threadIdx.x, q = tid >> 6, t = tid & 63;
-  constexpr int kMaxCap = 256;
-  __shared__ cplx vec[kMaxCap];
-  __shared__ cplx part[4][kMaxCap];
+  const int n = j.n;
+  const int cap = EXACT ? CAP : j.cap;
+  const int t = threadIdx.x, o0 = t >> 3, ks = t & 7;
+  __shared__ cplx vec[2][CAP];
   const bool left = blockIdx.y == 0;
   cplx* out = left ? j.lv : j.rv;
-  if (tid == 0) {
-    vec[0] = aqc::cmk(1, 0);
-    out[(size_t)(left ? 0 : n) * cap] = aqc::cmk(1, 0);
+  if (t < CAP) vec[0][t] = aqc::cmk(t == 0 ? 1.0 : 0.0, 0.0);
+  if (t == 0) out[(size_t)(left ? 0 : n) * cap] = aqc::cmk(1, 0);
+  // NK elements (k, o) of step `step`'s matrix (zero-padded to CAP x CAP by k_sweep_M, so no
+  // masks) for output pass `pass`, k chunk `kc`: left out[o] = sum_k vec[k] M[k][o], right
+  // out[o] = sum_k M[o][k] vec[k]
+  auto load = [&](int step, int pass, int kc, cplx (&m)[NK]) {
+    const int i = left ? step : n - 1 - step;
+    const cplx* Mi = j.M + (size_t)i * cap * cap;
+    // the lane's offset laundered per call: hoisted out of the step loop, the per-element
+    // addresses would stay live across it (and spill)
+    int o = o0 + 128 * pass, kq = ks + 128 * kc;
+    asm volatile("" : "+v"(o), "+v"(kq));
+    if constexpr (EXACT) {
+      // one lane offset, the element stride as the uniform offset
+      const auto rs = aqc::make_rsrc(Mi, CAP * CAP * 16);
+      const unsigned voff = 16u * (left ? (unsigned)(kq * CAP + o) : (unsigned)(o * CAP + kq));
+#pragma unroll
+      for (int kk = 0; kk < NK; ++kk) m[kk] = aqc::buf_ld(rs, voff, 16u * kk * (left ? 8 * CAP : 8));
+    } else {
+      const bool ov = o < cap;
+      const int oc = ov ? o : 0;
+#pragma unroll
+      for (int kk = 0; kk < NK; ++kk) {
+        const int k = kq + 8 * kk;
+        const bool ok = ov && k < cap;
+        const int kc2 = ok ? k : 0;
+        const cplx v = aqc::ldg(Mi + (left ? kc2 * cap + oc : oc * cap + kc2));
+        m[kk] = aqc::cmk(ok ? v.x : 0.0, ok ? v.y : 0.0);
+      }
+    }
+  };
+  const bool oact = o0 < CAP;  // CAP 64: waves 8..15 only join the barriers (uniform per wave)
+  cplx mc[NK];
+  if constexpr (PF) {
+    if (oact) load(0, 0, 0, mc);
   }
   __syncthreads();
+  int cur = 0;
   for (int step = 0; step < n; ++step) {
     const int i = left ? step : n - 1 - step;
-    const int cl = j.dims[i], cr = j.dims[i + 1];
-    const cplx* Mi = j.M + (size_t)i * cap * cap;
-    const int nout = left ? cr : cl, nin = left ? cl : cr;
-    for (int o = t; o < nout; o += 64) {
-      cplx acc = aqc::cmk(0, 0);
-#pragma unroll 4
-      for (int k = q; k < nin; k += 4) {
-        // left: out[r] = sum_l vec[l] M[l][r];  right: out[l] = sum_r M[l][r] vec[r]
-        const cplx m = left ? Mi[(size_t)k * cap + o] : Mi[(size_t)o * cap + k];
-        acc = aqc::cfma(vec[k], m, acc);
+    const int nout = left ? j.dims[i + 1] : j.dims[i];
+    if (oact) {
+#pragma unroll
+      for (int pass = 0; pass < NP; ++pass) {
+        cplx acc = aqc::cmk(0, 0);
+#pragma unroll
+        for (int kc = 0; kc < NC; ++kc) {
+          cplx m[NK];
+          if constexpr (PF) {
+#pragma unroll
+            for (int kk = 0; kk < NK; ++kk) m[kk] = mc[kk];
+            if (step + 1 < n) load(step + 1, 0, 0, mc);
+          } else {
+            load(step, pass, kc, m);
+          }
+#pragma unroll
+          for (int kk = 0; kk < NK; ++kk) {
+            acc = aqc::cfma(vec[cur][128 * kc + ks + 8 * kk], m[kk], acc);
+            if ((kk & 3) == 3) __builtin_amdgcn_sched_barrier(0);  // LDS reads in groups of 4
+          }
+        }
+        acc.x = aqc::row_sum8(acc.x);
+        acc.y = aqc::row_sum8(acc.y);
+        const int o = o0 + 128 * pass;
+        if (ks == 0) {
+          // M's zero padding makes acc = 0 beyond nout: the next step's vector stays clean
+          vec[cur ^ 1][o] = acc;
+          if (o < nout) out[(size_t)(left ? i + 1 : i) * cap + o] = acc;
+        }
       }
-      part[q][o] = acc;
     }
-    __syncthreads();
-    for (int o = tid; o < nout; o += kT) {
-      const cplx v = aqc::cadd(aqc::cadd(part[0][o], part[1][o]), aqc::cadd(part[2][o], part[3][o]));
-      vec[o] = v;
-      out[(size_t)(left ? i + 1 : i) * cap + o] = v;
+    lds_barrier();
+    cur ^= 1;
+  }
+}
+
+// The same chain for the exact capacities 64 and 128 with the whole next step's matrix share in
+// flight while the current one computes: 8 CAP threads, thread t owns output o = t / 8 and
+// k = (t % 8) + 8 kk (CAP / 8 elements), two register sets with the step loop unrolled by two
+// (a register copy of an in-flight load would wait for it; a spill reload would wait for every
+// older load, the prefetch included).
+template <int CAP>
+__global__ __launch_bounds__(CAP * 8) void k_sweep_lr_pf(const SweepJob* __restrict__ jobs) {
+  static_assert(CAP == 64 || CAP == 128, "k_sweep_lr_pf: capacity 64 or 128");
+  constexpr int LPO = 8, NK = CAP / LPO;
+  const SweepJob& j = jobs[blockIdx.x];
+  const int n = j.n;
+  const int t = threadIdx.x, o = t / LPO, ks = t % LPO;
+  __shared__ cplx vec[2][CAP];
+  const bool left = blockIdx.y == 0;
+  cplx* out = left ? j.lv : j.rv;
+  if (t < CAP) vec[0][t] = aqc::cmk(t == 0 ? 1.0 : 0.0, 0.0);
+  if (t == 0) out[(size_t)(left ? 0 : n) * CAP] = aqc::cmk(1, 0);
+  // left out[o] = sum_k vec[k] M[k][o], right out[o] = sum_k M[o][k] vec[k] (zero-padded M)
+  const unsigned voff = 16u * (left ? (unsigned)(ks * CAP + o) : (unsigned)(o * CAP + ks));
+  constexpr unsigned kstep_l = 16u * LPO * CAP, kstep_r = 16u * LPO;
+  auto load = [&](int step, cplx (&m)[NK]) {
+    const int i = left ? step : n - 1 - step;
+    const auto rs = aqc::make_rsrc(j.M + (size_t)i * CAP * CAP, CAP * CAP * 16);
+#pragma unroll
+    for (int kk = 0; kk < NK; ++kk) m[kk] = aqc::buf_ld(rs, voff, kk * (left ? kstep_l : kstep_r));
+  };
+  // rolling pipeline: element kk of step s + 1 is requested right after element kk of step s has
+  // been consumed, so NK loads are always in flight and each has a whole step to land
+  cplx m[NK];
+  load(0, m);
+  __syncthreads();
+  int cur = 0;
+  for (int step = 0; step < n; ++step) {
+    const int i = left ? step : n - 1 - step;
+    const int nout = left ? j.dims[i + 1] : j.dims[i];
+    const int inext = left ? min(step + 1, n - 1) : max(n - 2 - step, 0);
+    const auto rs = aqc::make_rsrc(j.M + (size_t)inext * CAP * CAP, CAP * CAP * 16);
+    cplx acc = aqc::cmk(0, 0);
+#pragma unroll
+    for (int kk = 0; kk < NK; ++kk) {
+      acc = aqc::cfma(vec[cur][ks + LPO * kk], m[kk], acc);
+      m[kk] = aqc::buf_ld(rs, voff, kk * (left ? kstep_l : kstep_r));
     }
-    __syncthreads();
+    acc.x = aqc::group_sum<LPO>(acc.x);
+    acc.y = aqc::group_sum<LPO>(acc.y);
+    if (ks == 0) {
+      vec[cur ^ 1][o] = acc;  // zero beyond nout (M's padding)
+      if (o < nout) out[(size_t)(left ? i + 1 : i) * CAP + o] = acc;
+    }
+    lds_barrier();
+    cur ^= 1;
+  }
+}
+
+// One chain per workgroup (the latency form, for a single state) at the exact capacities 64 and
+// 128: 8 CAP threads in the k_sweep_lr_pf layout propagate both row vectors v[sa] through M_b
+// (one load of each M element for the two rows), with M_{b+1} in flight during step b.
+template <int CAP>
+__global__ __launch_bounds__(CAP * 8) void k_sweep_chain_pf(const SweepJob* __restrict__ jobs,
+                                                            const int* __restrict__ alist) {
+  static_assert(CAP == 64 || CAP == 128, "k_sweep_chain_pf: capacity 64 or 128");
+  constexpr int LPO = 8, NK = CAP / LPO, NT = CAP * 8;
+  const SweepJob& j = jobs[blockIdx.y];
+  const int a = alist[blockIdx.x];
+  const int n = j.n;
+  if (a >= n - 1) return;
+  const int t = threadIdx.x, o = t / LPO, ks = t % LPO, wave = t >> 6, lane = t & 63;
+  __shared__ cplx v[2][2][CAP];
+  {
+    const int d0 = j.dims[a + 1];
+    for (int e = t; e < 2 * CAP; e += NT) {
+      const int sa = e / CAP, k = e % CAP;
+      v[0][sa][k] = k < d0 ? j.v0[((size_t)a * 2 + sa) * CAP + k] : aqc::cmk(0, 0);
+    }
+  }
+  const unsigned voff = 16u * (unsigned)(ks * CAP + o);
+  constexpr unsigned kstep = 16u * LPO * CAP;
+  auto load = [&](int b, cplx (&m)[NK]) {
+    const auto rs = aqc::make_rsrc(j.M + (size_t)b * CAP * CAP, CAP * CAP * 16);
+#pragma unroll
+    for (int kk = 0; kk < NK; ++kk) m[kk] = aqc::buf_ld(rs, voff, kk * kstep);
+  };
+  // rolling pipeline (k_sweep_lr_pf)
+  cplx m[NK];
+  load(a + 1, m);
+  __syncthreads();
+  int cur = 0;
+  for (int b = a + 1; b < n; ++b) {
+    const int db = j.dims[b];
+    // T_ab[sa][sb] = sum_k v[sa][k] w_b[sb][k]: wave w < 4 -> (sa, sb) = (w >> 1, w & 1)
+    if (wave < 4) {
+      const int sa = wave >> 1, sb = wave & 1;
+      const cplx* wb = j.w + ((size_t)b * 2 + sb) * CAP;
+      cplx acc = aqc::cmk(0, 0);
+      for (int k = lane; k < db; k += 64) acc = aqc::cfma(v[cur][sa][k], wb[k], acc);
+      acc.x = aqc::row_sum16(acc.x);
+      acc.y = aqc::row_sum16(acc.y);
+      acc.x += __shfl_xor(acc.x, 16);
+      acc.y += __shfl_xor(acc.y, 16);
+      acc.x += __shfl_xor(acc.x, 32);
+      acc.y += __shfl_xor(acc.y, 32);
+      if (lane == 0) j.T[((size_t)a * n + b) * 4 + wave] = acc;
+    }
+    if (b == n - 1) break;
+    const auto rs = aqc::make_rsrc(j.M + (size_t)min(b + 1, n - 1) * CAP * CAP, CAP * CAP * 16);
+    cplx a0 = aqc::cmk(0, 0), a1 = aqc::cmk(0, 0);
+#pragma unroll
+    for (int kk = 0; kk < NK; ++kk) {
+      const int k = ks + LPO * kk;
+      a0 = aqc::cfma(v[cur][0][k], m[kk], a0);
+      a1 = aqc::cfma(v[cur][1][k], m[kk], a1);
+      m[kk] = aqc::buf_ld(rs, voff, kk * kstep);
+    }
+    a0.x = aqc::group_sum<LPO>(a0.x);
+    a0.y = aqc::group_sum<LPO>(a0.y);
+    a1.x = aqc::group_sum<LPO>(a1.x);
+    a1.y = aqc::group_sum<LPO>(a1.y);
+    if (ks == 0) {
+      v[cur ^ 1][0][o] = a0;
+      v[cur ^ 1][1][o] = a1;
+    }
+    lds_barrier();
+    cur ^= 1;
   }
 }
 
@@ -191,6 +380,95 @@ __global__ __launch_bounds__(kT) void k_sweep_chain(const SweepJob* __restrict__
       v[cur ^ 1][s][r] = acc;
     }
     __syncthreads();
+    cur ^= 1;
+  }
+}
+
+// Grouped chains (the sweep batched over first qubits, one GEMM per site): one
+// 512-thread workgroup per (group of up to 8 consecutive first qubits of alist, job), capacity
+// 128.  The group's 16 row vectors (row 2c + sa: chain c, first-qubit value sa) advance through
+// M_b together as a 16 x 128 by 128 x 128 complex product on the FP64 matrix cores, so M_b is read
+// once per group instead of once per chain.  Wave w owns output columns 16w .. 16w + 15 (one
+// 16 x 16 tile of v_mfma_f64_16x16x4f64, four real products per complex one, split over two
+// accumulator pairs so that consecutive MFMAs are independent; A operand: lane l holds
+// A[l & 15][k = l >> 4], B: B[k = l >> 4][l & 15], D: row (l >> 4) + 4 q, column l & 15).  The
+// lane's 32 B elements of M_{b+1} are requested one by one as those of M_b are consumed (a
+// rolling pipeline: a whole step to land), under LDS-only barriers.  Rows of chains not yet
+// started (a >= b) keep v0_a.  M is zero-padded, so no masks.
+constexpr int kChain8Ld = 132;  // V row stride (complex)
+
+__global__ __launch_bounds__(512) void k_sweep_chain8(const SweepJob* __restrict__ jobs, const int* __restrict__ alist,
+                                                      int nal) {
+  constexpr int CAP = 128, NQ = CAP / 4;
+  const SweepJob& j = jobs[blockIdx.y];
+  const int g0 = blockIdx.x * 8;
+  const int n = j.n;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  __shared__ cplx V[2][16][kChain8Ld];
+  __shared__ int s_a[8];
+  if (tid < 8) s_a[tid] = g0 + tid < nal ? alist[g0 + tid] : n;  // n: never active
+  __syncthreads();
+  const int amin = s_a[0];  // alist is ascending
+  if (amin >= n - 1) return;  // uniform
+  for (int e = tid; e < 16 * CAP; e += 512) {
+    const int row = e / CAP, k = e % CAP, a = s_a[row >> 1];
+    cplx v = aqc::cmk(0, 0);
+    if (a < n - 1 && k < j.dims[a + 1]) v = j.v0[((size_t)a * 2 + (row & 1)) * CAP + k];
+    V[0][row][k] = v;
+  }
+  const int li = lane & 15, lk = lane >> 4, col = 16 * wave + li;
+  const unsigned voff = 16u * (unsigned)(lk * CAP + col);
+  constexpr unsigned qstep = 16u * 4 * CAP;
+  cplx bq[NQ];
+  {
+    const auto rs = aqc::make_rsrc(j.M + (size_t)(amin + 1) * CAP * CAP, CAP * CAP * 16);
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) bq[q] = aqc::buf_ld(rs, voff, q * qstep);
+  }
+  __syncthreads();
+  int cur = 0;
+  for (int b = amin + 1; b < n; ++b) {
+    const int db = j.dims[b];
+    // T_ab[sa][sb] = sum_k v[sa][k] w_b[sb][k]: 16 lanes per row, waves 0-3
+    if (tid < 256) {
+      const int row = tid >> 4, sub = tid & 15, a = s_a[row >> 1];
+      const cplx* w0 = j.w + ((size_t)b * 2) * CAP;
+      cplx t0 = aqc::cmk(0, 0), t1 = aqc::cmk(0, 0);
+      for (int k = sub; k < db; k += 16) {
+        const cplx v = V[cur][row][k];
+        t0 = aqc::cfma(v, w0[k], t0);
+        t1 = aqc::cfma(v, w0[CAP + k], t1);
+      }
+      t0.x = aqc::row_sum16(t0.x);
+      t0.y = aqc::row_sum16(t0.y);
+      t1.x = aqc::row_sum16(t1.x);
+      t1.y = aqc::row_sum16(t1.y);
+      if (sub == 0 && a < b) {
+        cplx* T = j.T + ((size_t)a * n + b) * 4 + 2 * (row & 1);
+        T[0] = t0;
+        T[1] = t1;
+      }
+    }
+    if (b == n - 1) break;
+    const auto rs = aqc::make_rsrc(j.M + (size_t)min(b + 1, n - 1) * CAP * CAP, CAP * CAP * 16);
+    aqc::d4_t cr0 = {0, 0, 0, 0}, ci0 = {0, 0, 0, 0}, cr1 = {0, 0, 0, 0}, ci1 = {0, 0, 0, 0};
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const cplx av = V[cur][li][4 * q + lk];
+      const cplx bv = bq[q];
+      bq[q] = aqc::buf_ld(rs, voff, q * qstep);
+      cr0 = __builtin_amdgcn_mfma_f64_16x16x4f64(av.x, bv.x, cr0, 0, 0, 0);
+      ci0 = __builtin_amdgcn_mfma_f64_16x16x4f64(av.x, bv.y, ci0, 0, 0, 0);
+      cr1 = __builtin_amdgcn_mfma_f64_16x16x4f64(-av.y, bv.y, cr1, 0, 0, 0);
+      ci1 = __builtin_amdgcn_mfma_f64_16x16x4f64(av.y, bv.x, ci1, 0, 0, 0);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int row = lk + 4 * q;
+      const bool act = s_a[row >> 1] < b;
+      V[cur ^ 1][row][col] = act ? aqc::cmk(cr0[q] + cr1[q], ci0[q] + ci1[q]) : V[cur][row][col];
+    }
+    lds_barrier();
     cur ^= 1;
   }
 }
@@ -547,6 +825,15 @@ int ensure_gw(aqc_mps_t h) {
   return AQC_OK;
 }
 
+// 0: automatic (grouped chains for batches of states at cap 128, one chain per workgroup for a
+// single state, where the per-step latency of 2 rows beats the 16-row group's), 1: one chain per
+// workgroup, 2: grouped (aqc_sweep_set_chain_mode)
+int g_chain_mode = 0;
+bool use_chain8(int cap, int ns) {
+  if (cap != 128 || g_chain_mode == 1) return false;
+  return g_chain_mode == 2 || ns >= 2;
+}
+
 SweepJob make_job(aqc_mps_t h, double* out) {
   SweepJob j;
   const size_t cap = h->d.cap, n = h->d.n;
@@ -655,7 +942,15 @@ int aqc_pair_grads_batch(aqc_mps_t* psis, int ns, const double* svec, const int*
   const int cap = psis[0]->d.cap;
   hipLaunchKernelGGL(k_sweep_M, dim3(n, ns), dim3(kT), 0, st, djobs, dsvec);
   AQC_CHECK_LAUNCH();
-  hipLaunchKernelGGL(k_sweep_lr, dim3(ns, 2), dim3(kT), 0, st, djobs);
+  {
+    const dim3 g(ns, 2), b(1024);
+    if (cap == 64) hipLaunchKernelGGL((k_sweep_lr_pf<64>), g, dim3(512), 0, st, djobs);
+    else if (cap == 128) hipLaunchKernelGGL((k_sweep_lr_pf<128>), g, dim3(1024), 0, st, djobs);
+    else if (cap == 256) hipLaunchKernelGGL((k_sweep_lr<256, true>), g, b, 0, st, djobs);
+    else if (cap < 64) hipLaunchKernelGGL((k_sweep_lr<64, false>), g, b, 0, st, djobs);
+    else if (cap < 128) hipLaunchKernelGGL((k_sweep_lr<128, false>), g, b, 0, st, djobs);
+    else hipLaunchKernelGGL((k_sweep_lr<256, false>), g, b, 0, st, djobs);
+  }
   AQC_CHECK_LAUNCH();
   hipLaunchKernelGGL(k_sweep_w, dim3(n, ns), dim3(kT), 0, st, djobs, (const int*)dstart);
   AQC_CHECK_LAUNCH();
@@ -666,7 +961,18 @@ int aqc_pair_grads_batch(aqc_mps_t* psis, int ns, const double* svec, const int*
     for (int a : alist) steps += (double)(n - 1 - a);
     if (!alist.empty()) {
       aqc::KernelTimer::begin(st, "grad_chain", ns * steps * c * c * 16.0, ns * steps * 2.0 * c * c * 8.0);
-      hipLaunchKernelGGL(k_sweep_chain, dim3((unsigned)alist.size(), ns), dim3(kT), 0, st, djobs, dalist);
+      if (use_chain8(cap, ns))
+        hipLaunchKernelGGL(k_sweep_chain8, dim3((unsigned)(alist.size() + 7) / 8, ns), dim3(512), 0, st, djobs,
+                           (const int*)dalist, (int)alist.size());
+      else
+        if (cap == 128)
+          hipLaunchKernelGGL(k_sweep_chain_pf<128>, dim3((unsigned)alist.size(), ns), dim3(1024), 0, st, djobs,
+                             (const int*)dalist);
+        else if (cap == 64)
+          hipLaunchKernelGGL(k_sweep_chain_pf<64>, dim3((unsigned)alist.size(), ns), dim3(512), 0, st, djobs,
+                             (const int*)dalist);
+        else
+          hipLaunchKernelGGL(k_sweep_chain, dim3((unsigned)alist.size(), ns), dim3(kT), 0, st, djobs, dalist);
       aqc::KernelTimer::end(st);
       AQC_CHECK_LAUNCH();
     }
@@ -691,6 +997,12 @@ int aqc_pair_grads_batch(aqc_mps_t* psis, int ns, const double* svec, const int*
   // the result (host, or device memory that the caller reads on its own stream, e.g. the
   // all-gather's) is complete on return: one wait at the end, none before the launches
   AQC_HIP_CHECK(hipStreamSynchronize(st));
+  return AQC_OK;
+}
+
+int aqc_sweep_set_chain_mode(int mode) {
+  AQC_REQUIRE(mode >= 0 && mode <= 2, "aqc_sweep_set_chain_mode: mode 0, 1 or 2");
+  g_chain_mode = mode;
   return AQC_OK;
 }
 

@@ -187,6 +187,11 @@ int aqc_pair_grads(aqc_mps_t psi, const double* svec, const int* pairs, int npai
 int aqc_pair_grads_batch(aqc_mps_t* psis, int nstates, const double* svec, const int* pairs,
                          int npairs, const double* u0, const double* gens, const double* degs,
                          int ngen, double* out /* nstates*npairs */, int out_is_device);
+/* Chain kernel of the sweep: 0 = automatic (first qubits in groups of 8 advancing together on the
+ * matrix cores for batches of states at bond capacity 128; one chain per workgroup for a single
+ * state), 1 = one chain per workgroup, 2 = grouped whenever the capacity allows.  Results are the
+ * same up to floating-point summation order. */
+int aqc_sweep_set_chain_mode(int mode);
 /* Best product-state (chi = 1) approximation of psi: the starting circuit
  * starting_circuit="tenpy_product_state" (approximate_compiler.py:222-242, which compresses with
  * tenpy's variational method: trunc_params chi_max = 1, min_sweeps 10, max_sweeps 50).  Alternating

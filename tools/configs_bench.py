@@ -111,7 +111,8 @@ def config4(states, reps):
     layer, gens, deg, u0, gm = bench.layer_inputs()
     svec = np.zeros((n, 2), complex)
     svec[:, 0] = 1.0
-    distinct = [bench.random_vidal_mps(n, chi, 2000 + k) for k in range(min(states, 4))]
+    # near-product states: gradients well above rounding (random Vidal states give ~1e-16)
+    distinct = [bench.near_product_mps(n, chi, 2000 + k) for k in range(min(states, 4))]
     st = []
     for s in range(states):
         d = DeviceMPS(n, chi, 1e-16, chi)
@@ -128,7 +129,7 @@ def config4(states, reps):
     roof = roof_flops("grad_chain")
     return {"metric": "candidate-sweep gradient evals/sec, 50-qubit MPS chi=128 (config 4, 1 GPU)",
             "value": states * len(cmap) * reps / el, "unit": "evals/s", "ms_per_sweep": 1e3 * el / (reps * states),
-            "dtype": "c128", "data": "synthetic random Vidal MPS",
+            "dtype": "c128", "data": "synthetic near-product Vidal MPS (bench.near_product_mps)",
             "config": {"workload": "config4: 1225-pair identity_resolvable sweep, |s>=|0..0>", "n_qubits": n,
                        "chi": chi, "states": states, "mean_grad": float(np.mean(out))},
             "roofline": roof}
@@ -191,7 +192,10 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--states4", type=int, default=32)
     ap.add_argument("--gates5", type=int, default=24)
+    ap.add_argument("--chain-mode", type=int, default=0, help="aqc_sweep_set_chain_mode (0 auto, 1, 2)")
     args = ap.parse_args()
+    import ctypes
+    _lib.check(_lib.lib().aqc_sweep_set_chain_mode(ctypes.c_int(args.chain_mode)))
     os.environ.setdefault("AQC_DEVICE", "0")
     for c in args.configs.split(","):
         if c == "2":
