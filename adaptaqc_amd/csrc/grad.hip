@@ -305,40 +305,47 @@ __global__ __launch_bounds__(CAP * 8) void k_sweep_chain_pf(const SweepJob* __re
   }
 }
 
-// blockIdx.x: site, blockIdx.y: job.  w_b[s][l] = sum_r A_b[s][l][r] rv[b+1][r];
-// v0_a[s][r] = sum_l lv[a][l] A_a[s][l][r], the latter only at chain starts (start[a]: the first
-// qubits of this rank's pair shard).  Each output's contraction is split into two contiguous
-// halves over the two halves of the workgroup (all 256 threads busy, half-length chains), summed
-// through LDS.
+// blockIdx.x: site, blockIdx.y: job.  w_b[s][l] = sum_r Gamma_b[s][l][r] x[r] with
+// x[r] = lambda_{b+1}[r] rv[b+1][r] (in LDS): rows (s, l) 8 lanes each, the lanes along r (one
+// 128-byte segment per row and instruction), summed through DPP; v0_a[s][r] = lambda_{a+1}[r]
+// sum_l lv[a][l] Gamma_a[s][l][r], only at chain starts (start[a]: the first qubits of this rank's
+// pair shard): a thread per (s, r), the lanes along r.
 __global__ __launch_bounds__(kT) void k_sweep_w(const SweepJob* __restrict__ jobs, const int* __restrict__ start) {
   const SweepJob& j = jobs[blockIdx.y];
   const int i = blockIdx.x, cap = j.cap;
   const int cl = j.dims[i], cr = j.dims[i + 1];
-  const int tid = threadIdx.x, hh = tid >> 7, t = tid & 127;
-  __shared__ cplx part[2][512];
+  const int tid = threadIdx.x;
+  __shared__ cplx x[256];
+  const cplx* G = j.gam + (size_t)i * 2 * cap * cap;
+  const double* lamr = j.lam + (size_t)(i + 1) * cap;
+  for (int r = tid; r < cr; r += kT) x[r] = aqc::cscale(j.rv[(size_t)(i + 1) * cap + r], lamr[r]);
+  __syncthreads();
   {
-    const int r0 = hh * ((cr + 1) / 2), r1 = hh ? cr : (cr + 1) / 2;
-    for (int e = t; e < 2 * cl; e += 128) {
-      const int s = e / cl, l = e % cl;
+    const int ks = tid & 7;
+    for (int row0 = 0; row0 < 2 * cl; row0 += kT / 8) {
+      const int row = row0 + (tid >> 3);  // (s, l) = (row / cl, row % cl)
+      const bool ok = row < 2 * cl;
+      const int sr = ok ? row / cl : 0, lr = ok ? row % cl : 0;
+      const cplx* g = G + ((size_t)sr * cap + lr) * cap;
       cplx acc = aqc::cmk(0, 0);
-      for (int r = r0; r < r1; ++r) acc = aqc::cfma(site_a(j, i, s, l, r), j.rv[(size_t)(i + 1) * cap + r], acc);
-      part[hh][e] = acc;
+      if (ok)
+        for (int r = ks; r < cr; r += 8) acc = aqc::cfma(aqc::ldg(g + r), x[r], acc);
+      acc.x = aqc::row_sum8(acc.x);
+      acc.y = aqc::row_sum8(acc.y);
+      if (ok && ks == 0) j.w[((size_t)i * 2 + sr) * cap + lr] = acc;
     }
-    __syncthreads();
-    for (int e = tid; e < 2 * cl; e += kT) j.w[((size_t)i * 2 + e / cl) * cap + e % cl] = aqc::cadd(part[0][e], part[1][e]);
   }
   if (!start[i]) return;  // uniform in the workgroup
   __syncthreads();
-  {
-    const int l0 = hh * ((cl + 1) / 2), l1 = hh ? cl : (cl + 1) / 2;
-    for (int e = t; e < 2 * cr; e += 128) {
-      const int s = e / cr, r = e % cr;
-      cplx acc = aqc::cmk(0, 0);
-      for (int l = l0; l < l1; ++l) acc = aqc::cfma(j.lv[(size_t)i * cap + l], site_a(j, i, s, l, r), acc);
-      part[hh][e] = acc;
-    }
-    __syncthreads();
-    for (int e = tid; e < 2 * cr; e += kT) j.v0[((size_t)i * 2 + e / cr) * cap + e % cr] = aqc::cadd(part[0][e], part[1][e]);
+  for (int l = tid; l < cl; l += kT) x[l] = j.lv[(size_t)i * cap + l];
+  __syncthreads();
+  for (int e = tid; e < 2 * cap; e += kT) {
+    const int sr = e / cap, r = e % cap;
+    if (r >= cr) continue;
+    const cplx* g = G + (size_t)sr * cap * cap + r;
+    cplx acc = aqc::cmk(0, 0);
+    for (int l = 0; l < cl; ++l) acc = aqc::cfma(x[l], aqc::ldg(g + (size_t)l * cap), acc);
+    j.v0[((size_t)i * 2 + sr) * cap + r] = aqc::cscale(acc, lamr[r]);
   }
 }
 

@@ -1,4 +1,17 @@
-"""Candidate-pair sharding across the GPUs of one node (one process per GPU).
+"""Candidate sweep sharding across the GPUs of one node (one process per GPU).
+
+Two decompositions of the sweep (gradients.general_grad_of_pairs) over ranks:
+
+* pairs (one sweep, latency): below.  Every rank rebuilds the environments of psi; the chains
+  of the owned first qubits are the only part that divides, so the sweep's critical path (the
+  n-step environment chain, bound by one CU's streaming rate) does not shrink with the rank count.
+* states (many sweeps, throughput; config 4's strong scaling): a fixed global batch of G states --
+  independent sweeps, e.g. the candidate states of a layer search or several targets compiled
+  together -- split into contiguous blocks of G / world states per rank (``StateShard``); each rank
+  runs its sweeps on its own GPU and one all-gather of the per-state (best pair, best score) gives
+  every rank all G selections.  No environment or psi is exchanged.
+
+Pairs:
 
 The sweep (gradients.general_grad_of_pairs) produces one score per coupling-map pair; the pair
 with the largest ``score * reuse_priority`` wins (adapt_compiler.py:832-837, np.argmax = first
@@ -76,3 +89,43 @@ def select_pairs(full_scores, priorities):
     """np.argmax(scores * priorities) per state (first index wins ties)."""
     s = np.asarray(full_scores, dtype=np.float64) * np.asarray(priorities, dtype=np.float64)
     return np.argmax(s, axis=-1)
+
+
+class StateShard:
+    """Contiguous block of a global batch of G independent states (one sweep each) for one rank."""
+
+    def __init__(self, global_states, rank, world):
+        if global_states % world:
+            raise ValueError(f"global batch {global_states} does not divide over {world} ranks")
+        self.global_states, self.rank, self.world = global_states, rank, world
+        self.per_rank = global_states // world
+        self.start = rank * self.per_rank
+        self.stop = self.start + self.per_rank
+
+    def indices(self):
+        return range(self.start, self.stop)
+
+
+def best_pairs(scores, priorities):
+    """Per-state arg-max of scores * priorities (first maximum, as np.argmax) and its score, on the
+    scores' device: ([S] int64, [S] float64)."""
+    import torch
+
+    s = scores * torch.as_tensor(np.asarray(priorities, dtype=np.float64), device=scores.device)
+    best = torch.argmax(s, dim=1)
+    return best, s.gather(1, best[:, None])[:, 0]
+
+
+def gather_best(best, score, shard: StateShard, group=None):
+    """All-gather every rank's per-state (best pair index, score) into global state order: one
+    collective of 2 x per_rank float64 per rank (RCCL over xGMI with backend "nccl")."""
+    import torch
+    import torch.distributed as dist
+
+    local = torch.stack([best.to(torch.float64), score.to(torch.float64)])  # [2, per_rank]
+    if shard.world == 1:
+        return best.to(torch.int64), score
+    out = torch.empty((shard.world, 2, shard.per_rank), dtype=torch.float64, device=local.device)
+    dist.all_gather_into_tensor(out, local.contiguous(), group=group)
+    out = out.permute(1, 0, 2).reshape(2, -1)
+    return out[0].to(torch.int64), out[1]

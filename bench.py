@@ -246,7 +246,12 @@ def main():
     ap.add_argument("--simulate-world", type=int, default=0,
                     help="projection only (1 process): rank 0's share of an N-GPU run -- pair shard of N, "
                          "sweep over N x states -- with the all-gather replaced by a local scatter")
+    ap.add_argument("--strong", action="store_true",
+                    help="config 4 strong scaling: a fixed global batch of chi=128 sweeps sharded by state")
+    ap.add_argument("--global-states", type=int, default=512, help="--strong: sweeps in the global batch")
     args = ap.parse_args()
+    if args.strong:
+        return strong_main(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -468,6 +473,129 @@ def main():
             "latency": latency,
         }
         print(json.dumps(line))
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+STRONG_CHI = 128
+COLLECTIVE_US_EST = 50.0  # all-gather of a few KB over xGMI at 8 GPUs (RCCL small-message latency)
+
+
+def strong_main(args):
+    """Config 4 (BASELINE.json): 50-qubit chi = 128 candidate sweeps, strong scaling.  The global
+    work is fixed: G independent sweeps (1225 pairs, identity_resolvable generators, |s> = |0..0>,
+    per-state arg-max), state-sharded over the ranks (sharding.StateShard), one all-gather of the
+    per-state (best pair, score).  value = G * 1225 gradient evaluations / step time (max over ranks).
+
+    With --simulate-world N on one GPU (projection, no collective): the whole batch (T_1) and rank
+    0's block of G / N (T_N) timed on the same GPU, projected speedup T_1 / (T_N + an all-gather
+    estimate); and for contrast one sweep pair-sharded (sharding.PairShard): every rank's pair
+    subset timed in turn, the slowest rank's time against the whole sweep."""
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    os.environ["AQC_DEVICE"] = str(local)
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    from adaptaqc_amd.device import DeviceMPS, pair_grads_batch
+    from adaptaqc_amd.sharding import PairShard, StateShard, best_pairs, gather_best
+    from adaptaqc_amd.utils.constants import coupling_map_fully_entangled
+
+    n, chi, G = N_QUBITS, STRONG_CHI, args.global_states
+    sim = args.simulate_world if (args.simulate_world > 1 and world == 1) else 0
+    shard = StateShard(G, rank, sim or world)
+    cmap = coupling_map_fully_entangled(n)
+    layer, gens, deg, u0, gm = layer_inputs()
+    svec = np.zeros((n, 2), complex)
+    svec[:, 0] = 1.0
+    prio = np.ones(len(cmap))
+    distinct = [near_product_mps(n, chi, 3000 + k) for k in range(min(args.distinct, 4))]
+    nres = G if sim else shard.per_rank  # resident states: the whole batch when projecting
+    states = []
+    for k in range(nres):
+        d = DeviceMPS(n, chi, 1e-16, chi)
+        d.load_aer(distinct[(shard.start + k if not sim else k) % len(distinct)])
+        states.append(d)
+
+    def barrier():
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+
+    def timed(fn, k):
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(k):
+            r = fn()
+        barrier()
+        el = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([el], dtype=torch.float64, device="cuda")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        return el / k, r
+
+    def make_step(sts, pairs=cmap, gather=True):
+        out = torch.zeros((len(sts), max(len(pairs), 1)), dtype=torch.float64, device="cuda")
+
+        def step():
+            pair_grads_batch(sts, svec, pairs, u0, gm, deg, out=out.data_ptr())
+            best, score = best_pairs(out[:, : len(pairs)], np.ones(len(pairs)))
+            return gather_best(best, score, shard) if gather else (best, score)
+        return step
+
+    own = states[: shard.per_rank] if sim else states
+    step = make_step(own, gather=not sim)
+    for _ in range(args.warmup):
+        step()
+    t_step, (best, score) = timed(step, args.steps)
+    value = G * len(cmap) / (t_step if not sim else float("nan"))
+    res = {"metric": "candidate-sweep gradient evals/sec, 50-qubit MPS chi=128 (config 4), strong scaling",
+           "unit": "evals/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+           "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "c128",
+           "data": "synthetic near-product chi=128 Vidal MPS (4 distinct, seeded)",
+           "config": {"workload": f"config4: {G} independent 1225-pair identity_resolvable sweeps "
+                                  "(|s>=|0..0>), state-sharded, per-state arg-max, one all-gather",
+                      "n_qubits": n, "chi": chi, "global_states": G, "states_per_rank": shard.per_rank,
+                      "parallelism": f"states sharded x{sim or world}"}}
+    if not sim:
+        res["value"] = value
+        res["ms_per_step"] = 1e3 * t_step
+        if rank == 0:
+            print(json.dumps(res))
+    else:
+        step_all = make_step(states, gather=False)
+        step_all()
+        t_all, _ = timed(step_all, args.steps)
+        # one sweep, pair-sharded: each rank's subset in turn, the slowest rank
+        one = [states[0]]
+        t_one, _ = timed(make_step(one, gather=False), args.steps)
+        t_ranks = []
+        for r in range(sim):
+            ps = PairShard(cmap, n, r, sim)
+            if ps.local_pairs:
+                t_r, _ = timed(make_step(one, ps.local_pairs, gather=False), args.steps)
+                t_ranks.append(t_r)
+        t_coll = COLLECTIVE_US_EST * 1e-6
+        res.update({
+            "projection": f"rank 0 of a {sim}-GPU run on one GPU (no collective; all-gather estimated "
+                          f"at {COLLECTIVE_US_EST:.0f} us)",
+            "ms_global_batch_1gpu": 1e3 * t_all, "ms_rank_block": 1e3 * t_step,
+            "value_1gpu": G * len(cmap) / t_all,
+            "projected_value": G * len(cmap) / (t_step + t_coll),
+            "projected_speedup": t_all / (t_step + t_coll),
+            "single_sweep_pair_sharded": {
+                "ms_whole_sweep": 1e3 * t_one, "ms_slowest_rank": 1e3 * max(t_ranks),
+                "projected_speedup": t_one / (max(t_ranks) + t_coll),
+                "note": "one sweep split by first qubit: every rank still runs the n-step environment "
+                        "chains, which bound the sweep's latency"},
+        })
+        print(json.dumps(res))
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
