@@ -125,7 +125,7 @@ def gather_best(best, score, shard: StateShard, group=None):
     local = torch.stack([best.to(torch.float64), score.to(torch.float64)])  # [2, per_rank]
     if shard.world == 1:
         return best.to(torch.int64), score
-    out = torch.empty((shard.world, 2, shard.per_rank), dtype=torch.float64, device=local.device)
+    out = torch.empty((shard.world * 2, shard.per_rank), dtype=torch.float64, device=local.device)
     dist.all_gather_into_tensor(out, local.contiguous(), group=group)
-    out = out.permute(1, 0, 2).reshape(2, -1)
+    out = out.view(shard.world, 2, shard.per_rank).permute(1, 0, 2).reshape(2, -1)
     return out[0].to(torch.int64), out[1]

@@ -43,6 +43,63 @@ def _worker(rank, world, port, n, out):
     dist.destroy_process_group()
 
 
+def _state_sweep_worker(rank, world, port, n, G, out):
+    """Each rank computes its own block of sweeps (the oracle's environment form on CPU) through
+    the product's state sharding, then one all-gather of (best pair, score)."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from adaptaqc_amd.sharding import StateShard, best_pairs, gather_best
+
+    sh = StateShard(G, rank, world)
+    cmap = H.coupling_map_full(n)
+    scores = torch.as_tensor(np.array([_sweep_scores(n, k, cmap) for k in sh.indices()]), dtype=torch.float64)
+    best, score = best_pairs(scores, np.ones(len(cmap)))
+    b_all, s_all = gather_best(best, score, sh)
+    out[rank] = (b_all.numpy().tolist(), s_all.numpy().tobytes(), list(sh.indices()))
+    dist.destroy_process_group()
+
+
+def _sweep_scores(n, k, cmap):
+    """1225-pair-style sweep of state k (random small MPS, seeded by k) by the oracle's env form."""
+    from oracle import gradients as ogr
+    from oracle import mps as M
+
+    rng = np.random.default_rng(500 + k)
+    ops = []
+    for q in range(n):
+        ops.append(("ry", (q,), (float(rng.uniform(0.1, 0.4)),)))
+    for q in range(n - 1):
+        ops.append(("cx", (q, q + 1), ()))
+        ops.append(("rz", (q + 1,), (float(rng.uniform(-np.pi, np.pi)),)))
+    psi = M.run_circuit(n, ops, 1e-16, 8).preprocessed()
+    layer = [("rz", (0,), (0.3,)), ("ry", (1,), (0.2,)), ("cx", (0, 1), ()), ("rx", (0,), (0.1,)), ("rx", (1,), (0.4,))]
+    gens, degs = ogr.get_generators_and_degeneracies(layer, True, True)
+    return ogr.general_grad_of_pairs_env(psi, n, ogr.inverse_ops(layer), gens, degs, cmap)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_state_sharded_sweeps_across_ranks(world):
+    """Config 4's decomposition: a global batch of 8 sweeps, each rank really computing its block,
+    every rank ending with all 8 (pair, score) selections equal to the single-process answer."""
+    n, G = 8, 8
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_state_sweep_worker, args=(world, _free_port(), n, G, out), nprocs=world, join=True)
+    cmap = H.coupling_map_full(n)
+    full = np.array([_sweep_scores(n, k, cmap) for k in range(G)])
+    want_b = np.argmax(full, axis=1)
+    want_s = full[np.arange(G), want_b]
+    assert np.max(full) > 1e-3
+    seen = []
+    for r in range(world):
+        b, s_bytes, idx = out[r]
+        assert b == want_b.tolist()
+        np.testing.assert_array_equal(np.frombuffer(s_bytes), want_s)
+        seen += idx
+    assert sorted(seen) == list(range(G))
+
+
 @pytest.mark.parametrize("world", [2, 3])
 def test_gather_and_argmax_across_ranks(world):
     n = 12
