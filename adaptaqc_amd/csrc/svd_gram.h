@@ -2,10 +2,13 @@
 // path of the 2 chi = 128 two-site update when the truncation keeps K <= 64 singular triplets.
 //
 // X = theta' (L x C, or its conjugate transpose so that L >= C):
-//   S1  G = X^H X                                  block GEMM on the FP64 matrix cores (aqc_gemm.h)
-//   S2  G into registers: thread t holds row t/8, columns t%8 + 8i (i < 16)
+//   S1  G = X^H X: the 64 x 64 blocks on and above the diagonal on the FP64 matrix cores
+//       (aqc_gemm.h block_cgemm_tile), left in the accumulators
+//   S2  G's upper triangle through the LDS (packed) into registers: thread t holds row t/8,
+//       columns t%8 + 8i (i < 16)
 //   S3  Householder tridiagonalisation G = Q T Q^H (LAPACK zhetd2, lower): two barriers per column,
-//       double-buffered LDS vectors, the reflectors packed into the work buffer
+//       the column, the reflector and p = tau G v in double-buffered LDS vectors (zeros at and
+//       above the diagonal: a mask-free rank-2 update), the reflectors packed into the work buffer
 //   S4  the top K eigenvalues of the real symmetric tridiagonal T by 17-section: 16 lanes per
 //       eigenvalue each evaluate one Sturm count, one ballot picks the subinterval (8 rounds)
 //   S5  inverse iteration (unpivoted LDL^T of T - lambda I, three solves) per eigenvector, Gram-

@@ -43,7 +43,7 @@ def _run(theta, variant, stop_after_qr=False):
 
     m, n = theta.shape
     c, l = min(m, n), max(m, n)
-    lw = c if variant in (2, 5) else l
+    lw = c if variant in (2, 5, 7) else l
     th = np.asfortranarray(theta.astype(np.complex128)).ravel(order="F").copy()
     w = np.zeros(c * lw, np.complex128)
     sig = np.zeros(c)
@@ -100,3 +100,63 @@ def test_rank_deficient_and_zero_columns():
         for variant in (3, 2, 5):
             _, sig, _, _ = _run(th, variant)
             _check_sigma(sig, s_ref)
+
+
+# ---- the Gram / tridiagonal fast path (aqc_svd_debug variant 7, svd_gram.h) -------------------
+def _gram_ticks():
+    from adaptaqc_amd import _lib
+
+    t = np.zeros(8)
+    _lib.check(_lib.lib().aqc_svd_gram_ticks(_lib.ptr(t)))
+    return t
+
+
+def _spectrum_theta(m, n, s, seed):
+    rng = np.random.default_rng(seed)
+    c = min(m, n)
+    u, _ = np.linalg.qr(rng.standard_normal((m, c)) + 1j * rng.standard_normal((m, c)))
+    v, _ = np.linalg.qr(rng.standard_normal((n, c)) + 1j * rng.standard_normal((n, c)))
+    return (u * s[None, :]) @ v.conj().T
+
+
+@pytest.mark.parametrize("m,n", [(128, 128), (128, 96), (96, 128), (128, 72), (80, 80)])
+def test_gram_path_vs_numpy(m, n):
+    """Spectrum decaying as 0.93^i (lambda_64 / lambda_1 ~ 1e-4 > 1e-9): the Gram path runs to the
+    end (its back-transformation ticks advance) and returns the top K = 64 triplets: sigma to
+    1e-12 sigma_1, the kept right subspace of X (theta or theta^H, L >= C) to 1e-10, W = V Sigma."""
+    c = min(m, n)
+    theta = _spectrum_theta(m, n, 0.93 ** np.arange(c), 7 + m + n)
+    t0 = _gram_ticks()
+    w, sig, _, _ = _run(theta, 7)
+    t1 = _gram_ticks()
+    assert t1[4] > t0[4], "the Gram path declined"
+    K = min(64, c)
+    x = theta if m >= n else theta.conj().T
+    _, s_ref, vh = np.linalg.svd(x)
+    order = np.argsort(-sig)
+    got = sig[order]
+    np.testing.assert_allclose(got[:K], s_ref[:K], rtol=0, atol=1e-12 * s_ref[0])
+    assert np.all(got[K:] == 0.0)
+    V = w[:, order[:K]] / got[None, :K]
+    Vr = vh[:K].conj().T
+    assert np.linalg.norm(V @ V.conj().T - Vr @ Vr.conj().T, 2) < 1e-10
+    assert np.max(np.abs(V.conj().T @ V - np.eye(K))) < 1e-11
+
+
+@pytest.mark.parametrize("kind", ["graded", "rank10", "zero_tail_cluster"])
+def test_gram_path_declines_to_jacobi(kind):
+    """Where the kept values reach the noise floor of the Gram form (lambda_K <= 1e-9 lambda_1) the
+    path declines and the register Jacobi answers: sigma as the Jacobi contract (_check_sigma)."""
+    m = n = 128
+    if kind == "graded":
+        theta = _theta(m, n, 3)  # 0.8^i columns: sigma_64 / sigma_1 ~ 1e-6
+    elif kind == "rank10":
+        theta = _theta(m, n, 4, rank=10)
+    else:
+        s = np.concatenate([np.ones(8), 1e-6 * np.ones(120)])
+        theta = _spectrum_theta(m, n, s, 5)
+    t0 = _gram_ticks()
+    w, sig, _, _ = _run(theta, 7)
+    t1 = _gram_ticks()
+    assert t1[4] == t0[4], "the Gram path should have declined"
+    _check_sigma(sig, np.linalg.svd(theta, compute_uv=False))
