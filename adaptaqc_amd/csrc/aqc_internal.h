@@ -107,13 +107,17 @@ __device__ __forceinline__ cplx buf_ld(__amdgpu_buffer_rsrc_t r, unsigned lane_o
   return __builtin_bit_cast(cplx, __builtin_amdgcn_raw_buffer_load_b128(r, lane_off, uni_off, 0));
 }
 
-// Sum over the 16 lanes of a DPP row, result in every lane of the row.  Pure VALU (DPP
-// quad_perm / row_ror), no LDS crossbar: ~2.5x cheaper than the ds_bpermute __shfl_xor path.
+// Sum over the 16 lanes of a DPP row, result in every lane of the row -- bit-identical in every
+// lane: with quad sums Q0..Q3, row_ror:8 first gives {Q0+Q2, Q1+Q3} in every lane (up to the order
+// of one commutative add) and row_ror:4 then their sum, whereas row_ror:4 first associates the
+// quads differently in alternate quads.  Callers branch on the sum (the Jacobi's rotation sign
+// for near-degenerate pairs), so lanes must agree.  Pure VALU (DPP quad_perm / row_ror), no LDS
+// crossbar: ~2.5x cheaper than the ds_bpermute __shfl_xor path.
 __device__ __forceinline__ double row_sum16(double v) {
   v += dpp_perm<0xB1>(v);   // quad_perm [1,0,3,2]
   v += dpp_perm<0x4E>(v);   // quad_perm [2,3,0,1]
-  v += dpp_perm<0x124>(v);  // row_ror:4
   v += dpp_perm<0x128>(v);  // row_ror:8
+  v += dpp_perm<0x124>(v);  // row_ror:4
   return v;
 }
 

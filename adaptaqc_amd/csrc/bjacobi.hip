@@ -15,8 +15,9 @@
 //   * launch boundaries are the only inter-workgroup synchronisation (no grid barrier, no
 //     cross-XCD coherence assumptions).
 // Rotation rule, thresholds and stop test are those of k_jacobi_reg (mps.hip): relative
-// threshold L eps, squared-norm floor ||W||^2 1e-24, a sweep without rotations above 4x the
-// threshold -- or with only |t| <= j.jtiny ones (default 1e-6) -- is the last.  Output: W's columns = U sigma,
+// threshold L eps (and the dot-product noise floor jnoise eps ||W|| (|a| + |b|)), squared-norm floor
+// ||W||^2 1e-24, a sweep without rotations above 4x the
+// threshold -- or with only rotations moving <= j.jtiny^2 of the norms (t|g|) -- is the last.  Output: W's columns = U sigma,
 // sig = their norms (the k_jacobi contract consumed by k_rank / k_split_*, qr = 0).
 #include "mps_internal.h"
 
@@ -130,8 +131,8 @@ __global__ __launch_bounds__(1024) void k_bj_init(const TwoSiteJob* __restrict__
 template <int MAXR>
 __device__ __forceinline__ bool rotate_pair(double (&sr)[MAXR], double (&si)[MAXR], double (&mr)[MAXR],
                                             double (&mi)[MAXR], double& na, double& da, double& ida, double& nb,
-                                            double& db, double& idb, double tol2, double floor2, double tiny2,
-                                            int& rot, int& big,
+                                            double& db, double& idb, double tol2, double nfl2, double floor2,
+                                            double tiny2, int& rot, int& big,
                                             double2* bcol = nullptr) {
   double gx = 0, gy = 0;
 #pragma unroll
@@ -143,13 +144,15 @@ __device__ __forceinline__ bool rotate_pair(double (&sr)[MAXR], double (&si)[MAX
   gx = wave_sum(gx) * dd;
   gy = wave_sum(gy) * dd;
   const double g2 = gx * gx + gy * gy;
-  const double ab = na * nb;
-  if (!(g2 > tol2 * ab && na > floor2 && nb > floor2)) return false;
+  // relative threshold, and the dot-product noise floor of columns with ~eps ||W|| absolute error
+  // (mps.hip, jacobi_reg_body): nfl2 = 2 (jnoise eps)^2 ||W||^2
+  const double thr = fmax(tol2 * na * nb, nfl2 * (na + nb));
+  if (!(g2 > thr && na > floor2 && nb > floor2)) return false;
   double te, c, p;  // te = t / |g|, p = 1 + t^2
   jacobi_te(na, nb, g2, te, c, p);
-  if (g2 > 16.0 * tol2 * ab) {
+  if (g2 > 16.0 * thr) {
     rot = 1;
-    if (p - 1.0 > tiny2) big = 1;
+    if (fabs(te) * g2 > tiny2 * (na + nb)) big = 1;  // t|g| above jtiny^2 of the norms (jacobi_reg_body)
   }
   const double ra = db * ida, ira = da * idb;
   const double mux = te * gx * ra, muy = -te * gy * ra;
@@ -248,7 +251,8 @@ __global__ __launch_bounds__(512) void k_bj_intra(const TwoSiteJob* __restrict__
       sr[i] = x.x, si[i] = x.y, mr[i] = y.x, mi[i] = y.y;
     }
     double na = cn[a], da = cd[a], ida = cid[a], nb = cn[b], db = cd[b], idb = cid[b];
-    if (rotate_pair<MAXR>(sr, si, mr, mi, na, da, ida, nb, db, idb, tol2, floor2, j.jtiny * j.jtiny, rot, big)) {
+    if (rotate_pair<MAXR>(sr, si, mr, mi, na, da, ida, nb, db, idb, tol2, jacobi_noise2(j, s.fro), floor2,
+                          j.jtiny * j.jtiny, rot, big)) {
 #pragma unroll
       for (int i = 0; i < MAXR; ++i) {
         cols[a * ldl + lane + 64 * i] = make_double2(sr[i], si[i]);
@@ -328,7 +332,8 @@ __global__ __launch_bounds__(1024) void k_bj_cross(const TwoSiteJob* __restrict_
       mr[i] = v.x, mi[i] = v.y;
     }
     double nb = cn[slot], db = cd[slot], idb = cid[slot];
-    if (rotate_pair<MAXR>(sr, si, mr, mi, na, da, ida, nb, db, idb, tol2, floor2, j.jtiny * j.jtiny, rot, big, col)) {
+    if (rotate_pair<MAXR>(sr, si, mr, mi, na, da, ida, nb, db, idb, tol2, jacobi_noise2(j, s.fro), floor2,
+                          j.jtiny * j.jtiny, rot, big, col)) {
       __builtin_amdgcn_wave_barrier();
       if (lane == 0) cn[slot] = nb, cd[slot] = db, cid[slot] = idb;
     }

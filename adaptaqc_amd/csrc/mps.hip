@@ -54,6 +54,10 @@ double g_jacobi_tol_factor = 1.0;
 // the remaining off-diagonal is O(t^2) (quadratic convergence) and no further sweep is run.
 constexpr double kDefaultTinyT = 1e-6;
 double g_jacobi_tiny_t = kDefaultTinyT;
+// dot-product noise floor of the Jacobi rotations, in units of eps ||W|| (|a| + |b|)
+// (aqc_mps_set_jacobi_noise; jacobi_reg_body)
+constexpr double kDefaultJacobiNoise = 0.0;
+double g_jacobi_noise = kDefaultJacobiNoise;
 int g_jacobi_variant = 2;
 // Fused per-state chain (k_chain) for batches of >= kChainMinStates states at 2 chi = 128.
 bool g_fused_chain = true;
@@ -171,7 +175,7 @@ __device__ __forceinline__ int rr_elem(int pos, int r, int c) {
 // Rotate the pairs of one round.  pair_of(p) -> (ja, jb) column slots in the panel (-1 = skip).
 template <int LPP, int MAXR, int JT, typename PairFn>
 __device__ __forceinline__ void jacobi_round(cplx* panel, int ld, int L, int npairs, double tol, double floor2,
-                                             PairFn pair_of, int* rot_count) {
+                                             double nfl, PairFn pair_of, int* rot_count) {
   const int tid = fresh_tid();
   const int grp = tid / LPP, lane = tid % LPP;
   constexpr int kGroups = JT / LPP;
@@ -211,7 +215,9 @@ __device__ __forceinline__ void jacobi_round(cplx* panel, int ld, int L, int npa
       // Columns below floor2 (squared norm) are rounding noise of exactly-zero singular values:
       // their direction is random, so relative orthogonality can never be reached; they are
       // far below the CHOP cut (s^2 <= 1e-16) and are left alone.
-      if (g > tol * sqrt(al * be) && al > floor2 && be > floor2) {
+      // (and below the dot-product noise floor nfl sqrt(|a|^2 + |b|^2): jacobi_reg_body)
+      const double thr = fmax(tol * sqrt(al * be), nfl * sqrt(al + be));
+      if (g > thr && al > floor2 && be > floor2) {
         const double zeta = (be - al) / (2.0 * g);
         const double t = (zeta >= 0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
         const double c = 1.0 / sqrt(1.0 + t * t);
@@ -231,7 +237,7 @@ __device__ __forceinline__ void jacobi_round(cplx* panel, int ld, int L, int npa
             cb[r] = aqc::cfma(se, a, aqc::cscale(b, c));
           }
         }
-        if (lane == 0 && g > 4.0 * tol * sqrt(al * be)) atomicAdd(rot_count, 1);  // above noise
+        if (lane == 0 && g > 4.0 * thr) atomicAdd(rot_count, 1);  // above noise
       }
     }
   }
@@ -269,6 +275,7 @@ __global__ __launch_bounds__(JT) void k_jacobi(const TwoSiteJob* __restrict__ jo
   // absolute noise floor for squared column norms, relative to ||W||_F^2
   const double floor2 = fred[0] * 1e-24;
   const double tol = j.jtol * (double)L * 2.220446049250313e-16;
+  const double nfl = sqrt(jacobi_noise2(j, fred[0]));  // dot-product noise floor (jacobi_reg_body)
   const int ld = (L + 15) & ~15;
   int sweeps = 0;
   if (C >= 2) {
@@ -282,7 +289,7 @@ __global__ __launch_bounds__(JT) void k_jacobi(const TwoSiteJob* __restrict__ jo
         if (tid == 0) rot = 0;
         __syncthreads();
         for (int r = 0; r < ce - 1; ++r) {
-          jacobi_round<LPP, MAXR, JT>(panel, ld, L, ce / 2, tol, floor2,
+          jacobi_round<LPP, MAXR, JT>(panel, ld, L, ce / 2, tol, floor2, nfl,
                                   [&](int p, int& a, int& b) {
                                     a = rr_elem(p, r, ce);
                                     b = rr_elem(ce - 1 - p, r, ce);
@@ -310,7 +317,7 @@ __global__ __launch_bounds__(JT) void k_jacobi(const TwoSiteJob* __restrict__ jo
             panel[(idx / L) * ld + idx % L] = W[(size_t)c0 * L + idx];
           __syncthreads();
           for (int r = 0; r < be - 1; ++r) {
-            jacobi_round<LPP, MAXR, JT>(panel, ld, L, be / 2, tol, floor2,
+            jacobi_round<LPP, MAXR, JT>(panel, ld, L, be / 2, tol, floor2, nfl,
                                     [&](int p, int& a, int& bb) {
                                       a = rr_elem(p, r, be);
                                       bb = rr_elem(be - 1 - p, r, be);
@@ -333,7 +340,7 @@ __global__ __launch_bounds__(JT) void k_jacobi(const TwoSiteJob* __restrict__ jo
               panel[(b + idx / L) * ld + idx % L] = W[(size_t)cJ * L + idx];
             __syncthreads();
             for (int r = 0; r < b; ++r) {
-              jacobi_round<LPP, MAXR, JT>(panel, ld, L, b, tol, floor2,
+              jacobi_round<LPP, MAXR, JT>(panel, ld, L, b, tol, floor2, nfl,
                                       [&](int p, int& a, int& bb) {
                                         const int q = (p + r) % b;
                                         a = p < nI ? p : -1;
@@ -451,14 +458,14 @@ __device__ __forceinline__ void qr_reflector(double (&xr)[MAXR], double (&xi)[MA
 // LPG = lanes per column group (16: 1024 threads at CP = 128; 8: 512 threads with 16 rows per
 // lane, the per-pair rotation parameters and reductions amortised over twice the rows).
 // (The body is a device function so that the fused per-state chain, k_chain, runs it too.)
-template <int CP, int MAXR, int LPG = 16>
+template <int CP, int MAXR, int LPG = 16, int XPAD = 0, int XNP = 0>
 __device__ __forceinline__ void jacobi_reg_body(const TwoSiteJob& j) {
   static_assert(LPG * MAXR == CP, "LPG lanes x MAXR rows must cover the CP rows of a column");
   constexpr int kG = CP / 2;       // groups
   constexpr int kThreads = kG * LPG;
   // exchange-buffer stride (compile time: no guards); narrow groups pad a slot by LPG complex so
   // that consecutive slots alternate LDS bank halves (a ds_read_b128 lane group spans groups)
-  constexpr int ld = LPG * MAXR + (LPG < 16 ? LPG : 0);
+  constexpr int ld = LPG * MAXR + (LPG < 16 ? LPG : 0) + XPAD;
   constexpr int ldt = CP + 1;      // transpose-buffer stride (odd: conflict-free column writes)
   extern __shared__ double2 xbuf[];  // max(kG * ld, kG * ldt) complex
   __shared__ double fred[kThreads / 64];
@@ -638,6 +645,13 @@ __device__ __forceinline__ void jacobi_reg_body(const TwoSiteJob& j) {
   const double floor2 = fred[0] * 1e-24;
   const double tol = j.jtol * (double)Lj * 2.220446049250313e-16;
   const double tol2 = tol * tol;
+  // Dot-product noise floor: columns made of rounding noise carry ~eps ||W|| absolute error (the
+  // QR's, theta's own), so their products a^H b are only resolved above ~eps ||W|| (|a| + |b|):
+  // below it a pair of small (near-)degenerate columns rotates by 45 degrees at noise level every
+  // sweep and the loop never stops (61 sweeps on a spectrum 8 x 1 + 120 x 1e-6, with 2.6e-5
+  // errors in the large values).  Rotations need |g|^2 > max(tol^2 |a|^2 |b|^2,
+  // 2 (jnoise eps)^2 ||W||^2 (|a|^2 + |b|^2)).
+  const double nfl2 = jacobi_noise2(j, fred[0]);
   qtick(3);
   const int max_sweeps = j.dbg >= 1 ? 0 : kMaxSweeps;
   const bool map_rows = use_qr && j.dbg == 0;
@@ -665,9 +679,10 @@ __device__ __forceinline__ void jacobi_reg_body(const TwoSiteJob& j) {
     xid[g] = mid;
     xscl[g] = 1.0;
   }
-  // Stop rule: a sweep whose counted rotations all had |t| <= j.jtiny (default 1e-6) leaves every
-  // off-diagonal at O(t^2) relative after it (quadratic convergence), so the confirming sweep
-  // with no rotation at all is skipped.
+  // Stop rule: a sweep whose counted rotations all moved at most jtiny^2 (default 1e-12) of their
+  // pair's squared norms (t|g| <= jtiny^2 (|a|^2 + |b|^2)) is the last: the next sweep would move
+  // them by less again (quadratic convergence), so the confirming sweep with no rotation at all is
+  // skipped.
   const double tiny2 = j.jtiny * j.jtiny;
   double sd = 1.0, sn = 0.0;  // S: scale and tracked squared norm (uniform in the group)
   int sweeps = 0;
@@ -716,7 +731,7 @@ __device__ __forceinline__ void jacobi_reg_body(const TwoSiteJob& j) {
         const double mn = xnrm[slot], md = xscl[slot], imd = xisc[slot];
         // NP partial sums: with 16+ rows per lane and 1-2 waves per SIMD a single chain would
         // expose its FMA latency
-        constexpr int NP = MAXR >= 16 ? 2 : 1;
+        constexpr int NP = XNP ? XNP : (MAXR >= 16 ? 2 : 1);
         double gxp[NP], gyp[NP];
 #pragma unroll
         for (int q = 0; q < NP; ++q) gxp[q] = gyp[q] = 0.0;
@@ -734,15 +749,19 @@ __device__ __forceinline__ void jacobi_reg_body(const TwoSiteJob& j) {
         gx *= dd;
         gy *= dd;
         const double g2 = gx * gx + gy * gy;
-        const double ab = sn * mn;
-        if (g2 > tol2 * ab && sn > floor2 && mn > floor2) {
+        const double thr = fmax(tol2 * sn * mn, nfl2 * (sn + mn));
+        if (g2 > thr && sn > floor2 && mn > floor2) {
           // only rotations above dot-product noise keep the sweep loop going: a pair of
           // (near-)degenerate columns can otherwise flip-flop at |g| ~ tol forever
           double te, c, p;  // te = t / |g|, p = 1 + t^2
           jacobi_te(sn, mn, g2, te, c, p);
-          if (g2 > 16.0 * tol2 * ab) {
+          if (g2 > 16.0 * thr) {
             my_rot = 1;
-            if (p - 1.0 > tiny2) my_big = 1;  // |t| > jtiny
+            // the rotation moves t|g| between the squared norms: above jtiny^2 of them it counts
+            // (t|g| ~ t^2 (|a|^2 - |b|^2) for separated pairs -- |t| > jtiny -- and ~ |g| for a
+            // (near-)degenerate pair, whose t stays O(1) at any |g|: a test on |t| alone stopped
+            // with |g| ~ 1e-6 |a|^2 - |b|^2| left, 3e-8 errors in a degenerate pair's sigma)
+            if (fabs(te) * g2 > tiny2 * (sn + mn)) my_big = 1;
           }
           const double ra = md * isd, ira = sd * imd;  // d_b / d_a and its inverse
           const double mux = te * gx * ra, muy = -te * gy * ra;   // mu = t conj(e) d_b / d_a
@@ -854,9 +873,9 @@ __device__ __forceinline__ void jacobi_reg_body(const TwoSiteJob& j) {
   }
 }
 
-template <int CP, int MAXR, int LPG = 16>
+template <int CP, int MAXR, int LPG = 16, int XPAD = 0, int XNP = 0>
 __global__ __launch_bounds__(CP / 2 * LPG) void k_jacobi_reg(const TwoSiteJob* __restrict__ jobs) {
-  jacobi_reg_body<CP, MAXR, LPG>(jobs[blockIdx.x]);
+  jacobi_reg_body<CP, MAXR, LPG, XPAD, XNP>(jobs[blockIdx.x]);
 }
 
 #include "jacobi32.h"
@@ -1696,6 +1715,7 @@ TwoSiteJob make_two(aqc_mps_t h, const DevOp& op, int slot = 0) {
   j.thr = h->thr;
   j.jtol = g_jacobi_tol_factor;
   j.jtiny = g_jacobi_tiny_t;
+  j.jnoise = g_jacobi_noise;
   j.gram = g_svd_gram;
   std::memcpy(j.G, op.m, sizeof(j.G));
   return j;
@@ -2112,8 +2132,8 @@ int aqc_svd_debug(const double* theta, int m, int n, int variant, int stop_after
   AQC_REQUIRE(m >= 1 && n >= 1 && m % 2 == 0 && n % 2 == 0 && m <= 128 && n <= 128,
               "aqc_svd_debug: m, n must be even and <= 128");
   AQC_REQUIRE(stop_after_qr >= 0 && stop_after_qr <= 2, "aqc_svd_debug: stop_after_qr must be 0, 1 or 2");
-  AQC_REQUIRE(variant == 2 || variant == 3 || variant == 5 || variant == 6 || variant == 7,
-              "aqc_svd_debug: variant must be 2, 3, 5, 6 or 7");
+  AQC_REQUIRE(variant == 2 || variant == 3 || (variant >= 5 && variant <= 9),
+              "aqc_svd_debug: variant must be 2, 3 or 5-9");
   AQC_REQUIRE(variant != 7 || (std::max(m, n) > 64 && stop_after_qr == 0),
               "aqc_svd_debug: variant 7 (Gram) needs 64 < max(m, n) <= 128 and no QR stop");
   AQC_REQUIRE(variant != 6 || (std::max(m, n) > 64 && stop_after_qr == 0),
@@ -2141,6 +2161,7 @@ int aqc_svd_debug(const double* theta, int m, int n, int variant, int stop_after
   j.flags = fl;
   j.jtol = g_jacobi_tol_factor;
   j.jtiny = g_jacobi_tiny_t;
+  j.jnoise = g_jacobi_noise;
   j.qr = variant != 3 ? 1 : 0;
   j.dbg = stop_after_qr;
   j.cap = 64;                     // the work buffer holds 128 x 128
@@ -2159,6 +2180,10 @@ int aqc_svd_debug(const double* theta, int m, int n, int variant, int stop_after
     hipLaunchKernelGGL(k_svd_gram, dim3(1), dim3(1024), kChainLdsBytes, st, dj);
   else if (variant == 2)  // the register Jacobi itself (not the Gram path in front of it)
     hipLaunchKernelGGL((k_jacobi_reg<128, 8>), dim3(1), dim3(1024), 64 * 129 * 16, st, dj);
+  else if (variant == 8)  // experiment: 16-lane groups with padded exchange slots
+    hipLaunchKernelGGL((k_jacobi_reg<128, 8, 16, 16>), dim3(1), dim3(1024), 64 * 144 * 16, st, dj);
+  else if (variant == 9)  // experiment: 16-lane groups, two partial sums per dot product
+    hipLaunchKernelGGL((k_jacobi_reg<128, 8, 16, 0, 2>), dim3(1), dim3(1024), 64 * 129 * 16, st, dj);
   else launch_jacobi_reg128(variant, 1, st, dj);
   AQC_CHECK_LAUNCH();
   const int L = std::max(m, n), C = std::min(m, n);
@@ -2182,6 +2207,12 @@ int aqc_mps_jacobi_stats(aqc_mps_t h, int* max_sweeps) {
   *max_sweeps = f[2];
   int z = 0;
   AQC_HIP_CHECK(hipMemcpy(h->d.flags + 2, &z, sizeof(int), hipMemcpyHostToDevice));
+  return AQC_OK;
+}
+
+int aqc_mps_set_jacobi_noise(double factor) {
+  AQC_REQUIRE(factor >= 0, "aqc_mps_set_jacobi_noise: factor must be >= 0");
+  g_jacobi_noise = factor;
   return AQC_OK;
 }
 

@@ -59,8 +59,16 @@ struct TwoSiteJob {
   int dbg;      // diagnostics (aqc_svd_debug): 1 = stop after the QR phase, write X unpermuted
   int gram;     // 1: try the Gram / tridiagonal SVD first (svd_gram.h), the Jacobi as fallback
   int pad_;
+  double jnoise;  // Jacobi dot-product noise floor, in units of eps ||W|| (|a| + |b|) (0: off)
   cplx G[16];  // row = 2*s1'+s2' (out), col = 2*s1+s2 (in)
 };
+
+// Squared dot-product noise floor factor of the Jacobi rotations: a pair rotates only if
+// |g|^2 > jacobi_noise2(j, ||W||^2) (|a|^2 + |b|^2) (mps.hip, jacobi_reg_body).
+__device__ __forceinline__ double jacobi_noise2(const TwoSiteJob& j, double fro2) {
+  const double e = j.jnoise * 2.220446049250313e-16;
+  return 2.0 * e * e * fro2;
+}
 
 // Rotation parameters of the pair (alpha, beta, gamma = gx + i gy): t = sgn(zeta) /
 // (|zeta| + sqrt(1 + zeta^2)), zeta = (beta - alpha) / (2|gamma|), c = 1/sqrt(1 + t^2) and

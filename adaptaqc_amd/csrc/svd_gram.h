@@ -480,9 +480,9 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
     }
   };
   // sum over the 16 lanes sharing (l & 3): rotations by 4 and 8 inside a DPP row, then rows
-  auto col_sum = [&](double v) {
-    v += aqc::dpp_perm<0x124>(v);  // row_ror:4
+  auto col_sum = [&](double v) {  // (row_ror:8 first: the same bits in all 16 lanes, row_sum16)
     v += aqc::dpp_perm<0x128>(v);  // row_ror:8
+    v += aqc::dpp_perm<0x124>(v);  // row_ror:4
     v += __shfl_xor(v, 16);
     v += __shfl_xor(v, 32);
     return v;

@@ -105,10 +105,13 @@ int aqc_mps_apply_sort_batch(aqc_mps_t* hs, int nstates, const aqc_op_t* const* 
 /* Diagnostics: largest Jacobi sweep count since the last call (then reset). */
 int aqc_mps_jacobi_stats(aqc_mps_t h, int* max_sweeps);
 /* Jacobi rotation threshold |a^H b| > factor * L * eps * |a||b| (default factor 1). */
+/* Register / block Jacobi: dot-product noise floor of the rotations in units of eps ||W|| (|a| + |b|)
+ * (default 0: the relative threshold alone). */
+int aqc_mps_set_jacobi_noise(double factor);
 int aqc_mps_set_jacobi_tol(double factor);
-/* Jacobi sweep stop: after a sweep whose counted rotations all had |t| <= tiny_t the
-   decomposition ends (default 1e-6: the off-diagonal left is O(1e-12) relative; tiny_t <= 0
-   restores it; must be < 1e-3). */
+/* Jacobi sweep stop: after a sweep whose counted rotations all moved at most tiny_t^2 of their
+   pair's squared norms (t |g| <= tiny_t^2 (|a|^2 + |b|^2); |t| <= tiny_t for separated pairs) the
+   decomposition ends (default 1e-6; tiny_t <= 0 restores it; must be < 1e-3). */
 int aqc_mps_set_jacobi_stop(double tiny_t);
 /* Two-site SVD at 2 chi = 128: gram = 1 (default) tries the Gram / tridiagonal path first (G = X^H X
    on the matrix cores, Householder tridiagonalisation, multisection, inverse iteration; taken when
