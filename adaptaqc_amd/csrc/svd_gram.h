@@ -175,146 +175,153 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
     __syncthreads();  // the reflectors' scratch reuses the LDS
   }
   tick(0);
-  // ---- S3: tridiagonalisation (zhetd2, lower) ----
-  // LDS (double-buffered by step parity b): xv = column k below the diagonal (0 at and above it),
-  // vb = the reflector v (0 at and above the diagonal, 1 at k + 1), pv = p = tau G v (0 at and
-  // above the diagonal), so the trailing-block update needs no masks
-  cplx* xv = xbuf;                                        // [2][128]
-  cplx* pv = xbuf + 256;                                  // [2][128]
-  cplx* vb = xbuf + 512;                                  // [2][128]
-  double* npart = reinterpret_cast<double*>(xbuf + 768);  // [2][16]
-  cplx* kpart = xbuf + 784;                               // [2][16]
-  cplx* hh = j.work;  // reflector k at hh[k (2C - k - 1) / 2 + (row - k - 1)]
+  // ---- S3: tridiagonalisation (zhetd2, lower), one barrier per column ----
+  // Reflector k (v_{k+1} = 1, p = tau G^(k) v, a2 = -tau (p^H v) / 2, w = p + a2 v,
+  // G^(k+1) = G^(k) - v w^H - w v^H on the trailing block) reaches the registers one phase late,
+  // fused with the next reflector's product: column k + 1 of G^(k+1) below the diagonal is
+  // z_r - s v_r with z_r = G^(k)[r][k+1] - p_r (known before the barrier) and the scalar
+  // s = conj(p_{k+1}) + 2 Re(a2) (after it).  A phase reads (p, v, z) of reflector k - 1 from the
+  // LDS, reduces p^H v and |z - s v|^2 in every wave (two rows per lane: no cross-wave partial
+  // sums, the column is formed explicitly, no cancellation), forms reflector k, updates g by
+  // reflector k - 1 and multiplies it by reflector k's column in one pass over the columns, and
+  // writes (p, v, z) of reflector k.  LDS vectors are double-buffered by phase parity and zero
+  // where the reflector vanishes, so neither the update nor the product needs masks.
+  cplx* pvb = xbuf;        // [2][128] p   (0 at and above row k)
+  cplx* vbb = xbuf + 256;  // [2][128] v   (0 at and above row k, 1 at k + 1)
+  cplx* zvb = xbuf + 512;  // [2][128] z   (0 at and above row k + 1)
+  cplx* hh = j.work;       // reflector k at hh[k (2C - k - 1) / 2 + (row - k - 1)]
+  // "reflector -1": none, and column 0 of G as z (s = 0)
+  if (q == 0) {
+    pvb[128 + r] = aqc::cmk(0, 0);
+    vbb[128 + r] = aqc::cmk(0, 0);
+    zvb[128 + r] = (r > 0 && r < C) ? g[0] : aqc::cmk(0, 0);
+  }
+  cplx tau_prev = aqc::cmk(0, 0);
+  __syncthreads();
+  // reflector k - 1's a2 and s from buffer bp, per wave
+  auto prev_scalars = [&](int k, int bp, cplx& a2, cplx& s) {
+    const cplx p0 = pvb[bp * 128 + lane], p1 = pvb[bp * 128 + 64 + lane];
+    const cplx v0 = vbb[bp * 128 + lane], v1 = vbb[bp * 128 + 64 + lane];
+    cplx kt;
+    kt.x = wave_sum_dpp(fma(p0.x, v0.x, fma(p0.y, v0.y, fma(p1.x, v1.x, p1.y * v1.y))));
+    kt.y = wave_sum_dpp(fma(p0.x, v0.y, fma(-p0.y, v0.x, fma(p1.x, v1.y, -p1.y * v1.x))));
+    a2 = aqc::cscale(aqc::cmul(tau_prev, kt), -0.5);
+    const cplx pk = pvb[bp * 128 + k];
+    s = aqc::cmk(pk.x + 2.0 * a2.x, -pk.y);
+  };
   for (int k = 0; k < C - 1; ++k) {
-    const int b = k & 1;
-    const int ik = k >> 3, qk = k & 7, ik1 = (k + 1) >> 3;
+    const int b = k & 1, bp = b ^ 1;
     // q and r laundered through an empty asm each step: otherwise the compiler hoists the 16
     // columns' loop-invariant index / address values out of the k loop and spills them
     int q = q0, r = r0;
     asm volatile("" : "+v"(q), "+v"(r));
-    // waves whose rows are all <= k and column blocks with all columns <= k sit the step out
-    // (uniform branches): the trailing block shrinks, so the work is a third of the full sweep
-    const bool wact = wave * 8 + 7 > k;
-    cplx x = pick16(g, ik);
-    double nrm = 0.0;
-    if (q == qk) {
-      const bool below = r > k;
-      xv[b * 128 + r] = aqc::cmk(below ? x.x : 0.0, below ? x.y : 0.0);
-      if (r >= k + 2) nrm = aqc::cnorm2(x);
-      if (r == k) s_d[k] = x.x;
-    }
-    if (wact) nrm = wave_sum_dpp(nrm);
-    if (lane == 0) npart[b * 16 + wave] = nrm;
-    __syncthreads();
-    tick_step(t_a);
-    // reflector scalars, redundantly in every thread (zlarfg)
-    double xn2 = 0.0;
-#pragma unroll
-    for (int w = 0; w < 16; ++w) xn2 += npart[b * 16 + w];
-    const cplx alpha = xv[b * 128 + k + 1];
-    double beta;
-    cplx tau, scl;
-    if (xn2 == 0.0 && alpha.y == 0.0) {
-      beta = alpha.x;
-      tau = aqc::cmk(0, 0);
-      scl = aqc::cmk(0, 0);
-    } else {
-      // rsq / rcp seeds with Newton steps (full precision) instead of the IEEE sqrt / divide
-      // sequences: this chain runs between the step's two barriers
+    // rows >= k change this phase (row k: reflector k - 1's update gives d_k): waves whose rows
+    // are all below k only clear their LDS entries (uniform branch)
+    const bool wact = wave * 8 + 7 >= k;
+    cplx tau = aqc::cmk(0, 0);
+    if (wact) {
+      cplx a2, s;
+      prev_scalars(k, bp, a2, s);
+      // column k of G^(k) below the diagonal: x_r = z_r - s v_r (r > k); alpha = x_{k+1}
+      double xn2;
+      {
+        const cplx z0 = zvb[bp * 128 + lane], z1 = zvb[bp * 128 + 64 + lane];
+        const cplx v0 = vbb[bp * 128 + lane], v1 = vbb[bp * 128 + 64 + lane];
+        const cplx x0 = aqc::cfma(aqc::cmk(-s.x, -s.y), v0, z0), x1 = aqc::cfma(aqc::cmk(-s.x, -s.y), v1, z1);
+        const double n0 = lane > k + 1 ? aqc::cnorm2(x0) : 0.0, n1 = lane + 64 > k + 1 ? aqc::cnorm2(x1) : 0.0;
+        xn2 = wave_sum_dpp(n0 + n1);
+      }
+      const cplx alpha = aqc::cfma(aqc::cmk(-s.x, -s.y), vbb[bp * 128 + k + 1], zvb[bp * 128 + k + 1]);
+      // reflector k's scalars (zlarfg), redundantly in every thread; rsq / rcp seeds with Newton
+      // steps (full precision) instead of the IEEE sqrt / divide sequences
       const double x2 = fma(alpha.x, alpha.x, fma(alpha.y, alpha.y, xn2));
       double rs = __builtin_amdgcn_rsq(x2);
       rs = rs * fma(-0.5 * x2 * rs, rs, 1.5);
       rs = rs * fma(-0.5 * x2 * rs, rs, 1.5);
       const double nn = x2 * rs;
-      beta = alpha.x >= 0.0 ? -nn : nn;
+      const bool triv = xn2 == 0.0 && alpha.y == 0.0;  // H = I
+      const double beta = triv ? alpha.x : (alpha.x >= 0.0 ? -nn : nn);
       const double ib = alpha.x >= 0.0 ? -rs : rs;  // 1 / beta
-      tau = aqc::cmk((beta - alpha.x) * ib, -alpha.y * ib);
       const double dr = alpha.x - beta, di = alpha.y, id2 = rcp_nr(fma(dr, dr, di * di));
-      scl = aqc::cmk(dr * id2, -di * id2);  // 1 / (alpha - beta)
-    }
-    // v = scl x' with x' = x except x'_{k+1} = alpha - beta, so G v = scl (G x'): the product
-    // reads the column straight from the LDS and patches the one entry k + 1
-    const bool rowact = r > k && r < C;
-    cplx vr = aqc::cmul(xv[b * 128 + r], scl);
-    if (!(r > k + 1)) vr = aqc::cmk(r == k + 1 ? 1.0 : 0.0, 0.0);
-    cplx kp = aqc::cmk(0, 0);
-    if (wact) {
+      tau = triv ? aqc::cmk(0, 0) : aqc::cmk((beta - alpha.x) * ib, -alpha.y * ib);
+      const cplx scl = triv ? aqc::cmk(0, 0) : aqc::cmk(dr * id2, -di * id2);  // 1 / (alpha - beta)
+      // the own row's reflector k - 1 entries, w_r, and reflector k's column entry
+      const cplx vr = vbb[bp * 128 + r], pr = pvb[bp * 128 + r], zr = zvb[bp * 128 + r];
+      const cplx wr = aqc::cfma(a2, vr, pr);
+      const double nvx = -vr.x, nvy = -vr.y, nwx = -wr.x, nwy = -wr.y, nsx = -s.x, nsy = -s.y;
+      // one pass: g -= v_r conj(w_c) + w_r conj(v_c) (reflector k - 1), acc += g x_c (reflector k)
       cplx acc = aqc::cmk(0, 0);
-      // column blocks in groups of 4 (one uniform branch per group, so each group's LDS reads
-      // issue together); x'_c = 0 for c <= k, so a partly finished group adds zeros
 #pragma unroll
       for (int gi = 0; gi < 4; ++gi) {
-        if (32 * gi + 31 > k) {
-#pragma unroll
-          for (int ii = 0; ii < 4; ++ii) {
-            const int i = 4 * gi + ii;
-            acc = aqc::cfma(g[i], xv[b * 128 + q + 8 * i], acc);
-          }
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      // x' differs from the stored column only at k + 1: alpha -> alpha - beta
-      if (q == ((k + 1) & 7)) {
-        const cplx gk1 = pick16(g, ik1);
-        acc.x = fma(-beta, gk1.x, acc.x);
-        acc.y = fma(-beta, gk1.y, acc.y);
-      }
-      acc.x = aqc::row_sum8(acc.x);
-      acc.y = aqc::row_sum8(acc.y);
-      cplx p = aqc::cmul(aqc::cmul(tau, scl), acc);
-      if (!rowact) p = aqc::cmk(0, 0);
-      if (q == 0) {
-        pv[b * 128 + r] = p;
-        vb[b * 128 + r] = vr;
-        if (rowact) hh[(size_t)k * (2 * C - k - 1) / 2 + (r - k - 1)] = vr;
-      }
-      const cplx kk = aqc::cmul(aqc::cconj(p), vr);
-      kp.x = wave_sum_dpp(q == 0 ? kk.x : 0.0);
-      kp.y = wave_sum_dpp(q == 0 ? kk.y : 0.0);
-      // the row's own p stays in registers for w_r below
-      x = p;
-    }
-    if (lane == 0) kpart[b * 16 + wave] = kp;
-    if (tid == 0) {
-      s_tau[k] = tau;
-      s_e[k] = beta;
-    }
-    __syncthreads();
-    tick_step(t_b);
-    if (wact) {
-      cplx kt = aqc::cmk(0, 0);
-#pragma unroll
-      for (int w = 0; w < 16; ++w) kt = aqc::cadd(kt, kpart[b * 16 + w]);
-      const cplx a2 = aqc::cscale(aqc::cmul(tau, kt), -0.5);
-      // w_r = a2 v_r + p_r (0 for rows at or above k, where v_r and p_r are 0)
-      const cplx wr = aqc::cfma(a2, vr, x);
-      const double nvx = -vr.x, nvy = -vr.y, nwx = -wr.x, nwy = -wr.y;
-#pragma unroll
-      for (int gi = 0; gi < 4; ++gi) {
-        if (32 * gi + 31 > k) {  // uniform; v_c = p_c = 0 for c <= k
+        if (32 * gi + 31 >= k) {  // uniform; v_c = p_c = z_c = 0 for c < k
 #pragma unroll
           for (int ii = 0; ii < 4; ++ii) {
             const int i = 4 * gi + ii;
             const int c = q + 8 * i;
-            const cplx vc = vb[b * 128 + c];
-            const cplx wc = aqc::cfma(a2, vc, pv[b * 128 + c]);
-            // g -= v_r conj(w_c) + w_r conj(v_c)  (zero outside the trailing block)
+            const cplx vc = vbb[bp * 128 + c], pc = pvb[bp * 128 + c], zc = zvb[bp * 128 + c];
+            const cplx wc = aqc::cfma(a2, vc, pc);
             g[i].x = fma(nvx, wc.x, fma(nvy, wc.y, fma(nwx, vc.x, fma(nwy, vc.y, g[i].x))));
             g[i].y = fma(nvy, wc.x, fma(vr.x, wc.y, fma(nwy, vc.x, fma(wr.x, vc.y, g[i].y))));
+            const cplx xc = aqc::cmk(fma(nsx, vc.x, fma(nsy, -vc.y, zc.x)), fma(nsx, vc.y, fma(nsy, vc.x, zc.y)));
+            acc = aqc::cfma(g[i], xc, acc);
             if (ii == 1) __builtin_amdgcn_sched_barrier(0);  // LDS reads in pairs: no spills
           }
         }
         __builtin_amdgcn_sched_barrier(0);
       }
+      // the product used x_k = -s (z_k = 0, v_k = 1) where reflector k has 0, and x_{k+1} = alpha
+      // where it has alpha - beta: one entry each, in the lanes that hold those columns
+      const cplx gk = pick16(g, k >> 3), gk1 = pick16(g, (k + 1) >> 3);
+      if (q == (k & 7)) acc = aqc::cfma(s, gk, acc);
+      if (q == ((k + 1) & 7)) {
+        acc.x = fma(-beta, gk1.x, acc.x);
+        acc.y = fma(-beta, gk1.y, acc.y);
+      }
+      acc.x = aqc::row_sum8(acc.x);
+      acc.y = aqc::row_sum8(acc.y);
+      const bool rowact = r > k && r < C;
+      cplx p = aqc::cmul(aqc::cmul(tau, scl), acc);
+      if (!rowact) p = aqc::cmk(0, 0);
+      // reflector k's v on the own row: 1 at k + 1, scl x_r below, 0 above
+      cplx v = aqc::cmul(aqc::cfma(aqc::cmk(nsx, nsy), vr, zr), scl);
+      if (!(r > k + 1 && r < C)) v = aqc::cmk(r == k + 1 ? 1.0 : 0.0, 0.0);
+      if (q == 0) {
+        pvb[b * 128 + r] = p;
+        vbb[b * 128 + r] = v;
+        if (rowact) hh[(size_t)k * (2 * C - k - 1) / 2 + (r - k - 1)] = v;
+        if (r == k + 1) {
+          s_tau[k] = tau;
+          s_e[k] = beta;
+        }
+      }
+      if (q == ((k + 1) & 7)) {  // z of reflector k: G^(k)[r][k+1] - p_r below row k + 1
+        const bool zr_ok = r > k + 1 && r < C;
+        zvb[b * 128 + r] = zr_ok ? aqc::csub(gk1, p) : aqc::cmk(0, 0);
+      }
+      if (q == (k & 7) && r == k) s_d[k] = gk.x;  // G^(k)[k][k]
+    } else {
+      if (q == 0) {
+        pvb[b * 128 + r] = aqc::cmk(0, 0);
+        vbb[b * 128 + r] = aqc::cmk(0, 0);
+      }
+      if (q == ((k + 1) & 7)) zvb[b * 128 + r] = aqc::cmk(0, 0);
     }
+    // tau of reflector k for the next phase (uniform: the inactive waves never need it)
+    tau_prev = tau;
+    __syncthreads();
+    tick_step(t_a);
   }
-  {
-    const int il = (C - 1) >> 3, ql = (C - 1) & 7;
-    cplx x = aqc::cmk(0, 0);
-#pragma unroll
-    for (int i = 0; i < 16; ++i)
-      if (i == il) x = g[i];
-    if (q == ql && r == C - 1) s_d[C - 1] = x.x;
+  // d_{C-1}: reflector C - 2's update of the last diagonal entry
+  if (wave == (C - 1) >> 3) {
+    const int bp = (C - 2) & 1;
+    cplx a2, s;
+    prev_scalars(C - 1, bp, a2, s);
+    if (r0 == C - 1 && q0 == ((C - 1) & 7)) {
+      const cplx v = vbb[bp * 128 + C - 1], p = pvb[bp * 128 + C - 1];
+      const cplx w = aqc::cfma(a2, v, p);
+      const cplx gl = pick16(g, (C - 1) >> 3);
+      s_d[C - 1] = gl.x - 2.0 * (v.x * w.x + v.y * w.y);  // Re(g - v conj(w) - w conj(v))
+    }
   }
   __syncthreads();
   if (tid == 0) {
