@@ -190,7 +190,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--configs", default="2,4,5")
     ap.add_argument("--reps", type=int, default=3)
-    ap.add_argument("--states4", type=int, default=32)
+    ap.add_argument("--states4", type=int, default=128)
     ap.add_argument("--gates5", type=int, default=24)
     ap.add_argument("--chain-mode", type=int, default=0, help="aqc_sweep_set_chain_mode (0 auto, 1, 2)")
     args = ap.parse_args()
