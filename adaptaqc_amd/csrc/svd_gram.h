@@ -13,7 +13,8 @@
 //       eigenvalue each evaluate one Sturm count, one ballot picks the subinterval (8 rounds)
 //   S5  inverse iteration (unpivoted LDL^T of T - lambda I, three solves) per eigenvector, Gram-
 //       Schmidt inside clusters (gaps below 1e-7 ||T||), sigma^2 = z^T T z
-//   S6  back-transformation V = Q Z (each wave owns four columns: no barriers), output W = V Sigma
+//   S6  back-transformation V = Q Z: blocks of 16 reflectors in compact WY form on the matrix
+//       cores, V in the accumulators throughout; output W = V Sigma
 // The output follows the QR-preconditioned register Jacobi's contract (TwoSiteJob::qr = 1): work
 // column c (length C, rows in X's column order) = right singular vector c of X times sigma_c, sig[c]
 // = sigma_c (0 for c >= K), so rank / split are unchanged.
@@ -393,26 +394,32 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
       h ^= h >> 15;
       zb[row * 64 + i] = (double)(h & 0xFFFFFu) * (2.0 / 1048576.0) - 1.0;
     }
-    for (int it = 0; it < 3; ++it) {
-      // L D L^T = T - lam I (no pivoting; tiny pivots -> +-eps ||T||); forward solve in place
-      double rdp = 0.0, yp = 0.0;
+    // L D L^T = T - lam I once (no pivoting; tiny pivots -> +-eps ||T||): 1 / D_row to Db
+    {
+      double rdp = 0.0;
       for (int row = 0; row < C; ++row) {
         double dj = s_d[row] - lam;
-        double y = zb[row * 64 + i];
-        if (row > 0) {
-          dj -= s_e2[row - 1] * rdp;
-          y -= s_e[row - 1] * rdp * yp;
-        }
+        if (row > 0) dj -= s_e2[row - 1] * rdp;
         if (fabs(dj) < piv) dj = dj >= 0.0 ? piv : -piv;
         const double rd = rcp_nr(dj);
-        zb[row * 64 + i] = y;
         Db[row * 64 + i] = rd;
         rdp = rd;
+      }
+    }
+    for (int it = 0; it < 3; ++it) {
+      // forward solve L y = z in place (L_{row, row-1} = e_{row-1} / D_{row-1}), then L^T-solve
+      // z = D^-1 y - L^T z from the bottom
+      double yp = zb[0 * 64 + i];
+#pragma unroll 8
+      for (int row = 1; row < C; ++row) {
+        const double y = zb[row * 64 + i] - s_e[row - 1] * Db[(row - 1) * 64 + i] * yp;
+        zb[row * 64 + i] = y;
         yp = y;
       }
       double zn = zb[(C - 1) * 64 + i] * Db[(C - 1) * 64 + i];
       zb[(C - 1) * 64 + i] = zn;
       double n2 = zn * zn;
+#pragma unroll 8
       for (int row = C - 2; row >= 0; --row) {
         zn = (zb[row * 64 + i] - s_e[row] * zn) * Db[row * 64 + i];
         zb[row * 64 + i] = zn;
@@ -461,90 +468,179 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
   }
   __syncthreads();
   tick(3);
-  // ---- S6: V = Q Z.  Wave w owns columns 4w .. 4w + 3 whole: lane l holds column 4w + (l & 3),
-  // rows (l >> 2) + 16 m (m < 8), so every reflector's dot products reduce inside the wave (DPP
-  // row rotations + two cross-row shuffles) -- no LDS, no barrier, each wave runs on its own ----
-  const int jc = 4 * wave + (lane & 3), rb = lane >> 2;
-  cplx V[8];
+  // ---- S6: V = Q Z on the matrix cores, 16 reflectors at a time in compact WY form (LAPACK
+  // zlarft / zlarfb, forward, columnwise): H_k0 ... H_k0+15 = I - Y T Y^H, V <- V - Y (T (Y^H V)),
+  // blocks from the last reflectors down.  V (C x 64) is 8 x 4 tiles of 16 x 16 in the MFMA
+  // accumulator layout: wave w holds column tile w & 3 and row tiles 2 (w >> 2), 2 (w >> 2) + 1
+  // (lane l: column l & 15, rows (l >> 4) + 4 q) -- which is also the B-operand layout of Y^H V, so
+  // V never leaves the registers.  Per block: Y^H V as four partial products per column tile
+  // (summed through the LDS), S = Y^H Y on the same A operands (four waves), T by the
+  // zlarft recurrence in one wave, W2 = T (Y^H V) on the VALU, V -= Y W2; five barriers. ----
+  const int nt = wave & 3, mg = wave >> 2, li = lane & 15, lk = lane >> 4;
+  aqc::d4_t vre[2], vim[2];
 #pragma unroll
-  for (int m = 0; m < 8; ++m) {
-    const int row = rb + 16 * m;
-    V[m] = aqc::cmk((jc < K && row < C) ? zb[row * 64 + jc] : 0.0, 0.0);
+  for (int t = 0; t < 2; ++t) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int row = 32 * mg + 16 * t + lk + 4 * q, col = 16 * nt + li;
+      vre[t][q] = (row < C && col < K) ? zb[row * 64 + col] : 0.0;
+      vim[t][q] = 0.0;
+    }
   }
-  // the packed reflectors (<= 8128 complex = 127 KiB) move into the LDS once: every wave reads
-  // every reflector, and LDS reads are a few hundred cycles closer than L2 ones
+  // LDS (complex units): Y [128][16] (column index swizzled by row & 15: conflict-free reads along
+  // rows and along columns), Y^H V partials of waves 4..15, S partials of waves 0, 10, 15 (then T),
+  // Y^H V, W2 = T Y^H V, S
+  cplx* Yl = xbuf;
+  cplx* Pw = Yl + 2048;
+  cplx* Ps = Pw + 12 * 256;
+  cplx* W1l = Ps + 3 * 256;
+  cplx* W2l = W1l + 16 * 64;
+  cplx* Sl = W2l + 16 * 64;  // ends at 8192
+  cplx* Tl = Ps;             // [16][17], after wave 5 has read the S partials
+  auto fetch_y = [&](int k0, int nb, cplx (&y)[2]) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int e = tid + 1024 * u, row = e >> 4, i = e & 15, k = k0 + i;
+      y[u] = (i < nb && row > k && row < C) ? aqc::ldg(hh + (size_t)k * (2 * C - k - 1) / 2 + (row - k - 1))
+                                            : aqc::cmk(0, 0);
+    }
+  };
+  cplx ynx[2];
+  {
+    const int k1 = C - 1, k0 = k1 > 16 ? k1 - 16 : 0;
+    fetch_y(k0, k1 - k0, ynx);
+  }
   __syncthreads();  // V's initial values are read from zb: the LDS can be overwritten now
-  const int nhh = (C - 1) * C / 2;
-  cplx* hl = xbuf;
-  for (int e = tid; e < nhh; e += 1024) hl[e] = hh[e];
-  __syncthreads();
-  auto load_v = [&](int k, cplx (&dst)[8]) {
-    const cplx* v = hl + (size_t)k * (2 * C - k - 1) / 2;
+  for (int k1 = C - 1; k1 > 0; k1 -= 16) {
+    const int k0 = k1 > 16 ? k1 - 16 : 0, nb = k1 - k0;
 #pragma unroll
-    for (int m = 0; m < 8; ++m) {
-      const int row = rb + 16 * m;
-      dst[m] = (row > k && row < C) ? v[row - k - 1] : aqc::cmk(0, 0);
+    for (int u = 0; u < 2; ++u) {
+      const int e = tid + 1024 * u, row = e >> 4, i = e & 15;
+      Yl[row * 16 + (i ^ (row & 15))] = ynx[u];
     }
-  };
-  // sum over the 16 lanes sharing (l & 3): rotations by 4 and 8 inside a DPP row, then rows
-  auto col_sum = [&](double v) {  // (row_ror:8 first: the same bits in all 16 lanes, row_sum16)
-    v += aqc::dpp_perm<0x128>(v);  // row_ror:8
-    v += aqc::dpp_perm<0x124>(v);  // row_ror:4
-    v += __shfl_xor(v, 16);
-    v += __shfl_xor(v, 32);
-    return v;
-  };
-  if (wave * 4 < K) {  // uniform per wave
-    // Two reflectors per pass (compact WY): with u_1 = v_k, u_2 = v_{k-1} (application order),
-    // s_i = u_i^H V from the pass's V and c = u_2^H u_1,
-    //   s'_1 = s_1,  s'_2 = s_2 - tau_1 c s'_1,  V <- V - tau_1 u_1 s'_1 - tau_2 u_2 s'_2,
-    // so the three reductions of a pass run side by side (four reflectors per pass spill: the
-    // 32 complex of u need more than the 128 VGPRs a 1024-thread workgroup allows).
-    int k = C - 2;
-    for (; k >= 1; k -= 2) {
-      cplx u1[8], u2[8];
-      load_v(k, u1);
-      load_v(k - 1, u2);
-      cplx s1 = aqc::cmk(0, 0), s2 = aqc::cmk(0, 0), c21 = aqc::cmk(0, 0);
+    if (k0 > 0) {  // the next block's reflectors, in flight during this one
+      const int n1 = k0, n0 = n1 > 16 ? n1 - 16 : 0;
+      fetch_y(n0, n1 - n0, ynx);
+    }
+    __syncthreads();  // B1: Y
+    // Y^H V over this wave's 32 rows (and Y^H Y on the waves mg == nt, one per SIMD): A[m = i][k = row] = conj(Y[row][i])
+    aqc::d4_t wr = {0, 0, 0, 0}, wi = {0, 0, 0, 0}, sr = {0, 0, 0, 0}, si = {0, 0, 0, 0};
 #pragma unroll
-      for (int m = 0; m < 8; ++m) {
-        s1 = aqc::cfmac(u1[m], V[m], s1);
-        s2 = aqc::cfmac(u2[m], V[m], s2);
-        c21 = aqc::cfmac(u2[m], u1[m], c21);
+    for (int t = 0; t < 2; ++t) {
+      if (32 * mg + 16 * t + 15 > k0) {  // rows <= k0 of Y are zero (uniform per wave)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const int row = 32 * mg + 16 * t + 4 * s + lk;
+          const cplx y = Yl[row * 16 + (li ^ (row & 15))];
+          wr = __builtin_amdgcn_mfma_f64_16x16x4f64(y.x, vre[t][s], wr, 0, 0, 0);
+          wr = __builtin_amdgcn_mfma_f64_16x16x4f64(y.y, vim[t][s], wr, 0, 0, 0);
+          wi = __builtin_amdgcn_mfma_f64_16x16x4f64(y.x, vim[t][s], wi, 0, 0, 0);
+          wi = __builtin_amdgcn_mfma_f64_16x16x4f64(-y.y, vre[t][s], wi, 0, 0, 0);
+          if (mg == nt) {
+            sr = __builtin_amdgcn_mfma_f64_16x16x4f64(y.x, y.x, sr, 0, 0, 0);
+            sr = __builtin_amdgcn_mfma_f64_16x16x4f64(y.y, y.y, sr, 0, 0, 0);
+            si = __builtin_amdgcn_mfma_f64_16x16x4f64(y.x, y.y, si, 0, 0, 0);
+            si = __builtin_amdgcn_mfma_f64_16x16x4f64(-y.y, y.x, si, 0, 0, 0);
+          }
+        }
       }
-      s1.x = col_sum(s1.x);
-      s1.y = col_sum(s1.y);
-      s2.x = col_sum(s2.x);
-      s2.y = col_sum(s2.y);
-      c21.x = col_sum(c21.x);
-      c21.y = col_sum(c21.y);
-      const cplx t1 = aqc::cmul(s_tau[k], s1);
-      const cplx t2 = aqc::cmul(s_tau[k - 1], aqc::csub(s2, aqc::cmul(c21, t1)));
-#pragma unroll
-      for (int m = 0; m < 8; ++m) V[m] = aqc::csub(V[m], aqc::cfma(u2[m], t2, aqc::cmul(u1[m], t1)));
     }
-    for (; k >= 0; --k) {  // the last reflector of an odd count
-      const cplx tk = s_tau[k];
-      cplx vr[8];
-      load_v(k, vr);
-      cplx part = aqc::cmk(0, 0);
+    // D layout: row b = lk + 4 q (reflector), column li
+    if (mg > 0) {
 #pragma unroll
-      for (int m = 0; m < 8; ++m) part = aqc::cfmac(vr[m], V[m], part);  // conj(v) . V
-      part.x = col_sum(part.x);
-      part.y = col_sum(part.y);
-      const cplx ts = aqc::cmul(tk, part);
-#pragma unroll
-      for (int m = 0; m < 8; ++m) V[m] = aqc::csub(V[m], aqc::cmul(vr[m], ts));
+      for (int q = 0; q < 4; ++q) Pw[((mg - 1) * 4 + nt) * 256 + (lk + 4 * q) * 16 + li] = aqc::cmk(wr[q], wi[q]);
     }
+    if (mg == nt && mg != 1) {
+      const int slot = mg == 0 ? 0 : mg - 1;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) Ps[slot * 256 + (lk + 4 * q) * 16 + li] = aqc::cmk(sr[q], si[q]);
+    }
+    __syncthreads();  // B2: partials
+    if (mg == 0) {  // Y^H V of column tile nt
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int b = lk + 4 * q;
+        cplx w = aqc::cmk(wr[q], wi[q]);
+#pragma unroll
+        for (int m = 0; m < 3; ++m) w = aqc::cadd(w, Pw[(m * 4 + nt) * 256 + b * 16 + li]);
+        W1l[b * 64 + 16 * nt + li] = w;
+      }
+    } else if (wave == 5) {  // S, then T (zlarft: T[a][i] = -tau_i sum_{a <= b < i} T[a][b] S[b][i])
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int b = lk + 4 * q;
+        cplx sv = aqc::cmk(sr[q], si[q]);
+#pragma unroll
+        for (int m = 0; m < 3; ++m) sv = aqc::cadd(sv, Ps[m * 256 + b * 16 + li]);
+        Sl[b * 16 + li] = sv;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // LDS: S written, partials read
+      {  // lane (a, g): T[a][g + 4 m] (m < 4) in registers; each column's sum over b splits over
+         // the quad g = 0..3 (T[a][b] = 0 for b < a falls out of the recurrence)
+        const int a = lane >> 2, g = lane & 3;
+        cplx tq[4] = {aqc::cmk(0, 0), aqc::cmk(0, 0), aqc::cmk(0, 0), aqc::cmk(0, 0)};
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const cplx tau = i < nb ? s_tau[k0 + i] : aqc::cmk(0, 0);
+          cplx acc = aqc::cmk(0, 0);
+#pragma unroll
+          for (int m = 0; m < 4; ++m) {
+            if (4 * m < i) {
+              const int bb = g + 4 * m;
+              const cplx sv = bb < i ? Sl[bb * 16 + i] : aqc::cmk(0, 0);
+              acc = aqc::cfma(tq[m], sv, acc);
+            }
+          }
+          acc.x = aqc::row_sum4(acc.x);
+          acc.y = aqc::row_sum4(acc.y);
+          const cplx ti = aqc::cmul(tau, acc);
+          const cplx val = a < i ? aqc::cmk(-ti.x, -ti.y) : (a == i ? tau : aqc::cmk(0, 0));
+          if (g == (i & 3)) tq[i >> 2] = val;
+        }
+#pragma unroll
+        for (int m = 0; m < 4; ++m) Tl[a * 17 + g + 4 * m] = tq[m];
+      }
+    }
+    __syncthreads();  // B3: Y^H V, T
+    {  // W2 = T (Y^H V): row i = wave (uniform), column = lane
+      const int i = wave;
+      cplx acc = aqc::cmk(0, 0);
+      for (int bb = i; bb < 16; ++bb) acc = aqc::cfma(Tl[i * 17 + bb], W1l[bb * 64 + lane], acc);
+      W2l[i * 64 + lane] = acc;
+    }
+    __syncthreads();  // B4: W2
+    // V -= Y W2: A[m = row][k = b] = Y[row][b], B[k = b][n] = W2[b][n]
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      if (32 * mg + 16 * t + 15 > k0) {
+        const int row = 32 * mg + 16 * t + li;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const int b = 4 * s + lk;
+          const cplx y = Yl[row * 16 + (b ^ (row & 15))];
+          const cplx w = W2l[b * 64 + 16 * nt + li];
+          vre[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(-y.x, w.x, vre[t], 0, 0, 0);
+          vre[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(y.y, w.y, vre[t], 0, 0, 0);
+          vim[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(-y.x, w.y, vim[t], 0, 0, 0);
+          vim[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(-y.y, w.x, vim[t], 0, 0, 0);
+        }
+      }
+    }
+    __syncthreads();  // B5: Y, W2 and the partials are overwritten next block
   }
-  __syncthreads();  // the reflectors are dead: W overwrites them
   tick(4);
-  if (jc < K) {
-    const double sg = sqrt(s_sig2[jc]);
+  {  // the reflectors are dead (last read before B1 of the last block): W overwrites them
+    const int col = 16 * nt + li;
+    if (col < K) {
+      const double sg = sqrt(s_sig2[col]);
 #pragma unroll
-    for (int m = 0; m < 8; ++m) {
-      const int row = rb + 16 * m;
-      if (row < C) j.work[(size_t)jc * C + row] = aqc::cscale(V[m], sg);
+      for (int t = 0; t < 2; ++t) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int row = 32 * mg + 16 * t + lk + 4 * q;
+          if (row < C) j.work[(size_t)col * C + row] = aqc::cmk(vre[t][q] * sg, vim[t][q] * sg);
+        }
+      }
     }
   }
   for (int c = tid; c < C; c += 1024) j.sig[c] = c < K ? sqrt(s_sig2[c]) : 0.0;
