@@ -998,12 +998,12 @@ int aqc_pair_grads_batch(aqc_mps_t* psis, int ns, const double* svec, const int*
   }
   AQC_HIP_CHECK(hipEventRecord(gb.done, st));
   gb.pending = true;
+  // a host result is complete on return (one wait at the end, none before the launches); a
+  // device result is complete on this stream -- the caller joins its own (aqc_stream_join)
   if (!out_is_device && npairs) {
     AQC_HIP_CHECK(hipMemcpyAsync(out, dout, (size_t)ns * npairs * sizeof(double), hipMemcpyDeviceToHost, st));
+    AQC_HIP_CHECK(hipStreamSynchronize(st));
   }
-  // the result (host, or device memory that the caller reads on its own stream, e.g. the
-  // all-gather's) is complete on return: one wait at the end, none before the launches
-  AQC_HIP_CHECK(hipStreamSynchronize(st));
   return AQC_OK;
 }
 

@@ -14,7 +14,11 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <atomic>
+#include <cstdlib>
 #include <mutex>
+#include <thread>
+#include <unordered_set>
 
 #include "aqc_gemm.h"
 #include "mps_internal.h"
@@ -1577,6 +1581,39 @@ struct Scheduler {
   }
 };
 
+// Host-side per-state work (scheduling, job building) over a few threads: a batch of 1024 states
+// takes ~2 ms on one core, during which the GPU would idle.  AQC_HOST_THREADS overrides the count
+// (default 8; 1 = serial).  f(s) must touch only state s's data.
+template <class F>
+void parallel_states(int ns, F&& f) {
+  static const int kThreads = [] {
+    const char* e = std::getenv("AQC_HOST_THREADS");
+    const int v = e ? std::atoi(e) : 8;
+    return v < 1 ? 1 : (v > 64 ? 64 : v);
+  }();
+  const int nt = std::min(kThreads, ns / 32);
+  if (nt <= 1) {
+    for (int s = 0; s < ns; ++s) f(s);
+    return;
+  }
+  std::vector<std::thread> th;
+  th.reserve(nt - 1);
+  for (int t = 1; t < nt; ++t)
+    th.emplace_back([&f, t, nt, ns] {
+      for (int s = t; s < ns; s += nt) f(s);
+    });
+  for (int s = 0; s < ns; s += nt) f(s);
+  for (auto& x : th) x.join();
+}
+
+bool distinct_handles(aqc_mps_t* hs, int ns) {
+  std::unordered_set<const void*> seen;
+  seen.reserve(2 * ns);
+  for (int s = 0; s < ns; ++s)
+    if (!seen.insert(hs[s]).second) return false;
+  return true;
+}
+
 int validate_ops(aqc_mps_t h, const aqc_op_t* ops, int nops) {
   for (int i = 0; i < nops; ++i) {
     const aqc_op_t& o = ops[i];
@@ -1773,32 +1810,26 @@ std::vector<std::vector<const DevOp*>> level_ops(const std::vector<DevOp>& ops, 
 // first, so that the short ones fill in behind them).
 int run_chains(aqc_mps_t* hs, int ns, std::vector<std::vector<DevOp>>& lists, int cap_max) {
   hipStream_t st = aqc::mps_stream();
-  std::vector<TwoSiteJob> two;
-  std::vector<OneSiteJob> one;
-  std::vector<int> codes;
-  std::vector<std::pair<int, int>> rng(ns);
+  // per-state job counts -> offsets, then every state's jobs written straight into the staging
+  // buffer (states in parallel)
+  std::vector<size_t> off2(ns + 1, 0), off1(ns + 1, 0), offc(ns + 1, 0);
   for (int s = 0; s < ns; ++s) {
-    const int start = (int)codes.size();
-    for (const DevOp& op : lists[s]) {
-      if (op.kind == 2) {
-        two.push_back(make_two(hs[s], op, 0));
-        two.back().qr = 1;
-        codes.push_back((int)two.size() - 1);
-      } else {
-        one.push_back(make_one(hs[s], op));
-        codes.push_back(-(int)one.size());
-      }
-    }
-    rng[s] = {start, (int)codes.size() - start};
+    size_t n2 = 0;
+    for (const DevOp& op : lists[s]) n2 += op.kind == 2;
+    off2[s + 1] = off2[s] + n2;
+    off1[s + 1] = off1[s] + (lists[s].size() - n2);
+    offc[s + 1] = offc[s] + lists[s].size();
   }
-  if (codes.empty()) return AQC_OK;
+  const size_t n_two = off2[ns], n_one = off1[ns], n_codes = offc[ns];
+  if (n_codes == 0) return AQC_OK;
   std::vector<int> order(ns);
   for (int s = 0; s < ns; ++s) order[s] = s;
-  std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return rng[a].second > rng[b].second; });
+  std::stable_sort(order.begin(), order.end(),
+                   [&](int a, int b) { return lists[a].size() > lists[b].size(); });
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
-  const size_t o_two = 0, o_one = al(o_two + two.size() * sizeof(TwoSiteJob));
-  const size_t o_codes = al(o_one + one.size() * sizeof(OneSiteJob));
-  const size_t o_chain = al(o_codes + codes.size() * sizeof(int));
+  const size_t o_two = 0, o_one = al(o_two + n_two * sizeof(TwoSiteJob));
+  const size_t o_codes = al(o_one + n_one * sizeof(OneSiteJob));
+  const size_t o_chain = al(o_codes + n_codes * sizeof(int));
   const size_t total = o_chain + (size_t)ns * sizeof(ChainJob);
   StagingLease lease(st);
   if (lease.rc() != AQC_OK) return lease.rc();
@@ -1807,18 +1838,31 @@ int run_chains(aqc_mps_t* hs, int ns, std::vector<std::vector<DevOp>>& lists, in
   if (rc != AQC_OK) return rc;
   char* hb = (char*)sg.host;
   char* db = (char*)sg.dev;
-  if (!two.empty()) std::memcpy(hb + o_two, two.data(), two.size() * sizeof(TwoSiteJob));
-  if (!one.empty()) std::memcpy(hb + o_one, one.data(), one.size() * sizeof(OneSiteJob));
-  std::memcpy(hb + o_codes, codes.data(), codes.size() * sizeof(int));
+  TwoSiteJob* h2 = (TwoSiteJob*)(hb + o_two);
+  OneSiteJob* h1 = (OneSiteJob*)(hb + o_one);
+  int* hcode = (int*)(hb + o_codes);
+  parallel_states(ns, [&](int s) {
+    size_t i2 = off2[s], i1 = off1[s], ic = offc[s];
+    for (const DevOp& op : lists[s]) {
+      if (op.kind == 2) {
+        h2[i2] = make_two(hs[s], op, 0);
+        h2[i2].qr = 1;
+        hcode[ic++] = (int)i2++;
+      } else {
+        h1[i1] = make_one(hs[s], op);
+        hcode[ic++] = -(int)(++i1);
+      }
+    }
+  });
   ChainJob* hc = (ChainJob*)(hb + o_chain);
   for (int k = 0; k < ns; ++k) {
     const int s = order[k];
-    hc[k].ops = (const int*)(db + o_codes) + rng[s].first;
-    hc[k].nops = rng[s].second;
+    hc[k].ops = (const int*)(db + o_codes) + offc[s];
+    hc[k].nops = (int)lists[s].size();
     hc[k].pad = 0;
   }
   AQC_HIP_CHECK(hipMemcpyAsync(sg.dev, sg.host, total, hipMemcpyHostToDevice, st));
-  const double c = cap_max, nj = (double)two.size();
+  const double c = cap_max, nj = (double)n_two;
   // algorithmic: the two sites' Gammas in and out; nominal SVD + theta + split flops
   aqc::KernelTimer::begin(st, "mps_chain", nj * 8.0 * c * c * 16, nj * (84.0 * 8.0 + 64.0) * c * c * c);
   hipLaunchKernelGGL(k_chain, dim3(ns), dim3(1024), kChainLds, st, (const ChainJob*)(db + o_chain),
@@ -1829,6 +1873,14 @@ int run_chains(aqc_mps_t* hs, int ns, std::vector<std::vector<DevOp>>& lists, in
 }
 
 int run_waves(aqc_mps_t* hs, int ns, std::vector<std::vector<DevOp>>& lists) {
+  for (int s = 0; s < ns; ++s) {  // every Gamma these lists write (reload bookkeeping)
+    int lo = 1 << 30, hi = -1;
+    for (const DevOp& op : lists[s]) {
+      lo = std::min(lo, op.p);
+      hi = std::max(hi, op.kind == 2 ? op.p + 1 : op.p);
+    }
+    if (hi >= 0) hs[s]->changed(lo, hi);
+  }
   {
     int cap_max = 0;
     for (int s = 0; s < ns; ++s) cap_max = std::max(cap_max, hs[s]->d.cap);
@@ -2022,13 +2074,20 @@ bool is_sorted_order(aqc_mps_t h) {
   return true;
 }
 
-int do_sort(aqc_mps_t* hs, int ns) {
-  std::vector<std::vector<DevOp>> lists(ns);
-  for (int s = 0; s < ns; ++s) {
-    Scheduler sc(hs[s]->d.n, hs[s]->order, hs[s]->loc, lists[s]);
+// Moves every state to sorted qubit order; *moved = number of states that needed swaps.
+int do_sort(aqc_mps_t* hs, int ns, int* moved = nullptr) {
+  std::vector<aqc_mps_t> todo;
+  for (int s = 0; s < ns; ++s)
+    if (!is_sorted_order(hs[s])) todo.push_back(hs[s]);
+  if (moved) *moved = (int)todo.size();
+  if (todo.empty()) return AQC_OK;
+  const int nt = (int)todo.size();
+  std::vector<std::vector<DevOp>> lists(nt);
+  for (int s = 0; s < nt; ++s) {
+    Scheduler sc(todo[s]->d.n, todo[s]->order, todo[s]->loc, lists[s]);
     sc.sort();
   }
-  return run_waves(hs, ns, lists);
+  return run_waves(todo.data(), nt, lists);
 }
 
 MeasJob make_meas(aqc_mps_t h, cplx* out) {
@@ -2068,6 +2127,8 @@ int aqc_mps_create(int n, int chi_cap, double threshold, int max_chi, aqc_mps_t*
   AQC_REQUIRE(n >= 1 && n <= 4096, "aqc_mps_create: bad n");
   AQC_REQUIRE(chi_cap >= 1 && chi_cap <= 256, "aqc_mps_create: chi_cap must be in [1, 256]");
   auto* h = new aqc_mps_s();
+  static std::atomic<unsigned long long> next_uid{1};
+  h->uid = next_uid++;
   h->d.n = n;
   h->d.cap = chi_cap;
   h->thr = threshold;
@@ -2310,6 +2371,7 @@ int aqc_mps_set_vidal(aqc_mps_t h, const int* dims, const double* gammas, const 
   AQC_HIP_CHECK(hipMemcpy(h->d.lam, l.data(), l.size() * sizeof(double), hipMemcpyHostToDevice));
   AQC_HIP_CHECK(hipMemcpy(h->d.dims, dims, (n + 1) * sizeof(int), hipMemcpyHostToDevice));
   for (int i = 0; i < n; ++i) h->order[i] = h->loc[i] = i;
+  h->changed_all();
   return AQC_OK;
 }
 
@@ -2331,9 +2393,10 @@ int aqc_mps_sort(aqc_mps_t h) {
 
 int aqc_mps_sort_batch(aqc_mps_t* hs, int ns) {
   AQC_REQUIRE(hs && ns >= 0, "aqc_mps_sort_batch: bad arguments");
-  int rc = do_sort(hs, ns);
+  int moved = 0;
+  int rc = do_sort(hs, ns, &moved);
   if (rc != AQC_OK) return rc;
-  return check_flags_batch(hs, ns);
+  return moved ? check_flags_batch(hs, ns) : AQC_OK;  // (no update ran: no flag can have risen)
 }
 
 int aqc_mps_get_vidal(aqc_mps_t h, int* dims, double* gammas, double* lambdas) {
@@ -2394,10 +2457,19 @@ int aqc_mps_copy_batch(aqc_mps_t* dst, const aqc_mps_t* src, int ns) {
     AQC_REQUIRE(dst[s] && src[s] && dst[s]->d.n == src[s]->d.n && dst[s]->d.cap == src[s]->d.cap,
                 "aqc_mps_copy_batch: handle mismatch");
     const size_t cap = src[s]->d.cap, n = src[s]->d.n;
+    aqc_mps_s* d = dst[s];
+    const aqc_mps_s* r = src[s];
+    // Gamma sites to copy: all, or -- when dst was last copied from this source and the source
+    // has not changed since -- only the sites dst has rewritten since then
+    size_t lo = 0, cnt = n;
+    if (d != r && d->synced_src == r->uid && d->synced_ver == r->version) {
+      lo = d->dirty_hi >= d->dirty_lo ? (size_t)d->dirty_lo : 0;
+      cnt = d->dirty_hi >= d->dirty_lo ? (size_t)(d->dirty_hi - d->dirty_lo + 1) : 0;
+    }
     CopyJob& j = jobs[s];
-    j.sg = src[s]->d.gam;
-    j.dg = dst[s]->d.gam;
-    j.ng = n * 2 * cap * cap;
+    j.sg = r->d.gam + lo * 2 * cap * cap;
+    j.dg = d->d.gam + lo * 2 * cap * cap;
+    j.ng = cnt * 2 * cap * cap;
     j.sl = src[s]->d.lam;
     j.dl = dst[s]->d.lam;
     j.nl = (n + 1) * cap;
@@ -2405,23 +2477,46 @@ int aqc_mps_copy_batch(aqc_mps_t* dst, const aqc_mps_t* src, int ns) {
     j.dd = dst[s]->d.dims;
     j.nd = (int)n + 1;
     j.pad = 0;
-    dst[s]->order = src[s]->order;
-    dst[s]->loc = src[s]->loc;
+    d->order = r->order;
+    d->loc = r->loc;
+    d->synced_src = r->uid;
+    d->synced_ver = r->version;
+    d->dirty_lo = 1 << 30;
+    d->dirty_hi = -1;
+    ++d->version;
   }
   hipStream_t st = aqc::mps_stream();
-  Staging& sg = staging();
-  AQC_HIP_CHECK(hipStreamSynchronize(st));  // staging may still feed earlier launches
+  StagingLease lease(st);  // (the ring: no wait for the stream's earlier work)
+  if (lease.rc() != AQC_OK) return lease.rc();
+  Staging& sg = lease.buf();
   const size_t bytes = jobs.size() * sizeof(CopyJob);
   int rc = ensure_staging(sg, bytes);
   if (rc != AQC_OK) return rc;
   std::memcpy(sg.host, jobs.data(), bytes);
   AQC_HIP_CHECK(hipMemcpyAsync(sg.dev, sg.host, bytes, hipMemcpyHostToDevice, st));
-  const size_t words = jobs[0].ng;
+  size_t words = jobs[0].nl / 2, moved = 0;
+  for (const CopyJob& j : jobs) {
+    words = std::max(words, j.ng);
+    moved += j.ng * 16 + j.nl * 8;
+  }
   const int chunks = (int)std::min<size_t>(64, (words + 8 * kT - 1) / (8 * kT));
-  aqc::KernelTimer::begin(st, "mps_copy", 2.0 * ns * (words * 16.0 + jobs[0].nl * 8.0), 0.0);
+  aqc::KernelTimer::begin(st, "mps_copy", 2.0 * (double)moved, 0.0);
   hipLaunchKernelGGL(k_copy_batch, dim3(std::max(chunks, 1), ns), dim3(kT), 0, st, (const CopyJob*)sg.dev);
   aqc::KernelTimer::end(st);
   AQC_CHECK_LAUNCH();
+  return AQC_OK;
+}
+
+int aqc_stream_join(void* stream) {
+  static std::mutex mu;
+  static hipEvent_t ev[64] = {nullptr};
+  int dev = 0;
+  AQC_HIP_CHECK(hipGetDevice(&dev));
+  AQC_REQUIRE(dev >= 0 && dev < 64, "aqc_stream_join: device index out of range");
+  std::lock_guard<std::mutex> lk(mu);
+  if (!ev[dev]) AQC_HIP_CHECK(hipEventCreateWithFlags(&ev[dev], hipEventDisableTiming));
+  AQC_HIP_CHECK(hipEventRecord(ev[dev], aqc::mps_stream()));
+  AQC_HIP_CHECK(hipStreamWaitEvent((hipStream_t)stream, ev[dev], 0));
   return AQC_OK;
 }
 
@@ -2434,6 +2529,13 @@ int aqc_mps_copy(aqc_mps_t dst, const aqc_mps_t src) {
   AQC_HIP_CHECK(hipMemcpyAsync(dst->d.dims, src->d.dims, (n + 1) * sizeof(int), hipMemcpyDeviceToDevice, st));
   dst->order = src->order;
   dst->loc = src->loc;
+  if (dst != src) {
+    dst->synced_src = src->uid;
+    dst->synced_ver = src->version;
+    dst->dirty_lo = 1 << 30;
+    dst->dirty_hi = -1;
+    ++dst->version;
+  }
   return AQC_OK;
 }
 
@@ -2445,7 +2547,11 @@ int apply_batch_impl(aqc_mps_t* hs, int ns, const aqc_op_t* const* ops, const in
     int rc = validate_ops(hs[s], ops[s], nops[s]);
     if (rc != AQC_OK) return rc;
   }
-  for (int s = 0; s < ns; ++s) schedule(hs[s], ops[s], nops[s], sort_after, lists[s]);
+  if (distinct_handles(hs, ns)) {
+    parallel_states(ns, [&](int s) { schedule(hs[s], ops[s], nops[s], sort_after, lists[s]); });
+  } else {  // a state listed twice: its op lists apply in order
+    for (int s = 0; s < ns; ++s) schedule(hs[s], ops[s], nops[s], sort_after, lists[s]);
+  }
   int rc = run_waves(hs, ns, lists);
   if (rc != AQC_OK) return rc;
   return check_flags_batch(hs, ns);

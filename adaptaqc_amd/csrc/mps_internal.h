@@ -161,6 +161,24 @@ struct aqc_mps_s {
   int max_chi = 0;
   std::vector<int> order;  // site -> qubit
   std::vector<int> loc;    // qubit -> site
+  // Reload bookkeeping (aqc_mps_copy_batch): `version` changes with every change of the device
+  // contents; after a copy from the handle with id `synced_src` at its version `synced_ver`, the
+  // Gamma sites changed since are [dirty_lo, dirty_hi], so a reload from the same, unchanged
+  // source rewrites only those (lambdas and dims in full): the result is that of a full copy.
+  unsigned long long uid = 0;
+  unsigned long long version = 0;
+  unsigned long long synced_src = 0;
+  unsigned long long synced_ver = 0;
+  int dirty_lo = 1 << 30, dirty_hi = -1;
+  void changed(int lo, int hi) {  // Gamma sites lo..hi rewritten
+    ++version;
+    dirty_lo = lo < dirty_lo ? lo : dirty_lo;
+    dirty_hi = hi > dirty_hi ? hi : dirty_hi;
+  }
+  void changed_all() {
+    ++version;
+    synced_src = 0;
+  }
   // scratch for the candidate sweep (grad.hip), allocated lazily
   aqc::cplx* gw = nullptr;
   size_t gw_bytes = 0;

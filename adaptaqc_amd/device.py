@@ -255,7 +255,9 @@ def overlap_zero_batch(states):
 
 
 def pair_grads_batch(states, svec, pairs, u0, gens, degs, out=None):
-    """Per-state gradient norms for every pair; ``out`` may be a device pointer (int)."""
+    """Per-state gradient norms for every pair; ``out`` may be a device pointer (int): then the call
+    returns once the work is queued, and torch's current stream is ordered after it
+    (aqc_stream_join), so torch ops on ``out`` (the all-gather, the arg-max) see the scores."""
     l = _lib.lib()
     svec = np.ascontiguousarray(np.asarray(svec, dtype=np.complex128).reshape(-1))
     pairs = np.ascontiguousarray(np.asarray(pairs, dtype=np.int32).reshape(-1))
@@ -275,4 +277,8 @@ def pair_grads_batch(states, svec, pairs, u0, gens, degs, out=None):
             _lib.ptr(gens) if ngen else None, _lib.ptr(degs) if ngen else None, ngen, outp, is_dev,
         )
     )
+    if is_dev:
+        import torch
+
+        _lib.check(l.aqc_stream_join(ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)))
     return host

@@ -79,9 +79,14 @@ def gather_scores(local_scores, shard: PairShard, group=None, nstates: int = 1):
     else:
         gathered = buf.unsqueeze(0)
     full = torch.empty((nstates, len(shard.coupling_map)), dtype=torch.float64, device=dev)
-    for r, idx in enumerate(shard.index_lists):
+    # the index lists go to the device once per shard and device: a fresh host->device copy here
+    # would wait for the scores' producer (the sweep) and stall the host every step
+    cache = shard.__dict__.setdefault("_index_dev", {})
+    if dev not in cache:
+        cache[dev] = [torch.as_tensor(idx, device=dev) if idx else None for idx in shard.index_lists]
+    for r, (idx, di) in enumerate(zip(shard.index_lists, cache[dev])):
         if idx:
-            full[:, torch.as_tensor(idx, device=dev)] = gathered[r, :, : len(idx)]
+            full[:, di] = gathered[r, :, : len(idx)]
     return full
 
 

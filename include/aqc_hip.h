@@ -183,7 +183,10 @@ int aqc_mps_amps_hw1(aqc_mps_t h, double* out);
  *   g_p = sqrt( sum_k degs[k] * ( -Im( <s|G_k|psi> <psi|U0^dag|s> ) )^2 )
  * |s> is the product state with per-qubit 2-vectors svec[n][2] (complex); u0 and gens are
  * 4x4 (little-endian over (control, target)) matrices of U0 and G_k (NOT their inverses).
- * out: npairs doubles; out_is_device != 0 means `out` is a device pointer (for RCCL). */
+ * out: npairs doubles; out_is_device != 0 means `out` is a device pointer (for RCCL).
+ * With a host `out` the call returns when the scores are there; with a device `out` it returns
+ * once the work is queued on the library's stream: aqc_stream_join orders another stream (the
+ * caller's, e.g. the all-gather's) after it. */
 int aqc_pair_grads(aqc_mps_t psi, const double* svec, const int* pairs, int npairs,
                    const double* u0, const double* gens, const double* degs, int ngen,
                    double* out, int out_is_device);
@@ -195,6 +198,9 @@ int aqc_pair_grads_batch(aqc_mps_t* psis, int nstates, const double* svec, const
  * state), 1 = one chain per workgroup, 2 = grouped whenever the capacity allows.  Results are the
  * same up to floating-point summation order. */
 int aqc_sweep_set_chain_mode(int mode);
+/* Orders `stream` (a hipStream_t of the current device; NULL = the legacy default stream) after
+   everything queued so far on the library's stream of that device, without a host wait. */
+int aqc_stream_join(void* stream);
 /* Best product-state (chi = 1) approximation of psi: the starting circuit
  * starting_circuit="tenpy_product_state" (approximate_compiler.py:222-242, which compresses with
  * tenpy's variational method: trunc_params chi_max = 1, min_sweeps 10, max_sweeps 50).  Alternating
