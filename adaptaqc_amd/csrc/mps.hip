@@ -1112,66 +1112,94 @@ __device__ unsigned long long g_chain_ticks[5];
 
 // The phases are separate (non-inlined) functions: inlined into one loop body the compiler kept
 // values live across them and spilled hundreds of bytes per lane inside the Jacobi rounds.
-// theta in the chain: k_theta's register-light VALU tiles (16 x 16 outputs with all four P's and
-// the gate mix in registers: no second pass over theta), sub-group sg of 256 threads taking tiles
-// sg, sg + 4, ...; every sub-group runs the same number of tiles and k steps so that the barriers
-// pair up.  (An MFMA form on aqc::block_cgemm needs more than the chain's 128 VGPRs per lane and
-// spilled inside its k loop: 118 us per update.)
+// theta in the chain on the VALU: sub-group sg of 256 threads computes the 32 x 32 output quadrant
+// (l0, r0) = 32 (sg >> 1, sg & 1) of all four P_{s1 s2} = (ll lm Gamma_p[s1]) (Gamma_q[s2] lr),
+// thread (ty, tx) = (lt / 16, lt % 16) rows l0 + tx + 16 i, columns r0 + ty + 16 jj (i, jj < 2):
+// 16 complex accumulators, 8 LDS reads per 64 FMAs (one output per thread read 4 per 16 and was
+// LDS-bound), then the gate mix in registers and coalesced theta writes (lanes along l).  Every
+// sub-group runs the same m steps, so the barriers pair up.  (An MFMA form needs more than the
+// chain's 128 VGPRs per lane: four P's of a quadrant are 16 accumulator tiles.)
+constexpr int kThetaLds = 2 * 32 * 9 + 2 * 8 * 33;  // complex per sub-group
+static_assert(4 * kThetaLds * 16 <= kChainLdsBytes, "theta staging exceeds the chain's LDS");
 __device__ __forceinline__ void chain_theta(const TwoSiteJob& j) {
   extern __shared__ double2 xbuf[];
   const int tid = fresh_tid(), sg = tid >> 8, lt = tid & 255;
-  cplx (*As)[16][17] = reinterpret_cast<cplx (*)[16][17]>(xbuf + sg * (4 * 16 * 17));
-  cplx (*Bs)[16][17] = As + 2;
+  cplx* base = xbuf + sg * kThetaLds;
+  cplx (*As)[32][9] = reinterpret_cast<cplx (*)[32][9]>(base);
+  cplx (*Bs)[8][33] = reinterpret_cast<cplx (*)[8][33]>(base + 2 * 32 * 9);
   const int chl = j.dims[0], chm = j.dims[1], chr = j.dims[2];
   const int cap = j.cap;
-  const int tiles_r = (cap + 15) / 16, ntiles = tiles_r * tiles_r;
-  const int ty = lt / 16, tx = lt % 16;
   const size_t half = (size_t)cap * cap;
   const int M = 2 * chl;
-  for (int t0 = 0; t0 < ntiles; t0 += 4) {
-    const int t = t0 + sg;
-    const int l0 = (t / tiles_r) * 16, r0 = (t % tiles_r) * 16;
-    const bool active = t < ntiles && l0 < chl && r0 < chr;
-    const int l = l0 + ty, r = r0 + tx;
-    cplx acc[4];
+  const int l0 = 32 * (sg >> 1), r0 = 32 * (sg & 1);
+  const bool active = l0 < chl && r0 < chr;
+  const int ty = lt >> 4, tx = lt & 15;
+  cplx acc[4][2][2];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) acc[i] = aqc::cmk(0, 0);
-    const double lll = active && l < chl ? j.ll[l] : 0.0;
-    const double lrr = active && r < chr ? j.lr[r] : 0.0;
-    for (int m0 = 0; m0 < chm; m0 += 16) {
-      const int ma = m0 + tx, mb = m0 + ty;
+  for (int q = 0; q < 4; ++q)
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        cplx a = aqc::cmk(0, 0), b = aqc::cmk(0, 0);
-        if (active && l < chl && ma < chm) a = aqc::cscale(j.gp[s * half + (size_t)l * cap + ma], lll * j.lm[ma]);
-        if (active && mb < chm && r < chr) b = aqc::cscale(j.gq[s * half + (size_t)mb * cap + r], lrr);
-        As[s][ty][tx] = a;
-        Bs[s][ty][tx] = b;
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) acc[q][i][jj] = aqc::cmk(0, 0);
+  for (int m0 = 0; m0 < chm; m0 += 8) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int e = lt + 256 * u, s = e >> 8;
+      {  // A: 8 consecutive m of one row per 8 lanes
+        const int row = (e >> 3) & 31, mm = e & 7, l = l0 + row, m = m0 + mm;
+        cplx a = aqc::cmk(0, 0);
+        if (active && l < chl && m < chm) a = aqc::cscale(j.gp[s * half + (size_t)l * cap + m], j.ll[l] * j.lm[m]);
+        As[s][row][mm] = a;
       }
-      __syncthreads();
-      if (active) {
-#pragma unroll 4
-        for (int mm = 0; mm < 16; ++mm) {
-          const cplx a0 = As[0][ty][mm], a1 = As[1][ty][mm];
-          const cplx b0 = Bs[0][mm][tx], b1 = Bs[1][mm][tx];
-          acc[0] = aqc::cfma(a0, b0, acc[0]);
-          acc[1] = aqc::cfma(a0, b1, acc[1]);
-          acc[2] = aqc::cfma(a1, b0, acc[2]);
-          acc[3] = aqc::cfma(a1, b1, acc[3]);
+      {  // B: 32 consecutive r of one row per 32 lanes
+        const int mm = (e >> 5) & 7, col = e & 31, m = m0 + mm, r = r0 + col;
+        cplx b = aqc::cmk(0, 0);
+        if (active && m < chm && r < chr) b = aqc::cscale(j.gq[s * half + (size_t)m * cap + r], j.lr[r]);
+        Bs[s][mm][col] = b;
+      }
+    }
+    __syncthreads();
+    if (active) {
+#pragma unroll 2
+      for (int mm = 0; mm < 8; ++mm) {
+        cplx av[2][2], bv[2][2];
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+          for (int i = 0; i < 2; ++i) {
+            av[s][i] = As[s][tx + 16 * i][mm];
+            bv[s][i] = Bs[s][mm][ty + 16 * i];
+          }
+#pragma unroll
+        for (int s1 = 0; s1 < 2; ++s1)
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+              for (int jj = 0; jj < 2; ++jj)
+                acc[2 * s1 + s2][i][jj] = aqc::cfma(av[s1][i], bv[s2][jj], acc[2 * s1 + s2][i][jj]);
+      }
+    }
+    __syncthreads();
+  }
+  if (active) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        const int l = l0 + tx + 16 * i, r = r0 + ty + 16 * jj;
+        if (l < chl && r < chr) {
+#pragma unroll
+          for (int o = 0; o < 4; ++o) {
+            cplx v = aqc::cmul(j.G[o * 4 + 0], acc[0][i][jj]);
+            v = aqc::cfma(j.G[o * 4 + 1], acc[1][i][jj], v);
+            v = aqc::cfma(j.G[o * 4 + 2], acc[2][i][jj], v);
+            v = aqc::cfma(j.G[o * 4 + 3], acc[3][i][jj], v);
+            j.theta[(size_t)((o & 1) * chr + r) * M + (o >> 1) * chl + l] = v;
+          }
         }
       }
-      __syncthreads();
-    }
-    if (active && l < chl && r < chr) {
-#pragma unroll
-      for (int o = 0; o < 4; ++o) {
-        cplx v = aqc::cmul(j.G[o * 4 + 0], acc[0]);
-        v = aqc::cfma(j.G[o * 4 + 1], acc[1], v);
-        v = aqc::cfma(j.G[o * 4 + 2], acc[2], v);
-        v = aqc::cfma(j.G[o * 4 + 3], acc[3], v);
-        j.theta[(size_t)((o & 1) * chr + r) * M + (o >> 1) * chl + l] = v;
-      }
-    }
   }
 }
 // the register Jacobi is the chain's fallback (Gram path off or refused): a real call, so that

@@ -9,8 +9,9 @@
 //   S3  Householder tridiagonalisation G = Q T Q^H (LAPACK zhetd2, lower): two barriers per column,
 //       the column, the reflector and p = tau G v in double-buffered LDS vectors (zeros at and
 //       above the diagonal: a mask-free rank-2 update), the reflectors packed into the work buffer
-//   S4  the top K eigenvalues of the real symmetric tridiagonal T by 17-section: 16 lanes per
-//       eigenvalue each evaluate one Sturm count, one ballot picks the subinterval (8 rounds)
+//   S4  the top K eigenvalues of the real symmetric tridiagonal T: one 1024-point Sturm pass and
+//       a binary search bracket each, then 17-section (16 lanes per eigenvalue each evaluate one
+//       Sturm count, one ballot picks the subinterval; 6 rounds)
 //   S5  inverse iteration (unpivoted LDL^T of T - lambda I, three solves) per eigenvector, Gram-
 //       Schmidt inside clusters (gaps below 1e-7 ||T||), sigma^2 = z^T T z
 //   S6  back-transformation V = Q Z: blocks of 16 reflectors in compact WY form on the matrix
@@ -247,10 +248,13 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
       tau = triv ? aqc::cmk(0, 0) : aqc::cmk((beta - alpha.x) * ib, -alpha.y * ib);
       const cplx scl = triv ? aqc::cmk(0, 0) : aqc::cmk(dr * id2, -di * id2);  // 1 / (alpha - beta)
       // the own row's reflector k - 1 entries, w_r, and reflector k's column entry
+      // (the Hermitian rank-2 update needs only Re(a2): v w^H + w v^H = v p^H + (p + 2 Re(a2) v) v^H,
+      // so no per-column w_c)
       const cplx vr = vbb[bp * 128 + r], pr = pvb[bp * 128 + r], zr = zvb[bp * 128 + r];
-      const cplx wr = aqc::cfma(a2, vr, pr);
+      const double a2r2 = 2.0 * a2.x;
+      const cplx wr = aqc::cmk(fma(a2r2, vr.x, pr.x), fma(a2r2, vr.y, pr.y));
       const double nvx = -vr.x, nvy = -vr.y, nwx = -wr.x, nwy = -wr.y, nsx = -s.x, nsy = -s.y;
-      // one pass: g -= v_r conj(w_c) + w_r conj(v_c) (reflector k - 1), acc += g x_c (reflector k)
+      // one pass: g -= v_r conj(p_c) + w_r conj(v_c) (reflector k - 1), acc += g x_c (reflector k)
       cplx acc = aqc::cmk(0, 0);
 #pragma unroll
       for (int gi = 0; gi < 4; ++gi) {
@@ -260,9 +264,8 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
             const int i = 4 * gi + ii;
             const int c = q + 8 * i;
             const cplx vc = vbb[bp * 128 + c], pc = pvb[bp * 128 + c], zc = zvb[bp * 128 + c];
-            const cplx wc = aqc::cfma(a2, vc, pc);
-            g[i].x = fma(nvx, wc.x, fma(nvy, wc.y, fma(nwx, vc.x, fma(nwy, vc.y, g[i].x))));
-            g[i].y = fma(nvy, wc.x, fma(vr.x, wc.y, fma(nwy, vc.x, fma(wr.x, vc.y, g[i].y))));
+            g[i].x = fma(nvx, pc.x, fma(nvy, pc.y, fma(nwx, vc.x, fma(nwy, vc.y, g[i].x))));
+            g[i].y = fma(nvy, pc.x, fma(vr.x, pc.y, fma(nwy, vc.x, fma(wr.x, vc.y, g[i].y))));
             const cplx xc = aqc::cmk(fma(nsx, vc.x, fma(nsy, -vc.y, zc.x)), fma(nsx, vc.y, fma(nsy, vc.x, zc.y)));
             acc = aqc::cfma(g[i], xc, acc);
             if (ii == 1) __builtin_amdgcn_sched_barrier(0);  // LDS reads in pairs: no spills
@@ -354,8 +357,38 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
     const int eid = tid >> 4, sub = tid & 15;
     const int a = C - 1 - eid;  // ascending index of the eid-th largest eigenvalue
     const double pivmin = 1e-290;
-    double lo = s_lo, hi = s_hi;
-    for (int round = 0; round < 8; ++round) {
+    // first pass: one Sturm count per thread at 1024 points across the Gershgorin interval, then
+    // each eigenvalue's bracket by a binary search over the counts (1024-section in one pass,
+    // where 17-section would need two and a half); six 17-section rounds follow
+    int* cntb = reinterpret_cast<int*>(xbuf);
+    const double lo0 = s_lo, span0 = s_hi - s_lo;
+    {
+      const double x = lo0 + span0 * (double)(tid + 1) * (1.0 / 1025.0);
+      double qv = s_de[0].x - x;
+      if (fabs(qv) < pivmin) qv = -pivmin;
+      int cnt = qv < 0.0;
+#pragma unroll 4
+      for (int i = 1; i < C; ++i) {
+        const double2 de = s_de[i];
+        qv = (de.x - x) - de.y * rcp_nr1(qv);
+        if (fabs(qv) < pivmin) qv = -pivmin;
+        cnt += qv < 0.0;
+      }
+      cntb[tid] = cnt;
+    }
+    __syncthreads();
+    double lo, hi;
+    {
+      int l = 0, h = 1024;  // first t with cnt[t] >= a + 1 (1024: none)
+      while (l < h) {
+        const int m = (l + h) >> 1;
+        if (cntb[m] >= a + 1) h = m;
+        else l = m + 1;
+      }
+      lo = l > 0 ? lo0 + span0 * (double)l * (1.0 / 1025.0) : s_lo;
+      hi = l < 1024 ? lo0 + span0 * (double)(l + 1) * (1.0 / 1025.0) : s_hi;
+    }
+    for (int round = 0; round < 6; ++round) {
       const double x = lo + (hi - lo) * (double)(sub + 1) * (1.0 / 17.0);
       double qv = s_de[0].x - x;
       if (fabs(qv) < pivmin) qv = -pivmin;
