@@ -1213,11 +1213,86 @@ __device__ __forceinline__ void chain_jacobi(const TwoSiteJob& j) {
   chain_jacobi_fallback(j);
 }
 __device__ __forceinline__ void chain_rank(const TwoSiteJob& j) { rank_body<1024>(j); }
-__device__ __forceinline__ void chain_split(const TwoSiteJob& j) {
+// The split GEMM in the chain: its output (k x N, or M x k) is two 64 x 64 blocks, so the four
+// sub-groups split the contraction length L in halves -- sub-group sg computes block sg >> 1 over
+// half sg & 1 -- and the second halves' accumulators meet the first halves' through the LDS.
+__device__ __forceinline__ void split_gemm_chain(const TwoSiteJob& j, int tid) {
   extern __shared__ double2 xbuf[];
+  const int sg = tid >> 8, lt = tid & 255, blk = sg >> 1, h = sg & 1;
+  const int chl = j.dims[0], k = j.dims[1], chr = j.dims[2];
+  const int M = 2 * chl, N = 2 * chr;
+  const bool tr = (M < N) != (j.qr != 0);
+  const int L = tr ? N : M;
+  const int cap = j.cap;
+  const size_t half = (size_t)cap * cap;
+  const double* ss = j.sig + 512;
+  const int rows = tr ? M : k, cols = tr ? k : N;
+  const int r0 = tr ? 64 * blk : 0, c0 = tr ? 0 : 64 * blk;
+  const bool active = r0 < rows && c0 < cols;
+  const int mb = active ? min(64, rows - r0) : 64, nb = active ? min(64, cols - c0) : 64;
+  const int kh = ((L + 1) / 2 + 15) & ~15, klo = h * kh;  // both halves run kh (barriers pair up)
+  const cplx* W = j.work;
+  const int* perm = j.perm;
+  const cplx* th = j.theta;
+  aqc::GemmLds& lds = reinterpret_cast<aqc::GemmLds*>(xbuf)[sg];
+  aqc::d4_t cr[2][2], ci[2][2];
+  if (!tr) {
+    aqc::block_cgemm_tile<true, true, false>(
+        mb, nb, kh, 0, 0,
+        [&](int kk, int R) {
+          return klo + R < L ? aqc::cconj(W[(size_t)perm[r0 + kk] * L + klo + R]) : aqc::cmk(0, 0);
+        },
+        [&](int R, int c) { return klo + R < L ? th[(size_t)(c0 + c) * M + klo + R] : aqc::cmk(0, 0); }, lds, lt,
+        active, cr, ci);
+  } else {
+    aqc::block_cgemm_tile<false, true, false>(
+        mb, nb, kh, 0, 0,
+        [&](int R, int c) { return klo + c < L ? th[(size_t)(klo + c) * M + r0 + R] : aqc::cmk(0, 0); },
+        [&](int c, int kk) { return klo + c < L ? W[(size_t)perm[c0 + kk] * L + klo + c] : aqc::cmk(0, 0); }, lds,
+        lt, active, cr, ci);
+  }
+  // (block_cgemm_tile ends on a barrier: the staging LDS is free)
+  cplx* part = xbuf + blk * (64 * 64);
+  const int wave = lt >> 6, lane = lt & 63;
+  const int wr = (wave >> 1) * 32, wc = (wave & 1) * 32, li = lane & 15, lk = lane >> 4;
+  if (active && h == 1) {
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          part[(wr + 16 * r + lk + 4 * q) * 64 + wc + 16 * c + li] = aqc::cmk(cr[r][c][q], ci[r][c][q]);
+  }
+  __syncthreads();
+  if (active && h == 0) {
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int i = wr + 16 * r + lk + 4 * q, jj = wc + 16 * c + li;
+          if (i < mb && jj < nb) {
+            const cplx o = part[i * 64 + jj];
+            const cplx v = aqc::cmk(cr[r][c][q] + o.x, ci[r][c][q] + o.y);
+            if (!tr) {  // Gq'[s2][kq][r] = Vh / sig^2 / lr[r]
+              const int kq = r0 + i, cc = c0 + jj, s2 = cc / chr, rr = cc % chr;
+              const double d = ss[kq] * ss[kq] * j.lr[rr];
+              j.gq[s2 * half + (size_t)kq * cap + rr] = d != 0.0 ? aqc::cscale(v, 1.0 / d) : aqc::cmk(0, 0);
+            } else {  // Gp'[s1][l][kq] = U / sig^2 / ll[l]
+              const int Rr = r0 + i, kq = c0 + jj, s1 = Rr / chl, l = Rr % chl;
+              const double d = ss[kq] * ss[kq] * j.ll[l];
+              j.gp[s1 * half + (size_t)l * cap + kq] = d != 0.0 ? aqc::cscale(v, 1.0 / d) : aqc::cmk(0, 0);
+            }
+          }
+        }
+  }
+}
+__device__ __forceinline__ void chain_split(const TwoSiteJob& j) {
   const int tid = fresh_tid();
   split_copy_body(j, tid, 1024);
-  split_gemm_body<false>(j, tid >> 8, reinterpret_cast<aqc::GemmLds*>(xbuf)[tid >> 8], tid & 255);
+  split_gemm_chain(j, tid);
 }
 
 __global__ __launch_bounds__(1024) void k_chain(const ChainJob* __restrict__ chains, const TwoSiteJob* __restrict__ two,
