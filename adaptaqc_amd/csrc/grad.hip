@@ -402,22 +402,24 @@ __global__ __launch_bounds__(kT) void k_sweep_chain(const SweepJob* __restrict__
 // lane's 32 B elements of M_{b+1} are requested one by one as those of M_b are consumed (a
 // rolling pipeline: a whole step to land), under LDS-only barriers.  Rows of chains not yet
 // started (a >= b) keep v0_a.  M is zero-padded, so no masks.
-constexpr int kChain8Ld = 132;  // V row stride (complex)
+template <int CAP>
+constexpr int kChain8Ld = CAP + 4;  // V row stride (complex)
 
-__global__ __launch_bounds__(512) void k_sweep_chain8(const SweepJob* __restrict__ jobs, const int* __restrict__ alist,
-                                                      int nal) {
-  constexpr int CAP = 128, NQ = CAP / 4;
+template <int CAP>
+__global__ __launch_bounds__(4 * CAP) void k_sweep_chain8(const SweepJob* __restrict__ jobs, const int* __restrict__ alist,
+                                                          int nal) {
+  constexpr int NQ = CAP / 4, NT = 4 * CAP;  // CAP / 16 waves, one 16-column tile each
   const SweepJob& j = jobs[blockIdx.y];
   const int g0 = blockIdx.x * 8;
   const int n = j.n;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  __shared__ cplx V[2][16][kChain8Ld];
+  __shared__ cplx V[2][16][kChain8Ld<CAP>];
   __shared__ int s_a[8];
   if (tid < 8) s_a[tid] = g0 + tid < nal ? alist[g0 + tid] : n;  // n: never active
   __syncthreads();
   const int amin = s_a[0];  // alist is ascending
   if (amin >= n - 1) return;  // uniform
-  for (int e = tid; e < 16 * CAP; e += 512) {
+  for (int e = tid; e < 16 * CAP; e += NT) {
     const int row = e / CAP, k = e % CAP, a = s_a[row >> 1];
     cplx v = aqc::cmk(0, 0);
     if (a < n - 1 && k < j.dims[a + 1]) v = j.v0[((size_t)a * 2 + (row & 1)) * CAP + k];
@@ -837,7 +839,7 @@ int ensure_gw(aqc_mps_t h) {
 // workgroup, 2: grouped (aqc_sweep_set_chain_mode)
 int g_chain_mode = 0;
 bool use_chain8(int cap, int ns) {
-  if (cap != 128 || g_chain_mode == 1) return false;
+  if ((cap != 128 && cap != 64) || g_chain_mode == 1) return false;
   return g_chain_mode == 2 || ns >= 2;
 }
 
@@ -968,8 +970,11 @@ int aqc_pair_grads_batch(aqc_mps_t* psis, int ns, const double* svec, const int*
     for (int a : alist) steps += (double)(n - 1 - a);
     if (!alist.empty()) {
       aqc::KernelTimer::begin(st, "grad_chain", ns * steps * c * c * 16.0, ns * steps * 2.0 * c * c * 8.0);
-      if (use_chain8(cap, ns))
-        hipLaunchKernelGGL(k_sweep_chain8, dim3((unsigned)(alist.size() + 7) / 8, ns), dim3(512), 0, st, djobs,
+      if (use_chain8(cap, ns) && cap == 128)
+        hipLaunchKernelGGL(k_sweep_chain8<128>, dim3((unsigned)(alist.size() + 7) / 8, ns), dim3(512), 0, st, djobs,
+                           (const int*)dalist, (int)alist.size());
+      else if (use_chain8(cap, ns))
+        hipLaunchKernelGGL(k_sweep_chain8<64>, dim3((unsigned)(alist.size() + 7) / 8, ns), dim3(256), 0, st, djobs,
                            (const int*)dalist, (int)alist.size());
       else
         if (cap == 128)

@@ -194,7 +194,7 @@ int aqc_pair_grads_batch(aqc_mps_t* psis, int nstates, const double* svec, const
                          int npairs, const double* u0, const double* gens, const double* degs,
                          int ngen, double* out /* nstates*npairs */, int out_is_device);
 /* Chain kernel of the sweep: 0 = automatic (first qubits in groups of 8 advancing together on the
- * matrix cores for batches of states at bond capacity 128; one chain per workgroup for a single
+ * matrix cores for batches of states at bond capacity 64 or 128; one chain per workgroup for a single
  * state), 1 = one chain per workgroup, 2 = grouped whenever the capacity allows.  Results are the
  * same up to floating-point summation order. */
 int aqc_sweep_set_chain_mode(int mode);
