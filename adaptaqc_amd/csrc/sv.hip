@@ -10,7 +10,10 @@
 // regardless of how many gates it holds.
 #include <algorithm>
 #include <array>
+#include <cmath>
+#include <cstdlib>
 #include <cstring>
+#include <mutex>
 
 #include "aqc_internal.h"
 
@@ -126,6 +129,174 @@ __global__ __launch_bounds__(kThreads) void k_sv_segment(cplx* __restrict__ stat
   }
 }
 
+// ---- register-resident tile passes (n >= kRegMinQubits) -------------------------------------
+// A 4096-amplitude tile per 256-thread workgroup.  The segment's fused gates are grouped on the
+// host into "phases" whose gates all act inside one set of kRegBits tile bits (the phase's slots).
+// In a phase every thread holds the 16 amplitudes that differ only in those slot bits in
+// registers, applies all of the phase's gates there (fully unrolled per slot pattern), and writes
+// them back: one LDS round trip and one barrier per phase instead of per gate, and 16
+// independent LDS reads per thread in flight instead of 4 dependent ones.  Gate matrices of
+// phase p+1 are staged into LDS (double buffer) while phase p computes.
+constexpr int kRegBits = 4;                 // slots per phase: 16 amplitudes per thread
+constexpr int kRegTileBits = 8 + kRegBits;  // 256 threads x 16 = 4096 amplitudes (64 KB LDS)
+constexpr int kRegMinQubits = 14;           // below: the per-gate kernel (too few tiles)
+constexpr int kPhaseMaxGates = 16;
+constexpr int kRegLowBits = 4;              // global bits 0..3 always in the tile (256-byte runs)
+static_assert(kRegTileBits <= kMaxTileBits, "tile header too small");
+
+struct PhaseHdr {
+  int32_t slotmask;  // the phase's kRegBits tile bits
+  int32_t gate_off;  // into the segment gate array (SegGate: t0 < t1 are slot indices 0..3)
+  int32_t ngates;
+  uint32_t lanemap;  // thread bit j -> tile bit (lanemap >> 4j) & 15 (the 8 non-slot bits)
+};
+
+// LDS layout: amplitude e of the tile lives at e ^ swz(e), where swz XORs a column of kSwzCol
+// into the low 4 bits per set bit of e >> 4.  With the 12 columns of the map e -> (e ^ swz(e)) & 15
+// distinct and non-zero (bits 0-3: 1, 2, 4, 8), any 8 of them span GF(2)^4, so for every slot set
+// the host can order the non-slot bits over the lanes (PhaseHdr::lanemap) such that each 16-lane
+// group of a ds_read_b128 (the cosets of lanes {1, 2, 12, 20}) and each 8-lane group of a
+// ds_write_b128 touches distinct 16-byte bank slots: conflict-free phases.  A linear layout puts
+// the 16 lanes of a phase whose slots are tile bits 0-3 on one bank slot (16-way).
+constexpr int kSwzCol[8] = {3, 6, 12, 9, 5, 10, 7, 14};
+__host__ __device__ __forceinline__ int swz_bits(int e) {
+  int v = 0;
+#pragma unroll
+  for (int b = 0; b < 8; ++b)
+    if ((e >> (4 + b)) & 1) v ^= kSwzCol[b];
+  return v;
+}
+__host__ __device__ __forceinline__ int swz(int e) { return e ^ swz_bits(e); }
+
+template <int S>
+__device__ __forceinline__ void reg_apply1(cplx (&a)[16], const SegGate& g) {
+  const cplx m00 = g.m[0], m01 = g.m[1], m10 = g.m[2], m11 = g.m[3];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    if ((r >> S) & 1) continue;
+    const int r1 = r | (1 << S);
+    const cplx a0 = a[r], a1 = a[r1];
+    a[r] = aqc::cfma(m01, a1, aqc::cmul(m00, a0));
+    a[r1] = aqc::cfma(m11, a1, aqc::cmul(m10, a0));
+  }
+}
+
+template <int S0, int S1>
+__device__ __forceinline__ void reg_apply2(cplx (&a)[16], const SegGate& g) {
+  cplx m[16];
+#pragma unroll
+  for (int e = 0; e < 16; ++e) m[e] = g.m[e];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    if (((r >> S0) & 1) || ((r >> S1) & 1)) continue;
+    int idx[4];
+    cplx v[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      idx[s] = r | ((s & 1) << S0) | ((s >> 1) << S1);
+      v[s] = a[idx[s]];
+    }
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+      cplx acc = aqc::cmul(m[4 * o], v[0]);
+      acc = aqc::cfma(m[4 * o + 1], v[1], acc);
+      acc = aqc::cfma(m[4 * o + 2], v[2], acc);
+      acc = aqc::cfma(m[4 * o + 3], v[3], acc);
+      a[idx[o]] = acc;
+    }
+  }
+}
+
+__device__ __forceinline__ void reg_apply(cplx (&a)[16], const SegGate& g) {
+  // wave-uniform dispatch on the slot pattern (t0 < t1 for 2-qubit gates, host-normalised)
+  const int code = __builtin_amdgcn_readfirstlane(g.nq == 1 ? g.t0 : 4 + 4 * g.t0 + g.t1);
+  switch (code) {
+    case 0: reg_apply1<0>(a, g); break;
+    case 1: reg_apply1<1>(a, g); break;
+    case 2: reg_apply1<2>(a, g); break;
+    case 3: reg_apply1<3>(a, g); break;
+    case 4 + 1: reg_apply2<0, 1>(a, g); break;
+    case 4 + 2: reg_apply2<0, 2>(a, g); break;
+    case 4 + 3: reg_apply2<0, 3>(a, g); break;
+    case 4 + 6: reg_apply2<1, 2>(a, g); break;
+    case 4 + 7: reg_apply2<1, 3>(a, g); break;
+    case 4 + 11: reg_apply2<2, 3>(a, g); break;
+    default: break;
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void k_sv_tile_reg(cplx* __restrict__ state, const SegHeader* __restrict__ hdr,
+                                                         const PhaseHdr* __restrict__ phases,
+                                                         const SegGate* __restrict__ gates) {
+  constexpr int K = kRegTileBits;
+  __shared__ cplx tile[1 << K];
+  __shared__ SegGate gl[2][kPhaseMaxGates];
+  const int tid = threadIdx.x;
+  int tb[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) tb[j] = hdr->tilebits[j];
+  uint64_t base = blockIdx.x;
+#pragma unroll
+  for (int j = 0; j < K; ++j) base = insert_zero(base, tb[j]);
+  auto gidx = [&](int x) {
+    uint64_t g = base;
+#pragma unroll
+    for (int j = 0; j < K; ++j) g |= (uint64_t)((x >> j) & 1) << tb[j];
+    return g;
+  };
+  constexpr int kPer = (1 << K) / kThreads;
+  {
+    cplx v[kPer];
+#pragma unroll
+    for (int r = 0; r < kPer; ++r) v[r] = aqc::ldg(state + gidx(tid + r * kThreads));
+#pragma unroll
+    for (int r = 0; r < kPer; ++r) tile[swz(tid + r * kThreads)] = v[r];
+  }
+  const int np = hdr->ngates;
+  const PhaseHdr* ph = phases + hdr->gate_off;
+  constexpr int kWords = (int)(sizeof(SegGate) / sizeof(double2));
+  auto stage = [&](int p) {
+    const int ng = ph[p].ngates;
+    const double2* src = reinterpret_cast<const double2*>(gates + ph[p].gate_off);
+    double2* dst = reinterpret_cast<double2*>(gl[p & 1]);
+    for (int w = tid; w < ng * kWords; w += kThreads) dst[w] = src[w];
+  };
+  if (np > 0) stage(0);
+  __syncthreads();
+  for (int p = 0; p < np; ++p) {
+    if (p + 1 < np) stage(p + 1);  // the other buffer: its last readers passed the barrier below
+    const int sm = __builtin_amdgcn_readfirstlane(ph[p].slotmask);
+    const unsigned lm = __builtin_amdgcn_readfirstlane(ph[p].lanemap);
+    // thread bits placed on the non-slot tile bits by the lane map, slot bits from r; the swizzle
+    // is linear, so the address is swz(thread part) ^ swz(slot part)
+    int lb = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) lb |= ((tid >> j) & 1) << ((lm >> (4 * j)) & 15);
+    lb = swz(lb);
+    int sb[kRegBits], c = 0;
+#pragma unroll
+    for (int j = 0; j < K; ++j)
+      if ((sm >> j) & 1) {
+        if (c < kRegBits) sb[c] = swz(1 << j);
+        ++c;
+      }
+    int off[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+      off[r] = lb ^ ((r & 1) ? sb[0] : 0) ^ ((r & 2) ? sb[1] : 0) ^ ((r & 4) ? sb[2] : 0) ^ ((r & 8) ? sb[3] : 0);
+    cplx a[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) a[r] = tile[off[r]];
+    const int ng = ph[p].ngates;
+    for (int gi = 0; gi < ng; ++gi) reg_apply(a, gl[p & 1][gi]);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) tile[off[r]] = a[r];
+    __syncthreads();
+  }
+#pragma unroll
+  for (int r = 0; r < kPer; ++r) aqc::stg(state + gidx(tid + r * kThreads), tile[swz(tid + r * kThreads)]);
+}
+
 // Per-workgroup partial probabilities: out[wg * (n+1) + i] = sum |a|^2 over amplitudes of this
 // workgroup with bit i set (i < n); out[wg*(n+1)+n] = total.
 constexpr int kZChunk = 16;  // amplitudes per thread
@@ -199,7 +370,7 @@ struct HostSeg {
   uint64_t qmask = 0;
 };
 
-std::vector<HostSeg> build_segments(const aqc_op_t* ops, int nops, int K, int n) {
+std::vector<HostSeg> build_segments(const aqc_op_t* ops, int nops, int K, int n, uint64_t reserve = 0) {
   std::vector<HostSeg> segs;
   std::vector<char> done(nops, 0);
   int remaining = nops;
@@ -216,7 +387,7 @@ std::vector<HostSeg> build_segments(const aqc_op_t* ops, int nops, int K, int n)
         blocked |= gm;
       } else {
         uint64_t u = seg.qmask | gm;
-        if (__builtin_popcountll(u) <= K) {
+        if (__builtin_popcountll(u | reserve) <= K) {
           seg.qmask = u;
           seg.gates.push_back(i);
           done[i] = 1;
@@ -240,30 +411,44 @@ std::vector<HostSeg> build_segments(const aqc_op_t* ops, int nops, int K, int n)
 // here every tile pass saves one LDS sweep and one barrier per absorbed gate.  Brickwork: 3 ops
 // per pair and layer become 1.
 typedef std::array<cplx, 16> Mat4;
+// host complex arithmetic without fma(): the x86 host build has no FMA instructions enabled, so
+// fma() is a libm call per operation (2.3 ns each made the fusion 0.35 ms of a 20-qubit
+// evaluation's host time)
+static inline cplx hmul(cplx a, cplx b) { return aqc::cmk(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x); }
+static inline cplx hfma(cplx a, cplx b, cplx c) {
+  return aqc::cmk(c.x + a.x * b.x - a.y * b.y, c.y + a.x * b.y + a.y * b.x);
+}
 
 static Mat4 mat4_mul(const Mat4& a, const Mat4& b) {  // a b
   Mat4 c;
   for (int r = 0; r < 4; ++r)
     for (int k = 0; k < 4; ++k) {
       cplx acc = aqc::cmk(0, 0);
-      for (int j = 0; j < 4; ++j) acc = aqc::cfma(a[4 * r + j], b[4 * j + k], acc);
+      for (int j = 0; j < 4; ++j) acc = hfma(a[4 * r + j], b[4 * j + k], acc);
       c[4 * r + k] = acc;
     }
   return c;
 }
 
-// 1-qubit u on bit `which` (0: the op's t0, 1: its t1) of a 4x4 (index 2 b1 + b0)
-static Mat4 embed1(const cplx* u, int which) {
-  Mat4 m;
-  for (int r = 0; r < 4; ++r)
-    for (int c = 0; c < 4; ++c) {
-      const int r0 = r & 1, r1 = r >> 1, c0 = c & 1, c1 = c >> 1;
-      cplx v = aqc::cmk(0, 0);
-      if (which == 0 && r1 == c1) v = u[2 * r0 + c0];
-      if (which == 1 && r0 == c0) v = u[2 * r1 + c1];
-      m[4 * r + c] = v;
-    }
-  return m;
+// E m and m E for E = the 1-qubit u on bit `which` (0: the op's t0, 1: its t1) of a 4x4 (index
+// 2 b1 + b0), without forming E: 32 complex products instead of 64
+static Mat4 left1(const cplx* u, int which, const Mat4& m) {
+  Mat4 o;
+  const int bit = 1 << which;
+  for (int r = 0; r < 4; ++r) {
+    const int rb = (r >> which) & 1, r0 = r & ~bit, r1 = r | bit;
+    for (int c = 0; c < 4; ++c) o[4 * r + c] = hfma(u[2 * rb + 1], m[4 * r1 + c], hmul(u[2 * rb], m[4 * r0 + c]));
+  }
+  return o;
+}
+static Mat4 right1(const Mat4& m, const cplx* u, int which) {
+  Mat4 o;
+  const int bit = 1 << which;
+  for (int c = 0; c < 4; ++c) {
+    const int cb = (c >> which) & 1, c0 = c & ~bit, c1 = c | bit;
+    for (int r = 0; r < 4; ++r) o[4 * r + c] = hfma(m[4 * r + c1], u[2 + cb], hmul(m[4 * r + c0], u[cb]));
+  }
+  return o;
 }
 
 static Mat4 swap_bits(const Mat4& a) {  // the same operator with t0 and t1 exchanged
@@ -294,10 +479,10 @@ std::vector<SegGate> fuse_segment(const aqc_op_t* ops, const std::vector<int>& i
       if (k >= 0 && f[k].nq == 1) {  // 2x2 product u * m
         Mat4 c = f[k].m;
         for (int r = 0; r < 2; ++r)
-          for (int cc = 0; cc < 2; ++cc) c[2 * r + cc] = aqc::cfma(u[2 * r + 1], f[k].m[2 + cc], aqc::cmul(u[2 * r], f[k].m[cc]));
+          for (int cc = 0; cc < 2; ++cc) c[2 * r + cc] = hfma(u[2 * r + 1], f[k].m[2 + cc], hmul(u[2 * r], f[k].m[cc]));
         f[k].m = c;
       } else if (k >= 0) {
-        f[k].m = mat4_mul(embed1(u, f[k].t0 == q ? 0 : 1), f[k].m);
+        f[k].m = left1(u, f[k].t0 == q ? 0 : 1, f[k].m);
       } else {
         F n;
         n.nq = 1, n.t0 = q, n.t1 = 0;
@@ -319,11 +504,11 @@ std::vector<SegGate> fuse_segment(const aqc_op_t* ops, const std::vector<int>& i
     // absorb pending single-qubit ops on a / b (their last op, nothing after them on that qubit)
     Mat4 m = g;
     if (ka >= 0 && f[ka].nq == 1) {
-      m = mat4_mul(m, embed1(f[ka].m.data(), 0));
+      m = right1(m, f[ka].m.data(), 0);
       f[ka].dead = true;
     }
     if (kb >= 0 && f[kb].nq == 1) {
-      m = mat4_mul(m, embed1(f[kb].m.data(), 1));
+      m = right1(m, f[kb].m.data(), 1);
       f[kb].dead = true;
     }
     F n;
@@ -341,6 +526,118 @@ std::vector<SegGate> fuse_segment(const aqc_op_t* ops, const std::vector<int>& i
     out.push_back(g);
   }
   return out;
+}
+
+// Phases of a fused segment (k_sv_tile_reg): greedy in application order, a gate joins the
+// current phase when its tile bits fit in the phase's kRegBits slots and it acts on no bit of a
+// gate left for a later phase (gates on disjoint bits commute).  Gate bits become slot indices
+// (t0 < t1, the 4x4 re-indexed when the order flips).
+// Lane map of a slot set: an order of the 8 non-slot tile bits over the thread bits whose first
+// five give conflict-free LDS groups under swz (checked by counting bank slots over the 64 lanes
+// of a wave; the first order with no conflict, else the one with the fewest extra cycles).
+// Cached per slot set.
+uint32_t lane_map(uint32_t S) {
+  static std::array<uint32_t, 1 << kRegTileBits> cache{};
+  static std::array<char, 1 << kRegTileBits> have{};
+  static std::mutex mu;
+  std::lock_guard<std::mutex> lock(mu);
+  if (have[S]) return cache[S];
+  int ns[8], nn = 0;
+  for (int b = 0; b < kRegTileBits; ++b)
+    if (!((S >> b) & 1u)) ns[nn++] = b;
+  auto cost = [&](const int* pos) {
+    int e[64];
+    for (int l = 0; l < 64; ++l) {
+      int v = 0;
+      for (int j = 0; j < 6; ++j) v |= ((l >> j) & 1) << pos[j];
+      e[l] = swz(v);
+    }
+    int c = 0;
+    static const int g128[16] = {0, 1, 2, 3, 12, 13, 14, 15, 20, 21, 22, 23, 24, 25, 26, 27};
+    for (int base : {0, 4, 32, 36}) {  // the four cosets of the b128 read group
+      int cnt[16] = {};
+      int mx = 0;
+      for (int k = 0; k < 16; ++k) mx = std::max(mx, ++cnt[e[base ^ g128[k]] & 15]);
+      c += mx - 1;
+    }
+    for (int g = 0; g < 64; g += 8) {  // b128 writes: 8 contiguous lanes, 8 bank slots
+      int cnt[8] = {};
+      int mx = 0;
+      for (int k = 0; k < 8; ++k) mx = std::max(mx, ++cnt[e[g + k] & 7]);
+      c += mx - 1;
+    }
+    return c;
+  };
+  int best[8], bc = 1 << 30;
+  int perm[8];
+  for (int i = 0; i < 8; ++i) perm[i] = i;
+  // the first six positions decide the wave's banks; the last two (threads across waves) follow
+  do {
+    int pos[8];
+    for (int i = 0; i < 8; ++i) pos[i] = ns[perm[i]];
+    const int c = cost(pos);
+    if (c < bc) {
+      bc = c;
+      std::memcpy(best, pos, sizeof(best));
+      if (c == 0) break;
+    }
+    std::reverse(perm + 6, perm + 8);  // skip orders that differ only in the last two
+  } while (std::next_permutation(perm, perm + 8));
+  uint32_t m = 0;
+  for (int j = 0; j < 8; ++j) m |= (uint32_t)best[j] << (4 * j);
+  cache[S] = m;
+  have[S] = 1;
+  return m;
+}
+
+void build_phases(const std::vector<SegGate>& fused, int K, std::vector<PhaseHdr>& ph, std::vector<SegGate>& out) {
+  std::vector<char> done(fused.size(), 0);
+  size_t remaining = fused.size(), first = 0;
+  while (remaining > 0) {
+    while (done[first]) ++first;
+    uint32_t S = 0, blocked = 0;
+    std::vector<size_t> members;
+    for (size_t i = first; i < fused.size() && (int)members.size() < kPhaseMaxGates; ++i) {
+      if (done[i]) continue;
+      const uint32_t gm = (1u << fused[i].t0) | (fused[i].nq == 2 ? (1u << fused[i].t1) : 0u);
+      if (gm & blocked) {
+        blocked |= gm;
+      } else if (__builtin_popcount(S | gm) <= kRegBits) {
+        S |= gm;
+        members.push_back(i);
+        done[i] = 1;
+        --remaining;
+      } else {
+        blocked |= gm;
+      }
+      if (__builtin_popcount(blocked) >= K) break;
+    }
+    for (int b = 0; b < K && __builtin_popcount(S) < kRegBits; ++b) S |= 1u << b;
+    auto slot = [&](int b) { return __builtin_popcount(S & ((1u << b) - 1u)); };
+    PhaseHdr h;
+    h.slotmask = (int32_t)S;
+    h.gate_off = (int32_t)out.size();
+    h.ngates = (int32_t)members.size();
+    h.lanemap = lane_map(S);
+    ph.push_back(h);
+    for (size_t i : members) {
+      SegGate g = fused[i];
+      if (g.nq == 1) {
+        g.t0 = slot(g.t0);
+      } else {
+        const int s0 = slot(g.t0), s1 = slot(g.t1);
+        if (s0 > s1) {
+          Mat4 m;
+          for (int e = 0; e < 16; ++e) m[e] = g.m[e];
+          m = swap_bits(m);
+          for (int e = 0; e < 16; ++e) g.m[e] = m[e];
+        }
+        g.t0 = s0 < s1 ? s0 : s1;
+        g.t1 = s0 < s1 ? s1 : s0;
+      }
+      out.push_back(g);
+    }
+  }
 }
 
 }  // namespace
@@ -456,10 +753,11 @@ struct aqc_sv_s {
   int K = 0;
   cplx* state = nullptr;
   hipStream_t stream = nullptr;
-  SegHeader* d_hdr = nullptr;
-  size_t hdr_cap = 0;
-  SegGate* d_gates = nullptr;
-  size_t gate_cap = 0;
+  char* d_plan = nullptr;  // [segment headers | phases | gates] of the last aqc_sv_apply
+  char* h_plan = nullptr;  // pinned staging copy
+  size_t plan_cap = 0;
+  hipEvent_t plan_ev = nullptr;
+  bool reg_tiles = false;
   double* d_zpart = nullptr;
   double* d_z = nullptr;
   int zwg = 0;
@@ -479,9 +777,76 @@ static int sv_scratch(aqc_sv_t h, size_t bytes, char** out) {
   return AQC_OK;
 }
 
-static int sv_launch_segment(aqc_sv_t h, const SegHeader* dh, const SegGate* dg, int nblocks) {
+// Host planning of one aqc_sv_apply: segments (tile bits + fused gates), and the phases of the
+// register-tile path.
+static void sv_plan(int n, int K, bool reg_tiles, const aqc_op_t* ops, int nops, std::vector<SegHeader>& hdr,
+                    std::vector<SegGate>& gts, std::vector<PhaseHdr>& phs, std::vector<double>* seg_flops = nullptr) {
+  // register tiles keep the lowest global bits in every tile (runs of 2^low contiguous amplitudes
+  // per lane group: a tile of high qubits only reads 16-byte pieces scattered 4 KB apart)
+  uint64_t reserve = 0;
+  if (reg_tiles) {
+    static const char* lb_env = std::getenv("AQC_SV_LOWBITS");
+    const int low = lb_env ? std::atoi(lb_env) : kRegLowBits;
+    reserve = (1ull << std::min(std::max(low, 0), 8)) - 1ull;
+  }
+  std::vector<HostSeg> segs = build_segments(ops, nops, K, n, reserve);
+  hdr.assign(segs.size(), SegHeader{});
+  gts.reserve(nops);
+  for (size_t s = 0; s < segs.size(); ++s) {
+    // tile bits: segment qubits + lowest free bits up to K
+    uint64_t mask = segs[s].qmask;
+    for (int b = 0; b < n && __builtin_popcountll(mask) < K; ++b) mask |= (1ull << b);
+    int pos[64];
+    int cnt = 0;
+    for (int b = 0; b < n; ++b)
+      if ((mask >> b) & 1ull) pos[cnt++] = b;
+    std::memset(&hdr[s], 0, sizeof(SegHeader));
+    int local_of[64];
+    for (int j = 0; j < cnt; ++j) {
+      hdr[s].tilebits[j] = pos[j];
+      local_of[pos[j]] = j;
+    }
+    const std::vector<SegGate> fused = fuse_segment(ops, segs[s].gates, local_of);
+    if (seg_flops) {  // real flops of the fused gates: 1q 2, 2q 4 complex MACs (8 flops) per amplitude
+      double f = 0.0;
+      for (const SegGate& g : fused) f += (g.nq == 1 ? 16.0 : 32.0) * std::ldexp(1.0, n);
+      seg_flops->push_back(f);
+    }
+    if (reg_tiles) {  // gate_off / ngates index the phase list
+      hdr[s].gate_off = (int)phs.size();
+      const size_t before = phs.size();
+      build_phases(fused, K, phs, gts);
+      hdr[s].ngates = (int)(phs.size() - before);
+      // timing experiments only (results wrong): AQC_SV_DEBUG=nogates / nophases
+      static const char* dbg = std::getenv("AQC_SV_DEBUG");
+      if (dbg && std::strcmp(dbg, "nophases") == 0) hdr[s].ngates = 0;
+      if (dbg && std::strcmp(dbg, "nogates") == 0)
+        for (size_t q = before; q < phs.size(); ++q) phs[q].ngates = 0;
+    } else {
+      hdr[s].gate_off = (int)gts.size();
+      hdr[s].ngates = (int)fused.size();
+      gts.insert(gts.end(), fused.begin(), fused.end());
+    }
+  }
+}
+
+static bool sv_reg_tiles(int n) {
+  // register-resident 4096-amplitude tiles from kRegMinQubits qubits (AQC_SV_TILE=lds keeps the
+  // per-gate LDS kernel, for A/B measurements)
+  const char* tile_env = std::getenv("AQC_SV_TILE");
+  return n >= kRegMinQubits && !(tile_env && std::strcmp(tile_env, "lds") == 0);
+}
+
+static int sv_launch_segment(aqc_sv_t h, const SegHeader* dh, const PhaseHdr* dp, const SegGate* dg, int nblocks,
+                             double flops) {
   const double bytes = 32.0 * (double)(1ull << h->n);
-  aqc::KernelTimer::begin(h->stream, "sv_segment", bytes, 0.0);
+  aqc::KernelTimer::begin(h->stream, "sv_segment", bytes, flops);
+  if (h->reg_tiles) {
+    hipLaunchKernelGGL(k_sv_tile_reg, dim3(nblocks), dim3(kThreads), 0, h->stream, h->state, dh, dp, dg);
+    aqc::KernelTimer::end(h->stream);
+    AQC_CHECK_LAUNCH();
+    return AQC_OK;
+  }
   switch (h->K) {
 #define AQC_SEG_CASE(KK)                                                                   \
   case KK:                                                                                 \
@@ -516,7 +881,8 @@ int aqc_sv_create(int n, aqc_sv_t* out) {
   AQC_REQUIRE(n >= 1 && n <= 34, "aqc_sv_create: n must be in [1, 34]");
   auto* h = new aqc_sv_s();
   h->n = n;
-  h->K = n < 10 ? n : 10;
+  h->reg_tiles = sv_reg_tiles(n);
+  h->K = h->reg_tiles ? kRegTileBits : (n < 10 ? n : 10);
   const uint64_t dim = 1ull << n;
   hipError_t e = hipMalloc(&h->state, dim * sizeof(cplx));
   if (e != hipSuccess) {
@@ -525,6 +891,7 @@ int aqc_sv_create(int n, aqc_sv_t* out) {
     return AQC_ERR_NOMEM;
   }
   AQC_HIP_CHECK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+  AQC_HIP_CHECK(hipEventCreateWithFlags(&h->plan_ev, hipEventDisableTiming));
   h->zwg = (int)((dim + kThreads * kZChunk - 1) / (kThreads * kZChunk));
   AQC_HIP_CHECK(hipMalloc(&h->d_zpart, sizeof(double) * (size_t)h->zwg * (n + 1)));
   AQC_HIP_CHECK(hipMalloc(&h->d_z, sizeof(double) * (n + 1)));
@@ -537,8 +904,9 @@ int aqc_sv_destroy(aqc_sv_t h) {
   if (!h) return AQC_OK;
   if (h->stream) hipStreamSynchronize(h->stream);
   hipFree(h->state);
-  hipFree(h->d_hdr);
-  hipFree(h->d_gates);
+  if (h->d_plan) hipFree(h->d_plan);
+  if (h->h_plan) hipHostFree(h->h_plan);
+  if (h->plan_ev) hipEventDestroy(h->plan_ev);
   hipFree(h->d_zpart);
   hipFree(h->d_z);
   if (h->d_scratch) hipFree(h->d_scratch);
@@ -578,54 +946,60 @@ int aqc_sv_apply(aqc_sv_t h, const aqc_op_t* ops, int nops) {
     }
   }
   const int K = h->K;
-  std::vector<HostSeg> segs = build_segments(ops, nops, K, h->n);
-  std::vector<SegHeader> hdr(segs.size());
+  std::vector<SegHeader> hdr;
   std::vector<SegGate> gts;
-  gts.reserve(nops);
-  for (size_t s = 0; s < segs.size(); ++s) {
-    // tile bits: segment qubits + lowest free bits up to K
-    uint64_t mask = segs[s].qmask;
-    for (int b = 0; b < h->n && __builtin_popcountll(mask) < K; ++b) mask |= (1ull << b);
-    int pos[64];
-    int cnt = 0;
-    for (int b = 0; b < h->n; ++b)
-      if ((mask >> b) & 1ull) pos[cnt++] = b;
-    std::memset(&hdr[s], 0, sizeof(SegHeader));
-    int local_of[64];
-    for (int j = 0; j < cnt; ++j) {
-      hdr[s].tilebits[j] = pos[j];
-      local_of[pos[j]] = j;
-    }
-    hdr[s].gate_off = (int)gts.size();
-    const std::vector<SegGate> fused = fuse_segment(ops, segs[s].gates, local_of);
-    hdr[s].ngates = (int)fused.size();
-    gts.insert(gts.end(), fused.begin(), fused.end());
-  }
-  if (hdr.size() > h->hdr_cap) {
+  std::vector<PhaseHdr> phs;
+  std::vector<double> flops;
+  sv_plan(h->n, K, h->reg_tiles, ops, nops, hdr, gts, phs, &flops);
+  // one pinned staging copy of the plan [headers | phases | gates]: the previous call's copy has
+  // finished reading it once plan_ev has completed; the device copy is ordered on the stream
+  // after the previous call's launches
+  auto al = [](size_t b) { return (b + 255) / 256 * 256; };
+  const size_t o_ph = al(sizeof(SegHeader) * hdr.size());
+  const size_t o_g = o_ph + al(sizeof(PhaseHdr) * phs.size());
+  const size_t bytes = o_g + sizeof(SegGate) * gts.size();
+  if (bytes > h->plan_cap) {
     AQC_HIP_CHECK(hipStreamSynchronize(h->stream));
-    hipFree(h->d_hdr);
-    h->hdr_cap = hdr.size() * 2;
-    AQC_HIP_CHECK(hipMalloc(&h->d_hdr, sizeof(SegHeader) * h->hdr_cap));
+    if (h->d_plan) AQC_HIP_CHECK(hipFree(h->d_plan));
+    if (h->h_plan) AQC_HIP_CHECK(hipHostFree(h->h_plan));
+    h->d_plan = nullptr, h->h_plan = nullptr;
+    h->plan_cap = std::max(bytes, 2 * h->plan_cap);
+    AQC_HIP_CHECK(hipMalloc(&h->d_plan, h->plan_cap));
+    AQC_HIP_CHECK(hipHostMalloc(&h->h_plan, h->plan_cap, hipHostMallocDefault));
   }
-  if (gts.size() > h->gate_cap) {
-    AQC_HIP_CHECK(hipStreamSynchronize(h->stream));
-    hipFree(h->d_gates);
-    h->gate_cap = gts.size() * 2;
-    AQC_HIP_CHECK(hipMalloc(&h->d_gates, sizeof(SegGate) * h->gate_cap));
-  }
-  // The previous call's launches may still read these buffers: order the copy on the stream.
-  AQC_HIP_CHECK(hipMemcpyAsync(h->d_hdr, hdr.data(), sizeof(SegHeader) * hdr.size(),
-                               hipMemcpyHostToDevice, h->stream));
-  AQC_HIP_CHECK(hipMemcpyAsync(h->d_gates, gts.data(), sizeof(SegGate) * gts.size(),
-                               hipMemcpyHostToDevice, h->stream));
-  // hipMemcpyAsync from pageable memory is staged before returning, so hdr/gts may go out
-  // of scope; synchronising keeps that guarantee explicit.
-  AQC_HIP_CHECK(hipStreamSynchronize(h->stream));
+  AQC_HIP_CHECK(hipEventSynchronize(h->plan_ev));
+  std::memcpy(h->h_plan, hdr.data(), sizeof(SegHeader) * hdr.size());
+  if (!phs.empty()) std::memcpy(h->h_plan + o_ph, phs.data(), sizeof(PhaseHdr) * phs.size());
+  if (!gts.empty()) std::memcpy(h->h_plan + o_g, gts.data(), sizeof(SegGate) * gts.size());
+  AQC_HIP_CHECK(hipMemcpyAsync(h->d_plan, h->h_plan, bytes, hipMemcpyHostToDevice, h->stream));
+  AQC_HIP_CHECK(hipEventRecord(h->plan_ev, h->stream));
+  const SegHeader* dh = reinterpret_cast<const SegHeader*>(h->d_plan);
+  const PhaseHdr* dp = reinterpret_cast<const PhaseHdr*>(h->d_plan + o_ph);
+  const SegGate* dg = reinterpret_cast<const SegGate*>(h->d_plan + o_g);
   const int nblocks = (int)(1ull << (h->n - K));
   for (size_t s = 0; s < hdr.size(); ++s) {
-    int rc = sv_launch_segment(h, h->d_hdr + s, h->d_gates, nblocks);
+    int rc = sv_launch_segment(h, dh + s, dp, dg, nblocks, flops[s]);
     if (rc != AQC_OK) return rc;
   }
+  return AQC_OK;
+}
+
+int aqc_sv_plan(int n, const aqc_op_t* ops, int nops, int* out) {
+  AQC_REQUIRE(out && n >= 1 && n <= 34 && nops >= 0 && (ops || nops == 0), "aqc_sv_plan: bad arguments");
+  for (int i = 0; i < nops; ++i)
+    AQC_REQUIRE((ops[i].nq == 1 || ops[i].nq == 2) && ops[i].q0 >= 0 && ops[i].q0 < n &&
+                    (ops[i].nq == 1 || (ops[i].q1 >= 0 && ops[i].q1 < n && ops[i].q1 != ops[i].q0)),
+                "aqc_sv_plan: bad op");
+  const bool reg = sv_reg_tiles(n);
+  const int K = reg ? kRegTileBits : (n < 10 ? n : 10);
+  std::vector<SegHeader> hdr;
+  std::vector<SegGate> gts;
+  std::vector<PhaseHdr> phs;
+  if (nops > 0) sv_plan(n, K, reg, ops, nops, hdr, gts, phs);
+  out[0] = (int)hdr.size();
+  out[1] = (int)phs.size();
+  out[2] = (int)gts.size();
+  out[3] = K;
   return AQC_OK;
 }
 

@@ -64,8 +64,12 @@ int aqc_sv_destroy(aqc_sv_t h);
 int aqc_sv_reset(aqc_sv_t h);
 int aqc_sv_copy(aqc_sv_t dst, const aqc_sv_t src);
 /* Apply ops in order (aer_sv_backend.py:42-47 simulator.run(full_circuit)).  Gates are
- * fused on the host into qubit-local segments (<= 10-bit tiles) that run in LDS. */
+ * fused on the host into qubit-local segments: 10-bit LDS tiles below 14 qubits, 12-bit
+ * register-resident tiles (4-bit phases) from 14 qubits. */
 int aqc_sv_apply(aqc_sv_t h, const aqc_op_t* ops, int nops);
+/* Host planning of aqc_sv_apply only (no GPU): out[0] segments (= launches), out[1] phases
+ * (register-tile path; 0 otherwise), out[2] fused gates, out[3] tile bits. */
+int aqc_sv_plan(int n, const aqc_op_t* ops, int nops, int* out);
 /* sv[0] (aer_sv_backend.py:29). */
 int aqc_sv_amp0(aqc_sv_t h, double* re, double* im);
 /* <Z_i> = p0 - p1 for all i (aer_sv_backend.py:49-59), out[n]. */

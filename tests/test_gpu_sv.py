@@ -146,3 +146,36 @@ def test_gate_fusion_patterns():
         d = DeviceSV(n)
         d.apply(device_ops(to_circuit(n, ops)))
         np.testing.assert_allclose(d.get(), osv.simulate(n, ops), atol=1e-12, err_msg=f"n={n}")
+
+
+def test_register_tile_path_vs_oracle_and_lds_kernel(monkeypatch):
+    """n >= 14 runs the register-resident tile kernel (gates grouped into 4-bit phases): random
+    1q/2q gates incl. fusion patterns, long-range pairs and reversed orders, against the oracle and
+    against the per-gate LDS kernel (AQC_SV_TILE=lds)."""
+    from adaptaqc_amd.circuit import device_ops
+    from adaptaqc_amd.device import DeviceSV
+
+    rng = np.random.default_rng(23)
+    for n in (14, 15, 17):
+        ops = brickwork(n, 4, n)
+        for _ in range(150):
+            k = rng.integers(6)
+            a, b = (int(x) for x in rng.choice(n, 2, replace=False))
+            if k < 3:
+                ops.append((["rx", "ry", "rz"][k], (a,), (rng.uniform(-np.pi, np.pi),)))
+            elif k == 3:
+                ops.append(("cx", (a, b), ()))
+            elif k == 4:
+                ops += [("cx", (a, b), ()), ("cx", (b, a), ()), ("rz", (b,), (0.4,)), ("cz", (a, b), ())]
+            else:
+                ops += [("h", (a,), ()), ("swap", (a, b), ()), ("ry", (a,), (1.3,))]
+        dops = device_ops(to_circuit(n, ops))
+        d = DeviceSV(n)
+        d.apply(dops)
+        got = d.get()
+        np.testing.assert_allclose(got, osv.simulate(n, ops), atol=1e-12, err_msg=f"n={n}")
+        monkeypatch.setenv("AQC_SV_TILE", "lds")
+        d2 = DeviceSV(n)
+        monkeypatch.delenv("AQC_SV_TILE")
+        d2.apply(dops)
+        np.testing.assert_allclose(got, d2.get(), atol=1e-13, err_msg=f"n={n} (lds kernel)")
