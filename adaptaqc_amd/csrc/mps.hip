@@ -1570,12 +1570,16 @@ struct DevOp {
 };
 
 inline cplx hc(double r, double i) { return aqc::cmk(r, i); }
+// host complex arithmetic without fma(): the x86 host build has no FMA instructions enabled, so
+// fma() is a libm call per operation
+inline cplx hmul(cplx a, cplx b) { return aqc::cmk(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x); }
+inline cplx hfma(cplx a, cplx b, cplx c) { return aqc::cmk(c.x + a.x * b.x - a.y * b.y, c.y + a.x * b.y + a.y * b.x); }
 
 void mat2_mul(const cplx* a, const cplx* b, cplx* out) {  // out = a b (2x2)
   cplx t[4];
   for (int r = 0; r < 2; ++r)
     for (int c = 0; c < 2; ++c)
-      t[r * 2 + c] = aqc::cfma(a[r * 2 + 1], b[2 + c], aqc::cmul(a[r * 2], b[c]));
+      t[r * 2 + c] = hfma(a[r * 2 + 1], b[2 + c], hmul(a[r * 2], b[c]));
   std::memcpy(out, t, sizeof(t));
 }
 
@@ -1633,12 +1637,12 @@ struct Scheduler {
     has[qa] = has[qb] = 0;
     cplx K[16];
     for (int r = 0; r < 4; ++r)
-      for (int c = 0; c < 4; ++c) K[r * 4 + c] = aqc::cmul(Pb[(r >> 1) * 2 + (c >> 1)], Pa[(r & 1) * 2 + (c & 1)]);
+      for (int c = 0; c < 4; ++c) K[r * 4 + c] = hmul(Pb[(r >> 1) * 2 + (c >> 1)], Pa[(r & 1) * 2 + (c & 1)]);
     cplx Mf[16];
     for (int r = 0; r < 4; ++r)
       for (int c = 0; c < 4; ++c) {
         cplx acc = hc(0, 0);
-        for (int t = 0; t < 4; ++t) acc = aqc::cfma(M4[r * 4 + t], K[t * 4 + c], acc);
+        for (int t = 0; t < 4; ++t) acc = hfma(M4[r * 4 + t], K[t * 4 + c], acc);
         Mf[r * 4 + c] = acc;
       }
     // to site order: G[(2 s1' + s2')][(2 s1 + s2)]
