@@ -31,7 +31,7 @@ EXPORTS = (
     "aqc_pair_grads", "aqc_pair_grads_batch", "aqc_argmax_scaled", "aqc_mps_jacobi_stats",
     "aqc_mps_set_jacobi_tol", "aqc_mps_set_jacobi_stop", "aqc_mps_set_jacobi_variant", "aqc_mps_set_fused_chain", "aqc_mps_chain_ticks", "aqc_svd_debug",
     "aqc_sv_pair_rdms", "aqc_mps_pair_rdms", "aqc_mps_pair_rdms_batch", "aqc_entanglement_measures",
-    "aqc_sv_transition", "aqc_mps_product_fit", "aqc_mps_set_jacobi32_stop", "aqc_mps_set_svd_path", "aqc_svd_gram_ticks",
+    "aqc_sv_transition", "aqc_mps_product_fit", "aqc_mps_set_jacobi32_stop", "aqc_mps_set_svd_path", "aqc_svd_gram_ticks", "aqc_bj_ticks",
     "aqc_sweep_set_chain_mode", "aqc_mps_set_jacobi_noise", "aqc_stream_join",
 )
 
@@ -105,6 +105,7 @@ _SIGS = {
     "aqc_mps_set_jacobi32_stop": ([_D], _I),
     "aqc_mps_set_svd_path": ([_I, _I], _I),
     "aqc_svd_gram_ticks": ([_P], _I),
+    "aqc_bj_ticks": ([_P], _I),
     "aqc_sweep_set_chain_mode": ([_I], _I),
     "aqc_stream_join": ([_P], _I),
     "aqc_mps_set_jacobi_noise": ([_D], _I),

@@ -19,6 +19,9 @@
 // ||W||^2 1e-24, a sweep without rotations above 4x the
 // threshold -- or with only rotations moving <= j.jtiny^2 of the norms (t|g|) -- is the last.  Output: W's columns = U sigma,
 // sig = their norms (the k_jacobi contract consumed by k_rank / k_split_*, qr = 0).
+#include <cstdlib>
+#include <cstring>
+
 #include "mps_internal.h"
 
 namespace aqc {
@@ -354,6 +357,299 @@ __global__ __launch_bounds__(1024) void k_bj_cross(const TwoSiteJob* __restrict_
   if (lane == 0 && big) atomicOr(&s.big, 1);
 }
 
+// Block-pair visit of tournament round `round` (the default path; k_bj_intra / k_bj_cross above
+// remain for A/B, AQC_BJ=rot): workgroup p orthogonalises the 32 columns of blocks I = rr(p) and
+// J = rr(nb-1-p) together through their Gram matrix -- Hestenes block Jacobi with one inner sweep:
+//   1. G = A^H A (A = [W_I W_J], L x 32) on the matrix cores: wave w takes a quarter of the rows,
+//      three 16 x 16 tiles (G is Hermitian), partial sums through the LDS;
+//   2. one cyclic Jacobi sweep on G: 31 rounds of 16 disjoint rotations (round-robin), each round
+//      G <- J^H G J and V <- V J computed elementwise from the previous round's copies (double-
+//      buffered LDS), the pair's own 2 x 2 block set exactly (a - t|g|, b + t|g|, 0); rotation rule,
+//      thresholds and stop flags those of rotate_pair on the Gram entries;
+//   3. A <- A V on the matrix cores as A'^T = V^T A^T (a lane group reads and writes 16
+//      consecutive rows of one column).
+// Every pair of columns -- the blocks' own pairs included -- is rotated once per visit, so no
+// intra launch is needed.  grid (nb / 2, nj), 256 threads.
+typedef double __attribute__((ext_vector_type(4))) d4_t;
+constexpr int kPairCols = 2 * kB;  // 32
+// true: the visit forms the blocks' own Gram blocks too; false: their off-diagonal entries are
+// taken as zero (each sweep's intra launch has just orthogonalised them), norms only
+constexpr bool kPairFullGram = false;
+struct PairLds {
+  cplx G[2][kPairCols][kPairCols + 1];
+  cplx V[2][kPairCols][kPairCols + 1];
+  double rc[kB], rtg[kB];
+  cplx rus[kB];
+};
+constexpr size_t kPairLdsBytes = sizeof(PairLds);  // dynamic LDS (> 64 KB of static)
+
+// shader-clock ticks of the pair visits' phases summed over workgroups (thread 0): Gram, Jacobi,
+// A V, visits (aqc_bj_ticks)
+__device__ unsigned long long g_bj_ticks[4];
+
+template <int MAXR>
+__global__ __launch_bounds__(256, 2) void k_bj_pair(const TwoSiteJob* __restrict__ jobs, BJState* __restrict__ st,
+                                                 int round, int nb) {
+  BJState& s = st[blockIdx.y];
+  if (s.done) return;
+  const TwoSiteJob& j = jobs[blockIdx.y];
+  int L, C;
+  bool tr;
+  job_shape(j, L, C, tr);
+  const int I = rr(blockIdx.x, round, nb), J = rr(nb - 1 - blockIdx.x, round, nb);
+  const int cI = I * kB, cJ = J * kB;
+  if (cI >= C && cJ >= C) return;
+  const int nI = max(0, min(kB, C - cI)), nJ = max(0, min(kB, C - cJ));
+  extern __shared__ double2 pair_raw[];
+  PairLds& sm = *reinterpret_cast<PairLds*>(pair_raw);
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, li = lane & 15, lk = lane >> 4;
+  // local column c (0..31) -> W column, or -1 (padding: zero)
+  auto wcol = [&](int c) { return c < kB ? (c < nI ? cI + c : -1) : (c - kB < nJ ? cJ + c - kB : -1); };
+  const cplx* W = j.work;
+  unsigned long long t0 = tid == 0 ? __builtin_amdgcn_s_memtime() : 0ull, t1 = 0, t2 = 0;
+  constexpr int RW = 16 * MAXR;  // rows per wave
+  const int r0 = w * RW;
+  // ---- 1: G = A^H A ----
+  {
+    d4_t gr[3], gi[3];
+#pragma unroll
+    for (int t = 0; t < 3; ++t) gr[t] = d4_t{0, 0, 0, 0}, gi[t] = d4_t{0, 0, 0, 0};
+    double n0 = 0.0, n1 = 0.0;
+    const int ca = wcol(li), cb = wcol(kB + li);
+    // loads kPf k steps ahead of the MFMAs (W streams from the Infinity Cache)
+    constexpr int kPf = 4;
+    cplx pa[kPf], pb[kPf];
+    auto ld = [&](int ks, cplx& x, cplx& y) {
+      const int row = r0 + 4 * ks + lk;
+      x = (ca >= 0 && row < L) ? ldg(W + (size_t)ca * L + row) : cmk(0, 0);
+      y = (cb >= 0 && row < L) ? ldg(W + (size_t)cb * L + row) : cmk(0, 0);
+    };
+#pragma unroll
+    for (int u = 0; u < kPf; ++u) ld(u, pa[u], pb[u]);
+#pragma unroll kPf
+    for (int ks = 0; ks < RW / 4; ++ks) {
+      const cplx a0 = pa[ks % kPf], a1 = pb[ks % kPf];
+      if (ks + kPf < RW / 4) ld(ks + kPf, pa[ks % kPf], pb[ks % kPf]);
+      // conj(x) y: Re += xr yr + xi yi, Im += xr yi - xi yr
+      auto acc = [&](int t, cplx x, cplx y) {
+        gr[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(x.x, y.x, gr[t], 0, 0, 0);
+        gr[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(x.y, y.y, gr[t], 0, 0, 0);
+        gi[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(x.x, y.y, gi[t], 0, 0, 0);
+        gi[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(-x.y, y.x, gi[t], 0, 0, 0);
+      };
+      if constexpr (kPairFullGram) {
+        acc(0, a0, a0);
+        acc(2, a1, a1);
+      } else {  // the blocks' own Gram entries: column norms only (intra launch orthogonalises them)
+        n0 = fma(a0.x, a0.x, fma(a0.y, a0.y, n0));
+        n1 = fma(a1.x, a1.x, fma(a1.y, a1.y, n1));
+      }
+      acc(1, a0, a1);
+    }
+    if constexpr (!kPairFullGram) {  // norms of columns li (block I) and 16 + li (J) in tiles 0, 2
+      n0 += __shfl_xor(n0, 16);
+      n0 += __shfl_xor(n0, 32);
+      n1 += __shfl_xor(n1, 16);
+      n1 += __shfl_xor(n1, 32);
+      // accumulator entry (row lk + 4q, col li): the diagonal sits at lk + 4q == li
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const bool dg = lk + 4 * q == li;
+        gr[0][q] = dg ? n0 : 0.0, gi[0][q] = 0.0;
+        gr[2][q] = dg ? n1 : 0.0, gi[2][q] = 0.0;
+      }
+    }
+    // partials: wave w's tile t entry (row lk + 4q, col li) at V[0..1] as scratch
+    cplx* part = &sm.G[0][0][0];  // 4 waves x 3 tiles x 256 over G[0..1] and V[0..1]
+    static_assert(4 * 3 * 256 <= 4 * kPairCols * (kPairCols + 1), "partial scratch");
+#pragma unroll
+    for (int t = 0; t < 3; ++t)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) part[(w * 3 + t) * 256 + (lk + 4 * q) * 16 + li] = cmk(gr[t][q], gi[t][q]);
+    __syncthreads();
+    cplx gsum[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const int e = tid + 256 * m, i = e >> 5, k = e & 31;
+      int t, a, b;
+      bool cj = false;
+      if (i < kB && k < kB) t = 0, a = i, b = k;
+      else if (i >= kB && k >= kB) t = 2, a = i - kB, b = k - kB;
+      else if (i < kB) t = 1, a = i, b = k - kB;
+      else t = 1, a = k, b = i - kB, cj = true;  // G[i][k] = conj(G[k][i])
+      cplx v = cmk(0, 0);
+#pragma unroll
+      for (int ww = 0; ww < 4; ++ww) {
+        const cplx x = part[(ww * 3 + t) * 256 + a * 16 + b];
+        v.x += x.x, v.y += x.y;
+      }
+      if (cj) v.y = -v.y;
+      if (i == k) v.y = 0.0;
+      gsum[m] = v;
+    }
+    __syncthreads();  // partials read
+#pragma unroll
+    for (int m = 0; m < 4; ++m) sm.G[0][(tid >> 5) + 8 * m][tid & 31] = gsum[m];
+    for (int e = tid; e < kPairCols * kPairCols; e += 256) {
+      const int i = e >> 5, k = e & 31;
+      sm.V[0][i][k] = cmk(i == k ? 1.0 : 0.0, 0.0);
+    }
+  }
+  if (tid == 0) t1 = __builtin_amdgcn_s_memtime();
+  // ---- 2: one cyclic Jacobi sweep on G ----
+  // Thread (P, Q) = (tid / 16, tid % 16) owns the 2 x 2 blocks of G and V at the rows of pair P and
+  // the columns of pair Q, and computes both pairs' rotations itself (redundantly across the 16
+  // threads sharing a pair): one barrier per round.  J[p][p] = J[q][q] = c, J[p][q] = us,
+  // J[q][p] = -conj(us); G' = J^H G J and V' = V J on the block; the diagonal blocks exact.
+  const double tol2 = tol_sq(j, L), floor2 = s.fro * 1e-24, nfl2 = jacobi_noise2(j, s.fro),
+               tiny2 = j.jtiny * j.jtiny;
+  const int P = tid >> 4, Q = tid & 15;
+  int rot = 0, big = 0, any = 0;
+  int cur = 0;
+  auto rrf = [](int pos, int r) {  // rr(pos, r, 32) without the division
+    if (pos == 0) return 0;
+    int v = pos - 1 + r;
+    if (v >= kPairCols - 1) v -= kPairCols - 1;
+    return v + 1;
+  };
+  (void)rrf;
+  for (int r = 0; r < kB; ++r) {
+    __syncthreads();  // G[cur] / V[cur] complete
+    // cross pairs only (block I column k with block J column (k + r) mod 16): 16 rounds of 16
+    // disjoint pairs; the blocks' own pairs are the intra launch's
+    const int pP = P, qP = kB + ((P + r) & (kB - 1)), pQ = Q, qQ = kB + ((Q + r) & (kB - 1));
+    auto rotation = [&](int p, int q, double& c, cplx& us, double& tg, int& flag_rot, int& flag_big) {
+      const double a = sm.G[cur][p][p].x, b = sm.G[cur][q][q].x;
+      const cplx g = sm.G[cur][p][q];
+      const double g2 = g.x * g.x + g.y * g.y;
+      const double thr = fmax(tol2 * a * b, nfl2 * (a + b));
+      c = 1.0, tg = 0.0, us = cmk(0, 0), flag_rot = 0, flag_big = 0;
+      if (g2 > thr && a > floor2 && b > floor2) {
+        double te, pp;
+        jacobi_te(a, b, g2, te, c, pp);
+        us = cmk(c * te * g.x, c * te * g.y);  // u s = c t g / |g|
+        tg = te * g2;                           // t |g|
+        if (g2 > 16.0 * thr) {
+          flag_rot = 1;
+          if (fabs(te) * g2 > tiny2 * (a + b)) flag_big = 1;
+        }
+        return true;
+      }
+      return false;
+    };
+    // each lane computes pair Q's rotation (Q = lane % 16); pair P's comes from the lane of its
+    // own row that holds Q = P (same wave: lane 16 (lane / 16) + P)
+    double cQ, tgQ;
+    cplx usQ;
+    int frQ, fbQ;
+    const bool didQ = rotation(pQ, qQ, cQ, usQ, tgQ, frQ, fbQ);
+    const int src = 16 * (lane >> 4) + P;
+    const double cP = __shfl(cQ, src), tgP = __shfl(tgQ, src);
+    const cplx usP = cmk(__shfl(usQ.x, src), __shfl(usQ.y, src));
+    const bool didP = __shfl((int)didQ, src) != 0;
+    const int frP = frQ, fbP = fbQ;  // used only where P == Q (src == lane)
+    const int nxt = cur ^ 1;
+    const cplx m_pp = sm.G[cur][pP][pQ], m_pq = sm.G[cur][pP][qQ], m_qp = sm.G[cur][qP][pQ], m_qq = sm.G[cur][qP][qQ];
+    cplx n_pp, n_pq, n_qp, n_qq;
+    if (P == Q) {
+      if (didP) {
+        n_pp = cmk(m_pp.x - tgP, 0.0), n_qq = cmk(m_qq.x + tgP, 0.0), n_pq = n_qp = cmk(0, 0);
+        any = 1, rot |= frP, big |= fbP;
+      } else {
+        n_pp = m_pp, n_pq = m_pq, n_qp = m_qp, n_qq = m_qq;
+      }
+    } else {
+      // T = M JQ (columns), then JP^H T (rows)
+      const cplx mus = cmk(-usQ.x, usQ.y);  // -conj(usQ) = J[q][p]
+      const cplx t_pp = cfma(m_pq, mus, cscale(m_pp, cQ)), t_pq = cfma(m_pp, usQ, cscale(m_pq, cQ));
+      const cplx t_qp = cfma(m_qq, mus, cscale(m_qp, cQ)), t_qq = cfma(m_qp, usQ, cscale(m_qq, cQ));
+      // conj(J[x][i]): i = p: conj(J[p][p]) = cP, conj(J[q][p]) = -usP; i = q: conj(J[p][q]) = conj(usP), cP
+      const cplx nus = cmk(-usP.x, -usP.y);
+      n_pp = cfma(nus, t_qp, cscale(t_pp, cP));
+      n_pq = cfma(nus, t_qq, cscale(t_pq, cP));
+      n_qp = cfmac(usP, t_pp, cscale(t_qp, cP));
+      n_qq = cfmac(usP, t_pq, cscale(t_qq, cP));
+    }
+    sm.G[nxt][pP][pQ] = n_pp, sm.G[nxt][pP][qQ] = n_pq, sm.G[nxt][qP][pQ] = n_qp, sm.G[nxt][qP][qQ] = n_qq;
+    {
+      const cplx mus = cmk(-usQ.x, usQ.y);
+      const cplx v_pp = sm.V[cur][pP][pQ], v_pq = sm.V[cur][pP][qQ], v_qp = sm.V[cur][qP][pQ], v_qq = sm.V[cur][qP][qQ];
+      sm.V[nxt][pP][pQ] = cfma(v_pq, mus, cscale(v_pp, cQ));
+      sm.V[nxt][pP][qQ] = cfma(v_pp, usQ, cscale(v_pq, cQ));
+      sm.V[nxt][qP][pQ] = cfma(v_qq, mus, cscale(v_qp, cQ));
+      sm.V[nxt][qP][qQ] = cfma(v_qp, usQ, cscale(v_qq, cQ));
+    }
+    (void)didQ;
+    cur = nxt;
+  }
+  if (tid == 0) t2 = __builtin_amdgcn_s_memtime();
+  // ---- 3: A <- A V (skipped when nothing rotated: uniform via the LDS flag) ----
+  __shared__ int s_any;
+  if (tid == 0) s_any = 0;
+  __syncthreads();
+  if (any) s_any = 1;
+  __syncthreads();
+  if (s_any) {
+    // V^T operands (A_op[i][k] = V[k][i]): jt output tile, ks k step; lane holds i = li, k = lk
+    cplx vt[2][8];
+#pragma unroll
+    for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks) vt[jt][ks] = sm.V[cur][4 * ks + lk][16 * jt + li];
+    int colk[8];
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) colk[ks] = wcol(4 * ks + lk);
+    cplx* Wm = j.work;
+    // row tile rt + 1's loads in flight while rt's MFMAs run
+    cplx bn[8];
+    auto ldt = [&](int rt, cplx (&b)[8]) {
+      const int row = r0 + 16 * rt + li;
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks) b[ks] = (colk[ks] >= 0 && row < L) ? ldg(Wm + (size_t)colk[ks] * L + row) : cmk(0, 0);
+    };
+    ldt(0, bn);
+#pragma unroll 2
+    for (int rt = 0; rt < MAXR; ++rt) {
+      const int row = r0 + 16 * rt + li;
+      cplx b[8];
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks) b[ks] = bn[ks];
+      if (rt + 1 < MAXR) ldt(rt + 1, bn);
+      d4_t orr[2], oi[2];
+#pragma unroll
+      for (int jt = 0; jt < 2; ++jt) {
+        orr[jt] = d4_t{0, 0, 0, 0}, oi[jt] = d4_t{0, 0, 0, 0};
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks) {
+          const cplx x = vt[jt][ks], y = b[ks];
+          orr[jt] = __builtin_amdgcn_mfma_f64_16x16x4f64(x.x, y.x, orr[jt], 0, 0, 0);
+          orr[jt] = __builtin_amdgcn_mfma_f64_16x16x4f64(-x.y, y.y, orr[jt], 0, 0, 0);
+          oi[jt] = __builtin_amdgcn_mfma_f64_16x16x4f64(x.x, y.y, oi[jt], 0, 0, 0);
+          oi[jt] = __builtin_amdgcn_mfma_f64_16x16x4f64(x.y, y.x, oi[jt], 0, 0, 0);
+        }
+      }
+      // every wave has read its rows' 32 columns before any lane writes them (the MFMA results
+      // depend on all the loads)
+#pragma unroll
+      for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int cc = wcol(16 * jt + lk + 4 * q);
+          if (cc >= 0 && row < L) Wm[(size_t)cc * L + row] = cmk(orr[jt][q], oi[jt][q]);
+        }
+    }
+  }
+  if (rot) atomicOr(&s.rot, 1);
+  if (big) atomicOr(&s.big, 1);
+  if (tid == 0) {
+    const unsigned long long t3 = __builtin_amdgcn_s_memtime();
+    atomicAdd(&g_bj_ticks[0], t1 - t0);
+    atomicAdd(&g_bj_ticks[1], t2 - t1);
+    atomicAdd(&g_bj_ticks[2], t3 - t2);
+    atomicAdd(&g_bj_ticks[3], 1ull);
+  }
+}
+
 // End of sweep: decide convergence, reset the sweep flags, count converged jobs.  grid (nj).
 __global__ void k_bj_sweep_end(BJState* __restrict__ st, int* __restrict__ ndone) {
   if (threadIdx.x != 0) return;
@@ -408,6 +704,15 @@ BJBuffers& bj_buffers() {
   return b;
 }
 
+// Block-pair visits on the matrix cores (default) or the per-rotation kernels (AQC_BJ=rot)
+bool bj_pair_mode() {
+  static const bool on = [] {
+    const char* e = std::getenv("AQC_BJ");
+    return !(e && std::strcmp(e, "rot") == 0);
+  }();
+  return on;
+}
+
 template <int MAXR>
 int run_block_jacobi(const TwoSiteJob* jobs, int nj, int cap_max, hipStream_t stream) {
   BJBuffers& b = bj_buffers();
@@ -431,11 +736,20 @@ int run_block_jacobi(const TwoSiteJob* jobs, int nj, int cap_max, hipStream_t st
   hipLaunchKernelGGL(k_bj_init, dim3(nj), dim3(1024), 0, stream, jobs, b.st);
   AQC_CHECK_LAUNCH();
   for (int sweep = 0; sweep < kMaxSweepsBJ; ++sweep) {
-    hipLaunchKernelGGL((k_bj_intra<MAXR>), dim3(nb, nj), dim3(512), lds, stream, jobs, b.st);
-    AQC_CHECK_LAUNCH();
-    for (int r = 0; r < nb - 1; ++r) {
-      hipLaunchKernelGGL((k_bj_cross<MAXR>), dim3(nb / 2, nj), dim3(1024), lds, stream, jobs, b.st, r, nb);
+    if (bj_pair_mode()) {
+      hipLaunchKernelGGL((k_bj_intra<MAXR>), dim3(nb, nj), dim3(512), lds, stream, jobs, b.st);
       AQC_CHECK_LAUNCH();
+      for (int r = 0; r < nb - 1; ++r) {
+        hipLaunchKernelGGL((k_bj_pair<MAXR>), dim3(nb / 2, nj), dim3(256), kPairLdsBytes, stream, jobs, b.st, r, nb);
+        AQC_CHECK_LAUNCH();
+      }
+    } else {
+      hipLaunchKernelGGL((k_bj_intra<MAXR>), dim3(nb, nj), dim3(512), lds, stream, jobs, b.st);
+      AQC_CHECK_LAUNCH();
+      for (int r = 0; r < nb - 1; ++r) {
+        hipLaunchKernelGGL((k_bj_cross<MAXR>), dim3(nb / 2, nj), dim3(1024), lds, stream, jobs, b.st, r, nb);
+        AQC_CHECK_LAUNCH();
+      }
     }
     hipLaunchKernelGGL(k_bj_sweep_end, dim3(nj), dim3(64), 0, stream, b.st, b.ndone);
     AQC_CHECK_LAUNCH();
@@ -460,6 +774,10 @@ int block_jacobi(const TwoSiteJob* jobs, int nj, int cap_max, hipStream_t st) {
     AQC_HIP_CHECK(hipFuncSetAttribute((const void*)k_bj_cross<8>, hipFuncAttributeMaxDynamicSharedMemorySize, 131072));
     AQC_HIP_CHECK(hipFuncSetAttribute((const void*)k_bj_intra<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 65536));
     AQC_HIP_CHECK(hipFuncSetAttribute((const void*)k_bj_cross<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 65536));
+    AQC_HIP_CHECK(hipFuncSetAttribute((const void*)k_bj_pair<8>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)kPairLdsBytes));
+    AQC_HIP_CHECK(hipFuncSetAttribute((const void*)k_bj_pair<4>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)kPairLdsBytes));
     attr = true;
   }
   AQC_REQUIRE(2 * cap_max <= 512, "block Jacobi supports 2 * chi_cap <= 512");
@@ -468,3 +786,13 @@ int block_jacobi(const TwoSiteJob* jobs, int nj, int cap_max, hipStream_t st) {
 }
 
 }  // namespace aqc
+
+extern "C" int aqc_bj_ticks(double* out) {
+  AQC_REQUIRE(out, "aqc_bj_ticks: null argument");
+  unsigned long long t[4];
+  AQC_HIP_CHECK(hipMemcpyFromSymbol(t, HIP_SYMBOL(aqc::g_bj_ticks), sizeof(t)));
+  for (int i = 0; i < 4; ++i) out[i] = (double)t[i];
+  unsigned long long z[4] = {0, 0, 0, 0};
+  AQC_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(aqc::g_bj_ticks), z, sizeof(z)));
+  return AQC_OK;
+}

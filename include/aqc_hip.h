@@ -125,6 +125,9 @@ int aqc_mps_set_svd_path(int gram, int debug_max_chi);
 /* Diagnostics: shader-clock ticks of the Gram path's phases (Gram GEMM, tridiagonalisation,
    eigenvalues, eigenvectors, back-transformation, output) since the last call (then reset); out[8]. */
 int aqc_svd_gram_ticks(double* out);
+/* Block Jacobi pair visits (2 chi > 128), shader-clock ticks summed over workgroups since the
+ * last call: out[0] Gram, out[1] inner Jacobi sweep, out[2] A V, out[3] visits.  Resets. */
+int aqc_bj_ticks(double* out);
 /* Sweep stop of the FP32 preconditioning stage of the mixed-precision two-site SVD (default 1e-3). */
 int aqc_mps_set_jacobi32_stop(double tiny_t);
 /* Jacobi kernel: 2 = register-resident columns with pivoted-QR preconditioning for

@@ -184,6 +184,11 @@ def config5(gates, reps):
     per_gate_ms = 1e3 * el / (reps * gates)
     # one lock-step wave holds all `gates` disjoint updates: nominal flops per launch = gates x
     roof = roof_flops("mps_svd", gates * bench.svd_nominal_flops(2 * chi, 2 * chi))
+    bj = np.zeros(4)
+    _lib.check(_lib.lib().aqc_bj_ticks(_lib.ptr(bj)))  # block-pair visit phases (pair mode)
+    if bj[3] > 0:
+        roof["pair_visit_ticks"] = {"gram": bj[0] / bj[3], "jacobi": bj[1] / bj[3], "apply": bj[2] / bj[3],
+                                    "visits": bj[3]}
     return {"metric": "two-site gate applications/sec at full chi, 100-qubit MPS chi=256 (config 5)",
             "value": reps * gates / el, "unit": "gates/s", "ms_per_gate": per_gate_ms,
             "nominal_tflops": nom / (per_gate_ms * 1e-3) / 1e12, "dtype": "c128", "data": "synthetic random Vidal MPS",
