@@ -2646,7 +2646,8 @@ int aqc_mps_copy(aqc_mps_t dst, const aqc_mps_t src) {
   return AQC_OK;
 }
 
-int apply_batch_impl(aqc_mps_t* hs, int ns, const aqc_op_t* const* ops, const int* nops, bool sort_after) {
+int apply_batch_impl(aqc_mps_t* hs, int ns, const aqc_op_t* const* ops, const int* nops, bool sort_after,
+                     bool check = true) {
   AQC_REQUIRE(hs && ops && nops && ns >= 0, "aqc_mps_apply_batch: null argument");
   std::vector<std::vector<DevOp>> lists(ns);
   for (int s = 0; s < ns; ++s) {
@@ -2661,7 +2662,7 @@ int apply_batch_impl(aqc_mps_t* hs, int ns, const aqc_op_t* const* ops, const in
   }
   int rc = run_waves(hs, ns, lists);
   if (rc != AQC_OK) return rc;
-  return check_flags_batch(hs, ns);
+  return check ? check_flags_batch(hs, ns) : AQC_OK;
 }
 
 int aqc_mps_apply_batch(aqc_mps_t* hs, int ns, const aqc_op_t* const* ops, const int* nops) {
@@ -2670,6 +2671,16 @@ int aqc_mps_apply_batch(aqc_mps_t* hs, int ns, const aqc_op_t* const* ops, const
 
 int aqc_mps_apply_sort_batch(aqc_mps_t* hs, int ns, const aqc_op_t* const* ops, const int* nops) {
   return apply_batch_impl(hs, ns, ops, nops, true);
+}
+
+int aqc_mps_apply_sort_batch_async(aqc_mps_t* hs, int ns, const aqc_op_t* const* ops, const int* nops) {
+  return apply_batch_impl(hs, ns, ops, nops, true, false);
+}
+
+int aqc_mps_check_batch(aqc_mps_t* hs, int ns) {
+  AQC_REQUIRE(hs && ns >= 0, "aqc_mps_check_batch: null argument");
+  for (int s = 0; s < ns; ++s) AQC_REQUIRE(hs[s], "aqc_mps_check_batch: null handle");
+  return check_flags_batch(hs, ns);
 }
 
 int aqc_mps_apply(aqc_mps_t h, const aqc_op_t* ops, int nops) {

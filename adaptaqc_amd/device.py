@@ -211,18 +211,30 @@ def _handles(states):
     return arr
 
 
-def apply_batch(states, ops_lists, sort=False):
+def apply_batch(states, ops_lists, sort=False, wait=True):
     """Apply per-state op lists (one batched launch sequence, or one fused chain per state); with
     sort=True every state also returns to sorted qubit order in the same schedule (an evaluation's
-    replay + save)."""
+    replay + save).  wait=False (sort=True only) returns once the work is queued; call
+    check_batch(states) before using the states."""
     if not states:
         return
     l = _lib.lib()
     arrs = [o if isinstance(o, np.ndarray) else _lib.ops_array(o) for o in ops_lists]
     ptrs = (ctypes.c_void_p * len(arrs))(*[a.ctypes.data if len(a) else 0 for a in arrs])
     counts = np.asarray([len(a) for a in arrs], dtype=np.int32)
+    if not wait and not sort:
+        raise ValueError("apply_batch: wait=False needs sort=True")
     fn = l.aqc_mps_apply_sort_batch if sort else l.aqc_mps_apply_batch
+    if not wait:
+        fn = l.aqc_mps_apply_sort_batch_async
     _lib.check(fn(_handles(states), len(states), ptrs, _lib.ptr(counts)))
+
+
+def check_batch(states):
+    """Wait for the states' queued work and raise on their error flags (after apply_batch(...,
+    wait=False))."""
+    if states:
+        _lib.check(_lib.lib().aqc_mps_check_batch(_handles(states), len(states)))
 
 
 EM_METHOD_CODES = {"concurrence": 0, "eof": 1, "negativity": 2, "log_negativity": 3}

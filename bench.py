@@ -243,6 +243,8 @@ def main():
     ap.add_argument("--cpu-workers", type=int, default=0, help="0: min(16, OMP_NUM_THREADS or cores)")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--no-latency", action="store_true")
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="sweep, then the overlap evaluations with a flag check after the chain (no overlap of host work)")
     ap.add_argument("--simulate-world", type=int, default=0,
                     help="projection only (1 process): rank 0's share of an N-GPU run -- pair shard of N, "
                          "sweep over N x states -- with the all-gather replaced by a local scatter")
@@ -272,7 +274,7 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     from adaptaqc_amd import _lib
-    from adaptaqc_amd.device import DeviceMPS, apply_batch, copy_batch, overlap_zero_batch, pair_grads_batch
+    from adaptaqc_amd.device import DeviceMPS, apply_batch, check_batch, copy_batch, overlap_zero_batch, pair_grads_batch
     from adaptaqc_amd.sharding import PairShard, gather_scores
     from adaptaqc_amd.utils.constants import coupling_map_fully_entangled
 
@@ -325,7 +327,15 @@ def main():
 
     def step():
         full, best = sweep()
-        costs = overlaps()
+        if args.no_pipeline:
+            return full, best, overlaps()
+        # the chain's flags are read after the cost read-back (one host wait per step instead of
+        # two): the overlap kernel's launch is prepared while the chain runs.  (Queuing the chain
+        # before the sweep measured no better: the step is GPU-bound, 59-60 ms either way.)
+        copy_batch(work, reload_src)
+        apply_batch(work, layer_ops, sort=True, wait=False)
+        costs = 1.0 - np.abs(overlap_zero_batch(work)) ** 2
+        check_batch(work)
         return full, best, costs
 
     def barrier():

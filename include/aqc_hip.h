@@ -106,6 +106,12 @@ int aqc_mps_apply_batch(aqc_mps_t* hs, int nstates, const aqc_op_t* const* ops, 
    -- one evaluation's replay + save of mps_from_circuit (aer_mps_backend.py:76-78), so that a
    state's swaps back run in the same fused chain as its gates. */
 int aqc_mps_apply_sort_batch(aqc_mps_t* hs, int nstates, const aqc_op_t* const* ops, const int* nops);
+/* As aqc_mps_apply_sort_batch, but returns once the work is queued: the states' error flags
+   (capacity, Jacobi sweep limit) are not read back -- call aqc_mps_check_batch before using the
+   results.  Lets the host prepare further work (the candidate sweep) while the chain runs. */
+int aqc_mps_apply_sort_batch_async(aqc_mps_t* hs, int nstates, const aqc_op_t* const* ops, const int* nops);
+/* Wait for the states' queued work and report their error flags (AQC_ERR_STATE etc.). */
+int aqc_mps_check_batch(aqc_mps_t* hs, int nstates);
 /* Diagnostics: largest Jacobi sweep count since the last call (then reset). */
 int aqc_mps_jacobi_stats(aqc_mps_t h, int* max_sweeps);
 /* Jacobi rotation threshold |a^H b| > factor * L * eps * |a||b| (default factor 1). */

@@ -19,7 +19,7 @@ def test_bench_overlap_workload_fused_chain_vs_oracle(kind):
     evaluation per distance, each from a different source state, against the oracle replay:
     exact bond dimensions and overlap within 1e-6 (truncated-MPS tolerance of BASELINE.json)."""
     from adaptaqc_amd import _lib
-    from adaptaqc_amd.device import DeviceMPS, apply_batch, copy_batch, overlap_zero_batch
+    from adaptaqc_amd.device import DeviceMPS, apply_batch, check_batch, copy_batch, overlap_zero_batch
 
     n, chi, B = bench.N_QUBITS, bench.CHI, 10
     distinct = bench.bench_states(n, chi, 4, kind)
@@ -34,8 +34,12 @@ def test_bench_overlap_workload_fused_chain_vs_oracle(kind):
            for s in range(B) for i, d in enumerate(bench.DISTANCES)]
     work = [DeviceMPS(n, chi, 1e-16, chi) for _ in ops]
     copy_batch(work, [src[k // 4] for k in range(len(work))])
-    apply_batch(work, ops, sort=True)
+    # the random-state case runs the bench's pipelined form: queued apply, read-back, deferred check
+    pipelined = kind == "random"
+    apply_batch(work, ops, sort=True, wait=not pipelined)
     ov = overlap_zero_batch(work)
+    if pipelined:
+        check_batch(work)
     checked = 0
     for i, d in enumerate(bench.DISTANCES):
         k = 4 * i + i  # state i (source i % 4), distance d
