@@ -334,23 +334,29 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
   }
   tick(1);
   // ---- S4: top-K eigenvalues of T by 17-section ----
-  if (tid == 0) {
-    double lo = 1e300, hi = -1e300, tn = 0.0, e2m = 0.0;
-    for (int i = 0; i < C; ++i) {
+  if (wave == 0) {  // Gershgorin interval, ||T||, e^2 and the (d, e^2) pairs: two rows per lane
+    double lo = 1e300, hi = -1e300, tn = 0.0;
+    for (int i = lane; i < C; i += 64) {
       const double el = i > 0 ? fabs(s_e[i - 1]) : 0.0, er = i < C - 1 ? fabs(s_e[i]) : 0.0;
-      lo = fmin(lo, s_d[i] - el - er);
-      hi = fmax(hi, s_d[i] + el + er);
-      tn = fmax(tn, fabs(s_d[i]) + el + er);
-      if (i < C - 1) {
-        s_e2[i] = s_e[i] * s_e[i];
-        e2m = fmax(e2m, s_e2[i]);
-      }
+      const double di = s_d[i];
+      lo = fmin(lo, di - el - er);
+      hi = fmax(hi, di + el + er);
+      tn = fmax(tn, fabs(di) + el + er);
+      if (i < C - 1) s_e2[i] = s_e[i] * s_e[i];
+      s_de[i] = make_double2(di, i > 0 ? s_e[i - 1] * s_e[i - 1] : 0.0);
     }
-    for (int i = 0; i < C; ++i) s_de[i] = make_double2(s_d[i], i > 0 ? s_e2[i - 1] : 0.0);
-    const double span = fmax(hi - lo, 1e-300);
-    s_lo = lo - 1e-12 * span;
-    s_hi = hi + 1e-12 * span;
-    s_tn = tn;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      lo = fmin(lo, __shfl_xor(lo, off));
+      hi = fmax(hi, __shfl_xor(hi, off));
+      tn = fmax(tn, __shfl_xor(tn, off));
+    }
+    if (lane == 0) {
+      const double span = fmax(hi - lo, 1e-300);
+      s_lo = lo - 1e-12 * span;
+      s_hi = hi + 1e-12 * span;
+      s_tn = tn;
+    }
   }
   __syncthreads();
   {
@@ -427,40 +433,89 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
       h ^= h >> 15;
       zb[row * 64 + i] = (double)(h & 0xFFFFFu) * (2.0 / 1048576.0) - 1.0;
     }
-    // L D L^T = T - lam I once (no pivoting; tiny pivots -> +-eps ||T||): 1 / D_row to Db
+    // L D L^T = T - lam I once (no pivoting; tiny pivots -> +-eps ||T||): 1 / D_row to Db.  The
+    // recurrences below are serial per lane: T's entries and the vectors' rows are loaded eight
+    // rows ahead of the dependent chain (read one at a time, every step waited out an LDS round
+    // trip: 161 K ticks for S5)
+    constexpr int U = 8;
+    // (full chunks unguarded -- C is uniform but not known to the compiler, whose per-row guards
+    // became exec-mask branches -- then a scalar tail; clamped indices with zero carries make the
+    // first / last rows regular)
+    auto fac_row = [&](int row, double d, double e2, double& rdp) {
+      double dj = fma(-e2, rdp, d - lam);
+      if (fabs(dj) < piv) dj = dj >= 0.0 ? piv : -piv;
+      const double rd = rcp_nr(dj);
+      Db[row * 64 + i] = rd;
+      rdp = rd;
+    };
     {
       double rdp = 0.0;
-      for (int row = 0; row < C; ++row) {
-        double dj = s_d[row] - lam;
-        if (row > 0) dj -= s_e2[row - 1] * rdp;
-        if (fabs(dj) < piv) dj = dj >= 0.0 ? piv : -piv;
-        const double rd = rcp_nr(dj);
-        Db[row * 64 + i] = rd;
-        rdp = rd;
+      int r0 = 0;
+      for (; r0 + U <= C; r0 += U) {
+        double dd[U], ee[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) dd[u] = s_d[r0 + u], ee[u] = s_e2[max(r0 + u - 1, 0)];
+#pragma unroll
+        for (int u = 0; u < U; ++u) fac_row(r0 + u, dd[u], ee[u], rdp);
       }
+      for (; r0 < C; ++r0) fac_row(r0, s_d[r0], s_e2[max(r0 - 1, 0)], rdp);
     }
+    double sc = 1.0;  // the previous iteration's normalisation, applied as the forward solve reads
     for (int it = 0; it < 3; ++it) {
-      // forward solve L y = z in place (L_{row, row-1} = e_{row-1} / D_{row-1}), then L^T-solve
+      // forward solve L y = sc z in place (L_{row, row-1} = e_{row-1} / D_{row-1}), then L^T-solve
       // z = D^-1 y - L^T z from the bottom
-      double yp = zb[0 * 64 + i];
-#pragma unroll 8
-      for (int row = 1; row < C; ++row) {
-        const double y = zb[row * 64 + i] - s_e[row - 1] * Db[(row - 1) * 64 + i] * yp;
+      double yp = 0.0;
+      auto fwd_row = [&](int row, double z, double e, double dp) {
+        const double y = fma(z, sc, -e * dp * yp);
         zb[row * 64 + i] = y;
         yp = y;
+      };
+      int r0 = 0;
+      for (; r0 + U <= C; r0 += U) {
+        double zz[U], ee[U], dp[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int rm = max(r0 + u - 1, 0);
+          zz[u] = zb[(r0 + u) * 64 + i], ee[u] = s_e[rm], dp[u] = Db[rm * 64 + i];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) fwd_row(r0 + u, zz[u], ee[u], dp[u]);
       }
-      double zn = zb[(C - 1) * 64 + i] * Db[(C - 1) * 64 + i];
-      zb[(C - 1) * 64 + i] = zn;
-      double n2 = zn * zn;
-#pragma unroll 8
-      for (int row = C - 2; row >= 0; --row) {
-        zn = (zb[row * 64 + i] - s_e[row] * zn) * Db[row * 64 + i];
+      for (; r0 < C; ++r0) {
+        const int rm = max(r0 - 1, 0);
+        fwd_row(r0, zb[r0 * 64 + i], s_e[rm], Db[rm * 64 + i]);
+      }
+      double zn = 0.0, n2 = 0.0;
+      auto bwd_row = [&](int row, double y, double e, double d) {
+        zn = (y - e * zn) * d;
         zb[row * 64 + i] = zn;
         n2 = fma(zn, zn, n2);
+      };
+      int r1 = C - 1;  // rows r1, r1 - 1, ..., r1 - U + 1
+      for (; r1 - U + 1 >= 0; r1 -= U) {
+        double yy[U], ee[U], dd[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int row = r1 - u;
+          yy[u] = zb[row * 64 + i], ee[u] = s_e[min(row, C - 2)], dd[u] = Db[row * 64 + i];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) bwd_row(r1 - u, yy[u], ee[u], dd[u]);
       }
-      const double sc = __builtin_amdgcn_rsq(n2);
-      const double scn = sc * fma(-0.5 * n2 * sc, sc, 1.5);
-      for (int row = 0; row < C; ++row) zb[row * 64 + i] *= scn;
+      for (; r1 >= 0; --r1) bwd_row(r1, zb[r1 * 64 + i], s_e[min(r1, C - 2)], Db[r1 * 64 + i]);
+      const double rs = __builtin_amdgcn_rsq(n2);
+      sc = rs * fma(-0.5 * n2 * rs, rs, 1.5);
+    }
+    {  // the last iteration's normalisation
+      int r0 = 0;
+      for (; r0 + U <= C; r0 += U) {
+        double zz[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) zz[u] = zb[(r0 + u) * 64 + i];
+#pragma unroll
+        for (int u = 0; u < U; ++u) zb[(r0 + u) * 64 + i] = zz[u] * sc;
+      }
+      for (; r0 < C; ++r0) zb[r0 * 64 + i] *= sc;
     }
   }
   __syncthreads();
