@@ -517,6 +517,7 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
       }
       for (; r0 < C; ++r0) zb[r0 * 64 + i] *= sc;
     }
+    if (tid == 0) atomicAdd(&g_gram_ticks[7], __builtin_amdgcn_s_memtime() - t_last);  // S5 A: inverse iteration
   }
   __syncthreads();
   if (wave == 0) {  // Gram-Schmidt inside clusters (uniform loop over wave 0)
@@ -546,12 +547,29 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
   __syncthreads();
   if (tid < K) {
     const int i = tid;
-    double s2 = 0.0;
-    for (int row = 0; row < C; ++row) {
-      const double z = zb[row * 64 + i];
-      s2 = fma(s_d[row] * z, z, s2);
-      if (row < C - 1) s2 = fma(2.0 * s_e[row] * z, zb[(row + 1) * 64 + i], s2);
+    // z^T T z with eight rows' loads in flight and two partial sums (the rows one at a time waited
+    // out an LDS round trip each); the last row's e term is masked by zeroing its factor
+    double s2a = 0.0, s2b = 0.0;
+    int r0 = 0;
+    constexpr int U = 8;
+    for (; r0 + U <= C; r0 += U) {
+      double zz[U + 1], dd[U], ee[U];
+#pragma unroll
+      for (int u = 0; u <= U; ++u) zz[u] = zb[min(r0 + u, C - 1) * 64 + i];
+#pragma unroll
+      for (int u = 0; u < U; ++u) dd[u] = s_d[r0 + u], ee[u] = r0 + u < C - 1 ? s_e[r0 + u] : 0.0;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        s2a = fma(dd[u] * zz[u], zz[u], s2a);
+        s2b = fma(2.0 * ee[u] * zz[u], zz[u + 1], s2b);
+      }
     }
+    for (; r0 < C; ++r0) {
+      const double z = zb[r0 * 64 + i];
+      s2a = fma(s_d[r0] * z, z, s2a);
+      if (r0 < C - 1) s2b = fma(2.0 * s_e[r0] * z, zb[(r0 + 1) * 64 + i], s2b);
+    }
+    const double s2 = s2a + s2b;
     s_sig2[i] = s2 > 0.0 ? s2 : 0.0;
   }
   __syncthreads();
