@@ -13,7 +13,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
-#include <mutex>
+#include <atomic>
 
 #include "aqc_internal.h"
 
@@ -466,6 +466,7 @@ std::vector<SegGate> fuse_segment(const aqc_op_t* ops, const std::vector<int>& i
     bool dead = false;
   };
   std::vector<F> f;
+  f.reserve(idx.size());
   int last[64];
   for (int q = 0; q < 64; ++q) last[q] = -1;
   for (int gi : idx) {
@@ -537,11 +538,11 @@ std::vector<SegGate> fuse_segment(const aqc_op_t* ops, const std::vector<int>& i
 // of a wave; the first order with no conflict, else the one with the fewest extra cycles).
 // Cached per slot set.
 uint32_t lane_map(uint32_t S) {
-  static std::array<uint32_t, 1 << kRegTileBits> cache{};
-  static std::array<char, 1 << kRegTileBits> have{};
-  static std::mutex mu;
-  std::lock_guard<std::mutex> lock(mu);
-  if (have[S]) return cache[S];
+  // cached per slot set: bit 32 marks a computed entry (lock-free reads; a race computes the same
+  // value twice)
+  static std::array<std::atomic<uint64_t>, 1 << kRegTileBits> cache{};
+  const uint64_t c = cache[S].load(std::memory_order_acquire);
+  if (c >> 32) return (uint32_t)c;
   int ns[8], nn = 0;
   for (int b = 0; b < kRegTileBits; ++b)
     if (!((S >> b) & 1u)) ns[nn++] = b;
@@ -585,8 +586,7 @@ uint32_t lane_map(uint32_t S) {
   } while (std::next_permutation(perm, perm + 8));
   uint32_t m = 0;
   for (int j = 0; j < 8; ++j) m |= (uint32_t)best[j] << (4 * j);
-  cache[S] = m;
-  have[S] = 1;
+  cache[S].store((1ull << 32) | m, std::memory_order_release);
   return m;
 }
 
@@ -596,15 +596,16 @@ void build_phases(const std::vector<SegGate>& fused, int K, std::vector<PhaseHdr
   while (remaining > 0) {
     while (done[first]) ++first;
     uint32_t S = 0, blocked = 0;
-    std::vector<size_t> members;
-    for (size_t i = first; i < fused.size() && (int)members.size() < kPhaseMaxGates; ++i) {
+    size_t members[kPhaseMaxGates];
+    int nm = 0;
+    for (size_t i = first; i < fused.size() && nm < kPhaseMaxGates; ++i) {
       if (done[i]) continue;
       const uint32_t gm = (1u << fused[i].t0) | (fused[i].nq == 2 ? (1u << fused[i].t1) : 0u);
       if (gm & blocked) {
         blocked |= gm;
       } else if (__builtin_popcount(S | gm) <= kRegBits) {
         S |= gm;
-        members.push_back(i);
+        members[nm++] = i;
         done[i] = 1;
         --remaining;
       } else {
@@ -617,11 +618,11 @@ void build_phases(const std::vector<SegGate>& fused, int K, std::vector<PhaseHdr
     PhaseHdr h;
     h.slotmask = (int32_t)S;
     h.gate_off = (int32_t)out.size();
-    h.ngates = (int32_t)members.size();
+    h.ngates = (int32_t)nm;
     h.lanemap = lane_map(S);
     ph.push_back(h);
-    for (size_t i : members) {
-      SegGate g = fused[i];
+    for (int mi = 0; mi < nm; ++mi) {
+      SegGate g = fused[members[mi]];
       if (g.nq == 1) {
         g.t0 = slot(g.t0);
       } else {
