@@ -88,8 +88,10 @@ __device__ __forceinline__ double rcp_nr(double x) {
 __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
   extern __shared__ double2 xbuf[];
   __shared__ double s_d[128], s_e[128], s_e2[128], s_lam[kGramMaxK], s_sig2[kGramMaxK];
-  __shared__ cplx s_tau[128];
+  __shared__ cplx s_tau1[129];  // s_tau1[0] = 0 ("reflector -1"), reflector k's tau at s_tau1[k + 1]
+  cplx* const s_tau = s_tau1 + 1;
   __shared__ double s_lo, s_hi, s_tn;
+  __shared__ cplx s_scl, s_ts, s_sprev;  // reflector k's 1 / (alpha - beta), tau / (alpha - beta); s
   __shared__ double2 s_de[128];
   const int chl = j.dims[0], chr = j.dims[2];
   const int M = 2 * chl, N = 2 * chr;
@@ -191,14 +193,16 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
   cplx* pvb = xbuf;        // [2][128] p   (0 at and above row k)
   cplx* vbb = xbuf + 256;  // [2][128] v   (0 at and above row k, 1 at k + 1)
   cplx* zvb = xbuf + 512;  // [2][128] z   (0 at and above row k + 1)
+  cplx* accp = xbuf + 768;   // [8][128] the column pass's partial products g x, per lane of a row
+  cplx* gk1b = xbuf + 1792;  // [128] G^(k)[r][k+1]
   cplx* hh = j.work;       // reflector k at hh[k (2C - k - 1) / 2 + (row - k - 1)]
   // "reflector -1": none, and column 0 of G as z (s = 0)
+  if (tid == 0) s_tau1[0] = aqc::cmk(0, 0);
   if (q == 0) {
     pvb[128 + r] = aqc::cmk(0, 0);
     vbb[128 + r] = aqc::cmk(0, 0);
     zvb[128 + r] = (r > 0 && r < C) ? g[0] : aqc::cmk(0, 0);
   }
-  cplx tau_prev = aqc::cmk(0, 0);
   __syncthreads();
   // reflector k - 1's a2 and s from buffer bp, per wave
   auto prev_scalars = [&](int k, int bp, cplx& a2, cplx& s) {
@@ -207,6 +211,7 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
     cplx kt;
     kt.x = wave_sum_dpp(fma(p0.x, v0.x, fma(p0.y, v0.y, fma(p1.x, v1.x, p1.y * v1.y))));
     kt.y = wave_sum_dpp(fma(p0.x, v0.y, fma(-p0.y, v0.x, fma(p1.x, v1.y, -p1.y * v1.x))));
+    const cplx tau_prev = s_tau[k - 1];
     a2 = aqc::cscale(aqc::cmul(tau_prev, kt), -0.5);
     const cplx pk = pvb[bp * 128 + k];
     s = aqc::cmk(pk.x + 2.0 * a2.x, -pk.y);
@@ -220,10 +225,14 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
     // rows >= k change this phase (row k: reflector k - 1's update gives d_k): waves whose rows
     // are all below k only clear their LDS entries (uniform branch)
     const bool wact = wave * 8 + 7 >= k;
-    cplx tau = aqc::cmk(0, 0);
-    if (wact) {
-      cplx a2, s;
-      prev_scalars(k, bp, a2, s);
+    // Phase A: reflector k - 1's scalars (every active wave: the column pass needs a2 and s), the
+    // column pass, and -- in wave 0 alone, whose rows are finished from k = 8 on -- reflector k's
+    // zlarfg scalars, handed to the other waves through the LDS behind a second barrier.  (With
+    // every wave forming them redundantly, four waves per SIMD issued the whole scalar chain: it
+    // was 60% of this loop's time.)
+    cplx a2 = aqc::cmk(0, 0), s = aqc::cmk(0, 0);
+    if (wact || wave == 0) prev_scalars(k, bp, a2, s);
+    if (wave == 0) {
       // column k of G^(k) below the diagonal: x_r = z_r - s v_r (r > k); alpha = x_{k+1}
       double xn2;
       {
@@ -234,8 +243,8 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
         xn2 = wave_sum_dpp(n0 + n1);
       }
       const cplx alpha = aqc::cfma(aqc::cmk(-s.x, -s.y), vbb[bp * 128 + k + 1], zvb[bp * 128 + k + 1]);
-      // reflector k's scalars (zlarfg), redundantly in every thread; rsq / rcp seeds with Newton
-      // steps (full precision) instead of the IEEE sqrt / divide sequences
+      // reflector k's scalars (zlarfg); rsq / rcp seeds with Newton steps (full precision)
+      // instead of the IEEE sqrt / divide sequences
       const double x2 = fma(alpha.x, alpha.x, fma(alpha.y, alpha.y, xn2));
       double rs = __builtin_amdgcn_rsq(x2);
       rs = rs * fma(-0.5 * x2 * rs, rs, 1.5);
@@ -245,17 +254,26 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
       const double beta = triv ? alpha.x : (alpha.x >= 0.0 ? -nn : nn);
       const double ib = alpha.x >= 0.0 ? -rs : rs;  // 1 / beta
       const double dr = alpha.x - beta, di = alpha.y, id2 = rcp_nr(fma(dr, dr, di * di));
-      tau = triv ? aqc::cmk(0, 0) : aqc::cmk((beta - alpha.x) * ib, -alpha.y * ib);
+      const cplx tau = triv ? aqc::cmk(0, 0) : aqc::cmk((beta - alpha.x) * ib, -alpha.y * ib);
       const cplx scl = triv ? aqc::cmk(0, 0) : aqc::cmk(dr * id2, -di * id2);  // 1 / (alpha - beta)
-      // the own row's reflector k - 1 entries, w_r, and reflector k's column entry
-      // (the Hermitian rank-2 update needs only Re(a2): v w^H + w v^H = v p^H + (p + 2 Re(a2) v) v^H,
-      // so no per-column w_c)
-      const cplx vr = vbb[bp * 128 + r], pr = pvb[bp * 128 + r], zr = zvb[bp * 128 + r];
+      if (lane == 0) {
+        s_tau[k] = tau;
+        s_e[k] = beta;
+        s_scl = scl;
+        s_ts = aqc::cmul(tau, scl);
+        s_sprev = s;
+      }
+    }
+    if (wact) {
+      // the own row's reflector k - 1 entries and w_r (the Hermitian rank-2 update needs only
+      // Re(a2): v w^H + w v^H = v p^H + (p + 2 Re(a2) v) v^H, so no per-column w_c)
+      cplx acc = aqc::cmk(0, 0);
+      const cplx vr = vbb[bp * 128 + r];
+      const cplx pr = pvb[bp * 128 + r];
       const double a2r2 = 2.0 * a2.x;
       const cplx wr = aqc::cmk(fma(a2r2, vr.x, pr.x), fma(a2r2, vr.y, pr.y));
       const double nvx = -vr.x, nvy = -vr.y, nwx = -wr.x, nwy = -wr.y, nsx = -s.x, nsy = -s.y;
       // one pass: g -= v_r conj(p_c) + w_r conj(v_c) (reflector k - 1), acc += g x_c (reflector k)
-      cplx acc = aqc::cmk(0, 0);
 #pragma unroll
       for (int gi = 0; gi < 4; ++gi) {
         if (32 * gi + 31 >= k) {  // uniform; v_c = p_c = z_c = 0 for c < k
@@ -273,45 +291,39 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
         }
         __builtin_amdgcn_sched_barrier(0);
       }
-      // the product used x_k = -s (z_k = 0, v_k = 1) where reflector k has 0, and x_{k+1} = alpha
-      // where it has alpha - beta: one entry each, in the lanes that hold those columns
+      // the product used x_k = -s (z_k = 0, v_k = 1) where reflector k has 0 (and x_{k+1} = alpha
+      // where it has alpha - beta: corrected in phase B): one entry in the lane holding column k
       const cplx gk = pick16(g, k >> 3), gk1 = pick16(g, (k + 1) >> 3);
       if (q == (k & 7)) acc = aqc::cfma(s, gk, acc);
-      if (q == ((k + 1) & 7)) {
-        acc.x = fma(-beta, gk1.x, acc.x);
-        acc.y = fma(-beta, gk1.y, acc.y);
-      }
-      acc.x = aqc::row_sum8(acc.x);
-      acc.y = aqc::row_sum8(acc.y);
-      const bool rowact = r > k && r < C;
-      cplx p = aqc::cmul(aqc::cmul(tau, scl), acc);
-      if (!rowact) p = aqc::cmk(0, 0);
-      // reflector k's v on the own row: 1 at k + 1, scl x_r below, 0 above
-      cplx v = aqc::cmul(aqc::cfma(aqc::cmk(nsx, nsy), vr, zr), scl);
-      if (!(r > k + 1 && r < C)) v = aqc::cmk(r == k + 1 ? 1.0 : 0.0, 0.0);
-      if (q == 0) {
-        pvb[b * 128 + r] = p;
-        vbb[b * 128 + r] = v;
-        if (rowact) hh[(size_t)k * (2 * C - k - 1) / 2 + (r - k - 1)] = v;
-        if (r == k + 1) {
-          s_tau[k] = tau;
-          s_e[k] = beta;
-        }
-      }
-      if (q == ((k + 1) & 7)) {  // z of reflector k: G^(k)[r][k+1] - p_r below row k + 1
-        const bool zr_ok = r > k + 1 && r < C;
-        zvb[b * 128 + r] = zr_ok ? aqc::csub(gk1, p) : aqc::cmk(0, 0);
-      }
       if (q == (k & 7) && r == k) s_d[k] = gk.x;  // G^(k)[k][k]
-    } else {
-      if (q == 0) {
-        pvb[b * 128 + r] = aqc::cmk(0, 0);
-        vbb[b * 128 + r] = aqc::cmk(0, 0);
-      }
-      if (q == ((k + 1) & 7)) zvb[b * 128 + r] = aqc::cmk(0, 0);
+      accp[q * 128 + r] = acc;
+      if (q == ((k + 1) & 7)) gk1b[r] = gk1;
     }
-    // tau of reflector k for the next phase (uniform: the inactive waves never need it)
-    tau_prev = tau;
+    __syncthreads();
+    // Phase B: reflector k's p, v and z, one row per thread of waves 0 and 1 (the row's eight
+    // partial products summed from the LDS; every row, so finished rows get their zeros)
+    int rr = tid;
+    asm volatile("" : "+v"(rr));  // (laundered like q and r)
+    if (rr < 128) {
+      const double beta = s_e[k];
+      const cplx ts = s_ts, scl = s_scl, sk = s_sprev, g1 = gk1b[rr];
+      cplx sum = aqc::cmk(0, 0);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) sum = aqc::cadd(sum, accp[u * 128 + rr]);
+      sum.x = fma(-beta, g1.x, sum.x);  // x_{k+1} = alpha where reflector k has alpha - beta
+      sum.y = fma(-beta, g1.y, sum.y);
+      const bool rowact = rr > k && rr < C, below = rr > k + 1 && rr < C;
+      cplx p = aqc::cmul(ts, sum);
+      if (!rowact) p = aqc::cmk(0, 0);
+      // reflector k's v: 1 at k + 1, scl x_r below, 0 above
+      cplx v = aqc::cmul(aqc::cfma(aqc::cmk(-sk.x, -sk.y), vbb[bp * 128 + rr], zvb[bp * 128 + rr]), scl);
+      if (!below) v = aqc::cmk(rr == k + 1 ? 1.0 : 0.0, 0.0);
+      pvb[b * 128 + rr] = p;
+      vbb[b * 128 + rr] = v;
+      if (rowact) hh[(size_t)k * (2 * C - k - 1) / 2 + (rr - k - 1)] = v;
+      // z of reflector k: G^(k)[r][k+1] - p_r below row k + 1
+      zvb[b * 128 + rr] = below ? aqc::csub(g1, p) : aqc::cmk(0, 0);
+    }
     __syncthreads();
     tick_step(t_a);
   }
