@@ -88,6 +88,7 @@ __device__ __forceinline__ double rcp_nr(double x) {
 __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
   extern __shared__ double2 xbuf[];
   __shared__ double s_d[128], s_e[128], s_e2[128], s_lam[kGramMaxK], s_sig2[kGramMaxK];
+  __shared__ cplx s_ktp[2];
   __shared__ cplx s_tau1[129];  // s_tau1[0] = 0 ("reflector -1"), reflector k's tau at s_tau1[k + 1]
   cplx* const s_tau = s_tau1 + 1;
   __shared__ double s_lo, s_hi, s_tn;
@@ -197,7 +198,10 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
   cplx* gk1b = xbuf + 1792;  // [128] G^(k)[r][k+1]
   cplx* hh = j.work;       // reflector k at hh[k (2C - k - 1) / 2 + (row - k - 1)]
   // "reflector -1": none, and column 0 of G as z (s = 0)
-  if (tid == 0) s_tau1[0] = aqc::cmk(0, 0);
+  if (tid == 0) {
+    s_tau1[0] = aqc::cmk(0, 0);
+    s_ktp[0] = s_ktp[1] = aqc::cmk(0, 0);
+  }
   if (q == 0) {
     pvb[128 + r] = aqc::cmk(0, 0);
     vbb[128 + r] = aqc::cmk(0, 0);
@@ -206,11 +210,8 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
   __syncthreads();
   // reflector k - 1's a2 and s from buffer bp, per wave
   auto prev_scalars = [&](int k, int bp, cplx& a2, cplx& s) {
-    const cplx p0 = pvb[bp * 128 + lane], p1 = pvb[bp * 128 + 64 + lane];
-    const cplx v0 = vbb[bp * 128 + lane], v1 = vbb[bp * 128 + 64 + lane];
-    cplx kt;
-    kt.x = wave_sum_dpp(fma(p0.x, v0.x, fma(p0.y, v0.y, fma(p1.x, v1.x, p1.y * v1.y))));
-    kt.y = wave_sum_dpp(fma(p0.x, v0.y, fma(-p0.y, v0.x, fma(p1.x, v1.y, -p1.y * v1.x))));
+    // p^H v from the two partial sums the p / v pass left (rows 0-63, 64-127)
+    const cplx kt = aqc::cadd(s_ktp[0], s_ktp[1]);
     const cplx tau_prev = s_tau[k - 1];
     a2 = aqc::cscale(aqc::cmul(tau_prev, kt), -0.5);
     const cplx pk = pvb[bp * 128 + k];
@@ -321,6 +322,9 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
       pvb[b * 128 + rr] = p;
       vbb[b * 128 + rr] = v;
       if (rowact) hh[(size_t)k * (2 * C - k - 1) / 2 + (rr - k - 1)] = v;
+      // this wave's share of p^H v for the next column's a2
+      const double ktx = wave_sum_dpp(fma(p.x, v.x, p.y * v.y)), kty = wave_sum_dpp(fma(p.x, v.y, -p.y * v.x));
+      if (lane == 0) s_ktp[wave] = aqc::cmk(ktx, kty);
       // z of reflector k: G^(k)[r][k+1] - p_r below row k + 1
       zvb[b * 128 + rr] = below ? aqc::csub(g1, p) : aqc::cmk(0, 0);
     }
