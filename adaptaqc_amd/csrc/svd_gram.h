@@ -6,9 +6,11 @@
 //       (aqc_gemm.h block_cgemm_tile), left in the accumulators
 //   S2  G's upper triangle through the LDS (packed) into registers: thread t holds row t/8,
 //       columns t%8 + 8i (i < 16)
-//   S3  Householder tridiagonalisation G = Q T Q^H (LAPACK zhetd2, lower): two barriers per column,
-//       the column, the reflector and p = tau G v in double-buffered LDS vectors (zeros at and
-//       above the diagonal: a mask-free rank-2 update), the reflectors packed into the work buffer
+//   S3  Householder tridiagonalisation G = Q T Q^H (LAPACK zhetd2, lower): two barriers per column
+//       (the column pass in every wave with reflector k's zlarfg scalars in wave 0 beside it; then
+//       the rows' p, v, z and p^H v partials, one row per thread of waves 0-1), the column, the
+//       reflector and p = tau G v in double-buffered LDS vectors (zeros at and above the diagonal:
+//       a mask-free rank-2 update), the reflectors packed into the work buffer
 //   S4  the top K eigenvalues of the real symmetric tridiagonal T: one 1024-point Sturm pass and
 //       a binary search bracket each, then 17-section (16 lanes per eigenvalue each evaluate one
 //       Sturm count, one ballot picks the subinterval; 6 rounds)
@@ -70,10 +72,20 @@ __device__ __forceinline__ cplx pick16(const cplx (&g)[16], int i) {
   }
 }
 
-__device__ __forceinline__ double rcp_nr1(double x) {  // one Newton step: ~2^-46
-  const double r = __builtin_amdgcn_rcp(x);
-  return r * fma(-x, r, 2.0);
+// One Sturm-count step q <- (d - x) - e^2 / q (d - x passed in).  The reciprocal is clamped to
+// +-2^600 before its Newton step instead of replacing |q| < pivmin by -pivmin: q = +0 then gives
+// a huge negative next q where LAPACK's guard counted the zero itself -- the same count after the
+// next step (a different count only for an exact zero in the last row, or next to an exact zero
+// off-diagonal).  Two fewer instructions per step than the compare-and-select guard.
+__device__ __forceinline__ double sturm_step(double q, double dmx, double e2) {
+  constexpr double kClamp = 0x1p600;
+  double r = __builtin_amdgcn_rcp(q);
+  r = __builtin_fmin(__builtin_fmax(r, -kClamp), kClamp);
+  r = r * fma(-q, r, 2.0);
+  return fma(-e2, r, dmx);
 }
+// 1 for a negative q (sign bit; q is never -0 here)
+__device__ __forceinline__ int sign_bit(double q) { return (int)((unsigned)__double2hiint(q) >> 31); }
 
 __device__ __forceinline__ double rcp_nr(double x) {
   double r = __builtin_amdgcn_rcp(x);
@@ -378,7 +390,6 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
   {
     const int eid = tid >> 4, sub = tid & 15;
     const int a = C - 1 - eid;  // ascending index of the eid-th largest eigenvalue
-    const double pivmin = 1e-290;
     // first pass: one Sturm count per thread at 1024 points across the Gershgorin interval, then
     // each eigenvalue's bracket by a binary search over the counts (1024-section in one pass,
     // where 17-section would need two and a half); six 17-section rounds follow
@@ -387,14 +398,12 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
     {
       const double x = lo0 + span0 * (double)(tid + 1) * (1.0 / 1025.0);
       double qv = s_de[0].x - x;
-      if (fabs(qv) < pivmin) qv = -pivmin;
-      int cnt = qv < 0.0;
+      int cnt = sign_bit(qv);
 #pragma unroll 4
       for (int i = 1; i < C; ++i) {
         const double2 de = s_de[i];
-        qv = (de.x - x) - de.y * rcp_nr1(qv);
-        if (fabs(qv) < pivmin) qv = -pivmin;
-        cnt += qv < 0.0;
+        qv = sturm_step(qv, de.x - x, de.y);
+        cnt += sign_bit(qv);
       }
       cntb[tid] = cnt;
     }
@@ -413,14 +422,12 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
     for (int round = 0; round < 6; ++round) {
       const double x = lo + (hi - lo) * (double)(sub + 1) * (1.0 / 17.0);
       double qv = s_de[0].x - x;
-      if (fabs(qv) < pivmin) qv = -pivmin;
-      int cnt = qv < 0.0;
+      int cnt = sign_bit(qv);
 #pragma unroll 4
       for (int i = 1; i < C; ++i) {
         const double2 de = s_de[i];  // (d_i, e_{i-1}^2)
-        qv = (de.x - x) - de.y * rcp_nr1(qv);
-        if (fabs(qv) < pivmin) qv = -pivmin;
-        cnt += qv < 0.0;
+        qv = sturm_step(qv, de.x - x, de.y);
+        cnt += sign_bit(qv);
       }
       const unsigned long long bal = __ballot(cnt >= a + 1);
       const unsigned int gm = (unsigned int)(bal >> (lane & ~15)) & 0xFFFFu;
