@@ -100,11 +100,8 @@ __device__ __forceinline__ double rcp_nr(double x) {
 __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
   extern __shared__ double2 xbuf[];
   __shared__ double s_d[128], s_e[128], s_e2[128], s_lam[kGramMaxK], s_sig2[kGramMaxK];
-  __shared__ cplx s_ktp[2];
-  __shared__ cplx s_tau1[129];  // s_tau1[0] = 0 ("reflector -1"), reflector k's tau at s_tau1[k + 1]
-  cplx* const s_tau = s_tau1 + 1;
+  __shared__ cplx s_tau[128];
   __shared__ double s_lo, s_hi, s_tn;
-  __shared__ cplx s_scl, s_ts, s_sprev;  // reflector k's 1 / (alpha - beta), tau / (alpha - beta); s
   __shared__ double2 s_de[128];
   const int chl = j.dims[0], chr = j.dims[2];
   const int M = 2 * chl, N = 2 * chr;
@@ -203,16 +200,35 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
   // reflector k - 1 and multiplies it by reflector k's column in one pass over the columns, and
   // writes (p, v, z) of reflector k.  LDS vectors are double-buffered by phase parity and zero
   // where the reflector vanishes, so neither the update nor the product needs masks.
-  cplx* pvb = xbuf;        // [2][128] p   (0 at and above row k)
-  cplx* vbb = xbuf + 256;  // [2][128] v   (0 at and above row k, 1 at k + 1)
-  cplx* zvb = xbuf + 512;  // [2][128] z   (0 at and above row k + 1)
-  cplx* accp = xbuf + 768;   // [8][128] the column pass's partial products g x, per lane of a row
-  cplx* gk1b = xbuf + 1792;  // [128] G^(k)[r][k+1]
+  // LDS addressing for the column loop from one base laundered once: from a non-inlined function
+  // the dynamic LDS base and the function's own __shared__ arrays are found through a table in
+  // memory, and the compiler re-read it with an s_load per column group -- whose lgkmcnt(0) wait
+  // drained every outstanding LDS read.  The loop's scalars live in the dynamic LDS too; d, e and
+  // tau go to the static arrays after the loop.
+#if defined(__HIP_DEVICE_COMPILE__)
+  using lcplx = __attribute__((address_space(3))) cplx;
+  using ldbl = __attribute__((address_space(3))) double;
+#else  // (the host pass only parses device code)
+  using lcplx = cplx;
+  using ldbl = double;
+#endif
+  lcplx* lb = (lcplx*)xbuf;
+  asm volatile("" : "+s"(lb));
+  lcplx* pvb = lb;           // [2][128] p   (0 at and above row k)
+  lcplx* vbb = lb + 256;     // [2][128] v   (0 at and above row k, 1 at k + 1)
+  lcplx* zvb = lb + 512;     // [2][128] z   (0 at and above row k + 1)
+  lcplx* accp = lb + 768;    // [8][128] the column pass's partial products g x, per lane of a row
+  lcplx* gk1b = lb + 1792;   // [128] G^(k)[r][k+1]
+  lcplx* tauS = lb + 1921;   // reflector k's tau at tauS[k]; tauS[-1] = 0 ("reflector -1")
+  ldbl* eS = (ldbl*)(lb + 2050);  // [128] beta_k = e_k
+  ldbl* dS = (ldbl*)(lb + 2114);  // [128] d_k
+  lcplx* ktp = lb + 2178;    // [2] p^H v partials of the last p / v pass (rows 0-63, 64-127)
+  lcplx* scal = lb + 2180;   // reflector k's 1 / (alpha - beta), tau / (alpha - beta); s of k - 1
   cplx* hh = j.work;       // reflector k at hh[k (2C - k - 1) / 2 + (row - k - 1)]
   // "reflector -1": none, and column 0 of G as z (s = 0)
   if (tid == 0) {
-    s_tau1[0] = aqc::cmk(0, 0);
-    s_ktp[0] = s_ktp[1] = aqc::cmk(0, 0);
+    tauS[-1] = aqc::cmk(0, 0);
+    ktp[0] = ktp[1] = aqc::cmk(0, 0);
   }
   if (q == 0) {
     pvb[128 + r] = aqc::cmk(0, 0);
@@ -223,8 +239,8 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
   // reflector k - 1's a2 and s from buffer bp, per wave
   auto prev_scalars = [&](int k, int bp, cplx& a2, cplx& s) {
     // p^H v from the two partial sums the p / v pass left (rows 0-63, 64-127)
-    const cplx kt = aqc::cadd(s_ktp[0], s_ktp[1]);
-    const cplx tau_prev = s_tau[k - 1];
+    const cplx kt = aqc::cadd(ktp[0], ktp[1]);
+    const cplx tau_prev = tauS[k - 1];
     a2 = aqc::cscale(aqc::cmul(tau_prev, kt), -0.5);
     const cplx pk = pvb[bp * 128 + k];
     s = aqc::cmk(pk.x + 2.0 * a2.x, -pk.y);
@@ -270,11 +286,11 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
       const cplx tau = triv ? aqc::cmk(0, 0) : aqc::cmk((beta - alpha.x) * ib, -alpha.y * ib);
       const cplx scl = triv ? aqc::cmk(0, 0) : aqc::cmk(dr * id2, -di * id2);  // 1 / (alpha - beta)
       if (lane == 0) {
-        s_tau[k] = tau;
-        s_e[k] = beta;
-        s_scl = scl;
-        s_ts = aqc::cmul(tau, scl);
-        s_sprev = s;
+        tauS[k] = tau;
+        eS[k] = beta;
+        scal[0] = scl;
+        scal[1] = aqc::cmul(tau, scl);
+        scal[2] = s;
       }
     }
     if (wact) {
@@ -308,7 +324,7 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
       // where it has alpha - beta: corrected in phase B): one entry in the lane holding column k
       const cplx gk = pick16(g, k >> 3), gk1 = pick16(g, (k + 1) >> 3);
       if (q == (k & 7)) acc = aqc::cfma(s, gk, acc);
-      if (q == (k & 7) && r == k) s_d[k] = gk.x;  // G^(k)[k][k]
+      if (q == (k & 7) && r == k) dS[k] = gk.x;  // G^(k)[k][k]
       accp[q * 128 + r] = acc;
       if (q == ((k + 1) & 7)) gk1b[r] = gk1;
     }
@@ -318,8 +334,8 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
     int rr = tid;
     asm volatile("" : "+v"(rr));  // (laundered like q and r)
     if (rr < 128) {
-      const double beta = s_e[k];
-      const cplx ts = s_ts, scl = s_scl, sk = s_sprev, g1 = gk1b[rr];
+      const double beta = eS[k];
+      const cplx ts = scal[1], scl = scal[0], sk = scal[2], g1 = gk1b[rr];
       cplx sum = aqc::cmk(0, 0);
 #pragma unroll
       for (int u = 0; u < 8; ++u) sum = aqc::cadd(sum, accp[u * 128 + rr]);
@@ -336,7 +352,7 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
       if (rowact) hh[(size_t)k * (2 * C - k - 1) / 2 + (rr - k - 1)] = v;
       // this wave's share of p^H v for the next column's a2
       const double ktx = wave_sum_dpp(fma(p.x, v.x, p.y * v.y)), kty = wave_sum_dpp(fma(p.x, v.y, -p.y * v.x));
-      if (lane == 0) s_ktp[wave] = aqc::cmk(ktx, kty);
+      if (lane == 0) ktp[wave] = aqc::cmk(ktx, kty);
       // z of reflector k: G^(k)[r][k+1] - p_r below row k + 1
       zvb[b * 128 + rr] = below ? aqc::csub(g1, p) : aqc::cmk(0, 0);
     }
@@ -352,7 +368,15 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
       const cplx v = vbb[bp * 128 + C - 1], p = pvb[bp * 128 + C - 1];
       const cplx w = aqc::cfma(a2, v, p);
       const cplx gl = pick16(g, (C - 1) >> 3);
-      s_d[C - 1] = gl.x - 2.0 * (v.x * w.x + v.y * w.y);  // Re(g - v conj(w) - w conj(v))
+      dS[C - 1] = gl.x - 2.0 * (v.x * w.x + v.y * w.y);  // Re(g - v conj(w) - w conj(v))
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < C; i += 1024) {
+    s_d[i] = dS[i];
+    if (i < C - 1) {
+      s_e[i] = eS[i];
+      s_tau[i] = tauS[i];
     }
   }
   __syncthreads();
