@@ -778,10 +778,7 @@ static int sv_scratch(aqc_sv_t h, size_t bytes, char** out) {
   return AQC_OK;
 }
 
-// Host planning of one aqc_sv_apply: segments (tile bits + fused gates), and the phases of the
-// register-tile path.
-static void sv_plan(int n, int K, bool reg_tiles, const aqc_op_t* ops, int nops, std::vector<SegHeader>& hdr,
-                    std::vector<SegGate>& gts, std::vector<PhaseHdr>& phs, std::vector<double>* seg_flops = nullptr) {
+static std::vector<HostSeg> sv_plan_segments(int n, int K, bool reg_tiles, const aqc_op_t* ops, int nops) {
   // register tiles keep the lowest global bits in every tile (runs of 2^low contiguous amplitudes
   // per lane group: a tile of high qubits only reads 16-byte pieces scattered 4 KB apart)
   uint64_t reserve = 0;
@@ -790,45 +787,58 @@ static void sv_plan(int n, int K, bool reg_tiles, const aqc_op_t* ops, int nops,
     const int low = lb_env ? std::atoi(lb_env) : kRegLowBits;
     reserve = (1ull << std::min(std::max(low, 0), 8)) - 1ull;
   }
-  std::vector<HostSeg> segs = build_segments(ops, nops, K, n, reserve);
+  return build_segments(ops, nops, K, n, reserve);
+}
+
+// Segment s of the plan: its header (hdr[s], sized by the caller), its fused gates and phases
+// appended to gts / phs (gate_off indexes the whole list).
+static void sv_plan_one(int n, int K, bool reg_tiles, const aqc_op_t* ops, const HostSeg& seg, size_t s,
+                        std::vector<SegHeader>& hdr, std::vector<SegGate>& gts, std::vector<PhaseHdr>& phs,
+                        std::vector<double>* seg_flops) {
+  // tile bits: segment qubits + lowest free bits up to K
+  uint64_t mask = seg.qmask;
+  for (int b = 0; b < n && __builtin_popcountll(mask) < K; ++b) mask |= (1ull << b);
+  int pos[64];
+  int cnt = 0;
+  for (int b = 0; b < n; ++b)
+    if ((mask >> b) & 1ull) pos[cnt++] = b;
+  std::memset(&hdr[s], 0, sizeof(SegHeader));
+  int local_of[64];
+  for (int j = 0; j < cnt; ++j) {
+    hdr[s].tilebits[j] = pos[j];
+    local_of[pos[j]] = j;
+  }
+  const std::vector<SegGate> fused = fuse_segment(ops, seg.gates, local_of);
+  if (seg_flops) {  // real flops of the fused gates: 1q 2, 2q 4 complex MACs (8 flops) per amplitude
+    double f = 0.0;
+    for (const SegGate& g : fused) f += (g.nq == 1 ? 16.0 : 32.0) * std::ldexp(1.0, n);
+    seg_flops->push_back(f);
+  }
+  if (reg_tiles) {  // gate_off / ngates index the phase list
+    hdr[s].gate_off = (int)phs.size();
+    const size_t before = phs.size();
+    build_phases(fused, K, phs, gts);
+    hdr[s].ngates = (int)(phs.size() - before);
+    // timing experiments only (results wrong): AQC_SV_DEBUG=nogates / nophases
+    static const char* dbg = std::getenv("AQC_SV_DEBUG");
+    if (dbg && std::strcmp(dbg, "nophases") == 0) hdr[s].ngates = 0;
+    if (dbg && std::strcmp(dbg, "nogates") == 0)
+      for (size_t q = before; q < phs.size(); ++q) phs[q].ngates = 0;
+  } else {
+    hdr[s].gate_off = (int)gts.size();
+    hdr[s].ngates = (int)fused.size();
+    gts.insert(gts.end(), fused.begin(), fused.end());
+  }
+}
+
+// Host planning of one aqc_sv_apply: segments (tile bits + fused gates), and the phases of the
+// register-tile path.
+static void sv_plan(int n, int K, bool reg_tiles, const aqc_op_t* ops, int nops, std::vector<SegHeader>& hdr,
+                    std::vector<SegGate>& gts, std::vector<PhaseHdr>& phs, std::vector<double>* seg_flops = nullptr) {
+  const std::vector<HostSeg> segs = sv_plan_segments(n, K, reg_tiles, ops, nops);
   hdr.assign(segs.size(), SegHeader{});
   gts.reserve(nops);
-  for (size_t s = 0; s < segs.size(); ++s) {
-    // tile bits: segment qubits + lowest free bits up to K
-    uint64_t mask = segs[s].qmask;
-    for (int b = 0; b < n && __builtin_popcountll(mask) < K; ++b) mask |= (1ull << b);
-    int pos[64];
-    int cnt = 0;
-    for (int b = 0; b < n; ++b)
-      if ((mask >> b) & 1ull) pos[cnt++] = b;
-    std::memset(&hdr[s], 0, sizeof(SegHeader));
-    int local_of[64];
-    for (int j = 0; j < cnt; ++j) {
-      hdr[s].tilebits[j] = pos[j];
-      local_of[pos[j]] = j;
-    }
-    const std::vector<SegGate> fused = fuse_segment(ops, segs[s].gates, local_of);
-    if (seg_flops) {  // real flops of the fused gates: 1q 2, 2q 4 complex MACs (8 flops) per amplitude
-      double f = 0.0;
-      for (const SegGate& g : fused) f += (g.nq == 1 ? 16.0 : 32.0) * std::ldexp(1.0, n);
-      seg_flops->push_back(f);
-    }
-    if (reg_tiles) {  // gate_off / ngates index the phase list
-      hdr[s].gate_off = (int)phs.size();
-      const size_t before = phs.size();
-      build_phases(fused, K, phs, gts);
-      hdr[s].ngates = (int)(phs.size() - before);
-      // timing experiments only (results wrong): AQC_SV_DEBUG=nogates / nophases
-      static const char* dbg = std::getenv("AQC_SV_DEBUG");
-      if (dbg && std::strcmp(dbg, "nophases") == 0) hdr[s].ngates = 0;
-      if (dbg && std::strcmp(dbg, "nogates") == 0)
-        for (size_t q = before; q < phs.size(); ++q) phs[q].ngates = 0;
-    } else {
-      hdr[s].gate_off = (int)gts.size();
-      hdr[s].ngates = (int)fused.size();
-      gts.insert(gts.end(), fused.begin(), fused.end());
-    }
-  }
+  for (size_t s = 0; s < segs.size(); ++s) sv_plan_one(n, K, reg_tiles, ops, segs[s], s, hdr, gts, phs, seg_flops);
 }
 
 static bool sv_reg_tiles(int n) {
@@ -947,18 +957,25 @@ int aqc_sv_apply(aqc_sv_t h, const aqc_op_t* ops, int nops) {
     }
   }
   const int K = h->K;
-  std::vector<SegHeader> hdr;
+  // Planned and launched in batches of 2, 4, 8, ... segments: the host plans the next batch while
+  // the GPU runs the previous one (planned whole, the GPU waited out the ~150 us of host fusion of
+  // a 20-qubit evaluation).  One pinned staging buffer [headers | phases | gates] with capacity
+  // offsets (phases and fused gates are each at most nops); each batch copies the byte range from
+  // its first header to its last gate -- bytes of later batches in that range are re-copied by
+  // their own batch, later in stream order.  The previous call's copies have finished reading the
+  // staging buffer once plan_ev has completed.
+  const std::vector<HostSeg> segs = sv_plan_segments(h->n, K, h->reg_tiles, ops, nops);
+  const size_t nseg = segs.size();
+  std::vector<SegHeader> hdr(nseg);
   std::vector<SegGate> gts;
   std::vector<PhaseHdr> phs;
   std::vector<double> flops;
-  sv_plan(h->n, K, h->reg_tiles, ops, nops, hdr, gts, phs, &flops);
-  // one pinned staging copy of the plan [headers | phases | gates]: the previous call's copy has
-  // finished reading it once plan_ev has completed; the device copy is ordered on the stream
-  // after the previous call's launches
+  gts.reserve(nops);
+  phs.reserve(nops);
   auto al = [](size_t b) { return (b + 255) / 256 * 256; };
-  const size_t o_ph = al(sizeof(SegHeader) * hdr.size());
-  const size_t o_g = o_ph + al(sizeof(PhaseHdr) * phs.size());
-  const size_t bytes = o_g + sizeof(SegGate) * gts.size();
+  const size_t o_ph = al(sizeof(SegHeader) * nseg);
+  const size_t o_g = o_ph + al(sizeof(PhaseHdr) * (size_t)nops);
+  const size_t bytes = o_g + sizeof(SegGate) * (size_t)nops;
   if (bytes > h->plan_cap) {
     AQC_HIP_CHECK(hipStreamSynchronize(h->stream));
     if (h->d_plan) AQC_HIP_CHECK(hipFree(h->d_plan));
@@ -969,20 +986,41 @@ int aqc_sv_apply(aqc_sv_t h, const aqc_op_t* ops, int nops) {
     AQC_HIP_CHECK(hipHostMalloc(&h->h_plan, h->plan_cap, hipHostMallocDefault));
   }
   AQC_HIP_CHECK(hipEventSynchronize(h->plan_ev));
-  std::memcpy(h->h_plan, hdr.data(), sizeof(SegHeader) * hdr.size());
-  if (!phs.empty()) std::memcpy(h->h_plan + o_ph, phs.data(), sizeof(PhaseHdr) * phs.size());
-  if (!gts.empty()) std::memcpy(h->h_plan + o_g, gts.data(), sizeof(SegGate) * gts.size());
-  AQC_HIP_CHECK(hipMemcpyAsync(h->d_plan, h->h_plan, bytes, hipMemcpyHostToDevice, h->stream));
-  AQC_HIP_CHECK(hipEventRecord(h->plan_ev, h->stream));
   const SegHeader* dh = reinterpret_cast<const SegHeader*>(h->d_plan);
   const PhaseHdr* dp = reinterpret_cast<const PhaseHdr*>(h->d_plan + o_ph);
   const SegGate* dg = reinterpret_cast<const SegGate*>(h->d_plan + o_g);
   const int nblocks = (int)(1ull << (h->n - K));
-  for (size_t s = 0; s < hdr.size(); ++s) {
-    int rc = sv_launch_segment(h, dh + s, dp, dg, nblocks, flops[s]);
-    if (rc != AQC_OK) return rc;
+  size_t ph_done = 0, g_done = 0;
+  int rc = AQC_OK;
+  for (size_t s0 = 0, batch = 2; s0 < nseg && rc == AQC_OK; batch *= 2) {
+    const size_t s1 = std::min(nseg, s0 + batch);
+    for (size_t s = s0; s < s1; ++s) sv_plan_one(h->n, K, h->reg_tiles, ops, segs[s], s, hdr, gts, phs, &flops);
+    if (phs.size() > (size_t)nops || gts.size() > (size_t)nops) {
+      aqc::set_error("aqc_sv_apply: plan exceeds its staging bound");
+      rc = AQC_ERR_STATE;
+      break;
+    }
+    std::memcpy(h->h_plan + sizeof(SegHeader) * s0, hdr.data() + s0, sizeof(SegHeader) * (s1 - s0));
+    if (phs.size() > ph_done)
+      std::memcpy(h->h_plan + o_ph + sizeof(PhaseHdr) * ph_done, phs.data() + ph_done,
+                  sizeof(PhaseHdr) * (phs.size() - ph_done));
+    if (gts.size() > g_done)
+      std::memcpy(h->h_plan + o_g + sizeof(SegGate) * g_done, gts.data() + g_done, sizeof(SegGate) * (gts.size() - g_done));
+    const size_t lo = sizeof(SegHeader) * s0, hi = o_g + sizeof(SegGate) * gts.size();
+    ph_done = phs.size();
+    g_done = gts.size();
+    hipError_t e = hipMemcpyAsync(h->d_plan + lo, h->h_plan + lo, hi - lo, hipMemcpyHostToDevice, h->stream);
+    if (e != hipSuccess) {
+      aqc::set_error(std::string("aqc_sv_apply: plan copy: ") + hipGetErrorString(e));
+      rc = AQC_ERR_HIP;
+      break;
+    }
+    for (size_t s = s0; s < s1 && rc == AQC_OK; ++s) rc = sv_launch_segment(h, dh + s, dp, dg, nblocks, flops[s]);
+    s0 = s1;
   }
-  return AQC_OK;
+  // (recorded on every path, so the next call never reuses the staging buffer under a live copy)
+  AQC_HIP_CHECK(hipEventRecord(h->plan_ev, h->stream));
+  return rc;
 }
 
 int aqc_sv_plan(int n, const aqc_op_t* ops, int nops, int* out) {
