@@ -32,7 +32,7 @@ EXPORTS = (
     "aqc_mps_set_jacobi_tol", "aqc_mps_set_jacobi_stop", "aqc_mps_set_jacobi_variant", "aqc_mps_set_fused_chain", "aqc_mps_chain_ticks", "aqc_svd_debug",
     "aqc_sv_pair_rdms", "aqc_mps_pair_rdms", "aqc_mps_pair_rdms_batch", "aqc_entanglement_measures",
     "aqc_sv_transition", "aqc_mps_product_fit", "aqc_mps_set_jacobi32_stop", "aqc_mps_set_svd_path", "aqc_svd_gram_ticks", "aqc_bj_ticks",
-    "aqc_sweep_set_chain_mode", "aqc_mps_set_jacobi_noise", "aqc_stream_join",
+    "aqc_sweep_set_chain_mode", "aqc_mps_set_jacobi_noise", "aqc_stream_join", "aqc_stream_wait",
 )
 
 
@@ -110,6 +110,7 @@ _SIGS = {
     "aqc_bj_ticks": ([_P], _I),
     "aqc_sweep_set_chain_mode": ([_I], _I),
     "aqc_stream_join": ([_P], _I),
+    "aqc_stream_wait": ([_P], _I),
     "aqc_mps_set_jacobi_noise": ([_D], _I),
 }
 

@@ -26,7 +26,7 @@ import numpy as np
 
 from ..circuit import device_ops, mps_payload
 from ..device import DeviceMPS
-from ..mps_operations import apply_checked, chi_cap_for, zero_aer_mps
+from ..mps_operations import DevicePreprocessedMPS, apply_checked, chi_cap_for, zero_aer_mps
 from .aqc_backend import AQCBackend
 
 logger = logging.getLogger(__name__)
@@ -123,8 +123,14 @@ class AerMPSBackend(AQCBackend):
         return 0.5 * (1 - np.mean(evals))
 
     def evaluate_circuit(self, compiler):
-        """Preprocessed MPS (list of (2, chi_l, chi_r) arrays), as the reference returns."""
-        return self.device_state(compiler.full_circuit).preprocessed()
+        """Preprocessed MPS (list of (2, chi_l, chi_r) arrays), as the reference returns -- a
+        ``DevicePreprocessedMPS``: the host arrays are fetched on first read, and a device snapshot
+        of the state rides along so the reference's per-pair ``mpsops.partial_trace`` in the ISL
+        sweep (entanglement_measures.py:76-79) runs on the device without re-uploading it."""
+        work = self.device_state(compiler.full_circuit)
+        snap = self.new_state()
+        snap.copy_from(work)
+        return DevicePreprocessedMPS(snap)
 
     def measure_qubit_expectation_values(self, compiler):
         psi = self.device_state(compiler.full_circuit)

@@ -28,8 +28,42 @@ from ..statevector import Statevector
 from .aqc_backend import AQCBackend
 
 
+class SVJob:
+    """What ``simulator.run`` returns: ``.result()`` is available at once (the device work is
+    already queued on the library's stream; reading the statevector synchronises)."""
+
+    def __init__(self, result):
+        self._result = result
+
+    def result(self):
+        return self._result
+
+    def status(self):
+        return "DONE"
+
+
+class SVResult:
+    def __init__(self, statevector):
+        self._sv = statevector
+
+    def get_statevector(self, experiment=None):
+        return self._sv
+
+    def get_counts(self, experiment=None):
+        raise NotImplementedError("the statevector simulator has no shot counts (shot sampling is outside the "
+                                  "MI355X overlap/gradient path)")
+
+
 class SVSimulator:
-    """Stand-in for Aer's ``statevector_simulator`` handle held as ``backend.simulator``."""
+    """Stand-in for Aer's ``statevector_simulator`` handle held as ``backend.simulator``.
+
+    ``run(circuit, **options)`` is the call the reference makes through
+    ``co.run_circuit_without_transpilation`` (circuit_operations_running.py:44-69, reached from the
+    ISL sweep, entanglement_measures.py:71-75): it simulates the circuit on the device and returns a
+    job whose ``.result().get_statevector()`` is a device-resident statevector.  The ISL sweep runs
+    the same ``full_circuit`` once per coupling-map pair (adapt_compiler.py:964-974); the last run's
+    gate list is kept with its device state, so an unchanged circuit is simulated once.  Backend
+    options and execute kwargs (method, shots, optimization_level, ...) have no meaning here."""
 
     name = "hip_statevector_simulator"
 
@@ -37,9 +71,31 @@ class SVSimulator:
         from types import SimpleNamespace
 
         self.options = SimpleNamespace(method="statevector")
+        self._last = None  # (n, ops bytes, DeviceStatevector)
+
+    def __getstate__(self):
+        d = dict(self.__dict__)
+        d["_last"] = None
+        return d
 
     def __repr__(self):
         return "SVSimulator(hip, gfx950)"
+
+    def run(self, circuit, **options):
+        from ..statevector import DeviceStatevector
+
+        from .. import _lib
+
+        ops = _lib.ops_array(device_ops(circuit))
+        n = circuit.num_qubits
+        key = ops.tobytes()
+        if self._last is not None and self._last[0] == n and self._last[1] == key:
+            return SVJob(SVResult(self._last[2]))
+        dev = DeviceSV(n)
+        dev.apply(ops)
+        sv = DeviceStatevector(dev)
+        self._last = (n, key, sv)
+        return SVJob(SVResult(sv))
 
 
 class AerSVBackend(AQCBackend):

@@ -2627,6 +2627,19 @@ int aqc_stream_join(void* stream) {
   return AQC_OK;
 }
 
+int aqc_stream_wait(void* stream) {
+  static std::mutex mu;
+  static hipEvent_t ev[64] = {nullptr};
+  int dev = 0;
+  AQC_HIP_CHECK(hipGetDevice(&dev));
+  AQC_REQUIRE(dev >= 0 && dev < 64, "aqc_stream_wait: device index out of range");
+  std::lock_guard<std::mutex> lk(mu);
+  if (!ev[dev]) AQC_HIP_CHECK(hipEventCreateWithFlags(&ev[dev], hipEventDisableTiming));
+  AQC_HIP_CHECK(hipEventRecord(ev[dev], (hipStream_t)stream));
+  AQC_HIP_CHECK(hipStreamWaitEvent(aqc::mps_stream(), ev[dev], 0));
+  return AQC_OK;
+}
+
 int aqc_mps_copy(aqc_mps_t dst, const aqc_mps_t src) {
   AQC_REQUIRE(dst && src && dst->d.n == src->d.n && dst->d.cap == src->d.cap, "aqc_mps_copy: handle mismatch");
   hipStream_t st = aqc::mps_stream();

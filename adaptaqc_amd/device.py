@@ -268,8 +268,10 @@ def overlap_zero_batch(states):
 
 def pair_grads_batch(states, svec, pairs, u0, gens, degs, out=None):
     """Per-state gradient norms for every pair; ``out`` may be a device pointer (int): then the call
-    returns once the work is queued, and torch's current stream is ordered after it
-    (aqc_stream_join), so torch ops on ``out`` (the all-gather, the arg-max) see the scores."""
+    returns once the work is queued and is ordered both ways against torch's current stream -- the
+    sweep waits for the torch work queued before it (aqc_stream_wait: a fill of ``out``, the
+    previous step's reads of it), and torch's stream waits for the sweep (aqc_stream_join), so
+    torch ops on ``out`` (the all-gather, the arg-max) see the scores."""
     l = _lib.lib()
     svec = np.ascontiguousarray(np.asarray(svec, dtype=np.complex128).reshape(-1))
     pairs = np.ascontiguousarray(np.asarray(pairs, dtype=np.int32).reshape(-1))
@@ -282,7 +284,10 @@ def pair_grads_batch(states, svec, pairs, u0, gens, degs, out=None):
         host = np.zeros((len(states), npairs))
         outp, is_dev = _lib.ptr(host), 0
     else:
+        import torch
+
         host, outp, is_dev = None, ctypes.c_void_p(int(out)), 1
+        _lib.check(l.aqc_stream_wait(ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)))
     _lib.check(
         l.aqc_pair_grads_batch(
             _handles(states), len(states), _lib.ptr(svec), _lib.ptr(pairs), npairs, _lib.ptr(u0),

@@ -114,6 +114,8 @@ def mps_from_circuit(circuit: QuantumCircuit, return_preprocessed=False, sim=Non
 def _as_device(mps, already_preprocessed, like: DeviceMPS | None = None):
     if isinstance(mps, DeviceMPS):
         return mps
+    if isinstance(mps, DevicePreprocessedMPS):
+        return mps.device
     if not already_preprocessed and check_mps(mps):
         aer = mps
     else:
@@ -128,8 +130,9 @@ def _as_device(mps, already_preprocessed, like: DeviceMPS | None = None):
 
 
 def _is_zero_state(mps, pre):
-    """Host MPS equal to |0...0> (every site a (2,1,1) tensor [1, 0])."""
-    if isinstance(mps, DeviceMPS):
+    """Host MPS equal to |0...0> (every site a (2,1,1) tensor [1, 0]).  Device-backed states
+    answer False: the check is only a fast path, and the general dot gives the same value."""
+    if isinstance(mps, (DeviceMPS, DevicePreprocessedMPS)):
         return False
     try:
         sites = mps if pre else _preprocess_mps(mps)
@@ -139,6 +142,8 @@ def _is_zero_state(mps, pre):
 
 
 def _to_aer_like(mps, pre):
+    if isinstance(mps, DevicePreprocessedMPS):
+        return mps.device.to_aer(), False
     if isinstance(mps, DeviceMPS):
         return mps.to_aer(), False
     return mps, pre
@@ -184,6 +189,81 @@ def extract_amplitude(mps, index, already_preprocessed=False):
     bd = DeviceMPS(n, d.chi_cap)
     bd.load_aer(basis)
     return bd.dot(d)
+
+
+class DevicePreprocessedMPS(list):
+    """A preprocessed MPS (list of (2, chi_l, chi_r) host arrays, what the reference's
+    ``AerMPSBackend.evaluate_circuit`` returns, aer_mps_backend.py:76-78) that also carries a device
+    snapshot of the same state.  ``partial_trace`` and the other helpers here use the snapshot
+    instead of uploading the host tensors again; the host arrays are fetched lazily."""
+
+    def __init__(self, device: DeviceMPS):
+        super().__init__()
+        self._device = device
+        self._filled = False
+        self._rdms = None
+
+    def _fill(self):
+        if not self._filled:
+            self._filled = True
+            super().extend(self._device.preprocessed())
+
+    # every read of the list contents goes through _fill
+    def __len__(self):
+        return self._device.n
+
+    def __getitem__(self, i):
+        self._fill()
+        return super().__getitem__(i)
+
+    def __iter__(self):
+        self._fill()
+        return super().__iter__()
+
+    def __reduce__(self):  # pickles (checkpoints) as the plain host list
+        self._fill()
+        return (list, (list(super().__iter__()),))
+
+    @property
+    def device(self) -> DeviceMPS:
+        return self._device
+
+    def all_pair_rdms(self):
+        """{(a, b): 4x4} for every a < b, computed in one batched device sweep and memoised."""
+        if self._rdms is None:
+            n = self._device.n
+            pairs = [(a, b) for a in range(n) for b in range(a + 1, n)]
+            r = self._device.pair_rdms(pairs) if pairs else np.zeros((0, 4, 4), complex)
+            self._rdms = {p: r[k] for k, p in enumerate(pairs)}
+        return self._rdms
+
+    def pair_rdms(self, pairs):
+        return self._device.pair_rdms(pairs)
+
+
+_pt_cache = {"obj": None, "dev": None, "rdms": None}
+
+
+def partial_trace(mps, qubits, already_preprocessed=False):
+    """aqc_research ``partial_trace(mps, [q1, q2], already_preprocessed)``: the 4x4 reduced density
+    matrix of two qubits (row index 2*bit(max) + bit(min), as qiskit's partial trace orders the
+    kept qubits), called per coupling-map pair by the reference's ISL sweep
+    (entanglement_measures.py:76-79, adapt_compiler.py:964-974).  The first call on a state computes
+    every pair's RDM in one device sweep (aqc_mps_pair_rdms); the following calls on the same state
+    are lookups."""
+    q = [int(x) for x in qubits]
+    if len(q) != 2 or q[0] == q[1]:
+        raise ValueError("partial_trace keeps exactly two distinct qubits")
+    key = (min(q), max(q))
+    if isinstance(mps, DevicePreprocessedMPS):
+        return mps.all_pair_rdms()[key].copy()
+    if _pt_cache["obj"] is not mps:
+        dev = _as_device(mps, already_preprocessed)
+        n = dev.n
+        pairs = [(a, b) for a in range(n) for b in range(a + 1, n)]
+        r = dev.pair_rdms(pairs)
+        _pt_cache.update(obj=mps, dev=dev, rdms={p: r[k] for k, p in enumerate(pairs)})
+    return _pt_cache["rdms"][key].copy()
 
 
 def mps_to_vector(mps, already_preprocessed=False):

@@ -121,7 +121,13 @@ def log_negativity(rho):
 
 
 def partial_trace(statevector, a, b):
-    """4x4 RDM of qubits a, b of a statevector (reference :326-340), computed on the device."""
+    """4x4 RDM of qubits a, b of a statevector (reference :326-340), computed on the device.  A
+    device-resident statevector (``SVSimulator.run(...).result().get_statevector()``) is traced
+    in place; host data is uploaded first."""
+    from ..statevector import DeviceStatevector
+
+    if isinstance(statevector, DeviceStatevector):
+        return statevector.pair_rdm(a, b).copy()
     psi = np.asarray(getattr(statevector, "data", statevector), dtype=np.complex128)
     n = int(round(np.log2(len(psi))))
     st = DeviceSV(n)

@@ -199,7 +199,8 @@ int aqc_mps_amps_hw1(aqc_mps_t h, double* out);
  * out: npairs doubles; out_is_device != 0 means `out` is a device pointer (for RCCL).
  * With a host `out` the call returns when the scores are there; with a device `out` it returns
  * once the work is queued on the library's stream: aqc_stream_join orders another stream (the
- * caller's, e.g. the all-gather's) after it. */
+ * caller's, e.g. the all-gather's) after it, and aqc_stream_wait (called before) orders the sweep
+ * after the caller's earlier work on `out`. */
 int aqc_pair_grads(aqc_mps_t psi, const double* svec, const int* pairs, int npairs,
                    const double* u0, const double* gens, const double* degs, int ngen,
                    double* out, int out_is_device);
@@ -214,6 +215,12 @@ int aqc_sweep_set_chain_mode(int mode);
 /* Orders `stream` (a hipStream_t of the current device; NULL = the legacy default stream) after
    everything queued so far on the library's stream of that device, without a host wait. */
 int aqc_stream_join(void* stream);
+/* The reverse order: the library's stream of the current device waits for everything queued so far
+ * on `stream`, without a host wait.  A device-output sweep (out_is_device) is ordered both ways by
+ * calling aqc_stream_wait(caller) before it -- so the sweep's writes to `out` follow the caller's
+ * earlier kernels on that buffer (a fill, the previous step's reads) -- and aqc_stream_join(caller)
+ * after it, so the caller's later kernels see the scores. */
+int aqc_stream_wait(void* stream);
 /* Best product-state (chi = 1) approximation of psi: the starting circuit
  * starting_circuit="tenpy_product_state" (approximate_compiler.py:222-242, which compresses with
  * tenpy's variational method: trunc_params chi_max = 1, min_sweeps 10, max_sweeps 50).  Alternating

@@ -88,7 +88,15 @@ def from_ir(ir_circuit):
 
 def fake_reference_modules():
     """Modules shaped like the reference's backend classes (an ABC AQCBackend with AerMPSBackend /
-    AerSVBackend subclasses) and the names reference_binding rebinds; installed in sys.modules."""
+    AerSVBackend subclasses) and the names reference_binding rebinds; installed in sys.modules.
+
+    The ISL sweep's reference path is restated here as the reference's own code runs it, every
+    cross-module name resolved at call time through the module objects as in the reference:
+    ``AdaptCompiler._get_all_qubit_pair_entanglement_measures`` (adapt_compiler.py:955-976) ->
+    ``calculate_entanglement_measure`` (entanglement_measures.py:39-98) ->
+    ``co.run_circuit_without_transpilation`` (circuit_operations_running.py:44-69) ->
+    ``backend.simulator.run(...).result().get_statevector()`` and ``partial_trace`` (:325-340), or
+    ``mpsops.partial_trace`` on the MPS from ``backend.evaluate_circuit``."""
     class AQCBackend(abc.ABC):
         @abc.abstractmethod
         def evaluate_global_cost(self, compiler):
@@ -108,8 +116,89 @@ def fake_reference_modules():
     mods = {}
     for name in ("adaptaqc", "adaptaqc.backends", "adaptaqc.backends.aqc_backend", "adaptaqc.backends.aer_mps_backend",
                  "adaptaqc.backends.aer_sv_backend", "adaptaqc.compilers", "adaptaqc.compilers.approximate_compiler",
-                 "adaptaqc.utils", "adaptaqc.utils.gradients", "aqc_research", "aqc_research.mps_operations"):
+                 "adaptaqc.compilers.adapt", "adaptaqc.compilers.adapt.adapt_compiler",
+                 "adaptaqc.utils", "adaptaqc.utils.gradients", "adaptaqc.utils.entanglement_measures",
+                 "adaptaqc.utils.circuit_operations", "adaptaqc.utils.utilityfunctions",
+                 "aqc_research", "aqc_research.mps_operations"):
         mods[name] = types.ModuleType(name)
+    em = mods["adaptaqc.utils.entanglement_measures"]
+    co = mods["adaptaqc.utils.circuit_operations"]
+    uf = mods["adaptaqc.utils.utilityfunctions"]
+    mpsops = mods["aqc_research.mps_operations"]
+    ac = mods["adaptaqc.compilers.adapt.adapt_compiler"]
+
+    def is_statevector_backend(backend):  # utilityfunctions.py:122-130
+        return isinstance(backend, AerSVBackend)
+
+    def run_circuit_without_transpilation(circuit, backend=None, backend_options=None, execute_kwargs=None,
+                                          return_statevector=False):  # circuit_operations_running.py:44-69
+        if execute_kwargs is None:
+            execute_kwargs = {}
+        backend_options = {}  # the device backends are not qiskit-aer AerBackends (:55-56)
+        job = backend.simulator.run(circuit, **backend_options, **execute_kwargs)
+        result = job.result()
+        if uf.is_statevector_backend(backend):
+            if return_statevector:
+                return result.get_statevector()
+            raise NotImplementedError("counts_data_from_statevector is not exercised here")
+        return result.get_counts()
+
+    def partial_trace(statevector, a, b):  # entanglement_measures.py:325-340 on the host (qi.partial_trace)
+        from oracle.entanglement import partial_trace_sv
+
+        return partial_trace_sv(np.asarray(statevector), a, b)
+
+    def calculate_entanglement_measure(method, circuit, qubit_1, qubit_2, backend, backend_options=None,
+                                       execute_kwargs=None, mps=None):  # entanglement_measures.py:39-98
+        from oracle import entanglement as oe
+
+        if method == "EM_OBSERVABLE_CONCURRENCE_LOWER_BOUND":
+            raise RuntimeError("reference shot path")
+        if uf.is_statevector_backend(backend):
+            statevector = co.run_circuit_without_transpilation(circuit, backend, return_statevector=True)
+            rho = em.partial_trace(statevector, qubit_1, qubit_2)
+        elif isinstance(backend, AerMPSBackend):
+            rho = mpsops.partial_trace(mps, [qubit_1, qubit_2], already_preprocessed=True)
+        else:
+            raise RuntimeError("reference tomography path")
+        return {"EM_TOMOGRAPHY_EOF": oe.eof, "EM_TOMOGRAPHY_CONCURRENCE": oe.concurrence,
+                "EM_TOMOGRAPHY_NEGATIVITY": oe.negativity,
+                "EM_TOMOGRAPHY_LOG_NEGATIVITY": oe.log_negativity}[method](np.asarray(rho))
+
+    class AdaptCompiler:
+        """The attributes and the ISL method of the reference compiler (adapt_compiler.py:137,
+        approximate_compiler.py:113, adapt_compiler.py:955-976)."""
+
+        def __init__(self, full_circuit, backend, coupling_map, entanglement_measure="EM_TOMOGRAPHY_CONCURRENCE"):
+            self.full_circuit = full_circuit
+            self.backend = backend
+            self.coupling_map = list(coupling_map)
+            self.entanglement_measure_method = entanglement_measure
+            self.backend_options = {}
+            self.execute_kwargs = {}
+            self.soften_global_cost = False
+            self.global_cost_history = []
+            self.is_aer_mps_backend = isinstance(self.backend, AerMPSBackend)
+
+        def _get_all_qubit_pair_entanglement_measures(self):
+            entanglement_measures = []
+            if self.is_aer_mps_backend:
+                self.circ_mps = self.backend.evaluate_circuit(self)
+            else:
+                self.circ_mps = None
+            for control, target in self.coupling_map:
+                entanglement_measures.append(ac.calculate_entanglement_measure(
+                    self.entanglement_measure_method, self.full_circuit, control, target, self.backend,
+                    self.backend_options, self.execute_kwargs, self.circ_mps))
+            return entanglement_measures
+
+    uf.is_statevector_backend = is_statevector_backend
+    co.run_circuit_without_transpilation = run_circuit_without_transpilation
+    em.partial_trace = partial_trace
+    em.calculate_entanglement_measure = calculate_entanglement_measure
+    ac.calculate_entanglement_measure = calculate_entanglement_measure  # imported by name (adapt_compiler.py:35)
+    ac.AdaptCompiler = AdaptCompiler
+    mpsops.partial_trace = _aer
     mods["adaptaqc.backends.aqc_backend"].AQCBackend = AQCBackend
     mods["adaptaqc.backends.aer_mps_backend"].AerMPSBackend = AerMPSBackend
     mods["adaptaqc.backends.aer_sv_backend"].AerSVBackend = AerSVBackend

@@ -26,9 +26,21 @@ def test_install_registers_and_patches():
         assert mods["adaptaqc.compilers.approximate_compiler"].mps_from_circuit is mps_from_circuit
         assert mods["aqc_research.mps_operations"].mps_from_circuit is mps_from_circuit
         assert mods["adaptaqc.utils.gradients"].general_grad_of_pairs is general_grad_of_pairs
+        # the ISL sweep's per-pair entry points and the batched compiler method
+        from adaptaqc_amd.mps_operations import partial_trace as mps_pt
+        from adaptaqc_amd.utils.entanglement_measures import partial_trace as sv_pt
+
+        assert mods["aqc_research.mps_operations"].partial_trace is mps_pt
+        assert mods["adaptaqc.utils.entanglement_measures"].partial_trace is sv_pt
+        AC = mods["adaptaqc.compilers.adapt.adapt_compiler"].AdaptCompiler
+        wrapped = AC._get_all_qubit_pair_entanglement_measures
+        assert wrapped.__wrapped__.__qualname__.endswith("AdaptCompiler._get_all_qubit_pair_entanglement_measures")
+        # the SV simulator handle has the run() the reference's run_circuit_without_transpilation calls
+        assert callable(getattr(sv_b.simulator, "run", None))
         # the reference reads these options from backend.simulator (approximate_compiler.py:224-226)
         assert mps_b.simulator.options.matrix_product_state_truncation_threshold == 1e-16
-    # uninstalled: the fake modules are gone again
+    # uninstalled: the fake modules are gone again, the class method restored
+    assert not hasattr(AC._get_all_qubit_pair_entanglement_measures, "__wrapped__")
     import sys
 
     assert "aqc_research.mps_operations" not in sys.modules
@@ -60,3 +72,22 @@ def test_qiskit_shaped_circuit_flattens_like_ir():
         np.testing.assert_allclose(ma, mb)
     text = qasm2_dumps(QuantumCircuit(2).rx(0.5, 0).cx(0, 1))
     assert "rx(0.5) q[0];" in text and "cx q[0],q[1];" in text
+
+
+def test_isl_wrapper_defers_to_reference_for_other_backends():
+    """With a backend that is not this package's, the wrapped ISL method runs the reference's own
+    loop (here the fake's restatement, which ends in the reference's tomography branch)."""
+    import pytest
+
+    from adaptaqc_amd import reference_binding as rb
+
+    with installed_fake_reference() as mods:
+        rb.install(import_missing=False)
+        AC = mods["adaptaqc.compilers.adapt.adapt_compiler"].AdaptCompiler
+
+        class OtherBackend:
+            pass
+
+        comp = AC(None, OtherBackend(), [(0, 1)])
+        with pytest.raises(RuntimeError, match="tomography"):
+            comp._get_all_qubit_pair_entanglement_measures()
