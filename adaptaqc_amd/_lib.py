@@ -32,7 +32,7 @@ EXPORTS = (
     "aqc_mps_set_jacobi_tol", "aqc_mps_set_jacobi_stop", "aqc_mps_set_jacobi_variant", "aqc_mps_set_fused_chain", "aqc_mps_chain_ticks", "aqc_svd_debug",
     "aqc_sv_pair_rdms", "aqc_mps_pair_rdms", "aqc_mps_pair_rdms_batch", "aqc_entanglement_measures",
     "aqc_sv_transition", "aqc_mps_product_fit", "aqc_mps_set_jacobi32_stop", "aqc_mps_set_svd_path", "aqc_svd_gram_ticks", "aqc_bj_ticks",
-    "aqc_sweep_set_chain_mode", "aqc_mps_set_jacobi_noise", "aqc_stream_join", "aqc_stream_wait",
+    "aqc_sweep_set_chain_mode", "aqc_mps_set_jacobi_noise", "aqc_stream_join", "aqc_stream_wait", "aqc_svd_gram_stats",
 )
 
 
@@ -111,6 +111,7 @@ _SIGS = {
     "aqc_sweep_set_chain_mode": ([_I], _I),
     "aqc_stream_join": ([_P], _I),
     "aqc_stream_wait": ([_P], _I),
+    "aqc_svd_gram_stats": ([_P], _I),
     "aqc_mps_set_jacobi_noise": ([_D], _I),
 }
 
@@ -192,3 +193,12 @@ def timing_query(name):
     n = ctypes.c_int64()
     check(load().aqc_timing_query(name.encode(), ctypes.byref(ms), ctypes.byref(n), ctypes.byref(b), ctypes.byref(f)))
     return {"ms": ms.value, "launches": n.value, "bytes": b.value, "flops": f.value}
+
+
+def gram_stats():
+    """Gram-path counters since the last call (aqc_svd_gram_stats): calls, taken, declined by
+    shape, declined at the eigenvalue floor."""
+    out = np.zeros(4)
+    check(load().aqc_svd_gram_stats(ptr(out)))
+    return {"calls": int(out[0]), "taken": int(out[1]), "declined_shape": int(out[2]),
+            "declined_floor": int(out[3])}

@@ -2400,6 +2400,16 @@ int aqc_svd_gram_ticks(double* out) {
   return AQC_OK;
 }
 
+int aqc_svd_gram_stats(double* out) {
+  AQC_REQUIRE(out, "aqc_svd_gram_stats: null argument");
+  unsigned long long t[4];
+  AQC_HIP_CHECK(hipMemcpyFromSymbol(t, HIP_SYMBOL(g_gram_stats), sizeof(t)));
+  for (int i = 0; i < 4; ++i) out[i] = (double)t[i];
+  unsigned long long z[4] = {0, 0, 0, 0};
+  AQC_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_gram_stats), z, sizeof(z)));
+  return AQC_OK;
+}
+
 int aqc_mps_set_svd_path(int gram, int debug_max_chi) {
   AQC_REQUIRE(gram == 0 || gram == 1, "aqc_mps_set_svd_path: gram must be 0 or 1");
   g_svd_gram = gram;

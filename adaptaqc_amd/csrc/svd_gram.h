@@ -37,6 +37,9 @@ constexpr int kGramMaxK = 64;
 constexpr double kGramRelFloor = 1e-9;
 // shader-clock ticks of the phases (thread 0), summed over calls: S1, S2+S3, S4, S5, S6, output
 __device__ unsigned long long g_gram_ticks[8];
+// path counters (thread 0 of each call): [0] calls, [1] taken, [2] declined by shape (K > 64, ...),
+// [3] declined at the eigenvalue floor (lambda_K <= 1e-9 lambda_1 -> the Jacobi runs)
+__device__ unsigned long long g_gram_stats[4];
 
 __device__ __forceinline__ double wave_sum_d(double v) {
 #pragma unroll
@@ -110,8 +113,12 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
   int K = C;
   if (j.max_chi > 0 && j.max_chi < K) K = j.max_chi;
   // (j.work holds the packed reflectors, <= 8128 complex: capacity 64)
-  if (K > kGramMaxK || C < 4 || C > 128 || L > 128 || j.cap < 64) return false;
   const int tid = fresh_tid(), lane = tid & 63, wave = tid >> 6;
+  if (tid == 0) atomicAdd(&g_gram_stats[0], 1ull);
+  if (K > kGramMaxK || C < 4 || C > 128 || L > 128 || j.cap < 64) {
+    if (tid == 0) atomicAdd(&g_gram_stats[2], 1ull);
+    return false;
+  }
   const cplx* th = j.theta;
   unsigned long long t_last = tid == 0 ? __builtin_amdgcn_s_memtime() : 0ull;
   auto tick = [&](int ph) {
@@ -465,7 +472,10 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
   }
   __syncthreads();
   tick(2);
-  if (!(s_lam[0] > 0.0) || !(s_lam[K - 1] > kGramRelFloor * s_lam[0])) return false;  // uniform
+  if (!(s_lam[0] > 0.0) || !(s_lam[K - 1] > kGramRelFloor * s_lam[0])) {  // uniform
+    if (tid == 0) atomicAdd(&g_gram_stats[3], 1ull);
+    return false;
+  }
   // ---- S5: inverse iteration, Gram-Schmidt in clusters, Rayleigh quotients ----
   double* zb = reinterpret_cast<double*>(xbuf);  // zb[row * 64 + i]
   double* Db = zb + 128 * 64;                    // 1 / D_row of vector i at Db[row * 64 + i]
@@ -797,7 +807,10 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
     }
   }
   for (int c = tid; c < C; c += 1024) j.sig[c] = c < K ? sqrt(s_sig2[c]) : 0.0;
-  if (tid == 0) atomicMax(&j.flags[2], 1);
+  if (tid == 0) {
+    atomicMax(&j.flags[2], 1);
+    atomicAdd(&g_gram_stats[1], 1ull);
+  }
   tick(5);
   return true;
 }

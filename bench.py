@@ -47,6 +47,8 @@ REF_OVERLAPS_PER_LAYER = 113  # Rotoselect evaluations per 4-rotation layer (SUR
 FP64_PEAK_TFLOPS = 78.6  # MI355X dense FP64 (vector = matrix), MI355X_MICROARCH.md / SURVEY 8(d)
 HBM_PEAK_GBS = 8000.0
 TRAFFIC_JSON = "r2_traffic.json"
+# executed FP64 work of k_chain per two-site update, from the committed PMC pass (tools/pmc_exec.py)
+EXEC_JSON = "r2_exec_k_chain.json"
 
 
 def vidal_from_tensors(A):
@@ -361,8 +363,10 @@ def main():
     barrier()
     _lib.timing_reset()
     _lib.timing_enable(True)
+    _lib.gram_stats()  # reset the Gram-path counters
     elapsed, (full, best, costs) = timed(step, args.steps)
     _lib.timing_enable(False)
+    gram = _lib.gram_stats()
     if world > 1:
         chk = best.to(torch.int64).clone()
         ref = chk.clone()
@@ -389,15 +393,31 @@ def main():
     launches = max(fd["launches"], 1)
     avg_ms = fd["ms"] / launches
     if dom == "mps_chain":
-        # fused per-state chain (k_chain): per two-site update the nominal SVD flops of the
-        # 128 x 128 theta (84 n^3) + theta (32 chi^3) + split GEMM (32 chi^3), from the launch's
-        # KernelTimer record; one launch serves every state of the step
+        # fused per-state chain (k_chain).  achieved = EXECUTED FP64 flops per launch (the committed
+        # PMC pass's FMA x 128 + (ADD + MUL) x 64 + MFMA MOPS x 512 per two-site update, times this
+        # launch's updates) / the live launch duration.  The SURVEY 8(d) nominal count (84 n^3 for
+        # the SVD of the 128 x 128 theta + 32 chi^3 theta + 32 chi^3 split, from the launch's
+        # KernelTimer record) is kept beside it: the Gram path executes fewer flops than LAPACK's
+        # nominal count, so the nominal rate overstates the pipes' utilisation.
+        nominal = fd["flops"] / launches / (avg_ms * 1e-3) / 1e12
+        upl = fd["flops"] / launches / ((84.0 * 8 + 64.0) * CHI ** 3)
         roof = {"kernel": "k_chain (fused two-site updates: theta, SVD, split)", "bound": "valu-fp64",
-                "achieved": fd["flops"] / launches / (avg_ms * 1e-3) / 1e12, "peak": FP64_PEAK_TFLOPS,
-                "unit": "TFLOP/s", "updates_per_launch": fd["flops"] / launches / ((84.0 * 8 + 64.0) * CHI ** 3),
-                "svd_share_of_flops": 84.0 * 8 / (84.0 * 8 + 64.0),
+                "achieved": nominal, "basis": "nominal", "peak": FP64_PEAK_TFLOPS,
+                "unit": "TFLOP/s", "updates_per_launch": upl,
+                "nominal_achieved": nominal, "nominal_frac": nominal / FP64_PEAK_TFLOPS,
+                "svd_share_of_nominal_flops": 84.0 * 8 / (84.0 * 8 + 64.0),
                 "peak_note": "FP64 VALU and FP64 MFMA share one 78.6 TFLOP/s ceiling on gfx950 "
-                             "(profiles/r2_fp64_pipes.txt)"}
+                             "(profiles/r2_fp64_pipes.txt)",
+                "gram_path": dict(gram, taken_rate=gram["taken"] / max(gram["calls"], 1),
+                                  taken_per_launch=gram["taken"] / launches)}
+        ej = os.path.join(ROOT, "profiles", EXEC_JSON)
+        if os.path.exists(ej):
+            with open(ej) as fh:
+                ex = json.load(fh)
+            executed = ex["executed_flops_per_unit"] * upl / (avg_ms * 1e-3) / 1e12
+            roof.update(achieved=executed, basis="executed (PMC)", executed_flops_per_update=ex["executed_flops_per_unit"],
+                        executed_source=f"profiles/{EXEC_JSON} ({ex['formula']})",
+                        pmc_wait_any_share=ex.get("wait_any_share"))
     elif dom == "mps_svd":
         jobs = fd["bytes"] / (2.0 * 4 * CHI * CHI * 16)
         achieved_flop = jobs / launches * svd_nominal_flops(2 * CHI, 2 * CHI)

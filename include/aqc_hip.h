@@ -131,6 +131,10 @@ int aqc_mps_set_svd_path(int gram, int debug_max_chi);
 /* Diagnostics: shader-clock ticks of the Gram path's phases (Gram GEMM, tridiagonalisation,
    eigenvalues, eigenvectors, back-transformation, output) since the last call (then reset); out[8]. */
 int aqc_svd_gram_ticks(double* out);
+/* Gram-path counters since the last call (then reset): out[0] two-site SVDs that tried the Gram
+   path, out[1] taken, out[2] declined by shape (K > 64, 2 chi != 128), out[3] declined at the
+   eigenvalue floor (lambda_K <= 1e-9 lambda_1; the register Jacobi ran instead).  out[4]. */
+int aqc_svd_gram_stats(double* out);
 /* Block Jacobi pair visits (2 chi > 128), shader-clock ticks summed over workgroups since the
  * last call: out[0] Gram, out[1] inner Jacobi sweep, out[2] A V, out[3] visits.  Resets. */
 int aqc_bj_ticks(double* out);

@@ -47,6 +47,9 @@ class MPS:
         self.l = [np.array(x, dtype=float) for x in lambdas]
         self.order = list(range(n))  # site -> qubit
         self.loc = list(range(n))  # qubit -> site
+        # test hook: when a list, every two-site update appends (site, singular values before
+        # truncation) -- lets tests predict which SVD path the device should take
+        self.svd_log = None
 
     @classmethod
     def from_aer(cls, qiskit_mps):
@@ -59,6 +62,7 @@ class MPS:
         m = MPS(self.n, [x.copy() for x in self.g], [x.copy() for x in self.l])
         m.order = list(self.order)
         m.loc = list(self.loc)
+        m.svd_log = self.svd_log
         return m
 
     def to_aer(self):
@@ -69,18 +73,31 @@ class MPS:
         p = self.loc[q]
         self.g[p] = np.einsum("ab,bij->aij", u, self.g[p])
 
-    def _two_site(self, p, op4, thr, max_chi):
-        """op4[s1', s2', s1, s2] acts on sites (p, p+1)."""
+    def theta_matrix(self, p, op4=None):
+        """theta' = op4 . (lam_l G_p lam_p G_{p+1} lam_r) as a (2 chi_l) x (2 chi_r) matrix, rows
+        (s1, l), columns (s2, r) -- the matrix a two-site update decomposes."""
         n = self.n
         ll = self.l[p - 1] if p > 0 else np.ones(1)
         lr = self.l[p + 1] if p + 1 < n - 1 else np.ones(1)
         a = self.g[p] * ll[None, :, None]
         b = self.g[p + 1] * lr[None, None, :]
         theta = np.einsum("aim,m,bmj->aibj", a, self.l[p], b)  # (s1, l, s2, r)
-        theta = np.einsum("cdab,aibj->cidj", op4, theta)
+        if op4 is not None:
+            theta = np.einsum("cdab,aibj->cidj", op4, theta)
         s1, chl, s2, chr_ = theta.shape
-        mat = theta.reshape(s1 * chl, s2 * chr_)
+        return theta.reshape(s1 * chl, s2 * chr_)
+
+    def _two_site(self, p, op4, thr, max_chi):
+        """op4[s1', s2', s1, s2] acts on sites (p, p+1)."""
+        n = self.n
+        ll = self.l[p - 1] if p > 0 else np.ones(1)
+        lr = self.l[p + 1] if p + 1 < n - 1 else np.ones(1)
+        mat = self.theta_matrix(p, op4)
+        s1, s2 = 2, 2
+        chl, chr_ = mat.shape[0] // 2, mat.shape[1] // 2
         u, s, vh = np.linalg.svd(mat, full_matrices=False)
+        if self.svd_log is not None:
+            self.svd_log.append((p, s.copy()))
         k = truncation_rank(s, thr, max_chi)
         s = s[:k]
         s = s / np.sqrt(np.sum(s * s))

@@ -18,3 +18,4 @@ pass write WRITE_SIZE
 python3 tools/pmc_summary.py gpurun_out/pmc_sq1 gpurun_out/pmc_sq2 gpurun_out/pmc_mfma gpurun_out/pmc_fetch gpurun_out/pmc_write > gpurun_out/pmc_summary.txt
 python3 tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write ${PMC_KERNEL:-k_chain} > gpurun_out/traffic.json
 rm -rf gpurun_out/pmc_sq1 gpurun_out/pmc_sq2 gpurun_out/pmc_mfma gpurun_out/pmc_fetch gpurun_out/pmc_write
+python3 tools/pmc_exec.py gpurun_out/pmc_summary.txt ${PMC_KERNEL:-k_chain} --units-per-dispatch ${PMC_UNITS:-15872} > gpurun_out/exec_k_chain.json
