@@ -6,12 +6,9 @@
 // one-sided Jacobi is spread over many CUs by column blocks (Hestenes block-Jacobi):
 //   * W (L rows x C columns, column-major, ld = L) is cut into nb blocks of kB = 16 columns;
 //   * one sweep = one "intra" launch (every block orthogonalises its own 16 columns, one
-//     workgroup per block, round-robin in LDS) + nb - 1 "cross" launches (round-robin tournament
-//     over the blocks: nb / 2 workgroups, each rotating every column of block I against every
-//     column of block J);
-//   * a cross visit keeps block I's 16 columns in VGPRs (one wave per column, lane l holds rows
-//     l + 64 i) and block J's 16 columns in LDS (128 KB at L = 512); round r pairs wave g with LDS
-//     slot (g + r) mod 16, so each round is a perfect matching and only the J half crosses LDS;
+//     workgroup per block, round-robin in LDS) + nb - 1 block-pair launches (round-robin
+//     tournament over the blocks: nb / 2 workgroups, each orthogonalising block I against block J
+//     through their 32 x 32 Gram matrix on the matrix cores, k_bj_pair below);
 //   * launch boundaries are the only inter-workgroup synchronisation (no grid barrier, no
 //     cross-XCD coherence assumptions).
 // Rotation rule, thresholds and stop test are those of k_jacobi_reg (mps.hip): relative
@@ -20,7 +17,6 @@
 // threshold -- or with only rotations moving <= j.jtiny^2 of the norms (t|g|) -- is the last.  Output: W's columns = U sigma,
 // sig = their norms (the k_jacobi contract consumed by k_rank / k_split_*, qr = 0).
 #include <cstdlib>
-#include <cstring>
 
 #include "mps_internal.h"
 
@@ -29,9 +25,6 @@ namespace {
 
 constexpr int kB = 16;        // columns per block
 constexpr int kMaxSweepsBJ = 40;
-// Cross visits run the 16-round shift this many times (2 passes: 17 -> 16 sweeps but 21% slower
-// per gate at config 5: the visits are compute-, not W-traffic-bound).
-constexpr int kCrossPasses = 1;
 
 struct BJState {
   double fro;   // ||W||_F^2
@@ -130,7 +123,7 @@ __global__ __launch_bounds__(1024) void k_bj_init(const TwoSiteJob* __restrict__
 // d' = c d, n_a' = n_a - t|g|, n_b' = n_b + t|g|, exact recompute on a 1e6 drop).  MAXR rows per
 // lane, 64 lanes.  Returns whether the pair was rotated; rot / big collect the stop-test flags.
 // With bcol != nullptr the new b goes straight to that LDS column (row lane + 64 i) instead of
-// back into mr / mi, which keeps the cross kernel (16 waves, 128 VGPRs) free of spills.
+// back into mr / mi.
 template <int MAXR>
 __device__ __forceinline__ bool rotate_pair(double (&sr)[MAXR], double (&si)[MAXR], double (&mr)[MAXR],
                                             double (&mi)[MAXR], double& na, double& da, double& ida, double& nb,
@@ -280,85 +273,7 @@ __global__ __launch_bounds__(512) void k_bj_intra(const TwoSiteJob* __restrict__
   if (lane == 0 && big) atomicOr(&s.big, 1);
 }
 
-// Cross visits of tournament round `round` over nb blocks: workgroup p rotates every column of
-// block I = rr(p) (VGPRs, one wave per column) against every column of block J = rr(nb-1-p) (LDS).
-// grid (nb / 2, nj), 16 waves.
-template <int MAXR>
-__global__ __launch_bounds__(1024) void k_bj_cross(const TwoSiteJob* __restrict__ jobs, BJState* __restrict__ st,
-                                                   int round, int nb) {
-  BJState& s = st[blockIdx.y];
-  if (s.done) return;
-  const TwoSiteJob& j = jobs[blockIdx.y];
-  int L, C;
-  bool tr;
-  job_shape(j, L, C, tr);
-  const int I = rr(blockIdx.x, round, nb), J = rr(nb - 1 - blockIdx.x, round, nb);
-  const int cI = I * kB, cJ = J * kB;
-  if (cI >= C || cJ >= C) return;
-  const int nI = min(kB, C - cI), nJ = min(kB, C - cJ);
-  extern __shared__ double2 cols[];  // kB x (64 MAXR): block J
-  constexpr int ldl = 64 * MAXR;
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  cplx* WI = j.work + (size_t)cI * L;
-  cplx* WJ = j.work + (size_t)cJ * L;
-  double sr[MAXR], si[MAXR], mr[MAXR], mi[MAXR];
-#pragma unroll
-  for (int i = 0; i < MAXR; ++i) {
-    const int row = lane + 64 * i;
-    const bool ok = row < L;
-    const double2 a = (ok && w < nI) ? WI[(size_t)w * L + row] : make_double2(0, 0);
-    const double2 b = (ok && w < nJ) ? WJ[(size_t)w * L + row] : make_double2(0, 0);
-    sr[i] = a.x, si[i] = a.y;
-    cols[w * ldl + row] = b;
-  }
-  __shared__ double cn[kB], cd[kB], cid[kB];  // tracked norms and scales of block J's columns
-  {
-    double x = 0;
-#pragma unroll
-    for (int i = 0; i < MAXR; ++i) {
-      const double2 v = cols[w * ldl + lane + 64 * i];
-      x = fma(v.x, v.x, fma(v.y, v.y, x));
-    }
-    x = wave_sum(x);
-    if (lane == 0) cn[w] = x, cd[w] = 1.0, cid[w] = 1.0;
-  }
-  double na = col_norm2<MAXR>(sr, si), da = 1.0, ida = 1.0;
-  __syncthreads();
-  const double tol2 = tol_sq(j, L), floor2 = s.fro * 1e-24;
-  int rot = 0, big = 0;
-  for (int r = 0; r < kCrossPasses * kB; ++r) {
-    const int slot = (w + r) & (kB - 1);
-    double2* col = cols + slot * ldl;
-#pragma unroll
-    for (int i = 0; i < MAXR; ++i) {
-      const double2 v = col[lane + 64 * i];
-      mr[i] = v.x, mi[i] = v.y;
-    }
-    double nb = cn[slot], db = cd[slot], idb = cid[slot];
-    if (rotate_pair<MAXR>(sr, si, mr, mi, na, da, ida, nb, db, idb, tol2, jacobi_noise2(j, s.fro), floor2,
-                          j.jtiny * j.jtiny, rot, big, col)) {
-      __builtin_amdgcn_wave_barrier();
-      if (lane == 0) cn[slot] = nb, cd[slot] = db, cid[slot] = idb;
-    }
-    __syncthreads();
-  }
-#pragma unroll
-  for (int i = 0; i < MAXR; ++i) {
-    const int row = lane + 64 * i;
-    if (row < L) {
-      if (w < nI) WI[(size_t)w * L + row] = make_double2(sr[i] * da, si[i] * da);
-      if (w < nJ) {
-        const double2 v = cols[w * ldl + row];
-        WJ[(size_t)w * L + row] = make_double2(v.x * cd[w], v.y * cd[w]);
-      }
-    }
-  }
-  if (lane == 0 && rot) atomicOr(&s.rot, 1);
-  if (lane == 0 && big) atomicOr(&s.big, 1);
-}
-
-// Block-pair visit of tournament round `round` (the default path; k_bj_intra / k_bj_cross above
-// remain for A/B, AQC_BJ=rot): workgroup p orthogonalises the 32 columns of blocks I = rr(p) and
+// Block-pair visit of tournament round `round` (after each sweep's intra launch): workgroup p orthogonalises the 32 columns of blocks I = rr(p) and
 // J = rr(nb-1-p) together through their Gram matrix -- Hestenes block Jacobi with one inner sweep:
 //   1. G = A^H A (A = [W_I W_J], L x 32) on the matrix cores: wave w takes a quarter of the rows,
 //      three 16 x 16 tiles (G is Hermitian), partial sums through the LDS;
@@ -704,15 +619,6 @@ BJBuffers& bj_buffers() {
   return b;
 }
 
-// Block-pair visits on the matrix cores (default) or the per-rotation kernels (AQC_BJ=rot)
-bool bj_pair_mode() {
-  static const bool on = [] {
-    const char* e = std::getenv("AQC_BJ");
-    return !(e && std::strcmp(e, "rot") == 0);
-  }();
-  return on;
-}
-
 template <int MAXR>
 int run_block_jacobi(const TwoSiteJob* jobs, int nj, int cap_max, hipStream_t stream) {
   BJBuffers& b = bj_buffers();
@@ -736,20 +642,11 @@ int run_block_jacobi(const TwoSiteJob* jobs, int nj, int cap_max, hipStream_t st
   hipLaunchKernelGGL(k_bj_init, dim3(nj), dim3(1024), 0, stream, jobs, b.st);
   AQC_CHECK_LAUNCH();
   for (int sweep = 0; sweep < kMaxSweepsBJ; ++sweep) {
-    if (bj_pair_mode()) {
-      hipLaunchKernelGGL((k_bj_intra<MAXR>), dim3(nb, nj), dim3(512), lds, stream, jobs, b.st);
+    hipLaunchKernelGGL((k_bj_intra<MAXR>), dim3(nb, nj), dim3(512), lds, stream, jobs, b.st);
+    AQC_CHECK_LAUNCH();
+    for (int r = 0; r < nb - 1; ++r) {
+      hipLaunchKernelGGL((k_bj_pair<MAXR>), dim3(nb / 2, nj), dim3(256), kPairLdsBytes, stream, jobs, b.st, r, nb);
       AQC_CHECK_LAUNCH();
-      for (int r = 0; r < nb - 1; ++r) {
-        hipLaunchKernelGGL((k_bj_pair<MAXR>), dim3(nb / 2, nj), dim3(256), kPairLdsBytes, stream, jobs, b.st, r, nb);
-        AQC_CHECK_LAUNCH();
-      }
-    } else {
-      hipLaunchKernelGGL((k_bj_intra<MAXR>), dim3(nb, nj), dim3(512), lds, stream, jobs, b.st);
-      AQC_CHECK_LAUNCH();
-      for (int r = 0; r < nb - 1; ++r) {
-        hipLaunchKernelGGL((k_bj_cross<MAXR>), dim3(nb / 2, nj), dim3(1024), lds, stream, jobs, b.st, r, nb);
-        AQC_CHECK_LAUNCH();
-      }
     }
     hipLaunchKernelGGL(k_bj_sweep_end, dim3(nj), dim3(64), 0, stream, b.st, b.ndone);
     AQC_CHECK_LAUNCH();
@@ -771,9 +668,7 @@ int block_jacobi(const TwoSiteJob* jobs, int nj, int cap_max, hipStream_t st) {
   if (!attr) {
     // 128 KB of dynamic LDS (block J's 16 columns of 512 rows)
     AQC_HIP_CHECK(hipFuncSetAttribute((const void*)k_bj_intra<8>, hipFuncAttributeMaxDynamicSharedMemorySize, 131072));
-    AQC_HIP_CHECK(hipFuncSetAttribute((const void*)k_bj_cross<8>, hipFuncAttributeMaxDynamicSharedMemorySize, 131072));
     AQC_HIP_CHECK(hipFuncSetAttribute((const void*)k_bj_intra<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 65536));
-    AQC_HIP_CHECK(hipFuncSetAttribute((const void*)k_bj_cross<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 65536));
     AQC_HIP_CHECK(hipFuncSetAttribute((const void*)k_bj_pair<8>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                       (int)kPairLdsBytes));
     AQC_HIP_CHECK(hipFuncSetAttribute((const void*)k_bj_pair<4>, hipFuncAttributeMaxDynamicSharedMemorySize,

@@ -62,7 +62,6 @@ double g_jacobi_tiny_t = kDefaultTinyT;
 // (aqc_mps_set_jacobi_noise; jacobi_reg_body)
 constexpr double kDefaultJacobiNoise = 0.0;
 double g_jacobi_noise = kDefaultJacobiNoise;
-int g_jacobi_variant = 2;
 // Fused per-state chain (k_chain) for batches of >= kChainMinStates states at 2 chi = 128.
 bool g_fused_chain = true;
 constexpr int kChainMinStates = 32;
@@ -158,226 +157,6 @@ __global__ __launch_bounds__(kT) void k_theta(const TwoSiteJob* __restrict__ job
       const int s1 = o >> 1, s2 = o & 1;
       j.theta[(size_t)(s2 * chr + r) * M + s1 * chl + l] = v;
     }
-  }
-}
-
-// ---- one-sided Jacobi ------------------------------------------------------------------
-// Columns of the working matrix W (L rows, C columns, column-major, ld = L) are orthogonalised
-// by complex plane rotations.  Columns are processed in LDS panels: blocks of b columns,
-// one cyclic sweep = every block's internal pairs (round robin) + every cross pair of every
-// block pair; with C <= panel capacity the whole matrix stays in LDS across sweeps.
-// LPP lanes cooperate on one column pair; each lane holds its MAXR rows of both columns in
-// registers for the round (rows interleaved by LPP -> conflict-free 16-B LDS accesses), so a
-// round is one LDS read + one LDS write per element, with every load of the round in flight.
-
-__device__ __forceinline__ int rr_elem(int pos, int r, int c) {
-  // round-robin tournament on c (even) players: position 0 fixed, others rotate.
-  if (pos == 0) return 0;
-  return ((pos - 1 + r) % (c - 1)) + 1;
-}
-
-// Rotate the pairs of one round.  pair_of(p) -> (ja, jb) column slots in the panel (-1 = skip).
-template <int LPP, int MAXR, int JT, typename PairFn>
-__device__ __forceinline__ void jacobi_round(cplx* panel, int ld, int L, int npairs, double tol, double floor2,
-                                             double nfl, PairFn pair_of, int* rot_count) {
-  const int tid = fresh_tid();
-  const int grp = tid / LPP, lane = tid % LPP;
-  constexpr int kGroups = JT / LPP;
-  for (int pbase = 0; pbase < npairs; pbase += kGroups) {
-    const int p = pbase + grp;
-    int ja = -1, jb = -1;
-    if (p < npairs) pair_of(p, ja, jb);
-    const bool active = (ja >= 0 && jb >= 0);
-    cplx ra[MAXR], rb[MAXR];
-    double al = 0, be = 0;
-    cplx ga = aqc::cmk(0, 0);
-    if (active) {
-      const cplx* ca = panel + ja * ld;
-      const cplx* cb = panel + jb * ld;
-#pragma unroll
-      for (int i = 0; i < MAXR; ++i) {
-        const int r = lane + i * LPP;
-        ra[i] = r < L ? ca[r] : aqc::cmk(0, 0);
-        rb[i] = r < L ? cb[r] : aqc::cmk(0, 0);
-      }
-#pragma unroll
-      for (int i = 0; i < MAXR; ++i) {
-        al += aqc::cnorm2(ra[i]);
-        be += aqc::cnorm2(rb[i]);
-        ga = aqc::cfmac(ra[i], rb[i], ga);
-      }
-    }
-#pragma unroll
-    for (int off = 1; off < LPP; off <<= 1) {
-      al += __shfl_xor(al, off, LPP);
-      be += __shfl_xor(be, off, LPP);
-      ga.x += __shfl_xor(ga.x, off, LPP);
-      ga.y += __shfl_xor(ga.y, off, LPP);
-    }
-    if (active) {
-      const double g = sqrt(aqc::cnorm2(ga));
-      // Columns below floor2 (squared norm) are rounding noise of exactly-zero singular values:
-      // their direction is random, so relative orthogonality can never be reached; they are
-      // far below the CHOP cut (s^2 <= 1e-16) and are left alone.
-      // (and below the dot-product noise floor nfl sqrt(|a|^2 + |b|^2): jacobi_reg_body)
-      const double thr = fmax(tol * sqrt(al * be), nfl * sqrt(al + be));
-      if (g > thr && al > floor2 && be > floor2) {
-        const double zeta = (be - al) / (2.0 * g);
-        const double t = (zeta >= 0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
-        const double c = 1.0 / sqrt(1.0 + t * t);
-        const double s = c * t;
-        const double ig = 1.0 / g;
-        const cplx se = aqc::cmk(ga.x * ig * s, ga.y * ig * s);    // s e
-        const cplx sec = aqc::cmk(ga.x * ig * s, -ga.y * ig * s);  // s conj(e)
-        cplx* ca = panel + ja * ld;
-        cplx* cb = panel + jb * ld;
-#pragma unroll
-        for (int i = 0; i < MAXR; ++i) {
-          const int r = lane + i * LPP;
-          // a' = c a - s conj(e) b ; b' = s e a + c b
-          const cplx a = ra[i], b = rb[i];
-          if (r < L) {
-            ca[r] = aqc::csub(aqc::cscale(a, c), aqc::cmul(sec, b));
-            cb[r] = aqc::cfma(se, a, aqc::cscale(b, c));
-          }
-        }
-        if (lane == 0 && g > 4.0 * thr) atomicAdd(rot_count, 1);  // above noise
-      }
-    }
-  }
-}
-
-template <int LPP, int MAXR, int JT, int PANEL>
-__global__ __launch_bounds__(JT) void k_jacobi(const TwoSiteJob* __restrict__ jobs) {
-  constexpr int kJT = JT;
-  constexpr int kPanelCplx = PANEL;
-  const TwoSiteJob& j = jobs[blockIdx.x];
-  __shared__ cplx panel[kPanelCplx];
-  __shared__ int rot;
-  __shared__ double fred[kJT];
-  const int chl = j.dims[0], chr = j.dims[2];
-  const int M = 2 * chl, N = 2 * chr;
-  const bool tr = M < N;
-  const int L = tr ? N : M;
-  const int C = tr ? M : N;
-  const int tid = fresh_tid();
-  cplx* W = j.work;
-  // W <- theta (or theta^H), column-major with ld = L; squared Frobenius norm on the way
-  double f = 0.0;
-  for (int idx = tid; idx < L * C; idx += kJT) {
-    const int col = idx / L, row = idx % L;
-    const cplx v = tr ? aqc::cconj(j.theta[(size_t)row * M + col]) : j.theta[(size_t)col * M + row];
-    W[idx] = v;
-    f += aqc::cnorm2(v);
-  }
-  fred[tid] = f;
-  __syncthreads();
-  for (int s = kJT / 2; s > 0; s >>= 1) {
-    if (tid < s) fred[tid] += fred[tid + s];
-    __syncthreads();
-  }
-  // absolute noise floor for squared column norms, relative to ||W||_F^2
-  const double floor2 = fred[0] * 1e-24;
-  const double tol = j.jtol * (double)L * 2.220446049250313e-16;
-  const double nfl = sqrt(jacobi_noise2(j, fred[0]));  // dot-product noise floor (jacobi_reg_body)
-  const int ld = (L + 15) & ~15;
-  int sweeps = 0;
-  if (C >= 2) {
-    const int cap_cols = kPanelCplx / ld;
-    if (C <= cap_cols) {
-      // whole matrix resident in LDS
-      for (int idx = tid; idx < L * C; idx += kJT) panel[(idx / L) * ld + idx % L] = W[idx];
-      __syncthreads();
-      const int ce = C + (C & 1);
-      for (sweeps = 0; sweeps < kMaxSweeps; ++sweeps) {
-        if (tid == 0) rot = 0;
-        __syncthreads();
-        for (int r = 0; r < ce - 1; ++r) {
-          jacobi_round<LPP, MAXR, JT>(panel, ld, L, ce / 2, tol, floor2, nfl,
-                                  [&](int p, int& a, int& b) {
-                                    a = rr_elem(p, r, ce);
-                                    b = rr_elem(ce - 1 - p, r, ce);
-                                    if (a >= C || b >= C) a = b = -1;
-                                  },
-                                  &rot);
-          __syncthreads();
-        }
-        if (rot == 0) break;
-        __syncthreads();
-      }
-      for (int idx = tid; idx < L * C; idx += kJT) W[idx] = panel[(idx / L) * ld + idx % L];
-      __syncthreads();
-    } else {
-      const int b = cap_cols / 2;
-      const int nb = (C + b - 1) / b;
-      const int be = b + (b & 1);
-      for (sweeps = 0; sweeps < kMaxSweeps; ++sweeps) {
-        if (tid == 0) rot = 0;
-        __syncthreads();
-        // intra-block visits
-        for (int I = 0; I < nb; ++I) {
-          const int c0 = I * b, cn = min(b, C - c0);
-          for (int idx = tid; idx < L * cn; idx += kJT)
-            panel[(idx / L) * ld + idx % L] = W[(size_t)c0 * L + idx];
-          __syncthreads();
-          for (int r = 0; r < be - 1; ++r) {
-            jacobi_round<LPP, MAXR, JT>(panel, ld, L, be / 2, tol, floor2, nfl,
-                                    [&](int p, int& a, int& bb) {
-                                      a = rr_elem(p, r, be);
-                                      bb = rr_elem(be - 1 - p, r, be);
-                                      if (a >= cn || bb >= cn) a = bb = -1;
-                                    },
-                                    &rot);
-            __syncthreads();
-          }
-          for (int idx = tid; idx < L * cn; idx += kJT)
-            W[(size_t)c0 * L + idx] = panel[(idx / L) * ld + idx % L];
-          __syncthreads();
-        }
-        // cross-block visits
-        for (int I = 0; I < nb; ++I) {
-          for (int J = I + 1; J < nb; ++J) {
-            const int cI = I * b, nI = min(b, C - cI);
-            const int cJ = J * b, nJ = min(b, C - cJ);
-            for (int idx = tid; idx < L * nI; idx += kJT) panel[(idx / L) * ld + idx % L] = W[(size_t)cI * L + idx];
-            for (int idx = tid; idx < L * nJ; idx += kJT)
-              panel[(b + idx / L) * ld + idx % L] = W[(size_t)cJ * L + idx];
-            __syncthreads();
-            for (int r = 0; r < b; ++r) {
-              jacobi_round<LPP, MAXR, JT>(panel, ld, L, b, tol, floor2, nfl,
-                                      [&](int p, int& a, int& bb) {
-                                        const int q = (p + r) % b;
-                                        a = p < nI ? p : -1;
-                                        bb = q < nJ ? b + q : -1;
-                                      },
-                                      &rot);
-              __syncthreads();
-            }
-            for (int idx = tid; idx < L * nI; idx += kJT) W[(size_t)cI * L + idx] = panel[(idx / L) * ld + idx % L];
-            for (int idx = tid; idx < L * nJ; idx += kJT)
-              W[(size_t)cJ * L + idx] = panel[(b + idx / L) * ld + idx % L];
-            __syncthreads();
-          }
-        }
-        if (rot == 0) break;
-        __syncthreads();
-      }
-    }
-  }
-  // column norms: LPP lanes per column, coalesced
-  {
-    const int grp = tid / LPP, lane = tid % LPP;
-    for (int col = grp; col < C; col += kJT / LPP) {
-      double s = 0;
-      for (int row = lane; row < L; row += LPP) s += aqc::cnorm2(W[(size_t)col * L + row]);
-#pragma unroll
-      for (int off = 1; off < LPP; off <<= 1) s += __shfl_xor(s, off, LPP);
-      if (lane == 0) j.sig[col] = sqrt(s);
-    }
-  }
-  if (tid == 0) {
-    if (sweeps >= kMaxSweeps) atomicOr(&j.flags[1], 1);
-    atomicMax(&j.flags[2], sweeps + 1);
   }
 }
 
@@ -882,30 +661,23 @@ __global__ __launch_bounds__(CP / 2 * LPG) void k_jacobi_reg(const TwoSiteJob* _
   jacobi_reg_body<CP, MAXR, LPG, XPAD, XNP>(jobs[blockIdx.x]);
 }
 
-#include "jacobi32.h"
-// sweep stop of the FP32 preconditioning stage (mixed-precision SVD)
-float g_jacobi32_tiny = 1e-3f;
 #include "svd_gram.h"
 // two-site SVDs at 2 chi = 128 try the Gram / tridiagonal path first (aqc_mps_set_svd_path)
 int g_svd_gram = 1;
 int g_debug_max_chi = 64;  // aqc_svd_debug's max_chi (the Gram path keeps K = min(C, max_chi))
 
-// 2 chi = 128 register Jacobi by variant: 5 = 8-lane groups (512 threads), otherwise 16-lane
-// groups (1024 threads).  Dynamic LDS = kG x max(ld, CP + 1) complex.  Measured on the bench's
-// thetas (tools/jacobi_ab.py, tools/svd_phase_timing.py): 8-lane groups cut the round's VALU
-// instructions by 26% but, at two waves per SIMD, run the sweeps at the same speed and the QR
-// phase 20% slower; 4-lane groups (one wave per SIMD, AGPR spills) 1.9x slower; four columns
-// per group with two independent rotations per step (git history, "block-pair register
-// Jacobi") 11% slower.
-void launch_jacobi_reg128(int variant, int nj, hipStream_t st, const TwoSiteJob* jp) {
-  if (variant == 2 && g_svd_gram) {  // Gram path, the register Jacobi as the in-kernel fallback
+// 2 chi = 128: the Gram path with the register Jacobi (16-lane groups, 1024 threads) as its
+// in-kernel fallback, or the register Jacobi alone (aqc_mps_set_svd_path(0, ...)).  Dynamic LDS =
+// kG x max(ld, CP + 1) complex.  Rejected shapes (measured on the bench's thetas, tools/jacobi_ab.py,
+// tools/svd_phase_timing.py; removed from the library in round 3, see tools/lab/README.md):
+// 8-lane groups (same sweep speed at two waves per SIMD, QR phase 20% slower), 4-lane groups
+// (AGPR spills, 1.9x slower), four columns per group (11% slower).
+void launch_jacobi_reg128(int nj, hipStream_t st, const TwoSiteJob* jp) {
+  if (g_svd_gram) {
     hipLaunchKernelGGL(k_svd_gram, dim3(nj), dim3(1024), kChainLdsBytes, st, jp);
     return;
   }
-  if (variant == 5)
-    hipLaunchKernelGGL((k_jacobi_reg<128, 16, 8>), dim3(nj), dim3(512), 64 * 136 * 16, st, jp);
-  else
-    hipLaunchKernelGGL((k_jacobi_reg<128, 8>), dim3(nj), dim3(1024), 64 * 129 * 16, st, jp);
+  hipLaunchKernelGGL((k_jacobi_reg<128, 8>), dim3(nj), dim3(1024), 64 * 129 * 16, st, jp);
 }
 
 // Sort singular values, apply reduce_zeros, write lambda_m / dims[1] / perm / sorted sig.
@@ -1991,7 +1763,7 @@ int run_waves(aqc_mps_t* hs, int ns, std::vector<std::vector<DevOp>>& lists) {
   {
     int cap_max = 0;
     for (int s = 0; s < ns; ++s) cap_max = std::max(cap_max, hs[s]->d.cap);
-    if (g_fused_chain && g_jacobi_variant == 2 && ns >= kChainMinStates && 2 * cap_max > 64 && 2 * cap_max <= 128)
+    if (g_fused_chain && ns >= kChainMinStates && 2 * cap_max > 64 && 2 * cap_max <= 128)
       return run_chains(hs, ns, lists, cap_max);
   }
   hipStream_t st = aqc::mps_stream();
@@ -2016,8 +1788,10 @@ int run_waves(aqc_mps_t* hs, int ns, std::vector<std::vector<DevOp>>& lists) {
   std::vector<std::pair<size_t, size_t>> two_rng(maxlen), one_rng(maxlen);
   int cap_max = 0;
   for (int s = 0; s < ns; ++s) cap_max = std::max(cap_max, hs[s]->d.cap);
-  const bool reg = (g_jacobi_variant == 2 || g_jacobi_variant == 3 || g_jacobi_variant == 5) && 2 * cap_max <= 128;
-  const int use_qr = reg && g_jacobi_variant != 3 ? 1 : 0;
+  // 2 chi <= 128: the register Jacobi with pivoted-QR preconditioning (the Gram path in front of
+  // it at 2 chi = 128); larger: the multi-workgroup block Jacobi
+  const bool reg = 2 * cap_max <= 128;
+  const int use_qr = reg ? 1 : 0;
   for (size_t w = 0; w < maxlen; ++w) {
     size_t t0 = two.size(), o0 = one.size();
     for (int s = 0; s < ns; ++s) {
@@ -2064,9 +1838,6 @@ int run_waves(aqc_mps_t* hs, int ns, std::vector<std::vector<DevOp>>& lists) {
       aqc::KernelTimer::end(st);
       AQC_CHECK_LAUNCH();
       aqc::KernelTimer::begin(st, "mps_svd", nj * 2.0 * (4.0 * c * c * 16), 0.0);
-      // rows per lane from the largest possible column length (2 * cap); variant 1 = half-size
-      // panel and workgroup so two decompositions share a CU
-      const bool half = g_jacobi_variant == 1;
       if (reg) {
         // register-resident kernel; column count padded to a power of two.  Dynamic LDS holds
         // the round exchange (kG x 16*MAXR) or the QR transpose (kG x (CP+1)), whichever is larger
@@ -2075,16 +1846,7 @@ int run_waves(aqc_mps_t* hs, int ns, std::vector<std::vector<DevOp>>& lists) {
         else if (2 * cap_max <= 64)
           hipLaunchKernelGGL((k_jacobi_reg<64, 4>), dim3(nj), dim3(512), 32 * 65 * 16, st, jp);
         else
-          launch_jacobi_reg128(g_jacobi_variant, nj, st, jp);
-      } else if (2 * cap_max <= 64) {
-        if (half) hipLaunchKernelGGL((k_jacobi<16, 4, 256, 4096>), dim3(nj), dim3(256), 0, st, jp);
-        else hipLaunchKernelGGL((k_jacobi<16, 4, 512, 8192>), dim3(nj), dim3(512), 0, st, jp);
-      } else if (2 * cap_max <= 128) {
-        if (half) hipLaunchKernelGGL((k_jacobi<16, 8, 256, 4096>), dim3(nj), dim3(256), 0, st, jp);
-        else hipLaunchKernelGGL((k_jacobi<16, 8, 512, 8192>), dim3(nj), dim3(512), 0, st, jp);
-      } else if (g_jacobi_variant == 4) {  // single-workgroup LDS-panel Jacobi (reference variant)
-        if (2 * cap_max <= 256) hipLaunchKernelGGL((k_jacobi<16, 16, 512, 8192>), dim3(nj), dim3(512), 0, st, jp);
-        else hipLaunchKernelGGL((k_jacobi<32, 16, 512, 8192>), dim3(nj), dim3(512), 0, st, jp);
+          launch_jacobi_reg128(nj, st, jp);
       } else {
         // 2 chi > 128: multi-workgroup block Jacobi (bjacobi.hip), W in HBM / L2
         const int brc = aqc::block_jacobi(jp, nj, cap_max, st);
@@ -2300,12 +2062,9 @@ int aqc_svd_debug(const double* theta, int m, int n, int variant, int stop_after
   AQC_REQUIRE(m >= 1 && n >= 1 && m % 2 == 0 && n % 2 == 0 && m <= 128 && n <= 128,
               "aqc_svd_debug: m, n must be even and <= 128");
   AQC_REQUIRE(stop_after_qr >= 0 && stop_after_qr <= 2, "aqc_svd_debug: stop_after_qr must be 0, 1 or 2");
-  AQC_REQUIRE(variant == 2 || variant == 3 || (variant >= 5 && variant <= 9),
-              "aqc_svd_debug: variant must be 2, 3 or 5-9");
+  AQC_REQUIRE(variant == 2 || variant == 7, "aqc_svd_debug: variant must be 2 (register Jacobi) or 7 (Gram path)");
   AQC_REQUIRE(variant != 7 || (std::max(m, n) > 64 && stop_after_qr == 0),
               "aqc_svd_debug: variant 7 (Gram) needs 64 < max(m, n) <= 128 and no QR stop");
-  AQC_REQUIRE(variant != 6 || (std::max(m, n) > 64 && stop_after_qr == 0),
-              "aqc_svd_debug: variant 6 (FP32) needs 64 < max(m, n) <= 128 and no QR stop");
   hipStream_t st = aqc::mps_stream();
   const int cp = std::max(m, n) <= 32 ? 32 : (std::max(m, n) <= 64 ? 64 : 128);
   const size_t mat = (size_t)128 * 128 * sizeof(cplx);
@@ -2330,7 +2089,7 @@ int aqc_svd_debug(const double* theta, int m, int n, int variant, int stop_after
   j.jtol = g_jacobi_tol_factor;
   j.jtiny = g_jacobi_tiny_t;
   j.jnoise = g_jacobi_noise;
-  j.qr = variant != 3 ? 1 : 0;
+  j.qr = 1;
   j.dbg = stop_after_qr;
   j.cap = 64;                     // the work buffer holds 128 x 128
   j.max_chi = g_debug_max_chi;    // Gram path: K = min(C, max_chi)
@@ -2342,17 +2101,10 @@ int aqc_svd_debug(const double* theta, int m, int n, int variant, int stop_after
   AQC_HIP_CHECK(hipMemsetAsync(wk, 0, mat, st));
   if (cp == 32) hipLaunchKernelGGL((k_jacobi_reg<32, 2>), dim3(1), dim3(256), 16 * 33 * 16, st, dj);
   else if (cp == 64) hipLaunchKernelGGL((k_jacobi_reg<64, 4>), dim3(1), dim3(512), 32 * 65 * 16, st, dj);
-  else if (variant == 6)
-    hipLaunchKernelGGL((k_jacobi32<128, 8, 16>), dim3(1), dim3(1024), 64 * 129 * 16, st, dj, g_jacobi32_tiny);
   else if (variant == 7)
     hipLaunchKernelGGL(k_svd_gram, dim3(1), dim3(1024), kChainLdsBytes, st, dj);
-  else if (variant == 2)  // the register Jacobi itself (not the Gram path in front of it)
+  else  // the register Jacobi itself (not the Gram path in front of it)
     hipLaunchKernelGGL((k_jacobi_reg<128, 8>), dim3(1), dim3(1024), 64 * 129 * 16, st, dj);
-  else if (variant == 8)  // experiment: 16-lane groups with padded exchange slots
-    hipLaunchKernelGGL((k_jacobi_reg<128, 8, 16, 16>), dim3(1), dim3(1024), 64 * 144 * 16, st, dj);
-  else if (variant == 9)  // experiment: 16-lane groups, two partial sums per dot product
-    hipLaunchKernelGGL((k_jacobi_reg<128, 8, 16, 0, 2>), dim3(1), dim3(1024), 64 * 129 * 16, st, dj);
-  else launch_jacobi_reg128(variant, 1, st, dj);
   AQC_CHECK_LAUNCH();
   const int L = std::max(m, n), C = std::min(m, n);
   const int Lw = j.qr ? C : L;
@@ -2417,11 +2169,6 @@ int aqc_mps_set_svd_path(int gram, int debug_max_chi) {
   return AQC_OK;
 }
 
-int aqc_mps_set_jacobi32_stop(double tiny_t) {
-  AQC_REQUIRE(tiny_t > 0.0 && tiny_t < 0.1, "aqc_mps_set_jacobi32_stop: need 0 < tiny_t < 0.1");
-  g_jacobi32_tiny = (float)tiny_t;
-  return AQC_OK;
-}
 
 int aqc_mps_set_jacobi_stop(double tiny_t) {
   AQC_REQUIRE(tiny_t < 1e-3, "aqc_mps_set_jacobi_stop: tiny_t must be < 1e-3 (<= 0 restores the default)");
@@ -2445,11 +2192,6 @@ int aqc_mps_set_fused_chain(int on) {
   return AQC_OK;
 }
 
-int aqc_mps_set_jacobi_variant(int variant) {
-  AQC_REQUIRE(variant >= 0 && variant <= 5, "aqc_mps_set_jacobi_variant: variant must be 0..5");
-  g_jacobi_variant = variant;
-  return AQC_OK;
-}
 
 int aqc_mps_set_truncation(aqc_mps_t h, double threshold, int max_chi) {
   AQC_REQUIRE(h, "aqc_mps_set_truncation: null handle");

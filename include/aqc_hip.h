@@ -138,14 +138,7 @@ int aqc_svd_gram_stats(double* out);
 /* Block Jacobi pair visits (2 chi > 128), shader-clock ticks summed over workgroups since the
  * last call: out[0] Gram, out[1] inner Jacobi sweep, out[2] A V, out[3] visits.  Resets. */
 int aqc_bj_ticks(double* out);
-/* Sweep stop of the FP32 preconditioning stage of the mixed-precision two-site SVD (default 1e-3). */
-int aqc_mps_set_jacobi32_stop(double tiny_t);
-/* Jacobi kernel: 2 = register-resident columns with pivoted-QR preconditioning for
-   2*chi <= 128 (default; larger chi uses 0), 3 = register-resident without QR,
-   5 = as 2 with 8-lane column groups at 2*chi = 128 (512 threads),
-   0 = 512 threads / 128 KiB LDS panel, 1 = 256 threads / 64 KiB panel (2 per CU). */
-int aqc_mps_set_jacobi_variant(int variant);
-/* Batched applies of >= 32 states at 2*chi = 128 (variant 2) run every state's whole op list in
+/* Batched applies of >= 32 states at 2*chi = 128 run every state's whole op list in
    one fused workgroup (theta, Jacobi, truncation, split per update: no grid-wide step between
    updates); on = 0 selects the lock-step launches per update.  Default on. */
 int aqc_mps_set_fused_chain(int on);
@@ -171,11 +164,10 @@ int aqc_sv_transition(aqc_sv_t bra, aqc_sv_t ket, int q, double* out);
    3 = log-negativity.  rdms / out in device memory when on_device. */
 int aqc_entanglement_measures(const double* rdms, int count, int method, double* out, int on_device);
 
-/* Diagnostics: one register-resident Jacobi launch (variant 2 / 5 = with pivoted QR, 3 = without)
-   on theta (m x n column-major complex, m, n even <= 128, as the two-site update builds it);
-   variant 6 = the FP32 register Jacobi (pivoted QR + sweeps in single precision, 64 < max(m, n)),
-   variant 7 = the Gram / tridiagonal path (Jacobi fallback inside the kernel; same output contract).
-   w_out receives min(m,n) columns of length (variant 2 / 5: min(m,n), 3: max(m,n)); sig_out their
+/* Diagnostics: one register-resident Jacobi launch with pivoted-QR preconditioning (variant 2)
+   on theta (m x n column-major complex, m, n even <= 128, as the two-site update builds it), or
+   the Gram / tridiagonal path (variant 7; Jacobi fallback inside the kernel; same output contract).
+   w_out receives min(m,n) columns of length min(m,n); sig_out their
    norms; perm_out (optional) the pivot order when stop_after_qr (then w_out holds X = R^H
    unsorted).  stop_after_qr = 2 also writes the QR phase's shader-clock ticks to sig_out[0..3]
    (downdate + pivot key, pivot barrier, reflector + barrier, update; 128 x 128 only).  For tests

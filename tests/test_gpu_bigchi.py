@@ -16,23 +16,16 @@ from oracle import mps as M
 pytestmark = pytest.mark.gpu
 
 
-def _check(n, chi, ops, seed, variant=None):
-    from adaptaqc_amd import _lib
+def _check(n, chi, ops, seed):
     from adaptaqc_amd.circuit import device_ops
     from adaptaqc_amd.device import DeviceMPS
 
     aer = random_vidal_mps(n, chi, seed)
     ref = M.run_circuit(n, ops, 1e-16, chi, mps=M.MPS.from_aer(aer))
-    if variant is not None:
-        _lib.check(_lib.lib().aqc_mps_set_jacobi_variant(variant))
-    try:
-        d = DeviceMPS(n, chi, 1e-16, chi)
-        d.load_aer(aer)
-        d.apply(device_ops(to_circuit(n, ops)))
-        dims = d.dims()
-    finally:
-        if variant is not None:
-            _lib.check(_lib.lib().aqc_mps_set_jacobi_variant(2))
+    d = DeviceMPS(n, chi, 1e-16, chi)
+    d.load_aer(aer)
+    d.apply(device_ops(to_circuit(n, ops)))
+    dims = d.dims()
     pre_ref = ref.preprocessed()
     np.testing.assert_array_equal(dims, [1] + [x.shape[2] for x in pre_ref])
     pre = d.preprocessed()
@@ -72,14 +65,6 @@ def test_block_jacobi_ragged_bonds():
     n, chi = 16, 100  # bonds 64 | 100 100 100 | 64: 200-row thetas (12.5 blocks), 128 x 200 (transposed)
     ops = _gates(n, rng, [(7, 8), (6, 7), (8, 9), (2, 3), (0, 1)])
     _check(n, chi, ops, seed=9)
-
-
-def test_panel_and_block_jacobi_agree():
-    """The single-workgroup LDS-panel kernel (variant 4) and the block Jacobi give the same state."""
-    rng = np.random.default_rng(4)
-    n, chi = 16, 128
-    ops = _gates(n, rng, [(7, 8), (6, 7)])
-    _check(n, chi, ops, seed=5, variant=4)
 
 
 def test_concurrent_disjoint_updates_match_sequential():

