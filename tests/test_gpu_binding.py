@@ -147,8 +147,8 @@ def test_reference_isl_sweep_mps():
     from oracle import sv as osv
 
     n = 12
-    target = _random_ir(n, 21)
-    tail = _random_ir(n, 22, layers=2)
+    target = _random_ir(n, 21, layers=3)  # shallow enough that pairs keep non-zero concurrence
+    tail = _random_ir(n, 22, layers=1)
     full = QuantumCircuit(n)
     full.set_matrix_product_state(mps_from_circuit(target))
     for ins in tail.data:
