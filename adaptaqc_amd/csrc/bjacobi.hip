@@ -67,15 +67,15 @@ __global__ __launch_bounds__(1024) void k_bj_init(const TwoSiteJob* __restrict__
   bool tr;
   job_shape(j, L, C, tr);
   const int M = 2 * j.dims[0];
-  __shared__ double key[512];
-  __shared__ int idx[512];
+  __shared__ double key[1024];
+  __shared__ int idx[1024];
   __shared__ double red[16];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   auto elem = [&](int row, int col) -> cplx {
     return tr ? cconj(j.theta[(size_t)row * M + col]) : j.theta[(size_t)col * M + row];
   };
   double f = 0.0;
-  for (int c = w; c < 512; c += 16) {  // column norms, one wave per column
+  for (int c = w; c < 1024; c += 16) {  // column norms, one wave per column
     double x = 0.0;
     if (c < C)
       for (int r = lane; r < L; r += 64) {
@@ -88,11 +88,11 @@ __global__ __launch_bounds__(1024) void k_bj_init(const TwoSiteJob* __restrict__
   }
   if (lane == 0) red[w] = f;
   __syncthreads();
-  // bitonic sort of 512 (key, idx), descending key (padding keys -1 sink to the end)
-  for (int k = 2; k <= 512; k <<= 1) {
+  // bitonic sort of 1024 (key, idx), descending key (padding keys -1 sink to the end)
+  for (int k = 2; k <= 1024; k <<= 1) {
     for (int jj = k >> 1; jj > 0; jj >>= 1) {
       const int i = threadIdx.x;
-      if (i < 512) {
+      {
         const int l = i ^ jj;
         if (l > i) {
           const bool desc = (i & k) == 0;
@@ -283,13 +283,13 @@ __global__ __launch_bounds__(512) void k_bj_intra(const TwoSiteJob* __restrict__
 //      thresholds and stop flags those of rotate_pair on the Gram entries;
 //   3. A <- A V on the matrix cores as A'^T = V^T A^T (a lane group reads and writes 16
 //      consecutive rows of one column).
-// Every pair of columns -- the blocks' own pairs included -- is rotated once per visit, so no
-// intra launch is needed.  grid (nb / 2, nj), 256 threads.
+// FULL = false (2 chi <= 512): the blocks' own Gram blocks are taken as diagonal (each sweep's
+// intra launch has just orthogonalised them; norms only) and the visit rotates the 16 x 16 cross
+// pairs in 16 rounds.  FULL = true (2 chi up to 1024, where the intra launch's block would not fit
+// the LDS): the visit forms all of G and rotates every pair of the 32 columns (31 round-robin
+// rounds), so no intra launch is needed.  grid (nb / 2, nj), 256 threads.
 typedef double __attribute__((ext_vector_type(4))) d4_t;
 constexpr int kPairCols = 2 * kB;  // 32
-// true: the visit forms the blocks' own Gram blocks too; false: their off-diagonal entries are
-// taken as zero (each sweep's intra launch has just orthogonalised them), norms only
-constexpr bool kPairFullGram = false;
 struct PairLds {
   cplx G[2][kPairCols][kPairCols + 1];
   cplx V[2][kPairCols][kPairCols + 1];
@@ -302,7 +302,7 @@ constexpr size_t kPairLdsBytes = sizeof(PairLds);  // dynamic LDS (> 64 KB of st
 // A V, visits (aqc_bj_ticks)
 __device__ unsigned long long g_bj_ticks[4];
 
-template <int MAXR>
+template <int MAXR, bool kPairFullGram>
 __global__ __launch_bounds__(256, 2) void k_bj_pair(const TwoSiteJob* __restrict__ jobs, BJState* __restrict__ st,
                                                  int round, int nb) {
   BJState& s = st[blockIdx.y];
@@ -428,11 +428,18 @@ __global__ __launch_bounds__(256, 2) void k_bj_pair(const TwoSiteJob* __restrict
     return v + 1;
   };
   (void)rrf;
-  for (int r = 0; r < kB; ++r) {
+  constexpr int kRounds = kPairFullGram ? kPairCols - 1 : kB;
+  for (int r = 0; r < kRounds; ++r) {
     __syncthreads();  // G[cur] / V[cur] complete
+    // FULL: every pair of the 32 columns, 31 round-robin rounds of 16 disjoint pairs; otherwise
     // cross pairs only (block I column k with block J column (k + r) mod 16): 16 rounds of 16
     // disjoint pairs; the blocks' own pairs are the intra launch's
-    const int pP = P, qP = kB + ((P + r) & (kB - 1)), pQ = Q, qQ = kB + ((Q + r) & (kB - 1));
+    int pP, qP, pQ, qQ;
+    if constexpr (kPairFullGram) {
+      pP = rrf(P, r), qP = rrf(kPairCols - 1 - P, r), pQ = rrf(Q, r), qQ = rrf(kPairCols - 1 - Q, r);
+    } else {
+      pP = P, qP = kB + ((P + r) & (kB - 1)), pQ = Q, qQ = kB + ((Q + r) & (kB - 1));
+    }
     auto rotation = [&](int p, int q, double& c, cplx& us, double& tg, int& flag_rot, int& flag_big) {
       const double a = sm.G[cur][p][p].x, b = sm.G[cur][q][q].x;
       const cplx g = sm.G[cur][p][q];
@@ -638,14 +645,18 @@ int run_block_jacobi(const TwoSiteJob* jobs, int nj, int cap_max, hipStream_t st
   const int L = 2 * cap_max;
   int nb = (L + kB - 1) / kB;
   nb += nb & 1;
-  const size_t lds = (size_t)kB * 64 * MAXR * sizeof(double2);
+  const size_t lds = MAXR > 8 ? 0 : (size_t)kB * 64 * MAXR * sizeof(double2);
   hipLaunchKernelGGL(k_bj_init, dim3(nj), dim3(1024), 0, stream, jobs, b.st);
   AQC_CHECK_LAUNCH();
   for (int sweep = 0; sweep < kMaxSweepsBJ; ++sweep) {
-    hipLaunchKernelGGL((k_bj_intra<MAXR>), dim3(nb, nj), dim3(512), lds, stream, jobs, b.st);
-    AQC_CHECK_LAUNCH();
+    constexpr bool kFull = MAXR > 8;  // 2 chi > 512: the intra block would not fit the LDS
+    if constexpr (!kFull) {
+      hipLaunchKernelGGL((k_bj_intra<MAXR>), dim3(nb, nj), dim3(512), lds, stream, jobs, b.st);
+      AQC_CHECK_LAUNCH();
+    }
     for (int r = 0; r < nb - 1; ++r) {
-      hipLaunchKernelGGL((k_bj_pair<MAXR>), dim3(nb / 2, nj), dim3(256), kPairLdsBytes, stream, jobs, b.st, r, nb);
+      hipLaunchKernelGGL((k_bj_pair<MAXR, kFull>), dim3(nb / 2, nj), dim3(256), kPairLdsBytes, stream, jobs, b.st, r,
+                         nb);
       AQC_CHECK_LAUNCH();
     }
     hipLaunchKernelGGL(k_bj_sweep_end, dim3(nj), dim3(64), 0, stream, b.st, b.ndone);
@@ -669,15 +680,18 @@ int block_jacobi(const TwoSiteJob* jobs, int nj, int cap_max, hipStream_t st) {
     // 128 KB of dynamic LDS (block J's 16 columns of 512 rows)
     AQC_HIP_CHECK(hipFuncSetAttribute((const void*)k_bj_intra<8>, hipFuncAttributeMaxDynamicSharedMemorySize, 131072));
     AQC_HIP_CHECK(hipFuncSetAttribute((const void*)k_bj_intra<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 65536));
-    AQC_HIP_CHECK(hipFuncSetAttribute((const void*)k_bj_pair<8>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    AQC_HIP_CHECK(hipFuncSetAttribute((const void*)k_bj_pair<8, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                       (int)kPairLdsBytes));
-    AQC_HIP_CHECK(hipFuncSetAttribute((const void*)k_bj_pair<4>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    AQC_HIP_CHECK(hipFuncSetAttribute((const void*)k_bj_pair<4, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)kPairLdsBytes));
+    AQC_HIP_CHECK(hipFuncSetAttribute((const void*)k_bj_pair<16, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                       (int)kPairLdsBytes));
     attr = true;
   }
-  AQC_REQUIRE(2 * cap_max <= 512, "block Jacobi supports 2 * chi_cap <= 512");
+  AQC_REQUIRE(2 * cap_max <= 1024, "block Jacobi supports 2 * chi_cap <= 1024");
   if (2 * cap_max <= 256) return run_block_jacobi<4>(jobs, nj, cap_max, st);
-  return run_block_jacobi<8>(jobs, nj, cap_max, st);
+  if (2 * cap_max <= 512) return run_block_jacobi<8>(jobs, nj, cap_max, st);
+  return run_block_jacobi<16>(jobs, nj, cap_max, st);
 }
 
 }  // namespace aqc

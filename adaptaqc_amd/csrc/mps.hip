@@ -78,6 +78,8 @@ struct OneSiteJob {
 };
 
 using aqc::TwoSiteJob;
+using aqc::kMaxCap;
+using aqc::kSigMax;
 
 // ------------------------------------------------------------------------------------------
 __global__ void k_mps_zero(cplx* gam, double* lam, int* dims, int n, int cap) {
@@ -681,10 +683,10 @@ void launch_jacobi_reg128(int nj, hipStream_t st, const TwoSiteJob* jp) {
 }
 
 // Sort singular values, apply reduce_zeros, write lambda_m / dims[1] / perm / sorted sig.
-template <int NT>
+template <int NT, int MAXC = kSigMax>
 __device__ __forceinline__ void rank_body(const TwoSiteJob& j) {
-  __shared__ double sv[512];
-  __shared__ int si[512];
+  __shared__ double sv[MAXC];
+  __shared__ int si[MAXC];
   __shared__ int kk_s;
   __shared__ double norm_s;
   const int chl = j.dims[0], chr = j.dims[2];
@@ -745,7 +747,7 @@ __device__ __forceinline__ void rank_body(const TwoSiteJob& j) {
   for (int i = tid; i < k; i += NT) {
     j.lm[i] = sv[i] / norm_s;
     j.perm[i] = si[i];
-    j.sig[i + 512] = sv[i];  // sorted copy lives past the raw norms
+    j.sig[i + kSigMax] = sv[i];  // sorted copy lives past the raw norms
   }
 }
 
@@ -761,7 +763,7 @@ __device__ __forceinline__ void split_copy_body(const TwoSiteJob& j, int start, 
   const int L = tr ? N : M;
   const int cap = j.cap;
   const size_t half = (size_t)cap * cap;
-  const double* ss = j.sig + 512;
+  const double* ss = j.sig + kSigMax;
   if (!tr) {
     // Gp'[s1][l][kk] = W[perm kk][s1*chl + l] / sig_kk / ll[l]
     for (int e = start; e < 2 * chl * k; e += stride) {
@@ -814,7 +816,7 @@ __device__ __forceinline__ void split_gemm_body(const TwoSiteJob& j, int blk, aq
   const int L = tr ? N : M;
   const int cap = j.cap;
   const size_t half = (size_t)cap * cap;
-  const double* ss = j.sig + 512;
+  const double* ss = j.sig + kSigMax;
   const int rows = tr ? M : k, cols = tr ? k : N;
   const int bcols = (2 * cap + 63) / 64;
   const int r0 = (blk / bcols) * 64, c0 = (blk % bcols) * 64;
@@ -984,7 +986,7 @@ __device__ __forceinline__ void chain_jacobi(const TwoSiteJob& j) {
   }
   chain_jacobi_fallback(j);
 }
-__device__ __forceinline__ void chain_rank(const TwoSiteJob& j) { rank_body<1024>(j); }
+__device__ __forceinline__ void chain_rank(const TwoSiteJob& j) { rank_body<1024, 128>(j); }
 // The split GEMM in the chain: its output (k x N, or M x k) is two 64 x 64 blocks, so the four
 // sub-groups split the contraction length L in halves -- sub-group sg computes block sg >> 1 over
 // half sg & 1 -- and the second halves' accumulators meet the first halves' through the LDS.
@@ -997,7 +999,7 @@ __device__ __forceinline__ void split_gemm_chain(const TwoSiteJob& j, int tid) {
   const int L = tr ? N : M;
   const int cap = j.cap;
   const size_t half = (size_t)cap * cap;
-  const double* ss = j.sig + 512;
+  const double* ss = j.sig + kSigMax;
   const int rows = tr ? M : k, cols = tr ? k : N;
   const int r0 = tr ? 64 * blk : 0, c0 = tr ? 0 : 64 * blk;
   const bool active = r0 < rows && c0 < cols;
@@ -1134,7 +1136,7 @@ __device__ __forceinline__ cplx site_a(const cplx* gam, const double* lam, int c
 // <0...0|psi>: v <- v A_i[0] from the left.  One workgroup per state.
 __global__ __launch_bounds__(kT) void k_overlap_zero(const MeasJob* __restrict__ jobs) {
   const MeasJob& j = jobs[blockIdx.x];
-  __shared__ cplx v[2][256];
+  __shared__ cplx v[2][kMaxCap];
   __shared__ cplx part[4][256];
   const int tid = fresh_tid();
   if (tid == 0) v[0][0] = aqc::cmk(1.0, 0.0);
@@ -1656,8 +1658,8 @@ int ensure_slots(aqc_mps_t h, int nslots) {
     aqc_mps_s::Slot sl;
     AQC_HIP_CHECK(hipMalloc(&sl.theta, 4 * cap * cap * sizeof(cplx)));
     AQC_HIP_CHECK(hipMalloc(&sl.work, 4 * cap * cap * sizeof(cplx)));
-    AQC_HIP_CHECK(hipMalloc(&sl.sig, 1024 * sizeof(double)));
-    AQC_HIP_CHECK(hipMalloc(&sl.perm, 512 * sizeof(int)));
+    AQC_HIP_CHECK(hipMalloc(&sl.sig, 2 * kSigMax * sizeof(double)));
+    AQC_HIP_CHECK(hipMalloc(&sl.perm, kSigMax * sizeof(int)));
     h->slots.push_back(sl);
   }
   return AQC_OK;
@@ -1727,6 +1729,10 @@ int run_chains(aqc_mps_t* hs, int ns, std::vector<std::vector<DevOp>>& lists, in
         h2[i2] = make_two(hs[s], op, 0);
         h2[i2].qr = 1;
         hcode[ic++] = (int)i2++;
+        std::vector<int>& ub = hs[s]->ub;  // the host bond bounds (run_waves)
+        int nb = std::min(2 * std::min(ub[op.p], ub[op.p + 2]), hs[s]->d.cap);
+        if (hs[s]->max_chi > 0) nb = std::min(nb, hs[s]->max_chi);
+        ub[op.p + 1] = std::max(nb, 1);
       } else {
         h1[i1] = make_one(hs[s], op);
         hcode[ic++] = -(int)(++i1);
@@ -1788,19 +1794,26 @@ int run_waves(aqc_mps_t* hs, int ns, std::vector<std::vector<DevOp>>& lists) {
   std::vector<std::pair<size_t, size_t>> two_rng(maxlen), one_rng(maxlen);
   int cap_max = 0;
   for (int s = 0; s < ns; ++s) cap_max = std::max(cap_max, hs[s]->d.cap);
-  // 2 chi <= 128: the register Jacobi with pivoted-QR preconditioning (the Gram path in front of
-  // it at 2 chi = 128); larger: the multi-workgroup block Jacobi
-  const bool reg = 2 * cap_max <= 128;
-  const int use_qr = reg ? 1 : 0;
+  // each wave's largest possible theta side (2 chi), from the host bond bounds advanced through
+  // the lists in wave order: 2 chi <= 128 runs the register Jacobi with pivoted-QR
+  // preconditioning (the Gram path in front of it at 2 chi = 128), larger the multi-workgroup
+  // block Jacobi sized by the bound -- so a large-capacity state with small bonds (an unbounded
+  // MPS early in a circuit) does not pay for its capacity
+  std::vector<int> wave_side(maxlen, 2);
   for (size_t w = 0; w < maxlen; ++w) {
     size_t t0 = two.size(), o0 = one.size();
     for (int s = 0; s < ns; ++s) {
       if (w >= lv[s].size()) continue;
       int slot = 0;
+      std::vector<int>& ub = hs[s]->ub;
       for (const DevOp* op : lv[s][w]) {
         if (op->kind == 2) {
           two.push_back(make_two(hs[s], *op, slot++));
-          two.back().qr = use_qr;
+          const int p = op->p;
+          wave_side[w] = std::max(wave_side[w], 2 * std::max(ub[p], ub[p + 2]));
+          int nb = std::min(2 * std::min(ub[p], ub[p + 2]), hs[s]->d.cap);
+          if (hs[s]->max_chi > 0) nb = std::min(nb, hs[s]->max_chi);
+          ub[p + 1] = std::max(nb, 1);
         } else {
           one.push_back(make_one(hs[s], *op));
         }
@@ -1808,6 +1821,8 @@ int run_waves(aqc_mps_t* hs, int ns, std::vector<std::vector<DevOp>>& lists) {
     }
     two_rng[w] = {t0, two.size() - t0};
     one_rng[w] = {o0, one.size() - o0};
+    const int qr = wave_side[w] <= 128 ? 1 : 0;
+    for (size_t k = t0; k < two.size(); ++k) two[k].qr = qr;
   }
   const size_t tb = two.size() * sizeof(TwoSiteJob), ob = one.size() * sizeof(OneSiteJob);
   StagingLease lease(st);
@@ -1838,18 +1853,20 @@ int run_waves(aqc_mps_t* hs, int ns, std::vector<std::vector<DevOp>>& lists) {
       aqc::KernelTimer::end(st);
       AQC_CHECK_LAUNCH();
       aqc::KernelTimer::begin(st, "mps_svd", nj * 2.0 * (4.0 * c * c * 16), 0.0);
-      if (reg) {
+      const int side = std::min(wave_side[w], 2 * cap_max);
+      if (side <= 128) {
         // register-resident kernel; column count padded to a power of two.  Dynamic LDS holds
         // the round exchange (kG x 16*MAXR) or the QR transpose (kG x (CP+1)), whichever is larger
-        if (2 * cap_max <= 32)
+        if (side <= 32)
           hipLaunchKernelGGL((k_jacobi_reg<32, 2>), dim3(nj), dim3(256), 16 * 33 * 16, st, jp);
-        else if (2 * cap_max <= 64)
+        else if (side <= 64)
           hipLaunchKernelGGL((k_jacobi_reg<64, 4>), dim3(nj), dim3(512), 32 * 65 * 16, st, jp);
         else
           launch_jacobi_reg128(nj, st, jp);
       } else {
-        // 2 chi > 128: multi-workgroup block Jacobi (bjacobi.hip), W in HBM / L2
-        const int brc = aqc::block_jacobi(jp, nj, cap_max, st);
+        // 2 chi > 128: multi-workgroup block Jacobi (bjacobi.hip), W in HBM / L2, sized by the
+        // wave's bound
+        const int brc = aqc::block_jacobi(jp, nj, (side + 1) / 2, st);
         if (brc != AQC_OK) return brc;
       }
       aqc::KernelTimer::end(st);
@@ -1994,7 +2011,7 @@ extern "C" {
 int aqc_mps_create(int n, int chi_cap, double threshold, int max_chi, aqc_mps_t* out) {
   AQC_REQUIRE(out, "aqc_mps_create: null out");
   AQC_REQUIRE(n >= 1 && n <= 4096, "aqc_mps_create: bad n");
-  AQC_REQUIRE(chi_cap >= 1 && chi_cap <= 256, "aqc_mps_create: chi_cap must be in [1, 256]");
+  AQC_REQUIRE(chi_cap >= 1 && chi_cap <= kMaxCap, "aqc_mps_create: chi_cap must be in [1, 512]");
   auto* h = new aqc_mps_s();
   static std::atomic<unsigned long long> next_uid{1};
   h->uid = next_uid++;
@@ -2005,6 +2022,7 @@ int aqc_mps_create(int n, int chi_cap, double threshold, int max_chi, aqc_mps_t*
   h->order.resize(n);
   h->loc.resize(n);
   for (int i = 0; i < n; ++i) h->order[i] = h->loc[i] = i;
+  h->ub.assign(n + 1, 1);
   const size_t cap = chi_cap;
   const size_t g = (size_t)n * 2 * cap * cap;
   hipStream_t st = aqc::mps_stream();
@@ -2013,8 +2031,8 @@ int aqc_mps_create(int n, int chi_cap, double threshold, int max_chi, aqc_mps_t*
   AQC_HIP_CHECK(hipMalloc(&h->d.dims, (size_t)(n + 1) * sizeof(int)));
   AQC_HIP_CHECK(hipMalloc(&h->d.theta, 4 * cap * cap * sizeof(cplx)));
   AQC_HIP_CHECK(hipMalloc(&h->d.work, 4 * cap * cap * sizeof(cplx)));
-  AQC_HIP_CHECK(hipMalloc(&h->d.sig, 1024 * sizeof(double)));
-  AQC_HIP_CHECK(hipMalloc(&h->d.perm, 512 * sizeof(int)));
+  AQC_HIP_CHECK(hipMalloc(&h->d.sig, 2 * kSigMax * sizeof(double)));
+  AQC_HIP_CHECK(hipMalloc(&h->d.perm, kSigMax * sizeof(int)));
   AQC_HIP_CHECK(hipMalloc(&h->d.flags, 4 * sizeof(int)));
   AQC_HIP_CHECK(hipMalloc(&h->d.vec, 2 * (size_t)(n + 1) * cap * sizeof(cplx)));
   AQC_HIP_CHECK(hipMalloc(&h->d.tmp, 2 * cap * cap * sizeof(cplx)));
@@ -2230,6 +2248,7 @@ int aqc_mps_set_vidal(aqc_mps_t h, const int* dims, const double* gammas, const 
   AQC_HIP_CHECK(hipMemcpy(h->d.lam, l.data(), l.size() * sizeof(double), hipMemcpyHostToDevice));
   AQC_HIP_CHECK(hipMemcpy(h->d.dims, dims, (n + 1) * sizeof(int), hipMemcpyHostToDevice));
   for (int i = 0; i < n; ++i) h->order[i] = h->loc[i] = i;
+  h->ub.assign(dims, dims + n + 1);
   h->changed_all();
   return AQC_OK;
 }
@@ -2239,6 +2258,7 @@ int aqc_mps_get_dims(aqc_mps_t h, int* dims) {
   hipStream_t st = aqc::mps_stream();
   AQC_HIP_CHECK(hipMemcpyAsync(dims, h->d.dims, (h->d.n + 1) * sizeof(int), hipMemcpyDeviceToHost, st));
   AQC_HIP_CHECK(hipStreamSynchronize(st));
+  h->ub.assign(dims, dims + h->d.n + 1);  // exact again
   return AQC_OK;
 }
 
@@ -2338,6 +2358,7 @@ int aqc_mps_copy_batch(aqc_mps_t* dst, const aqc_mps_t* src, int ns) {
     j.pad = 0;
     d->order = r->order;
     d->loc = r->loc;
+    d->ub = r->ub;
     d->synced_src = r->uid;
     d->synced_ver = r->version;
     d->dirty_lo = 1 << 30;
@@ -2400,6 +2421,7 @@ int aqc_mps_copy(aqc_mps_t dst, const aqc_mps_t src) {
   AQC_HIP_CHECK(hipMemcpyAsync(dst->d.lam, src->d.lam, (n + 1) * cap * sizeof(double), hipMemcpyDeviceToDevice, st));
   AQC_HIP_CHECK(hipMemcpyAsync(dst->d.dims, src->d.dims, (n + 1) * sizeof(int), hipMemcpyDeviceToDevice, st));
   dst->order = src->order;
+  dst->ub = src->ub;
   dst->loc = src->loc;
   if (dst != src) {
     dst->synced_src = src->uid;

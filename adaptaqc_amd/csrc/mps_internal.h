@@ -14,6 +14,11 @@ namespace aqc {
 //   lam : (n+1) bonds x cap doubles; bond b sits left of site b; lam[0] = lam[n] = {1}.
 //   dims: (n+1) ints on device, dims[0] = dims[n] = 1.
 // The qubit permutation created by Aer's swap routing lives on the host (order / loc).
+// Largest two-site column count 2 chi (bond capacity <= 512): the singular-value buffer holds the
+// raw column norms at [0, kSigMax) and the sorted values at [kSigMax, 2 kSigMax).
+constexpr int kSigMax = 1024;
+constexpr int kMaxCap = kSigMax / 2;
+
 struct MpsDev {
   int n = 0;
   int cap = 0;
@@ -23,8 +28,8 @@ struct MpsDev {
   // two-site workspace
   cplx* theta = nullptr;  // (2cap)^2, column-major M x N
   cplx* work = nullptr;   // (2cap)^2, Jacobi working columns
-  double* sig = nullptr;  // 2cap column norms
-  int* perm = nullptr;    // 2cap sorted -> column index
+  double* sig = nullptr;  // 2 kSigMax: column norms, then the sorted values
+  int* perm = nullptr;    // kSigMax sorted -> column index
   int* flags = nullptr;   // [0] capacity overflow, [1] jacobi non-convergence, [2] max sweeps used
   // measurement workspace
   cplx* env = nullptr;    // 2 * (n+1) * cap * cap  (left and right environments)
@@ -160,6 +165,10 @@ struct aqc_mps_s {
   double thr = 1e-16;
   int max_chi = 0;
   std::vector<int> order;  // site -> qubit
+  // host upper bounds of the bond dimensions (n + 1; exact after a load or a dims read-back, then
+  // advanced per two-site update as min(2 chi_l, 2 chi_r, cap, max_chi)): the lock-step path picks
+  // each wave's SVD kernel by the largest theta the wave can hold, not by the capacity
+  std::vector<int> ub;
   std::vector<int> loc;    // qubit -> site
   // Reload bookkeeping (aqc_mps_copy_batch): `version` changes with every change of the device
   // contents; after a copy from the handle with id `synced_src` at its version `synced_ver`, the

@@ -11,9 +11,10 @@
 //       the rows' p, v, z and p^H v partials, one row per thread of waves 0-1), the column, the
 //       reflector and p = tau G v in double-buffered LDS vectors (zeros at and above the diagonal:
 //       a mask-free rank-2 update), the reflectors packed into the work buffer
-//   S4  the top K eigenvalues of the real symmetric tridiagonal T: one 1024-point Sturm pass and
-//       a binary search bracket each, then 17-section (16 lanes per eigenvalue each evaluate one
-//       Sturm count, one ballot picks the subinterval; 6 rounds)
+//   S4  the top K eigenvalues of the real symmetric tridiagonal T: one 256-point Sturm pass and
+//       a binary search bracket each, then 5-section (4 lanes per eigenvalue each evaluate one
+//       Sturm count -- the minors' three-term recurrence, one dependent FMA per row -- one ballot
+//       picks the subinterval; 12 rounds)
 //   S5  inverse iteration (unpivoted LDL^T of T - lambda I, three solves) per eigenvector, Gram-
 //       Schmidt inside clusters (gaps below 1e-7 ||T||), sigma^2 = z^T T z
 //   S6  back-transformation V = Q Z: blocks of 16 reflectors in compact WY form on the matrix
@@ -34,6 +35,11 @@
 #pragma once
 
 constexpr int kGramMaxK = 64;
+// S3: wave 0 raises its issue priority while it forms a reflector's scalars (the other waves of
+// its SIMD are in the column pass, issue-bound, and would otherwise take 3 of every 4 issue slots)
+#ifndef AQC_S3_PRIO
+#define AQC_S3_PRIO 1
+#endif
 constexpr double kGramRelFloor = 1e-9;
 // shader-clock ticks of the phases (thread 0), summed over calls: S1, S2+S3, S4, S5, S6, output
 __device__ unsigned long long g_gram_ticks[8];
@@ -75,20 +81,47 @@ __device__ __forceinline__ cplx pick16(const cplx (&g)[16], int i) {
   }
 }
 
-// One Sturm-count step q <- (d - x) - e^2 / q (d - x passed in).  The reciprocal is clamped to
-// +-2^600 before its Newton step instead of replacing |q| < pivmin by -pivmin: q = +0 then gives
-// a huge negative next q where LAPACK's guard counted the zero itself -- the same count after the
-// next step (a different count only for an exact zero in the last row, or next to an exact zero
-// off-diagonal).  Two fewer instructions per step than the compare-and-select guard.
-__device__ __forceinline__ double sturm_step(double q, double dmx, double e2) {
-  constexpr double kClamp = 0x1p600;
-  double r = __builtin_amdgcn_rcp(q);
-  r = __builtin_fmin(__builtin_fmax(r, -kClamp), kClamp);
-  r = r * fma(-q, r, 2.0);
-  return fma(-e2, r, dmx);
-}
 // 1 for a negative q (sign bit; q is never -0 here)
 __device__ __forceinline__ int sign_bit(double q) { return (int)((unsigned)__double2hiint(q) >> 31); }
+
+// Sturm count (eigenvalues of T below x) by the three-term recurrence of the leading principal
+// minors, p_{i+1} = (d_i - x) p_i - e_{i-1}^2 p_{i-1} (Wilkinson's bisection), counting sign
+// changes.  Its dependent chain is one FMA per row -- the product e^2 p_{i-1} and d_i - x are off
+// it -- where the ratio form q = (d - x) - e^2 / q carried a reciprocal and its Newton step
+// (6 dependent FP64 operations per row).  de[i] = (d_i, e_{i-1}^2) pre-scaled by 1 / ||T|| (and
+// x with them), so |p| grows at most 3.1x per row; every 4 rows both minors are rescaled by the
+// larger one's binary exponent (a common positive factor leaves the signs alone), which also
+// keeps runs of tiny pivots from underflowing.  The sign of each minor is its high word shifted
+// arithmetically (0 or -1); the xor of consecutive ones is -1 on a change.
+__device__ __forceinline__ int sturm_count_poly(const double2* de, int C, double xn) {
+  double p0 = 1.0, p1 = de[0].x - xn;
+  int s1 = __double2hiint(p1) >> 31;
+  int neg = s1;  // -(sign changes): p_0 = 1 is positive
+  int i = 1;
+  auto step = [&](double2 e) {
+    const double p2 = fma(e.x - xn, p1, -(e.y * p0));
+    const int s2 = __double2hiint(p2) >> 31;
+    neg += s1 ^ s2;
+    s1 = s2;
+    p0 = p1;
+    p1 = p2;
+  };
+  auto rescale = [&]() {
+    const int ex = max(__builtin_amdgcn_frexp_exp(p0), __builtin_amdgcn_frexp_exp(p1));
+    p0 = __builtin_amdgcn_ldexp(p0, -ex);
+    p1 = __builtin_amdgcn_ldexp(p1, -ex);
+  };
+  for (; i + 4 <= C; i += 4) {
+    const double2 e0 = de[i], e1 = de[i + 1], e2 = de[i + 2], e3 = de[i + 3];
+    step(e0);
+    step(e1);
+    step(e2);
+    step(e3);
+    rescale();
+  }
+  for (; i < C; ++i) step(de[i]);
+  return -neg;
+}
 
 __device__ __forceinline__ double rcp_nr(double x) {
   double r = __builtin_amdgcn_rcp(x);
@@ -269,6 +302,7 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
     cplx a2 = aqc::cmk(0, 0), s = aqc::cmk(0, 0);
     if (wact || wave == 0) prev_scalars(k, bp, a2, s);
     if (wave == 0) {
+      if (AQC_S3_PRIO) __builtin_amdgcn_s_setprio(3);
       // column k of G^(k) below the diagonal: x_r = z_r - s v_r (r > k); alpha = x_{k+1}
       double xn2;
       {
@@ -299,6 +333,7 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
         scal[1] = aqc::cmul(tau, scl);
         scal[2] = s;
       }
+      if (AQC_S3_PRIO) __builtin_amdgcn_s_setprio(0);
     }
     if (wact) {
       // the own row's reflector k - 1 entries and w_r (the Hermitian rank-2 update needs only
@@ -392,7 +427,7 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
     atomicAdd(&g_gram_ticks[7], t_b);
   }
   tick(1);
-  // ---- S4: top-K eigenvalues of T by 17-section ----
+  // ---- S4: top-K eigenvalues of T by multisection ----
   if (wave == 0) {  // Gershgorin interval, ||T||, e^2 and the (d, e^2) pairs: two rows per lane
     double lo = 1e300, hi = -1e300, tn = 0.0;
     for (int i = lane; i < C; i += 64) {
@@ -416,59 +451,56 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
       s_hi = hi + 1e-12 * span;
       s_tn = tn;
     }
+    // the Sturm recurrence's rows scaled by 1 / ||T|| (sturm_count_poly)
+    const double itn = 1.0 / fmax(tn, 1e-300);
+    for (int i = lane; i < C; i += 64) {
+      const double2 de = s_de[i];
+      s_de[i] = make_double2(de.x * itn, de.y * itn * itn);
+    }
   }
   __syncthreads();
   {
-    const int eid = tid >> 4, sub = tid & 15;
+    // Multisection with the polynomial Sturm count (one dependent FMA per row): a pass is now
+    // issue-bound at ~7 VALU instructions per row and wave, so one wave per SIMD runs it.  One
+    // pass of kFirst = 256 shifts (waves 0-3) brackets every eigenvalue to span / 257, then
+    // kRounds rounds of (kG + 1)-section with kG = 4 lanes per eigenvalue (64 x 4 = 256 lanes)
+    // narrow it by 5^12 (span x 1.6e-11 at the end; the 1024-point pass + 17^6 of round 2 gave
+    // 4e-11).  Waves 4-15 sit S4 out.  (Ratio form, 16 lanes x 17-section, 7 passes: 0.20 M
+    // ticks; ratio form, 8 lanes x 9-section, 9 passes: 0.15 M.)
+    constexpr int kG = 4, kFirst = 256, kRounds = 12;
+    const int eid = tid / kG, sub = tid % kG;
     const int a = C - 1 - eid;  // ascending index of the eid-th largest eigenvalue
-    // first pass: one Sturm count per thread at 1024 points across the Gershgorin interval, then
-    // each eigenvalue's bracket by a binary search over the counts (1024-section in one pass,
-    // where 17-section would need two and a half); six 17-section rounds follow
     int* cntb = reinterpret_cast<int*>(xbuf);
     const double lo0 = s_lo, span0 = s_hi - s_lo;
-    {
-      const double x = lo0 + span0 * (double)(tid + 1) * (1.0 / 1025.0);
-      double qv = s_de[0].x - x;
-      int cnt = sign_bit(qv);
-#pragma unroll 4
-      for (int i = 1; i < C; ++i) {
-        const double2 de = s_de[i];
-        qv = sturm_step(qv, de.x - x, de.y);
-        cnt += sign_bit(qv);
-      }
-      cntb[tid] = cnt;
-    }
+    const double itn = 1.0 / fmax(s_tn, 1e-300);
+    constexpr double kInvF = 1.0 / (kFirst + 1), kInvG = 1.0 / (kG + 1);
+    if (tid < kFirst) cntb[tid] = sturm_count_poly(s_de, C, (lo0 + span0 * (double)(tid + 1) * kInvF) * itn);
     __syncthreads();
-    double lo, hi;
-    {
-      int l = 0, h = 1024;  // first t with cnt[t] >= a + 1 (1024: none)
-      while (l < h) {
-        const int m = (l + h) >> 1;
-        if (cntb[m] >= a + 1) h = m;
-        else l = m + 1;
+    if (tid < 64 * kG) {  // uniform per wave
+      double lo, hi;
+      {
+        int l = 0, h = kFirst;  // first t with cnt[t] >= a + 1 (kFirst: none)
+        while (l < h) {
+          const int m = (l + h) >> 1;
+          if (cntb[m] >= a + 1) h = m;
+          else l = m + 1;
+        }
+        lo = l > 0 ? lo0 + span0 * (double)l * kInvF : s_lo;
+        hi = l < kFirst ? lo0 + span0 * (double)(l + 1) * kInvF : s_hi;
       }
-      lo = l > 0 ? lo0 + span0 * (double)l * (1.0 / 1025.0) : s_lo;
-      hi = l < 1024 ? lo0 + span0 * (double)(l + 1) * (1.0 / 1025.0) : s_hi;
-    }
-    for (int round = 0; round < 6; ++round) {
-      const double x = lo + (hi - lo) * (double)(sub + 1) * (1.0 / 17.0);
-      double qv = s_de[0].x - x;
-      int cnt = sign_bit(qv);
-#pragma unroll 4
-      for (int i = 1; i < C; ++i) {
-        const double2 de = s_de[i];  // (d_i, e_{i-1}^2)
-        qv = sturm_step(qv, de.x - x, de.y);
-        cnt += sign_bit(qv);
+      for (int round = 0; round < kRounds; ++round) {
+        const double x = lo + (hi - lo) * (double)(sub + 1) * kInvG;
+        const int cnt = sturm_count_poly(s_de, C, x * itn);
+        const unsigned long long bal = __ballot(cnt >= a + 1);
+        const unsigned int gm = (unsigned int)(bal >> (lane & ~(kG - 1))) & ((1u << kG) - 1u);
+        const int f = gm ? __builtin_ctz(gm) : kG;
+        const double nhi = f < kG ? lo + (hi - lo) * (double)(f + 1) * kInvG : hi;
+        const double nlo = f > 0 ? lo + (hi - lo) * (double)f * kInvG : lo;
+        lo = nlo;
+        hi = nhi;
       }
-      const unsigned long long bal = __ballot(cnt >= a + 1);
-      const unsigned int gm = (unsigned int)(bal >> (lane & ~15)) & 0xFFFFu;
-      const int f = gm ? __builtin_ctz(gm) : 16;
-      const double nhi = f < 16 ? lo + (hi - lo) * (double)(f + 1) * (1.0 / 17.0) : hi;
-      const double nlo = f > 0 ? lo + (hi - lo) * (double)f * (1.0 / 17.0) : lo;
-      lo = nlo;
-      hi = nhi;
+      if (eid < K && sub == 0) s_lam[eid] = 0.5 * (lo + hi);
     }
-    if (eid < K && sub == 0) s_lam[eid] = 0.5 * (lo + hi);
   }
   __syncthreads();
   tick(2);
@@ -521,9 +553,11 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
     for (int it = 0; it < 3; ++it) {
       // forward solve L y = sc z in place (L_{row, row-1} = e_{row-1} / D_{row-1}), then L^T-solve
       // z = D^-1 y - L^T z from the bottom
+      // (one dependent FMA per row in both solves: the row's coefficients -e_{r-1} / D_{r-1} and
+      // z sc, or e_r / D_r and y / D_r, are formed off the chain)
       double yp = 0.0;
       auto fwd_row = [&](int row, double z, double e, double dp) {
-        const double y = fma(z, sc, -e * dp * yp);
+        const double y = fma(-e * dp, yp, z * sc);
         zb[row * 64 + i] = y;
         yp = y;
       };
@@ -544,7 +578,7 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
       }
       double zn = 0.0, n2 = 0.0;
       auto bwd_row = [&](int row, double y, double e, double d) {
-        zn = (y - e * zn) * d;
+        zn = fma(-e * d, zn, y * d);
         zb[row * 64 + i] = zn;
         n2 = fma(zn, zn, n2);
       };

@@ -117,3 +117,41 @@ def test_config5_full_size_vs_oracle():
     pre = d.preprocessed()
     fid = abs(M.mps_dot(pre_ref, pre)) / np.sqrt(abs(M.mps_dot(pre, pre)) * abs(M.mps_dot(pre_ref, pre_ref)))
     assert abs(fid - 1.0) < 1e-6, fid
+
+
+def test_unbounded_chi_above_256_deep_circuit():
+    """The reference's default MPS_SIM has no bond-dimension cap (python_default_backends.py:19,
+    aer_mps_backend.py:27-42).  A 20-qubit brickwork of depth 18 at max_chi = None grows the middle
+    bonds past 256 (oracle: ..., 256, 314, 482, 262, ...); the device replay (capacity 512, two-site
+    SVDs of up to 1024 x 1024 by the full-Gram block-pair Jacobi) matches the oracle's bond
+    dimensions exactly and its state to 1e-6 fidelity, with <0..0|psi> and <Z> beside it."""
+    from adaptaqc_amd.circuit import QuantumCircuit
+    from adaptaqc_amd.mps_operations import device_mps_from_circuit
+
+    n, depth = 20, 18
+    rng = np.random.default_rng(5)
+    ops = []
+    qc = QuantumCircuit(n)
+    for layer in range(depth):
+        for q in range(n):
+            a, b = float(rng.uniform(-np.pi, np.pi)), float(rng.uniform(-np.pi, np.pi))
+            ops += [("ry", (q,), (a,)), ("rz", (q,), (b,))]
+            qc.ry(a, q)
+            qc.rz(b, q)
+        for q in range(layer % 2, n - 1, 2):
+            ops.append(("cx", (q, q + 1), ()))
+            qc.cx(q, q + 1)
+    ref = M.run_circuit(n, ops)
+    pre_ref = ref.preprocessed()
+    want_dims = [1] + [x.shape[2] for x in pre_ref]
+    assert max(want_dims) > 256
+    d = device_mps_from_circuit(qc)
+    assert d.chi_cap == 512
+    np.testing.assert_array_equal(d.dims(), want_dims)
+    pre = d.preprocessed()
+    fid = abs(M.mps_dot(pre_ref, pre))
+    assert abs(fid - 1.0) < 1e-6, fid
+    assert abs(d.overlap_zero() - M.mps_dot(pre_ref, M.zero_mps(n))) < 1e-9
+    qs = [0, 7, 10, 13, 19]
+    zr = np.array([M.mps_expectation_z(pre_ref, q) for q in qs])
+    np.testing.assert_allclose(d.z_all()[qs], zr, atol=1e-6)

@@ -167,8 +167,9 @@ def test_mps_format_helpers():
     pre = _preprocess_mps(z)
     assert all(x.shape == (2, 1, 1) for x in pre)
     assert chi_cap_for(50, 64) == 64 and chi_cap_for(6, None) == 8
+    assert chi_cap_for(50, 512) == 512 and chi_cap_for(20, None) == 512 and chi_cap_for(16, None) == 256
     with pytest.raises(NotImplementedError):
-        chi_cap_for(50, 512)
+        chi_cap_for(50, 1024)
 
 
 def test_backends_pickle_without_device_state():

@@ -1,8 +1,8 @@
-"""FP32 register Jacobi (aqc_svd_debug variant 6) vs the FP64 one (variant 2) on the bench's
-swap-routed two-site thetas: singular values against numpy, sweep counts.  Run under
-``rocprofv3 --kernel-trace --stats`` for the kernel times (k_jacobi32 vs k_jacobi_reg).
+"""The Gram path (aqc_svd_debug variant 7) and the register Jacobi (variant 2) on the bench's
+swap-routed two-site thetas: singular values and kept subspace against numpy, the Gram path's
+phase ticks.  (Until round 2 it also ran the FP32 Jacobi, variant 6, now removed: tools/lab.)
 
-    python3 tools/svd32_probe.py [reps] [tiny32 ...]
+    python3 tools/svd32_probe.py [reps]
 """
 import ctypes
 import os
@@ -31,7 +31,6 @@ def main():
     if os.environ.get("AQC_LIB"):  # experiment builds
         _lib.load(os.environ["AQC_LIB"])
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 5
-    tinies = [float(x) for x in sys.argv[2:]] or [1e-3]
     L = _lib.lib()
     for kind in ("near-product", "random"):
         aer = bench.bench_states(50, 64, 1, kind)[0]
@@ -42,9 +41,7 @@ def main():
         w = np.zeros(2 * m * n)
         sig = np.zeros(max(m, n))
         sw = ctypes.c_int()
-        for v, tiny in [(2, None), (7, None)] + [(6, t) for t in tinies]:
-            if tiny is not None:
-                _lib.check(L.aqc_mps_set_jacobi32_stop(ctypes.c_double(tiny)))
+        for v, tiny in [(2, None), (7, None)]:
             for _ in range(reps):
                 _lib.check(L.aqc_svd_debug(_lib.ptr(th), m, n, v, 0, _lib.ptr(w), _lib.ptr(sig), None,
                                            ctypes.byref(sw)))
