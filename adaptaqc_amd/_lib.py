@@ -33,6 +33,8 @@ EXPORTS = (
     "aqc_sv_pair_rdms", "aqc_mps_pair_rdms", "aqc_mps_pair_rdms_batch", "aqc_entanglement_measures",
     "aqc_sv_transition", "aqc_mps_product_fit", "aqc_mps_set_svd_path", "aqc_svd_gram_ticks", "aqc_bj_ticks",
     "aqc_sweep_set_chain_mode", "aqc_mps_set_jacobi_noise", "aqc_stream_join", "aqc_stream_wait", "aqc_svd_gram_stats",
+    "aqc_comm_unique_id", "aqc_comm_init", "aqc_comm_destroy", "aqc_comm_rank", "aqc_allgather_f64",
+    "aqc_allgather_f64_host", "aqc_allreduce_max_f64",
 )
 
 
@@ -110,6 +112,13 @@ _SIGS = {
     "aqc_stream_join": ([_P], _I),
     "aqc_stream_wait": ([_P], _I),
     "aqc_svd_gram_stats": ([_P], _I),
+    "aqc_comm_unique_id": ([ctypes.c_char_p], _I),
+    "aqc_comm_init": ([ctypes.c_char_p, _I, _I, ctypes.POINTER(_P)], _I),
+    "aqc_comm_destroy": ([_P], _I),
+    "aqc_comm_rank": ([_P, _IP, _IP], _I),
+    "aqc_allgather_f64": ([_P, _P, _P, ctypes.c_size_t], _I),
+    "aqc_allgather_f64_host": ([_P, _P, _P, ctypes.c_size_t], _I),
+    "aqc_allreduce_max_f64": ([_P, _DP], _I),
     "aqc_mps_set_jacobi_noise": ([_D], _I),
 }
 

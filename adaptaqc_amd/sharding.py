@@ -90,6 +90,24 @@ def gather_scores(local_scores, shard: PairShard, group=None, nstates: int = 1):
     return full
 
 
+def gather_scores_host(local_scores, shard: PairShard, allgather):
+    """The same exchange with host arrays and any all-gather callable (``allgather(x)`` returns
+    (world, len(x)) in rank order): libaqchip's RCCL communicator (``comm.RcclComm.allgather``)
+    for callers without torch.distributed, or a gloo/MPI stand-in in tests.  local_scores:
+    [nstates, n_local] numpy.  Returns [nstates, n_pairs], identical on every rank."""
+    local = np.asarray(local_scores, dtype=np.float64)
+    nstates = local.shape[0]
+    m = shard.max_local
+    buf = np.zeros((nstates, m))
+    buf[:, : local.shape[1]] = local
+    gathered = np.asarray(allgather(buf.reshape(-1))).reshape(shard.world, nstates, m)
+    full = np.empty((nstates, len(shard.coupling_map)))
+    for r, idx in enumerate(shard.index_lists):
+        if idx:
+            full[:, idx] = gathered[r, :, : len(idx)]
+    return full
+
+
 def select_pairs(full_scores, priorities):
     """np.argmax(scores * priorities) per state (first index wins ties)."""
     s = np.asarray(full_scores, dtype=np.float64) * np.asarray(priorities, dtype=np.float64)

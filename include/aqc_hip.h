@@ -19,6 +19,7 @@
 #ifndef AQC_HIP_H
 #define AQC_HIP_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -43,6 +44,7 @@ typedef struct aqc_op {
 
 typedef struct aqc_sv_s* aqc_sv_t;
 typedef struct aqc_mps_s* aqc_mps_t;
+typedef struct aqc_comm_s* aqc_comm_t;
 
 /* ---- library -------------------------------------------------------------------- */
 const char* aqc_last_error(void);
@@ -228,9 +230,28 @@ int aqc_stream_wait(void* stream);
  * (psi normalised). */
 int aqc_mps_product_fit(aqc_mps_t psi, double* svec, int guess_from_gamma, int min_sweeps, int max_sweeps,
                         double tol, double* fidelity, int* sweeps);
-/* np.argmax(scores * priorities) with lowest-index tie-break (adapt_compiler.py:832-837). */
+/* np.argmax(scores * priorities) with lowest-index tie-break (adapt_compiler.py:832-837).  Device
+ * scores are read on the library's stream: order it after their producer (aqc_stream_wait). */
 int aqc_argmax_scaled(const double* scores, const double* prio, int count, int scores_is_device,
                       int* best);
+
+/* ---- multi-GPU exchange over RCCL ---------------------------------------------
+ * The candidate sweep shards the coupling-map pairs across ranks (one process per GPU); its one
+ * exchange is an all-gather of the per-pair scores, after which every rank takes the same arg-max
+ * (adapt_compiler.py:832-856 -- the reference has no collective: it runs on one host).  For
+ * callers without torch.distributed.  aqc_comm_unique_id on one rank, its 128 bytes passed to
+ * every rank by the caller's own channel, then aqc_comm_init(id, rank, world) on every rank
+ * (collective; the current device, see aqc_init).  Collectives run on the library's stream:
+ * aqc_allgather_f64 takes device buffers (send: count doubles, recv: world x count, rank order)
+ * and returns once queued, ordered after the library's earlier work (a device-output sweep);
+ * aqc_allgather_f64_host / aqc_allreduce_max_f64 take host memory and return complete. */
+int aqc_comm_unique_id(char* out /* 128 bytes */);
+int aqc_comm_init(const char* unique_id, int rank, int world, aqc_comm_t* out);
+int aqc_comm_destroy(aqc_comm_t c);
+int aqc_comm_rank(aqc_comm_t c, int* rank, int* world);
+int aqc_allgather_f64(aqc_comm_t c, const double* send, double* recv, size_t count);
+int aqc_allgather_f64_host(aqc_comm_t c, const double* send, double* recv, size_t count);
+int aqc_allreduce_max_f64(aqc_comm_t c, double* value);
 
 #ifdef __cplusplus
 }

@@ -126,3 +126,36 @@ def test_partition_balanced_and_complete():
         cmap = H.coupling_map_full(n)
         idx = sorted(i for r in range(world) for i in PairShard(cmap, n, r, world).local_index)
         assert idx == list(range(len(cmap)))
+
+
+def test_gather_scores_host_matches_global_order():
+    """The host-array exchange (used with libaqchip's RCCL communicator, comm.RcclComm) puts every
+    rank's shard back in the coupling-map order, for any world size, with the arg-max the
+    reference takes (np.argmax, lowest index on ties)."""
+    import numpy as np
+
+    from adaptaqc_amd.sharding import PairShard, gather_scores_host
+    from adaptaqc_amd.utils.constants import coupling_map_fully_entangled
+
+    n = 11
+    cmap = coupling_map_fully_entangled(n)
+    rng = np.random.default_rng(3)
+    truth = rng.random((2, len(cmap)))
+    truth[:, 7] = truth.max() + 1  # a unique maximum
+    for world in (1, 2, 3, 4):
+        shards = [PairShard(cmap, n, r, world) for r in range(world)]
+        locals_ = [truth[:, s.local_index] for s in shards]
+
+        def allgather(x, w=world):  # what every rank receives from RCCL's all-gather
+            m = shards[0].max_local
+            out = np.zeros((w, len(x)))
+            for r in range(w):
+                buf = np.zeros((2, m))
+                buf[:, : locals_[r].shape[1]] = locals_[r]
+                out[r] = buf.reshape(-1)
+            return out
+
+        for r in range(world):
+            full = gather_scores_host(locals_[r], shards[r], allgather)
+            np.testing.assert_array_equal(full, truth)
+            assert int(np.argmax(full[0])) == 7

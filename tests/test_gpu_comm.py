@@ -1,0 +1,60 @@
+"""libaqchip's RCCL exchange (aqc_comm_*, include/aqc_hip.h) on the GPU box: a one-rank
+communicator (the box has one GPU; RCCL refuses two ranks on one device), the host and device
+all-gathers, the max all-reduce, and the sharded candidate sweep's exchange through it against
+the unsharded sweep.  Multi-rank behaviour of the same gather / arg-max logic is covered over gloo
+(tests/test_distributed.py)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def test_rccl_one_rank_collectives():
+    import ctypes
+
+    import torch
+
+    from adaptaqc_amd import _lib
+    from adaptaqc_amd.comm import RcclComm
+
+    uid = RcclComm.unique_id()
+    comm = RcclComm(uid, 0, 1)
+    x = np.arange(5, dtype=np.float64) * 1.5
+    np.testing.assert_array_equal(comm.allgather(x), x[None, :])
+    assert comm.allreduce_max(2.25) == 2.25
+    # device buffers, ordered both ways against torch's stream
+    src = torch.arange(7, dtype=torch.float64, device="cuda") * 0.5
+    dst = torch.zeros(7, dtype=torch.float64, device="cuda")
+    l = _lib.lib()
+    cur = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    _lib.check(l.aqc_stream_wait(cur))
+    comm.allgather_device(src.data_ptr(), dst.data_ptr(), 7)
+    _lib.check(l.aqc_stream_join(cur))
+    torch.testing.assert_close(dst, src)
+    comm.close()
+
+
+def test_sharded_sweep_through_rccl_exchange():
+    """The pair-sharded sweep (sharding.PairShard), exchanged through the RCCL communicator with
+    the host-array gather, equals the unsharded sweep and picks the same pair."""
+    import bench
+    from adaptaqc_amd.comm import RcclComm
+    from adaptaqc_amd.device import DeviceMPS, pair_grads_batch
+    from adaptaqc_amd.sharding import PairShard, gather_scores_host
+    from adaptaqc_amd.utils.constants import coupling_map_fully_entangled
+
+    n, chi = 30, 32
+    cmap = coupling_map_fully_entangled(n)
+    layer, gens, deg, u0, gm = bench.layer_inputs()
+    svec = np.zeros((n, 2), complex)
+    svec[:, 0] = 1.0
+    d = DeviceMPS(n, chi, 1e-16, chi)
+    d.load_aer(bench.near_product_mps(n, chi, 77))
+    want = pair_grads_batch([d], svec, cmap, u0, gm, deg)
+    comm = RcclComm(RcclComm.unique_id(), 0, 1)
+    shard = PairShard(cmap, n, 0, 1)
+    local = pair_grads_batch([d], svec, shard.local_pairs, u0, gm, deg)
+    full = gather_scores_host(local, shard, comm.allgather)
+    np.testing.assert_allclose(full, want, rtol=0, atol=1e-14)
+    assert int(np.argmax(full[0])) == int(np.argmax(want[0]))
+    comm.close()
