@@ -834,10 +834,14 @@ int ensure_gw(aqc_mps_t h) {
   return AQC_OK;
 }
 
+#include "sweep_seg.h"
+
 // 0: automatic (grouped chains for batches of states at cap 128, one chain per workgroup for a
 // single state, where the per-step latency of 2 rows beats the 16-row group's), 1: one chain per
-// workgroup, 2: grouped (aqc_sweep_set_chain_mode)
+// workgroup, 2: grouped, 3: the segmented single-state sweep (sweep_seg.h) whenever one state is
+// swept (aqc_sweep_set_chain_mode)
 int g_chain_mode = 0;
+bool use_segments(int cap, int ns) { return ns == 1 && g_chain_mode == 3 && cap >= 16; }
 bool use_chain8(int cap, int ns) {
   if ((cap != 128 && cap != 64) || g_chain_mode == 1) return false;
   return g_chain_mode == 2 || ns >= 2;
@@ -951,6 +955,13 @@ int aqc_pair_grads_batch(aqc_mps_t* psis, int ns, const double* svec, const int*
   const int cap = psis[0]->d.cap;
   hipLaunchKernelGGL(k_sweep_M, dim3(n, ns), dim3(kT), 0, st, djobs, dsvec);
   AQC_CHECK_LAUNCH();
+  if (use_segments(cap, ns)) {
+    const SweepJob* hj0 = (const SweepJob*)(hbase + o_jobs);
+    aqc::KernelTimer::begin(st, "grad_seg", 0.0, 2.0 * n * 8.0 * (double)cap * cap * cap);
+    rc = run_segment_sweep(*hj0, djobs, pairs, dpairs, npairs, dstart, st);
+    aqc::KernelTimer::end(st);
+    if (rc != AQC_OK) return rc;
+  } else {
   {
     const dim3 g(ns, 2), b(1024);
     if (cap == 64) hipLaunchKernelGGL((k_sweep_lr_pf<64>), g, dim3(512), 0, st, djobs);
@@ -989,6 +1000,7 @@ int aqc_pair_grads_batch(aqc_mps_t* psis, int ns, const double* svec, const int*
       AQC_CHECK_LAUNCH();
     }
   }
+  }  // chain form
   if (npairs) {
     SweepConst c;
     c.npairs = npairs;
@@ -1013,7 +1025,7 @@ int aqc_pair_grads_batch(aqc_mps_t* psis, int ns, const double* svec, const int*
 }
 
 int aqc_sweep_set_chain_mode(int mode) {
-  AQC_REQUIRE(mode >= 0 && mode <= 2, "aqc_sweep_set_chain_mode: mode 0, 1 or 2");
+  AQC_REQUIRE(mode >= 0 && mode <= 3, "aqc_sweep_set_chain_mode: mode 0, 1, 2 or 3");
   g_chain_mode = mode;
   return AQC_OK;
 }
