@@ -9,10 +9,21 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def test_rccl_one_rank_collectives():
+def _hip():
+    """The HIP runtime libaqchip itself links (device buffers for the device-pointer all-gather;
+    torch is not used here: it would bring its own HIP runtime into the process)."""
     import ctypes
 
-    import torch
+    for name in ("libamdhip64.so", "/opt/rocm/lib/libamdhip64.so"):
+        try:
+            return ctypes.CDLL(name)
+        except OSError:
+            continue
+    raise RuntimeError("libamdhip64.so not found")
+
+
+def test_rccl_one_rank_collectives():
+    import ctypes
 
     from adaptaqc_amd import _lib
     from adaptaqc_amd.comm import RcclComm
@@ -22,15 +33,22 @@ def test_rccl_one_rank_collectives():
     x = np.arange(5, dtype=np.float64) * 1.5
     np.testing.assert_array_equal(comm.allgather(x), x[None, :])
     assert comm.allreduce_max(2.25) == 2.25
-    # device buffers, ordered both ways against torch's stream
-    src = torch.arange(7, dtype=torch.float64, device="cuda") * 0.5
-    dst = torch.zeros(7, dtype=torch.float64, device="cuda")
-    l = _lib.lib()
-    cur = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-    _lib.check(l.aqc_stream_wait(cur))
-    comm.allgather_device(src.data_ptr(), dst.data_ptr(), 7)
-    _lib.check(l.aqc_stream_join(cur))
-    torch.testing.assert_close(dst, src)
+    # device buffers on the library's stream
+    hip = _hip()
+    src_h = np.arange(7, dtype=np.float64) * 0.5
+    dst_h = np.zeros(7)
+    ds, dd = ctypes.c_void_p(), ctypes.c_void_p()
+    assert hip.hipMalloc(ctypes.byref(ds), ctypes.c_size_t(56)) == 0
+    assert hip.hipMalloc(ctypes.byref(dd), ctypes.c_size_t(56)) == 0
+    try:
+        assert hip.hipMemcpy(ds, src_h.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(56), 1) == 0  # H2D
+        comm.allgather_device(ds.value, dd.value, 7)
+        _lib.check(_lib.lib().aqc_stream_join(None))  # the legacy default stream waits for it
+        assert hip.hipMemcpy(dst_h.ctypes.data_as(ctypes.c_void_p), dd, ctypes.c_size_t(56), 2) == 0  # D2H
+        np.testing.assert_array_equal(dst_h, src_h)
+    finally:
+        hip.hipFree(ds)
+        hip.hipFree(dd)
     comm.close()
 
 
