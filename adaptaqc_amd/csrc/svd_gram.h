@@ -40,6 +40,10 @@ constexpr int kGramMaxK = 64;
 #ifndef AQC_S3_PRIO
 #define AQC_S3_PRIO 1
 #endif
+// S5: the LDL^T pivots from the leading minors' recurrence (one FMA + the guard on the chain)
+#ifndef AQC_S5_POLY
+#define AQC_S5_POLY 1
+#endif
 constexpr double kGramRelFloor = 1e-9;
 // shader-clock ticks of the phases (thread 0), summed over calls: S1, S2+S3, S4, S5, S6, output
 __device__ unsigned long long g_gram_ticks[8];
@@ -530,6 +534,26 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
     // (full chunks unguarded -- C is uniform but not known to the compiler, whose per-row guards
     // became exec-mask branches -- then a scalar tail; clamped indices with zero carries make the
     // first / last rows regular)
+#if AQC_S5_POLY
+    // The pivots as ratios of the leading minors of T - lam I (the recurrence of S4's Sturm count,
+    // in units of ||T||): D_row = p_row / p_{row-1}, p_row = (d - lam) p_{row-1} - e^2 p_{row-2},
+    // so the dependent chain is one FMA and the pivot guard (|D| < eps -> +-eps) per row; each
+    // 1 / D = p_{row-1} / p_row is formed off the chain.  Rescaled by the binary exponent every
+    // chunk of 8 rows (the guard bounds the shrink per row by eps, the growth by 3).
+    (void)piv;
+    const double itn = 1.0 / fmax(s_tn, 1e-300), lamn = lam * itn;
+    double p0 = 0.0, p1 = 1.0;  // p_{row-2}, p_{row-1}; row 0 has no e term
+    auto fac_row = [&](int row, double d, double e2, double& unused) {
+      (void)unused;
+      const double dmx = fma(d, itn, -lamn), t = (e2 * itn * itn) * p0;
+      const double lim = 2.220446049250313e-16 * fabs(p1);
+      double p = fma(dmx, p1, -t);
+      p = fabs(p) < lim ? copysign(lim, p) : p;
+      Db[row * 64 + i] = p1 * rcp_nr(p) * itn;
+      p0 = p1;
+      p1 = p;
+    };
+#else
     auto fac_row = [&](int row, double d, double e2, double& rdp) {
       double dj = fma(-e2, rdp, d - lam);
       if (fabs(dj) < piv) dj = dj >= 0.0 ? piv : -piv;
@@ -537,6 +561,7 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
       Db[row * 64 + i] = rd;
       rdp = rd;
     };
+#endif
     {
       double rdp = 0.0;
       int r0 = 0;
@@ -546,6 +571,11 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
         for (int u = 0; u < U; ++u) dd[u] = s_d[r0 + u], ee[u] = s_e2[max(r0 + u - 1, 0)];
 #pragma unroll
         for (int u = 0; u < U; ++u) fac_row(r0 + u, dd[u], ee[u], rdp);
+#if AQC_S5_POLY
+        const int ex = max(__builtin_amdgcn_frexp_exp(p0), __builtin_amdgcn_frexp_exp(p1));
+        p0 = __builtin_amdgcn_ldexp(p0, -ex);
+        p1 = __builtin_amdgcn_ldexp(p1, -ex);
+#endif
       }
       for (; r0 < C; ++r0) fac_row(r0, s_d[r0], s_e2[max(r0 - 1, 0)], rdp);
     }
