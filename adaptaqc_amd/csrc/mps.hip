@@ -1821,7 +1821,7 @@ int run_waves(aqc_mps_t* hs, int ns, std::vector<std::vector<DevOp>>& lists) {
     }
     two_rng[w] = {t0, two.size() - t0};
     one_rng[w] = {o0, one.size() - o0};
-    const int qr = wave_side[w] <= 128 ? 1 : 0;
+    const int qr = (2 * cap_max <= 128 || wave_side[w] <= 128) ? 1 : 0;
     for (size_t k = t0; k < two.size(); ++k) two[k].qr = qr;
   }
   const size_t tb = two.size() * sizeof(TwoSiteJob), ob = one.size() * sizeof(OneSiteJob);
@@ -1853,7 +1853,9 @@ int run_waves(aqc_mps_t* hs, int ns, std::vector<std::vector<DevOp>>& lists) {
       aqc::KernelTimer::end(st);
       AQC_CHECK_LAUNCH();
       aqc::KernelTimer::begin(st, "mps_svd", nj * 2.0 * (4.0 * c * c * 16), 0.0);
-      const int side = std::min(wave_side[w], 2 * cap_max);
+      // (capacities <= 64 keep their kernel choice: the lock-step path then matches the fused
+      // chain's arithmetic exactly)
+      const int side = 2 * cap_max <= 128 ? 2 * cap_max : std::min(wave_side[w], 2 * cap_max);
       if (side <= 128) {
         // register-resident kernel; column count padded to a power of two.  Dynamic LDS holds
         // the round exchange (kG x 16*MAXR) or the QR transpose (kG x (CP+1)), whichever is larger

@@ -711,7 +711,27 @@ def latency_block(q0, cpu):
         out[f"rotoselect_gate_7_evals_ms_d{d}"] = t
         if str(d) in cpu_ms:
             out[f"rotoselect_gate_speedup_vs_cpu_1core_d{d}"] = 7 * cpu_ms[str(d)] / t
-    out["note"] = "single state on one GPU; wall time of one evaluation (or one gate's 7 as one batch)"
+    # one candidate sweep of one state, the reference's per-layer call (gradients.py:81-122 from
+    # adapt_compiler.py:839-856): 1225 pairs, host result
+    from adaptaqc_amd.device import pair_grads_batch
+    from adaptaqc_amd.utils.constants import coupling_map_fully_entangled
+
+    cmap = coupling_map_fully_entangled(n)
+    _, _, deg, u0, gm = layer_inputs()
+    svec = np.zeros((n, 2), complex)
+    svec[:, 0] = 1.0
+    ts = []
+    for _ in range(8):
+        t0 = time.perf_counter()
+        pair_grads_batch([src], svec, cmap, u0, gm, deg)
+        ts.append(time.perf_counter() - t0)
+    out["single_sweep_ms"] = 1e3 * float(np.median(ts[2:]))
+    g = (cpu or {}).get("gradient", {})
+    if g.get("evals_per_s") and (cpu or {}).get("workers"):
+        per_core = g["evals_per_s"] / cpu["workers"]
+        out["cpu_port_single_sweep_ms_1core"] = 1e3 * len(cmap) / per_core
+        out["single_sweep_speedup_vs_cpu_1core"] = out["cpu_port_single_sweep_ms_1core"] / out["single_sweep_ms"]
+    out["note"] = "single state on one GPU; wall time of one evaluation (or one gate's 7 as one batch, or one sweep)"
     return out
 
 
