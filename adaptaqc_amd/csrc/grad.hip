@@ -67,7 +67,8 @@ __global__ __launch_bounds__(kT) void k_sweep_M(const SweepJob* __restrict__ job
   const cplx s0 = aqc::cconj(svec[2 * i]), s1 = aqc::cconj(svec[2 * i + 1]);
   cplx* Mi = j.M + (size_t)i * j.cap * j.cap;
   // the whole cap x cap block, zeros outside chi_l x chi_r: the chains read it without masks
-  for (int e = threadIdx.x; e < j.cap * j.cap; e += kT) {
+  // (blockIdx.z splits a site over several workgroups when few states are swept)
+  for (int e = blockIdx.z * kT + threadIdx.x; e < j.cap * j.cap; e += kT * gridDim.z) {
     const int l = e / j.cap, r = e % j.cap;
     Mi[e] = (l < cl && r < cr) ? aqc::cfma(s1, site_a(j, i, 1, l, r), aqc::cmul(s0, site_a(j, i, 0, l, r)))
                                : aqc::cmk(0, 0);
@@ -322,7 +323,7 @@ __global__ __launch_bounds__(kT) void k_sweep_w(const SweepJob* __restrict__ job
   __syncthreads();
   {
     const int ks = tid & 7;
-    for (int row0 = 0; row0 < 2 * cl; row0 += kT / 8) {
+    for (int row0 = blockIdx.z * (kT / 8); row0 < 2 * cl; row0 += (kT / 8) * gridDim.z) {
       const int row = row0 + (tid >> 3);  // (s, l) = (row / cl, row % cl)
       const bool ok = row < 2 * cl;
       const int sr = ok ? row / cl : 0, lr = ok ? row % cl : 0;
@@ -339,7 +340,7 @@ __global__ __launch_bounds__(kT) void k_sweep_w(const SweepJob* __restrict__ job
   __syncthreads();
   for (int l = tid; l < cl; l += kT) x[l] = j.lv[(size_t)i * cap + l];
   __syncthreads();
-  for (int e = tid; e < 2 * cap; e += kT) {
+  for (int e = blockIdx.z * kT + tid; e < 2 * cap; e += kT * gridDim.z) {
     const int sr = e / cap, r = e % cap;
     if (r >= cr) continue;
     const cplx* g = G + (size_t)sr * cap * cap + r;
@@ -953,7 +954,10 @@ int aqc_pair_grads_batch(aqc_mps_t* psis, int ns, const double* svec, const int*
   }
   AQC_HIP_CHECK(hipMemcpyAsync(base, hbase, image, hipMemcpyHostToDevice, st));
   const int cap = psis[0]->d.cap;
-  hipLaunchKernelGGL(k_sweep_M, dim3(n, ns), dim3(kT), 0, st, djobs, dsvec);
+  // few states: each site's M over several workgroups (the chains / GEMMs that follow are the
+  // single sweep's critical path)
+  const unsigned zsplit = ns >= 8 ? 1u : 8u;
+  hipLaunchKernelGGL(k_sweep_M, dim3(n, ns, zsplit), dim3(kT), 0, st, djobs, dsvec);
   AQC_CHECK_LAUNCH();
   if (use_segments(cap, ns)) {
     const SweepJob* hj0 = (const SweepJob*)(hbase + o_jobs);
@@ -972,7 +976,7 @@ int aqc_pair_grads_batch(aqc_mps_t* psis, int ns, const double* svec, const int*
     else hipLaunchKernelGGL((k_sweep_lr<256, false>), g, b, 0, st, djobs);
   }
   AQC_CHECK_LAUNCH();
-  hipLaunchKernelGGL(k_sweep_w, dim3(n, ns), dim3(kT), 0, st, djobs, (const int*)dstart);
+  hipLaunchKernelGGL(k_sweep_w, dim3(n, ns, zsplit), dim3(kT), 0, st, djobs, (const int*)dstart);
   AQC_CHECK_LAUNCH();
   {
     // algorithmic work of the chain: sum_a (n-a-1) steps of a 2 x chi x chi complex vec-mat

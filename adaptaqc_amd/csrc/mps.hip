@@ -1799,18 +1799,40 @@ int run_waves(aqc_mps_t* hs, int ns, std::vector<std::vector<DevOp>>& lists) {
   // preconditioning (the Gram path in front of it at 2 chi = 128), larger the multi-workgroup
   // block Jacobi sized by the bound -- so a large-capacity state with small bonds (an unbounded
   // MPS early in a circuit) does not pay for its capacity
-  std::vector<int> wave_side(maxlen, 2);
+  // Each two-site job's SVD kernel class from its own largest possible theta side (2 chi): the
+  // register Jacobi up to 128 (the Gram path in front of it at 128), the block Jacobi sized to the
+  // next power of two above (at most 2 cap) -- so a large-capacity state with small bonds does not
+  // pay for its capacity, and a job's kernel does not depend on the jobs it shares a wave with
+  // (a batched wave equals the same updates applied one call at a time, bit for bit).  Capacities
+  // <= 64 keep one class (2 cap): the lock-step path then matches the fused chain exactly.
+  struct ClassRange {
+    int cls;
+    size_t first, count;
+  };
+  std::vector<std::vector<ClassRange>> wave_cls(maxlen);
+  auto class_of = [&](int side) {
+    if (2 * cap_max <= 128) return 2 * cap_max;
+    if (side <= 32) return 32;
+    if (side <= 64) return 64;
+    if (side <= 128) return 128;
+    int c = 256;
+    while (c < side) c <<= 1;
+    return std::min(c, 2 * cap_max);
+  };
+  std::vector<std::pair<int, TwoSiteJob>> wjobs;
   for (size_t w = 0; w < maxlen; ++w) {
     size_t t0 = two.size(), o0 = one.size();
+    wjobs.clear();
     for (int s = 0; s < ns; ++s) {
       if (w >= lv[s].size()) continue;
       int slot = 0;
       std::vector<int>& ub = hs[s]->ub;
       for (const DevOp* op : lv[s][w]) {
         if (op->kind == 2) {
-          two.push_back(make_two(hs[s], *op, slot++));
           const int p = op->p;
-          wave_side[w] = std::max(wave_side[w], 2 * std::max(ub[p], ub[p + 2]));
+          const int cls = class_of(2 * std::max(ub[p], ub[p + 2]));
+          wjobs.push_back({cls, make_two(hs[s], *op, slot++)});
+          wjobs.back().second.qr = cls <= 128 ? 1 : 0;
           int nb = std::min(2 * std::min(ub[p], ub[p + 2]), hs[s]->d.cap);
           if (hs[s]->max_chi > 0) nb = std::min(nb, hs[s]->max_chi);
           ub[p + 1] = std::max(nb, 1);
@@ -1819,10 +1841,14 @@ int run_waves(aqc_mps_t* hs, int ns, std::vector<std::vector<DevOp>>& lists) {
         }
       }
     }
+    std::stable_sort(wjobs.begin(), wjobs.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
+    for (size_t k = 0; k < wjobs.size(); ++k) {
+      if (k == 0 || wjobs[k].first != wjobs[k - 1].first) wave_cls[w].push_back({wjobs[k].first, two.size(), 0});
+      wave_cls[w].back().count += 1;
+      two.push_back(wjobs[k].second);
+    }
     two_rng[w] = {t0, two.size() - t0};
     one_rng[w] = {o0, one.size() - o0};
-    const int qr = (2 * cap_max <= 128 || wave_side[w] <= 128) ? 1 : 0;
-    for (size_t k = t0; k < two.size(); ++k) two[k].qr = qr;
   }
   const size_t tb = two.size() * sizeof(TwoSiteJob), ob = one.size() * sizeof(OneSiteJob);
   StagingLease lease(st);
@@ -1853,23 +1879,24 @@ int run_waves(aqc_mps_t* hs, int ns, std::vector<std::vector<DevOp>>& lists) {
       aqc::KernelTimer::end(st);
       AQC_CHECK_LAUNCH();
       aqc::KernelTimer::begin(st, "mps_svd", nj * 2.0 * (4.0 * c * c * 16), 0.0);
-      // (capacities <= 64 keep their kernel choice: the lock-step path then matches the fused
-      // chain's arithmetic exactly)
-      const int side = 2 * cap_max <= 128 ? 2 * cap_max : std::min(wave_side[w], 2 * cap_max);
-      if (side <= 128) {
-        // register-resident kernel; column count padded to a power of two.  Dynamic LDS holds
-        // the round exchange (kG x 16*MAXR) or the QR transpose (kG x (CP+1)), whichever is larger
-        if (side <= 32)
-          hipLaunchKernelGGL((k_jacobi_reg<32, 2>), dim3(nj), dim3(256), 16 * 33 * 16, st, jp);
-        else if (side <= 64)
-          hipLaunchKernelGGL((k_jacobi_reg<64, 4>), dim3(nj), dim3(512), 32 * 65 * 16, st, jp);
-        else
-          launch_jacobi_reg128(nj, st, jp);
-      } else {
-        // 2 chi > 128: multi-workgroup block Jacobi (bjacobi.hip), W in HBM / L2, sized by the
-        // wave's bound
-        const int brc = aqc::block_jacobi(jp, nj, (side + 1) / 2, st);
-        if (brc != AQC_OK) return brc;
+      for (const ClassRange& cr : wave_cls[w]) {
+        const int side = cr.cls, nc = (int)cr.count;
+        const TwoSiteJob* jc = dtwo + cr.first;
+        if (side <= 128) {
+          // register-resident kernel; column count padded to a power of two.  Dynamic LDS holds
+          // the round exchange (kG x 16*MAXR) or the QR transpose (kG x (CP+1)), whichever is larger
+          if (side <= 32)
+            hipLaunchKernelGGL((k_jacobi_reg<32, 2>), dim3(nc), dim3(256), 16 * 33 * 16, st, jc);
+          else if (side <= 64)
+            hipLaunchKernelGGL((k_jacobi_reg<64, 4>), dim3(nc), dim3(512), 32 * 65 * 16, st, jc);
+          else
+            launch_jacobi_reg128(nc, st, jc);
+        } else {
+          // 2 chi > 128: multi-workgroup block Jacobi (bjacobi.hip), W in HBM / L2, sized by
+          // the class
+          const int brc = aqc::block_jacobi(jc, nc, side / 2, st);
+          if (brc != AQC_OK) return brc;
+        }
       }
       aqc::KernelTimer::end(st);
       AQC_CHECK_LAUNCH();

@@ -36,7 +36,7 @@ struct CgemmJob {
 // C = A B (complex) for a batch of jobs; one wave per 16 x 16 output tile: grid (tiles, jobs).
 // v_mfma_f64_16x16x4f64 operand layout: A[m = lane & 15][k = lane >> 4], B[k = lane >> 4][n =
 // lane & 15], D[m = (lane >> 4) + 4 q][n = lane & 15]; a complex product is four real ones into
-// two accumulators.  Eight k steps' operands are loaded before their MFMAs.
+// two accumulators.
 __global__ __launch_bounds__(64) void k_cgemm16(const CgemmJob* __restrict__ jobs) {
   const CgemmJob& jb = jobs[blockIdx.y];
   const int tm = blockIdx.x / jb.tiles_n, tn = blockIdx.x % jb.tiles_n;
@@ -48,23 +48,33 @@ __global__ __launch_bounds__(64) void k_cgemm16(const CgemmJob* __restrict__ job
   typedef double __attribute__((ext_vector_type(4))) d4;
   d4 cr = {0, 0, 0, 0}, ci = {0, 0, 0, 0};
   const int K = jb.k;
-  for (int k0 = 0; k0 < K; k0 += 32) {
-    cplx a[8], b[8];
+  // chunks of 4 k steps, double-buffered: chunk c + 1's operands are in flight while chunk c's
+  // MFMAs run (the operands stream from L2 / the Infinity Cache)
+  constexpr int CS = 4;
+  cplx a[2][CS], b[2][CS];
+  auto load = [&](int k0, cplx (&ra)[CS], cplx (&rb)[CS]) {
 #pragma unroll
-    for (int s = 0; s < 8; ++s) {
+    for (int s = 0; s < CS; ++s) {
       const int kk = k0 + 4 * s + lk;
       const bool kin = kk < K;
-      a[s] = (arow && kin) ? aqc::ldg(jb.A + (size_t)ia * jb.lda + kk) : aqc::cmk(0, 0);
-      b[s] = (bcol && kin) ? aqc::ldg(jb.B + (jb.tb ? (size_t)jc * jb.ldb + kk : (size_t)kk * jb.ldb + jc))
-                           : aqc::cmk(0, 0);
+      ra[s] = (arow && kin) ? aqc::ldg(jb.A + (size_t)ia * jb.lda + kk) : aqc::cmk(0, 0);
+      rb[s] = (bcol && kin) ? aqc::ldg(jb.B + (jb.tb ? (size_t)jc * jb.ldb + kk : (size_t)kk * jb.ldb + jc))
+                            : aqc::cmk(0, 0);
     }
+  };
+  load(0, a[0], b[0]);
+  int cur = 0;
+  for (int k0 = 0; k0 < K; k0 += 4 * CS) {
+    if (k0 + 4 * CS < K) load(k0 + 4 * CS, a[cur ^ 1], b[cur ^ 1]);
 #pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      cr = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s].x, b[s].x, cr, 0, 0, 0);
-      ci = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s].x, b[s].y, ci, 0, 0, 0);
-      cr = __builtin_amdgcn_mfma_f64_16x16x4f64(-a[s].y, b[s].y, cr, 0, 0, 0);
-      ci = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s].y, b[s].x, ci, 0, 0, 0);
+    for (int s = 0; s < CS; ++s) {
+      const cplx x = a[cur][s], y = b[cur][s];
+      cr = __builtin_amdgcn_mfma_f64_16x16x4f64(x.x, y.x, cr, 0, 0, 0);
+      ci = __builtin_amdgcn_mfma_f64_16x16x4f64(x.x, y.y, ci, 0, 0, 0);
+      cr = __builtin_amdgcn_mfma_f64_16x16x4f64(-x.y, y.y, cr, 0, 0, 0);
+      ci = __builtin_amdgcn_mfma_f64_16x16x4f64(x.y, y.x, ci, 0, 0, 0);
     }
+    cur ^= 1;
   }
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
@@ -126,6 +136,12 @@ struct SegScratch {
   size_t hbytes = 0;
   hipEvent_t done = nullptr;
   bool pending = false;
+  // the last plan (its job / pointer tables stay on the device): reused while the state's buffers
+  // and the pair list are the same -- the per-layer call repeats both
+  std::vector<unsigned long long> key;
+  std::vector<std::pair<size_t, size_t>> launches;
+  std::vector<int> ltiles;
+  size_t env_launches = 0, tbl_bytes = 0;
 };
 
 SegScratch& seg_scratch() {
@@ -245,12 +261,27 @@ int run_segment_sweep(const SweepJob& hj, const SweepJob* djob, const int* pairs
     }
     return env_launches;
   };
+  // the plan's identity: shapes, the state's buffers, the pair list
+  std::vector<unsigned long long> key = {(unsigned long long)n, (unsigned long long)cap, (unsigned long long)npairs,
+                                         (unsigned long long)(uintptr_t)hj.M, (unsigned long long)(uintptr_t)hj.lv,
+                                         (unsigned long long)(uintptr_t)hj.rv, (unsigned long long)(uintptr_t)hj.w,
+                                         (unsigned long long)(uintptr_t)hj.v0, (unsigned long long)(uintptr_t)hj.T};
+  {
+    unsigned long long h = 1469598103934665603ull;
+    for (int i = 0; i < 2 * npairs; ++i) h = (h ^ (unsigned long long)(unsigned)pairs[i]) * 1099511628211ull;
+    key.push_back(h);
+  }
+  const bool reuse = sc.dev && key == sc.key;
+  if (reuse) {
+    launches = sc.launches;
+    ltiles = sc.ltiles;
+  }
   // size the scratch: data + job table + pair pointer tables
-  size_t env_launches = plan(nullptr);
-  const size_t tbl_bytes = jobs.size() * sizeof(CgemmJob);
+  size_t env_launches = reuse ? sc.env_launches : plan(nullptr);
+  const size_t tbl_bytes = reuse ? sc.tbl_bytes : jobs.size() * sizeof(CgemmJob);
   const size_t ptr_bytes = 2 * (size_t)npairs * sizeof(cplx*);
   const size_t need = table_off_bytes + tbl_bytes + ptr_bytes + 256;
-  if (sc.pending) {
+  if (sc.pending && !reuse) {  // the last call's host staging may still be in flight
     AQC_HIP_CHECK(hipEventSynchronize(sc.done));
     sc.pending = false;
   }
@@ -258,6 +289,7 @@ int run_segment_sweep(const SweepJob& hj, const SweepJob* djob, const int* pairs
     if (sc.dev) hipFree(sc.dev);
     sc.dev = nullptr;
     sc.bytes = 0;
+    sc.key.clear();
     AQC_HIP_CHECK(hipMalloc(&sc.dev, need));
     sc.bytes = need;
   }
@@ -271,6 +303,8 @@ int run_segment_sweep(const SweepJob& hj, const SweepJob* djob, const int* pairs
   }
   if (!sc.done) AQC_HIP_CHECK(hipEventCreateWithFlags(&sc.done, hipEventDisableTiming));
   cplx* base = sc.dev;
+  char* dtab = reinterpret_cast<char*>(base) + table_off_bytes;
+  if (!reuse) {
   env_launches = plan(base);
   // pair operand pointers (step 6)
   auto Vp = [&](int a, int t) -> const cplx* { return base + oV + ((size_t)a * Tv + (t - 1)) * 2 * cap; };
@@ -293,8 +327,13 @@ int run_segment_sweep(const SweepJob& hj, const SweepJob* djob, const int* pairs
     }
   }
   std::memcpy(sc.host, jobs.data(), tbl_bytes);
-  char* dtab = reinterpret_cast<char*>(base) + table_off_bytes;
   AQC_HIP_CHECK(hipMemcpyAsync(dtab, sc.host, tbl_bytes + ptr_bytes, hipMemcpyHostToDevice, st));
+  sc.key = key;
+  sc.launches = launches;
+  sc.ltiles = ltiles;
+  sc.env_launches = env_launches;
+  sc.tbl_bytes = tbl_bytes;
+  }
   const CgemmJob* djobs = reinterpret_cast<const CgemmJob*>(dtab);
   const cplx* const* dx = reinterpret_cast<const cplx* const*>(dtab + tbl_bytes);
   const cplx* const* dy = dx + npairs;
@@ -308,7 +347,7 @@ int run_segment_sweep(const SweepJob& hj, const SweepJob* djob, const int* pairs
     AQC_CHECK_LAUNCH();
   }
   // 4. v0, w
-  hipLaunchKernelGGL(k_sweep_w, dim3(n, 1), dim3(kT), 0, st, djob, dstart);
+  hipLaunchKernelGGL(k_sweep_w, dim3(n, 1, 8), dim3(kT), 0, st, djob, dstart);
   AQC_CHECK_LAUNCH();
   // 5. hops
   for (size_t l = env_launches; l < launches.size(); ++l) {
