@@ -33,53 +33,56 @@ struct CgemmJob {
   int tiles_n;
 };
 
-// C = A B (complex) for a batch of jobs; one wave per 16 x 16 output tile: grid (tiles, jobs).
-// v_mfma_f64_16x16x4f64 operand layout: A[m = lane & 15][k = lane >> 4], B[k = lane >> 4][n =
-// lane & 15], D[m = (lane >> 4) + 4 q][n = lane & 15]; a complex product is four real ones into
-// two accumulators.
-__global__ __launch_bounds__(64) void k_cgemm16(const CgemmJob* __restrict__ jobs) {
+// C = A B (complex) for a batch of jobs; one 256-thread workgroup per 16 x 16 output tile, grid
+// (tiles, jobs).  The four waves split the contraction: wave w takes k steps w, w + 4, ... (4 k
+// values each), issues all of its operand loads at once (8 steps in flight; the operands stream
+// from L2 / the Infinity Cache), and the partial tiles meet in the LDS -- each launch is one
+// latency-bound step of the single sweep's dependent chain.  v_mfma_f64_16x16x4f64 operand
+// layout: A[m = lane & 15][k = lane >> 4], B[k = lane >> 4][n = lane & 15], D[m = (lane >> 4) +
+// 4 q][n = lane & 15]; a complex product is four real ones into two accumulators.
+__global__ __launch_bounds__(256) void k_cgemm16(const CgemmJob* __restrict__ jobs) {
   const CgemmJob& jb = jobs[blockIdx.y];
   const int tm = blockIdx.x / jb.tiles_n, tn = blockIdx.x % jb.tiles_n;
   const int i0 = tm * 16, j0 = tn * 16;
   if (i0 >= jb.m) return;
-  const int lane = threadIdx.x, li = lane & 15, lk = lane >> 4;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, li = lane & 15, lk = lane >> 4;
   const int ia = i0 + li, jc = j0 + li;
   const bool arow = ia < jb.m, bcol = jc < jb.n;
   typedef double __attribute__((ext_vector_type(4))) d4;
   d4 cr = {0, 0, 0, 0}, ci = {0, 0, 0, 0};
   const int K = jb.k;
-  // chunks of 4 k steps, double-buffered: chunk c + 1's operands are in flight while chunk c's
-  // MFMAs run (the operands stream from L2 / the Infinity Cache)
-  constexpr int CS = 4;
-  cplx a[2][CS], b[2][CS];
-  auto load = [&](int k0, cplx (&ra)[CS], cplx (&rb)[CS]) {
+  constexpr int CS = 8;  // k steps per wave per pass
+  for (int base = 0; base < K; base += 4 * 4 * CS) {
+    cplx a[CS], b[CS];
 #pragma unroll
     for (int s = 0; s < CS; ++s) {
-      const int kk = k0 + 4 * s + lk;
+      const int kk = base + 4 * (4 * s + wave) + lk;
       const bool kin = kk < K;
-      ra[s] = (arow && kin) ? aqc::ldg(jb.A + (size_t)ia * jb.lda + kk) : aqc::cmk(0, 0);
-      rb[s] = (bcol && kin) ? aqc::ldg(jb.B + (jb.tb ? (size_t)jc * jb.ldb + kk : (size_t)kk * jb.ldb + jc))
-                            : aqc::cmk(0, 0);
+      a[s] = (arow && kin) ? aqc::ldg(jb.A + (size_t)ia * jb.lda + kk) : aqc::cmk(0, 0);
+      b[s] = (bcol && kin) ? aqc::ldg(jb.B + (jb.tb ? (size_t)jc * jb.ldb + kk : (size_t)kk * jb.ldb + jc))
+                           : aqc::cmk(0, 0);
     }
-  };
-  load(0, a[0], b[0]);
-  int cur = 0;
-  for (int k0 = 0; k0 < K; k0 += 4 * CS) {
-    if (k0 + 4 * CS < K) load(k0 + 4 * CS, a[cur ^ 1], b[cur ^ 1]);
 #pragma unroll
     for (int s = 0; s < CS; ++s) {
-      const cplx x = a[cur][s], y = b[cur][s];
-      cr = __builtin_amdgcn_mfma_f64_16x16x4f64(x.x, y.x, cr, 0, 0, 0);
-      ci = __builtin_amdgcn_mfma_f64_16x16x4f64(x.x, y.y, ci, 0, 0, 0);
-      cr = __builtin_amdgcn_mfma_f64_16x16x4f64(-x.y, y.y, cr, 0, 0, 0);
-      ci = __builtin_amdgcn_mfma_f64_16x16x4f64(x.y, y.x, ci, 0, 0, 0);
+      cr = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s].x, b[s].x, cr, 0, 0, 0);
+      ci = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s].x, b[s].y, ci, 0, 0, 0);
+      cr = __builtin_amdgcn_mfma_f64_16x16x4f64(-a[s].y, b[s].y, cr, 0, 0, 0);
+      ci = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s].y, b[s].x, ci, 0, 0, 0);
     }
-    cur ^= 1;
   }
+  __shared__ double part[3][8][64];
+  if (wave > 0) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) part[wave - 1][q][lane] = cr[q], part[wave - 1][4 + q][lane] = ci[q];
+  }
+  __syncthreads();
+  if (wave > 0) return;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
+    const double re = cr[q] + part[0][q][lane] + part[1][q][lane] + part[2][q][lane];
+    const double im = ci[q] + part[0][4 + q][lane] + part[1][4 + q][lane] + part[2][4 + q][lane];
     const int row = i0 + lk + 4 * q;
-    if (row < jb.m && bcol) jb.C[(size_t)row * jb.ldc + jc] = aqc::cmk(cr[q], ci[q]);
+    if (row < jb.m && bcol) jb.C[(size_t)row * jb.ldc + jc] = aqc::cmk(re, im);
   }
 }
 
@@ -342,7 +345,7 @@ int run_segment_sweep(const SweepJob& hj, const SweepJob* djob, const int* pairs
   hipLaunchKernelGGL(k_seg_init, dim3(64), dim3(256), 0, st, hj.lv, hj.rv + (size_t)n * cap, hj.w, hj.v0, cap, wlen);
   AQC_CHECK_LAUNCH();
   for (size_t l = 0; l < env_launches; ++l) {
-    hipLaunchKernelGGL(k_cgemm16, dim3(ltiles[l], (unsigned)launches[l].second), dim3(64), 0, st,
+    hipLaunchKernelGGL(k_cgemm16, dim3(ltiles[l], (unsigned)launches[l].second), dim3(256), 0, st,
                        djobs + launches[l].first);
     AQC_CHECK_LAUNCH();
   }
@@ -351,7 +354,7 @@ int run_segment_sweep(const SweepJob& hj, const SweepJob* djob, const int* pairs
   AQC_CHECK_LAUNCH();
   // 5. hops
   for (size_t l = env_launches; l < launches.size(); ++l) {
-    hipLaunchKernelGGL(k_cgemm16, dim3(ltiles[l], (unsigned)launches[l].second), dim3(64), 0, st,
+    hipLaunchKernelGGL(k_cgemm16, dim3(ltiles[l], (unsigned)launches[l].second), dim3(256), 0, st,
                        djobs + launches[l].first);
     AQC_CHECK_LAUNCH();
   }
