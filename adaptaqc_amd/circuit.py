@@ -358,19 +358,63 @@ _QASM_NAMES = {"rx", "ry", "rz", "p", "u1", "u", "u3", "u2", "x", "y", "z", "h",
                "sxdg", "id", "cx", "cy", "cz", "swap", "crx", "cry", "crz", "cp", "cu1", "rzz", "ccx"}
 
 
+def u3_params(v):
+    """(theta, phi, lam, alpha) with v = exp(i alpha) u3(theta, phi, lam) for a 2x2 unitary."""
+    v = np.asarray(v, dtype=complex)
+    theta = 2.0 * float(np.arctan2(abs(v[1, 0]), abs(v[0, 0])))
+    if abs(v[0, 0]) > 1e-12:
+        alpha = float(np.angle(v[0, 0]))
+        phi = float(np.angle(v[1, 0])) - alpha if abs(v[1, 0]) > 1e-12 else 0.0
+        lam = float(np.angle(v[1, 1])) - alpha - phi if abs(v[1, 0]) <= 1e-12 else float(np.angle(-v[0, 1])) - alpha
+    else:  # theta = pi: only the off-diagonal is set; phi absorbs the phase
+        alpha, phi = float(np.angle(v[1, 0])), 0.0
+        lam = float(np.angle(-v[0, 1])) - alpha
+    return theta, phi, lam, alpha
+
+
+def unroll_two_qubit(u):
+    """Standard-gate pieces of a 4x4 unitary on local qubits (0, 1) (index 2*b1 + b0, gates.py), up
+    to a global phase: the cosine-sine split U = (A0 (+) A1) CS (B0 (+) B1) over bit 1, each
+    block-diagonal factor as u3 on qubit 0 then controlled-u3 from qubit 1 (with the control's u1
+    phase), and CS as ry on qubit 1 plus cry from qubit 0.  [(name, params, local qubits)]."""
+    from scipy.linalg import cossin
+
+    left, cs, right = cossin(np.asarray(u, dtype=complex), p=2, q=2)
+    th = np.arctan2(np.diag(cs[2:, :2]), np.diag(cs[:2, :2]))  # C = cos th, S = sin th (per bit 0)
+
+    def multiplexed(m):  # block_diag(a, b) over bit 1, acting on qubit 0
+        a, b = m[:2, :2], m[2:, 2:]
+        t, p, l, _ = u3_params(a)
+        t2, p2, l2, al2 = u3_params(b @ a.conj().T)
+        return [("u3", (t, p, l), (0,)), ("u1", (al2,), (1,)), ("cu3", (t2, p2, l2), (1, 0))]
+
+    return (multiplexed(right) + [("ry", (2 * th[0],), (1,)), ("cry", (2 * (th[1] - th[0]),), (0, 1))]
+            + multiplexed(left))
+
+
+def _qasm_pieces(op, qs):
+    """(name, params, qubits) pieces of one instruction in qelib1 gates: standard gates as they
+    are, any other 1- or 2-qubit gate unrolled through its matrix (the reference unrolls the
+    target to basis gates first, approximate_compiler.py:195, so its dumps never meets one)."""
+    if op.name in _QASM_NAMES:
+        return [(op.name, tuple(float(p) for p in op.params), qs)]
+    if len(qs) == 1:
+        t, p, l, _ = u3_params(op_matrix(op))
+        return [("u3", (t, p, l), qs)]
+    if len(qs) == 2:
+        return [(nm, ps, tuple(qs[i] for i in loc)) for nm, ps, loc in unroll_two_qubit(op_matrix(op))]
+    raise ValueError(f"qasm2_dumps: gate {op.name} on {len(qs)} qubits has no OpenQASM 2 form here")
+
+
 def qasm2_dumps(circuit) -> str:
-    """OpenQASM 2.0 text of a circuit (``qiskit.qasm2.dumps`` for the standard-gate circuits the
-    compiler builds; adapt_compiler.py:359-366 keeps one per layer in ``circuit_history``)."""
+    """OpenQASM 2.0 text of a circuit (``qiskit.qasm2.dumps``; adapt_compiler.py:359-366 keeps
+    one per layer in ``circuit_history``).  Gates outside qelib1 are unrolled (_qasm_pieces)."""
     lines = ["OPENQASM 2.0;", 'include "qelib1.inc";', f"qreg q[{circuit.num_qubits}];"]
     for ins in circuit.data:
         op = ins.operation
-        if op.name == "barrier":
+        if op.name in ("barrier", "delay"):
             continue
-        if op.name not in _QASM_NAMES:
-            raise ValueError(f"qasm2_dumps: gate {op.name} has no OpenQASM 2 form here")
-        ps = ""
-        if op.params:
-            ps = "(" + ",".join(repr(float(p)) for p in op.params) + ")"
-        qs = ",".join(f"q[{q}]" for q in qubit_indices(circuit, ins))
-        lines.append(f"{op.name}{ps} {qs};")
+        for name, params, qs in _qasm_pieces(op, qubit_indices(circuit, ins)):
+            ps = "(" + ",".join(repr(float(p)) for p in params) + ")" if params else ""
+            lines.append(f"{name}{ps} " + ",".join(f"q[{q}]" for q in qs) + ";")
     return "\n".join(lines) + "\n"

@@ -960,10 +960,9 @@ int aqc_sv_apply(aqc_sv_t h, const aqc_op_t* ops, int nops) {
   // Planned and launched in batches of 2, 4, 8, ... segments: the host plans the next batch while
   // the GPU runs the previous one (planned whole, the GPU waited out the ~150 us of host fusion of
   // a 20-qubit evaluation).  One pinned staging buffer [headers | phases | gates] with capacity
-  // offsets (phases and fused gates are each at most nops); each batch copies the byte range from
-  // its first header to its last gate -- bytes of later batches in that range are re-copied by
-  // their own batch, later in stream order.  The previous call's copies have finished reading the
-  // staging buffer once plan_ev has completed.
+  // offsets (phases and fused gates are each at most nops); each batch copies only its own new
+  // headers, phases and gates (up to three ranges), so plan traffic is one plan size in total.  The
+  // previous call's copies have finished reading the staging buffer once plan_ev has completed.
   const std::vector<HostSeg> segs = sv_plan_segments(h->n, K, h->reg_tiles, ops, nops);
   const size_t nseg = segs.size();
   std::vector<SegHeader> hdr(nseg);
@@ -1000,21 +999,25 @@ int aqc_sv_apply(aqc_sv_t h, const aqc_op_t* ops, int nops) {
       rc = AQC_ERR_STATE;
       break;
     }
-    std::memcpy(h->h_plan + sizeof(SegHeader) * s0, hdr.data() + s0, sizeof(SegHeader) * (s1 - s0));
-    if (phs.size() > ph_done)
-      std::memcpy(h->h_plan + o_ph + sizeof(PhaseHdr) * ph_done, phs.data() + ph_done,
-                  sizeof(PhaseHdr) * (phs.size() - ph_done));
-    if (gts.size() > g_done)
-      std::memcpy(h->h_plan + o_g + sizeof(SegGate) * g_done, gts.data() + g_done, sizeof(SegGate) * (gts.size() - g_done));
-    const size_t lo = sizeof(SegHeader) * s0, hi = o_g + sizeof(SegGate) * gts.size();
+    // this batch's new bytes only: headers [s0, s1), phases [ph_done, ..), gates [g_done, ..)
+    const size_t rng[3][2] = {{sizeof(SegHeader) * s0, sizeof(SegHeader) * s1},
+                              {o_ph + sizeof(PhaseHdr) * ph_done, o_ph + sizeof(PhaseHdr) * phs.size()},
+                              {o_g + sizeof(SegGate) * g_done, o_g + sizeof(SegGate) * gts.size()}};
+    std::memcpy(h->h_plan + rng[0][0], hdr.data() + s0, rng[0][1] - rng[0][0]);
+    if (rng[1][1] > rng[1][0]) std::memcpy(h->h_plan + rng[1][0], phs.data() + ph_done, rng[1][1] - rng[1][0]);
+    if (rng[2][1] > rng[2][0]) std::memcpy(h->h_plan + rng[2][0], gts.data() + g_done, rng[2][1] - rng[2][0]);
     ph_done = phs.size();
     g_done = gts.size();
-    hipError_t e = hipMemcpyAsync(h->d_plan + lo, h->h_plan + lo, hi - lo, hipMemcpyHostToDevice, h->stream);
-    if (e != hipSuccess) {
-      aqc::set_error(std::string("aqc_sv_apply: plan copy: ") + hipGetErrorString(e));
-      rc = AQC_ERR_HIP;
-      break;
+    for (int r = 0; r < 3 && rc == AQC_OK; ++r) {
+      if (rng[r][1] <= rng[r][0]) continue;
+      hipError_t e = hipMemcpyAsync(h->d_plan + rng[r][0], h->h_plan + rng[r][0], rng[r][1] - rng[r][0],
+                                    hipMemcpyHostToDevice, h->stream);
+      if (e != hipSuccess) {
+        aqc::set_error(std::string("aqc_sv_apply: plan copy: ") + hipGetErrorString(e));
+        rc = AQC_ERR_HIP;
+      }
     }
+    if (rc != AQC_OK) break;
     for (size_t s = s0; s < s1 && rc == AQC_OK; ++s) rc = sv_launch_segment(h, dh + s, dp, dg, nblocks, flops[s]);
     s0 = s1;
   }
