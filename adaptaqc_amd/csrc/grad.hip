@@ -840,9 +840,13 @@ int ensure_gw(aqc_mps_t h) {
 // 0: automatic (grouped chains for batches of states at cap 128, one chain per workgroup for a
 // single state, where the per-step latency of 2 rows beats the 16-row group's), 1: one chain per
 // workgroup, 2: grouped, 3: the segmented single-state sweep (sweep_seg.h) whenever one state is
-// swept (aqc_sweep_set_chain_mode)
+// swept (aqc_sweep_set_chain_mode).  Auto picks the segmented form for one state above cap 64:
+// 0.41 vs 0.92 ms at chi = 128 (50 qubits, 1225 pairs), 0.43 vs 0.41 ms at chi = 64
+// (tools/single_sweep_timing.py).
 int g_chain_mode = 0;
-bool use_segments(int cap, int ns) { return ns == 1 && g_chain_mode == 3 && cap >= 16; }
+bool use_segments(int cap, int ns) {
+  return ns == 1 && cap >= 16 && (g_chain_mode == 3 || (g_chain_mode == 0 && cap > 64));
+}
 bool use_chain8(int cap, int ns) {
   if ((cap != 128 && cap != 64) || g_chain_mode == 1) return false;
   return g_chain_mode == 2 || ns >= 2;

@@ -2,8 +2,8 @@
 // path of the 2 chi = 128 two-site update when the truncation keeps K <= 64 singular triplets.
 //
 // X = theta' (L x C, or its conjugate transpose so that L >= C):
-//   S1  G = X^H X: the 64 x 64 blocks on and above the diagonal on the FP64 matrix cores
-//       (aqc_gemm.h block_cgemm_tile), left in the accumulators
+//   S1  G = X^H X: the 16 x 16 tiles on and above the diagonal on the FP64 matrix cores, three
+//       real products per complex tile (3M), X streamed once through double-buffered LDS chunks
 //   S2  G's upper triangle through the LDS (packed) into registers: thread t holds row t/8,
 //       columns t%8 + 8i (i < 16)
 //   S3  Householder tridiagonalisation G = Q T Q^H (LAPACK zhetd2, lower): two barriers per column
@@ -45,8 +45,9 @@ constexpr int kGramMaxK = 64;
 #define AQC_S5_POLY 1
 #endif
 constexpr double kGramRelFloor = 1e-9;
-// shader-clock ticks of the phases (thread 0), summed over calls: S1, S2+S3, S4, S5, S6, output
-__device__ unsigned long long g_gram_ticks[8];
+// shader-clock ticks of the phases (thread 0), summed over calls: S1, S2+S3, S4, S5, S6, output,
+// S3's column steps, S5's inverse iteration, S3's phase A (column pass + zlarfg + first barrier)
+__device__ unsigned long long g_gram_ticks[10];
 // path counters (thread 0 of each call): [0] calls, [1] taken, [2] declined by shape (K > 64, ...),
 // [3] declined at the eigenvalue floor (lambda_K <= 1e-9 lambda_1 -> the Jacobi runs)
 __device__ unsigned long long g_gram_stats[4];
@@ -165,7 +166,8 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
       t_last = t;
     }
   };
-  // the tridiagonalisation's two per-step phases add up in registers (one atomic each at the end)
+  // the tridiagonalisation's two per-step phases (t_b: A, t_a: B) add up in registers (one atomic
+  // each at the end)
   unsigned long long t_a = 0, t_b = 0;
   auto tick_step = [&](unsigned long long& acc) {
     if (tid == 0) {
@@ -174,50 +176,92 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
       t_last = t;
     }
   };
-  // ---- S1: G = X^H X (256-thread sub-groups on the matrix cores, one 64 x 64 block each; G is
-  // Hermitian, so the block below the diagonal is not computed) ----
+  // ---- S1: G = X^H X on the matrix cores.  Only the 16 x 16 tiles on and above the diagonal
+  // (36 at C = 128), dealt to the 16 waves round-robin (at most 3 each, 9 per SIMD; the 64 x 64
+  // sub-group blocks of round 2 computed 48 tiles on 12 waves, 12 per SIMD).  Each complex tile
+  // is three real products (the 3M form of conj(a + ib)(c + id) = (ac + bd) + i(ad - bc)):
+  // P1 = Xr^T Xr, P2 = Xi^T Xi, P3 = (Xr + Xi)^T (Xr - Xi); Re G = P1 + P2, Im G = P1 - P2 - P3
+  // (absolute error a few eps ||X||^2, the Gram path's eps ||G|| budget).  X streams once through
+  // double-buffered LDS chunks of 8 rows (Xr, Xi, Xr + Xi, Xr - Xi), the next chunk's global
+  // load in flight during the current chunk's MFMAs: 256 KB read per SVD (768 KB before). ----
   const int r0 = tid >> 3, q0 = tid & 7;
   const int r = r0, q = q0;
   cplx g[16];
   {
-    aqc::GemmLds* lds = reinterpret_cast<aqc::GemmLds*>(xbuf);
-    const int sg = tid >> 8, lt = tid & 255;
-    const int bi = (sg >> 1) * 64, bj = (sg & 1) * 64;
-    const bool act = bi < C && bj < C && bi <= bj;
-    aqc::d4_t cr[2][2], ci[2][2];
-    if (!tr) {  // X[k][c] = theta[c * M + k]
-      aqc::block_cgemm_tile<true, true, false>(
-          C, C, L, bi, bj, [&](int i, int k) { return aqc::cconj(th[(size_t)i * M + k]); },
-          [&](int k, int jj) { return th[(size_t)jj * M + k]; }, lds[sg], lt, act, cr, ci);
-    } else {  // X[k][c] = conj(theta[k * M + c])
-      aqc::block_cgemm_tile<false, false, false>(
-          C, C, L, bi, bj, [&](int i, int k) { return th[(size_t)k * M + i]; },
-          [&](int k, int jj) { return aqc::cconj(th[(size_t)k * M + jj]); }, lds[sg], lt, act, cr, ci);
+    constexpr int KC = 8, PITCH = 144;  // rows per chunk; row pitch (doubles): rows k, k + 1 on
+                                        // opposite bank halves for the 16-lane operand reads
+    constexpr int ARR = KC * PITCH, BUF = 4 * ARR;
+    double* sb = reinterpret_cast<double*>(xbuf);
+    const int nt = (C + 15) >> 4, ntile = nt * (nt + 1) / 2;
+    int tI[3], tJ[3];
+    bool tact[3];
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {  // tile t -> (ti <= tj), row-major over the upper triangle
+      int t = wave + 16 * u, ti = 0;
+      tact[u] = t < ntile;
+      while (tact[u] && t >= nt - ti) t -= nt - ti++;
+      tI[u] = ti;
+      tJ[u] = ti + t;
     }
-    // ---- S2: the upper triangle through the LDS (the block barrier at the end of the tile freed
-    // it) into the tridiagonalisation's register layout: thread (r, q) holds row r, columns
-    // q + 8 i.  LDS: block (0, 1) square (row stride 65) then the packed upper triangles of the
-    // diagonal blocks (column-major, entry (a, b), a <= b, at b (b + 1) / 2 + a): 8320 complex ----
+    const int nch = (L + KC - 1) / KC;
+    auto fetch = [&](int ch) {  // this thread's element of chunk ch (zero outside X)
+      const int kk = ch * KC + (tr ? tid >> 7 : tid & 7), c = tr ? tid & 127 : tid >> 3;
+      if (kk >= L || c >= C) return aqc::cmk(0, 0);
+      return tr ? aqc::cconj(th[(size_t)kk * M + c]) : th[(size_t)c * M + kk];
+    };
+    auto stash = [&](int buf, cplx x) {
+      const int o = buf * BUF + (tr ? tid >> 7 : tid & 7) * PITCH + (tr ? tid & 127 : tid >> 3);
+      sb[o] = x.x;
+      sb[o + ARR] = x.y;
+      sb[o + 2 * ARR] = x.x + x.y;
+      sb[o + 3 * ARR] = x.x - x.y;
+    };
+    aqc::d4_t p1[3], p2[3], p3[3];
+#pragma unroll
+    for (int u = 0; u < 3; ++u) p1[u] = p2[u] = p3[u] = aqc::d4_t{0, 0, 0, 0};
+    stash(0, fetch(0));
+    __syncthreads();
+    for (int ch = 0; ch < nch; ++ch) {
+      const bool more = ch + 1 < nch;
+      cplx xn = aqc::cmk(0, 0);
+      if (more) xn = fetch(ch + 1);
+      const double* cb = sb + (ch & 1) * BUF;
+#pragma unroll
+      for (int ks = 0; ks < KC / 4; ++ks) {
+        const int row = (4 * ks + (lane >> 4)) * PITCH + (lane & 15);
+#pragma unroll
+        for (int u = 0; u < 3; ++u) {
+          if (tact[u]) {  // uniform per wave
+            const int oi = row + 16 * tI[u], oj = row + 16 * tJ[u];
+            p1[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(cb[oi], cb[oj], p1[u], 0, 0, 0);
+            p2[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(cb[ARR + oi], cb[ARR + oj], p2[u], 0, 0, 0);
+            p3[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(cb[2 * ARR + oi], cb[3 * ARR + oj], p3[u], 0, 0, 0);
+          }
+        }
+      }
+      if (more) stash((ch + 1) & 1, xn);
+      __syncthreads();
+    }
+    // ---- S2: the upper triangle through the LDS (free after the last chunk's barrier) into the
+    // tridiagonalisation's register layout: thread (r, q) holds row r, columns q + 8 i.  LDS:
+    // block (0, 1) square (row stride 65) then the packed upper triangles of the diagonal 64 x 64
+    // blocks (column-major, entry (a, b), a <= b, at b (b + 1) / 2 + a): 8320 complex ----
     cplx* gsq = xbuf;
-    cplx* gtri = xbuf + 64 * 65;
     auto up_index = [](int a, int b) {  // G[a][b], a <= b
       if (b < 64) return 64 * 65 + b * (b + 1) / 2 + a;
       if (a >= 64) return 64 * 65 + 2080 + (b - 64) * (b - 63) / 2 + (a - 64);
       return a * 65 + (b - 64);
     };
-    (void)gtri;
-    if (act) {
-      const int wv = lt >> 6, ln = lt & 63;
-      const int wr = (wv >> 1) * 32, wc = (wv & 1) * 32, li = ln & 15, lk = ln >> 4;
 #pragma unroll
-      for (int rr = 0; rr < 2; ++rr)
+    for (int u = 0; u < 3; ++u) {
+      if (tact[u]) {  // MFMA C/D layout: row (lane >> 4) + 4 q, column lane & 15
 #pragma unroll
-        for (int cc = 0; cc < 2; ++cc)
-#pragma unroll
-          for (int qq = 0; qq < 4; ++qq) {
-            const int a = bi + wr + 16 * rr + lk + 4 * qq, b = bj + wc + 16 * cc + li;
-            if (a <= b) gsq[up_index(a, b)] = aqc::cmk(cr[rr][cc][qq], ci[rr][cc][qq]);
-          }
+        for (int qq = 0; qq < 4; ++qq) {
+          const int a = 16 * tI[u] + (lane >> 4) + 4 * qq, b = 16 * tJ[u] + (lane & 15);
+          if (a <= b && b < C)
+            gsq[up_index(a, b)] = aqc::cmk(p1[u][qq] + p2[u][qq], p1[u][qq] - p2[u][qq] - p3[u][qq]);
+        }
+      }
     }
     __syncthreads();
 #pragma unroll
@@ -375,6 +419,7 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
       if (q == ((k + 1) & 7)) gk1b[r] = gk1;
     }
     __syncthreads();
+    tick_step(t_b);
     // Phase B: reflector k's p, v and z, one row per thread of waves 0 and 1 (the row's eight
     // partial products summed from the LDS; every row, so finished rows get their zeros)
     int rr = tid;
@@ -427,8 +472,8 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
   }
   __syncthreads();
   if (tid == 0) {
-    atomicAdd(&g_gram_ticks[6], t_a);
-    atomicAdd(&g_gram_ticks[7], t_b);
+    atomicAdd(&g_gram_ticks[6], t_a + t_b);
+    atomicAdd(&g_gram_ticks[8], t_b);
   }
   tick(1);
   // ---- S4: top-K eigenvalues of T by multisection ----

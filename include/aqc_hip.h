@@ -130,8 +130,9 @@ int aqc_mps_set_jacobi_stop(double tiny_t);
    the kept count K = min(2 chi, max_chi) <= 64 and lambda_K > 1e-9 lambda_1, else the register
    Jacobi runs), gram = 0 the register Jacobi only.  debug_max_chi: max_chi of aqc_svd_debug. */
 int aqc_mps_set_svd_path(int gram, int debug_max_chi);
-/* Diagnostics: shader-clock ticks of the Gram path's phases (Gram GEMM, tridiagonalisation,
-   eigenvalues, eigenvectors, back-transformation, output) since the last call (then reset); out[8]. */
+/* Diagnostics: shader-clock ticks of the Gram path's phases since the last call (then reset);
+   out[10]: Gram GEMM, tridiagonalisation, eigenvalues, eigenvectors, back-transformation, output,
+   then the tridiagonalisation's column steps, the inverse iteration, and the steps' phase A. */
 int aqc_svd_gram_ticks(double* out);
 /* Gram-path counters since the last call (then reset): out[0] two-site SVDs that tried the Gram
    path, out[1] taken, out[2] declined by shape (K > 64, 2 chi != 128), out[3] declined at the
@@ -206,8 +207,10 @@ int aqc_pair_grads_batch(aqc_mps_t* psis, int nstates, const double* svec, const
                          int npairs, const double* u0, const double* gens, const double* degs,
                          int ngen, double* out /* nstates*npairs */, int out_is_device);
 /* Chain kernel of the sweep: 0 = automatic (first qubits in groups of 8 advancing together on the
- * matrix cores for batches of states at bond capacity 64 or 128; one chain per workgroup for a single
- * state), 1 = one chain per workgroup, 2 = grouped whenever the capacity allows.  Results are the
+ * matrix cores for batches of states at bond capacity 64 or 128; for a single state the segmented
+ * sweep above capacity 64, else one chain per workgroup), 1 = one chain per workgroup, 2 = grouped
+ * whenever the capacity allows, 3 = the segmented sweep (prefix / suffix products of the site
+ * matrices over ~sqrt(n) segments as batched MFMA GEMMs) for every single state.  Results are the
  * same up to floating-point summation order. */
 int aqc_sweep_set_chain_mode(int mode);
 /* Orders `stream` (a hipStream_t of the current device; NULL = the legacy default stream) after
