@@ -14,8 +14,8 @@
 //      U_a^(q_a+1) = v0_a Q(a + 1), U_a^(q+1) = U_a^(q) F_q, and y_b = w_b P(b - 1)^T -- all in the
 //      same max(m - 2, S - 1) batched launches;
 //   6. T_ab = V_a^(b-a-1) w_b^T or U_a^(q_b) y_b^T, one wave per pair.
-// Every product is a batched complex GEMM on the FP64 matrix cores (k_cgemm16: one wave per 16 x 16
-// output tile), so each step spreads over hundreds of CUs.  ~2.5x the chain form's flops
+// Every product is a batched complex GEMM on the FP64 matrix cores (k_cgemm16: one workgroup per
+// 16 x 16 output tile), so each step spreads over hundreds of CUs.  ~2.5x the chain form's flops
 // (n chi^3 products against n^2 chi^2 vector steps) for ~10x less depth: the single-sweep path,
 // while batches of states keep the grouped chain kernel (k_sweep_chain8), whose throughput is
 // higher.  Reference: gradients.py:81-122 (one sweep per layer, adapt_compiler.py:839-856).

@@ -46,9 +46,12 @@ LAYER_A = 12
 REF_OVERLAPS_PER_LAYER = 113  # Rotoselect evaluations per 4-rotation layer
 FP64_PEAK_TFLOPS = 78.6  # MI355X dense FP64 (vector = matrix), MI355X_MICROARCH.md / SURVEY 8(d)
 HBM_PEAK_GBS = 8000.0
-TRAFFIC_JSON = "r2_traffic.json"
-# executed FP64 work of k_chain per two-site update, from the committed PMC pass (tools/pmc_exec.py)
-EXEC_JSON = "r2_exec_k_chain.json"
+# HBM traffic and executed FP64 work of k_chain per two-site update from the committed PMC passes
+# of this round's code (tools/pmc_bench.sh, tools/pmc_exec.py); the previous round's as fallback
+TRAFFIC_JSON = "r3_traffic.json" if os.path.exists(os.path.join(ROOT, "profiles", "r3_traffic.json")) \
+    else "r2_traffic.json"
+EXEC_JSON = "r3_exec_k_chain.json" if os.path.exists(os.path.join(ROOT, "profiles", "r3_exec_k_chain.json")) \
+    else "r2_exec_k_chain.json"
 
 
 def vidal_from_tensors(A):
@@ -622,8 +625,10 @@ def strong_main(args):
             "single_sweep_pair_sharded": {
                 "ms_whole_sweep": 1e3 * t_one, "ms_slowest_rank": 1e3 * max(t_ranks),
                 "projected_speedup": t_one / (max(t_ranks) + t_coll),
-                "note": "one sweep split by first qubit: every rank still runs the n-step environment "
-                        "chains, which bound the sweep's latency"},
+                "note": "one sweep split by first qubit (segmented form, sweep_seg.h): every rank "
+                        "still runs the segment products and boundary environments, the sweep's "
+                        "dependent depth of ~2 sqrt(n) latency-bound GEMM launches; fewer pairs "
+                        "per rank do not shorten it"},
         })
         print(json.dumps(res))
     if world > 1:

@@ -13,6 +13,9 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/ktrace -o run -
 python3 tools/rocpd_stats.py gpurun_out/ktrace/run_results.db > gpurun_out/kernel_stats.csv
 rm -rf gpurun_out/ktrace
 timeout -k 10 900 bash tools/pmc_bench.sh
+# the full bench line below reads this round's PMC results (copied back from gpurun_out/ locally)
+cp gpurun_out/exec_k_chain.json profiles/${ROUND:-r3}_exec_k_chain.json
+cp gpurun_out/traffic.json profiles/${ROUND:-r3}_traffic.json
 timeout -k 10 400 python3 bench.py --steps 20 --warmup 5 > gpurun_out/bench.json 2> gpurun_out/bench.err
 if [ -z "$SKIP_CONFIGS" ]; then
   timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/kcfg -o run -- python3 tools/configs_bench.py --configs 2,4,5 > gpurun_out/configs.json 2> gpurun_out/configs.err
