@@ -2191,10 +2191,10 @@ int aqc_mps_set_jacobi_tol(double factor) {
 
 int aqc_svd_gram_ticks(double* out) {
   AQC_REQUIRE(out, "aqc_svd_gram_ticks: null argument");
-  unsigned long long t[10];
+  unsigned long long t[12];
   AQC_HIP_CHECK(hipMemcpyFromSymbol(t, HIP_SYMBOL(g_gram_ticks), sizeof(t)));
-  for (int i = 0; i < 10; ++i) out[i] = (double)t[i];
-  unsigned long long z[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  for (int i = 0; i < 12; ++i) out[i] = (double)t[i];
+  unsigned long long z[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   AQC_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_gram_ticks), z, sizeof(z)));
   return AQC_OK;
 }

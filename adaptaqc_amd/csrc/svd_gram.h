@@ -46,8 +46,13 @@ constexpr int kGramMaxK = 64;
 #endif
 constexpr double kGramRelFloor = 1e-9;
 // shader-clock ticks of the phases (thread 0), summed over calls: S1, S2+S3, S4, S5, S6, output,
-// S3's column steps, S5's inverse iteration, S3's phase A (column pass + zlarfg + first barrier)
-__device__ unsigned long long g_gram_ticks[10];
+// S3's column steps, S5's inverse iteration, S3's phase A (column pass + zlarfg + first barrier);
+// with AQC_S3_DIAG: [9] wave 0's reflector scalars done (from the step's start), [10] wave 13's
+// column pass (its own step start to its end)
+__device__ unsigned long long g_gram_ticks[12];
+#ifndef AQC_S3_DIAG
+#define AQC_S3_DIAG 0
+#endif
 // path counters (thread 0 of each call): [0] calls, [1] taken, [2] declined by shape (K > 64, ...),
 // [3] declined at the eigenvalue floor (lambda_K <= 1e-9 lambda_1 -> the Jacobi runs)
 __device__ unsigned long long g_gram_stats[4];
@@ -333,8 +338,10 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
     const cplx pk = pvb[bp * 128 + k];
     s = aqc::cmk(pk.x + 2.0 * a2.x, -pk.y);
   };
+  unsigned long long t_z = 0, t_c = 0, t_c0 = 0;
   for (int k = 0; k < C - 1; ++k) {
     const int b = k & 1, bp = b ^ 1;
+    if (AQC_S3_DIAG && tid == 832) t_c0 = __builtin_amdgcn_s_memtime();
     // q and r laundered through an empty asm each step: otherwise the compiler hoists the 16
     // columns' loop-invariant index / address values out of the k loop and spills them
     int q = q0, r = r0;
@@ -382,6 +389,7 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
         scal[2] = s;
       }
       if (AQC_S3_PRIO) __builtin_amdgcn_s_setprio(0);
+      if (AQC_S3_DIAG && tid == 0) t_z += __builtin_amdgcn_s_memtime() - t_last;
     }
     if (wact) {
       // the own row's reflector k - 1 entries and w_r (the Hermitian rank-2 update needs only
@@ -417,6 +425,7 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
       if (q == (k & 7) && r == k) dS[k] = gk.x;  // G^(k)[k][k]
       accp[q * 128 + r] = acc;
       if (q == ((k + 1) & 7)) gk1b[r] = gk1;
+      if (AQC_S3_DIAG && tid == 832) t_c += __builtin_amdgcn_s_memtime() - t_c0;
     }
     __syncthreads();
     tick_step(t_b);
@@ -474,6 +483,10 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
   if (tid == 0) {
     atomicAdd(&g_gram_ticks[6], t_a + t_b);
     atomicAdd(&g_gram_ticks[8], t_b);
+    if (AQC_S3_DIAG) atomicAdd(&g_gram_ticks[9], t_z);
+  }
+  if (AQC_S3_DIAG && tid == 832) {
+    atomicAdd(&g_gram_ticks[10], t_c);
   }
   tick(1);
   // ---- S4: top-K eigenvalues of T by multisection ----

@@ -131,8 +131,9 @@ int aqc_mps_set_jacobi_stop(double tiny_t);
    Jacobi runs), gram = 0 the register Jacobi only.  debug_max_chi: max_chi of aqc_svd_debug. */
 int aqc_mps_set_svd_path(int gram, int debug_max_chi);
 /* Diagnostics: shader-clock ticks of the Gram path's phases since the last call (then reset);
-   out[10]: Gram GEMM, tridiagonalisation, eigenvalues, eigenvectors, back-transformation, output,
-   then the tridiagonalisation's column steps, the inverse iteration, and the steps' phase A. */
+   out[12]: Gram GEMM, tridiagonalisation, eigenvalues, eigenvectors, back-transformation, output,
+   then the tridiagonalisation's column steps, the inverse iteration, the steps' phase A, and two
+   diagnostics of a build with AQC_S3_DIAG (else 0). */
 int aqc_svd_gram_ticks(double* out);
 /* Gram-path counters since the last call (then reset): out[0] two-site SVDs that tried the Gram
    path, out[1] taken, out[2] declined by shape (K > 64, 2 chi != 128), out[3] declined at the

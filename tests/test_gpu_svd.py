@@ -107,7 +107,7 @@ def _gram_ticks():
     """Phase ticks accumulated since the last call (the call resets them)."""
     from adaptaqc_amd import _lib
 
-    t = np.zeros(10)
+    t = np.zeros(12)
     _lib.check(_lib.lib().aqc_svd_gram_ticks(_lib.ptr(t)))
     return t
 

@@ -61,10 +61,10 @@ def main():
                 sub = np.linalg.norm(Vk @ Vk.conj().T - Vt @ Vt.conj().T, 2)
                 print(f"   kept-subspace distance {sub:.2e}")
             if v == 7:
-                tk = np.zeros(10)
+                tk = np.zeros(12)
                 _lib.check(L.aqc_svd_gram_ticks(_lib.ptr(tk)))
-                print("   gram phase ticks per call (S1 gram, S3 tridiag [C part], S4 eig, S5 vec, S6 back, out, S3 column steps, S5 inverse iteration part, S3 phase A):",
-                      (tk[:9] / reps).astype(int).tolist())
+                print("   gram phase ticks per call (S1 gram, S3 tridiag [C part], S4 eig, S5 vec, S6 back, out, S3 column steps, S5 inverse iteration part, S3 phase A, [diag] zlarfg done, wave-13 column pass):",
+                      (tk[:11] / reps).astype(int).tolist())
             print(f"{kind:12s} variant {v} tiny {tiny}: sweeps {sw.value:2d}  max|sigma - ref|/sigma_1 {err:.2e}  "
                   f"max|V^H V - I| {orth:.2e}", flush=True)
 
