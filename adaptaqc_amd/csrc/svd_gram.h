@@ -53,6 +53,10 @@ __device__ unsigned long long g_gram_ticks[12];
 #ifndef AQC_S3_DIAG
 #define AQC_S3_DIAG 0
 #endif
+// S3: the column pass prefetches column i + 1's LDS operands while column i computes
+#ifndef AQC_S3_PIPE
+#define AQC_S3_PIPE 1
+#endif
 // path counters (thread 0 of each call): [0] calls, [1] taken, [2] declined by shape (K > 64, ...),
 // [3] declined at the eigenvalue floor (lambda_K <= 1e-9 lambda_1 -> the Jacobi runs)
 __device__ unsigned long long g_gram_stats[4];
@@ -89,6 +93,13 @@ __device__ __forceinline__ cplx pick16(const cplx (&g)[16], int i) {
     default:
       return g[15];
   }
+}
+
+// a wave-uniform double moved to SGPRs (readfirstlane of both halves)
+__device__ __forceinline__ double uniform_d(double v) {
+  const int lo = __builtin_amdgcn_readfirstlane(__double2loint(v));
+  const int hi = __builtin_amdgcn_readfirstlane(__double2hiint(v));
+  return __hiloint2double(hi, lo);
 }
 
 // 1 for a negative q (sign bit; q is never -0 here)
@@ -337,6 +348,10 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
     a2 = aqc::cscale(aqc::cmul(tau_prev, kt), -0.5);
     const cplx pk = pvb[bp * 128 + k];
     s = aqc::cmk(pk.x + 2.0 * a2.x, -pk.y);
+    // wave-uniform (LDS broadcasts): held in SGPRs, four VGPRs fewer in the column pass
+    a2.x = uniform_d(a2.x);
+    s.x = uniform_d(s.x);
+    s.y = uniform_d(s.y);
   };
   unsigned long long t_z = 0, t_c = 0, t_c0 = 0;
   for (int k = 0; k < C - 1; ++k) {
@@ -401,6 +416,73 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
       const cplx wr = aqc::cmk(fma(a2r2, vr.x, pr.x), fma(a2r2, vr.y, pr.y));
       const double nvx = -vr.x, nvy = -vr.y, nwx = -wr.x, nwy = -wr.y, nsx = -s.x, nsy = -s.y;
       // one pass: g -= v_r conj(p_c) + w_r conj(v_c) (reflector k - 1), acc += g x_c (reflector k)
+      auto col = [&](int i, const cplx& vc, const cplx& pc, const cplx& zc) {
+        g[i].x = fma(nvx, pc.x, fma(nvy, pc.y, fma(nwx, vc.x, fma(nwy, vc.y, g[i].x))));
+        g[i].y = fma(nvy, pc.x, fma(vr.x, pc.y, fma(nwy, vc.x, fma(wr.x, vc.y, g[i].y))));
+        const cplx xc = aqc::cmk(fma(nsx, vc.x, fma(nsy, -vc.y, zc.x)), fma(nsx, vc.y, fma(nsy, vc.x, zc.y)));
+        acc = aqc::cfma(g[i], xc, acc);
+      };
+#if AQC_S3_PIPE
+      // Rolling prefetch: column i + 1's v, p, z are requested before column i is computed, so
+      // each LDS round trip hides behind one column's 16 FMAs (loaded and consumed one column at a
+      // time, every column waited out a full LDS latency: ~4 K of a step's ~4.6 K ticks).  The
+      // active columns start at group k / 32 (uniform); its first column is loaded up front.
+      const int gi0 = k >> 5;
+#if AQC_S3_PIPE == 1
+      cplx cv, cp, cz;
+      {
+        const int c = q + 32 * gi0;
+        cv = vbb[bp * 128 + c], cp = pvb[bp * 128 + c], cz = zvb[bp * 128 + c];
+      }
+#pragma unroll
+      for (int gi = 0; gi < 4; ++gi) {
+        if (gi >= gi0) {  // uniform; v_c = p_c = z_c = 0 for c < k
+#pragma unroll
+          for (int ii = 0; ii < 4; ++ii) {
+            const int i = 4 * gi + ii;
+            cplx nv = cv, np = cp, nz = cz;
+            if (i + 1 < 16) {
+              const int c = q + 8 * (i + 1);
+              nv = vbb[bp * 128 + c], np = pvb[bp * 128 + c], nz = zvb[bp * 128 + c];
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            col(i, cv, cp, cz);
+            cv = nv, cp = np, cz = nz;
+          }
+        }
+      }
+#else
+      // two named operand sets, columns alternating between them (even i: A, odd i: B)
+      cplx av, ap, az, bv, bp_, bz;
+      auto ldA = [&](int i) {
+        const int c = q + 8 * i;
+        av = vbb[bp * 128 + c], ap = pvb[bp * 128 + c], az = zvb[bp * 128 + c];
+      };
+      auto ldB = [&](int i) {
+        const int c = q + 8 * i;
+        bv = vbb[bp * 128 + c], bp_ = pvb[bp * 128 + c], bz = zvb[bp * 128 + c];
+      };
+      {
+        const int c = q + 32 * gi0;  // first active column: even (A)
+        av = vbb[bp * 128 + c], ap = pvb[bp * 128 + c], az = zvb[bp * 128 + c];
+      }
+#pragma unroll
+      for (int gi = 0; gi < 4; ++gi) {
+        if (gi >= gi0) {  // uniform; v_c = p_c = z_c = 0 for c < k
+#pragma unroll
+          for (int ii = 0; ii < 4; ii += 2) {
+            const int i = 4 * gi + ii;
+            ldB(i + 1);
+            __builtin_amdgcn_sched_barrier(0);
+            col(i, av, ap, az);
+            if (i + 2 < 16) ldA(i + 2);
+            __builtin_amdgcn_sched_barrier(0);
+            col(i + 1, bv, bp_, bz);
+          }
+        }
+      }
+#endif
+#else
 #pragma unroll
       for (int gi = 0; gi < 4; ++gi) {
         if (32 * gi + 31 >= k) {  // uniform; v_c = p_c = z_c = 0 for c < k
@@ -408,16 +490,13 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
           for (int ii = 0; ii < 4; ++ii) {
             const int i = 4 * gi + ii;
             const int c = q + 8 * i;
-            const cplx vc = vbb[bp * 128 + c], pc = pvb[bp * 128 + c], zc = zvb[bp * 128 + c];
-            g[i].x = fma(nvx, pc.x, fma(nvy, pc.y, fma(nwx, vc.x, fma(nwy, vc.y, g[i].x))));
-            g[i].y = fma(nvy, pc.x, fma(vr.x, pc.y, fma(nwy, vc.x, fma(wr.x, vc.y, g[i].y))));
-            const cplx xc = aqc::cmk(fma(nsx, vc.x, fma(nsy, -vc.y, zc.x)), fma(nsx, vc.y, fma(nsy, vc.x, zc.y)));
-            acc = aqc::cfma(g[i], xc, acc);
+            col(i, vbb[bp * 128 + c], pvb[bp * 128 + c], zvb[bp * 128 + c]);
             if (ii == 1) __builtin_amdgcn_sched_barrier(0);  // LDS reads in pairs: no spills
           }
         }
         __builtin_amdgcn_sched_barrier(0);
       }
+#endif
       // the product used x_k = -s (z_k = 0, v_k = 1) where reflector k has 0 (and x_{k+1} = alpha
       // where it has alpha - beta: corrected in phase B): one entry in the lane holding column k
       const cplx gk = pick16(g, k >> 3), gk1 = pick16(g, (k + 1) >> 3);
