@@ -95,6 +95,7 @@ __device__ __forceinline__ void stg(cplx* p, cplx v) {
   q[0] = v.x;
   q[1] = v.y;
 }
+__device__ __forceinline__ void stg(double* p, double v) { *(gdouble*)p = v; }
 
 // Raw buffer loads: a uniform (SGPR) resource + one 32-bit lane offset + a uniform SGPR offset,
 // so a run of loads at uniform strides holds one VGPR of addressing instead of a 64-bit address

@@ -101,9 +101,9 @@ __global__ __launch_bounds__(kT) void k_1q(const OneSiteJob* __restrict__ jobs) 
   for (int e = blockIdx.x * kT + threadIdx.x; e < cl * cr; e += gridDim.x * kT) {
     const int l = e / cr, r = e % cr;
     const size_t o = (size_t)l * cap + r;
-    cplx a0 = j.g[o], a1 = j.g[half + o];
-    j.g[o] = aqc::cfma(j.u[1], a1, aqc::cmul(j.u[0], a0));
-    j.g[half + o] = aqc::cfma(j.u[3], a1, aqc::cmul(j.u[2], a0));
+    const cplx a0 = aqc::ldg(j.g + o), a1 = aqc::ldg(j.g + half + o);  // GLOBAL, not FLAT
+    aqc::stg(j.g + o, aqc::cfma(j.u[1], a1, aqc::cmul(j.u[0], a0)));
+    aqc::stg(j.g + half + o, aqc::cfma(j.u[3], a1, aqc::cmul(j.u[2], a0)));
   }
 }
 
@@ -696,7 +696,7 @@ __device__ __forceinline__ void rank_body(const TwoSiteJob& j) {
   while (P < C) P <<= 1;
   const int tid = fresh_tid();
   for (int i = tid; i < P; i += NT) {
-    sv[i] = i < C ? j.sig[i] : -1.0;
+    sv[i] = i < C ? aqc::ldg(j.sig + i) : -1.0;
     si[i] = i;
   }
   __syncthreads();
@@ -740,14 +740,14 @@ __device__ __forceinline__ void rank_body(const TwoSiteJob& j) {
     for (int i = 0; i < k; ++i) nn += sv[i] * sv[i];
     kk_s = k;
     norm_s = sqrt(nn);
-    j.dims[1] = k;
+    *(__attribute__((address_space(1))) int*)(j.dims + 1) = k;
   }
   __syncthreads();
   const int k = kk_s;
   for (int i = tid; i < k; i += NT) {
-    j.lm[i] = sv[i] / norm_s;
-    j.perm[i] = si[i];
-    j.sig[i + kSigMax] = sv[i];  // sorted copy lives past the raw norms
+    aqc::stg(j.lm + i, sv[i] / norm_s);  // (GLOBAL stores: FLAT ones would also count on LGKM_CNT)
+    *(__attribute__((address_space(1))) int*)(j.perm + i) = si[i];
+    aqc::stg(j.sig + i + kSigMax, sv[i]);  // sorted copy lives past the raw norms
   }
 }
 
@@ -769,18 +769,18 @@ __device__ __forceinline__ void split_copy_body(const TwoSiteJob& j, int start, 
     for (int e = start; e < 2 * chl * k; e += stride) {
       const int kk = e % k, rr = e / k;
       const int s1 = rr / chl, l = rr % chl;
-      const double d = ss[kk] * j.ll[l];
-      const cplx w = j.work[(size_t)j.perm[kk] * L + rr];
-      j.gp[s1 * half + (size_t)l * cap + kk] = d != 0.0 ? aqc::cscale(w, 1.0 / d) : aqc::cmk(0, 0);
+      const double d = aqc::ldg(ss + kk) * aqc::ldg(j.ll + l);
+      const cplx w = aqc::ldg(j.work + (size_t)j.perm[kk] * L + rr);
+      aqc::stg(j.gp + s1 * half + (size_t)l * cap + kk, d != 0.0 ? aqc::cscale(w, 1.0 / d) : aqc::cmk(0, 0));
     }
   } else {
     // Gq'[s2][kk][r] = conj(W[perm kk][s2*chr + r]) / sig_kk / lr[r]
     for (int e = start; e < 2 * chr * k; e += stride) {
       const int cc = e % N, kk = e / N;
       const int s2 = cc / chr, r = cc % chr;
-      const double d = ss[kk] * j.lr[r];
-      const cplx w = aqc::cconj(j.work[(size_t)j.perm[kk] * L + cc]);
-      j.gq[s2 * half + (size_t)kk * cap + r] = d != 0.0 ? aqc::cscale(w, 1.0 / d) : aqc::cmk(0, 0);
+      const double d = aqc::ldg(ss + kk) * aqc::ldg(j.lr + r);
+      const cplx w = aqc::cconj(aqc::ldg(j.work + (size_t)j.perm[kk] * L + cc));
+      aqc::stg(j.gq + s2 * half + (size_t)kk * cap + r, d != 0.0 ? aqc::cscale(w, 1.0 / d) : aqc::cmk(0, 0));
     }
   }
 }
@@ -868,9 +868,9 @@ __device__ __forceinline__ void one_site_body(const OneSiteJob& j, int start, in
   for (int e = start; e < cl * cr; e += stride) {
     const int l = e / cr, r = e % cr;
     const size_t o = (size_t)l * cap + r;
-    cplx a0 = j.g[o], a1 = j.g[half + o];
-    j.g[o] = aqc::cfma(j.u[1], a1, aqc::cmul(j.u[0], a0));
-    j.g[half + o] = aqc::cfma(j.u[3], a1, aqc::cmul(j.u[2], a0));
+    const cplx a0 = aqc::ldg(j.g + o), a1 = aqc::ldg(j.g + half + o);  // GLOBAL, not FLAT
+    aqc::stg(j.g + o, aqc::cfma(j.u[1], a1, aqc::cmul(j.u[0], a0)));
+    aqc::stg(j.g + half + o, aqc::cfma(j.u[3], a1, aqc::cmul(j.u[2], a0)));
   }
 }
 
@@ -922,13 +922,14 @@ __device__ __forceinline__ void chain_theta(const TwoSiteJob& j) {
       {  // A: 8 consecutive m of one row per 8 lanes
         const int row = (e >> 3) & 31, mm = e & 7, l = l0 + row, m = m0 + mm;
         cplx a = aqc::cmk(0, 0);
-        if (active && l < chl && m < chm) a = aqc::cscale(j.gp[s * half + (size_t)l * cap + m], j.ll[l] * j.lm[m]);
+        if (active && l < chl && m < chm)
+          a = aqc::cscale(aqc::ldg(j.gp + s * half + (size_t)l * cap + m), aqc::ldg(j.ll + l) * aqc::ldg(j.lm + m));
         As[s][row][mm] = a;
       }
       {  // B: 32 consecutive r of one row per 32 lanes
         const int mm = (e >> 5) & 7, col = e & 31, m = m0 + mm, r = r0 + col;
         cplx b = aqc::cmk(0, 0);
-        if (active && m < chm && r < chr) b = aqc::cscale(j.gq[s * half + (size_t)m * cap + r], j.lr[r]);
+        if (active && m < chm && r < chr) b = aqc::cscale(aqc::ldg(j.gq + s * half + (size_t)m * cap + r), aqc::ldg(j.lr + r));
         Bs[s][mm][col] = b;
       }
     }
@@ -970,7 +971,7 @@ __device__ __forceinline__ void chain_theta(const TwoSiteJob& j) {
             v = aqc::cfma(j.G[o * 4 + 1], acc[1][i][jj], v);
             v = aqc::cfma(j.G[o * 4 + 2], acc[2][i][jj], v);
             v = aqc::cfma(j.G[o * 4 + 3], acc[3][i][jj], v);
-            j.theta[(size_t)((o & 1) * chr + r) * M + (o >> 1) * chl + l] = v;
+            aqc::stg(j.theta + (size_t)((o & 1) * chr + r) * M + (o >> 1) * chl + l, v);  // GLOBAL, not FLAT
           }
         }
       }
@@ -1014,15 +1015,15 @@ __device__ __forceinline__ void split_gemm_chain(const TwoSiteJob& j, int tid) {
     aqc::block_cgemm_tile<true, true, false>(
         mb, nb, kh, 0, 0,
         [&](int kk, int R) {
-          return klo + R < L ? aqc::cconj(W[(size_t)perm[r0 + kk] * L + klo + R]) : aqc::cmk(0, 0);
+          return klo + R < L ? aqc::cconj(aqc::ldg(W + (size_t)perm[r0 + kk] * L + klo + R)) : aqc::cmk(0, 0);
         },
-        [&](int R, int c) { return klo + R < L ? th[(size_t)(c0 + c) * M + klo + R] : aqc::cmk(0, 0); }, lds, lt,
+        [&](int R, int c) { return klo + R < L ? aqc::ldg(th + (size_t)(c0 + c) * M + klo + R) : aqc::cmk(0, 0); }, lds, lt,
         active, cr, ci);
   } else {
     aqc::block_cgemm_tile<false, true, false>(
         mb, nb, kh, 0, 0,
-        [&](int R, int c) { return klo + c < L ? th[(size_t)(klo + c) * M + r0 + R] : aqc::cmk(0, 0); },
-        [&](int c, int kk) { return klo + c < L ? W[(size_t)perm[c0 + kk] * L + klo + c] : aqc::cmk(0, 0); }, lds,
+        [&](int R, int c) { return klo + c < L ? aqc::ldg(th + (size_t)(klo + c) * M + r0 + R) : aqc::cmk(0, 0); },
+        [&](int c, int kk) { return klo + c < L ? aqc::ldg(W + (size_t)perm[c0 + kk] * L + klo + c) : aqc::cmk(0, 0); }, lds,
         lt, active, cr, ci);
   }
   // (block_cgemm_tile ends on a barrier: the staging LDS is free)
@@ -1052,12 +1053,12 @@ __device__ __forceinline__ void split_gemm_chain(const TwoSiteJob& j, int tid) {
             const cplx v = aqc::cmk(cr[r][c][q] + o.x, ci[r][c][q] + o.y);
             if (!tr) {  // Gq'[s2][kq][r] = Vh / sig^2 / lr[r]
               const int kq = r0 + i, cc = c0 + jj, s2 = cc / chr, rr = cc % chr;
-              const double d = ss[kq] * ss[kq] * j.lr[rr];
-              j.gq[s2 * half + (size_t)kq * cap + rr] = d != 0.0 ? aqc::cscale(v, 1.0 / d) : aqc::cmk(0, 0);
+              const double sk = aqc::ldg(ss + kq), d = sk * sk * aqc::ldg(j.lr + rr);
+              aqc::stg(j.gq + s2 * half + (size_t)kq * cap + rr, d != 0.0 ? aqc::cscale(v, 1.0 / d) : aqc::cmk(0, 0));
             } else {  // Gp'[s1][l][kq] = U / sig^2 / ll[l]
               const int Rr = r0 + i, kq = c0 + jj, s1 = Rr / chl, l = Rr % chl;
-              const double d = ss[kq] * ss[kq] * j.ll[l];
-              j.gp[s1 * half + (size_t)l * cap + kq] = d != 0.0 ? aqc::cscale(v, 1.0 / d) : aqc::cmk(0, 0);
+              const double sk = aqc::ldg(ss + kq), d = sk * sk * aqc::ldg(j.ll + l);
+              aqc::stg(j.gp + s1 * half + (size_t)l * cap + kq, d != 0.0 ? aqc::cscale(v, 1.0 / d) : aqc::cmk(0, 0));
             }
           }
         }

@@ -132,13 +132,38 @@ __device__ __forceinline__ int sturm_count_poly(const double2* de, int C, double
     p0 = __builtin_amdgcn_ldexp(p0, -ex);
     p1 = __builtin_amdgcn_ldexp(p1, -ex);
   };
-  for (; i + 4 <= C; i += 4) {
-    const double2 e0 = de[i], e1 = de[i + 1], e2 = de[i + 2], e3 = de[i + 3];
-    step(e0);
-    step(e1);
-    step(e2);
-    step(e3);
+  // the next four rows' (d, e^2) are read while the current four run (read and used four at a
+  // time, every group of rows waited out an LDS round trip: about half of the pass).  Two named
+  // register sets alternate (a rotating copy would wait for its reads at the loop's end); the
+  // index is clamped at the end instead of a branch (the extra reads are unused).
+  auto rd4 = [&](int i0, double2& r0, double2& r1, double2& r2, double2& r3) {
+    r0 = de[min(i0, C - 1)], r1 = de[min(i0 + 1, C - 1)], r2 = de[min(i0 + 2, C - 1)], r3 = de[min(i0 + 3, C - 1)];
+  };
+  double2 a0, a1, a2, a3, b0, b1, b2, b3;
+  rd4(1, a0, a1, a2, a3);
+  for (; i + 8 <= C; i += 8) {
+    rd4(i + 4, b0, b1, b2, b3);
+    __builtin_amdgcn_sched_barrier(0);
+    step(a0);
+    step(a1);
+    step(a2);
+    step(a3);
     rescale();
+    rd4(i + 8, a0, a1, a2, a3);
+    __builtin_amdgcn_sched_barrier(0);
+    step(b0);
+    step(b1);
+    step(b2);
+    step(b3);
+    rescale();
+  }
+  if (i + 4 <= C) {
+    step(a0);
+    step(a1);
+    step(a2);
+    step(a3);
+    rescale();
+    i += 4;
   }
   for (; i < C; ++i) step(de[i]);
   return -neg;
@@ -223,7 +248,7 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
     auto fetch = [&](int ch) {  // this thread's element of chunk ch (zero outside X)
       const int kk = ch * KC + (tr ? tid >> 7 : tid & 7), c = tr ? tid & 127 : tid >> 3;
       if (kk >= L || c >= C) return aqc::cmk(0, 0);
-      return tr ? aqc::cconj(th[(size_t)kk * M + c]) : th[(size_t)c * M + kk];
+      return tr ? aqc::cconj(aqc::ldg(th + (size_t)kk * M + c)) : aqc::ldg(th + (size_t)c * M + kk);
     };
     auto stash = [&](int buf, cplx x) {
       const int o = buf * BUF + (tr ? tid >> 7 : tid & 7) * PITCH + (tr ? tid & 127 : tid >> 3);
@@ -528,7 +553,7 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
       if (!below) v = aqc::cmk(rr == k + 1 ? 1.0 : 0.0, 0.0);
       pvb[b * 128 + rr] = p;
       vbb[b * 128 + rr] = v;
-      if (rowact) hh[(size_t)k * (2 * C - k - 1) / 2 + (rr - k - 1)] = v;
+      if (rowact) aqc::stg(hh + (size_t)k * (2 * C - k - 1) / 2 + (rr - k - 1), v);  // GLOBAL, not FLAT
       // this wave's share of p^H v for the next column's a2
       const double ktx = wave_sum_dpp(fma(p.x, v.x, p.y * v.y)), kty = wave_sum_dpp(fma(p.x, v.y, -p.y * v.x));
       if (lane == 0) ktp[wave] = aqc::cmk(ktx, kty);
@@ -1002,12 +1027,12 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int row = 32 * mg + 16 * t + lk + 4 * q;
-          if (row < C) j.work[(size_t)col * C + row] = aqc::cmk(vre[t][q] * sg, vim[t][q] * sg);
+          if (row < C) aqc::stg(j.work + (size_t)col * C + row, aqc::cmk(vre[t][q] * sg, vim[t][q] * sg));
         }
       }
     }
   }
-  for (int c = tid; c < C; c += 1024) j.sig[c] = c < K ? sqrt(s_sig2[c]) : 0.0;
+  for (int c = tid; c < C; c += 1024) aqc::stg(j.sig + c, c < K ? sqrt(s_sig2[c]) : 0.0);
   if (tid == 0) {
     atomicMax(&j.flags[2], 1);
     atomicAdd(&g_gram_stats[1], 1ull);
