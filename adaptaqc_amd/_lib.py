@@ -34,7 +34,7 @@ EXPORTS = (
     "aqc_sv_transition", "aqc_mps_product_fit", "aqc_mps_set_svd_path", "aqc_svd_gram_ticks", "aqc_bj_ticks",
     "aqc_sweep_set_chain_mode", "aqc_mps_set_jacobi_noise", "aqc_stream_join", "aqc_stream_wait", "aqc_svd_gram_stats",
     "aqc_comm_unique_id", "aqc_comm_init", "aqc_comm_destroy", "aqc_comm_rank", "aqc_allgather_f64",
-    "aqc_allgather_f64_host", "aqc_allreduce_max_f64",
+    "aqc_allgather_f64_host", "aqc_allreduce_max_f64", "aqc_svd_gram_big_stats", "aqc_svd_gram_big_ticks",
 )
 
 
@@ -120,6 +120,8 @@ _SIGS = {
     "aqc_allgather_f64_host": ([_P, _P, _P, ctypes.c_size_t], _I),
     "aqc_allreduce_max_f64": ([_P, _DP], _I),
     "aqc_mps_set_jacobi_noise": ([_D], _I),
+    "aqc_svd_gram_big_stats": ([_P], _I),
+    "aqc_svd_gram_big_ticks": ([_P], _I),
 }
 
 
@@ -216,3 +218,13 @@ def gram_stats():
     check(load().aqc_svd_gram_stats(ptr(out)))
     return {"calls": int(out[0]), "taken": int(out[1]), "declined_shape": int(out[2]),
             "declined_floor": int(out[3])}
+
+
+def gram_big_stats():
+    """Counters of the multi-workgroup Gram path for 2 chi > 128 since the last call
+    (aqc_svd_gram_big_stats): calls, taken, declined, declined at the eigenvalue floor, exchange
+    timeouts."""
+    out = np.zeros(5)
+    check(load().aqc_svd_gram_big_stats(ptr(out)))
+    return {"calls": int(out[0]), "taken": int(out[1]), "declined": int(out[2]),
+            "declined_floor": int(out[3]), "timeouts": int(out[4])}

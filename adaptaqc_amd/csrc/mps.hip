@@ -1893,9 +1893,9 @@ int run_waves(aqc_mps_t* hs, int ns, std::vector<std::vector<DevOp>>& lists) {
           else
             launch_jacobi_reg128(nc, st, jc);
         } else {
-          // 2 chi > 128: multi-workgroup block Jacobi (bjacobi.hip), W in HBM / L2, sized by
-          // the class
-          const int brc = aqc::block_jacobi(jc, nc, side / 2, st);
+          // 2 chi > 128: the multi-workgroup Gram path (gram_big.hip), the block Jacobi
+          // (bjacobi.hip) for the jobs it declines; sized by the class
+          const int brc = aqc::big_svd(two.data() + cr.first, jc, nc, side, side / 2, st);
           if (brc != AQC_OK) return brc;
         }
       }

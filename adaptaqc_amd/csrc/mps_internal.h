@@ -156,6 +156,12 @@ __device__ __forceinline__ void jacobi_te(double al, double be, double g2, doubl
 // third on) to stop when every decomposition has converged.
 int block_jacobi(const TwoSiteJob* jobs, int nj, int cap_max, hipStream_t st);
 
+// Two-site SVDs at 2 chi = side in (128, 1024] (gram_big.hip): the multi-workgroup Gram path
+// (G = X^H X, tridiagonalisation over several workgroups per job, inverse iteration, V = Q Z;
+// output contract qr = 1, written into the device job), the block Jacobi for the jobs it declines.
+// hjobs: host copies of the device jobs (qr = 0).  Synchronises the host once.
+int big_svd(const TwoSiteJob* hjobs, const TwoSiteJob* jobs, int nj, int side, int cap_max, hipStream_t st);
+
 hipStream_t mps_stream();
 
 }  // namespace aqc

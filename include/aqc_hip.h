@@ -142,6 +142,19 @@ int aqc_svd_gram_stats(double* out);
 /* Block Jacobi pair visits (2 chi > 128), shader-clock ticks summed over workgroups since the
  * last call: out[0] Gram, out[1] inner Jacobi sweep, out[2] A V, out[3] visits.  Resets. */
 int aqc_bj_ticks(double* out);
+/* Two-site SVDs at 2 chi in (128, 1024] (gram_big.hip; replaces the block Jacobi of the reference's
+   Aer MPS truncation for chi = 128 ... 512, aer_mps_backend.py:76-78 via qiskit-aer's MPS two-site
+   SVD): counters since the last call (then reset): out[0] jobs that entered the multi-workgroup
+   Gram path, out[1] taken, out[2] declined (Gram path off for the job, or 2 chi < 4), out[3]
+   declined at the eigenvalue floor (lambda_K <= 1e-9 lambda_1), out[4] exchange timeouts (the
+   tridiagonalisation's workgroups did not all run together); declined jobs ran the block Jacobi.
+   The environment variable AQC_BIG_GRAM=0 selects the block Jacobi alone. */
+int aqc_svd_gram_big_stats(double* out);
+/* Diagnostics of the same path: shader-clock ticks summed over calls (then reset): out[0..4] the
+   tridiagonalisation's per-column phases on job 0's first workgroup (register pass + row sums,
+   publish, counter wait, reads + p^H v, w / new row / next reflector), out[5] k_gb_eig up to the
+   eigenvalues, out[6] k_gb_back (job 0, first block), out[7] k_gb_eig in all (job 0). */
+int aqc_svd_gram_big_ticks(double* out);
 /* Batched applies of >= 32 states at 2*chi = 128 run every state's whole op list in
    one fused workgroup (theta, Jacobi, truncation, split per update: no grid-wide step between
    updates); on = 0 selects the lock-step launches per update.  Default on. */

@@ -1,0 +1,131 @@
+"""Multi-workgroup Gram-path SVD for 2 chi > 128 (gram_big.hip) against the oracle and against the
+block Jacobi it replaces.
+
+The tridiagonalisation spreads each job's G over several workgroups that exchange one vector per
+column through global memory; these tests check the decompositions it feeds into the two-site
+update (bond dims exact, Schmidt values 1e-9, fidelity 1e-6 -- BASELINE.json's truncated-MPS bar),
+that the path was actually taken (its counters), that the block Jacobi (the Gram path switched
+off) gives the same state, and that a rank-deficient theta declines to the block Jacobi.
+"""
+import numpy as np
+import pytest
+
+from bench import random_vidal_mps  # noqa: E402
+from conftest import to_circuit
+from oracle import mps as M
+
+pytestmark = pytest.mark.gpu
+
+
+def _gates(n, rng, pairs):
+    ops = []
+    for a, b in pairs:
+        for q in (a, b):
+            ops.append(("ry", (q,), (rng.uniform(-np.pi, np.pi),)))
+            ops.append(("rz", (q,), (rng.uniform(-np.pi, np.pi),)))
+        ops.append(("cx", (a, b), ()))
+    return ops
+
+
+def _run(n, chi, ops, seed, gram=1):
+    from adaptaqc_amd import _lib
+    from adaptaqc_amd.circuit import device_ops
+    from adaptaqc_amd.device import DeviceMPS
+
+    _lib.check(_lib.load().aqc_mps_set_svd_path(gram, 64))
+    try:
+        _lib.gram_big_stats()
+        d = DeviceMPS(n, chi, 1e-16, chi)
+        d.load_aer(random_vidal_mps(n, chi, seed))
+        d.apply(device_ops(to_circuit(n, ops)))
+        stats = _lib.gram_big_stats()
+    finally:
+        _lib.check(_lib.load().aqc_mps_set_svd_path(1, 64))
+    return d, stats
+
+
+def _vs_oracle(d, n, chi, ops, seed):
+    ref = M.run_circuit(n, ops, 1e-16, chi, mps=M.MPS.from_aer(random_vidal_mps(n, chi, seed)))
+    pre_ref = ref.preprocessed()
+    np.testing.assert_array_equal(d.dims(), [1] + [x.shape[2] for x in pre_ref])
+    pre = d.preprocessed()
+    fid = abs(M.mps_dot(pre_ref, pre)) / np.sqrt(abs(M.mps_dot(pre, pre)) * abs(M.mps_dot(pre_ref, pre_ref)))
+    assert abs(fid - 1.0) < 1e-6, fid
+    return ref
+
+
+@pytest.mark.parametrize("n,chi", [(18, 128), (20, 256)])
+def test_gram_big_taken_and_matches_oracle(n, chi):
+    """Adjacent truncating updates at the cap (2 chi = 256 / 512): every one takes the Gram path
+    (no floor declines, no exchange timeouts) and the state matches the oracle."""
+    rng = np.random.default_rng(chi + 3)
+    m = n // 2
+    ops = _gates(n, rng, [(m - 1, m), (m, m + 1), (m - 2, m - 1)])
+    d, st = _run(n, chi, ops, seed=chi + 4)
+    assert st["calls"] == 3 and st["taken"] == 3 and st["timeouts"] == 0, st
+    ref = _vs_oracle(d, n, chi, ops, chi + 4)
+    _, lam = d.to_aer()
+    for b in (m - 1, m, m + 1):
+        np.testing.assert_allclose(lam[b - 1], ref.l[b - 1], atol=1e-9, err_msg=f"bond {b}")
+
+
+def test_gram_big_equals_block_jacobi():
+    """One wave of 8 disjoint updates at 2 chi = 512 (config 5's state) through the Gram path and
+    through the block Jacobi (Gram path off): same bond dimensions, Schmidt values within 1e-9,
+    states within 1e-6."""
+    n, chi = 100, 256
+    rng = np.random.default_rng(11)
+    ops = _gates(n, rng, [(a, a + 1) for a in range(40, 56, 2)])
+    g, st = _run(n, chi, ops, seed=5, gram=1)
+    assert st["taken"] == 8, st
+    b, st0 = _run(n, chi, ops, seed=5, gram=0)
+    assert st0["taken"] == 0, st0
+    np.testing.assert_array_equal(g.dims(), b.dims())
+    _, lg = g.to_aer()
+    _, lb = b.to_aer()
+    for x, y in zip(lg, lb):
+        np.testing.assert_allclose(x, y, atol=1e-9)
+    pg, pb = g.preprocessed(), b.preprocessed()
+    assert abs(abs(M.mps_dot(pg, pb)) / np.sqrt(abs(M.mps_dot(pg, pg)) * abs(M.mps_dot(pb, pb))) - 1.0) < 1e-6
+
+
+def test_gram_big_rank_deficient_declines_to_block_jacobi():
+    """A 2 chi = 256 update whose middle bond keeps only 4 non-zero Schmidt values (the rest set to
+    zero): theta' has rank <= 16, lambda_K sits at the noise floor, the Gram path declines and the
+    block Jacobi's result matches the oracle on the same input."""
+    from adaptaqc_amd import _lib
+    from adaptaqc_amd.circuit import device_ops
+    from adaptaqc_amd.device import DeviceMPS
+
+    n, chi = 16, 128
+    gam, lam = random_vidal_mps(n, chi, 21)
+    lam = [np.array(x, dtype=float) for x in lam]
+    b = 7  # the bond between sites 7 and 8
+    lam[b][4:] = 0.0
+    lam[b] /= np.linalg.norm(lam[b])
+    aer = (gam, lam)
+    rng = np.random.default_rng(2)
+    ops = _gates(n, rng, [(7, 8)])
+    _lib.gram_big_stats()
+    d = DeviceMPS(n, chi, 1e-16, None)
+    d.load_aer(aer)
+    d.apply(device_ops(to_circuit(n, ops)))
+    st = _lib.gram_big_stats()
+    assert st["declined_floor"] == 1 and st["taken"] == 0 and st["timeouts"] == 0, st
+    ref = M.run_circuit(n, ops, 1e-16, None, mps=M.MPS.from_aer(aer))
+    pre_ref = ref.preprocessed()
+    np.testing.assert_array_equal(d.dims(), [1] + [x.shape[2] for x in pre_ref])
+    pre = d.preprocessed()
+    fid = abs(M.mps_dot(pre_ref, pre)) / np.sqrt(abs(M.mps_dot(pre, pre)) * abs(M.mps_dot(pre_ref, pre_ref)))
+    assert abs(fid - 1.0) < 1e-6, fid
+
+
+def test_gram_big_config5_wave():
+    """Config 5's wave (100 qubits, chi = 256, 24 disjoint updates at the cap): all 24 on the Gram
+    path in one call."""
+    n, chi = 100, 256
+    rng = np.random.default_rng(5)
+    ops = _gates(n, rng, [(a, a + 1) for a in range(26, 74, 2)])
+    d, st = _run(n, chi, ops, seed=5)
+    assert st["taken"] == 24 and st["timeouts"] == 0, st
+    _vs_oracle(d, n, chi, ops, 5)

@@ -165,6 +165,9 @@ def config5(gates, reps):
     work.copy_from(base)
     work.apply(ops)
     work.dims()
+    _lib.gram_big_stats()  # reset
+    gbt = np.zeros(8)
+    _lib.check(_lib.lib().aqc_svd_gram_big_ticks(_lib.ptr(gbt)))  # reset
     _lib.timing_reset()
     _lib.timing_enable(True)
     t0 = time.perf_counter()
@@ -174,6 +177,13 @@ def config5(gates, reps):
         work.dims()  # synchronises
     el = time.perf_counter() - t0
     _lib.timing_enable(False)
+    gbs = _lib.gram_big_stats()
+    _lib.check(_lib.lib().aqc_svd_gram_big_ticks(_lib.ptr(gbt)))
+    if gbs["taken"]:
+        ncol = reps * (2 * chi - 1)  # job 0's columns over the timed calls
+        gbs["ticks_per_column"] = {k: gbt[i] / ncol for i, k in enumerate(
+            ("pass", "publish", "wait", "reads_pv", "w_row_reflector"))}
+        gbs["ticks_per_call"] = {"eigenvalues": gbt[5] / reps, "back": gbt[6] / reps, "inverse_iteration": gbt[7] / reps}
     import ctypes
     sw = ctypes.c_int()
     _lib.check(_lib.lib().aqc_mps_jacobi_stats(work.h, ctypes.byref(sw)))
@@ -194,6 +204,7 @@ def config5(gates, reps):
             "nominal_tflops": nom / (per_gate_ms * 1e-3) / 1e12, "dtype": "c128", "data": "synthetic random Vidal MPS",
             "config": {"workload": "config5: (rz ry rz)x(rz ry rz).CX on disjoint middle pairs, max_chi=256",
                        "n_qubits": n, "chi": chi, "gates": gates, "max_jacobi_sweeps": sw.value,
+                       "svd_path": "gram_big" if gbs["taken"] else "block_jacobi", "gram_big_stats": gbs,
                        "dims_after": [int(x) for x in work.dims()[mid:mid + 2 * gates + 1]]},
             "breakdown_ms_per_gate": {"svd": svd["ms"] / (reps * gates), "theta": th["ms"] / (reps * gates),
                                       "split": sp["ms"] / (reps * gates)},
