@@ -21,12 +21,15 @@
 //                 workgroup forms w = p - tau/2 (p^H v) v and, from the old row k + 1, the new row
 //                 k + 1 = old - conj(w) - w_{k+1} conj(v): the next column needs no second hand-off.
 //                 One exchange per column; spins bounded (100 ms, then the job declines).
-//   k_gb_eig      one workgroup per job: the top K eigenvalues of T by multisection with the
-//                 polynomial Sturm count, inverse iteration (LDL^T of T - lambda I, three solves,
-//                 vectors in a per-job scratch), Gram-Schmidt inside clusters, sigma^2 = z^T T z.
-//                 Declines (status 1) unless lambda_K > 1e-9 lambda_1, as the 2 chi = 128 path does.
-//   k_gb_back     V = Q Z, one wave per eigenvector: the reflectors, last first, staged through the
-//                 LDS eight at a time; output W = V Sigma, sig, qr = 1 -- the contract of the
+//   k_gb_eig      the top K eigenvalues of T by multisection with the polynomial Sturm count, 64
+//                 per workgroup;
+//   k_gb_inv      inverse iteration (LDL^T of T - lambda I, three solves, one lane per vector,
+//                 vectors in a per-job scratch), sigma^2 = z^T T z; declines (status 2) unless
+//                 lambda_K > 1e-9 lambda_1, as the 2 chi = 128 path does;
+//   k_gb_gs       Gram-Schmidt inside clusters of close eigenvalues.
+//   k_gb_tfac     compact WY factors T of the reflectors in blocks of 16 (LAPACK zlarft).
+//   k_gb_back     V = Q Z on the matrix cores, 16 columns per workgroup, blocks of 16 reflectors
+//                 from the last (V -= Y T Y^H V); output W = V Sigma, sig, qr = 1 -- the contract of the
 //                 2 chi = 128 Gram path (work column c = right singular vector c of X times
 //                 sigma_c), so k_rank / k_split_* run unchanged.
 // Jobs that decline (floor, timeout, gram disabled) run the block Jacobi afterwards (the host reads
@@ -43,8 +46,9 @@ namespace aqc {
 __device__ unsigned long long g_gbig_stats[5];
 // shader-clock ticks of job 0's first workgroup (thread 0), summed over calls: tridiagonalisation
 // phases [0] pass + row sums, [1] publish (stores, vmcnt, barrier), [2] counter wait, [3] reads + p^H v,
-// [4] w, new row, next reflector; [5] k_gb_eig, [6] k_gb_back (job 0, block 0)
-__device__ unsigned long long g_gbig_ticks[8];
+// [4] w, new row, partial norms; [5] k_gb_eig (job 0, block 0), [6] k_gb_back (job 0, block 0), [7] k_gb_inv (job 0,
+// lane 0), [8] the next reflector's zlarfg
+__device__ unsigned long long g_gbig_ticks[9];
 
 namespace {
 
@@ -69,6 +73,8 @@ __device__ __forceinline__ cplx ld_sc1(const cplx* p) {
 
 struct GBArgs {
   cplx* G;         // per job CT x CT: G, then the reflectors (row k = v_k at columns > k)
+  cplx* tfac;      // per job (CT / 16) x 16 x 16: compact WY factors T of the reflector blocks
+  cplx* yc;        // per job CT x CT: the reflectors column-major (v_k[row] at row * CT + k)
   double* d;       // per job CT
   double* e;       // per job CT
   cplx* tau;       // per job CT
@@ -108,7 +114,7 @@ __device__ __forceinline__ void job_dims(const TwoSiteJob& j, int& M, int& L, in
 }
 
 // ---- G = X^H X ------------------------------------------------------------------------------
-// grid ((CT / 64)^2, nj), 256 threads.  Entries outside C x C are zero.
+// grid (nbt (nbt + 1) / 2, nj) with nbt = CT / 64, 256 threads.  Entries outside C x C are zero.
 template <int CT>
 __global__ __launch_bounds__(256) void k_gb_gram(const TwoSiteJob* __restrict__ jobs, GBArgs a) {
   const int jb = blockIdx.y;
@@ -123,13 +129,20 @@ __global__ __launch_bounds__(256) void k_gb_gram(const TwoSiteJob* __restrict__ 
     if (st) atomicAdd(&g_gbig_stats[2], 1ull);
   }
   if (!j.gram || C < 4) return;
+  // blocks on and above the diagonal (bi <= bj), the one below mirrored: G is Hermitian
   constexpr int nbt = CT / 64;
-  const int bi = (blockIdx.x / nbt) * 64, bj = (blockIdx.x % nbt) * 64;
+  int bi = 0, rem = blockIdx.x;
+  while (rem >= nbt - bi) rem -= nbt - bi, ++bi;
+  const int bj = (bi + rem) * 64;
+  bi *= 64;
   cplx* G = a.G + (size_t)jb * CT * CT;
   const cplx* th = j.theta;
   __shared__ GemmLds lds;
   const int m = bi < C ? min(64, C - bi) : 0, n = bj < C ? min(64, C - bj) : 0;
-  auto store = [&](int i, int jj, cplx v) { stg(G + (size_t)(bi + i) * CT + bj + jj, v); };
+  auto store = [&](int i, int jj, cplx v) {
+    stg(G + (size_t)(bi + i) * CT + bj + jj, v);
+    if (bi != bj) stg(G + (size_t)(bj + jj) * CT + bi + i, cconj(v));
+  };
   if (m > 0 && n > 0) {
     if (!tr) {  // X[R][c] = theta[c * M + R]: contiguous along the contraction
       block_cgemm<true, true>(
@@ -143,121 +156,207 @@ __global__ __launch_bounds__(256) void k_gb_gram(const TwoSiteJob* __restrict__ 
   }
   for (int e = threadIdx.x; e < 4096; e += 256) {
     const int i = e >> 6, jj = e & 63;
-    if (i >= m || jj >= n) stg(G + (size_t)(bi + i) * CT + bj + jj, cmk(0, 0));
+    if (i >= m || jj >= n) {
+      stg(G + (size_t)(bi + i) * CT + bj + jj, cmk(0, 0));
+      stg(G + (size_t)(bj + jj) * CT + bi + i, cmk(0, 0));
+    }
   }
 }
 
-// zlarfg on (alpha, x) with ||x||^2 = xn2: beta (real), tau, scale = 1 / (alpha - beta)
-__device__ __forceinline__ void zlarfg_s(cplx alpha, double xn2, cplx& tau, double& beta, cplx& scale) {
+__device__ __forceinline__ double rcp_nr2(double x) {
+  double r = __builtin_amdgcn_rcp(x);
+  r = r * fma(-x, r, 2.0);
+  r = r * fma(-x, r, 2.0);
+  return r;
+}
+
+// ---- tridiagonalisation over P workgroups per job -----------------------------------------------
+// Column exchange: sc1 stores, s_waitcnt vmcnt(0), a barrier and one counter add per workgroup; the
+// consumers poll the counter with one lane (the MI355X guide's "Valid forms" row 1).  (The guide's
+// 8-byte {data, tag} granules -- every consumer thread polling its values' tags, no store
+// acknowledgement or counter -- measured slower at C = 512: 14.6 K ticks per column waiting against
+// 5.4 K, the 16 K polling threads per job crowd the fabric.)
+
+// sum over aligned groups of N (16, 32, 64) lanes, result in every lane of the group; VALU only
+// (DPP row sums, then v_permlane16_swap / v_permlane32_swap: the partner row's value without the
+// LDS crossbar)
+template <int N>
+__device__ __forceinline__ double lane_sum(double v) {
+  v = row_sum16(v);
+  if constexpr (N >= 32) {
+    const auto lo = __builtin_amdgcn_permlane16_swap(__double2loint(v), __double2loint(v), false, false);
+    const auto hi = __builtin_amdgcn_permlane16_swap(__double2hiint(v), __double2hiint(v), false, false);
+    v = __hiloint2double(hi[0], lo[0]) + __hiloint2double(hi[1], lo[1]);
+  }
+  if constexpr (N >= 64) {
+    const auto lo = __builtin_amdgcn_permlane32_swap(__double2loint(v), __double2loint(v), false, false);
+    const auto hi = __builtin_amdgcn_permlane32_swap(__double2hiint(v), __double2hiint(v), false, false);
+    v = __hiloint2double(hi[0], lo[0]) + __hiloint2double(hi[1], lo[1]);
+  }
+  return v;
+}
+
+// zlarfg with the divisions as reciprocals (rcp + two Newton steps: full precision)
+__device__ __forceinline__ void zlarfg_f(cplx alpha, double xn2, cplx& tau, double& beta, cplx& scale) {
   if (xn2 == 0.0 && alpha.y == 0.0) {
     tau = cmk(0, 0);
     beta = alpha.x;
     scale = cmk(0, 0);
     return;
   }
-  const double nrm = sqrt(alpha.x * alpha.x + alpha.y * alpha.y + xn2);
+  const double nrm = sqrt(fma(alpha.x, alpha.x, fma(alpha.y, alpha.y, xn2)));
   beta = alpha.x >= 0.0 ? -nrm : nrm;
-  tau = cmk((beta - alpha.x) / beta, -alpha.y / beta);
+  const double rb = rcp_nr2(beta);
+  tau = cmk((beta - alpha.x) * rb, -alpha.y * rb);
   const cplx den = cmk(alpha.x - beta, alpha.y);
-  const double id = 1.0 / cnorm2(den);
+  const double id = rcp_nr2(cnorm2(den));
   scale = cmk(den.x * id, -den.y * id);
 }
 
-// ---- tridiagonalisation over P workgroups per job -----------------------------------------------
-// grid (P * njobs_in_round), 1024 threads.  Thread t: local row t / TPR (global r = lr P + g),
-// columns q + TPR i (q = t % TPR, i < 16).  Per column k: one pass over the registers applies the
-// deferred rank-2 update of reflector k - 1 and forms (G v_k)_r; the exchange; p^H v; w_k and the new
-// row k + 1; reflector k + 1's zlarfg.  Five workgroup barriers per column.
-template <int CT>
+// grid (P * njobs_in_round), 1024 threads.  Thread t: row group t / TPG of RPL rows (local rows
+// RPL * group + u, global r = local P + g), columns q + TPG i (q = t % TPG, i < CPL).  Per column k:
+//   pass      the deferred rank-2 update G -= v w^H + w v^H of reflector k - 1 and s = (G v_k)_r in
+//             one sweep over the registers; column blocks and row groups at or above k are dead and
+//             skipped
+//   exchange  p_r = tau_k s_r (and the owner's row k + 1 as it was before this update) out, all p
+//             and that row in; d_k, e_k, tau_k and this workgroup's slice of v_k go to the scratch
+//             here, where their store latency hides behind the wait
+//   tail      p^H v (one workgroup reduction), w_k = p + a2 v, the new row k + 1 = old - conj(w) -
+//             w_{k+1} conj(v), its norm below the subdiagonal (a second reduction); wave 0 alone
+//             forms reflector k + 1 (zlarfg's scalars and v into the LDS; in every wave the
+//             redundant scalar chain cost 4x its issue)
+template <int CT, int RPL>
 __global__ __launch_bounds__(1024) void k_gb_tridiag(const TwoSiteJob* __restrict__ jobs, GBArgs a, int job0) {
-  constexpr int R = 16384 / CT, TPR = CT / 16, P = CT / R;
+  constexpr int CPL = 16 / RPL, TPG = CT / CPL;
+  constexpr int R = RPL * (1024 / TPG), P = CT / R;
+  static_assert(TPG <= 64 && TPG >= 16, "row group inside one wave");
   const int jb = job0 + (int)blockIdx.x / P, g = (int)blockIdx.x % P;
   if (*(const gi32*)(a.status + jb) != 0) return;  // uniform over the job's workgroups
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int lr = tid / TPR, q = tid % TPR, r = lr * P + g;
-  const bool tick = jb == 0 && g == 0 && tid == 0;
+  const int grp = tid / TPG, q = tid % TPG;
+  int rr[RPL];
+#pragma unroll
+  for (int u = 0; u < RPL; ++u) rr[u] = (grp * RPL + u) * P + g;
+  // (phase ticks on the last wave: its rows stay active to the end)
+  const bool tick = jb == 0 && g == 0 && tid == 960;
   cplx* G = a.G + (size_t)jb * CT * CT;
-  cplx* xch = a.xch + (size_t)jb * 4 * CT;
-  unsigned* cnt = a.cnt + (size_t)jb * 32;
   double* dd = a.d + (size_t)jb * CT;
   double* ee = a.e + (size_t)jb * CT;
   cplx* tt = a.tau + (size_t)jb * CT;
+  cplx* xch = a.xch + (size_t)jb * 4 * CT;
+  unsigned* cnt = a.cnt + (size_t)jb * 32;
   __shared__ cplx vL[2][CT], wL[CT], rhoL[CT];
   __shared__ double redd[16];
   __shared__ cplx redc[16];
+  __shared__ cplx s_tau;
+  __shared__ double s_beta, s_dk;
   __shared__ int s_abort;
-  unsigned long long tk[5] = {0, 0, 0, 0, 0}, tl = tick ? __builtin_amdgcn_s_memtime() : 0;
+  // phase ticks of job 0's first workgroup, thread 0 (kept in the LDS: per-lane counters would take
+  // 14 VGPRs from the register tile)
+  __shared__ unsigned long long s_tk[7];
+  if (tick) {
+    for (int i = 0; i < 6; ++i) s_tk[i] = 0;
+    s_tk[6] = __builtin_amdgcn_s_memtime();
+  }
   auto tmark = [&](int ph) {
     if (tick) {
       const unsigned long long t = __builtin_amdgcn_s_memtime();
-      tk[ph] += t - tl;
-      tl = t;
+      s_tk[ph] += t - s_tk[6];
+      s_tk[6] = t;
     }
   };
-  cplx A[16];
+  cplx A[RPL][CPL];
 #pragma unroll
-  for (int i = 0; i < 16; ++i) A[i] = ldg(G + (size_t)r * CT + q + TPR * i);
-  cplx vt = cmk(0, 0), tau = cmk(0, 0);
+  for (int u = 0; u < RPL; ++u)
+#pragma unroll
+    for (int i = 0; i < CPL; ++i) A[u][i] = ldg(G + (size_t)rr[u] * CT + q + TPG * i);
   if (tid < CT) {
     rhoL[tid] = ldg(G + tid);  // row 0
     wL[tid] = cmk(0, 0);       // no deferred update before column 0
     vL[1][tid] = cmk(0, 0);
   }
   if (tid == 0) s_abort = 0;
-  __syncthreads();
-  // reflector 0 from row 0
-  auto reflector = [&](int k, cplx xt) {  // after rhoL holds row k and redd the partial norms
+  // reflector k from rhoL = row k and the partial norms in redd, by wave 0 alone: zlarfg's scalars
+  // and v_k (1 at k + 1, conj(rho_k[c]) scale below, 0 above) into vL[k & 1]
+  auto reflector = [&](int k) {
     double xn2 = 0.0;
 #pragma unroll
     for (int w = 0; w < 16; ++w) xn2 += redd[w];
-    cplx sc;
+    cplx tau_, sc;
     double beta;
-    zlarfg_s(cconj(rhoL[k + 1]), xn2, tau, beta, sc);
-    vt = tid == k + 1 ? cmk(1, 0) : (tid > k + 1 && tid < CT ? cmul(xt, sc) : cmk(0, 0));
-    if (tid < CT) vL[k & 1][tid] = vt;
-    if (g == 0 && tid == 0) {
-      stg(dd + k, rhoL[k].x);
-      stg(ee + k, beta);
-      stg(tt + k, tau);
+    zlarfg_f(cconj(rhoL[k + 1]), xn2, tau_, beta, sc);
+#pragma unroll
+    for (int i = 0; i < CT / 64; ++i) {
+      const int c = lane + 64 * i;
+      vL[k & 1][c] = c == k + 1 ? cmk(1, 0) : (c > k + 1 ? cmul(cconj(rhoL[c]), sc) : cmk(0, 0));
+    }
+    if (lane == 0) {
+      s_tau = tau_;
+      s_beta = beta;
+      s_dk = rhoL[k].x;
     }
   };
+  __syncthreads();
   {
     const cplx xt = tid < CT ? cconj(rhoL[tid]) : cmk(0, 0);
-    const double part = wave_sum_b((tid >= 2 && tid < CT) ? cnorm2(xt) : 0.0);
+    const double part = lane_sum<64>((tid >= 2 && tid < CT) ? cnorm2(xt) : 0.0);
     if (lane == 0) redd[wave] = part;
     __syncthreads();
-    reflector(0, xt);
+    if (wave == 0) reflector(0);
     __syncthreads();
   }
   for (int k = 0; k < CT - 1; ++k) {
     const int cur = k & 1, prv = cur ^ 1;
-    // ---- the deferred update G -= v w^H + w v^H of reflector k - 1, then s = (G v_k)_r
-    cplx s = cmk(0, 0);
-    {
-      const cplx vr = vL[prv][r], wr = wL[r];
+    // ---- the deferred update of reflector k - 1, then s = (G v_k)_r
+    cplx s[RPL];
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int c = q + TPR * i;
-        A[i] = csub(A[i], cadd(cmulc(vr, wL[c]), cmulc(wr, vL[prv][c])));
-        s = cfma(A[i], vL[cur][c], s);
+    for (int u = 0; u < RPL; ++u) s[u] = cmk(0, 0);
+    if (rr[RPL - 1] > k) {
+      cplx vr[RPL], wr[RPL];
+#pragma unroll
+      for (int u = 0; u < RPL; ++u) vr[u] = vL[prv][rr[u]], wr[u] = wL[rr[u]];
+#pragma unroll
+      for (int i = 0; i < CPL; ++i) {
+        if (TPG * i + TPG - 1 > k) {
+          const int c = q + TPG * i;
+          const cplx vp = vL[prv][c], wc = wL[c], vc = vL[cur][c];
+#pragma unroll
+          for (int u = 0; u < RPL; ++u) {
+            A[u][i] = csub(A[u][i], cadd(cmulc(vr[u], wc), cmulc(wr[u], vp)));
+            s[u] = cfma(A[u][i], vc, s[u]);
+          }
+        }
       }
     }
-    s.x = group_reduce<TPR>(s.x);
-    s.y = group_reduce<TPR>(s.y);
-    const cplx pr = r > k ? cmul(tau, s) : cmk(0, 0);
+#pragma unroll
+    for (int u = 0; u < RPL; ++u) s[u] = cmk(lane_sum<TPG>(s[u].x), lane_sum<TPG>(s[u].y));
     tmark(0);
+    // (read after the pass: kept out of its register budget)
+    const cplx tau = s_tau;
+    const cplx vt = tid < CT ? vL[cur][tid] : cmk(0, 0);
     cplx* xp = xch + cur * CT;
     cplx* xr = xch + (2 + cur) * CT;
-    if (q == 0) st_sc1(xp + r, pr);
-    if (r == k + 1) {  // the row's owner: row k + 1 before this step's update
+    if (q == 0) {
 #pragma unroll
-      for (int i = 0; i < 16; ++i) st_sc1(xr + q + TPR * i, A[i]);
+      for (int u = 0; u < RPL; ++u) st_sc1(xp + rr[u], rr[u] > k ? cmul(tau, s[u]) : cmk(0, 0));
+    }
+#pragma unroll
+    for (int u = 0; u < RPL; ++u) {
+      if (rr[u] == k + 1) {  // the row's owner: row k + 1 before this step's update
+#pragma unroll
+        for (int i = 0; i < CPL; ++i) st_sc1(xr + q + TPG * i, A[u][i]);
+      }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     tmark(1);
     if (tid == 0) {
       __hip_atomic_fetch_add((gu32*)cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (g == 0) {  // the tridiagonal's entries and tau_k
+        stg(dd + k, s_dk);
+        stg(ee + k, s_beta);
+        stg(tt + k, tau);
+      }
       const unsigned target = (unsigned)P * (unsigned)(k + 1);
       const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
       while (__hip_atomic_load((gu32*)cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
@@ -268,6 +367,9 @@ __global__ __launch_bounds__(1024) void k_gb_tridiag(const TwoSiteJob* __restric
         }
       }
     }
+    // reflector k to row k of the scratch, each workgroup its own CT / P contiguous entries (a
+    // strided store here held the next publish wait: the stores must finish before it)
+    if (tid > k && tid / (CT / P) == g) stg(G + (size_t)k * CT + tid, vt);
     __syncthreads();
     if (s_abort) {
       if (tid == 0 && g == 0) {
@@ -277,15 +379,15 @@ __global__ __launch_bounds__(1024) void k_gb_tridiag(const TwoSiteJob* __restric
       return;
     }
     tmark(2);
-    // ---- w = p - tau / 2 (p^H v) v, the new row k + 1, reflector k to row k of the scratch
     const cplx pt = tid < CT ? ld_sc1(xp + tid) : cmk(0, 0);
     const cplx ro = tid < CT ? ld_sc1(xr + tid) : cmk(0, 0);
     const cplx pk1 = ld_sc1(xp + k + 1);
     const cplx pvp = cconjmul(pt, vt);
-    const double px = wave_sum_b(pvp.x), py = wave_sum_b(pvp.y);
+    const double px = lane_sum<64>(pvp.x), py = lane_sum<64>(pvp.y);
     if (lane == 0) redc[wave] = cmk(px, py);
     __syncthreads();
     tmark(3);
+    // ---- w = p - tau / 2 (p^H v) v, the new row k + 1 and its norm below the subdiagonal
     cplx pv = cmk(0, 0);
 #pragma unroll
     for (int w = 0; w < 16; ++w) pv = cadd(pv, redc[w]);
@@ -295,25 +397,23 @@ __global__ __launch_bounds__(1024) void k_gb_tridiag(const TwoSiteJob* __restric
     const cplx rho = csub(csub(ro, cconj(wt)), cmulc(wk1, vt));
     if (tid < CT) {
       wL[tid] = wt;  // (w_{k-1} was last read in this step's pass, before the exchange's barrier)
-      rhoL[tid] = rho;
-      if (g == 0 && tid > k) stg(G + (size_t)k * CT + tid, vt);
+      rhoL[tid] = rho;  // (row k: last read in the pass, for v_k)
     }
     if (k == CT - 2) {
       if (g == 0 && tid == CT - 1) stg(dd + CT - 1, rho.x);
       break;
     }
-    // ---- reflector k + 1 from the new row k + 1 (v_{k-1}'s buffer is free: read in the pass)
-    const cplx xt = tid < CT ? cconj(rho) : cmk(0, 0);
-    const double part = wave_sum_b((tid >= k + 3 && tid < CT) ? cnorm2(xt) : 0.0);
+    const double part = lane_sum<64>((tid >= k + 3 && tid < CT) ? cnorm2(rho) : 0.0);
     if (lane == 0) redd[wave] = part;
     __syncthreads();
-    reflector(k + 1, xt);
-    __syncthreads();
     tmark(4);
+    if (wave == 0) reflector(k + 1);
+    __syncthreads();
+    tmark(5);
   }
   if (tick) {
-#pragma unroll
-    for (int i = 0; i < 5; ++i) atomicAdd(&g_gbig_ticks[i], tk[i]);
+    for (int i = 0; i < 5; ++i) atomicAdd(&g_gbig_ticks[i], s_tk[i]);
+    atomicAdd(&g_gbig_ticks[8], s_tk[5]);
   }
 }
 
@@ -352,116 +452,90 @@ __device__ __forceinline__ int sturm_poly(const double2* de, int C, double xn) {
   return -neg;
 }
 
-__device__ __forceinline__ double rcp_nr2(double x) {
-  double r = __builtin_amdgcn_rcp(x);
-  r = r * fma(-x, r, 2.0);
-  r = r * fma(-x, r, 2.0);
-  return r;
-}
-
-// ---- eigenpairs of T: grid (nj), 1024 threads ----
+// ---- the top K eigenvalues of T: grid (ceil(K / 64), nj), 256 threads -----------------------
+// Multisection with the polynomial Sturm count (one dependent FMA per row; the pass is FP64-issue
+// bound): every workgroup brackets all eigenvalues with one pass of 256 shifts, then narrows its
+// 64 by 12 rounds of 5-section, 4 lanes per eigenvalue (span x 1.6e-11 at the end; the inverse
+// iteration and the Rayleigh quotient take sigma^2 from there).  Eigenvalues to the scratch,
+// descending; ||T|| (Gershgorin) with them.
 template <int CT>
-__global__ __launch_bounds__(1024) void k_gb_eig(const TwoSiteJob* __restrict__ jobs, GBArgs a) {
-  const int jb = blockIdx.x;
+__global__ __launch_bounds__(256) void k_gb_eig(const TwoSiteJob* __restrict__ jobs, GBArgs a) {
+  const int jb = blockIdx.y;
   if (*(const gi32*)(a.status + jb) != 0) return;
   const TwoSiteJob& j = jobs[jb];
   int M, L, C, K;
   bool tr;
   job_dims(j, M, L, C, tr, K);
+  if ((int)blockIdx.x * 64 >= K) return;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const unsigned long long t_start = __builtin_amdgcn_s_memtime();
-  __shared__ double s_d[CT], s_e[CT], s_e2[CT], s_lam[CT];
+  __shared__ double s_e[CT];
   __shared__ double2 s_de[CT];
   __shared__ int cntb[256];
-  __shared__ double s_lo, s_hi, s_tn;
-  __shared__ double rlo[16], rhi[16], rtn[16];
+  __shared__ double rlo[4], rhi[4], rtn[4];
   const double* dd = a.d + (size_t)jb * CT;
   const double* ee = a.e + (size_t)jb * CT;
-  for (int i = tid; i < CT; i += 1024) {
-    s_d[i] = ldg(dd + i);
-    s_e[i] = i < CT - 1 ? ldg(ee + i) : 0.0;
-  }
+  double lo = 1e300, hi = -1e300, tn = 0.0;
+  for (int i = tid; i < CT; i += 256) s_e[i] = i < CT - 1 ? ldg(ee + i) : 0.0;
   __syncthreads();
-  {
-    double lo = 1e300, hi = -1e300, tn = 0.0;
-    for (int i = tid; i < CT; i += 1024) {
-      const double el = i > 0 ? fabs(s_e[i - 1]) : 0.0, er = fabs(s_e[i]);
-      const double di = s_d[i];
-      lo = fmin(lo, di - el - er);
-      hi = fmax(hi, di + el + er);
-      tn = fmax(tn, fabs(di) + el + er);
-      s_e2[i] = s_e[i] * s_e[i];
-    }
+  for (int i = tid; i < CT; i += 256) {
+    const double el = i > 0 ? fabs(s_e[i - 1]) : 0.0, er = fabs(s_e[i]);
+    const double di = ldg(dd + i);
+    lo = fmin(lo, di - el - er);
+    hi = fmax(hi, di + el + er);
+    tn = fmax(tn, fabs(di) + el + er);
+    s_de[i] = make_double2(di, i > 0 ? s_e[i - 1] * s_e[i - 1] : 0.0);
+  }
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-      lo = fmin(lo, __shfl_xor(lo, off));
-      hi = fmax(hi, __shfl_xor(hi, off));
-      tn = fmax(tn, __shfl_xor(tn, off));
-    }
-    if (lane == 0) rlo[wave] = lo, rhi[wave] = hi, rtn[wave] = tn;
-    __syncthreads();
-    if (tid == 0) {
-      for (int w = 1; w < 16; ++w) lo = fmin(lo, rlo[w]), hi = fmax(hi, rhi[w]), tn = fmax(tn, rtn[w]);
-      lo = fmin(lo, rlo[0]), hi = fmax(hi, rhi[0]), tn = fmax(tn, rtn[0]);
-      const double span = fmax(hi - lo, 1e-300);
-      s_lo = lo - 1e-12 * span;
-      s_hi = hi + 1e-12 * span;
-      s_tn = tn;
-    }
-    __syncthreads();
-    const double itn = 1.0 / fmax(s_tn, 1e-300);
-    for (int i = tid; i < CT; i += 1024)
-      s_de[i] = make_double2(s_d[i] * itn, i > 0 ? s_e2[i - 1] * itn * itn : 0.0);
+  for (int off = 32; off > 0; off >>= 1) {
+    lo = fmin(lo, __shfl_xor(lo, off));
+    hi = fmax(hi, __shfl_xor(hi, off));
+    tn = fmax(tn, __shfl_xor(tn, off));
+  }
+  if (lane == 0) rlo[wave] = lo, rhi[wave] = hi, rtn[wave] = tn;
+  __syncthreads();
+  lo = fmin(fmin(rlo[0], rlo[1]), fmin(rlo[2], rlo[3]));
+  hi = fmax(fmax(rhi[0], rhi[1]), fmax(rhi[2], rhi[3]));
+  tn = fmax(fmax(rtn[0], rtn[1]), fmax(rtn[2], rtn[3]));
+  const double span = fmax(hi - lo, 1e-300);
+  const double lo0 = lo - 1e-12 * span, hi0 = hi + 1e-12 * span, span0 = hi0 - lo0;
+  const double itn = 1.0 / fmax(tn, 1e-300);
+  for (int i = tid; i < CT; i += 256) {  // the Sturm rows scaled by 1 / ||T||
+    const double2 de = s_de[i];
+    s_de[i] = make_double2(de.x * itn, de.y * itn * itn);
   }
   __syncthreads();
-  // multisection: one 256-shift pass, then 12 rounds of 5-section with 4 lanes per eigenvalue
+  constexpr int kG = 4, kFirst = 256, kRounds = 12;
+  constexpr double kInvF = 1.0 / (kFirst + 1), kInvG = 1.0 / (kG + 1);
+  cntb[tid] = sturm_poly(s_de, CT, (lo0 + span0 * (double)(tid + 1) * kInvF) * itn);
+  __syncthreads();
+  const int sub = tid % kG, eid = blockIdx.x * 64 + tid / kG;
+  const int a_ = CT - 1 - min(eid, CT - 1);  // ascending index of the eid-th largest
+  double l2, h2;
   {
-    constexpr int kG = 4, kFirst = 256, kRounds = 12;
-    const double lo0 = s_lo, span0 = s_hi - s_lo;
-    const double itn = 1.0 / fmax(s_tn, 1e-300);
-    constexpr double kInvF = 1.0 / (kFirst + 1), kInvG = 1.0 / (kG + 1);
-    if (tid < kFirst) cntb[tid] = sturm_poly(s_de, CT, (lo0 + span0 * (double)(tid + 1) * kInvF) * itn);
-    __syncthreads();
-    const int sub = tid % kG;
-    for (int b0 = 0; b0 < K; b0 += 1024 / kG) {
-      const int eid = b0 + tid / kG;
-      const int a_ = CT - 1 - min(eid, CT - 1);  // ascending index of the eid-th largest
-      double lo, hi;
-      {
-        int l = 0, h = kFirst;
-        while (l < h) {
-          const int m = (l + h) >> 1;
-          if (cntb[m] >= a_ + 1) h = m;
-          else l = m + 1;
-        }
-        lo = l > 0 ? lo0 + span0 * (double)l * kInvF : s_lo;
-        hi = l < kFirst ? lo0 + span0 * (double)(l + 1) * kInvF : s_hi;
-      }
-      for (int round = 0; round < kRounds; ++round) {
-        const double x = lo + (hi - lo) * (double)(sub + 1) * kInvG;
-        const int cnt = sturm_poly(s_de, CT, x * itn);
-        const unsigned long long bal = __ballot(cnt >= a_ + 1);
-        const unsigned int gm = (unsigned int)(bal >> (lane & ~(kG - 1))) & ((1u << kG) - 1u);
-        const int f = gm ? __builtin_ctz(gm) : kG;
-        const double nhi = f < kG ? lo + (hi - lo) * (double)(f + 1) * kInvG : hi;
-        const double nlo = f > 0 ? lo + (hi - lo) * (double)f * kInvG : lo;
-        lo = nlo;
-        hi = nhi;
-      }
-      if (eid < K && sub == 0) s_lam[eid] = 0.5 * (lo + hi);
+    int l = 0, h = kFirst;
+    while (l < h) {
+      const int m = (l + h) >> 1;
+      if (cntb[m] >= a_ + 1) h = m;
+      else l = m + 1;
     }
+    l2 = l > 0 ? lo0 + span0 * (double)l * kInvF : lo0;
+    h2 = l < kFirst ? lo0 + span0 * (double)(l + 1) * kInvF : hi0;
   }
-  __syncthreads();
-  if (!(s_lam[0] > 0.0) || !(s_lam[K - 1] > kGbRelFloor * s_lam[0])) {  // uniform
-    if (tid == 0) {
-      *(gi32*)(a.status + jb) = 2;
-      atomicAdd(&g_gbig_stats[3], 1ull);
-    }
-    return;
+  for (int round = 0; round < kRounds; ++round) {
+    const double x = l2 + (h2 - l2) * (double)(sub + 1) * kInvG;
+    const int cnt = sturm_poly(s_de, CT, x * itn);
+    const unsigned long long bal = __ballot(cnt >= a_ + 1);
+    const unsigned int gm = (unsigned int)(bal >> (lane & ~(kG - 1))) & ((1u << kG) - 1u);
+    const int f = gm ? __builtin_ctz(gm) : kG;
+    const double nhi = f < kG ? l2 + (h2 - l2) * (double)(f + 1) * kInvG : h2;
+    const double nlo = f > 0 ? l2 + (h2 - l2) * (double)f * kInvG : l2;
+    l2 = nlo;
+    h2 = nhi;
   }
-  for (int i = tid; i < K; i += 1024) stg(a.lam + (size_t)jb * CT + i, s_lam[i]);
-  if (tid == 0) stg(a.tn + jb, s_tn);
-  if (jb == 0 && tid == 0) atomicAdd(&g_gbig_ticks[5], __builtin_amdgcn_s_memtime() - t_start);
+  if (eid < K && sub == 0) stg(a.lam + (size_t)jb * CT + eid, 0.5 * (l2 + h2));
+  if (blockIdx.x == 0 && tid == 0) stg(a.tn + jb, tn);
+  if (jb == 0 && blockIdx.x == 0 && tid == 0) atomicAdd(&g_gbig_ticks[5], __builtin_amdgcn_s_memtime() - t_start);
 }
 
 typedef unsigned __attribute__((ext_vector_type(2))) u2_t;
@@ -496,6 +570,16 @@ __global__ __launch_bounds__(64) void k_gb_inv(const TwoSiteJob* __restrict__ jo
   }
   __syncthreads();
   const int i = blockIdx.x * 64 + threadIdx.x;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    // the Gram path's floor: every kept eigenvalue far above the noise of forming G, and above
+    // the CHOP (1e-16), or the job declines (k_gb_gs / k_gb_tfac / k_gb_back skip it; the host
+    // runs the block Jacobi)
+    const double l0 = ldg(a.lam + (size_t)jb * CT), lk = ldg(a.lam + (size_t)jb * CT + K - 1);
+    if (!(l0 > 0.0) || !(lk > kGbRelFloor * l0)) {
+      *(gi32*)(a.status + jb) = 2;
+      atomicAdd(&g_gbig_stats[3], 1ull);
+    }
+  }
   if (i >= K) return;  // (no barrier below)
   const double tn = ldg(a.tn + jb), itn = 1.0 / fmax(tn, 1e-300);
   const double lamn = ldg(a.lam + (size_t)jb * CT + i) * itn;
@@ -644,82 +728,179 @@ __global__ __launch_bounds__(64) void k_gb_gs(const TwoSiteJob* __restrict__ job
   }
 }
 
-// ---- V = Q Z, output: grid (CT / 16, nj), 1024 threads (one wave per eigenvector); dynamic LDS
-// kRB x CT complex (the staged reflectors) ----
-constexpr int kRB = 8;
-
+// ---- compact WY factors of the reflector blocks: grid (ceil((CT - 1) / 16), nj), 256 threads ----
+// Block b holds reflectors k0 = 16 b ... k0 + 15 (row k of the scratch: v_k[row] at k * CT + row,
+// rows > k); copied column-major (zeros at rows <= k) for k_gb_back.  S = Y^H Y (16 x 16,
+// thread (a, i) one entry), then LAPACK zlarft (forward, columnwise) with one thread per row of T:
+// T[a][i] = -tau_i sum_{a <= b < i} T[a][b] S[b][i], T[i][i] = tau_i.  H_k0 ... H_k0+15 = I - Y T Y^H.
 template <int CT>
-__global__ __launch_bounds__(1024) void k_gb_back(const TwoSiteJob* __restrict__ jobs, GBArgs a) {
-  constexpr int MR = CT / 64;  // rows per lane
+__global__ __launch_bounds__(256) void k_gb_tfac(const TwoSiteJob* __restrict__ jobs, GBArgs a) {
+  const int jb = blockIdx.y;
+  if (*(const gi32*)(a.status + jb) != 0) return;
+  const int k0 = blockIdx.x * 16, nb = min(16, CT - 1 - k0);
+  const cplx* Y = a.G + (size_t)jb * CT * CT;  // row k = v_k (entries > k)
+  cplx* Yc = a.yc + (size_t)jb * CT * CT;      // column-major copy, zeros at rows <= k
+  const cplx* tau = a.tau + (size_t)jb * CT;
+  __shared__ cplx S[16][17];
+  const int ia = threadIdx.x >> 4, ib = threadIdx.x & 15;
+  cplx acc = cmk(0, 0);
+  if (ia < nb && ib < nb) {
+    const int r0 = k0 + 1 + max(ia, ib);  // both vectors vanish at and above their own index
+    for (int row = r0; row < CT; ++row)
+      acc = cfmac(ldg(Y + (size_t)(k0 + ia) * CT + row), ldg(Y + (size_t)(k0 + ib) * CT + row), acc);
+  }
+  S[ia][ib] = acc;
+  for (int row = threadIdx.x; row < CT; row += 256) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int k = k0 + i;
+      stg(Yc + (size_t)row * CT + k, (i < nb && row > k) ? ldg(Y + (size_t)k * CT + row) : cmk(0, 0));
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < 16) {
+    const int ar = threadIdx.x;
+    cplx T[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const cplx ti = i < nb ? ldg(tau + k0 + i) : cmk(0, 0);
+      cplx v = cmk(0, 0);
+      if (i == ar) v = ti;
+      else if (i > ar) {
+        cplx sm = cmk(0, 0);
+#pragma unroll
+        for (int b = 0; b < 16; ++b)
+          if (b >= ar && b < i) sm = cfma(T[b], S[b][i], sm);
+        v = cscale(cmul(ti, sm), -1.0);
+      }
+      T[i] = v;
+    }
+    cplx* To = a.tfac + ((size_t)jb * (CT / 16) + blockIdx.x) * 256 + ar * 16;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) stg(To + i, T[i]);
+  }
+}
+
+// ---- V = Q Z on the matrix cores, output: grid (ceil(K / 16), nj), 256 threads ----
+// A workgroup owns 16 columns of V (C x 16, in the MFMA accumulator layout: wave w holds the row
+// tiles w, w + 4, ... -- cyclic, so the zero rows above each block are skipped evenly); per block
+// of 16 reflectors from the last: W1 = Y^H V (per wave over its rows, the four partials summed in
+// the LDS), W2 = T W1, V -= Y W2.  Y's operands straight from the (L2-resident) scratch: a block's
+// rows are contiguous in the column-major reflector store.  Output W = V Sigma, sig, qr = 1.
+template <int CT, int NW = (CT / 64 > 4 ? CT / 64 : 4)>
+__global__ __launch_bounds__(64 * NW) void k_gb_back(const TwoSiteJob* __restrict__ jobs, GBArgs a) {
+  constexpr int NT = CT / (16 * NW);  // row tiles per wave
   const int jb = blockIdx.y;
   if (*(const gi32*)(a.status + jb) != 0) return;
   TwoSiteJob& j = const_cast<TwoSiteJob&>(jobs[jb]);
   int M, L, C, K;
   bool tr;
   job_dims(j, M, L, C, tr, K);
-  extern __shared__ cplx Yl[];  // [kRB][CT]
-  __shared__ cplx s_tau[kRB];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int col = blockIdx.x * 16 + wave;
-  const bool act = col < K;
-  const double* zb = a.z + (size_t)jb * CT * CT;
-  const cplx* Y = a.G + (size_t)jb * CT * CT;
-  const cplx* tau = a.tau + (size_t)jb * CT;
+  const int col0 = blockIdx.x * 16;
+  if (col0 >= K) return;
   const unsigned long long t_start = __builtin_amdgcn_s_memtime();
-  cplx V[MR];
-#pragma unroll
-  for (int m = 0; m < MR; ++m) V[m] = cmk(act ? ldg(zb + (size_t)(lane + 64 * m) * CT + col) : 0.0, 0.0);
-  // the next group's reflectors are loaded into registers while the current group is applied
-  constexpr int PE = kRB * CT / 1024;
-  cplx ny[PE], ntau = cmk(0, 0);
-  auto fetch = [&](int k1) {
-    const int k0 = max(k1 - kRB + 1, 0), nb = k1 - k0 + 1;
-#pragma unroll
-    for (int u = 0; u < PE; ++u) {
-      const int e = tid + 1024 * u, b = e / CT, row = e % CT, k = k0 + b;
-      ny[u] = (b < nb && row > k) ? ldg(Y + (size_t)k * CT + row) : cmk(0, 0);
-    }
-    if (tid < kRB) ntau = tid < nb ? ldg(tau + k0 + tid) : cmk(0, 0);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 15, lk = lane >> 4;
+  const double* zb = a.z + (size_t)jb * CT * CT;
+  // reflector v_kk at row (kk < CT - 1, rows > kk; column-major store), through a buffer resource
+  const __amdgpu_buffer_rsrc_t ry = make_rsrc(a.yc + (size_t)jb * CT * CT, (unsigned)(CT * CT * 16));
+  auto yld = [&](int row, int kk) -> cplx {
+    const cplx v = buf_ld(ry, (unsigned)(row * CT + kk) * 16u, 0u);
+    return (row > kk && kk < CT - 1) ? v : cmk(0, 0);
   };
-  fetch(CT - 2);
-  for (int k1 = CT - 2; k1 >= 0; k1 -= kRB) {  // reflectors k1, k1 - 1, ..., k0 (last first)
-    const int k0 = max(k1 - kRB + 1, 0), nb = k1 - k0 + 1;
-    __syncthreads();  // the previous group's reflectors are consumed
+  const cplx* Tf = a.tfac + (size_t)jb * (CT / 16) * 256;
+  __shared__ cplx Pw[NW][16][16];
+  __shared__ cplx W1[16][17], W2[16][17], Tl[16][17];
+  d4_t vre[NT], vim[NT];
+  const int col = col0 + li;
 #pragma unroll
-    for (int u = 0; u < PE; ++u) Yl[tid + 1024 * u] = ny[u];
-    if (tid < kRB) s_tau[tid] = ntau;
-    __syncthreads();
-    if (k1 - kRB >= 0) fetch(k1 - kRB);
-    if (act) {
-      for (int b = nb - 1; b >= 0; --b) {
-        const int k = k0 + b;
-        const cplx* yv = Yl + b * CT;
-        cplx dot = cmk(0, 0);
+  for (int t = 0; t < NT; ++t) {
+    const int rt = w + NW * t;
 #pragma unroll
-        for (int m = 0; m < MR; ++m)
-          if (64 * m + 63 > k) dot = cfmac(yv[lane + 64 * m], V[m], dot);  // y^H V
-        dot.x = wave_sum_b(dot.x);
-        dot.y = wave_sum_b(dot.y);
-        const cplx f = cmul(s_tau[b], dot);
+    for (int q = 0; q < 4; ++q) {
+      const int row = 16 * rt + lk + 4 * q;
+      vre[t][q] = col < K ? ldg(zb + (size_t)row * CT + col) : 0.0;
+      vim[t][q] = 0.0;
+    }
+  }
+  for (int blk = (CT - 2) / 16; blk >= 0; --blk) {
+    const int k0 = 16 * blk;
+    if (tid < 256) Tl[tid >> 4][tid & 15] = ldg(Tf + (size_t)blk * 256 + tid);  // (>= 256 threads)
+    // W1 partial = Y^H V over this wave's rows: A[m = i][k = row] = conj(Y[row][k0 + i])
+    d4_t wr = {0, 0, 0, 0}, wi = {0, 0, 0, 0};
 #pragma unroll
-        for (int m = 0; m < MR; ++m)
-          if (64 * m + 63 > k) V[m] = csub(V[m], cmul(yv[lane + 64 * m], f));
+    for (int t = 0; t < NT; ++t) {
+      const int rt = w + NW * t;
+      if (16 * rt + 15 > k0) {  // rows <= k0 of the block vanish (uniform per wave)
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) {
+          const int row = 16 * rt + 4 * s4 + lk, kk = k0 + li;
+          const cplx y = yld(row, kk);
+          wr = __builtin_amdgcn_mfma_f64_16x16x4f64(y.x, vre[t][s4], wr, 0, 0, 0);
+          wr = __builtin_amdgcn_mfma_f64_16x16x4f64(y.y, vim[t][s4], wr, 0, 0, 0);
+          wi = __builtin_amdgcn_mfma_f64_16x16x4f64(y.x, vim[t][s4], wi, 0, 0, 0);
+          wi = __builtin_amdgcn_mfma_f64_16x16x4f64(-y.y, vre[t][s4], wi, 0, 0, 0);
+        }
       }
     }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) Pw[w][lk + 4 * q][li] = cmk(wr[q], wi[q]);
+    __syncthreads();
+    if (tid < 256) {
+      const int b = tid >> 4, c = tid & 15;
+      cplx acc = Pw[0][b][c];
+#pragma unroll
+      for (int ww = 1; ww < NW; ++ww) acc = cadd(acc, Pw[ww][b][c]);
+      W1[b][c] = acc;
+    }
+    __syncthreads();
+    if (tid < 256) {
+      const int i = tid >> 4, c = tid & 15;
+      cplx acc = cmk(0, 0);
+#pragma unroll
+      for (int b = 0; b < 16; ++b)
+        if (b >= i) acc = cfma(Tl[i][b], W1[b][c], acc);
+      W2[i][c] = acc;
+    }
+    __syncthreads();
+    // V -= Y W2: A[m = row][k = i] = Y[row][k0 + i], B[k = i][n = c] = W2[i][c]
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int rt = w + NW * t;
+      if (16 * rt + 15 > k0) {
+        const int row = 16 * rt + li;
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) {
+          const int kk = k0 + 4 * s4 + lk;
+          const cplx y = yld(row, kk);
+          const cplx ww = W2[4 * s4 + lk][li];
+          vre[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(-y.x, ww.x, vre[t], 0, 0, 0);
+          vre[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(y.y, ww.y, vre[t], 0, 0, 0);
+          vim[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(-y.x, ww.y, vim[t], 0, 0, 0);
+          vim[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(-y.y, ww.x, vim[t], 0, 0, 0);
+        }
+      }
+    }
+    __syncthreads();  // Tl, Pw, W1, W2 are overwritten next block
   }
-  if (act) {
+  if (col < K) {
     const double sg = sqrt(ldg(a.sig2 + (size_t)jb * CT + col));
 #pragma unroll
-    for (int m = 0; m < MR; ++m) {
-      const int row = lane + 64 * m;
-      if (row < C) stg(j.work + (size_t)col * C + row, cscale(V[m], sg));
+    for (int t = 0; t < NT; ++t) {
+      const int rt = w + NW * t;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int row = 16 * rt + lk + 4 * q;
+        if (row < C) stg(j.work + (size_t)col * C + row, cmk(vre[t][q] * sg, vim[t][q] * sg));
+      }
     }
-    if (lane == 0) stg(j.sig + col, sg);
+    if (w == 0 && lk == 0) stg(j.sig + col, sg);
   }
-  for (int c = blockIdx.x * 16 + tid; c < min(C, blockIdx.x * 16 + 16); c += 1024)
+  for (int c = col0 + tid; c < min(C, col0 + 16); c += 64 * NW)
     if (c >= K) stg(j.sig + c, 0.0);
-  if (jb == 0 && blockIdx.x == 0 && tid == 0) atomicAdd(&g_gbig_ticks[6], __builtin_amdgcn_s_memtime() - t_start);
+  if (blockIdx.x == 0)
+    for (int c = ((K + 15) / 16) * 16 + tid; c < C; c += 64 * NW) stg(j.sig + c, 0.0);
   if (blockIdx.x == 0 && tid == 0) {
+    if (jb == 0) atomicAdd(&g_gbig_ticks[6], __builtin_amdgcn_s_memtime() - t_start);
     j.qr = 1;
     atomicMax(&j.flags[2], 1);
     atomicAdd(&g_gbig_stats[1], 1ull);
@@ -731,6 +912,8 @@ struct GBBuffers {
   cplx* G = nullptr;
   double *d = nullptr, *e = nullptr, *z = nullptr, *dinv = nullptr, *sig2 = nullptr, *lam = nullptr, *tn = nullptr;
   cplx* tau = nullptr;
+  cplx* tfac = nullptr;
+  cplx* yc = nullptr;
   cplx* xch = nullptr;
   unsigned* cnt = nullptr;
   int* status = nullptr;
@@ -746,7 +929,7 @@ GBBuffers& gb_buffers() {
 
 void gb_free(GBBuffers& b) {
   hipFree(b.G), hipFree(b.d), hipFree(b.e), hipFree(b.z), hipFree(b.dinv), hipFree(b.sig2), hipFree(b.tau);
-  hipFree(b.lam), hipFree(b.tn);
+  hipFree(b.lam), hipFree(b.tn), hipFree(b.tfac), hipFree(b.yc);
   hipFree(b.xch), hipFree(b.cnt), hipFree(b.status), hipFree(b.djobs);
   hipHostFree(b.host_status), hipHostFree(b.hjobs);
   b = GBBuffers();
@@ -766,6 +949,8 @@ int gb_ensure(GBBuffers& b, int ct, int nj, hipStream_t st) {
   AQC_HIP_CHECK(hipMalloc(&b.sig2, (size_t)c * n * sizeof(double)));
   AQC_HIP_CHECK(hipMalloc(&b.lam, (size_t)c * n * sizeof(double)));
   AQC_HIP_CHECK(hipMalloc(&b.tn, (size_t)n * sizeof(double)));
+  AQC_HIP_CHECK(hipMalloc(&b.tfac, (size_t)(c / 16) * 256 * n * sizeof(cplx)));
+  AQC_HIP_CHECK(hipMalloc(&b.yc, cc * sizeof(cplx)));
   AQC_HIP_CHECK(hipMalloc(&b.tau, (size_t)c * n * sizeof(cplx)));
   AQC_HIP_CHECK(hipMalloc(&b.xch, (size_t)4 * c * n * sizeof(cplx)));
   AQC_HIP_CHECK(hipMalloc(&b.cnt, (size_t)32 * n * sizeof(unsigned)));
@@ -777,27 +962,26 @@ int gb_ensure(GBBuffers& b, int ct, int nj, hipStream_t st) {
   return AQC_OK;
 }
 
+// rows per lane of the tridiagonalisation at 2 chi <= 512 (AQC_GB_RPL = 1 or 2, default 1): two rows
+// per lane read each column's v, w operands from the LDS once for both, but the register tile then
+// spills (40 VGPRs at 2 chi = 512): 0.49 against 0.36 ms per config-5 gate
+int g_gb_rpl = -1;
+
 template <int CT>
 int run_gram_big(const TwoSiteJob* hjobs, const TwoSiteJob* jobs, int nj, int cap_max, hipStream_t st) {
   GBBuffers& b = gb_buffers();
+  if (g_gb_rpl < 0) {
+    const char* e = std::getenv("AQC_GB_RPL");
+    g_gb_rpl = (e && std::strcmp(e, "2") == 0) ? 2 : 1;
+  }
   int rc = gb_ensure(b, CT, nj, st);
   if (rc != AQC_OK) return rc;
-  static bool attr = false;
-  if (!attr) {
-    AQC_HIP_CHECK(hipFuncSetAttribute((const void*)k_gb_back<256>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      kRB * 256 * (int)sizeof(cplx)));
-    AQC_HIP_CHECK(hipFuncSetAttribute((const void*)k_gb_back<512>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      kRB * 512 * (int)sizeof(cplx)));
-    AQC_HIP_CHECK(hipFuncSetAttribute((const void*)k_gb_back<1024>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      kRB * 1024 * (int)sizeof(cplx)));
-    attr = true;
-  }
   GBArgs a;
   a.G = b.G, a.d = b.d, a.e = b.e, a.tau = b.tau, a.z = b.z, a.dinv = b.dinv, a.sig2 = b.sig2;
-  a.lam = b.lam, a.tn = b.tn;
+  a.lam = b.lam, a.tn = b.tn, a.tfac = b.tfac, a.yc = b.yc;
   a.xch = b.xch, a.cnt = b.cnt, a.status = b.status;
   AQC_HIP_CHECK(hipMemsetAsync(b.cnt, 0, (size_t)32 * nj * sizeof(unsigned), st));
-  hipLaunchKernelGGL((k_gb_gram<CT>), dim3((CT / 64) * (CT / 64), nj), dim3(256), 0, st, jobs, a);
+  hipLaunchKernelGGL((k_gb_gram<CT>), dim3((CT / 64) * (CT / 64 + 1) / 2, nj), dim3(256), 0, st, jobs, a);
   AQC_CHECK_LAUNCH();
   // the tridiagonalisation's workgroups of a job must all be resident together (they exchange a
   // vector per column): rounds of at most min(240, resident capacity) workgroups, whole jobs each
@@ -807,7 +991,7 @@ int run_gram_big(const TwoSiteJob* hjobs, const TwoSiteJob* jobs, int nj, int ca
     int dev = 0, ncu = 0, per_cu = 0;
     AQC_HIP_CHECK(hipGetDevice(&dev));
     AQC_HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-    AQC_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_gb_tridiag<CT>, 1024, 0));
+    AQC_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_gb_tridiag<CT, 1>, 1024, 0));
     resident = ncu * std::min(per_cu, 1);
   }
   const int per_round = std::min(240, resident) / P;
@@ -816,17 +1000,22 @@ int run_gram_big(const TwoSiteJob* hjobs, const TwoSiteJob* jobs, int nj, int ca
   } else {
     for (int j0 = 0; j0 < nj; j0 += per_round) {
       const int nr = std::min(per_round, nj - j0);
-      hipLaunchKernelGGL((k_gb_tridiag<CT>), dim3(P * nr), dim3(1024), 0, st, jobs, a, j0);
+      if (CT <= 512 && g_gb_rpl == 2)
+        hipLaunchKernelGGL((k_gb_tridiag<CT, CT <= 512 ? 2 : 1>), dim3(P * nr), dim3(1024), 0, st, jobs, a, j0);
+      else
+        hipLaunchKernelGGL((k_gb_tridiag<CT, 1>), dim3(P * nr), dim3(1024), 0, st, jobs, a, j0);
       AQC_CHECK_LAUNCH();
     }
   }
-  hipLaunchKernelGGL((k_gb_eig<CT>), dim3(nj), dim3(1024), 0, st, jobs, a);
+  hipLaunchKernelGGL((k_gb_eig<CT>), dim3(CT / 64, nj), dim3(256), 0, st, jobs, a);
   AQC_CHECK_LAUNCH();
   hipLaunchKernelGGL((k_gb_inv<CT>), dim3(CT / 64, nj), dim3(64), 0, st, jobs, a);
   AQC_CHECK_LAUNCH();
   hipLaunchKernelGGL((k_gb_gs<CT>), dim3(nj), dim3(64), 0, st, jobs, a);
   AQC_CHECK_LAUNCH();
-  hipLaunchKernelGGL((k_gb_back<CT>), dim3(CT / 16, nj), dim3(1024), kRB * CT * sizeof(cplx), st, jobs, a);
+  hipLaunchKernelGGL((k_gb_tfac<CT>), dim3((CT - 1 + 15) / 16, nj), dim3(256), 0, st, jobs, a);
+  AQC_CHECK_LAUNCH();
+  hipLaunchKernelGGL((k_gb_back<CT>), dim3(CT / 16, nj), dim3(CT / 64 > 4 ? CT : 256), 0, st, jobs, a);
   AQC_CHECK_LAUNCH();
   AQC_HIP_CHECK(hipMemcpyAsync(b.host_status, b.status, (size_t)nj * sizeof(int), hipMemcpyDeviceToHost, st));
   AQC_HIP_CHECK(hipStreamSynchronize(st));
@@ -857,10 +1046,10 @@ int big_svd(const TwoSiteJob* hjobs, const TwoSiteJob* jobs, int nj, int side, i
 
 extern "C" int aqc_svd_gram_big_ticks(double* out) {
   AQC_REQUIRE(out, "aqc_svd_gram_big_ticks: null argument");
-  unsigned long long t[8];
+  unsigned long long t[9];
   AQC_HIP_CHECK(hipMemcpyFromSymbol(t, HIP_SYMBOL(aqc::g_gbig_ticks), sizeof(t)));
-  for (int i = 0; i < 8; ++i) out[i] = (double)t[i];
-  unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int i = 0; i < 9; ++i) out[i] = (double)t[i];
+  unsigned long long z[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
   AQC_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(aqc::g_gbig_ticks), z, sizeof(z)));
   return AQC_OK;
 }

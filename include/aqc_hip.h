@@ -152,8 +152,9 @@ int aqc_bj_ticks(double* out);
 int aqc_svd_gram_big_stats(double* out);
 /* Diagnostics of the same path: shader-clock ticks summed over calls (then reset): out[0..4] the
    tridiagonalisation's per-column phases on job 0's first workgroup (register pass + row sums,
-   publish, counter wait, reads + p^H v, w / new row / next reflector), out[5] k_gb_eig up to the
-   eigenvalues, out[6] k_gb_back (job 0, first block), out[7] k_gb_eig in all (job 0). */
+   publish, counter wait, reads + p^H v, w / new row / partial norms), out[5] k_gb_eig (job 0),
+   out[6] k_gb_back (job 0, first block), out[7] k_gb_inv (job 0, lane 0), out[8] the next
+   reflector's zlarfg (per column, job 0's first workgroup). */
 int aqc_svd_gram_big_ticks(double* out);
 /* Batched applies of >= 32 states at 2*chi = 128 run every state's whole op list in
    one fused workgroup (theta, Jacobi, truncation, split per update: no grid-wide step between

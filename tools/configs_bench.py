@@ -166,7 +166,7 @@ def config5(gates, reps):
     work.apply(ops)
     work.dims()
     _lib.gram_big_stats()  # reset
-    gbt = np.zeros(8)
+    gbt = np.zeros(9)
     _lib.check(_lib.lib().aqc_svd_gram_big_ticks(_lib.ptr(gbt)))  # reset
     _lib.timing_reset()
     _lib.timing_enable(True)
@@ -182,7 +182,8 @@ def config5(gates, reps):
     if gbs["taken"]:
         ncol = reps * (2 * chi - 1)  # job 0's columns over the timed calls
         gbs["ticks_per_column"] = {k: gbt[i] / ncol for i, k in enumerate(
-            ("pass", "publish", "wait", "reads_pv", "w_row_reflector"))}
+            ("pass", "publish", "wait", "reads_pv", "w_row_norms"))}
+        gbs["ticks_per_column"]["zlarfg"] = gbt[8] / ncol
         gbs["ticks_per_call"] = {"eigenvalues": gbt[5] / reps, "back": gbt[6] / reps, "inverse_iteration": gbt[7] / reps}
     import ctypes
     sw = ctypes.c_int()
