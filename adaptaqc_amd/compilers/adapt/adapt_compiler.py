@@ -100,9 +100,11 @@ class AdaptCompiler(ApproximateCompiler):
 
     # -- layers ------------------------------------------------------------------------
     def construct_layer_2q_gate(self, custom_layer_2q_gate):
-        if custom_layer_2q_gate is None:
+        if custom_layer_2q_gate is None:  # adapt_compiler.py:224-233
             qc = QuantumCircuit(2)
             co.add_dressed_cnot(qc, 0, 1, True)
+            if self.general_initial_state:
+                co.add_dressed_cnot(qc, 0, 1, True, v1=False, v2=False)
             return qc
         for ins in custom_layer_2q_gate.data:
             if ins.operation.label is None and ins.operation.name in co.SUPPORTED_1Q_GATES:
@@ -116,8 +118,6 @@ class AdaptCompiler(ApproximateCompiler):
     def compile(self, initial_ansatz=None, optimise_initial_ansatz=True, checkpoint_every=0,
                 checkpoint_dir="checkpoint/", delete_prev_chkpt=False, freeze_prev_layers=False):
         """adapt_compiler.py:246-482."""
-        if initial_ansatz is not None:
-            raise NotImplementedError("initial_ansatz is not supported in this build")
         start_time = timeit.default_timer()
         if self.resume_from_layer is None:
             self.time_taken = 0
@@ -132,9 +132,17 @@ class AdaptCompiler(ApproximateCompiler):
             self.cnot_depth_history = []
             self.g_range = self.variational_circuit_range
             self.original_lhs_gate_count = self.lhs_gate_count
+            if freeze_prev_layers:
+                logger.warning("freeze_prev_layers only applies when resuming from a checkpoint")
+            # adapt_compiler.py:295-300: a provided ansatz is added (and optimised) first
+            self.initial_ansatz_already_successful = False
+            if initial_ansatz is not None:
+                self._add_initial_ansatz(initial_ansatz, optimise_initial_ansatz)
         else:
             start_point = self.resume_from_layer
             self.time_taken = self.prev_checkpoint_time_taken
+            if initial_ansatz is not None:
+                logger.warning("An initial ansatz will be ignored when resuming recompilation from a checkpoint")
             if freeze_prev_layers:
                 if self.is_aer_mps_backend:
                     num_gates = len(self.full_circuit) - self.rhs_gate_count - 1
@@ -147,6 +155,8 @@ class AdaptCompiler(ApproximateCompiler):
             Path(checkpoint_dir).mkdir(parents=True, exist_ok=True)
 
         for layer_count in range(start_point, self.adapt_config.max_layers):
+            if getattr(self, "initial_ansatz_already_successful", False):
+                break
             if self.optimise_local_cost:
                 self.local_cost = self._add_layer(layer_count)
                 self.global_cost = self.backend.evaluate_global_cost(self)
@@ -227,6 +237,37 @@ class AdaptCompiler(ApproximateCompiler):
                 os.remove(os.path.join(checkpoint_dir, f"{layer_count - checkpoint_every}.pkl"))
             except FileNotFoundError:
                 pass
+
+    def _add_initial_ansatz(self, initial_ansatz, optimise_initial_ansatz):
+        """adapt_compiler.py:536-583: the ansatz's inverse goes at the end of the variational
+        range, its rotations are optimised by Rotosolve (labels set so that Rotosolve recognises
+        them), and it is then frozen: absorbed into the cached MPS on the MPS backend, or moved
+        left of the variational range on the statevector backend."""
+        for ins in initial_ansatz.data:
+            if ins.operation.label is None and ins.operation.name in co.SUPPORTED_1Q_GATES:
+                ins.operation.label = ins.operation.name
+        co.add_to_circuit(self.full_circuit, co.circuit_by_inverting_circuit(initial_ansatz),
+                          self.variational_circuit_range()[1])
+        if optimise_initial_ansatz:
+            if not self.use_roto_algos:
+                raise NotImplementedError("PyBOBYQA is not available in this build")
+            cost = self.minimizer.minimize_cost(
+                algorithm_kind=ALG_ROTOSOLVE, tol=1e-3,
+                stop_val=0 if self.optimise_local_cost else self.adapt_config.sufficient_cost,
+                indexes_to_modify=self.variational_circuit_range())
+        else:
+            cost = self.evaluate_cost()
+        self.global_cost = self.backend.evaluate_global_cost(self) if self.optimise_local_cost else cost
+        self.cnot_depth = multi_qubit_gate_depth(initial_ansatz)
+        if self.global_cost < self.adapt_config.sufficient_cost:
+            self.initial_ansatz_already_successful = True
+            logger.debug("ADAPT-AQC successfully found approximate circuit using provided ansatz only")
+        if self.is_aer_mps_backend:
+            absorbed = self._absorb_n_gates_into_mps(n=len(initial_ansatz.data))
+            co.add_to_circuit(self.layers_saved_to_mps, absorbed)
+            self._update_reference_circuit()
+        else:
+            self.lhs_gate_count = self.variational_circuit_range()[1]
 
     def _add_layer(self, index):
         """adapt_compiler.py:585-689."""

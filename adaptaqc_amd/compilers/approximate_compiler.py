@@ -32,14 +32,28 @@ from ..utils.utilityfunctions import is_statevector_backend
 logger = logging.getLogger(__name__)
 
 
+def initial_state_to_circuit(initial_state):
+    """circuit_operations_full_circuit.py:385-410 for circuits; a state vector needs qiskit's
+    state-preparation synthesis (``initialize`` unrolled), which is not part of this build."""
+    if initial_state is None:
+        return None
+    if isinstance(initial_state, QuantumCircuit):
+        return initial_state.copy()
+    if hasattr(initial_state, "num_qubits") and hasattr(initial_state, "data"):  # qiskit-like circuit
+        qc = QuantumCircuit(initial_state.num_qubits)
+        co.add_to_circuit(qc, initial_state)
+        return qc
+    if isinstance(initial_state, (list, tuple)) or hasattr(initial_state, "shape"):
+        raise NotImplementedError("a state-vector initial_state needs qiskit's state preparation; pass a circuit")
+    raise TypeError("Invalid type of initial_state provided")
+
+
 class ApproximateCompiler(ABC):
     full_circuit: QuantumCircuit
 
     def __init__(self, target, backend, execute_kwargs=None, initial_state=None, qubit_subset=None,
                  general_initial_state=False, starting_circuit=None, optimise_local_cost=False,
                  soften_global_cost=False, itensor_chi=None, itensor_cutoff=None, rotosolve_fraction=1.0):
-        if initial_state is not None or general_initial_state:
-            raise NotImplementedError("initial_state / general_initial_state are outside the MI355X hot path")
         self.target = target
         self.original_circuit_classical_ops = None
         self.backend = backend if backend is not None else SV_SIM
@@ -52,15 +66,22 @@ class ApproximateCompiler(ABC):
         self.execute_kwargs.setdefault("shots", 1)
         self.execute_kwargs.setdefault("optimization_level", 0)
         self.backend_options = {"method": "automatic"}
-        self.initial_state_circuit = None
-        self.total_num_qubits = self.circuit_to_compile.num_qubits
+        if (initial_state is not None or general_initial_state) and self.is_aer_mps_backend:
+            # the MPS backend's full circuit starts from the target's MPS (set_matrix_product_state):
+            # a state prepared in front of it would be overwritten
+            raise NotImplementedError("initial_state / general_initial_state need a statevector backend")
+        self.initial_state_circuit = initial_state_to_circuit(initial_state)
+        self.total_num_qubits = (self.circuit_to_compile.num_qubits if self.initial_state_circuit is None
+                                 else self.initial_state_circuit.num_qubits)  # :289-294
         self.qubit_subset_to_compile = qubit_subset if qubit_subset else list(range(self.total_num_qubits))
-        self.general_initial_state = False
+        self.general_initial_state = general_initial_state
         self.starting_circuit = self.prepare_starting_circuit(starting_circuit)
         # approximate_compiler.py:133-135 builds this through Aer; it is |0..0> in preprocessed form
         self.zero_mps = _preprocess_mps(zero_aer_mps(self.total_num_qubits))
         self.optimise_local_cost = optimise_local_cost
         self.soften_global_cost = soften_global_cost
+        if initial_state is not None and general_initial_state:
+            raise ValueError("Can't compile for general initial state when specific initial state is provided")
         self.full_circuit, self.lhs_gate_count, self.rhs_gate_count = self._prepare_full_circuit()
         if not 0 < rotosolve_fraction <= 1:
             raise ValueError("rotosolve_fraction must be in the range (0,1]")
@@ -121,11 +142,28 @@ class ApproximateCompiler(ABC):
         raise NotImplementedError
 
     def _prepare_full_circuit(self):
-        qc = QuantumCircuit(self.total_num_qubits)
+        """approximate_compiler.py:435-512: |0> -- initial state -- circuit_to_compile -- (ansatz) --
+        initial state^-1 (or starting_circuit^-1); with general_initial_state the register doubles
+        and n Bell pairs (q, q + n) are made before and undone after (arXiv:1811.03147,
+        arXiv:1908.04416), so that the overlap with |0..0> measures the whole unitary."""
+        n = self.total_num_qubits
+        qc = QuantumCircuit(2 * n if self.general_initial_state else n)
+        if self.initial_state_circuit is not None:
+            co.add_to_circuit(qc, self.initial_state_circuit)
+        elif self.general_initial_state:
+            for q in range(n):
+                qc.h(q)
+                qc.cx(q, q + n)
         co.add_to_circuit(qc, self.circuit_to_compile, qubit_subset=self.qubit_subset_to_compile)
         lhs = len(qc.data)
+        if self.initial_state_circuit is not None:
+            co.add_to_circuit(qc, self.initial_state_circuit.inverse())
         if self.starting_circuit is not None:
             co.add_to_circuit(qc, self.starting_circuit.inverse())
+        elif self.general_initial_state:  # (as the reference: not after a starting circuit)
+            for q in range(n - 1, -1, -1):
+                qc.cx(q, q + n)
+                qc.h(q)
         return qc, lhs, len(qc.data) - lhs
 
     def get_compiled_circuit(self):

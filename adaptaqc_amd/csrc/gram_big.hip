@@ -459,8 +459,8 @@ __device__ __forceinline__ int sturm_poly(const double2* de, int C, double xn) {
 // iteration and the Rayleigh quotient take sigma^2 from there).  Eigenvalues to the scratch,
 // descending; ||T|| (Gershgorin) with them.
 template <int CT>
-__global__ __launch_bounds__(256) void k_gb_eig(const TwoSiteJob* __restrict__ jobs, GBArgs a) {
-  const int jb = blockIdx.y;
+__global__ __launch_bounds__(256) void k_gb_eig(const TwoSiteJob* __restrict__ jobs, GBArgs a, int job0) {
+  const int jb = job0 + (int)blockIdx.y;
   if (*(const gi32*)(a.status + jb) != 0) return;
   const TwoSiteJob& j = jobs[jb];
   int M, L, C, K;
@@ -554,8 +554,8 @@ __device__ __forceinline__ void bst(__amdgpu_buffer_rsrc_t r, unsigned lo, unsig
 // uniform offset); the solves' recurrences are serial per lane, so each row's operands are read
 // U rows ahead of the chain.
 template <int CT>
-__global__ __launch_bounds__(64) void k_gb_inv(const TwoSiteJob* __restrict__ jobs, GBArgs a) {
-  const int jb = blockIdx.y;
+__global__ __launch_bounds__(64) void k_gb_inv(const TwoSiteJob* __restrict__ jobs, GBArgs a, int job0) {
+  const int jb = job0 + (int)blockIdx.y;
   if (*(const gi32*)(a.status + jb) != 0) return;
   const TwoSiteJob& j = jobs[jb];
   int M, L, C, K;
@@ -684,8 +684,8 @@ __global__ __launch_bounds__(64) void k_gb_inv(const TwoSiteJob* __restrict__ jo
 // eigenvalues come out orthogonal to ~1e-14 from three inverse-iteration steps), then the cluster
 // members' sigma^2 again: grid (nj), one wave ----
 template <int CT>
-__global__ __launch_bounds__(64) void k_gb_gs(const TwoSiteJob* __restrict__ jobs, GBArgs a) {
-  const int jb = blockIdx.x;
+__global__ __launch_bounds__(64) void k_gb_gs(const TwoSiteJob* __restrict__ jobs, GBArgs a, int job0) {
+  const int jb = job0 + (int)blockIdx.x;
   if (*(const gi32*)(a.status + jb) != 0) return;
   const TwoSiteJob& j = jobs[jb];
   int M, L, C, K;
@@ -734,8 +734,8 @@ __global__ __launch_bounds__(64) void k_gb_gs(const TwoSiteJob* __restrict__ job
 // thread (a, i) one entry), then LAPACK zlarft (forward, columnwise) with one thread per row of T:
 // T[a][i] = -tau_i sum_{a <= b < i} T[a][b] S[b][i], T[i][i] = tau_i.  H_k0 ... H_k0+15 = I - Y T Y^H.
 template <int CT>
-__global__ __launch_bounds__(256) void k_gb_tfac(const TwoSiteJob* __restrict__ jobs, GBArgs a) {
-  const int jb = blockIdx.y;
+__global__ __launch_bounds__(256) void k_gb_tfac(const TwoSiteJob* __restrict__ jobs, GBArgs a, int job0) {
+  const int jb = job0 + (int)blockIdx.y;
   if (*(const gi32*)(a.status + jb) != 0) return;
   const int k0 = blockIdx.x * 16, nb = min(16, CT - 1 - k0);
   const cplx* Y = a.G + (size_t)jb * CT * CT;  // row k = v_k (entries > k)
@@ -788,9 +788,9 @@ __global__ __launch_bounds__(256) void k_gb_tfac(const TwoSiteJob* __restrict__ 
 // the LDS), W2 = T W1, V -= Y W2.  Y's operands straight from the (L2-resident) scratch: a block's
 // rows are contiguous in the column-major reflector store.  Output W = V Sigma, sig, qr = 1.
 template <int CT, int NW = (CT / 64 > 4 ? CT / 64 : 4)>
-__global__ __launch_bounds__(64 * NW) void k_gb_back(const TwoSiteJob* __restrict__ jobs, GBArgs a) {
+__global__ __launch_bounds__(64 * NW) void k_gb_back(const TwoSiteJob* __restrict__ jobs, GBArgs a, int job0) {
   constexpr int NT = CT / (16 * NW);  // row tiles per wave
-  const int jb = blockIdx.y;
+  const int jb = job0 + (int)blockIdx.y;
   if (*(const gi32*)(a.status + jb) != 0) return;
   TwoSiteJob& j = const_cast<TwoSiteJob&>(jobs[jb]);
   int M, L, C, K;
@@ -962,6 +962,24 @@ int gb_ensure(GBBuffers& b, int ct, int nj, hipStream_t st) {
   return AQC_OK;
 }
 
+hipStream_t gb_side_stream() {
+  static hipStream_t s[64] = {nullptr};
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (!s[dev]) (void)hipStreamCreateWithFlags(&s[dev], hipStreamNonBlocking);
+  return s[dev];
+}
+
+hipEvent_t gb_event(int i) {  // (per process; the library stream orders their reuse)
+  static std::vector<hipEvent_t> ev;
+  while ((int)ev.size() <= i) {
+    hipEvent_t e = nullptr;
+    (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
+    ev.push_back(e);
+  }
+  return ev[i];
+}
+
 // rows per lane of the tridiagonalisation at 2 chi <= 512 (AQC_GB_RPL = 1 or 2, default 1): two rows
 // per lane read each column's v, w operands from the LDS once for both, but the register tile then
 // spills (40 VGPRs at 2 chi = 512): 0.49 against 0.36 ms per config-5 gate
@@ -995,28 +1013,50 @@ int run_gram_big(const TwoSiteJob* hjobs, const TwoSiteJob* jobs, int nj, int ca
     resident = ncu * std::min(per_cu, 1);
   }
   const int per_round = std::min(240, resident) / P;
+  // the eigenpairs and back-transformation of a round's jobs run on a second stream, beside the next
+  // round's tridiagonalisation (which leaves CUs free: 9 of 24 config-5 jobs hold 144 of 256)
+  static int overlap = -1;  // AQC_GB_OVERLAP=0: everything on the library stream (A/B)
+  if (overlap < 0) {
+    const char* e = std::getenv("AQC_GB_OVERLAP");
+    overlap = (e && std::strcmp(e, "0") == 0) ? 0 : 1;
+  }
+  hipStream_t s2 = overlap ? gb_side_stream() : st;
+  auto post = [&](hipStream_t ps, int j0, int nr) -> int {
+    hipLaunchKernelGGL((k_gb_eig<CT>), dim3(CT / 64, nr), dim3(256), 0, ps, jobs, a, j0);
+    AQC_CHECK_LAUNCH();
+    hipLaunchKernelGGL((k_gb_inv<CT>), dim3(CT / 64, nr), dim3(64), 0, ps, jobs, a, j0);
+    AQC_CHECK_LAUNCH();
+    hipLaunchKernelGGL((k_gb_gs<CT>), dim3(nr), dim3(64), 0, ps, jobs, a, j0);
+    AQC_CHECK_LAUNCH();
+    hipLaunchKernelGGL((k_gb_tfac<CT>), dim3((CT - 1 + 15) / 16, nr), dim3(256), 0, ps, jobs, a, j0);
+    AQC_CHECK_LAUNCH();
+    hipLaunchKernelGGL((k_gb_back<CT>), dim3(CT / 16, nr), dim3(CT / 64 > 4 ? CT : 256), 0, ps, jobs, a, j0);
+    AQC_CHECK_LAUNCH();
+    return AQC_OK;
+  };
   if (per_round < 1) {  // cannot hold one job's workgroups at once: every job declines
     AQC_HIP_CHECK(hipMemsetAsync(b.status, 0x7f, (size_t)nj * sizeof(int), st));
+    rc = post(st, 0, nj);
+    if (rc != AQC_OK) return rc;
   } else {
-    for (int j0 = 0; j0 < nj; j0 += per_round) {
+    int r = 0;
+    for (int j0 = 0; j0 < nj; j0 += per_round, ++r) {
       const int nr = std::min(per_round, nj - j0);
       if (CT <= 512 && g_gb_rpl == 2)
         hipLaunchKernelGGL((k_gb_tridiag<CT, CT <= 512 ? 2 : 1>), dim3(P * nr), dim3(1024), 0, st, jobs, a, j0);
       else
         hipLaunchKernelGGL((k_gb_tridiag<CT, 1>), dim3(P * nr), dim3(1024), 0, st, jobs, a, j0);
       AQC_CHECK_LAUNCH();
+      hipEvent_t ev = gb_event(r);
+      AQC_HIP_CHECK(hipEventRecord(ev, st));
+      AQC_HIP_CHECK(hipStreamWaitEvent(s2, ev, 0));
+      rc = post(s2, j0, nr);
+      if (rc != AQC_OK) return rc;
     }
+    hipEvent_t done = gb_event(r);
+    AQC_HIP_CHECK(hipEventRecord(done, s2));
+    AQC_HIP_CHECK(hipStreamWaitEvent(st, done, 0));
   }
-  hipLaunchKernelGGL((k_gb_eig<CT>), dim3(CT / 64, nj), dim3(256), 0, st, jobs, a);
-  AQC_CHECK_LAUNCH();
-  hipLaunchKernelGGL((k_gb_inv<CT>), dim3(CT / 64, nj), dim3(64), 0, st, jobs, a);
-  AQC_CHECK_LAUNCH();
-  hipLaunchKernelGGL((k_gb_gs<CT>), dim3(nj), dim3(64), 0, st, jobs, a);
-  AQC_CHECK_LAUNCH();
-  hipLaunchKernelGGL((k_gb_tfac<CT>), dim3((CT - 1 + 15) / 16, nj), dim3(256), 0, st, jobs, a);
-  AQC_CHECK_LAUNCH();
-  hipLaunchKernelGGL((k_gb_back<CT>), dim3(CT / 16, nj), dim3(CT / 64 > 4 ? CT : 256), 0, st, jobs, a);
-  AQC_CHECK_LAUNCH();
   AQC_HIP_CHECK(hipMemcpyAsync(b.host_status, b.status, (size_t)nj * sizeof(int), hipMemcpyDeviceToHost, st));
   AQC_HIP_CHECK(hipStreamSynchronize(st));
   int nd = 0;

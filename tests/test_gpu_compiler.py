@@ -269,3 +269,99 @@ def test_cached_rotations_vs_oracle_sequence(backend_kind, rotoselect):
     assert [x[0] for x in got] == [x[0] for x in want]
     np.testing.assert_allclose([x[1] for x in got], [x[1] for x in want], atol=1e-9)
 
+
+
+def _ops_of(circuit):
+    return [(i.operation.name, i.qubits, tuple(i.operation.params)) for i in circuit.data]
+
+
+@pytest.mark.parametrize("backend_kind", ["sv", "mps"])
+def test_initial_ansatz_used_and_frozen(backend_kind):
+    """compile(initial_ansatz=...) (adapt_compiler.py:295-300, 536-583): the ansatz's rotations are
+    optimised first; here it has the target's own structure (angles perturbed), so it alone reaches
+    the sufficient cost and no layer is added; the compiled circuit reproduces the target."""
+    from adaptaqc_amd.backends import AerMPSBackend, AerSVBackend
+    from adaptaqc_amd.circuit import QuantumCircuit
+    from adaptaqc_amd.compilers import AdaptCompiler, AdaptConfig
+
+    angles = [0.7, -1.1, 0.4, 1.3, -0.6, 0.9]
+    target = QuantumCircuit(3)
+    ansatz = QuantumCircuit(3)
+    for qc, sh in ((target, 0.0), (ansatz, 0.25)):
+        qc.ry(angles[0] + sh, 0)
+        qc.ry(angles[1] + sh, 1)
+        qc.cx(0, 1)
+        qc.rz(angles[2] + sh, 1)
+        qc.ry(angles[3] + sh, 2)
+        qc.cx(1, 2)
+        qc.ry(angles[4] + sh, 2)
+        qc.rz(angles[5] + sh, 0)
+    backend = AerSVBackend() if backend_kind == "sv" else AerMPSBackend()
+    comp = AdaptCompiler(target, backend=backend, adapt_config=AdaptConfig(sufficient_cost=1e-4))
+    res = comp.compile(initial_ansatz=ansatz)
+    assert comp.initial_ansatz_already_successful
+    assert res.overlap > 1 - 1e-3
+    assert len(res.qubit_pair_history) == 0
+    want = osv.simulate(3, _ops_of(target))
+    got = osv.simulate(3, _ops_of(res.circuit))
+    assert abs(np.vdot(want, got)) ** 2 > 1 - 1e-3
+
+
+def test_initial_state_circuit_sv():
+    """initial_state (approximate_compiler.py:126-139, 458-492): full circuit = S, U, [ansatz],
+    S^-1, so the cost of an ansatz V (stored inverted) is 1 - |<s| V^dagger U |s>|^2 with |s> = S|0>
+    -- checked against the oracle for the exact V (cost 0) and a perturbed one.  (AdaptCompiler
+    passes initial_state=None, adapt_compiler.py:123-134: the option belongs to the base class.)"""
+    from adaptaqc_amd.circuit import QuantumCircuit
+    from adaptaqc_amd.compilers.approximate_compiler import ApproximateCompiler
+    from adaptaqc_amd.utils import circuit_operations as co
+
+    class _Fixed(ApproximateCompiler):
+        def compile(self):
+            raise NotImplementedError
+
+    n = 3
+    ops = _random_state_circuit(n, 2, 9)
+    target = to_circuit(n, ops)
+    init_ops = [("h", (0,), ()), ("ry", (1,), (0.8,)), ("cx", (1, 2), ()), ("rx", (2,), (0.3,))]
+    init = to_circuit(n, init_ops)
+    comp = _Fixed(target, None, initial_state=init)
+    assert comp.full_circuit.num_qubits == n and comp.lhs_gate_count == len(init_ops) + len(ops)
+    for shift, expect_zero in ((0.0, True), (0.2, False)):
+        v_ops = [(nm, qs, tuple(p + shift for p in ps)) for nm, qs, ps in ops]
+        c = _Fixed(target, None, initial_state=init)
+        co.add_to_circuit(c.full_circuit, co.circuit_by_inverting_circuit(to_circuit(n, v_ops)),
+                          c.variational_circuit_range()[1])
+        cost = c.evaluate_cost()
+        u_s = osv.simulate(n, init_ops + ops)
+        v_s = osv.simulate(n, init_ops + v_ops)
+        want = 1 - abs(np.vdot(v_s, u_s)) ** 2
+        assert abs(cost - want) < 1e-10, (cost, want)
+        assert (cost < 1e-10) == expect_zero
+    with pytest.raises(ValueError):
+        _Fixed(target, None, initial_state=init, general_initial_state=True)
+
+
+def test_general_initial_state_sv():
+    """general_initial_state (approximate_compiler.py:477-508, adapt_compiler.py:224-233): the
+    Bell-pair (Choi) form on 2n qubits compiles the whole unitary, |Tr(V^dagger U)| / 2^n ~ 1."""
+    from adaptaqc_amd.compilers import AdaptCompiler, AdaptConfig
+
+    n = 2
+    ops = [("ry", (0,), (0.9,)), ("cx", (0, 1), ()), ("rz", (1,), (-0.7,)), ("rx", (0,), (0.4,))]
+    target = to_circuit(n, ops)
+    comp = AdaptCompiler(target, general_initial_state=True, adapt_config=AdaptConfig(sufficient_cost=1e-4))
+    assert comp.full_circuit.num_qubits == 2 * n
+    res = comp.compile()
+    assert res.overlap > 1 - 1e-3
+
+    def unitary(o):
+        cols = []
+        for b in range(2 ** n):
+            prep = [("x", (q,), ()) for q in range(n) if (b >> q) & 1]
+            cols.append(osv.simulate(n, prep + o))
+        return np.stack(cols, axis=1)
+
+    u = unitary(ops)
+    v = unitary(_ops_of(res.circuit))
+    assert abs(np.trace(v.conj().T @ u)) / 2 ** n > 1 - 1e-3
