@@ -86,14 +86,14 @@ def add_to_circuit(original, to_add, location=None, qubit_subset=None):
     """Insert ``to_add``'s gates at ``location`` (qubit i of to_add -> qubit_subset[i])."""
     if location is None:
         location = len(original.data)
-    mapping = list(range(to_add.num_qubits)) if qubit_subset is None else (
-        [qubit_subset[i] for i in range(to_add.num_qubits)] if not isinstance(qubit_subset, dict)
-        else [qubit_subset[i] for i in range(to_add.num_qubits)])
+    # a dict maps only the qubits the gates use (the general-initial-state circuit has 2n qubits,
+    # its variational gates act on the first n)
+    mapping = (lambda q: q) if qubit_subset is None else (lambda q: qubit_subset[q])
     for k, ins in enumerate(to_add.data):
         op = ins.operation.copy()
         if op.label is None and op.name in SUPPORTED_1Q_GATES:
             op.label = op.name
-        original.data.insert(location + k, CircuitInstruction(op, [mapping[q] for q in ins.qubits]))
+        original.data.insert(location + k, CircuitInstruction(op, [mapping(q) for q in ins.qubits]))
 
 
 def extract_inner_circuit(circuit, gate_range):
