@@ -214,12 +214,15 @@ __device__ __forceinline__ void zlarfg_f(cplx alpha, double xn2, cplx& tau, doub
 }
 
 // grid (P * njobs_in_round), 1024 threads.  Thread t: row group t / TPG of RPL rows (local rows
-// RPL * group + u, global r = local P + g), columns q + TPG i (q = t % TPG, i < CPL).  Per column k:
+// RPL * group + u, global r = local P + g), columns q + TPG i (q = t % TPG, i < CPL).  RPL = 1 is
+// the one instantiated: two rows per lane read each column's v, w operands from the LDS once for
+// both, but the register tile then spilled (40 VGPRs at 2 chi = 512: 0.49 against 0.36 ms per
+// config-5 gate).  Per column k:
 //   pass      the deferred rank-2 update G -= v w^H + w v^H of reflector k - 1 and s = (G v_k)_r in
 //             one sweep over the registers; column blocks and row groups at or above k are dead and
 //             skipped
-//   exchange  p_r = tau_k s_r (and the owner's row k + 1 as it was before this update) out, all p
-//             and that row in; d_k, e_k, tau_k and this workgroup's slice of v_k go to the scratch
+//   exchange  p_r = tau_k s_r and conj(G[r][k + 1]) (row k + 1 as it was before this update, by
+//             symmetry: every workgroup its rows' entries) out, all p and that row in; d_k, e_k, tau_k and this workgroup's slice of v_k go to the scratch
 //             here, where their store latency hides behind the wait
 //   tail      p^H v (one workgroup reduction), w_k = p + a2 v, the new row k + 1 = old - conj(w) -
 //             w_{k+1} conj(v), its norm below the subdiagonal (a second reduction); wave 0 alone
@@ -308,9 +311,10 @@ __global__ __launch_bounds__(1024) void k_gb_tridiag(const TwoSiteJob* __restric
   for (int k = 0; k < CT - 1; ++k) {
     const int cur = k & 1, prv = cur ^ 1;
     // ---- the deferred update of reflector k - 1, then s = (G v_k)_r
-    cplx s[RPL];
+    cplx s[RPL], xcol[RPL];  // xcol: this lane's G[r][k + 1] after the update (its publish)
 #pragma unroll
-    for (int u = 0; u < RPL; ++u) s[u] = cmk(0, 0);
+    for (int u = 0; u < RPL; ++u) s[u] = cmk(0, 0), xcol[u] = cmk(0, 0);
+    const int ic = (k + 1) / TPG;  // the register holding column k + 1 (uniform)
     if (rr[RPL - 1] > k) {
       cplx vr[RPL], wr[RPL];
 #pragma unroll
@@ -324,6 +328,7 @@ __global__ __launch_bounds__(1024) void k_gb_tridiag(const TwoSiteJob* __restric
           for (int u = 0; u < RPL; ++u) {
             A[u][i] = csub(A[u][i], cadd(cmulc(vr[u], wc), cmulc(wr[u], vp)));
             s[u] = cfma(A[u][i], vc, s[u]);
+            if (i == ic) xcol[u] = A[u][i];
           }
         }
       }
@@ -340,12 +345,12 @@ __global__ __launch_bounds__(1024) void k_gb_tridiag(const TwoSiteJob* __restric
 #pragma unroll
       for (int u = 0; u < RPL; ++u) st_sc1(xp + rr[u], rr[u] > k ? cmul(tau, s[u]) : cmk(0, 0));
     }
+    // row k + 1 before this step's update, by Hermitian symmetry from column k + 1: every row's
+    // lane holding that column publishes conj(A[r][k + 1]) (the owner alone writing the whole row
+    // made its workgroup the last to publish every column)
+    if (q == (k + 1) % TPG) {
 #pragma unroll
-    for (int u = 0; u < RPL; ++u) {
-      if (rr[u] == k + 1) {  // the row's owner: row k + 1 before this step's update
-#pragma unroll
-        for (int i = 0; i < CPL; ++i) st_sc1(xr + q + TPG * i, A[u][i]);
-      }
+      for (int u = 0; u < RPL; ++u) st_sc1(xr + rr[u], cconj(xcol[u]));
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -980,18 +985,10 @@ hipEvent_t gb_event(int i) {  // (per process; the library stream orders their r
   return ev[i];
 }
 
-// rows per lane of the tridiagonalisation at 2 chi <= 512 (AQC_GB_RPL = 1 or 2, default 1): two rows
-// per lane read each column's v, w operands from the LDS once for both, but the register tile then
-// spills (40 VGPRs at 2 chi = 512): 0.49 against 0.36 ms per config-5 gate
-int g_gb_rpl = -1;
 
 template <int CT>
 int run_gram_big(const TwoSiteJob* hjobs, const TwoSiteJob* jobs, int nj, int cap_max, hipStream_t st) {
   GBBuffers& b = gb_buffers();
-  if (g_gb_rpl < 0) {
-    const char* e = std::getenv("AQC_GB_RPL");
-    g_gb_rpl = (e && std::strcmp(e, "2") == 0) ? 2 : 1;
-  }
   int rc = gb_ensure(b, CT, nj, st);
   if (rc != AQC_OK) return rc;
   GBArgs a;
@@ -1042,10 +1039,7 @@ int run_gram_big(const TwoSiteJob* hjobs, const TwoSiteJob* jobs, int nj, int ca
     int r = 0;
     for (int j0 = 0; j0 < nj; j0 += per_round, ++r) {
       const int nr = std::min(per_round, nj - j0);
-      if (CT <= 512 && g_gb_rpl == 2)
-        hipLaunchKernelGGL((k_gb_tridiag<CT, CT <= 512 ? 2 : 1>), dim3(P * nr), dim3(1024), 0, st, jobs, a, j0);
-      else
-        hipLaunchKernelGGL((k_gb_tridiag<CT, 1>), dim3(P * nr), dim3(1024), 0, st, jobs, a, j0);
+      hipLaunchKernelGGL((k_gb_tridiag<CT, 1>), dim3(P * nr), dim3(1024), 0, st, jobs, a, j0);
       AQC_CHECK_LAUNCH();
       hipEvent_t ev = gb_event(r);
       AQC_HIP_CHECK(hipEventRecord(ev, st));
