@@ -1071,9 +1071,19 @@ int big_svd(const TwoSiteJob* hjobs, const TwoSiteJob* jobs, int nj, int side, i
     g_gram_big = (s && std::strcmp(s, "0") == 0) ? 0 : 1;
   }
   if (!g_gram_big || side > 1024) return block_jacobi(jobs, nj, cap_max, st);
-  if (side <= 256) return run_gram_big<256>(hjobs, jobs, nj, cap_max, st);
-  if (side <= 512) return run_gram_big<512>(hjobs, jobs, nj, cap_max, st);
-  return run_gram_big<1024>(hjobs, jobs, nj, cap_max, st);
+  // chunks of at most 1.5 GB of per-job scratch (G, the two inverse-iteration arrays and the
+  // column-major reflectors: 64 C^2 bytes per job), so that a large batch does not hold it all
+  const int ct = side <= 256 ? 256 : side <= 512 ? 512 : 1024;
+  const int chunk = std::max(1, (int)((size_t)1536 << 20) / (64 * ct * ct));
+  for (int j0 = 0; j0 < nj; j0 += chunk) {
+    const int n = std::min(chunk, nj - j0);
+    int rc;
+    if (ct == 256) rc = run_gram_big<256>(hjobs + j0, jobs + j0, n, cap_max, st);
+    else if (ct == 512) rc = run_gram_big<512>(hjobs + j0, jobs + j0, n, cap_max, st);
+    else rc = run_gram_big<1024>(hjobs + j0, jobs + j0, n, cap_max, st);
+    if (rc != AQC_OK) return rc;
+  }
+  return AQC_OK;
 }
 
 }  // namespace aqc
