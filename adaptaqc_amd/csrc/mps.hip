@@ -908,6 +908,14 @@ __device__ __forceinline__ void chain_theta(const TwoSiteJob& j) {
   const int l0 = 32 * (sg >> 1), r0 = 32 * (sg & 1);
   const bool active = l0 < chl && r0 < chr;
   const int ty = lt >> 4, tx = lt & 15;
+  // the operand pointers held in SGPRs across the m loop: left to the compiler they were re-read
+  // from the job (s_load) every step, and each step's global loads waited on lgkmcnt(0) first
+  const cplx* gp = j.gp;
+  const cplx* gq = j.gq;
+  const double* llp = j.ll;
+  const double* lmp = j.lm;
+  const double* lrp = j.lr;
+  asm volatile("" : "+s"(gp), "+s"(gq), "+s"(llp), "+s"(lmp), "+s"(lrp));
   cplx acc[4][2][2];
 #pragma unroll
   for (int q = 0; q < 4; ++q)
@@ -923,13 +931,13 @@ __device__ __forceinline__ void chain_theta(const TwoSiteJob& j) {
         const int row = (e >> 3) & 31, mm = e & 7, l = l0 + row, m = m0 + mm;
         cplx a = aqc::cmk(0, 0);
         if (active && l < chl && m < chm)
-          a = aqc::cscale(aqc::ldg(j.gp + s * half + (size_t)l * cap + m), aqc::ldg(j.ll + l) * aqc::ldg(j.lm + m));
+          a = aqc::cscale(aqc::ldg(gp + s * half + (size_t)l * cap + m), aqc::ldg(llp + l) * aqc::ldg(lmp + m));
         As[s][row][mm] = a;
       }
       {  // B: 32 consecutive r of one row per 32 lanes
         const int mm = (e >> 5) & 7, col = e & 31, m = m0 + mm, r = r0 + col;
         cplx b = aqc::cmk(0, 0);
-        if (active && m < chm && r < chr) b = aqc::cscale(aqc::ldg(j.gq + s * half + (size_t)m * cap + r), aqc::ldg(j.lr + r));
+        if (active && m < chm && r < chr) b = aqc::cscale(aqc::ldg(gq + s * half + (size_t)m * cap + r), aqc::ldg(lrp + r));
         Bs[s][mm][col] = b;
       }
     }

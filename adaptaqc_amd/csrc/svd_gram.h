@@ -53,6 +53,14 @@ __device__ unsigned long long g_gram_ticks[12];
 #ifndef AQC_S3_DIAG
 #define AQC_S3_DIAG 0
 #endif
+// S3: the reflectors' base pointer in SGPRs (as a VGPR pair it was spilled and reloaded per column)
+#ifndef AQC_S3_HH_SGPR
+#define AQC_S3_HH_SGPR 1
+#endif
+// S3: the rows' partial products of the column pass summed in the wave (DPP) before phase B
+#ifndef AQC_S3_ROWSUM
+#define AQC_S3_ROWSUM 1
+#endif
 // S3: the column pass prefetches column i + 1's LDS operands while column i computes
 #ifndef AQC_S3_PIPE
 #define AQC_S3_PIPE 1
@@ -102,6 +110,14 @@ __device__ __forceinline__ double uniform_d(double v) {
   return __hiloint2double(hi, lo);
 }
 
+// a wave-uniform pointer moved to SGPRs
+template <class T>
+__device__ __forceinline__ T* uniform_ptr(T* p) {
+  const unsigned long long a = (unsigned long long)p;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
+  return (T*)(((unsigned long long)hi << 32) | lo);
+}
 // 1 for a negative q (sign bit; q is never -0 here)
 __device__ __forceinline__ int sign_bit(double q) { return (int)((unsigned)__double2hiint(q) >> 31); }
 
@@ -353,7 +369,9 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
   ldbl* dS = (ldbl*)(lb + 2114);  // [128] d_k
   lcplx* ktp = lb + 2178;    // [2] p^H v partials of the last p / v pass (rows 0-63, 64-127)
   lcplx* scal = lb + 2180;   // reflector k's 1 / (alpha - beta), tau / (alpha - beta); s of k - 1
-  cplx* hh = j.work;       // reflector k at hh[k (2C - k - 1) / 2 + (row - k - 1)]
+  // reflector k at hh[k (2C - k - 1) / 2 + (row - k - 1)].  The base is uniform: moved to SGPRs
+  // (as a VGPR pair it was spilled, and phase B's scratch reload waited out vmcnt(0) every column)
+  cplx* hh = AQC_S3_HH_SGPR ? uniform_ptr(j.work) : j.work;
   // "reflector -1": none, and column 0 of G as z (s = 0)
   if (tid == 0) {
     tauS[-1] = aqc::cmk(0, 0);
@@ -527,7 +545,15 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
       const cplx gk = pick16(g, k >> 3), gk1 = pick16(g, (k + 1) >> 3);
       if (q == (k & 7)) acc = aqc::cfma(s, gk, acc);
       if (q == (k & 7) && r == k) dS[k] = gk.x;  // G^(k)[k][k]
+#if AQC_S3_ROWSUM
+      // the row's eight partial products are in eight adjacent lanes of this wave: summed here
+      // (DPP, VALU slack -- the pass is LDS-bound), so phase B reads one value per row
+      acc.x = aqc::row_sum8(acc.x);
+      acc.y = aqc::row_sum8(acc.y);
+      if (q == 0) accp[r] = acc;
+#else
       accp[q * 128 + r] = acc;
+#endif
       if (q == ((k + 1) & 7)) gk1b[r] = gk1;
       if (AQC_S3_DIAG && tid == 832) t_c += __builtin_amdgcn_s_memtime() - t_c0;
     }
@@ -540,9 +566,13 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
     if (rr < 128) {
       const double beta = eS[k];
       const cplx ts = scal[1], scl = scal[0], sk = scal[2], g1 = gk1b[rr];
+#if AQC_S3_ROWSUM
+      cplx sum = accp[rr];
+#else
       cplx sum = aqc::cmk(0, 0);
 #pragma unroll
       for (int u = 0; u < 8; ++u) sum = aqc::cadd(sum, accp[u * 128 + rr]);
+#endif
       sum.x = fma(-beta, g1.x, sum.x);  // x_{k+1} = alpha where reflector k has alpha - beta
       sum.y = fma(-beta, g1.y, sum.y);
       const bool rowact = rr > k && rr < C, below = rr > k + 1 && rr < C;
