@@ -916,6 +916,10 @@ __device__ __forceinline__ void chain_theta(const TwoSiteJob& j) {
   const double* lmp = j.lm;
   const double* lrp = j.lr;
   asm volatile("" : "+s"(gp), "+s"(gq), "+s"(llp), "+s"(lmp), "+s"(lrp));
+  // the gate to the LDS (visible after the m loop's first barrier): read by the epilogue, where
+  // scalar loads of it waited out one scalar-cache round trip per 8 entries
+  __shared__ cplx sG[16];
+  if (tid < 16) sG[tid] = aqc::ldg(j.G + tid);
   cplx acc[4][2][2];
 #pragma unroll
   for (int q = 0; q < 4; ++q)
@@ -975,10 +979,10 @@ __device__ __forceinline__ void chain_theta(const TwoSiteJob& j) {
         if (l < chl && r < chr) {
 #pragma unroll
           for (int o = 0; o < 4; ++o) {
-            cplx v = aqc::cmul(j.G[o * 4 + 0], acc[0][i][jj]);
-            v = aqc::cfma(j.G[o * 4 + 1], acc[1][i][jj], v);
-            v = aqc::cfma(j.G[o * 4 + 2], acc[2][i][jj], v);
-            v = aqc::cfma(j.G[o * 4 + 3], acc[3][i][jj], v);
+            cplx v = aqc::cmul(sG[o * 4 + 0], acc[0][i][jj]);
+            v = aqc::cfma(sG[o * 4 + 1], acc[1][i][jj], v);
+            v = aqc::cfma(sG[o * 4 + 2], acc[2][i][jj], v);
+            v = aqc::cfma(sG[o * 4 + 3], acc[3][i][jj], v);
             aqc::stg(j.theta + (size_t)((o & 1) * chr + r) * M + (o >> 1) * chl + l, v);  // GLOBAL, not FLAT
           }
         }

@@ -53,6 +53,10 @@ __device__ unsigned long long g_gram_ticks[12];
 #ifndef AQC_S3_DIAG
 #define AQC_S3_DIAG 0
 #endif
+// S6: the next block's reflectors fetched after B4 (see the block loop)
+#ifndef AQC_S6_LATE_FETCH
+#define AQC_S6_LATE_FETCH 1
+#endif
 // S3: the reflectors' base pointer in SGPRs (as a VGPR pair it was spilled and reloaded per column)
 #ifndef AQC_S3_HH_SGPR
 #define AQC_S3_HH_SGPR 1
@@ -110,6 +114,13 @@ __device__ __forceinline__ double uniform_d(double v) {
   return __hiloint2double(hi, lo);
 }
 
+// this lane's index in the wave from the lane counter (mbcnt), recomputed where it is called
+// (the empty asm keeps it from being hoisted, and so from being spilled and reloaded)
+__device__ __forceinline__ int fresh_lane() {
+  int l = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+  asm volatile("" : "+v"(l));
+  return l;
+}
 // a wave-uniform pointer moved to SGPRs
 template <class T>
 __device__ __forceinline__ T* uniform_ptr(T* p) {
@@ -209,6 +220,7 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
   if (j.max_chi > 0 && j.max_chi < K) K = j.max_chi;
   // (j.work holds the packed reflectors, <= 8128 complex: capacity 64)
   const int tid = fresh_tid(), lane = tid & 63, wave = tid >> 6;
+  const int wave_s = __builtin_amdgcn_readfirstlane(wave);  // (uniform: an SGPR)
   if (tid == 0) atomicAdd(&g_gram_stats[0], 1ull);
   if (K > kGramMaxK || C < 4 || C > 128 || L > 128 || j.cap < 64) {
     if (tid == 0) atomicAdd(&g_gram_stats[2], 1ull);
@@ -264,9 +276,12 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
     auto fetch = [&](int ch) {  // this thread's element of chunk ch (zero outside X)
       const int kk = ch * KC + (tr ? tid >> 7 : tid & 7), c = tr ? tid & 127 : tid >> 3;
       if (kk >= L || c >= C) return aqc::cmk(0, 0);
-      return tr ? aqc::cconj(aqc::ldg(th + (size_t)kk * M + c)) : aqc::ldg(th + (size_t)c * M + kk);
+      // (raw: the conjugate of the transposed case is taken in stash, so that the load stays in
+      // flight during the chunk's MFMAs instead of being waited for here)
+      return tr ? aqc::ldg(th + (size_t)kk * M + c) : aqc::ldg(th + (size_t)c * M + kk);
     };
     auto stash = [&](int buf, cplx x) {
+      if (tr) x.y = -x.y;
       const int o = buf * BUF + (tr ? tid >> 7 : tid & 7) * PITCH + (tr ? tid & 127 : tid >> 3);
       sb[o] = x.x;
       sb[o + ARR] = x.y;
@@ -283,9 +298,12 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
       cplx xn = aqc::cmk(0, 0);
       if (more) xn = fetch(ch + 1);
       const double* cb = sb + (ch & 1) * BUF;
+      // the lane index from the lane counter, per chunk: derived from the (spilled) thread id, its
+      // reload's vmcnt wait drained the next chunk's load issued just above
+      const int fl = fresh_lane();
 #pragma unroll
       for (int ks = 0; ks < KC / 4; ++ks) {
-        const int row = (4 * ks + (lane >> 4)) * PITCH + (lane & 15);
+        const int row = (4 * ks + (fl >> 4)) * PITCH + (fl & 15);
 #pragma unroll
         for (int u = 0; u < 3; ++u) {
           if (tact[u]) {  // uniform per wave
@@ -937,10 +955,12 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
       const int e = tid + 1024 * u, row = e >> 4, i = e & 15;
       Yl[row * 16 + (i ^ (row & 15))] = ynx[u];
     }
+#if !AQC_S6_LATE_FETCH
     if (k0 > 0) {  // the next block's reflectors, in flight during this one
       const int n1 = k0, n0 = n1 > 16 ? n1 - 16 : 0;
       fetch_y(n0, n1 - n0, ynx);
     }
+#endif
     __syncthreads();  // B1: Y
     // Y^H V over this wave's 32 rows (and Y^H Y on the waves mg == nt, one per SIMD): A[m = i][k = row] = conj(Y[row][i])
     aqc::d4_t wr = {0, 0, 0, 0}, wi = {0, 0, 0, 0}, sr = {0, 0, 0, 0}, si = {0, 0, 0, 0};
@@ -996,7 +1016,7 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // LDS: S written, partials read
       {  // lane (a, g): T[a][g + 4 m] (m < 4) in registers; each column's sum over b splits over
          // the quad g = 0..3 (T[a][b] = 0 for b < a falls out of the recurrence)
-        const int a = lane >> 2, g = lane & 3;
+        const int fl = fresh_lane(), a = fl >> 2, g = fl & 3;  // (fresh: no spilled addresses)
         cplx tq[4] = {aqc::cmk(0, 0), aqc::cmk(0, 0), aqc::cmk(0, 0), aqc::cmk(0, 0)};
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
@@ -1028,16 +1048,28 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
       W2l[i * 64 + lane] = acc;
     }
     __syncthreads();  // B4: W2
-    // V -= Y W2: A[m = row][k = b] = Y[row][b], B[k = b][n] = W2[b][n]
+#if AQC_S6_LATE_FETCH
+    // the next block's reflectors, in flight during the V update: issued before B1 they were
+    // drained by the spill reloads' vmcnt(0) waits between B1 and B4
+    if (k0 > 0) {
+      const int n1 = k0, n0 = n1 > 16 ? n1 - 16 : 0;
+      fetch_y(n0, n1 - n0, ynx);
+    }
+#endif
+    // V -= Y W2: A[m = row][k = b] = Y[row][b], B[k = b][n] = W2[b][n].  The lane's indices come
+    // from the lane counter and the wave index in an SGPR: derived from the thread id (whose VGPR
+    // is spilled) their reload's vmcnt(0) drained the next block's reflector loads issued above
+    const int vl_ = fresh_lane();
+    const int vmg = wave_s >> 2, vnt = wave_s & 3, vli = vl_ & 15, vlk = vl_ >> 4;
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
-      if (32 * mg + 16 * t + 15 > k0) {
-        const int row = 32 * mg + 16 * t + li;
+      if (32 * vmg + 16 * t + 15 > k0) {
+        const int row = 32 * vmg + 16 * t + vli;
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
-          const int b = 4 * s + lk;
+          const int b = 4 * s + vlk;
           const cplx y = Yl[row * 16 + (b ^ (row & 15))];
-          const cplx w = W2l[b * 64 + 16 * nt + li];
+          const cplx w = W2l[b * 64 + 16 * vnt + vli];
           vre[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(-y.x, w.x, vre[t], 0, 0, 0);
           vre[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(y.y, w.y, vre[t], 0, 0, 0);
           vim[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(-y.x, w.y, vim[t], 0, 0, 0);
