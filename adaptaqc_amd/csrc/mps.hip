@@ -13,6 +13,7 @@
 // update of every state in the batch (blockIdx.y / blockIdx.x = job).
 #include <algorithm>
 #include <cmath>
+#include <chrono>
 #include <cstring>
 #include <atomic>
 #include <cstdlib>
@@ -1475,14 +1476,15 @@ struct Scheduler {
   }
 };
 
-// Host-side per-state work (scheduling, job building) over a few threads: a batch of 1024 states
-// takes ~2 ms on one core, during which the GPU would idle.  AQC_HOST_THREADS overrides the count
-// (default 8; 1 = serial).  f(s) must touch only state s's data.
+// Host-side per-state work (scheduling, job building), optionally over a few threads
+// (AQC_HOST_THREADS; f(s) must touch only state s's data).  Default 1: on the MI355X box a batch of
+// 1024 states took 0.5 ms to schedule and 0.4 ms to build on one thread, 0.9 + 0.9 ms on eight
+// (thread start-up and allocator contention outweigh the ~1 ms of work; AQC_HOST_TIMING=1).
 template <class F>
 void parallel_states(int ns, F&& f) {
   static const int kThreads = [] {
     const char* e = std::getenv("AQC_HOST_THREADS");
-    const int v = e ? std::atoi(e) : 8;
+    const int v = e ? std::atoi(e) : 1;
     return v < 1 ? 1 : (v > 64 ? 64 : v);
   }();
   const int nt = std::min(kThreads, ns / 32);
@@ -2475,21 +2477,39 @@ int aqc_mps_copy(aqc_mps_t dst, const aqc_mps_t src) {
   return AQC_OK;
 }
 
+// AQC_HOST_TIMING=1: host-side phase times of each batched apply to stderr (lab diagnostics)
+bool host_timing() {
+  static const bool on = [] {
+    const char* e = std::getenv("AQC_HOST_TIMING");
+    return e && std::strcmp(e, "0") != 0;
+  }();
+  return on;
+}
+double host_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 int apply_batch_impl(aqc_mps_t* hs, int ns, const aqc_op_t* const* ops, const int* nops, bool sort_after,
                      bool check = true) {
   AQC_REQUIRE(hs && ops && nops && ns >= 0, "aqc_mps_apply_batch: null argument");
+  const double t0 = host_timing() ? host_ms() : 0.0;
   std::vector<std::vector<DevOp>> lists(ns);
   for (int s = 0; s < ns; ++s) {
     AQC_REQUIRE(hs[s], "aqc_mps_apply_batch: null handle");
     int rc = validate_ops(hs[s], ops[s], nops[s]);
     if (rc != AQC_OK) return rc;
   }
+  const double t1 = host_timing() ? host_ms() : 0.0;
   if (distinct_handles(hs, ns)) {
     parallel_states(ns, [&](int s) { schedule(hs[s], ops[s], nops[s], sort_after, lists[s]); });
   } else {  // a state listed twice: its op lists apply in order
     for (int s = 0; s < ns; ++s) schedule(hs[s], ops[s], nops[s], sort_after, lists[s]);
   }
+  const double t2 = host_timing() ? host_ms() : 0.0;
   int rc = run_waves(hs, ns, lists);
+  if (host_timing())
+    std::fprintf(stderr, "[aqc host] apply %d states: validate %.3f ms, schedule %.3f ms, jobs+launch %.3f ms\n", ns,
+                 t1 - t0, t2 - t1, host_ms() - t2);
   if (rc != AQC_OK) return rc;
   return check ? check_flags_batch(hs, ns) : AQC_OK;
 }

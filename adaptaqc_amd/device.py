@@ -211,23 +211,41 @@ def _handles(states):
     return arr
 
 
+class OpsBatch:
+    """Per-state op lists marshalled once for the C ABI: the pointer array and the counts that
+    apply_batch would otherwise rebuild from the Python list on every call (1-2 ms for 1024 lists,
+    mostly ``ndarray.ctypes``).  It holds references to its arrays, so their contents may be
+    rewritten in place between calls (new angles) and the batch stays valid; replacing an array
+    needs a new OpsBatch."""
+
+    def __init__(self, ops_lists):
+        self.arrays = [np.ascontiguousarray(o) if isinstance(o, np.ndarray) else _lib.ops_array(o)
+                       for o in ops_lists]
+        self.ptrs = (ctypes.c_void_p * len(self.arrays))(*[a.ctypes.data if len(a) else 0 for a in self.arrays])
+        self.counts = np.asarray([len(a) for a in self.arrays], dtype=np.int32)
+
+    def __len__(self):
+        return len(self.arrays)
+
+
 def apply_batch(states, ops_lists, sort=False, wait=True):
     """Apply per-state op lists (one batched launch sequence, or one fused chain per state); with
     sort=True every state also returns to sorted qubit order in the same schedule (an evaluation's
-    replay + save).  wait=False (sort=True only) returns once the work is queued; call
-    check_batch(states) before using the states."""
+    replay + save).  ops_lists: a list of op lists / ops arrays, or an OpsBatch.  wait=False
+    (sort=True only) returns once the work is queued; call check_batch(states) before using the
+    states."""
     if not states:
         return
     l = _lib.lib()
-    arrs = [o if isinstance(o, np.ndarray) else _lib.ops_array(o) for o in ops_lists]
-    ptrs = (ctypes.c_void_p * len(arrs))(*[a.ctypes.data if len(a) else 0 for a in arrs])
-    counts = np.asarray([len(a) for a in arrs], dtype=np.int32)
+    batch = ops_lists if isinstance(ops_lists, OpsBatch) else OpsBatch(ops_lists)
+    if len(batch) != len(states):
+        raise ValueError("apply_batch: one op list per state")
     if not wait and not sort:
         raise ValueError("apply_batch: wait=False needs sort=True")
     fn = l.aqc_mps_apply_sort_batch if sort else l.aqc_mps_apply_batch
     if not wait:
         fn = l.aqc_mps_apply_sort_batch_async
-    _lib.check(fn(_handles(states), len(states), ptrs, _lib.ptr(counts)))
+    _lib.check(fn(_handles(states), len(states), batch.ptrs, _lib.ptr(batch.counts)))
 
 
 def check_batch(states):

@@ -279,7 +279,8 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     from adaptaqc_amd import _lib
-    from adaptaqc_amd.device import DeviceMPS, apply_batch, check_batch, copy_batch, overlap_zero_batch, pair_grads_batch
+    from adaptaqc_amd.device import (DeviceMPS, OpsBatch, apply_batch, check_batch, copy_batch, overlap_zero_batch,
+                                     pair_grads_batch)
     from adaptaqc_amd.sharding import PairShard, gather_scores
     from adaptaqc_amd.utils.constants import coupling_map_fully_entangled
 
@@ -309,6 +310,9 @@ def main():
             ang = rng.uniform(-np.pi, np.pi, 4)
             layer_angles.append(ang)
             layer_ops.append(_lib.ops_array(thin_layer_ops(LAYER_A, LAYER_A + d, ang)))
+    # the op lists marshalled for the C ABI once (device.OpsBatch), as a caller re-evaluating the
+    # same layer structure would (angles can change in place); the replay itself runs every step
+    layer_batch = OpsBatch(layer_ops)
     prio = np.ones(len(cmap))
     local_scores = torch.zeros((S, max(len(shard.local_pairs), 1)), dtype=torch.float64, device="cuda")
     prio_t = torch.as_tensor(prio, device="cuda")
@@ -327,7 +331,7 @@ def main():
     def overlaps():
         # (ii) overlap evals on own states: reload the cached MPS, replay + save, <0|psi>
         copy_batch(work, reload_src)
-        apply_batch(work, layer_ops, sort=True)
+        apply_batch(work, layer_batch, sort=True)
         return 1.0 - np.abs(overlap_zero_batch(work)) ** 2
 
     def step():
@@ -338,7 +342,7 @@ def main():
         # two): the overlap kernel's launch is prepared while the chain runs.  (Queuing the chain
         # before the sweep measured no better: the step is GPU-bound, 59-60 ms either way.)
         copy_batch(work, reload_src)
-        apply_batch(work, layer_ops, sort=True, wait=False)
+        apply_batch(work, layer_batch, sort=True, wait=False)
         costs = 1.0 - np.abs(overlap_zero_batch(work)) ** 2
         check_batch(work)
         return full, best, costs

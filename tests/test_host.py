@@ -216,3 +216,24 @@ def test_isl_pair_selection_host_logic(monkeypatch):
     comp.entanglement_measures_history.append(tiny)
     comp.qubit_pair_history.append(pick)
     assert comp._find_best_entanglement_qubit_pair(tiny) == "expectation"
+
+
+def test_ops_batch_marshalling():
+    """device.OpsBatch: one pointer and count per op list, pointing at the held arrays (so in-place
+    angle updates are seen by the next apply), lists converted like apply_batch's."""
+    import ctypes
+
+    from adaptaqc_amd import _lib, gates
+    from adaptaqc_amd.device import OpsBatch
+
+    lists = [[(gates.one_qubit("rx", [0.1 * k]), (0,)), (gates.TWO_QUBIT["cx"], (0, 1))] for k in range(5)]
+    lists.append([])
+    arrs = [_lib.ops_array(o) for o in lists[:3]] + lists[3:]
+    b = OpsBatch(arrs)
+    assert len(b) == 6
+    assert list(b.counts) == [2, 2, 2, 2, 2, 0]
+    assert b.arrays[0] is arrs[0]  # held, not copied: in-place updates stay visible
+    for k in range(3):
+        assert b.ptrs[k] == arrs[k].ctypes.data
+    assert b.ptrs[5] in (None, 0)
+    assert isinstance(b.ptrs, ctypes.Array)
