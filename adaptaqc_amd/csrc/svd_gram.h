@@ -560,7 +560,9 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
 #endif
       // the product used x_k = -s (z_k = 0, v_k = 1) where reflector k has 0 (and x_{k+1} = alpha
       // where it has alpha - beta: corrected in phase B): one entry in the lane holding column k
-      const cplx gk = pick16(g, k >> 3), gk1 = pick16(g, (k + 1) >> 3);
+      // (k + 1) >> 3 == k >> 3 except every eighth column: the same register, so one pick
+      const cplx gk = pick16(g, k >> 3);
+      const cplx gk1 = ((k + 1) & 7) ? gk : pick16(g, (k + 1) >> 3);
       if (q == (k & 7)) acc = aqc::cfma(s, gk, acc);
       if (q == (k & 7) && r == k) dS[k] = gk.x;  // G^(k)[k][k]
 #if AQC_S3_ROWSUM
