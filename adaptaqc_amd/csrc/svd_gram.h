@@ -41,6 +41,10 @@ constexpr int kGramMaxK = 64;
 #define AQC_S3_PRIO 1
 #endif
 // S5: the LDL^T pivots from the leading minors' recurrence (one FMA + the guard on the chain)
+// S5: inverse-iteration steps per eigenvector
+#ifndef AQC_S5_ITERS
+#define AQC_S5_ITERS 3
+#endif
 #ifndef AQC_S5_POLY
 #define AQC_S5_POLY 1
 #endif
@@ -792,7 +796,7 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
       for (; r0 < C; ++r0) fac_row(r0, s_d[r0], s_e2[max(r0 - 1, 0)], rdp);
     }
     double sc = 1.0;  // the previous iteration's normalisation, applied as the forward solve reads
-    for (int it = 0; it < 3; ++it) {
+    for (int it = 0; it < AQC_S5_ITERS; ++it) {
       // forward solve L y = sc z in place (L_{row, row-1} = e_{row-1} / D_{row-1}), then L^T-solve
       // z = D^-1 y - L^T z from the bottom
       // (one dependent FMA per row in both solves: the row's coefficients -e_{r-1} / D_{r-1} and
