@@ -268,13 +268,30 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
     const int nt = (C + 15) >> 4, ntile = nt * (nt + 1) / 2;
     int tI[3], tJ[3];
     bool tact[3];
+    // C = 128 (nt = 8): each wave's tiles share their row block, so the wave reads the A operands
+    // once per step for all its tiles (12 instead of 18 LDS operand reads; the pass is LDS-bound);
+    // 15 waves of 1-3 tiles, 9 tiles per SIMD (wave w on SIMD w % 4).  Entry: row block,
+    // first column block, tile count.
+    const bool rs = nt == 8;  // uniform
+    if (rs) {
+      constexpr unsigned kTab[16] = {0x300, 0x322, 0x333, 0x355, 0x330, 0x352, 0x241, 0x244,
+                                     0x311, 0x260, 0x261, 0x264, 0x000, 0x177, 0x263, 0x266};
+      const unsigned e = kTab[wave];
 #pragma unroll
-    for (int u = 0; u < 3; ++u) {  // tile t -> (ti <= tj), row-major over the upper triangle
-      int t = wave + 16 * u, ti = 0;
-      tact[u] = t < ntile;
-      while (tact[u] && t >= nt - ti) t -= nt - ti++;
-      tI[u] = ti;
-      tJ[u] = ti + t;
+      for (int u = 0; u < 3; ++u) {
+        tact[u] = u < (int)(e >> 8);
+        tI[u] = e & 15;
+        tJ[u] = ((e >> 4) & 15) + u;
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < 3; ++u) {  // tile t -> (ti <= tj), row-major over the upper triangle
+        int t = wave + 16 * u, ti = 0;
+        tact[u] = t < ntile;
+        while (tact[u] && t >= nt - ti) t -= nt - ti++;
+        tI[u] = ti;
+        tJ[u] = ti + t;
+      }
     }
     const int nch = (L + KC - 1) / KC;
     auto fetch = [&](int ch) {  // this thread's element of chunk ch (zero outside X)
@@ -308,13 +325,27 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
 #pragma unroll
       for (int ks = 0; ks < KC / 4; ++ks) {
         const int row = (4 * ks + (fl >> 4)) * PITCH + (fl & 15);
+        if (rs) {  // uniform: the row block's operands once, then each tile's column block
+          const int oi = row + 16 * tI[0];
+          const double ar = cb[oi], ai = cb[ARR + oi], as = cb[2 * ARR + oi];
 #pragma unroll
-        for (int u = 0; u < 3; ++u) {
-          if (tact[u]) {  // uniform per wave
-            const int oi = row + 16 * tI[u], oj = row + 16 * tJ[u];
-            p1[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(cb[oi], cb[oj], p1[u], 0, 0, 0);
-            p2[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(cb[ARR + oi], cb[ARR + oj], p2[u], 0, 0, 0);
-            p3[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(cb[2 * ARR + oi], cb[3 * ARR + oj], p3[u], 0, 0, 0);
+          for (int u = 0; u < 3; ++u) {
+            if (tact[u]) {  // uniform per wave
+              const int oj = row + 16 * tJ[u];
+              p1[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(ar, cb[oj], p1[u], 0, 0, 0);
+              p2[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(ai, cb[ARR + oj], p2[u], 0, 0, 0);
+              p3[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(as, cb[3 * ARR + oj], p3[u], 0, 0, 0);
+            }
+          }
+        } else {
+#pragma unroll
+          for (int u = 0; u < 3; ++u) {
+            if (tact[u]) {  // uniform per wave
+              const int oi = row + 16 * tI[u], oj = row + 16 * tJ[u];
+              p1[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(cb[oi], cb[oj], p1[u], 0, 0, 0);
+              p2[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(cb[ARR + oi], cb[ARR + oj], p2[u], 0, 0, 0);
+              p3[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(cb[2 * ARR + oi], cb[3 * ARR + oj], p3[u], 0, 0, 0);
+            }
           }
         }
       }
