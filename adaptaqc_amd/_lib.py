@@ -3,6 +3,7 @@
 The HIP library is the only compute path: if it is missing or no GPU is visible, every
 backend call raises ``AqcError`` -- there is no CPU fallback.
 """
+import atexit
 import ctypes
 import os
 import threading
@@ -35,6 +36,7 @@ EXPORTS = (
     "aqc_sweep_set_chain_mode", "aqc_mps_set_jacobi_noise", "aqc_stream_join", "aqc_stream_wait", "aqc_svd_gram_stats",
     "aqc_comm_unique_id", "aqc_comm_init", "aqc_comm_destroy", "aqc_comm_rank", "aqc_allgather_f64",
     "aqc_allgather_f64_host", "aqc_allreduce_max_f64", "aqc_svd_gram_big_stats", "aqc_svd_gram_big_ticks",
+    "aqc_gb_set_spin_limit", "aqc_debug_hog",
 )
 
 
@@ -122,6 +124,8 @@ _SIGS = {
     "aqc_mps_set_jacobi_noise": ([_D], _I),
     "aqc_svd_gram_big_stats": ([_P], _I),
     "aqc_svd_gram_big_ticks": ([_P], _I),
+    "aqc_gb_set_spin_limit": ([_D], _I),
+    "aqc_debug_hog": ([_I, _D], _I),
 }
 
 
@@ -169,8 +173,17 @@ def lib():
     dev = device_index()
     if _initialised_device != dev:
         check(l.aqc_init(dev))
+        if _initialised_device is None:
+            # drain the device and release the library's lazily created streams / events / buffer
+            # sets before the interpreter (and the HIP runtime) tear down
+            atexit.register(_finalize)
         _initialised_device = dev
     return l
+
+
+def _finalize():
+    if _lib is not None:
+        _lib.aqc_finalize()
 
 
 def ptr(a):

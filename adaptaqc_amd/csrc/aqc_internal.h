@@ -143,6 +143,14 @@ __device__ __forceinline__ double group_sum(double v) {
   else return row_sum16(v);
 }
 
+// ---- teardown ----------------------------------------------------------------------------
+// Lazily created HIP objects (side streams, events, cached buffer sets) register a cleanup here
+// when they are first created; aqc_finalize synchronises every device the library touched, runs
+// the cleanups (newest first) and forgets them, so the objects are recreated on next use.  The
+// Python loader calls aqc_finalize from atexit, before the HIP runtime's own teardown.
+void on_finalize(void (*fn)());
+void note_device(int dev);
+
 // ---- kernel timing (HIP events on the launching stream) ------------------------------
 struct KernelTimer {
   // Begin/End bracket one launch on `stream` when timing is enabled.

@@ -621,9 +621,17 @@ struct BJBuffers {
   int cap = 0;
 };
 
+BJBuffers g_bj_buffers;
+void release_bj_buffers() {
+  BJBuffers& b = g_bj_buffers;
+  if (b.st) (void)hipFree(b.st);
+  if (b.ndone) (void)hipFree(b.ndone);
+  if (b.host) (void)hipHostFree(b.host);
+  b = BJBuffers();
+}
 BJBuffers& bj_buffers() {
-  static BJBuffers b;
-  return b;
+  aqc::on_finalize(release_bj_buffers);
+  return g_bj_buffers;
 }
 
 template <int MAXR>

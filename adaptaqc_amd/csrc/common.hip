@@ -1,4 +1,11 @@
-// Library-wide state: error strings, device selection, per-family kernel timing.
+// Library-wide state: error strings, device selection, per-family kernel timing, teardown.
+#include <execinfo.h>
+#include <signal.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <cstdlib>
+#include <cstring>
 #include <map>
 #include <mutex>
 
@@ -9,6 +16,57 @@ namespace aqc {
 static thread_local std::string g_last_error;
 
 void set_error(const std::string& msg) { g_last_error = msg; }
+
+namespace {
+std::mutex g_fin_mutex;
+std::vector<void (*)()> g_fin;         // cleanups, in registration order
+std::atomic<unsigned long long> g_devs{0};  // bit d: device d was used
+}  // namespace
+
+void on_finalize(void (*fn)()) {
+  std::lock_guard<std::mutex> lk(g_fin_mutex);
+  for (auto f : g_fin)
+    if (f == fn) return;
+  g_fin.push_back(fn);
+}
+
+void note_device(int dev) {
+  if (dev >= 0 && dev < 64) g_devs.fetch_or(1ull << dev);
+}
+
+namespace {
+// Fatal-signal report: the signal and a native backtrace on stderr, then the previous handler
+// (Python's faulthandler, the default action) runs as if we had never been there.  Installed when
+// the library is loaded unless AQC_CRASH_TRACE=0.
+struct sigaction g_old_segv, g_old_bus, g_old_abrt;
+void crash_handler(int sig, siginfo_t* si, void* uc) {
+  (void)uc;
+  char msg[128];
+  const int n = snprintf(msg, sizeof(msg), "libaqchip: fatal signal %d (fault address %p), native backtrace:\n", sig,
+                         si ? si->si_addr : nullptr);
+  if (n > 0) (void)!write(2, msg, (size_t)n);
+  void* frames[64];
+  const int nf = backtrace(frames, 64);
+  backtrace_symbols_fd(frames, nf, 2);
+  const struct sigaction* old = sig == SIGSEGV ? &g_old_segv : sig == SIGBUS ? &g_old_bus : &g_old_abrt;
+  sigaction(sig, old, nullptr);
+  raise(sig);
+}
+__attribute__((constructor)) void install_crash_handler() {
+  const char* e = std::getenv("AQC_CRASH_TRACE");
+  if (e && std::strcmp(e, "0") == 0) return;
+  void* warm[2];
+  (void)backtrace(warm, 2);  // loads libgcc's unwinder now, not inside the handler
+  struct sigaction sa;
+  std::memset(&sa, 0, sizeof(sa));
+  sa.sa_sigaction = crash_handler;
+  sa.sa_flags = SA_SIGINFO;
+  sigemptyset(&sa.sa_mask);
+  sigaction(SIGSEGV, &sa, &g_old_segv);
+  sigaction(SIGBUS, &sa, &g_old_bus);
+  sigaction(SIGABRT, &sa, &g_old_abrt);
+}
+}  // namespace
 
 namespace {
 struct PendingEvent {
@@ -68,9 +126,42 @@ void KernelTimer::end(hipStream_t stream) {
   if (g_pending.size() > 4096) drain_locked();
 }
 
+// Test load: every workgroup holds its CU for a staggered time (block b: (b % 16 + 1) / 16 of
+// `ticks`), so that kernels queued behind it on other streams get their workgroups dispatched one
+// CU at a time -- the late-start case of the multi-workgroup exchanges (gram_big.hip).
+__global__ __launch_bounds__(256) void k_hog(unsigned long long ticks) {
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  const unsigned long long lim = ticks * (unsigned long long)(blockIdx.x % 16 + 1) / 16ull;
+  while (__builtin_amdgcn_s_memrealtime() - t0 < lim) __builtin_amdgcn_s_sleep(8);
+}
+
+namespace {
+hipStream_t g_hog_stream[64] = {nullptr};
+void release_hog_streams() {
+  for (auto& s : g_hog_stream)
+    if (s) (void)hipStreamDestroy(s), s = nullptr;
+}
+}  // namespace
+
 }  // namespace aqc
 
 extern "C" {
+
+int aqc_debug_hog(int nblocks, double ms) {
+  AQC_REQUIRE(nblocks > 0 && nblocks <= 65536 && ms >= 0 && ms <= 1000, "aqc_debug_hog: bad arguments");
+  int dev = 0;
+  AQC_HIP_CHECK(hipGetDevice(&dev));
+  AQC_REQUIRE(dev >= 0 && dev < 64, "aqc_debug_hog: device index out of range");
+  if (!aqc::g_hog_stream[dev]) {
+    AQC_HIP_CHECK(hipStreamCreateWithFlags(&aqc::g_hog_stream[dev], hipStreamNonBlocking));
+    aqc::note_device(dev);
+    aqc::on_finalize(aqc::release_hog_streams);
+  }
+  hipLaunchKernelGGL(aqc::k_hog, dim3(nblocks), dim3(256), 0, aqc::g_hog_stream[dev],
+                     (unsigned long long)(ms * 1e5));
+  AQC_CHECK_LAUNCH();
+  return AQC_OK;
+}
 
 const char* aqc_last_error(void) { return aqc::g_last_error.c_str(); }
 
@@ -81,13 +172,36 @@ int aqc_init(int device) {
   AQC_HIP_CHECK(hipGetDeviceCount(&count));
   AQC_REQUIRE(device >= 0 && device < count, "aqc_init: device index out of range");
   AQC_HIP_CHECK(hipSetDevice(device));
+  aqc::note_device(device);
   return AQC_OK;
 }
 
 int aqc_finalize(void) {
-  std::lock_guard<std::mutex> lk(aqc::g_timing_mutex);
-  aqc::drain_locked();
-  return AQC_OK;
+  {
+    std::lock_guard<std::mutex> lk(aqc::g_timing_mutex);
+    aqc::drain_locked();
+  }
+  // every device the library used: drain all its streams (the side streams' kernels are ordered
+  // only by events), then release the lazily created objects
+  int cur = 0;
+  const bool have_cur = hipGetDevice(&cur) == hipSuccess;
+  const unsigned long long devs = aqc::g_devs.load();
+  int rc = AQC_OK;
+  for (int d = 0; d < 64; ++d) {
+    if (!(devs >> d & 1ull)) continue;
+    if (hipSetDevice(d) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+      aqc::set_error("aqc_finalize: device synchronisation failed");
+      rc = AQC_ERR_HIP;
+    }
+  }
+  if (have_cur) (void)hipSetDevice(cur);
+  std::vector<void (*)()> fin;
+  {
+    std::lock_guard<std::mutex> lk(aqc::g_fin_mutex);
+    fin.swap(aqc::g_fin);
+  }
+  for (auto it = fin.rbegin(); it != fin.rend(); ++it) (*it)();
+  return rc;
 }
 
 int aqc_timing_enable(int on) {

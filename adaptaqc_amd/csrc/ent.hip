@@ -354,11 +354,18 @@ struct RdmBuffers {
   size_t cap = 0;
 };
 
+RdmBuffers g_rbuf[64];
+void release_rbuf() {
+  for (auto& b : g_rbuf) {
+    if (b.dev) (void)hipFree(b.dev);
+    b = RdmBuffers();
+  }
+}
 RdmBuffers& rbuf() {
-  static RdmBuffers b[64];
   int dev = 0;
   hipGetDevice(&dev);
-  return b[dev];
+  aqc::on_finalize(release_rbuf);
+  return g_rbuf[dev];
 }
 
 int ensure(RdmBuffers& b, size_t need) {

@@ -625,8 +625,8 @@ __device__ void top_pair_2x2(const cplx F[4], cplx u[2], cplx v[2], double& sigm
 __global__ __launch_bounds__(kT) void k_product_fit(const FitJob* __restrict__ jobs) {
   const FitJob& j = jobs[blockIdx.x];
   const int n = j.n, cap = j.cap, tid = threadIdx.x;
-  __shared__ cplx vec[256];       // running l (left-to-right) or r (right-to-left)
-  __shared__ cplx uw[2][2][256];  // u[s][m], w[s][m]
+  __shared__ cplx vec[aqc::kMaxCap];       // running l (left-to-right) or r (right-to-left)
+  __shared__ cplx uw[2][2][aqc::kMaxCap];  // u[s][m], w[s][m]
   __shared__ cplx part[4][kT / 64];
   __shared__ cplx sv[2][2];       // the updated pair
   __shared__ double fid_s;
@@ -797,11 +797,23 @@ struct GradRing {
   int next = 0;
 };
 
+GradRing g_gring[64];
+void release_gring() {
+  for (auto& r : g_gring)
+    for (auto& b : r.b) {
+      if (b.done) (void)hipEventDestroy(b.done);
+      if (b.dev) (void)hipFree(b.dev);
+      if (b.host) (void)hipHostFree(b.host);
+      b.done = nullptr, b.dev = nullptr, b.host = nullptr;
+      b.cap = b.hcap = 0;
+      b.pending = false;
+    }
+}
 GradRing& gring() {
-  static GradRing g[64];
   int dev = 0;
   hipGetDevice(&dev);
-  return g[dev];
+  aqc::on_finalize(release_gring);
+  return g_gring[dev];
 }
 
 int grad_buffers(GradBuffers& gb, size_t need) {
@@ -845,6 +857,7 @@ int ensure_gw(aqc_mps_t h) {
 // (tools/single_sweep_timing.py).
 int g_chain_mode = 0;
 bool use_segments(int cap, int ns) {
+  if (cap > 256) return true;  // (one state: aqc_pair_grads_batch splits larger batches)
   return ns == 1 && cap >= 16 && (g_chain_mode == 3 || (g_chain_mode == 0 && cap > 64));
 }
 bool use_chain8(int cap, int ns) {
@@ -889,8 +902,18 @@ int aqc_pair_grads_batch(aqc_mps_t* psis, int ns, const double* svec, const int*
   const int n = psis[0]->d.n;
   for (int s = 0; s < ns; ++s) AQC_REQUIRE(psis[s] && psis[s]->d.n == n, "aqc_pair_grads_batch: all states need n qubits");
   for (int s = 0; s < ns; ++s)
-    AQC_REQUIRE(psis[s]->d.cap <= 256 && psis[s]->d.cap == psis[0]->d.cap,
-                "aqc_pair_grads_batch: states need one bond capacity <= 256");
+    AQC_REQUIRE(psis[s]->d.cap == psis[0]->d.cap, "aqc_pair_grads_batch: states need one bond capacity");
+  if (psis[0]->d.cap > 256 && ns > 1) {
+    // capacities above 256 (the unbounded MPS of aer_mps_backend.py:27-42 grows to 512): the chain
+    // kernels hold a row vector per lane group up to 256 only, the segmented single-state sweep is
+    // capacity-agnostic -- one state at a time through it
+    for (int s = 0; s < ns; ++s) {
+      const int rc = aqc_pair_grads_batch(psis + s, 1, svec, pairs, npairs, u0, gens, degs, ngen,
+                                          out + (size_t)s * npairs, out_is_device);
+      if (rc != AQC_OK) return rc;
+    }
+    return AQC_OK;
+  }
   for (int p = 0; p < npairs; ++p) {
     const int a = pairs[2 * p], b = pairs[2 * p + 1];
     AQC_REQUIRE(a >= 0 && a < n && b >= 0 && b < n && a != b, "aqc_pair_grads_batch: bad pair");
@@ -1046,7 +1069,7 @@ int aqc_pair_grads(aqc_mps_t psi, const double* svec, const int* pairs, int npai
 int aqc_mps_product_fit(aqc_mps_t psi, double* svec, int guess_from_gamma, int min_sweeps, int max_sweeps,
                         double tol, double* fidelity, int* sweeps) {
   AQC_REQUIRE(psi && svec && max_sweeps >= 1 && min_sweeps >= 0 && tol >= 0.0, "aqc_mps_product_fit: bad arguments");
-  AQC_REQUIRE(psi->d.cap <= 256, "aqc_mps_product_fit: bond capacity above 256");
+  AQC_REQUIRE(psi->d.cap <= aqc::kMaxCap, "aqc_mps_product_fit: bond capacity above the library's maximum");
   int rc = aqc_mps_sort(psi);  // the fit runs in qubit order
   if (rc != AQC_OK) return rc;
   rc = ensure_gw(psi);
@@ -1116,6 +1139,14 @@ int aqc_argmax_scaled(const double* scores, const double* prio, int count, int s
     size_t cap = 0;  // doubles
   };
   static ArgmaxBuf bufs[64];
+  static void (*release)() = [] {
+    for (auto& b : bufs) {
+      if (b.dev) (void)hipFree(b.dev);
+      if (b.host) (void)hipHostFree(b.host);
+      b.dev = nullptr, b.host = nullptr, b.cap = 0;
+    }
+  };
+  aqc::on_finalize(release);
   int devi = 0;
   hipGetDevice(&devi);
   ArgmaxBuf& ab = bufs[devi];

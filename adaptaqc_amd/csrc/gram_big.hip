@@ -54,6 +54,8 @@ namespace {
 
 constexpr double kGbRelFloor = 1e-9;
 constexpr unsigned long long kSpinTicks = 10000000ull;  // s_memrealtime (100 MHz): 100 ms
+// the counter-wait limit in force (aqc_gb_set_spin_limit: tests force the timeout decline with 0)
+unsigned long long g_gb_spin = kSpinTicks;
 
 typedef __attribute__((address_space(1))) double gdbl;
 typedef __attribute__((address_space(1))) unsigned gu32;
@@ -86,6 +88,7 @@ struct GBArgs {
   cplx* xch;       // per job 4 x CT: p (two buffers), old row k + 1 (two buffers)
   unsigned* cnt;   // per job 32 words (128 B)
   int* status;     // per job: 0 ok, 1 declined (gram off / shape), 2 floor, 3 exchange timeout
+  unsigned long long spin;  // counter-wait limit (s_memrealtime ticks, 100 MHz) before a timeout
 };
 
 __device__ __forceinline__ double wave_sum_b(double v) {
@@ -366,16 +369,22 @@ __global__ __launch_bounds__(1024) void k_gb_tridiag(const TwoSiteJob* __restric
       const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
       while (__hip_atomic_load((gu32*)cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
         __builtin_amdgcn_s_sleep(1);
-        if (__builtin_amdgcn_s_memrealtime() - t0 > kSpinTicks) {
+        if (__builtin_amdgcn_s_memrealtime() - t0 > a.spin) {
           s_abort = 1;
           break;
         }
       }
     }
     // reflector k to row k of the scratch, each workgroup its own CT / P contiguous entries (a
-    // strided store here held the next publish wait: the stores must finish before it)
-    if (tid > k && tid / (CT / P) == g) stg(G + (size_t)k * CT + tid, vt);
+    // strided store here held the next publish wait: the stores must finish before it).  Row 0 is
+    // read at entry by every workgroup of the job (rhoL, and workgroup 0's register rows), so at
+    // k = 0 the store waits for the barrier behind thread 0's counter wait: only then has every
+    // workgroup published column 0, i.e. passed its entry loads.  From k = 1 on this workgroup has
+    // already seen step k - 1's full count, so every workgroup is past its entry.
+    const bool own_row = tid > k && tid / (CT / P) == g;
+    if (k > 0 && own_row) stg(G + (size_t)k * CT + tid, vt);
     __syncthreads();
+    if (k == 0 && own_row && !s_abort) stg(G + tid, vt);
     if (s_abort) {
       if (tid == 0 && g == 0) {
         *(gi32*)(a.status + jb) = 3;
@@ -927,17 +936,19 @@ struct GBBuffers {
   TwoSiteJob* hjobs = nullptr;  // pinned
 };
 
-GBBuffers& gb_buffers() {
-  static GBBuffers b;
-  return b;
-}
-
 void gb_free(GBBuffers& b) {
   hipFree(b.G), hipFree(b.d), hipFree(b.e), hipFree(b.z), hipFree(b.dinv), hipFree(b.sig2), hipFree(b.tau);
   hipFree(b.lam), hipFree(b.tn), hipFree(b.tfac), hipFree(b.yc);
   hipFree(b.xch), hipFree(b.cnt), hipFree(b.status), hipFree(b.djobs);
   hipHostFree(b.host_status), hipHostFree(b.hjobs);
   b = GBBuffers();
+}
+
+GBBuffers g_gb_buffers;
+void release_gb_buffers() { gb_free(g_gb_buffers); }
+GBBuffers& gb_buffers() {
+  aqc::on_finalize(release_gb_buffers);
+  return g_gb_buffers;
 }
 
 int gb_ensure(GBBuffers& b, int ct, int nj, hipStream_t st) {
@@ -967,22 +978,36 @@ int gb_ensure(GBBuffers& b, int ct, int nj, hipStream_t st) {
   return AQC_OK;
 }
 
+// The side stream and the round events: created on first use, released (after aqc_finalize's
+// device synchronisation) by release_gb_sync -- at exit the side stream's post kernels are ordered
+// only by these events, so they must be drained before the runtime tears down.
+hipStream_t g_gb_side[64] = {nullptr};
+std::vector<hipEvent_t> g_gb_events;
+void release_gb_sync() {
+  for (auto& s : g_gb_side)
+    if (s) (void)hipStreamDestroy(s), s = nullptr;
+  for (hipEvent_t e : g_gb_events) (void)hipEventDestroy(e);
+  g_gb_events.clear();
+}
+
 hipStream_t gb_side_stream() {
-  static hipStream_t s[64] = {nullptr};
   int dev = 0;
   (void)hipGetDevice(&dev);
-  if (!s[dev]) (void)hipStreamCreateWithFlags(&s[dev], hipStreamNonBlocking);
-  return s[dev];
+  if (!g_gb_side[dev]) {
+    (void)hipStreamCreateWithFlags(&g_gb_side[dev], hipStreamNonBlocking);
+    aqc::on_finalize(release_gb_sync);
+  }
+  return g_gb_side[dev];
 }
 
 hipEvent_t gb_event(int i) {  // (per process; the library stream orders their reuse)
-  static std::vector<hipEvent_t> ev;
-  while ((int)ev.size() <= i) {
+  aqc::on_finalize(release_gb_sync);
+  while ((int)g_gb_events.size() <= i) {
     hipEvent_t e = nullptr;
     (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
-    ev.push_back(e);
+    g_gb_events.push_back(e);
   }
-  return ev[i];
+  return g_gb_events[i];
 }
 
 
@@ -995,6 +1020,7 @@ int run_gram_big(const TwoSiteJob* hjobs, const TwoSiteJob* jobs, int nj, int ca
   a.G = b.G, a.d = b.d, a.e = b.e, a.tau = b.tau, a.z = b.z, a.dinv = b.dinv, a.sig2 = b.sig2;
   a.lam = b.lam, a.tn = b.tn, a.tfac = b.tfac, a.yc = b.yc;
   a.xch = b.xch, a.cnt = b.cnt, a.status = b.status;
+  a.spin = g_gb_spin;
   AQC_HIP_CHECK(hipMemsetAsync(b.cnt, 0, (size_t)32 * nj * sizeof(unsigned), st));
   hipLaunchKernelGGL((k_gb_gram<CT>), dim3((CT / 64) * (CT / 64 + 1) / 2, nj), dim3(256), 0, st, jobs, a);
   AQC_CHECK_LAUNCH();
@@ -1105,5 +1131,14 @@ extern "C" int aqc_svd_gram_big_stats(double* out) {
   for (int i = 0; i < 5; ++i) out[i] = (double)t[i];
   unsigned long long z[5] = {0, 0, 0, 0, 0};
   AQC_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(aqc::g_gbig_stats), z, sizeof(z)));
+  return AQC_OK;
+}
+
+/* Counter-wait limit of the multi-workgroup tridiagonalisation, in microseconds (< 0: the default,
+   100 ms).  A workgroup that waits longer for the rest of its job declines the job (status 3), which
+   then runs the block Jacobi.  0 makes any wait that is not already satisfied a timeout: the tests
+   use it to exercise the decline path. */
+extern "C" int aqc_gb_set_spin_limit(double us) {
+  aqc::g_gb_spin = us < 0 ? aqc::kSpinTicks : (unsigned long long)(us * 100.0);
   return AQC_OK;
 }

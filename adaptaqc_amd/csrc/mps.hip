@@ -28,14 +28,26 @@ using aqc::cplx;
 
 namespace aqc {
 
+namespace {
+std::mutex g_mps_stream_mu;
+hipStream_t g_mps_streams[64] = {nullptr};
+void release_mps_streams() {
+  std::lock_guard<std::mutex> lk(g_mps_stream_mu);
+  for (auto& s : g_mps_streams)
+    if (s) (void)hipStreamDestroy(s), s = nullptr;
+}
+}  // namespace
+
 hipStream_t mps_stream() {
-  static std::mutex mu;
-  static hipStream_t s[64] = {nullptr};
   int dev = 0;
   hipGetDevice(&dev);
-  std::lock_guard<std::mutex> lk(mu);
-  if (!s[dev]) hipStreamCreateWithFlags(&s[dev], hipStreamNonBlocking);
-  return s[dev];
+  std::lock_guard<std::mutex> lk(g_mps_stream_mu);
+  if (!g_mps_streams[dev]) {
+    hipStreamCreateWithFlags(&g_mps_streams[dev], hipStreamNonBlocking);
+    note_device(dev);
+    on_finalize(release_mps_streams);
+  }
+  return g_mps_streams[dev];
 }
 
 }  // namespace aqc
@@ -1552,11 +1564,20 @@ int ensure_staging(Staging& st, size_t bytes) {
   return AQC_OK;
 }
 
+void free_staging(Staging& s) {
+  if (s.dev) (void)hipFree(s.dev);
+  if (s.host) (void)hipHostFree(s.host);
+  s = Staging();
+}
+Staging g_staging[64];
+void release_staging() {
+  for (auto& s : g_staging) free_staging(s);
+}
 Staging& staging() {
-  static Staging s[64];
   int dev = 0;
   hipGetDevice(&dev);
-  return s[dev];
+  aqc::on_finalize(release_staging);
+  return g_staging[dev];
 }
 
 // Job staging for the gate-application launches: a ring of buffer sets per device, each with an
@@ -1573,15 +1594,25 @@ struct StagingSet {
 // lifetime (several host threads may drive one device) and records the set's event on the stream
 // on EVERY exit path -- an early error return included -- so the set is never handed out again
 // while kernels queued before the error may still read it.
+constexpr int kStagingRing = 4;
+StagingSet g_stage_sets[64][kStagingRing];
+void release_stage_sets() {
+  for (auto& dev_sets : g_stage_sets)
+    for (auto& s : dev_sets) {
+      if (s.done) (void)hipEventDestroy(s.done);
+      free_staging(s.buf);
+      s.done = nullptr;
+      s.pending = false;
+    }
+}
 class StagingLease {
  public:
   explicit StagingLease(hipStream_t st) : st_(st), lk_(mutex_for(device())) {
-    constexpr int kRing = 4;
-    static StagingSet sets[64][kRing];
     static int next[64] = {0};
     const int dev = device();
-    ss_ = &sets[dev][next[dev]];
-    next[dev] = (next[dev] + 1) % kRing;
+    aqc::on_finalize(release_stage_sets);
+    ss_ = &g_stage_sets[dev][next[dev]];
+    next[dev] = (next[dev] + 1) % kStagingRing;
     if (ss_->pending) {
       const hipError_t e = hipEventSynchronize(ss_->done);
       if (e != hipSuccess) {
@@ -1964,6 +1995,14 @@ int check_flags_batch(aqc_mps_t* hs, int ns) {
     size_t hcap = 0;
   };
   static FlagStage stages[64];
+  static void (*release)() = [] {
+    for (auto& f : stages) {
+      if (f.dev) (void)hipFree(f.dev);
+      if (f.host) (void)hipHostFree(f.host);
+      f = FlagStage();
+    }
+  };
+  aqc::on_finalize(release);
   int dev = 0;
   hipGetDevice(&dev);
   FlagStage& fs = stages[dev];
@@ -2434,6 +2473,11 @@ int aqc_mps_copy_batch(aqc_mps_t* dst, const aqc_mps_t* src, int ns) {
 int aqc_stream_join(void* stream) {
   static std::mutex mu;
   static hipEvent_t ev[64] = {nullptr};
+  static void (*release)() = [] {
+    for (auto& e : ev)
+      if (e) (void)hipEventDestroy(e), e = nullptr;
+  };
+  aqc::on_finalize(release);
   int dev = 0;
   AQC_HIP_CHECK(hipGetDevice(&dev));
   AQC_REQUIRE(dev >= 0 && dev < 64, "aqc_stream_join: device index out of range");
@@ -2447,6 +2491,11 @@ int aqc_stream_join(void* stream) {
 int aqc_stream_wait(void* stream) {
   static std::mutex mu;
   static hipEvent_t ev[64] = {nullptr};
+  static void (*release)() = [] {
+    for (auto& e : ev)
+      if (e) (void)hipEventDestroy(e), e = nullptr;
+  };
+  aqc::on_finalize(release);
   int dev = 0;
   AQC_HIP_CHECK(hipGetDevice(&dev));
   AQC_REQUIRE(dev >= 0 && dev < 64, "aqc_stream_wait: device index out of range");
@@ -2543,6 +2592,11 @@ int aqc_mps_overlap_zero_batch(aqc_mps_t* hs, int ns, double* out) {
   if (rc != AQC_OK) return rc;
   static cplx* dres[64] = {nullptr};
   static int dres_n[64] = {0};
+  static void (*release)() = [] {
+    for (int d = 0; d < 64; ++d)
+      if (dres[d]) (void)hipFree(dres[d]), dres[d] = nullptr, dres_n[d] = 0;
+  };
+  aqc::on_finalize(release);
   int dev = 0;
   hipGetDevice(&dev);
   if (dres_n[dev] < ns) {

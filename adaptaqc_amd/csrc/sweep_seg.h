@@ -147,11 +147,20 @@ struct SegScratch {
   size_t env_launches = 0, tbl_bytes = 0;
 };
 
+SegScratch g_seg_scratch[64];
+void release_seg_scratch() {
+  for (auto& s : g_seg_scratch) {
+    if (s.done) (void)hipEventDestroy(s.done);
+    if (s.dev) (void)hipFree(s.dev);
+    if (s.host) (void)hipHostFree(s.host);
+    s = SegScratch();
+  }
+}
 SegScratch& seg_scratch() {
-  static SegScratch s[64];
   int dev = 0;
   hipGetDevice(&dev);
-  return s[dev];
+  aqc::on_finalize(release_seg_scratch);
+  return g_seg_scratch[dev];
 }
 
 int run_segment_sweep(const SweepJob& hj, const SweepJob* djob, const int* pairs, const int* dpairs, int npairs,

@@ -156,6 +156,13 @@ int aqc_svd_gram_big_stats(double* out);
    out[6] k_gb_back (job 0, first block), out[7] k_gb_inv (job 0, lane 0), out[8] the next
    reflector's zlarfg (per column, job 0's first workgroup). */
 int aqc_svd_gram_big_ticks(double* out);
+/* Counter-wait limit of the same path's tridiagonalisation in microseconds (< 0: default 100 ms);
+   a job whose workgroups wait longer declines to the block Jacobi (out[4] above).  0 forces the
+   decline wherever a wait is not already satisfied (tests). */
+int aqc_gb_set_spin_limit(double us);
+/* Test load: nblocks 256-thread workgroups on a private stream, block b spinning (b % 16 + 1) / 16
+   of `ms` milliseconds, so work queued on other streams starts one CU at a time.  Asynchronous. */
+int aqc_debug_hog(int nblocks, double ms);
 /* Batched applies of >= 32 states at 2*chi = 128 run every state's whole op list in
    one fused workgroup (theta, Jacobi, truncation, split per update: no grid-wide step between
    updates); on = 0 selects the lock-step launches per update.  Default on. */

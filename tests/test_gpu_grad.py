@@ -199,3 +199,49 @@ def test_config4_full_size_chi128_vs_oracle():
     ref = ogr.general_grad_of_pairs_env(psi, n, ogr.inverse_ops(o_layer), o_gens, o_deg, cmap)
     assert np.max(ref) > 1e-3
     np.testing.assert_allclose(got, ref, atol=1e-10)
+
+
+def test_unbounded_cap512_general_gradient():
+    """an unbounded MPS (max_chi None, the reference's default MPS_SIM) at
+    n = 18 gets capacity 512 (chi_cap_for); general_grad_of_pairs on it runs the capacity-agnostic
+    segmented sweep (one state, and a batch of two split into single states) and matches the
+    oracle's environment form."""
+    from adaptaqc_amd import _lib
+    from adaptaqc_amd.circuit import device_ops
+    from adaptaqc_amd.device import DeviceMPS
+    from adaptaqc_amd.mps_operations import chi_cap_for
+    from adaptaqc_amd.utils.gradients import grads_for_state, layer_operators, pair_grads_batch
+
+    n = 18
+    assert chi_cap_for(n, None) == 512
+    rng = np.random.default_rng(18)
+    ops = []
+    for layer in range(3):
+        for q in range(n):
+            ops.append(("ry", (q,), (float(rng.uniform(-np.pi, np.pi)),)))
+        for q in range(layer % 2, n - 1, 2):
+            ops.append(("cx", (q, q + 1), ()))
+    inv0, gens, deg = _inputs("identity_resolvable")
+    cmap = [(a, a + d) for d in range(1, n) for a in range(n - d)]
+    states = []
+    for k in range(2):
+        d = DeviceMPS(n, 512, 1e-16, None)
+        d.apply(device_ops(to_circuit(n, ops[: len(ops) - 5 * k])))
+        states.append(d)
+    one = np.array(grads_for_state(states[0], n, inv0, gens, deg, cmap))
+    u0, gmats = layer_operators(inv0, gens)
+    svec = np.zeros((n, 2), dtype=complex)
+    svec[:, 0] = 1.0
+    both = np.array(pair_grads_batch(states, svec, cmap, u0, np.stack(gmats), np.asarray(deg, dtype=float)))
+    o_layer = [(i.operation.name, i.qubits, tuple(i.operation.params)) for i in _layer("identity_resolvable").data]
+    og, od = ogr.get_generators_and_degeneracies(o_layer, True, True)
+    for k in range(2):
+        ref = ogr.general_grad_of_pairs_env(M.run_circuit(n, ops[: len(ops) - 5 * k]).preprocessed(), n,
+                                            ogr.inverse_ops(o_layer), og, od, cmap)
+        got = one if k == 0 else both[1]
+        np.testing.assert_allclose(got, ref, rtol=0, atol=1e-10 * max(1.0, np.max(np.abs(ref))))
+    np.testing.assert_allclose(both[0], one, rtol=0, atol=1e-13)
+    # the chi = 1 product fit (starting_circuit="tenpy_product_state") at the same capacity
+    f = states[0].product_fit(None, 10, 50, 1e-12)[1]
+    assert 0.0 < f <= 1.0 + 1e-12
+    assert _lib.load() is not None

@@ -129,3 +129,43 @@ def test_gram_big_config5_wave():
     d, st = _run(n, chi, ops, seed=5)
     assert st["taken"] == 24 and st["timeouts"] == 0, st
     _vs_oracle(d, n, chi, ops, 5)
+
+
+def test_gram_big_exchange_timeout_declines_to_block_jacobi():
+    """The counter-wait limit at 0 (aqc_gb_set_spin_limit): a workgroup that finds its job's count
+    short at any column declines the job (status 3).  The declined jobs run the
+    block Jacobi after the status read-back and the state still matches the oracle (exact bond dims,
+    fidelity 1e-6)."""
+    from adaptaqc_amd import _lib
+
+    n, chi = 18, 128
+    rng = np.random.default_rng(chi + 3)
+    m = n // 2
+    ops = _gates(n, rng, [(m - 1, m), (m, m + 1), (m - 2, m - 1)])
+    _lib.check(_lib.load().aqc_gb_set_spin_limit(0.0))
+    try:
+        d, st = _run(n, chi, ops, seed=chi + 4)
+    finally:
+        _lib.check(_lib.load().aqc_gb_set_spin_limit(-1.0))
+    assert st["calls"] == 3 and st["timeouts"] >= 1, st
+    assert st["taken"] + st["timeouts"] == 3, st
+    _vs_oracle(d, n, chi, ops, chi + 4)
+
+
+def test_gram_big_late_workgroup_start():
+    """the tridiagonalisation's workgroups of one job may start late (CUs held by
+    other work).  A staggered CU-holding load on another stream (aqc_debug_hog: blocks release
+    their CUs over 2 ... 30 ms) is queued first, so the jobs' workgroups are dispatched one CU at a
+    time; reflector row 0 must not be overwritten before every workgroup has read it.  Same result
+    as the oracle, no timeout (30 ms is well inside the 100 ms limit)."""
+    from adaptaqc_amd import _lib
+
+    n, chi = 20, 256
+    rng = np.random.default_rng(chi + 3)
+    m = n // 2
+    ops = _gates(n, rng, [(m - 1, m), (m, m + 1), (m - 2, m - 1)])
+    lib = _lib.lib()
+    _lib.check(lib.aqc_debug_hog(2048, 30.0))
+    d, st = _run(n, chi, ops, seed=chi + 4)
+    assert st["calls"] == 3 and st["taken"] == 3 and st["timeouts"] == 0, st
+    _vs_oracle(d, n, chi, ops, chi + 4)
