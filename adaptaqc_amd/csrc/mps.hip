@@ -1096,8 +1096,11 @@ __device__ __forceinline__ void chain_split(const TwoSiteJob& j) {
 }
 
 __global__ __launch_bounds__(1024) void k_chain(const ChainJob* __restrict__ chains, const TwoSiteJob* __restrict__ two,
-                                                const OneSiteJob* __restrict__ one) {
+                                                const OneSiteJob* __restrict__ one, const int* __restrict__ resume) {
   const ChainJob& c = chains[blockIdx.x];
+  // resume != nullptr: the tail of a list that k_chain256 handed over (from op resume[b]; < 0: none)
+  const int o0 = resume ? __builtin_amdgcn_readfirstlane(resume[blockIdx.x]) : 0;
+  if (o0 < 0) return;
   const int tid = fresh_tid();
   // shader-clock ticks of the phases (thread 0 of each workgroup; aqc_mps_chain_ticks), kept in
   // LDS so that no VGPR stays live across the phases
@@ -1111,7 +1114,7 @@ __global__ __launch_bounds__(1024) void k_chain(const ChainJob* __restrict__ cha
     }
   };
   tick(-1);
-  for (int o = 0; o < c.nops; ++o) {
+  for (int o = o0; o < c.nops; ++o) {
     // wave-uniform (SGPR) op code, so the job's fields are scalar loads and hold no VGPRs
     const int code = __builtin_amdgcn_readfirstlane(c.ops[o]);
     if (code < 0) {
@@ -1136,6 +1139,163 @@ __global__ __launch_bounds__(1024) void k_chain(const ChainJob* __restrict__ cha
   }
   if (tid == 0)
     for (int ph = 0; ph < 5; ++ph) atomicAdd(&g_chain_ticks[ph], tk[ph]);
+}
+
+// ---- fused per-state chain at 256 threads, two states per CU (svd_tri.h) -----------------------
+// The same op list as k_chain, in a 256-thread workgroup with <= ~76 KB of LDS and <= 256 VGPRs:
+// two states' chains share each CU, so one state's serial phases (the tridiagonalisation's
+// per-column chain and barriers, S4 / S5 on a wave or two) run beside the other's issue.  theta by
+// quadrants, the Gram SVD of svd_tri.h, rank, the split's two 64 x 64 GEMM blocks one after the
+// other.  An update whose Gram path declines (shape, eigenvalue floor) stops the chain: its op
+// index goes to resume[b] and k_chain (1024 threads, register Jacobi fallback) runs the rest.
+#include "svd_tri.h"
+
+__device__ __forceinline__ void chain_theta256(const TwoSiteJob& j) {
+  extern __shared__ double2 xbuf[];
+  const int lt = fresh_tid();
+  cplx (*As)[32][9] = reinterpret_cast<cplx (*)[32][9]>(xbuf);
+  cplx (*Bs)[8][33] = reinterpret_cast<cplx (*)[8][33]>(xbuf + 2 * 32 * 9);
+  __shared__ cplx sG2[16];
+  if (lt < 16) sG2[lt] = aqc::ldg(j.G + lt);
+  const int chl = j.dims[0], chm = j.dims[1], chr = j.dims[2];
+  const int cap = j.cap;
+  const size_t half = (size_t)cap * cap;
+  const int M = 2 * chl;
+  const cplx* gp = j.gp;
+  const cplx* gq = j.gq;
+  const double* llp = j.ll;
+  const double* lmp = j.lm;
+  const double* lrp = j.lr;
+  asm volatile("" : "+s"(gp), "+s"(gq), "+s"(llp), "+s"(lmp), "+s"(lrp));
+  const int ty = lt >> 4, tx = lt & 15;
+  for (int sg = 0; sg < 4; ++sg) {  // the four 32 x 32 output quadrants in turn
+    const int l0 = 32 * (sg >> 1), r0 = 32 * (sg & 1);
+    if (l0 >= chl || r0 >= chr) continue;  // (uniform)
+    cplx acc[4][2][2];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) acc[q][i][jj] = aqc::cmk(0, 0);
+    for (int m0 = 0; m0 < chm; m0 += 8) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int e = lt + 256 * u, s = e >> 8;
+        {
+          const int row = (e >> 3) & 31, mm = e & 7, l = l0 + row, m = m0 + mm;
+          cplx a = aqc::cmk(0, 0);
+          if (l < chl && m < chm) a = aqc::cscale(aqc::ldg(gp + s * half + (size_t)l * cap + m), aqc::ldg(llp + l) * aqc::ldg(lmp + m));
+          As[s][row][mm] = a;
+        }
+        {
+          const int mm = (e >> 5) & 7, col = e & 31, m = m0 + mm, r = r0 + col;
+          cplx b = aqc::cmk(0, 0);
+          if (m < chm && r < chr) b = aqc::cscale(aqc::ldg(gq + s * half + (size_t)m * cap + r), aqc::ldg(lrp + r));
+          Bs[s][mm][col] = b;
+        }
+      }
+      __syncthreads();
+#pragma unroll 2
+      for (int mm = 0; mm < 8; ++mm) {
+        cplx av[2][2], bv[2][2];
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+          for (int i = 0; i < 2; ++i) {
+            av[s][i] = As[s][tx + 16 * i][mm];
+            bv[s][i] = Bs[s][mm][ty + 16 * i];
+          }
+#pragma unroll
+        for (int s1 = 0; s1 < 2; ++s1)
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+              for (int jj = 0; jj < 2; ++jj)
+                acc[2 * s1 + s2][i][jj] = aqc::cfma(av[s1][i], bv[s2][jj], acc[2 * s1 + s2][i][jj]);
+      }
+      __syncthreads();
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        const int l = l0 + tx + 16 * i, r = r0 + ty + 16 * jj;
+        if (l < chl && r < chr) {
+#pragma unroll
+          for (int o = 0; o < 4; ++o) {
+            cplx v = aqc::cmul(sG2[o * 4 + 0], acc[0][i][jj]);
+            v = aqc::cfma(sG2[o * 4 + 1], acc[1][i][jj], v);
+            v = aqc::cfma(sG2[o * 4 + 2], acc[2][i][jj], v);
+            v = aqc::cfma(sG2[o * 4 + 3], acc[3][i][jj], v);
+            aqc::stg(j.theta + (size_t)((o & 1) * chr + r) * M + (o >> 1) * chl + l, v);
+          }
+        }
+      }
+  }
+}
+
+__device__ __forceinline__ void chain_split256(const TwoSiteJob& j) {
+  extern __shared__ double2 xbuf[];
+  const int tid = fresh_tid();
+  split_copy_body(j, tid, 256);
+  aqc::GemmLds& lds = *reinterpret_cast<aqc::GemmLds*>(xbuf);
+  for (int blk = 0; blk < 4; ++blk)
+    if (split_block_active(j, blk)) split_gemm_body<true>(j, blk, lds, -1);  // (uniform)
+}
+
+__device__ unsigned long long g_chain256_ticks[5];
+
+__global__ __launch_bounds__(256, 2) void k_chain256(const ChainJob* __restrict__ chains, const TwoSiteJob* __restrict__ two,
+                                                     const OneSiteJob* __restrict__ one, int* __restrict__ resume) {
+  const ChainJob& c = chains[blockIdx.x];
+  const int tid = fresh_tid();
+  __shared__ unsigned long long tk[6];
+  if (tid == 0) tk[0] = tk[1] = tk[2] = tk[3] = tk[4] = tk[5] = 0;
+  auto tick = [&](int ph) {
+    if (tid == 0) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      if (ph >= 0) tk[ph] += t - tk[5];
+      tk[5] = t;
+    }
+  };
+  tick(-1);
+  for (int o = 0; o < c.nops; ++o) {
+    const int code = __builtin_amdgcn_readfirstlane(c.ops[o]);
+    if (code < 0) {
+      one_site_body(one[-code - 1], tid, 256);
+      __syncthreads();
+      tick(4);
+      continue;
+    }
+    const TwoSiteJob& j = two[code];
+    chain_theta256(j);
+    __syncthreads();
+    tick(0);
+    const bool ok = j.gram && tri::gram256_body(j);
+    __syncthreads();
+    tick(1);
+    if (!ok) {  // the 1024-thread chain takes over from this update (theta is recomputed there)
+      if (tid == 0) resume[blockIdx.x] = o;
+      break;
+    }
+    rank_body<256, 128>(j);
+    __syncthreads();
+    tick(2);
+    chain_split256(j);
+    __syncthreads();
+    tick(3);
+  }
+  if (tid == 0)
+    for (int ph = 0; ph < 5; ++ph) atomicAdd(&g_chain256_ticks[ph], tk[ph]);
+}
+
+// single-job Gram SVD on 256 threads (aqc_svd_debug variant 8)
+__global__ __launch_bounds__(256, 2) void k_svd_gram256(const TwoSiteJob* __restrict__ jobs) {
+  const TwoSiteJob& j = jobs[blockIdx.x];
+  if (!tri::gram256_body(j) && threadIdx.x == 0) j.flags[2] = -1;
 }
 
 // ---- measurements -------------------------------------------------------------------------
@@ -1735,6 +1895,17 @@ std::vector<std::vector<const DevOp*>> level_ops(const std::vector<DevOp>& ops, 
 
 // Batches at 2 chi = 128: every state's op list runs in one k_chain workgroup (longest lists
 // first, so that the short ones fill in behind them).
+// k_chain256 (two states per CU) unless AQC_CHAIN=1024 or the Gram path is off (its fallback, the
+// register Jacobi, needs the 1024-thread chain)
+int g_chain256 = -1;
+bool use_chain256() {
+  if (g_chain256 < 0) {
+    const char* e = std::getenv("AQC_CHAIN");
+    g_chain256 = (e && std::strcmp(e, "1024") == 0) ? 0 : 1;
+  }
+  return g_chain256 && g_svd_gram;
+}
+
 int run_chains(aqc_mps_t* hs, int ns, std::vector<std::vector<DevOp>>& lists, int cap_max) {
   hipStream_t st = aqc::mps_stream();
   // per-state job counts -> offsets, then every state's jobs written straight into the staging
@@ -1758,10 +1929,11 @@ int run_chains(aqc_mps_t* hs, int ns, std::vector<std::vector<DevOp>>& lists, in
   const size_t o_codes = al(o_one + n_one * sizeof(OneSiteJob));
   const size_t o_chain = al(o_codes + n_codes * sizeof(int));
   const size_t total = o_chain + (size_t)ns * sizeof(ChainJob);
+  const size_t o_resume = al(total);  // device-only: k_chain256's hand-over indices
   StagingLease lease(st);
   if (lease.rc() != AQC_OK) return lease.rc();
   Staging& sg = lease.buf();
-  int rc = ensure_staging(sg, total);
+  int rc = ensure_staging(sg, o_resume + (size_t)ns * sizeof(int));
   if (rc != AQC_OK) return rc;
   char* hb = (char*)sg.host;
   char* db = (char*)sg.dev;
@@ -1796,8 +1968,19 @@ int run_chains(aqc_mps_t* hs, int ns, std::vector<std::vector<DevOp>>& lists, in
   const double c = cap_max, nj = (double)n_two;
   // algorithmic: the two sites' Gammas in and out; nominal SVD + theta + split flops
   aqc::KernelTimer::begin(st, "mps_chain", nj * 8.0 * c * c * 16, nj * (84.0 * 8.0 + 64.0) * c * c * c);
-  hipLaunchKernelGGL(k_chain, dim3(ns), dim3(1024), kChainLds, st, (const ChainJob*)(db + o_chain),
-                     (const TwoSiteJob*)(db + o_two), (const OneSiteJob*)(db + o_one));
+  if (use_chain256()) {
+    // two states per CU; a state whose Gram path declines continues on the 1024-thread chain
+    int* dres = (int*)(db + o_resume);
+    AQC_HIP_CHECK(hipMemsetAsync(dres, 0xff, (size_t)ns * sizeof(int), st));
+    hipLaunchKernelGGL(k_chain256, dim3(ns), dim3(256), tri::kLdsBytes, st, (const ChainJob*)(db + o_chain),
+                       (const TwoSiteJob*)(db + o_two), (const OneSiteJob*)(db + o_one), dres);
+    AQC_CHECK_LAUNCH();
+    hipLaunchKernelGGL(k_chain, dim3(ns), dim3(1024), kChainLds, st, (const ChainJob*)(db + o_chain),
+                       (const TwoSiteJob*)(db + o_two), (const OneSiteJob*)(db + o_one), (const int*)dres);
+  } else {
+    hipLaunchKernelGGL(k_chain, dim3(ns), dim3(1024), kChainLds, st, (const ChainJob*)(db + o_chain),
+                       (const TwoSiteJob*)(db + o_two), (const OneSiteJob*)(db + o_one), (const int*)nullptr);
+  }
   aqc::KernelTimer::end(st);
   AQC_CHECK_LAUNCH();
   return AQC_OK;  // the lease records the set's event
@@ -2163,9 +2346,10 @@ int aqc_svd_debug(const double* theta, int m, int n, int variant, int stop_after
   AQC_REQUIRE(m >= 1 && n >= 1 && m % 2 == 0 && n % 2 == 0 && m <= 128 && n <= 128,
               "aqc_svd_debug: m, n must be even and <= 128");
   AQC_REQUIRE(stop_after_qr >= 0 && stop_after_qr <= 2, "aqc_svd_debug: stop_after_qr must be 0, 1 or 2");
-  AQC_REQUIRE(variant == 2 || variant == 7, "aqc_svd_debug: variant must be 2 (register Jacobi) or 7 (Gram path)");
-  AQC_REQUIRE(variant != 7 || (std::max(m, n) > 64 && stop_after_qr == 0),
-              "aqc_svd_debug: variant 7 (Gram) needs 64 < max(m, n) <= 128 and no QR stop");
+  AQC_REQUIRE(variant == 2 || variant == 7 || variant == 8,
+              "aqc_svd_debug: variant must be 2 (register Jacobi), 7 (Gram path) or 8 (Gram path, 256 threads)");
+  AQC_REQUIRE(variant < 7 || (std::max(m, n) > 64 && stop_after_qr == 0),
+              "aqc_svd_debug: variants 7 / 8 (Gram) need 64 < max(m, n) <= 128 and no QR stop");
   hipStream_t st = aqc::mps_stream();
   const int cp = std::max(m, n) <= 32 ? 32 : (std::max(m, n) <= 64 ? 64 : 128);
   const size_t mat = (size_t)128 * 128 * sizeof(cplx);
@@ -2194,7 +2378,7 @@ int aqc_svd_debug(const double* theta, int m, int n, int variant, int stop_after
   j.dbg = stop_after_qr;
   j.cap = 64;                     // the work buffer holds 128 x 128
   j.max_chi = g_debug_max_chi;    // Gram path: K = min(C, max_chi)
-  j.gram = variant == 7;  // 1: stop after the QR phase; 2: also QR phase clock ticks in sig[0..3]
+  j.gram = variant >= 7;  // 1: stop after the QR phase; 2: also QR phase clock ticks in sig[0..3]
   int hd[8] = {m / 2, 0, n / 2, 0, 0, 0, 0, 0};  // dims, then zeroed flags
   AQC_HIP_CHECK(hipMemcpyAsync(th, theta, (size_t)m * n * sizeof(cplx), hipMemcpyHostToDevice, st));
   AQC_HIP_CHECK(hipMemcpyAsync(dm, hd, sizeof(hd), hipMemcpyHostToDevice, st));
@@ -2204,6 +2388,8 @@ int aqc_svd_debug(const double* theta, int m, int n, int variant, int stop_after
   else if (cp == 64) hipLaunchKernelGGL((k_jacobi_reg<64, 4>), dim3(1), dim3(512), 32 * 65 * 16, st, dj);
   else if (variant == 7)
     hipLaunchKernelGGL(k_svd_gram, dim3(1), dim3(1024), kChainLdsBytes, st, dj);
+  else if (variant == 8)  // (flags[2] = -1: declined)
+    hipLaunchKernelGGL(k_svd_gram256, dim3(1), dim3(256), tri::kLdsBytes, st, dj);
   else  // the register Jacobi itself (not the Gram path in front of it)
     hipLaunchKernelGGL((k_jacobi_reg<128, 8>), dim3(1), dim3(1024), 64 * 129 * 16, st, dj);
   AQC_CHECK_LAUNCH();

@@ -88,6 +88,109 @@ def _batched_isl(original):
     return _get_all_qubit_pair_entanglement_measures
 
 
+# ---- the reference's own Rotoselect / Rotosolve, batched (cost_minimiser.py:267-368) --------------
+# The reference's CostMinimiser asks ``self.cost_finder()`` (the compiler's evaluate_cost,
+# approximate_compiler.py:150-158, 514-527) once per candidate: 1 + 3 x 2 = 7 evaluations per gate in
+# replace_with_best_1q_gate, 3 (2 with the identity cost given) in find_best_angle, each a full
+# replay.  With this package's backends and the global, unsoftened cost, the wrappers below take all
+# candidates of a gate from one batched evaluation of utils/cached_rotations.py (statevector: a 2x2
+# transition matrix of the prefix and the undone suffix; MPS: the cached prefix MPS and all
+# candidates replayed through the suffix in one lock-step batch), and then run the reference's own
+# code on those numbers: its SUPPORTED_1Q_GATES order, its minimum_of_sinusoidal, its strict `<`,
+# its co.replace_1q_gate edits of full_circuit, and cost_evaluation_counter advanced by the number
+# of evaluate_cost calls it would have made.  An evaluator lives for one _reduce_cost sweep (the
+# gates are visited in index order; only the gate just optimised changes between them).  Anything
+# else (local or softened cost, other backends, NLopt / SciPy paths) runs the reference's code.
+
+def _rotations_evaluator(minimiser):
+    from .utils.cached_rotations import MPSPrefixBatch, SVTransitionSweep
+
+    compiler = getattr(minimiser.cost_finder, "__self__", None)
+    if compiler is None or getattr(compiler, "full_circuit", None) is not minimiser.full_circuit:
+        return None
+    if getattr(compiler, "optimise_local_cost", False) or getattr(compiler, "soften_global_cost", False):
+        return None
+    backend = getattr(compiler, "backend", None)
+    if isinstance(backend, HipMPSBackend):
+        return MPSPrefixBatch(compiler)
+    if isinstance(backend, HipSVBackend):
+        return SVTransitionSweep(compiler)
+    return None
+
+
+def _reference_module(name):
+    return sys.modules.get(name)
+
+
+def _batched_reduce_cost(original):
+    def _reduce_cost(self, *args, **kwargs):
+        prev = getattr(self, "_aqc_rotations", None)
+        self._aqc_rotations = _rotations_evaluator(self)
+        try:
+            return original(self, *args, **kwargs)
+        finally:
+            self._aqc_rotations = prev
+
+    _reduce_cost.__wrapped__ = original
+    return _reduce_cost
+
+
+def _candidate(name, theta):
+    from .utils.cached_rotations import rotation
+
+    return rotation(name, theta)
+
+
+def _batched_replace_with_best_1q_gate(original):
+    def replace_with_best_1q_gate(self, gate_index):
+        ev = getattr(self, "_aqc_rotations", None)
+        cm = _reference_module(type(self).__module__)
+        if ev is None or cm is None:
+            return original(self, gate_index)
+        names = list(cm.SUPPORTED_1Q_GATES)
+        ev.goto(gate_index)
+        mats = [_candidate("rx", 0.0)]
+        for name in names:
+            mats += [_candidate(name, cm.np.pi / 2), _candidate(name, -cm.np.pi / 2)]
+        c = ev.costs(gate_index, mats)
+        ev.count(len(mats))
+        # cost_minimiser.py:327-342 on those numbers (find_best_angle's replace / restore of the
+        # gate is a no-op on the circuit once it holds rx(0))
+        cm.co.replace_1q_gate(self.full_circuit, gate_index, "rx", 0)
+        cost_identity = c[0]
+        best_gate_name, best_gate_angle, best_gate_cost = None, None, 1
+        for k, gate_name in enumerate(names):
+            min_angle, cost = cm.minimum_of_sinusoidal(cost_identity, c[1 + 2 * k], c[2 + 2 * k])
+            if cost < best_gate_cost:
+                best_gate_name, best_gate_angle, best_gate_cost = gate_name, min_angle, cost
+        cm.co.replace_1q_gate(self.full_circuit, gate_index, best_gate_name, best_gate_angle)
+        return best_gate_cost
+
+    replace_with_best_1q_gate.__wrapped__ = original
+    return replace_with_best_1q_gate
+
+
+def _batched_find_best_angle(original):
+    def find_best_angle(self, gate_index, gate_name, cost_for_identity=None):
+        ev = getattr(self, "_aqc_rotations", None)
+        cm = _reference_module(type(self).__module__)
+        if ev is None or cm is None:
+            return original(self, gate_index, gate_name, cost_for_identity)
+        # cost_minimiser.py:344-368: [0, pi/2, -pi/2], the identity cost reused when given
+        angles = [0, cm.np.pi / 2, -cm.np.pi / 2]
+        costs = []
+        if cost_for_identity is not None:
+            costs.append(cost_for_identity)
+            angles.remove(0)
+        ev.goto(gate_index)
+        costs += ev.costs(gate_index, [_candidate(gate_name, float(t)) for t in angles])
+        ev.count(len(angles))
+        return cm.minimum_of_sinusoidal(costs[0], costs[1], costs[2])
+
+    find_best_angle.__wrapped__ = original
+    return find_best_angle
+
+
 # (module, attribute path, replacement) -- the reference's own call sites resolve these names at
 # call time (module globals, module attributes, class attributes), so rebinding them is enough
 PATCHES = (
@@ -98,6 +201,10 @@ PATCHES = (
     ("adaptaqc.utils.gradients", "general_grad_of_pairs", device_general_grad_of_pairs),
     ("adaptaqc.compilers.adapt.adapt_compiler", "AdaptCompiler._get_all_qubit_pair_entanglement_measures",
      _Wrap(_batched_isl)),
+    ("adaptaqc.utils.cost_minimiser", "CostMinimiser._reduce_cost", _Wrap(_batched_reduce_cost)),
+    ("adaptaqc.utils.cost_minimiser", "CostMinimiser.replace_with_best_1q_gate",
+     _Wrap(_batched_replace_with_best_1q_gate)),
+    ("adaptaqc.utils.cost_minimiser", "CostMinimiser.find_best_angle", _Wrap(_batched_find_best_angle)),
 )
 REGISTRATIONS = (
     ("adaptaqc.backends.aer_mps_backend", "AerMPSBackend", HipMPSBackend),

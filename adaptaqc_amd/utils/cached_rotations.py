@@ -39,11 +39,35 @@ from .. import gates as G
 from .._lib import ops_array
 from ..circuit import device_ops
 from ..device import DeviceSV, apply_batch, copy_batch, overlap_zero_batch
-from . import circuit_operations as co
 
 
-def _slice(circuit, lo, hi):
-    return co.extract_inner_circuit(circuit, (lo, hi))
+class _View:
+    """``circuit.data[lo:hi]`` with the circuit's own qubit resolution: this IR's circuits or the
+    reference's qiskit circuits (``find_bit``), so the evaluators also serve the reference's own
+    CostMinimiser under reference_binding.install()."""
+
+    def __init__(self, circuit, lo, hi):
+        self.data = circuit.data[lo:hi]
+        self.num_qubits = circuit.num_qubits
+        self._c = circuit
+
+    def find_bit(self, q):
+        return self._c.find_bit(q)
+
+
+def _ops(circuit, lo, hi):
+    return device_ops(_View(circuit, lo, hi))
+
+
+def _inverse_ops(ops):
+    return [(np.conj(np.asarray(m)).T, qs) for m, qs in reversed(ops)]
+
+
+def _ops_qubit(circuit, index):
+    """Integer qubit of the single-qubit gate at ``index`` (this IR or qiskit-shaped)."""
+    from ..circuit import qubit_indices
+
+    return qubit_indices(circuit, circuit.data[index])[0]
 
 
 class _SweepBase:
@@ -68,16 +92,17 @@ class SVTransitionSweep(_SweepBase):
         circ = self.compiler.full_circuit
         if self.pos is None or index < self.pos:
             self.phi.reset()
-            self.phi.apply(device_ops(_slice(circ, 0, index)))
+            self.phi.apply(_ops(circ, 0, index))
             self.chi.reset()
-            self.chi.apply(device_ops(_slice(circ, index + 1, len(circ.data)).inverse()))
+            self.chi.apply(_inverse_ops(_ops(circ, index + 1, len(circ.data))))
         elif index > self.pos:
-            self.phi.apply(device_ops(_slice(circ, self.pos, index)))
-            self.chi.apply(device_ops(_slice(circ, self.pos + 1, index + 1)))
+            self.phi.apply(_ops(circ, self.pos, index))
+            self.chi.apply(_ops(circ, self.pos + 1, index + 1))
         self.pos = index
 
     def costs(self, index, mats):
-        q = self.compiler.full_circuit.data[index].qubits[0]
+        circ = self.compiler.full_circuit
+        q = _ops_qubit(circ, index)
         t = self.chi.transition(self.phi, q)
         return [float(1.0 - abs(np.sum(m * t)) ** 2) for m in mats]
 
@@ -98,15 +123,15 @@ class MPSPrefixBatch(_SweepBase):
             self.phi = self.backend.new_state()
         if self.pos is None or index < self.pos:
             self.phi.copy_from(base)
-            self.phi.apply(device_ops(_slice(circ, start, index)))
+            self.phi.apply(_ops(circ, start, index))
         elif index > self.pos:
-            self.phi.apply(device_ops(_slice(circ, self.pos, index)))
+            self.phi.apply(_ops(circ, self.pos, index))
         self.pos = index
 
     def costs(self, index, mats):
         circ = self.compiler.full_circuit
-        q = circ.data[index].qubits[0]
-        suffix = ops_array(device_ops(_slice(circ, index + 1, len(circ.data))))
+        q = _ops_qubit(circ, index)
+        suffix = ops_array(_ops(circ, index + 1, len(circ.data)))
         while len(self.pool) < len(mats):
             self.pool.append(self.backend.new_state())
         states = self.pool[: len(mats)]

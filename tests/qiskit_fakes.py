@@ -18,11 +18,12 @@ class Qubit:
 
 
 class Gate:
-    def __init__(self, name, num_qubits, params=(), matrix=None):
+    def __init__(self, name, num_qubits, params=(), matrix=None, label=None):
         self.name = name
         self.num_qubits = num_qubits
         self.params = list(params)
         self._m = matrix
+        self.label = label
 
     def to_matrix(self):
         if self._m is not None:
@@ -81,7 +82,7 @@ def from_ir(ir_circuit):
         elif op.name == "unitary":
             g = Gate("unitary", op.num_qubits, [], np.asarray(op.params[0]))
         else:
-            g = Gate(op.name, op.num_qubits, op.params)
+            g = Gate(op.name, op.num_qubits, op.params, label=getattr(op, "label", None))
         out.append(g, list(ins.qubits))
     return out
 
@@ -118,6 +119,7 @@ def fake_reference_modules():
                  "adaptaqc.backends.aer_sv_backend", "adaptaqc.compilers", "adaptaqc.compilers.approximate_compiler",
                  "adaptaqc.compilers.adapt", "adaptaqc.compilers.adapt.adapt_compiler",
                  "adaptaqc.utils", "adaptaqc.utils.gradients", "adaptaqc.utils.entanglement_measures",
+                 "adaptaqc.utils.cost_minimiser",
                  "adaptaqc.utils.circuit_operations", "adaptaqc.utils.utilityfunctions",
                  "aqc_research", "aqc_research.mps_operations"):
         mods[name] = types.ModuleType(name)
@@ -192,6 +194,107 @@ def fake_reference_modules():
                     self.backend_options, self.execute_kwargs, self.circ_mps))
             return entanglement_measures
 
+    # ---- the Rotoselect / Rotosolve path: cost_minimiser.py:267-368 as the reference runs it, with
+    # circuit_operations_basic.py:70-99 (replace_1q_gate), :202 (SUPPORTED_1Q_GATES) and
+    # utilityfunctions.py:34-57 (minimum_of_sinusoidal, restated in oracle/adapt_host.py) ----
+    cmod = mods["adaptaqc.utils.cost_minimiser"]
+
+    def create_1q_gate(gate_name, angle):  # circuit_operations_basic.py:20-34
+        return Gate(gate_name, 1, [angle], label=gate_name)
+
+    def replace_1q_gate(circuit, gate_index, gate_name, angle):
+        if gate_name is None:
+            return
+        ci = circuit.data[gate_index]
+        circuit.data[gate_index] = CircuitInstruction(create_1q_gate(gate_name, angle), ci.qubits, ci.clbits)
+
+    def is_supported_1q_gate(gate):
+        return gate.name in co.SUPPORTED_1Q_GATES
+
+    class CostMinimiser:
+        def __init__(self, cost_finder, variational_circuit_range, full_circuit, rotosolve_fraction=1.0):
+            self.cost_finder = cost_finder
+            self.variational_circuit_range = variational_circuit_range
+            self.full_circuit = full_circuit
+            self.rotosolve_fraction = rotosolve_fraction
+
+        def _reduce_cost(self, change_1q_gate_kind=False, indexes_to_modify=None):
+            cost = 1
+            variational_circuit_range = self.variational_circuit_range()
+            if indexes_to_modify is None:
+                indexes_to_modify = variational_circuit_range
+            else:
+                indexes_to_modify = (max(indexes_to_modify[0], variational_circuit_range[0]),
+                                     min(indexes_to_modify[1], variational_circuit_range[1]))
+            sample = list(range(*indexes_to_modify))
+            for index in sample:
+                old_gate = self.full_circuit.data[index].operation
+                if change_1q_gate_kind and cmod.co.is_supported_1q_gate(old_gate):
+                    cost = self.replace_with_best_1q_gate(index)
+                elif cmod.co.is_supported_1q_gate(old_gate):
+                    angle, cost = self.find_best_angle(index, old_gate.label)
+                    cmod.co.replace_1q_gate(self.full_circuit, index, old_gate.label, angle)
+                else:
+                    continue
+            return cost
+
+        def replace_with_best_1q_gate(self, gate_index):
+            cmod.co.replace_1q_gate(self.full_circuit, gate_index, "rx", 0)
+            cost_identity = self.cost_finder()
+            best_gate_name, best_gate_angle, best_gate_cost = None, None, 1
+            for gate_name in cmod.SUPPORTED_1Q_GATES:
+                min_angle, cost = self.find_best_angle(gate_index, gate_name, cost_identity)
+                if cost < best_gate_cost:
+                    best_gate_name, best_gate_angle, best_gate_cost = gate_name, min_angle, cost
+            cmod.co.replace_1q_gate(self.full_circuit, gate_index, best_gate_name, best_gate_angle)
+            return best_gate_cost
+
+        def find_best_angle(self, gate_index, gate_name, cost_for_identity=None):
+            circ_instr = self.full_circuit.data[gate_index]
+            costs = []
+            angles_to_run = [0, cmod.np.pi / 2, -cmod.np.pi / 2]
+            if cost_for_identity is not None:
+                costs.append(cost_for_identity)
+                angles_to_run.remove(0)
+            for theta in angles_to_run:
+                cmod.co.replace_1q_gate(self.full_circuit, gate_index, gate_name, theta)
+                costs.append(self.cost_finder())
+            theta_min, cost_min = cmod.minimum_of_sinusoidal(costs[0], costs[1], costs[2])
+            self.full_circuit.data[gate_index] = circ_instr
+            return theta_min, cost_min
+
+    CostMinimiser.__module__ = "adaptaqc.utils.cost_minimiser"
+
+    class ApproximateCompiler:
+        """The attributes evaluate_cost and the backends read (approximate_compiler.py:514-527)."""
+
+        def __init__(self, full_circuit, backend):
+            self.full_circuit = full_circuit
+            self.backend = backend
+            self.cost_evaluation_counter = 0
+            self.optimise_local_cost = False
+            self.soften_global_cost = False
+            self.global_cost_history = []
+            self.backend_options = {}
+            self.execute_kwargs = {}
+
+        def evaluate_cost(self):
+            self.cost_evaluation_counter += 1
+            if self.optimise_local_cost:
+                return self.backend.evaluate_local_cost(self)
+            return self.backend.evaluate_global_cost(self)
+
+    from oracle.adapt_host import minimum_of_sinusoidal
+
+    co.SUPPORTED_1Q_GATES = ["rx", "ry", "rz"]
+    co.replace_1q_gate = replace_1q_gate
+    co.is_supported_1q_gate = is_supported_1q_gate
+    cmod.np = np
+    cmod.co = co
+    cmod.SUPPORTED_1Q_GATES = co.SUPPORTED_1Q_GATES
+    cmod.minimum_of_sinusoidal = minimum_of_sinusoidal
+    cmod.CostMinimiser = CostMinimiser
+    mods["adaptaqc.compilers.approximate_compiler"].ApproximateCompiler = ApproximateCompiler
     uf.is_statevector_backend = is_statevector_backend
     co.run_circuit_without_transpilation = run_circuit_without_transpilation
     em.partial_trace = partial_trace
