@@ -2470,6 +2470,10 @@ int aqc_mps_chain_ticks(double* out) {
   AQC_HIP_CHECK(hipMemcpyFromSymbol(t, HIP_SYMBOL(g_chain_ticks), sizeof(t)));
   const unsigned long long z[5] = {0, 0, 0, 0, 0};
   AQC_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_chain_ticks), z, sizeof(z)));
+  unsigned long long t2[5] = {0, 0, 0, 0, 0};  // k_chain256's (the two chains' phases add up)
+  AQC_HIP_CHECK(hipMemcpyFromSymbol(t2, HIP_SYMBOL(g_chain256_ticks), sizeof(t2)));
+  AQC_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_chain256_ticks), z, sizeof(z)));
+  for (int i = 0; i < 5; ++i) t[i] += t2[i];
   for (int i = 0; i < 5; ++i) out[i] = (double)t[i];
   return AQC_OK;
 }

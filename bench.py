@@ -253,6 +253,10 @@ def main():
     ap.add_argument("--simulate-world", type=int, default=0,
                     help="projection only (1 process): rank 0's share of an N-GPU run -- pair shard of N, "
                          "sweep over N x states -- with the all-gather replaced by a local scatter")
+    ap.add_argument("--shard", default="states", choices=("states", "pairs"),
+                    help="states (default): each rank sweeps all 1225 pairs of its own states, one all-gather "
+                         "of the per-state (best pair, score); pairs: every rank holds all N x states and "
+                         "sweeps its pair shard, all-gather of the scores (the single-state layout)")
     ap.add_argument("--strong", action="store_true",
                     help="config 4 strong scaling: a fixed global batch of chi=128 sweeps sharded by state")
     ap.add_argument("--global-states", type=int, default=512, help="--strong: sweeps in the global batch")
@@ -281,26 +285,31 @@ def main():
     from adaptaqc_amd import _lib
     from adaptaqc_amd.device import (DeviceMPS, OpsBatch, apply_batch, check_batch, copy_batch, overlap_zero_batch,
                                      pair_grads_batch)
-    from adaptaqc_amd.sharding import PairShard, gather_scores
+    from adaptaqc_amd.sharding import PairShard, StateShard, best_pairs, gather_best, gather_scores
     from adaptaqc_amd.utils.constants import coupling_map_fully_entangled
 
     n, B = N_QUBITS, args.states
     sim = args.simulate_world if (args.simulate_world > 1 and world == 1) else 0
     shard_world = sim or world
     S = shard_world * B
+    by_state = args.shard == "states"
     cmap = coupling_map_fully_entangled(n)
-    shard = PairShard(cmap, n, rank, shard_world)
+    # pair sharding: every rank sweeps its pairs over all S states; state sharding: all pairs of its
+    # own B states (the shard below then covers every pair)
+    shard = PairShard(cmap, n, 0 if by_state else rank, 1 if by_state else shard_world)
+    sshard = StateShard(S, 0 if sim else rank, shard_world)
     layer, gens, deg, u0, gm = layer_inputs()
     svec = np.zeros((n, 2), complex)
     svec[:, 0] = 1.0
 
     distinct = bench_states(n, CHI, min(args.distinct, S), args.state_kind)
     states = []
-    for s in range(S):
+    # state sharding holds only this rank's B states (global indices rank B ..); pair sharding all S
+    for s in (range(rank * B, (rank + 1) * B) if by_state else range(S)):
         d = DeviceMPS(n, CHI, 1e-16, CHI)
         d.load_aer(distinct[s % len(distinct)])
         states.append(d)
-    own = states[rank * B:(rank + 1) * B]
+    own = states if by_state else states[rank * B:(rank + 1) * B]
     work = [DeviceMPS(n, CHI, 1e-16, CHI) for _ in range(B * len(DISTANCES))]
     reload_src = [own[k // len(DISTANCES)] for k in range(len(work))]
     rng = np.random.default_rng(7)
@@ -314,11 +323,19 @@ def main():
     # same layer structure would (angles can change in place); the replay itself runs every step
     layer_batch = OpsBatch(layer_ops)
     prio = np.ones(len(cmap))
-    local_scores = torch.zeros((S, max(len(shard.local_pairs), 1)), dtype=torch.float64, device="cuda")
+    local_scores = torch.zeros((len(states), max(len(shard.local_pairs), 1)), dtype=torch.float64, device="cuda")
     prio_t = torch.as_tensor(prio, device="cuda")
 
     def sweep():
         # (i) sharded candidate sweep + all-gather + arg-max
+        if by_state:
+            # every pair of this rank's states, the per-state arg-max on the rank, then one all-gather
+            # of (best pair, score) per state (RCCL over xGMI; the projection repeats rank 0's block)
+            pair_grads_batch(states, svec, shard.local_pairs, u0, gm, deg, out=local_scores.data_ptr())
+            b, sc = best_pairs(local_scores, prio)
+            if sim:
+                return local_scores, b.repeat(sim)
+            return local_scores, gather_best(b, sc, sshard)[0]
         if shard.local_pairs:
             pair_grads_batch(states, svec, shard.local_pairs, u0, gm, deg, out=local_scores.data_ptr())
         if sim:  # projection: rank 0's scores scattered locally, no collective
@@ -493,7 +510,9 @@ def main():
                 "workload": "config3: 50-qubit chi=64 MPS; per state 1225-pair identity_resolvable gradient sweep "
                             "(sharded, RCCL all-gather, arg-max) + 4 thinly-dressed-layer overlap evals (d=1,2,5,25)",
                 "n_qubits": n, "chi": CHI, "states_per_rank": B, "global_states": S,
-                "pairs": len(cmap), "generators": int(len(deg)), "parallelism": f"pairs sharded x{world}",
+                "pairs": len(cmap), "generators": int(len(deg)),
+                "parallelism": (f"states sharded x{world} (all-gather of per-state best pair)" if by_state
+                                else f"pairs sharded x{world}"),
             },
             "breakdown_ms": {f: round(v["ms"] / args.steps, 3) for f, v in fams.items()},
             "by_kind": {

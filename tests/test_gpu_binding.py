@@ -171,3 +171,166 @@ def test_reference_isl_sweep_mps():
     np.testing.assert_allclose(per_pair, want, atol=1e-9)
     np.testing.assert_allclose(batched, want, atol=1e-9)
     assert int(np.argmax(per_pair)) == int(np.argmax(want)) == int(np.argmax(batched))
+
+
+def _thin_layer_ir(full, pairs, rng):
+    """Thinly-dressed CNOT layers (rz, rz, cx, rz, rz with the kinds as labels,
+    circuit_operations_basic.py:135-189) with random angles appended to ``full``."""
+    from adaptaqc_amd.circuit import Operation
+
+    for a, b in pairs:
+        for q in (a, b):
+            full.append(Operation("rz", 1, [float(rng.uniform(-np.pi, np.pi))], "rz"), [q])
+        full.cx(a, b)
+        for q in (a, b):
+            full.append(Operation("rz", 1, [float(rng.uniform(-np.pi, np.pi))], "rz"), [q])
+
+
+def _oracle_rotoselect(n, aer, full_ir, start, rotoselect, chi):
+    """oracle/adapt_host.py's call sequence (cost_minimiser.py:267-368) with the oracle's MPS replay
+    as the cost: (final ops, final cost, evaluation log)."""
+    from oracle import adapt_host as AH
+    from oracle import mps as M
+
+    ops = []
+    for ins in full_ir.data[start:]:
+        op = ins.operation
+        ops.append([op.name, tuple(ins.qubits), [float(p) for p in op.params], op.label])
+    base = M.MPS.from_aer(aer) if aer is not None else None
+
+    def cost_fn(o):
+        st = M.run_circuit(n, [(x[0], x[1], tuple(x[2])) for x in o], 1e-16, chi, mps=base)
+        return 1.0 - abs(M.mps_dot(st.preprocessed(), M.zero_mps(n))) ** 2
+
+    log = []
+    cost = AH.reduce_cost(ops, cost_fn, rotoselect, (0, len(ops)), log)
+    return ops, cost, log
+
+
+@pytest.mark.parametrize("rotoselect", [True, False])
+def test_reference_rotoselect_batched_mps(rotoselect):
+    """the reference's own CostMinimiser (restated in qiskit_fakes) on a 50-qubit
+    chi = 64 MPS target with one thinly-dressed layer, after install(): every gate's 7 (Rotoselect) or
+    3 (Rotosolve) candidates come from one batched evaluation (cached prefix MPS + the candidates
+    replayed through the suffix together), the reference's selection code runs on them.  Same gate
+    kinds and angles as the oracle's call sequence (angles 1e-6, costs 1e-6), the reference's
+    cost_evaluation_counter, and the same circuit as the reference's per-candidate path through the
+    same device backend (1e-9).  The batched gate's latency is reported against this package's
+    own compiler path on the same circuit (cached_rotations) and bounded at 1.5x it."""
+    import time
+
+    import bench
+    from adaptaqc_amd import reference_binding as rb
+    from adaptaqc_amd.backends import AerMPSBackend, mps_sim_with_args
+    from adaptaqc_amd.circuit import QuantumCircuit
+
+    n, chi = 50, 64
+    rng = np.random.default_rng(77)
+    aer = bench.near_product_mps(n, chi, 12)
+    full = QuantumCircuit(n)
+    full.set_matrix_product_state(aer)
+    _thin_layer_ir(full, [(20, 21)], rng)
+    want_ops, want_cost, log = _oracle_rotoselect(n, aer, full, 1, rotoselect, chi)
+    n_rot = sum(1 for ins in full.data[1:] if ins.operation.name == "rz")
+    be = AerMPSBackend(mps_sim_with_args(max_chi=chi))
+    # this package's own compiler path on the same circuit (utils/cached_rotations.py), warmed once
+    from adaptaqc_amd.utils.cached_rotations import make_evaluator
+    from adaptaqc_amd.utils.cost_minimiser import CostMinimiser as OwnCM
+    from conftest import FakeCompiler
+
+    def own_run():
+        fc = FakeCompiler(full.copy())
+        fc.backend = be
+        fc.cost_evaluation_counter = 0
+        fc.optimise_local_cost = False
+
+        def own_cost():
+            fc.cost_evaluation_counter += 1
+            return be.evaluate_global_cost(fc)
+
+        own = OwnCM(own_cost, lambda: (1, len(fc.full_circuit.data)), fc.full_circuit,
+                    evaluator_factory=lambda: make_evaluator(fc))
+        own_cost()
+        t0 = time.perf_counter()
+        own._reduce_cost(rotoselect, None)
+        return time.perf_counter() - t0
+
+    own_run()
+    t_own = own_run()
+    with installed_fake_reference() as mods:
+        rb.install(import_missing=False)
+        CM = mods["adaptaqc.utils.cost_minimiser"].CostMinimiser
+        AC = mods["adaptaqc.compilers.approximate_compiler"].ApproximateCompiler
+        runs = {}
+        for mode in ("per_candidate", "batched"):
+            q = from_ir(full)
+            comp = AC(q, be)
+            cmz = CM(comp.evaluate_cost, lambda q=q: (1, len(q.data)), q)
+            comp.evaluate_cost()  # the cached payload on the device
+            comp.cost_evaluation_counter = 0
+            t0 = time.perf_counter()
+            if mode == "batched":
+                cost = cmz._reduce_cost(rotoselect, None)
+            else:  # the reference's own per-candidate code on the same device backend
+                cost = CM._reduce_cost.__wrapped__(cmz, rotoselect, None)
+            runs[mode] = (q, cost, comp.cost_evaluation_counter, time.perf_counter() - t0)
+        q, cost, count, t_b = runs["batched"]
+        assert count == (7 if rotoselect else 3) * n_rot == len(log)
+        assert runs["per_candidate"][2] == count
+        assert abs(cost - want_cost) < 1e-6, (cost, want_cost)
+        assert abs(cost - runs["per_candidate"][1]) < 1e-9
+        for k, ins in enumerate(q.data[1:]):
+            w = want_ops[k]
+            assert ins.operation.name == w[0], (k, ins.operation.name, w[0])
+            if ins.operation.params:
+                assert abs(float(ins.operation.params[0]) - w[2][0]) < 1e-6
+                qp = runs["per_candidate"][0].data[1 + k].operation
+                assert abs(float(ins.operation.params[0]) - float(qp.params[0])) < 1e-9
+    print(f"\nper gate: reference CostMinimiser batched {1e3 * t_b / n_rot:.2f} ms, per-candidate "
+          f"{1e3 * runs['per_candidate'][3] / n_rot:.2f} ms, this package's compiler {1e3 * t_own / n_rot:.2f} ms")
+    assert t_b <= 1.5 * t_own + 2e-3 * n_rot
+    assert t_b < runs["per_candidate"][3]
+
+
+def test_reference_rotoselect_batched_sv():
+    """The same drop-in on the statevector backend (the transition-matrix evaluator): a 10-qubit
+    random state plus one thinly-dressed layer, Rotoselect through the reference's CostMinimiser
+    after install(): gate kinds / angles / costs as the oracle's call sequence with exact SV costs
+    (1e-10), the reference's evaluation count."""
+    import os
+
+    from adaptaqc_amd import reference_binding as rb
+    from adaptaqc_amd.backends import AerSVBackend
+    from oracle import adapt_host as AH
+    from oracle import sv as osv
+
+    os.environ.setdefault("QISKIT_IN_PARALLEL", "FALSE")
+    n = 10
+    full = _random_ir(n, 5, layers=3)
+    start = len(full.data)
+    _thin_layer_ir(full, [(3, 4), (6, 2)], np.random.default_rng(5))
+    ops = []
+    for ins in full.data:
+        op = ins.operation
+        ops.append([op.name, tuple(ins.qubits), [float(p) for p in op.params], op.label])
+
+    def cost_fn(o):
+        return 1.0 - abs(osv.simulate(n, [(x[0], x[1], tuple(x[2])) for x in o])[0]) ** 2
+
+    log = []
+    want = AH.reduce_cost(ops, cost_fn, True, (start, len(ops)), log)
+    with installed_fake_reference() as mods:
+        rb.install(import_missing=False)
+        CM = mods["adaptaqc.utils.cost_minimiser"].CostMinimiser
+        AC = mods["adaptaqc.compilers.approximate_compiler"].ApproximateCompiler
+        q = from_ir(full)
+        comp = AC(q, AerSVBackend())
+        cmz = CM(comp.evaluate_cost, lambda: (start, len(q.data)), q)
+        cost = cmz._reduce_cost(True, None)
+        assert comp.cost_evaluation_counter == len(log)
+        assert abs(cost - want) < 1e-10
+        for k in range(start, len(q.data)):
+            op = q.data[k].operation
+            assert op.name == ops[k][0]
+            if op.params:
+                assert abs(float(op.params[0]) - ops[k][2][0]) < 1e-8

@@ -179,3 +179,45 @@ def test_register_tile_path_vs_oracle_and_lds_kernel(monkeypatch):
         monkeypatch.delenv("AQC_SV_TILE")
         d2.apply(dops)
         np.testing.assert_allclose(got, d2.get(), atol=1e-13, err_msg=f"n={n} (lds kernel)")
+
+
+def test_config2_exact_workload_vs_oracle_goldens():
+    """BASELINE config 2 exactly as tools/configs_bench.py times it -- 20 qubits,
+    brickwork depth 20, seeds 0..9, with 0 / 10 / 50 thinly-dressed layers -- all 30 circuits
+    through the register-tile SV path against the oracle's values (tests/golden/config2_sv.npz, made
+    by tests/golden/make_config2_golden.py from oracle/sv.py): global cost within 1e-10, the 20 <Z_i>
+    within 1e-10, four projections of the whole state onto seeded random unit vectors within 1e-10.
+    The op lists are checked to be the profiled workload's (configs_bench.brickwork_sv_ops)."""
+    import os
+    import sys
+
+    from adaptaqc_amd import gates as G
+    from adaptaqc_amd import _lib
+    from adaptaqc_amd.device import DeviceSV
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, os.path.join(here, "golden"))
+    sys.path.insert(0, os.path.join(os.path.dirname(here), "tools"))
+    import configs_bench
+    import make_config2_golden as mk
+
+    gold = np.load(os.path.join(here, "golden", "config2_sv.npz"))
+    R = mk.probes()
+    d = DeviceSV(mk.N)
+    k = 0
+    for seed in mk.SEEDS:
+        for tail in mk.TAILS:
+            named = mk.config2_named_ops(seed, tail)
+            ops = configs_bench.brickwork_sv_ops(mk.N, mk.DEPTH, seed, tail)
+            assert len(ops) == len(named)
+            want = _lib.ops_array([(G.one_qubit(nm, list(p)) if len(q) == 1 else G.TWO_QUBIT[nm], q) for nm, q, p in named])
+            np.testing.assert_array_equal(ops, want)
+            d.reset()
+            d.apply(ops)
+            a0 = d.amp0()
+            assert abs((1 - abs(a0) ** 2) - (1 - abs(gold["amp0"][k]) ** 2)) < TOL
+            assert abs(a0 - gold["amp0"][k]) < TOL
+            np.testing.assert_allclose(d.z_all(), gold["z"][k], atol=1e-10)
+            psi = d.get()
+            np.testing.assert_allclose(R.conj() @ psi, gold["proj"][k], atol=1e-10)
+            k += 1

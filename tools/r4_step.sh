@@ -19,3 +19,6 @@ run suite 700 python3 -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-me
 [ "${STAGE:-2}" -ge 4 ] || exit 0
 run bench 400 python3 bench.py --steps 20 --warmup 5 || exit $?
 cp gpurun_out/bench.log gpurun_out/bench.json
+# (STAGE>=5) the same bench on the 1024-thread chain for comparison
+[ "${STAGE:-2}" -ge 5 ] || exit 0
+AQC_CHAIN=1024 run bench1024 400 python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-latency --no-parity || exit $?
