@@ -180,6 +180,17 @@ __device__ __noinline__ void s3_stage(const S3Ctx& cx_in, int k0, int k1, bool f
   const int gdr0 = base + dr[0], gdc0 = base + dc[0], gdr1 = base + dr[1], gdc1 = base + dc[1];
   cplx g[TR][TC];
   cplx gd[2] = {aqc::cmk(0, 0), aqc::cmk(0, 0)};
+  // phase ticks of thread 0 (summed into g_gram_ticks: [6] pass + zlarfg + barrier A, [7] row sums
+  // + p / v / z + barrier B, [9] S1, [10] the stage's entry load / exit repack)
+  unsigned long long t_pa = 0, t_pb = 0, t_m = tid == 0 ? __builtin_amdgcn_s_memtime() : 0ull;
+  auto lap = [&](unsigned long long& acc) {
+    if (tid == 0) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      acc += t - t_m;
+      t_m = t;
+    }
+  };
+  unsigned long long t_s1 = 0, t_io = 0;
   if (first) {
     // ---- S1: G = X^H X into the tiles and diagonal elements: X staged through the LDS in chunks
     // of 8 rows, column c at position (c & 3) 32 + (c >> 2) (lanes with consecutive R read
@@ -262,6 +273,7 @@ __device__ __noinline__ void s3_stage(const S3Ctx& cx_in, int k0, int k1, bool f
       const int a = s ? gdr1 : gdr0, b = s ? gdc1 : gdc0;
       if (dr[s] >= 0 && b == 0 && a > 0) vec[3 * a + 2] = gd[s];
     }
+    lap(t_s1);
   } else {
     // ---- the trailing block from the scratch (lower triangle, row-major S x S) ----
     auto ld = [&](int r, int c) {  // global indices >= base
@@ -276,6 +288,7 @@ __device__ __noinline__ void s3_stage(const S3Ctx& cx_in, int k0, int k1, bool f
     if (dr[1] >= 0) gd[1] = ld(gdr1, gdc1);
   }
   __syncthreads();
+  lap(first ? t_s1 : t_io);
   // ---- the columns ----
   for (int k = k0; k < k1; ++k) {
     const int kl = k - base;
@@ -410,6 +423,7 @@ __device__ __noinline__ void s3_stage(const S3Ctx& cx_in, int k0, int k1, bool f
       if (AQC_S3_PRIO) __builtin_amdgcn_s_setprio(0);
     }
     __syncthreads();  // A: partials, gk1b, reflector k's scalars
+    lap(t_pa);
     {
       // rows of the stage: GPR threads each, a row's sum over its contribution list
       int t = tid;
@@ -417,8 +431,17 @@ __device__ __noinline__ void s3_stage(const S3Ctx& cx_in, int k0, int k1, bool f
       const int rloc = t / GPR, h = t % GPR;
       const int Rr = rloc / TR, ir = rloc % TR, n = 32 - (Rr >> 1);
       const lcplx* gl = grid + TR * tri_off(Rr) + ir;
-      cplx y = aqc::cmk(0, 0);
-      for (int o = h; o < n; o += GPR) y = aqc::cadd(y, gl[TR * o]);
+      // (a fixed count of independent loads, clamped and masked: issued together instead of one
+      // LDS round trip per contribution)
+      constexpr int NO = (32 + GPR - 1) / GPR;
+      cplx part[4] = {aqc::cmk(0, 0), aqc::cmk(0, 0), aqc::cmk(0, 0), aqc::cmk(0, 0)};
+#pragma unroll
+      for (int u = 0; u < NO; ++u) {
+        const int o = h + GPR * u;
+        const cplx v = gl[TR * (o < n ? o : n - 1)];
+        if (o < n) part[u & 3] = aqc::cadd(part[u & 3], v);
+      }
+      cplx y = aqc::cadd(aqc::cadd(part[0], part[1]), aqc::cadd(part[2], part[3]));
       y.x = group_sum_n<GPR>(y.x);
       y.y = group_sum_n<GPR>(y.y);
       const int r = base + rloc;
@@ -447,6 +470,7 @@ __device__ __noinline__ void s3_stage(const S3Ctx& cx_in, int k0, int k1, bool f
       if (lane == 0) ktp[wave] = aqc::cmk(ktx, kty);
     }
     __syncthreads();  // B: reflector k's p, v, z and p^H v
+    lap(t_pb);
   }
   if (k1 < C - 1) {
     // ---- repack: the next stage's trailing block (rows / columns >= nb) to the scratch ----
@@ -486,6 +510,13 @@ __device__ __noinline__ void s3_stage(const S3Ctx& cx_in, int k0, int k1, bool f
       if (dr[sl] >= 0 && r == kk && c == kk) dS[kk] = gd[sl].x - upd;
     }
     __syncthreads();
+  }
+  lap(t_io);
+  if (tid == 0) {
+    atomicAdd(&g_gram_ticks[6], t_pa);
+    atomicAdd(&g_gram_ticks[7], t_pb);
+    atomicAdd(&g_gram_ticks[9], t_s1);
+    atomicAdd(&g_gram_ticks[10], t_io);
   }
 }
 

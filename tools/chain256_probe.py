@@ -54,5 +54,7 @@ for ns in sizes:
            "us_per_update_wall": 1e3 * launch_ms * reps / upd,
            "ticks_per_update": {k: round(float(v) / upd) for k, v in zip(("theta", "svd", "rank", "split", "one_site"), t)},
            "gram_ticks_per_svd": {k: round(float(g[i]) / upd) for k, i in
-                                  (("S1", 0), ("S1S3|S3", 1), ("S4", 2), ("S5", 3), ("S6", 4), ("out", 5))}}
+                                  (("S1", 0), ("S1S3|S3", 1), ("S4", 2), ("S5", 3), ("S6", 4), ("out", 5),
+                                   ("256:S3pass+A|1024:S3steps", 6), ("256:S3rows+B|1024:S5inv", 7),
+                                   ("1024:S3phaseA", 8), ("256:S1", 9), ("256:repack", 10))}}
     print(json.dumps(row), flush=True)
