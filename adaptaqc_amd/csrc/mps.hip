@@ -75,9 +75,10 @@ double g_jacobi_tiny_t = kDefaultTinyT;
 // (aqc_mps_set_jacobi_noise; jacobi_reg_body)
 constexpr double kDefaultJacobiNoise = 0.0;
 double g_jacobi_noise = kDefaultJacobiNoise;
-// Fused per-state chain (k_chain) for batches of >= kChainMinStates states at 2 chi = 128.
+// Fused per-state chain (k_chain) for batches of >= g_chain_min_states states at 2 chi = 128
+// (aqc_mps_set_fused_chain: 0 off, 1 from 32 states, 2 from one state).
 bool g_fused_chain = true;
-constexpr int kChainMinStates = 32;
+int g_chain_min_states = 32;
 // dynamic LDS of the 1024-thread two-site kernels: four 64 x 64 GEMM tiles (>= the register
 // Jacobi's 64 x 129 complex exchange buffer)
 constexpr int kChainLdsBytes = 4 * (int)sizeof(aqc::GemmLds);
@@ -1895,13 +1896,14 @@ std::vector<std::vector<const DevOp*>> level_ops(const std::vector<DevOp>& ops, 
 
 // Batches at 2 chi = 128: every state's op list runs in one k_chain workgroup (longest lists
 // first, so that the short ones fill in behind them).
-// k_chain256 (two states per CU) unless AQC_CHAIN=1024 or the Gram path is off (its fallback, the
-// register Jacobi, needs the 1024-thread chain)
+// k_chain (one state per CU) unless aqc_mps_set_chain_threads(256) / AQC_CHAIN=256 selects
+// k_chain256 (two states per CU, measured slower: DESIGN.md "two updates per CU") -- and only while
+// the Gram path is on (its fallback, the register Jacobi, needs the 1024-thread chain)
 int g_chain256 = -1;
 bool use_chain256() {
   if (g_chain256 < 0) {
     const char* e = std::getenv("AQC_CHAIN");
-    g_chain256 = (e && std::strcmp(e, "1024") == 0) ? 0 : 1;
+    g_chain256 = (e && std::strcmp(e, "256") == 0) ? 1 : 0;
   }
   return g_chain256 && g_svd_gram;
 }
@@ -1998,7 +2000,7 @@ int run_waves(aqc_mps_t* hs, int ns, std::vector<std::vector<DevOp>>& lists) {
   {
     int cap_max = 0;
     for (int s = 0; s < ns; ++s) cap_max = std::max(cap_max, hs[s]->d.cap);
-    if (g_fused_chain && ns >= kChainMinStates && 2 * cap_max > 64 && 2 * cap_max <= 128)
+    if (g_fused_chain && ns >= g_chain_min_states && 2 * cap_max > 64 && 2 * cap_max <= 128)
       return run_chains(hs, ns, lists, cap_max);
   }
   hipStream_t st = aqc::mps_stream();
@@ -2479,7 +2481,15 @@ int aqc_mps_chain_ticks(double* out) {
 }
 
 int aqc_mps_set_fused_chain(int on) {
+  AQC_REQUIRE(on >= 0 && on <= 2, "aqc_mps_set_fused_chain: 0, 1 or 2");
   g_fused_chain = on != 0;
+  g_chain_min_states = on == 2 ? 1 : 32;
+  return AQC_OK;
+}
+
+int aqc_mps_set_chain_threads(int threads) {
+  AQC_REQUIRE(threads == 256 || threads == 1024, "aqc_mps_set_chain_threads: 256 or 1024");
+  g_chain256 = threads == 256 ? 1 : 0;
   return AQC_OK;
 }
 

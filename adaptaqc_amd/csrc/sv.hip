@@ -227,7 +227,7 @@ __device__ __forceinline__ void reg_apply(cplx (&a)[16], const SegGate& g) {
 
 __global__ __launch_bounds__(kThreads) void k_sv_tile_reg(cplx* __restrict__ state, const SegHeader* __restrict__ hdr,
                                                          const PhaseHdr* __restrict__ phases,
-                                                         const SegGate* __restrict__ gates) {
+                                                         const SegGate* __restrict__ gates, int from_zero) {
   constexpr int K = kRegTileBits;
   __shared__ cplx tile[1 << K];
   __shared__ SegGate gl[2][kPhaseMaxGates];
@@ -247,8 +247,13 @@ __global__ __launch_bounds__(kThreads) void k_sv_tile_reg(cplx* __restrict__ sta
   constexpr int kPer = (1 << K) / kThreads;
   {
     cplx v[kPer];
+    if (from_zero) {  // a deferred aqc_sv_reset: the tile of |0...0> (index 0 in tile 0)
 #pragma unroll
-    for (int r = 0; r < kPer; ++r) v[r] = aqc::ldg(state + gidx(tid + r * kThreads));
+      for (int r = 0; r < kPer; ++r) v[r] = aqc::cmk(blockIdx.x == 0 && tid + r * kThreads == 0 ? 1.0 : 0.0, 0.0);
+    } else {
+#pragma unroll
+      for (int r = 0; r < kPer; ++r) v[r] = aqc::ldg(state + gidx(tid + r * kThreads));
+    }
 #pragma unroll
     for (int r = 0; r < kPer; ++r) tile[swz(tid + r * kThreads)] = v[r];
   }
@@ -370,14 +375,22 @@ struct HostSeg {
   uint64_t qmask = 0;
 };
 
-std::vector<HostSeg> build_segments(const aqc_op_t* ops, int nops, int K, int n, uint64_t reserve = 0) {
-  std::vector<HostSeg> segs;
-  std::vector<char> done(nops, 0);
-  int remaining = nops;
-  int first = 0;
-  while (remaining > 0) {
+// Greedy segmentation, one segment per next(): a segment takes every not-yet-placed op, in order,
+// whose qubits fit in the K tile bits and that no skipped op on its qubits precedes.  Produced one
+// at a time so that aqc_sv_apply launches the first segment before the rest are formed.
+struct SegBuilder {
+  const aqc_op_t* ops;
+  int nops, K, n;
+  uint64_t reserve;
+  std::vector<char> done;
+  int remaining, first = 0;
+  SegBuilder(const aqc_op_t* o, int no, int k, int nq, uint64_t res)
+      : ops(o), nops(no), K(k), n(nq), reserve(res), done(no, 0), remaining(no) {}
+  bool next(HostSeg& seg) {
+    seg.gates.clear();
+    seg.qmask = 0;
+    if (remaining <= 0) return false;
     while (first < nops && done[first]) ++first;
-    HostSeg seg;
     uint64_t blocked = 0;
     for (int i = first; i < nops; ++i) {
       if (done[i]) continue;
@@ -398,8 +411,15 @@ std::vector<HostSeg> build_segments(const aqc_op_t* ops, int nops, int K, int n,
       }
       if (__builtin_popcountll(blocked) >= n) break;
     }
-    segs.push_back(std::move(seg));
+    return true;
   }
+};
+
+std::vector<HostSeg> build_segments(const aqc_op_t* ops, int nops, int K, int n, uint64_t reserve = 0) {
+  std::vector<HostSeg> segs;
+  SegBuilder b(ops, nops, K, n, reserve);
+  HostSeg seg;
+  while (b.next(seg)) segs.push_back(seg);
   return segs;
 }
 
@@ -765,7 +785,21 @@ struct aqc_sv_s {
   cplx* h_pinned = nullptr;
   char* d_scratch = nullptr;  // grow-only workspace of the reduction kernels (RDMs, transition)
   size_t scratch_cap = 0;
+  // aqc_sv_reset on the register-tile path is deferred: the next aqc_sv_apply's first pass forms
+  // |0...0> in its tiles instead of reading the state (no reset kernel, one 2^n read less); any
+  // other reader materialises it first (sv_materialize)
+  bool zero_pending = false;
 };
+
+static int sv_materialize(aqc_sv_t h) {
+  if (!h->zero_pending) return AQC_OK;
+  const uint64_t dim = 1ull << h->n;
+  unsigned grid = (unsigned)std::min<uint64_t>((dim + 255) / 256, 65536);
+  hipLaunchKernelGGL(k_sv_reset, dim3(grid), dim3(256), 0, h->stream, h->state, dim);
+  AQC_CHECK_LAUNCH();
+  h->zero_pending = false;
+  return AQC_OK;
+}
 
 static int sv_scratch(aqc_sv_t h, size_t bytes, char** out) {
   if (bytes > h->scratch_cap) {
@@ -778,16 +812,17 @@ static int sv_scratch(aqc_sv_t h, size_t bytes, char** out) {
   return AQC_OK;
 }
 
+// register tiles keep the lowest global bits in every tile (runs of 2^low contiguous amplitudes
+// per lane group: a tile of high qubits only reads 16-byte pieces scattered 4 KB apart)
+static uint64_t sv_reserved_bits(bool reg_tiles) {
+  if (!reg_tiles) return 0;
+  static const char* lb_env = std::getenv("AQC_SV_LOWBITS");
+  const int low = lb_env ? std::atoi(lb_env) : kRegLowBits;
+  return (1ull << std::min(std::max(low, 0), 8)) - 1ull;
+}
+
 static std::vector<HostSeg> sv_plan_segments(int n, int K, bool reg_tiles, const aqc_op_t* ops, int nops) {
-  // register tiles keep the lowest global bits in every tile (runs of 2^low contiguous amplitudes
-  // per lane group: a tile of high qubits only reads 16-byte pieces scattered 4 KB apart)
-  uint64_t reserve = 0;
-  if (reg_tiles) {
-    static const char* lb_env = std::getenv("AQC_SV_LOWBITS");
-    const int low = lb_env ? std::atoi(lb_env) : kRegLowBits;
-    reserve = (1ull << std::min(std::max(low, 0), 8)) - 1ull;
-  }
-  return build_segments(ops, nops, K, n, reserve);
+  return build_segments(ops, nops, K, n, sv_reserved_bits(reg_tiles));
 }
 
 // Segment s of the plan: its header (hdr[s], sized by the caller), its fused gates and phases
@@ -850,10 +885,12 @@ static bool sv_reg_tiles(int n) {
 
 static int sv_launch_segment(aqc_sv_t h, const SegHeader* dh, const PhaseHdr* dp, const SegGate* dg, int nblocks,
                              double flops) {
-  const double bytes = 32.0 * (double)(1ull << h->n);
+  const int from_zero = h->zero_pending ? 1 : 0;
+  const double bytes = (from_zero ? 16.0 : 32.0) * (double)(1ull << h->n);
   aqc::KernelTimer::begin(h->stream, "sv_segment", bytes, flops);
   if (h->reg_tiles) {
-    hipLaunchKernelGGL(k_sv_tile_reg, dim3(nblocks), dim3(kThreads), 0, h->stream, h->state, dh, dp, dg);
+    hipLaunchKernelGGL(k_sv_tile_reg, dim3(nblocks), dim3(kThreads), 0, h->stream, h->state, dh, dp, dg, from_zero);
+    h->zero_pending = false;
     aqc::KernelTimer::end(h->stream);
     AQC_CHECK_LAUNCH();
     return AQC_OK;
@@ -929,15 +966,16 @@ int aqc_sv_destroy(aqc_sv_t h) {
 
 int aqc_sv_reset(aqc_sv_t h) {
   AQC_REQUIRE(h, "aqc_sv_reset: null handle");
-  const uint64_t dim = 1ull << h->n;
-  unsigned grid = (unsigned)std::min<uint64_t>((dim + 255) / 256, 65536);
-  hipLaunchKernelGGL(k_sv_reset, dim3(grid), dim3(256), 0, h->stream, h->state, dim);
-  AQC_CHECK_LAUNCH();
-  return AQC_OK;
+  h->zero_pending = true;
+  return h->reg_tiles ? AQC_OK : sv_materialize(h);
 }
 
 int aqc_sv_copy(aqc_sv_t dst, const aqc_sv_t src) {
   AQC_REQUIRE(dst && src && dst->n == src->n, "aqc_sv_copy: handle mismatch");
+  if (dst == src) return sv_materialize(src);
+  int rc = sv_materialize(src);
+  if (rc != AQC_OK) return rc;
+  dst->zero_pending = false;  // overwritten below
   AQC_HIP_CHECK(hipStreamSynchronize(src->stream));
   AQC_HIP_CHECK(hipMemcpyAsync(dst->state, src->state, sizeof(cplx) << dst->n,
                                hipMemcpyDeviceToDevice, dst->stream));
@@ -957,69 +995,71 @@ int aqc_sv_apply(aqc_sv_t h, const aqc_op_t* ops, int nops) {
     }
   }
   const int K = h->K;
-  // Planned and launched in batches of 2, 4, 8, ... segments: the host plans the next batch while
-  // the GPU runs the previous one (planned whole, the GPU waited out the ~150 us of host fusion of
-  // a 20-qubit evaluation).  One pinned staging buffer [headers | phases | gates] with capacity
-  // offsets (phases and fused gates are each at most nops); each batch copies only its own new
-  // headers, phases and gates (up to three ranges), so plan traffic is one plan size in total.  The
-  // previous call's copies have finished reading the staging buffer once plan_ev has completed.
-  const std::vector<HostSeg> segs = sv_plan_segments(h->n, K, h->reg_tiles, ops, nops);
-  const size_t nseg = segs.size();
-  std::vector<SegHeader> hdr(nseg);
+  // Planned and launched in batches of 1, 2, 4, ... segments, each segment formed as it is needed
+  // (SegBuilder): the host plans the next batch while the GPU runs the previous one, and the first
+  // pass starts after one segment's planning (planned whole, the GPU waited out the ~150 us of host
+  // segmentation and fusion of a 20-qubit evaluation).  One pinned staging buffer; each batch
+  // appends its [headers | phases | gates] contiguously (offsets relative to the batch) and goes
+  // over in ONE copy -- a small H2D copy is a ~4 us blit on the stream, three per batch had cost
+  // ~40 us per evaluation.  The previous call's copies have finished reading the staging buffer
+  // once plan_ev has completed.
+  auto al = [](size_t x) { return (x + 255) / 256 * 256; };
+  constexpr size_t kMaxBatches = 40;  // batch sizes double: 2^40 segments
+  const size_t cap = sizeof(SegHeader) * (size_t)nops + sizeof(PhaseHdr) * (size_t)nops +
+                     sizeof(SegGate) * (size_t)nops + 3 * 256 * kMaxBatches;
+  if (cap > h->plan_cap) {
+    AQC_HIP_CHECK(hipStreamSynchronize(h->stream));
+    if (h->d_plan) AQC_HIP_CHECK(hipFree(h->d_plan));
+    if (h->h_plan) AQC_HIP_CHECK(hipHostFree(h->h_plan));
+    h->d_plan = nullptr, h->h_plan = nullptr;
+    h->plan_cap = std::max(cap, 2 * h->plan_cap);
+    AQC_HIP_CHECK(hipMalloc(&h->d_plan, h->plan_cap));
+    AQC_HIP_CHECK(hipHostMalloc(&h->h_plan, h->plan_cap, hipHostMallocDefault));
+  }
+  AQC_HIP_CHECK(hipEventSynchronize(h->plan_ev));
+  const int nblocks = (int)(1ull << (h->n - K));
+  SegBuilder sb(ops, nops, K, h->n, sv_reserved_bits(h->reg_tiles));
+  std::vector<HostSeg> segs;
+  std::vector<SegHeader> hdr;
   std::vector<SegGate> gts;
   std::vector<PhaseHdr> phs;
   std::vector<double> flops;
   gts.reserve(nops);
   phs.reserve(nops);
-  auto al = [](size_t b) { return (b + 255) / 256 * 256; };
-  const size_t o_ph = al(sizeof(SegHeader) * nseg);
-  const size_t o_g = o_ph + al(sizeof(PhaseHdr) * (size_t)nops);
-  const size_t bytes = o_g + sizeof(SegGate) * (size_t)nops;
-  if (bytes > h->plan_cap) {
-    AQC_HIP_CHECK(hipStreamSynchronize(h->stream));
-    if (h->d_plan) AQC_HIP_CHECK(hipFree(h->d_plan));
-    if (h->h_plan) AQC_HIP_CHECK(hipHostFree(h->h_plan));
-    h->d_plan = nullptr, h->h_plan = nullptr;
-    h->plan_cap = std::max(bytes, 2 * h->plan_cap);
-    AQC_HIP_CHECK(hipMalloc(&h->d_plan, h->plan_cap));
-    AQC_HIP_CHECK(hipHostMalloc(&h->h_plan, h->plan_cap, hipHostMallocDefault));
-  }
-  AQC_HIP_CHECK(hipEventSynchronize(h->plan_ev));
-  const SegHeader* dh = reinterpret_cast<const SegHeader*>(h->d_plan);
-  const PhaseHdr* dp = reinterpret_cast<const PhaseHdr*>(h->d_plan + o_ph);
-  const SegGate* dg = reinterpret_cast<const SegGate*>(h->d_plan + o_g);
-  const int nblocks = (int)(1ull << (h->n - K));
-  size_t ph_done = 0, g_done = 0;
+  size_t off = 0;
   int rc = AQC_OK;
-  for (size_t s0 = 0, batch = 2; s0 < nseg && rc == AQC_OK; batch *= 2) {
-    const size_t s1 = std::min(nseg, s0 + batch);
-    for (size_t s = s0; s < s1; ++s) sv_plan_one(h->n, K, h->reg_tiles, ops, segs[s], s, hdr, gts, phs, &flops);
-    if (phs.size() > (size_t)nops || gts.size() > (size_t)nops) {
+  for (size_t batch = 1, nb_done = 0; rc == AQC_OK; batch *= 2, ++nb_done) {
+    segs.clear();
+    HostSeg seg;
+    while (segs.size() < batch && sb.next(seg)) segs.push_back(seg);
+    if (segs.empty()) break;
+    const size_t nb = segs.size();
+    hdr.assign(nb, SegHeader{});
+    gts.clear();
+    phs.clear();
+    flops.clear();
+    for (size_t s = 0; s < nb; ++s) sv_plan_one(h->n, K, h->reg_tiles, ops, segs[s], s, hdr, gts, phs, &flops);
+    const size_t o_h = off, o_p = al(o_h + sizeof(SegHeader) * nb), o_g = al(o_p + sizeof(PhaseHdr) * phs.size());
+    const size_t end = o_g + sizeof(SegGate) * gts.size();
+    if (end > h->plan_cap || nb_done >= kMaxBatches) {
       aqc::set_error("aqc_sv_apply: plan exceeds its staging bound");
       rc = AQC_ERR_STATE;
       break;
     }
-    // this batch's new bytes only: headers [s0, s1), phases [ph_done, ..), gates [g_done, ..)
-    const size_t rng[3][2] = {{sizeof(SegHeader) * s0, sizeof(SegHeader) * s1},
-                              {o_ph + sizeof(PhaseHdr) * ph_done, o_ph + sizeof(PhaseHdr) * phs.size()},
-                              {o_g + sizeof(SegGate) * g_done, o_g + sizeof(SegGate) * gts.size()}};
-    std::memcpy(h->h_plan + rng[0][0], hdr.data() + s0, rng[0][1] - rng[0][0]);
-    if (rng[1][1] > rng[1][0]) std::memcpy(h->h_plan + rng[1][0], phs.data() + ph_done, rng[1][1] - rng[1][0]);
-    if (rng[2][1] > rng[2][0]) std::memcpy(h->h_plan + rng[2][0], gts.data() + g_done, rng[2][1] - rng[2][0]);
-    ph_done = phs.size();
-    g_done = gts.size();
-    for (int r = 0; r < 3 && rc == AQC_OK; ++r) {
-      if (rng[r][1] <= rng[r][0]) continue;
-      hipError_t e = hipMemcpyAsync(h->d_plan + rng[r][0], h->h_plan + rng[r][0], rng[r][1] - rng[r][0],
-                                    hipMemcpyHostToDevice, h->stream);
-      if (e != hipSuccess) {
-        aqc::set_error(std::string("aqc_sv_apply: plan copy: ") + hipGetErrorString(e));
-        rc = AQC_ERR_HIP;
-      }
+    std::memcpy(h->h_plan + o_h, hdr.data(), sizeof(SegHeader) * nb);
+    if (!phs.empty()) std::memcpy(h->h_plan + o_p, phs.data(), sizeof(PhaseHdr) * phs.size());
+    if (!gts.empty()) std::memcpy(h->h_plan + o_g, gts.data(), sizeof(SegGate) * gts.size());
+    hipError_t e = hipMemcpyAsync(h->d_plan + o_h, h->h_plan + o_h, end - o_h, hipMemcpyHostToDevice, h->stream);
+    if (e != hipSuccess) {
+      aqc::set_error(std::string("aqc_sv_apply: plan copy: ") + hipGetErrorString(e));
+      rc = AQC_ERR_HIP;
+      break;
     }
-    if (rc != AQC_OK) break;
-    for (size_t s = s0; s < s1 && rc == AQC_OK; ++s) rc = sv_launch_segment(h, dh + s, dp, dg, nblocks, flops[s]);
-    s0 = s1;
+    const SegHeader* dh = reinterpret_cast<const SegHeader*>(h->d_plan + o_h);
+    const PhaseHdr* dp = reinterpret_cast<const PhaseHdr*>(h->d_plan + o_p);
+    const SegGate* dg = reinterpret_cast<const SegGate*>(h->d_plan + o_g);
+    for (size_t s = 0; s < nb && rc == AQC_OK; ++s) rc = sv_launch_segment(h, dh + s, dp, dg, nblocks, flops[s]);
+    off = al(end);
   }
   // (recorded on every path, so the next call never reuses the staging buffer under a live copy)
   AQC_HIP_CHECK(hipEventRecord(h->plan_ev, h->stream));
@@ -1047,6 +1087,7 @@ int aqc_sv_plan(int n, const aqc_op_t* ops, int nops, int* out) {
 
 int aqc_sv_amp0(aqc_sv_t h, double* re, double* im) {
   AQC_REQUIRE(h && re && im, "aqc_sv_amp0: null argument");
+  if (int rc = sv_materialize(h)) return rc;
   AQC_HIP_CHECK(hipMemcpyAsync(h->h_pinned, h->state, sizeof(cplx), hipMemcpyDeviceToHost, h->stream));
   AQC_HIP_CHECK(hipStreamSynchronize(h->stream));
   *re = h->h_pinned[0].x;
@@ -1056,6 +1097,7 @@ int aqc_sv_amp0(aqc_sv_t h, double* re, double* im) {
 
 int aqc_sv_z_all(aqc_sv_t h, double* out) {
   AQC_REQUIRE(h && out, "aqc_sv_z_all: null argument");
+  if (int rc = sv_materialize(h)) return rc;
   aqc::KernelTimer::begin(h->stream, "sv_zall", 16.0 * (double)(1ull << h->n), 0.0);
   hipLaunchKernelGGL(k_sv_zpartial, dim3(h->zwg), dim3(kThreads), 0, h->stream, h->state, h->n,
                      h->d_zpart);
@@ -1076,6 +1118,7 @@ int aqc_sv_pair_rdms(aqc_sv_t h, const int* pairs, int npairs, double* out) {
     AQC_REQUIRE(a >= 0 && a < h->n && b >= 0 && b < h->n && a != b, "aqc_sv_pair_rdms: bad pair");
   }
   if (npairs == 0) return AQC_OK;
+  if (int rc = sv_materialize(h)) return rc;
   const size_t rest = size_t(1) << (h->n - 2);
   // about 2048 workgroups in total, at least 4 rest indices per thread
   const size_t per_pair = std::max<size_t>(1, std::min<size_t>(rest / (4 * kThreads), (2048 + npairs - 1) / npairs));
@@ -1106,6 +1149,8 @@ int aqc_sv_transition(aqc_sv_t bra, aqc_sv_t ket, int q, double* out) {
   AQC_REQUIRE(bra && ket && out, "aqc_sv_transition: null argument");
   AQC_REQUIRE(bra->n == ket->n && q >= 0 && q < bra->n, "aqc_sv_transition: bad qubit or size mismatch");
   const int n = bra->n;
+  if (int rc = sv_materialize(bra)) return rc;
+  if (int rc = sv_materialize(ket)) return rc;
   // ket and bra live on their own streams: order the reads after both states' pending work
   AQC_HIP_CHECK(hipStreamSynchronize(bra->stream));
   const size_t half = size_t(1) << (n - 1);
@@ -1126,6 +1171,7 @@ int aqc_sv_transition(aqc_sv_t bra, aqc_sv_t ket, int q, double* out) {
 
 int aqc_sv_get(aqc_sv_t h, double* out) {
   AQC_REQUIRE(h && out, "aqc_sv_get: null argument");
+  if (int rc = sv_materialize(h)) return rc;
   AQC_HIP_CHECK(hipMemcpyAsync(out, h->state, sizeof(cplx) << h->n, hipMemcpyDeviceToHost, h->stream));
   AQC_HIP_CHECK(hipStreamSynchronize(h->stream));
   return AQC_OK;
@@ -1133,6 +1179,7 @@ int aqc_sv_get(aqc_sv_t h, double* out) {
 
 int aqc_sv_set(aqc_sv_t h, const double* in) {
   AQC_REQUIRE(h && in, "aqc_sv_set: null argument");
+  h->zero_pending = false;  // overwritten
   AQC_HIP_CHECK(hipMemcpyAsync(h->state, in, sizeof(cplx) << h->n, hipMemcpyHostToDevice, h->stream));
   AQC_HIP_CHECK(hipStreamSynchronize(h->stream));
   return AQC_OK;

@@ -165,8 +165,13 @@ int aqc_gb_set_spin_limit(double us);
 int aqc_debug_hog(int nblocks, double ms);
 /* Batched applies of >= 32 states at 2*chi = 128 run every state's whole op list in
    one fused workgroup (theta, Jacobi, truncation, split per update: no grid-wide step between
-   updates); on = 0 selects the lock-step launches per update.  Default on. */
+   updates); on = 0 selects the lock-step launches per update, on = 2 the fused chain for batches
+   of any size (lab: single evaluations).  Default 1. */
 int aqc_mps_set_fused_chain(int on);
+/* The fused chain's workgroup: 1024 threads, one state per CU (k_chain, default), or 256 threads,
+   two states per CU (k_chain256: lower-triangle Gram SVD; a state whose Gram path declines finishes
+   its list on k_chain).  Also AQC_CHAIN=256 at load.  Other values: AQC_ERR_ARG. */
+int aqc_mps_set_chain_threads(int threads);
 /* Diagnostics: shader-clock ticks spent by the fused chain's workgroups (thread 0) in theta,
    Jacobi, rank, split and one-site ops since the last call (then reset); out[5]. */
 int aqc_mps_chain_ticks(double* out);

@@ -221,3 +221,65 @@ def test_config2_exact_workload_vs_oracle_goldens():
             psi = d.get()
             np.testing.assert_allclose(R.conj() @ psi, gold["proj"][k], atol=1e-10)
             k += 1
+
+
+def test_deferred_reset_every_reader():
+    """aqc_sv_reset on the register-tile path (n >= 14) launches nothing: the next apply's first
+    pass forms |0...0> in its tiles, and every other reader (amp0, get, z_all, pair RDMs, transition,
+    copy in either direction, set) sees |0...0> or overwrites it.  Each case follows an apply that
+    left a non-trivial state behind, so a reader that skipped the reset would see that state."""
+    from adaptaqc_amd.circuit import device_ops
+    from adaptaqc_amd.device import DeviceSV
+
+    n = 14
+    ops = brickwork(n, 4, 5)
+    psi = osv.simulate(n, ops)
+    dev_ops = device_ops(to_circuit(n, ops))
+    e0 = np.zeros(2 ** n, complex)
+    e0[0] = 1.0
+
+    def dirty():
+        d = DeviceSV(n)
+        d.apply(dev_ops)
+        d.reset()
+        return d
+
+    d = dirty()
+    assert abs(d.amp0() - 1.0) < 1e-15
+    np.testing.assert_array_equal(dirty().get(), e0)
+    np.testing.assert_allclose(dirty().z_all(), np.ones(n), atol=1e-15)
+    rd = dirty().pair_rdms([(0, 1)])
+    want = np.zeros((4, 4), complex)
+    want[0, 0] = 1.0
+    np.testing.assert_allclose(np.asarray(rd).reshape(4, 4), want, atol=1e-15)
+    # apply after reset: the first pass starts from |0...0>, twice in a row
+    d = dirty()
+    d.apply(dev_ops)
+    np.testing.assert_allclose(d.get(), psi, atol=1e-12)
+    d.reset()
+    d.apply(dev_ops)
+    np.testing.assert_allclose(d.get(), psi, atol=1e-12)
+    # copy from a pending source; copy onto a pending destination
+    src, dst = dirty(), DeviceSV(n)
+    dst.apply(dev_ops)
+    dst.copy_from(src)
+    np.testing.assert_array_equal(dst.get(), e0)
+    src = DeviceSV(n)
+    src.apply(dev_ops)
+    dst = dirty()
+    dst.copy_from(src)
+    np.testing.assert_allclose(dst.get(), psi, atol=1e-12)
+    # set on a pending state overwrites it
+    d = dirty()
+    d.set(psi)
+    np.testing.assert_allclose(d.get(), psi, atol=0)
+    # transition <0|(|a><b|)_q|psi> with a pending bra: row a = 0 only
+    bra, ket = dirty(), DeviceSV(n)
+    ket.apply(dev_ops)
+    t = bra.transition(ket, 3)
+    np.testing.assert_allclose(t, [[psi[0], psi[1 << 3]], [0, 0]], atol=1e-15)
+    # and a pending ket: <psi|(|a><b|)_q|0> = conj(psi[a << q]) for b = 0
+    bra, ket = DeviceSV(n), dirty()
+    bra.apply(dev_ops)
+    t = bra.transition(ket, 3)
+    np.testing.assert_allclose(t, [[np.conj(psi[0]), 0], [np.conj(psi[1 << 3]), 0]], atol=1e-15)
