@@ -32,17 +32,42 @@ from ..utils.utilityfunctions import is_statevector_backend
 logger = logging.getLogger(__name__)
 
 
+def _without_resets(circuit):
+    """The initial-state circuit without reset, barrier and delay instructions -- what the
+    reference inverts (approximate_compiler.py:481-483: unroll, ``co.remove_reset_gates``,
+    ``inverse()``).  Forward, Aer runs the resets from |0..0>, where a reset before any gate on its
+    qubit does nothing; a reset after a gate is a non-unitary mid-circuit operation, which the
+    pure-state backends here do not run, and raises."""
+    from ..circuit import CircuitInstruction, qubit_indices
+
+    out = QuantumCircuit(circuit.num_qubits)
+    touched = set()
+    for ins in circuit.data:
+        name = ins.operation.name
+        qs = qubit_indices(circuit, ins)
+        if name in ("barrier", "delay"):
+            continue
+        if name == "reset":
+            if any(q in touched for q in qs):
+                raise NotImplementedError("initial_state: a reset after a gate on its qubit (mid-circuit reset) "
+                                          "is not supported by the pure-state backends")
+            continue
+        touched.update(qs)
+        out.data.append(CircuitInstruction(ins.operation.copy(), list(qs)))
+    return out
+
+
 def initial_state_to_circuit(initial_state):
     """circuit_operations_full_circuit.py:385-410 for circuits; a state vector needs qiskit's
     state-preparation synthesis (``initialize`` unrolled), which is not part of this build."""
     if initial_state is None:
         return None
     if isinstance(initial_state, QuantumCircuit):
-        return initial_state.copy()
+        return _without_resets(initial_state)
     if hasattr(initial_state, "num_qubits") and hasattr(initial_state, "data"):  # qiskit-like circuit
         qc = QuantumCircuit(initial_state.num_qubits)
         co.add_to_circuit(qc, initial_state)
-        return qc
+        return _without_resets(qc)
     if isinstance(initial_state, (list, tuple)) or hasattr(initial_state, "shape"):
         raise NotImplementedError("a state-vector initial_state needs qiskit's state preparation; pass a circuit")
     raise TypeError("Invalid type of initial_state provided")

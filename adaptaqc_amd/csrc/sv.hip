@@ -225,6 +225,12 @@ __device__ __forceinline__ void reg_apply(cplx (&a)[16], const SegGate& g) {
   }
 }
 
+// Phase flags in PhaseHdr::slotmask above the tile bits: the segment's first phase reads its
+// registers straight from global memory, its last phase writes them straight back (no LDS round
+// trip, no barrier).  The host sets them when the phase's lane map can put thread bits 0-3 on tile
+// bits 0-3 (no low slot bit): a wave then reads / writes 16 runs of 256 contiguous bytes.
+constexpr int kPhaseDirectIn = 1 << 30, kPhaseDirectOut = 1 << 29, kPhaseSlotBits = (1 << kRegTileBits) - 1;
+
 __global__ __launch_bounds__(kThreads) void k_sv_tile_reg(cplx* __restrict__ state, const SegHeader* __restrict__ hdr,
                                                          const PhaseHdr* __restrict__ phases,
                                                          const SegGate* __restrict__ gates, int from_zero) {
@@ -245,11 +251,22 @@ __global__ __launch_bounds__(kThreads) void k_sv_tile_reg(cplx* __restrict__ sta
     return g;
   };
   constexpr int kPer = (1 << K) / kThreads;
-  {
-    cplx v[kPer];
-    if (from_zero) {  // a deferred aqc_sv_reset: the tile of |0...0> (index 0 in tile 0)
+  if (from_zero && blockIdx.x != 0) {
+    // a deferred aqc_sv_reset: every tile but tile 0 (which holds index 0) is zero in and out --
+    // the segment's gates act inside the tile -- so it is written without loads or gates
 #pragma unroll
-      for (int r = 0; r < kPer; ++r) v[r] = aqc::cmk(blockIdx.x == 0 && tid + r * kThreads == 0 ? 1.0 : 0.0, 0.0);
+    for (int r = 0; r < kPer; ++r) aqc::stg(state + gidx(tid + r * kThreads), aqc::cmk(0.0, 0.0));
+    return;
+  }
+  const int np = hdr->ngates;
+  const PhaseHdr* ph = phases + hdr->gate_off;
+  const bool d_in = np > 0 && (ph[0].slotmask & kPhaseDirectIn);
+  const bool d_out = np > 0 && (ph[np - 1].slotmask & kPhaseDirectOut);
+  if (!d_in) {
+    cplx v[kPer];
+    if (from_zero) {
+#pragma unroll
+      for (int r = 0; r < kPer; ++r) v[r] = aqc::cmk(tid + r * kThreads == 0 ? 1.0 : 0.0, 0.0);
     } else {
 #pragma unroll
       for (int r = 0; r < kPer; ++r) v[r] = aqc::ldg(state + gidx(tid + r * kThreads));
@@ -257,8 +274,6 @@ __global__ __launch_bounds__(kThreads) void k_sv_tile_reg(cplx* __restrict__ sta
 #pragma unroll
     for (int r = 0; r < kPer; ++r) tile[swz(tid + r * kThreads)] = v[r];
   }
-  const int np = hdr->ngates;
-  const PhaseHdr* ph = phases + hdr->gate_off;
   constexpr int kWords = (int)(sizeof(SegGate) / sizeof(double2));
   auto stage = [&](int p) {
     const int ng = ph[p].ngates;
@@ -270,36 +285,70 @@ __global__ __launch_bounds__(kThreads) void k_sv_tile_reg(cplx* __restrict__ sta
   __syncthreads();
   for (int p = 0; p < np; ++p) {
     if (p + 1 < np) stage(p + 1);  // the other buffer: its last readers passed the barrier below
-    const int sm = __builtin_amdgcn_readfirstlane(ph[p].slotmask);
+    const int sm = __builtin_amdgcn_readfirstlane(ph[p].slotmask) & kPhaseSlotBits;
     const unsigned lm = __builtin_amdgcn_readfirstlane(ph[p].lanemap);
     // thread bits placed on the non-slot tile bits by the lane map, slot bits from r; the swizzle
-    // is linear, so the address is swz(thread part) ^ swz(slot part)
-    int lb = 0;
+    // is linear, so the LDS address is swz(thread part) ^ swz(slot part), and the global index
+    // is the OR of the two parts' scattered bits
+    int lraw = 0;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) lb |= ((tid >> j) & 1) << ((lm >> (4 * j)) & 15);
-    lb = swz(lb);
-    int sb[kRegBits], c = 0;
+    for (int j = 0; j < 8; ++j) lraw |= ((tid >> j) & 1) << ((lm >> (4 * j)) & 15);
+    // the kRegBits slot bits, lowest first (the host pads every phase to exactly kRegBits), and
+    // their global bits (no per-lane indexing: the arrays stay in registers)
+    int sraw[kRegBits];
+    uint64_t sg[kRegBits];
+    {
+      int m = sm;
 #pragma unroll
-    for (int j = 0; j < K; ++j)
-      if ((sm >> j) & 1) {
-        if (c < kRegBits) sb[c] = swz(1 << j);
-        ++c;
+      for (int i = 0; i < kRegBits; ++i) {
+        sraw[i] = m & -m;
+        m ^= sraw[i];
+        sg[i] = gidx(sraw[i]) ^ base;
       }
+    }
+    const bool in_g = p == 0 && d_in, out_g = p == np - 1 && d_out;
+    const int lb = swz(lraw);
     int off[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r)
-      off[r] = lb ^ ((r & 1) ? sb[0] : 0) ^ ((r & 2) ? sb[1] : 0) ^ ((r & 4) ? sb[2] : 0) ^ ((r & 8) ? sb[3] : 0);
+      off[r] = lb ^ ((r & 1) ? swz(sraw[0]) : 0) ^ ((r & 2) ? swz(sraw[1]) : 0) ^ ((r & 4) ? swz(sraw[2]) : 0) ^
+               ((r & 8) ? swz(sraw[3]) : 0);
+    auto gaddr = [&](int r) {
+      return state + (gidx(lraw) | ((r & 1) ? sg[0] : 0) | ((r & 2) ? sg[1] : 0) | ((r & 4) ? sg[2] : 0) |
+                      ((r & 8) ? sg[3] : 0));
+    };
     cplx a[16];
+    if (in_g) {
+      if (from_zero) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) a[r] = tile[off[r]];
+        for (int r = 0; r < 16; ++r) {
+          const int x = lraw | ((r & 1) ? sraw[0] : 0) | ((r & 2) ? sraw[1] : 0) | ((r & 4) ? sraw[2] : 0) |
+                        ((r & 8) ? sraw[3] : 0);
+          a[r] = aqc::cmk(x == 0 ? 1.0 : 0.0, 0.0);
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) a[r] = aqc::ldg(gaddr(r));
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) a[r] = tile[off[r]];
+    }
     const int ng = ph[p].ngates;
     for (int gi = 0; gi < ng; ++gi) reg_apply(a, gl[p & 1][gi]);
+    if (out_g) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) tile[off[r]] = a[r];
-    __syncthreads();
+      for (int r = 0; r < 16; ++r) aqc::stg(gaddr(r), a[r]);
+    } else {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) tile[off[r]] = a[r];
+      __syncthreads();
+    }
   }
+  if (!d_out) {
 #pragma unroll
-  for (int r = 0; r < kPer; ++r) aqc::stg(state + gidx(tid + r * kThreads), tile[swz(tid + r * kThreads)]);
+    for (int r = 0; r < kPer; ++r) aqc::stg(state + gidx(tid + r * kThreads), tile[swz(tid + r * kThreads)]);
+  }
 }
 
 // Per-workgroup partial probabilities: out[wg * (n+1) + i] = sum |a|^2 over amplitudes of this
@@ -610,6 +659,32 @@ uint32_t lane_map(uint32_t S) {
   return m;
 }
 
+// The segment's first / last phase: non-slot tile bits in ascending order over the thread bits,
+// flagged for direct global reads / writes (k_sv_tile_reg) when no slot is a low tile bit
+uint32_t lane_map_coalesced(uint32_t S) {
+  uint32_t m = 0;
+  int j = 0;
+  for (int b = 0; b < kRegTileBits && j < 8; ++b)
+    if (!((S >> b) & 1u)) m |= (uint32_t)b << (4 * j++);
+  return m;
+}
+
+void mark_direct_phases(PhaseHdr* first, PhaseHdr* last) {
+  static const char* dbg = std::getenv("AQC_SV_DIRECT");  // "0": LDS round trips only (A/B)
+  if (dbg && std::strcmp(dbg, "0") == 0) return;
+  if ((first->slotmask & 15) == 0) {
+    first->lanemap = lane_map_coalesced((uint32_t)first->slotmask);
+    first->slotmask |= kPhaseDirectIn;
+  }
+  if (((last->slotmask & kPhaseSlotBits) & 15) == 0) {
+    if (last != first) last->lanemap = lane_map_coalesced((uint32_t)(last->slotmask & kPhaseSlotBits));
+    last->slotmask |= kPhaseDirectOut;
+  }
+  // one phase both reading and writing global memory needs one lane map for both
+  if (first == last && (first->slotmask & kPhaseDirectIn) == 0 && (first->slotmask & kPhaseDirectOut))
+    first->lanemap = lane_map_coalesced((uint32_t)(first->slotmask & kPhaseSlotBits));
+}
+
 void build_phases(const std::vector<SegGate>& fused, int K, std::vector<PhaseHdr>& ph, std::vector<SegGate>& out) {
   std::vector<char> done(fused.size(), 0);
   size_t remaining = fused.size(), first = 0;
@@ -854,6 +929,7 @@ static void sv_plan_one(int n, int K, bool reg_tiles, const aqc_op_t* ops, const
     const size_t before = phs.size();
     build_phases(fused, K, phs, gts);
     hdr[s].ngates = (int)(phs.size() - before);
+    if (phs.size() > before) mark_direct_phases(&phs[before], &phs.back());
     // timing experiments only (results wrong): AQC_SV_DEBUG=nogates / nophases
     static const char* dbg = std::getenv("AQC_SV_DEBUG");
     if (dbg && std::strcmp(dbg, "nophases") == 0) hdr[s].ngates = 0;

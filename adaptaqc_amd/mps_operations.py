@@ -241,7 +241,40 @@ class DevicePreprocessedMPS(list):
         return self._device.pair_rdms(pairs)
 
 
-_pt_cache = {"obj": None, "dev": None, "rdms": None}
+def _filling(name):
+    """list method ``name`` run on the filled storage (C-level list methods read the internal
+    array directly, which is empty until the first fill)."""
+    base = getattr(list, name)
+
+    def method(self, *args, **kwargs):
+        self._fill()
+        return base(self, *args, **kwargs)
+
+    method.__name__ = name
+    method.__doc__ = base.__doc__
+    return method
+
+
+for _name in ("copy", "__eq__", "__ne__", "__lt__", "__le__", "__gt__", "__ge__", "__reversed__", "__add__",
+              "__mul__", "__rmul__", "__contains__", "index", "count", "__repr__", "append", "extend", "insert",
+              "pop", "remove", "sort", "reverse", "__setitem__", "__delitem__", "__iadd__", "__imul__", "clear"):
+    setattr(DevicePreprocessedMPS, _name, _filling(_name))
+del _name
+
+
+def _dpm_radd(self, other):  # [..] + mps: Python tries a subclass's reflected method first
+    self._fill()
+    return list(other) + list(super(DevicePreprocessedMPS, self).__iter__())
+
+
+DevicePreprocessedMPS.__radd__ = _dpm_radd
+
+# partial_trace on a host list: every pair's RDM from one device sweep, kept for the following
+# calls on the same list (the reference's ISL loop calls it once per pair).  Keyed on the list and
+# the identities of its site tensors (a site replaced in place starts a new sweep; tensors mutated
+# in place are not detected); the device copy of the state is released as soon as the RDMs are
+# read back.
+_pt_cache = {"obj": None, "sites": None, "rdms": None}
 
 
 def partial_trace(mps, qubits, already_preprocessed=False):
@@ -257,13 +290,29 @@ def partial_trace(mps, qubits, already_preprocessed=False):
     key = (min(q), max(q))
     if isinstance(mps, DevicePreprocessedMPS):
         return mps.all_pair_rdms()[key].copy()
-    if _pt_cache["obj"] is not mps:
+    sites = _site_objects(mps)
+    old = _pt_cache["sites"]
+    if (_pt_cache["obj"] is not mps or sites is None or old is None or len(old) != len(sites)
+            or any(a is not b for a, b in zip(old, sites))):
         dev = _as_device(mps, already_preprocessed)
         n = dev.n
         pairs = [(a, b) for a in range(n) for b in range(a + 1, n)]
         r = dev.pair_rdms(pairs)
-        _pt_cache.update(obj=mps, dev=dev, rdms={p: r[k] for k, p in enumerate(pairs)})
+        del dev
+        _pt_cache.update(obj=mps, sites=sites, rdms={p: r[k] for k, p in enumerate(pairs)})
     return _pt_cache["rdms"][key].copy()
+
+
+def _site_objects(mps):
+    """The objects a host MPS holds (a preprocessed list of site tensors, or Aer's (gammas,
+    lambdas) pair), held by the cache and compared by identity: replacing any of them invalidates
+    the partial-trace cache."""
+    try:
+        if isinstance(mps, tuple) and len(mps) == 2:
+            return tuple(x for part in mps for x in part)
+        return tuple(mps)
+    except TypeError:
+        return None
 
 
 def mps_to_vector(mps, already_preprocessed=False):

@@ -501,9 +501,19 @@ def main():
         latency = latency_block(distinct[0], cpu)
 
     if rank == 0 and sim:
+        # the collective the projection leaves out: state sharding all-gathers one (best pair, score)
+        # per state (16 B x S), pair sharding the whole score matrix (8 B x S x 1225); bounded by
+        # RCCL's small-message latency over xGMI (COLLECTIVE_US_EST) plus the bytes at one link's
+        # ~100 GB/s effective (unmeasured: the driver's SCALE run is the first multi-GPU measurement)
+        ag_bytes = 16.0 * S if by_state else 8.0 * S * len(cmap)
+        ag_ms = 1e-3 * COLLECTIVE_US_EST + ag_bytes / 100e9 * 1e3
         print(json.dumps({"projection": f"rank 0 of a {sim}-GPU run on one GPU (no collective)",
-                          "ms_per_step": ms_step, "per_gpu_evals_per_s": evals_per_step / sim * args.steps / elapsed,
+                          "shard": args.shard, "ms_per_step": ms_step,
+                          "per_gpu_evals_per_s": evals_per_step / sim * args.steps / elapsed,
                           "projected_value": evals_per_step * args.steps / elapsed,
+                          "all_gather_bytes": ag_bytes, "all_gather_ms_bound": ag_ms,
+                          "ms_per_step_with_all_gather": ms_step + ag_ms,
+                          "projected_value_with_all_gather": evals_per_step / (1e-3 * (ms_step + ag_ms)),
                           "breakdown_ms": {f: round(v["ms"] / args.steps, 3) for f, v in fams.items()}}))
     elif rank == 0:
         cpu_line = None

@@ -237,3 +237,86 @@ def test_ops_batch_marshalling():
         assert b.ptrs[k] == arrs[k].ctypes.data
     assert b.ptrs[5] in (None, 0)
     assert isinstance(b.ptrs, ctypes.Array)
+
+
+def test_device_preprocessed_mps_list_protocol():
+    """DevicePreprocessedMPS fills lazily; every list operation -- the C-level ones
+    included (copy, ==, reversed, +, count / index, in-place edits) -- sees the filled contents."""
+    from adaptaqc_amd.mps_operations import DevicePreprocessedMPS
+
+    host = [10, 11, 12, 13]  # (stand-ins for the site tensors: the list protocol is what is tested)
+
+    class FakeDevice:
+        n = 4
+
+        def preprocessed(self):
+            return list(host)
+
+    def fresh():
+        return DevicePreprocessedMPS(FakeDevice())
+
+    assert len(fresh()) == 4
+    assert fresh().copy() == host
+    assert fresh() == host and not (fresh() != host)
+    assert list(reversed(fresh())) == host[::-1]
+    assert fresh() + [1] == host + [1]
+    assert [1] + fresh() == [1] + host
+    assert fresh() * 2 == host * 2
+    assert fresh().count(12) == 1 and fresh().index(13) == 3
+    assert 11 in fresh() and 99 not in fresh()
+    d = fresh()
+    d.append(7)
+    assert len(list(d)) == 5 and d[4] == 7
+    d = fresh()
+    d[0] = None
+    assert d[0] is None and d[1] == 11
+    assert repr(fresh()) == repr(host)
+
+
+def test_partial_trace_cache_invalidates_on_site_replacement(monkeypatch):
+    """partial_trace's cache is keyed on the host list and its site objects; replacing
+    a site recomputes, and the device copy is not retained."""
+    from adaptaqc_amd import mps_operations as mo
+
+    calls = []
+
+    class FakeDev:
+        n = 3
+
+        def pair_rdms(self, pairs):
+            calls.append(len(pairs))
+            return np.stack([np.eye(4, dtype=complex) * len(calls)] * len(pairs))
+
+    monkeypatch.setattr(mo, "_as_device", lambda mps, pre: FakeDev())
+    monkeypatch.setattr(mo, "_pt_cache", {"obj": None, "sites": None, "rdms": None})
+    mps = [np.zeros((2, 1, 1), complex) for _ in range(3)]
+    r1 = mo.partial_trace(mps, [0, 2], True)
+    r2 = mo.partial_trace(mps, [1, 0], True)
+    assert len(calls) == 1 and r1[0, 0] == 1 and r2[0, 0] == 1
+    mps[1] = np.zeros((2, 1, 1), complex)
+    r3 = mo.partial_trace(mps, [0, 1], True)
+    assert len(calls) == 2 and r3[0, 0] == 2
+    assert "dev" not in mo._pt_cache
+
+
+def test_initial_state_resets_stripped():
+    """ADVICE r3 / approximate_compiler.py:481-483: resets (and barriers, delays) leave the
+    initial-state circuit before it is used and inverted; a reset after a gate on its qubit
+    raises (non-unitary mid-circuit operation)."""
+    from adaptaqc_amd.circuit import Operation, QuantumCircuit
+    from adaptaqc_amd.compilers.approximate_compiler import initial_state_to_circuit
+
+    qc = QuantumCircuit(3)
+    qc.append(Operation("reset", 1), [0])
+    qc.h(0)
+    qc.append(Operation("barrier", 3), [0, 1, 2])
+    qc.cx(0, 1)
+    qc.append(Operation("reset", 1), [2])
+    out = initial_state_to_circuit(qc)
+    assert [i.operation.name for i in out.data] == ["h", "cx"]
+    assert [i.operation.name for i in out.inverse().data] == ["cx", "h"]
+    bad = QuantumCircuit(2)
+    bad.h(0)
+    bad.append(Operation("reset", 1), [0])
+    with pytest.raises(NotImplementedError):
+        initial_state_to_circuit(bad)
