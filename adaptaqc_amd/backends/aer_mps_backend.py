@@ -65,6 +65,7 @@ class AerMPSBackend(AQCBackend):
         d = dict(self.__dict__)
         d["_base"] = None
         d["_work"] = None
+        d.pop("_scratch_pools", None)
         return d
 
     def _options(self):
@@ -97,6 +98,19 @@ class AerMPSBackend(AQCBackend):
         base = self._base[1]
         thr, max_chi = self._options()
         return DeviceMPS(base.n, base.chi_cap, thr, max_chi)
+
+    def scratch_states(self, k):
+        """k device MPS shaped like the cached base, kept on the backend across calls (the cached
+        Rotoselect / Rotosolve evaluators' candidate states: scratch, overwritten by every use)."""
+        base = self._base[1]
+        thr, max_chi = self._options()
+        pools = self.__dict__.setdefault("_scratch_pools", {})
+        pool = pools.setdefault((base.n, base.chi_cap), [])
+        while len(pool) < k:
+            pool.append(DeviceMPS(base.n, base.chi_cap, thr, max_chi))
+        for d in pool[:k]:
+            d.set_truncation(thr, max_chi)
+        return pool[:k]
 
     def device_state(self, circuit):
         """Replay ``circuit`` on the device; returns the (sorted) work DeviceMPS."""

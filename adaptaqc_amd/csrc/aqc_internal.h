@@ -151,6 +151,17 @@ __device__ __forceinline__ double group_sum(double v) {
 void on_finalize(void (*fn)());
 void note_device(int dev);
 
+// ---- cached device memory ------------------------------------------------------------------
+// Blocks freed by the library go to a per-device free list keyed by size (4 KB granules) and are
+// handed out again to the next request of that size: handle creation and destruction (a batched
+// Rotoselect gate creates and drops its candidate states) cost a list lookup instead of hipMalloc /
+// hipFree, whose implicit device synchronisation took ~0.25 ms per MPS handle.  The caller frees
+// only memory no queued work still uses (the same rule as hipFree's).  The cache holds at most
+// AQC_POOL_MB (default 8192) MB; an allocation that fails first releases the cache and retries.
+// aqc_finalize returns every cached block to the runtime.
+void* dev_alloc(size_t bytes);
+void dev_free(void* p);
+
 // ---- kernel timing (HIP events on the launching stream) ------------------------------
 struct KernelTimer {
   // Begin/End bracket one launch on `stream` when timing is enabled.

@@ -3,6 +3,7 @@
 #include <signal.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <atomic>
 #include <cstdlib>
 #include <cstring>
@@ -32,6 +33,90 @@ void on_finalize(void (*fn)()) {
 
 void note_device(int dev) {
   if (dev >= 0 && dev < 64) g_devs.fetch_or(1ull << dev);
+}
+
+namespace {
+std::mutex g_pool_mutex;
+struct PoolKey {
+  int dev;
+  size_t bytes;
+  bool operator<(const PoolKey& o) const { return dev != o.dev ? dev < o.dev : bytes < o.bytes; }
+};
+std::map<PoolKey, std::vector<void*>> g_pool_free;  // cached blocks
+std::map<void*, PoolKey> g_pool_live;               // blocks handed out
+size_t g_pool_cached = 0, g_pool_limit = 0;
+
+void pool_release_locked() {
+  int cur = 0;
+  const bool have = hipGetDevice(&cur) == hipSuccess;
+  for (auto& kv : g_pool_free) {
+    if (kv.second.empty()) continue;
+    (void)hipSetDevice(kv.first.dev);
+    for (void* p : kv.second) (void)hipFree(p);
+    kv.second.clear();
+  }
+  if (have) (void)hipSetDevice(cur);
+  g_pool_free.clear();
+  g_pool_cached = 0;
+}
+
+void pool_release() {
+  std::lock_guard<std::mutex> lk(g_pool_mutex);
+  pool_release_locked();
+}
+}  // namespace
+
+void* dev_alloc(size_t bytes) {
+  const size_t b = (std::max<size_t>(bytes, 1) + 4095) & ~(size_t)4095;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lk(g_pool_mutex);
+  if (g_pool_limit == 0) {
+    const char* e = std::getenv("AQC_POOL_MB");
+    g_pool_limit = (size_t)(e ? std::max(0.0, std::atof(e)) : 8192.0) * (1ull << 20) + 1;
+    on_finalize(pool_release);
+  }
+  const PoolKey key{dev, b};
+  void* p = nullptr;
+  auto it = g_pool_free.find(key);
+  if (it != g_pool_free.end() && !it->second.empty()) {
+    p = it->second.back();
+    it->second.pop_back();
+    g_pool_cached -= b;
+  } else if (hipMalloc(&p, b) != hipSuccess) {
+    (void)hipGetLastError();
+    pool_release_locked();
+    (void)hipSetDevice(dev);
+    if (hipMalloc(&p, b) != hipSuccess) {
+      (void)hipGetLastError();
+      return nullptr;
+    }
+  }
+  g_pool_live[p] = key;
+  note_device(dev);
+  return p;
+}
+
+void dev_free(void* p) {
+  if (!p) return;
+  std::lock_guard<std::mutex> lk(g_pool_mutex);
+  auto it = g_pool_live.find(p);
+  if (it == g_pool_live.end()) {  // (not from dev_alloc)
+    (void)hipFree(p);
+    return;
+  }
+  const PoolKey key = it->second;
+  g_pool_live.erase(it);
+  if (g_pool_cached + key.bytes < g_pool_limit) {
+    g_pool_free[key].push_back(p);
+    g_pool_cached += key.bytes;
+  } else {
+    int cur = 0;
+    const bool have = hipGetDevice(&cur) == hipSuccess;
+    (void)hipSetDevice(key.dev);
+    (void)hipFree(p);
+    if (have) (void)hipSetDevice(cur);
+  }
 }
 
 namespace {

@@ -841,8 +841,16 @@ int ensure_gw(aqc_mps_t h) {
   const size_t cap = h->d.cap, n = h->d.n;
   const size_t need = (n * cap * cap + 2 * (n + 1) * cap + 4 * n * cap + n * n * 4) * sizeof(cplx);
   if (h->gw_bytes >= need) return AQC_OK;
-  if (h->gw) hipFree(h->gw);
-  AQC_HIP_CHECK(hipMalloc(&h->gw, need));
+  if (h->gw) {  // (queued sweeps may still read the old block: the pool reuses it at once)
+    AQC_HIP_CHECK(hipStreamSynchronize(aqc::mps_stream()));
+    aqc::dev_free(h->gw);
+  }
+  h->gw = (cplx*)aqc::dev_alloc(need);
+  if (!h->gw) {
+    h->gw_bytes = 0;
+    aqc::set_error("ensure_gw: out of device memory");
+    return AQC_ERR_NOMEM;
+  }
   h->gw_bytes = need;
   return AQC_OK;
 }

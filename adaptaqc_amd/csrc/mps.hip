@@ -1863,10 +1863,15 @@ int ensure_slots(aqc_mps_t h, int nslots) {
   const size_t cap = h->d.cap;
   while ((int)h->slots.size() + 1 < nslots) {
     aqc_mps_s::Slot sl;
-    AQC_HIP_CHECK(hipMalloc(&sl.theta, 4 * cap * cap * sizeof(cplx)));
-    AQC_HIP_CHECK(hipMalloc(&sl.work, 4 * cap * cap * sizeof(cplx)));
-    AQC_HIP_CHECK(hipMalloc(&sl.sig, 2 * kSigMax * sizeof(double)));
-    AQC_HIP_CHECK(hipMalloc(&sl.perm, kSigMax * sizeof(int)));
+    sl.theta = (cplx*)aqc::dev_alloc(4 * cap * cap * sizeof(cplx));
+    sl.work = (cplx*)aqc::dev_alloc(4 * cap * cap * sizeof(cplx));
+    sl.sig = (double*)aqc::dev_alloc(2 * kSigMax * sizeof(double));
+    sl.perm = (int*)aqc::dev_alloc(kSigMax * sizeof(int));
+    if (!sl.theta || !sl.work || !sl.sig || !sl.perm) {
+      aqc::dev_free(sl.theta), aqc::dev_free(sl.work), aqc::dev_free(sl.sig), aqc::dev_free(sl.perm);
+      aqc::set_error("ensure_slots: out of device memory");
+      return AQC_ERR_NOMEM;
+    }
     h->slots.push_back(sl);
   }
   return AQC_OK;
@@ -2294,17 +2299,36 @@ int aqc_mps_create(int n, int chi_cap, double threshold, int max_chi, aqc_mps_t*
   const size_t cap = chi_cap;
   const size_t g = (size_t)n * 2 * cap * cap;
   hipStream_t st = aqc::mps_stream();
-  AQC_HIP_CHECK(hipMalloc(&h->d.gam, g * sizeof(cplx)));
-  AQC_HIP_CHECK(hipMalloc(&h->d.lam, (size_t)(n + 1) * cap * sizeof(double)));
-  AQC_HIP_CHECK(hipMalloc(&h->d.dims, (size_t)(n + 1) * sizeof(int)));
-  AQC_HIP_CHECK(hipMalloc(&h->d.theta, 4 * cap * cap * sizeof(cplx)));
-  AQC_HIP_CHECK(hipMalloc(&h->d.work, 4 * cap * cap * sizeof(cplx)));
-  AQC_HIP_CHECK(hipMalloc(&h->d.sig, 2 * kSigMax * sizeof(double)));
-  AQC_HIP_CHECK(hipMalloc(&h->d.perm, kSigMax * sizeof(int)));
-  AQC_HIP_CHECK(hipMalloc(&h->d.flags, 4 * sizeof(int)));
-  AQC_HIP_CHECK(hipMalloc(&h->d.vec, 2 * (size_t)(n + 1) * cap * sizeof(cplx)));
-  AQC_HIP_CHECK(hipMalloc(&h->d.tmp, 2 * cap * cap * sizeof(cplx)));
-  AQC_HIP_CHECK(hipMalloc(&h->d.scal, (size_t)(2 * n + 8) * sizeof(cplx)));
+  // the fixed buffers carved from one cached device block (256-byte aligned pieces)
+  {
+    const size_t sz[11] = {g * sizeof(cplx), (size_t)(n + 1) * cap * sizeof(double), (size_t)(n + 1) * sizeof(int),
+                           4 * cap * cap * sizeof(cplx), 4 * cap * cap * sizeof(cplx), 2 * kSigMax * sizeof(double),
+                           kSigMax * sizeof(int), 4 * sizeof(int), 2 * (size_t)(n + 1) * cap * sizeof(cplx),
+                           2 * cap * cap * sizeof(cplx), (size_t)(2 * n + 8) * sizeof(cplx)};
+    size_t off[11], total = 0;
+    for (int i = 0; i < 11; ++i) {
+      off[i] = total;
+      total += (sz[i] + 255) & ~(size_t)255;
+    }
+    char* b = (char*)aqc::dev_alloc(total);
+    if (!b) {
+      delete h;
+      aqc::set_error("aqc_mps_create: out of device memory");
+      return AQC_ERR_NOMEM;
+    }
+    h->base = b;
+    h->d.gam = (cplx*)(b + off[0]);
+    h->d.lam = (double*)(b + off[1]);
+    h->d.dims = (int*)(b + off[2]);
+    h->d.theta = (cplx*)(b + off[3]);
+    h->d.work = (cplx*)(b + off[4]);
+    h->d.sig = (double*)(b + off[5]);
+    h->d.perm = (int*)(b + off[6]);
+    h->d.flags = (int*)(b + off[7]);
+    h->d.vec = (cplx*)(b + off[8]);
+    h->d.tmp = (cplx*)(b + off[9]);
+    h->d.scal = (cplx*)(b + off[10]);
+  }
   h->d.env = nullptr;  // allocated lazily for dot / z_all
   AQC_HIP_CHECK(hipMemsetAsync(h->d.gam, 0, g * sizeof(cplx), st));
   AQC_HIP_CHECK(hipMemsetAsync(h->d.lam, 0, (size_t)(n + 1) * cap * sizeof(double), st));
@@ -2319,24 +2343,14 @@ int aqc_mps_create(int n, int chi_cap, double threshold, int max_chi, aqc_mps_t*
 int aqc_mps_destroy(aqc_mps_t h) {
   if (!h) return AQC_OK;
   hipStreamSynchronize(aqc::mps_stream());
-  hipFree(h->d.gam);
-  hipFree(h->d.lam);
-  hipFree(h->d.dims);
-  hipFree(h->d.theta);
-  hipFree(h->d.work);
-  hipFree(h->d.sig);
-  hipFree(h->d.perm);
-  hipFree(h->d.flags);
-  hipFree(h->d.vec);
-  hipFree(h->d.tmp);
-  hipFree(h->d.scal);
-  if (h->d.env) hipFree(h->d.env);
-  if (h->gw) hipFree(h->gw);
+  aqc::dev_free(h->base);
+  aqc::dev_free(h->d.env);
+  aqc::dev_free(h->gw);
   for (auto& sl : h->slots) {
-    hipFree(sl.theta);
-    hipFree(sl.work);
-    hipFree(sl.sig);
-    hipFree(sl.perm);
+    aqc::dev_free(sl.theta);
+    aqc::dev_free(sl.work);
+    aqc::dev_free(sl.sig);
+    aqc::dev_free(sl.perm);
   }
   delete h;
   return AQC_OK;
@@ -2857,7 +2871,11 @@ int aqc_mps_amps_hw1(aqc_mps_t h, double* out) {
 static int ensure_env(aqc_mps_t h) {
   if (h->d.env) return AQC_OK;
   const size_t cap = h->d.cap;
-  AQC_HIP_CHECK(hipMalloc(&h->d.env, 2 * (size_t)(h->d.n + 1) * cap * cap * sizeof(cplx)));
+  h->d.env = (cplx*)aqc::dev_alloc(2 * (size_t)(h->d.n + 1) * cap * cap * sizeof(cplx));
+  if (!h->d.env) {
+    aqc::set_error("aqc_mps: out of device memory (environments)");
+    return AQC_ERR_NOMEM;
+  }
   return AQC_OK;
 }
 

@@ -194,6 +194,8 @@ struct aqc_mps_s {
     ++version;
     synced_src = 0;
   }
+  // the one device block the handle's fixed buffers are carved from (aqc::dev_alloc)
+  void* base = nullptr;
   // scratch for the candidate sweep (grad.hip), allocated lazily
   aqc::cplx* gw = nullptr;
   size_t gw_bytes = 0;

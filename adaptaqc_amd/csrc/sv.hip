@@ -1008,10 +1008,10 @@ int aqc_sv_create(int n, aqc_sv_t* out) {
   h->reg_tiles = sv_reg_tiles(n);
   h->K = h->reg_tiles ? kRegTileBits : (n < 10 ? n : 10);
   const uint64_t dim = 1ull << n;
-  hipError_t e = hipMalloc(&h->state, dim * sizeof(cplx));
-  if (e != hipSuccess) {
+  h->state = (cplx*)aqc::dev_alloc(dim * sizeof(cplx));
+  if (!h->state) {
     delete h;
-    aqc::set_error(std::string("aqc_sv_create: hipMalloc state: ") + hipGetErrorString(e));
+    aqc::set_error("aqc_sv_create: out of device memory for the state");
     return AQC_ERR_NOMEM;
   }
   AQC_HIP_CHECK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
@@ -1027,7 +1027,7 @@ int aqc_sv_create(int n, aqc_sv_t* out) {
 int aqc_sv_destroy(aqc_sv_t h) {
   if (!h) return AQC_OK;
   if (h->stream) hipStreamSynchronize(h->stream);
-  hipFree(h->state);
+  aqc::dev_free(h->state);
   if (h->d_plan) hipFree(h->d_plan);
   if (h->h_plan) hipHostFree(h->h_plan);
   if (h->plan_ev) hipEventDestroy(h->plan_ev);

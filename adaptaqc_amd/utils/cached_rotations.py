@@ -114,7 +114,6 @@ class MPSPrefixBatch(_SweepBase):
         super().__init__(compiler)
         self.backend = compiler.backend
         self.phi = None
-        self.pool = []
 
     def goto(self, index):
         circ = self.compiler.full_circuit
@@ -132,9 +131,7 @@ class MPSPrefixBatch(_SweepBase):
         circ = self.compiler.full_circuit
         q = _ops_qubit(circ, index)
         suffix = ops_array(_ops(circ, index + 1, len(circ.data)))
-        while len(self.pool) < len(mats):
-            self.pool.append(self.backend.new_state())
-        states = self.pool[: len(mats)]
+        states = self.backend.scratch_states(len(mats))
         copy_batch(states, [self.phi] * len(mats))
         lists = [np.concatenate([ops_array([(m, (q,))]), suffix]) for m in mats]
         apply_batch(states, lists)
