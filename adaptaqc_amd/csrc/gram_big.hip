@@ -1025,25 +1025,20 @@ int run_gram_big(const TwoSiteJob* hjobs, const TwoSiteJob* jobs, int nj, int ca
   hipLaunchKernelGGL((k_gb_gram<CT>), dim3((CT / 64) * (CT / 64 + 1) / 2, nj), dim3(256), 0, st, jobs, a);
   AQC_CHECK_LAUNCH();
   // the tridiagonalisation's workgroups of a job must all be resident together (they exchange a
-  // vector per column): rounds of at most min(240, CUs) x (workgroups per CU) workgroups, whole jobs
-  // each.  Two workgroups per CU (64 VGPRs x 8 waves per SIMD, 2 x 33 KB of LDS) put config 5's 24
-  // jobs (384 workgroups) in one round: the per-column exchange is latency-bound (SQ_WAIT_ANY 71%
-  // at one per CU), so a second workgroup's pass and waits fill the first one's.  The hand-off is
-  // sc1 stores / loads through L2, which two workgroups on one CU see as any two CUs do.
-  // AQC_GB_PER_CU=1 restores one per CU (A/B).
+  // vector per column): rounds of at most min(240, resident capacity) workgroups, whole jobs each.
+  // (One workgroup per CU: the 1024-thread workgroup holds 16 complex of G per thread in 128 VGPRs,
+  // the whole register file at four waves per SIMD; a job's G is 4 MB at C = 512 against 512 KB of
+  // registers per CU, so 24 config-5 jobs cannot be resident at once whatever the split.)
   constexpr int P = CT * CT / 16384;
-  static int resident = -1, per_cu_used = 1;
+  static int resident = -1;
   if (resident < 0) {
     int dev = 0, ncu = 0, per_cu = 0;
     AQC_HIP_CHECK(hipGetDevice(&dev));
     AQC_HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
     AQC_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_gb_tridiag<CT, 1>, 1024, 0));
-    const char* e = std::getenv("AQC_GB_PER_CU");
-    const int want = e ? std::max(1, std::atoi(e)) : 2;
-    per_cu_used = std::max(1, std::min(per_cu, want));
-    resident = std::min(ncu, 240) * per_cu_used;
+    resident = ncu * std::min(per_cu, 1);
   }
-  const int per_round = resident / P;
+  const int per_round = std::min(240, resident) / P;
   // the eigenpairs and back-transformation of a round's jobs run on a second stream, beside the next
   // round's tridiagonalisation (which leaves CUs free: 9 of 24 config-5 jobs hold 144 of 256)
   static int overlap = -1;  // AQC_GB_OVERLAP=0: everything on the library stream (A/B)

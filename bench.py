@@ -48,10 +48,15 @@ FP64_PEAK_TFLOPS = 78.6  # MI355X dense FP64 (vector = matrix), MI355X_MICROARCH
 HBM_PEAK_GBS = 8000.0
 # HBM traffic and executed FP64 work of k_chain per two-site update from the committed PMC passes
 # of this round's code (tools/pmc_bench.sh, tools/pmc_exec.py); the previous round's as fallback
-TRAFFIC_JSON = "r3_traffic.json" if os.path.exists(os.path.join(ROOT, "profiles", "r3_traffic.json")) \
-    else "r2_traffic.json"
-EXEC_JSON = "r3_exec_k_chain.json" if os.path.exists(os.path.join(ROOT, "profiles", "r3_exec_k_chain.json")) \
-    else "r2_exec_k_chain.json"
+def _latest_profile(suffix):
+    for r in ("r4", "r3", "r2"):
+        if os.path.exists(os.path.join(ROOT, "profiles", f"{r}_{suffix}")):
+            return f"{r}_{suffix}"
+    return f"r2_{suffix}"
+
+
+TRAFFIC_JSON = _latest_profile("traffic.json")
+EXEC_JSON = _latest_profile("exec_k_chain.json")
 
 
 def vidal_from_tensors(A):
