@@ -23,7 +23,7 @@ assert OP_DTYPE.itemsize == 272
 EXPORTS = (
     "aqc_last_error", "aqc_version", "aqc_init", "aqc_finalize", "aqc_timing_enable",
     "aqc_timing_query", "aqc_timing_reset",
-    "aqc_sv_create", "aqc_sv_destroy", "aqc_sv_reset", "aqc_sv_copy", "aqc_sv_apply", "aqc_sv_plan",
+    "aqc_sv_create", "aqc_sv_destroy", "aqc_sv_reset", "aqc_sv_copy", "aqc_sv_apply", "aqc_sv_plan", "aqc_sv_set_slots",
     "aqc_sv_amp0", "aqc_sv_z_all", "aqc_sv_get", "aqc_sv_set",
     "aqc_mps_create", "aqc_mps_destroy", "aqc_mps_set_truncation", "aqc_mps_set_vidal",
     "aqc_mps_get_vidal", "aqc_mps_get_dims", "aqc_mps_copy", "aqc_mps_copy_batch", "aqc_mps_apply",
@@ -68,6 +68,7 @@ _SIGS = {
     "aqc_sv_copy": ([_P, _P], _I),
     "aqc_sv_apply": ([_P, _P, _I], _I),
     "aqc_sv_plan": ([_I, _P, _I, _P], _I),
+    "aqc_sv_set_slots": ([_I], _I),
     "aqc_sv_amp0": ([_P, _DP, _DP], _I),
     "aqc_sv_z_all": ([_P, _DP], _I),
     "aqc_sv_get": ([_P, _P], _I),

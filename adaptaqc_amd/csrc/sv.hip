@@ -130,25 +130,27 @@ __global__ __launch_bounds__(kThreads) void k_sv_segment(cplx* __restrict__ stat
 }
 
 // ---- register-resident tile passes (n >= kRegMinQubits) -------------------------------------
-// A 4096-amplitude tile per 256-thread workgroup.  The segment's fused gates are grouped on the
-// host into "phases" whose gates all act inside one set of kRegBits tile bits (the phase's slots).
-// In a phase every thread holds the 16 amplitudes that differ only in those slot bits in
-// registers, applies all of the phase's gates there (fully unrolled per slot pattern), and writes
-// them back: one LDS round trip and one barrier per phase instead of per gate, and 16
-// independent LDS reads per thread in flight instead of 4 dependent ones.  Gate matrices of
-// phase p+1 are staged into LDS (double buffer) while phase p computes.
-constexpr int kRegBits = 4;                 // slots per phase: 16 amplitudes per thread
-constexpr int kRegTileBits = 8 + kRegBits;  // 256 threads x 16 = 4096 amplitudes (64 KB LDS)
-constexpr int kRegMinQubits = 14;           // below: the per-gate kernel (too few tiles)
+// A 4096-amplitude tile per workgroup.  The segment's fused gates are grouped on the host into
+// "phases" whose gates all act inside one set of NS tile bits (the phase's slots).  In a phase
+// every thread holds the 2^NS amplitudes that differ only in those slot bits in registers, applies
+// all of the phase's gates there (fully unrolled per slot pattern), and writes them back: one LDS
+// round trip and one barrier per phase instead of per gate, and 2^NS independent LDS reads per
+// thread in flight instead of 2 or 4 dependent ones.  Gate matrices of phase p+1 are staged into
+// LDS (double buffer) while phase p computes.  NS = 4: 256 threads x 16 amplitudes (one wave per
+// SIMD at n = 20, where there are 256 tiles); NS = 3: 512 threads x 8 (two waves per SIMD, about
+// 1.7x the phases: three slots hold fewer gates).  AQC_SV_SLOTS selects (default 4).
+constexpr int kRegTileBits = 12;   // 4096 amplitudes (64 KB LDS)
+constexpr int kRegMinQubits = 14;  // below: the per-gate kernel (too few tiles)
 constexpr int kPhaseMaxGates = 16;
-constexpr int kRegLowBits = 4;              // global bits 0..3 always in the tile (256-byte runs)
+constexpr int kRegLowBits = 4;     // global bits 0..3 always in the tile (256-byte runs)
 static_assert(kRegTileBits <= kMaxTileBits, "tile header too small");
 
 struct PhaseHdr {
-  int32_t slotmask;  // the phase's kRegBits tile bits
-  int32_t gate_off;  // into the segment gate array (SegGate: t0 < t1 are slot indices 0..3)
+  int32_t slotmask;  // the phase's NS tile bits (+ the direct-I/O flags below)
+  int32_t gate_off;  // into the segment gate array (SegGate: t0 < t1 are slot indices 0..NS-1)
   int32_t ngates;
-  uint32_t lanemap;  // thread bit j -> tile bit (lanemap >> 4j) & 15 (the 8 non-slot bits)
+  int32_t pad;
+  uint64_t lanemap;  // thread bit j -> tile bit (lanemap >> 4j) & 15 (the 12 - NS non-slot bits)
 };
 
 // LDS layout: amplitude e of the tile lives at e ^ swz(e), where swz XORs a column of kSwzCol
@@ -168,11 +170,11 @@ __host__ __device__ __forceinline__ int swz_bits(int e) {
 }
 __host__ __device__ __forceinline__ int swz(int e) { return e ^ swz_bits(e); }
 
-template <int S>
-__device__ __forceinline__ void reg_apply1(cplx (&a)[16], const SegGate& g) {
+template <int S, int NA>
+__device__ __forceinline__ void reg_apply1(cplx (&a)[NA], const SegGate& g) {
   const cplx m00 = g.m[0], m01 = g.m[1], m10 = g.m[2], m11 = g.m[3];
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
+  for (int r = 0; r < NA; ++r) {
     if ((r >> S) & 1) continue;
     const int r1 = r | (1 << S);
     const cplx a0 = a[r], a1 = a[r1];
@@ -181,13 +183,13 @@ __device__ __forceinline__ void reg_apply1(cplx (&a)[16], const SegGate& g) {
   }
 }
 
-template <int S0, int S1>
-__device__ __forceinline__ void reg_apply2(cplx (&a)[16], const SegGate& g) {
+template <int S0, int S1, int NA>
+__device__ __forceinline__ void reg_apply2(cplx (&a)[NA], const SegGate& g) {
   cplx m[16];
 #pragma unroll
   for (int e = 0; e < 16; ++e) m[e] = g.m[e];
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
+  for (int r = 0; r < NA; ++r) {
     if (((r >> S0) & 1) || ((r >> S1) & 1)) continue;
     int idx[4];
     cplx v[4];
@@ -207,21 +209,29 @@ __device__ __forceinline__ void reg_apply2(cplx (&a)[16], const SegGate& g) {
   }
 }
 
-__device__ __forceinline__ void reg_apply(cplx (&a)[16], const SegGate& g) {
+template <int NS>
+__device__ __forceinline__ void reg_apply(cplx (&a)[1 << NS], const SegGate& g) {
   // wave-uniform dispatch on the slot pattern (t0 < t1 for 2-qubit gates, host-normalised)
+  constexpr int NA = 1 << NS;
   const int code = __builtin_amdgcn_readfirstlane(g.nq == 1 ? g.t0 : 4 + 4 * g.t0 + g.t1);
   switch (code) {
-    case 0: reg_apply1<0>(a, g); break;
-    case 1: reg_apply1<1>(a, g); break;
-    case 2: reg_apply1<2>(a, g); break;
-    case 3: reg_apply1<3>(a, g); break;
-    case 4 + 1: reg_apply2<0, 1>(a, g); break;
-    case 4 + 2: reg_apply2<0, 2>(a, g); break;
-    case 4 + 3: reg_apply2<0, 3>(a, g); break;
-    case 4 + 6: reg_apply2<1, 2>(a, g); break;
-    case 4 + 7: reg_apply2<1, 3>(a, g); break;
-    case 4 + 11: reg_apply2<2, 3>(a, g); break;
-    default: break;
+    case 0: reg_apply1<0, NA>(a, g); break;
+    case 1: reg_apply1<1, NA>(a, g); break;
+    case 2: reg_apply1<2, NA>(a, g); break;
+    case 4 + 1: reg_apply2<0, 1, NA>(a, g); break;
+    case 4 + 2: reg_apply2<0, 2, NA>(a, g); break;
+    case 4 + 6: reg_apply2<1, 2, NA>(a, g); break;
+    default:
+      if constexpr (NS == 4) {
+        switch (code) {
+          case 3: reg_apply1<3, NA>(a, g); break;
+          case 4 + 3: reg_apply2<0, 3, NA>(a, g); break;
+          case 4 + 7: reg_apply2<1, 3, NA>(a, g); break;
+          case 4 + 11: reg_apply2<2, 3, NA>(a, g); break;
+          default: break;
+        }
+      }
+      break;
   }
 }
 
@@ -231,10 +241,11 @@ __device__ __forceinline__ void reg_apply(cplx (&a)[16], const SegGate& g) {
 // bits 0-3 (no low slot bit): a wave then reads / writes 16 runs of 256 contiguous bytes.
 constexpr int kPhaseDirectIn = 1 << 30, kPhaseDirectOut = 1 << 29, kPhaseSlotBits = (1 << kRegTileBits) - 1;
 
-__global__ __launch_bounds__(kThreads) void k_sv_tile_reg(cplx* __restrict__ state, const SegHeader* __restrict__ hdr,
-                                                         const PhaseHdr* __restrict__ phases,
-                                                         const SegGate* __restrict__ gates, int from_zero) {
-  constexpr int K = kRegTileBits;
+template <int NS>
+__global__ __launch_bounds__(4096 >> NS) void k_sv_tile_reg(cplx* __restrict__ state, const SegHeader* __restrict__ hdr,
+                                                           const PhaseHdr* __restrict__ phases,
+                                                           const SegGate* __restrict__ gates, int from_zero) {
+  constexpr int K = kRegTileBits, kThr = 4096 >> NS, kTB = K - NS, NA = 1 << NS;
   __shared__ cplx tile[1 << K];
   __shared__ SegGate gl[2][kPhaseMaxGates];
   const int tid = threadIdx.x;
@@ -250,12 +261,12 @@ __global__ __launch_bounds__(kThreads) void k_sv_tile_reg(cplx* __restrict__ sta
     for (int j = 0; j < K; ++j) g |= (uint64_t)((x >> j) & 1) << tb[j];
     return g;
   };
-  constexpr int kPer = (1 << K) / kThreads;
+  constexpr int kPer = (1 << K) / kThr;
   if (from_zero && blockIdx.x != 0) {
     // a deferred aqc_sv_reset: every tile but tile 0 (which holds index 0) is zero in and out --
     // the segment's gates act inside the tile -- so it is written without loads or gates
 #pragma unroll
-    for (int r = 0; r < kPer; ++r) aqc::stg(state + gidx(tid + r * kThreads), aqc::cmk(0.0, 0.0));
+    for (int r = 0; r < kPer; ++r) aqc::stg(state + gidx(tid + r * kThr), aqc::cmk(0.0, 0.0));
     return;
   }
   const int np = hdr->ngates;
@@ -266,41 +277,42 @@ __global__ __launch_bounds__(kThreads) void k_sv_tile_reg(cplx* __restrict__ sta
     cplx v[kPer];
     if (from_zero) {
 #pragma unroll
-      for (int r = 0; r < kPer; ++r) v[r] = aqc::cmk(tid + r * kThreads == 0 ? 1.0 : 0.0, 0.0);
+      for (int r = 0; r < kPer; ++r) v[r] = aqc::cmk(tid + r * kThr == 0 ? 1.0 : 0.0, 0.0);
     } else {
 #pragma unroll
-      for (int r = 0; r < kPer; ++r) v[r] = aqc::ldg(state + gidx(tid + r * kThreads));
+      for (int r = 0; r < kPer; ++r) v[r] = aqc::ldg(state + gidx(tid + r * kThr));
     }
 #pragma unroll
-    for (int r = 0; r < kPer; ++r) tile[swz(tid + r * kThreads)] = v[r];
+    for (int r = 0; r < kPer; ++r) tile[swz(tid + r * kThr)] = v[r];
   }
   constexpr int kWords = (int)(sizeof(SegGate) / sizeof(double2));
   auto stage = [&](int p) {
     const int ng = ph[p].ngates;
     const double2* src = reinterpret_cast<const double2*>(gates + ph[p].gate_off);
     double2* dst = reinterpret_cast<double2*>(gl[p & 1]);
-    for (int w = tid; w < ng * kWords; w += kThreads) dst[w] = src[w];
+    for (int w = tid; w < ng * kWords; w += kThr) dst[w] = src[w];
   };
   if (np > 0) stage(0);
   __syncthreads();
   for (int p = 0; p < np; ++p) {
     if (p + 1 < np) stage(p + 1);  // the other buffer: its last readers passed the barrier below
     const int sm = __builtin_amdgcn_readfirstlane(ph[p].slotmask) & kPhaseSlotBits;
-    const unsigned lm = __builtin_amdgcn_readfirstlane(ph[p].lanemap);
+    const uint64_t lm = ((uint64_t)(unsigned)__builtin_amdgcn_readfirstlane((int)(ph[p].lanemap >> 32)) << 32) |
+                        (unsigned)__builtin_amdgcn_readfirstlane((int)ph[p].lanemap);
     // thread bits placed on the non-slot tile bits by the lane map, slot bits from r; the swizzle
     // is linear, so the LDS address is swz(thread part) ^ swz(slot part), and the global index
     // is the OR of the two parts' scattered bits
     int lraw = 0;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) lraw |= ((tid >> j) & 1) << ((lm >> (4 * j)) & 15);
-    // the kRegBits slot bits, lowest first (the host pads every phase to exactly kRegBits), and
-    // their global bits (no per-lane indexing: the arrays stay in registers)
-    int sraw[kRegBits];
-    uint64_t sg[kRegBits];
+    for (int j = 0; j < kTB; ++j) lraw |= ((tid >> j) & 1) << ((int)(lm >> (4 * j)) & 15);
+    // the NS slot bits, lowest first (the host pads every phase to exactly NS), and their global
+    // bits (no per-lane indexing: the arrays stay in registers)
+    int sraw[4] = {0, 0, 0, 0};
+    uint64_t sg[4] = {0, 0, 0, 0};
     {
       int m = sm;
 #pragma unroll
-      for (int i = 0; i < kRegBits; ++i) {
+      for (int i = 0; i < NS; ++i) {
         sraw[i] = m & -m;
         m ^= sraw[i];
         sg[i] = gidx(sraw[i]) ^ base;
@@ -308,46 +320,46 @@ __global__ __launch_bounds__(kThreads) void k_sv_tile_reg(cplx* __restrict__ sta
     }
     const bool in_g = p == 0 && d_in, out_g = p == np - 1 && d_out;
     const int lb = swz(lraw);
-    int off[16];
+    int off[NA];
 #pragma unroll
-    for (int r = 0; r < 16; ++r)
+    for (int r = 0; r < NA; ++r)
       off[r] = lb ^ ((r & 1) ? swz(sraw[0]) : 0) ^ ((r & 2) ? swz(sraw[1]) : 0) ^ ((r & 4) ? swz(sraw[2]) : 0) ^
                ((r & 8) ? swz(sraw[3]) : 0);
     auto gaddr = [&](int r) {
       return state + (gidx(lraw) | ((r & 1) ? sg[0] : 0) | ((r & 2) ? sg[1] : 0) | ((r & 4) ? sg[2] : 0) |
                       ((r & 8) ? sg[3] : 0));
     };
-    cplx a[16];
+    cplx a[NA];
     if (in_g) {
       if (from_zero) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
+        for (int r = 0; r < NA; ++r) {
           const int x = lraw | ((r & 1) ? sraw[0] : 0) | ((r & 2) ? sraw[1] : 0) | ((r & 4) ? sraw[2] : 0) |
                         ((r & 8) ? sraw[3] : 0);
           a[r] = aqc::cmk(x == 0 ? 1.0 : 0.0, 0.0);
         }
       } else {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) a[r] = aqc::ldg(gaddr(r));
+        for (int r = 0; r < NA; ++r) a[r] = aqc::ldg(gaddr(r));
       }
     } else {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) a[r] = tile[off[r]];
+      for (int r = 0; r < NA; ++r) a[r] = tile[off[r]];
     }
     const int ng = ph[p].ngates;
-    for (int gi = 0; gi < ng; ++gi) reg_apply(a, gl[p & 1][gi]);
+    for (int gi = 0; gi < ng; ++gi) reg_apply<NS>(a, gl[p & 1][gi]);
     if (out_g) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) aqc::stg(gaddr(r), a[r]);
+      for (int r = 0; r < NA; ++r) aqc::stg(gaddr(r), a[r]);
     } else {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) tile[off[r]] = a[r];
+      for (int r = 0; r < NA; ++r) tile[off[r]] = a[r];
       __syncthreads();
     }
   }
   if (!d_out) {
 #pragma unroll
-    for (int r = 0; r < kPer; ++r) aqc::stg(state + gidx(tid + r * kThreads), tile[swz(tid + r * kThreads)]);
+    for (int r = 0; r < kPer; ++r) aqc::stg(state + gidx(tid + r * kThr), tile[swz(tid + r * kThr)]);
   }
 }
 
@@ -599,22 +611,24 @@ std::vector<SegGate> fuse_segment(const aqc_op_t* ops, const std::vector<int>& i
 }
 
 // Phases of a fused segment (k_sv_tile_reg): greedy in application order, a gate joins the
-// current phase when its tile bits fit in the phase's kRegBits slots and it acts on no bit of a
-// gate left for a later phase (gates on disjoint bits commute).  Gate bits become slot indices
-// (t0 < t1, the 4x4 re-indexed when the order flips).
-// Lane map of a slot set: an order of the 8 non-slot tile bits over the thread bits whose first
-// five give conflict-free LDS groups under swz (checked by counting bank slots over the 64 lanes
-// of a wave; the first order with no conflict, else the one with the fewest extra cycles).
-// Cached per slot set.
-uint32_t lane_map(uint32_t S) {
-  // cached per slot set: bit 32 marks a computed entry (lock-free reads; a race computes the same
-  // value twice)
-  static std::array<std::atomic<uint64_t>, 1 << kRegTileBits> cache{};
-  const uint64_t c = cache[S].load(std::memory_order_acquire);
-  if (c >> 32) return (uint32_t)c;
-  int ns[8], nn = 0;
+// current phase when its tile bits fit in the phase's NS slots and it acts on no bit of a gate
+// left for a later phase (gates on disjoint bits commute).  Gate bits become slot indices (t0 < t1,
+// the 4x4 re-indexed when the order flips).
+// Lane map of a slot set: an order of the 12 - NS non-slot tile bits over the thread bits whose
+// first six (the wave's lanes) give conflict-free LDS groups under swz (checked by counting bank
+// slots over the 64 lanes of a wave; the first order with no conflict, else the one with the
+// fewest extra cycles).  Cached per slot set.
+uint64_t lane_map(uint32_t S, int NS) {
+  // cached per (NS, slot set): bit 63 marks a computed entry (lock-free reads; a race computes
+  // the same value twice)
+  static std::array<std::atomic<uint64_t>, 2 << kRegTileBits> cache{};
+  std::atomic<uint64_t>& slot_entry = cache[(NS == 3 ? (1 << kRegTileBits) : 0) + S];
+  const uint64_t c = slot_entry.load(std::memory_order_acquire);
+  if (c >> 63) return c & ~(1ull << 63);
+  const int TB = kRegTileBits - NS;
+  int ns[9], nn = 0;
   for (int b = 0; b < kRegTileBits; ++b)
-    if (!((S >> b) & 1u)) ns[nn++] = b;
+    if (!((S >> b) & 1u) && nn < 9) ns[nn++] = b;
   auto cost = [&](const int* pos) {
     int e[64];
     for (int l = 0; l < 64; ++l) {
@@ -638,34 +652,34 @@ uint32_t lane_map(uint32_t S) {
     }
     return c;
   };
-  int best[8], bc = 1 << 30;
-  int perm[8];
-  for (int i = 0; i < 8; ++i) perm[i] = i;
-  // the first six positions decide the wave's banks; the last two (threads across waves) follow
+  int best[9], bc = 1 << 30;
+  int perm[9];
+  for (int i = 0; i < TB; ++i) perm[i] = i;
+  // the first six positions decide the wave's banks; the rest (threads across waves) follow
   do {
-    int pos[8];
-    for (int i = 0; i < 8; ++i) pos[i] = ns[perm[i]];
+    int pos[9];
+    for (int i = 0; i < TB; ++i) pos[i] = ns[perm[i]];
     const int c = cost(pos);
     if (c < bc) {
       bc = c;
-      std::memcpy(best, pos, sizeof(best));
+      std::memcpy(best, pos, sizeof(int) * TB);
       if (c == 0) break;
     }
-    std::reverse(perm + 6, perm + 8);  // skip orders that differ only in the last two
-  } while (std::next_permutation(perm, perm + 8));
-  uint32_t m = 0;
-  for (int j = 0; j < 8; ++j) m |= (uint32_t)best[j] << (4 * j);
-  cache[S].store((1ull << 32) | m, std::memory_order_release);
+    std::reverse(perm + 6, perm + TB);  // skip orders that differ only past the sixth position
+  } while (std::next_permutation(perm, perm + TB));
+  uint64_t m = 0;
+  for (int j = 0; j < TB; ++j) m |= (uint64_t)best[j] << (4 * j);
+  slot_entry.store((1ull << 63) | m, std::memory_order_release);
   return m;
 }
 
 // The segment's first / last phase: non-slot tile bits in ascending order over the thread bits,
 // flagged for direct global reads / writes (k_sv_tile_reg) when no slot is a low tile bit
-uint32_t lane_map_coalesced(uint32_t S) {
-  uint32_t m = 0;
+uint64_t lane_map_coalesced(uint32_t S) {
+  uint64_t m = 0;
   int j = 0;
-  for (int b = 0; b < kRegTileBits && j < 8; ++b)
-    if (!((S >> b) & 1u)) m |= (uint32_t)b << (4 * j++);
+  for (int b = 0; b < kRegTileBits; ++b)
+    if (!((S >> b) & 1u)) m |= (uint64_t)b << (4 * j++);
   return m;
 }
 
@@ -680,12 +694,10 @@ void mark_direct_phases(PhaseHdr* first, PhaseHdr* last) {
     if (last != first) last->lanemap = lane_map_coalesced((uint32_t)(last->slotmask & kPhaseSlotBits));
     last->slotmask |= kPhaseDirectOut;
   }
-  // one phase both reading and writing global memory needs one lane map for both
-  if (first == last && (first->slotmask & kPhaseDirectIn) == 0 && (first->slotmask & kPhaseDirectOut))
-    first->lanemap = lane_map_coalesced((uint32_t)(first->slotmask & kPhaseSlotBits));
 }
 
-void build_phases(const std::vector<SegGate>& fused, int K, std::vector<PhaseHdr>& ph, std::vector<SegGate>& out) {
+void build_phases(const std::vector<SegGate>& fused, int K, int NS, std::vector<PhaseHdr>& ph,
+                  std::vector<SegGate>& out) {
   std::vector<char> done(fused.size(), 0);
   size_t remaining = fused.size(), first = 0;
   while (remaining > 0) {
@@ -698,7 +710,7 @@ void build_phases(const std::vector<SegGate>& fused, int K, std::vector<PhaseHdr
       const uint32_t gm = (1u << fused[i].t0) | (fused[i].nq == 2 ? (1u << fused[i].t1) : 0u);
       if (gm & blocked) {
         blocked |= gm;
-      } else if (__builtin_popcount(S | gm) <= kRegBits) {
+      } else if (__builtin_popcount(S | gm) <= NS) {
         S |= gm;
         members[nm++] = i;
         done[i] = 1;
@@ -708,13 +720,14 @@ void build_phases(const std::vector<SegGate>& fused, int K, std::vector<PhaseHdr
       }
       if (__builtin_popcount(blocked) >= K) break;
     }
-    for (int b = 0; b < K && __builtin_popcount(S) < kRegBits; ++b) S |= 1u << b;
+    for (int b = 0; b < K && __builtin_popcount(S) < NS; ++b) S |= 1u << b;
     auto slot = [&](int b) { return __builtin_popcount(S & ((1u << b) - 1u)); };
     PhaseHdr h;
     h.slotmask = (int32_t)S;
     h.gate_off = (int32_t)out.size();
     h.ngates = (int32_t)nm;
-    h.lanemap = lane_map(S);
+    h.pad = 0;
+    h.lanemap = lane_map(S, NS);
     ph.push_back(h);
     for (int mi = 0; mi < nm; ++mi) {
       SegGate g = fused[members[mi]];
@@ -902,6 +915,19 @@ static std::vector<HostSeg> sv_plan_segments(int n, int K, bool reg_tiles, const
 
 // Segment s of the plan: its header (hdr[s], sized by the caller), its fused gates and phases
 // appended to gts / phs (gate_off indexes the whole list).
+// slots per phase of the register-tile path: aqc_sv_set_slots, else AQC_SV_SLOTS = 3 or 4 (read at
+// first use), else 4.  Each aqc_sv_apply plans and launches with one value.
+static std::atomic<int> g_sv_slots{0};
+static int sv_slots() {
+  int ns = g_sv_slots.load(std::memory_order_relaxed);
+  if (ns == 0) {
+    const char* e = std::getenv("AQC_SV_SLOTS");
+    ns = (e && std::atoi(e) == 3) ? 3 : 4;
+    g_sv_slots.store(ns, std::memory_order_relaxed);
+  }
+  return ns;
+}
+
 static void sv_plan_one(int n, int K, bool reg_tiles, const aqc_op_t* ops, const HostSeg& seg, size_t s,
                         std::vector<SegHeader>& hdr, std::vector<SegGate>& gts, std::vector<PhaseHdr>& phs,
                         std::vector<double>* seg_flops) {
@@ -927,7 +953,7 @@ static void sv_plan_one(int n, int K, bool reg_tiles, const aqc_op_t* ops, const
   if (reg_tiles) {  // gate_off / ngates index the phase list
     hdr[s].gate_off = (int)phs.size();
     const size_t before = phs.size();
-    build_phases(fused, K, phs, gts);
+    build_phases(fused, K, sv_slots(), phs, gts);
     hdr[s].ngates = (int)(phs.size() - before);
     if (phs.size() > before) mark_direct_phases(&phs[before], &phs.back());
     // timing experiments only (results wrong): AQC_SV_DEBUG=nogates / nophases
@@ -965,7 +991,10 @@ static int sv_launch_segment(aqc_sv_t h, const SegHeader* dh, const PhaseHdr* dp
   const double bytes = (from_zero ? 16.0 : 32.0) * (double)(1ull << h->n);
   aqc::KernelTimer::begin(h->stream, "sv_segment", bytes, flops);
   if (h->reg_tiles) {
-    hipLaunchKernelGGL(k_sv_tile_reg, dim3(nblocks), dim3(kThreads), 0, h->stream, h->state, dh, dp, dg, from_zero);
+    if (sv_slots() == 3)
+      hipLaunchKernelGGL(k_sv_tile_reg<3>, dim3(nblocks), dim3(512), 0, h->stream, h->state, dh, dp, dg, from_zero);
+    else
+      hipLaunchKernelGGL(k_sv_tile_reg<4>, dim3(nblocks), dim3(256), 0, h->stream, h->state, dh, dp, dg, from_zero);
     h->zero_pending = false;
     aqc::KernelTimer::end(h->stream);
     AQC_CHECK_LAUNCH();
@@ -1140,6 +1169,12 @@ int aqc_sv_apply(aqc_sv_t h, const aqc_op_t* ops, int nops) {
   // (recorded on every path, so the next call never reuses the staging buffer under a live copy)
   AQC_HIP_CHECK(hipEventRecord(h->plan_ev, h->stream));
   return rc;
+}
+
+int aqc_sv_set_slots(int slots) {
+  AQC_REQUIRE(slots == 3 || slots == 4, "aqc_sv_set_slots: 3 or 4");
+  g_sv_slots.store(slots, std::memory_order_relaxed);
+  return AQC_OK;
 }
 
 int aqc_sv_plan(int n, const aqc_op_t* ops, int nops, int* out) {

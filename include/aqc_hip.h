@@ -72,6 +72,10 @@ int aqc_sv_apply(aqc_sv_t h, const aqc_op_t* ops, int nops);
 /* Host planning of aqc_sv_apply only (no GPU): out[0] segments (= launches), out[1] phases
  * (register-tile path; 0 otherwise), out[2] fused gates, out[3] tile bits. */
 int aqc_sv_plan(int n, const aqc_op_t* ops, int nops, int* out);
+/* Slots per phase of the register-tile kernel (n >= 14): 4 (default; 256 threads x 16 amplitudes
+   per 4096-amplitude tile) or 3 (512 threads x 8: two waves per SIMD at n = 20, more phases).
+   Also AQC_SV_SLOTS at first use.  Results equal up to summation order. */
+int aqc_sv_set_slots(int slots);
 /* sv[0] (aer_sv_backend.py:29). */
 int aqc_sv_amp0(aqc_sv_t h, double* re, double* im);
 /* <Z_i> = p0 - p1 for all i (aer_sv_backend.py:49-59), out[n]. */

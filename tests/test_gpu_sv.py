@@ -148,10 +148,22 @@ def test_gate_fusion_patterns():
         np.testing.assert_allclose(d.get(), osv.simulate(n, ops), atol=1e-12, err_msg=f"n={n}")
 
 
-def test_register_tile_path_vs_oracle_and_lds_kernel(monkeypatch):
-    """n >= 14 runs the register-resident tile kernel (gates grouped into 4-bit phases): random
-    1q/2q gates incl. fusion patterns, long-range pairs and reversed orders, against the oracle and
-    against the per-gate LDS kernel (AQC_SV_TILE=lds)."""
+@pytest.fixture(params=[4, 3], ids=["slots4", "slots3"])
+def sv_slots(request):
+    """The register-tile kernel's phase width (aqc_sv_set_slots): 4 slots / 256 threads (default)
+    or 3 slots / 512 threads."""
+    from adaptaqc_amd import _lib
+
+    L = _lib.lib()
+    _lib.check(L.aqc_sv_set_slots(request.param))
+    yield request.param
+    _lib.check(L.aqc_sv_set_slots(4))
+
+
+def test_register_tile_path_vs_oracle_and_lds_kernel(monkeypatch, sv_slots):
+    """n >= 14 runs the register-resident tile kernel (gates grouped into 4- or 3-bit phases):
+    random 1q/2q gates incl. fusion patterns, long-range pairs and reversed orders, against the
+    oracle and against the per-gate LDS kernel (AQC_SV_TILE=lds)."""
     from adaptaqc_amd.circuit import device_ops
     from adaptaqc_amd.device import DeviceSV
 
@@ -181,7 +193,7 @@ def test_register_tile_path_vs_oracle_and_lds_kernel(monkeypatch):
         np.testing.assert_allclose(got, d2.get(), atol=1e-13, err_msg=f"n={n} (lds kernel)")
 
 
-def test_config2_exact_workload_vs_oracle_goldens():
+def test_config2_exact_workload_vs_oracle_goldens(sv_slots):
     """BASELINE config 2 exactly as tools/configs_bench.py times it -- 20 qubits,
     brickwork depth 20, seeds 0..9, with 0 / 10 / 50 thinly-dressed layers -- all 30 circuits
     through the register-tile SV path against the oracle's values (tests/golden/config2_sv.npz, made
@@ -223,7 +235,7 @@ def test_config2_exact_workload_vs_oracle_goldens():
             k += 1
 
 
-def test_deferred_reset_every_reader():
+def test_deferred_reset_every_reader(sv_slots):
     """aqc_sv_reset on the register-tile path (n >= 14) launches nothing: the next apply's first
     pass forms |0...0> in its tiles, and every other reader (amp0, get, z_all, pair RDMs, transition,
     copy in either direction, set) sees |0...0> or overwrites it.  Each case follows an apply that
