@@ -45,6 +45,7 @@ struct PoolKey {
 std::map<PoolKey, std::vector<void*>> g_pool_free;  // cached blocks
 std::map<void*, PoolKey> g_pool_live;               // blocks handed out
 size_t g_pool_cached = 0, g_pool_limit = 0;
+unsigned long long g_pool_hits = 0, g_pool_misses = 0;
 
 void pool_release_locked() {
   int cur = 0;
@@ -83,7 +84,8 @@ void* dev_alloc(size_t bytes) {
     p = it->second.back();
     it->second.pop_back();
     g_pool_cached -= b;
-  } else if (hipMalloc(&p, b) != hipSuccess) {
+    ++g_pool_hits;
+  } else if (++g_pool_misses, hipMalloc(&p, b) != hipSuccess) {
     (void)hipGetLastError();
     pool_release_locked();
     (void)hipSetDevice(dev);
@@ -245,6 +247,19 @@ int aqc_debug_hog(int nblocks, double ms) {
   hipLaunchKernelGGL(aqc::k_hog, dim3(nblocks), dim3(256), 0, aqc::g_hog_stream[dev],
                      (unsigned long long)(ms * 1e5));
   AQC_CHECK_LAUNCH();
+  return AQC_OK;
+}
+
+int aqc_pool_stats(double* out) {
+  AQC_REQUIRE(out, "aqc_pool_stats: null out");
+  std::lock_guard<std::mutex> lk(aqc::g_pool_mutex);
+  size_t live = 0;
+  for (const auto& kv : aqc::g_pool_live) live += kv.second.bytes;
+  out[0] = (double)aqc::g_pool_cached;
+  out[1] = (double)live;
+  out[2] = (double)aqc::g_pool_live.size();
+  out[3] = (double)aqc::g_pool_hits;
+  out[4] = (double)aqc::g_pool_misses;
   return AQC_OK;
 }
 

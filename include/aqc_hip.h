@@ -167,6 +167,10 @@ int aqc_gb_set_spin_limit(double us);
 /* Test load: nblocks 256-thread workgroups on a private stream, block b spinning (b % 16 + 1) / 16
    of `ms` milliseconds, so work queued on other streams starts one CU at a time.  Asynchronous. */
 int aqc_debug_hog(int nblocks, double ms);
+/* Device-memory cache of the library (MPS / SV handle buffers): out[0] bytes cached (freed, kept
+   for reuse), out[1] bytes handed out, out[2] blocks handed out, out[3] requests served from the
+   cache, out[4] requests that went to hipMalloc.  Limit: AQC_POOL_MB (default 8192). */
+int aqc_pool_stats(double* out);
 /* Batched applies of >= 32 states at 2*chi = 128 run every state's whole op list in
    one fused workgroup (theta, Jacobi, truncation, split per update: no grid-wide step between
    updates); on = 0 selects the lock-step launches per update, on = 2 the fused chain for batches

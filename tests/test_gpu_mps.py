@@ -323,3 +323,44 @@ def test_fused_chain_matches_lockstep_and_oracle(sort):
         ref = M.run_circuit(n, circuits[s], 1e-16, chi)
         ov_ref = M.mps_dot(ref.preprocessed(), M.zero_mps(n))
         assert abs(res[1][0][s] - ov_ref) <= 1e-9 * abs(ov_ref) + 1e-18
+
+
+def test_device_memory_cache_reuses_blocks_and_results_unchanged():
+    """Handles take their buffers from the library's device-memory cache: creating and dropping
+    the same shape again is served from the cache (no hipMalloc), the handed-out bytes return to
+    their starting value, and a state built in a reused block is the oracle's (the block is
+    re-initialised, nothing of the previous owner leaks in)."""
+    import ctypes
+
+    from adaptaqc_amd import _lib
+    from adaptaqc_amd.circuit import device_ops
+    from adaptaqc_amd.device import DeviceMPS
+
+    L = _lib.lib()
+
+    def stats():
+        out = (ctypes.c_double * 5)()
+        _lib.check(L.aqc_pool_stats(out))
+        return list(out)
+
+    n, chi = 12, 16
+    ops = []
+    rng = np.random.default_rng(5)
+    for layer in range(5):
+        for q in range(n):
+            ops.append(("ry", (q,), (rng.uniform(-np.pi, np.pi),)))
+        for q in range(layer % 2, n - 1, 2):
+            ops.append(("cx", (q, q + 1), ()))
+    dops = device_ops(to_circuit(n, ops))
+    want = M.mps_dot(M.run_circuit(n, ops, 1e-16, chi).preprocessed(), M.zero_mps(n))
+    for it in range(21):  # (the first pass allocates the shape's blocks: handle, environments)
+        if it == 1:
+            s0 = stats()
+        d = DeviceMPS(n, chi, 1e-16, chi)
+        d.apply(dops)
+        assert abs(d.overlap_zero() - want) < 1e-10
+        d.close()
+    s1 = stats()
+    assert s1[4] == s0[4], (s0, s1)          # no new hipMalloc for the repeated shape
+    assert s1[3] >= s0[3] + 20, (s0, s1)     # every creation served from the cache
+    assert s1[1] == s0[1] and s1[2] == s0[2]  # nothing left handed out
