@@ -2362,7 +2362,7 @@ int aqc_svd_debug(const double* theta, int m, int n, int variant, int stop_after
   AQC_REQUIRE(m >= 1 && n >= 1 && m % 2 == 0 && n % 2 == 0 && m <= 128 && n <= 128,
               "aqc_svd_debug: m, n must be even and <= 128");
   AQC_REQUIRE(stop_after_qr >= 0 && stop_after_qr <= 2, "aqc_svd_debug: stop_after_qr must be 0, 1 or 2");
-  AQC_REQUIRE(variant == 2 || variant == 7 || variant == 8,
+  AQC_REQUIRE(variant == 2 || variant == 7 || variant == 8 || variant == 9,
               "aqc_svd_debug: variant must be 2 (register Jacobi), 7 (Gram path) or 8 (Gram path, 256 threads)");
   AQC_REQUIRE(variant < 7 || (std::max(m, n) > 64 && stop_after_qr == 0),
               "aqc_svd_debug: variants 7 / 8 (Gram) need 64 < max(m, n) <= 128 and no QR stop");
@@ -2394,7 +2394,7 @@ int aqc_svd_debug(const double* theta, int m, int n, int variant, int stop_after
   j.dbg = stop_after_qr;
   j.cap = 64;                     // the work buffer holds 128 x 128
   j.max_chi = g_debug_max_chi;    // Gram path: K = min(C, max_chi)
-  j.gram = variant >= 7;  // 1: stop after the QR phase; 2: also QR phase clock ticks in sig[0..3]
+  j.gram = variant == 9 ? 2 : variant >= 7;  // (stop_after_qr 1: stop after the QR phase; 2: also its ticks)
   int hd[8] = {m / 2, 0, n / 2, 0, 0, 0, 0, 0};  // dims, then zeroed flags
   AQC_HIP_CHECK(hipMemcpyAsync(th, theta, (size_t)m * n * sizeof(cplx), hipMemcpyHostToDevice, st));
   AQC_HIP_CHECK(hipMemcpyAsync(dm, hd, sizeof(hd), hipMemcpyHostToDevice, st));
@@ -2402,7 +2402,7 @@ int aqc_svd_debug(const double* theta, int m, int n, int variant, int stop_after
   AQC_HIP_CHECK(hipMemsetAsync(wk, 0, mat, st));
   if (cp == 32) hipLaunchKernelGGL((k_jacobi_reg<32, 2>), dim3(1), dim3(256), 16 * 33 * 16, st, dj);
   else if (cp == 64) hipLaunchKernelGGL((k_jacobi_reg<64, 4>), dim3(1), dim3(512), 32 * 65 * 16, st, dj);
-  else if (variant == 7)
+  else if (variant == 7 || variant == 9)  // 9: the Gram path with the lower-triangle S3 (j.gram = 2)
     hipLaunchKernelGGL(k_svd_gram, dim3(1), dim3(1024), kChainLdsBytes, st, dj);
   else if (variant == 8)  // (flags[2] = -1: declined)
     hipLaunchKernelGGL(k_svd_gram256, dim3(1), dim3(256), tri::kLdsBytes, st, dj);
@@ -2466,7 +2466,7 @@ int aqc_svd_gram_stats(double* out) {
 }
 
 int aqc_mps_set_svd_path(int gram, int debug_max_chi) {
-  AQC_REQUIRE(gram == 0 || gram == 1, "aqc_mps_set_svd_path: gram must be 0 or 1");
+  AQC_REQUIRE(gram >= 0 && gram <= 2, "aqc_mps_set_svd_path: gram must be 0, 1 or 2");
   g_svd_gram = gram;
   g_debug_max_chi = debug_max_chi;
   return AQC_OK;

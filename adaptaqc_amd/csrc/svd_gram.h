@@ -207,10 +207,42 @@ __device__ __forceinline__ double rcp_nr(double x) {
   return r;
 }
 
+// The lower-triangle tridiagonalisation of svd_tri.h (defined there), which gram_svd_body<true>
+// runs at 1024 threads in place of its full-matrix S3
+namespace tri {
+struct S3Ctx {
+  int C;               // matrix size
+  cplx* hh;            // packed reflectors (global, SGPR)
+  cplx* scratch;       // repack scratch (global)
+  const cplx* th;      // theta' (S1)
+  int M, L, tr;        // X = theta' (L x C) or its conjugate transpose
+};
+template <int TR, int NT>
+__device__ __noinline__ void s3_stage(const S3Ctx& cx_in, int k0, int k1, int mode);
+constexpr size_t kScratchOff = 8192;  // (= tri::kScratch)
+// The tridiagonalisation's LDS map (complex units) per workgroup size: at 256 threads svd_tri.h's
+// constants (kVec ...); at 1024 threads a grid of up to 6176 entries (TR = 2, NB = 64), then the
+// vectors, scalars, 16 waves' p^H v and d / e / tau of its own (copied to the body's arrays
+// after S3)
+template <int NT>
+struct TriLds {
+  static constexpr int kGrid = 0, kVec = 3136, kGk1 = 3544, kScal = 3672, kKtp = 3676, kD = 4096, kE = 4160,
+                       kTau = 4480;
+};
+template <>
+struct TriLds<1024> {
+  static constexpr int kGrid = 0, kVec = 6176, kGk1 = 6584, kScal = 6712, kKtp = 6716, kD = 6736, kE = 6800,
+                       kTau = 6864, kEnd = 6994;
+};
+}  // namespace tri
+
 // Gram-path SVD of one 2 chi x 2 chi theta'; 1024 threads; `xbuf` = the workgroup's dynamic LDS
 // (>= 4 GemmLds).  Returns false (work untouched beyond scratch, caller runs the Jacobi) when the
-// fast path does not apply.  Uniform in the workgroup.
-__device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
+// fast path does not apply.  Uniform in the workgroup.  TRI (j.gram == 2): S3 as the lower-triangle
+// stages of svd_tri.h on all 16 waves (tiles 2 x 4 over the trailing 128, then 1 x 2 over the
+// trailing 64) instead of the full Hermitian matrix in registers.
+template <bool TRI>
+__device__ __noinline__ bool gram_svd_body_t(const TwoSiteJob& j) {
   extern __shared__ double2 xbuf[];
   __shared__ double s_d[128], s_e[128], s_e2[128], s_lam[kGramMaxK], s_sig2[kGramMaxK];
   __shared__ cplx s_tau[128];
@@ -374,19 +406,51 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
       }
     }
     __syncthreads();
+    if constexpr (!TRI) {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int c = q + 8 * i;
-      cplx v = aqc::cmk(0, 0);
-      if (r < C && c < C) {
-        v = gsq[c >= r ? up_index(r, c) : up_index(c, r)];
-        if (c < r) v.y = -v.y;
+      for (int i = 0; i < 16; ++i) {
+        const int c = q + 8 * i;
+        cplx v = aqc::cmk(0, 0);
+        if (r < C && c < C) {
+          v = gsq[c >= r ? up_index(r, c) : up_index(c, r)];
+          if (c < r) v.y = -v.y;
+        }
+        g[i] = v;
       }
-      g[i] = v;
+      __syncthreads();  // the reflectors' scratch reuses the LDS
     }
-    __syncthreads();  // the reflectors' scratch reuses the LDS
   }
   tick(0);
+  // reflector k at hh[k (2C - k - 1) / 2 + (row - k - 1)].  The base is uniform: moved to SGPRs
+  // (as a VGPR pair it was spilled, and phase B's scratch reload waited out vmcnt(0) every column)
+  cplx* hh = AQC_S3_HH_SGPR ? uniform_ptr(j.work) : j.work;
+  if constexpr (TRI) {
+    tri::S3Ctx cx;
+    cx.C = C;
+    cx.hh = uniform_ptr(j.work);
+    cx.scratch = uniform_ptr(j.work + tri::kScratchOff);
+    cx.th = th;
+    cx.M = M;
+    cx.L = L;
+    cx.tr = tr;
+    const int kend = C - 1;
+    tri::s3_stage<2, 1024>(cx, 0, kend < 64 ? kend : 64, 2);
+    if (kend > 64) tri::s3_stage<1, 1024>(cx, 64, kend, 1);
+    {  // d, e, tau from the stages' LDS to the body's arrays
+      using Map = tri::TriLds<1024>;
+      const double* dT = reinterpret_cast<const double*>(xbuf + Map::kD);
+      const double* eT = reinterpret_cast<const double*>(xbuf + Map::kE);
+      const cplx* tT = xbuf + Map::kTau + 1;
+      for (int i = tid; i < C; i += 1024) {
+        s_d[i] = dT[i];
+        if (i < C - 1) {
+          s_e[i] = eT[i];
+          s_tau[i] = tT[i];
+        }
+      }
+      __syncthreads();
+    }
+  } else {
   // ---- S3: tridiagonalisation (zhetd2, lower), one barrier per column ----
   // Reflector k (v_{k+1} = 1, p = tau G^(k) v, a2 = -tau (p^H v) / 2, w = p + a2 v,
   // G^(k+1) = G^(k) - v w^H - w v^H on the trailing block) reaches the registers one phase late,
@@ -422,9 +486,6 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
   ldbl* dS = (ldbl*)(lb + 2114);  // [128] d_k
   lcplx* ktp = lb + 2178;    // [2] p^H v partials of the last p / v pass (rows 0-63, 64-127)
   lcplx* scal = lb + 2180;   // reflector k's 1 / (alpha - beta), tau / (alpha - beta); s of k - 1
-  // reflector k at hh[k (2C - k - 1) / 2 + (row - k - 1)].  The base is uniform: moved to SGPRs
-  // (as a VGPR pair it was spilled, and phase B's scratch reload waited out vmcnt(0) every column)
-  cplx* hh = AQC_S3_HH_SGPR ? uniform_ptr(j.work) : j.work;
   // "reflector -1": none, and column 0 of G as z (s = 0)
   if (tid == 0) {
     tauS[-1] = aqc::cmk(0, 0);
@@ -677,6 +738,7 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
   if (AQC_S3_DIAG && tid == 832) {
     atomicAdd(&g_gram_ticks[10], t_c);
   }
+  }  // (!TRI: the full-matrix S3)
   tick(1);
   // ---- S4: top-K eigenvalues of T by multisection ----
   if (wave == 0) {  // Gershgorin interval, ||T||, e^2 and the (d, e^2) pairs: two rows per lane
@@ -1138,6 +1200,10 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
   }
   tick(5);
   return true;
+}
+
+__device__ __forceinline__ bool gram_svd_body(const TwoSiteJob& j) {
+  return j.gram == 2 ? gram_svd_body_t<true>(j) : gram_svd_body_t<false>(j);
 }
 
 __global__ __launch_bounds__(1024) void k_svd_gram(const TwoSiteJob* __restrict__ jobs) {

@@ -52,6 +52,10 @@ constexpr int kLdsComplex = 4616;
 constexpr int kLdsBytes = kLdsComplex * 16;
 constexpr size_t kScratch = 8192;  // complex offset of the global scratch in j.work (reflectors below)
 
+// (TriLds, the LDS map per workgroup size: svd_gram.h)
+static_assert(TriLds<256>::kVec == kVec && TriLds<256>::kD == kD && TriLds<256>::kE == kE && TriLds<256>::kTau == kTau,
+              "the 256-thread LDS map");
+
 #if defined(__HIP_DEVICE_COMPILE__)
 using lcplx = __attribute__((address_space(3))) cplx;
 using ldbl = __attribute__((address_space(3))) double;
@@ -64,32 +68,36 @@ using ldbl2 = double2;
 using lint = int;
 #endif
 
-__device__ __forceinline__ int tri_cum(int c) { return c * (32 - c); }
-// first grid entry of row block R (entries of TR complex): 32 - R / 2 entries per row block
+// NB row blocks of height TR over the trailing S = NB TR rows (NB = 32 at 256 threads, 64 at
+// 1024): column block c (width 2 TR) holds tiles R = 2c + 1 .. NB - 1
+template <int NB>
+__device__ __forceinline__ int tri_cum(int c) { return c * (NB - c); }
+// first grid entry of row block R (entries of TR complex): NB - R / 2 entries per row block
+template <int NB>
 __device__ __forceinline__ int tri_off(int R) {
   const int m = R >> 1, e = R & 1;
-  return 64 * m - m * (m - 1) + e * (32 - m);
+  return 2 * NB * m - m * (m - 1) + e * (NB - m);
 }
 
-// Lane t's work in a stage of tile height TR (width 2 TR, trailing size 32 TR): tile (R, Cb) and
-// up to two elements of the even diagonal blocks (local row / col, -1: none); last = the lane's
-// last live stage-local column.
-template <int TR>
+// Lane t's work in a stage of tile height TR (width 2 TR, trailing size NB TR) on NT threads:
+// tile (R, Cb) and up to two elements of the even diagonal blocks (local row / col, -1: none);
+// last = the lane's last live stage-local column.
+template <int TR, int NT>
 __device__ __forceinline__ void tri_map(int t, int& R, int& Cb, int (&dr)[2], int (&dc)[2], int& last) {
-  constexpr int TC = 2 * TR, Q = TR * TR;
+  constexpr int TC = 2 * TR, Q = TR * TR, NB = NT == 256 ? 32 : 64;
   int c = 0;
-  while (c < 15 && tri_cum(c + 1) <= t) ++c;
+  while (c < NB / 2 - 1 && tri_cum<NB>(c + 1) <= t) ++c;
   Cb = c;
-  R = 2 * c + 1 + (t - tri_cum(c));
+  R = 2 * c + 1 + (t - tri_cum<NB>(c));
   last = TC * Cb + (R == 2 * Cb + 1 ? TR : TC) - 1;
   dr[0] = dc[0] = dr[1] = dc[1] = -1;
   int prev = -Q, ovf = 0;
-  for (int B = 0; B < 16; ++B) {
-    int a = (tri_cum(B) + Q - 1) / Q * Q;
+  for (int B = 0; B < NB / 2; ++B) {
+    int a = (tri_cum<NB>(B) + Q - 1) / Q * Q;
     a = a > prev + Q ? a : prev + Q;
     int slot = 0;
-    if (a + Q > 256) {  // no room left among the tiles that outlive it: wave 3's second slot
-      a = 192 + Q * ovf++;
+    if (a + Q > NT) {  // no room left among the tiles that outlive it: the last wave's second slot
+      a = NT - 64 + Q * ovf++;
       slot = 1;
     } else {
       prev = a;
@@ -120,20 +128,32 @@ __device__ __forceinline__ int wave_max_i(int v) {
   return __builtin_amdgcn_readfirstlane(v);
 }
 
-struct S3Ctx {
-  int C;               // matrix size
-  cplx* hh;            // packed reflectors (global, SGPR)
-  cplx* scratch;       // repack scratch (global)
-  const cplx* th;      // theta' (S1)
-  int M, L, tr;        // X = theta' (L x C) or its conjugate transpose
-};
+// sum of the NW waves' p^H v partials (LDS broadcasts)
+template <int NW>
+__device__ __forceinline__ cplx ktp_sum(const lcplx* ktp) {
+  cplx t[4] = {aqc::cmk(0, 0), aqc::cmk(0, 0), aqc::cmk(0, 0), aqc::cmk(0, 0)};
+#pragma unroll
+  for (int w = 0; w < NW; ++w) t[w & 3] = aqc::cadd(t[w & 3], ktp[w]);
+  return aqc::cadd(aqc::cadd(t[0], t[1]), aqc::cadd(t[2], t[3]));
+}
 
-// One stage of the tridiagonalisation: columns k0 .. k1 - 1 with tiles of height TR.  first: the
-// tiles are formed from X (S1); otherwise they are loaded from the repack scratch (trailing block
-// from 128 - 32 TR).  If k1 < C - 1 the stage ends by writing the next stage's trailing block to
-// the scratch; otherwise it forms d_{C-1}.
-template <int TR>
-__device__ __noinline__ void s3_stage(const S3Ctx& cx_in, int k0, int k1, bool first) {
+// (S3Ctx: svd_gram.h, where gram_svd_body<true> calls the stages at 1024 threads)
+
+// G[a][b] (a <= b) in gram_svd_body's packed LDS copy of the upper triangle (its S2): block (0, 1)
+// square (row stride 65), then the packed upper triangles of the diagonal 64 x 64 blocks
+__device__ __forceinline__ int gsq_index(int a, int b) {
+  if (b < 64) return 64 * 65 + b * (b + 1) / 2 + a;
+  if (a >= 64) return 64 * 65 + 2080 + (b - 64) * (b - 63) / 2 + (a - 64);
+  return a * 65 + (b - 64);
+}
+
+// One stage of the tridiagonalisation on NT threads: columns k0 .. k1 - 1 with tiles of height TR
+// over the trailing NB TR rows.  mode 0 (256 threads): the tiles are formed from X (S1); 1: loaded
+// from the repack scratch (trailing block from 128 - NB TR); 2 (1024 threads, the first stage):
+// from gram_svd_body's packed LDS copy of G (gsq_index).  If k1 < C - 1 the stage ends by writing
+// the next stage's trailing block to the scratch; otherwise it forms d_{C-1}.
+template <int TR, int NT>
+__device__ __noinline__ void s3_stage(const S3Ctx& cx_in, int k0, int k1, int mode) {
   // (arguments arrive in VGPRs: the uniform ones back to SGPRs, so the column loop and its tests
   // are scalar)
   S3Ctx cx;
@@ -146,36 +166,38 @@ __device__ __noinline__ void s3_stage(const S3Ctx& cx_in, int k0, int k1, bool f
   cx.tr = __builtin_amdgcn_readfirstlane(cx_in.tr);
   k0 = __builtin_amdgcn_readfirstlane(k0);
   k1 = __builtin_amdgcn_readfirstlane(k1);
-  first = __builtin_amdgcn_readfirstlane((int)first) != 0;
-  constexpr int TC = 2 * TR, S = 32 * TR, GPR = 256 / S;
+  mode = __builtin_amdgcn_readfirstlane(mode);
+  constexpr int NB = NT == 256 ? 32 : 64, NW = NT / 64;
+  constexpr int TC = 2 * TR, S = NB * TR, GPR = NT / S;
+  using Map = TriLds<NT>;
   extern __shared__ double2 xbuf[];
   lcplx* lb = (lcplx*)xbuf;
   asm volatile("" : "+s"(lb));
-  lcplx* grid = lb + kGrid;
-  lcplx* vec = lb + kVec;
-  lcplx* gk1b = lb + kGk1;
-  lcplx* scal = lb + kScal;
-  lcplx* ktp = lb + kKtp;
-  ldbl* dS = (ldbl*)(lb + kD);
-  ldbl* eS = (ldbl*)(lb + kE);
-  lcplx* tauS = lb + kTau + 1;  // tauS[-1] = 0
+  lcplx* grid = lb + Map::kGrid;
+  lcplx* vec = lb + Map::kVec;
+  lcplx* gk1b = lb + Map::kGk1;
+  lcplx* scal = lb + Map::kScal;
+  lcplx* ktp = lb + Map::kKtp;
+  ldbl* dS = (ldbl*)(lb + Map::kD);
+  ldbl* eS = (ldbl*)(lb + Map::kE);
+  lcplx* tauS = lb + Map::kTau + 1;  // tauS[-1] = 0
   const int C = cx.C;
   const int base = 128 - S;
   const int tid = fresh_tid(), lane = tid & 63, wave = tid >> 6;
   int R, Cb, dr[2], dc[2], last;
-  tri_map<TR>(tid, R, Cb, dr, dc, last);
+  tri_map<TR, NT>(tid, R, Cb, dr, dc, last);
   const int wlast = wave_max_i(last);  // (uniform)
   const bool half = R == 2 * Cb + 1;
   const int rl0 = base + TR * R, cl0 = base + TC * Cb;  // global first row / column of the tile
   // the grid entries this lane writes (complex units)
-  const int o_row = TR * (tri_off(R) + Cb);
-  const int o_clo = TR * (tri_off(2 * Cb) + R - Cb - 1);
-  const int o_chi = TR * (tri_off(2 * Cb + 1) + R - Cb);
+  const int o_row = TR * (tri_off<NB>(R) + Cb);
+  const int o_clo = TR * (tri_off<NB>(2 * Cb) + R - Cb - 1);
+  const int o_chi = TR * (tri_off<NB>(2 * Cb + 1) + R - Cb);
   int o_d[2];
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
     const int B = dr[s] >= 0 ? dr[s] / (2 * TR) : 0;
-    o_d[s] = dr[s] >= 0 ? TR * (tri_off(2 * B) + 31 - B) + (dr[s] - 2 * B * TR) : 0;
+    o_d[s] = dr[s] >= 0 ? TR * (tri_off<NB>(2 * B) + NB - 1 - B) + (dr[s] - 2 * B * TR) : 0;
   }
   const int gdr0 = base + dr[0], gdc0 = base + dc[0], gdr1 = base + dr[1], gdc1 = base + dc[1];
   cplx g[TR][TC];
@@ -191,7 +213,9 @@ __device__ __noinline__ void s3_stage(const S3Ctx& cx_in, int k0, int k1, bool f
     }
   };
   unsigned long long t_s1 = 0, t_io = 0;
-  if (first) {
+  if (mode != 1) {
+    if constexpr (NT == 256) {
+      if (mode == 0) {
     // ---- S1: G = X^H X into the tiles and diagonal elements: X staged through the LDS in chunks
     // of 8 rows, column c at position (c & 3) 32 + (c >> 2) (lanes with consecutive R read
     // consecutive complex), double-buffered with the next chunk's global loads in flight
@@ -258,9 +282,29 @@ __device__ __noinline__ void s3_stage(const S3Ctx& cx_in, int k0, int k1, bool f
       if (more) stash((ch + 1) & 1, xn);
       __syncthreads();
     }
+      }
+    }
+    if (mode == 2) {
+      // ---- G from gram_svd_body's packed LDS copy of its upper triangle (trailing block = all of G)
+      auto ldq = [&](int r, int c) {
+        cplx v = aqc::cmk(0, 0);
+        if (r < C && c < C) {
+          v = lb[r <= c ? gsq_index(r, c) : gsq_index(c, r)];
+          if (r > c) v.y = -v.y;
+        }
+        return v;
+      };
+#pragma unroll
+      for (int i = 0; i < TR; ++i)
+#pragma unroll
+        for (int jj = 0; jj < TC; ++jj) g[i][jj] = ldq(rl0 + i, cl0 + jj);
+      if (dr[0] >= 0) gd[0] = ldq(gdr0, gdc0);
+      if (dr[1] >= 0) gd[1] = ldq(gdr1, gdc1);
+      __syncthreads();  // (the vectors below overwrite the packed G)
+    }
     // VEC: zeros, then "reflector -1": z = column 0 below the diagonal
-    for (int e = tid; e < 3 * 136; e += 256) vec[e] = aqc::cmk(0, 0);
-    if (tid < 4) ktp[tid] = aqc::cmk(0, 0);
+    for (int e = tid; e < 3 * 136; e += NT) vec[e] = aqc::cmk(0, 0);
+    if (tid < NW) ktp[tid] = aqc::cmk(0, 0);
     if (tid == 0) tauS[-1] = aqc::cmk(0, 0);
     __syncthreads();
     if (cl0 == 0) {
@@ -288,14 +332,14 @@ __device__ __noinline__ void s3_stage(const S3Ctx& cx_in, int k0, int k1, bool f
     if (dr[1] >= 0) gd[1] = ld(gdr1, gdc1);
   }
   __syncthreads();
-  lap(first ? t_s1 : t_io);
+  lap(mode != 1 ? t_s1 : t_io);
   // ---- the columns ----
   for (int k = k0; k < k1; ++k) {
     const int kl = k - base;
     // reflector k - 1's a2 and s (every wave, uniform: LDS broadcasts)
     cplx a2, s;
     {
-      const cplx kt = aqc::cadd(aqc::cadd(ktp[0], ktp[1]), aqc::cadd(ktp[2], ktp[3]));
+      const cplx kt = ktp_sum<NW>(ktp);
       a2 = aqc::cscale(aqc::cmul(tauS[k - 1], kt), -0.5);
       const cplx pk = vec[3 * k + 1];
       s = aqc::cmk(pk.x + 2.0 * a2.x, -pk.y);
@@ -369,7 +413,7 @@ __device__ __noinline__ void s3_stage(const S3Ctx& cx_in, int k0, int k1, bool f
       // the even diagonal blocks: one or two elements, row products summed over the TR lanes of a row
 #pragma unroll
       for (int sl = 0; sl < 2; ++sl) {
-        if (sl == 1 && wave != 3) continue;  // (uniform: the second slot exists in wave 3 only)
+        if (sl == 1 && wave != NW - 1) continue;  // (uniform: the second slot exists in the last wave only)
         const bool act = dr[sl] >= 0;
         const int rd = act ? (sl ? gdr1 : gdr0) : 128, cd = act ? (sl ? gdc1 : gdc0) : 128;
         const cplx v = vec[3 * rd], p = vec[3 * rd + 1];
@@ -429,11 +473,11 @@ __device__ __noinline__ void s3_stage(const S3Ctx& cx_in, int k0, int k1, bool f
       int t = tid;
       asm volatile("" : "+v"(t));
       const int rloc = t / GPR, h = t % GPR;
-      const int Rr = rloc / TR, ir = rloc % TR, n = 32 - (Rr >> 1);
-      const lcplx* gl = grid + TR * tri_off(Rr) + ir;
+      const int Rr = rloc / TR, ir = rloc % TR, n = NB - (Rr >> 1);
+      const lcplx* gl = grid + TR * tri_off<NB>(Rr) + ir;
       // (a fixed count of independent loads, clamped and masked: issued together instead of one
       // LDS round trip per contribution)
-      constexpr int NO = (32 + GPR - 1) / GPR;
+      constexpr int NO = (NB + GPR - 1) / GPR;
       cplx part[4] = {aqc::cmk(0, 0), aqc::cmk(0, 0), aqc::cmk(0, 0), aqc::cmk(0, 0)};
 #pragma unroll
       for (int u = 0; u < NO; ++u) {
@@ -493,7 +537,7 @@ __device__ __noinline__ void s3_stage(const S3Ctx& cx_in, int k0, int k1, bool f
     const int kk = C - 1;
     cplx a2;
     {
-      const cplx kt = aqc::cadd(aqc::cadd(ktp[0], ktp[1]), aqc::cadd(ktp[2], ktp[3]));
+      const cplx kt = ktp_sum<NW>(ktp);
       a2 = aqc::cscale(aqc::cmul(tauS[kk - 1], kt), -0.5);
     }
     const cplx v = vec[3 * kk], p = vec[3 * kk + 1];
@@ -563,9 +607,9 @@ __device__ __noinline__ bool gram256_body(const TwoSiteJob& j) {
   cx.L = L;
   cx.tr = tr;
   const int kend = C - 1;
-  s3_stage<4>(cx, 0, kend < 64 ? kend : 64, true);
-  if (kend > 64) s3_stage<2>(cx, 64, kend < 96 ? kend : 96, false);
-  if (kend > 96) s3_stage<1>(cx, 96, kend, false);
+  s3_stage<4, 256>(cx, 0, kend < 64 ? kend : 64, 0);
+  if (kend > 64) s3_stage<2, 256>(cx, 64, kend < 96 ? kend : 96, 1);
+  if (kend > 96) s3_stage<1, 256>(cx, 96, kend, 1);
   tick(1);
   // ---- S4: top-K eigenvalues of T by multisection (as gram_svd_body) ----
   if (wave == 0) {

@@ -132,7 +132,9 @@ int aqc_mps_set_jacobi_stop(double tiny_t);
 /* Two-site SVD at 2 chi = 128: gram = 1 (default) tries the Gram / tridiagonal path first (G = X^H X
    on the matrix cores, Householder tridiagonalisation, multisection, inverse iteration; taken when
    the kept count K = min(2 chi, max_chi) <= 64 and lambda_K > 1e-9 lambda_1, else the register
-   Jacobi runs), gram = 0 the register Jacobi only.  debug_max_chi: max_chi of aqc_svd_debug. */
+   Jacobi runs), gram = 0 the register Jacobi only, gram = 2 the Gram path with the lower-triangle
+   tridiagonalisation (svd_tri.h's stages on the 1024-thread workgroup).  debug_max_chi: max_chi of
+   aqc_svd_debug. */
 int aqc_mps_set_svd_path(int gram, int debug_max_chi);
 /* Diagnostics: shader-clock ticks of the Gram path's phases since the last call (then reset);
    out[12]: Gram GEMM, tridiagonalisation, eigenvalues, eigenvectors, back-transformation, output,
@@ -204,7 +206,9 @@ int aqc_entanglement_measures(const double* rdms, int count, int method, double*
 
 /* Diagnostics: one register-resident Jacobi launch with pivoted-QR preconditioning (variant 2)
    on theta (m x n column-major complex, m, n even <= 128, as the two-site update builds it), or
-   the Gram / tridiagonal path (variant 7; Jacobi fallback inside the kernel; same output contract).
+   the Gram / tridiagonal path (variant 7; Jacobi fallback inside the kernel; same output contract;
+   variant 8: its 256-thread form, declines reported in the flags; variant 9: the 1024-thread form
+   with the lower-triangle tridiagonalisation).
    w_out receives min(m,n) columns of length min(m,n); sig_out their
    norms; perm_out (optional) the pivot order when stop_after_qr (then w_out holds X = R^H
    unsorted).  stop_after_qr = 2 also writes the QR phase's shader-clock ticks to sig_out[0..3]

@@ -30,7 +30,7 @@ def _gram_expectation(svd_logs, max_chi):
     return calls, take, decline
 
 
-@pytest.mark.parametrize("chain", [1024, 256])
+@pytest.mark.parametrize("chain", [1024, 256, "tri1024"])
 @pytest.mark.parametrize("kind", ["near-product", "random"])
 def test_bench_overlap_workload_fused_chain_vs_oracle(kind, chain):
     """10 states x 4 distances = 40 evaluations in one apply + sort batch (k_chain), every one
@@ -60,7 +60,10 @@ def test_bench_overlap_workload_fused_chain_vs_oracle(kind, chain):
     pipelined = kind == "random"
     _lib.gram_stats()  # reset
     L = _lib.lib()
-    _lib.check(L.aqc_mps_set_chain_threads(chain))
+    # tri1024: k_chain with the lower-triangle tridiagonalisation in its Gram SVD (svd path 2)
+    _lib.check(L.aqc_mps_set_chain_threads(256 if chain == 256 else 1024))
+    if chain == "tri1024":
+        _lib.check(L.aqc_mps_set_svd_path(2, 64))
     try:
         apply_batch(work, ops, sort=True, wait=not pipelined)
         ov = overlap_zero_batch(work)
@@ -68,6 +71,7 @@ def test_bench_overlap_workload_fused_chain_vs_oracle(kind, chain):
             check_batch(work)
     finally:
         _lib.check(L.aqc_mps_set_chain_threads(1024))
+        _lib.check(L.aqc_mps_set_svd_path(1, 64))
     gram = _lib.gram_stats()
     logs = []
     nontrivial = 0

@@ -187,16 +187,18 @@ def test_jacobi_degenerate_clusters(n, kind):
 
 
 # ---- the same path on 256 threads (aqc_svd_debug variant 8, svd_tri.h: k_chain256's SVD) --------
+@pytest.mark.parametrize("variant", [8, 9], ids=["tri256", "tri1024"])
 @pytest.mark.parametrize("m,n", [(128, 128), (128, 96), (96, 128), (128, 72), (80, 80), (128, 40), (66, 128)])
-def test_gram256_vs_numpy_and_1024(m, n):
-    """The two-states-per-CU layout (lower-triangle tiles in three stages, two barriers per column,
-    S5 in two batches) against numpy and against the 1024-thread body on the same theta: sigma to
-    1e-12 sigma_1, the kept subspace to 1e-10, orthonormal to 1e-11, sigma equal to the 1024-thread
-    path's within 1e-13 sigma_1."""
+def test_gram256_vs_numpy_and_1024(m, n, variant):
+    """The lower-triangle tridiagonalisation (tiles in stages, two barriers per column) -- on 256
+    threads with S5 in two batches (variant 8, k_chain256's SVD) and on the 1024-thread body
+    (variant 9, j.gram = 2) -- against numpy and against the full-matrix 1024-thread body on the
+    same theta: sigma to 1e-12 sigma_1, the kept subspace to 1e-10, orthonormal to 1e-11, sigma
+    equal to the full-matrix path's within 1e-13 sigma_1."""
     c = min(m, n)
     theta = _spectrum_theta(m, n, 0.93 ** np.arange(c), 11 + m + n)
-    w8, sig8, _, sw8 = _run(theta, 8)
-    assert sw8 == 1, "the 256-thread Gram path declined"
+    w8, sig8, _, sw8 = _run(theta, variant)
+    assert sw8 == 1, "the lower-triangle Gram path declined"
     w7, sig7, _, _ = _run(theta, 7)
     K = min(64, c)
     x = theta if m >= n else theta.conj().T

@@ -25,6 +25,8 @@ for q in src_q:
     d.load_aer(q)
     srcs.append(d)
 L = _lib.lib()
+svd_path = int(os.environ.get("AQC_SVD_PATH", "1"))  # 2: the lower-triangle S3 in the 1024-thread body
+_lib.check(L.aqc_mps_set_svd_path(svd_path, 64))
 rng = np.random.default_rng(5)
 for ns in sizes:
     work = [DeviceMPS(n, chi, 1e-16, chi) for _ in range(ns)]
@@ -50,7 +52,7 @@ for ns in sizes:
     _lib.check(L.aqc_svd_gram_ticks(_lib.ptr(g)))
     upd = (2 * (dist - 1) + 1) * reps * ns
     launch_ms = tq["ms"] / max(tq["launches"], 1)
-    row = {"chain": os.environ.get("AQC_CHAIN", "256"), "states": ns, "launch_ms": launch_ms,
+    row = {"chain": os.environ.get("AQC_CHAIN", "1024"), "svd_path": svd_path, "states": ns, "launch_ms": launch_ms,
            "us_per_update_wall": 1e3 * launch_ms * reps / upd,
            "ticks_per_update": {k: round(float(v) / upd) for k, v in zip(("theta", "svd", "rank", "split", "one_site"), t)},
            "gram_ticks_per_svd": {k: round(float(g[i]) / upd) for k, i in
