@@ -678,8 +678,13 @@ __global__ __launch_bounds__(CP / 2 * LPG) void k_jacobi_reg(const TwoSiteJob* _
 }
 
 #include "svd_gram.h"
-// two-site SVDs at 2 chi = 128 try the Gram / tridiagonal path first (aqc_mps_set_svd_path)
-int g_svd_gram = 1;
+// two-site SVDs at 2 chi = 128 try the Gram / tridiagonal path first (aqc_mps_set_svd_path; the
+// initial value from AQC_SVD_PATH = 0, 1 or 2, default 1)
+int g_svd_gram = [] {
+  const char* e = std::getenv("AQC_SVD_PATH");
+  const int v = e ? std::atoi(e) : 1;
+  return v >= 0 && v <= 2 ? v : 1;
+}();
 int g_debug_max_chi = 64;  // aqc_svd_debug's max_chi (the Gram path keeps K = min(C, max_chi))
 
 // 2 chi = 128: the Gram path with the register Jacobi (16-lane groups, 1024 threads) as its
