@@ -221,7 +221,7 @@ template <int TR, int NT>
 __device__ __noinline__ void s3_stage(const S3Ctx& cx_in, int k0, int k1, int mode);
 constexpr size_t kScratchOff = 8192;  // (= tri::kScratch)
 // The tridiagonalisation's LDS map (complex units) per workgroup size: at 256 threads svd_tri.h's
-// constants (kVec ...); at 1024 threads a grid of up to 6176 entries (TR = 2, NB = 64), then the
+// constants (kVec ...); at 1024 threads a grid of up to 6208 entries (TR = 2, NB = 64), then the
 // vectors, scalars, 16 waves' p^H v and d / e / tau of its own (copied to the body's arrays
 // after S3)
 template <int NT>
@@ -231,8 +231,8 @@ struct TriLds {
 };
 template <>
 struct TriLds<1024> {
-  static constexpr int kGrid = 0, kVec = 6176, kGk1 = 6584, kScal = 6712, kKtp = 6716, kD = 6736, kE = 6800,
-                       kTau = 6864, kEnd = 6994;
+  static constexpr int kGrid = 0, kVec = 6208, kGk1 = 6616, kScal = 6744, kKtp = 6748, kD = 6768, kE = 6832,
+                       kTau = 6896, kEnd = 7026;
 };
 }  // namespace tri
 

@@ -55,6 +55,14 @@ constexpr size_t kScratch = 8192;  // complex offset of the global scratch in j.
 // (TriLds, the LDS map per workgroup size: svd_gram.h)
 static_assert(TriLds<256>::kVec == kVec && TriLds<256>::kD == kD && TriLds<256>::kE == kE && TriLds<256>::kTau == kTau,
               "the 256-thread LDS map");
+// grid sizes: TR x tri_off<NB>(NB) entries (NB - R / 2 per row block R) -- 4 x 784 at 256 threads,
+// 2 x 3104 at 1024 -- below each map's vectors; the 1024-thread map inside the chain's dynamic LDS
+static_assert(4 * (2 * 32 * 16 - 16 * 15) <= TriLds<256>::kVec, "256-thread grid");
+static_assert(2 * (2 * 64 * 32 - 32 * 31) <= TriLds<1024>::kVec, "1024-thread grid");
+static_assert(TriLds<1024>::kVec + 3 * 136 <= TriLds<1024>::kGk1 && TriLds<1024>::kGk1 + 128 <= TriLds<1024>::kScal &&
+                  TriLds<1024>::kKtp + 16 <= TriLds<1024>::kD && TriLds<1024>::kD + 64 <= TriLds<1024>::kE &&
+                  TriLds<1024>::kE + 64 <= TriLds<1024>::kTau && TriLds<1024>::kEnd * 16 <= kChainLdsBytes,
+              "1024-thread LDS map");
 
 #if defined(__HIP_DEVICE_COMPILE__)
 using lcplx = __attribute__((address_space(3))) cplx;
