@@ -120,12 +120,14 @@ __device__ __forceinline__ void tri_map(int t, int& R, int& Cb, int (&dr)[2], in
   }
 }
 
-// sum over aligned groups of N lanes (N = 1, 2, 4, 8)
+// sum over aligned groups of N lanes (N = 1, 2, 4, 8, 16)
 template <int N>
 __device__ __forceinline__ double group_sum_n(double v) {
+  static_assert(N == 1 || N == 2 || N == 4 || N == 8 || N == 16, "group size");
   if constexpr (N == 2) return v + aqc::dpp_perm<0xB1>(v);
   else if constexpr (N == 4) return aqc::row_sum4(v);
   else if constexpr (N == 8) return aqc::row_sum8(v);
+  else if constexpr (N == 16) return aqc::row_sum16(v);
   else return v;
 }
 
