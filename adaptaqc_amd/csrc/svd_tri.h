@@ -97,7 +97,7 @@ __device__ __forceinline__ void tri_map(int t, int& R, int& Cb, int (&dr)[2], in
   while (c < NB / 2 - 1 && tri_cum<NB>(c + 1) <= t) ++c;
   Cb = c;
   R = 2 * c + 1 + (t - tri_cum<NB>(c));
-  last = TC * Cb + (R == 2 * Cb + 1 ? TR : TC) - 1;
+  last = TC * Cb + TC - 1;  // (a half tile's right half is the odd diagonal block: live to its last column)
   dr[0] = dc[0] = dr[1] = dc[1] = -1;
   int prev = -Q, ovf = 0;
   for (int B = 0; B < NB / 2; ++B) {
