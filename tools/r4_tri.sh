@@ -12,7 +12,8 @@ step() {
   echo "$name rc=$rc" >> gpurun_out/tri_steps.txt
   return $rc
 }
-step tri_svd 300 python3 -u -m pytest tests/test_gpu_svd.py -x -v --timeout 120 --timeout-method thread -k "gram256" || exit $?
+step tri_diag 120 python3 tools/tri_diag.py || exit $?
+step tri_svd 300 python3 -u -m pytest tests/test_gpu_svd.py -x -v --timeout 120 --timeout-method thread -k "gram" || exit $?
 step tri_headline 400 python3 -u -m pytest tests/test_gpu_headline.py -x -v --timeout 300 --timeout-method thread || exit $?
 step tri_probe 300 env AQC_SVD_PATH=2 python3 tools/chain256_probe.py 25 32,256 || exit $?
 step full_probe 300 python3 tools/chain256_probe.py 25 32,256 || exit $?
