@@ -912,14 +912,24 @@ __device__ unsigned long long g_chain_ticks[5];
 // LDS-bound), then the gate mix in registers and coalesced theta writes (lanes along l).  Every
 // sub-group runs the same m steps, so the barriers pair up.  (An MFMA form needs more than the
 // chain's 128 VGPRs per lane: four P's of a quadrant are 16 accumulator tiles.)
-constexpr int kThetaLds = 2 * 32 * 9 + 2 * 8 * 33;  // complex per sub-group
+// m is staged KCH at a time (AQC_THETA_CH: 8, or 16 with A's rows XOR-swizzled instead of padded,
+// half the barriers and twice the loads in flight per step)
+#ifndef AQC_THETA_CH
+#define AQC_THETA_CH 8
+#endif
+constexpr int kThetaCh = AQC_THETA_CH;
+static_assert(kThetaCh == 8 || kThetaCh == 16, "theta chunk");
+constexpr int kThetaAPitch = kThetaCh == 8 ? 9 : 16;
+constexpr int kThetaLds = 2 * 32 * kThetaAPitch + 2 * kThetaCh * 33;  // complex per sub-group
 static_assert(4 * kThetaLds * 16 <= kChainLdsBytes, "theta staging exceeds the chain's LDS");
+__device__ __forceinline__ int theta_acol(int row, int mm) { return kThetaCh == 8 ? mm : mm ^ (row & 15); }
 __device__ __forceinline__ void chain_theta(const TwoSiteJob& j) {
   extern __shared__ double2 xbuf[];
   const int tid = fresh_tid(), sg = tid >> 8, lt = tid & 255;
+  constexpr int KCH = kThetaCh;
   cplx* base = xbuf + sg * kThetaLds;
-  cplx (*As)[32][9] = reinterpret_cast<cplx (*)[32][9]>(base);
-  cplx (*Bs)[8][33] = reinterpret_cast<cplx (*)[8][33]>(base + 2 * 32 * 9);
+  cplx (*As)[32][kThetaAPitch] = reinterpret_cast<cplx (*)[32][kThetaAPitch]>(base);
+  cplx (*Bs)[KCH][33] = reinterpret_cast<cplx (*)[KCH][33]>(base + 2 * 32 * kThetaAPitch);
   const int chl = j.dims[0], chm = j.dims[1], chr = j.dims[2];
   const int cap = j.cap;
   const size_t half = (size_t)cap * cap;
@@ -946,19 +956,19 @@ __device__ __forceinline__ void chain_theta(const TwoSiteJob& j) {
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int jj = 0; jj < 2; ++jj) acc[q][i][jj] = aqc::cmk(0, 0);
-  for (int m0 = 0; m0 < chm; m0 += 8) {
+  for (int m0 = 0; m0 < chm; m0 += KCH) {
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int e = lt + 256 * u, s = e >> 8;
-      {  // A: 8 consecutive m of one row per 8 lanes
-        const int row = (e >> 3) & 31, mm = e & 7, l = l0 + row, m = m0 + mm;
+    for (int u = 0; u < KCH / 4; ++u) {
+      const int e = lt + 256 * u, s = e / (32 * KCH);
+      {  // A: KCH consecutive m of one row per KCH lanes
+        const int row = (e / KCH) & 31, mm = e % KCH, l = l0 + row, m = m0 + mm;
         cplx a = aqc::cmk(0, 0);
         if (active && l < chl && m < chm)
           a = aqc::cscale(aqc::ldg(gp + s * half + (size_t)l * cap + m), aqc::ldg(llp + l) * aqc::ldg(lmp + m));
-        As[s][row][mm] = a;
+        As[s][row][theta_acol(row, mm)] = a;
       }
       {  // B: 32 consecutive r of one row per 32 lanes
-        const int mm = (e >> 5) & 7, col = e & 31, m = m0 + mm, r = r0 + col;
+        const int mm = (e >> 5) % KCH, col = e & 31, m = m0 + mm, r = r0 + col;
         cplx b = aqc::cmk(0, 0);
         if (active && m < chm && r < chr) b = aqc::cscale(aqc::ldg(gq + s * half + (size_t)m * cap + r), aqc::ldg(lrp + r));
         Bs[s][mm][col] = b;
@@ -967,13 +977,13 @@ __device__ __forceinline__ void chain_theta(const TwoSiteJob& j) {
     __syncthreads();
     if (active) {
 #pragma unroll 2
-      for (int mm = 0; mm < 8; ++mm) {
+      for (int mm = 0; mm < KCH; ++mm) {
         cplx av[2][2], bv[2][2];
 #pragma unroll
         for (int s = 0; s < 2; ++s)
 #pragma unroll
           for (int i = 0; i < 2; ++i) {
-            av[s][i] = As[s][tx + 16 * i][mm];
+            av[s][i] = As[s][tx + 16 * i][theta_acol(tx + 16 * i, mm)];
             bv[s][i] = Bs[s][mm][ty + 16 * i];
           }
 #pragma unroll

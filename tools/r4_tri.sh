@@ -22,3 +22,5 @@ step bench_full 400 python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --n
 step sv_tests 400 python3 -u -m pytest tests/test_gpu_sv.py tests/test_gpu_binding.py -x -q --timeout 200 --timeout-method thread || exit $?
 step cfg2_s4 300 python3 tools/configs_bench.py --configs 2 || exit $?
 step cfg2_s3 300 env AQC_SV_SLOTS=3 python3 tools/configs_bench.py --configs 2 || exit $?
+step bench_t16 400 env AQC_LIB=$PWD/adaptaqc_amd/libaqchip_theta16.so python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-latency --no-parity || exit $?
+step bench_t8 400 python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-latency --no-parity || exit $?
