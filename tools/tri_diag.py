@@ -5,7 +5,9 @@ import sys
 
 import numpy as np
 
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests"))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
 from test_gpu_svd import _run, _spectrum_theta  # noqa: E402
 
 for m, n in ((128, 40), (128, 64), (128, 66), (128, 80), (128, 96), (128, 128)):
