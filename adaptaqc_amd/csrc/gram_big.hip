@@ -56,6 +56,8 @@ constexpr double kGbRelFloor = 1e-9;
 constexpr unsigned long long kSpinTicks = 10000000ull;  // s_memrealtime (100 MHz): 100 ms
 // the counter-wait limit in force (aqc_gb_set_spin_limit: tests force the timeout decline with 0)
 unsigned long long g_gb_spin = kSpinTicks;
+// the trailing 128 columns in one workgroup (aqc_gb_set_tail; -1: from AQC_GB_TAIL, default on)
+int g_gb_tail = -1;
 
 typedef __attribute__((address_space(1))) double gdbl;
 typedef __attribute__((address_space(1))) unsigned gu32;
@@ -231,7 +233,7 @@ __device__ __forceinline__ void zlarfg_f(cplx alpha, double xn2, cplx& tau, doub
 //             w_{k+1} conj(v), its norm below the subdiagonal (a second reduction); wave 0 alone
 //             forms reflector k + 1 (zlarfg's scalars and v into the LDS; in every wave the
 //             redundant scalar chain cost 4x its issue)
-template <int CT, int RPL>
+template <int CT, int RPL, bool TAIL>
 __global__ __launch_bounds__(1024) void k_gb_tridiag(const TwoSiteJob* __restrict__ jobs, GBArgs a, int job0) {
   constexpr int CPL = 16 / RPL, TPG = CT / CPL;
   constexpr int R = RPL * (1024 / TPG), P = CT / R;
@@ -291,10 +293,16 @@ __global__ __launch_bounds__(1024) void k_gb_tridiag(const TwoSiteJob* __restric
     cplx tau_, sc;
     double beta;
     zlarfg_f(cconj(rhoL[k + 1]), xn2, tau_, beta, sc);
+    // (one base address per lane, offsets 1 KB apart: with c = lane + 64 i kept per i, the eight
+    // addresses were hoisted out of the column loop and spilled -- a scratch reload and a full
+    // vmcnt wait per entry on the zlarfg chain)
+    const cplx* rp = rhoL + lane;
+    cplx* vp = vL[k & 1] + lane;
+    const int d0 = lane - (k + 1);
 #pragma unroll
     for (int i = 0; i < CT / 64; ++i) {
-      const int c = lane + 64 * i;
-      vL[k & 1][c] = c == k + 1 ? cmk(1, 0) : (c > k + 1 ? cmul(cconj(rhoL[c]), sc) : cmk(0, 0));
+      const int d = d0 + 64 * i;
+      vp[64 * i] = d == 0 ? cmk(1, 0) : (d > 0 ? cmul(cconj(rp[64 * i]), sc) : cmk(0, 0));
     }
     if (lane == 0) {
       s_tau = tau_;
@@ -311,7 +319,10 @@ __global__ __launch_bounds__(1024) void k_gb_tridiag(const TwoSiteJob* __restric
     if (wave == 0) reflector(0);
     __syncthreads();
   }
-  for (int k = 0; k < CT - 1; ++k) {
+  // with TAIL the loop stops at kt = CT - 128: the trailing 128 columns run in k_gb_tail
+  int kt = TAIL ? CT - 128 : CT - 1;
+  asm volatile("" : "+s"(kt));  // (opaque: a constant trip count spilled the register tile)
+  for (int k = 0; k < kt; ++k) {
     const int cur = k & 1, prv = cur ^ 1;
     // ---- the deferred update of reflector k - 1, then s = (G v_k)_r
     cplx s[RPL], xcol[RPL];  // xcol: this lane's G[r][k + 1] after the update (its publish)
@@ -425,9 +436,183 @@ __global__ __launch_bounds__(1024) void k_gb_tridiag(const TwoSiteJob* __restric
     __syncthreads();
     tmark(5);
   }
+  if constexpr (TAIL) {
+    // ---- hand-off to k_gb_tail: the trailing block (rows and columns >= kt, reflector kt - 1's
+    // update still deferred) to rows kt.. of the scratch (free until their reflectors: rows < kt
+    // hold v_0 .. v_kt-1); workgroup 0 adds v_kt-1, v_kt, w_kt-1 and reflector kt's scalars
+#pragma unroll
+    for (int u = 0; u < RPL; ++u) {
+      if (rr[u] >= kt) {
+#pragma unroll
+        for (int i = 0; i < CPL; ++i) {
+          const int c = q + TPG * i;
+          if (TPG * i + TPG - 1 >= kt && c >= kt) stg(G + (size_t)rr[u] * CT + c, A[u][i]);
+        }
+      }
+    }
+    if (g == 0) {
+      if (tid < CT) {
+        stg(xch + tid, vL[0][tid]);
+        stg(xch + CT + tid, vL[1][tid]);
+        stg(xch + 2 * CT + tid, wL[tid]);
+      }
+      if (tid == 0) {
+        stg(xch + 3 * CT, s_tau);
+        stg(xch + 3 * CT + 1, cmk(s_beta, s_dk));
+      }
+    }
+  }
   if (tick) {
     for (int i = 0; i < 5; ++i) atomicAdd(&g_gbig_ticks[i], s_tk[i]);
     atomicAdd(&g_gbig_ticks[8], s_tk[5]);
+  }
+}
+
+// ---- the last 128 columns in one workgroup: grid (njobs_in_round), 1024 threads ----
+// k_gb_tridiag stops at column kt = CT - 128 and leaves the trailing block (reflector kt - 1's
+// update still deferred) in rows kt.. of the scratch, v_kt-1, v_kt, w_kt-1 and reflector kt's
+// scalars in the exchange buffer.  Thread t holds local row t / 8, columns t % 8 + 8 i (i < 16);
+// per column the pass (as k_gb_tridiag's), p and the old row k + 1 into the LDS, one barrier; then
+// wave 0 alone (two columns per lane) forms p^H v, w, the new row k + 1, its norm and the next
+// reflector -- all reductions inside the wave -- and a second barrier.  No cross-workgroup
+// exchange: this is the part of the tridiagonalisation where the trailing block is too small to
+// pay for one.  Launched on the side stream, so a round's tails run beside the next round's
+// k_gb_tridiag.
+__device__ __forceinline__ double readlane_d(double v, int l) {
+  return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l),
+                          __builtin_amdgcn_readlane(__double2loint(v), l));
+}
+
+template <int CT>
+__global__ __launch_bounds__(1024) void k_gb_tail(const TwoSiteJob* __restrict__ jobs, GBArgs a, int job0) {
+  constexpr int NT = 128, kt = CT - NT;
+  const int jb = job0 + (int)blockIdx.x;
+  if (*(const gi32*)(a.status + jb) != 0) return;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tr = tid >> 3, tq = tid & 7;
+  const bool tick = jb == 0 && tid == 0;
+  cplx* G = a.G + (size_t)jb * CT * CT;
+  double* dd = a.d + (size_t)jb * CT;
+  double* ee = a.e + (size_t)jb * CT;
+  cplx* tt = a.tau + (size_t)jb * CT;
+  const cplx* xch = a.xch + (size_t)jb * 4 * CT;
+  __shared__ cplx vL[2][NT], wL[NT], pL[NT], roL[NT];
+  __shared__ cplx s_tau;
+  __shared__ double s_beta, s_dk;
+  __shared__ unsigned long long tk[6];  // phase ticks of job 0, thread 0 ([5]: the last mark)
+  if (tick) {
+    for (int i = 0; i < 5; ++i) tk[i] = 0;
+    tk[5] = __builtin_amdgcn_s_memtime();
+  }
+  auto tmark = [&](int ph) {
+    if (tick) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      tk[ph] += t - tk[5];
+      tk[5] = t;
+    }
+  };
+  cplx T[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) T[i] = ldg(G + (size_t)(kt + tr) * CT + kt + tq + 8 * i);
+  if (tid < NT) {
+    vL[0][tid] = ldg(xch + kt + tid);
+    vL[1][tid] = ldg(xch + CT + kt + tid);
+    wL[tid] = ldg(xch + 2 * CT + kt + tid);
+  }
+  if (tid == 0) {
+    s_tau = ldg(xch + 3 * CT);
+    const cplx bd = ldg(xch + 3 * CT + 1);
+    s_beta = bd.x;
+    s_dk = bd.y;
+  }
+  __syncthreads();
+  for (int k = kt; k < CT - 1; ++k) {
+    const int cur = k & 1, prv = cur ^ 1;
+    const int kl = k - kt, kk = kl + 1, ic = kk >> 3;
+    cplx s = cmk(0, 0), xcol = cmk(0, 0);
+    if (tr > kl) {
+      const cplx vr = vL[prv][tr], wr = wL[tr];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        if (8 * i + 7 > kl) {
+          const int c = tq + 8 * i;
+          const cplx vp = vL[prv][c], wc = wL[c], vc = vL[cur][c];
+          T[i] = csub(T[i], cadd(cmulc(vr, wc), cmulc(wr, vp)));
+          s = cfma(T[i], vc, s);
+          if (i == ic) xcol = T[i];
+        }
+      }
+    }
+    s = cmk(group_sum<8>(s.x), group_sum<8>(s.y));
+    tmark(0);
+    const cplx tau = s_tau;
+    if (tq == 0) pL[tr] = tr > kl ? cmul(tau, s) : cmk(0, 0);
+    if (tq == (kk & 7)) roL[tr] = cconj(xcol);
+    __syncthreads();
+    tmark(1);
+    if (wave == 0) {
+      if (lane == 0) {
+        stg(dd + k, s_dk);
+        stg(ee + k, s_beta);
+        stg(tt + k, tau);
+      }
+      cplx vt[2], pt[2], ro[2];
+      cplx pvp = cmk(0, 0);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int c = lane + 64 * h;
+        vt[h] = vL[cur][c];
+        pt[h] = pL[c];
+        ro[h] = roL[c];
+        pvp = cadd(pvp, cconjmul(pt[h], vt[h]));
+        if (c > kl) stg(G + (size_t)k * CT + kt + c, vt[h]);  // reflector k to row k of the scratch
+      }
+      const cplx pv = cmk(lane_sum<64>(pvp.x), lane_sum<64>(pvp.y));
+      const cplx a2 = cscale(cmul(tau, pv), -0.5);
+      const cplx wk1 = cadd(pL[kk], a2);
+      cplx rho[2];
+      double part = 0.0;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int c = lane + 64 * h;
+        const cplx wt = cfma(a2, vt[h], pt[h]);
+        wL[c] = wt;  // (w_k-1 was last read in this step's pass, before the barrier)
+        rho[h] = csub(csub(ro[h], cconj(wt)), cmulc(wk1, vt[h]));
+        if (c > kl + 2) part += cnorm2(rho[h]);
+      }
+      tmark(3);
+      if (k == CT - 2) {
+        if (lane == 63) stg(dd + CT - 1, rho[1].x);
+      } else {
+        // reflector k + 1 from the new row k + 1 (local column kl + 2 is alpha)
+        const double xn2 = lane_sum<64>(part);
+        const int ca = kl + 2, cd = kl + 1;
+        const cplx ra = (ca >> 6) ? rho[1] : rho[0];
+        const double dk1 = readlane_d(((cd >> 6) ? rho[1] : rho[0]).x, cd & 63);
+        const cplx alpha = cmk(readlane_d(ra.x, ca & 63), -readlane_d(ra.y, ca & 63));
+        cplx tau_, sc;
+        double beta;
+        zlarfg_f(alpha, xn2, tau_, beta, sc);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int c = lane + 64 * h;
+          vL[prv][c] = c == ca ? cmk(1, 0) : (c > ca ? cmul(cconj(rho[h]), sc) : cmk(0, 0));
+        }
+        if (lane == 0) {
+          s_tau = tau_;
+          s_beta = beta;
+          s_dk = dk1;
+        }
+        tmark(4);
+      }
+    }
+    if (k == CT - 2) break;
+    __syncthreads();
+    tmark(2);
+  }
+  if (tick) {
+    for (int i = 0; i < 4; ++i) atomicAdd(&g_gbig_ticks[i], tk[i]);
+    atomicAdd(&g_gbig_ticks[8], tk[4]);
   }
 }
 
@@ -1021,6 +1206,10 @@ int run_gram_big(const TwoSiteJob* hjobs, const TwoSiteJob* jobs, int nj, int ca
   a.lam = b.lam, a.tn = b.tn, a.tfac = b.tfac, a.yc = b.yc;
   a.xch = b.xch, a.cnt = b.cnt, a.status = b.status;
   a.spin = g_gb_spin;
+  if (g_gb_tail < 0) {
+    const char* e = std::getenv("AQC_GB_TAIL");
+    g_gb_tail = (e && std::strcmp(e, "0") == 0) ? 0 : 1;
+  }
   AQC_HIP_CHECK(hipMemsetAsync(b.cnt, 0, (size_t)32 * nj * sizeof(unsigned), st));
   hipLaunchKernelGGL((k_gb_gram<CT>), dim3((CT / 64) * (CT / 64 + 1) / 2, nj), dim3(256), 0, st, jobs, a);
   AQC_CHECK_LAUNCH();
@@ -1035,7 +1224,7 @@ int run_gram_big(const TwoSiteJob* hjobs, const TwoSiteJob* jobs, int nj, int ca
     int dev = 0, ncu = 0, per_cu = 0;
     AQC_HIP_CHECK(hipGetDevice(&dev));
     AQC_HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-    AQC_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_gb_tridiag<CT, 1>, 1024, 0));
+    AQC_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_gb_tridiag<CT, 1, true>, 1024, 0));
     resident = ncu * std::min(per_cu, 1);
   }
   const int per_round = std::min(240, resident) / P;
@@ -1068,11 +1257,18 @@ int run_gram_big(const TwoSiteJob* hjobs, const TwoSiteJob* jobs, int nj, int ca
     int r = 0;
     for (int j0 = 0; j0 < nj; j0 += per_round, ++r) {
       const int nr = std::min(per_round, nj - j0);
-      hipLaunchKernelGGL((k_gb_tridiag<CT, 1>), dim3(P * nr), dim3(1024), 0, st, jobs, a, j0);
+      if (g_gb_tail)
+        hipLaunchKernelGGL((k_gb_tridiag<CT, 1, true>), dim3(P * nr), dim3(1024), 0, st, jobs, a, j0);
+      else
+        hipLaunchKernelGGL((k_gb_tridiag<CT, 1, false>), dim3(P * nr), dim3(1024), 0, st, jobs, a, j0);
       AQC_CHECK_LAUNCH();
       hipEvent_t ev = gb_event(r);
       AQC_HIP_CHECK(hipEventRecord(ev, st));
       AQC_HIP_CHECK(hipStreamWaitEvent(s2, ev, 0));
+      if (g_gb_tail) {
+        hipLaunchKernelGGL((k_gb_tail<CT>), dim3(nr), dim3(1024), 0, s2, jobs, a, j0);
+        AQC_CHECK_LAUNCH();
+      }
       rc = post(s2, j0, nr);
       if (rc != AQC_OK) return rc;
     }
@@ -1143,5 +1339,13 @@ extern "C" int aqc_svd_gram_big_stats(double* out) {
    use it to exercise the decline path. */
 extern "C" int aqc_gb_set_spin_limit(double us) {
   aqc::g_gb_spin = us < 0 ? aqc::kSpinTicks : (unsigned long long)(us * 100.0);
+  return AQC_OK;
+}
+
+/* The multi-workgroup tridiagonalisation's last 128 columns in one workgroup (1, the default) or
+   over all of the job's workgroups to the end (0). */
+extern "C" int aqc_gb_set_tail(int on) {
+  AQC_REQUIRE(on == 0 || on == 1, "aqc_gb_set_tail: on must be 0 or 1");
+  aqc::g_gb_tail = on;
   return AQC_OK;
 }

@@ -166,6 +166,10 @@ int aqc_svd_gram_big_ticks(double* out);
    a job whose workgroups wait longer declines to the block Jacobi (out[4] above).  0 forces the
    decline wherever a wait is not already satisfied (tests). */
 int aqc_gb_set_spin_limit(double us);
+/* The same tridiagonalisation's last 128 columns: in one workgroup (on = 1, the default: the
+   trailing block goes to the job's first workgroup, which finishes without the per-column
+   exchange), or over all of the job's workgroups to the end (on = 0).  AQC_GB_TAIL=0 also selects 0. */
+int aqc_gb_set_tail(int on);
 /* Test load: nblocks 256-thread workgroups on a private stream, block b spinning (b % 16 + 1) / 16
    of `ms` milliseconds, so work queued on other streams starts one CU at a time.  Asynchronous. */
 int aqc_debug_hog(int nblocks, double ms);

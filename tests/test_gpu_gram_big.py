@@ -17,6 +17,19 @@ from oracle import mps as M
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(params=[1, 0], ids=["tail", "exchange_to_end"])
+def gb_tail(request):
+    """The last 128 columns of the tridiagonalisation in one workgroup (k_gb_tail, the default) or
+    over all of the job's workgroups with the per-column exchange to the end."""
+    from adaptaqc_amd import _lib
+
+    _lib.check(_lib.load().aqc_gb_set_tail(request.param))
+    try:
+        yield request.param
+    finally:
+        _lib.check(_lib.load().aqc_gb_set_tail(1))
+
+
 def _gates(n, rng, pairs):
     ops = []
     for a, b in pairs:
@@ -55,7 +68,7 @@ def _vs_oracle(d, n, chi, ops, seed):
 
 
 @pytest.mark.parametrize("n,chi", [(18, 128), (20, 256)])
-def test_gram_big_taken_and_matches_oracle(n, chi):
+def test_gram_big_taken_and_matches_oracle(n, chi, gb_tail):
     """Adjacent truncating updates at the cap (2 chi = 256 / 512): every one takes the Gram path
     (no floor declines, no exchange timeouts) and the state matches the oracle."""
     rng = np.random.default_rng(chi + 3)
@@ -120,7 +133,7 @@ def test_gram_big_rank_deficient_declines_to_block_jacobi():
     assert abs(fid - 1.0) < 1e-6, fid
 
 
-def test_gram_big_config5_wave():
+def test_gram_big_config5_wave(gb_tail):
     """Config 5's wave (100 qubits, chi = 256, 24 disjoint updates at the cap): all 24 on the Gram
     path in one call."""
     n, chi = 100, 256
@@ -131,7 +144,7 @@ def test_gram_big_config5_wave():
     _vs_oracle(d, n, chi, ops, 5)
 
 
-def test_gram_big_exchange_timeout_declines_to_block_jacobi():
+def test_gram_big_exchange_timeout_declines_to_block_jacobi(gb_tail):
     """The counter-wait limit at 0 (aqc_gb_set_spin_limit): a workgroup that finds its job's count
     short at any column declines the job (status 3).  The declined jobs run the
     block Jacobi after the status read-back and the state still matches the oracle (exact bond dims,
@@ -152,7 +165,7 @@ def test_gram_big_exchange_timeout_declines_to_block_jacobi():
     _vs_oracle(d, n, chi, ops, chi + 4)
 
 
-def test_gram_big_late_workgroup_start():
+def test_gram_big_late_workgroup_start(gb_tail):
     """the tridiagonalisation's workgroups of one job may start late (CUs held by
     other work).  A staggered CU-holding load on another stream (aqc_debug_hog: blocks release
     their CUs over 2 ... 30 ms) is queued first, so the jobs' workgroups are dispatched one CU at a
@@ -169,3 +182,28 @@ def test_gram_big_late_workgroup_start():
     d, st = _run(n, chi, ops, seed=chi + 4)
     assert st["calls"] == 3 and st["taken"] == 3 and st["timeouts"] == 0, st
     _vs_oracle(d, n, chi, ops, chi + 4)
+
+
+def test_gram_big_tail_equals_exchange_to_end():
+    """Config 5's state, 8 disjoint updates at 2 chi = 512 with the single-workgroup tail and with
+    the exchange to the end: the same arithmetic on the same data, so the same bond dimensions and
+    Schmidt values within 1e-12."""
+    from adaptaqc_amd import _lib
+
+    n, chi = 100, 256
+    rng = np.random.default_rng(13)
+    ops = _gates(n, rng, [(a, a + 1) for a in range(40, 56, 2)])
+    res = []
+    for tail in (1, 0):
+        _lib.check(_lib.load().aqc_gb_set_tail(tail))
+        try:
+            d, st = _run(n, chi, ops, seed=6)
+        finally:
+            _lib.check(_lib.load().aqc_gb_set_tail(1))
+        assert st["taken"] == 8, st
+        res.append(d)
+    np.testing.assert_array_equal(res[0].dims(), res[1].dims())
+    _, l0 = res[0].to_aer()
+    _, l1 = res[1].to_aer()
+    for x, y in zip(l0, l1):
+        np.testing.assert_allclose(x, y, atol=1e-12)
