@@ -425,6 +425,14 @@ __global__ void k_sv_zfinal(const double* __restrict__ part, int nwg, int n, dou
   if (i < n) z[i] = t - 2.0 * s;  // p0 - p1 with p0 = total - p1
 }
 
+// The plan of one batch from the pinned staging buffer into device memory, read over the bus by
+// the kernel itself: a kernel -> kernel dependency on the stream instead of a copy-engine transfer
+// (the SDMA path that hipMemcpyAsync takes for the larger batches cost ~10-25 us of idle GPU per
+// copy in the config-2 timeline, profiles/r4_cfg2_timeline_gaps.json).  16-byte units.
+__global__ __launch_bounds__(256) void k_plan_copy(const uint4* __restrict__ src, uint4* __restrict__ dst, int n) {
+  for (int i = (int)(blockIdx.x * 256 + threadIdx.x); i < n; i += (int)gridDim.x * 256) dst[i] = src[i];
+}
+
 __global__ void k_sv_reset(cplx* state, uint64_t dim) {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   for (; i < dim; i += (uint64_t)gridDim.x * blockDim.x) state[i] = aqc::cmk(i == 0 ? 1.0 : 0.0, 0.0);
@@ -491,20 +499,21 @@ std::vector<HostSeg> build_segments(const aqc_op_t* ops, int nops, int K, int n,
 // between acts on other qubits and commutes).  Aer fuses too (fusion_enable at >= 14 qubits);
 // here every tile pass saves one LDS sweep and one barrier per absorbed gate.  Brickwork: 3 ops
 // per pair and layer become 1.
-typedef std::array<cplx, 16> Mat4;
-// host complex arithmetic without fma(): the x86 host build has no FMA instructions enabled, so
-// fma() is a libm call per operation (2.3 ns each made the fusion 0.35 ms of a 20-qubit
-// evaluation's host time)
-static inline cplx hmul(cplx a, cplx b) { return aqc::cmk(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x); }
-static inline cplx hfma(cplx a, cplx b, cplx c) {
-  return aqc::cmk(c.x + a.x * b.x - a.y * b.y, c.y + a.x * b.y + a.y * b.x);
-}
+// Host arithmetic on a plain {re, im} pair: HIP's vector type kept the fusion from optimising
+// (0.13 us per gate, 88 us of a 20-qubit evaluation's ~140 us host plan), and no fma() -- the x86
+// host build has no FMA instructions enabled, so fma() is a libm call per operation.
+struct hc {
+  double r, i;
+};
+typedef std::array<hc, 16> Mat4;
+static inline hc hmul(hc a, hc b) { return {a.r * b.r - a.i * b.i, a.r * b.i + a.i * b.r}; }
+static inline hc hfma(hc a, hc b, hc c) { return {c.r + a.r * b.r - a.i * b.i, c.i + a.r * b.i + a.i * b.r}; }
 
 static Mat4 mat4_mul(const Mat4& a, const Mat4& b) {  // a b
   Mat4 c;
   for (int r = 0; r < 4; ++r)
     for (int k = 0; k < 4; ++k) {
-      cplx acc = aqc::cmk(0, 0);
+      hc acc = {0.0, 0.0};
       for (int j = 0; j < 4; ++j) acc = hfma(a[4 * r + j], b[4 * j + k], acc);
       c[4 * r + k] = acc;
     }
@@ -513,23 +522,29 @@ static Mat4 mat4_mul(const Mat4& a, const Mat4& b) {  // a b
 
 // E m and m E for E = the 1-qubit u on bit `which` (0: the op's t0, 1: its t1) of a 4x4 (index
 // 2 b1 + b0), without forming E: 32 complex products instead of 64
-static Mat4 left1(const cplx* u, int which, const Mat4& m) {
-  Mat4 o;
+static void left1(const hc* u, int which, Mat4& m) {
   const int bit = 1 << which;
-  for (int r = 0; r < 4; ++r) {
-    const int rb = (r >> which) & 1, r0 = r & ~bit, r1 = r | bit;
-    for (int c = 0; c < 4; ++c) o[4 * r + c] = hfma(u[2 * rb + 1], m[4 * r1 + c], hmul(u[2 * rb], m[4 * r0 + c]));
+  for (int r0 = 0; r0 < 4; ++r0) {
+    if (r0 & bit) continue;
+    const int r1 = r0 | bit;
+    for (int c = 0; c < 4; ++c) {
+      const hc a = m[4 * r0 + c], b = m[4 * r1 + c];
+      m[4 * r0 + c] = hfma(u[1], b, hmul(u[0], a));
+      m[4 * r1 + c] = hfma(u[3], b, hmul(u[2], a));
+    }
   }
-  return o;
 }
-static Mat4 right1(const Mat4& m, const cplx* u, int which) {
-  Mat4 o;
+static void right1(Mat4& m, const hc* u, int which) {
   const int bit = 1 << which;
-  for (int c = 0; c < 4; ++c) {
-    const int cb = (c >> which) & 1, c0 = c & ~bit, c1 = c | bit;
-    for (int r = 0; r < 4; ++r) o[4 * r + c] = hfma(m[4 * r + c1], u[2 + cb], hmul(m[4 * r + c0], u[cb]));
+  for (int c0 = 0; c0 < 4; ++c0) {
+    if (c0 & bit) continue;
+    const int c1 = c0 | bit;
+    for (int r = 0; r < 4; ++r) {
+      const hc a = m[4 * r + c0], b = m[4 * r + c1];
+      m[4 * r + c0] = hfma(b, u[2], hmul(a, u[0]));
+      m[4 * r + c1] = hfma(b, u[3], hmul(a, u[1]));
+    }
   }
-  return o;
 }
 
 static Mat4 swap_bits(const Mat4& a) {  // the same operator with t0 and t1 exchanged
@@ -543,69 +558,70 @@ static Mat4 swap_bits(const Mat4& a) {  // the same operator with t0 and t1 exch
 std::vector<SegGate> fuse_segment(const aqc_op_t* ops, const std::vector<int>& idx, const int* local_of) {
   struct F {
     int nq, t0, t1;
+    bool dead;
     Mat4 m;  // nq == 1: m[0..3] = 2x2
-    bool dead = false;
   };
-  std::vector<F> f;
+  thread_local std::vector<F> f;  // (reused: one allocation per thread, not per segment)
+  f.clear();
   f.reserve(idx.size());
   int last[64];
   for (int q = 0; q < 64; ++q) last[q] = -1;
   for (int gi : idx) {
     const aqc_op_t& o = ops[gi];
-    cplx u[16];
-    const int nel = o.nq == 1 ? 4 : 16;
-    for (int e = 0; e < nel; ++e) u[e] = aqc::cmk(o.m[2 * e], o.m[2 * e + 1]);
+    const hc* u = reinterpret_cast<const hc*>(o.m);  // (re, im) pairs, row-major
     if (o.nq == 1) {
       const int q = local_of[o.q0];
       const int k = last[q];
       if (k >= 0 && f[k].nq == 1) {  // 2x2 product u * m
-        Mat4 c = f[k].m;
-        for (int r = 0; r < 2; ++r)
-          for (int cc = 0; cc < 2; ++cc) c[2 * r + cc] = hfma(u[2 * r + 1], f[k].m[2 + cc], hmul(u[2 * r], f[k].m[cc]));
-        f[k].m = c;
+        Mat4& m = f[k].m;
+        const hc m0 = m[0], m1 = m[1], m2 = m[2], m3 = m[3];
+        m[0] = hfma(u[1], m2, hmul(u[0], m0));
+        m[1] = hfma(u[1], m3, hmul(u[0], m1));
+        m[2] = hfma(u[3], m2, hmul(u[2], m0));
+        m[3] = hfma(u[3], m3, hmul(u[2], m1));
       } else if (k >= 0) {
-        f[k].m = left1(u, f[k].t0 == q ? 0 : 1, f[k].m);
+        left1(u, f[k].t0 == q ? 0 : 1, f[k].m);
       } else {
-        F n;
-        n.nq = 1, n.t0 = q, n.t1 = 0;
-        n.m = Mat4{};
+        f.emplace_back();
+        F& n = f.back();
+        n.nq = 1, n.t0 = q, n.t1 = 0, n.dead = false;
         for (int e = 0; e < 4; ++e) n.m[e] = u[e];
-        f.push_back(n);
         last[q] = (int)f.size() - 1;
       }
       continue;
     }
     const int a = local_of[o.q0], b = local_of[o.q1];
-    Mat4 g;
-    for (int e = 0; e < 16; ++e) g[e] = u[e];
     const int ka = last[a], kb = last[b];
     if (ka >= 0 && ka == kb && f[ka].nq == 2) {  // same pair again
+      Mat4 g;
+      for (int e = 0; e < 16; ++e) g[e] = u[e];
       f[ka].m = mat4_mul(f[ka].t0 == a ? g : swap_bits(g), f[ka].m);
       continue;
     }
     // absorb pending single-qubit ops on a / b (their last op, nothing after them on that qubit)
-    Mat4 m = g;
+    f.emplace_back();
+    F& n = f.back();
+    n.nq = 2, n.t0 = a, n.t1 = b, n.dead = false;
+    for (int e = 0; e < 16; ++e) n.m[e] = u[e];
     if (ka >= 0 && f[ka].nq == 1) {
-      m = right1(m, f[ka].m.data(), 0);
+      right1(n.m, f[ka].m.data(), 0);
       f[ka].dead = true;
     }
     if (kb >= 0 && f[kb].nq == 1) {
-      m = right1(m, f[kb].m.data(), 1);
+      right1(n.m, f[kb].m.data(), 1);
       f[kb].dead = true;
     }
-    F n;
-    n.nq = 2, n.t0 = a, n.t1 = b, n.m = m;
-    f.push_back(n);
     last[a] = last[b] = (int)f.size() - 1;
   }
   std::vector<SegGate> out;
+  out.reserve(f.size());
   for (const F& x : f) {
     if (x.dead) continue;
-    SegGate g;
+    out.emplace_back();
+    SegGate& g = out.back();
     std::memset(&g, 0, sizeof(g));
     g.nq = x.nq, g.t0 = x.t0, g.t1 = x.t1;
-    for (int e = 0; e < (x.nq == 1 ? 4 : 16); ++e) g.m[e] = x.m[e];
-    out.push_back(g);
+    for (int e = 0; e < (x.nq == 1 ? 4 : 16); ++e) g.m[e] = aqc::cmk(x.m[e].r, x.m[e].i);
   }
   return out;
 }
@@ -737,9 +753,9 @@ void build_phases(const std::vector<SegGate>& fused, int K, int NS, std::vector<
         const int s0 = slot(g.t0), s1 = slot(g.t1);
         if (s0 > s1) {
           Mat4 m;
-          for (int e = 0; e < 16; ++e) m[e] = g.m[e];
+          for (int e = 0; e < 16; ++e) m[e] = {g.m[e].x, g.m[e].y};
           m = swap_bits(m);
-          for (int e = 0; e < 16; ++e) g.m[e] = m[e];
+          for (int e = 0; e < 16; ++e) g.m[e] = aqc::cmk(m[e].r, m[e].i);
         }
         g.t0 = s0 < s1 ? s0 : s1;
         g.t1 = s0 < s1 ? s1 : s0;
@@ -985,6 +1001,15 @@ static bool sv_reg_tiles(int n) {
   return n >= kRegMinQubits && !(tile_env && std::strcmp(tile_env, "lds") == 0);
 }
 
+// AQC_SV_PLAN_COPY=memcpy: the plan goes over with hipMemcpyAsync (A/B); default the copy kernel
+static bool plan_copy_kernel() {
+  static const bool k = [] {
+    const char* e = std::getenv("AQC_SV_PLAN_COPY");
+    return !(e && std::strcmp(e, "memcpy") == 0);
+  }();
+  return k;
+}
+
 static int sv_launch_segment(aqc_sv_t h, const SegHeader* dh, const PhaseHdr* dp, const SegGate* dg, int nblocks,
                              double flops) {
   const int from_zero = h->zero_pending ? 1 : 0;
@@ -1154,7 +1179,15 @@ int aqc_sv_apply(aqc_sv_t h, const aqc_op_t* ops, int nops) {
     std::memcpy(h->h_plan + o_h, hdr.data(), sizeof(SegHeader) * nb);
     if (!phs.empty()) std::memcpy(h->h_plan + o_p, phs.data(), sizeof(PhaseHdr) * phs.size());
     if (!gts.empty()) std::memcpy(h->h_plan + o_g, gts.data(), sizeof(SegGate) * gts.size());
-    hipError_t e = hipMemcpyAsync(h->d_plan + o_h, h->h_plan + o_h, end - o_h, hipMemcpyHostToDevice, h->stream);
+    hipError_t e = hipSuccess;
+    if (plan_copy_kernel()) {
+      const int n16 = (int)((end - o_h + 15) / 16);  // (o_h is 256-aligned; end <= plan_cap - 16)
+      hipLaunchKernelGGL(k_plan_copy, dim3(std::min(64, (n16 + 255) / 256)), dim3(256), 0, h->stream,
+                         reinterpret_cast<const uint4*>(h->h_plan + o_h), reinterpret_cast<uint4*>(h->d_plan + o_h), n16);
+      e = hipGetLastError();
+    } else {
+      e = hipMemcpyAsync(h->d_plan + o_h, h->h_plan + o_h, end - o_h, hipMemcpyHostToDevice, h->stream);
+    }
     if (e != hipSuccess) {
       aqc::set_error(std::string("aqc_sv_apply: plan copy: ") + hipGetErrorString(e));
       rc = AQC_ERR_HIP;
