@@ -151,6 +151,13 @@ __device__ __forceinline__ double group_sum(double v) {
 void on_finalize(void (*fn)());
 void note_device(int dev);
 
+// Host -> device copy of a pinned (hipHostMalloc) staging buffer on `st`, done by a kernel that
+// reads the host memory over the bus: the stream's next kernel then depends on a kernel, not on a
+// copy-engine transfer (each of those cost ~10-25 us of idle GPU in the measured timelines,
+// profiles/r4_cfg2_timeline_gaps.json).  hipMemcpyAsync below AQC_UPLOAD_MIN_KB (16) and for
+// unaligned pointers; AQC_UPLOAD=memcpy selects it everywhere (A/B).
+int upload_async(void* dst, const void* pinned_src, size_t bytes, hipStream_t st);
+
 // ---- cached device memory ------------------------------------------------------------------
 // Blocks freed by the library go to a per-device free list keyed by size (4 KB granules) and are
 // handed out again to the next request of that size: handle creation and destruction (a batched

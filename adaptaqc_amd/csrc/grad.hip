@@ -987,7 +987,7 @@ int aqc_pair_grads_batch(aqc_mps_t* psis, int ns, const double* svec, const int*
     for (int a = 0; a < n; ++a) hstart[a] = 0;
     for (int a : alist) hstart[a] = 1;
   }
-  AQC_HIP_CHECK(hipMemcpyAsync(base, hbase, image, hipMemcpyHostToDevice, st));
+  if (int e = aqc::upload_async(base, hbase, image, st)) return e;
   const int cap = psis[0]->d.cap;
   // few states: each site's M over several workgroups (the chains / GEMMs that follow are the
   // single sweep's critical path)
@@ -1174,8 +1174,8 @@ int aqc_argmax_scaled(const double* scores, const double* prio, int count, int s
   int* db = (int*)(ab.dev + 2 * (size_t)count);
   std::memcpy(ab.host, prio, count * sizeof(double));
   if (!scores_is_device) std::memcpy(ab.host + count, scores, count * sizeof(double));
-  AQC_HIP_CHECK(hipMemcpyAsync(dp, ab.host, (scores_is_device ? 1 : 2) * (size_t)count * sizeof(double),
-                               hipMemcpyHostToDevice, st));
+  if (int e = aqc::upload_async(dp, ab.host, (scores_is_device ? 1 : 2) * (size_t)count * sizeof(double), st))
+    return e;
   hipLaunchKernelGGL(k_argmax, dim3(1), dim3(256), 0, st, scores_is_device ? scores : ds, dp, count, db);
   AQC_CHECK_LAUNCH();
   int* hb = (int*)(ab.host + 2 * (size_t)count);

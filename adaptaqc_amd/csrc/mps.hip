@@ -1986,7 +1986,7 @@ int run_chains(aqc_mps_t* hs, int ns, std::vector<std::vector<DevOp>>& lists, in
     hc[k].nops = (int)lists[s].size();
     hc[k].pad = 0;
   }
-  AQC_HIP_CHECK(hipMemcpyAsync(sg.dev, sg.host, total, hipMemcpyHostToDevice, st));
+  if (int e = aqc::upload_async(sg.dev, sg.host, total, st)) return e;
   const double c = cap_max, nj = (double)n_two;
   // algorithmic: the two sites' Gammas in and out; nominal SVD + theta + split flops
   aqc::KernelTimer::begin(st, "mps_chain", nj * 8.0 * c * c * 16, nj * (84.0 * 8.0 + 64.0) * c * c * c);
@@ -2109,7 +2109,7 @@ int run_waves(aqc_mps_t* hs, int ns, std::vector<std::vector<DevOp>>& lists) {
   if (rc != AQC_OK) return rc;
   std::memcpy(sg.host, two.data(), tb);
   std::memcpy((char*)sg.host + tb, one.data(), ob);
-  AQC_HIP_CHECK(hipMemcpyAsync(sg.dev, sg.host, tb + ob, hipMemcpyHostToDevice, st));
+  if (int e = aqc::upload_async(sg.dev, sg.host, tb + ob, st)) return e;
   const TwoSiteJob* dtwo = (const TwoSiteJob*)sg.dev;
   const OneSiteJob* done = (const OneSiteJob*)((char*)sg.dev + tb);
   const int tiles = ((cap_max + 15) / 16) * ((cap_max + 15) / 16);
@@ -2287,7 +2287,7 @@ int upload_jobs(const std::vector<T>& jobs, const T** dptr) {
   int rc = ensure_staging(sg, b + 64);
   if (rc != AQC_OK) return rc;
   std::memcpy(sg.host, jobs.data(), b);
-  AQC_HIP_CHECK(hipMemcpyAsync(sg.dev, sg.host, b, hipMemcpyHostToDevice, st));
+  if (int e = aqc::upload_async(sg.dev, sg.host, b, st)) return e;
   *dptr = (const T*)sg.dev;
   return AQC_OK;
 }
@@ -2685,7 +2685,7 @@ int aqc_mps_copy_batch(aqc_mps_t* dst, const aqc_mps_t* src, int ns) {
   int rc = ensure_staging(sg, bytes);
   if (rc != AQC_OK) return rc;
   std::memcpy(sg.host, jobs.data(), bytes);
-  AQC_HIP_CHECK(hipMemcpyAsync(sg.dev, sg.host, bytes, hipMemcpyHostToDevice, st));
+  if (int e = aqc::upload_async(sg.dev, sg.host, bytes, st)) return e;
   size_t words = jobs[0].nl / 2, moved = 0;
   for (const CopyJob& j : jobs) {
     words = std::max(words, j.ng);

@@ -425,14 +425,6 @@ __global__ void k_sv_zfinal(const double* __restrict__ part, int nwg, int n, dou
   if (i < n) z[i] = t - 2.0 * s;  // p0 - p1 with p0 = total - p1
 }
 
-// The plan of one batch from the pinned staging buffer into device memory, read over the bus by
-// the kernel itself: a kernel -> kernel dependency on the stream instead of a copy-engine transfer
-// (the SDMA path that hipMemcpyAsync takes for the larger batches cost ~10-25 us of idle GPU per
-// copy in the config-2 timeline, profiles/r4_cfg2_timeline_gaps.json).  16-byte units.
-__global__ __launch_bounds__(256) void k_plan_copy(const uint4* __restrict__ src, uint4* __restrict__ dst, int n) {
-  for (int i = (int)(blockIdx.x * 256 + threadIdx.x); i < n; i += (int)gridDim.x * 256) dst[i] = src[i];
-}
-
 __global__ void k_sv_reset(cplx* state, uint64_t dim) {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   for (; i < dim; i += (uint64_t)gridDim.x * blockDim.x) state[i] = aqc::cmk(i == 0 ? 1.0 : 0.0, 0.0);
@@ -1001,15 +993,6 @@ static bool sv_reg_tiles(int n) {
   return n >= kRegMinQubits && !(tile_env && std::strcmp(tile_env, "lds") == 0);
 }
 
-// AQC_SV_PLAN_COPY=memcpy: the plan goes over with hipMemcpyAsync (A/B); default the copy kernel
-static bool plan_copy_kernel() {
-  static const bool k = [] {
-    const char* e = std::getenv("AQC_SV_PLAN_COPY");
-    return !(e && std::strcmp(e, "memcpy") == 0);
-  }();
-  return k;
-}
-
 static int sv_launch_segment(aqc_sv_t h, const SegHeader* dh, const PhaseHdr* dp, const SegGate* dg, int nblocks,
                              double flops) {
   const int from_zero = h->zero_pending ? 1 : 0;
@@ -1179,20 +1162,10 @@ int aqc_sv_apply(aqc_sv_t h, const aqc_op_t* ops, int nops) {
     std::memcpy(h->h_plan + o_h, hdr.data(), sizeof(SegHeader) * nb);
     if (!phs.empty()) std::memcpy(h->h_plan + o_p, phs.data(), sizeof(PhaseHdr) * phs.size());
     if (!gts.empty()) std::memcpy(h->h_plan + o_g, gts.data(), sizeof(SegGate) * gts.size());
-    hipError_t e = hipSuccess;
-    if (plan_copy_kernel()) {
-      const int n16 = (int)((end - o_h + 15) / 16);  // (o_h is 256-aligned; end <= plan_cap - 16)
-      hipLaunchKernelGGL(k_plan_copy, dim3(std::min(64, (n16 + 255) / 256)), dim3(256), 0, h->stream,
-                         reinterpret_cast<const uint4*>(h->h_plan + o_h), reinterpret_cast<uint4*>(h->d_plan + o_h), n16);
-      e = hipGetLastError();
-    } else {
-      e = hipMemcpyAsync(h->d_plan + o_h, h->h_plan + o_h, end - o_h, hipMemcpyHostToDevice, h->stream);
-    }
-    if (e != hipSuccess) {
-      aqc::set_error(std::string("aqc_sv_apply: plan copy: ") + hipGetErrorString(e));
-      rc = AQC_ERR_HIP;
-      break;
-    }
+    // (by a copy kernel, aqc::upload_async: the SDMA transfers hipMemcpyAsync used for the larger
+    // batches cost ~10-25 us of idle GPU each in the config-2 timeline)
+    rc = aqc::upload_async(h->d_plan + o_h, h->h_plan + o_h, end - o_h, h->stream);
+    if (rc != AQC_OK) break;
     const SegHeader* dh = reinterpret_cast<const SegHeader*>(h->d_plan + o_h);
     const PhaseHdr* dp = reinterpret_cast<const PhaseHdr*>(h->d_plan + o_p);
     const SegGate* dg = reinterpret_cast<const SegGate*>(h->d_plan + o_g);

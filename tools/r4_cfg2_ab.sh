@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-4 call: config 2 with the plan uploaded by a copy kernel (default) and by hipMemcpyAsync
-# (AQC_SV_PLAN_COPY=memcpy), alternating, after the SV tests; then the device timeline of the default.
+# (AQC_UPLOAD=memcpy), alternating, after the SV tests; then the device timeline of the default.
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
 : > gpurun_out/cfg2ab_steps.txt
@@ -14,7 +14,7 @@ step() {
 step sv_tests 300 python3 -u -m pytest tests/test_gpu_sv.py -x -q --timeout 120 --timeout-method thread || exit $?
 for i in 1 2; do
   step cfg2_kernel_$i 200 python3 tools/configs_bench.py --configs 2 || exit $?
-  AQC_SV_PLAN_COPY=memcpy step cfg2_memcpy_$i 200 python3 tools/configs_bench.py --configs 2 || exit $?
+  AQC_UPLOAD=memcpy step cfg2_memcpy_$i 200 python3 tools/configs_bench.py --configs 2 || exit $?
 done
 step tl2 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d gpurun_out/tl2 -o run -- python3 tools/configs_bench.py --configs 2 --reps 1 || exit $?
 python3 tools/timeline_gaps.py gpurun_out/tl2/run > gpurun_out/cfg2_gaps_kernelcopy.json
