@@ -73,6 +73,14 @@ __device__ unsigned long long g_gram_ticks[12];
 #ifndef AQC_S3_PIPE
 #define AQC_S3_PIPE 1
 #endif
+// S3 register layout: 1 -- row tid / 8, columns tid % 8 + 8 i (i < 16); 2 (round-4 experiment,
+// measured slower) -- thread (wave w, lane l) holds rows 8 w + l / 16 and that + 4, columns
+// l % 16 + 16 i (i < 8), so each column's v, p, z LDS operands serve two rows: half the column
+// pass's LDS reads and 14 instead of 16 FP64 operations per element, but S3 took 0.68 M ticks
+// against 0.64 M (with a v / p prefetch, which spilled two g entries: 0.71 M)
+#ifndef AQC_S3_RPL
+#define AQC_S3_RPL 1
+#endif
 // path counters (thread 0 of each call): [0] calls, [1] taken, [2] declined by shape (K > 64, ...),
 // [3] declined at the eigenvalue floor (lambda_K <= 1e-9 lambda_1 -> the Jacobi runs)
 __device__ unsigned long long g_gram_stats[4];
@@ -289,7 +297,13 @@ __device__ __noinline__ bool gram_svd_body_t(const TwoSiteJob& j) {
   // (absolute error a few eps ||X||^2, the Gram path's eps ||G|| budget).  X streams once through
   // double-buffered LDS chunks of 8 rows (Xr, Xi, Xr + Xi, Xr - Xi), the next chunk's global
   // load in flight during the current chunk's MFMAs: 256 KB read per SVD (768 KB before). ----
+#if AQC_S3_RPL == 2
+  // rows ra0 (g[0..7]) and ra0 + 4 (g[8..15]), columns q0 + 16 i
+  const int ra0 = 8 * wave + (lane >> 4), q0 = lane & 15;
+  const int r0 = ra0;
+#else
   const int r0 = tid >> 3, q0 = tid & 7;
+#endif
   const int r = r0, q = q0;
   cplx g[16];
   {
@@ -409,11 +423,15 @@ __device__ __noinline__ bool gram_svd_body_t(const TwoSiteJob& j) {
     if constexpr (!TRI) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        const int c = q + 8 * i;
+#if AQC_S3_RPL == 2
+        const int c = q + 16 * (i & 7), rw = r + 4 * (i >> 3);
+#else
+        const int c = q + 8 * i, rw = r;
+#endif
         cplx v = aqc::cmk(0, 0);
-        if (r < C && c < C) {
-          v = gsq[c >= r ? up_index(r, c) : up_index(c, r)];
-          if (c < r) v.y = -v.y;
+        if (rw < C && c < C) {
+          v = gsq[c >= rw ? up_index(rw, c) : up_index(c, rw)];
+          if (c < rw) v.y = -v.y;
         }
         g[i] = v;
       }
@@ -495,6 +513,11 @@ __device__ __noinline__ bool gram_svd_body_t(const TwoSiteJob& j) {
     pvb[128 + r] = aqc::cmk(0, 0);
     vbb[128 + r] = aqc::cmk(0, 0);
     zvb[128 + r] = (r > 0 && r < C) ? g[0] : aqc::cmk(0, 0);
+#if AQC_S3_RPL == 2
+    pvb[128 + r + 4] = aqc::cmk(0, 0);
+    vbb[128 + r + 4] = aqc::cmk(0, 0);
+    zvb[128 + r + 4] = (r + 4 < C) ? g[8] : aqc::cmk(0, 0);
+#endif
   }
   __syncthreads();
   // reflector k - 1's a2 and s from buffer bp, per wave
@@ -563,6 +586,68 @@ __device__ __noinline__ bool gram_svd_body_t(const TwoSiteJob& j) {
       if (AQC_S3_PRIO) __builtin_amdgcn_s_setprio(0);
       if (AQC_S3_DIAG && tid == 0) t_z += __builtin_amdgcn_s_memtime() - t_last;
     }
+#if AQC_S3_RPL == 2
+    static_assert(AQC_S3_ROWSUM, "two rows per lane: in-wave row sums");
+    if (wact) {
+      // rows r (g[0..7]) and r + 4 (g[8..15]); each column's v, p, z read once for both
+      const int rb = r + 4;
+      const double a2r2 = 2.0 * a2.x;
+      const cplx vra = vbb[bp * 128 + r], pra = pvb[bp * 128 + r];
+      const cplx vrb = vbb[bp * 128 + rb], prb = pvb[bp * 128 + rb];
+      const cplx wra = aqc::cmk(fma(a2r2, vra.x, pra.x), fma(a2r2, vra.y, pra.y));
+      const cplx wrb = aqc::cmk(fma(a2r2, vrb.x, prb.x), fma(a2r2, vrb.y, prb.y));
+      cplx acca = aqc::cmk(0, 0), accb = aqc::cmk(0, 0);
+      const double nsx = -s.x, nsy = -s.y;
+      // g -= v_r conj(p_c) + w_r conj(v_c) (reflector k - 1), acc += g x_c (reflector k)
+      auto upd = [](cplx& gg, const cplx& vr, const cplx& wr, const cplx& vc, const cplx& pc) {
+        gg.x = fma(-vr.x, pc.x, fma(-vr.y, pc.y, fma(-wr.x, vc.x, fma(-wr.y, vc.y, gg.x))));
+        gg.y = fma(-vr.y, pc.x, fma(vr.x, pc.y, fma(-wr.y, vc.x, fma(wr.x, vc.y, gg.y))));
+      };
+      auto col = [&](int i, const cplx& vc, const cplx& pc, const cplx& zc) {
+        const cplx xc = aqc::cmk(fma(nsx, vc.x, fma(nsy, -vc.y, zc.x)), fma(nsx, vc.y, fma(nsy, vc.x, zc.y)));
+        upd(g[i], vra, wra, vc, pc);
+        acca = aqc::cfma(g[i], xc, acca);
+        upd(g[8 + i], vrb, wrb, vc, pc);
+        accb = aqc::cfma(g[8 + i], xc, accb);
+      };
+      // over the active column blocks (16 columns each; v_c = p_c = z_c = 0 for c < k, so the first
+      // block's dead columns need no mask), each column's operands loaded where they are used
+      const int i0 = k >> 4;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        if (i >= i0) {  // uniform
+          const int c = q + 16 * i;
+          col(i, vbb[bp * 128 + c], pvb[bp * 128 + c], zvb[bp * 128 + c]);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      // the correction for x_k (see below) and G^(k)[r][k], G^(k)[r][k + 1] from the lanes
+      // holding columns k and k + 1 (the same register unless k + 1 starts a block)
+      const cplx gka = pick16(g, k >> 4), gkb = pick16(g, 8 + (k >> 4));
+      const bool same = ((k + 1) & 15) != 0;
+      const cplx gk1a = same ? gka : pick16(g, (k + 1) >> 4);
+      const cplx gk1bv = same ? gkb : pick16(g, 8 + ((k + 1) >> 4));
+      if (q == (k & 15)) {
+        acca = aqc::cfma(s, gka, acca);
+        accb = aqc::cfma(s, gkb, accb);
+        if (r == k) dS[k] = gka.x;
+        if (rb == k) dS[k] = gkb.x;
+      }
+      acca.x = aqc::row_sum16(acca.x);
+      acca.y = aqc::row_sum16(acca.y);
+      accb.x = aqc::row_sum16(accb.x);
+      accb.y = aqc::row_sum16(accb.y);
+      if (q == 0) {
+        accp[r] = acca;
+        accp[rb] = accb;
+      }
+      if (q == ((k + 1) & 15)) {
+        gk1b[r] = gk1a;
+        gk1b[rb] = gk1bv;
+      }
+      if (AQC_S3_DIAG && tid == 832) t_c += __builtin_amdgcn_s_memtime() - t_c0;
+    }
+#else
     if (wact) {
       // the own row's reflector k - 1 entries and w_r (the Hermitian rank-2 update needs only
       // Re(a2): v w^H + w v^H = v p^H + (p + 2 Re(a2) v) v^H, so no per-column w_c)
@@ -673,6 +758,7 @@ __device__ __noinline__ bool gram_svd_body_t(const TwoSiteJob& j) {
       if (q == ((k + 1) & 7)) gk1b[r] = gk1;
       if (AQC_S3_DIAG && tid == 832) t_c += __builtin_amdgcn_s_memtime() - t_c0;
     }
+#endif
     __syncthreads();
     tick_step(t_b);
     // Phase B: reflector k's p, v and z, one row per thread of waves 0 and 1 (the row's eight
@@ -714,10 +800,17 @@ __device__ __noinline__ bool gram_svd_body_t(const TwoSiteJob& j) {
     const int bp = (C - 2) & 1;
     cplx a2, s;
     prev_scalars(C - 1, bp, a2, s);
-    if (r0 == C - 1 && q0 == ((C - 1) & 7)) {
+#if AQC_S3_RPL == 2
+    const bool own = (r0 == C - 1 || r0 + 4 == C - 1) && q0 == ((C - 1) & 15);
+    const int gi = ((C - 1) >> 4) + (r0 + 4 == C - 1 ? 8 : 0);
+#else
+    const bool own = r0 == C - 1 && q0 == ((C - 1) & 7);
+    const int gi = (C - 1) >> 3;
+#endif
+    if (own) {
       const cplx v = vbb[bp * 128 + C - 1], p = pvb[bp * 128 + C - 1];
       const cplx w = aqc::cfma(a2, v, p);
-      const cplx gl = pick16(g, (C - 1) >> 3);
+      const cplx gl = pick16(g, gi);
       dS[C - 1] = gl.x - 2.0 * (v.x * w.x + v.y * w.y);  // Re(g - v conj(w) - w conj(v))
     }
   }
