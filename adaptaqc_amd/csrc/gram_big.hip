@@ -1167,22 +1167,26 @@ int gb_ensure(GBBuffers& b, int ct, int nj, hipStream_t st) {
 // device synchronisation) by release_gb_sync -- at exit the side stream's post kernels are ordered
 // only by these events, so they must be drained before the runtime tears down.
 hipStream_t g_gb_side[64] = {nullptr};
+hipStream_t g_gb_side2[64] = {nullptr};  // the compact-WY factors beside the eigenpairs
 std::vector<hipEvent_t> g_gb_events;
 void release_gb_sync() {
   for (auto& s : g_gb_side)
+    if (s) (void)hipStreamDestroy(s), s = nullptr;
+  for (auto& s : g_gb_side2)
     if (s) (void)hipStreamDestroy(s), s = nullptr;
   for (hipEvent_t e : g_gb_events) (void)hipEventDestroy(e);
   g_gb_events.clear();
 }
 
-hipStream_t gb_side_stream() {
+hipStream_t gb_side_stream(int which = 0) {
   int dev = 0;
   (void)hipGetDevice(&dev);
-  if (!g_gb_side[dev]) {
-    (void)hipStreamCreateWithFlags(&g_gb_side[dev], hipStreamNonBlocking);
+  hipStream_t* tab = which ? g_gb_side2 : g_gb_side;
+  if (!tab[dev]) {
+    (void)hipStreamCreateWithFlags(&tab[dev], hipStreamNonBlocking);
     aqc::on_finalize(release_gb_sync);
   }
-  return g_gb_side[dev];
+  return tab[dev];
 }
 
 hipEvent_t gb_event(int i) {  // (per process; the library stream orders their reuse)
@@ -1236,15 +1240,34 @@ int run_gram_big(const TwoSiteJob* hjobs, const TwoSiteJob* jobs, int nj, int ca
     overlap = (e && std::strcmp(e, "0") == 0) ? 0 : 1;
   }
   hipStream_t s2 = overlap ? gb_side_stream() : st;
+  // the compact-WY factors need only the reflectors: on a third stream beside the eigenvalues,
+  // inverse iteration and Gram-Schmidt (which need only T), joined before the back-transformation
+  static int tfac_side = -1;  // AQC_GB_TFAC_SIDE=0: the factors in line on the post stream (A/B)
+  if (tfac_side < 0) {
+    const char* e = std::getenv("AQC_GB_TFAC_SIDE");
+    tfac_side = (e && std::strcmp(e, "0") == 0) ? 0 : 1;
+  }
+  hipStream_t s3 = overlap && tfac_side ? gb_side_stream(1) : s2;
+  int evi = 0;  // events of this call, in order (gb_event: per process, reused call to call)
   auto post = [&](hipStream_t ps, int j0, int nr) -> int {
+    if (s3 != ps) {
+      hipEvent_t e0 = gb_event(evi++);
+      AQC_HIP_CHECK(hipEventRecord(e0, ps));
+      AQC_HIP_CHECK(hipStreamWaitEvent(s3, e0, 0));
+    }
+    hipLaunchKernelGGL((k_gb_tfac<CT>), dim3((CT - 1 + 15) / 16, nr), dim3(256), 0, s3, jobs, a, j0);
+    AQC_CHECK_LAUNCH();
     hipLaunchKernelGGL((k_gb_eig<CT>), dim3(CT / 64, nr), dim3(256), 0, ps, jobs, a, j0);
     AQC_CHECK_LAUNCH();
     hipLaunchKernelGGL((k_gb_inv<CT>), dim3(CT / 64, nr), dim3(64), 0, ps, jobs, a, j0);
     AQC_CHECK_LAUNCH();
     hipLaunchKernelGGL((k_gb_gs<CT>), dim3(nr), dim3(64), 0, ps, jobs, a, j0);
     AQC_CHECK_LAUNCH();
-    hipLaunchKernelGGL((k_gb_tfac<CT>), dim3((CT - 1 + 15) / 16, nr), dim3(256), 0, ps, jobs, a, j0);
-    AQC_CHECK_LAUNCH();
+    if (s3 != ps) {
+      hipEvent_t e1 = gb_event(evi++);
+      AQC_HIP_CHECK(hipEventRecord(e1, s3));
+      AQC_HIP_CHECK(hipStreamWaitEvent(ps, e1, 0));
+    }
     hipLaunchKernelGGL((k_gb_back<CT>), dim3(CT / 16, nr), dim3(CT / 64 > 4 ? CT : 256), 0, ps, jobs, a, j0);
     AQC_CHECK_LAUNCH();
     return AQC_OK;
@@ -1254,15 +1277,14 @@ int run_gram_big(const TwoSiteJob* hjobs, const TwoSiteJob* jobs, int nj, int ca
     rc = post(st, 0, nj);
     if (rc != AQC_OK) return rc;
   } else {
-    int r = 0;
-    for (int j0 = 0; j0 < nj; j0 += per_round, ++r) {
+    for (int j0 = 0; j0 < nj; j0 += per_round) {
       const int nr = std::min(per_round, nj - j0);
       if (g_gb_tail)
         hipLaunchKernelGGL((k_gb_tridiag<CT, 1, true>), dim3(P * nr), dim3(1024), 0, st, jobs, a, j0);
       else
         hipLaunchKernelGGL((k_gb_tridiag<CT, 1, false>), dim3(P * nr), dim3(1024), 0, st, jobs, a, j0);
       AQC_CHECK_LAUNCH();
-      hipEvent_t ev = gb_event(r);
+      hipEvent_t ev = gb_event(evi++);
       AQC_HIP_CHECK(hipEventRecord(ev, st));
       AQC_HIP_CHECK(hipStreamWaitEvent(s2, ev, 0));
       if (g_gb_tail) {
@@ -1272,7 +1294,7 @@ int run_gram_big(const TwoSiteJob* hjobs, const TwoSiteJob* jobs, int nj, int ca
       rc = post(s2, j0, nr);
       if (rc != AQC_OK) return rc;
     }
-    hipEvent_t done = gb_event(r);
+    hipEvent_t done = gb_event(evi++);
     AQC_HIP_CHECK(hipEventRecord(done, s2));
     AQC_HIP_CHECK(hipStreamWaitEvent(st, done, 0));
   }
