@@ -357,18 +357,20 @@ def main():
     local_scores = torch.zeros((len(states), max(len(shard.local_pairs), 1)), dtype=torch.float64, device="cuda")
     prio_t = torch.as_tensor(prio, device="cuda")
 
-    def sweep():
-        # (i) sharded candidate sweep + all-gather + arg-max
+    def sweep_launch():
+        # (i) the sharded candidate sweep's kernels (queued on the library stream)
+        if by_state or shard.local_pairs:
+            pair_grads_batch(states, svec, shard.local_pairs, u0, gm, deg, out=local_scores.data_ptr())
+
+    def sweep_select():
+        # ... then the all-gather + arg-max
         if by_state:
             # every pair of this rank's states, the per-state arg-max on the rank, then one all-gather
             # of (best pair, score) per state (RCCL over xGMI; the projection repeats rank 0's block)
-            pair_grads_batch(states, svec, shard.local_pairs, u0, gm, deg, out=local_scores.data_ptr())
             b, sc = best_pairs(local_scores, prio)
             if sim:
                 return local_scores, b.repeat(sim)
             return local_scores, gather_best(b, sc, sshard)[0]
-        if shard.local_pairs:
-            pair_grads_batch(states, svec, shard.local_pairs, u0, gm, deg, out=local_scores.data_ptr())
         if sim:  # projection: rank 0's scores scattered locally, no collective
             full = torch.zeros((S, len(cmap)), dtype=torch.float64, device="cuda")
             full[:, torch.as_tensor(shard.local_index, device="cuda")] = local_scores[:, : len(shard.local_pairs)]
@@ -382,15 +384,23 @@ def main():
         apply_batch(work, layer_batch, sort=True)
         return 1.0 - np.abs(overlap_zero_batch(work)) ** 2
 
+    def sweep():
+        sweep_launch()
+        return sweep_select()
+
     def step():
-        full, best = sweep()
         if args.no_pipeline:
+            full, best = sweep()
             return full, best, overlaps()
-        # the chain's flags are read after the cost read-back (one host wait per step instead of
-        # two): the overlap kernel's launch is prepared while the chain runs.  (Queuing the chain
-        # before the sweep measured no better: the step is GPU-bound, 59-60 ms either way.)
+        # the sweep's kernels first, then the chain's host preparation (~1-1.7 ms for 1024 states)
+        # while the GPU runs them, then the arg-max / all-gather (queued behind the sweep, beside the
+        # chain); the chain's flags are read after the cost read-back (one host wait per step).
+        # (Preparing the chain after the arg-max left the GPU idle ~1.1 ms per step before the
+        # chain: profiles/r4_bench_timeline_gaps.json.)
+        sweep_launch()
         copy_batch(work, reload_src)
         apply_batch(work, layer_batch, sort=True, wait=False)
+        full, best = sweep_select()
         costs = 1.0 - np.abs(overlap_zero_batch(work)) ** 2
         check_batch(work)
         return full, best, costs
