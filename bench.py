@@ -396,7 +396,7 @@ def main():
         # while the GPU runs them, then the arg-max / all-gather (queued behind the sweep, beside the
         # chain); the chain's flags are read after the cost read-back (one host wait per step).
         # (Preparing the chain after the arg-max left the GPU idle ~1.1 ms per step before the
-        # chain: profiles/r4_bench_timeline_gaps.json.)
+        # chain in the traced timeline, tools/r4_bench_timeline.sh: 43.3 -> 42.6 ms per step.)
         sweep_launch()
         copy_batch(work, reload_src)
         apply_batch(work, layer_batch, sort=True, wait=False)
