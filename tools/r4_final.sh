@@ -21,3 +21,4 @@ rm -rf gpurun_out/fktrace
 timeout -k 10 900 bash tools/pmc_bench.sh
 rc=$?; echo "pmc rc=$rc" >> gpurun_out/final_steps.txt; [ $rc -eq 0 ] || exit $rc
 step fconfigs 400 python3 tools/configs_bench.py --configs 2,4,5 || exit $?
+step fbench 600 python3 bench.py || exit $?
