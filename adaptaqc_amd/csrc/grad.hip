@@ -406,21 +406,25 @@ __global__ __launch_bounds__(kT) void k_sweep_chain(const SweepJob* __restrict__
 template <int CAP>
 constexpr int kChain8Ld = CAP + 4;  // V row stride (complex)
 
-template <int CAP>
+// G first qubits per workgroup: 8 (default), or 16 (round-4 experiment: M_b read once per 16
+// chains, each MFMA step's B operands serving two row tiles -- measured slower, sweep_group())
+template <int CAP, int G>
 __global__ __launch_bounds__(4 * CAP) void k_sweep_chain8(const SweepJob* __restrict__ jobs, const int* __restrict__ alist,
                                                           int nal) {
   constexpr int NQ = CAP / 4, NT = 4 * CAP;  // CAP / 16 waves, one 16-column tile each
+  constexpr int R = 2 * G, RT = R / 16;      // rows (chain c, first-qubit value sa: 2c + sa), row tiles
+  static_assert(G == 8 || G == 16, "8 or 16 chains per workgroup");
   const SweepJob& j = jobs[blockIdx.y];
-  const int g0 = blockIdx.x * 8;
+  const int g0 = blockIdx.x * G;
   const int n = j.n;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  __shared__ cplx V[2][16][kChain8Ld<CAP>];
-  __shared__ int s_a[8];
-  if (tid < 8) s_a[tid] = g0 + tid < nal ? alist[g0 + tid] : n;  // n: never active
+  __shared__ cplx V[2][R][kChain8Ld<CAP>];
+  __shared__ int s_a[G];
+  if (tid < G) s_a[tid] = g0 + tid < nal ? alist[g0 + tid] : n;  // n: never active
   __syncthreads();
   const int amin = s_a[0];  // alist is ascending
   if (amin >= n - 1) return;  // uniform
-  for (int e = tid; e < 16 * CAP; e += NT) {
+  for (int e = tid; e < R * CAP; e += NT) {
     const int row = e / CAP, k = e % CAP, a = s_a[row >> 1];
     cplx v = aqc::cmk(0, 0);
     if (a < n - 1 && k < j.dims[a + 1]) v = j.v0[((size_t)a * 2 + (row & 1)) * CAP + k];
@@ -439,44 +443,57 @@ __global__ __launch_bounds__(4 * CAP) void k_sweep_chain8(const SweepJob* __rest
   int cur = 0;
   for (int b = amin + 1; b < n; ++b) {
     const int db = j.dims[b];
-    // T_ab[sa][sb] = sum_k v[sa][k] w_b[sb][k]: 16 lanes per row, waves 0-3
-    if (tid < 256) {
-      const int row = tid >> 4, sub = tid & 15, a = s_a[row >> 1];
-      const cplx* w0 = j.w + ((size_t)b * 2) * CAP;
-      cplx t0 = aqc::cmk(0, 0), t1 = aqc::cmk(0, 0);
-      for (int k = sub; k < db; k += 16) {
-        const cplx v = V[cur][row][k];
-        t0 = aqc::cfma(v, w0[k], t0);
-        t1 = aqc::cfma(v, w0[CAP + k], t1);
-      }
-      t0.x = aqc::row_sum16(t0.x);
-      t0.y = aqc::row_sum16(t0.y);
-      t1.x = aqc::row_sum16(t1.x);
-      t1.y = aqc::row_sum16(t1.y);
-      if (sub == 0 && a < b) {
-        cplx* T = j.T + ((size_t)a * n + b) * 4 + 2 * (row & 1);
-        T[0] = t0;
-        T[1] = t1;
+    // T_ab[sa][sb] = sum_k v[sa][k] w_b[sb][k]: 16 lanes per row
+    for (int base = 0; base < 16 * R; base += NT) {
+      const int t = base + tid;
+      if (t < 16 * R) {
+        const int row = t >> 4, sub = t & 15, a = s_a[row >> 1];
+        const cplx* w0 = j.w + ((size_t)b * 2) * CAP;
+        cplx t0 = aqc::cmk(0, 0), t1 = aqc::cmk(0, 0);
+        for (int k = sub; k < db; k += 16) {
+          const cplx v = V[cur][row][k];
+          t0 = aqc::cfma(v, w0[k], t0);
+          t1 = aqc::cfma(v, w0[CAP + k], t1);
+        }
+        t0.x = aqc::row_sum16(t0.x);
+        t0.y = aqc::row_sum16(t0.y);
+        t1.x = aqc::row_sum16(t1.x);
+        t1.y = aqc::row_sum16(t1.y);
+        if (sub == 0 && a < b) {
+          cplx* T = j.T + ((size_t)a * n + b) * 4 + 2 * (row & 1);
+          T[0] = t0;
+          T[1] = t1;
+        }
       }
     }
     if (b == n - 1) break;
     const auto rs = aqc::make_rsrc(j.M + (size_t)min(b + 1, n - 1) * CAP * CAP, CAP * CAP * 16);
-    aqc::d4_t cr0 = {0, 0, 0, 0}, ci0 = {0, 0, 0, 0}, cr1 = {0, 0, 0, 0}, ci1 = {0, 0, 0, 0};
+    aqc::d4_t cr0[RT], ci0[RT], cr1[RT], ci1[RT];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) cr0[rt] = ci0[rt] = cr1[rt] = ci1[rt] = aqc::d4_t{0, 0, 0, 0};
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
-      const cplx av = V[cur][li][4 * q + lk];
       const cplx bv = bq[q];
+      cplx av[RT];
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) av[rt] = V[cur][16 * rt + li][4 * q + lk];
       bq[q] = aqc::buf_ld(rs, voff, q * qstep);
-      cr0 = __builtin_amdgcn_mfma_f64_16x16x4f64(av.x, bv.x, cr0, 0, 0, 0);
-      ci0 = __builtin_amdgcn_mfma_f64_16x16x4f64(av.x, bv.y, ci0, 0, 0, 0);
-      cr1 = __builtin_amdgcn_mfma_f64_16x16x4f64(-av.y, bv.y, cr1, 0, 0, 0);
-      ci1 = __builtin_amdgcn_mfma_f64_16x16x4f64(av.y, bv.x, ci1, 0, 0, 0);
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) {
+        cr0[rt] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[rt].x, bv.x, cr0[rt], 0, 0, 0);
+        ci0[rt] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[rt].x, bv.y, ci0[rt], 0, 0, 0);
+        cr1[rt] = __builtin_amdgcn_mfma_f64_16x16x4f64(-av[rt].y, bv.y, cr1[rt], 0, 0, 0);
+        ci1[rt] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[rt].y, bv.x, ci1[rt], 0, 0, 0);
+      }
     }
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int row = lk + 4 * q;
-      const bool act = s_a[row >> 1] < b;
-      V[cur ^ 1][row][col] = act ? aqc::cmk(cr0[q] + cr1[q], ci0[q] + ci1[q]) : V[cur][row][col];
+    for (int rt = 0; rt < RT; ++rt) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int row = 16 * rt + lk + 4 * q;
+        const bool act = s_a[row >> 1] < b;
+        V[cur ^ 1][row][col] = act ? aqc::cmk(cr0[rt][q] + cr1[rt][q], ci0[rt][q] + ci1[rt][q]) : V[cur][row][col];
+      }
     }
     lds_barrier();
     cur ^= 1;
@@ -872,6 +889,17 @@ bool use_chain8(int cap, int ns) {
   if ((cap != 128 && cap != 64) || g_chain_mode == 1) return false;
   return g_chain_mode == 2 || ns >= 2;
 }
+// first qubits per grouped-chain workgroup: 8 (default) or AQC_SWEEP_GROUP=16 (measured slower:
+// config 4 34.3-34.8 M against 35.9-36.8 M evals/s, the bench's sweep chain 1.04 against 0.75 ms --
+// profiles/r4_sweep_group16_ab.json; 16 chains hold 135 KB of LDS at CAP = 128, one workgroup per
+// CU, and a group's later chains idle through more of its sites)
+int sweep_group() {
+  static const int g = [] {
+    const char* e = std::getenv("AQC_SWEEP_GROUP");
+    return (e && std::atoi(e) == 16) ? 16 : 8;
+  }();
+  return g;
+}
 
 SweepJob make_job(aqc_mps_t h, double* out) {
   SweepJob j;
@@ -1020,12 +1048,23 @@ int aqc_pair_grads_batch(aqc_mps_t* psis, int ns, const double* svec, const int*
     for (int a : alist) steps += (double)(n - 1 - a);
     if (!alist.empty()) {
       aqc::KernelTimer::begin(st, "grad_chain", ns * steps * c * c * 16.0, ns * steps * 2.0 * c * c * 8.0);
-      if (use_chain8(cap, ns) && cap == 128)
-        hipLaunchKernelGGL(k_sweep_chain8<128>, dim3((unsigned)(alist.size() + 7) / 8, ns), dim3(512), 0, st, djobs,
-                           (const int*)dalist, (int)alist.size());
-      else if (use_chain8(cap, ns))
-        hipLaunchKernelGGL(k_sweep_chain8<64>, dim3((unsigned)(alist.size() + 7) / 8, ns), dim3(256), 0, st, djobs,
-                           (const int*)dalist, (int)alist.size());
+      const bool g16 = sweep_group() == 16;
+      const unsigned ng = (unsigned)(alist.size() + (g16 ? 15 : 7)) / (g16 ? 16 : 8);
+      if (use_chain8(cap, ns) && cap == 128) {
+        if (g16)
+          hipLaunchKernelGGL((k_sweep_chain8<128, 16>), dim3(ng, ns), dim3(512), 0, st, djobs, (const int*)dalist,
+                             (int)alist.size());
+        else
+          hipLaunchKernelGGL((k_sweep_chain8<128, 8>), dim3(ng, ns), dim3(512), 0, st, djobs, (const int*)dalist,
+                             (int)alist.size());
+      } else if (use_chain8(cap, ns)) {
+        if (g16)
+          hipLaunchKernelGGL((k_sweep_chain8<64, 16>), dim3(ng, ns), dim3(256), 0, st, djobs, (const int*)dalist,
+                             (int)alist.size());
+        else
+          hipLaunchKernelGGL((k_sweep_chain8<64, 8>), dim3(ng, ns), dim3(256), 0, st, djobs, (const int*)dalist,
+                             (int)alist.size());
+      }
       else
         if (cap == 128)
           hipLaunchKernelGGL(k_sweep_chain_pf<128>, dim3((unsigned)alist.size(), ns), dim3(1024), 0, st, djobs,
