@@ -42,6 +42,15 @@ constexpr int kGramMaxK = 64;
 #endif
 // S5: the LDL^T pivots from the leading minors' recurrence (one FMA + the guard on the chain)
 // S5: inverse-iteration steps per eigenvector
+// S4: lanes per eigenvalue (kG, (kG + 1)-section) and rounds after the first 256-shift pass.  The
+// pass is FP64-issue-bound: 8 x 9-section x 9 rounds took 108 K ticks and 16 x 17 x 7 145 K against
+// 98 K (profiles/r4_s4_shapes_ab.json)
+#ifndef AQC_S4_G
+#define AQC_S4_G 4
+#endif
+#ifndef AQC_S4_ROUNDS
+#define AQC_S4_ROUNDS 12
+#endif
 #ifndef AQC_S5_ITERS
 #define AQC_S5_ITERS 3
 #endif
@@ -873,7 +882,8 @@ __device__ __noinline__ bool gram_svd_body_t(const TwoSiteJob& j) {
     // narrow it by 5^12 (span x 1.6e-11 at the end; the 1024-point pass + 17^6 of round 2 gave
     // 4e-11).  Waves 4-15 sit S4 out.  (Ratio form, 16 lanes x 17-section, 7 passes: 0.20 M
     // ticks; ratio form, 8 lanes x 9-section, 9 passes: 0.15 M.)
-    constexpr int kG = 4, kFirst = 256, kRounds = 12;
+    constexpr int kG = AQC_S4_G, kFirst = 256, kRounds = AQC_S4_ROUNDS;
+    static_assert(kG == 4 || kG == 8 || kG == 16, "lanes per eigenvalue");
     const int eid = tid / kG, sub = tid % kG;
     const int a = C - 1 - eid;  // ascending index of the eid-th largest eigenvalue
     int* cntb = reinterpret_cast<int*>(xbuf);
