@@ -199,17 +199,24 @@ def dptr(a):
 
 
 def ops_array(ops):
-    """[(matrix (2x2 or 4x4 complex), qubits tuple)] -> contiguous aqc_op_t array."""
-    arr = np.zeros(len(ops), dtype=OP_DTYPE)
-    for i, (m, qubits) in enumerate(ops):
-        m = np.asarray(m, dtype=np.complex128)
-        k = len(qubits)
-        arr[i]["nq"] = k
-        arr[i]["q0"] = qubits[0]
-        arr[i]["q1"] = qubits[1] if k == 2 else 0
-        flat = m.reshape(-1)
-        arr[i]["m"][: 2 * flat.size : 2] = flat.real
-        arr[i]["m"][1 : 2 * flat.size : 2] = flat.imag
+    """[(matrix (2x2 or 4x4 complex), qubits tuple)] -> contiguous aqc_op_t array (filled per
+    field over all ops at once: per-op structured-array stores cost ~6 us an op)."""
+    n = len(ops)
+    arr = np.zeros(n, dtype=OP_DTYPE)
+    if n == 0:
+        return arr
+    nq = np.fromiter((len(q) for _, q in ops), dtype=np.int32, count=n)
+    if not np.all((nq == 1) | (nq == 2)):
+        raise ValueError("ops_array: only 1- and 2-qubit ops")
+    arr["nq"] = nq
+    arr["q0"] = np.fromiter((q[0] for _, q in ops), dtype=np.int32, count=n)
+    arr["q1"] = np.fromiter((q[1] if len(q) == 2 else 0 for _, q in ops), dtype=np.int32, count=n)
+    m = arr["m"]
+    for k, width in ((1, 4), (2, 16)):
+        idx = np.flatnonzero(nq == k)
+        if idx.size:
+            mats = np.asarray([ops[i][0] for i in idx], dtype=np.complex128).reshape(idx.size, width)
+            m[idx, : 2 * width] = mats.view(np.float64)
     return arr
 
 

@@ -24,7 +24,7 @@ from types import SimpleNamespace
 
 import numpy as np
 
-from ..circuit import device_ops, mps_payload
+from ..circuit import device_ops_array, mps_payload
 from ..device import DeviceMPS
 from ..mps_operations import DevicePreprocessedMPS, apply_checked, chi_cap_for, zero_aer_mps
 from .aqc_backend import AQCBackend
@@ -119,7 +119,7 @@ class AerMPSBackend(AQCBackend):
         work = self._work
         work.set_truncation(thr, max_chi)
         work.copy_from(base)
-        apply_checked(work, device_ops(circuit, start))
+        apply_checked(work, device_ops_array(circuit, start))
         work.sort()
         return work
 

@@ -22,7 +22,7 @@ import os
 
 import numpy as np
 
-from ..circuit import device_ops
+from ..circuit import device_ops_array
 from ..device import DeviceSV
 from ..statevector import Statevector
 from .aqc_backend import AQCBackend
@@ -86,7 +86,7 @@ class SVSimulator:
 
         from .. import _lib
 
-        ops = _lib.ops_array(device_ops(circuit))
+        ops = device_ops_array(circuit)
         n = circuit.num_qubits
         key = ops.tobytes()
         if self._last is not None and self._last[0] == n and self._last[1] == key:
@@ -119,7 +119,7 @@ class AerSVBackend(AQCBackend):
             self._state = DeviceSV(n)
         else:
             self._state.reset()
-        self._state.apply(device_ops(circ))
+        self._state.apply(device_ops_array(circ))
         return self._state
 
     def evaluate_global_cost(self, compiler):

@@ -8,7 +8,7 @@ from __future__ import annotations
 
 import numpy as np
 
-from .circuit import QuantumCircuit, device_ops, mps_payload
+from .circuit import QuantumCircuit, device_ops_array, mps_payload
 from .device import DeviceMPS
 
 MAX_CHI_CAP = 512
@@ -94,7 +94,7 @@ def device_mps_from_circuit(circuit: QuantumCircuit, sim=None, trunc_thr=None, o
         out.load_aer(loaded)
     else:
         out.load_aer(zero_aer_mps(n))
-    apply_checked(out, device_ops(circuit, start))
+    apply_checked(out, device_ops_array(circuit, start))
     out.sort()
     return out
 

@@ -74,10 +74,10 @@ def calculate_entanglement_measure(method, circuit, qubit_1, qubit_2, backend, b
     name = _measure_name(method)
     kind = _kind(backend)
     if kind == "sv":
-        from ..circuit import device_ops
+        from ..circuit import device_ops_array
 
         st = DeviceSV(circuit.num_qubits)
-        st.apply(device_ops(circuit))
+        st.apply(device_ops_array(circuit))
         rho = st.pair_rdms([(qubit_1, qubit_2)])
     elif kind == "mps":
         from ..device import DeviceMPS
