@@ -244,7 +244,8 @@ constexpr int kPhaseDirectIn = 1 << 30, kPhaseDirectOut = 1 << 29, kPhaseSlotBit
 template <int NS>
 __global__ __launch_bounds__(4096 >> NS) void k_sv_tile_reg(cplx* __restrict__ state, const SegHeader* __restrict__ hdr,
                                                            const PhaseHdr* __restrict__ phases,
-                                                           const SegGate* __restrict__ gates, int from_zero) {
+                                                           const SegGate* __restrict__ gates, int from_zero,
+                                                           cplx* __restrict__ amp0_out) {
   constexpr int K = kRegTileBits, kThr = 4096 >> NS, kTB = K - NS, NA = 1 << NS;
   __shared__ cplx tile[1 << K];
   __shared__ SegGate gl[2][kPhaseMaxGates];
@@ -351,6 +352,9 @@ __global__ __launch_bounds__(4096 >> NS) void k_sv_tile_reg(cplx* __restrict__ s
     if (out_g) {
 #pragma unroll
       for (int r = 0; r < NA; ++r) aqc::stg(gaddr(r), a[r]);
+      // the apply's last pass hands <0...0|psi> (tile 0, thread 0, r = 0: global index 0) straight
+      // to the pinned host buffer, so aqc_sv_amp0 needs no copy of its own
+      if (amp0_out && blockIdx.x == 0 && tid == 0) *amp0_out = a[0];
     } else {
 #pragma unroll
       for (int r = 0; r < NA; ++r) tile[off[r]] = a[r];
@@ -360,6 +364,7 @@ __global__ __launch_bounds__(4096 >> NS) void k_sv_tile_reg(cplx* __restrict__ s
   if (!d_out) {
 #pragma unroll
     for (int r = 0; r < kPer; ++r) aqc::stg(state + gidx(tid + r * kThr), tile[swz(tid + r * kThr)]);
+    if (amp0_out && blockIdx.x == 0 && tid == 0) *amp0_out = tile[swz(0)];
   }
 }
 
@@ -885,6 +890,8 @@ struct aqc_sv_s {
   // |0...0> in its tiles instead of reading the state (no reset kernel, one 2^n read less); any
   // other reader materialises it first (sv_materialize)
   bool zero_pending = false;
+  // the last aqc_sv_apply's final pass wrote amp 0 to h_pinned[0] (valid once the stream is drained)
+  bool amp0_ready = false;
 };
 
 static int sv_materialize(aqc_sv_t h) {
@@ -993,16 +1000,18 @@ static bool sv_reg_tiles(int n) {
   return n >= kRegMinQubits && !(tile_env && std::strcmp(tile_env, "lds") == 0);
 }
 
-static int sv_launch_segment(aqc_sv_t h, const SegHeader* dh, const PhaseHdr* dp, const SegGate* dg, int nblocks,
+static int sv_launch_segment(aqc_sv_t h, const SegHeader* dh, const PhaseHdr* dp, const SegGate* dg, int nblocks, cplx* amp0_out,
                              double flops) {
   const int from_zero = h->zero_pending ? 1 : 0;
   const double bytes = (from_zero ? 16.0 : 32.0) * (double)(1ull << h->n);
   aqc::KernelTimer::begin(h->stream, "sv_segment", bytes, flops);
   if (h->reg_tiles) {
     if (sv_slots() == 3)
-      hipLaunchKernelGGL(k_sv_tile_reg<3>, dim3(nblocks), dim3(512), 0, h->stream, h->state, dh, dp, dg, from_zero);
+      hipLaunchKernelGGL(k_sv_tile_reg<3>, dim3(nblocks), dim3(512), 0, h->stream, h->state, dh, dp, dg, from_zero,
+                         amp0_out);
     else
-      hipLaunchKernelGGL(k_sv_tile_reg<4>, dim3(nblocks), dim3(256), 0, h->stream, h->state, dh, dp, dg, from_zero);
+      hipLaunchKernelGGL(k_sv_tile_reg<4>, dim3(nblocks), dim3(256), 0, h->stream, h->state, dh, dp, dg, from_zero,
+                         amp0_out);
     h->zero_pending = false;
     aqc::KernelTimer::end(h->stream);
     AQC_CHECK_LAUNCH();
@@ -1080,6 +1089,7 @@ int aqc_sv_destroy(aqc_sv_t h) {
 int aqc_sv_reset(aqc_sv_t h) {
   AQC_REQUIRE(h, "aqc_sv_reset: null handle");
   h->zero_pending = true;
+  h->amp0_ready = false;
   return h->reg_tiles ? AQC_OK : sv_materialize(h);
 }
 
@@ -1089,6 +1099,7 @@ int aqc_sv_copy(aqc_sv_t dst, const aqc_sv_t src) {
   int rc = sv_materialize(src);
   if (rc != AQC_OK) return rc;
   dst->zero_pending = false;  // overwritten below
+  dst->amp0_ready = false;
   AQC_HIP_CHECK(hipStreamSynchronize(src->stream));
   AQC_HIP_CHECK(hipMemcpyAsync(dst->state, src->state, sizeof(cplx) << dst->n,
                                hipMemcpyDeviceToDevice, dst->stream));
@@ -1108,6 +1119,7 @@ int aqc_sv_apply(aqc_sv_t h, const aqc_op_t* ops, int nops) {
     }
   }
   const int K = h->K;
+  h->amp0_ready = false;
   // Planned and launched in batches of 1, 2, 4, ... segments, each segment formed as it is needed
   // (SegBuilder): the host plans the next batch while the GPU runs the previous one, and the first
   // pass starts after one segment's planning (planned whole, the GPU waited out the ~150 us of host
@@ -1169,7 +1181,13 @@ int aqc_sv_apply(aqc_sv_t h, const aqc_op_t* ops, int nops) {
     const SegHeader* dh = reinterpret_cast<const SegHeader*>(h->d_plan + o_h);
     const PhaseHdr* dp = reinterpret_cast<const PhaseHdr*>(h->d_plan + o_p);
     const SegGate* dg = reinterpret_cast<const SegGate*>(h->d_plan + o_g);
-    for (size_t s = 0; s < nb && rc == AQC_OK; ++s) rc = sv_launch_segment(h, dh + s, dp, dg, nblocks, flops[s]);
+    // the apply's final segment (no op left to place) hands amp 0 to the pinned buffer
+    const bool final_batch = sb.remaining == 0 && h->reg_tiles;
+    for (size_t s = 0; s < nb && rc == AQC_OK; ++s) {
+      cplx* a0 = final_batch && s + 1 == nb ? h->h_pinned : nullptr;
+      rc = sv_launch_segment(h, dh + s, dp, dg, nblocks, a0, flops[s]);
+      if (rc == AQC_OK && a0) h->amp0_ready = true;
+    }
     off = al(end);
   }
   // (recorded on every path, so the next call never reuses the staging buffer under a live copy)
@@ -1205,7 +1223,9 @@ int aqc_sv_plan(int n, const aqc_op_t* ops, int nops, int* out) {
 int aqc_sv_amp0(aqc_sv_t h, double* re, double* im) {
   AQC_REQUIRE(h && re && im, "aqc_sv_amp0: null argument");
   if (int rc = sv_materialize(h)) return rc;
-  AQC_HIP_CHECK(hipMemcpyAsync(h->h_pinned, h->state, sizeof(cplx), hipMemcpyDeviceToHost, h->stream));
+  // after an apply the final pass already wrote it (amp0_ready); otherwise one small copy
+  if (!h->amp0_ready)
+    AQC_HIP_CHECK(hipMemcpyAsync(h->h_pinned, h->state, sizeof(cplx), hipMemcpyDeviceToHost, h->stream));
   AQC_HIP_CHECK(hipStreamSynchronize(h->stream));
   *re = h->h_pinned[0].x;
   *im = h->h_pinned[0].y;
@@ -1297,6 +1317,7 @@ int aqc_sv_get(aqc_sv_t h, double* out) {
 int aqc_sv_set(aqc_sv_t h, const double* in) {
   AQC_REQUIRE(h && in, "aqc_sv_set: null argument");
   h->zero_pending = false;  // overwritten
+  h->amp0_ready = false;
   AQC_HIP_CHECK(hipMemcpyAsync(h->state, in, sizeof(cplx) << h->n, hipMemcpyHostToDevice, h->stream));
   AQC_HIP_CHECK(hipStreamSynchronize(h->stream));
   return AQC_OK;

@@ -295,3 +295,33 @@ def test_deferred_reset_every_reader(sv_slots):
     bra.apply(dev_ops)
     t = bra.transition(ket, 3)
     np.testing.assert_allclose(t, [[np.conj(psi[0]), 0], [np.conj(psi[1 << 3]), 0]], atol=1e-15)
+
+
+def test_amp0_handed_off_by_the_final_pass(sv_slots):
+    """After an apply on the register-tile path the final pass writes <0...0|psi> to the pinned
+    host buffer and aqc_sv_amp0 reads it without a copy: equal to the state's first amplitude after
+    applies, an empty apply (state unchanged), a reset, a copy into the handle and a set."""
+    from adaptaqc_amd.circuit import device_ops
+    from adaptaqc_amd.device import DeviceSV
+
+    n = 15
+    ops_a = device_ops(to_circuit(n, brickwork(n, 4, 8)))
+    ops_b = device_ops(to_circuit(n, brickwork(n, 3, 9)))
+    d, e = DeviceSV(n), DeviceSV(n)
+    d.apply(ops_a)
+    a = d.amp0()
+    assert abs(a - d.get()[0]) == 0.0
+    d.apply([])  # no ops: the state and its handed-off amp 0 stay
+    assert d.amp0() == a
+    d.apply(ops_b)
+    b = d.amp0()
+    assert abs(b - d.get()[0]) == 0.0 and abs(b - a) > 1e-6
+    d.reset()
+    assert d.amp0() == 1.0
+    e.apply(ops_a)
+    d.copy_from(e)
+    assert d.amp0() == a
+    psi = np.zeros(2 ** n, complex)
+    psi[0], psi[5] = 0.6, 0.8
+    d.set(psi)
+    assert abs(d.amp0() - 0.6) < 1e-15
