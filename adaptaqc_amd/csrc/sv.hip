@@ -892,6 +892,10 @@ struct aqc_sv_s {
   bool zero_pending = false;
   // the last aqc_sv_apply's final pass wrote amp 0 to h_pinned[0] (valid once the stream is drained)
   bool amp0_ready = false;
+  // plans of an apply's second and later batches go over on this stream while the previous batch's
+  // passes run; the state's stream waits on the batch's event before its first pass
+  hipStream_t up_stream = nullptr;
+  hipEvent_t up_ev[2] = {nullptr, nullptr};
 };
 
 static int sv_materialize(aqc_sv_t h) {
@@ -1000,6 +1004,15 @@ static bool sv_reg_tiles(int n) {
   return n >= kRegMinQubits && !(tile_env && std::strcmp(tile_env, "lds") == 0);
 }
 
+// AQC_SV_SIDE_UPLOAD=0: every batch's plan on the state's stream (A/B)
+static bool sv_side_upload() {
+  static const bool on = [] {
+    const char* e = std::getenv("AQC_SV_SIDE_UPLOAD");
+    return !(e && std::strcmp(e, "0") == 0);
+  }();
+  return on;
+}
+
 static int sv_launch_segment(aqc_sv_t h, const SegHeader* dh, const PhaseHdr* dp, const SegGate* dg, int nblocks, cplx* amp0_out,
                              double flops) {
   const int from_zero = h->zero_pending ? 1 : 0;
@@ -1062,6 +1075,8 @@ int aqc_sv_create(int n, aqc_sv_t* out) {
   }
   AQC_HIP_CHECK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
   AQC_HIP_CHECK(hipEventCreateWithFlags(&h->plan_ev, hipEventDisableTiming));
+  AQC_HIP_CHECK(hipStreamCreateWithFlags(&h->up_stream, hipStreamNonBlocking));
+  for (auto& e : h->up_ev) AQC_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   h->zwg = (int)((dim + kThreads * kZChunk - 1) / (kThreads * kZChunk));
   AQC_HIP_CHECK(hipMalloc(&h->d_zpart, sizeof(double) * (size_t)h->zwg * (n + 1)));
   AQC_HIP_CHECK(hipMalloc(&h->d_z, sizeof(double) * (n + 1)));
@@ -1081,6 +1096,9 @@ int aqc_sv_destroy(aqc_sv_t h) {
   hipFree(h->d_z);
   if (h->d_scratch) hipFree(h->d_scratch);
   if (h->h_pinned) hipHostFree(h->h_pinned);
+  if (h->up_stream) hipStreamSynchronize(h->up_stream), hipStreamDestroy(h->up_stream);
+  for (hipEvent_t e : h->up_ev)
+    if (e) hipEventDestroy(e);
   if (h->stream) hipStreamDestroy(h->stream);
   delete h;
   return AQC_OK;
@@ -1176,8 +1194,16 @@ int aqc_sv_apply(aqc_sv_t h, const aqc_op_t* ops, int nops) {
     if (!gts.empty()) std::memcpy(h->h_plan + o_g, gts.data(), sizeof(SegGate) * gts.size());
     // (by a copy kernel, aqc::upload_async: the SDMA transfers hipMemcpyAsync used for the larger
     // batches cost ~10-25 us of idle GPU each in the config-2 timeline)
-    rc = aqc::upload_async(h->d_plan + o_h, h->h_plan + o_h, end - o_h, h->stream);
-    if (rc != AQC_OK) break;
+    if (nb_done > 0 && sv_side_upload()) {
+      // (the batch's plan region is fresh: no pass reads it before the event below)
+      hipEvent_t ev = h->up_ev[nb_done & 1];
+      AQC_HIP_CHECK(hipMemcpyAsync(h->d_plan + o_h, h->h_plan + o_h, end - o_h, hipMemcpyHostToDevice, h->up_stream));
+      AQC_HIP_CHECK(hipEventRecord(ev, h->up_stream));
+      AQC_HIP_CHECK(hipStreamWaitEvent(h->stream, ev, 0));
+    } else {
+      rc = aqc::upload_async(h->d_plan + o_h, h->h_plan + o_h, end - o_h, h->stream);
+      if (rc != AQC_OK) break;
+    }
     const SegHeader* dh = reinterpret_cast<const SegHeader*>(h->d_plan + o_h);
     const PhaseHdr* dp = reinterpret_cast<const PhaseHdr*>(h->d_plan + o_p);
     const SegGate* dg = reinterpret_cast<const SegGate*>(h->d_plan + o_g);
