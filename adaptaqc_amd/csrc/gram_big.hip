@@ -20,14 +20,18 @@
 //                 hand-off form of the MI355X guide's "Valid forms" table, row 1).  From p every
 //                 workgroup forms w = p - tau/2 (p^H v) v and, from the old row k + 1, the new row
 //                 k + 1 = old - conj(w) - w_{k+1} conj(v): the next column needs no second hand-off.
-//                 One exchange per column; spins bounded (100 ms, then the job declines).
+//                 One exchange per column; spins bounded (100 ms, then the job declines).  Stops at
+//                 column C - 128 (aqc_gb_set_tail, the default) and leaves the trailing block to:
+//   k_gb_tail     the last 128 columns of a job in one workgroup (exchange through the LDS, wave 0
+//                 forms the reflectors); on the side stream, beside the next round's k_gb_tridiag.
 //   k_gb_eig      the top K eigenvalues of T by multisection with the polynomial Sturm count, 64
 //                 per workgroup;
 //   k_gb_inv      inverse iteration (LDL^T of T - lambda I, three solves, one lane per vector,
 //                 vectors in a per-job scratch), sigma^2 = z^T T z; declines (status 2) unless
 //                 lambda_K > 1e-9 lambda_1, as the 2 chi = 128 path does;
 //   k_gb_gs       Gram-Schmidt inside clusters of close eigenvalues.
-//   k_gb_tfac     compact WY factors T of the reflectors in blocks of 16 (LAPACK zlarft).
+//   k_gb_tfac     compact WY factors T of the reflectors in blocks of 16 (LAPACK zlarft), on a
+//                 third stream beside k_gb_eig / k_gb_inv / k_gb_gs.
 //   k_gb_back     V = Q Z on the matrix cores, 16 columns per workgroup, blocks of 16 reflectors
 //                 from the last (V -= Y T Y^H V); output W = V Sigma, sig, qr = 1 -- the contract of the
 //                 2 chi = 128 Gram path (work column c = right singular vector c of X times
