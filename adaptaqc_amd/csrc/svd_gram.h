@@ -66,6 +66,12 @@ __device__ unsigned long long g_gram_ticks[12];
 #ifndef AQC_S3_DIAG
 #define AQC_S3_DIAG 0
 #endif
+// S6: the compact-WY factors T of every reflector block computed during S5 by the idle waves 4..11
+// (S = Y^H Y on the matrix cores, zlarft), read back per block -- off the block loop's critical path
+// (there wave 5 ran the 16-step zlarft chain between B2 and B3 while the other waves waited)
+#ifndef AQC_S6_TPRE
+#define AQC_S6_TPRE 1
+#endif
 // S6: the next block's reflectors fetched after B4 (see the block loop)
 #ifndef AQC_S6_LATE_FETCH
 #define AQC_S6_LATE_FETCH 1
@@ -223,6 +229,11 @@ __device__ __forceinline__ double rcp_nr(double x) {
   r = r * fma(-x, r, 2.0);
   return r;
 }
+
+// S6's precomputed compact-WY factors in the work buffer: after the reflectors (at most 8128 complex
+// at C = 128) and clear of the output W written after S6's loop, 512 complex per block (S, then T)
+constexpr size_t kTfacOff = 8192;
+typedef __attribute__((address_space(1))) double gdbl_t;
 
 // The lower-triangle tridiagonalisation of svd_tri.h (defined there), which gram_svd_body<true>
 // runs at 1024 threads in place of its full-matrix S3
@@ -1052,6 +1063,55 @@ __device__ __noinline__ bool gram_svd_body_t(const TwoSiteJob& j) {
     }
     if (tid == 0) atomicAdd(&g_gram_ticks[7], __builtin_amdgcn_s_memtime() - t_last);  // S5 A: inverse iteration
   }
+#if AQC_S6_TPRE
+  else if (wave >= 4 && wave < 4 + ((C - 1 + 15) >> 4)) {  // (uniform per wave)
+    // block b of S6's loop (reflectors k0 .. k1 - 1, counted from the last): S = Y^H Y, then T by
+    // zlarft, into the work scratch after the reflectors (S at [0, 256), T at [256, 512) of the
+    // block's 512).  Read back through agent-scope loads: the same addresses were read by the
+    // previous update's S6 on this CU, so the L1 may hold them.
+    const int b = wave - 4, k1 = C - 1 - 16 * b, k0 = k1 > 16 ? k1 - 16 : 0, nb = k1 - k0;
+    const int li = lane & 15, lk = lane >> 4;
+    aqc::d4_t sr = {0, 0, 0, 0}, si = {0, 0, 0, 0};
+    for (int r0 = 0; r0 < C; r0 += 4) {  // A[m = i][k = row] = conj(Y[row][i]), B = Y
+      const int row = r0 + lk, k = k0 + li;
+      const cplx y = (li < nb && row > k && row < C) ? aqc::ldg(hh + (size_t)k * (2 * C - k - 1) / 2 + (row - k - 1))
+                                                     : aqc::cmk(0, 0);
+      sr = __builtin_amdgcn_mfma_f64_16x16x4f64(y.x, y.x, sr, 0, 0, 0);
+      sr = __builtin_amdgcn_mfma_f64_16x16x4f64(y.y, y.y, sr, 0, 0, 0);
+      si = __builtin_amdgcn_mfma_f64_16x16x4f64(y.x, y.y, si, 0, 0, 0);
+      si = __builtin_amdgcn_mfma_f64_16x16x4f64(-y.y, y.x, si, 0, 0, 0);
+    }
+    cplx* Sg = hh + kTfacOff + (size_t)b * 512;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) aqc::stg(Sg + (lk + 4 * q) * 16 + li, aqc::cmk(sr[q], si[q]));
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // zlarft (forward, columnwise): lane (a, g) holds T[a][g + 4 m]; T[a][i] = -tau_i sum_{a <= bb < i}
+    // T[a][bb] S[bb][i], T[i][i] = tau_i -- the recurrence of the in-loop form
+    const int a = lane >> 2, g = lane & 3;
+    cplx tq[4] = {aqc::cmk(0, 0), aqc::cmk(0, 0), aqc::cmk(0, 0), aqc::cmk(0, 0)};
+    for (int i = 0; i < 16; ++i) {
+      const cplx tau = i < nb ? s_tau[k0 + i] : aqc::cmk(0, 0);
+      cplx acc = aqc::cmk(0, 0);
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const int bb = g + 4 * m;
+        if (4 * m < i && bb < i) {
+          const gdbl_t* sp = (const gdbl_t*)(const double*)(Sg + bb * 16 + i);
+          const cplx sv = aqc::cmk(__hip_atomic_load(sp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                                   __hip_atomic_load(sp + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+          acc = aqc::cfma(tq[m], sv, acc);
+        }
+      }
+      acc.x = aqc::row_sum4(acc.x);
+      acc.y = aqc::row_sum4(acc.y);
+      const cplx ti = aqc::cmul(tau, acc);
+      const cplx val = a < i ? aqc::cmk(-ti.x, -ti.y) : (a == i ? tau : aqc::cmk(0, 0));
+      if (g == (i & 3)) tq[i >> 2] = val;
+    }
+#pragma unroll
+    for (int m = 0; m < 4; ++m) aqc::stg(Sg + 256 + a * 16 + g + 4 * m, tq[m]);
+  }
+#endif
   __syncthreads();
   if (wave == 0) {  // Gram-Schmidt inside clusters (uniform loop over wave 0)
     // clusters: gaps below 1e-7 ||T|| (dstein's 1e-3 is far more conservative than three
@@ -1157,6 +1217,13 @@ __device__ __noinline__ bool gram_svd_body_t(const TwoSiteJob& j) {
       const int e = tid + 1024 * u, row = e >> 4, i = e & 15;
       Yl[row * 16 + (i ^ (row & 15))] = ynx[u];
     }
+#if AQC_S6_TPRE
+    if (tid < 256) {  // this block's T from S5 (agent-scope loads: see the precompute)
+      const gdbl_t* tp = (const gdbl_t*)(const double*)(hh + kTfacOff + (size_t)((C - 1 - k1) >> 4) * 512 + 256 + tid);
+      Tl[(tid >> 4) * 17 + (tid & 15)] = aqc::cmk(__hip_atomic_load(tp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                                                  __hip_atomic_load(tp + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    }
+#endif
 #if !AQC_S6_LATE_FETCH
     if (k0 > 0) {  // the next block's reflectors, in flight during this one
       const int n1 = k0, n0 = n1 > 16 ? n1 - 16 : 0;
@@ -1177,7 +1244,7 @@ __device__ __noinline__ bool gram_svd_body_t(const TwoSiteJob& j) {
           wr = __builtin_amdgcn_mfma_f64_16x16x4f64(y.y, vim[t][s], wr, 0, 0, 0);
           wi = __builtin_amdgcn_mfma_f64_16x16x4f64(y.x, vim[t][s], wi, 0, 0, 0);
           wi = __builtin_amdgcn_mfma_f64_16x16x4f64(-y.y, vre[t][s], wi, 0, 0, 0);
-          if (mg == nt) {
+          if (!AQC_S6_TPRE && mg == nt) {
             sr = __builtin_amdgcn_mfma_f64_16x16x4f64(y.x, y.x, sr, 0, 0, 0);
             sr = __builtin_amdgcn_mfma_f64_16x16x4f64(y.y, y.y, sr, 0, 0, 0);
             si = __builtin_amdgcn_mfma_f64_16x16x4f64(y.x, y.y, si, 0, 0, 0);
@@ -1191,7 +1258,7 @@ __device__ __noinline__ bool gram_svd_body_t(const TwoSiteJob& j) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) Pw[((mg - 1) * 4 + nt) * 256 + (lk + 4 * q) * 16 + li] = aqc::cmk(wr[q], wi[q]);
     }
-    if (mg == nt && mg != 1) {
+    if (!AQC_S6_TPRE && mg == nt && mg != 1) {
       const int slot = mg == 0 ? 0 : mg - 1;
 #pragma unroll
       for (int q = 0; q < 4; ++q) Ps[slot * 256 + (lk + 4 * q) * 16 + li] = aqc::cmk(sr[q], si[q]);
@@ -1206,7 +1273,7 @@ __device__ __noinline__ bool gram_svd_body_t(const TwoSiteJob& j) {
         for (int m = 0; m < 3; ++m) w = aqc::cadd(w, Pw[(m * 4 + nt) * 256 + b * 16 + li]);
         W1l[b * 64 + 16 * nt + li] = w;
       }
-    } else if (wave == 5) {  // S, then T (zlarft: T[a][i] = -tau_i sum_{a <= b < i} T[a][b] S[b][i])
+    } else if (!AQC_S6_TPRE && wave == 5) {  // S, then T (zlarft: T[a][i] = -tau_i sum_{a <= b < i} T[a][b] S[b][i])
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int b = lk + 4 * q;
