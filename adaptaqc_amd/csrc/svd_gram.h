@@ -72,6 +72,10 @@ __device__ unsigned long long g_gram_ticks[12];
 #ifndef AQC_S6_TPRE
 #define AQC_S6_TPRE 1
 #endif
+// S6 with the precomputed T: W2 = T (Y^H V) on the matrix cores inside the mg == 0 waves (no B3)
+#ifndef AQC_S6_W2MFMA
+#define AQC_S6_W2MFMA 1
+#endif
 // S6: the next block's reflectors fetched after B4 (see the block loop)
 #ifndef AQC_S6_LATE_FETCH
 #define AQC_S6_LATE_FETCH 1
@@ -1264,7 +1268,31 @@ __device__ __noinline__ bool gram_svd_body_t(const TwoSiteJob& j) {
       for (int q = 0; q < 4; ++q) Ps[slot * 256 + (lk + 4 * q) * 16 + li] = aqc::cmk(sr[q], si[q]);
     }
     __syncthreads();  // B2: partials
-    if (mg == 0) {  // Y^H V of column tile nt
+    if (AQC_S6_TPRE && AQC_S6_W2MFMA && mg == 0) {
+      // Y^H V of column tile nt summed in registers, then W2 = T (Y^H V) for that tile on the matrix
+      // cores right here: the sum's D layout (row lk + 4 q, column li) is the B operand of k-step q
+      // and T (in the LDS since B1) the A operand -- no W1 round trip through the LDS, no B3
+      aqc::d4_t br, bi, w2r = {0, 0, 0, 0}, w2i = {0, 0, 0, 0};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int b = lk + 4 * q;
+        cplx w = aqc::cmk(wr[q], wi[q]);
+#pragma unroll
+        for (int m = 0; m < 3; ++m) w = aqc::cadd(w, Pw[(m * 4 + nt) * 256 + b * 16 + li]);
+        br[q] = w.x;
+        bi[q] = w.y;
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const cplx t = Tl[li * 17 + 4 * q + lk];  // A[m = li][k = lk] = T[li][4 q + lk]
+        w2r = __builtin_amdgcn_mfma_f64_16x16x4f64(t.x, br[q], w2r, 0, 0, 0);
+        w2r = __builtin_amdgcn_mfma_f64_16x16x4f64(-t.y, bi[q], w2r, 0, 0, 0);
+        w2i = __builtin_amdgcn_mfma_f64_16x16x4f64(t.x, bi[q], w2i, 0, 0, 0);
+        w2i = __builtin_amdgcn_mfma_f64_16x16x4f64(t.y, br[q], w2i, 0, 0, 0);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) W2l[(lk + 4 * q) * 64 + 16 * nt + li] = aqc::cmk(w2r[q], w2i[q]);
+    } else if (mg == 0) {  // Y^H V of column tile nt
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int b = lk + 4 * q;
@@ -1309,6 +1337,7 @@ __device__ __noinline__ bool gram_svd_body_t(const TwoSiteJob& j) {
         for (int m = 0; m < 4; ++m) Tl[a * 17 + g + 4 * m] = tq[m];
       }
     }
+#if !(AQC_S6_TPRE && AQC_S6_W2MFMA)
     __syncthreads();  // B3: Y^H V, T
     {  // W2 = T (Y^H V): row i = wave (uniform), column = lane
       const int i = wave;
@@ -1316,6 +1345,7 @@ __device__ __noinline__ bool gram_svd_body_t(const TwoSiteJob& j) {
       for (int bb = i; bb < 16; ++bb) acc = aqc::cfma(Tl[i * 17 + bb], W1l[bb * 64 + lane], acc);
       W2l[i * 64 + lane] = acc;
     }
+#endif
     __syncthreads();  // B4: W2
 #if AQC_S6_LATE_FETCH
     // the next block's reflectors, in flight during the V update: issued before B1 they were
