@@ -72,6 +72,12 @@ __device__ unsigned long long g_gram_ticks[12];
 #ifndef AQC_S6_TPRE
 #define AQC_S6_TPRE 1
 #endif
+// S6's precompute on the waves 1-3, 5-7, 9-11 (not the waves 4 and 8, which share SIMD 0 with
+// wave 0's inverse iteration) instead of the waves 4..11
+#ifndef AQC_S6_TPRE_SKIP0
+#define AQC_S6_TPRE_SKIP0 0
+#endif
+static_assert(kGramMaxK <= 64, "S5: the inverse iteration (tid < K) must stay on wave 0");
 // S6 with the precomputed T: W2 = T (Y^H V) on the matrix cores inside the mg == 0 waves (no B3)
 #ifndef AQC_S6_W2MFMA
 #define AQC_S6_W2MFMA 1
@@ -1068,12 +1074,13 @@ __device__ __noinline__ bool gram_svd_body_t(const TwoSiteJob& j) {
     if (tid == 0) atomicAdd(&g_gram_ticks[7], __builtin_amdgcn_s_memtime() - t_last);  // S5 A: inverse iteration
   }
 #if AQC_S6_TPRE
-  else if (wave >= 4 && wave < 4 + ((C - 1 + 15) >> 4)) {  // (uniform per wave)
+  else if (AQC_S6_TPRE_SKIP0 ? ((wave & 3) != 0 && wave - 1 - (wave >> 2) < ((C - 1 + 15) >> 4))
+                              : (wave >= 4 && wave < 4 + ((C - 1 + 15) >> 4))) {  // (uniform per wave)
     // block b of S6's loop (reflectors k0 .. k1 - 1, counted from the last): S = Y^H Y, then T by
     // zlarft, into the work scratch after the reflectors (S at [0, 256), T at [256, 512) of the
     // block's 512).  Read back through agent-scope loads: the same addresses were read by the
     // previous update's S6 on this CU, so the L1 may hold them.
-    const int b = wave - 4, k1 = C - 1 - 16 * b, k0 = k1 > 16 ? k1 - 16 : 0, nb = k1 - k0;
+    const int b = AQC_S6_TPRE_SKIP0 ? wave - 1 - (wave >> 2) : wave - 4, k1 = C - 1 - 16 * b, k0 = k1 > 16 ? k1 - 16 : 0, nb = k1 - k0;
     const int li = lane & 15, lk = lane >> 4;
     aqc::d4_t sr = {0, 0, 0, 0}, si = {0, 0, 0, 0};
     for (int r0 = 0; r0 < C; r0 += 4) {  // A[m = i][k = row] = conj(Y[row][i]), B = Y
