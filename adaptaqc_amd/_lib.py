@@ -19,21 +19,22 @@ OP_DTYPE = np.dtype(
 )
 assert OP_DTYPE.itemsize == 272
 
-# every symbol declared in include/aqc_hip.h
+# every symbol declared in include/aqc_hip.h (the drop-in boundary) and include/aqc_hip_diag.h
+# (diagnostics and test hooks)
 EXPORTS = (
     "aqc_last_error", "aqc_version", "aqc_init", "aqc_finalize", "aqc_timing_enable",
     "aqc_timing_query", "aqc_timing_reset",
-    "aqc_sv_create", "aqc_sv_destroy", "aqc_sv_reset", "aqc_sv_copy", "aqc_sv_apply", "aqc_sv_plan", "aqc_sv_set_slots",
+    "aqc_sv_create", "aqc_sv_destroy", "aqc_sv_reset", "aqc_sv_copy", "aqc_sv_apply", "aqc_sv_plan",
     "aqc_sv_amp0", "aqc_sv_z_all", "aqc_sv_get", "aqc_sv_set",
     "aqc_mps_create", "aqc_mps_destroy", "aqc_mps_set_truncation", "aqc_mps_set_vidal",
     "aqc_mps_get_vidal", "aqc_mps_get_dims", "aqc_mps_copy", "aqc_mps_copy_batch", "aqc_mps_apply",
     "aqc_mps_apply_batch", "aqc_mps_apply_sort_batch", "aqc_mps_apply_sort_batch_async", "aqc_mps_check_batch", "aqc_mps_sort", "aqc_mps_sort_batch", "aqc_mps_overlap_zero",
     "aqc_mps_overlap_zero_batch", "aqc_mps_dot", "aqc_mps_z_all", "aqc_mps_amps_hw1",
     "aqc_pair_grads", "aqc_pair_grads_batch", "aqc_argmax_scaled", "aqc_mps_jacobi_stats",
-    "aqc_mps_set_jacobi_tol", "aqc_mps_set_jacobi_stop", "aqc_mps_set_fused_chain", "aqc_mps_set_chain_threads", "aqc_mps_chain_ticks", "aqc_svd_debug",
+    "aqc_mps_set_jacobi_tol", "aqc_mps_set_jacobi_stop", "aqc_mps_set_fused_chain", "aqc_mps_chain_ticks", "aqc_svd_debug",
     "aqc_sv_pair_rdms", "aqc_mps_pair_rdms", "aqc_mps_pair_rdms_batch", "aqc_entanglement_measures",
     "aqc_sv_transition", "aqc_mps_product_fit", "aqc_mps_set_svd_path", "aqc_svd_gram_ticks", "aqc_bj_ticks",
-    "aqc_sweep_set_chain_mode", "aqc_mps_set_jacobi_noise", "aqc_stream_join", "aqc_stream_wait", "aqc_svd_gram_stats",
+    "aqc_sweep_set_chain_mode", "aqc_stream_join", "aqc_stream_wait", "aqc_svd_gram_stats",
     "aqc_comm_unique_id", "aqc_comm_init", "aqc_comm_destroy", "aqc_comm_rank", "aqc_allgather_f64",
     "aqc_allgather_f64_host", "aqc_allreduce_max_f64", "aqc_svd_gram_big_stats", "aqc_svd_gram_big_ticks",
     "aqc_gb_set_spin_limit", "aqc_gb_set_tail", "aqc_debug_hog", "aqc_pool_stats",
@@ -68,7 +69,6 @@ _SIGS = {
     "aqc_sv_copy": ([_P, _P], _I),
     "aqc_sv_apply": ([_P, _P, _I], _I),
     "aqc_sv_plan": ([_I, _P, _I, _P], _I),
-    "aqc_sv_set_slots": ([_I], _I),
     "aqc_sv_amp0": ([_P, _DP, _DP], _I),
     "aqc_sv_z_all": ([_P, _DP], _I),
     "aqc_sv_get": ([_P, _P], _I),
@@ -100,7 +100,6 @@ _SIGS = {
     "aqc_mps_set_jacobi_tol": ([_D], _I),
     "aqc_mps_set_jacobi_stop": ([_D], _I),
     "aqc_mps_set_fused_chain": ([_I], _I),
-    "aqc_mps_set_chain_threads": ([_I], _I),
     "aqc_mps_chain_ticks": ([_P], _I),
     "aqc_svd_debug": ([_P, _I, _I, _I, _I, _P, _P, _P, _P], _I),
     "aqc_sv_pair_rdms": ([_P, _P, _I, _P], _I),
@@ -123,7 +122,6 @@ _SIGS = {
     "aqc_allgather_f64": ([_P, _P, _P, ctypes.c_size_t], _I),
     "aqc_allgather_f64_host": ([_P, _P, _P, ctypes.c_size_t], _I),
     "aqc_allreduce_max_f64": ([_P, _DP], _I),
-    "aqc_mps_set_jacobi_noise": ([_D], _I),
     "aqc_svd_gram_big_stats": ([_P], _I),
     "aqc_svd_gram_big_ticks": ([_P], _I),
     "aqc_gb_set_spin_limit": ([_D], _I),

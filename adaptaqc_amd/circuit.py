@@ -383,9 +383,26 @@ def _memo_put(circuit, start, entries):
     _OPS_MEMO[key] = (ref, start, entries)
 
 
+def _from_tables(op):
+    """True when op's matrix comes from the gate tables by (name, params) alone -- this IR's
+    Operation, or a qiskit-shaped standard gate -- so equal names and parameters mean equal rows.
+    A custom gate's matrix comes from its own to_matrix() / definition, which its name and
+    parameters need not determine."""
+    if isinstance(op, Operation):
+        return True
+    name = op.name
+    n = getattr(op, "num_qubits", None)
+    if name in _SKIP_NAMES or name == "ccx":
+        return True
+    return (n == 1 and (name in G.CONST_1Q or name in ONE_Q)) or (n == 2 and name in TWO_Q)
+
+
 def _params_snapshot(op):
     """The gate's parameters as a list for equality checks, or None when they are not plain numbers
-    (a unitary's matrix, symbolic parameters): such gates are re-converted every time."""
+    (a unitary's matrix, symbolic parameters) or the matrix does not come from the gate tables
+    (a custom gate): such gates are re-converted every time."""
+    if not _from_tables(op):
+        return None
     ps = list(getattr(op, "params", ()))
     for p in ps:
         if not isinstance(p, (int, float, complex, np.number)):
@@ -412,7 +429,8 @@ def device_ops_array(circuit, start: int = 0):
         c = old[k] if k < len(old) else None
         if c is not None:
             cop, cps, cqs, cblock = c
-            if (cps is not None and cqs == qs and (cop is op or cop.name == op.name)
+            if (cps is not None and cqs == qs
+                    and (cop is op or (type(cop) is type(op) and cop.name == op.name))
                     and list(getattr(op, "params", ())) == cps):
                 entries.append(c)
                 blocks.append(cblock)

@@ -9,6 +9,7 @@
 #include <vector>
 
 #include "../../include/aqc_hip.h"
+#include "../../include/aqc_hip_diag.h"
 
 namespace aqc {
 
@@ -162,8 +163,11 @@ int upload_async(void* dst, const void* pinned_src, size_t bytes, hipStream_t st
 // Blocks freed by the library go to a per-device free list keyed by size (4 KB granules) and are
 // handed out again to the next request of that size: handle creation and destruction (a batched
 // Rotoselect gate creates and drops its candidate states) cost a list lookup instead of hipMalloc /
-// hipFree, whose implicit device synchronisation took ~0.25 ms per MPS handle.  The caller frees
-// only memory no queued work still uses (the same rule as hipFree's).  The cache holds at most
+// hipFree, whose implicit device synchronisation took ~0.25 ms per MPS handle.  Unlike hipFree,
+// dev_free does not synchronise: the caller frees only memory that no queued work on any stream
+// still uses.  Each handle's destroy drains its own stream first, and every kernel or copy that
+// reads a handle's buffers on another stream (aqc_sv_copy) makes the owner's stream wait on an
+// event recorded after it, so that drain covers the reader too.  The cache holds at most
 // AQC_POOL_MB (default 8192) MB; an allocation that fails first releases the cache and retries.
 // aqc_finalize returns every cached block to the runtime.
 void* dev_alloc(size_t bytes);

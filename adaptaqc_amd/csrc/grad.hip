@@ -889,17 +889,10 @@ bool use_chain8(int cap, int ns) {
   if ((cap != 128 && cap != 64) || g_chain_mode == 1) return false;
   return g_chain_mode == 2 || ns >= 2;
 }
-// first qubits per grouped-chain workgroup: 8 (default) or AQC_SWEEP_GROUP=16 (measured slower:
-// config 4 34.3-34.8 M against 35.9-36.8 M evals/s, the bench's sweep chain 1.04 against 0.75 ms --
-// profiles/r4_sweep_group16_ab.json; 16 chains hold 135 KB of LDS at CAP = 128, one workgroup per
-// CU, and a group's later chains idle through more of its sites)
-int sweep_group() {
-  static const int g = [] {
-    const char* e = std::getenv("AQC_SWEEP_GROUP");
-    return (e && std::atoi(e) == 16) ? 16 : 8;
-  }();
-  return g;
-}
+// first qubits per grouped-chain workgroup: 8 (16 measured slower: config 4 34.3-34.8 M against
+// 35.9-36.8 M evals/s, profiles/r4_sweep_group16_ab.json; 16 chains hold 135 KB of LDS at CAP = 128,
+// one workgroup per CU, and a group's later chains idle through more of its sites)
+constexpr int kSweepGroup = 8;
 
 SweepJob make_job(aqc_mps_t h, double* out) {
   SweepJob j;
@@ -1048,22 +1041,13 @@ int aqc_pair_grads_batch(aqc_mps_t* psis, int ns, const double* svec, const int*
     for (int a : alist) steps += (double)(n - 1 - a);
     if (!alist.empty()) {
       aqc::KernelTimer::begin(st, "grad_chain", ns * steps * c * c * 16.0, ns * steps * 2.0 * c * c * 8.0);
-      const bool g16 = sweep_group() == 16;
-      const unsigned ng = (unsigned)(alist.size() + (g16 ? 15 : 7)) / (g16 ? 16 : 8);
+      const unsigned ng = (unsigned)(alist.size() + kSweepGroup - 1) / kSweepGroup;
       if (use_chain8(cap, ns) && cap == 128) {
-        if (g16)
-          hipLaunchKernelGGL((k_sweep_chain8<128, 16>), dim3(ng, ns), dim3(512), 0, st, djobs, (const int*)dalist,
-                             (int)alist.size());
-        else
-          hipLaunchKernelGGL((k_sweep_chain8<128, 8>), dim3(ng, ns), dim3(512), 0, st, djobs, (const int*)dalist,
-                             (int)alist.size());
+        hipLaunchKernelGGL((k_sweep_chain8<128, kSweepGroup>), dim3(ng, ns), dim3(512), 0, st, djobs,
+                           (const int*)dalist, (int)alist.size());
       } else if (use_chain8(cap, ns)) {
-        if (g16)
-          hipLaunchKernelGGL((k_sweep_chain8<64, 16>), dim3(ng, ns), dim3(256), 0, st, djobs, (const int*)dalist,
-                             (int)alist.size());
-        else
-          hipLaunchKernelGGL((k_sweep_chain8<64, 8>), dim3(ng, ns), dim3(256), 0, st, djobs, (const int*)dalist,
-                             (int)alist.size());
+        hipLaunchKernelGGL((k_sweep_chain8<64, kSweepGroup>), dim3(ng, ns), dim3(256), 0, st, djobs, (const int*)dalist,
+                           (int)alist.size());
       }
       else
         if (cap == 128)

@@ -1238,20 +1238,10 @@ int run_gram_big(const TwoSiteJob* hjobs, const TwoSiteJob* jobs, int nj, int ca
   const int per_round = std::min(240, resident) / P;
   // the eigenpairs and back-transformation of a round's jobs run on a second stream, beside the next
   // round's tridiagonalisation (which leaves CUs free: 9 of 24 config-5 jobs hold 144 of 256)
-  static int overlap = -1;  // AQC_GB_OVERLAP=0: everything on the library stream (A/B)
-  if (overlap < 0) {
-    const char* e = std::getenv("AQC_GB_OVERLAP");
-    overlap = (e && std::strcmp(e, "0") == 0) ? 0 : 1;
-  }
-  hipStream_t s2 = overlap ? gb_side_stream() : st;
+  hipStream_t s2 = gb_side_stream();
   // the compact-WY factors need only the reflectors: on a third stream beside the eigenvalues,
   // inverse iteration and Gram-Schmidt (which need only T), joined before the back-transformation
-  static int tfac_side = -1;  // AQC_GB_TFAC_SIDE=0: the factors in line on the post stream (A/B)
-  if (tfac_side < 0) {
-    const char* e = std::getenv("AQC_GB_TFAC_SIDE");
-    tfac_side = (e && std::strcmp(e, "0") == 0) ? 0 : 1;
-  }
-  hipStream_t s3 = overlap && tfac_side ? gb_side_stream(1) : s2;
+  hipStream_t s3 = gb_side_stream(1);
   int evi = 0;  // events of this call, in order (gb_event: per process, reused call to call)
   auto post = [&](hipStream_t ps, int j0, int nr) -> int {
     if (s3 != ps) {

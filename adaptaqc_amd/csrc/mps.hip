@@ -50,6 +50,13 @@ hipStream_t mps_stream() {
   return g_mps_streams[dev];
 }
 
+// device dev's MPS stream if it exists (nullptr after aqc_finalize released it, or before first use)
+hipStream_t mps_stream_if_any(int dev) {
+  if (dev < 0 || dev >= 64) return nullptr;
+  std::lock_guard<std::mutex> lk(g_mps_stream_mu);
+  return g_mps_streams[dev];
+}
+
 }  // namespace aqc
 
 namespace {
@@ -71,10 +78,9 @@ double g_jacobi_tol_factor = 1.0;
 // the remaining off-diagonal is O(t^2) (quadratic convergence) and no further sweep is run.
 constexpr double kDefaultTinyT = 1e-6;
 double g_jacobi_tiny_t = kDefaultTinyT;
-// dot-product noise floor of the Jacobi rotations, in units of eps ||W|| (|a| + |b|)
-// (aqc_mps_set_jacobi_noise; jacobi_reg_body)
-constexpr double kDefaultJacobiNoise = 0.0;
-double g_jacobi_noise = kDefaultJacobiNoise;
+// dot-product noise floor of the Jacobi rotations, in units of eps ||W|| (|a| + |b|): off (a
+// floor costs graded matrices their small singular vectors)
+constexpr double kJacobiNoise = 0.0;
 // Fused per-state chain (k_chain) for batches of >= g_chain_min_states states at 2 chi = 128
 // (aqc_mps_set_fused_chain: 0 off, 1 from 32 states, 2 from one state).
 bool g_fused_chain = true;
@@ -679,11 +685,11 @@ __global__ __launch_bounds__(CP / 2 * LPG) void k_jacobi_reg(const TwoSiteJob* _
 
 #include "svd_gram.h"
 // two-site SVDs at 2 chi = 128 try the Gram / tridiagonal path first (aqc_mps_set_svd_path; the
-// initial value from AQC_SVD_PATH = 0, 1 or 2, default 1)
+// initial value from AQC_SVD_PATH = 0 or 1, default 1)
 int g_svd_gram = [] {
   const char* e = std::getenv("AQC_SVD_PATH");
   const int v = e ? std::atoi(e) : 1;
-  return v >= 0 && v <= 2 ? v : 1;
+  return v >= 0 && v <= 1 ? v : 1;
 }();
 int g_debug_max_chi = 64;  // aqc_svd_debug's max_chi (the Gram path keeps K = min(C, max_chi))
 
@@ -912,17 +918,12 @@ __device__ unsigned long long g_chain_ticks[5];
 // LDS-bound), then the gate mix in registers and coalesced theta writes (lanes along l).  Every
 // sub-group runs the same m steps, so the barriers pair up.  (An MFMA form needs more than the
 // chain's 128 VGPRs per lane: four P's of a quadrant are 16 accumulator tiles.)
-// m is staged KCH at a time (AQC_THETA_CH: 8, or 16 with A's rows XOR-swizzled instead of padded,
-// half the barriers and twice the loads in flight per step)
-#ifndef AQC_THETA_CH
-#define AQC_THETA_CH 8
-#endif
-constexpr int kThetaCh = AQC_THETA_CH;
-static_assert(kThetaCh == 8 || kThetaCh == 16, "theta chunk");
-constexpr int kThetaAPitch = kThetaCh == 8 ? 9 : 16;
+// m is staged 8 at a time (16, with A's rows XOR-swizzled instead of padded -- half the barriers,
+// twice the loads in flight per step -- measured slower: 41.9 against 39.3 ms per k_chain launch)
+constexpr int kThetaCh = 8;
+constexpr int kThetaAPitch = 9;
 constexpr int kThetaLds = 2 * 32 * kThetaAPitch + 2 * kThetaCh * 33;  // complex per sub-group
 static_assert(4 * kThetaLds * 16 <= kChainLdsBytes, "theta staging exceeds the chain's LDS");
-__device__ __forceinline__ int theta_acol(int row, int mm) { return kThetaCh == 8 ? mm : mm ^ (row & 15); }
 __device__ __forceinline__ void chain_theta(const TwoSiteJob& j) {
   extern __shared__ double2 xbuf[];
   const int tid = fresh_tid(), sg = tid >> 8, lt = tid & 255;
@@ -965,7 +966,7 @@ __device__ __forceinline__ void chain_theta(const TwoSiteJob& j) {
         cplx a = aqc::cmk(0, 0);
         if (active && l < chl && m < chm)
           a = aqc::cscale(aqc::ldg(gp + s * half + (size_t)l * cap + m), aqc::ldg(llp + l) * aqc::ldg(lmp + m));
-        As[s][row][theta_acol(row, mm)] = a;
+        As[s][row][mm] = a;
       }
       {  // B: 32 consecutive r of one row per 32 lanes
         const int mm = (e >> 5) % KCH, col = e & 31, m = m0 + mm, r = r0 + col;
@@ -983,7 +984,7 @@ __device__ __forceinline__ void chain_theta(const TwoSiteJob& j) {
         for (int s = 0; s < 2; ++s)
 #pragma unroll
           for (int i = 0; i < 2; ++i) {
-            av[s][i] = As[s][tx + 16 * i][theta_acol(tx + 16 * i, mm)];
+            av[s][i] = As[s][tx + 16 * i][mm];
             bv[s][i] = Bs[s][mm][ty + 16 * i];
           }
 #pragma unroll
@@ -1112,11 +1113,8 @@ __device__ __forceinline__ void chain_split(const TwoSiteJob& j) {
 }
 
 __global__ __launch_bounds__(1024) void k_chain(const ChainJob* __restrict__ chains, const TwoSiteJob* __restrict__ two,
-                                                const OneSiteJob* __restrict__ one, const int* __restrict__ resume) {
+                                                const OneSiteJob* __restrict__ one) {
   const ChainJob& c = chains[blockIdx.x];
-  // resume != nullptr: the tail of a list that k_chain256 handed over (from op resume[b]; < 0: none)
-  const int o0 = resume ? __builtin_amdgcn_readfirstlane(resume[blockIdx.x]) : 0;
-  if (o0 < 0) return;
   const int tid = fresh_tid();
   // shader-clock ticks of the phases (thread 0 of each workgroup; aqc_mps_chain_ticks), kept in
   // LDS so that no VGPR stays live across the phases
@@ -1130,7 +1128,7 @@ __global__ __launch_bounds__(1024) void k_chain(const ChainJob* __restrict__ cha
     }
   };
   tick(-1);
-  for (int o = o0; o < c.nops; ++o) {
+  for (int o = 0; o < c.nops; ++o) {
     // wave-uniform (SGPR) op code, so the job's fields are scalar loads and hold no VGPRs
     const int code = __builtin_amdgcn_readfirstlane(c.ops[o]);
     if (code < 0) {
@@ -1155,163 +1153,6 @@ __global__ __launch_bounds__(1024) void k_chain(const ChainJob* __restrict__ cha
   }
   if (tid == 0)
     for (int ph = 0; ph < 5; ++ph) atomicAdd(&g_chain_ticks[ph], tk[ph]);
-}
-
-// ---- fused per-state chain at 256 threads, two states per CU (svd_tri.h) -----------------------
-// The same op list as k_chain, in a 256-thread workgroup with <= ~76 KB of LDS and <= 256 VGPRs:
-// two states' chains share each CU, so one state's serial phases (the tridiagonalisation's
-// per-column chain and barriers, S4 / S5 on a wave or two) run beside the other's issue.  theta by
-// quadrants, the Gram SVD of svd_tri.h, rank, the split's two 64 x 64 GEMM blocks one after the
-// other.  An update whose Gram path declines (shape, eigenvalue floor) stops the chain: its op
-// index goes to resume[b] and k_chain (1024 threads, register Jacobi fallback) runs the rest.
-#include "svd_tri.h"
-
-__device__ __forceinline__ void chain_theta256(const TwoSiteJob& j) {
-  extern __shared__ double2 xbuf[];
-  const int lt = fresh_tid();
-  cplx (*As)[32][9] = reinterpret_cast<cplx (*)[32][9]>(xbuf);
-  cplx (*Bs)[8][33] = reinterpret_cast<cplx (*)[8][33]>(xbuf + 2 * 32 * 9);
-  __shared__ cplx sG2[16];
-  if (lt < 16) sG2[lt] = aqc::ldg(j.G + lt);
-  const int chl = j.dims[0], chm = j.dims[1], chr = j.dims[2];
-  const int cap = j.cap;
-  const size_t half = (size_t)cap * cap;
-  const int M = 2 * chl;
-  const cplx* gp = j.gp;
-  const cplx* gq = j.gq;
-  const double* llp = j.ll;
-  const double* lmp = j.lm;
-  const double* lrp = j.lr;
-  asm volatile("" : "+s"(gp), "+s"(gq), "+s"(llp), "+s"(lmp), "+s"(lrp));
-  const int ty = lt >> 4, tx = lt & 15;
-  for (int sg = 0; sg < 4; ++sg) {  // the four 32 x 32 output quadrants in turn
-    const int l0 = 32 * (sg >> 1), r0 = 32 * (sg & 1);
-    if (l0 >= chl || r0 >= chr) continue;  // (uniform)
-    cplx acc[4][2][2];
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int jj = 0; jj < 2; ++jj) acc[q][i][jj] = aqc::cmk(0, 0);
-    for (int m0 = 0; m0 < chm; m0 += 8) {
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int e = lt + 256 * u, s = e >> 8;
-        {
-          const int row = (e >> 3) & 31, mm = e & 7, l = l0 + row, m = m0 + mm;
-          cplx a = aqc::cmk(0, 0);
-          if (l < chl && m < chm) a = aqc::cscale(aqc::ldg(gp + s * half + (size_t)l * cap + m), aqc::ldg(llp + l) * aqc::ldg(lmp + m));
-          As[s][row][mm] = a;
-        }
-        {
-          const int mm = (e >> 5) & 7, col = e & 31, m = m0 + mm, r = r0 + col;
-          cplx b = aqc::cmk(0, 0);
-          if (m < chm && r < chr) b = aqc::cscale(aqc::ldg(gq + s * half + (size_t)m * cap + r), aqc::ldg(lrp + r));
-          Bs[s][mm][col] = b;
-        }
-      }
-      __syncthreads();
-#pragma unroll 2
-      for (int mm = 0; mm < 8; ++mm) {
-        cplx av[2][2], bv[2][2];
-#pragma unroll
-        for (int s = 0; s < 2; ++s)
-#pragma unroll
-          for (int i = 0; i < 2; ++i) {
-            av[s][i] = As[s][tx + 16 * i][mm];
-            bv[s][i] = Bs[s][mm][ty + 16 * i];
-          }
-#pragma unroll
-        for (int s1 = 0; s1 < 2; ++s1)
-#pragma unroll
-          for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-            for (int i = 0; i < 2; ++i)
-#pragma unroll
-              for (int jj = 0; jj < 2; ++jj)
-                acc[2 * s1 + s2][i][jj] = aqc::cfma(av[s1][i], bv[s2][jj], acc[2 * s1 + s2][i][jj]);
-      }
-      __syncthreads();
-    }
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int jj = 0; jj < 2; ++jj) {
-        const int l = l0 + tx + 16 * i, r = r0 + ty + 16 * jj;
-        if (l < chl && r < chr) {
-#pragma unroll
-          for (int o = 0; o < 4; ++o) {
-            cplx v = aqc::cmul(sG2[o * 4 + 0], acc[0][i][jj]);
-            v = aqc::cfma(sG2[o * 4 + 1], acc[1][i][jj], v);
-            v = aqc::cfma(sG2[o * 4 + 2], acc[2][i][jj], v);
-            v = aqc::cfma(sG2[o * 4 + 3], acc[3][i][jj], v);
-            aqc::stg(j.theta + (size_t)((o & 1) * chr + r) * M + (o >> 1) * chl + l, v);
-          }
-        }
-      }
-  }
-}
-
-__device__ __forceinline__ void chain_split256(const TwoSiteJob& j) {
-  extern __shared__ double2 xbuf[];
-  const int tid = fresh_tid();
-  split_copy_body(j, tid, 256);
-  aqc::GemmLds& lds = *reinterpret_cast<aqc::GemmLds*>(xbuf);
-  for (int blk = 0; blk < 4; ++blk)
-    if (split_block_active(j, blk)) split_gemm_body<true>(j, blk, lds, -1);  // (uniform)
-}
-
-__device__ unsigned long long g_chain256_ticks[5];
-
-__global__ __launch_bounds__(256, 2) void k_chain256(const ChainJob* __restrict__ chains, const TwoSiteJob* __restrict__ two,
-                                                     const OneSiteJob* __restrict__ one, int* __restrict__ resume) {
-  const ChainJob& c = chains[blockIdx.x];
-  const int tid = fresh_tid();
-  __shared__ unsigned long long tk[6];
-  if (tid == 0) tk[0] = tk[1] = tk[2] = tk[3] = tk[4] = tk[5] = 0;
-  auto tick = [&](int ph) {
-    if (tid == 0) {
-      const unsigned long long t = __builtin_amdgcn_s_memtime();
-      if (ph >= 0) tk[ph] += t - tk[5];
-      tk[5] = t;
-    }
-  };
-  tick(-1);
-  for (int o = 0; o < c.nops; ++o) {
-    const int code = __builtin_amdgcn_readfirstlane(c.ops[o]);
-    if (code < 0) {
-      one_site_body(one[-code - 1], tid, 256);
-      __syncthreads();
-      tick(4);
-      continue;
-    }
-    const TwoSiteJob& j = two[code];
-    chain_theta256(j);
-    __syncthreads();
-    tick(0);
-    const bool ok = j.gram && tri::gram256_body(j);
-    __syncthreads();
-    tick(1);
-    if (!ok) {  // the 1024-thread chain takes over from this update (theta is recomputed there)
-      if (tid == 0) resume[blockIdx.x] = o;
-      break;
-    }
-    rank_body<256, 128>(j);
-    __syncthreads();
-    tick(2);
-    chain_split256(j);
-    __syncthreads();
-    tick(3);
-  }
-  if (tid == 0)
-    for (int ph = 0; ph < 5; ++ph) atomicAdd(&g_chain256_ticks[ph], tk[ph]);
-}
-
-// single-job Gram SVD on 256 threads (aqc_svd_debug variant 8)
-__global__ __launch_bounds__(256, 2) void k_svd_gram256(const TwoSiteJob* __restrict__ jobs) {
-  const TwoSiteJob& j = jobs[blockIdx.x];
-  if (!tri::gram256_body(j) && threadIdx.x == 0) j.flags[2] = -1;
 }
 
 // ---- measurements -------------------------------------------------------------------------
@@ -1855,7 +1696,7 @@ TwoSiteJob make_two(aqc_mps_t h, const DevOp& op, int slot = 0) {
   j.thr = h->thr;
   j.jtol = g_jacobi_tol_factor;
   j.jtiny = g_jacobi_tiny_t;
-  j.jnoise = g_jacobi_noise;
+  j.jnoise = kJacobiNoise;
   j.gram = g_svd_gram;
   std::memcpy(j.G, op.m, sizeof(j.G));
   return j;
@@ -1916,18 +1757,6 @@ std::vector<std::vector<const DevOp*>> level_ops(const std::vector<DevOp>& ops, 
 
 // Batches at 2 chi = 128: every state's op list runs in one k_chain workgroup (longest lists
 // first, so that the short ones fill in behind them).
-// k_chain (one state per CU) unless aqc_mps_set_chain_threads(256) / AQC_CHAIN=256 selects
-// k_chain256 (two states per CU, measured slower: DESIGN.md "two updates per CU") -- and only while
-// the Gram path is on (its fallback, the register Jacobi, needs the 1024-thread chain)
-int g_chain256 = -1;
-bool use_chain256() {
-  if (g_chain256 < 0) {
-    const char* e = std::getenv("AQC_CHAIN");
-    g_chain256 = (e && std::strcmp(e, "256") == 0) ? 1 : 0;
-  }
-  return g_chain256 && g_svd_gram;
-}
-
 int run_chains(aqc_mps_t* hs, int ns, std::vector<std::vector<DevOp>>& lists, int cap_max) {
   hipStream_t st = aqc::mps_stream();
   // per-state job counts -> offsets, then every state's jobs written straight into the staging
@@ -1951,11 +1780,10 @@ int run_chains(aqc_mps_t* hs, int ns, std::vector<std::vector<DevOp>>& lists, in
   const size_t o_codes = al(o_one + n_one * sizeof(OneSiteJob));
   const size_t o_chain = al(o_codes + n_codes * sizeof(int));
   const size_t total = o_chain + (size_t)ns * sizeof(ChainJob);
-  const size_t o_resume = al(total);  // device-only: k_chain256's hand-over indices
   StagingLease lease(st);
   if (lease.rc() != AQC_OK) return lease.rc();
   Staging& sg = lease.buf();
-  int rc = ensure_staging(sg, o_resume + (size_t)ns * sizeof(int));
+  int rc = ensure_staging(sg, total);
   if (rc != AQC_OK) return rc;
   char* hb = (char*)sg.host;
   char* db = (char*)sg.dev;
@@ -1990,19 +1818,8 @@ int run_chains(aqc_mps_t* hs, int ns, std::vector<std::vector<DevOp>>& lists, in
   const double c = cap_max, nj = (double)n_two;
   // algorithmic: the two sites' Gammas in and out; nominal SVD + theta + split flops
   aqc::KernelTimer::begin(st, "mps_chain", nj * 8.0 * c * c * 16, nj * (84.0 * 8.0 + 64.0) * c * c * c);
-  if (use_chain256()) {
-    // two states per CU; a state whose Gram path declines continues on the 1024-thread chain
-    int* dres = (int*)(db + o_resume);
-    AQC_HIP_CHECK(hipMemsetAsync(dres, 0xff, (size_t)ns * sizeof(int), st));
-    hipLaunchKernelGGL(k_chain256, dim3(ns), dim3(256), tri::kLdsBytes, st, (const ChainJob*)(db + o_chain),
-                       (const TwoSiteJob*)(db + o_two), (const OneSiteJob*)(db + o_one), dres);
-    AQC_CHECK_LAUNCH();
-    hipLaunchKernelGGL(k_chain, dim3(ns), dim3(1024), kChainLds, st, (const ChainJob*)(db + o_chain),
-                       (const TwoSiteJob*)(db + o_two), (const OneSiteJob*)(db + o_one), (const int*)dres);
-  } else {
-    hipLaunchKernelGGL(k_chain, dim3(ns), dim3(1024), kChainLds, st, (const ChainJob*)(db + o_chain),
-                       (const TwoSiteJob*)(db + o_two), (const OneSiteJob*)(db + o_one), (const int*)nullptr);
-  }
+  hipLaunchKernelGGL(k_chain, dim3(ns), dim3(1024), kChainLds, st, (const ChainJob*)(db + o_chain),
+                     (const TwoSiteJob*)(db + o_two), (const OneSiteJob*)(db + o_one));
   aqc::KernelTimer::end(st);
   AQC_CHECK_LAUNCH();
   return AQC_OK;  // the lease records the set's event
@@ -2303,6 +2120,7 @@ int aqc_mps_create(int n, int chi_cap, double threshold, int max_chi, aqc_mps_t*
   auto* h = new aqc_mps_s();
   static std::atomic<unsigned long long> next_uid{1};
   h->uid = next_uid++;
+  AQC_HIP_CHECK(hipGetDevice(&h->dev));
   h->d.n = n;
   h->d.cap = chi_cap;
   h->thr = threshold;
@@ -2357,7 +2175,15 @@ int aqc_mps_create(int n, int chi_cap, double threshold, int max_chi, aqc_mps_t*
 
 int aqc_mps_destroy(aqc_mps_t h) {
   if (!h) return AQC_OK;
-  hipStreamSynchronize(aqc::mps_stream());
+  // drain the handle's own device's MPS stream (the caller may have switched devices since), and
+  // do not create one: after aqc_finalize (interpreter teardown) no stream is left, nor any work
+  if (hipStream_t st = aqc::mps_stream_if_any(h->dev)) {
+    int cur = 0;
+    const bool have = hipGetDevice(&cur) == hipSuccess;
+    if (!have || cur != h->dev) (void)hipSetDevice(h->dev);
+    (void)hipStreamSynchronize(st);
+    if (have && cur != h->dev) (void)hipSetDevice(cur);
+  }
   aqc::dev_free(h->base);
   aqc::dev_free(h->d.env);
   aqc::dev_free(h->gw);
@@ -2377,10 +2203,9 @@ int aqc_svd_debug(const double* theta, int m, int n, int variant, int stop_after
   AQC_REQUIRE(m >= 1 && n >= 1 && m % 2 == 0 && n % 2 == 0 && m <= 128 && n <= 128,
               "aqc_svd_debug: m, n must be even and <= 128");
   AQC_REQUIRE(stop_after_qr >= 0 && stop_after_qr <= 2, "aqc_svd_debug: stop_after_qr must be 0, 1 or 2");
-  AQC_REQUIRE(variant == 2 || variant == 7 || variant == 8 || variant == 9,
-              "aqc_svd_debug: variant must be 2 (register Jacobi), 7 (Gram path) or 8 (Gram path, 256 threads)");
+  AQC_REQUIRE(variant == 2 || variant == 7, "aqc_svd_debug: variant must be 2 (register Jacobi) or 7 (Gram path)");
   AQC_REQUIRE(variant < 7 || (std::max(m, n) > 64 && stop_after_qr == 0),
-              "aqc_svd_debug: variants 7 / 8 (Gram) need 64 < max(m, n) <= 128 and no QR stop");
+              "aqc_svd_debug: variant 7 (Gram) needs 64 < max(m, n) <= 128 and no QR stop");
   hipStream_t st = aqc::mps_stream();
   const int cp = std::max(m, n) <= 32 ? 32 : (std::max(m, n) <= 64 ? 64 : 128);
   const size_t mat = (size_t)128 * 128 * sizeof(cplx);
@@ -2404,12 +2229,12 @@ int aqc_svd_debug(const double* theta, int m, int n, int variant, int stop_after
   j.flags = fl;
   j.jtol = g_jacobi_tol_factor;
   j.jtiny = g_jacobi_tiny_t;
-  j.jnoise = g_jacobi_noise;
+  j.jnoise = kJacobiNoise;
   j.qr = 1;
   j.dbg = stop_after_qr;
   j.cap = 64;                     // the work buffer holds 128 x 128
   j.max_chi = g_debug_max_chi;    // Gram path: K = min(C, max_chi)
-  j.gram = variant == 9 ? 2 : variant >= 7;  // (stop_after_qr 1: stop after the QR phase; 2: also its ticks)
+  j.gram = variant == 7;  // (stop_after_qr 1: stop after the QR phase; 2: also its ticks)
   int hd[8] = {m / 2, 0, n / 2, 0, 0, 0, 0, 0};  // dims, then zeroed flags
   AQC_HIP_CHECK(hipMemcpyAsync(th, theta, (size_t)m * n * sizeof(cplx), hipMemcpyHostToDevice, st));
   AQC_HIP_CHECK(hipMemcpyAsync(dm, hd, sizeof(hd), hipMemcpyHostToDevice, st));
@@ -2417,10 +2242,8 @@ int aqc_svd_debug(const double* theta, int m, int n, int variant, int stop_after
   AQC_HIP_CHECK(hipMemsetAsync(wk, 0, mat, st));
   if (cp == 32) hipLaunchKernelGGL((k_jacobi_reg<32, 2>), dim3(1), dim3(256), 16 * 33 * 16, st, dj);
   else if (cp == 64) hipLaunchKernelGGL((k_jacobi_reg<64, 4>), dim3(1), dim3(512), 32 * 65 * 16, st, dj);
-  else if (variant == 7 || variant == 9)  // 9: the Gram path with the lower-triangle S3 (j.gram = 2)
+  else if (variant == 7)
     hipLaunchKernelGGL(k_svd_gram, dim3(1), dim3(1024), kChainLdsBytes, st, dj);
-  else if (variant == 8)  // (flags[2] = -1: declined)
-    hipLaunchKernelGGL(k_svd_gram256, dim3(1), dim3(256), tri::kLdsBytes, st, dj);
   else  // the register Jacobi itself (not the Gram path in front of it)
     hipLaunchKernelGGL((k_jacobi_reg<128, 8>), dim3(1), dim3(1024), 64 * 129 * 16, st, dj);
   AQC_CHECK_LAUNCH();
@@ -2445,12 +2268,6 @@ int aqc_mps_jacobi_stats(aqc_mps_t h, int* max_sweeps) {
   *max_sweeps = f[2];
   int z = 0;
   AQC_HIP_CHECK(hipMemcpy(h->d.flags + 2, &z, sizeof(int), hipMemcpyHostToDevice));
-  return AQC_OK;
-}
-
-int aqc_mps_set_jacobi_noise(double factor) {
-  AQC_REQUIRE(factor >= 0, "aqc_mps_set_jacobi_noise: factor must be >= 0");
-  g_jacobi_noise = factor;
   return AQC_OK;
 }
 
@@ -2481,7 +2298,7 @@ int aqc_svd_gram_stats(double* out) {
 }
 
 int aqc_mps_set_svd_path(int gram, int debug_max_chi) {
-  AQC_REQUIRE(gram >= 0 && gram <= 2, "aqc_mps_set_svd_path: gram must be 0, 1 or 2");
+  AQC_REQUIRE(gram >= 0 && gram <= 1, "aqc_mps_set_svd_path: gram must be 0 or 1");
   g_svd_gram = gram;
   g_debug_max_chi = debug_max_chi;
   return AQC_OK;
@@ -2501,10 +2318,6 @@ int aqc_mps_chain_ticks(double* out) {
   AQC_HIP_CHECK(hipMemcpyFromSymbol(t, HIP_SYMBOL(g_chain_ticks), sizeof(t)));
   const unsigned long long z[5] = {0, 0, 0, 0, 0};
   AQC_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_chain_ticks), z, sizeof(z)));
-  unsigned long long t2[5] = {0, 0, 0, 0, 0};  // k_chain256's (the two chains' phases add up)
-  AQC_HIP_CHECK(hipMemcpyFromSymbol(t2, HIP_SYMBOL(g_chain256_ticks), sizeof(t2)));
-  AQC_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_chain256_ticks), z, sizeof(z)));
-  for (int i = 0; i < 5; ++i) t[i] += t2[i];
   for (int i = 0; i < 5; ++i) out[i] = (double)t[i];
   return AQC_OK;
 }
@@ -2513,12 +2326,6 @@ int aqc_mps_set_fused_chain(int on) {
   AQC_REQUIRE(on >= 0 && on <= 2, "aqc_mps_set_fused_chain: 0, 1 or 2");
   g_fused_chain = on != 0;
   g_chain_min_states = on == 2 ? 1 : 32;
-  return AQC_OK;
-}
-
-int aqc_mps_set_chain_threads(int threads) {
-  AQC_REQUIRE(threads == 256 || threads == 1024, "aqc_mps_set_chain_threads: 256 or 1024");
-  g_chain256 = threads == 256 ? 1 : 0;
   return AQC_OK;
 }
 

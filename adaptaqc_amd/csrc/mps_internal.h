@@ -163,6 +163,7 @@ int block_jacobi(const TwoSiteJob* jobs, int nj, int cap_max, hipStream_t st);
 int big_svd(const TwoSiteJob* hjobs, const TwoSiteJob* jobs, int nj, int side, int cap_max, hipStream_t st);
 
 hipStream_t mps_stream();
+hipStream_t mps_stream_if_any(int dev);
 
 }  // namespace aqc
 
@@ -170,6 +171,7 @@ struct aqc_mps_s {
   aqc::MpsDev d;
   double thr = 1e-16;
   int max_chi = 0;
+  int dev = 0;  // the device the handle's buffers live on (aqc_mps_create's current device)
   std::vector<int> order;  // site -> qubit
   // host upper bounds of the bond dimensions (n + 1; exact after a load or a dims read-back, then
   // advanced per two-site update as min(2 chi_l, 2 chi_r, cap, max_chi)): the lock-step path picks

@@ -137,8 +137,9 @@ __global__ __launch_bounds__(kThreads) void k_sv_segment(cplx* __restrict__ stat
 // round trip and one barrier per phase instead of per gate, and 2^NS independent LDS reads per
 // thread in flight instead of 2 or 4 dependent ones.  Gate matrices of phase p+1 are staged into
 // LDS (double buffer) while phase p computes.  NS = 4: 256 threads x 16 amplitudes (one wave per
-// SIMD at n = 20, where there are 256 tiles); NS = 3: 512 threads x 8 (two waves per SIMD, about
-// 1.7x the phases: three slots hold fewer gates).  AQC_SV_SLOTS selects (default 4).
+// SIMD at n = 20, where there are 256 tiles).  (NS = 3, 512 threads x 8 amplitudes and two waves per
+// SIMD, measured 4% slower at 1.7x the phases; removed from the library in round 5.)
+constexpr int kSlots = 4;
 constexpr int kRegTileBits = 12;   // 4096 amplitudes (64 KB LDS)
 constexpr int kRegMinQubits = 14;  // below: the per-gate kernel (too few tiles)
 constexpr int kPhaseMaxGates = 16;
@@ -697,8 +698,6 @@ uint64_t lane_map_coalesced(uint32_t S) {
 }
 
 void mark_direct_phases(PhaseHdr* first, PhaseHdr* last) {
-  static const char* dbg = std::getenv("AQC_SV_DIRECT");  // "0": LDS round trips only (A/B)
-  if (dbg && std::strcmp(dbg, "0") == 0) return;
   if ((first->slotmask & 15) == 0) {
     first->lanemap = lane_map_coalesced((uint32_t)first->slotmask);
     first->slotmask |= kPhaseDirectIn;
@@ -896,6 +895,10 @@ struct aqc_sv_s {
   // passes run; the state's stream waits on the batch's event before its first pass
   hipStream_t up_stream = nullptr;
   hipEvent_t up_ev[2] = {nullptr, nullptr};
+  // recorded on this state's stream after a copy that reads another state (aqc_sv_copy): the
+  // source's stream waits on it, so the source is neither rewritten nor freed (and its pooled block
+  // handed out again) while the copy still reads it
+  hipEvent_t read_ev = nullptr;
 };
 
 static int sv_materialize(aqc_sv_t h) {
@@ -923,9 +926,7 @@ static int sv_scratch(aqc_sv_t h, size_t bytes, char** out) {
 // per lane group: a tile of high qubits only reads 16-byte pieces scattered 4 KB apart)
 static uint64_t sv_reserved_bits(bool reg_tiles) {
   if (!reg_tiles) return 0;
-  static const char* lb_env = std::getenv("AQC_SV_LOWBITS");
-  const int low = lb_env ? std::atoi(lb_env) : kRegLowBits;
-  return (1ull << std::min(std::max(low, 0), 8)) - 1ull;
+  return (1ull << kRegLowBits) - 1ull;
 }
 
 static std::vector<HostSeg> sv_plan_segments(int n, int K, bool reg_tiles, const aqc_op_t* ops, int nops) {
@@ -934,19 +935,6 @@ static std::vector<HostSeg> sv_plan_segments(int n, int K, bool reg_tiles, const
 
 // Segment s of the plan: its header (hdr[s], sized by the caller), its fused gates and phases
 // appended to gts / phs (gate_off indexes the whole list).
-// slots per phase of the register-tile path: aqc_sv_set_slots, else AQC_SV_SLOTS = 3 or 4 (read at
-// first use), else 4.  Each aqc_sv_apply plans and launches with one value.
-static std::atomic<int> g_sv_slots{0};
-static int sv_slots() {
-  int ns = g_sv_slots.load(std::memory_order_relaxed);
-  if (ns == 0) {
-    const char* e = std::getenv("AQC_SV_SLOTS");
-    ns = (e && std::atoi(e) == 3) ? 3 : 4;
-    g_sv_slots.store(ns, std::memory_order_relaxed);
-  }
-  return ns;
-}
-
 static void sv_plan_one(int n, int K, bool reg_tiles, const aqc_op_t* ops, const HostSeg& seg, size_t s,
                         std::vector<SegHeader>& hdr, std::vector<SegGate>& gts, std::vector<PhaseHdr>& phs,
                         std::vector<double>* seg_flops) {
@@ -972,14 +960,9 @@ static void sv_plan_one(int n, int K, bool reg_tiles, const aqc_op_t* ops, const
   if (reg_tiles) {  // gate_off / ngates index the phase list
     hdr[s].gate_off = (int)phs.size();
     const size_t before = phs.size();
-    build_phases(fused, K, sv_slots(), phs, gts);
+    build_phases(fused, K, kSlots, phs, gts);
     hdr[s].ngates = (int)(phs.size() - before);
     if (phs.size() > before) mark_direct_phases(&phs[before], &phs.back());
-    // timing experiments only (results wrong): AQC_SV_DEBUG=nogates / nophases
-    static const char* dbg = std::getenv("AQC_SV_DEBUG");
-    if (dbg && std::strcmp(dbg, "nophases") == 0) hdr[s].ngates = 0;
-    if (dbg && std::strcmp(dbg, "nogates") == 0)
-      for (size_t q = before; q < phs.size(); ++q) phs[q].ngates = 0;
   } else {
     hdr[s].gate_off = (int)gts.size();
     hdr[s].ngates = (int)fused.size();
@@ -998,19 +981,10 @@ static void sv_plan(int n, int K, bool reg_tiles, const aqc_op_t* ops, int nops,
 }
 
 static bool sv_reg_tiles(int n) {
-  // register-resident 4096-amplitude tiles from kRegMinQubits qubits (AQC_SV_TILE=lds keeps the
-  // per-gate LDS kernel, for A/B measurements)
+  // register-resident 4096-amplitude tiles from kRegMinQubits qubits (below: the per-gate LDS kernel;
+  // AQC_SV_TILE=lds keeps it above too, which the tests use to check one kernel against the other)
   const char* tile_env = std::getenv("AQC_SV_TILE");
   return n >= kRegMinQubits && !(tile_env && std::strcmp(tile_env, "lds") == 0);
-}
-
-// AQC_SV_SIDE_UPLOAD=0: every batch's plan on the state's stream (A/B)
-static bool sv_side_upload() {
-  static const bool on = [] {
-    const char* e = std::getenv("AQC_SV_SIDE_UPLOAD");
-    return !(e && std::strcmp(e, "0") == 0);
-  }();
-  return on;
 }
 
 static int sv_launch_segment(aqc_sv_t h, const SegHeader* dh, const PhaseHdr* dp, const SegGate* dg, int nblocks, cplx* amp0_out,
@@ -1019,12 +993,8 @@ static int sv_launch_segment(aqc_sv_t h, const SegHeader* dh, const PhaseHdr* dp
   const double bytes = (from_zero ? 16.0 : 32.0) * (double)(1ull << h->n);
   aqc::KernelTimer::begin(h->stream, "sv_segment", bytes, flops);
   if (h->reg_tiles) {
-    if (sv_slots() == 3)
-      hipLaunchKernelGGL(k_sv_tile_reg<3>, dim3(nblocks), dim3(512), 0, h->stream, h->state, dh, dp, dg, from_zero,
-                         amp0_out);
-    else
-      hipLaunchKernelGGL(k_sv_tile_reg<4>, dim3(nblocks), dim3(256), 0, h->stream, h->state, dh, dp, dg, from_zero,
-                         amp0_out);
+    hipLaunchKernelGGL(k_sv_tile_reg<kSlots>, dim3(nblocks), dim3(4096 >> kSlots), 0, h->stream, h->state, dh, dp, dg,
+                       from_zero, amp0_out);
     h->zero_pending = false;
     aqc::KernelTimer::end(h->stream);
     AQC_CHECK_LAUNCH();
@@ -1077,6 +1047,7 @@ int aqc_sv_create(int n, aqc_sv_t* out) {
   AQC_HIP_CHECK(hipEventCreateWithFlags(&h->plan_ev, hipEventDisableTiming));
   AQC_HIP_CHECK(hipStreamCreateWithFlags(&h->up_stream, hipStreamNonBlocking));
   for (auto& e : h->up_ev) AQC_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  AQC_HIP_CHECK(hipEventCreateWithFlags(&h->read_ev, hipEventDisableTiming));
   h->zwg = (int)((dim + kThreads * kZChunk - 1) / (kThreads * kZChunk));
   AQC_HIP_CHECK(hipMalloc(&h->d_zpart, sizeof(double) * (size_t)h->zwg * (n + 1)));
   AQC_HIP_CHECK(hipMalloc(&h->d_z, sizeof(double) * (n + 1)));
@@ -1099,6 +1070,7 @@ int aqc_sv_destroy(aqc_sv_t h) {
   if (h->up_stream) hipStreamSynchronize(h->up_stream), hipStreamDestroy(h->up_stream);
   for (hipEvent_t e : h->up_ev)
     if (e) hipEventDestroy(e);
+  if (h->read_ev) hipEventDestroy(h->read_ev);
   if (h->stream) hipStreamDestroy(h->stream);
   delete h;
   return AQC_OK;
@@ -1121,6 +1093,10 @@ int aqc_sv_copy(aqc_sv_t dst, const aqc_sv_t src) {
   AQC_HIP_CHECK(hipStreamSynchronize(src->stream));
   AQC_HIP_CHECK(hipMemcpyAsync(dst->state, src->state, sizeof(cplx) << dst->n,
                                hipMemcpyDeviceToDevice, dst->stream));
+  // the copy reads src on dst's stream: later work on src's stream (an apply that rewrites it,
+  // or the synchronisation in aqc_sv_destroy before its block returns to the pool) waits for it
+  AQC_HIP_CHECK(hipEventRecord(dst->read_ev, dst->stream));
+  AQC_HIP_CHECK(hipStreamWaitEvent(src->stream, dst->read_ev, 0));
   return AQC_OK;
 }
 
@@ -1194,7 +1170,7 @@ int aqc_sv_apply(aqc_sv_t h, const aqc_op_t* ops, int nops) {
     if (!gts.empty()) std::memcpy(h->h_plan + o_g, gts.data(), sizeof(SegGate) * gts.size());
     // (by a copy kernel, aqc::upload_async: the SDMA transfers hipMemcpyAsync used for the larger
     // batches cost ~10-25 us of idle GPU each in the config-2 timeline)
-    if (nb_done > 0 && sv_side_upload()) {
+    if (nb_done > 0) {
       // (the batch's plan region is fresh: no pass reads it before the event below)
       hipEvent_t ev = h->up_ev[nb_done & 1];
       AQC_HIP_CHECK(hipMemcpyAsync(h->d_plan + o_h, h->h_plan + o_h, end - o_h, hipMemcpyHostToDevice, h->up_stream));
@@ -1219,12 +1195,6 @@ int aqc_sv_apply(aqc_sv_t h, const aqc_op_t* ops, int nops) {
   // (recorded on every path, so the next call never reuses the staging buffer under a live copy)
   AQC_HIP_CHECK(hipEventRecord(h->plan_ev, h->stream));
   return rc;
-}
-
-int aqc_sv_set_slots(int slots) {
-  AQC_REQUIRE(slots == 3 || slots == 4, "aqc_sv_set_slots: 3 or 4");
-  g_sv_slots.store(slots, std::memory_order_relaxed);
-  return AQC_OK;
 }
 
 int aqc_sv_plan(int n, const aqc_op_t* ops, int nops, int* out) {

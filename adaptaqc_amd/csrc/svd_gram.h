@@ -35,77 +35,28 @@
 #pragma once
 
 constexpr int kGramMaxK = 64;
-// S3: wave 0 raises its issue priority while it forms a reflector's scalars (the other waves of
-// its SIMD are in the column pass, issue-bound, and would otherwise take 3 of every 4 issue slots)
-#ifndef AQC_S3_PRIO
-#define AQC_S3_PRIO 1
-#endif
-// S5: the LDL^T pivots from the leading minors' recurrence (one FMA + the guard on the chain)
-// S5: inverse-iteration steps per eigenvector
-// S4: lanes per eigenvalue (kG, (kG + 1)-section) and rounds after the first 256-shift pass.  The
-// pass is FP64-issue-bound: 8 x 9-section x 9 rounds took 108 K ticks and 16 x 17 x 7 145 K against
-// 98 K (profiles/r4_s4_shapes_ab.json)
-#ifndef AQC_S4_G
-#define AQC_S4_G 4
-#endif
-#ifndef AQC_S4_ROUNDS
-#define AQC_S4_ROUNDS 12
-#endif
-#ifndef AQC_S5_ITERS
-#define AQC_S5_ITERS 3
-#endif
-#ifndef AQC_S5_POLY
-#define AQC_S5_POLY 1
-#endif
+// Settled choices (each measured against its alternative):
+// S3: wave 0 raises its issue priority while it forms a reflector's scalars; the reflectors' base
+//     pointer in SGPRs; the rows' partial products summed in the wave (DPP) before phase B; the
+//     column pass prefetches column i + 1's LDS operands while column i computes; one row per lane
+//     (two rows per lane measured slower: 0.68 M against 0.64 M ticks)
+// S4: 4 lanes per eigenvalue (5-section), 12 rounds after the first 256-shift pass (8 x 9 x 9 and
+//     16 x 17 x 7 measured 108 K / 145 K against 98 K ticks: the pass is FP64-issue-bound)
+// S5: three inverse-iteration steps per eigenvector; the LDL^T pivots from the leading minors'
+//     recurrence (one FMA + the guard on the chain)
+// S6: the compact-WY factors of every reflector block precomputed during S5 by the idle waves
+//     4..11; W2 = T (Y^H V) on the matrix cores inside the mg == 0 waves; the next block's
+//     reflectors fetched after B4
 constexpr double kGramRelFloor = 1e-9;
 // shader-clock ticks of the phases (thread 0), summed over calls: S1, S2+S3, S4, S5, S6, output,
-// S3's column steps, S5's inverse iteration, S3's phase A (column pass + zlarfg + first barrier);
-// with AQC_S3_DIAG: [9] wave 0's reflector scalars done (from the step's start), [10] wave 13's
-// column pass (its own step start to its end)
+// S3's column steps, S5's inverse iteration, S3's phase A (column pass + zlarfg + first barrier)
 __device__ unsigned long long g_gram_ticks[12];
-#ifndef AQC_S3_DIAG
-#define AQC_S3_DIAG 0
-#endif
-// S6: the compact-WY factors T of every reflector block computed during S5 by the idle waves 4..11
-// (S = Y^H Y on the matrix cores, zlarft), read back per block -- off the block loop's critical path
-// (there wave 5 ran the 16-step zlarft chain between B2 and B3 while the other waves waited)
-#ifndef AQC_S6_TPRE
-#define AQC_S6_TPRE 1
-#endif
 // S6's precompute on the waves 1-3, 5-7, 9-11 (not the waves 4 and 8, which share SIMD 0 with
-// wave 0's inverse iteration) instead of the waves 4..11
+// wave 0's inverse iteration) instead of the waves 4..11 (A/B pending)
 #ifndef AQC_S6_TPRE_SKIP0
 #define AQC_S6_TPRE_SKIP0 0
 #endif
 static_assert(kGramMaxK <= 64, "S5: the inverse iteration (tid < K) must stay on wave 0");
-// S6 with the precomputed T: W2 = T (Y^H V) on the matrix cores inside the mg == 0 waves (no B3)
-#ifndef AQC_S6_W2MFMA
-#define AQC_S6_W2MFMA 1
-#endif
-// S6: the next block's reflectors fetched after B4 (see the block loop)
-#ifndef AQC_S6_LATE_FETCH
-#define AQC_S6_LATE_FETCH 1
-#endif
-// S3: the reflectors' base pointer in SGPRs (as a VGPR pair it was spilled and reloaded per column)
-#ifndef AQC_S3_HH_SGPR
-#define AQC_S3_HH_SGPR 1
-#endif
-// S3: the rows' partial products of the column pass summed in the wave (DPP) before phase B
-#ifndef AQC_S3_ROWSUM
-#define AQC_S3_ROWSUM 1
-#endif
-// S3: the column pass prefetches column i + 1's LDS operands while column i computes
-#ifndef AQC_S3_PIPE
-#define AQC_S3_PIPE 1
-#endif
-// S3 register layout: 1 -- row tid / 8, columns tid % 8 + 8 i (i < 16); 2 (round-4 experiment,
-// measured slower) -- thread (wave w, lane l) holds rows 8 w + l / 16 and that + 4, columns
-// l % 16 + 16 i (i < 8), so each column's v, p, z LDS operands serve two rows: half the column
-// pass's LDS reads and 14 instead of 16 FP64 operations per element, but S3 took 0.68 M ticks
-// against 0.64 M (with a v / p prefetch, which spilled two g entries: 0.71 M)
-#ifndef AQC_S3_RPL
-#define AQC_S3_RPL 1
-#endif
 // path counters (thread 0 of each call): [0] calls, [1] taken, [2] declined by shape (K > 64, ...),
 // [3] declined at the eigenvalue floor (lambda_K <= 1e-9 lambda_1 -> the Jacobi runs)
 __device__ unsigned long long g_gram_stats[4];
@@ -245,42 +196,10 @@ __device__ __forceinline__ double rcp_nr(double x) {
 constexpr size_t kTfacOff = 8192;
 typedef __attribute__((address_space(1))) double gdbl_t;
 
-// The lower-triangle tridiagonalisation of svd_tri.h (defined there), which gram_svd_body<true>
-// runs at 1024 threads in place of its full-matrix S3
-namespace tri {
-struct S3Ctx {
-  int C;               // matrix size
-  cplx* hh;            // packed reflectors (global, SGPR)
-  cplx* scratch;       // repack scratch (global)
-  const cplx* th;      // theta' (S1)
-  int M, L, tr;        // X = theta' (L x C) or its conjugate transpose
-};
-template <int TR, int NT>
-__device__ __noinline__ void s3_stage(const S3Ctx& cx_in, int k0, int k1, int mode);
-constexpr size_t kScratchOff = 8192;  // (= tri::kScratch)
-// The tridiagonalisation's LDS map (complex units) per workgroup size: at 256 threads svd_tri.h's
-// constants (kVec ...); at 1024 threads a grid of up to 6208 entries (TR = 2, NB = 64), then the
-// vectors, scalars, 16 waves' p^H v and d / e / tau of its own (copied to the body's arrays
-// after S3)
-template <int NT>
-struct TriLds {
-  static constexpr int kGrid = 0, kVec = 3136, kGk1 = 3544, kScal = 3672, kKtp = 3676, kD = 4096, kE = 4160,
-                       kTau = 4480;
-};
-template <>
-struct TriLds<1024> {
-  static constexpr int kGrid = 0, kVec = 6208, kGk1 = 6616, kScal = 6744, kKtp = 6748, kD = 6768, kE = 6832,
-                       kTau = 6896, kEnd = 7026;
-};
-}  // namespace tri
-
 // Gram-path SVD of one 2 chi x 2 chi theta'; 1024 threads; `xbuf` = the workgroup's dynamic LDS
 // (>= 4 GemmLds).  Returns false (work untouched beyond scratch, caller runs the Jacobi) when the
-// fast path does not apply.  Uniform in the workgroup.  TRI (j.gram == 2): S3 as the lower-triangle
-// stages of svd_tri.h on all 16 waves (tiles 2 x 4 over the trailing 128, then 1 x 2 over the
-// trailing 64) instead of the full Hermitian matrix in registers.
-template <bool TRI>
-__device__ __noinline__ bool gram_svd_body_t(const TwoSiteJob& j) {
+// fast path does not apply.  Uniform in the workgroup.
+__device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
   extern __shared__ double2 xbuf[];
   __shared__ double s_d[128], s_e[128], s_e2[128], s_lam[kGramMaxK], s_sig2[kGramMaxK];
   __shared__ cplx s_tau[128];
@@ -327,13 +246,7 @@ __device__ __noinline__ bool gram_svd_body_t(const TwoSiteJob& j) {
   // (absolute error a few eps ||X||^2, the Gram path's eps ||G|| budget).  X streams once through
   // double-buffered LDS chunks of 8 rows (Xr, Xi, Xr + Xi, Xr - Xi), the next chunk's global
   // load in flight during the current chunk's MFMAs: 256 KB read per SVD (768 KB before). ----
-#if AQC_S3_RPL == 2
-  // rows ra0 (g[0..7]) and ra0 + 4 (g[8..15]), columns q0 + 16 i
-  const int ra0 = 8 * wave + (lane >> 4), q0 = lane & 15;
-  const int r0 = ra0;
-#else
   const int r0 = tid >> 3, q0 = tid & 7;
-#endif
   const int r = r0, q = q0;
   cplx g[16];
   {
@@ -450,55 +363,22 @@ __device__ __noinline__ bool gram_svd_body_t(const TwoSiteJob& j) {
       }
     }
     __syncthreads();
-    if constexpr (!TRI) {
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-#if AQC_S3_RPL == 2
-        const int c = q + 16 * (i & 7), rw = r + 4 * (i >> 3);
-#else
-        const int c = q + 8 * i, rw = r;
-#endif
-        cplx v = aqc::cmk(0, 0);
-        if (rw < C && c < C) {
-          v = gsq[c >= rw ? up_index(rw, c) : up_index(c, rw)];
-          if (c < rw) v.y = -v.y;
-        }
-        g[i] = v;
+    for (int i = 0; i < 16; ++i) {
+      const int c = q + 8 * i, rw = r;
+      cplx v = aqc::cmk(0, 0);
+      if (rw < C && c < C) {
+        v = gsq[c >= rw ? up_index(rw, c) : up_index(c, rw)];
+        if (c < rw) v.y = -v.y;
       }
-      __syncthreads();  // the reflectors' scratch reuses the LDS
+      g[i] = v;
     }
+    __syncthreads();  // the reflectors' scratch reuses the LDS
   }
   tick(0);
   // reflector k at hh[k (2C - k - 1) / 2 + (row - k - 1)].  The base is uniform: moved to SGPRs
   // (as a VGPR pair it was spilled, and phase B's scratch reload waited out vmcnt(0) every column)
-  cplx* hh = AQC_S3_HH_SGPR ? uniform_ptr(j.work) : j.work;
-  if constexpr (TRI) {
-    tri::S3Ctx cx;
-    cx.C = C;
-    cx.hh = uniform_ptr(j.work);
-    cx.scratch = uniform_ptr(j.work + tri::kScratchOff);
-    cx.th = th;
-    cx.M = M;
-    cx.L = L;
-    cx.tr = tr;
-    const int kend = C - 1;
-    tri::s3_stage<2, 1024>(cx, 0, kend < 64 ? kend : 64, 2);
-    if (kend > 64) tri::s3_stage<1, 1024>(cx, 64, kend, 1);
-    {  // d, e, tau from the stages' LDS to the body's arrays
-      using Map = tri::TriLds<1024>;
-      const double* dT = reinterpret_cast<const double*>(xbuf + Map::kD);
-      const double* eT = reinterpret_cast<const double*>(xbuf + Map::kE);
-      const cplx* tT = xbuf + Map::kTau + 1;
-      for (int i = tid; i < C; i += 1024) {
-        s_d[i] = dT[i];
-        if (i < C - 1) {
-          s_e[i] = eT[i];
-          s_tau[i] = tT[i];
-        }
-      }
-      __syncthreads();
-    }
-  } else {
+  cplx* hh = uniform_ptr(j.work);
   // ---- S3: tridiagonalisation (zhetd2, lower), one barrier per column ----
   // Reflector k (v_{k+1} = 1, p = tau G^(k) v, a2 = -tau (p^H v) / 2, w = p + a2 v,
   // G^(k+1) = G^(k) - v w^H - w v^H on the trailing block) reaches the registers one phase late,
@@ -543,11 +423,6 @@ __device__ __noinline__ bool gram_svd_body_t(const TwoSiteJob& j) {
     pvb[128 + r] = aqc::cmk(0, 0);
     vbb[128 + r] = aqc::cmk(0, 0);
     zvb[128 + r] = (r > 0 && r < C) ? g[0] : aqc::cmk(0, 0);
-#if AQC_S3_RPL == 2
-    pvb[128 + r + 4] = aqc::cmk(0, 0);
-    vbb[128 + r + 4] = aqc::cmk(0, 0);
-    zvb[128 + r + 4] = (r + 4 < C) ? g[8] : aqc::cmk(0, 0);
-#endif
   }
   __syncthreads();
   // reflector k - 1's a2 and s from buffer bp, per wave
@@ -563,10 +438,8 @@ __device__ __noinline__ bool gram_svd_body_t(const TwoSiteJob& j) {
     s.x = uniform_d(s.x);
     s.y = uniform_d(s.y);
   };
-  unsigned long long t_z = 0, t_c = 0, t_c0 = 0;
   for (int k = 0; k < C - 1; ++k) {
     const int b = k & 1, bp = b ^ 1;
-    if (AQC_S3_DIAG && tid == 832) t_c0 = __builtin_amdgcn_s_memtime();
     // q and r laundered through an empty asm each step: otherwise the compiler hoists the 16
     // columns' loop-invariant index / address values out of the k loop and spills them
     int q = q0, r = r0;
@@ -582,7 +455,7 @@ __device__ __noinline__ bool gram_svd_body_t(const TwoSiteJob& j) {
     cplx a2 = aqc::cmk(0, 0), s = aqc::cmk(0, 0);
     if (wact || wave == 0) prev_scalars(k, bp, a2, s);
     if (wave == 0) {
-      if (AQC_S3_PRIO) __builtin_amdgcn_s_setprio(3);
+      __builtin_amdgcn_s_setprio(3);
       // column k of G^(k) below the diagonal: x_r = z_r - s v_r (r > k); alpha = x_{k+1}
       double xn2;
       {
@@ -613,71 +486,8 @@ __device__ __noinline__ bool gram_svd_body_t(const TwoSiteJob& j) {
         scal[1] = aqc::cmul(tau, scl);
         scal[2] = s;
       }
-      if (AQC_S3_PRIO) __builtin_amdgcn_s_setprio(0);
-      if (AQC_S3_DIAG && tid == 0) t_z += __builtin_amdgcn_s_memtime() - t_last;
+      __builtin_amdgcn_s_setprio(0);
     }
-#if AQC_S3_RPL == 2
-    static_assert(AQC_S3_ROWSUM, "two rows per lane: in-wave row sums");
-    if (wact) {
-      // rows r (g[0..7]) and r + 4 (g[8..15]); each column's v, p, z read once for both
-      const int rb = r + 4;
-      const double a2r2 = 2.0 * a2.x;
-      const cplx vra = vbb[bp * 128 + r], pra = pvb[bp * 128 + r];
-      const cplx vrb = vbb[bp * 128 + rb], prb = pvb[bp * 128 + rb];
-      const cplx wra = aqc::cmk(fma(a2r2, vra.x, pra.x), fma(a2r2, vra.y, pra.y));
-      const cplx wrb = aqc::cmk(fma(a2r2, vrb.x, prb.x), fma(a2r2, vrb.y, prb.y));
-      cplx acca = aqc::cmk(0, 0), accb = aqc::cmk(0, 0);
-      const double nsx = -s.x, nsy = -s.y;
-      // g -= v_r conj(p_c) + w_r conj(v_c) (reflector k - 1), acc += g x_c (reflector k)
-      auto upd = [](cplx& gg, const cplx& vr, const cplx& wr, const cplx& vc, const cplx& pc) {
-        gg.x = fma(-vr.x, pc.x, fma(-vr.y, pc.y, fma(-wr.x, vc.x, fma(-wr.y, vc.y, gg.x))));
-        gg.y = fma(-vr.y, pc.x, fma(vr.x, pc.y, fma(-wr.y, vc.x, fma(wr.x, vc.y, gg.y))));
-      };
-      auto col = [&](int i, const cplx& vc, const cplx& pc, const cplx& zc) {
-        const cplx xc = aqc::cmk(fma(nsx, vc.x, fma(nsy, -vc.y, zc.x)), fma(nsx, vc.y, fma(nsy, vc.x, zc.y)));
-        upd(g[i], vra, wra, vc, pc);
-        acca = aqc::cfma(g[i], xc, acca);
-        upd(g[8 + i], vrb, wrb, vc, pc);
-        accb = aqc::cfma(g[8 + i], xc, accb);
-      };
-      // over the active column blocks (16 columns each; v_c = p_c = z_c = 0 for c < k, so the first
-      // block's dead columns need no mask), each column's operands loaded where they are used
-      const int i0 = k >> 4;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        if (i >= i0) {  // uniform
-          const int c = q + 16 * i;
-          col(i, vbb[bp * 128 + c], pvb[bp * 128 + c], zvb[bp * 128 + c]);
-          __builtin_amdgcn_sched_barrier(0);
-        }
-      }
-      // the correction for x_k (see below) and G^(k)[r][k], G^(k)[r][k + 1] from the lanes
-      // holding columns k and k + 1 (the same register unless k + 1 starts a block)
-      const cplx gka = pick16(g, k >> 4), gkb = pick16(g, 8 + (k >> 4));
-      const bool same = ((k + 1) & 15) != 0;
-      const cplx gk1a = same ? gka : pick16(g, (k + 1) >> 4);
-      const cplx gk1bv = same ? gkb : pick16(g, 8 + ((k + 1) >> 4));
-      if (q == (k & 15)) {
-        acca = aqc::cfma(s, gka, acca);
-        accb = aqc::cfma(s, gkb, accb);
-        if (r == k) dS[k] = gka.x;
-        if (rb == k) dS[k] = gkb.x;
-      }
-      acca.x = aqc::row_sum16(acca.x);
-      acca.y = aqc::row_sum16(acca.y);
-      accb.x = aqc::row_sum16(accb.x);
-      accb.y = aqc::row_sum16(accb.y);
-      if (q == 0) {
-        accp[r] = acca;
-        accp[rb] = accb;
-      }
-      if (q == ((k + 1) & 15)) {
-        gk1b[r] = gk1a;
-        gk1b[rb] = gk1bv;
-      }
-      if (AQC_S3_DIAG && tid == 832) t_c += __builtin_amdgcn_s_memtime() - t_c0;
-    }
-#else
     if (wact) {
       // the own row's reflector k - 1 entries and w_r (the Hermitian rank-2 update needs only
       // Re(a2): v w^H + w v^H = v p^H + (p + 2 Re(a2) v) v^H, so no per-column w_c)
@@ -694,13 +504,11 @@ __device__ __noinline__ bool gram_svd_body_t(const TwoSiteJob& j) {
         const cplx xc = aqc::cmk(fma(nsx, vc.x, fma(nsy, -vc.y, zc.x)), fma(nsx, vc.y, fma(nsy, vc.x, zc.y)));
         acc = aqc::cfma(g[i], xc, acc);
       };
-#if AQC_S3_PIPE
       // Rolling prefetch: column i + 1's v, p, z are requested before column i is computed, so
       // each LDS round trip hides behind one column's 16 FMAs (loaded and consumed one column at a
       // time, every column waited out a full LDS latency: ~4 K of a step's ~4.6 K ticks).  The
       // active columns start at group k / 32 (uniform); its first column is loaded up front.
       const int gi0 = k >> 5;
-#if AQC_S3_PIPE == 1
       cplx cv, cp, cz;
       {
         const int c = q + 32 * gi0;
@@ -723,52 +531,6 @@ __device__ __noinline__ bool gram_svd_body_t(const TwoSiteJob& j) {
           }
         }
       }
-#else
-      // two named operand sets, columns alternating between them (even i: A, odd i: B)
-      cplx av, ap, az, bv, bp_, bz;
-      auto ldA = [&](int i) {
-        const int c = q + 8 * i;
-        av = vbb[bp * 128 + c], ap = pvb[bp * 128 + c], az = zvb[bp * 128 + c];
-      };
-      auto ldB = [&](int i) {
-        const int c = q + 8 * i;
-        bv = vbb[bp * 128 + c], bp_ = pvb[bp * 128 + c], bz = zvb[bp * 128 + c];
-      };
-      {
-        const int c = q + 32 * gi0;  // first active column: even (A)
-        av = vbb[bp * 128 + c], ap = pvb[bp * 128 + c], az = zvb[bp * 128 + c];
-      }
-#pragma unroll
-      for (int gi = 0; gi < 4; ++gi) {
-        if (gi >= gi0) {  // uniform; v_c = p_c = z_c = 0 for c < k
-#pragma unroll
-          for (int ii = 0; ii < 4; ii += 2) {
-            const int i = 4 * gi + ii;
-            ldB(i + 1);
-            __builtin_amdgcn_sched_barrier(0);
-            col(i, av, ap, az);
-            if (i + 2 < 16) ldA(i + 2);
-            __builtin_amdgcn_sched_barrier(0);
-            col(i + 1, bv, bp_, bz);
-          }
-        }
-      }
-#endif
-#else
-#pragma unroll
-      for (int gi = 0; gi < 4; ++gi) {
-        if (32 * gi + 31 >= k) {  // uniform; v_c = p_c = z_c = 0 for c < k
-#pragma unroll
-          for (int ii = 0; ii < 4; ++ii) {
-            const int i = 4 * gi + ii;
-            const int c = q + 8 * i;
-            col(i, vbb[bp * 128 + c], pvb[bp * 128 + c], zvb[bp * 128 + c]);
-            if (ii == 1) __builtin_amdgcn_sched_barrier(0);  // LDS reads in pairs: no spills
-          }
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      }
-#endif
       // the product used x_k = -s (z_k = 0, v_k = 1) where reflector k has 0 (and x_{k+1} = alpha
       // where it has alpha - beta: corrected in phase B): one entry in the lane holding column k
       // (k + 1) >> 3 == k >> 3 except every eighth column: the same register, so one pick
@@ -776,19 +538,13 @@ __device__ __noinline__ bool gram_svd_body_t(const TwoSiteJob& j) {
       const cplx gk1 = ((k + 1) & 7) ? gk : pick16(g, (k + 1) >> 3);
       if (q == (k & 7)) acc = aqc::cfma(s, gk, acc);
       if (q == (k & 7) && r == k) dS[k] = gk.x;  // G^(k)[k][k]
-#if AQC_S3_ROWSUM
       // the row's eight partial products are in eight adjacent lanes of this wave: summed here
       // (DPP, VALU slack -- the pass is LDS-bound), so phase B reads one value per row
       acc.x = aqc::row_sum8(acc.x);
       acc.y = aqc::row_sum8(acc.y);
       if (q == 0) accp[r] = acc;
-#else
-      accp[q * 128 + r] = acc;
-#endif
       if (q == ((k + 1) & 7)) gk1b[r] = gk1;
-      if (AQC_S3_DIAG && tid == 832) t_c += __builtin_amdgcn_s_memtime() - t_c0;
     }
-#endif
     __syncthreads();
     tick_step(t_b);
     // Phase B: reflector k's p, v and z, one row per thread of waves 0 and 1 (the row's eight
@@ -798,13 +554,7 @@ __device__ __noinline__ bool gram_svd_body_t(const TwoSiteJob& j) {
     if (rr < 128) {
       const double beta = eS[k];
       const cplx ts = scal[1], scl = scal[0], sk = scal[2], g1 = gk1b[rr];
-#if AQC_S3_ROWSUM
       cplx sum = accp[rr];
-#else
-      cplx sum = aqc::cmk(0, 0);
-#pragma unroll
-      for (int u = 0; u < 8; ++u) sum = aqc::cadd(sum, accp[u * 128 + rr]);
-#endif
       sum.x = fma(-beta, g1.x, sum.x);  // x_{k+1} = alpha where reflector k has alpha - beta
       sum.y = fma(-beta, g1.y, sum.y);
       const bool rowact = rr > k && rr < C, below = rr > k + 1 && rr < C;
@@ -830,13 +580,8 @@ __device__ __noinline__ bool gram_svd_body_t(const TwoSiteJob& j) {
     const int bp = (C - 2) & 1;
     cplx a2, s;
     prev_scalars(C - 1, bp, a2, s);
-#if AQC_S3_RPL == 2
-    const bool own = (r0 == C - 1 || r0 + 4 == C - 1) && q0 == ((C - 1) & 15);
-    const int gi = ((C - 1) >> 4) + (r0 + 4 == C - 1 ? 8 : 0);
-#else
     const bool own = r0 == C - 1 && q0 == ((C - 1) & 7);
     const int gi = (C - 1) >> 3;
-#endif
     if (own) {
       const cplx v = vbb[bp * 128 + C - 1], p = pvb[bp * 128 + C - 1];
       const cplx w = aqc::cfma(a2, v, p);
@@ -856,12 +601,7 @@ __device__ __noinline__ bool gram_svd_body_t(const TwoSiteJob& j) {
   if (tid == 0) {
     atomicAdd(&g_gram_ticks[6], t_a + t_b);
     atomicAdd(&g_gram_ticks[8], t_b);
-    if (AQC_S3_DIAG) atomicAdd(&g_gram_ticks[9], t_z);
   }
-  if (AQC_S3_DIAG && tid == 832) {
-    atomicAdd(&g_gram_ticks[10], t_c);
-  }
-  }  // (!TRI: the full-matrix S3)
   tick(1);
   // ---- S4: top-K eigenvalues of T by multisection ----
   if (wave == 0) {  // Gershgorin interval, ||T||, e^2 and the (d, e^2) pairs: two rows per lane
@@ -903,7 +643,7 @@ __device__ __noinline__ bool gram_svd_body_t(const TwoSiteJob& j) {
     // narrow it by 5^12 (span x 1.6e-11 at the end; the 1024-point pass + 17^6 of round 2 gave
     // 4e-11).  Waves 4-15 sit S4 out.  (Ratio form, 16 lanes x 17-section, 7 passes: 0.20 M
     // ticks; ratio form, 8 lanes x 9-section, 9 passes: 0.15 M.)
-    constexpr int kG = AQC_S4_G, kFirst = 256, kRounds = AQC_S4_ROUNDS;
+    constexpr int kG = 4, kFirst = 256, kRounds = 12;
     static_assert(kG == 4 || kG == 8 || kG == 16, "lanes per eigenvalue");
     const int eid = tid / kG, sub = tid % kG;
     const int a = C - 1 - eid;  // ascending index of the eid-th largest eigenvalue
@@ -967,7 +707,6 @@ __device__ __noinline__ bool gram_svd_body_t(const TwoSiteJob& j) {
     // (full chunks unguarded -- C is uniform but not known to the compiler, whose per-row guards
     // became exec-mask branches -- then a scalar tail; clamped indices with zero carries make the
     // first / last rows regular)
-#if AQC_S5_POLY
     // The pivots as ratios of the leading minors of T - lam I (the recurrence of S4's Sturm count,
     // in units of ||T||): D_row = p_row / p_{row-1}, p_row = (d - lam) p_{row-1} - e^2 p_{row-2},
     // so the dependent chain is one FMA and the pivot guard (|D| < eps -> +-eps) per row; each
@@ -986,15 +725,6 @@ __device__ __noinline__ bool gram_svd_body_t(const TwoSiteJob& j) {
       p0 = p1;
       p1 = p;
     };
-#else
-    auto fac_row = [&](int row, double d, double e2, double& rdp) {
-      double dj = fma(-e2, rdp, d - lam);
-      if (fabs(dj) < piv) dj = dj >= 0.0 ? piv : -piv;
-      const double rd = rcp_nr(dj);
-      Db[row * 64 + i] = rd;
-      rdp = rd;
-    };
-#endif
     {
       double rdp = 0.0;
       int r0 = 0;
@@ -1004,16 +734,14 @@ __device__ __noinline__ bool gram_svd_body_t(const TwoSiteJob& j) {
         for (int u = 0; u < U; ++u) dd[u] = s_d[r0 + u], ee[u] = s_e2[max(r0 + u - 1, 0)];
 #pragma unroll
         for (int u = 0; u < U; ++u) fac_row(r0 + u, dd[u], ee[u], rdp);
-#if AQC_S5_POLY
         const int ex = max(__builtin_amdgcn_frexp_exp(p0), __builtin_amdgcn_frexp_exp(p1));
         p0 = __builtin_amdgcn_ldexp(p0, -ex);
         p1 = __builtin_amdgcn_ldexp(p1, -ex);
-#endif
       }
       for (; r0 < C; ++r0) fac_row(r0, s_d[r0], s_e2[max(r0 - 1, 0)], rdp);
     }
     double sc = 1.0;  // the previous iteration's normalisation, applied as the forward solve reads
-    for (int it = 0; it < AQC_S5_ITERS; ++it) {
+    for (int it = 0; it < 3; ++it) {
       // forward solve L y = sc z in place (L_{row, row-1} = e_{row-1} / D_{row-1}), then L^T-solve
       // z = D^-1 y - L^T z from the bottom
       // (one dependent FMA per row in both solves: the row's coefficients -e_{r-1} / D_{r-1} and
@@ -1073,7 +801,6 @@ __device__ __noinline__ bool gram_svd_body_t(const TwoSiteJob& j) {
     }
     if (tid == 0) atomicAdd(&g_gram_ticks[7], __builtin_amdgcn_s_memtime() - t_last);  // S5 A: inverse iteration
   }
-#if AQC_S6_TPRE
   else if (AQC_S6_TPRE_SKIP0 ? ((wave & 3) != 0 && wave - 1 - (wave >> 2) < ((C - 1 + 15) >> 4))
                               : (wave >= 4 && wave < 4 + ((C - 1 + 15) >> 4))) {  // (uniform per wave)
     // block b of S6's loop (reflectors k0 .. k1 - 1, counted from the last): S = Y^H Y, then T by
@@ -1122,7 +849,6 @@ __device__ __noinline__ bool gram_svd_body_t(const TwoSiteJob& j) {
 #pragma unroll
     for (int m = 0; m < 4; ++m) aqc::stg(Sg + 256 + a * 16 + g + 4 * m, tq[m]);
   }
-#endif
   __syncthreads();
   if (wave == 0) {  // Gram-Schmidt inside clusters (uniform loop over wave 0)
     // clusters: gaps below 1e-7 ||T|| (dstein's 1e-3 is far more conservative than three
@@ -1184,8 +910,8 @@ __device__ __noinline__ bool gram_svd_body_t(const TwoSiteJob& j) {
   // accumulator layout: wave w holds column tile w & 3 and row tiles 2 (w >> 2), 2 (w >> 2) + 1
   // (lane l: column l & 15, rows (l >> 4) + 4 q) -- which is also the B-operand layout of Y^H V, so
   // V never leaves the registers.  Per block: Y^H V as four partial products per column tile
-  // (summed through the LDS), S = Y^H Y on the same A operands (four waves), T by the
-  // zlarft recurrence in one wave, W2 = T (Y^H V) on the VALU, V -= Y W2; five barriers. ----
+  // (three of them through the LDS), T from S5's precompute, W2 = T (Y^H V) on the matrix cores in
+  // the summing waves, V -= Y W2; four barriers. ----
   const int nt = wave & 3, mg = wave >> 2, li = lane & 15, lk = lane >> 4;
   aqc::d4_t vre[2], vim[2];
 #pragma unroll
@@ -1198,15 +924,11 @@ __device__ __noinline__ bool gram_svd_body_t(const TwoSiteJob& j) {
     }
   }
   // LDS (complex units): Y [128][16] (column index swizzled by row & 15: conflict-free reads along
-  // rows and along columns), Y^H V partials of waves 4..15, S partials of waves 0, 10, 15 (then T),
-  // Y^H V, W2 = T Y^H V, S
+  // rows and along columns), Y^H V partials of waves 4..15, T (from S5's precompute), W2 = T Y^H V
   cplx* Yl = xbuf;
   cplx* Pw = Yl + 2048;
-  cplx* Ps = Pw + 12 * 256;
-  cplx* W1l = Ps + 3 * 256;
-  cplx* W2l = W1l + 16 * 64;
-  cplx* Sl = W2l + 16 * 64;  // ends at 8192
-  cplx* Tl = Ps;             // [16][17], after wave 5 has read the S partials
+  cplx* Tl = Pw + 12 * 256;      // [16][17]
+  cplx* W2l = Tl + 3 * 256 + 16 * 64;
   auto fetch_y = [&](int k0, int nb, cplx (&y)[2]) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
@@ -1222,28 +944,20 @@ __device__ __noinline__ bool gram_svd_body_t(const TwoSiteJob& j) {
   }
   __syncthreads();  // V's initial values are read from zb: the LDS can be overwritten now
   for (int k1 = C - 1; k1 > 0; k1 -= 16) {
-    const int k0 = k1 > 16 ? k1 - 16 : 0, nb = k1 - k0;
+    const int k0 = k1 > 16 ? k1 - 16 : 0;
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int e = tid + 1024 * u, row = e >> 4, i = e & 15;
       Yl[row * 16 + (i ^ (row & 15))] = ynx[u];
     }
-#if AQC_S6_TPRE
     if (tid < 256) {  // this block's T from S5 (agent-scope loads: see the precompute)
       const gdbl_t* tp = (const gdbl_t*)(const double*)(hh + kTfacOff + (size_t)((C - 1 - k1) >> 4) * 512 + 256 + tid);
       Tl[(tid >> 4) * 17 + (tid & 15)] = aqc::cmk(__hip_atomic_load(tp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
                                                   __hip_atomic_load(tp + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     }
-#endif
-#if !AQC_S6_LATE_FETCH
-    if (k0 > 0) {  // the next block's reflectors, in flight during this one
-      const int n1 = k0, n0 = n1 > 16 ? n1 - 16 : 0;
-      fetch_y(n0, n1 - n0, ynx);
-    }
-#endif
     __syncthreads();  // B1: Y
-    // Y^H V over this wave's 32 rows (and Y^H Y on the waves mg == nt, one per SIMD): A[m = i][k = row] = conj(Y[row][i])
-    aqc::d4_t wr = {0, 0, 0, 0}, wi = {0, 0, 0, 0}, sr = {0, 0, 0, 0}, si = {0, 0, 0, 0};
+    // Y^H V over this wave's 32 rows: A[m = i][k = row] = conj(Y[row][i])
+    aqc::d4_t wr = {0, 0, 0, 0}, wi = {0, 0, 0, 0};
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       if (32 * mg + 16 * t + 15 > k0) {  // rows <= k0 of Y are zero (uniform per wave)
@@ -1255,12 +969,6 @@ __device__ __noinline__ bool gram_svd_body_t(const TwoSiteJob& j) {
           wr = __builtin_amdgcn_mfma_f64_16x16x4f64(y.y, vim[t][s], wr, 0, 0, 0);
           wi = __builtin_amdgcn_mfma_f64_16x16x4f64(y.x, vim[t][s], wi, 0, 0, 0);
           wi = __builtin_amdgcn_mfma_f64_16x16x4f64(-y.y, vre[t][s], wi, 0, 0, 0);
-          if (!AQC_S6_TPRE && mg == nt) {
-            sr = __builtin_amdgcn_mfma_f64_16x16x4f64(y.x, y.x, sr, 0, 0, 0);
-            sr = __builtin_amdgcn_mfma_f64_16x16x4f64(y.y, y.y, sr, 0, 0, 0);
-            si = __builtin_amdgcn_mfma_f64_16x16x4f64(y.x, y.y, si, 0, 0, 0);
-            si = __builtin_amdgcn_mfma_f64_16x16x4f64(-y.y, y.x, si, 0, 0, 0);
-          }
         }
       }
     }
@@ -1269,13 +977,8 @@ __device__ __noinline__ bool gram_svd_body_t(const TwoSiteJob& j) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) Pw[((mg - 1) * 4 + nt) * 256 + (lk + 4 * q) * 16 + li] = aqc::cmk(wr[q], wi[q]);
     }
-    if (!AQC_S6_TPRE && mg == nt && mg != 1) {
-      const int slot = mg == 0 ? 0 : mg - 1;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) Ps[slot * 256 + (lk + 4 * q) * 16 + li] = aqc::cmk(sr[q], si[q]);
-    }
     __syncthreads();  // B2: partials
-    if (AQC_S6_TPRE && AQC_S6_W2MFMA && mg == 0) {
+    if (mg == 0) {
       // Y^H V of column tile nt summed in registers, then W2 = T (Y^H V) for that tile on the matrix
       // cores right here: the sum's D layout (row lk + 4 q, column li) is the B operand of k-step q
       // and T (in the LDS since B1) the A operand -- no W1 round trip through the LDS, no B3
@@ -1299,69 +1002,14 @@ __device__ __noinline__ bool gram_svd_body_t(const TwoSiteJob& j) {
       }
 #pragma unroll
       for (int q = 0; q < 4; ++q) W2l[(lk + 4 * q) * 64 + 16 * nt + li] = aqc::cmk(w2r[q], w2i[q]);
-    } else if (mg == 0) {  // Y^H V of column tile nt
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int b = lk + 4 * q;
-        cplx w = aqc::cmk(wr[q], wi[q]);
-#pragma unroll
-        for (int m = 0; m < 3; ++m) w = aqc::cadd(w, Pw[(m * 4 + nt) * 256 + b * 16 + li]);
-        W1l[b * 64 + 16 * nt + li] = w;
-      }
-    } else if (!AQC_S6_TPRE && wave == 5) {  // S, then T (zlarft: T[a][i] = -tau_i sum_{a <= b < i} T[a][b] S[b][i])
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int b = lk + 4 * q;
-        cplx sv = aqc::cmk(sr[q], si[q]);
-#pragma unroll
-        for (int m = 0; m < 3; ++m) sv = aqc::cadd(sv, Ps[m * 256 + b * 16 + li]);
-        Sl[b * 16 + li] = sv;
-      }
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // LDS: S written, partials read
-      {  // lane (a, g): T[a][g + 4 m] (m < 4) in registers; each column's sum over b splits over
-         // the quad g = 0..3 (T[a][b] = 0 for b < a falls out of the recurrence)
-        const int fl = fresh_lane(), a = fl >> 2, g = fl & 3;  // (fresh: no spilled addresses)
-        cplx tq[4] = {aqc::cmk(0, 0), aqc::cmk(0, 0), aqc::cmk(0, 0), aqc::cmk(0, 0)};
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const cplx tau = i < nb ? s_tau[k0 + i] : aqc::cmk(0, 0);
-          cplx acc = aqc::cmk(0, 0);
-#pragma unroll
-          for (int m = 0; m < 4; ++m) {
-            if (4 * m < i) {
-              const int bb = g + 4 * m;
-              const cplx sv = bb < i ? Sl[bb * 16 + i] : aqc::cmk(0, 0);
-              acc = aqc::cfma(tq[m], sv, acc);
-            }
-          }
-          acc.x = aqc::row_sum4(acc.x);
-          acc.y = aqc::row_sum4(acc.y);
-          const cplx ti = aqc::cmul(tau, acc);
-          const cplx val = a < i ? aqc::cmk(-ti.x, -ti.y) : (a == i ? tau : aqc::cmk(0, 0));
-          if (g == (i & 3)) tq[i >> 2] = val;
-        }
-#pragma unroll
-        for (int m = 0; m < 4; ++m) Tl[a * 17 + g + 4 * m] = tq[m];
-      }
     }
-#if !(AQC_S6_TPRE && AQC_S6_W2MFMA)
-    __syncthreads();  // B3: Y^H V, T
-    {  // W2 = T (Y^H V): row i = wave (uniform), column = lane
-      const int i = wave;
-      cplx acc = aqc::cmk(0, 0);
-      for (int bb = i; bb < 16; ++bb) acc = aqc::cfma(Tl[i * 17 + bb], W1l[bb * 64 + lane], acc);
-      W2l[i * 64 + lane] = acc;
-    }
-#endif
     __syncthreads();  // B4: W2
-#if AQC_S6_LATE_FETCH
     // the next block's reflectors, in flight during the V update: issued before B1 they were
     // drained by the spill reloads' vmcnt(0) waits between B1 and B4
     if (k0 > 0) {
       const int n1 = k0, n0 = n1 > 16 ? n1 - 16 : 0;
       fetch_y(n0, n1 - n0, ynx);
     }
-#endif
     // V -= Y W2: A[m = row][k = b] = Y[row][b], B[k = b][n] = W2[b][n].  The lane's indices come
     // from the lane counter and the wave index in an SGPR: derived from the thread id (whose VGPR
     // is spilled) their reload's vmcnt(0) drained the next block's reflector loads issued above
@@ -1407,10 +1055,6 @@ __device__ __noinline__ bool gram_svd_body_t(const TwoSiteJob& j) {
   }
   tick(5);
   return true;
-}
-
-__device__ __forceinline__ bool gram_svd_body(const TwoSiteJob& j) {
-  return j.gram == 2 ? gram_svd_body_t<true>(j) : gram_svd_body_t<false>(j);
 }
 
 __global__ __launch_bounds__(1024) void k_svd_gram(const TwoSiteJob* __restrict__ jobs) {

@@ -72,10 +72,6 @@ int aqc_sv_apply(aqc_sv_t h, const aqc_op_t* ops, int nops);
 /* Host planning of aqc_sv_apply only (no GPU): out[0] segments (= launches), out[1] phases
  * (register-tile path; 0 otherwise), out[2] fused gates, out[3] tile bits. */
 int aqc_sv_plan(int n, const aqc_op_t* ops, int nops, int* out);
-/* Slots per phase of the register-tile kernel (n >= 14): 4 (default; 256 threads x 16 amplitudes
-   per 4096-amplitude tile) or 3 (512 threads x 8: two waves per SIMD at n = 20, more phases).
-   Also AQC_SV_SLOTS at first use.  Results equal up to summation order. */
-int aqc_sv_set_slots(int slots);
 /* sv[0] (aer_sv_backend.py:29). */
 int aqc_sv_amp0(aqc_sv_t h, double* re, double* im);
 /* <Z_i> = p0 - p1 for all i (aer_sv_backend.py:49-59), out[n]. */
@@ -118,77 +114,6 @@ int aqc_mps_apply_sort_batch(aqc_mps_t* hs, int nstates, const aqc_op_t* const* 
 int aqc_mps_apply_sort_batch_async(aqc_mps_t* hs, int nstates, const aqc_op_t* const* ops, const int* nops);
 /* Wait for the states' queued work and report their error flags (AQC_ERR_STATE etc.). */
 int aqc_mps_check_batch(aqc_mps_t* hs, int nstates);
-/* Diagnostics: largest Jacobi sweep count since the last call (then reset). */
-int aqc_mps_jacobi_stats(aqc_mps_t h, int* max_sweeps);
-/* Jacobi rotation threshold |a^H b| > factor * L * eps * |a||b| (default factor 1). */
-/* Register / block Jacobi: dot-product noise floor of the rotations in units of eps ||W|| (|a| + |b|)
- * (default 0: the relative threshold alone). */
-int aqc_mps_set_jacobi_noise(double factor);
-int aqc_mps_set_jacobi_tol(double factor);
-/* Jacobi sweep stop: after a sweep whose counted rotations all moved at most tiny_t^2 of their
-   pair's squared norms (t |g| <= tiny_t^2 (|a|^2 + |b|^2); |t| <= tiny_t for separated pairs) the
-   decomposition ends (default 1e-6; tiny_t <= 0 restores it; must be < 1e-3). */
-int aqc_mps_set_jacobi_stop(double tiny_t);
-/* Two-site SVD at 2 chi = 128: gram = 1 (default) tries the Gram / tridiagonal path first (G = X^H X
-   on the matrix cores, Householder tridiagonalisation, multisection, inverse iteration; taken when
-   the kept count K = min(2 chi, max_chi) <= 64 and lambda_K > 1e-9 lambda_1, else the register
-   Jacobi runs), gram = 0 the register Jacobi only, gram = 2 the Gram path with the lower-triangle
-   tridiagonalisation (svd_tri.h's stages on the 1024-thread workgroup).  debug_max_chi: max_chi of
-   aqc_svd_debug. */
-int aqc_mps_set_svd_path(int gram, int debug_max_chi);
-/* Diagnostics: shader-clock ticks of the Gram path's phases since the last call (then reset);
-   out[12]: Gram GEMM, tridiagonalisation, eigenvalues, eigenvectors, back-transformation, output,
-   then the tridiagonalisation's column steps, the inverse iteration, the steps' phase A, and two
-   diagnostics of a build with AQC_S3_DIAG (else 0). */
-int aqc_svd_gram_ticks(double* out);
-/* Gram-path counters since the last call (then reset): out[0] two-site SVDs that tried the Gram
-   path, out[1] taken, out[2] declined by shape (K > 64, 2 chi != 128), out[3] declined at the
-   eigenvalue floor (lambda_K <= 1e-9 lambda_1; the register Jacobi ran instead).  out[4]. */
-int aqc_svd_gram_stats(double* out);
-/* Block Jacobi pair visits (2 chi > 128), shader-clock ticks summed over workgroups since the
- * last call: out[0] Gram, out[1] inner Jacobi sweep, out[2] A V, out[3] visits.  Resets. */
-int aqc_bj_ticks(double* out);
-/* Two-site SVDs at 2 chi in (128, 1024] (gram_big.hip; replaces the block Jacobi of the reference's
-   Aer MPS truncation for chi = 128 ... 512, aer_mps_backend.py:76-78 via qiskit-aer's MPS two-site
-   SVD): counters since the last call (then reset): out[0] jobs that entered the multi-workgroup
-   Gram path, out[1] taken, out[2] declined (Gram path off for the job, or 2 chi < 4), out[3]
-   declined at the eigenvalue floor (lambda_K <= 1e-9 lambda_1), out[4] exchange timeouts (the
-   tridiagonalisation's workgroups did not all run together); declined jobs ran the block Jacobi.
-   The environment variable AQC_BIG_GRAM=0 selects the block Jacobi alone. */
-int aqc_svd_gram_big_stats(double* out);
-/* Diagnostics of the same path: shader-clock ticks summed over calls (then reset): out[0..4] the
-   tridiagonalisation's per-column phases on job 0's first workgroup (register pass + row sums,
-   publish, counter wait, reads + p^H v, w / new row / partial norms), out[5] k_gb_eig (job 0),
-   out[6] k_gb_back (job 0, first block), out[7] k_gb_inv (job 0, lane 0), out[8] the next
-   reflector's zlarfg (per column, job 0's first workgroup). */
-int aqc_svd_gram_big_ticks(double* out);
-/* Counter-wait limit of the same path's tridiagonalisation in microseconds (< 0: default 100 ms);
-   a job whose workgroups wait longer declines to the block Jacobi (out[4] above).  0 forces the
-   decline wherever a wait is not already satisfied (tests). */
-int aqc_gb_set_spin_limit(double us);
-/* The same tridiagonalisation's last 128 columns: in one workgroup (on = 1, the default: the
-   trailing block goes to the job's first workgroup, which finishes without the per-column
-   exchange), or over all of the job's workgroups to the end (on = 0).  AQC_GB_TAIL=0 also selects 0. */
-int aqc_gb_set_tail(int on);
-/* Test load: nblocks 256-thread workgroups on a private stream, block b spinning (b % 16 + 1) / 16
-   of `ms` milliseconds, so work queued on other streams starts one CU at a time.  Asynchronous. */
-int aqc_debug_hog(int nblocks, double ms);
-/* Device-memory cache of the library (MPS / SV handle buffers): out[0] bytes cached (freed, kept
-   for reuse), out[1] bytes handed out, out[2] blocks handed out, out[3] requests served from the
-   cache, out[4] requests that went to hipMalloc.  Limit: AQC_POOL_MB (default 8192). */
-int aqc_pool_stats(double* out);
-/* Batched applies of >= 32 states at 2*chi = 128 run every state's whole op list in
-   one fused workgroup (theta, Jacobi, truncation, split per update: no grid-wide step between
-   updates); on = 0 selects the lock-step launches per update, on = 2 the fused chain for batches
-   of any size (lab: single evaluations).  Default 1. */
-int aqc_mps_set_fused_chain(int on);
-/* The fused chain's workgroup: 1024 threads, one state per CU (k_chain, default), or 256 threads,
-   two states per CU (k_chain256: lower-triangle Gram SVD; a state whose Gram path declines finishes
-   its list on k_chain).  Also AQC_CHAIN=256 at load.  Other values: AQC_ERR_ARG. */
-int aqc_mps_set_chain_threads(int threads);
-/* Diagnostics: shader-clock ticks spent by the fused chain's workgroups (thread 0) in theta,
-   Jacobi, rank, split and one-site ops since the last call (then reset); out[5]. */
-int aqc_mps_chain_ticks(double* out);
 /* ---- ISL entanglement sweep (adapt_compiler.py:955-976 -> entanglement_measures.py:39-98) ----
    Two-qubit reduced density matrices for npairs pairs (pairs[2p], pairs[2p+1]), out = npairs x
    4 x 4 complex (row-major), row index 2*bit(max) + bit(min) as qiskit's partial_trace orders
@@ -208,18 +133,6 @@ int aqc_sv_transition(aqc_sv_t bra, aqc_sv_t ket, int q, double* out);
    3 = log-negativity.  rdms / out in device memory when on_device. */
 int aqc_entanglement_measures(const double* rdms, int count, int method, double* out, int on_device);
 
-/* Diagnostics: one register-resident Jacobi launch with pivoted-QR preconditioning (variant 2)
-   on theta (m x n column-major complex, m, n even <= 128, as the two-site update builds it), or
-   the Gram / tridiagonal path (variant 7; Jacobi fallback inside the kernel; same output contract;
-   variant 8: its 256-thread form, declines reported in the flags; variant 9: the 1024-thread form
-   with the lower-triangle tridiagonalisation).
-   w_out receives min(m,n) columns of length min(m,n); sig_out their
-   norms; perm_out (optional) the pivot order when stop_after_qr (then w_out holds X = R^H
-   unsorted).  stop_after_qr = 2 also writes the QR phase's shader-clock ticks to sig_out[0..3]
-   (downdate + pivot key, pivot barrier, reflector + barrier, update; 128 x 128 only).  For tests
-   and tools only: allocates and frees device memory per call. */
-int aqc_svd_debug(const double* theta, int m, int n, int variant, int stop_after_qr, double* w_out,
-                  double* sig_out, int* perm_out, int* sweeps);
 /* move_all_qubits_to_sorted_ordering (done implicitly by every measurement below). */
 int aqc_mps_sort(aqc_mps_t h);
 int aqc_mps_sort_batch(aqc_mps_t* hs, int nstates);
@@ -249,13 +162,6 @@ int aqc_pair_grads(aqc_mps_t psi, const double* svec, const int* pairs, int npai
 int aqc_pair_grads_batch(aqc_mps_t* psis, int nstates, const double* svec, const int* pairs,
                          int npairs, const double* u0, const double* gens, const double* degs,
                          int ngen, double* out /* nstates*npairs */, int out_is_device);
-/* Chain kernel of the sweep: 0 = automatic (first qubits in groups of 8 advancing together on the
- * matrix cores for batches of states at bond capacity 64 or 128; for a single state the segmented
- * sweep above capacity 64, else one chain per workgroup), 1 = one chain per workgroup, 2 = grouped
- * whenever the capacity allows, 3 = the segmented sweep (prefix / suffix products of the site
- * matrices over ~sqrt(n) segments as batched MFMA GEMMs) for every single state.  Results are the
- * same up to floating-point summation order. */
-int aqc_sweep_set_chain_mode(int mode);
 /* Orders `stream` (a hipStream_t of the current device; NULL = the legacy default stream) after
    everything queued so far on the library's stream of that device, without a host wait. */
 int aqc_stream_join(void* stream);
@@ -280,6 +186,10 @@ int aqc_mps_product_fit(aqc_mps_t psi, double* svec, int guess_from_gamma, int m
  * scores are read on the library's stream: order it after their producer (aqc_stream_wait). */
 int aqc_argmax_scaled(const double* scores, const double* prio, int count, int scores_is_device,
                       int* best);
+
+/* Diagnostics, lab switches and test hooks (path selection, phase ticks, path counters, a CU-holding
+   test load, the SVD kernel on its own) are declared in aqc_hip_diag.h: they are not part of the
+   drop-in boundary. */
 
 /* ---- multi-GPU exchange over RCCL ---------------------------------------------
  * The candidate sweep shards the coupling-map pairs across ranks (one process per GPU); its one

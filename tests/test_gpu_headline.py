@@ -30,15 +30,13 @@ def _gram_expectation(svd_logs, max_chi):
     return calls, take, decline
 
 
-@pytest.mark.parametrize("chain", [1024, 256, "tri1024"])
 @pytest.mark.parametrize("kind", ["near-product", "random"])
-def test_bench_overlap_workload_fused_chain_vs_oracle(kind, chain):
+def test_bench_overlap_workload_fused_chain_vs_oracle(kind):
     """10 states x 4 distances = 40 evaluations in one apply + sort batch (k_chain), every one
     against the oracle replay: exact bond dimensions and overlap within 1e-6 (truncated-MPS
     tolerance of BASELINE.json).  The Gram-path counters (aqc_svd_gram_stats) must show every
     update going through the SVD, the Gram path taken wherever the oracle's spectrum puts lambda_K
-    a decade above its 1e-9 lambda_1 floor and declined wherever it is a decade below.  chain: the
-    fused chain's workgroup (k_chain, or k_chain256 with its hand-over of declined updates)."""
+    a decade above its 1e-9 lambda_1 floor and declined wherever it is a decade below."""
     from adaptaqc_amd import _lib
     from adaptaqc_amd.device import DeviceMPS, apply_batch, check_batch, copy_batch, overlap_zero_batch
 
@@ -59,19 +57,10 @@ def test_bench_overlap_workload_fused_chain_vs_oracle(kind, chain):
     # the random-state case runs the bench's pipelined form: queued apply, read-back, deferred check
     pipelined = kind == "random"
     _lib.gram_stats()  # reset
-    L = _lib.lib()
-    # tri1024: k_chain with the lower-triangle tridiagonalisation in its Gram SVD (svd path 2)
-    _lib.check(L.aqc_mps_set_chain_threads(256 if chain == 256 else 1024))
-    if chain == "tri1024":
-        _lib.check(L.aqc_mps_set_svd_path(2, 64))
-    try:
-        apply_batch(work, ops, sort=True, wait=not pipelined)
-        ov = overlap_zero_batch(work)
-        if pipelined:
-            check_batch(work)
-    finally:
-        _lib.check(L.aqc_mps_set_chain_threads(1024))
-        _lib.check(L.aqc_mps_set_svd_path(1, 64))
+    apply_batch(work, ops, sort=True, wait=not pipelined)
+    ov = overlap_zero_batch(work)
+    if pipelined:
+        check_batch(work)
     gram = _lib.gram_stats()
     logs = []
     nontrivial = 0

@@ -148,20 +148,8 @@ def test_gate_fusion_patterns():
         np.testing.assert_allclose(d.get(), osv.simulate(n, ops), atol=1e-12, err_msg=f"n={n}")
 
 
-@pytest.fixture(params=[4, 3], ids=["slots4", "slots3"])
-def sv_slots(request):
-    """The register-tile kernel's phase width (aqc_sv_set_slots): 4 slots / 256 threads (default)
-    or 3 slots / 512 threads."""
-    from adaptaqc_amd import _lib
-
-    L = _lib.lib()
-    _lib.check(L.aqc_sv_set_slots(request.param))
-    yield request.param
-    _lib.check(L.aqc_sv_set_slots(4))
-
-
-def test_register_tile_path_vs_oracle_and_lds_kernel(monkeypatch, sv_slots):
-    """n >= 14 runs the register-resident tile kernel (gates grouped into 4- or 3-bit phases):
+def test_register_tile_path_vs_oracle_and_lds_kernel(monkeypatch):
+    """n >= 14 runs the register-resident tile kernel (gates grouped into 4-bit phases):
     random 1q/2q gates incl. fusion patterns, long-range pairs and reversed orders, against the
     oracle and against the per-gate LDS kernel (AQC_SV_TILE=lds)."""
     from adaptaqc_amd.circuit import device_ops
@@ -193,7 +181,7 @@ def test_register_tile_path_vs_oracle_and_lds_kernel(monkeypatch, sv_slots):
         np.testing.assert_allclose(got, d2.get(), atol=1e-13, err_msg=f"n={n} (lds kernel)")
 
 
-def test_config2_exact_workload_vs_oracle_goldens(sv_slots):
+def test_config2_exact_workload_vs_oracle_goldens():
     """BASELINE config 2 exactly as tools/configs_bench.py times it -- 20 qubits,
     brickwork depth 20, seeds 0..9, with 0 / 10 / 50 thinly-dressed layers -- all 30 circuits
     through the register-tile SV path against the oracle's values (tests/golden/config2_sv.npz, made
@@ -235,7 +223,7 @@ def test_config2_exact_workload_vs_oracle_goldens(sv_slots):
             k += 1
 
 
-def test_deferred_reset_every_reader(sv_slots):
+def test_deferred_reset_every_reader():
     """aqc_sv_reset on the register-tile path (n >= 14) launches nothing: the next apply's first
     pass forms |0...0> in its tiles, and every other reader (amp0, get, z_all, pair RDMs, transition,
     copy in either direction, set) sees |0...0> or overwrites it.  Each case follows an apply that
@@ -297,7 +285,7 @@ def test_deferred_reset_every_reader(sv_slots):
     np.testing.assert_allclose(t, [[np.conj(psi[0]), 0], [np.conj(psi[1 << 3]), 0]], atol=1e-15)
 
 
-def test_amp0_handed_off_by_the_final_pass(sv_slots):
+def test_amp0_handed_off_by_the_final_pass():
     """After an apply on the register-tile path the final pass writes <0...0|psi> to the pinned
     host buffer and aqc_sv_amp0 reads it without a copy: equal to the state's first amplitude after
     applies, an empty apply (state unchanged), a reset, a copy into the handle and a set."""
@@ -325,3 +313,28 @@ def test_amp0_handed_off_by_the_final_pass(sv_slots):
     psi[0], psi[5] = 0.6, 0.8
     d.set(psi)
     assert abs(d.amp0() - 0.6) < 1e-15
+
+
+def test_copy_then_destroy_source_then_reuse_block():
+    """aqc_sv_copy queues a copy that reads the source on the destination's stream.  The
+    source destroyed right after, and a new state of the same size taking its pooled block and
+    writing it at once, must not corrupt the copy (the source's stream waits for the copy)."""
+    from adaptaqc_amd.circuit import device_ops
+    from adaptaqc_amd.device import DeviceSV
+
+    n = 20
+    ops = brickwork(n, 6, 5)
+    want = osv.simulate(n, ops)
+    dops = device_ops(to_circuit(n, ops))
+    for _ in range(3):
+        src = DeviceSV(n)
+        src.apply(dops)
+        dst = DeviceSV(n)
+        dst.copy_from(src)
+        src.close()
+        other = DeviceSV(n)  # (same size: the pool hands out src's block)
+        other.apply(device_ops(to_circuit(n, brickwork(n, 8, 9))))
+        other.amp0()
+        np.testing.assert_allclose(dst.get(), want, atol=1e-12)
+        dst.close()
+        other.close()

@@ -186,38 +186,3 @@ def test_jacobi_degenerate_clusters(n, kind):
         assert sweeps < 40
 
 
-# ---- the same path on 256 threads (aqc_svd_debug variant 8, svd_tri.h: k_chain256's SVD) --------
-@pytest.mark.parametrize("variant", [8, 9], ids=["tri256", "tri1024"])
-@pytest.mark.parametrize("m,n", [(128, 128), (128, 96), (96, 128), (128, 72), (80, 80), (128, 40), (66, 128)])
-def test_gram256_vs_numpy_and_1024(m, n, variant):
-    """The lower-triangle tridiagonalisation (tiles in stages, two barriers per column) -- on 256
-    threads with S5 in two batches (variant 8, k_chain256's SVD) and on the 1024-thread body
-    (variant 9, j.gram = 2) -- against numpy and against the full-matrix 1024-thread body on the
-    same theta: sigma to 1e-12 sigma_1, the kept subspace to 1e-10, orthonormal to 1e-11, sigma
-    equal to the full-matrix path's within 1e-13 sigma_1."""
-    c = min(m, n)
-    theta = _spectrum_theta(m, n, 0.93 ** np.arange(c), 11 + m + n)
-    w8, sig8, _, sw8 = _run(theta, variant)
-    assert sw8 == 1, "the lower-triangle Gram path declined"
-    w7, sig7, _, _ = _run(theta, 7)
-    K = min(64, c)
-    x = theta if m >= n else theta.conj().T
-    _, s_ref, vh = np.linalg.svd(x)
-    order = np.argsort(-sig8)
-    got = sig8[order]
-    np.testing.assert_allclose(got[:K], s_ref[:K], rtol=0, atol=1e-12 * s_ref[0])
-    assert np.all(got[K:] == 0.0)
-    np.testing.assert_allclose(np.sort(sig8)[::-1], np.sort(sig7)[::-1], rtol=0, atol=1e-13 * s_ref[0])
-    V = w8[:, order[:K]] / got[None, :K]
-    Vr = vh[:K].conj().T
-    assert np.linalg.norm(V @ V.conj().T - Vr @ Vr.conj().T, 2) < 1e-10
-    assert np.max(np.abs(V.conj().T @ V - np.eye(K))) < 1e-11
-
-
-@pytest.mark.parametrize("kind", ["graded", "rank10"])
-def test_gram256_declines(kind):
-    """Below the Gram form's noise floor the 256-thread body declines too (flags[2] = -1 here; in
-    k_chain256 the update is handed to the 1024-thread chain)."""
-    theta = _theta(128, 128, 3) if kind == "graded" else _theta(128, 128, 4, rank=10)
-    _, _, _, sw = _run(theta, 8)
-    assert sw == -1

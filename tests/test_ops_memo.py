@@ -88,3 +88,35 @@ def test_device_ops_array_memo_released_with_circuit():
     del qc
     gc.collect()
     assert key not in C._OPS_MEMO
+
+
+class _CustomGate:
+    """A qiskit-shaped custom gate: a non-standard name, no parameters, its matrix from
+    to_matrix() (two instances with the same name can hold different matrices)."""
+
+    def __init__(self, name, mat):
+        self.name = name
+        self.num_qubits = 1
+        self.params = []
+        self._m = np.asarray(mat, dtype=complex)
+
+    def to_matrix(self):
+        return self._m
+
+
+class _SubclassedRz(Operation):
+    pass
+
+
+def test_memo_reconverts_custom_gates_and_other_types():
+    qc = _brickwork(4, 2, 3)
+    qc.data.append(CircuitInstruction(_CustomGate("mygate", [[0, 1], [1, 0]]), (1,)))
+    assert device_ops_array(qc).tobytes() == _fresh(qc)
+    # the same name at the same index with another matrix: must not reuse the memoised rows
+    qc.data[-1] = CircuitInstruction(_CustomGate("mygate", [[1, 0], [0, -1]]), (1,))
+    assert device_ops_array(qc).tobytes() == _fresh(qc)
+    assert C._params_snapshot(qc.data[-1].operation) is None
+    # a standard gate swapped for an object of another type with equal name and parameters
+    op = qc.data[0].operation
+    qc.data[0] = CircuitInstruction(_SubclassedRz(op.name, 1, list(op.params)), qc.data[0].qubits)
+    assert device_ops_array(qc).tobytes() == _fresh(qc)
