@@ -100,6 +100,8 @@ struct OneSiteJob {
 using aqc::TwoSiteJob;
 using aqc::kMaxCap;
 using aqc::kSigMax;
+using aqc::kSigTail;
+using aqc::kSigLen;
 
 // ------------------------------------------------------------------------------------------
 __global__ void k_mps_zero(cplx* gam, double* lam, int* dims, int n, int cap) {
@@ -752,14 +754,18 @@ __device__ __forceinline__ void rank_body(const TwoSiteJob& j) {
       if (sv[i] * sv[i] > kChop) ++k;
     if (k < 1) k = 1;
     if (j.max_chi > 0 && k > j.max_chi) k = j.max_chi;
-    if (k > j.cap) {
-      k = j.cap;
-      atomicOr(&j.flags[0], 1);
-    }
-    double tail = 0.0;
+    // (a Gram path that decided the kept count hands over the tail it removed: sig[kSigTail])
+    double tail = aqc::ldg(j.sig + kSigTail);
     while (k > 1 && tail + sv[k - 1] * sv[k - 1] < j.thr) {
       tail += sv[k - 1] * sv[k - 1];
       --k;
+    }
+    aqc::stg(j.sig + kSigTail, 0.0);
+    // the bond capacity is this library's limit, not Aer's: only a kept count above it (after the
+    // whole reduce_zeros rule) overflows
+    if (k > j.cap) {
+      k = j.cap;
+      atomicOr(&j.flags[0], 1);
     }
     double nn = 0.0;
     for (int i = 0; i < k; ++i) nn += sv[i] * sv[i];
@@ -1720,14 +1726,15 @@ int ensure_slots(aqc_mps_t h, int nslots) {
   while ((int)h->slots.size() + 1 < nslots) {
     aqc_mps_s::Slot sl;
     sl.theta = (cplx*)aqc::dev_alloc(4 * cap * cap * sizeof(cplx));
-    sl.work = (cplx*)aqc::dev_alloc(4 * cap * cap * sizeof(cplx));
-    sl.sig = (double*)aqc::dev_alloc(2 * kSigMax * sizeof(double));
+    sl.work = (cplx*)aqc::dev_alloc(aqc::work_elems(cap) * sizeof(cplx));
+    sl.sig = (double*)aqc::dev_alloc(kSigLen * sizeof(double));
     sl.perm = (int*)aqc::dev_alloc(kSigMax * sizeof(int));
     if (!sl.theta || !sl.work || !sl.sig || !sl.perm) {
       aqc::dev_free(sl.theta), aqc::dev_free(sl.work), aqc::dev_free(sl.sig), aqc::dev_free(sl.perm);
       aqc::set_error("ensure_slots: out of device memory");
       return AQC_ERR_NOMEM;
     }
+    AQC_HIP_CHECK(hipMemsetAsync(sl.sig, 0, kSigLen * sizeof(double), aqc::mps_stream()));
     h->slots.push_back(sl);
   }
   return AQC_OK;
@@ -2135,7 +2142,7 @@ int aqc_mps_create(int n, int chi_cap, double threshold, int max_chi, aqc_mps_t*
   // the fixed buffers carved from one cached device block (256-byte aligned pieces)
   {
     const size_t sz[11] = {g * sizeof(cplx), (size_t)(n + 1) * cap * sizeof(double), (size_t)(n + 1) * sizeof(int),
-                           4 * cap * cap * sizeof(cplx), 4 * cap * cap * sizeof(cplx), 2 * kSigMax * sizeof(double),
+                           4 * cap * cap * sizeof(cplx), aqc::work_elems(cap) * sizeof(cplx), kSigLen * sizeof(double),
                            kSigMax * sizeof(int), 4 * sizeof(int), 2 * (size_t)(n + 1) * cap * sizeof(cplx),
                            2 * cap * cap * sizeof(cplx), (size_t)(2 * n + 8) * sizeof(cplx)};
     size_t off[11], total = 0;
@@ -2166,6 +2173,7 @@ int aqc_mps_create(int n, int chi_cap, double threshold, int max_chi, aqc_mps_t*
   AQC_HIP_CHECK(hipMemsetAsync(h->d.gam, 0, g * sizeof(cplx), st));
   AQC_HIP_CHECK(hipMemsetAsync(h->d.lam, 0, (size_t)(n + 1) * cap * sizeof(double), st));
   AQC_HIP_CHECK(hipMemsetAsync(h->d.flags, 0, 4 * sizeof(int), st));
+  AQC_HIP_CHECK(hipMemsetAsync(h->d.sig, 0, kSigLen * sizeof(double), st));
   hipLaunchKernelGGL(k_mps_zero, dim3(1 + n / 256), dim3(256), 0, st, h->d.gam, h->d.lam, h->d.dims, n, chi_cap);
   AQC_CHECK_LAUNCH();
   AQC_HIP_CHECK(hipStreamSynchronize(st));
@@ -2208,14 +2216,14 @@ int aqc_svd_debug(const double* theta, int m, int n, int variant, int stop_after
               "aqc_svd_debug: variant 7 (Gram) needs 64 < max(m, n) <= 128 and no QR stop");
   hipStream_t st = aqc::mps_stream();
   const int cp = std::max(m, n) <= 32 ? 32 : (std::max(m, n) <= 64 ? 64 : 128);
-  const size_t mat = (size_t)128 * 128 * sizeof(cplx);
+  const size_t mat = (size_t)128 * 128 * sizeof(cplx), wmat = aqc::work_elems(64) * sizeof(cplx);
   char* buf = nullptr;
-  AQC_HIP_CHECK(hipMalloc(&buf, 2 * mat + 1024 * sizeof(double) + 512 * sizeof(int) + 8 * sizeof(int) +
+  AQC_HIP_CHECK(hipMalloc(&buf, mat + wmat + kSigLen * sizeof(double) + 512 * sizeof(int) + 8 * sizeof(int) +
                                     sizeof(TwoSiteJob)));
   cplx* th = (cplx*)buf;
   cplx* wk = (cplx*)(buf + mat);
-  double* sg = (double*)(buf + 2 * mat);
-  int* pm = (int*)(sg + 1024);
+  double* sg = (double*)(buf + mat + wmat);
+  int* pm = (int*)(sg + kSigLen);
   int* dm = pm + 512;  // dims[3] + flags share this tail
   int* fl = dm + 4;
   TwoSiteJob* dj = (TwoSiteJob*)(fl + 4);
@@ -2239,7 +2247,8 @@ int aqc_svd_debug(const double* theta, int m, int n, int variant, int stop_after
   AQC_HIP_CHECK(hipMemcpyAsync(th, theta, (size_t)m * n * sizeof(cplx), hipMemcpyHostToDevice, st));
   AQC_HIP_CHECK(hipMemcpyAsync(dm, hd, sizeof(hd), hipMemcpyHostToDevice, st));
   AQC_HIP_CHECK(hipMemcpyAsync(dj, &j, sizeof(j), hipMemcpyHostToDevice, st));
-  AQC_HIP_CHECK(hipMemsetAsync(wk, 0, mat, st));
+  AQC_HIP_CHECK(hipMemsetAsync(wk, 0, wmat, st));
+  AQC_HIP_CHECK(hipMemsetAsync(sg, 0, kSigLen * sizeof(double), st));
   if (cp == 32) hipLaunchKernelGGL((k_jacobi_reg<32, 2>), dim3(1), dim3(256), 16 * 33 * 16, st, dj);
   else if (cp == 64) hipLaunchKernelGGL((k_jacobi_reg<64, 4>), dim3(1), dim3(512), 32 * 65 * 16, st, dj);
   else if (variant == 7)

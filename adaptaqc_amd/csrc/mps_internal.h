@@ -15,9 +15,19 @@ namespace aqc {
 //   dims: (n+1) ints on device, dims[0] = dims[n] = 1.
 // The qubit permutation created by Aer's swap routing lives on the host (order / loc).
 // Largest two-site column count 2 chi (bond capacity <= 512): the singular-value buffer holds the
-// raw column norms at [0, kSigMax) and the sorted values at [kSigMax, 2 kSigMax).
+// raw column norms at [0, kSigMax) and the sorted values at [kSigMax, 2 kSigMax).  sig[kSigTail]:
+// the part of the reduce_zeros tail sum that an SVD path which decides the kept count itself (the
+// Gram paths, svd_gram.h / gram_big.hip) has already removed -- it writes the kept singular values
+// and zeros, and the rank step's tail rule continues from this sum (then resets it to 0).
 constexpr int kSigMax = 1024;
 constexpr int kMaxCap = kSigMax / 2;
+constexpr int kSigTail = 2 * kSigMax;
+constexpr int kSigLen = 2 * kSigMax + 2;  // doubles
+// Two-site work buffer (complex elements): 4 cap^2 (the Jacobi's working columns), and at least what
+// the 2 chi = 128 Gram path lays out in it (svd_gram.h: reflectors, W, the compact-WY factors and the
+// inverse-iteration scratch of more than 64 kept vectors)
+constexpr size_t kGramWorkElems = 36864;
+inline size_t work_elems(size_t cap) { return 4 * cap * cap > kGramWorkElems ? 4 * cap * cap : kGramWorkElems; }
 
 struct MpsDev {
   int n = 0;
@@ -27,8 +37,8 @@ struct MpsDev {
   int* dims = nullptr;
   // two-site workspace
   cplx* theta = nullptr;  // (2cap)^2, column-major M x N
-  cplx* work = nullptr;   // (2cap)^2, Jacobi working columns
-  double* sig = nullptr;  // 2 kSigMax: column norms, then the sorted values
+  cplx* work = nullptr;   // work_elems(cap): Jacobi working columns / Gram-path scratch
+  double* sig = nullptr;  // kSigLen: column norms, then the sorted values, then the removed tail
   int* perm = nullptr;    // kSigMax sorted -> column index
   int* flags = nullptr;   // [0] capacity overflow, [1] jacobi non-convergence, [2] max sweeps used
   // measurement workspace

@@ -45,17 +45,13 @@ constexpr int kGramMaxK = 64;
 // S5: three inverse-iteration steps per eigenvector; the LDL^T pivots from the leading minors'
 //     recurrence (one FMA + the guard on the chain)
 // S6: the compact-WY factors of every reflector block precomputed during S5 by the idle waves
-//     4..11; W2 = T (Y^H V) on the matrix cores inside the mg == 0 waves; the next block's
+//     1-3, 5-7, 9-11 (not 4 and 8, which share SIMD 0 with wave 0's inverse iteration: S5 133 K ->
+//     120 K ticks, k_chain -0.8% against waves 4..11, profiles/r5_s6_skip0_ab.json); W2 = T (Y^H V) on the matrix cores inside the mg == 0 waves; the next block's
 //     reflectors fetched after B4
 constexpr double kGramRelFloor = 1e-9;
 // shader-clock ticks of the phases (thread 0), summed over calls: S1, S2+S3, S4, S5, S6, output,
 // S3's column steps, S5's inverse iteration, S3's phase A (column pass + zlarfg + first barrier)
 __device__ unsigned long long g_gram_ticks[12];
-// S6's precompute on the waves 1-3, 5-7, 9-11 (not the waves 4 and 8, which share SIMD 0 with
-// wave 0's inverse iteration) instead of the waves 4..11 (A/B pending)
-#ifndef AQC_S6_TPRE_SKIP0
-#define AQC_S6_TPRE_SKIP0 0
-#endif
 static_assert(kGramMaxK <= 64, "S5: the inverse iteration (tid < K) must stay on wave 0");
 // path counters (thread 0 of each call): [0] calls, [1] taken, [2] declined by shape (K > 64, ...),
 // [3] declined at the eigenvalue floor (lambda_K <= 1e-9 lambda_1 -> the Jacobi runs)
@@ -196,12 +192,56 @@ __device__ __forceinline__ double rcp_nr(double x) {
 constexpr size_t kTfacOff = 8192;
 typedef __attribute__((address_space(1))) double gdbl_t;
 
+// reduce_zeros (oracle/mps.py truncation_rank: Aer's rule as the reference drives it,
+// aer_mps_backend.py:27-42) on the top KE eigenvalues lam (descending, = sigma^2) of G, each known to
+// +-err: CHOP (sigma^2 > 1e-16), the max_chi cap, then the tail rule (drop the smallest while the
+// dropped sum stays below thr).  Every comparison must hold for any values inside the error bars --
+// err is the multisection bracket, plus the noise of forming and reducing G (16 C eps ||T||) -- and
+// the kept values must clear the Gram path's floor (lambda_K > 1e-9 lambda_1); otherwise -1 (the
+// caller declines and the Jacobi decides).  An eigenvalue whose CHOP decision is open may still be
+// dropped by the tail rule from either start, which then decides nothing: it enters the tail as
+// [0, lam + err].  Returns the kept count K, and in tail_out the dropped tail sum (handed to
+// rank_body through sig[kSigTail], whose own tail rule then keeps all K).
+__device__ __noinline__ int gram_keep(const double* lam, const double* err, int KE, int C, int max_chi, double thr,
+                                      double tn, double& tail_out) {
+  const double noise = 16.0 * C * 2.220446049250313e-16 * tn;
+  int k_lo = 0, k_hi = 0;  // counts surely / possibly above the CHOP (lam descending)
+  for (int i = 0; i < KE; ++i) {
+    const double e = err[i] + noise;
+    if (lam[i] - e > kChop) k_lo = i + 1;
+    if (lam[i] + e > kChop) k_hi = i + 1;
+  }
+  int k = k_hi < 1 ? 1 : k_hi;
+  if (max_chi > 0 && k > max_chi) k = max_chi;
+  double tail = 0.0, unc = 0.0;
+  while (k > 1) {
+    const int i = k - 1;
+    const double e = err[i] + noise;
+    double v = lam[i], ev = e;
+    if (i >= k_lo) {  // CHOP open: contributes anything in [0, lam + e] if dropped
+      v = 0.5 * (lam[i] + e);
+      ev = v;
+    }
+    const double sum = tail + v, m = unc + ev;
+    if (fabs(sum - thr) <= m) return -1;  // the comparison is open
+    if (sum >= thr) break;
+    tail = sum;
+    unc = m;
+    --k;
+  }
+  if (k > k_lo) return -1;  // a kept value whose CHOP is open (also far below the floor)
+  if (!(lam[0] > 0.0) || !(lam[k - 1] > kGramRelFloor * lam[0])) return -1;
+  tail_out = tail;
+  return k;
+}
+
 // Gram-path SVD of one 2 chi x 2 chi theta'; 1024 threads; `xbuf` = the workgroup's dynamic LDS
 // (>= 4 GemmLds).  Returns false (work untouched beyond scratch, caller runs the Jacobi) when the
 // fast path does not apply.  Uniform in the workgroup.
 __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
   extern __shared__ double2 xbuf[];
-  __shared__ double s_d[128], s_e[128], s_e2[128], s_lam[kGramMaxK], s_sig2[kGramMaxK];
+  __shared__ double s_d[128], s_e[128], s_e2[128], s_lam[128], s_err[128], s_sig2[kGramMaxK], s_tail;
+  __shared__ int s_K;
   __shared__ cplx s_tau[128];
   __shared__ double s_lo, s_hi, s_tn;
   __shared__ double2 s_de[128];
@@ -209,13 +249,14 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
   const int M = 2 * chl, N = 2 * chr;
   const bool tr = M < N;
   const int L = tr ? N : M, C = tr ? M : N;
-  int K = C;
-  if (j.max_chi > 0 && j.max_chi < K) K = j.max_chi;
+  // eigenvalues computed: the top KE (max_chi, if it binds, caps the kept count first); the kept
+  // count K itself follows reduce_zeros on them after S4 (gram_keep)
+  const int KE = (j.max_chi > 0 && j.max_chi < C) ? j.max_chi : C;
   // (j.work holds the packed reflectors, <= 8128 complex: capacity 64)
   const int tid = fresh_tid(), lane = tid & 63, wave = tid >> 6;
   const int wave_s = __builtin_amdgcn_readfirstlane(wave);  // (uniform: an SGPR)
   if (tid == 0) atomicAdd(&g_gram_stats[0], 1ull);
-  if (K > kGramMaxK || C < 4 || C > 128 || L > 128 || j.cap < 64) {
+  if (C < 4 || C > 128 || L > 128 || j.cap < 64) {
     if (tid == 0) atomicAdd(&g_gram_stats[2], 1ull);
     return false;
   }
@@ -653,7 +694,11 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
     constexpr double kInvF = 1.0 / (kFirst + 1), kInvG = 1.0 / (kG + 1);
     if (tid < kFirst) cntb[tid] = sturm_count_poly(s_de, C, (lo0 + span0 * (double)(tid + 1) * kInvF) * itn);
     __syncthreads();
-    if (tid < 64 * kG) {  // uniform per wave
+    // with a tail threshold above the Gram form's noise the reduce_zeros decisions compare sums of
+    // small eigenvalues with it: three more rounds bring the brackets (span x 1.6e-11) down to that
+    // noise (gram_keep)
+    const int rounds = kRounds + (j.thr > 1e-12 * s_tn ? 3 : 0);
+    if (tid < KE * kG) {  // (whole kG-lane groups)
       double lo, hi;
       {
         int l = 0, h = kFirst;  // first t with cnt[t] >= a + 1 (kFirst: none)
@@ -665,7 +710,7 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
         lo = l > 0 ? lo0 + span0 * (double)l * kInvF : s_lo;
         hi = l < kFirst ? lo0 + span0 * (double)(l + 1) * kInvF : s_hi;
       }
-      for (int round = 0; round < kRounds; ++round) {
+      for (int round = 0; round < rounds; ++round) {
         const double x = lo + (hi - lo) * (double)(sub + 1) * kInvG;
         const int cnt = sturm_count_poly(s_de, C, x * itn);
         const unsigned long long bal = __ballot(cnt >= a + 1);
@@ -676,13 +721,19 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
         lo = nlo;
         hi = nhi;
       }
-      if (eid < K && sub == 0) s_lam[eid] = 0.5 * (lo + hi);
+      if (sub == 0) {
+        s_lam[eid] = 0.5 * (lo + hi);
+        s_err[eid] = 0.5 * (hi - lo);
+      }
     }
   }
   __syncthreads();
+  if (tid == 0) s_K = gram_keep(s_lam, s_err, KE, C, j.max_chi, j.thr, s_tn, s_tail);
+  __syncthreads();
   tick(2);
-  if (!(s_lam[0] > 0.0) || !(s_lam[K - 1] > kGramRelFloor * s_lam[0])) {  // uniform
-    if (tid == 0) atomicAdd(&g_gram_stats[3], 1ull);
+  const int K = s_K;  // (uniform)
+  if (K < 0 || K > kGramMaxK) {  // open decisions / below the floor; more than 64 kept
+    if (tid == 0) atomicAdd(&g_gram_stats[K < 0 ? 3 : 2], 1ull);
     return false;
   }
   // ---- S5: inverse iteration, Gram-Schmidt in clusters, Rayleigh quotients ----
@@ -801,13 +852,13 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
     }
     if (tid == 0) atomicAdd(&g_gram_ticks[7], __builtin_amdgcn_s_memtime() - t_last);  // S5 A: inverse iteration
   }
-  else if (AQC_S6_TPRE_SKIP0 ? ((wave & 3) != 0 && wave - 1 - (wave >> 2) < ((C - 1 + 15) >> 4))
-                              : (wave >= 4 && wave < 4 + ((C - 1 + 15) >> 4))) {  // (uniform per wave)
+  else if ((wave & 3) != 0 && wave - 1 - (wave >> 2) < ((C - 1 + 15) >> 4)) {  // (uniform per wave)
     // block b of S6's loop (reflectors k0 .. k1 - 1, counted from the last): S = Y^H Y, then T by
     // zlarft, into the work scratch after the reflectors (S at [0, 256), T at [256, 512) of the
     // block's 512).  Read back through agent-scope loads: the same addresses were read by the
     // previous update's S6 on this CU, so the L1 may hold them.
-    const int b = AQC_S6_TPRE_SKIP0 ? wave - 1 - (wave >> 2) : wave - 4, k1 = C - 1 - 16 * b, k0 = k1 > 16 ? k1 - 16 : 0, nb = k1 - k0;
+    // (waves 1-3, 5-7, 9-11: block b = wave - 1 - wave / 4)
+    const int b = wave - 1 - (wave >> 2), k1 = C - 1 - 16 * b, k0 = k1 > 16 ? k1 - 16 : 0, nb = k1 - k0;
     const int li = lane & 15, lk = lane >> 4;
     aqc::d4_t sr = {0, 0, 0, 0}, si = {0, 0, 0, 0};
     for (int r0 = 0; r0 < C; r0 += 4) {  // A[m = i][k = row] = conj(Y[row][i]), B = Y
@@ -1049,6 +1100,7 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
     }
   }
   for (int c = tid; c < C; c += 1024) aqc::stg(j.sig + c, c < K ? sqrt(s_sig2[c]) : 0.0);
+  if (tid == 0) aqc::stg(j.sig + kSigTail, s_tail);  // the tail gram_keep dropped (rank_body)
   if (tid == 0) {
     atomicMax(&j.flags[2], 1);
     atomicAdd(&g_gram_stats[1], 1ull);
