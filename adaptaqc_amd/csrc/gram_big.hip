@@ -90,6 +90,9 @@ struct GBArgs {
   double* dinv;    // per job CT x CT: inverse-iteration pivots
   double* sig2;    // per job CT
   double* lam;     // per job CT: the top K eigenvalues of T, descending
+  double* err;     // per job CT: their multisection brackets' half widths
+  int* kept;       // per job: the kept count (reduce_zeros on lam, k_gb_keep)
+  double* tail;    // per job: the tail sum that decision dropped (to sig[kSigTail])
   double* tn;      // per job: ||T|| (Gershgorin)
   cplx* xch;       // per job 4 x CT: p (two buffers), old row k + 1 (two buffers)
   unsigned* cnt;   // per job 32 words (128 B)
@@ -710,6 +713,8 @@ __global__ __launch_bounds__(256) void k_gb_eig(const TwoSiteJob* __restrict__ j
   __syncthreads();
   constexpr int kG = 4, kFirst = 256, kRounds = 12;
   constexpr double kInvF = 1.0 / (kFirst + 1), kInvG = 1.0 / (kG + 1);
+  // three more rounds when the tail threshold sits above the Gram form's noise (aqc::gram_keep)
+  const int rounds = kRounds + (j.thr > 1e-12 * tn ? 3 : 0);
   cntb[tid] = sturm_poly(s_de, CT, (lo0 + span0 * (double)(tid + 1) * kInvF) * itn);
   __syncthreads();
   const int sub = tid % kG, eid = blockIdx.x * 64 + tid / kG;
@@ -725,7 +730,7 @@ __global__ __launch_bounds__(256) void k_gb_eig(const TwoSiteJob* __restrict__ j
     l2 = l > 0 ? lo0 + span0 * (double)l * kInvF : lo0;
     h2 = l < kFirst ? lo0 + span0 * (double)(l + 1) * kInvF : hi0;
   }
-  for (int round = 0; round < kRounds; ++round) {
+  for (int round = 0; round < rounds; ++round) {
     const double x = l2 + (h2 - l2) * (double)(sub + 1) * kInvG;
     const int cnt = sturm_poly(s_de, CT, x * itn);
     const unsigned long long bal = __ballot(cnt >= a_ + 1);
@@ -736,10 +741,38 @@ __global__ __launch_bounds__(256) void k_gb_eig(const TwoSiteJob* __restrict__ j
     l2 = nlo;
     h2 = nhi;
   }
-  if (eid < K && sub == 0) stg(a.lam + (size_t)jb * CT + eid, 0.5 * (l2 + h2));
+  if (eid < K && sub == 0) {
+    stg(a.lam + (size_t)jb * CT + eid, 0.5 * (l2 + h2));
+    stg(a.err + (size_t)jb * CT + eid, 0.5 * (h2 - l2));
+  }
   if (blockIdx.x == 0 && tid == 0) stg(a.tn + jb, tn);
   if (jb == 0 && blockIdx.x == 0 && tid == 0) atomicAdd(&g_gbig_ticks[5], __builtin_amdgcn_s_memtime() - t_start);
 }
+
+// ---- the kept count: reduce_zeros on the eigenvalues (aqc::gram_keep, as the 2 chi = 128 path):
+// grid (nj), one thread.  An open decision or a kept value below the floor declines the job
+// (status 2: the block Jacobi decides).  The kernels after it use the kept count. ----
+template <int CT>
+__global__ __launch_bounds__(64) void k_gb_keep(const TwoSiteJob* __restrict__ jobs, GBArgs a, int job0) {
+  const int jb = job0 + (int)blockIdx.x;
+  if (threadIdx.x != 0 || *(const gi32*)(a.status + jb) != 0) return;
+  const TwoSiteJob& j = jobs[jb];
+  int M, L, C, K;
+  bool tr;
+  job_dims(j, M, L, C, tr, K);
+  double tail = 0.0;
+  const int k = gram_keep(a.lam + (size_t)jb * CT, a.err + (size_t)jb * CT, K, C, j.max_chi, j.thr, ldg(a.tn + jb),
+                          kGbRelFloor, tail);
+  if (k < 0) {
+    *(gi32*)(a.status + jb) = 2;
+    atomicAdd(&g_gbig_stats[3], 1ull);
+    return;
+  }
+  *(gi32*)(a.kept + jb) = k;
+  stg(a.tail + jb, tail);
+}
+
+__device__ __forceinline__ int kept_count(const GBArgs& a, int jb) { return *(const gi32*)(a.kept + jb); }
 
 typedef unsigned __attribute__((ext_vector_type(2))) u2_t;
 __device__ __forceinline__ double bld(__amdgpu_buffer_rsrc_t r, unsigned lo, unsigned uo) {
@@ -764,6 +797,7 @@ __global__ __launch_bounds__(64) void k_gb_inv(const TwoSiteJob* __restrict__ jo
   int M, L, C, K;
   bool tr;
   job_dims(j, M, L, C, tr, K);
+  K = kept_count(a, jb);
   if ((int)blockIdx.x * 64 >= K) return;
   const unsigned long long t_start = __builtin_amdgcn_s_memtime();
   __shared__ double s_d[CT], s_e[CT];
@@ -773,16 +807,6 @@ __global__ __launch_bounds__(64) void k_gb_inv(const TwoSiteJob* __restrict__ jo
   }
   __syncthreads();
   const int i = blockIdx.x * 64 + threadIdx.x;
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    // the Gram path's floor: every kept eigenvalue far above the noise of forming G, and above
-    // the CHOP (1e-16), or the job declines (k_gb_gs / k_gb_tfac / k_gb_back skip it; the host
-    // runs the block Jacobi)
-    const double l0 = ldg(a.lam + (size_t)jb * CT), lk = ldg(a.lam + (size_t)jb * CT + K - 1);
-    if (!(l0 > 0.0) || !(lk > kGbRelFloor * l0)) {
-      *(gi32*)(a.status + jb) = 2;
-      atomicAdd(&g_gbig_stats[3], 1ull);
-    }
-  }
   if (i >= K) return;  // (no barrier below)
   const double tn = ldg(a.tn + jb), itn = 1.0 / fmax(tn, 1e-300);
   const double lamn = ldg(a.lam + (size_t)jb * CT + i) * itn;
@@ -894,6 +918,7 @@ __global__ __launch_bounds__(64) void k_gb_gs(const TwoSiteJob* __restrict__ job
   int M, L, C, K;
   bool tr;
   job_dims(j, M, L, C, tr, K);
+  K = kept_count(a, jb);
   const int lane = threadIdx.x;
   const double* lam = a.lam + (size_t)jb * CT;
   const double ortol = 1e-7 * ldg(a.tn + jb);
@@ -999,7 +1024,9 @@ __global__ __launch_bounds__(64 * NW) void k_gb_back(const TwoSiteJob* __restric
   int M, L, C, K;
   bool tr;
   job_dims(j, M, L, C, tr, K);
+  K = kept_count(a, jb);
   const int col0 = blockIdx.x * 16;
+  if (blockIdx.x == 0 && threadIdx.x == 0) stg(j.sig + kSigTail, ldg(a.tail + jb));  // (rank_body)
   if (col0 >= K) return;
   const unsigned long long t_start = __builtin_amdgcn_s_memtime();
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 15, lk = lane >> 4;
@@ -1114,6 +1141,8 @@ struct GBBuffers {
   int ct = 0, nj = 0;
   cplx* G = nullptr;
   double *d = nullptr, *e = nullptr, *z = nullptr, *dinv = nullptr, *sig2 = nullptr, *lam = nullptr, *tn = nullptr;
+  double *err = nullptr, *tail = nullptr;
+  int* kept = nullptr;
   cplx* tau = nullptr;
   cplx* tfac = nullptr;
   cplx* yc = nullptr;
@@ -1128,6 +1157,7 @@ struct GBBuffers {
 void gb_free(GBBuffers& b) {
   hipFree(b.G), hipFree(b.d), hipFree(b.e), hipFree(b.z), hipFree(b.dinv), hipFree(b.sig2), hipFree(b.tau);
   hipFree(b.lam), hipFree(b.tn), hipFree(b.tfac), hipFree(b.yc);
+  hipFree(b.err), hipFree(b.tail), hipFree(b.kept);
   hipFree(b.xch), hipFree(b.cnt), hipFree(b.status), hipFree(b.djobs);
   hipHostFree(b.host_status), hipHostFree(b.hjobs);
   b = GBBuffers();
@@ -1154,6 +1184,9 @@ int gb_ensure(GBBuffers& b, int ct, int nj, hipStream_t st) {
   AQC_HIP_CHECK(hipMalloc(&b.sig2, (size_t)c * n * sizeof(double)));
   AQC_HIP_CHECK(hipMalloc(&b.lam, (size_t)c * n * sizeof(double)));
   AQC_HIP_CHECK(hipMalloc(&b.tn, (size_t)n * sizeof(double)));
+  AQC_HIP_CHECK(hipMalloc(&b.err, (size_t)c * n * sizeof(double)));
+  AQC_HIP_CHECK(hipMalloc(&b.tail, (size_t)n * sizeof(double)));
+  AQC_HIP_CHECK(hipMalloc(&b.kept, (size_t)n * sizeof(int)));
   AQC_HIP_CHECK(hipMalloc(&b.tfac, (size_t)(c / 16) * 256 * n * sizeof(cplx)));
   AQC_HIP_CHECK(hipMalloc(&b.yc, cc * sizeof(cplx)));
   AQC_HIP_CHECK(hipMalloc(&b.tau, (size_t)c * n * sizeof(cplx)));
@@ -1212,6 +1245,7 @@ int run_gram_big(const TwoSiteJob* hjobs, const TwoSiteJob* jobs, int nj, int ca
   GBArgs a;
   a.G = b.G, a.d = b.d, a.e = b.e, a.tau = b.tau, a.z = b.z, a.dinv = b.dinv, a.sig2 = b.sig2;
   a.lam = b.lam, a.tn = b.tn, a.tfac = b.tfac, a.yc = b.yc;
+  a.err = b.err, a.kept = b.kept, a.tail = b.tail;
   a.xch = b.xch, a.cnt = b.cnt, a.status = b.status;
   a.spin = g_gb_spin;
   if (g_gb_tail < 0) {
@@ -1252,6 +1286,8 @@ int run_gram_big(const TwoSiteJob* hjobs, const TwoSiteJob* jobs, int nj, int ca
     hipLaunchKernelGGL((k_gb_tfac<CT>), dim3((CT - 1 + 15) / 16, nr), dim3(256), 0, s3, jobs, a, j0);
     AQC_CHECK_LAUNCH();
     hipLaunchKernelGGL((k_gb_eig<CT>), dim3(CT / 64, nr), dim3(256), 0, ps, jobs, a, j0);
+    AQC_CHECK_LAUNCH();
+    hipLaunchKernelGGL((k_gb_keep<CT>), dim3(nr), dim3(64), 0, ps, jobs, a, j0);
     AQC_CHECK_LAUNCH();
     hipLaunchKernelGGL((k_gb_inv<CT>), dim3(CT / 64, nr), dim3(64), 0, ps, jobs, a, j0);
     AQC_CHECK_LAUNCH();

@@ -160,6 +160,51 @@ __device__ __forceinline__ void jacobi_te(double al, double be, double g2, doubl
   c = cc;
 }
 
+constexpr double kReduceChop = 1e-16;  // reduce_zeros' CHOP on sigma^2 (mps.hip kChop)
+
+// reduce_zeros (oracle/mps.py truncation_rank: Aer's rule as the reference drives it,
+// aer_mps_backend.py:27-42) on the top KE eigenvalues lam (descending, = sigma^2) of G, each known to
+// +-err: CHOP (sigma^2 > 1e-16), the max_chi cap, then the tail rule (drop the smallest while the
+// dropped sum stays below thr).  Every comparison must hold for any values inside the error bars --
+// err is the multisection bracket, plus the noise of forming and reducing G (16 C eps ||T||) -- and
+// the kept values must clear the Gram path's floor (lambda_K > floor lambda_1, 1e-9); otherwise -1 (the
+// caller declines and the Jacobi decides).  An eigenvalue whose CHOP decision is open may still be
+// dropped by the tail rule from either start, which then decides nothing: it enters the tail as
+// [0, lam + err].  Returns the kept count K, and in tail_out the dropped tail sum (handed to
+// rank_body through sig[kSigTail], whose own tail rule then keeps all K).
+[[maybe_unused]] static __device__ __noinline__ int gram_keep(const double* lam, const double* err, int KE, int C, int max_chi,
+                                             double thr, double tn, double floor, double& tail_out) {
+  const double noise = 16.0 * C * 2.220446049250313e-16 * tn;
+  int k_lo = 0, k_hi = 0;  // counts surely / possibly above the CHOP (lam descending)
+  for (int i = 0; i < KE; ++i) {
+    const double e = err[i] + noise;
+    if (lam[i] - e > kReduceChop) k_lo = i + 1;
+    if (lam[i] + e > kReduceChop) k_hi = i + 1;
+  }
+  int k = k_hi < 1 ? 1 : k_hi;
+  if (max_chi > 0 && k > max_chi) k = max_chi;
+  double tail = 0.0, unc = 0.0;
+  while (k > 1) {
+    const int i = k - 1;
+    const double e = err[i] + noise;
+    double v = lam[i], ev = e;
+    if (i >= k_lo) {  // CHOP open: contributes anything in [0, lam + e] if dropped
+      v = 0.5 * (lam[i] + e);
+      ev = v;
+    }
+    const double sum = tail + v, m = unc + ev;
+    if (fabs(sum - thr) <= m) return -1;  // the comparison is open
+    if (sum >= thr) break;
+    tail = sum;
+    unc = m;
+    --k;
+  }
+  if (k > k_lo) return -1;  // a kept value whose CHOP is open (also far below the floor)
+  if (!(lam[0] > 0.0) || !(lam[k - 1] > floor * lam[0])) return -1;
+  tail_out = tail;
+  return k;
+}
+
 // Multi-workgroup block one-sided Jacobi SVD for 2 * chi > 128 (bjacobi.hip): factors the nj
 // two-site thetas of `jobs` (device array) into the k_jacobi output contract (W columns = U sigma,
 // sig = column norms, qr = 0).  Enqueued on `st`; synchronises the host once per sweep (from the

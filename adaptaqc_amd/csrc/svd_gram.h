@@ -192,49 +192,6 @@ __device__ __forceinline__ double rcp_nr(double x) {
 constexpr size_t kTfacOff = 8192;
 typedef __attribute__((address_space(1))) double gdbl_t;
 
-// reduce_zeros (oracle/mps.py truncation_rank: Aer's rule as the reference drives it,
-// aer_mps_backend.py:27-42) on the top KE eigenvalues lam (descending, = sigma^2) of G, each known to
-// +-err: CHOP (sigma^2 > 1e-16), the max_chi cap, then the tail rule (drop the smallest while the
-// dropped sum stays below thr).  Every comparison must hold for any values inside the error bars --
-// err is the multisection bracket, plus the noise of forming and reducing G (16 C eps ||T||) -- and
-// the kept values must clear the Gram path's floor (lambda_K > 1e-9 lambda_1); otherwise -1 (the
-// caller declines and the Jacobi decides).  An eigenvalue whose CHOP decision is open may still be
-// dropped by the tail rule from either start, which then decides nothing: it enters the tail as
-// [0, lam + err].  Returns the kept count K, and in tail_out the dropped tail sum (handed to
-// rank_body through sig[kSigTail], whose own tail rule then keeps all K).
-__device__ __noinline__ int gram_keep(const double* lam, const double* err, int KE, int C, int max_chi, double thr,
-                                      double tn, double& tail_out) {
-  const double noise = 16.0 * C * 2.220446049250313e-16 * tn;
-  int k_lo = 0, k_hi = 0;  // counts surely / possibly above the CHOP (lam descending)
-  for (int i = 0; i < KE; ++i) {
-    const double e = err[i] + noise;
-    if (lam[i] - e > kChop) k_lo = i + 1;
-    if (lam[i] + e > kChop) k_hi = i + 1;
-  }
-  int k = k_hi < 1 ? 1 : k_hi;
-  if (max_chi > 0 && k > max_chi) k = max_chi;
-  double tail = 0.0, unc = 0.0;
-  while (k > 1) {
-    const int i = k - 1;
-    const double e = err[i] + noise;
-    double v = lam[i], ev = e;
-    if (i >= k_lo) {  // CHOP open: contributes anything in [0, lam + e] if dropped
-      v = 0.5 * (lam[i] + e);
-      ev = v;
-    }
-    const double sum = tail + v, m = unc + ev;
-    if (fabs(sum - thr) <= m) return -1;  // the comparison is open
-    if (sum >= thr) break;
-    tail = sum;
-    unc = m;
-    --k;
-  }
-  if (k > k_lo) return -1;  // a kept value whose CHOP is open (also far below the floor)
-  if (!(lam[0] > 0.0) || !(lam[k - 1] > kGramRelFloor * lam[0])) return -1;
-  tail_out = tail;
-  return k;
-}
-
 // Gram-path SVD of one 2 chi x 2 chi theta'; 1024 threads; `xbuf` = the workgroup's dynamic LDS
 // (>= 4 GemmLds).  Returns false (work untouched beyond scratch, caller runs the Jacobi) when the
 // fast path does not apply.  Uniform in the workgroup.
@@ -728,7 +685,7 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
     }
   }
   __syncthreads();
-  if (tid == 0) s_K = gram_keep(s_lam, s_err, KE, C, j.max_chi, j.thr, s_tn, s_tail);
+  if (tid == 0) s_K = aqc::gram_keep(s_lam, s_err, KE, C, j.max_chi, j.thr, s_tn, kGramRelFloor, s_tail);
   __syncthreads();
   tick(2);
   const int K = s_K;  // (uniform)

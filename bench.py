@@ -99,6 +99,21 @@ def random_vidal_mps(n, chi, seed):
     return vidal_from_tensors(A)
 
 
+def graded_vidal_mps(n, chi, seed, decay):
+    """Random MPS whose Schmidt spectra decay geometrically: complex-normal tensors with right bond
+    index k scaled by decay^k, canonicalised (Aer tuple; bonds min(2^k, 2^(n-k), chi)).  At decay
+    0.9 and chi = 64 a thin layer's two-site spectra cross the reference example's truncation
+    threshold 1e-8 (examples/advanced_mps_example.py:46) around the 50th value, so the tail rule of
+    reduce_zeros decides the kept count (tests/test_gpu_threshold.py, tools/unbounded_profile.py)."""
+    rng = np.random.default_rng(seed)
+    dims = [min(2 ** k, 2 ** (n - k), chi) for k in range(n + 1)]
+    A = []
+    for i in range(n):
+        t = rng.standard_normal((2, dims[i], dims[i + 1])) + 1j * rng.standard_normal((2, dims[i], dims[i + 1]))
+        A.append(t * (decay ** np.arange(dims[i + 1]))[None, None, :])
+    return vidal_from_tensors(A)
+
+
 def near_product_mps(n, chi, seed, alpha=0.6):
     """|psi> ~ alpha |p> + |phi> in Vidal form: |p> a product of single-qubit states near |0>
     (angles 0.15-0.3, random phases), |phi> random with bonds min(2^k - 1, 2^(n-k) - 1, chi - 1),

@@ -1,0 +1,111 @@
+"""The truncation threshold of the reference's own MPS example (1e-8,
+examples/advanced_mps_example.py:46; mps_sim_with_args, aer_mps_backend.py:27-42) on the device,
+against the oracle (oracle/mps.py, reduce_zeros restated: CHOP, max_chi, tail sum below the
+threshold): exact bond dimensions and the fidelity between the device and oracle states within
+1e-6 (BASELINE.json's truncated-MPS bar), at max_chi = None and at a binding max_chi, through the
+fused per-state chain (k_chain, >= 32 states), the lock-step path (one state at a time) and the
+multi-workgroup path (2 chi = 256).
+
+The states (bench.graded_vidal_mps) have geometrically decaying Schmidt spectra, so every
+two-site update's singular values straddle the tail boundary: the kept count comes from the tail
+rule (about 50 of 128 at decay 0.9), or from max_chi with the tail rule acting after it (decay
+0.95).  Capacities are chosen so that the unbounded runs never need more than the capacity (the
+oracle's kept counts for these seeds and layers stay at or below it)."""
+import numpy as np
+import pytest
+
+import bench
+from oracle import mps as M
+
+pytestmark = pytest.mark.gpu
+THR = 1e-8
+
+
+def _layer(n, a, d, seed):
+    rng = np.random.default_rng(seed)
+    return bench.thin_layer_oracle_ops(a, a + d, rng.uniform(-np.pi, np.pi, 4))
+
+
+def _oracle(n, aer, ops, max_chi):
+    st = M.run_circuit(n, ops, THR, max_chi, mps=M.MPS.from_aer(aer))
+    pre = st.preprocessed()
+    return [1] + [x.shape[2] for x in pre], pre
+
+
+def _check(dev, ref_dims, ref_pre, label):
+    np.testing.assert_array_equal(dev.dims(), ref_dims, err_msg=label)
+    pre = dev.preprocessed()
+    nrm = abs(M.mps_dot(pre, pre))
+    fid = abs(M.mps_dot(ref_pre, pre)) ** 2
+    assert abs(nrm - 1.0) < 1e-10, (label, nrm)
+    assert abs(fid - 1.0) < 1e-6, (label, fid)
+
+
+def _run_batch(n, cap, max_chi, states, layers, batch):
+    """states: Aer tuples; layers: (state index, oracle ops); batch: one apply_batch call (fused
+    chain when >= 32 states at 2 chi = 128) or one state at a time (lock-step)."""
+    from adaptaqc_amd import _lib
+    from adaptaqc_amd.circuit import device_ops
+    from adaptaqc_amd.device import DeviceMPS, apply_batch
+    from conftest import to_circuit
+
+    work = []
+    for si, _ in layers:
+        d = DeviceMPS(n, cap, THR, max_chi)
+        d.load_aer(states[si])
+        work.append(d)
+    ops = [_lib.ops_array(device_ops(to_circuit(n, o))) for _, o in layers]
+    _lib.gram_stats()
+    _lib.gram_big_stats()
+    if batch:
+        apply_batch(work, ops, sort=True)
+    else:
+        for d, o in zip(work, ops):
+            d.apply(o)
+            d.sort()
+    stats = (_lib.gram_stats(), _lib.gram_big_stats())
+    for k, (si, o) in enumerate(layers):
+        ref_dims, ref_pre = _oracle(n, states[si], o, max_chi)
+        _check(work[k], ref_dims, ref_pre, f"evaluation {k} (state {si})")
+    return stats
+
+
+@pytest.mark.parametrize("max_chi,decay,dists", [(None, 0.9, (1, 2, 3)), (64, 0.9, (1, 2, 3)),
+                                                 (64, 0.95, (1, 2, 5, 25))],
+                         ids=["unbounded", "maxchi64", "maxchi64-binding"])
+def test_threshold_fused_chain_vs_oracle(max_chi, decay, dists):
+    """>= 32 states in one batch: k_chain (capacity 64, 2 chi = 128) with the Gram path deciding the
+    kept count by the tail rule (gram_keep) or the register Jacobi where it declines."""
+    n, cap = 50, 64
+    states = [bench.graded_vidal_mps(n, 64, 300 + s, decay) for s in range(4)]
+    reps = -(-32 // (len(states) * len(dists)))
+    layers = [(si, _layer(n, 20, d, 1000 * r + 10 * si + d)) for r in range(reps) for si in range(len(states))
+              for d in dists]
+    assert len(layers) >= 32
+    gram, _ = _run_batch(n, cap, max_chi, states, layers, batch=True)
+    assert gram["calls"] > 0
+    # the tail rule keeps ~50 of 128 at decay 0.9: the Gram path must take most of those updates
+    if decay == 0.9:
+        assert gram["taken"] >= 0.5 * gram["calls"], gram
+
+
+@pytest.mark.parametrize("max_chi", [None, 64])
+def test_threshold_lockstep_single_states_vs_oracle(max_chi):
+    """The same truncation one state at a time (the lock-step launches of a single evaluation)."""
+    n, cap = 50, 64
+    states = [bench.graded_vidal_mps(n, 64, 310 + s, 0.9) for s in range(2)]
+    layers = [(si, _layer(n, 18, d, 77 + d)) for si in range(2) for d in (1, 3)]
+    _run_batch(n, cap, max_chi, states, layers, batch=False)
+
+
+@pytest.mark.parametrize("max_chi,decay,dists", [(None, 0.9, (1, 2)), (128, 0.95, (1, 3)), (None, 0.95, (2,))],
+                         ids=["unbounded", "maxchi128", "unbounded-wide"])
+def test_threshold_multi_workgroup_vs_oracle(max_chi, decay, dists):
+    """2 chi = 256 two-site updates (capacity 128, 24 qubits at chi = 128): the multi-workgroup Gram
+    path (gram_big.hip) or the block Jacobi where it declines, and the 2 chi = 128 path for the
+    smaller thetas of the routed gates."""
+    n, cap = 24, 128
+    states = [bench.graded_vidal_mps(n, 128, 320 + s, decay) for s in range(2)]
+    layers = [(si, _layer(n, 9, d, 55 + 10 * si + d)) for si in range(2) for d in dists]
+    _, big = _run_batch(n, cap, max_chi, states, layers, batch=True)
+    assert big["calls"] > 0
