@@ -34,7 +34,8 @@
 // Included into mps.hip's anonymous namespace.
 #pragma once
 
-constexpr int kGramMaxK = 64;
+constexpr int kGramMaxK = 128;    // kept triplets (the whole 2 chi = 128 side)
+constexpr int kGramNarrowK = 64;  // up to here S5 runs on wave 0 from the LDS and S6 in one pass
 // Settled choices (each measured against its alternative):
 // S3: wave 0 raises its issue priority while it forms a reflector's scalars; the reflectors' base
 //     pointer in SGPRs; the rows' partial products summed in the wave (DPP) before phase B; the
@@ -52,7 +53,7 @@ constexpr double kGramRelFloor = 1e-9;
 // shader-clock ticks of the phases (thread 0), summed over calls: S1, S2+S3, S4, S5, S6, output,
 // S3's column steps, S5's inverse iteration, S3's phase A (column pass + zlarfg + first barrier)
 __device__ unsigned long long g_gram_ticks[12];
-static_assert(kGramMaxK <= 64, "S5: the inverse iteration (tid < K) must stay on wave 0");
+static_assert(kGramNarrowK == 64, "S5: the narrow inverse iteration (tid < K) stays on wave 0");
 // path counters (thread 0 of each call): [0] calls, [1] taken, [2] declined by shape (K > 64, ...),
 // [3] declined at the eigenvalue floor (lambda_K <= 1e-9 lambda_1 -> the Jacobi runs)
 __device__ unsigned long long g_gram_stats[4];
@@ -189,8 +190,394 @@ __device__ __forceinline__ double rcp_nr(double x) {
 
 // S6's precomputed compact-WY factors in the work buffer: after the reflectors (at most 8128 complex
 // at C = 128) and clear of the output W written after S6's loop, 512 complex per block (S, then T)
-constexpr size_t kTfacOff = 8192;
+constexpr size_t kTfacOff = 16384;
+// K > 64: the inverse iteration's pivots (128 x 128 doubles, row-major, vector i in column i), then
+// (after S5) the first 64 vectors, stashed for S6's second pass; complex offset in the work buffer
+// (aqc::kGramWorkElems covers it)
+constexpr size_t kWideOff = 20480;
+static_assert(kWideOff + 8192 <= aqc::kGramWorkElems, "Gram-path scratch exceeds the work buffer");
+static_assert(kChainLdsBytes >= 128 * 128 * 8, "S5 (K > 64): 128 x 128 vectors in the dynamic LDS");
 typedef __attribute__((address_space(1))) double gdbl_t;
+
+// S6's compact-WY factors of reflector block b, computed during S5 by an idle wave (gram_svd_body)
+__device__ __forceinline__ void s6_factors(int b, int C, cplx* hh, const cplx* s_tau, int lane) {
+  // block b of S6's loop (reflectors k0 .. k1 - 1, counted from the last): S = Y^H Y, then T by
+  // zlarft, into the work scratch after the reflectors (S at [0, 256), T at [256, 512) of the
+  // block's 512).  Read back through agent-scope loads: the same addresses were read by the
+  // previous update's S6 on this CU, so the L1 may hold them.
+  const int k1 = C - 1 - 16 * b, k0 = k1 > 16 ? k1 - 16 : 0, nb = k1 - k0;
+  const int li = lane & 15, lk = lane >> 4;
+  aqc::d4_t sr = {0, 0, 0, 0}, si = {0, 0, 0, 0};
+  for (int r0 = 0; r0 < C; r0 += 4) {  // A[m = i][k = row] = conj(Y[row][i]), B = Y
+    const int row = r0 + lk, k = k0 + li;
+    const cplx y = (li < nb && row > k && row < C) ? aqc::ldg(hh + (size_t)k * (2 * C - k - 1) / 2 + (row - k - 1))
+                                                   : aqc::cmk(0, 0);
+    sr = __builtin_amdgcn_mfma_f64_16x16x4f64(y.x, y.x, sr, 0, 0, 0);
+    sr = __builtin_amdgcn_mfma_f64_16x16x4f64(y.y, y.y, sr, 0, 0, 0);
+    si = __builtin_amdgcn_mfma_f64_16x16x4f64(y.x, y.y, si, 0, 0, 0);
+    si = __builtin_amdgcn_mfma_f64_16x16x4f64(-y.y, y.x, si, 0, 0, 0);
+  }
+  cplx* Sg = hh + kTfacOff + (size_t)b * 512;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) aqc::stg(Sg + (lk + 4 * q) * 16 + li, aqc::cmk(sr[q], si[q]));
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // zlarft (forward, columnwise): lane (a, g) holds T[a][g + 4 m]; T[a][i] = -tau_i sum_{a <= bb < i}
+  // T[a][bb] S[bb][i], T[i][i] = tau_i -- the recurrence of the in-loop form
+  const int a = lane >> 2, g = lane & 3;
+  cplx tq[4] = {aqc::cmk(0, 0), aqc::cmk(0, 0), aqc::cmk(0, 0), aqc::cmk(0, 0)};
+  for (int i = 0; i < 16; ++i) {
+    const cplx tau = i < nb ? s_tau[k0 + i] : aqc::cmk(0, 0);
+    cplx acc = aqc::cmk(0, 0);
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const int bb = g + 4 * m;
+      if (4 * m < i && bb < i) {
+        const gdbl_t* sp = (const gdbl_t*)(const double*)(Sg + bb * 16 + i);
+        const cplx sv = aqc::cmk(__hip_atomic_load(sp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                                 __hip_atomic_load(sp + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        acc = aqc::cfma(tq[m], sv, acc);
+      }
+    }
+    acc.x = aqc::row_sum4(acc.x);
+    acc.y = aqc::row_sum4(acc.y);
+    const cplx ti = aqc::cmul(tau, acc);
+    const cplx val = a < i ? aqc::cmk(-ti.x, -ti.y) : (a == i ? tau : aqc::cmk(0, 0));
+    if (g == (i & 3)) tq[i >> 2] = val;
+  }
+#pragma unroll
+  for (int m = 0; m < 4; ++m) aqc::stg(Sg + 256 + a * 16 + g + 4 * m, tq[m]);
+}
+
+// Gram-Schmidt inside clusters of the S5 vectors (zb[row * ZS + i]), one wave
+template <int ZS>
+__device__ __forceinline__ void gs_clusters(int K, int C, double* zb, const double* s_lam, double s_tn, int lane) {
+  // clusters: gaps below 1e-7 ||T|| (dstein's 1e-3 is far more conservative than three
+  // inverse-iteration steps need: at gaps above ~1e-10 the vectors come out orthogonal to
+  // 1e-14 on their own, tools/gram_svd_proto.py)
+  const double ortol = 1e-7 * s_tn;
+  int start = 0;
+  for (int i = 1; i < K; ++i) {
+    if (s_lam[i - 1] - s_lam[i] >= ortol) {
+      start = i;
+      continue;
+    }
+    for (int jj = start; jj < i; ++jj) {
+      double dp = 0.0;
+      for (int row = lane; row < C; row += 64) dp = fma(zb[row * ZS + i], zb[row * ZS + jj], dp);
+      dp = wave_sum_d(dp);
+      for (int row = lane; row < C; row += 64) zb[row * ZS + i] = fma(-dp, zb[row * ZS + jj], zb[row * ZS + i]);
+    }
+    double n2 = 0.0;
+    for (int row = lane; row < C; row += 64) n2 = fma(zb[row * ZS + i], zb[row * ZS + i], n2);
+    n2 = wave_sum_d(n2);
+    const double sc = 1.0 / sqrt(n2);
+    for (int row = lane; row < C; row += 64) zb[row * ZS + i] *= sc;
+  }
+}
+
+// sigma^2 of S5 vector i: the Rayleigh quotient z^T T z (zb[row * ZS + i])
+template <int ZS>
+__device__ __forceinline__ double rayleigh(int i, int C, const double* zb, const double* s_d, const double* s_e) {
+  // z^T T z with eight rows' loads in flight and two partial sums (the rows one at a time waited
+  // out an LDS round trip each); the last row's e term is masked by zeroing its factor
+  double s2a = 0.0, s2b = 0.0;
+  int r0 = 0;
+  constexpr int U = 8;
+  for (; r0 + U <= C; r0 += U) {
+    double zz[U + 1], dd[U], ee[U];
+#pragma unroll
+    for (int u = 0; u <= U; ++u) zz[u] = zb[min(r0 + u, C - 1) * ZS + i];
+#pragma unroll
+    for (int u = 0; u < U; ++u) dd[u] = s_d[r0 + u], ee[u] = r0 + u < C - 1 ? s_e[r0 + u] : 0.0;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      s2a = fma(dd[u] * zz[u], zz[u], s2a);
+      s2b = fma(2.0 * ee[u] * zz[u], zz[u + 1], s2b);
+    }
+  }
+  for (; r0 < C; ++r0) {
+    const double z = zb[r0 * ZS + i];
+    s2a = fma(s_d[r0] * z, z, s2a);
+    if (r0 < C - 1) s2b = fma(2.0 * s_e[r0] * z, zb[(r0 + 1) * ZS + i], s2b);
+  }
+  const double s2 = s2a + s2b;
+  return s2 > 0.0 ? s2 : 0.0;
+}
+
+// S6's block loop: V (C x 64 from column c0 of Z, in the MFMA accumulator layout -- see
+// gram_svd_body) -= Y (T (Y^H V)) over the reflector blocks from the last, then W columns c0 + col
+// = V sigma into the work buffer.  Every thread of the workgroup.
+__device__ __forceinline__ void s6_back(const TwoSiteJob& j, cplx* hh, int C, int K, int c0, aqc::d4_t (&vre)[2],
+                                        aqc::d4_t (&vim)[2], const double* s_sig2, int tid, int lane, int wave,
+                                        int wave_s) {
+  extern __shared__ double2 xbuf[];
+  const int nt = wave & 3, mg = wave >> 2, li = lane & 15, lk = lane >> 4;
+  // LDS (complex units): Y [128][16] (column index swizzled by row & 15: conflict-free reads along
+  // rows and along columns), Y^H V partials of waves 4..15, T (from S5's precompute), W2 = T Y^H V
+  cplx* Yl = xbuf;
+  cplx* Pw = Yl + 2048;
+  cplx* Tl = Pw + 12 * 256;      // [16][17]
+  cplx* W2l = Tl + 3 * 256 + 16 * 64;
+  auto fetch_y = [&](int k0, int nb, cplx (&y)[2]) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int e = tid + 1024 * u, row = e >> 4, i = e & 15, k = k0 + i;
+      y[u] = (i < nb && row > k && row < C) ? aqc::ldg(hh + (size_t)k * (2 * C - k - 1) / 2 + (row - k - 1))
+                                            : aqc::cmk(0, 0);
+    }
+  };
+  cplx ynx[2];
+  {
+    const int k1 = C - 1, k0 = k1 > 16 ? k1 - 16 : 0;
+    fetch_y(k0, k1 - k0, ynx);
+  }
+  __syncthreads();  // V's initial values are read from zb: the LDS can be overwritten now
+  for (int k1 = C - 1; k1 > 0; k1 -= 16) {
+    const int k0 = k1 > 16 ? k1 - 16 : 0;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int e = tid + 1024 * u, row = e >> 4, i = e & 15;
+      Yl[row * 16 + (i ^ (row & 15))] = ynx[u];
+    }
+    if (tid < 256) {  // this block's T from S5 (agent-scope loads: see the precompute)
+      const gdbl_t* tp = (const gdbl_t*)(const double*)(hh + kTfacOff + (size_t)((C - 1 - k1) >> 4) * 512 + 256 + tid);
+      Tl[(tid >> 4) * 17 + (tid & 15)] = aqc::cmk(__hip_atomic_load(tp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                                                  __hip_atomic_load(tp + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    }
+    __syncthreads();  // B1: Y
+    // Y^H V over this wave's 32 rows: A[m = i][k = row] = conj(Y[row][i])
+    aqc::d4_t wr = {0, 0, 0, 0}, wi = {0, 0, 0, 0};
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      if (32 * mg + 16 * t + 15 > k0) {  // rows <= k0 of Y are zero (uniform per wave)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const int row = 32 * mg + 16 * t + 4 * s + lk;
+          const cplx y = Yl[row * 16 + (li ^ (row & 15))];
+          wr = __builtin_amdgcn_mfma_f64_16x16x4f64(y.x, vre[t][s], wr, 0, 0, 0);
+          wr = __builtin_amdgcn_mfma_f64_16x16x4f64(y.y, vim[t][s], wr, 0, 0, 0);
+          wi = __builtin_amdgcn_mfma_f64_16x16x4f64(y.x, vim[t][s], wi, 0, 0, 0);
+          wi = __builtin_amdgcn_mfma_f64_16x16x4f64(-y.y, vre[t][s], wi, 0, 0, 0);
+        }
+      }
+    }
+    // D layout: row b = lk + 4 q (reflector), column li
+    if (mg > 0) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) Pw[((mg - 1) * 4 + nt) * 256 + (lk + 4 * q) * 16 + li] = aqc::cmk(wr[q], wi[q]);
+    }
+    __syncthreads();  // B2: partials
+    if (mg == 0) {
+      // Y^H V of column tile nt summed in registers, then W2 = T (Y^H V) for that tile on the matrix
+      // cores right here: the sum's D layout (row lk + 4 q, column li) is the B operand of k-step q
+      // and T (in the LDS since B1) the A operand -- no W1 round trip through the LDS, no B3
+      aqc::d4_t br, bi, w2r = {0, 0, 0, 0}, w2i = {0, 0, 0, 0};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int b = lk + 4 * q;
+        cplx w = aqc::cmk(wr[q], wi[q]);
+#pragma unroll
+        for (int m = 0; m < 3; ++m) w = aqc::cadd(w, Pw[(m * 4 + nt) * 256 + b * 16 + li]);
+        br[q] = w.x;
+        bi[q] = w.y;
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const cplx t = Tl[li * 17 + 4 * q + lk];  // A[m = li][k = lk] = T[li][4 q + lk]
+        w2r = __builtin_amdgcn_mfma_f64_16x16x4f64(t.x, br[q], w2r, 0, 0, 0);
+        w2r = __builtin_amdgcn_mfma_f64_16x16x4f64(-t.y, bi[q], w2r, 0, 0, 0);
+        w2i = __builtin_amdgcn_mfma_f64_16x16x4f64(t.x, bi[q], w2i, 0, 0, 0);
+        w2i = __builtin_amdgcn_mfma_f64_16x16x4f64(t.y, br[q], w2i, 0, 0, 0);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) W2l[(lk + 4 * q) * 64 + 16 * nt + li] = aqc::cmk(w2r[q], w2i[q]);
+    }
+    __syncthreads();  // B4: W2
+    // the next block's reflectors, in flight during the V update: issued before B1 they were
+    // drained by the spill reloads' vmcnt(0) waits between B1 and B4
+    if (k0 > 0) {
+      const int n1 = k0, n0 = n1 > 16 ? n1 - 16 : 0;
+      fetch_y(n0, n1 - n0, ynx);
+    }
+    // V -= Y W2: A[m = row][k = b] = Y[row][b], B[k = b][n] = W2[b][n].  The lane's indices come
+    // from the lane counter and the wave index in an SGPR: derived from the thread id (whose VGPR
+    // is spilled) their reload's vmcnt(0) drained the next block's reflector loads issued above
+    const int vl_ = fresh_lane();
+    const int vmg = wave_s >> 2, vnt = wave_s & 3, vli = vl_ & 15, vlk = vl_ >> 4;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      if (32 * vmg + 16 * t + 15 > k0) {
+        const int row = 32 * vmg + 16 * t + vli;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const int b = 4 * s + vlk;
+          const cplx y = Yl[row * 16 + (b ^ (row & 15))];
+          const cplx w = W2l[b * 64 + 16 * vnt + vli];
+          vre[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(-y.x, w.x, vre[t], 0, 0, 0);
+          vre[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(y.y, w.y, vre[t], 0, 0, 0);
+          vim[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(-y.x, w.y, vim[t], 0, 0, 0);
+          vim[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(-y.y, w.x, vim[t], 0, 0, 0);
+        }
+      }
+    }
+    __syncthreads();  // B5: Y, W2 and the partials are overwritten next block
+  }
+  {  // the reflectors are dead (last read before B1 of the last block): W overwrites them (a
+     // first pass of K > 64 writes columns 64.. past them)
+    const int col = c0 + 16 * nt + li;
+    if (col < K) {
+      const double sg = sqrt(s_sig2[col]);
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int row = 32 * mg + 16 * t + lk + 4 * q;
+          if (row < C) aqc::stg(j.work + (size_t)col * C + row, aqc::cmk(vre[t][q] * sg, vim[t][q] * sg));
+        }
+      }
+    }
+  }
+}
+
+// S5 for K > 64 kept vectors (gram_svd_body): the inverse iteration of the narrow path for vector i
+// by thread i (waves 0-1), the vectors in the LDS at stride 128 (zb[row * 128 + i]), the pivots in
+// the work scratch (Db[row * 128 + i], lanes along a row: one 512-byte access per wave).  The pivots
+// are read back through agent-scope loads, eight rows ahead of the chain: a previous update's reads
+// of the same addresses on this CU may sit in the L1.
+__device__ __noinline__ void s5_wide(int i, int C, const double* s_d, const double* s_e, const double* s_e2,
+                                     double lam, double tn, double* zb, double* Db) {
+  for (int row = 0; row < C; ++row) {  // deterministic start vector, in [-1, 1) (as the narrow path)
+    unsigned int h = (unsigned int)(row * 2654435761u) ^ (unsigned int)((i + 1) * 40503u);
+    h ^= h >> 13;
+    h *= 0x5bd1e995u;
+    h ^= h >> 15;
+    zb[row * 128 + i] = (double)(h & 0xFFFFFu) * (2.0 / 1048576.0) - 1.0;
+  }
+  auto ldd = [&](int row) {
+    return __hip_atomic_load((const gdbl_t*)(Db + row * 128 + i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+  constexpr int U = 8;
+  const double itn = 1.0 / fmax(tn, 1e-300), lamn = lam * itn;
+  {  // L D L^T = T - lam I, the pivots from the leading minors (see the narrow path)
+    double p0 = 0.0, p1 = 1.0;
+    for (int row = 0; row < C; ++row) {
+      const double d = s_d[row], e2 = s_e2[max(row - 1, 0)];
+      const double dmx = fma(d, itn, -lamn), t = (e2 * itn * itn) * p0;
+      const double lim = 2.220446049250313e-16 * fabs(p1);
+      double p = fma(dmx, p1, -t);
+      p = fabs(p) < lim ? copysign(lim, p) : p;
+      aqc::stg(Db + row * 128 + i, p1 * rcp_nr(p) * itn);
+      p0 = p1;
+      p1 = p;
+      if ((row & 7) == 7) {
+        const int ex = max(__builtin_amdgcn_frexp_exp(p0), __builtin_amdgcn_frexp_exp(p1));
+        p0 = __builtin_amdgcn_ldexp(p0, -ex);
+        p1 = __builtin_amdgcn_ldexp(p1, -ex);
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  double sc = 1.0;
+  for (int it = 0; it < 3; ++it) {
+    double yp = 0.0;
+    int r0 = 0;
+    for (; r0 + U <= C; r0 += U) {
+      double zz[U], ee[U], dp[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int rm = max(r0 + u - 1, 0);
+        zz[u] = zb[(r0 + u) * 128 + i], ee[u] = s_e[rm], dp[u] = ldd(rm);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const double y = fma(-ee[u] * dp[u], yp, zz[u] * sc);
+        zb[(r0 + u) * 128 + i] = y;
+        yp = y;
+      }
+    }
+    for (; r0 < C; ++r0) {
+      const int rm = max(r0 - 1, 0);
+      const double y = fma(-s_e[rm] * ldd(rm), yp, zb[r0 * 128 + i] * sc);
+      zb[r0 * 128 + i] = y;
+      yp = y;
+    }
+    double zn = 0.0, n2 = 0.0;
+    int r1 = C - 1;
+    for (; r1 - U + 1 >= 0; r1 -= U) {
+      double yy[U], ee[U], dd[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int row = r1 - u;
+        yy[u] = zb[row * 128 + i], ee[u] = s_e[min(row, C - 2)], dd[u] = ldd(row);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        zn = fma(-ee[u] * dd[u], zn, yy[u] * dd[u]);
+        zb[(r1 - u) * 128 + i] = zn;
+        n2 = fma(zn, zn, n2);
+      }
+    }
+    for (; r1 >= 0; --r1) {
+      const double d = ldd(r1);
+      zn = fma(-s_e[min(r1, C - 2)] * d, zn, zb[r1 * 128 + i] * d);
+      zb[r1 * 128 + i] = zn;
+      n2 = fma(zn, zn, n2);
+    }
+    const double rs = __builtin_amdgcn_rsq(n2);
+    sc = rs * fma(-0.5 * n2 * rs, rs, 1.5);
+  }
+  for (int row = 0; row < C; ++row) zb[row * 128 + i] *= sc;
+}
+
+// S5 and S6 of gram_svd_body for K > 64 kept triplets (kept out of the body's register allocation:
+// the K <= 64 path is the one the batched chains run).  S5: vector i by thread i of waves 0-1
+// (s5_wide), the factors' precompute on the waves off SIMDs 0 and 1 (2-3, 6-7, 10-11, 14-15);
+// Gram-Schmidt and the Rayleigh quotients at stride 128; S6 in two passes of 64 columns, the last
+// vectors first (their W lands in [64 C, 128 C), past the reflectors), the first 64 stashed in the
+// work scratch (the pivots there are dead by then) and read back with agent-scope loads.
+__device__ __noinline__ void gram_wide(const TwoSiteJob& j, cplx* hh, int C, int K, const double* s_d,
+                                       const double* s_e, const double* s_e2, const double* s_lam, double s_tn,
+                                       const cplx* s_tau, double* s_sig2) {
+  extern __shared__ double2 xbuf[];
+  const int tid = fresh_tid(), lane = tid & 63, wave = tid >> 6;
+  const int wave_s = __builtin_amdgcn_readfirstlane(wave);
+  double* zb = reinterpret_cast<double*>(xbuf);  // zb[row * 128 + i]
+  double* scratch = reinterpret_cast<double*>(j.work + kWideOff);
+  const int nblk = (C - 1 + 15) >> 4;
+  if (tid < K) {
+    s5_wide(tid, C, s_d, s_e, s_e2, s_lam[tid], s_tn, zb, scratch);
+  } else if ((wave & 3) >= 2) {
+    const int b = 2 * (wave >> 2) + (wave & 3) - 2;  // (uniform per wave)
+    if (b < nblk) s6_factors(b, C, hh, s_tau, lane);
+  }
+  __syncthreads();
+  if (wave == 0) gs_clusters<128>(K, C, zb, s_lam, s_tn, lane);
+  __syncthreads();
+  if (tid < K) s_sig2[tid] = rayleigh<128>(tid, C, zb, s_d, s_e);
+  __syncthreads();
+  const int nt = wave & 3, mg = wave >> 2, li = lane & 15, lk = lane >> 4;
+  for (int pass = 0; pass < 2; ++pass) {
+    const int c0 = pass == 0 ? kGramNarrowK : 0;
+    aqc::d4_t vre[2], vim[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int row = 32 * mg + 16 * t + lk + 4 * q, col = 16 * nt + li;
+        double v = 0.0;
+        if (row < C && c0 + col < K)
+          v = pass == 0 ? zb[row * 128 + c0 + col]
+                        : __hip_atomic_load((const gdbl_t*)(scratch + row * 64 + col), __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT);
+        vre[t][q] = v;
+        vim[t][q] = 0.0;
+      }
+    }
+    if (pass == 0)  // the first 64 vectors to the scratch (read before s6_back's first barrier)
+      for (int e = tid; e < C * 64; e += 1024) aqc::stg(scratch + e, zb[(e >> 6) * 128 + (e & 63)]);
+    s6_back(j, hh, C, K, c0, vre, vim, s_sig2, tid, lane, wave, wave_s);
+  }
+}
 
 // Gram-path SVD of one 2 chi x 2 chi theta'; 1024 threads; `xbuf` = the workgroup's dynamic LDS
 // (>= 4 GemmLds).  Returns false (work untouched beyond scratch, caller runs the Jacobi) when the
@@ -689,10 +1076,14 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
   __syncthreads();
   tick(2);
   const int K = s_K;  // (uniform)
-  if (K < 0 || K > kGramMaxK) {  // open decisions / below the floor; more than 64 kept
-    if (tid == 0) atomicAdd(&g_gram_stats[K < 0 ? 3 : 2], 1ull);
+  if (K < 0) {  // open decisions / below the floor
+    if (tid == 0) atomicAdd(&g_gram_stats[3], 1ull);
     return false;
   }
+  if (K > kGramNarrowK) {  // (uniform)
+    gram_wide(j, hh, C, K, s_d, s_e, s_e2, s_lam, s_tn, s_tau, s_sig2);
+    tick(4);
+  } else {
   // ---- S5: inverse iteration, Gram-Schmidt in clusters, Rayleigh quotients ----
   double* zb = reinterpret_cast<double*>(xbuf);  // zb[row * 64 + i]
   double* Db = zb + 128 * 64;                    // 1 / D_row of vector i at Db[row * 64 + i]
@@ -810,106 +1201,12 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
     if (tid == 0) atomicAdd(&g_gram_ticks[7], __builtin_amdgcn_s_memtime() - t_last);  // S5 A: inverse iteration
   }
   else if ((wave & 3) != 0 && wave - 1 - (wave >> 2) < ((C - 1 + 15) >> 4)) {  // (uniform per wave)
-    // block b of S6's loop (reflectors k0 .. k1 - 1, counted from the last): S = Y^H Y, then T by
-    // zlarft, into the work scratch after the reflectors (S at [0, 256), T at [256, 512) of the
-    // block's 512).  Read back through agent-scope loads: the same addresses were read by the
-    // previous update's S6 on this CU, so the L1 may hold them.
-    // (waves 1-3, 5-7, 9-11: block b = wave - 1 - wave / 4)
-    const int b = wave - 1 - (wave >> 2), k1 = C - 1 - 16 * b, k0 = k1 > 16 ? k1 - 16 : 0, nb = k1 - k0;
-    const int li = lane & 15, lk = lane >> 4;
-    aqc::d4_t sr = {0, 0, 0, 0}, si = {0, 0, 0, 0};
-    for (int r0 = 0; r0 < C; r0 += 4) {  // A[m = i][k = row] = conj(Y[row][i]), B = Y
-      const int row = r0 + lk, k = k0 + li;
-      const cplx y = (li < nb && row > k && row < C) ? aqc::ldg(hh + (size_t)k * (2 * C - k - 1) / 2 + (row - k - 1))
-                                                     : aqc::cmk(0, 0);
-      sr = __builtin_amdgcn_mfma_f64_16x16x4f64(y.x, y.x, sr, 0, 0, 0);
-      sr = __builtin_amdgcn_mfma_f64_16x16x4f64(y.y, y.y, sr, 0, 0, 0);
-      si = __builtin_amdgcn_mfma_f64_16x16x4f64(y.x, y.y, si, 0, 0, 0);
-      si = __builtin_amdgcn_mfma_f64_16x16x4f64(-y.y, y.x, si, 0, 0, 0);
-    }
-    cplx* Sg = hh + kTfacOff + (size_t)b * 512;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) aqc::stg(Sg + (lk + 4 * q) * 16 + li, aqc::cmk(sr[q], si[q]));
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    // zlarft (forward, columnwise): lane (a, g) holds T[a][g + 4 m]; T[a][i] = -tau_i sum_{a <= bb < i}
-    // T[a][bb] S[bb][i], T[i][i] = tau_i -- the recurrence of the in-loop form
-    const int a = lane >> 2, g = lane & 3;
-    cplx tq[4] = {aqc::cmk(0, 0), aqc::cmk(0, 0), aqc::cmk(0, 0), aqc::cmk(0, 0)};
-    for (int i = 0; i < 16; ++i) {
-      const cplx tau = i < nb ? s_tau[k0 + i] : aqc::cmk(0, 0);
-      cplx acc = aqc::cmk(0, 0);
-#pragma unroll
-      for (int m = 0; m < 4; ++m) {
-        const int bb = g + 4 * m;
-        if (4 * m < i && bb < i) {
-          const gdbl_t* sp = (const gdbl_t*)(const double*)(Sg + bb * 16 + i);
-          const cplx sv = aqc::cmk(__hip_atomic_load(sp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                                   __hip_atomic_load(sp + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-          acc = aqc::cfma(tq[m], sv, acc);
-        }
-      }
-      acc.x = aqc::row_sum4(acc.x);
-      acc.y = aqc::row_sum4(acc.y);
-      const cplx ti = aqc::cmul(tau, acc);
-      const cplx val = a < i ? aqc::cmk(-ti.x, -ti.y) : (a == i ? tau : aqc::cmk(0, 0));
-      if (g == (i & 3)) tq[i >> 2] = val;
-    }
-#pragma unroll
-    for (int m = 0; m < 4; ++m) aqc::stg(Sg + 256 + a * 16 + g + 4 * m, tq[m]);
+    s6_factors(wave - 1 - (wave >> 2), C, hh, s_tau, lane);
   }
   __syncthreads();
-  if (wave == 0) {  // Gram-Schmidt inside clusters (uniform loop over wave 0)
-    // clusters: gaps below 1e-7 ||T|| (dstein's 1e-3 is far more conservative than three
-    // inverse-iteration steps need: at gaps above ~1e-10 the vectors come out orthogonal to
-    // 1e-14 on their own, tools/gram_svd_proto.py)
-    const double ortol = 1e-7 * s_tn;
-    int start = 0;
-    for (int i = 1; i < K; ++i) {
-      if (s_lam[i - 1] - s_lam[i] >= ortol) {
-        start = i;
-        continue;
-      }
-      for (int jj = start; jj < i; ++jj) {
-        double dp = 0.0;
-        for (int row = lane; row < C; row += 64) dp = fma(zb[row * 64 + i], zb[row * 64 + jj], dp);
-        dp = wave_sum_d(dp);
-        for (int row = lane; row < C; row += 64) zb[row * 64 + i] = fma(-dp, zb[row * 64 + jj], zb[row * 64 + i]);
-      }
-      double n2 = 0.0;
-      for (int row = lane; row < C; row += 64) n2 = fma(zb[row * 64 + i], zb[row * 64 + i], n2);
-      n2 = wave_sum_d(n2);
-      const double sc = 1.0 / sqrt(n2);
-      for (int row = lane; row < C; row += 64) zb[row * 64 + i] *= sc;
-    }
-  }
+  if (wave == 0) gs_clusters<64>(K, C, zb, s_lam, s_tn, lane);  // (uniform loop over wave 0)
   __syncthreads();
-  if (tid < K) {
-    const int i = tid;
-    // z^T T z with eight rows' loads in flight and two partial sums (the rows one at a time waited
-    // out an LDS round trip each); the last row's e term is masked by zeroing its factor
-    double s2a = 0.0, s2b = 0.0;
-    int r0 = 0;
-    constexpr int U = 8;
-    for (; r0 + U <= C; r0 += U) {
-      double zz[U + 1], dd[U], ee[U];
-#pragma unroll
-      for (int u = 0; u <= U; ++u) zz[u] = zb[min(r0 + u, C - 1) * 64 + i];
-#pragma unroll
-      for (int u = 0; u < U; ++u) dd[u] = s_d[r0 + u], ee[u] = r0 + u < C - 1 ? s_e[r0 + u] : 0.0;
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        s2a = fma(dd[u] * zz[u], zz[u], s2a);
-        s2b = fma(2.0 * ee[u] * zz[u], zz[u + 1], s2b);
-      }
-    }
-    for (; r0 < C; ++r0) {
-      const double z = zb[r0 * 64 + i];
-      s2a = fma(s_d[r0] * z, z, s2a);
-      if (r0 < C - 1) s2b = fma(2.0 * s_e[r0] * z, zb[(r0 + 1) * 64 + i], s2b);
-    }
-    const double s2 = s2a + s2b;
-    s_sig2[i] = s2 > 0.0 ? s2 : 0.0;
-  }
+  if (tid < K) s_sig2[tid] = rayleigh<64>(tid, C, zb, s_d, s_e);
   __syncthreads();
   tick(3);
   // ---- S6: V = Q Z on the matrix cores, 16 reflectors at a time in compact WY form (LAPACK
@@ -931,131 +1228,9 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
       vim[t][q] = 0.0;
     }
   }
-  // LDS (complex units): Y [128][16] (column index swizzled by row & 15: conflict-free reads along
-  // rows and along columns), Y^H V partials of waves 4..15, T (from S5's precompute), W2 = T Y^H V
-  cplx* Yl = xbuf;
-  cplx* Pw = Yl + 2048;
-  cplx* Tl = Pw + 12 * 256;      // [16][17]
-  cplx* W2l = Tl + 3 * 256 + 16 * 64;
-  auto fetch_y = [&](int k0, int nb, cplx (&y)[2]) {
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int e = tid + 1024 * u, row = e >> 4, i = e & 15, k = k0 + i;
-      y[u] = (i < nb && row > k && row < C) ? aqc::ldg(hh + (size_t)k * (2 * C - k - 1) / 2 + (row - k - 1))
-                                            : aqc::cmk(0, 0);
-    }
-  };
-  cplx ynx[2];
-  {
-    const int k1 = C - 1, k0 = k1 > 16 ? k1 - 16 : 0;
-    fetch_y(k0, k1 - k0, ynx);
-  }
-  __syncthreads();  // V's initial values are read from zb: the LDS can be overwritten now
-  for (int k1 = C - 1; k1 > 0; k1 -= 16) {
-    const int k0 = k1 > 16 ? k1 - 16 : 0;
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int e = tid + 1024 * u, row = e >> 4, i = e & 15;
-      Yl[row * 16 + (i ^ (row & 15))] = ynx[u];
-    }
-    if (tid < 256) {  // this block's T from S5 (agent-scope loads: see the precompute)
-      const gdbl_t* tp = (const gdbl_t*)(const double*)(hh + kTfacOff + (size_t)((C - 1 - k1) >> 4) * 512 + 256 + tid);
-      Tl[(tid >> 4) * 17 + (tid & 15)] = aqc::cmk(__hip_atomic_load(tp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                                                  __hip_atomic_load(tp + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    }
-    __syncthreads();  // B1: Y
-    // Y^H V over this wave's 32 rows: A[m = i][k = row] = conj(Y[row][i])
-    aqc::d4_t wr = {0, 0, 0, 0}, wi = {0, 0, 0, 0};
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      if (32 * mg + 16 * t + 15 > k0) {  // rows <= k0 of Y are zero (uniform per wave)
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          const int row = 32 * mg + 16 * t + 4 * s + lk;
-          const cplx y = Yl[row * 16 + (li ^ (row & 15))];
-          wr = __builtin_amdgcn_mfma_f64_16x16x4f64(y.x, vre[t][s], wr, 0, 0, 0);
-          wr = __builtin_amdgcn_mfma_f64_16x16x4f64(y.y, vim[t][s], wr, 0, 0, 0);
-          wi = __builtin_amdgcn_mfma_f64_16x16x4f64(y.x, vim[t][s], wi, 0, 0, 0);
-          wi = __builtin_amdgcn_mfma_f64_16x16x4f64(-y.y, vre[t][s], wi, 0, 0, 0);
-        }
-      }
-    }
-    // D layout: row b = lk + 4 q (reflector), column li
-    if (mg > 0) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) Pw[((mg - 1) * 4 + nt) * 256 + (lk + 4 * q) * 16 + li] = aqc::cmk(wr[q], wi[q]);
-    }
-    __syncthreads();  // B2: partials
-    if (mg == 0) {
-      // Y^H V of column tile nt summed in registers, then W2 = T (Y^H V) for that tile on the matrix
-      // cores right here: the sum's D layout (row lk + 4 q, column li) is the B operand of k-step q
-      // and T (in the LDS since B1) the A operand -- no W1 round trip through the LDS, no B3
-      aqc::d4_t br, bi, w2r = {0, 0, 0, 0}, w2i = {0, 0, 0, 0};
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int b = lk + 4 * q;
-        cplx w = aqc::cmk(wr[q], wi[q]);
-#pragma unroll
-        for (int m = 0; m < 3; ++m) w = aqc::cadd(w, Pw[(m * 4 + nt) * 256 + b * 16 + li]);
-        br[q] = w.x;
-        bi[q] = w.y;
-      }
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const cplx t = Tl[li * 17 + 4 * q + lk];  // A[m = li][k = lk] = T[li][4 q + lk]
-        w2r = __builtin_amdgcn_mfma_f64_16x16x4f64(t.x, br[q], w2r, 0, 0, 0);
-        w2r = __builtin_amdgcn_mfma_f64_16x16x4f64(-t.y, bi[q], w2r, 0, 0, 0);
-        w2i = __builtin_amdgcn_mfma_f64_16x16x4f64(t.x, bi[q], w2i, 0, 0, 0);
-        w2i = __builtin_amdgcn_mfma_f64_16x16x4f64(t.y, br[q], w2i, 0, 0, 0);
-      }
-#pragma unroll
-      for (int q = 0; q < 4; ++q) W2l[(lk + 4 * q) * 64 + 16 * nt + li] = aqc::cmk(w2r[q], w2i[q]);
-    }
-    __syncthreads();  // B4: W2
-    // the next block's reflectors, in flight during the V update: issued before B1 they were
-    // drained by the spill reloads' vmcnt(0) waits between B1 and B4
-    if (k0 > 0) {
-      const int n1 = k0, n0 = n1 > 16 ? n1 - 16 : 0;
-      fetch_y(n0, n1 - n0, ynx);
-    }
-    // V -= Y W2: A[m = row][k = b] = Y[row][b], B[k = b][n] = W2[b][n].  The lane's indices come
-    // from the lane counter and the wave index in an SGPR: derived from the thread id (whose VGPR
-    // is spilled) their reload's vmcnt(0) drained the next block's reflector loads issued above
-    const int vl_ = fresh_lane();
-    const int vmg = wave_s >> 2, vnt = wave_s & 3, vli = vl_ & 15, vlk = vl_ >> 4;
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      if (32 * vmg + 16 * t + 15 > k0) {
-        const int row = 32 * vmg + 16 * t + vli;
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          const int b = 4 * s + vlk;
-          const cplx y = Yl[row * 16 + (b ^ (row & 15))];
-          const cplx w = W2l[b * 64 + 16 * vnt + vli];
-          vre[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(-y.x, w.x, vre[t], 0, 0, 0);
-          vre[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(y.y, w.y, vre[t], 0, 0, 0);
-          vim[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(-y.x, w.y, vim[t], 0, 0, 0);
-          vim[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(-y.y, w.x, vim[t], 0, 0, 0);
-        }
-      }
-    }
-    __syncthreads();  // B5: Y, W2 and the partials are overwritten next block
-  }
+  s6_back(j, hh, C, K, 0, vre, vim, s_sig2, tid, lane, wave, wave_s);
   tick(4);
-  {  // the reflectors are dead (last read before B1 of the last block): W overwrites them
-    const int col = 16 * nt + li;
-    if (col < K) {
-      const double sg = sqrt(s_sig2[col]);
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int row = 32 * mg + 16 * t + lk + 4 * q;
-          if (row < C) aqc::stg(j.work + (size_t)col * C + row, aqc::cmk(vre[t][q] * sg, vim[t][q] * sg));
-        }
-      }
-    }
-  }
+  }  // (K <= 64)
   for (int c = tid; c < C; c += 1024) aqc::stg(j.sig + c, c < K ? sqrt(s_sig2[c]) : 0.0);
   if (tid == 0) aqc::stg(j.sig + kSigTail, s_tail);  // the tail gram_keep dropped (rank_body)
   if (tid == 0) {

@@ -143,6 +143,35 @@ def test_gram_path_vs_numpy(m, n):
     assert np.max(np.abs(V.conj().T @ V - np.eye(K))) < 1e-11
 
 
+@pytest.mark.parametrize("m,n,decay", [(128, 128, 0.97), (128, 96, 0.97), (96, 128, 0.95), (128, 80, 0.98)])
+def test_gram_path_wide_k_vs_numpy(m, n, decay):
+    """max_chi unbounded (debug max_chi 0) and no tail threshold: every value above the CHOP is kept,
+    K = C > 64 -- the wide S5 (waves 0-1, pivots in the work scratch) and S6 in two passes.  Sigma
+    to 1e-12 sigma_1, each W column an eigenvector of X^H X (residual 1e-11 sigma_1^2), V unitary."""
+    from adaptaqc_amd import _lib
+
+    c = min(m, n)
+    theta = _spectrum_theta(m, n, decay ** np.arange(c), 3 + m + n)
+    L = _lib.lib()
+    _lib.check(L.aqc_mps_set_svd_path(1, 0))
+    try:
+        _gram_ticks()
+        w, sig, _, _ = _run(theta, 7)
+        assert _gram_ticks()[4] > 0, "the Gram path declined"
+    finally:
+        _lib.check(L.aqc_mps_set_svd_path(1, 64))
+    x = theta if m >= n else theta.conj().T
+    s_ref = np.linalg.svd(x, compute_uv=False)
+    order = np.argsort(-sig)
+    got = sig[order]
+    np.testing.assert_allclose(got, s_ref, rtol=0, atol=1e-12 * s_ref[0])
+    V = w[:, order] / got[None, :]
+    G = x.conj().T @ x
+    res = np.linalg.norm(G @ V - V * got[None, :] ** 2, axis=0)
+    assert res.max() < 1e-11 * s_ref[0] ** 2, res.max()
+    assert np.max(np.abs(V.conj().T @ V - np.eye(c))) < 1e-11
+
+
 @pytest.mark.parametrize("kind", ["graded", "rank10", "zero_tail_cluster"])
 def test_gram_path_declines_to_jacobi(kind):
     """Where the kept values reach the noise floor of the Gram form (lambda_K <= 1e-9 lambda_1) the
