@@ -29,7 +29,8 @@ EXPORTS = (
     "aqc_mps_create", "aqc_mps_destroy", "aqc_mps_set_truncation", "aqc_mps_set_vidal",
     "aqc_mps_get_vidal", "aqc_mps_get_dims", "aqc_mps_copy", "aqc_mps_copy_batch", "aqc_mps_apply",
     "aqc_mps_apply_batch", "aqc_mps_apply_sort_batch", "aqc_mps_apply_sort_batch_async", "aqc_mps_check_batch", "aqc_mps_sort", "aqc_mps_sort_batch", "aqc_mps_overlap_zero",
-    "aqc_mps_overlap_zero_batch", "aqc_mps_dot", "aqc_mps_z_all", "aqc_mps_amps_hw1",
+    "aqc_mps_overlap_zero_batch", "aqc_mps_dot", "aqc_mps_z_all", "aqc_mps_amps_hw1", "aqc_mps_z_all_batch",
+    "aqc_mps_amps_hw1_batch",
     "aqc_pair_grads", "aqc_pair_grads_batch", "aqc_argmax_scaled", "aqc_mps_jacobi_stats",
     "aqc_mps_set_jacobi_tol", "aqc_mps_set_jacobi_stop", "aqc_mps_set_fused_chain", "aqc_mps_chain_ticks", "aqc_svd_debug",
     "aqc_sv_pair_rdms", "aqc_mps_pair_rdms", "aqc_mps_pair_rdms_batch", "aqc_entanglement_measures",
@@ -93,6 +94,8 @@ _SIGS = {
     "aqc_mps_dot": ([_P, _P, _DP, _DP], _I),
     "aqc_mps_z_all": ([_P, _P], _I),
     "aqc_mps_amps_hw1": ([_P, _P], _I),
+    "aqc_mps_z_all_batch": ([_P, _I, _P], _I),
+    "aqc_mps_amps_hw1_batch": ([_P, _I, _P], _I),
     "aqc_pair_grads": ([_P, _P, _P, _I, _P, _P, _P, _I, _P, _I], _I),
     "aqc_pair_grads_batch": ([_P, _I, _P, _P, _I, _P, _P, _P, _I, _P, _I], _I),
     "aqc_argmax_scaled": ([_P, _P, _I, _I, _IP], _I),
@@ -246,7 +249,8 @@ def gram_big_stats():
     """Counters of the multi-workgroup Gram path for 2 chi > 128 since the last call
     (aqc_svd_gram_big_stats): calls, taken, declined, declined at the eigenvalue floor, exchange
     timeouts."""
-    out = np.zeros(5)
+    out = np.zeros(8)
     check(load().aqc_svd_gram_big_stats(ptr(out)))
     return {"calls": int(out[0]), "taken": int(out[1]), "declined": int(out[2]),
-            "declined_floor": int(out[3]), "timeouts": int(out[4])}
+            "declined_floor": int(out[3]), "timeouts": int(out[4]), "certificates": int(out[5]),
+            "certified": int(out[6]), "declined_certificate": int(out[7])}

@@ -99,12 +99,14 @@ __global__ __launch_bounds__(kT) void k_rdm_env(const RdmJob* __restrict__ jobs)
   }
 }
 
-// P_b[s][sb] = A_b^s R_{b+1} A_b^{sb dag}; m = 0: (0,0), 1: (0,1), 2: (1,1).  grid (n, 3, states)
-__global__ __launch_bounds__(kT) void k_rdm_P(const RdmJob* __restrict__ jobs) {
+// P_b[s][sb] = A_b^s R_{b+1} A_b^{sb dag}; m = 0: (0,0), 1: (0,1), 2: (1,1).  grid (n, 3 or 2, states);
+// with two m, the diagonal pair (0,0), (1,1) only (single-site <Z>).  first_site: site 0 too (pair
+// RDMs never need it: it is never the second qubit of a pair)
+__global__ __launch_bounds__(kT) void k_rdm_P(const RdmJob* __restrict__ jobs, int first_site) {
   const RdmJob& j = jobs[blockIdx.z];
   __shared__ aqc::GemmLds lds;
-  const int b = blockIdx.x, m = blockIdx.y;
-  if (b == 0) return;  // site 0 is never the second qubit of a pair
+  const int b = blockIdx.x, m = gridDim.y == 2 ? 2 * (int)blockIdx.y : (int)blockIdx.y;
+  if (b == 0 && !first_site) return;
   const int s = m == 2 ? 1 : 0, sb = m == 0 ? 0 : 1;
   const int cap = j.cap;
   const size_t cc = (size_t)cap * cap;
@@ -202,6 +204,33 @@ __global__ __launch_bounds__(kT) void k_rdm_chain(const RdmJob* __restrict__ job
 }
 
 // requested pairs (c, t) -> rho of (min, max); grid over pairs x states
+// <Z_b> = rho_b[0][0] - rho_b[1][1], rho_b[s][sb] = Tr(L_b P_b[s][sb]) (the single-site RDM of the
+// same environments).  grid (n, states)
+__global__ __launch_bounds__(kT) void k_rdm_ztrace(const RdmJob* __restrict__ jobs, double* __restrict__ out) {
+  const RdmJob& j = jobs[blockIdx.y];
+  const int b = blockIdx.x, cap = j.cap;
+  const size_t cc = (size_t)cap * cap;
+  const int cl = j.dims[b];
+  const cplx* L = j.Lenv + (size_t)b * cc;
+  const cplx* P0 = j.P + ((size_t)b * 3 + 0) * cc;
+  const cplx* P1 = j.P + ((size_t)b * 3 + 2) * cc;
+  __shared__ double red[kT];
+  double acc = 0.0;
+  for (int e = threadIdx.x; e < cl * cl; e += kT) {
+    const int c = e / cl, cp = e % cl;  // L[cp][c] P[c][cp]
+    const cplx l = L[(size_t)cp * cap + c];
+    const cplx d = aqc::csub(P0[(size_t)c * cap + cp], P1[(size_t)c * cap + cp]);
+    acc = fma(l.x, d.x, fma(-l.y, d.y, acc));
+  }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int k = kT / 2; k > 0; k >>= 1) {
+    if ((int)threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[(size_t)blockIdx.y * j.n + b] = red[0];
+}
+
 __global__ void k_rdm_gather(const RdmJob* __restrict__ jobs, const int* __restrict__ pairs, int npairs,
                              cplx* __restrict__ out) {
   const RdmJob& j = jobs[blockIdx.y];
@@ -451,7 +480,7 @@ int aqc_mps_pair_rdms_batch(aqc_mps_t* hs, int ns, const int* pairs, int npairs,
   hipLaunchKernelGGL(k_rdm_env, dim3(2, ns), dim3(kT), 0, st, djobs);
   aqc::KernelTimer::end(st);
   AQC_CHECK_LAUNCH();
-  hipLaunchKernelGGL(k_rdm_P, dim3(n, 3, ns), dim3(kT), 0, st, djobs);
+  hipLaunchKernelGGL(k_rdm_P, dim3(n, 3, ns), dim3(kT), 0, st, djobs, 0);
   AQC_CHECK_LAUNCH();
   double steps = 0.0;
   for (int a : alist) steps += (double)(n - 1 - a);
@@ -463,6 +492,64 @@ int aqc_mps_pair_rdms_batch(aqc_mps_t* hs, int ns, const int* pairs, int npairs,
   AQC_CHECK_LAUNCH();
   if (!out_is_device)
     AQC_HIP_CHECK(hipMemcpyAsync(out, dout, (size_t)ns * npairs * 16 * sizeof(cplx), hipMemcpyDeviceToHost, st));
+  AQC_HIP_CHECK(hipStreamSynchronize(st));
+  return AQC_OK;
+}
+
+int aqc_mps_z_all_batch(aqc_mps_t* hs, int ns, double* out) {
+  AQC_REQUIRE(hs && ns >= 0 && (out || ns == 0), "aqc_mps_z_all_batch: bad arguments");
+  if (ns == 0) return AQC_OK;
+  const int n = hs[0]->d.n, cap = hs[0]->d.cap;
+  for (int s = 0; s < ns; ++s)
+    AQC_REQUIRE(hs[s] && hs[s]->d.n == n && hs[s]->d.cap == cap, "aqc_mps_z_all_batch: all states need the same n and capacity");
+  int rc = aqc_mps_sort_batch(hs, ns);
+  if (rc != AQC_OK) return rc;
+  const size_t cc = (size_t)cap * cap;
+  const size_t per_state = (2 * (size_t)(n + 1) * cc + 4 * cc + 6 * (size_t)n * cc) * sizeof(cplx);
+  const size_t jb = ((ns * sizeof(RdmJob) + 255) / 256) * 256;
+  const size_t ob = (((size_t)ns * n * sizeof(double) + 255) / 256) * 256;
+  hipStream_t st = aqc::mps_stream();
+  RdmBuffers& rb = rbuf();
+  AQC_HIP_CHECK(hipStreamSynchronize(st));
+  rc = ensure(rb, jb + ob + ns * per_state + 1024);
+  if (rc != AQC_OK) return rc;
+  char* base = (char*)rb.dev;
+  RdmJob* djobs = (RdmJob*)base;
+  double* dout = (double*)(base + jb);
+  cplx* work = (cplx*)(base + jb + ob);
+  std::vector<RdmJob> jobs(ns);
+  for (int s = 0; s < ns; ++s) {
+    RdmJob& j = jobs[s];
+    std::memset(&j, 0, sizeof(j));
+    j.gam = hs[s]->d.gam;
+    j.lam = hs[s]->d.lam;
+    j.dims = hs[s]->d.dims;
+    j.n = n;
+    j.cap = cap;
+    cplx* p = work + (size_t)s * (per_state / sizeof(cplx));
+    j.Lenv = p;
+    p += (size_t)(n + 1) * cc;
+    j.Renv = p;
+    p += (size_t)(n + 1) * cc;
+    j.tmpL = p;
+    p += 2 * cc;
+    j.tmpR = p;
+    p += 2 * cc;
+    j.P = p;
+    p += 3 * (size_t)n * cc;
+    j.U = p;
+  }
+  AQC_HIP_CHECK(hipMemcpyAsync(djobs, jobs.data(), ns * sizeof(RdmJob), hipMemcpyHostToDevice, st));
+  const double c3 = (double)cap * cap * cap;
+  aqc::KernelTimer::begin(st, "mps_zall", 0.0, ns * 2.0 * n * 4.0 * c3 * 8.0);
+  hipLaunchKernelGGL(k_rdm_env, dim3(2, ns), dim3(kT), 0, st, djobs);
+  AQC_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_rdm_P, dim3(n, 2, ns), dim3(kT), 0, st, djobs, 1);
+  AQC_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_rdm_ztrace, dim3(n, ns), dim3(kT), 0, st, djobs, dout);
+  aqc::KernelTimer::end(st);
+  AQC_CHECK_LAUNCH();
+  AQC_HIP_CHECK(hipMemcpyAsync(out, dout, (size_t)ns * n * sizeof(double), hipMemcpyDeviceToHost, st));
   AQC_HIP_CHECK(hipStreamSynchronize(st));
   return AQC_OK;
 }

@@ -47,7 +47,7 @@
 namespace aqc {
 
 // calls, taken, declined (gram off / shape), declined at the eigenvalue floor, exchange timeouts
-__device__ unsigned long long g_gbig_stats[5];
+__device__ unsigned long long g_gbig_stats[8];
 // shader-clock ticks of job 0's first workgroup (thread 0), summed over calls: tridiagonalisation
 // phases [0] pass + row sums, [1] publish (stores, vmcnt, barrier), [2] counter wait, [3] reads + p^H v,
 // [4] w, new row, partial norms; [5] k_gb_eig (job 0, block 0), [6] k_gb_back (job 0, block 0), [7] k_gb_inv (job 0,
@@ -93,6 +93,8 @@ struct GBArgs {
   double* err;     // per job CT: their multisection brackets' half widths
   int* kept;       // per job: the kept count (reduce_zeros on lam, k_gb_keep)
   double* tail;    // per job: the tail sum that decision dropped (to sig[kSigTail])
+  int* cert;       // per job: the decision assumed the open-CHOP values chopped (k_gb_cert checks)
+  double* certsum; // per job: ||X - X V V^H||_F^2 (k_gb_cert)
   double* tn;      // per job: ||T|| (Gershgorin)
   cplx* xch;       // per job 4 x CT: p (two buffers), old row k + 1 (two buffers)
   unsigned* cnt;   // per job 32 words (128 B)
@@ -761,15 +763,19 @@ __global__ __launch_bounds__(64) void k_gb_keep(const TwoSiteJob* __restrict__ j
   bool tr;
   job_dims(j, M, L, C, tr, K);
   double tail = 0.0;
+  int cert = 0;
   const int k = gram_keep(a.lam + (size_t)jb * CT, a.err + (size_t)jb * CT, K, C, j.max_chi, j.thr, ldg(a.tn + jb),
-                          kGbRelFloor, tail);
+                          kGbRelFloor, tail, &cert);
   if (k < 0) {
     *(gi32*)(a.status + jb) = 2;
     atomicAdd(&g_gbig_stats[3], 1ull);
     return;
   }
   *(gi32*)(a.kept + jb) = k;
+  *(gi32*)(a.cert + jb) = cert;
+  stg(a.certsum + jb, 0.0);
   stg(a.tail + jb, tail);
+  if (cert) atomicAdd(&g_gbig_stats[5], 1ull);
 }
 
 __device__ __forceinline__ int kept_count(const GBArgs& a, int jb) { return *(const gi32*)(a.kept + jb); }
@@ -1137,12 +1143,91 @@ __global__ __launch_bounds__(64 * NW) void k_gb_back(const TwoSiteJob* __restric
   }
 }
 
+// ---- the certificate of a rank-deficient decision (aqc::gram_keep's cert): every dropped sigma^2 is
+// at most ||X - X V V^H||_F^2 (V the K kept right vectors, W / sigma from k_gb_back), computed from X
+// itself -- so to eps ||X|| in sigma, where G's eigenvalues carry eps ||G||.  Below CHOP / 2 the
+// open-CHOP values were all chopped, as LAPACK's sigma^2 ~ (eps sigma_1)^2 are in Aer; otherwise the
+// job declines (status 4: the block Jacobi decides).  Y = X V into the (dead) G scratch, then
+// R = X - Y V^H tile by tile with the squares summed per job; grid (ceil(CT / 64), ceil(CT / 64), nj).
+template <int CT>
+__device__ __forceinline__ cplx xval(const TwoSiteJob& j, bool tr, int M, int R, int c) {
+  return tr ? cconj(ldg(j.theta + (size_t)R * M + c)) : ldg(j.theta + (size_t)c * M + R);
+}
+
+template <int CT>
+__global__ __launch_bounds__(256) void k_gb_cert_y(const TwoSiteJob* __restrict__ jobs, GBArgs a, int job0) {
+  const int jb = job0 + (int)blockIdx.z;
+  if (*(const gi32*)(a.status + jb) != 0 || !*(const gi32*)(a.cert + jb)) return;
+  const TwoSiteJob& j = jobs[jb];
+  int M, L, C, K;
+  bool tr;
+  job_dims(j, M, L, C, tr, K);
+  K = kept_count(a, jb);
+  const int r0 = blockIdx.x * 64, c0 = blockIdx.y * 64;
+  if (r0 >= L || c0 >= K) return;
+  __shared__ GemmLds lds;
+  cplx* Y = a.G + (size_t)jb * CT * CT;  // Y[R][kk] at R * CT + kk
+  const double* sg = j.sig;
+  block_cgemm(
+      min(64, L - r0), min(64, K - c0), C, [&](int i, int c) { return xval<CT>(j, tr, M, r0 + i, c); },
+      [&](int c, int kk) { return cscale(ldg(j.work + (size_t)(c0 + kk) * C + c), 1.0 / ldg(sg + c0 + kk)); },
+      [&](int i, int kk, cplx v) { stg(Y + (size_t)(r0 + i) * CT + c0 + kk, v); }, lds);
+}
+
+template <int CT>
+__global__ __launch_bounds__(256) void k_gb_cert_r(const TwoSiteJob* __restrict__ jobs, GBArgs a, int job0) {
+  const int jb = job0 + (int)blockIdx.z;
+  if (*(const gi32*)(a.status + jb) != 0 || !*(const gi32*)(a.cert + jb)) return;
+  const TwoSiteJob& j = jobs[jb];
+  int M, L, C, K;
+  bool tr;
+  job_dims(j, M, L, C, tr, K);
+  K = kept_count(a, jb);
+  const int r0 = blockIdx.x * 64, c0 = blockIdx.y * 64;
+  if (r0 >= L || c0 >= C) return;
+  __shared__ GemmLds lds;
+  __shared__ double red[256];
+  const cplx* Y = a.G + (size_t)jb * CT * CT;
+  const double* sg = j.sig;
+  double acc = 0.0;
+  block_cgemm(
+      min(64, L - r0), min(64, C - c0), K, [&](int i, int kk) { return ldg(Y + (size_t)(r0 + i) * CT + kk); },
+      [&](int kk, int c) { return cconj(cscale(ldg(j.work + (size_t)kk * C + c0 + c), 1.0 / ldg(sg + kk))); },
+      [&](int i, int c, cplx v) { acc += cnorm2(csub(xval<CT>(j, tr, M, r0 + i, c0 + c), v)); }, lds);
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int k = 128; k > 0; k >>= 1) {
+    if ((int)threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) atomicAdd(a.certsum + jb, red[0]);
+}
+
+// grid (nj): decline the jobs whose certificate fails (their W / sig were written by k_gb_back: the
+// Jacobi contract is restored -- qr = 0, no handed-over tail -- before the host re-runs them)
+template <int CT>
+__global__ __launch_bounds__(64) void k_gb_cert_end(const TwoSiteJob* __restrict__ jobs, GBArgs a, int job0) {
+  const int jb = job0 + (int)blockIdx.x;
+  if (threadIdx.x != 0 || *(const gi32*)(a.status + jb) != 0 || !*(const gi32*)(a.cert + jb)) return;
+  TwoSiteJob& j = const_cast<TwoSiteJob&>(jobs[jb]);
+  const double r2 = __hip_atomic_load((const gdbl*)(a.certsum + jb), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (r2 < 0.5 * kReduceChop) {
+    atomicAdd(&g_gbig_stats[6], 1ull);
+    return;
+  }
+  *(gi32*)(a.status + jb) = 4;
+  j.qr = 0;
+  stg(j.sig + kSigTail, 0.0);
+  atomicAdd(&g_gbig_stats[7], 1ull);
+  atomicAdd(&g_gbig_stats[1], ~0ull);  // (k_gb_back counted it as taken)
+}
+
 struct GBBuffers {
   int ct = 0, nj = 0;
   cplx* G = nullptr;
   double *d = nullptr, *e = nullptr, *z = nullptr, *dinv = nullptr, *sig2 = nullptr, *lam = nullptr, *tn = nullptr;
-  double *err = nullptr, *tail = nullptr;
-  int* kept = nullptr;
+  double *err = nullptr, *tail = nullptr, *certsum = nullptr;
+  int *kept = nullptr, *cert = nullptr;
   cplx* tau = nullptr;
   cplx* tfac = nullptr;
   cplx* yc = nullptr;
@@ -1157,7 +1242,7 @@ struct GBBuffers {
 void gb_free(GBBuffers& b) {
   hipFree(b.G), hipFree(b.d), hipFree(b.e), hipFree(b.z), hipFree(b.dinv), hipFree(b.sig2), hipFree(b.tau);
   hipFree(b.lam), hipFree(b.tn), hipFree(b.tfac), hipFree(b.yc);
-  hipFree(b.err), hipFree(b.tail), hipFree(b.kept);
+  hipFree(b.err), hipFree(b.tail), hipFree(b.kept), hipFree(b.cert), hipFree(b.certsum);
   hipFree(b.xch), hipFree(b.cnt), hipFree(b.status), hipFree(b.djobs);
   hipHostFree(b.host_status), hipHostFree(b.hjobs);
   b = GBBuffers();
@@ -1187,6 +1272,8 @@ int gb_ensure(GBBuffers& b, int ct, int nj, hipStream_t st) {
   AQC_HIP_CHECK(hipMalloc(&b.err, (size_t)c * n * sizeof(double)));
   AQC_HIP_CHECK(hipMalloc(&b.tail, (size_t)n * sizeof(double)));
   AQC_HIP_CHECK(hipMalloc(&b.kept, (size_t)n * sizeof(int)));
+  AQC_HIP_CHECK(hipMalloc(&b.cert, (size_t)n * sizeof(int)));
+  AQC_HIP_CHECK(hipMalloc(&b.certsum, (size_t)n * sizeof(double)));
   AQC_HIP_CHECK(hipMalloc(&b.tfac, (size_t)(c / 16) * 256 * n * sizeof(cplx)));
   AQC_HIP_CHECK(hipMalloc(&b.yc, cc * sizeof(cplx)));
   AQC_HIP_CHECK(hipMalloc(&b.tau, (size_t)c * n * sizeof(cplx)));
@@ -1245,7 +1332,7 @@ int run_gram_big(const TwoSiteJob* hjobs, const TwoSiteJob* jobs, int nj, int ca
   GBArgs a;
   a.G = b.G, a.d = b.d, a.e = b.e, a.tau = b.tau, a.z = b.z, a.dinv = b.dinv, a.sig2 = b.sig2;
   a.lam = b.lam, a.tn = b.tn, a.tfac = b.tfac, a.yc = b.yc;
-  a.err = b.err, a.kept = b.kept, a.tail = b.tail;
+  a.err = b.err, a.kept = b.kept, a.tail = b.tail, a.cert = b.cert, a.certsum = b.certsum;
   a.xch = b.xch, a.cnt = b.cnt, a.status = b.status;
   a.spin = g_gb_spin;
   if (g_gb_tail < 0) {
@@ -1299,6 +1386,12 @@ int run_gram_big(const TwoSiteJob* hjobs, const TwoSiteJob* jobs, int nj, int ca
       AQC_HIP_CHECK(hipStreamWaitEvent(ps, e1, 0));
     }
     hipLaunchKernelGGL((k_gb_back<CT>), dim3(CT / 16, nr), dim3(CT / 64 > 4 ? CT : 256), 0, ps, jobs, a, j0);
+    AQC_CHECK_LAUNCH();
+    hipLaunchKernelGGL((k_gb_cert_y<CT>), dim3(CT / 64, CT / 64, nr), dim3(256), 0, ps, jobs, a, j0);
+    AQC_CHECK_LAUNCH();
+    hipLaunchKernelGGL((k_gb_cert_r<CT>), dim3(CT / 64, CT / 64, nr), dim3(256), 0, ps, jobs, a, j0);
+    AQC_CHECK_LAUNCH();
+    hipLaunchKernelGGL((k_gb_cert_end<CT>), dim3(nr), dim3(64), 0, ps, jobs, a, j0);
     AQC_CHECK_LAUNCH();
     return AQC_OK;
   };
@@ -1377,10 +1470,10 @@ extern "C" int aqc_svd_gram_big_ticks(double* out) {
 
 extern "C" int aqc_svd_gram_big_stats(double* out) {
   AQC_REQUIRE(out, "aqc_svd_gram_big_stats: null argument");
-  unsigned long long t[5];
+  unsigned long long t[8];
   AQC_HIP_CHECK(hipMemcpyFromSymbol(t, HIP_SYMBOL(aqc::g_gbig_stats), sizeof(t)));
-  for (int i = 0; i < 5; ++i) out[i] = (double)t[i];
-  unsigned long long z[5] = {0, 0, 0, 0, 0};
+  for (int i = 0; i < 8; ++i) out[i] = (double)t[i];
+  unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   AQC_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(aqc::g_gbig_stats), z, sizeof(z)));
   return AQC_OK;
 }

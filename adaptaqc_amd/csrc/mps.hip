@@ -2681,6 +2681,44 @@ int aqc_mps_overlap_zero(aqc_mps_t h, double* re, double* im) {
   return rc;
 }
 
+int aqc_mps_amps_hw1_batch(aqc_mps_t* hs, int ns, double* out) {
+  AQC_REQUIRE(hs && ns >= 0 && (out || ns == 0), "aqc_mps_amps_hw1_batch: null argument");
+  if (ns == 0) return AQC_OK;
+  const int n = hs[0]->d.n;
+  for (int s = 0; s < ns; ++s) AQC_REQUIRE(hs[s] && hs[s]->d.n == n, "aqc_mps_amps_hw1_batch: all states need the same n");
+  int rc = aqc_mps_sort_batch(hs, ns);
+  if (rc != AQC_OK) return rc;
+  static cplx* dres[64] = {nullptr};
+  static size_t dres_n[64] = {0};
+  static void (*release)() = [] {
+    for (int d = 0; d < 64; ++d)
+      if (dres[d]) (void)hipFree(dres[d]), dres[d] = nullptr, dres_n[d] = 0;
+  };
+  aqc::on_finalize(release);
+  int dev = 0;
+  hipGetDevice(&dev);
+  hipStream_t st = aqc::mps_stream();
+  const size_t need = (size_t)ns * n;
+  if (dres_n[dev] < need) {
+    AQC_HIP_CHECK(hipStreamSynchronize(st));
+    if (dres[dev]) hipFree(dres[dev]);
+    dres_n[dev] = std::max(need, 2 * dres_n[dev]);
+    AQC_HIP_CHECK(hipMalloc(&dres[dev], dres_n[dev] * sizeof(cplx)));
+  }
+  std::vector<MeasJob> jobs(ns);
+  for (int s = 0; s < ns; ++s) jobs[s] = make_meas(hs[s], dres[dev] + (size_t)s * n);
+  const MeasJob* dj = nullptr;
+  rc = upload_jobs(jobs, &dj);
+  if (rc != AQC_OK) return rc;
+  hipLaunchKernelGGL(k_zero_chains, dim3(ns, 2), dim3(kT), 0, st, dj);
+  AQC_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_hw1, dim3(n, ns), dim3(kT), 0, st, dj);
+  AQC_CHECK_LAUNCH();
+  AQC_HIP_CHECK(hipMemcpyAsync(out, dres[dev], need * sizeof(cplx), hipMemcpyDeviceToHost, st));
+  AQC_HIP_CHECK(hipStreamSynchronize(st));
+  return AQC_OK;
+}
+
 int aqc_mps_amps_hw1(aqc_mps_t h, double* out) {
   AQC_REQUIRE(h && out, "aqc_mps_amps_hw1: null argument");
   int rc = aqc_mps_sort(h);

@@ -172,8 +172,13 @@ constexpr double kReduceChop = 1e-16;  // reduce_zeros' CHOP on sigma^2 (mps.hip
 // dropped by the tail rule from either start, which then decides nothing: it enters the tail as
 // [0, lam + err].  Returns the kept count K, and in tail_out the dropped tail sum (handed to
 // rank_body through sig[kSigTail], whose own tail rule then keeps all K).
+// cert (optional): where that fails only because of values in the CHOP's open band -- a rank-deficient
+// theta', whose numerically zero eigenvalues come out of G as +-(noise) -- the decision that they all
+// fall below the CHOP, with *cert = 1: valid if the caller then shows ||X - X V V^H||_F^2 < CHOP / 2
+// for the K kept right vectors V (every dropped sigma^2 is then below it; gram_big.hip k_gb_cert).
 [[maybe_unused]] static __device__ __noinline__ int gram_keep(const double* lam, const double* err, int KE, int C, int max_chi,
-                                             double thr, double tn, double floor, double& tail_out) {
+                                             double thr, double tn, double floor, double& tail_out,
+                                             int* cert = nullptr) {
   const double noise = 16.0 * C * 2.220446049250313e-16 * tn;
   int k_lo = 0, k_hi = 0;  // counts surely / possibly above the CHOP (lam descending)
   for (int i = 0; i < KE; ++i) {
@@ -181,28 +186,45 @@ constexpr double kReduceChop = 1e-16;  // reduce_zeros' CHOP on sigma^2 (mps.hip
     if (lam[i] - e > kReduceChop) k_lo = i + 1;
     if (lam[i] + e > kReduceChop) k_hi = i + 1;
   }
-  int k = k_hi < 1 ? 1 : k_hi;
-  if (max_chi > 0 && k > max_chi) k = max_chi;
-  double tail = 0.0, unc = 0.0;
-  while (k > 1) {
-    const int i = k - 1;
-    const double e = err[i] + noise;
-    double v = lam[i], ev = e;
-    if (i >= k_lo) {  // CHOP open: contributes anything in [0, lam + e] if dropped
-      v = 0.5 * (lam[i] + e);
-      ev = v;
+  if (cert) *cert = 0;
+  for (int attempt = 0; attempt < 2; ++attempt) {
+    // attempt 0: the open values as [0, lam + err]; attempt 1 (cert): the open values chopped
+    if (attempt == 1 && !(cert && k_hi > k_lo)) return -1;
+    int k = attempt == 0 ? k_hi : k_lo;
+    if (k < 1) k = 1;
+    if (max_chi > 0 && k > max_chi) k = max_chi;
+    double tail = 0.0, unc = 0.0;
+    bool ok = true;
+    while (k > 1) {
+      const int i = k - 1;
+      const double e = err[i] + noise;
+      double v = lam[i], ev = e;
+      if (i >= k_lo) {  // CHOP open: contributes anything in [0, lam + e] if dropped
+        v = 0.5 * (lam[i] + e);
+        ev = v;
+      }
+      const double sum = tail + v, m = unc + ev;
+      if (fabs(sum - thr) <= m) {  // the comparison is open
+        ok = false;
+        break;
+      }
+      if (sum >= thr) break;
+      if (attempt == 1) {  // (a surely-kept value dropped: the certificate cannot tell them apart)
+        ok = false;
+        break;
+      }
+      tail = sum;
+      unc = m;
+      --k;
     }
-    const double sum = tail + v, m = unc + ev;
-    if (fabs(sum - thr) <= m) return -1;  // the comparison is open
-    if (sum >= thr) break;
-    tail = sum;
-    unc = m;
-    --k;
+    if (!ok) continue;
+    if (k > k_lo) continue;  // a kept value whose CHOP is open (also far below the floor)
+    if (!(lam[0] > 0.0) || !(lam[k - 1] > floor * lam[0])) return -1;
+    tail_out = tail;
+    if (attempt == 1) *cert = !(max_chi > 0 && k_lo >= max_chi);
+    return k;
   }
-  if (k > k_lo) return -1;  // a kept value whose CHOP is open (also far below the floor)
-  if (!(lam[0] > 0.0) || !(lam[k - 1] > floor * lam[0])) return -1;
-  tail_out = tail;
-  return k;
+  return -1;
 }
 
 // Multi-workgroup block one-sided Jacobi SVD for 2 * chi > 128 (bjacobi.hip): factors the nj

@@ -284,6 +284,27 @@ def overlap_zero_batch(states):
     return out[0::2] + 1j * out[1::2]
 
 
+def z_all_batch(states):
+    """<Z_i> of every state (rows), one set of launches (aqc_mps_z_all_batch)."""
+    if not states:
+        return np.zeros((0, 0))
+    n = states[0].n
+    out = np.zeros(len(states) * n)
+    _lib.check(_lib.lib().aqc_mps_z_all_batch(_handles(states), len(states), _lib.ptr(out)))
+    return out.reshape(len(states), n)
+
+
+def amps_hw1_batch(states):
+    """Amplitudes <e_i|psi> of every state (rows, complex), one set of launches
+    (aqc_mps_amps_hw1_batch)."""
+    if not states:
+        return np.zeros((0, 0), dtype=complex)
+    n = states[0].n
+    out = np.zeros(2 * len(states) * n)
+    _lib.check(_lib.lib().aqc_mps_amps_hw1_batch(_handles(states), len(states), _lib.ptr(out)))
+    return (out[0::2] + 1j * out[1::2]).reshape(len(states), n)
+
+
 def pair_grads_batch(states, svec, pairs, u0, gens, degs, out=None):
     """Per-state gradient norms for every pair; ``out`` may be a device pointer (int): then the call
     returns once the work is queued and is ordered both ways against torch's current stream -- the

@@ -92,29 +92,33 @@ def _batched_isl(original):
 # The reference's CostMinimiser asks ``self.cost_finder()`` (the compiler's evaluate_cost,
 # approximate_compiler.py:150-158, 514-527) once per candidate: 1 + 3 x 2 = 7 evaluations per gate in
 # replace_with_best_1q_gate, 3 (2 with the identity cost given) in find_best_angle, each a full
-# replay.  With this package's backends and the global, unsoftened cost, the wrappers below take all
+# replay.  With this package's backends, the wrappers below take all
 # candidates of a gate from one batched evaluation of utils/cached_rotations.py (statevector: a 2x2
 # transition matrix of the prefix and the undone suffix; MPS: the cached prefix MPS and all
 # candidates replayed through the suffix in one lock-step batch), and then run the reference's own
 # code on those numbers: its SUPPORTED_1Q_GATES order, its minimum_of_sinusoidal, its strict `<`,
 # its co.replace_1q_gate edits of full_circuit, and cost_evaluation_counter advanced by the number
 # of evaluate_cost calls it would have made.  An evaluator lives for one _reduce_cost sweep (the
-# gates are visited in index order; only the gate just optimised changes between them).  Anything
-# else (local or softened cost, other backends, NLopt / SciPy paths) runs the reference's code.
+# gates are visited in index order; only the gate just optimised changes between them).  The local
+# and softened costs batch the same way (every candidate's <Z_i> or HW-1 amplitudes in one set of
+# launches; on the statevector backend the local cost from a cached prefix state).  Anything else
+# (the softened cost on SV, other backends, NLopt / SciPy paths) runs the reference's code.
 
 def _rotations_evaluator(minimiser):
-    from .utils.cached_rotations import MPSPrefixBatch, SVTransitionSweep
+    from .utils.cached_rotations import MPSPrefixBatch, SVPrefixBatch, SVTransitionSweep, _cost_kind
 
     compiler = getattr(minimiser.cost_finder, "__self__", None)
     if compiler is None or getattr(compiler, "full_circuit", None) is not minimiser.full_circuit:
         return None
-    if getattr(compiler, "optimise_local_cost", False) or getattr(compiler, "soften_global_cost", False):
-        return None
+    kind = _cost_kind(compiler)  # the branch evaluate_cost takes (approximate_compiler.py:514-527)
     backend = getattr(compiler, "backend", None)
     if isinstance(backend, HipMPSBackend):
-        return MPSPrefixBatch(compiler)
+        return MPSPrefixBatch(compiler, kind)
     if isinstance(backend, HipSVBackend):
-        return SVTransitionSweep(compiler)
+        if kind == "global":
+            return SVTransitionSweep(compiler)
+        if kind == "local":
+            return SVPrefixBatch(compiler)
     return None
 
 

@@ -28,7 +28,13 @@ candidates differ in one single-qubit gate, so:
   reference does, so only the prefix is cached (the MPS after the gates before the varied
   one, which is what every replay computes first) and the candidates replay the suffix together
   in lock-step batched launches (aqc_mps_copy_batch / apply_batch / overlap_zero_batch).
-* Local cost or softened global cost: no shortcut; the minimiser uses the generic path.
+* MPS, local cost (0.5 (1 - mean <Z_i>), aer_mps_backend.py:72-74, 80-86) or softened global cost
+  (1 - |<0|psi>|^2 - alpha sum_i |<e_i|psi>|^2, :49-70): the same prefix batch, then every
+  candidate's <Z_i> (aqc_mps_z_all_batch) or HW-1 amplitudes (aqc_mps_amps_hw1_batch) in one set of
+  launches.
+* Statevector, local cost (aer_sv_backend.py:32-35, 49-59): no transition shortcut (every <Z_i> of
+  every candidate); the prefix state is cached and the candidates replay the suffix from it.
+  The softened cost raises on the statevector backend, as in the reference (generic path).
 
 The compiler's ``cost_evaluation_counter`` advances by the number of evaluations the reference
 would have made, so histories and logs stay comparable.
@@ -38,7 +44,7 @@ import numpy as np
 from .. import gates as G
 from .._lib import ops_array
 from ..circuit import device_ops
-from ..device import DeviceSV, apply_batch, copy_batch, overlap_zero_batch
+from ..device import DeviceSV, amps_hw1_batch, apply_batch, copy_batch, overlap_zero_batch, z_all_batch
 
 
 class _View:
@@ -107,13 +113,31 @@ class SVTransitionSweep(_SweepBase):
         return [float(1.0 - abs(np.sum(m * t)) ** 2) for m in mats]
 
 
-class MPSPrefixBatch(_SweepBase):
-    """Prefix MPS cached across candidates and gates; candidates replay the suffix in one batch."""
+def _cost_kind(compiler):
+    if getattr(compiler, "optimise_local_cost", False):
+        return "local"
+    if getattr(compiler, "soften_global_cost", False):
+        return "soft"
+    return "global"
 
-    def __init__(self, compiler):
+
+def _soften_alpha(compiler):
+    """aer_mps_backend.py:63-66: alpha = |C_prev - sufficient_cost|, C_prev the last global cost of
+    the history (1 when empty) -- read per evaluation, as the reference does."""
+    hist = compiler.global_cost_history
+    previous_cost = hist[-1] if len(hist) > 0 else 1
+    return abs(previous_cost - compiler.adapt_config.sufficient_cost)
+
+
+class MPSPrefixBatch(_SweepBase):
+    """Prefix MPS cached across candidates and gates; candidates replay the suffix in one batch,
+    then the compiler's cost (global, softened global or local) of every candidate together."""
+
+    def __init__(self, compiler, kind="global"):
         super().__init__(compiler)
         self.backend = compiler.backend
         self.phi = None
+        self.kind = kind
 
     def goto(self, index):
         circ = self.compiler.full_circuit
@@ -134,9 +158,51 @@ class MPSPrefixBatch(_SweepBase):
         states = self.backend.scratch_states(len(mats))
         copy_batch(states, [self.phi] * len(mats))
         lists = [np.concatenate([ops_array([(m, (q,))]), suffix]) for m in mats]
-        apply_batch(states, lists)
+        apply_batch(states, lists, sort=True)
+        if self.kind == "local":
+            z = z_all_batch(states)
+            return [float(0.5 * (1 - np.mean(row))) for row in z]
         ov = overlap_zero_batch(states)
-        return [float(1.0 - abs(v) ** 2) for v in ov]
+        costs = [float(1.0 - abs(v) ** 2) for v in ov]
+        if self.kind == "soft":
+            alpha = _soften_alpha(self.compiler)
+            amps = amps_hw1_batch(states)
+            costs = [c - alpha * float(np.sum(np.abs(a) ** 2)) for c, a in zip(costs, amps)]
+        return costs
+
+
+class SVPrefixBatch(_SweepBase):
+    """Statevector, local cost: the prefix state cached across candidates and gates (advanced gate
+    by gate as the sweep moves); each candidate replays its gate and the suffix from it, then
+    <Z_i> of every qubit (aqc_sv_z_all)."""
+
+    def __init__(self, compiler):
+        super().__init__(compiler)
+        n = compiler.full_circuit.num_qubits
+        self.phi = DeviceSV(n)
+        self.cand = []
+
+    def goto(self, index):
+        circ = self.compiler.full_circuit
+        if self.pos is None or index < self.pos:
+            self.phi.reset()
+            self.phi.apply(_ops(circ, 0, index))
+        elif index > self.pos:
+            self.phi.apply(_ops(circ, self.pos, index))
+        self.pos = index
+
+    def costs(self, index, mats):
+        circ = self.compiler.full_circuit
+        q = _ops_qubit(circ, index)
+        suffix = ops_array(_ops(circ, index + 1, len(circ.data)))
+        while len(self.cand) < len(mats):
+            self.cand.append(DeviceSV(self.phi.n))
+        out = []
+        for m, st in zip(mats, self.cand):
+            st.copy_from(self.phi)
+            st.apply(np.concatenate([ops_array([(m, (q,))]), suffix]))
+            out.append(float(0.5 * (1 - np.mean(st.z_all()))))
+        return out
 
 
 def make_evaluator(compiler):
@@ -144,13 +210,15 @@ def make_evaluator(compiler):
     from ..backends.aer_mps_backend import AerMPSBackend
     from ..backends.aer_sv_backend import AerSVBackend
 
-    if getattr(compiler, "optimise_local_cost", False) or getattr(compiler, "soften_global_cost", False):
-        return None
+    kind = _cost_kind(compiler)
     if isinstance(compiler.backend, AerMPSBackend):
-        return MPSPrefixBatch(compiler)
+        return MPSPrefixBatch(compiler, kind)
     if isinstance(compiler.backend, AerSVBackend):
-        return SVTransitionSweep(compiler)
-    return None
+        if kind == "global":
+            return SVTransitionSweep(compiler)
+        if kind == "local":
+            return SVPrefixBatch(compiler)
+    return None  # (the softened cost on the statevector backend raises, as the reference does)
 
 
 def rotation(name, theta):

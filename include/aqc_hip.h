@@ -145,6 +145,14 @@ int aqc_mps_dot(aqc_mps_t a, aqc_mps_t b, double* re, double* im);
 int aqc_mps_z_all(aqc_mps_t h, double* out);
 /* extract_amplitude(psi, 2**i) for all i (aer_mps_backend.py:88-93), out[2n]. */
 int aqc_mps_amps_hw1(aqc_mps_t h, double* out);
+/* Batched forms for many states of the same n (and, for z_all, the same capacity): one set of
+   launches for every state -- the softened global cost (aer_mps_backend.py:58-70) and the local cost
+   (:72-74, 80-86) of a Rotoselect gate's candidates (cost_minimiser.py:318-368).  out: nstates x n
+   doubles (<Z_i>) or nstates x 2n (complex amplitudes).  z_all_batch contracts the left / right
+   environments as matrix products (the ISL RDM machinery) instead of aqc_mps_z_all's per-site
+   chains; both are full contractions (no canonical form assumed). */
+int aqc_mps_z_all_batch(aqc_mps_t* hs, int nstates, double* out);
+int aqc_mps_amps_hw1_batch(aqc_mps_t* hs, int nstates, double* out);
 
 /* ---- candidate sweep: replaces gradients.py:23-124 ------------------------------ */
 /* For every pair (pairs[2p], pairs[2p+1]) = (control, target):

@@ -35,8 +35,10 @@ int aqc_mps_set_svd_path(int gram, int debug_max_chi);
    unused, 0). */
 int aqc_svd_gram_ticks(double* out);
 /* Gram-path counters since the last call (then reset): out[0] two-site SVDs that tried the Gram
-   path, out[1] taken, out[2] declined by shape (K > 64, 2 chi != 128), out[3] declined at the
-   eigenvalue floor (lambda_K <= 1e-9 lambda_1; the register Jacobi ran instead).  out[4]. */
+   path, out[1] taken, out[2] declined by shape (2 chi != 128), out[3] declined at the
+   eigenvalue floor (lambda_K <= 1e-9 lambda_1; the register Jacobi ran instead) or with a
+   reduce_zeros decision the eigenvalues' error bars leave open; K follows reduce_zeros on the
+   eigenvalues (aqc::gram_keep, up to the whole side).  out[4]. */
 int aqc_svd_gram_stats(double* out);
 /* Block Jacobi pair visits (2 chi > 128), shader-clock ticks summed over workgroups since the
  * last call: out[0] Gram, out[1] inner Jacobi sweep, out[2] A V, out[3] visits.  Resets. */
@@ -47,6 +49,9 @@ int aqc_bj_ticks(double* out);
    Gram path, out[1] taken, out[2] declined (Gram path off for the job, or 2 chi < 4), out[3]
    declined at the eigenvalue floor (lambda_K <= 1e-9 lambda_1), out[4] exchange timeouts (the
    tridiagonalisation's workgroups did not all run together); declined jobs ran the block Jacobi.
+   out[3] also counts kept-count decisions that the eigenvalues' error bars leave open (the kept
+   count follows reduce_zeros on them: aqc::gram_keep).  out[5] rank-deficient decisions that needed
+   the certificate ||X - X V V^H||_F^2 < CHOP / 2, out[6] certified, out[7] not (declined).  out[8].
    The environment variable AQC_BIG_GRAM=0 selects the block Jacobi alone. */
 int aqc_svd_gram_big_stats(double* out);
 /* Diagnostics of the same path: shader-clock ticks summed over calls (then reset): out[0..4] the

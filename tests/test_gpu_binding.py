@@ -327,6 +327,159 @@ def test_reference_rotoselect_batched_mps(rotoselect):
     assert t_b < runs["per_candidate"][3]
 
 
+def _oracle_cost_fn(n, aer, chi, kind, alpha):
+    """The oracle's restatement of the MPS backend's costs (aer_mps_backend.py:49-86): global,
+    softened global (1 - |<0|psi>|^2 - alpha sum_i |<e_i|psi>|^2) or local (0.5 (1 - mean <Z_i>))."""
+    from oracle import mps as M
+
+    base = M.MPS.from_aer(aer)
+
+    def cost_fn(o):
+        st = M.run_circuit(n, [(x[0], x[1], tuple(x[2])) for x in o], 1e-16, chi, mps=base)
+        pre = st.preprocessed()
+        if kind == "local":
+            return 0.5 * (1 - np.mean([M.mps_expectation_z(pre, q) for q in range(n)]))
+        g = 1.0 - abs(M.mps_dot(pre, M.zero_mps(n))) ** 2
+        if kind == "soft":
+            g -= alpha * sum(abs(M.extract_amplitude(pre, 2 ** i)) ** 2 for i in range(n))
+        return g
+
+    return cost_fn
+
+
+@pytest.mark.parametrize("kind", ["local", "soft"])
+def test_reference_rotoselect_batched_mps_local_and_softened(kind):
+    """the local cost (optimise_local_cost) and the softened global cost
+    (soften_global_cost) through the reference's own CostMinimiser after install(): every gate's 7
+    Rotoselect candidates from one batch (cached prefix MPS, the candidates replayed through the
+    suffix together, then every candidate's <Z_i> -- aqc_mps_z_all_batch -- or HW-1 amplitudes --
+    aqc_mps_amps_hw1_batch -- in one set of launches).  Against the oracle's call sequence
+    (cost_minimiser.py:267-368 restated, oracle/adapt_host.py) with the oracle's costs: gate kinds,
+    resolved angles, final cost 1e-6, the reference's evaluation count; against the reference's
+    per-candidate path on the same device backend (1e-9).  Per-gate latency bounded at 1.5x the
+    global-cost batch of the same layer."""
+    import time
+    from types import SimpleNamespace
+
+    import bench
+    from adaptaqc_amd import reference_binding as rb
+    from adaptaqc_amd.backends import AerMPSBackend, mps_sim_with_args
+    from adaptaqc_amd.circuit import QuantumCircuit
+    from oracle import adapt_host as AH
+
+    n, chi = 50, 64
+    rng = np.random.default_rng(78)
+    aer = bench.near_product_mps(n, chi, 13)
+    full = QuantumCircuit(n)
+    full.set_matrix_product_state(aer)
+    _thin_layer_ir(full, [(20, 21)], rng)
+    history, sufficient = [0.31], 1e-2
+    alpha = abs(history[-1] - sufficient)
+    ops = []
+    for ins in full.data[1:]:
+        op = ins.operation
+        ops.append([op.name, tuple(ins.qubits), [float(p) for p in op.params], op.label])
+    cost_fn = _oracle_cost_fn(n, aer, chi, kind, alpha)
+    log, seen = [], []
+
+    def rec(o):
+        c = cost_fn(o)
+        seen.append(c)
+        return c
+
+    want_cost = AH.reduce_cost(ops, rec, True, (0, len(ops)), log)
+    amps = _amplitudes(ops, seen, True)
+    n_rot = sum(1 for ins in full.data[1:] if ins.operation.name == "rz")
+    be = AerMPSBackend(mps_sim_with_args(max_chi=chi))
+    with installed_fake_reference() as mods:
+        rb.install(import_missing=False)
+        CM = mods["adaptaqc.utils.cost_minimiser"].CostMinimiser
+        AC = mods["adaptaqc.compilers.approximate_compiler"].ApproximateCompiler
+        runs = {}
+        for mode in ("global", "per_candidate", "batched", "global", "batched"):
+            q = from_ir(full)
+            comp = AC(q, be)
+            comp.optimise_local_cost = kind == "local" and mode != "global"
+            comp.soften_global_cost = kind == "soft" and mode != "global"
+            comp.global_cost_history = list(history)
+            comp.adapt_config = SimpleNamespace(sufficient_cost=sufficient)
+            cmz = CM(comp.evaluate_cost, lambda q=q: (1, len(q.data)), q)
+            comp.evaluate_cost()  # the cached payload on the device
+            comp.cost_evaluation_counter = 0
+            t0 = time.perf_counter()
+            if mode == "per_candidate":  # the reference's own per-candidate code on the same backend
+                cost = CM._reduce_cost.__wrapped__(cmz, True, None)
+            else:
+                cost = cmz._reduce_cost(True, None)
+            runs[mode] = (q, cost, comp.cost_evaluation_counter, time.perf_counter() - t0)
+        q, cost, count, t_b = runs["batched"]
+        assert count == 7 * n_rot == len(log)
+        assert runs["per_candidate"][2] == count
+        assert abs(cost - want_cost) < 1e-6, (cost, want_cost)
+        assert abs(cost - runs["per_candidate"][1]) < 1e-9
+        r = 0
+        for k, ins in enumerate(q.data[1:]):
+            w = ops[k]
+            assert ins.operation.name == w[0], (k, ins.operation.name, w[0])
+            if ins.operation.params:
+                qp = runs["per_candidate"][0].data[1 + k].operation
+                assert _angle_gap(float(ins.operation.params[0]), float(qp.params[0])) < 1e-9
+                if amps[r] > 1e-7:
+                    assert _angle_gap(float(ins.operation.params[0]), w[2][0]) < 1e-6 / amps[r] + 1e-6
+                r += 1
+    t_g = runs["global"][3]
+    print(f"\nper gate ({kind}): batched {1e3 * t_b / n_rot:.2f} ms, global-cost batch {1e3 * t_g / n_rot:.2f} ms, "
+          f"per-candidate {1e3 * runs['per_candidate'][3] / n_rot:.2f} ms")
+    assert t_b <= 1.5 * t_g + 1e-3 * n_rot
+    assert t_b < runs["per_candidate"][3]
+
+
+def test_reference_rotoselect_batched_sv_local_cost():
+    """The local cost on the statevector backend through the reference's CostMinimiser: the cached
+    prefix state, each candidate's gate and suffix replayed from it, every <Z_i>; against the
+    oracle's call sequence with exact SV local costs (1e-10) and the reference's evaluation count."""
+    import os
+
+    from adaptaqc_amd import reference_binding as rb
+    from adaptaqc_amd.backends import AerSVBackend
+    from oracle import adapt_host as AH
+    from oracle import sv as osv
+
+    os.environ.setdefault("QISKIT_IN_PARALLEL", "FALSE")
+    n = 10
+    full = _random_ir(n, 6, layers=3)
+    start = len(full.data)
+    _thin_layer_ir(full, [(3, 4), (6, 2)], np.random.default_rng(6))
+    ops = []
+    for ins in full.data:
+        op = ins.operation
+        ops.append([op.name, tuple(ins.qubits), [float(p) for p in op.params], op.label])
+
+    def cost_fn(o):
+        psi = osv.simulate(n, [(x[0], x[1], tuple(x[2])) for x in o])
+        return 0.5 * (1 - np.mean(osv.z_expectations(psi, n)))
+
+    log = []
+    want = AH.reduce_cost(ops, cost_fn, True, (start, len(ops)), log)
+    with installed_fake_reference() as mods:
+        rb.install(import_missing=False)
+        CM = mods["adaptaqc.utils.cost_minimiser"].CostMinimiser
+        AC = mods["adaptaqc.compilers.approximate_compiler"].ApproximateCompiler
+        q = from_ir(full)
+        comp = AC(q, AerSVBackend())
+        comp.optimise_local_cost = True
+        cmz = CM(comp.evaluate_cost, lambda: (start, len(q.data)), q)
+        assert cmz._reduce_cost.__name__ == "_reduce_cost"
+        cost = cmz._reduce_cost(True, None)
+        assert comp.cost_evaluation_counter == len(log)
+        assert abs(cost - want) < 1e-10
+        for k in range(start, len(q.data)):
+            op = q.data[k].operation
+            assert op.name == ops[k][0]
+            if op.params:
+                assert _angle_gap(float(op.params[0]), ops[k][2][0]) < 1e-8
+
+
 def test_reference_rotoselect_batched_sv():
     """The same drop-in on the statevector backend (the transition-matrix evaluator): a 10-qubit
     random state plus one thinly-dressed layer, Rotoselect through the reference's CostMinimiser

@@ -150,11 +150,13 @@ def _insert_ansatz(comp, seed):
         co.add_gate(comp.full_circuit, g, pos + k, qs)
 
 
-@pytest.mark.parametrize("backend_kind", ["sv", "mps"])
+@pytest.mark.parametrize("backend_kind,cost", [("sv", "global"), ("mps", "global"), ("sv", "local"), ("mps", "local"),
+                                               ("mps", "soft")])
 @pytest.mark.parametrize("rotoselect", [False, True])
-def test_cached_rotations_match_generic(backend_kind, rotoselect):
+def test_cached_rotations_match_generic(backend_kind, cost, rotoselect):
     """Cached candidates (utils/cached_rotations.py) reproduce the reference's one-simulation-
-    per-candidate sweep: same gates, angles (1e-9), costs (1e-10) and evaluation count."""
+    per-candidate sweep: same gates, angles (1e-9), costs (1e-10) and evaluation count -- for the
+    global cost, the local cost (optimise_local_cost) and the softened global cost (MPS)."""
     from adaptaqc_amd.backends import AerMPSBackend, AerSVBackend
     from adaptaqc_amd.compilers import AdaptCompiler
 
@@ -162,6 +164,10 @@ def test_cached_rotations_match_generic(backend_kind, rotoselect):
     for cached in (False, True):
         backend = AerSVBackend() if backend_kind == "sv" else AerMPSBackend()
         comp = AdaptCompiler(to_circuit(4, _random_state_circuit(4, 3, 21)), backend=backend)
+        comp.optimise_local_cost = cost == "local"
+        comp.soften_global_cost = cost == "soft"
+        if cost == "soft":
+            comp.global_cost_history.append(0.4)
         comp.use_cached_rotations = cached
         _insert_ansatz(comp, 5)
         rng = comp.variational_circuit_range()

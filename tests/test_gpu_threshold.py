@@ -109,3 +109,48 @@ def test_threshold_multi_workgroup_vs_oracle(max_chi, decay, dists):
     layers = [(si, _layer(n, 9, d, 55 + 10 * si + d)) for si in range(2) for d in dists]
     _, big = _run_batch(n, cap, max_chi, states, layers, batch=True)
     assert big["calls"] > 0
+
+
+def _deficient_state(seed, tiny=None):
+    """16 qubits with bonds ... 64 128 | 64 | 128 64 ...: the two-site block of sites (7, 8) is 256 x 256
+    but has rank <= 2 x 64 after a CNOT -- 128 numerically zero singular values, which the Gram form
+    cannot tell from 1e-16 (the CHOP).  tiny: the last 8 Schmidt values of the middle bond scaled
+    by tiny (1e-4: sigma^2 from 7e-14 down to 8e-16 -- kept by the reference, inside the Gram form's
+    noise band)."""
+    rng = np.random.default_rng(seed)
+    dims = [1, 2, 4, 8, 16, 32, 64, 128, 64, 128, 64, 32, 16, 8, 4, 2, 1]
+    A = [rng.standard_normal((2, dims[i], dims[i + 1])) + 1j * rng.standard_normal((2, dims[i], dims[i + 1]))
+         for i in range(16)]
+    if tiny is not None:
+        A[7][:, :, -8:] *= tiny
+    return bench.vidal_from_tensors(A)
+
+
+@pytest.mark.parametrize("tiny", [None, 1e-4], ids=["exact-zeros", "tiny-values"])
+def test_rank_deficient_two_site_block_certificate(tiny):
+    """The reference's default truncation (threshold 1e-16, max_chi None) on a 256 x 256 two-site
+    block of rank 128: the multi-workgroup Gram path keeps the 128 values clear of the CHOP's band,
+    assumes the other 128 chopped, and certifies it with ||X - X V V^H||_F^2 < CHOP / 2 computed from
+    X (gram_big.hip k_gb_cert).  With true values of sigma^2 ~ 1e-14 among the dropped ones the
+    certificate fails and the block Jacobi decides.  Exact bond dimensions and fidelity 1e-6 against
+    the oracle either way."""
+    n = 16
+    aer = _deficient_state(41, tiny)
+    rng = np.random.default_rng(5)
+    ops = [("rz", (7,), (rng.uniform(-3, 3),)), ("rz", (8,), (rng.uniform(-3, 3),)), ("cx", (7, 8), ()),
+           ("ry", (7,), (rng.uniform(-3, 3),)), ("ry", (8,), (rng.uniform(-3, 3),))]
+    _, big = _run_batch_thr(n, 128, None, [aer], [(0, ops)], 1e-16)
+    assert big["certificates"] >= 1, big
+    if tiny is None:
+        assert big["certified"] >= 1 and big["taken"] >= 1, big
+    else:
+        assert big["declined_certificate"] >= 1, big
+
+
+def _run_batch_thr(n, cap, max_chi, states, layers, thr):
+    global THR
+    old, THR = THR, thr
+    try:
+        return _run_batch(n, cap, max_chi, states, layers, batch=False)
+    finally:
+        THR = old
