@@ -167,15 +167,15 @@ def test_cached_rotations_match_generic(backend_kind, cost, rotoselect):
         comp.optimise_local_cost = cost == "local"
         comp.soften_global_cost = cost == "soft"
         if cost == "soft":
-            comp.global_cost_history.append(0.4)
+            comp.global_cost_history = [0.4]  # (set by compile(); the softening reads its last entry)
         comp.use_cached_rotations = cached
         _insert_ansatz(comp, 5)
         rng = comp.variational_circuit_range()
         assert rng[1] - rng[0] > 10
         start_count = comp.cost_evaluation_counter
-        cost = comp.minimizer._reduce_cost(rotoselect, rng)
+        reduced = comp.minimizer._reduce_cost(rotoselect, rng)
         gates = [(i.operation.name, tuple(i.qubits), tuple(i.operation.params)) for i in comp.full_circuit.data]
-        results.append((cost, gates, comp.cost_evaluation_counter - start_count, comp.evaluate_cost()))
+        results.append((reduced, gates, comp.cost_evaluation_counter - start_count, comp.evaluate_cost()))
     (c0, g0, n0, e0), (c1, g1, n1, e1) = results
     assert n0 == n1
     assert abs(c0 - c1) < 1e-10 and abs(e0 - e1) < 1e-10

@@ -102,10 +102,12 @@ def test_gram_big_equals_block_jacobi():
     assert abs(abs(M.mps_dot(pg, pb)) / np.sqrt(abs(M.mps_dot(pg, pg)) * abs(M.mps_dot(pb, pb))) - 1.0) < 1e-6
 
 
-def test_gram_big_rank_deficient_declines_to_block_jacobi():
+def test_gram_big_rank_deficient_certified():
     """A 2 chi = 256 update whose middle bond keeps only 4 non-zero Schmidt values (the rest set to
-    zero): theta' has rank <= 16, lambda_K sits at the noise floor, the Gram path declines and the
-    block Jacobi's result matches the oracle on the same input."""
+    zero): theta' has rank <= 16 and the eigenvalues past it sit at the noise floor, inside CHOP's
+    error band.  The kept count assumes them chopped and k_gb_cert proves it (||X - X V V^H||_F^2 <
+    CHOP / 2), so the Gram path keeps the update (round 4 declined it to the block Jacobi, which the
+    exchange-timeout test below still covers); the result matches the oracle on the same input."""
     from adaptaqc_amd import _lib
     from adaptaqc_amd.circuit import device_ops
     from adaptaqc_amd.device import DeviceMPS
@@ -124,7 +126,8 @@ def test_gram_big_rank_deficient_declines_to_block_jacobi():
     d.load_aer(aer)
     d.apply(device_ops(to_circuit(n, ops)))
     st = _lib.gram_big_stats()
-    assert st["declined_floor"] == 1 and st["taken"] == 0 and st["timeouts"] == 0, st
+    assert st["taken"] == 1 and st["certificates"] == 1 and st["certified"] == 1, st
+    assert st["declined_floor"] == 0 and st["timeouts"] == 0, st
     ref = M.run_circuit(n, ops, 1e-16, None, mps=M.MPS.from_aer(aer))
     pre_ref = ref.preprocessed()
     np.testing.assert_array_equal(d.dims(), [1] + [x.shape[2] for x in pre_ref])
