@@ -99,6 +99,13 @@ __device__ __forceinline__ double uniform_d(double v) {
   return __hiloint2double(hi, lo);
 }
 
+// lane l's double broadcast to the wave (readlane of both halves; l uniform)
+__device__ __forceinline__ double bcast_d(double v, int l) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
+  return __hiloint2double(hi, lo);
+}
+
 // this lane's index in the wave from the lane counter (mbcnt), recomputed where it is called
 // (the empty asm keeps it from being hoisted, and so from being spilled and reloaded)
 __device__ __forceinline__ int fresh_lane() {
@@ -791,38 +798,29 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
   asm volatile("" : "+s"(lb));
   lcplx* pvb = lb;           // [2][128] p   (0 at and above row k)
   lcplx* vbb = lb + 256;     // [2][128] v   (0 at and above row k, 1 at k + 1)
-  lcplx* zvb = lb + 512;     // [2][128] z   (0 at and above row k + 1)
+  lcplx* xvb = lb + 512;     // [2][128] x = z - s v, column k + 1 of G^(k+1) below row k + 1 (else 0)
   lcplx* accp = lb + 768;    // [8][128] the column pass's partial products g x, per lane of a row
   lcplx* gk1b = lb + 1792;   // [128] G^(k)[r][k+1]
   lcplx* tauS = lb + 1921;   // reflector k's tau at tauS[k]; tauS[-1] = 0 ("reflector -1")
   ldbl* eS = (ldbl*)(lb + 2050);  // [128] beta_k = e_k
   ldbl* dS = (ldbl*)(lb + 2114);  // [128] d_k
-  lcplx* ktp = lb + 2178;    // [2] p^H v partials of the last p / v pass (rows 0-63, 64-127)
-  lcplx* scal = lb + 2180;   // reflector k's 1 / (alpha - beta), tau / (alpha - beta); s of k - 1
-  // "reflector -1": none, and column 0 of G as z (s = 0)
+  lcplx* a2b = lb + 2178;    // [2] reflector k's a2 = -tau (p^H v) / 2, by phase parity
+  lcplx* scal = lb + 2180;   // reflector k's 1 / (alpha - beta), tau / (alpha - beta)
+  lcplx* ktp = lb + 2183;    // [2] p^H v partials of phase B's two waves (rows 0-63, 64-127)
+  volatile __attribute__((address_space(3))) int* hsf =
+      (volatile __attribute__((address_space(3))) int*)(lb + 2185);  // [2] phase B's hand-off flags: k + 1
+  // "reflector -1": none, and column 0 of G as x (s = 0)
   if (tid == 0) {
     tauS[-1] = aqc::cmk(0, 0);
-    ktp[0] = ktp[1] = aqc::cmk(0, 0);
+    a2b[1] = aqc::cmk(0, 0);
+    hsf[0] = hsf[1] = 0;
   }
   if (q == 0) {
     pvb[128 + r] = aqc::cmk(0, 0);
     vbb[128 + r] = aqc::cmk(0, 0);
-    zvb[128 + r] = (r > 0 && r < C) ? g[0] : aqc::cmk(0, 0);
+    xvb[128 + r] = (r > 0 && r < C) ? g[0] : aqc::cmk(0, 0);
   }
   __syncthreads();
-  // reflector k - 1's a2 and s from buffer bp, per wave
-  auto prev_scalars = [&](int k, int bp, cplx& a2, cplx& s) {
-    // p^H v from the two partial sums the p / v pass left (rows 0-63, 64-127)
-    const cplx kt = aqc::cadd(ktp[0], ktp[1]);
-    const cplx tau_prev = tauS[k - 1];
-    a2 = aqc::cscale(aqc::cmul(tau_prev, kt), -0.5);
-    const cplx pk = pvb[bp * 128 + k];
-    s = aqc::cmk(pk.x + 2.0 * a2.x, -pk.y);
-    // wave-uniform (LDS broadcasts): held in SGPRs, four VGPRs fewer in the column pass
-    a2.x = uniform_d(a2.x);
-    s.x = uniform_d(s.x);
-    s.y = uniform_d(s.y);
-  };
   for (int k = 0; k < C - 1; ++k) {
     const int b = k & 1, bp = b ^ 1;
     // q and r laundered through an empty asm each step: otherwise the compiler hoists the 16
@@ -837,20 +835,18 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
     // zlarfg scalars, handed to the other waves through the LDS behind a second barrier.  (With
     // every wave forming them redundantly, four waves per SIMD issued the whole scalar chain: it
     // was 60% of this loop's time.)
-    cplx a2 = aqc::cmk(0, 0), s = aqc::cmk(0, 0);
-    if (wact || wave == 0) prev_scalars(k, bp, a2, s);
+    double a2x = 0.0;  // Re(a2) of reflector k - 1 (an LDS broadcast, held in an SGPR)
+    if (wact) a2x = uniform_d(a2b[bp].x);
     if (wave == 0) {
       __builtin_amdgcn_s_setprio(3);
-      // column k of G^(k) below the diagonal: x_r = z_r - s v_r (r > k); alpha = x_{k+1}
+      // column k of G^(k) below the diagonal: x_r (r > k, formed by phase B); alpha = x_{k+1}
       double xn2;
       {
-        const cplx z0 = zvb[bp * 128 + lane], z1 = zvb[bp * 128 + 64 + lane];
-        const cplx v0 = vbb[bp * 128 + lane], v1 = vbb[bp * 128 + 64 + lane];
-        const cplx x0 = aqc::cfma(aqc::cmk(-s.x, -s.y), v0, z0), x1 = aqc::cfma(aqc::cmk(-s.x, -s.y), v1, z1);
+        const cplx x0 = xvb[bp * 128 + lane], x1 = xvb[bp * 128 + 64 + lane];
         const double n0 = lane > k + 1 ? aqc::cnorm2(x0) : 0.0, n1 = lane + 64 > k + 1 ? aqc::cnorm2(x1) : 0.0;
         xn2 = wave_sum_dpp(n0 + n1);
       }
-      const cplx alpha = aqc::cfma(aqc::cmk(-s.x, -s.y), vbb[bp * 128 + k + 1], zvb[bp * 128 + k + 1]);
+      const cplx alpha = xvb[bp * 128 + k + 1];
       // reflector k's scalars (zlarfg); rsq / rcp seeds with Newton steps (full precision)
       // instead of the IEEE sqrt / divide sequences
       const double x2 = fma(alpha.x, alpha.x, fma(alpha.y, alpha.y, xn2));
@@ -869,7 +865,6 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
         eS[k] = beta;
         scal[0] = scl;
         scal[1] = aqc::cmul(tau, scl);
-        scal[2] = s;
       }
       __builtin_amdgcn_s_setprio(0);
     }
@@ -879,36 +874,43 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
       cplx acc = aqc::cmk(0, 0);
       const cplx vr = vbb[bp * 128 + r];
       const cplx pr = pvb[bp * 128 + r];
-      const double a2r2 = 2.0 * a2.x;
+      const double a2r2 = 2.0 * a2x;
       const cplx wr = aqc::cmk(fma(a2r2, vr.x, pr.x), fma(a2r2, vr.y, pr.y));
-      const double nvx = -vr.x, nvy = -vr.y, nwx = -wr.x, nwy = -wr.y, nsx = -s.x, nsy = -s.y;
-      // one pass: g -= v_r conj(p_c) + w_r conj(v_c) (reflector k - 1), acc += g x_c (reflector k)
-      auto col = [&](int i, const cplx& vc, const cplx& pc, const cplx& zc) {
+      const double nvx = -vr.x, nvy = -vr.y, nwx = -wr.x, nwy = -wr.y;
+      // one pass: g -= v_r conj(p_c) + w_r conj(v_c) (reflector k - 1), acc += g x_c (reflector k):
+      // 12 FMAs per element (x_c comes formed from phase B, not re-formed from z_c - s v_c by each
+      // of the eight row lanes holding column c: 16 until round 5)
+      auto col = [&](int i, const cplx& vc, const cplx& pc, const cplx& xc) {
         g[i].x = fma(nvx, pc.x, fma(nvy, pc.y, fma(nwx, vc.x, fma(nwy, vc.y, g[i].x))));
         g[i].y = fma(nvy, pc.x, fma(vr.x, pc.y, fma(nwy, vc.x, fma(wr.x, vc.y, g[i].y))));
-        const cplx xc = aqc::cmk(fma(nsx, vc.x, fma(nsy, -vc.y, zc.x)), fma(nsx, vc.y, fma(nsy, vc.x, zc.y)));
         acc = aqc::cfma(g[i], xc, acc);
       };
       // Rolling prefetch: column i + 1's v, p, z are requested before column i is computed, so
       // each LDS round trip hides behind one column's 16 FMAs (loaded and consumed one column at a
       // time, every column waited out a full LDS latency: ~4 K of a step's ~4.6 K ticks).  The
-      // active columns start at group k / 32 (uniform); its first column is loaded up front.
-      const int gi0 = k >> 5;
+      // active columns start at group k / (8 GR) of GR column registers (uniform: every column q + 8 i
+      // of a lower group is below k, so v_c = p_c = z_c = 0 there and the pass would change nothing);
+      // its first column is loaded up front.  (Groups of four registers -- 32 columns -- until round 5.)
+#ifndef AQC_S3_GROUP
+#define AQC_S3_GROUP 2
+#endif
+      constexpr int GR = AQC_S3_GROUP;  // column registers per skip group
+      const int gi0 = k / (8 * GR);
       cplx cv, cp, cz;
       {
-        const int c = q + 32 * gi0;
-        cv = vbb[bp * 128 + c], cp = pvb[bp * 128 + c], cz = zvb[bp * 128 + c];
+        const int c = q + 8 * GR * gi0;
+        cv = vbb[bp * 128 + c], cp = pvb[bp * 128 + c], cz = xvb[bp * 128 + c];
       }
 #pragma unroll
-      for (int gi = 0; gi < 4; ++gi) {
+      for (int gi = 0; gi < 16 / GR; ++gi) {
         if (gi >= gi0) {  // uniform; v_c = p_c = z_c = 0 for c < k
 #pragma unroll
-          for (int ii = 0; ii < 4; ++ii) {
-            const int i = 4 * gi + ii;
+          for (int ii = 0; ii < GR; ++ii) {
+            const int i = GR * gi + ii;
             cplx nv = cv, np = cp, nz = cz;
             if (i + 1 < 16) {
               const int c = q + 8 * (i + 1);
-              nv = vbb[bp * 128 + c], np = pvb[bp * 128 + c], nz = zvb[bp * 128 + c];
+              nv = vbb[bp * 128 + c], np = pvb[bp * 128 + c], nz = xvb[bp * 128 + c];
             }
             __builtin_amdgcn_sched_barrier(0);
             col(i, cv, cp, cz);
@@ -916,12 +918,13 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
           }
         }
       }
-      // the product used x_k = -s (z_k = 0, v_k = 1) where reflector k has 0 (and x_{k+1} = alpha
-      // where it has alpha - beta: corrected in phase B): one entry in the lane holding column k
+      // (the product used x_{k+1} = alpha where reflector k has alpha - beta: corrected in phase B)
       // (k + 1) >> 3 == k >> 3 except every eighth column: the same register, so one pick
-      const cplx gk = pick16(g, k >> 3);
+      cplx gk = pick16(g, k >> 3);
+      // (materialised here: picked only under the d_k store below, it moved into that branch and
+      // the allocator spilled g's imaginary parts for the whole pass)
+      asm volatile("" : "+v"(gk.x), "+v"(gk.y));
       const cplx gk1 = ((k + 1) & 7) ? gk : pick16(g, (k + 1) >> 3);
-      if (q == (k & 7)) acc = aqc::cfma(s, gk, acc);
       if (q == (k & 7) && r == k) dS[k] = gk.x;  // G^(k)[k][k]
       // the row's eight partial products are in eight adjacent lanes of this wave: summed here
       // (DPP, VALU slack -- the pass is LDS-bound), so phase B reads one value per row
@@ -932,13 +935,19 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
     }
     __syncthreads();
     tick_step(t_b);
-    // Phase B: reflector k's p, v and z, one row per thread of waves 0 and 1 (the row's eight
-    // partial products summed from the LDS; every row, so finished rows get their zeros)
-    int rr = tid;
-    asm volatile("" : "+v"(rr));  // (laundered like q and r)
-    if (rr < 128) {
+    // Phase B, one row per thread of waves 0 and 1: reflector k's p and v (the row's eight partial
+    // products summed from the LDS; every row, so finished rows get their zeros); the two waves hand
+    // each other their halves of p^H v through the LDS (a flag per wave, no workgroup barrier), then
+    // each forms a2, s = conj(p_{k+1}) + 2 Re(a2) and its rows' x = z - s v with z_r = G^(k)[r][k+1]
+    // - p_r -- the next column pass's operand, formed once here instead of by each of the eight row
+    // lanes holding a column.  (All 128 rows in wave 0 alone, two per lane: phase B 131 K -> 226 K
+    // ticks, which ate the pass's gain.)
+    if (wave < 2) {
+      int rr = tid;
+      asm volatile("" : "+v"(rr));  // (laundered like q and r)
       const double beta = eS[k];
-      const cplx ts = scal[1], scl = scal[0], sk = scal[2], g1 = gk1b[rr];
+      const cplx ts = scal[1], scl = scal[0];
+      const cplx g1 = gk1b[rr];
       cplx sum = accp[rr];
       sum.x = fma(-beta, g1.x, sum.x);  // x_{k+1} = alpha where reflector k has alpha - beta
       sum.y = fma(-beta, g1.y, sum.y);
@@ -946,16 +955,28 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
       cplx p = aqc::cmul(ts, sum);
       if (!rowact) p = aqc::cmk(0, 0);
       // reflector k's v: 1 at k + 1, scl x_r below, 0 above
-      cplx v = aqc::cmul(aqc::cfma(aqc::cmk(-sk.x, -sk.y), vbb[bp * 128 + rr], zvb[bp * 128 + rr]), scl);
+      cplx v = aqc::cmul(xvb[bp * 128 + rr], scl);
       if (!below) v = aqc::cmk(rr == k + 1 ? 1.0 : 0.0, 0.0);
       pvb[b * 128 + rr] = p;
       vbb[b * 128 + rr] = v;
       if (rowact) aqc::stg(hh + (size_t)k * (2 * C - k - 1) / 2 + (rr - k - 1), v);  // GLOBAL, not FLAT
-      // this wave's share of p^H v for the next column's a2
+      // z_r parked in x's slot until s is known (nothing of the row stays live across the wait)
+      xvb[b * 128 + rr] = below ? aqc::csub(g1, p) : aqc::cmk(0, 0);
       const double ktx = wave_sum_dpp(fma(p.x, v.x, p.y * v.y)), kty = wave_sum_dpp(fma(p.x, v.y, -p.y * v.x));
       if (lane == 0) ktp[wave] = aqc::cmk(ktx, kty);
-      // z of reflector k: G^(k)[r][k+1] - p_r below row k + 1
-      zvb[b * 128 + rr] = below ? aqc::csub(g1, p) : aqc::cmk(0, 0);
+      // (the LDS serves one wave's requests in order: partial, then flag; the fence keeps the
+      // compiler from reordering the two stores and waits for both)
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      if (lane == 0) hsf[wave] = k + 1;
+      while (hsf[wave ^ 1] != k + 1) __builtin_amdgcn_s_sleep(1);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      const cplx a2 = aqc::cscale(aqc::cmul(tauS[k], aqc::cadd(ktp[0], ktp[1])), -0.5);  // (same order in both)
+      const cplx pk = pvb[b * 128 + k + 1];
+      const double sx = -(pk.x + 2.0 * a2.x), sy = pk.y;  // -s
+      int r2 = tid;
+      asm volatile("" : "+v"(r2));
+      if (r2 > k + 1 && r2 < C) xvb[b * 128 + r2] = aqc::cfma(aqc::cmk(sx, sy), vbb[b * 128 + r2], xvb[b * 128 + r2]);
+      if (tid == 0) a2b[b] = a2;
     }
     __syncthreads();
     tick_step(t_a);
@@ -963,8 +984,7 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
   // d_{C-1}: reflector C - 2's update of the last diagonal entry
   if (wave == (C - 1) >> 3) {
     const int bp = (C - 2) & 1;
-    cplx a2, s;
-    prev_scalars(C - 1, bp, a2, s);
+    const cplx a2 = a2b[bp];
     const bool own = r0 == C - 1 && q0 == ((C - 1) & 7);
     const int gi = (C - 1) >> 3;
     if (own) {

@@ -364,3 +364,26 @@ def test_device_memory_cache_reuses_blocks_and_results_unchanged():
     assert s1[4] == s0[4], (s0, s1)          # no new hipMalloc for the repeated shape
     assert s1[3] >= s0[3] + 20, (s0, s1)     # every creation served from the cache
     assert s1[1] == s0[1] and s1[2] == s0[2]  # nothing left handed out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,cap", [(14, 64), (16, 128), (18, 256)])
+def test_z_all_batch_split_environments_vs_oracle(n, cap):
+    """<Z_i> of a batch of random states whose capacity splits over the four-workgroup environment
+    chains (k_env_split: 16, 32 and 64 columns per workgroup, bonds at the capacity in the middle):
+    every value against the oracle's full contraction at 1e-12, and the batch against one state at
+    a time."""
+    import bench
+    from adaptaqc_amd.device import DeviceMPS, z_all_batch
+
+    states, want = [], []
+    for seed in range(3):
+        q = bench.random_vidal_mps(n, cap, 40 + seed)
+        d = DeviceMPS(n, cap, 1e-16, cap)
+        d.load_aer(q)
+        states.append(d)
+        pre = M.MPS.from_aer(q).preprocessed()
+        want.append([M.mps_expectation_z(pre, i) for i in range(n)])
+    got = z_all_batch(states)
+    np.testing.assert_allclose(got, np.array(want), atol=1e-12)
+    np.testing.assert_allclose(states[1].z_all(), got[1], atol=1e-13)

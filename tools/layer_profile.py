@@ -10,7 +10,10 @@ algorithm structure: per-pair / per-generator MPS builds and dots for the sweep,
 Rotoselect / Rotosolve candidate) on one host core for the same layer-10 circuit: a bounded sample
 of its stages, scaled (stated in the output).
 
-    python3 tools/layer_profile.py [--layers 11] [--max-chi 0] [--cpu-budget 60] > gpurun_out/r5_layer.json
+Per layer also the largest bond of the full circuit's MPS after the layer (one extra evaluation,
+outside the stage timers) and the layer's two-site SVD paths (Gram path taken / declined).
+
+    python3 tools/layer_profile.py [--target near-product|graded] [--layers 11] [--max-chi 0] > out.json
 """
 import argparse
 import json
@@ -50,7 +53,13 @@ def gpu_layers(args):
     from adaptaqc_amd.utils.ansatzes import identity_resolvable
     from adaptaqc_amd.utils.constants import ALG_ROTOSELECT
 
-    target = bench.near_product_mps(bench.N_QUBITS, bench.CHI, args.seed)
+    from adaptaqc_amd import _lib
+    from adaptaqc_amd.mps_operations import device_mps_from_circuit
+
+    if args.target == "graded":  # decaying Schmidt spectra, as a ground state's (bench.graded_vidal_mps)
+        target = bench.graded_vidal_mps(bench.N_QUBITS, bench.CHI, args.seed, 0.9)
+    else:
+        target = bench.near_product_mps(bench.N_QUBITS, bench.CHI, args.seed)
     sim = mps_sim_with_args(mps_truncation_threshold=args.threshold, max_chi=args.max_chi or None)
     config = AdaptConfig(method="general_gradient", cost_improvement_num_layers=1e3, rotosolve_frequency=10,
                          max_layers=args.layers)
@@ -69,13 +78,19 @@ def gpu_layers(args):
     def add_layer(index):
         st.t = {}
         c0 = comp.cost_evaluation_counter
+        _lib.gram_stats(), _lib.gram_big_stats()
         t1 = time.perf_counter()
         cost = add(index)
         wall = time.perf_counter() - t1
+        g, gb = _lib.gram_stats(), _lib.gram_big_stats()
+        bond = int(max(device_mps_from_circuit(comp.full_circuit, sim).dims()))
         row = {"layer": index, "wall_ms": 1e3 * wall,
                "stages_ms": {k: round(1e3 * v, 3) for k, v in st.t.items()},
                "other_ms": round(1e3 * (wall - sum(st.t.values())), 3),
-               "cost_evaluations": comp.cost_evaluation_counter - c0, "cost": float(cost),
+               "cost_evaluations": comp.cost_evaluation_counter - c0, "cost": float(cost), "max_bond_after": bond,
+               "svd": {"gram128_taken": g["taken"], "gram128_declined": g["declined_shape"] + g["declined_floor"],
+                       "gram_big_taken": gb["taken"], "gram_big_declined": gb["declined"] + gb["declined_floor"]
+                       + gb["timeouts"] + gb["declined_certificate"]},
                "pair": [int(x) for x in comp.qubit_pair_history[-1]]}
         layers.append(row)
         print(json.dumps(row), flush=True)
@@ -143,6 +158,7 @@ def cpu_port_layer(comp, typical_evals, threshold, max_chi, pairs_sample):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--layers", type=int, default=11)
+    ap.add_argument("--target", choices=["near-product", "graded"], default="near-product")
     ap.add_argument("--threshold", type=float, default=1e-8)
     ap.add_argument("--max-chi", type=int, default=0)
     ap.add_argument("--seed", type=int, default=21)
@@ -152,7 +168,8 @@ def main():
     typical = [r for r in layers if r["layer"] > 0 and "rotosolve" not in r["stages_ms"]]
     with_rs = [r for r in layers if "rotosolve" in r["stages_ms"]]
     out = {"workload": "paper setting (examples/advanced_mps_example.py:40-58) on a 50-qubit chi=64 target "
-                       "(bench.near_product_mps)", "threshold": args.threshold, "max_chi": args.max_chi or None,
+                       f"({'bench.graded_vidal_mps, decay 0.9' if args.target == 'graded' else 'bench.near_product_mps'})",
+           "threshold": args.threshold, "max_chi": args.max_chi or None,
            **summary,
            "median_layer_ms": float(np.median([r["wall_ms"] for r in typical])) if typical else None,
            "median_stages_ms": {k: float(np.median([r["stages_ms"].get(k, 0.0) for r in typical]))
