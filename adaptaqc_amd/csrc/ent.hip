@@ -27,6 +27,12 @@ using aqc::cplx;
 namespace {
 
 constexpr int kT = aqc::kGemmThreads;
+// the GEMMs of the environment chains fetch the next k tile's operands while the matrix cores run
+// on the current one: a chain's steps are dependent, so each tile's global round trip was exposed
+#ifndef AQC_ENV_PF
+#define AQC_ENV_PF 1
+#endif
+constexpr bool kEnvPf = AQC_ENV_PF != 0;
 
 struct RdmJob {
   const cplx* gam;
@@ -62,13 +68,13 @@ __global__ __launch_bounds__(kT) void k_rdm_env(const RdmJob* __restrict__ jobs)
       const int cl = j.dims[i], cr = j.dims[i + 1];
       const cplx* L = j.Lenv + (size_t)i * cc;
       cplx* T = j.tmpL;  // T[l][t*cap + r] = (L A^t)[l][r]
-      aqc::block_cgemm(
+      aqc::block_cgemm<true, false, kEnvPf>(
           cl, 2 * cap, cl, [&](int r, int k) { return L[(size_t)r * cap + k]; },
           [&](int k, int c) { const int t = c / cap, r = c % cap; return r < cr ? aval(j, i, t, k, r) : aqc::cmk(0, 0); },
           [&](int r, int c, cplx v) { T[(size_t)r * 2 * cap + c] = v; }, lds);
       __syncthreads();
       cplx* Ln = j.Lenv + (size_t)(i + 1) * cc;
-      aqc::block_cgemm(
+      aqc::block_cgemm<false, false, kEnvPf>(
           cr, cr, 2 * cl,
           [&](int r, int kk) { const int t = kk / cl, k = kk % cl; return aqc::cconj(aval(j, i, t, k, r)); },
           [&](int kk, int c) { const int t = kk / cl, k = kk % cl; return T[(size_t)k * 2 * cap + t * cap + c]; },
@@ -82,20 +88,201 @@ __global__ __launch_bounds__(kT) void k_rdm_env(const RdmJob* __restrict__ jobs)
       const int cl = j.dims[i], cr = j.dims[i + 1];
       const cplx* R = j.Renv + (size_t)(i + 1) * cc;
       cplx* T = j.tmpR;  // T[t*cap + l][r] = (A^t R)[l][r]
-      aqc::block_cgemm(
+      aqc::block_cgemm<true, false, kEnvPf>(
           2 * cap, cr, cr,
           [&](int rr, int k) { const int t = rr / cap, l = rr % cap; return l < cl ? aval(j, i, t, l, k) : aqc::cmk(0, 0); },
           [&](int k, int c) { return R[(size_t)k * cap + c]; }, [&](int rr, int c, cplx v) { T[(size_t)rr * cap + c] = v; },
           lds);
       __syncthreads();
       cplx* Rn = j.Renv + (size_t)i * cc;
-      aqc::block_cgemm(
+      aqc::block_cgemm<true, true, kEnvPf>(
           cl, cl, 2 * cr,
           [&](int l, int kk) { const int t = kk / cr, k = kk % cr; return T[(size_t)(t * cap + l) * cap + k]; },
           [&](int kk, int c) { const int t = kk / cr, k = kk % cr; return aqc::cconj(aval(j, i, t, c, k)); },
           [&](int l, int c, cplx v) { Rn[(size_t)l * cap + c] = v; }, lds);
       __syncthreads();
     }
+  }
+}
+
+// ---- environments over four workgroups per chain ---------------------------------------------
+// k_rdm_env runs a chain (left or right, one state) in one workgroup: its n - 1 steps are dependent
+// and each is ~1 M complex MACs at 2 chi = 128, so one CU's matrix cores bound it (~27 us a step at
+// peak, 55 us measured: ~2.7 ms for a 50-site state).  Here kEnvNW workgroups share a chain by
+// output columns: workgroup w owns columns c0 = w CW .. c0 + CW of every environment and computes
+//   left:  T = L_i A_i^t[:, cols] (cl x 2 CW, both t),  L_{i+1}[:, cols] = sum_t A_i^{t dag} T_t
+//   right: T = R_{i+1} conj(A_i^t[cols, :])^T,         R_i[:, cols]     = sum_t A_i^t T_t
+// -- its own columns need only its own T, so a step has no exchange inside it.  Between steps the
+// chain's workgroups hand the new environment over as gram_big.hip's column exchange does (sc1
+// stores, s_waitcnt vmcnt(0), a barrier, one agent-scope counter add, one lane polling the counter;
+// the next step reads the environment with sc1 loads).  Spins are bounded: a timeout sets *err and
+// the host reports it.  The GEMMs keep each wave on 16 output rows and all of a block's (<= 64)
+// columns, so a 16-column chunk wastes no MFMAs (block_cgemm's 64 x 64 blocks would waste 3/4).
+constexpr int kEnvNW = 4;
+constexpr int kEnvKT = 32;
+struct NarrowLds {
+  cplx As[kEnvKT][65];
+  cplx Bs[kEnvKT][65];
+};
+
+typedef __attribute__((address_space(1))) double env_gdbl;
+__device__ __forceinline__ void env_st(cplx* p, cplx v) {
+  env_gdbl* q = (env_gdbl*)(double*)p;
+  __hip_atomic_store(q, v.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(q + 1, v.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ cplx env_ld(const cplx* p) {
+  env_gdbl* q = (env_gdbl*)(double*)p;
+  return aqc::cmk(__hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                  __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
+// C[i][j] = sum_k a(i, k) b(k, j) for i < m, j < n: blocks of 64 rows x NB columns, wave w on rows
+// 16 w .. 16 w + 15 and all NB / 16 column tiles (v_mfma_f64_16x16x4_f64, a complex product as four
+// real MFMAs); k in LDS tiles of kEnvKT with the next tile's operands fetched into registers while
+// the matrix cores run.  AK / BK: consecutive threads walk k in a's / b's fetch (a source contiguous
+// along k).  Ends on a barrier.
+template <int NB, bool AK, bool BK, typename FA, typename FB, typename FS>
+__device__ __forceinline__ void narrow_cgemm(int m, int n, int k, FA a, FB b, FS store, NarrowLds& lds) {
+  constexpr int NT = NB / 16, EA = kEnvKT * 64 / kT, EB = kEnvKT * NB / kT;
+  static_assert(NB % 16 == 0 && NB <= 64 && EB >= 1, "narrow_cgemm block width");
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, li = lane & 15, lk = lane >> 4;
+  for (int bi = 0; bi < m; bi += 64) {
+    for (int bj = 0; bj < n; bj += NB) {
+      aqc::d4_t cr[NT], ci[NT];
+#pragma unroll
+      for (int c = 0; c < NT; ++c) cr[c] = aqc::d4_t{0, 0, 0, 0}, ci[c] = aqc::d4_t{0, 0, 0, 0};
+      cplx pa[EA], pb[EB];
+      auto fetch = [&](int k0) {
+#pragma unroll
+        for (int q = 0; q < EA; ++q) {
+          const int e = tid + q * kT, ka = AK ? e % kEnvKT : e / 64, ia = AK ? e / kEnvKT : e % 64;
+          pa[q] = (bi + ia < m && k0 + ka < k) ? a(bi + ia, k0 + ka) : aqc::cmk(0, 0);
+        }
+#pragma unroll
+        for (int q = 0; q < EB; ++q) {
+          const int e = tid + q * kT, kb = BK ? e % kEnvKT : e / NB, ib = BK ? e / kEnvKT : e % NB;
+          pb[q] = (bj + ib < n && k0 + kb < k) ? b(k0 + kb, bj + ib) : aqc::cmk(0, 0);
+        }
+      };
+      fetch(0);
+      for (int k0 = 0; k0 < k; k0 += kEnvKT) {
+#pragma unroll
+        for (int q = 0; q < EA; ++q) {
+          const int e = tid + q * kT, ka = AK ? e % kEnvKT : e / 64, ia = AK ? e / kEnvKT : e % 64;
+          lds.As[ka][ia] = pa[q];
+        }
+#pragma unroll
+        for (int q = 0; q < EB; ++q) {
+          const int e = tid + q * kT, kb = BK ? e % kEnvKT : e / NB, ib = BK ? e / kEnvKT : e % NB;
+          lds.Bs[kb][ib] = pb[q];
+        }
+        __syncthreads();
+        if (k0 + kEnvKT < k) fetch(k0 + kEnvKT);
+#pragma unroll
+        for (int ks = 0; ks < kEnvKT / 4; ++ks) {
+          const int kk = 4 * ks + lk;
+          const cplx av = lds.As[kk][16 * wave + li];
+#pragma unroll
+          for (int c = 0; c < NT; ++c) {
+            const cplx bv = lds.Bs[kk][16 * c + li];
+            cr[c] = __builtin_amdgcn_mfma_f64_16x16x4f64(av.x, bv.x, cr[c], 0, 0, 0);
+            cr[c] = __builtin_amdgcn_mfma_f64_16x16x4f64(-av.y, bv.y, cr[c], 0, 0, 0);
+            ci[c] = __builtin_amdgcn_mfma_f64_16x16x4f64(av.x, bv.y, ci[c], 0, 0, 0);
+            ci[c] = __builtin_amdgcn_mfma_f64_16x16x4f64(av.y, bv.x, ci[c], 0, 0, 0);
+          }
+        }
+        __syncthreads();
+      }
+#pragma unroll
+      for (int c = 0; c < NT; ++c)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int i = bi + 16 * wave + lk + 4 * q, jj = bj + 16 * c + li;
+          if (i < m && jj < n) store(i, jj, aqc::cmk(cr[c][q], ci[c][q]));
+        }
+    }
+  }
+}
+
+// grid (kEnvNW, 2 directions, states), kT threads; CW = cap / kEnvNW output columns per workgroup.
+// Counters: cnt[32 (2 state + dir)] (zeroed by the host).
+template <int CW>
+__global__ __launch_bounds__(kT) void k_env_split(const RdmJob* __restrict__ jobs, unsigned* __restrict__ cnt,
+                                                  int* __restrict__ err, unsigned long long spin) {
+  constexpr int NB1 = 2 * CW < 64 ? 2 * CW : 64, NB2 = CW < 64 ? CW : 64;
+  const int w = blockIdx.x, dir = blockIdx.y, tid = threadIdx.x;
+  const RdmJob& j = jobs[blockIdx.z];
+  unsigned* ctr = cnt + 32 * (2 * blockIdx.z + dir);
+  __shared__ NarrowLds lds;
+  __shared__ int s_abort;
+  const int n = j.n, cap = j.cap;
+  const size_t cc = (size_t)cap * cap;
+  const int c0 = w * CW;
+  cplx* Tw = (dir == 0 ? j.tmpL : j.tmpR) + (size_t)w * cap * 2 * CW;
+  if (tid == 0) {
+    s_abort = 0;
+    if (w == 0) {  // the boundary environments, for the kernels after this one
+      if (dir == 0) j.Lenv[0] = aqc::cmk(1, 0);
+      else j.Renv[(size_t)n * cc] = aqc::cmk(1, 0);
+    }
+  }
+  for (int step = 0; step < n - 1; ++step) {
+    if (dir == 0) {
+      const int i = step, cl = j.dims[i], cr = j.dims[i + 1];
+      const cplx* L = j.Lenv + (size_t)i * cc;
+      narrow_cgemm<NB1, true, false>(
+          cl, 2 * CW, cl, [&](int l, int k) { return i == 0 ? aqc::cmk(1, 0) : env_ld(L + (size_t)l * cap + k); },
+          [&](int k, int c2) {
+            const int t = c2 / CW, c = c0 + c2 % CW;
+            return c < cr ? aval(j, i, t, k, c) : aqc::cmk(0, 0);
+          },
+          [&](int l, int c2, cplx v) { Tw[(size_t)l * 2 * CW + c2] = v; }, lds);
+      __syncthreads();
+      cplx* Ln = j.Lenv + (size_t)(i + 1) * cc;
+      narrow_cgemm<NB2, false, false>(
+          cr, min(CW, cr - c0), 2 * cl,
+          [&](int r, int kk) { const int t = kk / cl, k = kk % cl; return aqc::cconj(aval(j, i, t, k, r)); },
+          [&](int kk, int c) { const int t = kk / cl, k = kk % cl; return Tw[(size_t)k * 2 * CW + t * CW + c]; },
+          [&](int r, int c, cplx v) { env_st(Ln + (size_t)r * cap + c0 + c, v); }, lds);
+    } else {
+      const int i = n - 1 - step, cl = j.dims[i], cr = j.dims[i + 1];
+      const cplx* R = j.Renv + (size_t)(i + 1) * cc;
+      // T[k][t CW + c] = sum_k' R[k][k'] conj(A_t[c0 + c][k'])
+      narrow_cgemm<NB1, true, true>(
+          cr, 2 * CW, cr, [&](int k, int k2) { return i == n - 1 ? aqc::cmk(1, 0) : env_ld(R + (size_t)k * cap + k2); },
+          [&](int k2, int c2) {
+            const int t = c2 / CW, c = c0 + c2 % CW;
+            return c < cl ? aqc::cconj(aval(j, i, t, c, k2)) : aqc::cmk(0, 0);
+          },
+          [&](int k, int c2, cplx v) { Tw[(size_t)k * 2 * CW + c2] = v; }, lds);
+      __syncthreads();
+      cplx* Rn = j.Renv + (size_t)i * cc;
+      // R_i[l][c0 + c] = sum_{t, k} A_t[l][k] T[k][t CW + c]
+      narrow_cgemm<NB2, true, false>(
+          cl, min(CW, cl - c0), 2 * cr,
+          [&](int l, int kk) { const int t = kk / cr, k = kk % cr; return aval(j, i, t, l, k); },
+          [&](int kk, int c) { const int t = kk / cr, k = kk % cr; return Tw[(size_t)k * 2 * CW + t * CW + c]; },
+          [&](int l, int c, cplx v) { env_st(Rn + (size_t)l * cap + c0 + c, v); }, lds);
+    }
+    // hand-off: every workgroup's columns of the new environment stored before the count
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned target = (unsigned)kEnvNW * (unsigned)(step + 1);
+      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+      while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+        __builtin_amdgcn_s_sleep(1);
+        if (__builtin_amdgcn_s_memrealtime() - t0 > spin) {
+          s_abort = 1;
+          atomicOr(err, 1);
+          break;
+        }
+      }
+    }
+    __syncthreads();
+    if (s_abort) return;
   }
 }
 
@@ -114,11 +301,11 @@ __global__ __launch_bounds__(kT) void k_rdm_P(const RdmJob* __restrict__ jobs, i
   const cplx* R = j.Renv + (size_t)(b + 1) * cc;
   cplx* U = j.U + ((size_t)b * 3 + m) * cc;
   cplx* P = j.P + ((size_t)b * 3 + m) * cc;
-  aqc::block_cgemm(
+  aqc::block_cgemm<true, false, kEnvPf>(
       cl, cr, cr, [&](int l, int k) { return aval(j, b, s, l, k); }, [&](int k, int c) { return R[(size_t)k * cap + c]; },
       [&](int l, int c, cplx v) { U[(size_t)l * cap + c] = v; }, lds);
   __syncthreads();
-  aqc::block_cgemm(
+  aqc::block_cgemm<true, true, kEnvPf>(
       cl, cl, cr, [&](int l, int k) { return U[(size_t)l * cap + k]; },
       [&](int k, int c) { return aqc::cconj(aval(j, b, sb, c, k)); }, [&](int l, int c, cplx v) { P[(size_t)l * cap + c] = v; },
       lds);
@@ -139,12 +326,12 @@ __global__ __launch_bounds__(kT) void k_rdm_chain(const RdmJob* __restrict__ job
   {
     const int cl = j.dims[a], cr = j.dims[a + 1];
     const cplx* L = j.Lenv + (size_t)a * cc;
-    aqc::block_cgemm(
+    aqc::block_cgemm<true, false, kEnvPf>(
         cl, cr, cl, [&](int r, int k) { return L[(size_t)r * cap + k]; }, [&](int k, int c) { return aval(j, a, s, k, c); },
         [&](int r, int c, cplx v) { T[(size_t)r * 2 * cap + c] = v; }, lds);
     __syncthreads();
     cplx* E = Eb[0];
-    aqc::block_cgemm(
+    aqc::block_cgemm<false, false, kEnvPf>(
         cr, cr, cl, [&](int r, int k) { return aqc::cconj(aval(j, a, sb, k, r)); },
         [&](int k, int c) { return T[(size_t)k * 2 * cap + c]; }, [&](int r, int c, cplx v) { E[(size_t)r * cap + c] = v; },
         lds);
@@ -187,13 +374,13 @@ __global__ __launch_bounds__(kT) void k_rdm_chain(const RdmJob* __restrict__ job
     __syncthreads();
     if (b + 1 >= n) break;
     // transfer through site b: E' = sum_t A_b^{t dag} E A_b^t
-    aqc::block_cgemm(
+    aqc::block_cgemm<true, false, kEnvPf>(
         cl, 2 * cap, cl, [&](int r, int k) { return E[(size_t)r * cap + k]; },
         [&](int k, int c) { const int t = c / cap, r = c % cap; return r < cr ? aval(j, b, t, k, r) : aqc::cmk(0, 0); },
         [&](int r, int c, cplx v) { T[(size_t)r * 2 * cap + c] = v; }, lds);
     __syncthreads();
     cplx* En = Eb[cur ^ 1];
-    aqc::block_cgemm(
+    aqc::block_cgemm<false, false, kEnvPf>(
         cr, cr, 2 * cl,
         [&](int r, int kk) { const int t = kk / cl, k = kk % cl; return aqc::cconj(aval(j, b, t, k, r)); },
         [&](int kk, int c) { const int t = kk / cl, k = kk % cl; return T[(size_t)k * 2 * cap + t * cap + c]; },
@@ -406,6 +593,48 @@ int ensure(RdmBuffers& b, size_t need) {
   return AQC_OK;
 }
 
+// Counter / error words behind the jobs of an environment launch: 32 words per chain, one error word.
+size_t env_sync_bytes(int ns) { return (((size_t)ns * 2 * 32 + 32) * sizeof(unsigned) + 255) / 256 * 256; }
+
+// The left / right environments of every state: k_env_split (kEnvNW workgroups per chain) where the
+// capacity splits into 16-column multiples, else k_rdm_env; states in rounds small enough that every
+// chain's workgroups are resident together (two per CU).  sync: env_sync_bytes(ns) of device memory.
+int launch_envs(RdmJob* djobs, int ns, int cap, hipStream_t st, void* sync) {
+  if (cap % (16 * kEnvNW) != 0) {
+    hipLaunchKernelGGL(k_rdm_env, dim3(2, ns), dim3(kT), 0, st, djobs);
+    AQC_CHECK_LAUNCH();
+    return AQC_OK;
+  }
+  unsigned* cnt = (unsigned*)sync;
+  int* err = (int*)(cnt + (size_t)ns * 2 * 32);
+  AQC_HIP_CHECK(hipMemsetAsync(sync, 0, env_sync_bytes(ns), st));
+  constexpr unsigned long long kSpin = 200000000ull;  // s_memrealtime (100 MHz): 2 s
+  constexpr int kRound = 28;  // 28 x 8 workgroups: one per CU (~400 VGPRs a lane) leaves room
+  for (int s0 = 0; s0 < ns; s0 += kRound) {
+    const int m = std::min(kRound, ns - s0);
+    const dim3 grid(kEnvNW, 2, m);
+    RdmJob* jb = djobs + s0;
+    unsigned* cb = cnt + (size_t)s0 * 2 * 32;
+    switch (cap / kEnvNW) {
+      case 16: hipLaunchKernelGGL(k_env_split<16>, grid, dim3(kT), 0, st, jb, cb, err, kSpin); break;
+      case 32: hipLaunchKernelGGL(k_env_split<32>, grid, dim3(kT), 0, st, jb, cb, err, kSpin); break;
+      case 64: hipLaunchKernelGGL(k_env_split<64>, grid, dim3(kT), 0, st, jb, cb, err, kSpin); break;
+      default: hipLaunchKernelGGL(k_env_split<128>, grid, dim3(kT), 0, st, jb, cb, err, kSpin); break;
+    }
+    AQC_CHECK_LAUNCH();
+  }
+  return AQC_OK;
+}
+
+// after the stream synchronised: a chain whose workgroups were not resident together timed out
+int env_check(void* sync, int ns, int cap) {
+  if (cap % (16 * kEnvNW) != 0) return AQC_OK;
+  int e = 0;
+  AQC_HIP_CHECK(hipMemcpy(&e, (int*)((unsigned*)sync + (size_t)ns * 2 * 32), sizeof(int), hipMemcpyDeviceToHost));
+  AQC_REQUIRE(e == 0, "environment chains: a workgroup hand-off timed out (workgroups not co-resident)");
+  return AQC_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -439,10 +668,12 @@ int aqc_mps_pair_rdms_batch(aqc_mps_t* hs, int ns, const int* pairs, int npairs,
   hipStream_t st = aqc::mps_stream();
   RdmBuffers& rb = rbuf();
   AQC_HIP_CHECK(hipStreamSynchronize(st));
-  rc = ensure(rb, jb + pb + ob + ns * per_state + 1024);
+  const size_t sb = env_sync_bytes(ns);
+  rc = ensure(rb, jb + pb + ob + ns * per_state + sb + 1024);
   if (rc != AQC_OK) return rc;
   char* base = (char*)rb.dev;
   RdmJob* djobs = (RdmJob*)base;
+  void* dsync = base + jb + pb + ob + ns * per_state;
   int* dpairs = (int*)(base + jb);
   int* dalist = dpairs + 2 * npairs;
   cplx* dout = out_is_device ? (cplx*)out : (cplx*)(base + jb + pb);
@@ -477,9 +708,9 @@ int aqc_mps_pair_rdms_batch(aqc_mps_t* hs, int ns, const int* pairs, int npairs,
   AQC_HIP_CHECK(hipMemcpyAsync(dalist, alist.data(), na * sizeof(int), hipMemcpyHostToDevice, st));
   const double c3 = (double)cap * cap * cap;
   aqc::KernelTimer::begin(st, "rdm_env", 0.0, ns * 2.0 * n * 4.0 * c3 * 8.0);
-  hipLaunchKernelGGL(k_rdm_env, dim3(2, ns), dim3(kT), 0, st, djobs);
+  rc = launch_envs(djobs, ns, cap, st, dsync);
   aqc::KernelTimer::end(st);
-  AQC_CHECK_LAUNCH();
+  if (rc != AQC_OK) return rc;
   hipLaunchKernelGGL(k_rdm_P, dim3(n, 3, ns), dim3(kT), 0, st, djobs, 0);
   AQC_CHECK_LAUNCH();
   double steps = 0.0;
@@ -493,7 +724,7 @@ int aqc_mps_pair_rdms_batch(aqc_mps_t* hs, int ns, const int* pairs, int npairs,
   if (!out_is_device)
     AQC_HIP_CHECK(hipMemcpyAsync(out, dout, (size_t)ns * npairs * 16 * sizeof(cplx), hipMemcpyDeviceToHost, st));
   AQC_HIP_CHECK(hipStreamSynchronize(st));
-  return AQC_OK;
+  return env_check(dsync, ns, cap);
 }
 
 int aqc_mps_z_all_batch(aqc_mps_t* hs, int ns, double* out) {
@@ -511,11 +742,13 @@ int aqc_mps_z_all_batch(aqc_mps_t* hs, int ns, double* out) {
   hipStream_t st = aqc::mps_stream();
   RdmBuffers& rb = rbuf();
   AQC_HIP_CHECK(hipStreamSynchronize(st));
-  rc = ensure(rb, jb + ob + ns * per_state + 1024);
+  const size_t sb = env_sync_bytes(ns);
+  rc = ensure(rb, jb + ob + ns * per_state + sb + 1024);
   if (rc != AQC_OK) return rc;
   char* base = (char*)rb.dev;
   RdmJob* djobs = (RdmJob*)base;
   double* dout = (double*)(base + jb);
+  void* dsync = base + jb + ob + ns * per_state;
   cplx* work = (cplx*)(base + jb + ob);
   std::vector<RdmJob> jobs(ns);
   for (int s = 0; s < ns; ++s) {
@@ -542,8 +775,8 @@ int aqc_mps_z_all_batch(aqc_mps_t* hs, int ns, double* out) {
   AQC_HIP_CHECK(hipMemcpyAsync(djobs, jobs.data(), ns * sizeof(RdmJob), hipMemcpyHostToDevice, st));
   const double c3 = (double)cap * cap * cap;
   aqc::KernelTimer::begin(st, "mps_zall", 0.0, ns * 2.0 * n * 4.0 * c3 * 8.0);
-  hipLaunchKernelGGL(k_rdm_env, dim3(2, ns), dim3(kT), 0, st, djobs);
-  AQC_CHECK_LAUNCH();
+  rc = launch_envs(djobs, ns, cap, st, dsync);
+  if (rc != AQC_OK) return rc;
   hipLaunchKernelGGL(k_rdm_P, dim3(n, 2, ns), dim3(kT), 0, st, djobs, 1);
   AQC_CHECK_LAUNCH();
   hipLaunchKernelGGL(k_rdm_ztrace, dim3(n, ns), dim3(kT), 0, st, djobs, dout);
@@ -551,7 +784,7 @@ int aqc_mps_z_all_batch(aqc_mps_t* hs, int ns, double* out) {
   AQC_CHECK_LAUNCH();
   AQC_HIP_CHECK(hipMemcpyAsync(out, dout, (size_t)ns * n * sizeof(double), hipMemcpyDeviceToHost, st));
   AQC_HIP_CHECK(hipStreamSynchronize(st));
-  return AQC_OK;
+  return env_check(dsync, ns, cap);
 }
 
 int aqc_mps_pair_rdms(aqc_mps_t h, const int* pairs, int npairs, double* out) {
