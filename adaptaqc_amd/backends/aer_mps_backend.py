@@ -26,7 +26,8 @@ import numpy as np
 
 from ..circuit import device_ops_array, mps_payload
 from ..device import DeviceMPS
-from ..mps_operations import DevicePreprocessedMPS, apply_checked, chi_cap_for, zero_aer_mps
+from ..mps_operations import (DevicePreprocessedMPS, apply_checked, chi_cap_for, grow_capacity, is_capacity_error,
+                              zero_aer_mps)
 from .aqc_backend import AQCBackend
 
 logger = logging.getLogger(__name__)
@@ -112,14 +113,28 @@ class AerMPSBackend(AQCBackend):
             d.set_truncation(thr, max_chi)
         return pool[:k]
 
+    def grow_on_overflow(self, e):
+        """After an error from a replay on states shaped like the base: True if it was a capacity
+        overflow of an unbounded run and the capacity grew (the next ensure_base rebuilds the base,
+        new_state / scratch_states follow it), else False."""
+        _, max_chi = self._options()
+        return (self._base is not None and is_capacity_error(e)
+                and grow_capacity(self._base[1].n, max_chi, self._base[1].chi_cap))
+
     def device_state(self, circuit):
         """Replay ``circuit`` on the device; returns the (sorted) work DeviceMPS."""
         thr, max_chi = self._options()
-        base, start = self.ensure_base(circuit)
-        work = self._work
-        work.set_truncation(thr, max_chi)
-        work.copy_from(base)
-        apply_checked(work, device_ops_array(circuit, start))
+        while True:
+            base, start = self.ensure_base(circuit)
+            work = self._work
+            work.set_truncation(thr, max_chi)
+            work.copy_from(base)
+            try:
+                apply_checked(work, device_ops_array(circuit, start))
+                break
+            except Exception as e:
+                if not self.grow_on_overflow(e):
+                    raise
         work.sort()
         return work
 

@@ -42,12 +42,46 @@ def _preprocess_mps(qiskit_mps):
     return out
 
 
+# Unbounded runs (max_chi None, the reference default) grow their capacity on demand, as Aer's MPS
+# grows its bonds: a replay starts at the smallest power of two >= 64 that holds the loaded MPS and
+# whatever an earlier replay on as many qubits needed, and a capacity overflow re-runs it at twice
+# the capacity (up to min(512, 2^(n/2))).  Until round 4 they took that upper bound at once, and
+# every kernel whose work follows the capacity -- the candidate sweep's cap x cap transfer
+# matrices, whole-state copies -- paid for 512 at bond 64 (~100 ms per sweep, 0.4 ms at 64).
+_UNBOUNDED_CAP = {}  # n -> the capacity the last unbounded replay on n qubits needed (only grows)
+
+
+def _full_cap(n):
+    return min(MAX_CHI_CAP, 2 ** (n // 2))
+
+
 def chi_cap_for(n, max_chi, loaded_max=1):
-    cap = int(max_chi) if max_chi else min(MAX_CHI_CAP, 2 ** (n // 2))
+    if max_chi:
+        cap = int(max_chi)
+    else:
+        full = _full_cap(n)
+        want = max(_UNBOUNDED_CAP.get(n, 0), int(loaded_max), min(64, full))
+        cap = 1
+        while cap < want:
+            cap <<= 1
+        cap = min(cap, full)
     cap = max(cap, int(loaded_max), 1)
     if cap > MAX_CHI_CAP:
         raise NotImplementedError(f"bond dimension {cap} exceeds the supported maximum {MAX_CHI_CAP}")
     return cap
+
+
+def is_capacity_error(e) -> bool:
+    return "capacity (chi_cap) exceeded" in str(e)
+
+
+def grow_capacity(n, max_chi, cap) -> bool:
+    """After a capacity overflow at ``cap``: raise the unbounded capacity for n qubits to 2 cap
+    (chi_cap_for returns it from now on); False when the run is bounded or already at the limit."""
+    if max_chi or cap >= _full_cap(n):
+        return False
+    _UNBOUNDED_CAP[n] = max(_UNBOUNDED_CAP.get(n, 0), min(2 * cap, _full_cap(n)))
+    return True
 
 
 def apply_checked(state: DeviceMPS, ops):
@@ -85,16 +119,23 @@ def device_mps_from_circuit(circuit: QuantumCircuit, sim=None, trunc_thr=None, o
         loaded = mps_payload(circuit.data[0].operation)
         start = 1
     lmax = max(np.asarray(a).shape[1] for a, _ in loaded[0]) if loaded is not None else 1
-    cap = chi_cap_for(n, max_chi, lmax)
-    if out is None or out.n != n or out.chi_cap < cap:
-        out = DeviceMPS(n, cap, thr, max_chi)
-    else:
-        out.set_truncation(thr, max_chi)
-    if loaded is not None:
-        out.load_aer(loaded)
-    else:
-        out.load_aer(zero_aer_mps(n))
-    apply_checked(out, device_ops_array(circuit, start))
+    ops = device_ops_array(circuit, start)
+    while True:
+        cap = chi_cap_for(n, max_chi, lmax)
+        if out is None or out.n != n or out.chi_cap < cap:
+            out = DeviceMPS(n, cap, thr, max_chi)
+        else:
+            out.set_truncation(thr, max_chi)
+        if loaded is not None:
+            out.load_aer(loaded)
+        else:
+            out.load_aer(zero_aer_mps(n))
+        try:
+            apply_checked(out, ops)
+            break
+        except Exception as e:  # an unbounded run outgrew its capacity: again at twice the capacity
+            if not (is_capacity_error(e) and grow_capacity(n, max_chi, out.chi_cap)):
+                raise
     out.sort()
     return out
 

@@ -139,11 +139,36 @@ class MPSPrefixBatch(_SweepBase):
         self.phi = None
         self.kind = kind
 
+    def _grown(self, e):
+        """A capacity overflow of an unbounded run: the backend grew its capacity, so the prefix
+        is rebuilt at the new one (the retry replays it)."""
+        if not self.backend.grow_on_overflow(e):
+            return False
+        self.phi, self.pos = None, None
+        return True
+
     def goto(self, index):
+        while True:
+            try:
+                return self._goto(index)
+            except Exception as e:
+                if not self._grown(e):
+                    raise
+
+    def costs(self, index, mats):
+        while True:
+            try:
+                return self._costs(index, mats)
+            except Exception as e:
+                if not self._grown(e):
+                    raise
+                self.goto(index)
+
+    def _goto(self, index):
         circ = self.compiler.full_circuit
         base, start = self.backend.ensure_base(circ)
-        if self.phi is None:
-            self.phi = self.backend.new_state()
+        if self.phi is None or self.phi.chi_cap != base.chi_cap:
+            self.phi, self.pos = self.backend.new_state(), None
         if self.pos is None or index < self.pos:
             self.phi.copy_from(base)
             self.phi.apply(_ops(circ, start, index))
@@ -151,7 +176,7 @@ class MPSPrefixBatch(_SweepBase):
             self.phi.apply(_ops(circ, self.pos, index))
         self.pos = index
 
-    def costs(self, index, mats):
+    def _costs(self, index, mats):
         circ = self.compiler.full_circuit
         q = _ops_qubit(circ, index)
         suffix = ops_array(_ops(circ, index + 1, len(circ.data)))

@@ -122,9 +122,11 @@ def test_config5_full_size_vs_oracle():
 def test_unbounded_chi_above_256_deep_circuit():
     """The reference's default MPS_SIM has no bond-dimension cap (python_default_backends.py:19,
     aer_mps_backend.py:27-42).  A 20-qubit brickwork of depth 18 at max_chi = None grows the middle
-    bonds past 256 (oracle: ..., 256, 314, 482, 262, ...); the device replay (capacity 512, two-site
-    SVDs of up to 1024 x 1024 by the full-Gram block-pair Jacobi) matches the oracle's bond
-    dimensions exactly and its state to 1e-6 fidelity, with <0..0|psi> and <Z> beside it."""
+    bonds past 256 (oracle: ..., 256, 314, 482, 262, ...); the device replay (the capacity grown on
+    demand to 512 -- each overflow re-runs the replay at twice the capacity -- two-site SVDs of up
+    to 1024 x 1024) matches the oracle's bond dimensions exactly and its state to 1e-6 fidelity,
+    with <0..0|psi> and <Z> beside it."""
+    from adaptaqc_amd import mps_operations as mo
     from adaptaqc_amd.circuit import QuantumCircuit
     from adaptaqc_amd.mps_operations import device_mps_from_circuit
 
@@ -145,8 +147,9 @@ def test_unbounded_chi_above_256_deep_circuit():
     pre_ref = ref.preprocessed()
     want_dims = [1] + [x.shape[2] for x in pre_ref]
     assert max(want_dims) > 256
+    mo._UNBOUNDED_CAP.pop(n, None)  # (start from the smallest capacity: the replay must grow)
     d = device_mps_from_circuit(qc)
-    assert d.chi_cap == 512
+    assert d.chi_cap == 512 and mo._UNBOUNDED_CAP[n] == 512
     np.testing.assert_array_equal(d.dims(), want_dims)
     pre = d.preprocessed()
     fid = abs(M.mps_dot(pre_ref, pre))

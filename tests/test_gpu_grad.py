@@ -203,9 +203,9 @@ def test_config4_full_size_chi128_vs_oracle():
 
 def test_unbounded_cap512_general_gradient():
     """an unbounded MPS (max_chi None, the reference's default MPS_SIM) at
-    n = 18 gets capacity 512 (chi_cap_for); general_grad_of_pairs on it runs the capacity-agnostic
-    segmented sweep (one state, and a batch of two split into single states) and matches the
-    oracle's environment form."""
+    n = 18 that has grown to capacity 512 (chi_cap_for's limit min(512, 2^(n/2))); general_grad_of_pairs
+    on it runs the capacity-agnostic segmented sweep (one state, and a batch of two split into
+    single states) and matches the oracle's environment form."""
     from adaptaqc_amd import _lib
     from adaptaqc_amd.circuit import device_ops
     from adaptaqc_amd.device import DeviceMPS
@@ -213,7 +213,7 @@ def test_unbounded_cap512_general_gradient():
     from adaptaqc_amd.utils.gradients import grads_for_state, layer_operators, pair_grads_batch
 
     n = 18
-    assert chi_cap_for(n, None) == 512
+    assert chi_cap_for(n, None, 300) == 512
     rng = np.random.default_rng(18)
     ops = []
     for layer in range(3):
