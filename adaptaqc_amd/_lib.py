@@ -238,11 +238,12 @@ def timing_query(name):
 
 def gram_stats():
     """Gram-path counters since the last call (aqc_svd_gram_stats): calls, taken, declined by
-    shape, declined at the eigenvalue floor."""
-    out = np.zeros(4)
+    shape, declined at the kept-count decision / eigenvalue floor / failed certificate,
+    rank-deficiency certificates run and passed."""
+    out = np.zeros(6)
     check(load().aqc_svd_gram_stats(ptr(out)))
     return {"calls": int(out[0]), "taken": int(out[1]), "declined_shape": int(out[2]),
-            "declined_floor": int(out[3])}
+            "declined_floor": int(out[3]), "certificates": int(out[4]), "certified": int(out[5])}
 
 
 def gram_big_stats():

@@ -1030,8 +1030,10 @@ __device__ __forceinline__ void chain_theta(const TwoSiteJob& j) {
 __device__ __noinline__ void chain_jacobi_fallback(const TwoSiteJob& j) { jacobi_reg_body<128, 8, 16>(j); }
 __device__ __forceinline__ void chain_jacobi(const TwoSiteJob& j) {
   if (j.gram) {
-    if (gram_svd_body(j)) return;
+    const int g = gram_svd_body(j);
+    if (g == 1) return;
     __syncthreads();
+    if (g == 2 && gram_certified(j)) return;
   }
   chain_jacobi_fallback(j);
 }
@@ -2298,10 +2300,10 @@ int aqc_svd_gram_ticks(double* out) {
 
 int aqc_svd_gram_stats(double* out) {
   AQC_REQUIRE(out, "aqc_svd_gram_stats: null argument");
-  unsigned long long t[4];
+  unsigned long long t[6];
   AQC_HIP_CHECK(hipMemcpyFromSymbol(t, HIP_SYMBOL(g_gram_stats), sizeof(t)));
-  for (int i = 0; i < 4; ++i) out[i] = (double)t[i];
-  unsigned long long z[4] = {0, 0, 0, 0};
+  for (int i = 0; i < 6; ++i) out[i] = (double)t[i];
+  unsigned long long z[6] = {0, 0, 0, 0, 0, 0};
   AQC_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_gram_stats), z, sizeof(z)));
   return AQC_OK;
 }

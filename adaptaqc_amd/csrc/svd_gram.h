@@ -56,7 +56,7 @@ __device__ unsigned long long g_gram_ticks[12];
 static_assert(kGramNarrowK == 64, "S5: the narrow inverse iteration (tid < K) stays on wave 0");
 // path counters (thread 0 of each call): [0] calls, [1] taken, [2] declined by shape (K > 64, ...),
 // [3] declined at the eigenvalue floor (lambda_K <= 1e-9 lambda_1 -> the Jacobi runs)
-__device__ unsigned long long g_gram_stats[4];
+__device__ unsigned long long g_gram_stats[6];  // calls, taken, declined (shape), declined (decision / floor), certificates, certified
 
 __device__ __forceinline__ double wave_sum_d(double v) {
 #pragma unroll
@@ -586,13 +586,85 @@ __device__ __noinline__ void gram_wide(const TwoSiteJob& j, cplx* hh, int C, int
   }
 }
 
+// The kept count assumed the values in CHOP's error band chopped (gram_keep's second attempt):
+// ||X - X V V^H||_F^2, the exact weight of X outside the kept right singular space, must then be
+// below CHOP / 2 (gram_big.hip's k_gb_cert at 2 chi > 128).  V = W / sigma from S6's output (work,
+// column c at c * C).  Y = X V (L x K) into the work scratch past W, then the residual in 64 x 64
+// blocks on the matrix cores, one block per 256-thread sub-group.  Returns the sum (every thread).
+// (A call: its accumulators stay out of the body's register allocation.)
+__device__ __noinline__ double gram_cert128(const TwoSiteJob& j, int C, int K, const double* sig2) {
+  extern __shared__ double2 xbuf[];
+  __shared__ double red[16];
+  const int tid = fresh_tid(), sg = tid >> 8, lt = tid & 255, wave = lt >> 6, lane = tid & 63;
+  const int M = 2 * j.dims[0], N = 2 * j.dims[2];
+  const bool tr = M < N;
+  const int L = tr ? N : M;
+  const cplx* th = j.theta;
+  const cplx* W = j.work;
+  cplx* Y = j.work + 16384;  // L x K, row stride 128
+  static_assert(16384 + 128 * 128 <= aqc::kGramWorkElems, "certificate scratch");
+  auto xel = [&](int R, int c) { return tr ? aqc::cconj(aqc::ldg(th + (size_t)R * M + c)) : aqc::ldg(th + (size_t)c * M + R); };
+  // W and Y through agent-scope loads: this CU's previous update (its certificate, its split) read
+  // the same addresses, and the L1 may still hold those lines (as for S6's factors)
+  auto lda = [](const cplx* p) {
+    const gdbl_t* q = (const gdbl_t*)(const double*)p;
+    return aqc::cmk(__hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                    __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  };
+  aqc::GemmLds& lds = reinterpret_cast<aqc::GemmLds*>(xbuf)[sg];
+  const int bi = 64 * (sg >> 1), bj = 64 * (sg & 1);
+  const int wr = (wave >> 1) * 32, wc = (wave & 1) * 32, li = lane & 15, lk = lane >> 4;
+  aqc::d4_t cr[2][2], ci[2][2];
+  aqc::block_cgemm_tile<false, false, false>(
+      L, K, C, bi, bj, [&](int R, int c) { return xel(R, c); },
+      [&](int c, int k) { return aqc::cscale(lda(W + (size_t)k * C + c), 1.0 / sqrt(sig2[k])); }, lds, lt,
+      bi < L && bj < K, cr, ci);
+#pragma unroll
+  for (int r = 0; r < 2; ++r)
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int row = bi + wr + 16 * r + lk + 4 * q, col = bj + wc + 16 * c + li;
+        if (row < L && col < K) aqc::stg(Y + (size_t)row * 128 + col, aqc::cmk(cr[r][c][q], ci[r][c][q]));
+      }
+  __syncthreads();
+  aqc::block_cgemm_tile<false, false, false>(
+      L, C, K, bi, bj, [&](int R, int k) { return lda(Y + (size_t)R * 128 + k); },
+      [&](int k, int c) { return aqc::cscale(aqc::cconj(lda(W + (size_t)k * C + c)), 1.0 / sqrt(sig2[k])); }, lds,
+      lt, bi < L && bj < C, cr, ci);
+  double acc = 0.0;
+#pragma unroll
+  for (int r = 0; r < 2; ++r)
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int row = bi + wr + 16 * r + lk + 4 * q, col = bj + wc + 16 * c + li;
+        if (row < L && col < C) {
+          const cplx x = xel(row, col);
+          const double dx = x.x - cr[r][c][q], dy = x.y - ci[r][c][q];
+          acc = fma(dx, dx, fma(dy, dy, acc));
+        }
+      }
+  acc = wave_sum_dpp(acc);
+  if (lane == 0) red[tid >> 6] = acc;
+  __syncthreads();
+  double t = 0.0;
+#pragma unroll
+  for (int w = 0; w < 16; ++w) t += red[w];
+  __syncthreads();
+  return t;
+}
+
 // Gram-path SVD of one 2 chi x 2 chi theta'; 1024 threads; `xbuf` = the workgroup's dynamic LDS
 // (>= 4 GemmLds).  Returns false (work untouched beyond scratch, caller runs the Jacobi) when the
 // fast path does not apply.  Uniform in the workgroup.
-__device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
+// Returns 0: declined (the caller runs the register Jacobi), 1: done, 2: done if gram_certified.
+__device__ __noinline__ int gram_svd_body(const TwoSiteJob& j) {
   extern __shared__ double2 xbuf[];
   __shared__ double s_d[128], s_e[128], s_e2[128], s_lam[128], s_err[128], s_sig2[kGramMaxK], s_tail;
-  __shared__ int s_K;
+  __shared__ int s_K, s_cert;
   __shared__ cplx s_tau[128];
   __shared__ double s_lo, s_hi, s_tn;
   __shared__ double2 s_de[128];
@@ -609,7 +681,7 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
   if (tid == 0) atomicAdd(&g_gram_stats[0], 1ull);
   if (C < 4 || C > 128 || L > 128 || j.cap < 64) {
     if (tid == 0) atomicAdd(&g_gram_stats[2], 1ull);
-    return false;
+    return 0;
   }
   const cplx* th = j.theta;
   unsigned long long t_last = tid == 0 ? __builtin_amdgcn_s_memtime() : 0ull;
@@ -1092,13 +1164,13 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
     }
   }
   __syncthreads();
-  if (tid == 0) s_K = aqc::gram_keep(s_lam, s_err, KE, C, j.max_chi, j.thr, s_tn, kGramRelFloor, s_tail);
+  if (tid == 0) s_K = aqc::gram_keep(s_lam, s_err, KE, C, j.max_chi, j.thr, s_tn, kGramRelFloor, s_tail, &s_cert);
   __syncthreads();
   tick(2);
   const int K = s_K;  // (uniform)
   if (K < 0) {  // open decisions / below the floor
     if (tid == 0) atomicAdd(&g_gram_stats[3], 1ull);
-    return false;
+    return 0;
   }
   if (K > kGramNarrowK) {  // (uniform)
     gram_wide(j, hh, C, K, s_d, s_e, s_e2, s_lam, s_tn, s_tau, s_sig2);
@@ -1253,18 +1325,53 @@ __device__ __noinline__ bool gram_svd_body(const TwoSiteJob& j) {
   }  // (K <= 64)
   for (int c = tid; c < C; c += 1024) aqc::stg(j.sig + c, c < K ? sqrt(s_sig2[c]) : 0.0);
   if (tid == 0) aqc::stg(j.sig + kSigTail, s_tail);  // the tail gram_keep dropped (rank_body)
+  tick(5);
+  if (s_cert) return 2;  // (uniform) the caller runs gram_certified
   if (tid == 0) {
     atomicMax(&j.flags[2], 1);
     atomicAdd(&g_gram_stats[1], 1ull);
   }
-  tick(5);
-  return true;
+  return 1;
+}
+
+// After gram_svd_body returned 2 (its kept count assumed the values in CHOP's error band chopped):
+// the certificate on its output (W, sig); true if it holds (the update stands), false if not (the
+// caller runs the register Jacobi, which rewrites W and sig).  A separate call so that neither its
+// accumulators nor the call itself enter the body's register allocation.
+__device__ __noinline__ bool gram_certified(const TwoSiteJob& j) {
+  const int tid = fresh_tid();
+  __shared__ double s_s2[128];
+  __shared__ int s_k;
+  const int M = 2 * j.dims[0], N = 2 * j.dims[2], C = M < N ? M : N;
+  if (tid == 0) s_k = 0;
+  __syncthreads();
+  if (tid < C) {
+    const double sg = aqc::ldg(j.sig + tid);
+    s_s2[tid] = sg * sg;
+    if (sg > 0.0) atomicMax(&s_k, tid + 1);
+  }
+  __syncthreads();
+  if (tid == 0) atomicAdd(&g_gram_stats[4], 1ull);
+  const double cs = gram_cert128(j, C, s_k, s_s2);
+  const bool ok = cs < 0.5 * aqc::kReduceChop;
+  if (tid == 0) {
+    atomicAdd(&g_gram_stats[ok ? 5 : 3], 1ull);
+    if (ok) {
+      atomicMax(&j.flags[2], 1);
+      atomicAdd(&g_gram_stats[1], 1ull);
+    } else {
+      aqc::stg(j.sig + kSigTail, 0.0);  // (the body's tail belongs to its kept count, not the Jacobi's)
+    }
+  }
+  __syncthreads();
+  return ok;
 }
 
 __global__ __launch_bounds__(1024) void k_svd_gram(const TwoSiteJob* __restrict__ jobs) {
   const TwoSiteJob& j = jobs[blockIdx.x];
-  if (!j.gram || !gram_svd_body(j)) {
-    __syncthreads();
-    jacobi_reg_body<128, 8, 16>(j);
-  }
+  const int g = j.gram ? gram_svd_body(j) : 0;
+  if (g == 1) return;
+  __syncthreads();
+  if (g == 2 && gram_certified(j)) return;
+  jacobi_reg_body<128, 8, 16>(j);
 }

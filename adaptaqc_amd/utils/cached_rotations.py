@@ -222,12 +222,12 @@ class SVPrefixBatch(_SweepBase):
         suffix = ops_array(_ops(circ, index + 1, len(circ.data)))
         while len(self.cand) < len(mats):
             self.cand.append(DeviceSV(self.phi.n))
-        out = []
+        # every candidate's replay queued first (each state has its own stream, so the candidates'
+        # passes run side by side: two or more tile workgroups per CU), the <Z_i> read afterwards
         for m, st in zip(mats, self.cand):
             st.copy_from(self.phi)
             st.apply(np.concatenate([ops_array([(m, (q,))]), suffix]))
-            out.append(float(0.5 * (1 - np.mean(st.z_all()))))
-        return out
+        return [float(0.5 * (1 - np.mean(st.z_all()))) for st in self.cand[:len(mats)]]
 
 
 def make_evaluator(compiler):

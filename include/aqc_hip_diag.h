@@ -37,8 +37,10 @@ int aqc_svd_gram_ticks(double* out);
 /* Gram-path counters since the last call (then reset): out[0] two-site SVDs that tried the Gram
    path, out[1] taken, out[2] declined by shape (2 chi != 128), out[3] declined at the
    eigenvalue floor (lambda_K <= 1e-9 lambda_1; the register Jacobi ran instead) or with a
-   reduce_zeros decision the eigenvalues' error bars leave open; K follows reduce_zeros on the
-   eigenvalues (aqc::gram_keep, up to the whole side).  out[4]. */
+   reduce_zeros decision the eigenvalues' error bars leave open, or with a failed certificate;
+   K follows reduce_zeros on the eigenvalues (aqc::gram_keep, up to the whole side).  out[4]
+   rank-deficiency certificates run (values in CHOP's error band assumed chopped, then
+   ||X - X V V^H||_F^2 < CHOP / 2 checked), out[5] passed.  out[6]. */
 int aqc_svd_gram_stats(double* out);
 /* Block Jacobi pair visits (2 chi > 128), shader-clock ticks summed over workgroups since the
  * last call: out[0] Gram, out[1] inner Jacobi sweep, out[2] A V, out[3] visits.  Resets. */

@@ -307,16 +307,26 @@ def test_fused_chain_matches_lockstep_and_oracle(sort):
         circuits.append(ops)
     lists = [device_ops(to_circuit(n, ops)) for ops in circuits]
     L = _lib.lib()
-    res = {}
+    res, stats = {}, {}
     try:
         for fused in (1, 0):
             _lib.check(L.aqc_mps_set_fused_chain(fused))
             st = [DeviceMPS(n, chi, 1e-16, chi) for _ in range(ns)]
+            _lib.gram_stats()
             apply_batch(st, lists, sort=sort)
+            stats[fused] = _lib.gram_stats()
             res[fused] = (overlap_zero_batch(st), [d.dims() for d in st])
     finally:
         _lib.check(L.aqc_mps_set_fused_chain(1))
-    np.testing.assert_allclose(res[1][0], res[0][0], rtol=1e-12, atol=1e-16)
+    # The two paths form theta' with different kernels (the chain's VALU pass, the lock-step MFMA
+    # GEMM), equal to the last bits.  Rank-deficient updates (these |0>-started circuits have many)
+    # keep their values above CHOP's band on the Gram path under the certificate, down to its
+    # floor lambda_K > 1e-9 lambda_1, where the kept subspace carries eps lambda_1 / lambda_K of
+    # error: there last-bit input differences reach the overlaps at ~1e-11, and the paths agree to
+    # the Gram path's accuracy (as each does with the oracle below) instead of bit for bit.
+    assert stats[1]["certificates"] == stats[0]["certificates"], stats
+    tol = 1e-12 if stats[1]["certificates"] == 0 else 1e-9
+    np.testing.assert_allclose(res[1][0], res[0][0], rtol=tol, atol=1e-16)
     for a, b in zip(res[1][1], res[0][1]):
         np.testing.assert_array_equal(a, b)
     for s in (0, 7, 39):

@@ -174,8 +174,13 @@ def test_gram_path_wide_k_vs_numpy(m, n, decay):
 
 @pytest.mark.parametrize("kind", ["graded", "rank10", "zero_tail_cluster"])
 def test_gram_path_declines_to_jacobi(kind):
-    """Where the kept values reach the noise floor of the Gram form (lambda_K <= 1e-9 lambda_1) the
-    path declines and the register Jacobi answers: sigma as the Jacobi contract (_check_sigma)."""
+    """Where kept values reach the noise floor of the Gram form the path declines and the register
+    Jacobi answers: graded (lambda_K <= 1e-9 lambda_1) at once; zero_tail_cluster (120 values of
+    sigma^2 = 1e-12, inside the eigenvalue brackets' band around CHOP) after its certificate
+    (||X - X V V^H||^2 < CHOP / 2) fails.  rank10 (118 exact zeros) passes the certificate and stays
+    on the Gram path.  sigma as the Jacobi contract (_check_sigma) either way."""
+    from adaptaqc_amd import _lib
+
     m = n = 128
     if kind == "graded":
         theta = _theta(m, n, 3)  # 0.8^i columns: sigma_64 / sigma_1 ~ 1e-6
@@ -184,9 +189,14 @@ def test_gram_path_declines_to_jacobi(kind):
     else:
         s = np.concatenate([np.ones(8), 1e-6 * np.ones(120)])
         theta = _spectrum_theta(m, n, s, 5)
-    _gram_ticks()
+    _lib.gram_stats()
     w, sig, _, _ = _run(theta, 7)
-    assert _gram_ticks()[4] == 0, "the Gram path should have declined"
+    st = _lib.gram_stats()
+    if kind == "rank10":
+        assert st["taken"] == 1 and st["certificates"] == 1 and st["certified"] == 1, st
+    else:
+        assert st["taken"] == 0 and st["declined_floor"] == 1, st
+        assert st["certificates"] == (1 if kind == "zero_tail_cluster" else 0) and st["certified"] == 0, st
     _check_sigma(sig, np.linalg.svd(theta, compute_uv=False))
 
 

@@ -147,6 +147,37 @@ def test_rank_deficient_two_site_block_certificate(tiny):
         assert big["declined_certificate"] >= 1, big
 
 
+def _deficient_state_128(seed, tiny):
+    """14 qubits with bonds ... 32 64 | 32 | 64 32 ...: the two-site block of sites (6, 7) is 128 x 128
+    (the 1024-thread Gram path) with rank <= 2 x 32 after a CNOT; tiny as in _deficient_state."""
+    rng = np.random.default_rng(seed)
+    dims = [1, 2, 4, 8, 16, 32, 64, 32, 64, 32, 16, 8, 4, 2, 1]
+    A = [rng.standard_normal((2, dims[i], dims[i + 1])) + 1j * rng.standard_normal((2, dims[i], dims[i + 1]))
+         for i in range(14)]
+    if tiny is not None:
+        A[6][:, :, -4:] *= tiny
+    return bench.vidal_from_tensors(A)
+
+
+@pytest.mark.parametrize("tiny", [None, 1e-4], ids=["exact-zeros", "tiny-values"])
+def test_rank_deficient_two_site_block_certificate_128(tiny):
+    """The same at 2 chi = 128 (gram_svd_body / gram_certified): 64 of the 128 values are exact zeros
+    (or, with tiny, four of the kept ones sit inside the Gram form's noise band), the kept count
+    assumes the open ones chopped and ||X - X V V^H||_F^2 < CHOP / 2 certifies it -- or fails, and the
+    register Jacobi decides.  Exact bond dimensions and fidelity 1e-6 against the oracle."""
+    n = 14
+    aer = _deficient_state_128(43, tiny)
+    rng = np.random.default_rng(6)
+    ops = [("rz", (6,), (rng.uniform(-3, 3),)), ("rz", (7,), (rng.uniform(-3, 3),)), ("cx", (6, 7), ()),
+           ("ry", (6,), (rng.uniform(-3, 3),)), ("ry", (7,), (rng.uniform(-3, 3),))]
+    g, _ = _run_batch_thr(n, 64, None, [aer], [(0, ops)], 1e-16)
+    assert g["certificates"] >= 1, g
+    if tiny is None:
+        assert g["certified"] >= 1 and g["taken"] >= 1, g
+    else:
+        assert g["certified"] < g["certificates"], g
+
+
 def _run_batch_thr(n, cap, max_chi, states, layers, thr):
     global THR
     old, THR = THR, thr

@@ -103,7 +103,40 @@ def config2(reps):
     if fl["frac"] > roof["frac"]:
         roof["bound_note"] = "FP64 arithmetic of the fused gates exceeds the HBM fraction (MALL-resident state)"
     gates = float(np.mean([len(c) for c in circuits]))
+    # Independent evaluations side by side (Rotoselect candidates, several compiles): B state
+    # vectors, each on its own stream, the B circuits' passes in flight together (two tile
+    # workgroups per CU: two waves per SIMD) -- reported beside the one-at-a-time rate, checked
+    # against it value for value.
+    conc = {}
+    seq_costs = []
+    for ops in circuits:
+        sv.reset()
+        sv.apply(ops)
+        seq_costs.append(1.0 - abs(sv.amp0()) ** 2)
+    for B in (2, 4):
+        svs = [DeviceSV(n) for _ in range(B)]
+
+        def run_b():
+            n_ev, costs = 0, []
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                for g in range(0, len(circuits), B):
+                    grp = circuits[g:g + B]
+                    for st, ops in zip(svs, grp):
+                        st.reset()
+                        st.apply(ops)
+                    for st, _ in zip(svs, grp):
+                        costs.append(1.0 - abs(st.amp0()) ** 2)
+                        n_ev += 1
+            return n_ev, time.perf_counter() - t0, costs
+
+        run_b()
+        nb, elb, costs = run_b()
+        same = float(np.max(np.abs(np.array(costs[:len(circuits)]) - np.array(seq_costs))))
+        conc[f"streams_{B}"] = {"evals_per_s": nb / elb, "max_abs_diff_vs_one_at_a_time": same}
+        del svs
     return {"metric": "SV evaluate_global_cost evals/sec, 20 qubits (config 2)", "value": evals / el,
+            "concurrent": conc,
             "unit": "evals/s", "ms_per_eval": 1e3 * el / evals, "dtype": "c128", "data": "synthetic",
             "config": {"workload": "config2: 20-qubit brickwork depth 20 (seeds 0-9) + 0/10/50 thin layers; "
                                    "full re-simulation from |0> + amp0 per eval", "n_qubits": n,
