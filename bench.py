@@ -49,10 +49,15 @@ HBM_PEAK_GBS = 8000.0
 # HBM traffic and executed FP64 work of k_chain per two-site update from the committed PMC passes
 # of this round's code (tools/pmc_bench.sh, tools/pmc_exec.py); the previous round's as fallback
 def _latest_profile(suffix):
-    for r in ("r4", "r3", "r2"):
-        if os.path.exists(os.path.join(ROOT, "profiles", f"{r}_{suffix}")):
-            return f"{r}_{suffix}"
-    return f"r2_{suffix}"
+    """The newest round's committed PMC result (profiles/rN_<suffix>, highest N)."""
+    import re
+
+    rounds = []
+    for f in os.listdir(os.path.join(ROOT, "profiles")):
+        m = re.fullmatch(r"r(\d+)_" + re.escape(suffix), f)
+        if m:
+            rounds.append(int(m.group(1)))
+    return f"r{max(rounds)}_{suffix}" if rounds else f"r2_{suffix}"
 
 
 TRAFFIC_JSON = _latest_profile("traffic.json")
