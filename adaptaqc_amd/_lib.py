@@ -35,7 +35,7 @@ EXPORTS = (
     "aqc_mps_set_jacobi_tol", "aqc_mps_set_jacobi_stop", "aqc_mps_set_fused_chain", "aqc_mps_chain_ticks", "aqc_svd_debug",
     "aqc_sv_pair_rdms", "aqc_mps_pair_rdms", "aqc_mps_pair_rdms_batch", "aqc_entanglement_measures",
     "aqc_sv_transition", "aqc_mps_product_fit", "aqc_mps_set_svd_path", "aqc_svd_gram_ticks", "aqc_bj_ticks",
-    "aqc_sweep_set_chain_mode", "aqc_stream_join", "aqc_stream_wait", "aqc_svd_gram_stats",
+    "aqc_sweep_set_chain_mode", "aqc_stream_join", "aqc_stream_wait", "aqc_svd_gram_stats", "aqc_env_ticks",
     "aqc_comm_unique_id", "aqc_comm_init", "aqc_comm_destroy", "aqc_comm_rank", "aqc_allgather_f64",
     "aqc_allgather_f64_host", "aqc_allreduce_max_f64", "aqc_svd_gram_big_stats", "aqc_svd_gram_big_ticks",
     "aqc_gb_set_spin_limit", "aqc_gb_set_tail", "aqc_debug_hog", "aqc_pool_stats",
@@ -118,6 +118,7 @@ _SIGS = {
     "aqc_stream_join": ([_P], _I),
     "aqc_stream_wait": ([_P], _I),
     "aqc_svd_gram_stats": ([_P], _I),
+    "aqc_env_ticks": ([_P], _I),
     "aqc_comm_unique_id": ([ctypes.c_char_p], _I),
     "aqc_comm_init": ([ctypes.c_char_p, _I, _I, ctypes.POINTER(_P)], _I),
     "aqc_comm_destroy": ([_P], _I),

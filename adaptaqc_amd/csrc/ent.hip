@@ -205,6 +205,10 @@ __device__ __forceinline__ void narrow_cgemm(int m, int n, int k, FA a, FB b, FS
   }
 }
 
+// shader-clock ticks of workgroup (0, 0, 0)'s steps (aqc_env_ticks): T, the new environment's
+// columns, the hand-off; then the steps counted
+__device__ unsigned long long g_env_ticks[4];
+
 // grid (kEnvNW, 2 directions, states), kT threads; CW = cap / kEnvNW output columns per workgroup.
 // Counters: cnt[32 (2 state + dir)] (zeroed by the host).
 template <int CW>
@@ -227,6 +231,15 @@ __global__ __launch_bounds__(kT) void k_env_split(const RdmJob* __restrict__ job
       else j.Renv[(size_t)n * cc] = aqc::cmk(1, 0);
     }
   }
+  const bool tk = tid == 0 && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0;
+  unsigned long long t_last = tk ? __builtin_amdgcn_s_memtime() : 0ull, acc[3] = {0, 0, 0};
+  auto tick = [&](int ph) {
+    if (tk) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      acc[ph] += t - t_last;
+      t_last = t;
+    }
+  };
   for (int step = 0; step < n - 1; ++step) {
     if (dir == 0) {
       const int i = step, cl = j.dims[i], cr = j.dims[i + 1];
@@ -239,6 +252,7 @@ __global__ __launch_bounds__(kT) void k_env_split(const RdmJob* __restrict__ job
           },
           [&](int l, int c2, cplx v) { Tw[(size_t)l * 2 * CW + c2] = v; }, lds);
       __syncthreads();
+      tick(0);
       cplx* Ln = j.Lenv + (size_t)(i + 1) * cc;
       narrow_cgemm<NB2, false, false>(
           cr, min(CW, cr - c0), 2 * cl,
@@ -257,6 +271,7 @@ __global__ __launch_bounds__(kT) void k_env_split(const RdmJob* __restrict__ job
           },
           [&](int k, int c2, cplx v) { Tw[(size_t)k * 2 * CW + c2] = v; }, lds);
       __syncthreads();
+      tick(0);
       cplx* Rn = j.Renv + (size_t)i * cc;
       // R_i[l][c0 + c] = sum_{t, k} A_t[l][k] T[k][t CW + c]
       narrow_cgemm<NB2, true, false>(
@@ -265,6 +280,7 @@ __global__ __launch_bounds__(kT) void k_env_split(const RdmJob* __restrict__ job
           [&](int kk, int c) { const int t = kk / cr, k = kk % cr; return Tw[(size_t)k * 2 * CW + t * CW + c]; },
           [&](int l, int c, cplx v) { env_st(Rn + (size_t)l * cap + c0 + c, v); }, lds);
     }
+    tick(1);
     // hand-off: every workgroup's columns of the new environment stored before the count
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -282,7 +298,12 @@ __global__ __launch_bounds__(kT) void k_env_split(const RdmJob* __restrict__ job
       }
     }
     __syncthreads();
+    tick(2);
     if (s_abort) return;
+  }
+  if (tk) {
+    for (int ph = 0; ph < 3; ++ph) atomicAdd(&g_env_ticks[ph], acc[ph]);
+    atomicAdd(&g_env_ticks[3], (unsigned long long)(n - 1));
   }
 }
 
@@ -785,6 +806,16 @@ int aqc_mps_z_all_batch(aqc_mps_t* hs, int ns, double* out) {
   AQC_HIP_CHECK(hipMemcpyAsync(out, dout, (size_t)ns * n * sizeof(double), hipMemcpyDeviceToHost, st));
   AQC_HIP_CHECK(hipStreamSynchronize(st));
   return env_check(dsync, ns, cap);
+}
+
+int aqc_env_ticks(double* out) {
+  AQC_REQUIRE(out, "aqc_env_ticks: null argument");
+  unsigned long long t[4];
+  AQC_HIP_CHECK(hipMemcpyFromSymbol(t, HIP_SYMBOL(g_env_ticks), sizeof(t)));
+  for (int i = 0; i < 4; ++i) out[i] = (double)t[i];
+  unsigned long long z[4] = {0, 0, 0, 0};
+  AQC_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_env_ticks), z, sizeof(z)));
+  return AQC_OK;
 }
 
 int aqc_mps_pair_rdms(aqc_mps_t h, const int* pairs, int npairs, double* out) {

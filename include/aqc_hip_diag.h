@@ -42,6 +42,11 @@ int aqc_svd_gram_ticks(double* out);
    rank-deficiency certificates run (values in CHOP's error band assumed chopped, then
    ||X - X V V^H||_F^2 < CHOP / 2 checked), out[5] passed.  out[6]. */
 int aqc_svd_gram_stats(double* out);
+/* The four-workgroup environment chains (z_all / pair RDMs at capacities in multiples of 64):
+   shader-clock ticks of one workgroup summed over its steps since the last call -- out[0] the
+   T product, out[1] its columns of the new environment, out[2] the hand-off -- and out[3] the
+   steps counted.  Resets. */
+int aqc_env_ticks(double* out);
 /* Block Jacobi pair visits (2 chi > 128), shader-clock ticks summed over workgroups since the
  * last call: out[0] Gram, out[1] inner Jacobi sweep, out[2] A V, out[3] visits.  Resets. */
 int aqc_bj_ticks(double* out);
