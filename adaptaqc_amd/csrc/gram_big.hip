@@ -62,6 +62,8 @@ constexpr unsigned long long kSpinTicks = 10000000ull;  // s_memrealtime (100 MH
 unsigned long long g_gb_spin = kSpinTicks;
 // the trailing 128 columns in one workgroup (aqc_gb_set_tail; -1: from AQC_GB_TAIL, default on)
 int g_gb_tail = -1;
+// two exchange stages at 2 chi = 512 (-1: from AQC_GB_STAGES, default 2)
+int g_gb_stages = -1;
 
 typedef __attribute__((address_space(1))) double gdbl;
 typedef __attribute__((address_space(1))) unsigned gu32;
@@ -96,7 +98,9 @@ struct GBArgs {
   int* cert;       // per job: the decision assumed the open-CHOP values chopped (k_gb_cert checks)
   double* certsum; // per job: ||X - X V V^H||_F^2 (k_gb_cert)
   double* tn;      // per job: ||T|| (Gershgorin)
-  cplx* xch;       // per job 4 x CT: p (two buffers), old row k + 1 (two buffers)
+  cplx* xch;       // per job 8 x CT: p (two buffers), old row k + 1 (two buffers); from 4 CT the
+                   // hand-off to the next stage (v, v', w, the scalars: apart from the exchange
+                   // buffers, which a slower workgroup may still be reading when workgroup 0 ends)
   unsigned* cnt;   // per job 32 words (128 B)
   int* status;     // per job: 0 ok, 1 declined (gram off / shape), 2 floor, 3 exchange timeout
   unsigned long long spin;  // counter-wait limit (s_memrealtime ticks, 100 MHz) before a timeout
@@ -210,6 +214,16 @@ __device__ __forceinline__ double lane_sum(double v) {
   return v;
 }
 
+// sum of f(0) .. f(N - 1) as a balanced tree (log2 N dependent adds instead of N - 1)
+template <int N, class F>
+__device__ __forceinline__ double tree_sum(F f) {
+  if constexpr (N == 1) {
+    return f(0);
+  } else {
+    return tree_sum<N / 2>(f) + tree_sum<N - N / 2>([&](int w) { return f(w + N / 2); });
+  }
+}
+
 // zlarfg with the divisions as reciprocals (rcp + two Newton steps: full precision)
 __device__ __forceinline__ void zlarfg_f(cplx alpha, double xn2, cplx& tau, double& beta, cplx& scale) {
   if (xn2 == 0.0 && alpha.y == 0.0) {
@@ -242,11 +256,23 @@ __device__ __forceinline__ void zlarfg_f(cplx alpha, double xn2, cplx& tau, doub
 //             w_{k+1} conj(v), its norm below the subdiagonal (a second reduction); wave 0 alone
 //             forms reflector k + 1 (zlarfg's scalars and v into the LDS; in every wave the
 //             redundant scalar chain cost 4x its issue)
-template <int CT, int RPL, bool TAIL>
+//
+// Stages (CF: the job's size; CT: the trailing block this launch starts from, K0 = CF - CT; TS: the
+// trailing block it hands off, with TAIL): CF = CT = 512 runs columns 0 .. 255 over 16 workgroups
+// and hands the trailing 256 over to CT = 256 (4 workgroups, columns 256 .. 383, from the hand-off
+// of reflector 255: its deferred update, v_256 and its scalars), which hands the last 128 to
+// k_gb_tail.  A job's workgroups then fall from 16 to 4 for the second stage, so one round's
+// second stages run beside the next round's first (the columns in the exchange per wave of rounds:
+// 256 + 256 + 128 instead of 384 + 384).
+template <int CT, int RPL, bool TAIL, int CF = CT, int TS = 128>
 __global__ __launch_bounds__(1024) void k_gb_tridiag(const TwoSiteJob* __restrict__ jobs, GBArgs a, int job0) {
+  constexpr int K0 = CF - CT;
+  static_assert(K0 >= 0 && TS >= 128 && TS < CT, "stage sizes");
   constexpr int CPL = 16 / RPL, TPG = CT / CPL;
   constexpr int R = RPL * (1024 / TPG), P = CT / R;
   static_assert(TPG <= 64 && TPG >= 16, "row group inside one wave");
+  // waves holding entries of the CT-long vectors (the others' partial sums are zero)
+  constexpr int kRW = CT / 64 < 16 ? CT / 64 : 16;
   const int jb = job0 + (int)blockIdx.x / P, g = (int)blockIdx.x % P;
   if (*(const gi32*)(a.status + jb) != 0) return;  // uniform over the job's workgroups
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -256,16 +282,18 @@ __global__ __launch_bounds__(1024) void k_gb_tridiag(const TwoSiteJob* __restric
   for (int u = 0; u < RPL; ++u) rr[u] = (grp * RPL + u) * P + g;
   // (phase ticks on the last wave: its rows stay active to the end)
   const bool tick = jb == 0 && g == 0 && tid == 960;
-  cplx* G = a.G + (size_t)jb * CT * CT;
-  double* dd = a.d + (size_t)jb * CT;
-  double* ee = a.e + (size_t)jb * CT;
-  cplx* tt = a.tau + (size_t)jb * CT;
-  cplx* xch = a.xch + (size_t)jb * 4 * CT;
-  unsigned* cnt = a.cnt + (size_t)jb * 32;
+  // (local indices: the stage's trailing block starts at row / column K0 of the job's G)
+  cplx* G = a.G + (size_t)jb * CF * CF + (size_t)K0 * CF + K0;
+  double* dd = a.d + (size_t)jb * CF + K0;
+  double* ee = a.e + (size_t)jb * CF + K0;
+  cplx* tt = a.tau + (size_t)jb * CF + K0;
+  cplx* xch = a.xch + (size_t)jb * 8 * CF;
+  cplx* hoff = xch + 4 * CF;  // the stage hand-off
+  unsigned* cnt = a.cnt + (size_t)jb * 32 + (K0 ? 16 : 0);  // (a second stage: its own 64-byte line)
   __shared__ cplx vL[2][CT], wL[CT], rhoL[CT];
   __shared__ double redd[16];
   __shared__ cplx redc[16];
-  __shared__ cplx s_tau;
+  __shared__ cplx s_tau, s_pk1;
   __shared__ double s_beta, s_dk;
   __shared__ int s_abort;
   // phase ticks of job 0's first workgroup, thread 0 (kept in the LDS: per-lane counters would take
@@ -286,19 +314,31 @@ __global__ __launch_bounds__(1024) void k_gb_tridiag(const TwoSiteJob* __restric
 #pragma unroll
   for (int u = 0; u < RPL; ++u)
 #pragma unroll
-    for (int i = 0; i < CPL; ++i) A[u][i] = ldg(G + (size_t)rr[u] * CT + q + TPG * i);
-  if (tid < CT) {
-    rhoL[tid] = ldg(G + tid);  // row 0
-    wL[tid] = cmk(0, 0);       // no deferred update before column 0
-    vL[1][tid] = cmk(0, 0);
+    for (int i = 0; i < CPL; ++i) A[u][i] = ldg(G + (size_t)rr[u] * CF + q + TPG * i);
+  if constexpr (K0 == 0) {
+    if (tid < CT) {
+      rhoL[tid] = ldg(G + tid);  // row 0
+      wL[tid] = cmk(0, 0);       // no deferred update before column 0
+      vL[1][tid] = cmk(0, 0);
+    }
+  } else {  // the previous stage's hand-off (K0 even: v_K0 in vL[0])
+    if (tid < CT) {
+      vL[0][tid] = ldg(hoff + K0 + tid);
+      vL[1][tid] = ldg(hoff + CF + K0 + tid);
+      wL[tid] = ldg(hoff + 2 * CF + K0 + tid);
+    }
+    if (tid == 0) {
+      s_tau = ldg(hoff + 3 * CF);
+      const cplx bd = ldg(hoff + 3 * CF + 1);
+      s_beta = bd.x;
+      s_dk = bd.y;
+    }
   }
   if (tid == 0) s_abort = 0;
   // reflector k from rhoL = row k and the partial norms in redd, by wave 0 alone: zlarfg's scalars
   // and v_k (1 at k + 1, conj(rho_k[c]) scale below, 0 above) into vL[k & 1]
   auto reflector = [&](int k) {
-    double xn2 = 0.0;
-#pragma unroll
-    for (int w = 0; w < 16; ++w) xn2 += redd[w];
+    double xn2 = tree_sum<kRW>([&](int w) { return redd[w]; });
     cplx tau_, sc;
     double beta;
     zlarfg_f(cconj(rhoL[k + 1]), xn2, tau_, beta, sc);
@@ -320,7 +360,7 @@ __global__ __launch_bounds__(1024) void k_gb_tridiag(const TwoSiteJob* __restric
     }
   };
   __syncthreads();
-  {
+  if constexpr (K0 == 0) {
     const cplx xt = tid < CT ? cconj(rhoL[tid]) : cmk(0, 0);
     const double part = lane_sum<64>((tid >= 2 && tid < CT) ? cnorm2(xt) : 0.0);
     if (lane == 0) redd[wave] = part;
@@ -328,8 +368,8 @@ __global__ __launch_bounds__(1024) void k_gb_tridiag(const TwoSiteJob* __restric
     if (wave == 0) reflector(0);
     __syncthreads();
   }
-  // with TAIL the loop stops at kt = CT - 128: the trailing 128 columns run in k_gb_tail
-  int kt = TAIL ? CT - 128 : CT - 1;
+  // with TAIL the loop stops at kt = CT - TS: the trailing TS columns run in the next stage
+  int kt = TAIL ? CT - TS : CT - 1;
   asm volatile("" : "+s"(kt));  // (opaque: a constant trip count spilled the register tile)
   for (int k = 0; k < kt; ++k) {
     const int cur = k & 1, prv = cur ^ 1;
@@ -402,7 +442,7 @@ __global__ __launch_bounds__(1024) void k_gb_tridiag(const TwoSiteJob* __restric
     // workgroup published column 0, i.e. passed its entry loads.  From k = 1 on this workgroup has
     // already seen step k - 1's full count, so every workgroup is past its entry.
     const bool own_row = tid > k && tid / (CT / P) == g;
-    if (k > 0 && own_row) stg(G + (size_t)k * CT + tid, vt);
+    if (k > 0 && own_row) stg(G + (size_t)k * CF + tid, vt);
     __syncthreads();
     if (k == 0 && own_row && !s_abort) stg(G + tid, vt);
     if (s_abort) {
@@ -415,16 +455,19 @@ __global__ __launch_bounds__(1024) void k_gb_tridiag(const TwoSiteJob* __restric
     tmark(2);
     const cplx pt = tid < CT ? ld_sc1(xp + tid) : cmk(0, 0);
     const cplx ro = tid < CT ? ld_sc1(xr + tid) : cmk(0, 0);
-    const cplx pk1 = ld_sc1(xp + k + 1);
+    // p_{k+1} to every thread through the LDS (one sc1 load of the same 16 bytes by every wave of
+    // every workgroup queued at one memory channel)
+    if (tid == k + 1) s_pk1 = pt;
     const cplx pvp = cconjmul(pt, vt);
     const double px = lane_sum<64>(pvp.x), py = lane_sum<64>(pvp.y);
     if (lane == 0) redc[wave] = cmk(px, py);
     __syncthreads();
+    const cplx pk1 = s_pk1;
     tmark(3);
     // ---- w = p - tau / 2 (p^H v) v, the new row k + 1 and its norm below the subdiagonal
     cplx pv = cmk(0, 0);
 #pragma unroll
-    for (int w = 0; w < 16; ++w) pv = cadd(pv, redc[w]);
+    for (int w = 0; w < kRW; ++w) pv = cadd(pv, redc[w]);
     const cplx a2 = cscale(cmul(tau, pv), -0.5);
     const cplx wt = cfma(a2, vt, pt);
     const cplx wk1 = cadd(pk1, a2);
@@ -455,19 +498,19 @@ __global__ __launch_bounds__(1024) void k_gb_tridiag(const TwoSiteJob* __restric
 #pragma unroll
         for (int i = 0; i < CPL; ++i) {
           const int c = q + TPG * i;
-          if (TPG * i + TPG - 1 >= kt && c >= kt) stg(G + (size_t)rr[u] * CT + c, A[u][i]);
+          if (TPG * i + TPG - 1 >= kt && c >= kt) stg(G + (size_t)rr[u] * CF + c, A[u][i]);
         }
       }
     }
     if (g == 0) {
       if (tid < CT) {
-        stg(xch + tid, vL[0][tid]);
-        stg(xch + CT + tid, vL[1][tid]);
-        stg(xch + 2 * CT + tid, wL[tid]);
+        stg(hoff + K0 + tid, vL[0][tid]);
+        stg(hoff + CF + K0 + tid, vL[1][tid]);
+        stg(hoff + 2 * CF + K0 + tid, wL[tid]);
       }
       if (tid == 0) {
-        stg(xch + 3 * CT, s_tau);
-        stg(xch + 3 * CT + 1, cmk(s_beta, s_dk));
+        stg(hoff + 3 * CF, s_tau);
+        stg(hoff + 3 * CF + 1, cmk(s_beta, s_dk));
       }
     }
   }
@@ -504,7 +547,7 @@ __global__ __launch_bounds__(1024) void k_gb_tail(const TwoSiteJob* __restrict__
   double* dd = a.d + (size_t)jb * CT;
   double* ee = a.e + (size_t)jb * CT;
   cplx* tt = a.tau + (size_t)jb * CT;
-  const cplx* xch = a.xch + (size_t)jb * 4 * CT;
+  const cplx* xch = a.xch + (size_t)jb * 8 * CT + 4 * CT;  // the previous stage's hand-off
   __shared__ cplx vL[2][NT], wL[NT], pL[NT], roL[NT];
   __shared__ cplx s_tau;
   __shared__ double s_beta, s_dk;
@@ -1277,7 +1320,7 @@ int gb_ensure(GBBuffers& b, int ct, int nj, hipStream_t st) {
   AQC_HIP_CHECK(hipMalloc(&b.tfac, (size_t)(c / 16) * 256 * n * sizeof(cplx)));
   AQC_HIP_CHECK(hipMalloc(&b.yc, cc * sizeof(cplx)));
   AQC_HIP_CHECK(hipMalloc(&b.tau, (size_t)c * n * sizeof(cplx)));
-  AQC_HIP_CHECK(hipMalloc(&b.xch, (size_t)4 * c * n * sizeof(cplx)));
+  AQC_HIP_CHECK(hipMalloc(&b.xch, (size_t)8 * c * n * sizeof(cplx)));
   AQC_HIP_CHECK(hipMalloc(&b.cnt, (size_t)32 * n * sizeof(unsigned)));
   AQC_HIP_CHECK(hipMalloc(&b.status, (size_t)n * sizeof(int)));
   AQC_HIP_CHECK(hipMalloc(&b.djobs, (size_t)n * sizeof(TwoSiteJob)));
@@ -1292,11 +1335,14 @@ int gb_ensure(GBBuffers& b, int ct, int nj, hipStream_t st) {
 // only by these events, so they must be drained before the runtime tears down.
 hipStream_t g_gb_side[64] = {nullptr};
 hipStream_t g_gb_side2[64] = {nullptr};  // the compact-WY factors beside the eigenpairs
+hipStream_t g_gb_side3[64] = {nullptr};  // a round's eigenpairs beside the next round's second stage
 std::vector<hipEvent_t> g_gb_events;
 void release_gb_sync() {
   for (auto& s : g_gb_side)
     if (s) (void)hipStreamDestroy(s), s = nullptr;
   for (auto& s : g_gb_side2)
+    if (s) (void)hipStreamDestroy(s), s = nullptr;
+  for (auto& s : g_gb_side3)
     if (s) (void)hipStreamDestroy(s), s = nullptr;
   for (hipEvent_t e : g_gb_events) (void)hipEventDestroy(e);
   g_gb_events.clear();
@@ -1305,7 +1351,7 @@ void release_gb_sync() {
 hipStream_t gb_side_stream(int which = 0) {
   int dev = 0;
   (void)hipGetDevice(&dev);
-  hipStream_t* tab = which ? g_gb_side2 : g_gb_side;
+  hipStream_t* tab = which == 2 ? g_gb_side3 : which ? g_gb_side2 : g_gb_side;
   if (!tab[dev]) {
     (void)hipStreamCreateWithFlags(&tab[dev], hipStreamNonBlocking);
     aqc::on_finalize(release_gb_sync);
@@ -1356,7 +1402,15 @@ int run_gram_big(const TwoSiteJob* hjobs, const TwoSiteJob* jobs, int nj, int ca
     AQC_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_gb_tridiag<CT, 1, true>, 1024, 0));
     resident = ncu * std::min(per_cu, 1);
   }
-  const int per_round = std::min(240, resident) / P;
+  if (g_gb_stages < 0) {
+    const char* e = std::getenv("AQC_GB_STAGES");
+    g_gb_stages = (e && std::strcmp(e, "1") == 0) ? 1 : 2;
+  }
+  constexpr bool kCan2 = CT == 512;
+  const bool two = kCan2 && g_gb_tail && g_gb_stages == 2;
+  // (two stages: a round's first stage runs beside the previous round's second, P + P / 4
+  // workgroups per job resident together)
+  const int per_round = std::min(240, resident) / (two ? P + P / 4 : P);
   // the eigenpairs and back-transformation of a round's jobs run on a second stream, beside the next
   // round's tridiagonalisation (which leaves CUs free: 9 of 24 config-5 jobs hold 144 of 256)
   hipStream_t s2 = gb_side_stream();
@@ -1400,9 +1454,15 @@ int run_gram_big(const TwoSiteJob* hjobs, const TwoSiteJob* jobs, int nj, int ca
     rc = post(st, 0, nj);
     if (rc != AQC_OK) return rc;
   } else {
+    // 2 chi = 512 with the tail: two exchange stages (k_gb_tridiag's comment); a round's second
+    // stage and tail on s2, its eigenpairs and back-transformation on s4, so that the next round's
+    // second stage does not queue behind them
+    hipStream_t s4 = two ? gb_side_stream(2) : s2;
     for (int j0 = 0; j0 < nj; j0 += per_round) {
       const int nr = std::min(per_round, nj - j0);
-      if (g_gb_tail)
+      if (two)
+        hipLaunchKernelGGL((k_gb_tridiag<CT, 1, true, CT, (kCan2 ? CT / 2 : 128)>), dim3(P * nr), dim3(1024), 0, st, jobs, a, j0);
+      else if (g_gb_tail)
         hipLaunchKernelGGL((k_gb_tridiag<CT, 1, true>), dim3(P * nr), dim3(1024), 0, st, jobs, a, j0);
       else
         hipLaunchKernelGGL((k_gb_tridiag<CT, 1, false>), dim3(P * nr), dim3(1024), 0, st, jobs, a, j0);
@@ -1410,15 +1470,25 @@ int run_gram_big(const TwoSiteJob* hjobs, const TwoSiteJob* jobs, int nj, int ca
       hipEvent_t ev = gb_event(evi++);
       AQC_HIP_CHECK(hipEventRecord(ev, st));
       AQC_HIP_CHECK(hipStreamWaitEvent(s2, ev, 0));
+      if (two) {
+        constexpr int CH = kCan2 ? CT / 2 : CT;
+        hipLaunchKernelGGL((k_gb_tridiag<CH, 1, true, CT, 128>), dim3(CH * CH / 16384 * nr), dim3(1024), 0, s2, jobs, a, j0);
+        AQC_CHECK_LAUNCH();
+      }
       if (g_gb_tail) {
         hipLaunchKernelGGL((k_gb_tail<CT>), dim3(nr), dim3(1024), 0, s2, jobs, a, j0);
         AQC_CHECK_LAUNCH();
       }
-      rc = post(s2, j0, nr);
+      if (two) {
+        hipEvent_t e2 = gb_event(evi++);
+        AQC_HIP_CHECK(hipEventRecord(e2, s2));
+        AQC_HIP_CHECK(hipStreamWaitEvent(s4, e2, 0));
+      }
+      rc = post(s4, j0, nr);
       if (rc != AQC_OK) return rc;
     }
     hipEvent_t done = gb_event(evi++);
-    AQC_HIP_CHECK(hipEventRecord(done, s2));
+    AQC_HIP_CHECK(hipEventRecord(done, s4));
     AQC_HIP_CHECK(hipStreamWaitEvent(st, done, 0));
   }
   AQC_HIP_CHECK(hipMemcpyAsync(b.host_status, b.status, (size_t)nj * sizeof(int), hipMemcpyDeviceToHost, st));
@@ -1492,5 +1562,12 @@ extern "C" int aqc_gb_set_spin_limit(double us) {
 extern "C" int aqc_gb_set_tail(int on) {
   AQC_REQUIRE(on == 0 || on == 1, "aqc_gb_set_tail: on must be 0 or 1");
   aqc::g_gb_tail = on;
+  return AQC_OK;
+}
+
+/* 2 chi = 512 with the tail: the exchange in two stages (2, the default) or one (1). */
+extern "C" int aqc_gb_set_stages(int n) {
+  AQC_REQUIRE(n == 1 || n == 2, "aqc_gb_set_stages: n must be 1 or 2");
+  aqc::g_gb_stages = n;
   return AQC_OK;
 }

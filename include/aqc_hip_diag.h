@@ -75,6 +75,10 @@ int aqc_gb_set_spin_limit(double us);
    trailing block goes to the job's first workgroup, which finishes without the per-column
    exchange), or over all of the job's workgroups to the end (on = 0).  AQC_GB_TAIL=0 also selects 0. */
 int aqc_gb_set_tail(int on);
+/* With the tail at 2 chi = 512: columns 0 .. 255 over the job's 16 workgroups, then 256 .. 383 over
+   4 (n = 2, the default: a round's second stage runs beside the next round's first), or 0 .. 383
+   over 16 (n = 1).  AQC_GB_STAGES=1 also selects 1. */
+int aqc_gb_set_stages(int n);
 /* Test load: nblocks 256-thread workgroups on a private stream, block b spinning (b % 16 + 1) / 16
    of `ms` milliseconds, so work queued on other streams starts one CU at a time.  Asynchronous. */
 int aqc_debug_hog(int nblocks, double ms);

@@ -187,6 +187,32 @@ def test_gram_big_late_workgroup_start(gb_tail):
     _vs_oracle(d, n, chi, ops, chi + 4)
 
 
+def test_gram_big_two_stages_equal_one_stage():
+    """Config 5's state, 16 disjoint updates at 2 chi = 512 (two rounds: a round's second stage
+    beside the next round's first) with the exchange in two stages (16 then 4 workgroups per job)
+    and in one: the same bond dimensions and Schmidt values within 1e-12 (the stages differ only in
+    the lane grouping of the row sums)."""
+    from adaptaqc_amd import _lib
+
+    n, chi = 100, 256
+    rng = np.random.default_rng(17)
+    ops = _gates(n, rng, [(a, a + 1) for a in range(34, 66, 2)])
+    res = []
+    for stages in (2, 1):
+        _lib.check(_lib.load().aqc_gb_set_stages(stages))
+        try:
+            d, st = _run(n, chi, ops, seed=6)
+        finally:
+            _lib.check(_lib.load().aqc_gb_set_stages(2))
+        assert st["taken"] == 16 and st["timeouts"] == 0, st
+        res.append(d)
+    np.testing.assert_array_equal(res[0].dims(), res[1].dims())
+    _, l0 = res[0].to_aer()
+    _, l1 = res[1].to_aer()
+    for x, y in zip(l0, l1):
+        np.testing.assert_allclose(x, y, atol=1e-12)
+
+
 def test_gram_big_tail_equals_exchange_to_end():
     """Config 5's state, 8 disjoint updates at 2 chi = 512 with the single-workgroup tail and with
     the exchange to the end: the same arithmetic on the same data, so the same bond dimensions and
