@@ -307,6 +307,188 @@ __global__ __launch_bounds__(kT) void k_env_split(const RdmJob* __restrict__ job
   }
 }
 
+// ---- the chains at capacity 64 (chi = 64: the local-cost and entanglement workloads) -----------
+// k_env_split's steps are latency-bound, not matrix-core-bound (tools/env_probe.py: ~56 K ticks a
+// step against ~16 K of MFMA issue): every 32-deep k tile goes through the LDS behind two barriers
+// with its global fetch one tile ahead, and the site operands are fetched after the hand-off.  Here
+// (same split: four workgroups per chain, workgroup w owns output columns 16 w .. 16 w + 15, four
+// waves of 16 rows each) the operands stay resident for the whole step:
+//   - the site operands of step s + 1 do not depend on the environment: they are fetched while
+//     step s's hand-off is polled -- GEMM 2's A fragments into registers (32 complex a lane), GEMM
+//     1's B (the site's 16 columns, both physical indices) staged through registers into the LDS;
+//   - after the hand-off only the environment fragments are on the path (16 complex a lane, sc1);
+//   - GEMM 1 runs its whole contraction from registers and the LDS without a barrier, T goes to the
+//     LDS (one barrier), GEMM 2 reads it from there;
+//   - complex products in 3M form: P1 = ar br, P2 = ai bi, P3 = (ar + ai)(br + bi), Re = P1 - P2,
+//     Im = P3 - P1 - P2 (three real MFMAs instead of four).
+// Unified over the directions: E (ke x ke: L_i, or R_{i+1}) is GEMM 1's A operand,
+//   T[l][16 t + c]   = sum_k E[l][k] B1[k][16 t + c],   B1 = A_t[k][c0 + c] (left) or conj(A_t[c0 + c][k]) (right)
+//   out[r][c0 + c]   = sum_{t, k} A2[r][t, k] T[k][16 t + c],  A2 = conj(A_t[k][r]) (left) or A_t[r][k] (right)
+// with out = L_{i+1} (m2 = dims[i + 1]) or R_i (m2 = dims[i]).
+// Measured (tools/env_probe.py, 7 fifty-qubit states): 1.40 -> 1.28 ms per z_all call; per step
+// GEMM 2 36 K -> 7 K ticks (at its MFMA issue), GEMM 1 20 K, the hand-off 4 K -> 26 K: it now
+// carries the operand prefetch (160 KB a workgroup), which no ordering tried hid behind the poll
+// (wave 0 fetching after the poll: 1.67 ms, profiles/r5_env_chain_ab.json).
+struct Env64Lds {
+  cplx B1[64][33];
+  cplx Ts[64][33];
+};
+
+__device__ __forceinline__ void mfma3(aqc::d4_t& p1, aqc::d4_t& p2, aqc::d4_t& p3, cplx a, cplx b) {
+  p1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a.x, b.x, p1, 0, 0, 0);
+  p2 = __builtin_amdgcn_mfma_f64_16x16x4f64(a.y, b.y, p2, 0, 0, 0);
+  p3 = __builtin_amdgcn_mfma_f64_16x16x4f64(a.x + a.y, b.x + b.y, p3, 0, 0, 0);
+}
+
+// grid (4, 2 directions, states), 256 threads; cap == 64.  Counters as k_env_split's.
+__global__ __launch_bounds__(256) void k_env64(const RdmJob* __restrict__ jobs, unsigned* __restrict__ cnt,
+                                               int* __restrict__ err, unsigned long long spin) {
+  constexpr int cap = 64;
+  constexpr size_t cc = 64 * 64;
+  const int w = blockIdx.x, dir = blockIdx.y, tid = threadIdx.x;
+  const int wave = tid >> 6, lane = tid & 63, li = lane & 15, lk = lane >> 4;
+  const RdmJob& j = jobs[blockIdx.z];
+  unsigned* ctr = cnt + 32 * (2 * blockIdx.z + dir);
+  __shared__ Env64Lds lds;
+  __shared__ int s_abort;
+  const int n = j.n, c0 = 16 * w, r0 = 16 * wave;
+  if (tid == 0) {
+    s_abort = 0;
+    if (w == 0) {
+      if (dir == 0) j.Lenv[0] = aqc::cmk(1, 0);
+      else j.Renv[(size_t)n * cc] = aqc::cmk(1, 0);
+    }
+  }
+  const bool tk = tid == 0 && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0;
+  unsigned long long t_last = tk ? __builtin_amdgcn_s_memtime() : 0ull, acc[3] = {0, 0, 0};
+  auto tick = [&](int ph) {
+    if (tk) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      acc[ph] += t - t_last;
+      t_last = t;
+    }
+  };
+  // step s: site i, ke = the environment's dimension (both GEMMs' contraction), m2 = the output's
+  auto site = [&](int s, int& i, int& ke, int& m2) {
+    i = dir == 0 ? s : n - 1 - s;
+    ke = dir == 0 ? j.dims[i] : j.dims[i + 1];
+    m2 = dir == 0 ? j.dims[i + 1] : j.dims[i];
+  };
+  cplx b1[8], a2[2][16];
+  auto fetch_site = [&](int s) {
+    int i, ke, m2;
+    site(s, i, ke, m2);
+    const cplx* g = j.gam + (size_t)i * 2 * cc;
+    const double* lam = j.lam + (size_t)(i + 1) * cap;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int e = tid + 256 * q;
+      if (dir == 0) {  // B1[k][16 t + c] = A_t[k][c0 + c]: c fastest (256-byte runs)
+        const int c = e & 15, t = (e >> 4) & 1, k = e >> 5, col = c0 + c;
+        b1[q] = (k < ke && col < m2) ? aqc::cscale(g[t * cc + k * cap + col], lam[col]) : aqc::cmk(0, 0);
+      } else {  // conj(A_t[c0 + c][k]): k fastest
+        const int k = e & 63, t = (e >> 6) & 1, c = e >> 7, row = c0 + c;
+        b1[q] = (k < ke && row < m2) ? aqc::cconj(aqc::cscale(g[t * cc + row * cap + k], lam[k])) : aqc::cmk(0, 0);
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int ks = 0; ks < 16; ++ks) {
+        const int r = r0 + li, k = 4 * ks + lk;
+        cplx v = aqc::cmk(0, 0);
+        if (r < m2 && k < ke)
+          v = dir == 0 ? aqc::cconj(aqc::cscale(g[t * cc + k * cap + r], lam[r])) : aqc::cscale(g[t * cc + r * cap + k], lam[k]);
+        a2[t][ks] = v;
+      }
+  };
+  fetch_site(0);
+  for (int step = 0; step < n - 1; ++step) {
+    int i, ke, m2;
+    site(step, i, ke, m2);
+    const int nks = (ke + 3) >> 2;  // 4-deep k steps holding the contraction
+    // B1 into the LDS (its previous contents were last read before the previous step's T barrier)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int e = tid + 256 * q;
+      if (dir == 0) lds.B1[e >> 5][16 * ((e >> 4) & 1) + (e & 15)] = b1[q];
+      else lds.B1[e & 63][16 * ((e >> 6) & 1) + (e >> 7)] = b1[q];
+    }
+    // the environment's fragments: E[r0 + li][4 ks + lk]
+    cplx ef[16];
+    const cplx* E = dir == 0 ? j.Lenv + (size_t)i * cc : j.Renv + (size_t)(i + 1) * cc;
+    const bool first = step == 0;  // E = [[1]] (ke = 1)
+#pragma unroll
+    for (int ks = 0; ks < 16; ++ks) {
+      const int r = r0 + li, k = 4 * ks + lk;
+      ef[ks] = (r < ke && k < ke) ? (first ? aqc::cmk(1, 0) : env_ld(E + (size_t)r * cap + k)) : aqc::cmk(0, 0);
+    }
+    __syncthreads();
+    // ---- GEMM 1: T = E B1 (this wave's 16 rows, both t)
+    {
+      aqc::d4_t p1[2], p2[2], p3[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) p1[t] = p2[t] = p3[t] = aqc::d4_t{0, 0, 0, 0};
+#pragma unroll
+      for (int ks = 0; ks < 16; ++ks) {
+        if (ks < nks) {
+#pragma unroll
+          for (int t = 0; t < 2; ++t) mfma3(p1[t], p2[t], p3[t], ef[ks], lds.B1[4 * ks + lk][16 * t + li]);
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          lds.Ts[r0 + lk + 4 * q][16 * t + li] = aqc::cmk(p1[t][q] - p2[t][q], p3[t][q] - p1[t][q] - p2[t][q]);
+    }
+    __syncthreads();
+    tick(0);
+    // ---- GEMM 2: out[r][c0 + c] = sum_{t, k} A2[r][t, k] T[k][16 t + c]
+    {
+      aqc::d4_t p1 = aqc::d4_t{0, 0, 0, 0}, p2 = p1, p3 = p1;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int ks = 0; ks < 16; ++ks)
+          if (ks < nks) mfma3(p1, p2, p3, a2[t][ks], lds.Ts[4 * ks + lk][16 * t + li]);
+      cplx* out = dir == 0 ? j.Lenv + (size_t)(i + 1) * cc : j.Renv + (size_t)i * cc;
+      const int col = c0 + li;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int r = r0 + lk + 4 * q;
+        if (r < m2 && col < m2) env_st(out + (size_t)r * cap + col, aqc::cmk(p1[q] - p2[q], p3[q] - p1[q] - p2[q]));
+      }
+    }
+    tick(1);
+    // hand-off: this workgroup's columns stored before the count; the next step's site operands are
+    // fetched while thread 0 polls
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (step + 1 < n - 1) fetch_site(step + 1);
+    if (tid == 0) {
+      const unsigned target = 4u * (unsigned)(step + 1);
+      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+      while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+        __builtin_amdgcn_s_sleep(1);
+        if (__builtin_amdgcn_s_memrealtime() - t0 > spin) {
+          s_abort = 1;
+          atomicOr(err, 1);
+          break;
+        }
+      }
+    }
+    __syncthreads();
+    tick(2);
+    if (s_abort) return;
+  }
+  if (tk) {
+    for (int ph = 0; ph < 3; ++ph) atomicAdd(&g_env_ticks[ph], acc[ph]);
+    atomicAdd(&g_env_ticks[3], (unsigned long long)(n - 1));
+  }
+}
+
 // P_b[s][sb] = A_b^s R_{b+1} A_b^{sb dag}; m = 0: (0,0), 1: (0,1), 2: (1,1).  grid (n, 3 or 2, states);
 // with two m, the diagonal pair (0,0), (1,1) only (single-site <Z>).  first_site: site 0 too (pair
 // RDMs never need it: it is never the second qubit of a pair)
@@ -637,7 +819,7 @@ int launch_envs(RdmJob* djobs, int ns, int cap, hipStream_t st, void* sync) {
     RdmJob* jb = djobs + s0;
     unsigned* cb = cnt + (size_t)s0 * 2 * 32;
     switch (cap / kEnvNW) {
-      case 16: hipLaunchKernelGGL(k_env_split<16>, grid, dim3(kT), 0, st, jb, cb, err, kSpin); break;
+      case 16: hipLaunchKernelGGL(k_env64, grid, dim3(256), 0, st, jb, cb, err, kSpin); break;
       case 32: hipLaunchKernelGGL(k_env_split<32>, grid, dim3(kT), 0, st, jb, cb, err, kSpin); break;
       case 64: hipLaunchKernelGGL(k_env_split<64>, grid, dim3(kT), 0, st, jb, cb, err, kSpin); break;
       default: hipLaunchKernelGGL(k_env_split<128>, grid, dim3(kT), 0, st, jb, cb, err, kSpin); break;

@@ -353,20 +353,26 @@ __device__ __forceinline__ void s6_back(const TwoSiteJob& j, cplx* hh, int C, in
     }
     __syncthreads();  // B1: Y
     // Y^H V over this wave's 32 rows: A[m = i][k = row] = conj(Y[row][i])
-    aqc::d4_t wr = {0, 0, 0, 0}, wi = {0, 0, 0, 0};
+    // (3M: conj(y) v = P1 - P2 + i (P3 - P1 - P2), P1 = yr vr, P2 = -yi vi, P3 = (yr - yi)(vr + vi):
+    // three MFMAs per k step instead of four -- S6 is matrix-core-bound)
+    aqc::d4_t wr, wi;
+    {
+      aqc::d4_t p1 = {0, 0, 0, 0}, p2 = {0, 0, 0, 0}, p3 = {0, 0, 0, 0};
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      if (32 * mg + 16 * t + 15 > k0) {  // rows <= k0 of Y are zero (uniform per wave)
+      for (int t = 0; t < 2; ++t) {
+        if (32 * mg + 16 * t + 15 > k0) {  // rows <= k0 of Y are zero (uniform per wave)
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          const int row = 32 * mg + 16 * t + 4 * s + lk;
-          const cplx y = Yl[row * 16 + (li ^ (row & 15))];
-          wr = __builtin_amdgcn_mfma_f64_16x16x4f64(y.x, vre[t][s], wr, 0, 0, 0);
-          wr = __builtin_amdgcn_mfma_f64_16x16x4f64(y.y, vim[t][s], wr, 0, 0, 0);
-          wi = __builtin_amdgcn_mfma_f64_16x16x4f64(y.x, vim[t][s], wi, 0, 0, 0);
-          wi = __builtin_amdgcn_mfma_f64_16x16x4f64(-y.y, vre[t][s], wi, 0, 0, 0);
+          for (int s = 0; s < 4; ++s) {
+            const int row = 32 * mg + 16 * t + 4 * s + lk;
+            const cplx y = Yl[row * 16 + (li ^ (row & 15))];
+            p1 = __builtin_amdgcn_mfma_f64_16x16x4f64(y.x, vre[t][s], p1, 0, 0, 0);
+            p2 = __builtin_amdgcn_mfma_f64_16x16x4f64(-y.y, vim[t][s], p2, 0, 0, 0);
+            p3 = __builtin_amdgcn_mfma_f64_16x16x4f64(y.x - y.y, vre[t][s] + vim[t][s], p3, 0, 0, 0);
+          }
         }
       }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) wr[q] = p1[q] - p2[q], wi[q] = p3[q] - p1[q] - p2[q];
     }
     // D layout: row b = lk + 4 q (reflector), column li
     if (mg > 0) {
@@ -378,7 +384,7 @@ __device__ __forceinline__ void s6_back(const TwoSiteJob& j, cplx* hh, int C, in
       // Y^H V of column tile nt summed in registers, then W2 = T (Y^H V) for that tile on the matrix
       // cores right here: the sum's D layout (row lk + 4 q, column li) is the B operand of k-step q
       // and T (in the LDS since B1) the A operand -- no W1 round trip through the LDS, no B3
-      aqc::d4_t br, bi, w2r = {0, 0, 0, 0}, w2i = {0, 0, 0, 0};
+      aqc::d4_t br, bi, p1 = {0, 0, 0, 0}, p2 = {0, 0, 0, 0}, p3 = {0, 0, 0, 0};
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int b = lk + 4 * q;
@@ -391,13 +397,12 @@ __device__ __forceinline__ void s6_back(const TwoSiteJob& j, cplx* hh, int C, in
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const cplx t = Tl[li * 17 + 4 * q + lk];  // A[m = li][k = lk] = T[li][4 q + lk]
-        w2r = __builtin_amdgcn_mfma_f64_16x16x4f64(t.x, br[q], w2r, 0, 0, 0);
-        w2r = __builtin_amdgcn_mfma_f64_16x16x4f64(-t.y, bi[q], w2r, 0, 0, 0);
-        w2i = __builtin_amdgcn_mfma_f64_16x16x4f64(t.x, bi[q], w2i, 0, 0, 0);
-        w2i = __builtin_amdgcn_mfma_f64_16x16x4f64(t.y, br[q], w2i, 0, 0, 0);
+        p1 = __builtin_amdgcn_mfma_f64_16x16x4f64(t.x, br[q], p1, 0, 0, 0);
+        p2 = __builtin_amdgcn_mfma_f64_16x16x4f64(t.y, bi[q], p2, 0, 0, 0);
+        p3 = __builtin_amdgcn_mfma_f64_16x16x4f64(t.x + t.y, br[q] + bi[q], p3, 0, 0, 0);
       }
 #pragma unroll
-      for (int q = 0; q < 4; ++q) W2l[(lk + 4 * q) * 64 + 16 * nt + li] = aqc::cmk(w2r[q], w2i[q]);
+      for (int q = 0; q < 4; ++q) W2l[(lk + 4 * q) * 64 + 16 * nt + li] = aqc::cmk(p1[q] - p2[q], p3[q] - p1[q] - p2[q]);
     }
     __syncthreads();  // B4: W2
     // the next block's reflectors, in flight during the V update: issued before B1 they were
@@ -411,20 +416,24 @@ __device__ __forceinline__ void s6_back(const TwoSiteJob& j, cplx* hh, int C, in
     // is spilled) their reload's vmcnt(0) drained the next block's reflector loads issued above
     const int vl_ = fresh_lane();
     const int vmg = wave_s >> 2, vnt = wave_s & 3, vli = vl_ & 15, vlk = vl_ >> 4;
+    // (3M: y w = P1 - P2 + i (P3 - P1 - P2), P1 = yr wr, P2 = yi wi, P3 = (yr + yi)(wr + wi); -P3
+    // straight into vim, P1 and P2 into two temporaries)
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       if (32 * vmg + 16 * t + 15 > k0) {
         const int row = 32 * vmg + 16 * t + vli;
+        aqc::d4_t p1 = {0, 0, 0, 0}, p2 = {0, 0, 0, 0};
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
           const int b = 4 * s + vlk;
           const cplx y = Yl[row * 16 + (b ^ (row & 15))];
           const cplx w = W2l[b * 64 + 16 * vnt + vli];
-          vre[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(-y.x, w.x, vre[t], 0, 0, 0);
-          vre[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(y.y, w.y, vre[t], 0, 0, 0);
-          vim[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(-y.x, w.y, vim[t], 0, 0, 0);
-          vim[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(-y.y, w.x, vim[t], 0, 0, 0);
+          p1 = __builtin_amdgcn_mfma_f64_16x16x4f64(y.x, w.x, p1, 0, 0, 0);
+          p2 = __builtin_amdgcn_mfma_f64_16x16x4f64(y.y, w.y, p2, 0, 0, 0);
+          vim[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(-(y.x + y.y), w.x + w.y, vim[t], 0, 0, 0);
         }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) vre[t][q] += p2[q] - p1[q], vim[t][q] += p1[q] + p2[q];
       }
     }
     __syncthreads();  // B5: Y, W2 and the partials are overwritten next block
