@@ -1,18 +1,14 @@
 #!/bin/bash
-# Round-5 GPU call 21: BASELINE configs 2 / 4 / 5 without the kernel trace (under rocprofv3
-# --kernel-trace config 5's two-stage rounds lose their cross-stream overlap: 0.37 against 0.29 ms
-# per gate; the traced run is kept for the kernel summary only), twice.
+# Round-5 GPU call 22: k_env64 with a chain's four workgroups on one XCD (grid (chains rounded up to
+# 8, 4): linear ids chain + 8m w, libaqchip_xcd.so) -- parity, step phases, local-cost latency against
+# the library as built.
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
-for r in 1 2; do
-  timeout -k 10 400 python3 tools/configs_bench.py --configs 2,4,5 > gpurun_out/r5c21_configs_$r.json 2> gpurun_out/r5c21_configs_$r.err || exit $?
-done
-# (call 22: k_env64 with a chain's workgroups on one XCD)
 L=$PWD/adaptaqc_amd
 AQC_LIB=$L/libaqchip_xcd.so timeout -k 10 300 python3 -u -m pytest tests/test_gpu_ent.py tests/test_gpu_mps.py::test_z_all_batch_split_environments_vs_oracle \
   -x -q --timeout 200 --timeout-method thread > gpurun_out/r5c22_xcd_tests.log 2>&1
 rc=$?
-echo "xcd tests rc=$rc" > gpurun_out/r5c21.rc
+echo "xcd tests rc=$rc" > gpurun_out/r5c22.rc
 if [ $rc -ne 0 ]; then exit $rc; fi
 for t in xcd cur; do
   if [ "$t" = cur ]; then lib=$L/libaqchip.so; else lib=$L/libaqchip_$t.so; fi
