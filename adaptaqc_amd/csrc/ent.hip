@@ -799,9 +799,10 @@ int ensure(RdmBuffers& b, size_t need) {
 // Counter / error words behind the jobs of an environment launch: 32 words per chain, one error word.
 size_t env_sync_bytes(int ns) { return (((size_t)ns * 2 * 32 + 32) * sizeof(unsigned) + 255) / 256 * 256; }
 
-// The left / right environments of every state: k_env_split (kEnvNW workgroups per chain) where the
-// capacity splits into 16-column multiples, else k_rdm_env; states in rounds small enough that every
-// chain's workgroups are resident together (two per CU).  sync: env_sync_bytes(ns) of device memory.
+// The left / right environments of every state: kEnvNW workgroups per chain where the capacity
+// splits into 16-column multiples (k_env64 at capacity 64, k_env_split above), else k_rdm_env;
+// states in rounds small enough that every chain's workgroups are resident together.  sync:
+// env_sync_bytes(ns) of device memory.
 int launch_envs(RdmJob* djobs, int ns, int cap, hipStream_t st, void* sync) {
   if (cap % (16 * kEnvNW) != 0) {
     hipLaunchKernelGGL(k_rdm_env, dim3(2, ns), dim3(kT), 0, st, djobs);
