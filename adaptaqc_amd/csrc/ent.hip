@@ -325,7 +325,8 @@ __global__ __launch_bounds__(kT) void k_env_split(const RdmJob* __restrict__ job
 //   T[l][16 t + c]   = sum_k E[l][k] B1[k][16 t + c],   B1 = A_t[k][c0 + c] (left) or conj(A_t[c0 + c][k]) (right)
 //   out[r][c0 + c]   = sum_{t, k} A2[r][t, k] T[k][16 t + c],  A2 = conj(A_t[k][r]) (left) or A_t[r][k] (right)
 // with out = L_{i+1} (m2 = dims[i + 1]) or R_i (m2 = dims[i]).
-// Measured (tools/env_probe.py, 7 fifty-qubit states): 1.40 -> 1.28 ms per z_all call; per step
+// Measured (tools/env_probe.py, 7 fifty-qubit states): 1.40 -> 1.28 ms per z_all call (1.12 with
+// a chain's workgroups on one XCD, below); per step
 // GEMM 2 36 K -> 7 K ticks (at its MFMA issue), GEMM 1 20 K, the hand-off 4 K -> 26 K: it now
 // carries the operand prefetch (160 KB a workgroup), which no ordering tried hid behind the poll
 // (wave 0 fetching after the poll: 1.67 ms, profiles/r5_env_chain_ab.json).
@@ -340,15 +341,21 @@ __device__ __forceinline__ void mfma3(aqc::d4_t& p1, aqc::d4_t& p2, aqc::d4_t& p
   p3 = __builtin_amdgcn_mfma_f64_16x16x4f64(a.x + a.y, b.x + b.y, p3, 0, 0, 0);
 }
 
-// grid (4, 2 directions, states), 256 threads; cap == 64.  Counters as k_env_split's.
+// grid (2 states rounded up to 8, 4), 256 threads; cap == 64.  Counters as k_env_split's.
 __global__ __launch_bounds__(256) void k_env64(const RdmJob* __restrict__ jobs, unsigned* __restrict__ cnt,
-                                               int* __restrict__ err, unsigned long long spin) {
+                                               int* __restrict__ err, unsigned long long spin, int nchains) {
   constexpr int cap = 64;
   constexpr size_t cc = 64 * 64;
-  const int w = blockIdx.x, dir = blockIdx.y, tid = threadIdx.x;
+  // grid (chains rounded up to 8, 4): the chain's four workgroups at linear ids chain + 8 m w, on
+  // one XCD under the dispatcher's round-robin placement, so that the three after the first find
+  // the site's operands in that XCD's L2 (placement is a speed matter only: the hand-off stays
+  // agent-scope).  Measured: the hand-off 26.7 K -> 17.6 K ticks a step, z_all 1.29 -> 1.12 ms.
+  const int chain = blockIdx.x, w = blockIdx.y, tid = threadIdx.x;
+  if (chain >= nchains) return;  // (the padding: whole workgroups)
+  const int st = chain >> 1, dir = chain & 1;
   const int wave = tid >> 6, lane = tid & 63, li = lane & 15, lk = lane >> 4;
-  const RdmJob& j = jobs[blockIdx.z];
-  unsigned* ctr = cnt + 32 * (2 * blockIdx.z + dir);
+  const RdmJob& j = jobs[st];
+  unsigned* ctr = cnt + 32 * (2 * st + dir);
   __shared__ Env64Lds lds;
   __shared__ int s_abort;
   const int n = j.n, c0 = 16 * w, r0 = 16 * wave;
@@ -359,7 +366,7 @@ __global__ __launch_bounds__(256) void k_env64(const RdmJob* __restrict__ jobs, 
       else j.Renv[(size_t)n * cc] = aqc::cmk(1, 0);
     }
   }
-  const bool tk = tid == 0 && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0;
+  const bool tk = tid == 0 && chain == 0 && w == 0;
   unsigned long long t_last = tk ? __builtin_amdgcn_s_memtime() : 0ull, acc[3] = {0, 0, 0};
   auto tick = [&](int ph) {
     if (tk) {
@@ -820,7 +827,7 @@ int launch_envs(RdmJob* djobs, int ns, int cap, hipStream_t st, void* sync) {
     RdmJob* jb = djobs + s0;
     unsigned* cb = cnt + (size_t)s0 * 2 * 32;
     switch (cap / kEnvNW) {
-      case 16: hipLaunchKernelGGL(k_env64, grid, dim3(256), 0, st, jb, cb, err, kSpin); break;
+      case 16: hipLaunchKernelGGL(k_env64, dim3((2 * m + 7) / 8 * 8, kEnvNW), dim3(256), 0, st, jb, cb, err, kSpin, 2 * m); break;
       case 32: hipLaunchKernelGGL(k_env_split<32>, grid, dim3(kT), 0, st, jb, cb, err, kSpin); break;
       case 64: hipLaunchKernelGGL(k_env_split<64>, grid, dim3(kT), 0, st, jb, cb, err, kSpin); break;
       default: hipLaunchKernelGGL(k_env_split<128>, grid, dim3(kT), 0, st, jb, cb, err, kSpin); break;
