@@ -1335,14 +1335,11 @@ int gb_ensure(GBBuffers& b, int ct, int nj, hipStream_t st) {
 // only by these events, so they must be drained before the runtime tears down.
 hipStream_t g_gb_side[64] = {nullptr};
 hipStream_t g_gb_side2[64] = {nullptr};  // the compact-WY factors beside the eigenpairs
-hipStream_t g_gb_side3[64] = {nullptr};  // a round's eigenpairs beside the next round's second stage
 std::vector<hipEvent_t> g_gb_events;
 void release_gb_sync() {
   for (auto& s : g_gb_side)
     if (s) (void)hipStreamDestroy(s), s = nullptr;
   for (auto& s : g_gb_side2)
-    if (s) (void)hipStreamDestroy(s), s = nullptr;
-  for (auto& s : g_gb_side3)
     if (s) (void)hipStreamDestroy(s), s = nullptr;
   for (hipEvent_t e : g_gb_events) (void)hipEventDestroy(e);
   g_gb_events.clear();
@@ -1351,7 +1348,7 @@ void release_gb_sync() {
 hipStream_t gb_side_stream(int which = 0) {
   int dev = 0;
   (void)hipGetDevice(&dev);
-  hipStream_t* tab = which == 2 ? g_gb_side3 : which ? g_gb_side2 : g_gb_side;
+  hipStream_t* tab = which ? g_gb_side2 : g_gb_side;
   if (!tab[dev]) {
     (void)hipStreamCreateWithFlags(&tab[dev], hipStreamNonBlocking);
     aqc::on_finalize(release_gb_sync);
@@ -1455,9 +1452,13 @@ int run_gram_big(const TwoSiteJob* hjobs, const TwoSiteJob* jobs, int nj, int ca
     if (rc != AQC_OK) return rc;
   } else {
     // 2 chi = 512 with the tail: two exchange stages (k_gb_tridiag's comment); a round's second
-    // stage and tail on s2, its eigenpairs and back-transformation on s4, so that the next round's
-    // second stage does not queue behind them
-    hipStream_t s4 = two ? gb_side_stream(2) : s2;
+    // stage and tail on s2, its compact-WY factors, eigenpairs and back-transformation on s3, so
+    // that the next round's second stage does not queue behind them.  (Three streams, not four: a
+    // process has four hardware queues by default, and with a fourth stream here the schedule's
+    // streams shared queues with the caller's -- config 5 after config 2's four evaluation streams
+    // ran 0.367 ms per gate against 0.293 alone; on three streams 0.290 both ways,
+    // profiles/r5_cfg5_streams.json.)
+    hipStream_t s4 = two ? s3 : s2;
     for (int j0 = 0; j0 < nj; j0 += per_round) {
       const int nr = std::min(per_round, nj - j0);
       if (two)
