@@ -326,10 +326,12 @@ __global__ __launch_bounds__(kT) void k_env_split(const RdmJob* __restrict__ job
 //   out[r][c0 + c]   = sum_{t, k} A2[r][t, k] T[k][16 t + c],  A2 = conj(A_t[k][r]) (left) or A_t[r][k] (right)
 // with out = L_{i+1} (m2 = dims[i + 1]) or R_i (m2 = dims[i]).
 // Measured (tools/env_probe.py, 7 fifty-qubit states): 1.40 -> 1.28 ms per z_all call (1.12 with
-// a chain's workgroups on one XCD, below); per step
+// a chain's workgroups on one XCD, below; 1.05 with the hand-off traffic as 16-byte sc1 buffer
+// accesses: T 20.5 K -> 17.4 K ticks); per step
 // GEMM 2 36 K -> 7 K ticks (at its MFMA issue), GEMM 1 20 K, the hand-off 4 K -> 26 K: it now
 // carries the operand prefetch (160 KB a workgroup), which no ordering tried hid behind the poll
 // (wave 0 fetching after the poll: 1.67 ms, profiles/r5_env_chain_ab.json).
+typedef unsigned env_u4 __attribute__((ext_vector_type(4)));
 struct Env64Lds {
   cplx B1[64][33];
   cplx Ts[64][33];
@@ -422,13 +424,19 @@ __global__ __launch_bounds__(256) void k_env64(const RdmJob* __restrict__ jobs, 
       else lds.B1[e & 63][16 * ((e >> 6) & 1) + (e >> 7)] = b1[q];
     }
     // the environment's fragments: E[r0 + li][4 ks + lk]
+    // (16-byte agent-coherent loads: a buffer load with sc1, aux = 16 -- half the instructions of two
+    // 8-byte atomic loads; the hand-off's counter orders them)
     cplx ef[16];
     const cplx* E = dir == 0 ? j.Lenv + (size_t)i * cc : j.Renv + (size_t)(i + 1) * cc;
+    const auto re = aqc::make_rsrc(E, (unsigned)(cc * sizeof(cplx)));
     const bool first = step == 0;  // E = [[1]] (ke = 1)
 #pragma unroll
     for (int ks = 0; ks < 16; ++ks) {
       const int r = r0 + li, k = 4 * ks + lk;
-      ef[ks] = (r < ke && k < ke) ? (first ? aqc::cmk(1, 0) : env_ld(E + (size_t)r * cap + k)) : aqc::cmk(0, 0);
+      ef[ks] = (r < ke && k < ke)
+                   ? (first ? aqc::cmk(1, 0)
+                            : __builtin_bit_cast(cplx, __builtin_amdgcn_raw_buffer_load_b128(re, (unsigned)(r * cap + k) * 16u, 0u, 16)))
+                   : aqc::cmk(0, 0);
     }
     __syncthreads();
     // ---- GEMM 1: T = E B1 (this wave's 16 rows, both t)
@@ -460,11 +468,14 @@ __global__ __launch_bounds__(256) void k_env64(const RdmJob* __restrict__ jobs, 
         for (int ks = 0; ks < 16; ++ks)
           if (ks < nks) mfma3(p1, p2, p3, a2[t][ks], lds.Ts[4 * ks + lk][16 * t + li]);
       cplx* out = dir == 0 ? j.Lenv + (size_t)(i + 1) * cc : j.Renv + (size_t)i * cc;
+      const auto ro = aqc::make_rsrc(out, (unsigned)(cc * sizeof(cplx)));
       const int col = c0 + li;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int r = r0 + lk + 4 * q;
-        if (r < m2 && col < m2) env_st(out + (size_t)r * cap + col, aqc::cmk(p1[q] - p2[q], p3[q] - p1[q] - p2[q]));
+        if (r < m2 && col < m2)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(env_u4, aqc::cmk(p1[q] - p2[q], p3[q] - p1[q] - p2[q])), ro,
+                                                 (unsigned)(r * cap + col) * 16u, 0u, 16);
       }
     }
     tick(1);
