@@ -410,12 +410,17 @@ constexpr int kChain8Ld = CAP + 4;  // V row stride (complex)
 // chains, each MFMA step's B operands serving two row tiles -- measured slower, sweep_group())
 template <int CAP, int G>
 __global__ __launch_bounds__(4 * CAP) void k_sweep_chain8(const SweepJob* __restrict__ jobs, const int* __restrict__ alist,
-                                                          int nal) {
+                                                          int nal, int ns) {
   constexpr int NQ = CAP / 4, NT = 4 * CAP;  // CAP / 16 waves, one 16-column tile each
   constexpr int R = 2 * G, RT = R / 16;      // rows (chain c, first-qubit value sa: 2c + sa), row tiles
   static_assert(G == 8 || G == 16, "8 or 16 chains per workgroup");
-  const SweepJob& j = jobs[blockIdx.y];
-  const int g0 = blockIdx.x * G;
+  // 1-D grid over (state slot, group): linear id = state + nsp group with nsp = ns rounded up to 8,
+  // so a state's groups -- which read the same M_b matrices at about the same time -- share one XCD
+  // (and its L2) under the dispatcher's round-robin placement (a speed matter only)
+  const int nsp = (ns + 7) & ~7, sj = (int)blockIdx.x % nsp;
+  if (sj >= ns) return;  // (padding: whole workgroups)
+  const SweepJob& j = jobs[sj];
+  const int g0 = ((int)blockIdx.x / nsp) * G;
   const int n = j.n;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   __shared__ cplx V[2][R][kChain8Ld<CAP>];
@@ -1043,11 +1048,11 @@ int aqc_pair_grads_batch(aqc_mps_t* psis, int ns, const double* svec, const int*
       aqc::KernelTimer::begin(st, "grad_chain", ns * steps * c * c * 16.0, ns * steps * 2.0 * c * c * 8.0);
       const unsigned ng = (unsigned)(alist.size() + kSweepGroup - 1) / kSweepGroup;
       if (use_chain8(cap, ns) && cap == 128) {
-        hipLaunchKernelGGL((k_sweep_chain8<128, kSweepGroup>), dim3(ng, ns), dim3(512), 0, st, djobs,
-                           (const int*)dalist, (int)alist.size());
+        hipLaunchKernelGGL((k_sweep_chain8<128, kSweepGroup>), dim3(ng * ((ns + 7) & ~7)), dim3(512), 0, st, djobs,
+                           (const int*)dalist, (int)alist.size(), ns);
       } else if (use_chain8(cap, ns)) {
-        hipLaunchKernelGGL((k_sweep_chain8<64, kSweepGroup>), dim3(ng, ns), dim3(256), 0, st, djobs, (const int*)dalist,
-                           (int)alist.size());
+        hipLaunchKernelGGL((k_sweep_chain8<64, kSweepGroup>), dim3(ng * ((ns + 7) & ~7)), dim3(256), 0, st, djobs,
+                           (const int*)dalist, (int)alist.size(), ns);
       }
       else
         if (cap == 128)
