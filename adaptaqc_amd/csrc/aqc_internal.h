@@ -102,6 +102,18 @@ __device__ __forceinline__ void stg(double* p, double v) { *(gdouble*)p = v; }
 // so a run of loads at uniform strides holds one VGPR of addressing instead of a 64-bit address
 // each.  Offsets past `bytes` (lane offset + instruction offset) read as zero.  0x00020000 is the
 // gfx9 data-format word of the resource.
+// Per-job grids laid out so that a job's workgroups share one XCD (and its L2) under the
+// dispatcher's round-robin placement: a 1-D grid of nblk x njp blocks (njp = nj rounded up to 8),
+// block id = job + njp blk.  False for the padding's blocks (whole workgroups: return at once).
+// Placement is a speed matter only.
+__device__ __forceinline__ bool xcd_job_block(int nj, int& job, int& blk) {
+  const int njp = (nj + 7) & ~7;
+  job = (int)blockIdx.x % njp;
+  blk = (int)blockIdx.x / njp;
+  return job < nj;
+}
+inline unsigned xcd_grid(int nblk, int nj) { return (unsigned)nblk * (unsigned)((nj + 7) & ~7); }
+
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, unsigned bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
 }

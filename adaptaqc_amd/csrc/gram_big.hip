@@ -134,13 +134,14 @@ __device__ __forceinline__ void job_dims(const TwoSiteJob& j, int& M, int& L, in
 // ---- G = X^H X ------------------------------------------------------------------------------
 // grid (nbt (nbt + 1) / 2, nj) with nbt = CT / 64, 256 threads.  Entries outside C x C are zero.
 template <int CT>
-__global__ __launch_bounds__(256) void k_gb_gram(const TwoSiteJob* __restrict__ jobs, GBArgs a) {
-  const int jb = blockIdx.y;
+__global__ __launch_bounds__(256) void k_gb_gram(const TwoSiteJob* __restrict__ jobs, GBArgs a, int nj) {
+  int jb, bx;
+  if (!xcd_job_block(nj, jb, bx)) return;  // (a job's blocks on one XCD: they share X's panels)
   const TwoSiteJob& j = jobs[jb];
   int M, L, C, K;
   bool tr;
   job_dims(j, M, L, C, tr, K);
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
+  if (bx == 0 && threadIdx.x == 0) {
     atomicAdd(&g_gbig_stats[0], 1ull);
     const int st = (!j.gram || C < 4) ? 1 : 0;
     *(gi32*)(a.status + jb) = st;
@@ -149,7 +150,7 @@ __global__ __launch_bounds__(256) void k_gb_gram(const TwoSiteJob* __restrict__ 
   if (!j.gram || C < 4) return;
   // blocks on and above the diagonal (bi <= bj), the one below mirrored: G is Hermitian
   constexpr int nbt = CT / 64;
-  int bi = 0, rem = blockIdx.x;
+  int bi = 0, rem = bx;
   while (rem >= nbt - bi) rem -= nbt - bi, ++bi;
   const int bj = (bi + rem) * 64;
   bi *= 64;
@@ -1065,17 +1066,19 @@ __global__ __launch_bounds__(256) void k_gb_tfac(const TwoSiteJob* __restrict__ 
 // the LDS), W2 = T W1, V -= Y W2.  Y's operands straight from the (L2-resident) scratch: a block's
 // rows are contiguous in the column-major reflector store.  Output W = V Sigma, sig, qr = 1.
 template <int CT, int NW = (CT / 64 > 4 ? CT / 64 : 4)>
-__global__ __launch_bounds__(64 * NW) void k_gb_back(const TwoSiteJob* __restrict__ jobs, GBArgs a, int job0) {
+__global__ __launch_bounds__(64 * NW) void k_gb_back(const TwoSiteJob* __restrict__ jobs, GBArgs a, int job0, int nr) {
   constexpr int NT = CT / (16 * NW);  // row tiles per wave
-  const int jb = job0 + (int)blockIdx.y;
+  int jr, bx;
+  if (!xcd_job_block(nr, jr, bx)) return;  // (a job's column groups on one XCD: they share Y)
+  const int jb = job0 + jr;
   if (*(const gi32*)(a.status + jb) != 0) return;
   TwoSiteJob& j = const_cast<TwoSiteJob&>(jobs[jb]);
   int M, L, C, K;
   bool tr;
   job_dims(j, M, L, C, tr, K);
   K = kept_count(a, jb);
-  const int col0 = blockIdx.x * 16;
-  if (blockIdx.x == 0 && threadIdx.x == 0) stg(j.sig + kSigTail, ldg(a.tail + jb));  // (rank_body)
+  const int col0 = bx * 16;
+  if (bx == 0 && threadIdx.x == 0) stg(j.sig + kSigTail, ldg(a.tail + jb));  // (rank_body)
   if (col0 >= K) return;
   const unsigned long long t_start = __builtin_amdgcn_s_memtime();
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 15, lk = lane >> 4;
@@ -1176,9 +1179,9 @@ __global__ __launch_bounds__(64 * NW) void k_gb_back(const TwoSiteJob* __restric
   }
   for (int c = col0 + tid; c < min(C, col0 + 16); c += 64 * NW)
     if (c >= K) stg(j.sig + c, 0.0);
-  if (blockIdx.x == 0)
+  if (bx == 0)
     for (int c = ((K + 15) / 16) * 16 + tid; c < C; c += 64 * NW) stg(j.sig + c, 0.0);
-  if (blockIdx.x == 0 && tid == 0) {
+  if (bx == 0 && tid == 0) {
     if (jb == 0) atomicAdd(&g_gbig_ticks[6], __builtin_amdgcn_s_memtime() - t_start);
     j.qr = 1;
     atomicMax(&j.flags[2], 1);
@@ -1383,7 +1386,7 @@ int run_gram_big(const TwoSiteJob* hjobs, const TwoSiteJob* jobs, int nj, int ca
     g_gb_tail = (e && std::strcmp(e, "0") == 0) ? 0 : 1;
   }
   AQC_HIP_CHECK(hipMemsetAsync(b.cnt, 0, (size_t)32 * nj * sizeof(unsigned), st));
-  hipLaunchKernelGGL((k_gb_gram<CT>), dim3((CT / 64) * (CT / 64 + 1) / 2, nj), dim3(256), 0, st, jobs, a);
+  hipLaunchKernelGGL((k_gb_gram<CT>), dim3(xcd_grid((CT / 64) * (CT / 64 + 1) / 2, nj)), dim3(256), 0, st, jobs, a, nj);
   AQC_CHECK_LAUNCH();
   // the tridiagonalisation's workgroups of a job must all be resident together (they exchange a
   // vector per column): rounds of at most min(240, resident capacity) workgroups, whole jobs each.
@@ -1436,7 +1439,7 @@ int run_gram_big(const TwoSiteJob* hjobs, const TwoSiteJob* jobs, int nj, int ca
       AQC_HIP_CHECK(hipEventRecord(e1, s3));
       AQC_HIP_CHECK(hipStreamWaitEvent(ps, e1, 0));
     }
-    hipLaunchKernelGGL((k_gb_back<CT>), dim3(CT / 16, nr), dim3(CT / 64 > 4 ? CT : 256), 0, ps, jobs, a, j0);
+    hipLaunchKernelGGL((k_gb_back<CT>), dim3(xcd_grid(CT / 16, nr)), dim3(CT / 64 > 4 ? CT : 256), 0, ps, jobs, a, j0, nr);
     AQC_CHECK_LAUNCH();
     hipLaunchKernelGGL((k_gb_cert_y<CT>), dim3(CT / 64, CT / 64, nr), dim3(256), 0, ps, jobs, a, j0);
     AQC_CHECK_LAUNCH();

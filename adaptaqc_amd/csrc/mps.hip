@@ -131,12 +131,14 @@ __global__ __launch_bounds__(kT) void k_1q(const OneSiteJob* __restrict__ jobs) 
 
 // theta[(s2*chr + r)*M + s1*chl + l] = sum_in G[out][in] * P_in[l][r],
 // P_{s1' s2'}[l][r] = sum_m ll[l] Gp[s1'][l][m] lm[m] Gq[s2'][m][r] lr[r].
-__global__ __launch_bounds__(kT) void k_theta(const TwoSiteJob* __restrict__ jobs) {
-  const TwoSiteJob& j = jobs[blockIdx.y];
+__global__ __launch_bounds__(kT) void k_theta(const TwoSiteJob* __restrict__ jobs, int nj) {
+  int jb, tile;
+  if (!aqc::xcd_job_block(nj, jb, tile)) return;  // (a job's tiles on one XCD: they share panels)
+  const TwoSiteJob& j = jobs[jb];
   const int chl = j.dims[0], chm = j.dims[1], chr = j.dims[2];
   const int cap = j.cap;
   const int tiles_r = (cap + 15) / 16;
-  const int l0 = (blockIdx.x / tiles_r) * 16, r0 = (blockIdx.x % tiles_r) * 16;
+  const int l0 = (tile / tiles_r) * 16, r0 = (tile % tiles_r) * 16;
   if (l0 >= chl || r0 >= chr) return;
   __shared__ cplx As[2][16][17];
   __shared__ cplx Bs[2][16][17];
@@ -879,11 +881,13 @@ __device__ __forceinline__ void split_gemm_body(const TwoSiteJob& j, int blk, aq
   }
 }
 
-__global__ __launch_bounds__(aqc::kGemmThreads) void k_split_gemm(const TwoSiteJob* __restrict__ jobs) {
-  const TwoSiteJob& j = jobs[blockIdx.y];
+__global__ __launch_bounds__(aqc::kGemmThreads) void k_split_gemm(const TwoSiteJob* __restrict__ jobs, int nj) {
+  int jb, blk;
+  if (!aqc::xcd_job_block(nj, jb, blk)) return;  // (a job's blocks on one XCD: they share panels)
+  const TwoSiteJob& j = jobs[jb];
   __shared__ aqc::GemmLds lds;
-  if (!split_block_active(j, blockIdx.x)) return;
-  split_gemm_body(j, blockIdx.x, lds, -1);
+  if (!split_block_active(j, blk)) return;
+  split_gemm_body(j, blk, lds, -1);
 }
 
 // ---- fused per-state chain (2 chi = 128) ----------------------------------------------------
@@ -1952,7 +1956,7 @@ int run_waves(aqc_mps_t* hs, int ns, std::vector<std::vector<DevOp>>& lists) {
       const TwoSiteJob* jp = dtwo + two_rng[w].first;
       const double c = cap_max;
       aqc::KernelTimer::begin(st, "mps_theta", nj * (6.0 * c * c * 16 + 4.0 * c * c * 16), nj * 4.0 * c * c * c * 8);
-      hipLaunchKernelGGL(k_theta, dim3(tiles, nj), dim3(kT), 0, st, jp);
+      hipLaunchKernelGGL(k_theta, dim3(aqc::xcd_grid(tiles, nj)), dim3(kT), 0, st, jp, nj);
       aqc::KernelTimer::end(st);
       AQC_CHECK_LAUNCH();
       aqc::KernelTimer::begin(st, "mps_svd", nj * 2.0 * (4.0 * c * c * 16), 0.0);
@@ -1982,7 +1986,7 @@ int run_waves(aqc_mps_t* hs, int ns, std::vector<std::vector<DevOp>>& lists) {
       hipLaunchKernelGGL(k_split_copy, dim3(std::max(1, (4 * cap_max * cap_max + kT - 1) / kT), nj), dim3(kT), 0, st, jp);
       AQC_CHECK_LAUNCH();
       aqc::KernelTimer::begin(st, "mps_split", 0.0, nj * 2.0 * c * c * 2.0 * c * 8);
-      hipLaunchKernelGGL(k_split_gemm, dim3(blocks_split, nj), dim3(aqc::kGemmThreads), 0, st, jp);
+      hipLaunchKernelGGL(k_split_gemm, dim3(aqc::xcd_grid(blocks_split, nj)), dim3(aqc::kGemmThreads), 0, st, jp, nj);
       aqc::KernelTimer::end(st);
       AQC_CHECK_LAUNCH();
     }
