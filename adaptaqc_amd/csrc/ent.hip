@@ -209,15 +209,18 @@ __device__ __forceinline__ void narrow_cgemm(int m, int n, int k, FA a, FB b, FS
 // columns, the hand-off; then the steps counted
 __device__ unsigned long long g_env_ticks[4];
 
-// grid (kEnvNW, 2 directions, states), kT threads; CW = cap / kEnvNW output columns per workgroup.
-// Counters: cnt[32 (2 state + dir)] (zeroed by the host).
+// grid (2 states rounded up to 8, kEnvNW), kT threads; CW = cap / kEnvNW output columns per
+// workgroup.  Counters: cnt[32 (2 state + dir)] (zeroed by the host).
 template <int CW>
 __global__ __launch_bounds__(kT) void k_env_split(const RdmJob* __restrict__ jobs, unsigned* __restrict__ cnt,
-                                                  int* __restrict__ err, unsigned long long spin) {
+                                                  int* __restrict__ err, unsigned long long spin, int nchains) {
   constexpr int NB1 = 2 * CW < 64 ? 2 * CW : 64, NB2 = CW < 64 ? CW : 64;
-  const int w = blockIdx.x, dir = blockIdx.y, tid = threadIdx.x;
-  const RdmJob& j = jobs[blockIdx.z];
-  unsigned* ctr = cnt + 32 * (2 * blockIdx.z + dir);
+  // (grid as k_env64's: a chain's workgroups on one XCD)
+  const int chain = blockIdx.x, w = blockIdx.y, tid = threadIdx.x;
+  if (chain >= nchains) return;
+  const int dir = chain & 1;
+  const RdmJob& j = jobs[chain >> 1];
+  unsigned* ctr = cnt + 32 * chain;
   __shared__ NarrowLds lds;
   __shared__ int s_abort;
   const int n = j.n, cap = j.cap;
@@ -231,7 +234,7 @@ __global__ __launch_bounds__(kT) void k_env_split(const RdmJob* __restrict__ job
       else j.Renv[(size_t)n * cc] = aqc::cmk(1, 0);
     }
   }
-  const bool tk = tid == 0 && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0;
+  const bool tk = tid == 0 && chain == 0 && w == 0;
   unsigned long long t_last = tk ? __builtin_amdgcn_s_memtime() : 0ull, acc[3] = {0, 0, 0};
   auto tick = [&](int ph) {
     if (tk) {
@@ -834,14 +837,14 @@ int launch_envs(RdmJob* djobs, int ns, int cap, hipStream_t st, void* sync) {
   constexpr int kRound = 28;  // 28 x 8 workgroups: one per CU (~400 VGPRs a lane) leaves room
   for (int s0 = 0; s0 < ns; s0 += kRound) {
     const int m = std::min(kRound, ns - s0);
-    const dim3 grid(kEnvNW, 2, m);
+    const dim3 xg((2 * m + 7) / 8 * 8, kEnvNW);  // (chains padded to 8, workgroup: one XCD per chain)
     RdmJob* jb = djobs + s0;
     unsigned* cb = cnt + (size_t)s0 * 2 * 32;
     switch (cap / kEnvNW) {
-      case 16: hipLaunchKernelGGL(k_env64, dim3((2 * m + 7) / 8 * 8, kEnvNW), dim3(256), 0, st, jb, cb, err, kSpin, 2 * m); break;
-      case 32: hipLaunchKernelGGL(k_env_split<32>, grid, dim3(kT), 0, st, jb, cb, err, kSpin); break;
-      case 64: hipLaunchKernelGGL(k_env_split<64>, grid, dim3(kT), 0, st, jb, cb, err, kSpin); break;
-      default: hipLaunchKernelGGL(k_env_split<128>, grid, dim3(kT), 0, st, jb, cb, err, kSpin); break;
+      case 16: hipLaunchKernelGGL(k_env64, xg, dim3(256), 0, st, jb, cb, err, kSpin, 2 * m); break;
+      case 32: hipLaunchKernelGGL(k_env_split<32>, xg, dim3(kT), 0, st, jb, cb, err, kSpin, 2 * m); break;
+      case 64: hipLaunchKernelGGL(k_env_split<64>, xg, dim3(kT), 0, st, jb, cb, err, kSpin, 2 * m); break;
+      default: hipLaunchKernelGGL(k_env_split<128>, xg, dim3(kT), 0, st, jb, cb, err, kSpin, 2 * m); break;
     }
     AQC_CHECK_LAUNCH();
   }
