@@ -20,8 +20,11 @@
 //                 hand-off form of the MI355X guide's "Valid forms" table, row 1).  From p every
 //                 workgroup forms w = p - tau/2 (p^H v) v and, from the old row k + 1, the new row
 //                 k + 1 = old - conj(w) - w_{k+1} conj(v): the next column needs no second hand-off.
-//                 One exchange per column; spins bounded (100 ms, then the job declines).  Stops at
-//                 column C - 128 (aqc_gb_set_tail, the default) and leaves the trailing block to:
+//                 One exchange per column; spins bounded (100 ms, then the job declines).  At C = 512
+//                 in two stages (aqc_gb_set_stages, the default): columns 0 .. 255 over 16
+//                 workgroups, 256 .. 383 over 4 from the first stage's hand-off, a round's second
+//                 stage beside the next round's first.  Stops at column C - 128 (aqc_gb_set_tail,
+//                 the default) and leaves the trailing block to:
 //   k_gb_tail     the last 128 columns of a job in one workgroup (exchange through the LDS, wave 0
 //                 forms the reflectors); on the side stream, beside the next round's k_gb_tridiag.
 //   k_gb_eig      the top K eigenvalues of T by multisection with the polynomial Sturm count, 64
@@ -38,6 +41,8 @@
 //                 sigma_c), so k_rank / k_split_* run unchanged.
 // Jobs that decline (floor, timeout, gram disabled) run the block Jacobi afterwards (the host reads
 // the statuses once, after k_gb_eig).
+// The per-job GEMM kernels (k_gb_gram, k_gb_back) run on 1-D grids that put a job's workgroups on
+// one XCD (aqc_internal.h xcd_job_block: they share the job's operand panels in that XCD's L2).
 #include <cstdlib>
 #include <cstring>
 
