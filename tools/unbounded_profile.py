@@ -2,7 +2,7 @@
 (mps_sim_with_args, aer_mps_backend.py:27-42: max_chi=None; python_default_backends.py:19) and the
 reference example's threshold 1e-8 (examples/advanced_mps_example.py:46): the bench's thin layers
 (distances 1, 2, 5, 25, Aer swap routing, sort back) on 50-qubit chi = 64 states, capacity
-chi_cap_for(50, None) = 512 (the bond dimensions grow as the layers need), one batch per
+512 (the unbounded limit at n = 50; the bond dimensions grow as the layers need), one batch per
 configuration.  Per configuration: the Gram-path counters of both SVD paths (2 chi = 128:
 aqc_svd_gram_stats; 2 chi > 128: aqc_svd_gram_big_stats), the kernel-family times (HIP events), the
 wall time of the batch, the bond dimensions reached, and the time per two-site update.  For
@@ -72,9 +72,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--states", type=int, default=8)
     args = ap.parse_args()
-    from adaptaqc_amd.mps_operations import chi_cap_for
+    from adaptaqc_amd.mps_operations import _full_cap
 
-    cap = chi_cap_for(bench.N_QUBITS, None)
+    # the whole unbounded limit from the start (chi_cap_for now starts unbounded runs small and the
+    # product paths grow the capacity on overflow; this lab tool applies one batch directly)
+    cap = _full_cap(bench.N_QUBITS)
     cache = {}
     rows = []
     for kind in ("near-product", "random"):
