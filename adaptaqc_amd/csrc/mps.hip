@@ -137,53 +137,72 @@ __global__ __launch_bounds__(kT) void k_theta(const TwoSiteJob* __restrict__ job
   const TwoSiteJob& j = jobs[jb];
   const int chl = j.dims[0], chm = j.dims[1], chr = j.dims[2];
   const int cap = j.cap;
-  const int tiles_r = (cap + 15) / 16;
-  const int l0 = (tile / tiles_r) * 16, r0 = (tile % tiles_r) * 16;
+  // 32 x 32 output tiles, each thread 2 x 2 (l, r) positions x the four (s1, s2) products: per
+  // 16-deep m step 8 LDS operand reads for 16 complex FMAs (16 x 16 tiles with one position per
+  // thread read 4 for 4: the LDS port, not the FP64 rate, bounded them)
+  const int tiles_r = (cap + 31) / 32;
+  const int l0 = (tile / tiles_r) * 32, r0 = (tile % tiles_r) * 32;
   if (l0 >= chl || r0 >= chr) return;
-  __shared__ cplx As[2][16][17];
-  __shared__ cplx Bs[2][16][17];
-  const int ty = threadIdx.x / 16, tx = threadIdx.x % 16;
-  const int l = l0 + ty, r = r0 + tx;
+  __shared__ cplx As[2][32][17];
+  __shared__ cplx Bs[2][16][33];
+  const int tid = threadIdx.x, ty = tid >> 4, tx = tid & 15;
   const size_t half = (size_t)cap * cap;
-  cplx acc[4];
+  cplx acc[2][2][4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) acc[i] = aqc::cmk(0, 0);
-  const double lll = l < chl ? j.ll[l] : 0.0;
-  const double lrr = r < chr ? j.lr[r] : 0.0;
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+      for (int o = 0; o < 4; ++o) acc[i][jj][o] = aqc::cmk(0, 0);
   for (int m0 = 0; m0 < chm; m0 += 16) {
-    const int ma = m0 + tx, mb = m0 + ty;
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      cplx a = aqc::cmk(0, 0), b = aqc::cmk(0, 0);
-      if (l < chl && ma < chm) a = aqc::cscale(j.gp[s * half + (size_t)l * cap + ma], lll * j.lm[ma]);
-      if (mb < chm && r < chr) b = aqc::cscale(j.gq[s * half + (size_t)mb * cap + r], lrr);
-      As[s][ty][tx] = a;
-      Bs[s][ty][tx] = b;
+    for (int q = 0; q < 4; ++q) {
+      const int e = tid + kT * q;
+      {  // As[s][li][mm] = ll[l] Gp[s][l][m] lm[m]: consecutive threads along m
+        const int s = e >> 9, li = (e >> 4) & 31, mm = e & 15, l = l0 + li, m = m0 + mm;
+        As[s][li][mm] = (l < chl && m < chm) ? aqc::cscale(j.gp[s * half + (size_t)l * cap + m], j.ll[l] * j.lm[m])
+                                             : aqc::cmk(0, 0);
+      }
+      {  // Bs[s][mm][ri] = Gq[s][m][r] lr[r]: consecutive threads along r
+        const int s = e >> 9, mm = (e >> 5) & 15, ri = e & 31, m = m0 + mm, r = r0 + ri;
+        Bs[s][mm][ri] = (m < chm && r < chr) ? aqc::cscale(j.gq[s * half + (size_t)m * cap + r], j.lr[r]) : aqc::cmk(0, 0);
+      }
     }
     __syncthreads();
 #pragma unroll 4
     for (int mm = 0; mm < 16; ++mm) {
-      const cplx a0 = As[0][ty][mm], a1 = As[1][ty][mm];
-      const cplx b0 = Bs[0][mm][tx], b1 = Bs[1][mm][tx];
-      acc[0] = aqc::cfma(a0, b0, acc[0]);
-      acc[1] = aqc::cfma(a0, b1, acc[1]);
-      acc[2] = aqc::cfma(a1, b0, acc[2]);
-      acc[3] = aqc::cfma(a1, b1, acc[3]);
+      cplx a[2][2], b[2][2];  // [s][i] / [s][jj]
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int i = 0; i < 2; ++i) a[s2][i] = As[s2][ty + 16 * i][mm], b[s2][i] = Bs[s2][mm][tx + 16 * i];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+          for (int o = 0; o < 4; ++o) acc[i][jj][o] = aqc::cfma(a[o >> 1][i], b[o & 1][jj], acc[i][jj][o]);
     }
     __syncthreads();
   }
-  if (l < chl && r < chr) {
-    const int M = 2 * chl;
+  const int M = 2 * chl;
 #pragma unroll
-    for (int o = 0; o < 4; ++o) {
-      cplx v = aqc::cmul(j.G[o * 4 + 0], acc[0]);
-      v = aqc::cfma(j.G[o * 4 + 1], acc[1], v);
-      v = aqc::cfma(j.G[o * 4 + 2], acc[2], v);
-      v = aqc::cfma(j.G[o * 4 + 3], acc[3], v);
-      const int s1 = o >> 1, s2 = o & 1;
-      j.theta[(size_t)(s2 * chr + r) * M + s1 * chl + l] = v;
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      const int l = l0 + ty + 16 * i, r = r0 + tx + 16 * jj;
+      if (l < chl && r < chr) {
+#pragma unroll
+        for (int o = 0; o < 4; ++o) {
+          cplx v = aqc::cmul(j.G[o * 4 + 0], acc[i][jj][0]);
+          v = aqc::cfma(j.G[o * 4 + 1], acc[i][jj][1], v);
+          v = aqc::cfma(j.G[o * 4 + 2], acc[i][jj][2], v);
+          v = aqc::cfma(j.G[o * 4 + 3], acc[i][jj][3], v);
+          const int s1 = o >> 1, s2 = o & 1;
+          j.theta[(size_t)(s2 * chr + r) * M + s1 * chl + l] = v;
+        }
+      }
     }
-  }
 }
 
 // ---- register-resident one-sided Jacobi (2*chi <= 128) ----------------------------------
@@ -1942,7 +1961,7 @@ int run_waves(aqc_mps_t* hs, int ns, std::vector<std::vector<DevOp>>& lists) {
   if (int e = aqc::upload_async(sg.dev, sg.host, tb + ob, st)) return e;
   const TwoSiteJob* dtwo = (const TwoSiteJob*)sg.dev;
   const OneSiteJob* done = (const OneSiteJob*)((char*)sg.dev + tb);
-  const int tiles = ((cap_max + 15) / 16) * ((cap_max + 15) / 16);
+  const int tiles = ((cap_max + 31) / 32) * ((cap_max + 31) / 32);  // (k_theta's 32 x 32 tiles)
   const int blocks_split = ((2 * cap_max + 63) / 64) * ((2 * cap_max + 63) / 64);
   for (size_t w = 0; w < maxlen; ++w) {
     if (one_rng[w].second) {
