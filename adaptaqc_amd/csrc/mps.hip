@@ -137,6 +137,64 @@ __global__ __launch_bounds__(kT) void k_theta(const TwoSiteJob* __restrict__ job
   const TwoSiteJob& j = jobs[jb];
   const int chl = j.dims[0], chm = j.dims[1], chr = j.dims[2];
   const int cap = j.cap;
+  // (16 x 16 tiles, one position per thread: the small batches -- a single state's update at
+  // capacity 64 is 16 workgroups here, 4 in k_theta32)
+  const int tiles_r = (cap + 15) / 16;
+  const int l0 = (tile / tiles_r) * 16, r0 = (tile % tiles_r) * 16;
+  if (l0 >= chl || r0 >= chr) return;
+  __shared__ cplx As[2][16][17];
+  __shared__ cplx Bs[2][16][17];
+  const int ty = threadIdx.x / 16, tx = threadIdx.x % 16;
+  const int l = l0 + ty, r = r0 + tx;
+  const size_t half = (size_t)cap * cap;
+  cplx acc[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) acc[i] = aqc::cmk(0, 0);
+  const double lll = l < chl ? j.ll[l] : 0.0;
+  const double lrr = r < chr ? j.lr[r] : 0.0;
+  for (int m0 = 0; m0 < chm; m0 += 16) {
+    const int ma = m0 + tx, mb = m0 + ty;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      cplx a = aqc::cmk(0, 0), b = aqc::cmk(0, 0);
+      if (l < chl && ma < chm) a = aqc::cscale(j.gp[s * half + (size_t)l * cap + ma], lll * j.lm[ma]);
+      if (mb < chm && r < chr) b = aqc::cscale(j.gq[s * half + (size_t)mb * cap + r], lrr);
+      As[s][ty][tx] = a;
+      Bs[s][ty][tx] = b;
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int mm = 0; mm < 16; ++mm) {
+      const cplx a0 = As[0][ty][mm], a1 = As[1][ty][mm];
+      const cplx b0 = Bs[0][mm][tx], b1 = Bs[1][mm][tx];
+      acc[0] = aqc::cfma(a0, b0, acc[0]);
+      acc[1] = aqc::cfma(a0, b1, acc[1]);
+      acc[2] = aqc::cfma(a1, b0, acc[2]);
+      acc[3] = aqc::cfma(a1, b1, acc[3]);
+    }
+    __syncthreads();
+  }
+  if (l < chl && r < chr) {
+    const int M = 2 * chl;
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+      cplx v = aqc::cmul(j.G[o * 4 + 0], acc[0]);
+      v = aqc::cfma(j.G[o * 4 + 1], acc[1], v);
+      v = aqc::cfma(j.G[o * 4 + 2], acc[2], v);
+      v = aqc::cfma(j.G[o * 4 + 3], acc[3], v);
+      const int s1 = o >> 1, s2 = o & 1;
+      j.theta[(size_t)(s2 * chr + r) * M + s1 * chl + l] = v;
+    }
+  }
+}
+
+// The same with 32 x 32 tiles (the batches that fill the GPU with them: config 5's waves):
+__global__ __launch_bounds__(kT) void k_theta32(const TwoSiteJob* __restrict__ jobs, int nj) {
+  int jb, tile;
+  if (!aqc::xcd_job_block(nj, jb, tile)) return;  // (a job's tiles on one XCD: they share panels)
+  const TwoSiteJob& j = jobs[jb];
+  const int chl = j.dims[0], chm = j.dims[1], chr = j.dims[2];
+  const int cap = j.cap;
   // 32 x 32 output tiles, each thread 2 x 2 (l, r) positions x the four (s1, s2) products: per
   // 16-deep m step 8 LDS operand reads for 16 complex FMAs (16 x 16 tiles with one position per
   // thread read 4 for 4: the LDS port, not the FP64 rate, bounded them)
@@ -1961,7 +2019,8 @@ int run_waves(aqc_mps_t* hs, int ns, std::vector<std::vector<DevOp>>& lists) {
   if (int e = aqc::upload_async(sg.dev, sg.host, tb + ob, st)) return e;
   const TwoSiteJob* dtwo = (const TwoSiteJob*)sg.dev;
   const OneSiteJob* done = (const OneSiteJob*)((char*)sg.dev + tb);
-  const int tiles = ((cap_max + 31) / 32) * ((cap_max + 31) / 32);  // (k_theta's 32 x 32 tiles)
+  const int tiles = ((cap_max + 15) / 16) * ((cap_max + 15) / 16);
+  const int tiles32 = ((cap_max + 31) / 32) * ((cap_max + 31) / 32);
   const int blocks_split = ((2 * cap_max + 63) / 64) * ((2 * cap_max + 63) / 64);
   for (size_t w = 0; w < maxlen; ++w) {
     if (one_rng[w].second) {
@@ -1975,7 +2034,10 @@ int run_waves(aqc_mps_t* hs, int ns, std::vector<std::vector<DevOp>>& lists) {
       const TwoSiteJob* jp = dtwo + two_rng[w].first;
       const double c = cap_max;
       aqc::KernelTimer::begin(st, "mps_theta", nj * (6.0 * c * c * 16 + 4.0 * c * c * 16), nj * 4.0 * c * c * c * 8);
-      hipLaunchKernelGGL(k_theta, dim3(aqc::xcd_grid(tiles, nj)), dim3(kT), 0, st, jp, nj);
+      if (tiles32 * nj >= 256)  // (enough 32 x 32 tiles to fill the GPU)
+        hipLaunchKernelGGL(k_theta32, dim3(aqc::xcd_grid(tiles32, nj)), dim3(kT), 0, st, jp, nj);
+      else
+        hipLaunchKernelGGL(k_theta, dim3(aqc::xcd_grid(tiles, nj)), dim3(kT), 0, st, jp, nj);
       aqc::KernelTimer::end(st);
       AQC_CHECK_LAUNCH();
       aqc::KernelTimer::begin(st, "mps_svd", nj * 2.0 * (4.0 * c * c * 16), 0.0);
