@@ -397,3 +397,27 @@ def test_z_all_batch_split_environments_vs_oracle(n, cap):
     got = z_all_batch(states)
     np.testing.assert_allclose(got, np.array(want), atol=1e-12)
     np.testing.assert_allclose(states[1].z_all(), got[1], atol=1e-13)
+
+
+@pytest.mark.gpu
+def test_z_all_batch_two_rounds_of_chains():
+    """30 states at capacity 64: the environment chains run in two rounds (28 states, then 2), on the
+    XCD-grouped grid with its padding (56 and 4 chains, padded to 56 and 8): every state's <Z_i>
+    equal to its own single-state call, and three of them against the oracle at 1e-12."""
+    import bench
+    from adaptaqc_amd.device import DeviceMPS, z_all_batch
+
+    n, cap = 14, 64
+    states, aers = [], []
+    for seed in range(30):
+        q = bench.random_vidal_mps(n, cap, 300 + seed)
+        d = DeviceMPS(n, cap, 1e-16, cap)
+        d.load_aer(q)
+        states.append(d)
+        aers.append(q)
+    got = z_all_batch(states)
+    for k in range(30):
+        np.testing.assert_allclose(states[k].z_all(), got[k], atol=1e-13)
+    for k in (0, 27, 29):
+        pre = M.MPS.from_aer(aers[k]).preprocessed()
+        np.testing.assert_allclose(got[k], [M.mps_expectation_z(pre, i) for i in range(n)], atol=1e-12)
