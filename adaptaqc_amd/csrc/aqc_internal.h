@@ -103,16 +103,25 @@ __device__ __forceinline__ void stg(double* p, double v) { *(gdouble*)p = v; }
 // each.  Offsets past `bytes` (lane offset + instruction offset) read as zero.  0x00020000 is the
 // gfx9 data-format word of the resource.
 // Per-job grids laid out so that a job's workgroups share one XCD (and its L2) under the
-// dispatcher's round-robin placement: a 1-D grid of nblk x njp blocks (njp = nj rounded up to 8),
-// block id = job + njp blk.  False for the padding's blocks (whole workgroups: return at once).
-// Placement is a speed matter only.
-__device__ __forceinline__ bool xcd_job_block(int nj, int& job, int& blk) {
-  const int njp = (nj + 7) & ~7;
+// dispatcher's round-robin placement: a 1-D grid of nblk x njp blocks, block id = job + njp blk,
+// njp = nj rounded up to 8.  With `fair` set, njp = nj itself below 8 jobs: a job's blocks then
+// cycle over 8 / gcd(nj, 8) XCDs, its share of the chip -- for jobs of many more workgroups than
+// one XCD has CUs (one pair-RDM state's 147 chains on one XCD ran 2.5x slower; the lock-step
+// per-job kernels measured no better either way, profiles/r5_xcd_fair_ab.json, and keep the
+// plain rule).  False for the padding's blocks (whole workgroups: return at once).  Placement
+// is a speed matter only.
+__host__ __device__ __forceinline__ int xcd_pad(int nj, bool fair = false) {
+  return fair && nj < 8 ? nj : (nj + 7) & ~7;
+}
+__device__ __forceinline__ bool xcd_job_block(int nj, int& job, int& blk, bool fair = false) {
+  const int njp = xcd_pad(nj, fair);
   job = (int)blockIdx.x % njp;
   blk = (int)blockIdx.x / njp;
   return job < nj;
 }
-inline unsigned xcd_grid(int nblk, int nj) { return (unsigned)nblk * (unsigned)((nj + 7) & ~7); }
+inline unsigned xcd_grid(int nblk, int nj, bool fair = false) {
+  return (unsigned)nblk * (unsigned)xcd_pad(nj, fair);
+}
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, unsigned bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);

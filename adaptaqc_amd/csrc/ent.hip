@@ -536,15 +536,20 @@ __global__ __launch_bounds__(kT) void k_rdm_P(const RdmJob* __restrict__ jobs, i
 }
 
 // grid (3 bra/ket combos of site a, first qubits, states)
-__global__ __launch_bounds__(kT) void k_rdm_chain(const RdmJob* __restrict__ jobs, const int* __restrict__ alist) {
-  const RdmJob& j = jobs[blockIdx.z];
+__global__ __launch_bounds__(kT) void k_rdm_chain(const RdmJob* __restrict__ jobs, const int* __restrict__ alist,
+                                                  int ns) {
+  // (from 8 states up, a state's chains -- which read the same P_b and site tensors -- on one
+  // XCD; below, over the state's share of the XCDs: aqc_internal.h xcd_job_block; block = 3 ai + m)
+  int st, blk;
+  if (!aqc::xcd_job_block(ns, st, blk, true)) return;
+  const RdmJob& j = jobs[st];
   __shared__ aqc::GemmLds lds;
   __shared__ double red[8][kT];
-  const int m = blockIdx.x, a = alist[blockIdx.y];
+  const int m = blk % 3, ai = blk / 3, a = alist[ai];
   const int sb = m == 2 ? 1 : 0, s = m == 0 ? 0 : 1;  // E[sb][s]: bra index sb, ket index s
   const int n = j.n, cap = j.cap, tid = threadIdx.x;
   const size_t cc = (size_t)cap * cap;
-  cplx* base = j.chain + ((size_t)blockIdx.y * 3 + m) * 4 * cc;
+  cplx* base = j.chain + ((size_t)ai * 3 + m) * 4 * cc;
   cplx* Eb[2] = {base, base + cc};
   cplx* T = base + 2 * cc;  // cap x 2cap
   {
@@ -941,7 +946,7 @@ int aqc_mps_pair_rdms_batch(aqc_mps_t* hs, int ns, const int* pairs, int npairs,
   double steps = 0.0;
   for (int a : alist) steps += (double)(n - 1 - a);
   aqc::KernelTimer::begin(st, "rdm_chain", 0.0, ns * steps * 3.0 * 4.0 * c3 * 8.0);
-  hipLaunchKernelGGL(k_rdm_chain, dim3(3, na, ns), dim3(kT), 0, st, djobs, dalist);
+  hipLaunchKernelGGL(k_rdm_chain, dim3(aqc::xcd_grid(3 * na, ns, true)), dim3(kT), 0, st, djobs, dalist, ns);
   aqc::KernelTimer::end(st);
   AQC_CHECK_LAUNCH();
   hipLaunchKernelGGL(k_rdm_gather, dim3((npairs * 16 + 255) / 256, ns), dim3(256), 0, st, djobs, dpairs, npairs, dout);
