@@ -510,7 +510,9 @@ __global__ __launch_bounds__(256) void k_env64(const RdmJob* __restrict__ jobs, 
   }
 }
 
-// P_b[s][sb] = A_b^s R_{b+1} A_b^{sb dag}; m = 0: (0,0), 1: (0,1), 2: (1,1).  grid (n, 3 or 2, states);
+// P_b[s][sb] = A_b^s R_{b+1} A_b^{sb dag}, stored transposed (j.P holds P^T: the traces against it,
+// Tr(E P) in the pair chains and Tr(L P) in k_rdm_ztrace, then read both operands along rows);
+// m = 0: (0,0), 1: (0,1), 2: (1,1).  grid (n, 3 or 2, states);
 // with two m, the diagonal pair (0,0), (1,1) only (single-site <Z>).  first_site: site 0 too (pair
 // RDMs never need it: it is never the second qubit of a pair)
 __global__ __launch_bounds__(kT) void k_rdm_P(const RdmJob* __restrict__ jobs, int first_site) {
@@ -531,7 +533,7 @@ __global__ __launch_bounds__(kT) void k_rdm_P(const RdmJob* __restrict__ jobs, i
   __syncthreads();
   aqc::block_cgemm<true, true, kEnvPf>(
       cl, cl, cr, [&](int l, int k) { return U[(size_t)l * cap + k]; },
-      [&](int k, int c) { return aqc::cconj(aval(j, b, sb, c, k)); }, [&](int l, int c, cplx v) { P[(size_t)l * cap + c] = v; },
+      [&](int k, int c) { return aqc::cconj(aval(j, b, sb, c, k)); }, [&](int l, int c, cplx v) { P[(size_t)c * cap + l] = v; },
       lds);
 }
 
@@ -544,7 +546,7 @@ __global__ __launch_bounds__(kT) void k_rdm_chain(const RdmJob* __restrict__ job
   if (!aqc::xcd_job_block(ns, st, blk, true)) return;
   const RdmJob& j = jobs[st];
   __shared__ aqc::GemmLds lds;
-  __shared__ double red[8][kT];
+  __shared__ double red[8][kT / 64];
   const int m = blk % 3, ai = blk / 3, a = alist[ai];
   const int sb = m == 2 ? 1 : 0, s = m == 0 ? 0 : 1;  // E[sb][s]: bra index sb, ket index s
   const int n = j.n, cap = j.cap, tid = threadIdx.x;
@@ -571,6 +573,7 @@ __global__ __launch_bounds__(kT) void k_rdm_chain(const RdmJob* __restrict__ job
     const int cl = j.dims[b], cr = j.dims[b + 1];
     const cplx* E = Eb[cur];
     // closing: v[s_b][sb_b] = sum_{ij} E[i][j] P_b[s_b][sb_b][j][i], with P[1][0] = P[0][1]^dag
+    // (j.P holds P^T: E and three of the four operands read along rows)
     const cplx* P00 = j.P + ((size_t)b * 3 + 0) * cc;
     const cplx* P01 = j.P + ((size_t)b * 3 + 1) * cc;
     const cplx* P11 = j.P + ((size_t)b * 3 + 2) * cc;
@@ -578,24 +581,30 @@ __global__ __launch_bounds__(kT) void k_rdm_chain(const RdmJob* __restrict__ job
     for (int e = tid; e < cl * cl; e += kT) {
       const int i = e / cl, jj = e % cl;
       const cplx ev = E[(size_t)i * cap + jj];
-      const cplx p00 = P00[(size_t)jj * cap + i], p01 = P01[(size_t)jj * cap + i], p11 = P11[(size_t)jj * cap + i];
-      const cplx p10 = aqc::cconj(P01[(size_t)i * cap + jj]);
+      const cplx p00 = P00[(size_t)i * cap + jj], p01 = P01[(size_t)i * cap + jj], p11 = P11[(size_t)i * cap + jj];
+      const cplx p10 = aqc::cconj(P01[(size_t)jj * cap + i]);
       const cplx v00 = aqc::cmul(ev, p00), v01 = aqc::cmul(ev, p01), v10 = aqc::cmul(ev, p10), v11 = aqc::cmul(ev, p11);
       acc[0] += v00.x, acc[1] += v00.y, acc[2] += v01.x, acc[3] += v01.y;
       acc[4] += v10.x, acc[5] += v10.y, acc[6] += v11.x, acc[7] += v11.y;
     }
+    // wave sums (DPP rows, then readlane), the waves' partials through the LDS
 #pragma unroll
-    for (int q = 0; q < 8; ++q) red[q][tid] = acc[q];
-    __syncthreads();
-    for (int h = kT / 2; h > 0; h >>= 1) {
-      if (tid < h)
+    for (int q = 0; q < 8; ++q) {
+      const double w = aqc::row_sum16(acc[q]);
+      double t = 0.0;
 #pragma unroll
-        for (int q = 0; q < 8; ++q) red[q][tid] += red[q][tid + h];
-      __syncthreads();
+      for (int rr = 0; rr < 4; ++rr)
+        t += __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(w), 16 * rr),
+                              __builtin_amdgcn_readlane(__double2loint(w), 16 * rr));
+      if ((tid & 63) == 0) red[q][tid >> 6] = t;
     }
+    __syncthreads();
     if (tid < 4) {
       const int sbk = tid >> 1, sbb = tid & 1;  // ket / bra index of site b
-      const cplx v = aqc::cmk(red[2 * tid][0], red[2 * tid + 1][0]);
+      double re = 0.0, im = 0.0;
+#pragma unroll
+      for (int w = 0; w < kT / 64; ++w) re += red[2 * tid][w], im += red[2 * tid + 1][w];
+      const cplx v = aqc::cmk(re, im);
       cplx* rho = j.rho + ((size_t)a * n + b) * 16;
       rho[(2 * sbk + s) * 4 + (2 * sbb + sb)] = v;
       if (m == 1) rho[(2 * sbb + sb) * 4 + (2 * sbk + s)] = aqc::cconj(v);  // the (sb=1, s=0) block
@@ -633,9 +642,9 @@ __global__ __launch_bounds__(kT) void k_rdm_ztrace(const RdmJob* __restrict__ jo
   __shared__ double red[kT];
   double acc = 0.0;
   for (int e = threadIdx.x; e < cl * cl; e += kT) {
-    const int c = e / cl, cp = e % cl;  // L[cp][c] P[c][cp]
+    const int c = e % cl, cp = e / cl;  // L[cp][c] P[c][cp] (j.P holds P^T: both along rows)
     const cplx l = L[(size_t)cp * cap + c];
-    const cplx d = aqc::csub(P0[(size_t)c * cap + cp], P1[(size_t)c * cap + cp]);
+    const cplx d = aqc::csub(P0[(size_t)cp * cap + c], P1[(size_t)cp * cap + c]);
     acc = fma(l.x, d.x, fma(-l.y, d.y, acc));
   }
   red[threadIdx.x] = acc;
