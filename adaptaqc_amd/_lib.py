@@ -39,6 +39,7 @@ EXPORTS = (
     "aqc_comm_unique_id", "aqc_comm_init", "aqc_comm_destroy", "aqc_comm_rank", "aqc_allgather_f64",
     "aqc_allgather_f64_host", "aqc_allreduce_max_f64", "aqc_svd_gram_big_stats", "aqc_svd_gram_big_ticks",
     "aqc_gb_set_spin_limit", "aqc_gb_set_tail", "aqc_gb_set_stages", "aqc_debug_hog", "aqc_pool_stats",
+    "aqc_env_fallbacks", "aqc_env_set_single", "aqc_env_set_spin_limit",
 )
 
 
@@ -129,6 +130,9 @@ _SIGS = {
     "aqc_svd_gram_big_stats": ([_P], _I),
     "aqc_svd_gram_big_ticks": ([_P], _I),
     "aqc_gb_set_spin_limit": ([_D], _I),
+    "aqc_env_fallbacks": ([ctypes.POINTER(ctypes.c_longlong)], _I),
+    "aqc_env_set_single": ([_I], _I),
+    "aqc_env_set_spin_limit": ([_D], _I),
     "aqc_gb_set_tail": ([_I], _I),
     "aqc_gb_set_stages": ([_I], _I),
     "aqc_debug_hog": ([_I, _D], _I),

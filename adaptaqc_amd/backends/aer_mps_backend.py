@@ -27,7 +27,7 @@ import numpy as np
 from ..circuit import device_ops_array, mps_payload
 from ..device import DeviceMPS
 from ..mps_operations import (DevicePreprocessedMPS, apply_checked, chi_cap_for, grow_capacity, is_capacity_error,
-                              zero_aer_mps)
+                              learned_capacities, zero_aer_mps)
 from .aqc_backend import AQCBackend
 
 logger = logging.getLogger(__name__)
@@ -85,7 +85,7 @@ class AerMPSBackend(AQCBackend):
             start = 1
         key = id(payload) if payload is not None else ("zero", n)
         lmax = max(np.asarray(a).shape[1] for a, _ in payload[0]) if payload is not None else 1
-        cap = chi_cap_for(n, max_chi, lmax)
+        cap = chi_cap_for(n, max_chi, lmax, learned_capacities(self.simulator))
         if self._base is None or self._base[0] != key or self._base[2] is not payload or self._base[1].chi_cap != cap:
             base = DeviceMPS(n, cap, thr, max_chi)
             base.load_aer(payload if payload is not None else zero_aer_mps(n))
@@ -106,6 +106,8 @@ class AerMPSBackend(AQCBackend):
         base = self._base[1]
         thr, max_chi = self._options()
         pools = self.__dict__.setdefault("_scratch_pools", {})
+        for key in [key for key in pools if key != (base.n, base.chi_cap)]:
+            del pools[key]  # (states of an outgrown capacity: released)
         pool = pools.setdefault((base.n, base.chi_cap), [])
         while len(pool) < k:
             pool.append(DeviceMPS(base.n, base.chi_cap, thr, max_chi))
@@ -119,7 +121,12 @@ class AerMPSBackend(AQCBackend):
         new_state / scratch_states follow it), else False."""
         _, max_chi = self._options()
         return (self._base is not None and is_capacity_error(e)
-                and grow_capacity(self._base[1].n, max_chi, self._base[1].chi_cap))
+                and grow_capacity(self._base[1].n, max_chi, self._base[1].chi_cap, learned_capacities(self.simulator)))
+
+    def reset_learned_capacity(self):
+        """Forget the capacities unbounded replays needed (called at the start of each compile, so a
+        compile starts from the smallest capacity that holds its own states)."""
+        learned_capacities(self.simulator).clear()
 
     def device_state(self, circuit):
         """Replay ``circuit`` on the device; returns the (sorted) work DeviceMPS."""

@@ -120,6 +120,9 @@ class AdaptCompiler(ApproximateCompiler):
         """adapt_compiler.py:246-482."""
         start_time = timeit.default_timer()
         if self.resume_from_layer is None:
+            reset = getattr(self.backend, "reset_learned_capacity", None)
+            if reset is not None:  # (capacity learned by earlier compiles on this backend: not ours)
+                reset()
             self.time_taken = 0
             start_point = 0
             self.cost_evaluation_counter = 0

@@ -834,12 +834,33 @@ int ensure(RdmBuffers& b, size_t need) {
 // Counter / error words behind the jobs of an environment launch: 32 words per chain, one error word.
 size_t env_sync_bytes(int ns) { return (((size_t)ns * 2 * 32 + 32) * sizeof(unsigned) + 255) / 256 * 256; }
 
+// Output columns per workgroup of the split environment chains for a capacity, or 0 where the
+// chains run one workgroup each (k_rdm_env).  Each split kernel's slices of tmpL / tmpR are sized for
+// exactly cap = kEnvNW x CW (cap = 192, 320, 384, 448 once fell to k_env_split<128> and its
+// slices ran past the 2 cap^2 scratch), so only these four capacities take them.
+int env_split_cols(int cap) {
+  switch (cap) {
+    case 64: return 16;
+    case 128: return 32;
+    case 256: return 64;
+    case 512: return 128;
+    default: return 0;
+  }
+}
+
+// environment launches that timed out on a hand-off and were re-run by k_rdm_env (aqc_env_fallbacks)
+unsigned long long g_env_fallbacks = 0;
+int g_env_single = 0;  // aqc_env_set_single: every chain on one workgroup
+constexpr unsigned long long kEnvSpin = 200000000ull;  // s_memrealtime (100 MHz): 2 s
+unsigned long long g_env_spin = kEnvSpin;  // aqc_env_set_spin_limit (0: any unsatisfied wait times out)
+
 // The left / right environments of every state: kEnvNW workgroups per chain where the capacity
-// splits into 16-column multiples (k_env64 at capacity 64, k_env_split above), else k_rdm_env;
-// states in rounds small enough that every chain's workgroups are resident together.  sync:
-// env_sync_bytes(ns) of device memory.
-int launch_envs(RdmJob* djobs, int ns, int cap, hipStream_t st, void* sync) {
-  if (cap % (16 * kEnvNW) != 0) {
+// is one of env_split_cols' (k_env64 at capacity 64, k_env_split above), else -- or with single --
+// k_rdm_env; states in rounds small enough that every chain's workgroups are resident together.
+// sync: env_sync_bytes(ns) of device memory.
+int launch_envs(RdmJob* djobs, int ns, int cap, hipStream_t st, void* sync, bool single = false) {
+  const int cw = (single || g_env_single) ? 0 : env_split_cols(cap);
+  if (cw == 0) {
     hipLaunchKernelGGL(k_rdm_env, dim3(2, ns), dim3(kT), 0, st, djobs);
     AQC_CHECK_LAUNCH();
     return AQC_OK;
@@ -847,30 +868,38 @@ int launch_envs(RdmJob* djobs, int ns, int cap, hipStream_t st, void* sync) {
   unsigned* cnt = (unsigned*)sync;
   int* err = (int*)(cnt + (size_t)ns * 2 * 32);
   AQC_HIP_CHECK(hipMemsetAsync(sync, 0, env_sync_bytes(ns), st));
-  constexpr unsigned long long kSpin = 200000000ull;  // s_memrealtime (100 MHz): 2 s
+  const unsigned long long kSpin = g_env_spin;
   constexpr int kRound = 28;  // 28 x 8 workgroups: one per CU (~400 VGPRs a lane) leaves room
   for (int s0 = 0; s0 < ns; s0 += kRound) {
     const int m = std::min(kRound, ns - s0);
     const dim3 xg((2 * m + 7) / 8 * 8, kEnvNW);  // (chains padded to 8, workgroup: one XCD per chain)
     RdmJob* jb = djobs + s0;
     unsigned* cb = cnt + (size_t)s0 * 2 * 32;
-    switch (cap / kEnvNW) {
+    switch (cw) {
       case 16: hipLaunchKernelGGL(k_env64, xg, dim3(256), 0, st, jb, cb, err, kSpin, 2 * m); break;
       case 32: hipLaunchKernelGGL(k_env_split<32>, xg, dim3(kT), 0, st, jb, cb, err, kSpin, 2 * m); break;
       case 64: hipLaunchKernelGGL(k_env_split<64>, xg, dim3(kT), 0, st, jb, cb, err, kSpin, 2 * m); break;
-      default: hipLaunchKernelGGL(k_env_split<128>, xg, dim3(kT), 0, st, jb, cb, err, kSpin, 2 * m); break;
+      case 128: hipLaunchKernelGGL(k_env_split<128>, xg, dim3(kT), 0, st, jb, cb, err, kSpin, 2 * m); break;
+      default: aqc::set_error("launch_envs: no split environment kernel for this capacity"); return AQC_ERR_ARG;
     }
     AQC_CHECK_LAUNCH();
   }
   return AQC_OK;
 }
 
-// after the stream synchronised: a chain whose workgroups were not resident together timed out
-int env_check(void* sync, int ns, int cap) {
-  if (cap % (16 * kEnvNW) != 0) return AQC_OK;
+// After the stream synchronised: did a split chain's hand-off time out (its workgroups were not all
+// resident together, e.g. while other streams' kernels held CUs)?  *timed_out = true: the caller
+// re-runs the call with single-workgroup chains (k_rdm_env, no co-residency needed) -- a scheduling
+// condition, not a failure of the evaluation; gram_big declines to the block Jacobi the same way.
+int env_timed_out(void* sync, int ns, int cap, bool& timed_out) {
+  timed_out = false;
+  if (g_env_single || env_split_cols(cap) == 0) return AQC_OK;
   int e = 0;
   AQC_HIP_CHECK(hipMemcpy(&e, (int*)((unsigned*)sync + (size_t)ns * 2 * 32), sizeof(int), hipMemcpyDeviceToHost));
-  AQC_REQUIRE(e == 0, "environment chains: a workgroup hand-off timed out (workgroups not co-resident)");
+  if (e != 0) {
+    timed_out = true;
+    ++g_env_fallbacks;
+  }
   return AQC_OK;
 }
 
@@ -946,24 +975,31 @@ int aqc_mps_pair_rdms_batch(aqc_mps_t* hs, int ns, const int* pairs, int npairs,
   AQC_HIP_CHECK(hipMemcpyAsync(dpairs, pairs, 2 * npairs * sizeof(int), hipMemcpyHostToDevice, st));
   AQC_HIP_CHECK(hipMemcpyAsync(dalist, alist.data(), na * sizeof(int), hipMemcpyHostToDevice, st));
   const double c3 = (double)cap * cap * cap;
-  aqc::KernelTimer::begin(st, "rdm_env", 0.0, ns * 2.0 * n * 4.0 * c3 * 8.0);
-  rc = launch_envs(djobs, ns, cap, st, dsync);
-  aqc::KernelTimer::end(st);
-  if (rc != AQC_OK) return rc;
-  hipLaunchKernelGGL(k_rdm_P, dim3(n, 3, ns), dim3(kT), 0, st, djobs, 0);
-  AQC_CHECK_LAUNCH();
   double steps = 0.0;
   for (int a : alist) steps += (double)(n - 1 - a);
-  aqc::KernelTimer::begin(st, "rdm_chain", 0.0, ns * steps * 3.0 * 4.0 * c3 * 8.0);
-  hipLaunchKernelGGL(k_rdm_chain, dim3(aqc::xcd_grid(3 * na, ns, true)), dim3(kT), 0, st, djobs, dalist, ns);
-  aqc::KernelTimer::end(st);
-  AQC_CHECK_LAUNCH();
-  hipLaunchKernelGGL(k_rdm_gather, dim3((npairs * 16 + 255) / 256, ns), dim3(256), 0, st, djobs, dpairs, npairs, dout);
-  AQC_CHECK_LAUNCH();
-  if (!out_is_device)
-    AQC_HIP_CHECK(hipMemcpyAsync(out, dout, (size_t)ns * npairs * 16 * sizeof(cplx), hipMemcpyDeviceToHost, st));
-  AQC_HIP_CHECK(hipStreamSynchronize(st));
-  return env_check(dsync, ns, cap);
+  for (int attempt = 0;; ++attempt) {  // attempt 1: the split chains timed out, single-workgroup chains
+    aqc::KernelTimer::begin(st, "rdm_env", 0.0, ns * 2.0 * n * 4.0 * c3 * 8.0);
+    rc = launch_envs(djobs, ns, cap, st, dsync, attempt > 0);
+    aqc::KernelTimer::end(st);
+    if (rc != AQC_OK) return rc;
+    hipLaunchKernelGGL(k_rdm_P, dim3(n, 3, ns), dim3(kT), 0, st, djobs, 0);
+    AQC_CHECK_LAUNCH();
+    aqc::KernelTimer::begin(st, "rdm_chain", 0.0, ns * steps * 3.0 * 4.0 * c3 * 8.0);
+    hipLaunchKernelGGL(k_rdm_chain, dim3(aqc::xcd_grid(3 * na, ns, true)), dim3(kT), 0, st, djobs, dalist, ns);
+    aqc::KernelTimer::end(st);
+    AQC_CHECK_LAUNCH();
+    hipLaunchKernelGGL(k_rdm_gather, dim3((npairs * 16 + 255) / 256, ns), dim3(256), 0, st, djobs, dpairs, npairs, dout);
+    AQC_CHECK_LAUNCH();
+    if (!out_is_device)
+      AQC_HIP_CHECK(hipMemcpyAsync(out, dout, (size_t)ns * npairs * 16 * sizeof(cplx), hipMemcpyDeviceToHost, st));
+    AQC_HIP_CHECK(hipStreamSynchronize(st));
+    bool again = false;
+    if (attempt == 0) {
+      rc = env_timed_out(dsync, ns, cap, again);
+      if (rc != AQC_OK) return rc;
+    }
+    if (!again) return AQC_OK;
+  }
 }
 
 int aqc_mps_z_all_batch(aqc_mps_t* hs, int ns, double* out) {
@@ -1013,17 +1049,48 @@ int aqc_mps_z_all_batch(aqc_mps_t* hs, int ns, double* out) {
   }
   AQC_HIP_CHECK(hipMemcpyAsync(djobs, jobs.data(), ns * sizeof(RdmJob), hipMemcpyHostToDevice, st));
   const double c3 = (double)cap * cap * cap;
-  aqc::KernelTimer::begin(st, "mps_zall", 0.0, ns * 2.0 * n * 4.0 * c3 * 8.0);
-  rc = launch_envs(djobs, ns, cap, st, dsync);
-  if (rc != AQC_OK) return rc;
-  hipLaunchKernelGGL(k_rdm_P, dim3(n, 2, ns), dim3(kT), 0, st, djobs, 1);
-  AQC_CHECK_LAUNCH();
-  hipLaunchKernelGGL(k_rdm_ztrace, dim3(n, ns), dim3(kT), 0, st, djobs, dout);
-  aqc::KernelTimer::end(st);
-  AQC_CHECK_LAUNCH();
-  AQC_HIP_CHECK(hipMemcpyAsync(out, dout, (size_t)ns * n * sizeof(double), hipMemcpyDeviceToHost, st));
-  AQC_HIP_CHECK(hipStreamSynchronize(st));
-  return env_check(dsync, ns, cap);
+  for (int attempt = 0;; ++attempt) {  // attempt 1: the split chains timed out, single-workgroup chains
+    aqc::KernelTimer::begin(st, "mps_zall", 0.0, ns * 2.0 * n * 4.0 * c3 * 8.0);
+    rc = launch_envs(djobs, ns, cap, st, dsync, attempt > 0);
+    if (rc != AQC_OK) return rc;
+    hipLaunchKernelGGL(k_rdm_P, dim3(n, 2, ns), dim3(kT), 0, st, djobs, 1);
+    AQC_CHECK_LAUNCH();
+    hipLaunchKernelGGL(k_rdm_ztrace, dim3(n, ns), dim3(kT), 0, st, djobs, dout);
+    aqc::KernelTimer::end(st);
+    AQC_CHECK_LAUNCH();
+    AQC_HIP_CHECK(hipMemcpyAsync(out, dout, (size_t)ns * n * sizeof(double), hipMemcpyDeviceToHost, st));
+    AQC_HIP_CHECK(hipStreamSynchronize(st));
+    bool again = false;
+    if (attempt == 0) {
+      rc = env_timed_out(dsync, ns, cap, again);
+      if (rc != AQC_OK) return rc;
+    }
+    if (!again) return AQC_OK;
+  }
+}
+
+/* Environment launches whose split chains timed out on a hand-off and were re-run with
+   single-workgroup chains since the last call (then reset). */
+int aqc_env_fallbacks(long long* out) {
+  AQC_REQUIRE(out, "aqc_env_fallbacks: null argument");
+  *out = (long long)g_env_fallbacks;
+  g_env_fallbacks = 0;
+  return AQC_OK;
+}
+
+/* Force single-workgroup environment chains (1) or the default per-capacity choice (0): the tests'
+   reference for the split kernels. */
+int aqc_env_set_single(int on) {
+  AQC_REQUIRE(on == 0 || on == 1, "aqc_env_set_single: on must be 0 or 1");
+  g_env_single = on;
+  return AQC_OK;
+}
+
+/* Hand-off wait limit of the split environment chains in microseconds (< 0: the default, 2 s).
+   0 makes any wait not already satisfied a timeout: the tests use it to exercise the re-run. */
+int aqc_env_set_spin_limit(double us) {
+  g_env_spin = us < 0 ? kEnvSpin : (unsigned long long)(us * 100.0);
+  return AQC_OK;
 }
 
 int aqc_env_ticks(double* out) {

@@ -45,22 +45,41 @@ def _preprocess_mps(qiskit_mps):
 # Unbounded runs (max_chi None, the reference default) grow their capacity on demand, as Aer's MPS
 # grows its bonds: a replay starts at the smallest power of two >= 64 that holds the loaded MPS and
 # whatever an earlier replay on as many qubits needed, and a capacity overflow re-runs it at twice
-# the capacity (up to min(512, 2^(n/2))).  Until round 4 they took that upper bound at once, and
-# every kernel whose work follows the capacity -- the candidate sweep's cap x cap transfer
+# the capacity (up to min(MAX_CHI_CAP, 2^(n/2))).  Until round 4 they took that upper bound at once,
+# and every kernel whose work follows the capacity -- the candidate sweep's cap x cap transfer
 # matrices, whole-state copies -- paid for 512 at bond 64 (~100 ms per sweep, 0.4 ms at 64).
-_UNBOUNDED_CAP = {}  # n -> the capacity the last unbounded replay on n qubits needed (only grows)
+# The learned capacities (n -> capacity) belong to a simulator -- the backend's MPSSimulator, whose
+# compiler resets them at the start of each compile (one process-wide table made every
+# later compile on n qubits start at the largest capacity any earlier run had needed); calls without
+# a simulator share the module table below.
+_UNBOUNDED_CAP = {}
+
+
+def learned_capacities(sim=None) -> dict:
+    """The n -> capacity table of unbounded replays driven by ``sim`` (created on first use)."""
+    if sim is None:
+        return _UNBOUNDED_CAP
+    table = getattr(sim, "aqc_learned_cap", None)
+    if table is None:
+        table = {}
+        try:
+            sim.aqc_learned_cap = table
+        except AttributeError:  # (a simulator object that takes no attributes: the shared table)
+            return _UNBOUNDED_CAP
+    return table
 
 
 def _full_cap(n):
     return min(MAX_CHI_CAP, 2 ** (n // 2))
 
 
-def chi_cap_for(n, max_chi, loaded_max=1):
+def chi_cap_for(n, max_chi, loaded_max=1, learned=None):
     if max_chi:
         cap = int(max_chi)
     else:
+        table = _UNBOUNDED_CAP if learned is None else learned
         full = _full_cap(n)
-        want = max(_UNBOUNDED_CAP.get(n, 0), int(loaded_max), min(64, full))
+        want = max(table.get(n, 0), int(loaded_max), min(64, full))
         cap = 1
         while cap < want:
             cap <<= 1
@@ -75,12 +94,14 @@ def is_capacity_error(e) -> bool:
     return "capacity (chi_cap) exceeded" in str(e)
 
 
-def grow_capacity(n, max_chi, cap) -> bool:
-    """After a capacity overflow at ``cap``: raise the unbounded capacity for n qubits to 2 cap
-    (chi_cap_for returns it from now on); False when the run is bounded or already at the limit."""
+def grow_capacity(n, max_chi, cap, learned=None) -> bool:
+    """After a capacity overflow at ``cap``: raise the unbounded capacity for n qubits to 2 cap in
+    ``learned`` (default: the module table; chi_cap_for returns it from now on); False when the run
+    is bounded or already at the limit."""
     if max_chi or cap >= _full_cap(n):
         return False
-    _UNBOUNDED_CAP[n] = max(_UNBOUNDED_CAP.get(n, 0), min(2 * cap, _full_cap(n)))
+    table = _UNBOUNDED_CAP if learned is None else learned
+    table[n] = max(table.get(n, 0), min(2 * cap, _full_cap(n)))
     return True
 
 
@@ -120,8 +141,9 @@ def device_mps_from_circuit(circuit: QuantumCircuit, sim=None, trunc_thr=None, o
         start = 1
     lmax = max(np.asarray(a).shape[1] for a, _ in loaded[0]) if loaded is not None else 1
     ops = device_ops_array(circuit, start)
+    learned = learned_capacities(sim)
     while True:
-        cap = chi_cap_for(n, max_chi, lmax)
+        cap = chi_cap_for(n, max_chi, lmax, learned)
         if out is None or out.n != n or out.chi_cap < cap:
             out = DeviceMPS(n, cap, thr, max_chi)
         else:
@@ -134,7 +156,7 @@ def device_mps_from_circuit(circuit: QuantumCircuit, sim=None, trunc_thr=None, o
             apply_checked(out, ops)
             break
         except Exception as e:  # an unbounded run outgrew its capacity: again at twice the capacity
-            if not (is_capacity_error(e) and grow_capacity(n, max_chi, out.chi_cap)):
+            if not (is_capacity_error(e) and grow_capacity(n, max_chi, out.chi_cap, learned)):
                 raise
     out.sort()
     return out

@@ -47,6 +47,16 @@ int aqc_svd_gram_stats(double* out);
    T product, out[1] its columns of the new environment, out[2] the hand-off -- and out[3] the
    steps counted.  Resets. */
 int aqc_env_ticks(double* out);
+/* Environment launches (z_all / pair RDMs) whose split chains timed out on a hand-off -- their
+   workgroups were not all resident together -- and were re-run with one workgroup per chain
+   (k_rdm_env), since the last call (then reset). */
+int aqc_env_fallbacks(long long* out);
+/* on = 1: every environment chain on one workgroup (k_rdm_env, any capacity); 0: the default, the
+   split chains at capacities 64, 128, 256 and 512. */
+int aqc_env_set_single(int on);
+/* Hand-off wait limit of the split environment chains in microseconds (< 0: the default, 2 s); 0
+   makes every wait not already satisfied a timeout, which re-runs the call on single chains (tests). */
+int aqc_env_set_spin_limit(double us);
 /* Block Jacobi pair visits (2 chi > 128), shader-clock ticks summed over workgroups since the
  * last call: out[0] Gram, out[1] inner Jacobi sweep, out[2] A V, out[3] visits.  Resets. */
 int aqc_bj_ticks(double* out);

@@ -198,3 +198,68 @@ def test_isl_compile_on_mps():
     assert res.overlap > 1 - 1e-2
     got = osv.simulate(5, [(i.operation.name, i.qubits, tuple(i.operation.params)) for i in res.circuit.data])
     assert abs(np.vdot(osv.simulate(5, ops), got)) ** 2 > 1 - 1e-2
+
+
+@pytest.mark.parametrize("cap", [100, 192, 384, 512])
+def test_env_chains_every_capacity_vs_oracle(cap):
+    """z_all_batch and pair RDMs at capacities outside the split chains' four (192, 320,
+    384 and 448 once ran k_env_split<128>, whose slices overran the scratch) and at 512: two states
+    of bond 96 loaded into capacity `cap`, against the oracle's contractions."""
+    import bench
+    from adaptaqc_amd.device import DeviceMPS, z_all_batch
+
+    n = 14
+    qs = [bench.random_vidal_mps(n, 96, 40 + s) for s in range(2)]
+    ds = []
+    for q in qs:
+        d = DeviceMPS(n, cap, 1e-16, None)
+        d.load_aer(q)
+        ds.append(d)
+    z = z_all_batch(ds)
+    pairs = [(0, 1), (2, 9), (6, 7), (0, 13), (12, 13)]
+    for s, q in enumerate(qs):
+        ref = M.MPS.from_aer(q)
+        np.testing.assert_allclose(z[s], [M.mps_expectation_z(ref, i) for i in range(n)], atol=1e-11)
+        pre = ref.preprocessed()
+        for (a, b), r in zip(pairs, ds[s].pair_rdms(pairs)):
+            np.testing.assert_allclose(r, OE.mps_rdm(pre, a, b), atol=1e-11)
+
+
+@pytest.mark.parametrize("cap", [64, 128])
+def test_env_chain_timeout_reruns_single_workgroup(cap):
+    """A split chain whose hand-off times out (spin limit 0: every wait not already satisfied) is
+    re-run with one workgroup per chain instead of failing the call, counted by
+    aqc_env_fallbacks; the values equal the default run's."""
+    import ctypes
+
+    import bench
+    from adaptaqc_amd import _lib
+    from adaptaqc_amd.device import DeviceMPS, z_all_batch
+
+    n = 12
+    ds = []
+    for s in range(3):
+        d = DeviceMPS(n, cap, 1e-16, None)
+        d.load_aer(bench.random_vidal_mps(n, 48, 70 + s))
+        ds.append(d)
+    lib = _lib.load()
+    cnt = ctypes.c_longlong(0)
+    _lib.check(lib.aqc_env_fallbacks(ctypes.byref(cnt)))
+    want = z_all_batch(ds)
+    want_rdm = ds[0].pair_rdms([(0, 5), (3, 4)])
+    _lib.check(lib.aqc_env_set_spin_limit(0.0))
+    try:
+        got = z_all_batch(ds)
+        got_rdm = ds[0].pair_rdms([(0, 5), (3, 4)])
+    finally:
+        _lib.check(lib.aqc_env_set_spin_limit(-1.0))
+    _lib.check(lib.aqc_env_fallbacks(ctypes.byref(cnt)))
+    assert cnt.value >= 1
+    np.testing.assert_allclose(got, want, atol=1e-12)
+    np.testing.assert_allclose(got_rdm, want_rdm, atol=1e-12)
+    _lib.check(lib.aqc_env_set_single(1))
+    try:
+        single = z_all_batch(ds)
+    finally:
+        _lib.check(lib.aqc_env_set_single(0))
+    np.testing.assert_allclose(single, want, atol=1e-12)

@@ -194,6 +194,21 @@ def test_unbounded_capacity_grows_on_demand():
         mo._UNBOUNDED_CAP.update(saved)
 
 
+def test_learned_capacity_is_scoped_to_the_simulator():
+    """the capacity an unbounded replay needed belongs to the backend's simulator (not
+    the process) and a compile starts afresh: another backend on as many qubits starts at 64."""
+    from adaptaqc_amd import mps_operations as mo
+    from adaptaqc_amd.backends.aer_mps_backend import AerMPSBackend
+
+    a, b = AerMPSBackend(), AerMPSBackend()
+    la, lb = mo.learned_capacities(a.simulator), mo.learned_capacities(b.simulator)
+    assert la is not lb and la is not mo._UNBOUNDED_CAP
+    assert mo.grow_capacity(20, None, 64, la) and mo.grow_capacity(20, None, 128, la)
+    assert mo.chi_cap_for(20, None, 1, la) == 256 and mo.chi_cap_for(20, None, 1, lb) == 64
+    a.reset_learned_capacity()
+    assert mo.chi_cap_for(20, None, 1, mo.learned_capacities(a.simulator)) == 64
+
+
 def test_backends_pickle_without_device_state():
     import pickle
 
