@@ -31,7 +31,7 @@ EXPORTS = (
     "aqc_mps_apply_batch", "aqc_mps_apply_sort_batch", "aqc_mps_apply_sort_batch_async", "aqc_mps_check_batch", "aqc_mps_sort", "aqc_mps_sort_batch", "aqc_mps_overlap_zero",
     "aqc_mps_overlap_zero_batch", "aqc_mps_dot", "aqc_mps_z_all", "aqc_mps_amps_hw1", "aqc_mps_z_all_batch",
     "aqc_mps_amps_hw1_batch",
-    "aqc_pair_grads", "aqc_pair_grads_batch", "aqc_argmax_scaled", "aqc_mps_jacobi_stats",
+    "aqc_pair_grads", "aqc_pair_grads_batch", "aqc_argmax_scaled", "aqc_argmax_scaled_batch", "aqc_mps_jacobi_stats",
     "aqc_mps_set_jacobi_tol", "aqc_mps_set_jacobi_stop", "aqc_mps_set_fused_chain", "aqc_mps_chain_ticks", "aqc_svd_debug",
     "aqc_sv_pair_rdms", "aqc_mps_pair_rdms", "aqc_mps_pair_rdms_batch", "aqc_entanglement_measures",
     "aqc_sv_transition", "aqc_mps_product_fit", "aqc_mps_set_svd_path", "aqc_svd_gram_ticks", "aqc_bj_ticks",
@@ -100,6 +100,7 @@ _SIGS = {
     "aqc_pair_grads": ([_P, _P, _P, _I, _P, _P, _P, _I, _P, _I], _I),
     "aqc_pair_grads_batch": ([_P, _I, _P, _P, _I, _P, _P, _P, _I, _P, _I], _I),
     "aqc_argmax_scaled": ([_P, _P, _I, _I, _IP], _I),
+    "aqc_argmax_scaled_batch": ([_P, _I, _P, _I, _I, _P], _I),
     "aqc_mps_jacobi_stats": ([_P, _IP], _I),
     "aqc_mps_set_jacobi_tol": ([_D], _I),
     "aqc_mps_set_jacobi_stop": ([_D], _I),

@@ -42,6 +42,7 @@ from ..approximate_compiler import ApproximateCompiler
 from .adapt_config import AdaptConfig
 from .adapt_result import AdaptResult
 from .pair_selection import reuse_priorities
+from ...sharding import as_comm
 from ...utils.entanglement_measures import EM_TOMOGRAPHY_CONCURRENCE
 
 logger = logging.getLogger(__name__)
@@ -54,7 +55,7 @@ class AdaptCompiler(ApproximateCompiler):
                  use_rotoselect=True, use_advanced_transpilation=False, rotosolve_fraction=1.0,
                  perform_final_minimisation=False, optimise_local_cost=False, soften_global_cost=False,
                  debug_log_full_ansatz=False, initial_single_qubit_layer=False, itensor_chi=None,
-                 itensor_cutoff=None):
+                 itensor_cutoff=None, comm=None):
         super().__init__(target=target, initial_state=None, backend=backend, execute_kwargs=execute_kwargs,
                          general_initial_state=general_initial_state, starting_circuit=starting_circuit,
                          optimise_local_cost=optimise_local_cost, rotosolve_fraction=rotosolve_fraction)
@@ -95,6 +96,11 @@ class AdaptCompiler(ApproximateCompiler):
                 self.layer_2q_gate, use_rotoselect, inverse=True)
             self.inverse_zero_ansatz = self.layer_2q_gate.inverse()
         self.soften_global_cost = soften_global_cost
+        # (not in the reference) the ranks of one node share each layer's pair sweep -- general
+        # gradient and ISL -- through this communicator (sharding.as_comm: a TorchComm / torch
+        # process group over RCCL, or comm.RcclComm); every rank runs the same compile and picks the
+        # same pair.  None: one process.
+        self.comm = as_comm(comm)
         if self.soften_global_cost and self.optimise_local_cost:
             raise ValueError("soften_global_cost must be False when optimising local cost")
 
@@ -233,8 +239,15 @@ class AdaptCompiler(ApproximateCompiler):
         """adapt_compiler.py:484-506 (the backend drops its device state when pickled)."""
         self.resume_from_layer = layer_count + 1
         self.prev_checkpoint_time_taken = self.time_taken + (timeit.default_timer() - start_time)
-        with open(os.path.join(checkpoint_dir, f"{layer_count}.pkl"), "wb") as f:
-            pickle.dump(self, f)
+        comm = getattr(self, "comm", None)
+        if comm is not None and comm.rank != 0:
+            return  # (ranks sharing the sweeps run the same compile: rank 0 writes the checkpoint)
+        self.comm = None  # (a communicator does not pickle; a resumed compile passes its own)
+        try:
+            with open(os.path.join(checkpoint_dir, f"{layer_count}.pkl"), "wb") as f:
+                pickle.dump(self, f)
+        finally:
+            self.comm = comm
         if delete_prev_chkpt:
             try:
                 os.remove(os.path.join(checkpoint_dir, f"{layer_count - checkpoint_every}.pkl"))
@@ -401,14 +414,16 @@ class AdaptCompiler(ApproximateCompiler):
             rng = (0, len(self.full_circuit))
         circuit = co.extract_inner_circuit(self.full_circuit, rng)
         return gr.general_grad_of_pairs(circuit, self.inverse_zero_ansatz, self.generators, self.degeneracies,
-                                        self.coupling_map, self.starting_circuit, self.backend)
+                                        self.coupling_map, self.starting_circuit, self.backend,
+                                        comm=getattr(self, "comm", None))
 
     def _get_all_qubit_pair_entanglement_measures(self):
         """adapt_compiler.py:955-976: one device state, every pair's RDM and measure in batches."""
         from ...utils.entanglement_measures import pair_entanglement_measures
 
         self.circ_mps = None  # the reference keeps the host MPS here; the sweep stays on the device
-        return pair_entanglement_measures(self.entanglement_measure_method, self, self.coupling_map)
+        return pair_entanglement_measures(self.entanglement_measure_method, self, self.coupling_map,
+                                          comm=getattr(self, "comm", None))
 
     def _find_best_entanglement_qubit_pair(self, entanglement_measures):
         """adapt_compiler.py:858-919: entanglement x reuse priority, bad-pair memory, threshold

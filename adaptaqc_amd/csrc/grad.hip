@@ -545,7 +545,9 @@ __global__ void k_sweep_grad(const SweepJob* __restrict__ jobs, SweepConst c) {
   j.out[p] = sqrt(g);  // out is per job (make_job)
 }
 
-__global__ void k_argmax(const double* s, const double* prio, int count, int* best) {
+// np.argmax(s * prio) over one row in one 256-thread workgroup: the first maximum (lowest index on
+// ties), NaN winning as in numpy.  Thread 0 gets (index, value).
+__device__ void argmax_row(const double* s, const double* prio, int count, int& best, double& val) {
   __shared__ double bv[256];
   __shared__ int bi[256];
   double v = -1.0 / 0.0;
@@ -577,7 +579,28 @@ __global__ void k_argmax(const double* s, const double* prio, int count, int* be
     }
     __syncthreads();
   }
-  if (threadIdx.x == 0) *best = bi[0];
+  best = bi[0];
+  val = bv[0];
+}
+
+__global__ __launch_bounds__(256) void k_argmax(const double* s, const double* prio, int count, int* best) {
+  int b;
+  double v;
+  argmax_row(s, prio, count, b, v);
+  if (threadIdx.x == 0) *best = b;
+}
+
+// one row (state) per workgroup: out[r] = its arg-max index (as a double), out[nrows + r] = the
+// scaled score there -- the [2][nrows] block the state-sharded sweep all-gathers (sharding.gather_best)
+__global__ __launch_bounds__(256) void k_argmax_rows(const double* __restrict__ s, int ld, const double* __restrict__ prio,
+                                                     int count, int nrows, double* __restrict__ out) {
+  int b;
+  double v;
+  argmax_row(s + (size_t)blockIdx.x * ld, prio, count, b, v);
+  if (threadIdx.x == 0) {
+    out[blockIdx.x] = (double)b;
+    out[nrows + blockIdx.x] = v;
+  }
 }
 
 // ---- chi = 1 variational compression (tenpy_product_state, approximate_compiler.py:222-242) ----
@@ -1210,6 +1233,13 @@ int aqc_argmax_scaled(const double* scores, const double* prio, int count, int s
   AQC_HIP_CHECK(hipMemcpyAsync(hb, db, sizeof(int), hipMemcpyDeviceToHost, st));
   AQC_HIP_CHECK(hipStreamSynchronize(st));
   *best = *hb;
+  return AQC_OK;
+}
+
+int aqc_argmax_scaled_batch(const double* scores, int ld, const double* prio, int count, int nrows, double* out) {
+  AQC_REQUIRE(scores && prio && out && count > 0 && nrows > 0 && ld >= count, "aqc_argmax_scaled_batch: bad arguments");
+  hipLaunchKernelGGL(k_argmax_rows, dim3(nrows), dim3(256), 0, aqc::mps_stream(), scores, ld, prio, count, nrows, out);
+  AQC_CHECK_LAUNCH();
   return AQC_OK;
 }
 

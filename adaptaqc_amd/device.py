@@ -338,3 +338,25 @@ def pair_grads_batch(states, svec, pairs, u0, gens, degs, out=None):
 
         _lib.check(l.aqc_stream_join(ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)))
     return host
+
+
+def argmax_rows(scores, prio):
+    """Per-row np.argmax(scores * prio) (first maximum) of a device score matrix on libaqchip's
+    kernel (aqc_argmax_scaled_batch), ordered both ways against torch's current stream like a
+    device-output sweep.  scores: [S, ld] float64 CUDA tensor (the first len(prio) columns are
+    scored), prio: [count] float64 CUDA tensor.  Returns ([S] int64 index, [S] float64 score)."""
+    import torch
+
+    l = _lib.lib()
+    S, ld = scores.shape
+    count = prio.shape[0]
+    if not (scores.is_cuda and prio.is_cuda and scores.dtype == torch.float64 and prio.dtype == torch.float64
+            and scores.is_contiguous() and prio.is_contiguous() and count <= ld):
+        raise ValueError("argmax_rows: contiguous float64 CUDA tensors with len(prio) <= scores.shape[1]")
+    out = torch.empty((2, S), dtype=torch.float64, device=scores.device)
+    cur = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    _lib.check(l.aqc_stream_wait(cur))
+    _lib.check(l.aqc_argmax_scaled_batch(ctypes.c_void_p(scores.data_ptr()), ld, ctypes.c_void_p(prio.data_ptr()),
+                                         count, S, ctypes.c_void_p(out.data_ptr())))
+    _lib.check(l.aqc_stream_join(cur))
+    return out[0].to(torch.int64), out[1]

@@ -131,10 +131,18 @@ class StateShard:
 
 def best_pairs(scores, priorities):
     """Per-state arg-max of scores * priorities (first maximum, as np.argmax) and its score, on the
-    scores' device: ([S] int64, [S] float64)."""
+    scores' device: ([S] int64, [S] float64).  On a GPU: libaqchip's arg-max kernel
+    (device.argmax_rows); host tensors (gloo tests) take torch's."""
     import torch
 
-    s = scores * torch.as_tensor(np.asarray(priorities, dtype=np.float64), device=scores.device)
+    p = priorities if isinstance(priorities, torch.Tensor) else torch.as_tensor(
+        np.asarray(priorities, dtype=np.float64))
+    p = p.to(device=scores.device, dtype=torch.float64)
+    if scores.is_cuda:
+        from .device import argmax_rows
+
+        return argmax_rows(scores.contiguous(), p.contiguous())
+    s = scores[:, : p.shape[0]] * p
     best = torch.argmax(s, dim=1)
     return best, s.gather(1, best[:, None])[:, 0]
 
@@ -152,3 +160,67 @@ def gather_best(best, score, shard: StateShard, group=None):
     dist.all_gather_into_tensor(out, local.contiguous(), group=group)
     out = out.view(shard.world, 2, shard.per_rank).permute(1, 0, 2).reshape(2, -1)
     return out[0].to(torch.int64), out[1]
+
+
+# ---- the product's communicator: one per-layer pair sweep over the ranks of one node -----------
+class TorchComm:
+    """A torch.distributed process group as the sweep's communicator: ``allgather`` of host float64
+    scores in rank order.  Backend "nccl" (RCCL over xGMI on MI355X) gathers through a device
+    buffer on this rank's GPU; gloo (CPU, the tests) on host tensors."""
+
+    def __init__(self, group=None):
+        import torch.distributed as dist
+
+        if not dist.is_initialized():
+            raise RuntimeError("TorchComm needs torch.distributed.init_process_group first")
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        self._nccl = dist.get_backend(group) == "nccl"
+
+    def allgather(self, local) -> np.ndarray:
+        import torch
+        import torch.distributed as dist
+
+        x = torch.as_tensor(np.ascontiguousarray(np.asarray(local, dtype=np.float64).reshape(-1)))
+        if self._nccl:
+            x = x.to(f"cuda:{torch.cuda.current_device()}")
+        out = torch.empty((self.world * x.numel(),), dtype=torch.float64, device=x.device)
+        dist.all_gather_into_tensor(out, x, group=self.group)
+        return out.cpu().numpy().reshape(self.world, -1)
+
+    def __reduce__(self):  # (a compiler pickled at a checkpoint drops the communicator)
+        return (_no_comm, ())
+
+
+def _no_comm():
+    return None
+
+
+def as_comm(comm):
+    """None (one process), an object with ``rank``, ``world`` and ``allgather`` (``TorchComm``,
+    ``comm.RcclComm``), a torch.distributed ProcessGroup, or True for the default group."""
+    if comm is None or comm is False:
+        return None
+    if comm is True:
+        return TorchComm()
+    if hasattr(comm, "allgather") and hasattr(comm, "world") and hasattr(comm, "rank"):
+        return comm
+    return TorchComm(comm)
+
+
+def sharded_pair_scores(score_pairs, pairs, n, comm):
+    """Scores of every pair of ``pairs`` (coupling-map order) with this rank computing only its
+    share: ``score_pairs(local_pairs) -> list`` runs on the rank's GPU for the pairs whose first
+    qubit min(c, t) the rank owns (PairShard: first qubits balanced by chain length), and one
+    all-gather of the float64 scores gives every rank the whole vector -- so every rank's np.argmax
+    (adapt_compiler.py:832-837, first maximum on ties) picks the same pair.  One process: the
+    plain sweep."""
+    comm = as_comm(comm)
+    pairs = list(pairs)
+    if comm is None or comm.world == 1:
+        return [float(x) for x in score_pairs(pairs)]
+    shard = PairShard(pairs, n, comm.rank, comm.world)
+    local = np.asarray(score_pairs(shard.local_pairs) if shard.local_pairs else [], dtype=np.float64)
+    full = gather_scores_host(local[None, :], shard, comm.allgather)[0]
+    return [float(x) for x in full]

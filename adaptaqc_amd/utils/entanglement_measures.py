@@ -92,13 +92,22 @@ def calculate_entanglement_measure(method, circuit, qubit_1, qubit_2, backend, b
     return float(entanglement_measures(rho, name)[0])
 
 
-def pair_entanglement_measures(method, compiler, pairs):
-    """Batched ISL sweep: the measure for every pair of ``pairs`` on the compiler's current state."""
+def pair_entanglement_measures(method, compiler, pairs, comm=None):
+    """Batched ISL sweep: the measure for every pair of ``pairs`` on the compiler's current state.
+    With ``comm`` (sharding.sharded_pair_scores) each rank computes the RDMs and measures of the
+    pairs whose first qubit it owns -- its share of the pair-RDM chains -- and one all-gather gives
+    every rank the whole list."""
+    from ..sharding import sharded_pair_scores
+
     name = _measure_name(method)
     if not pairs:
         return []
-    rdms = compiler.backend.pair_rdms(compiler, pairs)
-    return [float(x) for x in entanglement_measures(rdms, name)]
+
+    def score(local):
+        rdms = compiler.backend.pair_rdms(compiler, local)
+        return [float(x) for x in entanglement_measures(rdms, name)]
+
+    return sharded_pair_scores(score, pairs, compiler.full_circuit.num_qubits, comm)
 
 
 # -- measures of a single 4x4 density matrix (device kernels) -----------------------------------

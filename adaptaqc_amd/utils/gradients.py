@@ -88,18 +88,30 @@ def general_grad_of_pairs(
     coupling_map: List[Tuple],
     starting_circuit=None,
     backend=None,
+    comm=None,
 ):
     """Euclidean norm over the layer's generators of dC/dtheta at theta=0, for every pair.
 
     g_ct = sqrt(sum_k deg_k * (-Im(<s|G_k|psi> <psi|U0^dag|s>))^2)  (gradients.py:23-124).
     ``generators`` are the circuits of G_k^dag and ``inverse_zero_ansatz`` that of U0^dag, as
     in the reference (adapt_compiler.py:213-216).
+
+    ``comm`` (not in the reference; None = one process): the ranks of one node share the sweep --
+    every rank replays |psi> on its own GPU (deterministic, the same on every rank), scores the
+    pairs whose first qubit it owns, and one all-gather of the float64 scores returns the whole
+    list on every rank (sharding.sharded_pair_scores; ``TorchComm`` over RCCL / gloo, or
+    ``comm.RcclComm`` through the C ABI).
     """
+    from ..sharding import sharded_pair_scores
+
     if backend is None:
         from ..backends.python_default_backends import MPS_SIM as backend
     psi = device_mps_from_circuit(circuit.copy(), sim=backend.simulator)
-    return grads_for_state(psi, circuit.num_qubits, inverse_zero_ansatz, generators, degeneracies,
-                           coupling_map, starting_circuit, backend)
+    n = circuit.num_qubits
+    return sharded_pair_scores(
+        lambda pairs: grads_for_state(psi, n, inverse_zero_ansatz, generators, degeneracies, pairs,
+                                      starting_circuit, backend),
+        coupling_map, n, comm)
 
 
 def layer_operators(inverse_zero_ansatz, generators):

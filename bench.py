@@ -387,7 +387,7 @@ def main():
         if by_state:
             # every pair of this rank's states, the per-state arg-max on the rank, then one all-gather
             # of (best pair, score) per state (RCCL over xGMI; the projection repeats rank 0's block)
-            b, sc = best_pairs(local_scores, prio)
+            b, sc = best_pairs(local_scores, prio_t)
             if sim:
                 return local_scores, b.repeat(sim)
             return local_scores, gather_best(b, sc, sshard)[0]
@@ -675,10 +675,11 @@ def strong_main(args):
 
     def make_step(sts, pairs=cmap, gather=True):
         out = torch.zeros((len(sts), max(len(pairs), 1)), dtype=torch.float64, device="cuda")
+        ones_t = torch.ones(max(len(pairs), 1), dtype=torch.float64, device="cuda")
 
         def step():
             pair_grads_batch(sts, svec, pairs, u0, gm, deg, out=out.data_ptr())
-            best, score = best_pairs(out[:, : len(pairs)], np.ones(len(pairs)))
+            best, score = best_pairs(out, ones_t)
             return gather_best(best, score, shard) if gather else (best, score)
         return step
 

@@ -194,6 +194,12 @@ int aqc_mps_product_fit(aqc_mps_t psi, double* svec, int guess_from_gamma, int m
  * scores are read on the library's stream: order it after their producer (aqc_stream_wait). */
 int aqc_argmax_scaled(const double* scores, const double* prio, int count, int scores_is_device,
                       int* best);
+/* The same rule for each of nrows score rows at once (row r at scores + r * ld), all pointers on the
+ * device, queued on the library's stream without a host wait (order it with aqc_stream_wait /
+ * aqc_stream_join): out[r] = row r's arg-max index (as a double), out[nrows + r] = its scaled score
+ * -- the per-state selection of a batch of sweeps, laid out for one all-gather. */
+int aqc_argmax_scaled_batch(const double* scores, int ld, const double* prio, int count, int nrows,
+                            double* out);
 
 /* Diagnostics, lab switches and test hooks (path selection, phase ticks, path counters, a CU-holding
    test load, the SVD kernel on its own) are declared in aqc_hip_diag.h: they are not part of the

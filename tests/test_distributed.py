@@ -159,3 +159,117 @@ def test_gather_scores_host_matches_global_order():
             full = gather_scores_host(locals_[r], shards[r], allgather)
             np.testing.assert_array_equal(full, truth)
             assert int(np.argmax(full[0])) == 7
+
+
+def _product_sweep_setup(n):
+    """A circuit (ry layer + CX ladder + rz) and the identity-resolvable layer's generators, in the
+    product's types and the oracle's."""
+    from adaptaqc_amd.circuit import QuantumCircuit
+    from adaptaqc_amd.utils import ansatzes
+    from adaptaqc_amd.utils.gradients import get_generators_and_degeneracies
+    from oracle import gradients as ogr
+
+    rng = np.random.default_rng(9)
+    qc = QuantumCircuit(n)
+    for q in range(n):
+        qc.ry(float(rng.uniform(0.1, 0.4)), q)
+    for q in range(n - 1):
+        qc.cx(q, q + 1)
+        qc.rz(float(rng.uniform(-np.pi, np.pi)), q + 1)
+    layer = ansatzes.identity_resolvable()
+    gens, degs = get_generators_and_degeneracies(layer, rotoselect=True, inverse=True)
+    o_layer = [(i.operation.name, i.qubits, tuple(i.operation.params)) for i in layer.data]
+    og, od = ogr.get_generators_and_degeneracies(o_layer, True, True)
+    return qc, layer, gens, degs, o_layer, og, od
+
+
+def _oracle_scorer(calls):
+    """Stand-ins for the device replay and the device sweep (no GPU here): the oracle's MPS of the
+    circuit and its environment-form gradients of exactly the pairs asked for."""
+    from oracle import gradients as ogr
+    from oracle import mps as M
+
+    def replay(circuit, sim=None, **_):
+        ops = [(i.operation.name, i.qubits, tuple(i.operation.params)) for i in circuit.data]
+        return M.run_circuit(circuit.num_qubits, ops, 1e-16, 8).preprocessed()
+
+    def grads(psi, n, inverse_zero_ansatz, generators, degeneracies, pairs, starting_circuit=None, backend=None):
+        calls.append(list(pairs))
+        o_inv = [(i.operation.name, i.qubits, tuple(i.operation.params)) for i in inverse_zero_ansatz.data]
+        o_gens = [[(i.operation.name, i.qubits, tuple(i.operation.params)) for i in g.data] for g in generators]
+        return ogr.general_grad_of_pairs_env(psi, n, o_inv, o_gens, list(degeneracies), list(pairs))
+
+    return replay, grads
+
+
+def _product_comm_worker(rank, world, port, n, out):
+    """The product's general_grad_of_pairs and AdaptCompiler's pair choice with a TorchComm (gloo):
+    each rank scores its share (oracle injected for the device), one all-gather, same selection."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from types import SimpleNamespace
+
+    from adaptaqc_amd.compilers.adapt.adapt_compiler import AdaptCompiler
+    from adaptaqc_amd.compilers.adapt.adapt_config import AdaptConfig
+    from adaptaqc_amd.sharding import TorchComm
+    from adaptaqc_amd.utils import gradients as gr
+
+    qc, layer, gens, degs, _, _, _ = _product_sweep_setup(n)
+    cmap = H.coupling_map_full(n)
+    calls = []
+    gr.device_mps_from_circuit, gr.grads_for_state = _oracle_scorer(calls)
+    comm = TorchComm()
+    got = gr.general_grad_of_pairs(qc, layer.inverse(), gens, degs, cmap, None, SimpleNamespace(simulator=None),
+                                   comm=comm)
+    # the compiler's own sweep and selection (adapt_compiler.py:832-856) on the same communicator
+    ac = object.__new__(AdaptCompiler)
+    ac.__dict__.update(starting_circuit=None, full_circuit=qc, inverse_zero_ansatz=layer.inverse(), generators=gens,
+                       degeneracies=degs, coupling_map=cmap, backend=SimpleNamespace(simulator=None), comm=comm,
+                       qubit_pair_history=[(0, 1), (2, 3)], adapt_config=AdaptConfig(), initial_single_qubit_layer=False)
+    g2 = ac._get_all_qubit_pair_gradients()
+    pick = ac._find_best_gradient_qubit_pair(g2)
+    out[rank] = (np.asarray(got).tobytes(), np.asarray(g2).tobytes(), tuple(pick), calls)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_product_sweep_shares_pairs_across_ranks(world):
+    """the product's general_grad_of_pairs / AdaptCompiler with a communicator.  Every
+    rank scores only the pairs of its first qubits, and every rank ends with the single-process
+    gradient list (bit for bit: the same oracle scores, gathered) and the same selected pair."""
+    from types import SimpleNamespace
+
+    from adaptaqc_amd.compilers.adapt.adapt_compiler import AdaptCompiler
+    from adaptaqc_amd.compilers.adapt.adapt_config import AdaptConfig
+    from adaptaqc_amd.utils import gradients as gr
+
+    n = 9
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_product_comm_worker, args=(world, _free_port(), n, out), nprocs=world, join=True)
+    qc, layer, gens, degs, _, _, _ = _product_sweep_setup(n)
+    cmap = H.coupling_map_full(n)
+    calls = []
+    saved = gr.device_mps_from_circuit, gr.grads_for_state
+    try:
+        gr.device_mps_from_circuit, gr.grads_for_state = _oracle_scorer(calls)
+        want = gr.general_grad_of_pairs(qc, layer.inverse(), gens, degs, cmap, None, SimpleNamespace(simulator=None))
+        ac = object.__new__(AdaptCompiler)
+        ac.__dict__.update(starting_circuit=None, full_circuit=qc, inverse_zero_ansatz=layer.inverse(), generators=gens,
+                           degeneracies=degs, coupling_map=cmap, backend=SimpleNamespace(simulator=None), comm=None,
+                           qubit_pair_history=[(0, 1), (2, 3)], adapt_config=AdaptConfig(),
+                           initial_single_qubit_layer=False)
+        want_pick = ac._find_best_gradient_qubit_pair(ac._get_all_qubit_pair_gradients())
+    finally:
+        gr.device_mps_from_circuit, gr.grads_for_state = saved
+    assert calls[0] == cmap and max(want) > 1e-3
+    scored = []
+    for r in range(world):
+        got, g2, pick, rcalls = out[r]
+        np.testing.assert_array_equal(np.frombuffer(got), want)
+        np.testing.assert_array_equal(np.frombuffer(g2), want)
+        assert pick == tuple(want_pick)
+        assert len(rcalls) == 2 and rcalls[0] == rcalls[1] and len(rcalls[0]) < len(cmap)
+        scored += rcalls[0]
+    assert sorted(scored) == sorted(cmap)  # every pair scored by exactly one rank

@@ -169,6 +169,25 @@ def test_argmax_c_abi_tie_break():
         assert best.value == int(np.argmax(s * p))
 
 
+def test_argmax_rows_batch_matches_numpy():
+    """aqc_argmax_scaled_batch (the state-sharded bench's per-state selection, sharding.best_pairs):
+    every row's first maximum, including ties and a padded row stride, against np.argmax."""
+    import torch
+
+    from adaptaqc_amd.sharding import best_pairs
+
+    rng = np.random.default_rng(3)
+    S, ld, count = 37, 1230, 1225
+    s = rng.integers(0, 5, (S, ld)).astype(float)
+    p = rng.choice([0.25, 0.5, 1.0], count)
+    s[5, :] = 2.0  # a whole row tied: index 0 unless p decides
+    best, score = best_pairs(torch.as_tensor(s, device="cuda"), p)
+    torch.cuda.synchronize()
+    want = np.argmax(s[:, :count] * p, axis=1)
+    assert best.cpu().numpy().tolist() == want.tolist()
+    np.testing.assert_array_equal(score.cpu().numpy(), (s[:, :count] * p)[np.arange(S), want])
+
+
 def _near_zero_state(n, chi, seed, alpha=0.6):
     """bench.near_product_mps: every bond at min(2^k, 2^(n-k), chi), gradients far from zero."""
     from bench import near_product_mps
