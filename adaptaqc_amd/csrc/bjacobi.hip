@@ -61,21 +61,25 @@ __device__ __forceinline__ int rr(int pos, int r, int c) { return pos == 0 ? 0 :
 // st.fro.  One workgroup per job.  The column order of W is free (k_rank sorts the singular
 // values, k_split recovers the other side from theta), and a one-sided Jacobi started on
 // norm-sorted columns converges in fewer sweeps (de Rijk).  grid (nj), 1024 threads.
+// (up to kInitCols = 2048 columns: bond capacity 1024; two sort entries per thread)
+constexpr int kInitCols = 2048;
 __global__ __launch_bounds__(1024) void k_bj_init(const TwoSiteJob* __restrict__ jobs, BJState* __restrict__ st) {
   const TwoSiteJob& j = jobs[blockIdx.x];
   int L, C;
   bool tr;
   job_shape(j, L, C, tr);
   const int M = 2 * j.dims[0];
-  __shared__ double key[1024];
-  __shared__ int idx[1024];
+  __shared__ double key[kInitCols];
+  __shared__ int idx[kInitCols];
   __shared__ double red[16];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   auto elem = [&](int row, int col) -> cplx {
     return tr ? cconj(j.theta[(size_t)row * M + col]) : j.theta[(size_t)col * M + row];
   };
+  int P = 1024;  // sort length: 1024, or the columns rounded up to a power of two above it
+  while (P < C) P <<= 1;
   double f = 0.0;
-  for (int c = w; c < 1024; c += 16) {  // column norms, one wave per column
+  for (int c = w; c < P; c += 16) {  // column norms, one wave per column
     double x = 0.0;
     if (c < C)
       for (int r = lane; r < L; r += 64) {
@@ -88,11 +92,10 @@ __global__ __launch_bounds__(1024) void k_bj_init(const TwoSiteJob* __restrict__
   }
   if (lane == 0) red[w] = f;
   __syncthreads();
-  // bitonic sort of 1024 (key, idx), descending key (padding keys -1 sink to the end)
-  for (int k = 2; k <= 1024; k <<= 1) {
+  // bitonic sort of P (key, idx), descending key (padding keys -1 sink to the end)
+  for (int k = 2; k <= P; k <<= 1) {
     for (int jj = k >> 1; jj > 0; jj >>= 1) {
-      const int i = threadIdx.x;
-      {
+      for (int i = threadIdx.x; i < P; i += 1024) {
         const int l = i ^ jj;
         if (l > i) {
           const bool desc = (i & k) == 0;
@@ -286,8 +289,8 @@ __global__ __launch_bounds__(512) void k_bj_intra(const TwoSiteJob* __restrict__
 // FULL = false (2 chi <= 512): the blocks' own Gram blocks are taken as diagonal (each sweep's
 // intra launch has just orthogonalised them; norms only) and the visit rotates the 16 x 16 cross
 // pairs in 16 rounds.  FULL = true (2 chi up to 1024, where the intra launch's block would not fit
-// the LDS): the visit forms all of G and rotates every pair of the 32 columns (31 round-robin
-// rounds), so no intra launch is needed.  grid (nb / 2, nj), 256 threads.
+// the LDS; 2 chi = 2048 too, bond capacity 1024): the visit forms all of G and rotates every pair of
+// the 32 columns (31 round-robin rounds), so no intra launch is needed.  grid (nb / 2, nj), 256 threads.
 typedef double __attribute__((ext_vector_type(4))) d4_t;
 constexpr int kPairCols = 2 * kB;  // 32
 struct PairLds {
@@ -694,12 +697,15 @@ int block_jacobi(const TwoSiteJob* jobs, int nj, int cap_max, hipStream_t st) {
                                       (int)kPairLdsBytes));
     AQC_HIP_CHECK(hipFuncSetAttribute((const void*)k_bj_pair<16, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                       (int)kPairLdsBytes));
+    AQC_HIP_CHECK(hipFuncSetAttribute((const void*)k_bj_pair<32, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)kPairLdsBytes));
     attr = true;
   }
-  AQC_REQUIRE(2 * cap_max <= 1024, "block Jacobi supports 2 * chi_cap <= 1024");
+  AQC_REQUIRE(2 * cap_max <= 2048, "block Jacobi supports 2 * chi_cap <= 2048");
   if (2 * cap_max <= 256) return run_block_jacobi<4>(jobs, nj, cap_max, st);
   if (2 * cap_max <= 512) return run_block_jacobi<8>(jobs, nj, cap_max, st);
-  return run_block_jacobi<16>(jobs, nj, cap_max, st);
+  if (2 * cap_max <= 1024) return run_block_jacobi<16>(jobs, nj, cap_max, st);
+  return run_block_jacobi<32>(jobs, nj, cap_max, st);
 }
 
 }  // namespace aqc

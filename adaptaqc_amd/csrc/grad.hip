@@ -667,11 +667,15 @@ __device__ void top_pair_2x2(const cplx F[4], cplx u[2], cplx v[2], double& sigm
   }
 }
 
+// largest bond capacity of the chi = 1 fit (its running vectors sit in the LDS; the starting-circuit
+// fit runs on the target's capacity, at most 512 in the paper setting)
+constexpr int kFitMaxCap = 512;
+
 __global__ __launch_bounds__(kT) void k_product_fit(const FitJob* __restrict__ jobs) {
   const FitJob& j = jobs[blockIdx.x];
   const int n = j.n, cap = j.cap, tid = threadIdx.x;
-  __shared__ cplx vec[aqc::kMaxCap];       // running l (left-to-right) or r (right-to-left)
-  __shared__ cplx uw[2][2][aqc::kMaxCap];  // u[s][m], w[s][m]
+  __shared__ cplx vec[kFitMaxCap];       // running l (left-to-right) or r (right-to-left)
+  __shared__ cplx uw[2][2][kFitMaxCap];  // u[s][m], w[s][m]
   __shared__ cplx part[4][kT / 64];
   __shared__ cplx sv[2][2];       // the updated pair
   __shared__ double fid_s;
@@ -1128,7 +1132,7 @@ int aqc_pair_grads(aqc_mps_t psi, const double* svec, const int* pairs, int npai
 int aqc_mps_product_fit(aqc_mps_t psi, double* svec, int guess_from_gamma, int min_sweeps, int max_sweeps,
                         double tol, double* fidelity, int* sweeps) {
   AQC_REQUIRE(psi && svec && max_sweeps >= 1 && min_sweeps >= 0 && tol >= 0.0, "aqc_mps_product_fit: bad arguments");
-  AQC_REQUIRE(psi->d.cap <= aqc::kMaxCap, "aqc_mps_product_fit: bond capacity above the library's maximum");
+  AQC_REQUIRE(psi->d.cap <= kFitMaxCap, "aqc_mps_product_fit: bond capacity above 512");
   int rc = aqc_mps_sort(psi);  // the fit runs in qubit order
   if (rc != AQC_OK) return rc;
   rc = ensure_gw(psi);

@@ -86,8 +86,15 @@ __device__ __forceinline__ cplx ld_sc1(const cplx* p) {
              __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 }
 
+// rows of X (L = max(2 chi_l, 2 chi_r)) per Gram side C: at CT = 1024 a job may have L = 2048 (bond
+// capacity 1024); the certificate's Y = X V (L x K) then needs twice the C x C G scratch
+template <int CT>
+constexpr int kGLong = CT >= 1024 ? 2 : 1;
+
 struct GBArgs {
-  cplx* G;         // per job CT x CT: G, then the reflectors (row k = v_k at columns > k)
+  cplx* G;         // per job CT x CT: G, then the reflectors (row k = v_k at columns > k); the
+                   // certificate's Y (kGLong CT x CT) after them
+  size_t gstride;  // elements of G per job: kGLong<CT> CT^2
   cplx* tfac;      // per job (CT / 16) x 16 x 16: compact WY factors T of the reflector blocks
   cplx* yc;        // per job CT x CT: the reflectors column-major (v_k[row] at row * CT + k)
   double* d;       // per job CT
@@ -146,20 +153,21 @@ __global__ __launch_bounds__(256) void k_gb_gram(const TwoSiteJob* __restrict__ 
   int M, L, C, K;
   bool tr;
   job_dims(j, M, L, C, tr, K);
+  // (C > CT: both sides above the class -- 2 chi_l, 2 chi_r > 1024 -- declines to the block Jacobi)
+  const bool decline = !j.gram || C < 4 || C > CT;
   if (bx == 0 && threadIdx.x == 0) {
     atomicAdd(&g_gbig_stats[0], 1ull);
-    const int st = (!j.gram || C < 4) ? 1 : 0;
-    *(gi32*)(a.status + jb) = st;
-    if (st) atomicAdd(&g_gbig_stats[2], 1ull);
+    *(gi32*)(a.status + jb) = decline ? 1 : 0;
+    if (decline) atomicAdd(&g_gbig_stats[2], 1ull);
   }
-  if (!j.gram || C < 4) return;
+  if (decline) return;
   // blocks on and above the diagonal (bi <= bj), the one below mirrored: G is Hermitian
   constexpr int nbt = CT / 64;
   int bi = 0, rem = bx;
   while (rem >= nbt - bi) rem -= nbt - bi, ++bi;
   const int bj = (bi + rem) * 64;
   bi *= 64;
-  cplx* G = a.G + (size_t)jb * CT * CT;
+  cplx* G = a.G + (size_t)jb * a.gstride;
   const cplx* th = j.theta;
   __shared__ GemmLds lds;
   const int m = bi < C ? min(64, C - bi) : 0, n = bj < C ? min(64, C - bj) : 0;
@@ -289,7 +297,7 @@ __global__ __launch_bounds__(1024) void k_gb_tridiag(const TwoSiteJob* __restric
   // (phase ticks on the last wave: its rows stay active to the end)
   const bool tick = jb == 0 && g == 0 && tid == 960;
   // (local indices: the stage's trailing block starts at row / column K0 of the job's G)
-  cplx* G = a.G + (size_t)jb * CF * CF + (size_t)K0 * CF + K0;
+  cplx* G = a.G + (size_t)jb * a.gstride + (size_t)K0 * CF + K0;
   double* dd = a.d + (size_t)jb * CF + K0;
   double* ee = a.e + (size_t)jb * CF + K0;
   cplx* tt = a.tau + (size_t)jb * CF + K0;
@@ -549,7 +557,7 @@ __global__ __launch_bounds__(1024) void k_gb_tail(const TwoSiteJob* __restrict__
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int tr = tid >> 3, tq = tid & 7;
   const bool tick = jb == 0 && tid == 0;
-  cplx* G = a.G + (size_t)jb * CT * CT;
+  cplx* G = a.G + (size_t)jb * a.gstride;
   double* dd = a.d + (size_t)jb * CT;
   double* ee = a.e + (size_t)jb * CT;
   cplx* tt = a.tau + (size_t)jb * CT;
@@ -1021,7 +1029,7 @@ __global__ __launch_bounds__(256) void k_gb_tfac(const TwoSiteJob* __restrict__ 
   const int jb = job0 + (int)blockIdx.y;
   if (*(const gi32*)(a.status + jb) != 0) return;
   const int k0 = blockIdx.x * 16, nb = min(16, CT - 1 - k0);
-  const cplx* Y = a.G + (size_t)jb * CT * CT;  // row k = v_k (entries > k)
+  const cplx* Y = a.G + (size_t)jb * a.gstride;  // row k = v_k (entries > k)
   cplx* Yc = a.yc + (size_t)jb * CT * CT;      // column-major copy, zeros at rows <= k
   const cplx* tau = a.tau + (size_t)jb * CT;
   __shared__ cplx S[16][17];
@@ -1198,8 +1206,9 @@ __global__ __launch_bounds__(64 * NW) void k_gb_back(const TwoSiteJob* __restric
 // at most ||X - X V V^H||_F^2 (V the K kept right vectors, W / sigma from k_gb_back), computed from X
 // itself -- so to eps ||X|| in sigma, where G's eigenvalues carry eps ||G||.  Below CHOP / 2 the
 // open-CHOP values were all chopped, as LAPACK's sigma^2 ~ (eps sigma_1)^2 are in Aer; otherwise the
-// job declines (status 4: the block Jacobi decides).  Y = X V into the (dead) G scratch, then
-// R = X - Y V^H tile by tile with the squares summed per job; grid (ceil(CT / 64), ceil(CT / 64), nj).
+// job declines (status 4: the block Jacobi decides).  Y = X V into the (dead) G scratch (kGLong CT x CT
+// per job: X has L <= kGLong CT rows), then R = X - Y V^H tile by tile with the squares summed per job;
+// grid (kGLong CT / 64, CT / 64, nj).
 template <int CT>
 __device__ __forceinline__ cplx xval(const TwoSiteJob& j, bool tr, int M, int R, int c) {
   return tr ? cconj(ldg(j.theta + (size_t)R * M + c)) : ldg(j.theta + (size_t)c * M + R);
@@ -1217,7 +1226,7 @@ __global__ __launch_bounds__(256) void k_gb_cert_y(const TwoSiteJob* __restrict_
   const int r0 = blockIdx.x * 64, c0 = blockIdx.y * 64;
   if (r0 >= L || c0 >= K) return;
   __shared__ GemmLds lds;
-  cplx* Y = a.G + (size_t)jb * CT * CT;  // Y[R][kk] at R * CT + kk
+  cplx* Y = a.G + (size_t)jb * a.gstride;  // Y[R][kk] at R * CT + kk
   const double* sg = j.sig;
   block_cgemm(
       min(64, L - r0), min(64, K - c0), C, [&](int i, int c) { return xval<CT>(j, tr, M, r0 + i, c); },
@@ -1238,7 +1247,7 @@ __global__ __launch_bounds__(256) void k_gb_cert_r(const TwoSiteJob* __restrict_
   if (r0 >= L || c0 >= C) return;
   __shared__ GemmLds lds;
   __shared__ double red[256];
-  const cplx* Y = a.G + (size_t)jb * CT * CT;
+  const cplx* Y = a.G + (size_t)jb * a.gstride;
   const double* sg = j.sig;
   double acc = 0.0;
   block_cgemm(
@@ -1312,7 +1321,7 @@ int gb_ensure(GBBuffers& b, int ct, int nj, hipStream_t st) {
   const int c = std::max(ct, b.ct), n = std::max(nj, b.nj);
   gb_free(b);
   const size_t cc = (size_t)c * c * n;
-  AQC_HIP_CHECK(hipMalloc(&b.G, cc * sizeof(cplx)));
+  AQC_HIP_CHECK(hipMalloc(&b.G, (c >= 1024 ? 2 : 1) * cc * sizeof(cplx)));  // (kGLong)
   AQC_HIP_CHECK(hipMalloc(&b.z, cc * sizeof(double)));
   AQC_HIP_CHECK(hipMalloc(&b.dinv, cc * sizeof(double)));
   AQC_HIP_CHECK(hipMalloc(&b.d, (size_t)c * n * sizeof(double)));
@@ -1382,6 +1391,7 @@ int run_gram_big(const TwoSiteJob* hjobs, const TwoSiteJob* jobs, int nj, int ca
   if (rc != AQC_OK) return rc;
   GBArgs a;
   a.G = b.G, a.d = b.d, a.e = b.e, a.tau = b.tau, a.z = b.z, a.dinv = b.dinv, a.sig2 = b.sig2;
+  a.gstride = (size_t)kGLong<CT> * CT * CT;
   a.lam = b.lam, a.tn = b.tn, a.tfac = b.tfac, a.yc = b.yc;
   a.err = b.err, a.kept = b.kept, a.tail = b.tail, a.cert = b.cert, a.certsum = b.certsum;
   a.xch = b.xch, a.cnt = b.cnt, a.status = b.status;
@@ -1446,9 +1456,9 @@ int run_gram_big(const TwoSiteJob* hjobs, const TwoSiteJob* jobs, int nj, int ca
     }
     hipLaunchKernelGGL((k_gb_back<CT>), dim3(xcd_grid(CT / 16, nr)), dim3(CT / 64 > 4 ? CT : 256), 0, ps, jobs, a, j0, nr);
     AQC_CHECK_LAUNCH();
-    hipLaunchKernelGGL((k_gb_cert_y<CT>), dim3(CT / 64, CT / 64, nr), dim3(256), 0, ps, jobs, a, j0);
+    hipLaunchKernelGGL((k_gb_cert_y<CT>), dim3(kGLong<CT> * CT / 64, CT / 64, nr), dim3(256), 0, ps, jobs, a, j0);
     AQC_CHECK_LAUNCH();
-    hipLaunchKernelGGL((k_gb_cert_r<CT>), dim3(CT / 64, CT / 64, nr), dim3(256), 0, ps, jobs, a, j0);
+    hipLaunchKernelGGL((k_gb_cert_r<CT>), dim3(kGLong<CT> * CT / 64, CT / 64, nr), dim3(256), 0, ps, jobs, a, j0);
     AQC_CHECK_LAUNCH();
     hipLaunchKernelGGL((k_gb_cert_end<CT>), dim3(nr), dim3(64), 0, ps, jobs, a, j0);
     AQC_CHECK_LAUNCH();
@@ -1519,11 +1529,11 @@ int big_svd(const TwoSiteJob* hjobs, const TwoSiteJob* jobs, int nj, int side, i
     const char* s = std::getenv("AQC_BIG_GRAM");
     g_gram_big = (s && std::strcmp(s, "0") == 0) ? 0 : 1;
   }
-  if (!g_gram_big || side > 1024) return block_jacobi(jobs, nj, cap_max, st);
+  if (!g_gram_big || side > 2048) return block_jacobi(jobs, nj, cap_max, st);
   // chunks of at most 1.5 GB of per-job scratch (G, the two inverse-iteration arrays and the
   // column-major reflectors: 64 C^2 bytes per job), so that a large batch does not hold it all
   const int ct = side <= 256 ? 256 : side <= 512 ? 512 : 1024;
-  const int chunk = std::max(1, (int)((size_t)1536 << 20) / (64 * ct * ct));
+  const int chunk = std::max(1, (int)(((size_t)1536 << 20) / ((size_t)80 * ct * ct)));
   for (int j0 = 0; j0 < nj; j0 += chunk) {
     const int n = std::min(chunk, nj - j0);
     int rc;

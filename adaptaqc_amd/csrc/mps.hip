@@ -2210,7 +2210,7 @@ extern "C" {
 int aqc_mps_create(int n, int chi_cap, double threshold, int max_chi, aqc_mps_t* out) {
   AQC_REQUIRE(out, "aqc_mps_create: null out");
   AQC_REQUIRE(n >= 1 && n <= 4096, "aqc_mps_create: bad n");
-  AQC_REQUIRE(chi_cap >= 1 && chi_cap <= kMaxCap, "aqc_mps_create: chi_cap must be in [1, 512]");
+  AQC_REQUIRE(chi_cap >= 1 && chi_cap <= kMaxCap, "aqc_mps_create: chi_cap must be in [1, 1024]");
   auto* h = new aqc_mps_s();
   static std::atomic<unsigned long long> next_uid{1};
   h->uid = next_uid++;

@@ -14,12 +14,12 @@ namespace aqc {
 //   lam : (n+1) bonds x cap doubles; bond b sits left of site b; lam[0] = lam[n] = {1}.
 //   dims: (n+1) ints on device, dims[0] = dims[n] = 1.
 // The qubit permutation created by Aer's swap routing lives on the host (order / loc).
-// Largest two-site column count 2 chi (bond capacity <= 512): the singular-value buffer holds the
+// Largest two-site column count 2 chi (bond capacity <= 1024): the singular-value buffer holds the
 // raw column norms at [0, kSigMax) and the sorted values at [kSigMax, 2 kSigMax).  sig[kSigTail]:
 // the part of the reduce_zeros tail sum that an SVD path which decides the kept count itself (the
 // Gram paths, svd_gram.h / gram_big.hip) has already removed -- it writes the kept singular values
 // and zeros, and the rank step's tail rule continues from this sum (then resets it to 0).
-constexpr int kSigMax = 1024;
+constexpr int kSigMax = 2048;
 constexpr int kMaxCap = kSigMax / 2;
 constexpr int kSigTail = 2 * kSigMax;
 constexpr int kSigLen = 2 * kSigMax + 2;  // doubles
@@ -233,9 +233,10 @@ constexpr double kReduceChop = 1e-16;  // reduce_zeros' CHOP on sigma^2 (mps.hip
 // third on) to stop when every decomposition has converged.
 int block_jacobi(const TwoSiteJob* jobs, int nj, int cap_max, hipStream_t st);
 
-// Two-site SVDs at 2 chi = side in (128, 1024] (gram_big.hip): the multi-workgroup Gram path
-// (G = X^H X, tridiagonalisation over several workgroups per job, inverse iteration, V = Q Z;
-// output contract qr = 1, written into the device job), the block Jacobi for the jobs it declines.
+// Two-site SVDs at 2 chi = side in (128, 2048] (gram_big.hip): the multi-workgroup Gram path
+// (G = X^H X of the C x C side, C = min(2 chi_l, 2 chi_r) <= 1024; tridiagonalisation over several
+// workgroups per job, inverse iteration, V = Q Z; output contract qr = 1, written into the device
+// job), the block Jacobi for the jobs it declines (and for C > 1024).
 // hjobs: host copies of the device jobs (qr = 0).  Synchronises the host once.
 int big_svd(const TwoSiteJob* hjobs, const TwoSiteJob* jobs, int nj, int side, int cap_max, hipStream_t st);
 

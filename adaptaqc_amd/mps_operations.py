@@ -11,7 +11,7 @@ import numpy as np
 from .circuit import QuantumCircuit, device_ops_array, mps_payload
 from .device import DeviceMPS
 
-MAX_CHI_CAP = 512
+MAX_CHI_CAP = 1024
 
 
 def check_mps(obj) -> bool:

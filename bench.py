@@ -258,6 +258,37 @@ def _cpu_worker_body(kind, wid, budget_s, layer_seed):
     return count, time.perf_counter() - t0, per_d
 
 
+def host_description(workers):
+    """The host the CPU baseline ran on: logical CPUs (os.cpu_count()), the CPUs this process may run
+    on (sched_getaffinity), sockets and physical cores and the model name (/proc/cpuinfo), and why
+    the baseline uses `workers` processes rather than every core."""
+    model, phys, cores_per = None, set(), None
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                k, _, v = line.partition(":")
+                k, v = k.strip(), v.strip()
+                if k == "model name" and model is None:
+                    model = v
+                elif k == "physical id":
+                    phys.add(v)
+                elif k == "cpu cores" and cores_per is None:
+                    cores_per = int(v)
+    except (OSError, ValueError):
+        pass
+    logical = os.cpu_count() or 1
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else logical
+    sockets = max(len(phys), 1)
+    physical = sockets * cores_per if cores_per else logical
+    return {"cpu_model": model, "host_logical_cpus": logical, "host_physical_cores": physical, "sockets": sockets,
+            "affinity_cpus": aff, "workers": workers,
+            "why_not_every_core": (f"the GPU box gives one GPU's process a share of {workers} CPUs of the node's "
+                                   f"{logical} (os.cpu_count() reports the whole node; the pool asks jobs to size "
+                                   "worker pools to that share), so the port runs on {workers} single-threaded "
+                                   "processes; node_linear_bound scales it to every physical core, an upper bound "
+                                   "(perfect scaling, no shared-memory-bandwidth loss)").replace("{workers}", str(workers))}
+
+
 def cpu_baselines(budget_s, workers):
     """Gradient and overlap evaluations / s of the oracle port on `workers` processes (fork, before
     any GPU call), BLAS single-threaded in each.  Returns per-kind rates and the step-mix rate."""
@@ -325,6 +356,7 @@ def main():
         workers = args.cpu_workers or min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)))
         cpu = cpu_baselines(args.cpu_budget, workers)
         cpu["workers"] = workers
+        cpu["host"] = host_description(workers)
 
     import torch
     import torch.distributed as dist
@@ -568,7 +600,15 @@ def main():
                 # against the reference's per-pair structure
                 "gradient_env_evals_per_s": cpu["gradient_env"]["evals_per_s"],
                 "gradient_env_note": "oracle/gradients.py general_grad_of_pairs_env: whole 1225-pair sweeps",
+                "host": cpu["host"],
             }
+            # every physical core of the node at the measured per-process rate (an upper bound)
+            pc = cpu["host"]["host_physical_cores"] / cpu["workers"]
+            cpu_line["node_linear_bound"] = {
+                "cores": cpu["host"]["host_physical_cores"], "value": step_mix * pc,
+                "reference_mix_evals_per_s": cpu_line["reference_mix_evals_per_s"] * pc,
+                "gradient_env_evals_per_s": cpu_line["gradient_env_evals_per_s"] * pc,
+                "gpu_vs": value / (step_mix * pc)}
         line = {
             "metric": "overlap+gradient evals/sec, 50-qubit MPS chi=64, 1/2/4/8 MI355X",
             "value": value,
@@ -598,7 +638,12 @@ def main():
                 "vs_cpu": ({"gradient": grad_rate / cpu_line["gradient_evals_per_s"],
                             "gradient_like_for_like_env": grad_rate / cpu_line["gradient_env_evals_per_s"],
                             "overlap": ov_rate / cpu_line["overlap_evals_per_s"],
-                            "reference_mix": ref_mix / cpu_line["reference_mix_evals_per_s"]} if cpu_line else None),
+                            "reference_mix": ref_mix / cpu_line["reference_mix_evals_per_s"],
+                            "reference_mix_vs_node_linear_bound":
+                                ref_mix / cpu_line["node_linear_bound"]["reference_mix_evals_per_s"],
+                            "gradient_env_vs_node_linear_bound":
+                                grad_rate / cpu_line["node_linear_bound"]["gradient_env_evals_per_s"]}
+                           if cpu_line else None),
             },
             "roofline": roof,
             "cpu_baseline": cpu_line,

@@ -81,7 +81,7 @@ int aqc_sv_get(aqc_sv_t h, double* out);
 int aqc_sv_set(aqc_sv_t h, const double* in);
 
 /* ---- MPS: replaces aer_mps_backend.py:27-93 and aqc_research.mps_operations ----- */
-/* |0...0> on n qubits, bond capacity chi_cap; truncation as mps_sim_with_args
+/* |0...0> on n qubits, bond capacity chi_cap (1 ... 1024); truncation as mps_sim_with_args
  * (aer_mps_backend.py:27-42): threshold on the discarded tail sum of s^2, max_chi <= 0
  * means unlimited (bounded by chi_cap). */
 int aqc_mps_create(int n, int chi_cap, double threshold, int max_chi, aqc_mps_t* out);

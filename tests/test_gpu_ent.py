@@ -218,9 +218,8 @@ def test_env_chains_every_capacity_vs_oracle(cap):
     z = z_all_batch(ds)
     pairs = [(0, 1), (2, 9), (6, 7), (0, 13), (12, 13)]
     for s, q in enumerate(qs):
-        ref = M.MPS.from_aer(q)
-        np.testing.assert_allclose(z[s], [M.mps_expectation_z(ref, i) for i in range(n)], atol=1e-11)
-        pre = ref.preprocessed()
+        pre = M.MPS.from_aer(q).preprocessed()
+        np.testing.assert_allclose(z[s], [M.mps_expectation_z(pre, i) for i in range(n)], atol=1e-11)
         for (a, b), r in zip(pairs, ds[s].pair_rdms(pairs)):
             np.testing.assert_allclose(r, OE.mps_rdm(pre, a, b), atol=1e-11)
 

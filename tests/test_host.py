@@ -167,14 +167,14 @@ def test_mps_format_helpers():
     pre = _preprocess_mps(z)
     assert all(x.shape == (2, 1, 1) for x in pre)
     assert chi_cap_for(50, 64) == 64 and chi_cap_for(6, None) == 8
-    assert chi_cap_for(50, 512) == 512
+    assert chi_cap_for(50, 512) == 512 and chi_cap_for(50, 1024) == 1024
     with pytest.raises(NotImplementedError):
-        chi_cap_for(50, 1024)
+        chi_cap_for(50, 2048)
 
 
 def test_unbounded_capacity_grows_on_demand():
     """max_chi None: the smallest power of two >= 64 holding the loaded MPS, doubled after each
-    overflow up to min(512, 2^(n/2)); bounded runs never grow."""
+    overflow up to min(1024, 2^(n/2)); bounded runs never grow."""
     from adaptaqc_amd import mps_operations as mo
 
     saved = dict(mo._UNBOUNDED_CAP)
@@ -184,7 +184,8 @@ def test_unbounded_capacity_grows_on_demand():
         assert mo.chi_cap_for(20, None, 100) == 128 and mo.chi_cap_for(6, None) == 8
         assert mo.grow_capacity(20, None, 64) and mo.chi_cap_for(20, None) == 128
         assert mo.grow_capacity(20, None, 128) and mo.grow_capacity(20, None, 256)
-        assert mo.chi_cap_for(20, None) == 512 and not mo.grow_capacity(20, None, 512)
+        assert mo.chi_cap_for(20, None) == 512 and mo.grow_capacity(20, None, 512)
+        assert mo.chi_cap_for(20, None) == 1024 and not mo.grow_capacity(20, None, 1024)
         assert mo.chi_cap_for(16, None) == 64 and not mo.grow_capacity(16, 64, 64)
         assert mo.grow_capacity(16, None, 128) and mo.chi_cap_for(16, None) == 256
         assert not mo.grow_capacity(16, None, 256)  # 2^(16/2)

@@ -105,12 +105,113 @@ def gpu_layers(args):
         return cost
 
     comp._add_layer = add_layer_snap
+    # the cached Rotoselect / Rotosolve evaluator's calls of every layer (the like-for-like CPU
+    # column replays them: the same prefix caching and candidate batching, on the oracle)
+    from adaptaqc_amd.utils import cached_rotations as cr
+
+    calls = snap.setdefault("calls", {})
+    orig_goto, orig_costs = cr.MPSPrefixBatch._goto, cr.MPSPrefixBatch._costs
+
+    def rec(kind, obj, index, mats=None):
+        layer = len(layers)
+        circ = obj.compiler.full_circuit
+        calls.setdefault(layer, []).append((kind, int(index), (circ.num_qubits, _oracle_ops(circ)),
+                                            None if mats is None else [np.array(m, dtype=complex) for m in mats]))
+
+    def goto(obj, index):
+        rec("goto", obj, index)
+        return orig_goto(obj, index)
+
+    def costs(obj, index, mats):
+        rec("costs", obj, index, mats)
+        return orig_costs(obj, index, mats)
+
+    cr.MPSPrefixBatch._goto, cr.MPSPrefixBatch._costs = goto, costs
     t1 = time.perf_counter()
     res = comp.compile()
+    cr.MPSPrefixBatch._goto, cr.MPSPrefixBatch._costs = orig_goto, orig_costs
     total = time.perf_counter() - t1
     comp._profile_snapshot = snap
     return comp, layers, {"setup_s": setup_s, "compile_s": total, "overlap": float(res.overlap),
                           "layers": len(layers), "cost_evaluations": int(res.cost_evaluations)}
+
+
+def _oracle_ops(circ):
+    from adaptaqc_amd.circuit import qubit_indices
+
+    ops = []
+    for ins in circ.data:
+        name = ins.operation.name
+        if name == "set_matrix_product_state":
+            ops.append(("set_mps", (), (ins.operation.params[0],)))
+        else:
+            ops.append((name, tuple(qubit_indices(circ, ins)), tuple(float(p) for p in ins.operation.params)))
+    return ops
+
+
+def _apply(st, ops, thr, max_chi):
+    """oracle/mps.py run_circuit's gate loop on `st` in place (no sort)."""
+    from oracle import gates as OG
+
+    for name, qubits, params in ops:
+        if name in ("barrier", "measure", "id", "set_mps"):
+            continue
+        m = OG.matrix(name, params)
+        if len(qubits) == 1:
+            st.apply_1q(qubits[0], m)
+        else:
+            st.apply_2q(qubits[0], qubits[1], m, thr, max_chi)
+
+
+def cpu_cached_replay(log, threshold, max_chi, budget_s):
+    """Like for like: the device's cached evaluator (cached_rotations.MPSPrefixBatch) replayed on the
+    oracle on one core -- the prefix MPS kept across candidates and gates (rebuilt from the cached
+    target only when the varied gate moves left or the payload changes), each candidate's gate plus
+    the suffix from a copy of it, the sort, <0|psi>.  The calls run in order until budget_s; the rest
+    is scaled by candidate count (stated)."""
+    from threadpoolctl import threadpool_limits
+
+    from oracle import mps as M
+
+    phi, pos, key = None, None, None
+    t_goto = t_cand = 0.0
+    n_cand_done = 0
+    n_cand_all = sum(len(c[3]) for c in log if c[0] == "costs")  # (kind, index, (n, ops), mats)
+    n_goto_all = sum(1 for c in log if c[0] == "goto")
+    n_goto_done = 0
+    t_start = time.perf_counter()
+    with threadpool_limits(limits=1):
+        for kind, index, (nq, ops), mats in log:
+            if time.perf_counter() - t_start > budget_s and n_cand_done:
+                break
+            t0 = time.perf_counter()
+            if kind == "goto":
+                start = 1 if ops and ops[0][0] == "set_mps" else 0
+                k = id(ops[0][2][0]) if start else None
+                if phi is None or pos is None or index < pos or k != key:
+                    phi = M.MPS.from_aer(ops[0][2][0]) if start else M.MPS(nq)
+                    _apply(phi, ops[start:index], threshold, max_chi)
+                else:
+                    _apply(phi, ops[pos:index], threshold, max_chi)
+                pos, key = index, k
+                t_goto += time.perf_counter() - t0
+                n_goto_done += 1
+            else:
+                q = ops[index][1][0]
+                n = phi.n
+                for m in mats:
+                    st = phi.copy()
+                    st.apply_1q(q, m)
+                    _apply(st, ops[index + 1:], threshold, max_chi)
+                    st.sort_qubits(threshold, max_chi)
+                    _ = 1 - abs(M.mps_dot(st.preprocessed(), M.zero_mps(n))) ** 2
+                t_cand += time.perf_counter() - t0
+                n_cand_done += len(mats)
+    per_cand = t_cand / max(n_cand_done, 1)
+    per_goto = t_goto / max(n_goto_done, 1)
+    est = t_goto + t_cand + per_cand * (n_cand_all - n_cand_done) + per_goto * (n_goto_all - n_goto_done)
+    return {"cores": 1, "candidates": n_cand_all, "candidates_timed": n_cand_done, "prefix_moves": n_goto_all,
+            "prefix_moves_timed": n_goto_done, "s_per_candidate": per_cand, "s_estimate": est}
 
 
 def cpu_port_layer(comp, typical_evals, threshold, max_chi, pairs_sample):
@@ -163,6 +264,7 @@ def main():
     ap.add_argument("--max-chi", type=int, default=0)
     ap.add_argument("--seed", type=int, default=21)
     ap.add_argument("--cpu-pairs", type=int, default=6)
+    ap.add_argument("--cpu-budget", type=float, default=60.0, help="s per like-for-like replay before scaling")
     args = ap.parse_args()
     comp, layers, summary = gpu_layers(args)
     typical = [r for r in layers if r["layer"] > 0 and "rotosolve" not in r["stages_ms"]]
@@ -179,6 +281,37 @@ def main():
         evals = int(np.median([r["cost_evaluations"] for r in typical]))
         out["cpu_port"] = cpu_port_layer(comp, evals, args.threshold, args.max_chi or None, args.cpu_pairs)
         out["speedup_vs_cpu_1core"] = out["cpu_port"]["layer_s_estimate"] / (1e-3 * out["median_layer_ms"])
+        # like for like: the device's algorithms on one CPU core -- the environment-form sweep
+        # (oracle/gradients.py, the device's factorisation through T_ab) and the cached evaluator's
+        # calls of the median typical layer replayed on the oracle (same prefix caching / batching)
+        from threadpoolctl import threadpool_limits
+
+        from oracle import adapt_host, gradients as ogr, mps as M
+
+        psi = M.MPS.from_aer(bench.near_product_mps(bench.N_QUBITS, bench.CHI, 21)).preprocessed()
+        _, og, od, inv0 = bench.oracle_layer()
+        cmap = adapt_host.coupling_map_full(bench.N_QUBITS)
+        with threadpool_limits(limits=1):
+            t0 = time.perf_counter()
+            ogr.general_grad_of_pairs_env(psi, bench.N_QUBITS, inv0, og, od, cmap)
+            sweep_env_s = time.perf_counter() - t0
+        calls = comp._profile_snapshot.get("calls", {})
+        med = sorted(typical, key=lambda r: r["wall_ms"])[len(typical) // 2]
+        roto = cpu_cached_replay(calls.get(med["layer"], []), args.threshold, args.max_chi or None, args.cpu_budget)
+        layer_s = sweep_env_s + roto["s_estimate"]
+        out["cpu_like_for_like"] = {
+            "cores": 1, "layer": med["layer"], "gpu_layer_ms": med["wall_ms"], "sweep_env_s": sweep_env_s,
+            "rotoselect_cached": roto, "layer_s_estimate": layer_s,
+            "speedup_vs_cpu_1core_like_for_like": layer_s / (1e-3 * med["wall_ms"]),
+            "note": "the device's algorithms on the oracle, one core: environment-form sweep (timed) + the "
+                    "cached evaluator's recorded calls of this layer replayed with the same prefix caching "
+                    "and candidate batching (timed up to the budget, the rest scaled by candidate count)"}
+        if with_rs:
+            rs = with_rs[0]
+            rr = cpu_cached_replay(calls.get(rs["layer"], []), args.threshold, args.max_chi or None, args.cpu_budget)
+            out["cpu_like_for_like"]["rotosolve_layer"] = {
+                "layer": rs["layer"], "gpu_layer_ms": rs["wall_ms"], "cached": rr,
+                "speedup_vs_cpu_1core_like_for_like": (sweep_env_s + rr["s_estimate"]) / (1e-3 * rs["wall_ms"])}
     print(json.dumps(out), flush=True)
 
 
