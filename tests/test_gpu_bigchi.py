@@ -39,6 +39,16 @@ def _check(n, chi, ops, seed):
     return dims
 
 
+def _blas_threads():
+    """numpy's BLAS on up to 16 threads for the oracle's large SVDs and contractions (importing bench
+    may have pinned it to one for the CPU baseline's workers)."""
+    import os
+
+    from threadpoolctl import threadpool_limits
+
+    return threadpool_limits(limits=min(16, os.cpu_count() or 1))
+
+
 def _gates(n, rng, pairs):
     ops = []
     for a, b in pairs:
@@ -186,7 +196,8 @@ def test_unbounded_chi_above_512_threshold_1e8():
         for q in range(layer % 2, n - 1, 2):
             ops.append(("cx", (q, q + 1), ()))
             qc.cx(q, q + 1)
-    ref = M.run_circuit(n, ops, 1e-8, None)
+    with _blas_threads():  # (the oracle's numpy SVDs of up to 1600 x 1024 blocks: ~30 s on 8 threads)
+        ref = M.run_circuit(n, ops, 1e-8, None)
     pre_ref = ref.preprocessed()
     want_dims = [1] + [x.shape[2] for x in pre_ref]
     assert max(want_dims) > 512
@@ -198,7 +209,8 @@ def test_unbounded_chi_above_512_threshold_1e8():
     for b in (9, 10, 11):  # the bonds above 512 and beside them: Schmidt values
         np.testing.assert_allclose(lam[b], ref.l[b], atol=1e-9, err_msg=f"bond {b}")
     pre = d.preprocessed()
-    fid = abs(M.mps_dot(pre_ref, pre)) / np.sqrt(abs(M.mps_dot(pre, pre)) * abs(M.mps_dot(pre_ref, pre_ref)))
+    with _blas_threads():
+        fid = abs(M.mps_dot(pre_ref, pre)) / np.sqrt(abs(M.mps_dot(pre, pre)) * abs(M.mps_dot(pre_ref, pre_ref)))
     assert abs(fid - 1.0) < 1e-6, fid
     assert abs(d.overlap_zero() - M.mps_dot(pre_ref, M.zero_mps(n))) < 1e-9
     qs = [0, 9, 10, 11, 20]
@@ -213,19 +225,21 @@ def test_capacity_1024_gram_side_above_1024_block_jacobi():
     from adaptaqc_amd.circuit import device_ops
     from adaptaqc_amd.device import DeviceMPS
 
-    n, chi = 24, 600
+    n, chi = 22, 600
     rng = np.random.default_rng(8)
-    aer = random_vidal_mps(n, chi, 8)
-    ops = _gates(n, rng, [(11, 12)])
-    ref = M.run_circuit(n, ops, 1e-16, 1024, mps=M.MPS.from_aer(aer))
+    with _blas_threads():  # (~25 s on 8 threads: the chi = 600 canonical form and one 1200 x 1200 SVD)
+        aer = random_vidal_mps(n, chi, 8)
+        ops = _gates(n, rng, [(10, 11)])
+        ref = M.run_circuit(n, ops, 1e-16, 1024, mps=M.MPS.from_aer(aer))
     d = DeviceMPS(n, 1024, 1e-16, 1024)
     d.load_aer(aer)
     d.apply(device_ops(to_circuit(n, ops)))
     pre_ref = ref.preprocessed()
     np.testing.assert_array_equal(d.dims(), [1] + [x.shape[2] for x in pre_ref])
-    assert d.dims()[12] == 1024
+    assert d.dims()[11] == 1024
     gam, lam = d.to_aer()
-    np.testing.assert_allclose(lam[11], ref.l[11], atol=1e-9)
+    np.testing.assert_allclose(lam[10], ref.l[10], atol=1e-9)
     pre = d.preprocessed()
-    fid = abs(M.mps_dot(pre_ref, pre)) / np.sqrt(abs(M.mps_dot(pre, pre)) * abs(M.mps_dot(pre_ref, pre_ref)))
+    with _blas_threads():
+        fid = abs(M.mps_dot(pre_ref, pre)) / np.sqrt(abs(M.mps_dot(pre, pre)) * abs(M.mps_dot(pre_ref, pre_ref)))
     assert abs(fid - 1.0) < 1e-6, fid
