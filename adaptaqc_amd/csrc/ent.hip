@@ -209,9 +209,10 @@ __device__ __forceinline__ void narrow_cgemm(int m, int n, int k, FA a, FB b, FS
 // columns, the hand-off; then the steps counted
 __device__ unsigned long long g_env_ticks[4];
 
-// grid (2 states rounded up to 8, kEnvNW), kT threads; CW = cap / kEnvNW output columns per
-// workgroup.  Counters: cnt[32 (2 state + dir)] (zeroed by the host).
-template <int CW>
+// grid (2 states rounded up to 8, NW), kT threads; CW = cap / NW output columns per workgroup (NW =
+// kEnvNW = 4 up to capacity 512; 16 workgroups of 64 columns at capacity 1024).  Counters:
+// cnt[32 (2 state + dir)] (zeroed by the host).
+template <int CW, int NW = kEnvNW>
 __global__ __launch_bounds__(kT) void k_env_split(const RdmJob* __restrict__ jobs, unsigned* __restrict__ cnt,
                                                   int* __restrict__ err, unsigned long long spin, int nchains) {
   constexpr int NB1 = 2 * CW < 64 ? 2 * CW : 64, NB2 = CW < 64 ? CW : 64;
@@ -289,7 +290,7 @@ __global__ __launch_bounds__(kT) void k_env_split(const RdmJob* __restrict__ job
     __syncthreads();
     if (tid == 0) {
       __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const unsigned target = (unsigned)kEnvNW * (unsigned)(step + 1);
+      const unsigned target = (unsigned)NW * (unsigned)(step + 1);
       const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
       while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
         __builtin_amdgcn_s_sleep(1);
@@ -844,9 +845,12 @@ int env_split_cols(int cap) {
     case 128: return 32;
     case 256: return 64;
     case 512: return 128;
+    case 1024: return 64;  // (16 workgroups per chain: env_split_nw)
     default: return 0;
   }
 }
+// workgroups per chain of the split kernels
+int env_split_nw(int cap) { return cap == 1024 ? 16 : kEnvNW; }
 
 // environment launches that timed out on a hand-off and were re-run by k_rdm_env (aqc_env_fallbacks)
 unsigned long long g_env_fallbacks = 0;
@@ -869,13 +873,17 @@ int launch_envs(RdmJob* djobs, int ns, int cap, hipStream_t st, void* sync, bool
   int* err = (int*)(cnt + (size_t)ns * 2 * 32);
   AQC_HIP_CHECK(hipMemsetAsync(sync, 0, env_sync_bytes(ns), st));
   const unsigned long long kSpin = g_env_spin;
-  constexpr int kRound = 28;  // 28 x 8 workgroups: one per CU (~400 VGPRs a lane) leaves room
+  const int nw = env_split_nw(cap);
+  // 28 states x 2 chains x 4 workgroups (224, one per CU: ~400 VGPRs a lane) leave room; as many
+  // workgroups in a round at 16 per chain
+  const int kRound = std::max(1, 224 / (2 * nw));
   for (int s0 = 0; s0 < ns; s0 += kRound) {
     const int m = std::min(kRound, ns - s0);
-    const dim3 xg((2 * m + 7) / 8 * 8, kEnvNW);  // (chains padded to 8, workgroup: one XCD per chain)
+    const dim3 xg((2 * m + 7) / 8 * 8, nw);  // (chains padded to 8, workgroup: one XCD per chain)
     RdmJob* jb = djobs + s0;
     unsigned* cb = cnt + (size_t)s0 * 2 * 32;
-    switch (cw) {
+    switch (nw == kEnvNW ? cw : -cw) {
+      case -64: hipLaunchKernelGGL((k_env_split<64, 16>), xg, dim3(kT), 0, st, jb, cb, err, kSpin, 2 * m); break;
       case 16: hipLaunchKernelGGL(k_env64, xg, dim3(256), 0, st, jb, cb, err, kSpin, 2 * m); break;
       case 32: hipLaunchKernelGGL(k_env_split<32>, xg, dim3(kT), 0, st, jb, cb, err, kSpin, 2 * m); break;
       case 64: hipLaunchKernelGGL(k_env_split<64>, xg, dim3(kT), 0, st, jb, cb, err, kSpin, 2 * m); break;

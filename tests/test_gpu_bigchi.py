@@ -177,14 +177,21 @@ def _golden_cap1024():
 
 
 def _product_overlaps(d, phi):
-    """<phi_k|psi> on the device: each product state loaded at the state's capacity, mps_dot."""
+    """<phi_k|psi> on the device without a cap^3 environment chain: a copy of psi rotated qubit by
+    qubit by W_q (W_q phi_q = |0>: exact one-qubit gates, no truncation), then <0..0|W psi> =
+    <phi|psi> through the zero-chain overlap (overlap_zero returns <psi|0..0>)."""
+    from adaptaqc_amd.circuit import QuantumCircuit, device_ops
     from adaptaqc_amd.device import DeviceMPS
 
     out = []
+    c = DeviceMPS(d.n, d.chi_cap, 1e-16, None)
     for p in phi:
-        ps = DeviceMPS(d.n, d.chi_cap)
-        ps.load_aer(([(np.array([[v[0]]]), np.array([[v[1]]])) for v in p], [np.ones(1)] * (d.n - 1)))
-        out.append(ps.dot(d))
+        qc = QuantumCircuit(d.n)
+        for q, (a, b) in enumerate(p):
+            qc.unitary(np.array([[np.conj(a), np.conj(b)], [-b, a]]), [q])
+        c.copy_from(d)
+        c.apply(device_ops(qc))
+        out.append(np.conj(c.overlap_zero()))
     return np.array(out)
 
 
