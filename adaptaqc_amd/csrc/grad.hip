@@ -667,15 +667,17 @@ __device__ void top_pair_2x2(const cplx F[4], cplx u[2], cplx v[2], double& sigm
   }
 }
 
-// largest bond capacity of the chi = 1 fit (its running vectors sit in the LDS; the starting-circuit
-// fit runs on the target's capacity, at most 512 in the paper setting)
-constexpr int kFitMaxCap = 512;
+// largest bond capacity of the chi = 1 fit (its running vectors sit in the dynamic LDS: 5 cap complex)
+constexpr int kFitMaxCap = 1024;
 
 __global__ __launch_bounds__(kT) void k_product_fit(const FitJob* __restrict__ jobs) {
   const FitJob& j = jobs[blockIdx.x];
   const int n = j.n, cap = j.cap, tid = threadIdx.x;
-  __shared__ cplx vec[kFitMaxCap];       // running l (left-to-right) or r (right-to-left)
-  __shared__ cplx uw[2][2][kFitMaxCap];  // u[s][m], w[s][m]
+  // dynamic LDS (5 cap complex): the running l (left-to-right) or r (right-to-left), then u[s][m],
+  // w[s][m]
+  extern __shared__ cplx fit_lds[];
+  cplx* vec = fit_lds;
+  cplx* fit_uw = fit_lds + cap;
   __shared__ cplx part[4][kT / 64];
   __shared__ cplx sv[2][2];       // the updated pair
   __shared__ double fid_s;
@@ -742,8 +744,8 @@ __global__ __launch_bounds__(kT) void k_product_fit(const FitJob* __restrict__ j
       cplx a = aqc::cmk(0, 0), b = aqc::cmk(0, 0);
       for (int l = 0; l < cl; ++l) a = aqc::cfma(lv[l], fit_a(j, i, s, l, m), a);
       for (int r = 0; r < cr; ++r) b = aqc::cfma(fit_a(j, i + 1, s, m, r), rv[r], b);
-      uw[0][s][m] = a;
-      uw[1][s][m] = b;
+      fit_uw[((0) * 2 + (s)) * cap + (m)] = a;
+      fit_uw[((1) * 2 + (s)) * cap + (m)] = b;
     }
     __syncthreads();
     // F[a][b] = sum_m u[a][m] w[b][m]: wave q -> entry q
@@ -751,7 +753,7 @@ __global__ __launch_bounds__(kT) void k_product_fit(const FitJob* __restrict__ j
       const int q = tid >> 6, lane = tid & 63;
       const int a = q >> 1, b = q & 1;
       cplx acc = aqc::cmk(0, 0);
-      for (int m = lane; m < cm; m += 64) acc = aqc::cfma(uw[0][a][m], uw[1][b][m], acc);
+      for (int m = lane; m < cm; m += 64) acc = aqc::cfma(fit_uw[((0) * 2 + (a)) * cap + (m)], fit_uw[((1) * 2 + (b)) * cap + (m)], acc);
 #pragma unroll
       for (int off = 32; off > 0; off >>= 1) {
         acc.x += __shfl_xor(acc.x, off);
@@ -799,7 +801,7 @@ __global__ __launch_bounds__(kT) void k_product_fit(const FitJob* __restrict__ j
       update(i, vec, j.Rv + (size_t)(i + 2) * cap);
       const int cm = j.dims[i + 1];
       for (int m = tid; m < cm; m += kT)
-        vec[m] = aqc::cfma(aqc::cconj(sv[0][1]), uw[0][1][m], aqc::cmul(aqc::cconj(sv[0][0]), uw[0][0][m]));
+        vec[m] = aqc::cfma(aqc::cconj(sv[0][1]), fit_uw[((0) * 2 + (1)) * cap + (m)], aqc::cmul(aqc::cconj(sv[0][0]), fit_uw[((0) * 2 + (0)) * cap + (m)]));
       __syncthreads();
     }
     // right to left
@@ -810,7 +812,7 @@ __global__ __launch_bounds__(kT) void k_product_fit(const FitJob* __restrict__ j
       update(i, j.Lv + (size_t)i * cap, vec);
       const int cm = j.dims[i + 1];
       for (int m = tid; m < cm; m += kT)
-        vec[m] = aqc::cfma(aqc::cconj(sv[1][1]), uw[1][1][m], aqc::cmul(aqc::cconj(sv[1][0]), uw[1][0][m]));
+        vec[m] = aqc::cfma(aqc::cconj(sv[1][1]), fit_uw[((1) * 2 + (1)) * cap + (m)], aqc::cmul(aqc::cconj(sv[1][0]), fit_uw[((1) * 2 + (0)) * cap + (m)]));
       __syncthreads();
     }
     const double f = fid_s;
@@ -1132,7 +1134,7 @@ int aqc_pair_grads(aqc_mps_t psi, const double* svec, const int* pairs, int npai
 int aqc_mps_product_fit(aqc_mps_t psi, double* svec, int guess_from_gamma, int min_sweeps, int max_sweeps,
                         double tol, double* fidelity, int* sweeps) {
   AQC_REQUIRE(psi && svec && max_sweeps >= 1 && min_sweeps >= 0 && tol >= 0.0, "aqc_mps_product_fit: bad arguments");
-  AQC_REQUIRE(psi->d.cap <= kFitMaxCap, "aqc_mps_product_fit: bond capacity above 512");
+  AQC_REQUIRE(psi->d.cap <= kFitMaxCap, "aqc_mps_product_fit: bond capacity above 1024");
   int rc = aqc_mps_sort(psi);  // the fit runs in qubit order
   if (rc != AQC_OK) return rc;
   rc = ensure_gw(psi);
@@ -1172,7 +1174,14 @@ int aqc_mps_product_fit(aqc_mps_t psi, double* svec, int guess_from_gamma, int m
       err = AQC_ERR_HIP;
       break;
     }
-    hipLaunchKernelGGL(k_product_fit, dim3(1), dim3(kT), 0, st, (const FitJob*)dj);
+    const size_t lds = 5 * (size_t)psi->d.cap * sizeof(cplx);  // (80 KB at capacity 1024)
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute((const void*)k_product_fit, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)(5 * kFitMaxCap * sizeof(cplx)));
+      attr = true;
+    }
+    hipLaunchKernelGGL(k_product_fit, dim3(1), dim3(kT), lds, st, (const FitJob*)dj);
     if (hipGetLastError() != hipSuccess ||
         hipMemcpyAsync(svec, dsv, 2 * (size_t)n * sizeof(cplx), hipMemcpyDeviceToHost, st) != hipSuccess ||
         hipMemcpyAsync(hout.data(), dout, ob, hipMemcpyDeviceToHost, st) != hipSuccess ||
