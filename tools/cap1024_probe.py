@@ -47,7 +47,7 @@ def main():
             break
 
 
-if __name__ == "__main__" and (len(sys.argv) < 2 or sys.argv[1] != "steps"):
+if __name__ == "__main__" and (len(sys.argv) < 2 or sys.argv[1].isdigit()):
     main()
 
 
