@@ -1437,37 +1437,6 @@ __global__ __launch_bounds__(kT) void k_env(const EnvJob* __restrict__ jobs) {
   }
 }
 
-// <Z_i> = sum_s z_s sum conj(A[s][l][r]) L[l][l'] A[s][l'][r'] R[r][r'].  blockIdx.x = site.
-__global__ __launch_bounds__(kT) void k_zexp(const cplx* gam, const double* lam, const int* dims, int n, int cap,
-                                             const cplx* Lenv, const cplx* Renv, cplx* out) {
-  const int i = blockIdx.x;
-  const size_t cc = (size_t)cap * cap;
-  const cplx* Lm = Lenv + (size_t)i * cc;
-  const cplx* Rm = Renv + (size_t)(i + 1) * cc;
-  const int cl = dims[i], cr = dims[i + 1];
-  __shared__ double red[kT];
-  double acc = 0.0;
-  // sum over (s, l, r): conj(A[s][l][r]) * (sum_{l'} L[l][l'] * (sum_{r'} A[s][l'][r'] R[r][r']))
-  for (int e = threadIdx.x; e < 2 * cl * cr; e += kT) {
-    const int s = e / (cl * cr), rem = e % (cl * cr), l = rem / cr, r = rem % cr;
-    cplx t = aqc::cmk(0, 0);
-    for (int lp = 0; lp < cl; ++lp) {
-      cplx u = aqc::cmk(0, 0);
-      for (int rp = 0; rp < cr; ++rp) u = aqc::cfma(site_a(gam, lam, cap, i, s, lp, rp), Rm[(size_t)r * cap + rp], u);
-      t = aqc::cfma(Lm[(size_t)l * cap + lp], u, t);
-    }
-    const cplx v = aqc::cconjmul(site_a(gam, lam, cap, i, s, l, r), t);
-    acc += (s == 0 ? 1.0 : -1.0) * v.x;
-  }
-  red[threadIdx.x] = acc;
-  __syncthreads();
-  for (int s = kT / 2; s > 0; s >>= 1) {
-    if (threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) out[i] = aqc::cmk(red[0], 0.0);
-}
-
 // ---- host-side scheduling ---------------------------------------------------------------
 struct DevOp {
   int kind;  // 1: one-site, 2: two-site (p, p+1)
@@ -2881,46 +2850,11 @@ int aqc_mps_dot(aqc_mps_t a, aqc_mps_t b, double* re, double* im) {
 
 int aqc_mps_z_all(aqc_mps_t h, double* out) {
   AQC_REQUIRE(h && out, "aqc_mps_z_all: null argument");
-  int rc = aqc_mps_sort(h);
-  if (rc != AQC_OK) return rc;
-  rc = ensure_env(h);
-  if (rc != AQC_OK) return rc;
-  const int n = h->d.n;
-  const size_t cc = (size_t)h->d.cap * h->d.cap;
-  cplx* Lenv = h->d.env;
-  cplx* Renv = h->d.env + (size_t)(n + 1) * cc;
-  // right chain needs its own tmp: use the theta workspace (4 cap^2 >= 2 cap^2)
-  EnvJob jl;
-  std::memset(&jl, 0, sizeof(jl));
-  jl.ga = jl.gb = h->d.gam;
-  jl.la = jl.lb = h->d.lam;
-  jl.da = jl.db = h->d.dims;
-  jl.n = n;
-  jl.cap = h->d.cap;
-  jl.env = Lenv;
-  jl.tmp = h->d.tmp;
-  jl.keep_all = 1;
-  jl.right = 0;
-  jl.out = nullptr;
-  EnvJob jr = jl;
-  jr.env = Renv;
-  jr.tmp = h->d.theta;
-  jr.right = 1;
-  std::vector<EnvJob> jobs = {jl, jr};
-  const EnvJob* dj = nullptr;
-  rc = upload_jobs(jobs, &dj);
-  if (rc != AQC_OK) return rc;
-  hipStream_t st = aqc::mps_stream();
-  hipLaunchKernelGGL(k_env, dim3(2), dim3(kT), 0, st, dj);
-  AQC_CHECK_LAUNCH();
-  hipLaunchKernelGGL(k_zexp, dim3(n), dim3(kT), 0, st, h->d.gam, h->d.lam, h->d.dims, n, h->d.cap, Lenv, Renv,
-                     h->d.scal);
-  AQC_CHECK_LAUNCH();
-  std::vector<cplx> z(n);
-  AQC_HIP_CHECK(hipMemcpyAsync(z.data(), h->d.scal, n * sizeof(cplx), hipMemcpyDeviceToHost, st));
-  AQC_HIP_CHECK(hipStreamSynchronize(st));
-  for (int i = 0; i < n; ++i) out[i] = z[i].x;
-  return AQC_OK;
+  // the batched path (ent.hip: left / right environment chains over several workgroups on the
+  // matrix cores, P_b per site, one trace each): O(n chi^3).  The per-site kernel used until round
+  // 6 contracted L A R for each output entry, O(chi^4) per site -- 83 s for one 21-qubit state at
+  // bond 512 (profiles/r6_zall_cap1024_kernel_stats.csv).
+  return aqc_mps_z_all_batch(&h, 1, out);
 }
 
 }  // extern "C"
