@@ -42,8 +42,8 @@ would have made, so histories and logs stay comparable.
 import numpy as np
 
 from .. import gates as G
-from .._lib import ops_array
-from ..circuit import device_ops
+from .._lib import OP_DTYPE, ops_array
+from ..circuit import device_ops, device_ops_rows
 from ..device import DeviceSV, amps_hw1_batch, apply_batch, copy_batch, overlap_zero_batch, z_all_batch
 
 
@@ -171,18 +171,23 @@ class MPSPrefixBatch(_SweepBase):
             self.phi, self.pos = self.backend.new_state(), None
         if self.pos is None or index < self.pos:
             self.phi.copy_from(base)
-            self.phi.apply(_ops(circ, start, index))
+            self.phi.apply(device_ops_rows(circ, start, index))
         elif index > self.pos:
-            self.phi.apply(_ops(circ, self.pos, index))
+            self.phi.apply(device_ops_rows(circ, self.pos, index))
         self.pos = index
 
     def _costs(self, index, mats):
         circ = self.compiler.full_circuit
         q = _ops_qubit(circ, index)
-        suffix = ops_array(_ops(circ, index + 1, len(circ.data)))
+        # the suffix's rows from the circuit's memoised conversion (device_ops_rows), the candidates'
+        # gates in one conversion, each list joined as bytes (a structured-array concatenate costs
+        # ~16 us)
+        suffix = device_ops_rows(circ, index + 1, len(circ.data)).tobytes()
+        cand = ops_array([(m, (q,)) for m in mats]).tobytes()
+        size = len(cand) // len(mats)
         states = self.backend.scratch_states(len(mats))
         copy_batch(states, [self.phi] * len(mats))
-        lists = [np.concatenate([ops_array([(m, (q,))]), suffix]) for m in mats]
+        lists = [np.frombuffer(cand[i * size:(i + 1) * size] + suffix, dtype=OP_DTYPE) for i in range(len(mats))]
         apply_batch(states, lists, sort=True)
         if self.kind == "local":
             z = z_all_batch(states)

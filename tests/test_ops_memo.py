@@ -120,3 +120,36 @@ def test_memo_reconverts_custom_gates_and_other_types():
     op = qc.data[0].operation
     qc.data[0] = CircuitInstruction(_SubclassedRz(op.name, 1, list(op.params)), qc.data[0].qubits)
     assert device_ops_array(qc).tobytes() == _fresh(qc)
+
+
+def test_device_ops_rows_slices_the_memo():
+    """circuit.device_ops_rows (the cached MPS evaluator's suffix): the rows of any instruction range
+    equal a direct conversion of that range, also after an angle is rewritten in place, a gate
+    replaced and instructions inserted (every op, a ccx's several rows included)."""
+    from adaptaqc_amd import _lib
+    from adaptaqc_amd.circuit import QuantumCircuit, device_ops_rows
+    from adaptaqc_amd.utils.cached_rotations import _ops
+
+    rng = np.random.default_rng(0)
+    qc = QuantumCircuit(6)
+    for layer in range(5):
+        for q in range(6):
+            qc.rz(float(rng.uniform()), q)
+            qc.ry(float(rng.uniform()), q)
+        for q in range(layer % 2, 5, 2):
+            qc.cx(q, q + 1)
+    qc.ccx(0, 2, 4)
+
+    def same(lo, hi):
+        assert device_ops_rows(qc, lo, hi).tobytes() == _lib.ops_array(_ops(qc, lo, hi)).tobytes()
+
+    for lo, hi in [(0, len(qc.data)), (3, 17), (20, len(qc.data)), (len(qc.data) - 2, len(qc.data)), (9, 9)]:
+        same(lo, hi)
+    qc.data[5].operation.params = [0.77]
+    same(2, 30)
+    other = QuantumCircuit(6)
+    other.rx(0.4, 3)
+    qc.data[7] = other.data[0]
+    same(0, len(qc.data))
+    qc.cx(1, 2)
+    same(10, len(qc.data))

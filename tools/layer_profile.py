@@ -47,7 +47,7 @@ class Stages:
         setattr(obj, name, wrapped)
 
 
-def gpu_layers(args):
+def gpu_layers(args, record=False):
     from adaptaqc_amd.backends import AerMPSBackend, mps_sim_with_args
     from adaptaqc_amd.compilers import AdaptCompiler, AdaptConfig
     from adaptaqc_amd.utils.ansatzes import identity_resolvable
@@ -106,11 +106,14 @@ def gpu_layers(args):
 
     comp._add_layer = add_layer_snap
     # the cached Rotoselect / Rotosolve evaluator's calls of every layer (the like-for-like CPU
-    # column replays them: the same prefix caching and candidate batching, on the oracle)
+    # column replays them: the same prefix caching and candidate batching, on the oracle); recorded
+    # in a second, untimed compile (recording snapshots the circuit per call: ~0.2 ms each)
     from adaptaqc_amd.utils import cached_rotations as cr
 
     calls = snap.setdefault("calls", {})
     orig_goto, orig_costs = cr.MPSPrefixBatch._goto, cr.MPSPrefixBatch._costs
+    if not record:
+        orig_goto = orig_costs = None
 
     def rec(kind, obj, index, mats=None):
         layer = len(layers)
@@ -126,10 +129,12 @@ def gpu_layers(args):
         rec("costs", obj, index, mats)
         return orig_costs(obj, index, mats)
 
-    cr.MPSPrefixBatch._goto, cr.MPSPrefixBatch._costs = goto, costs
+    if record:
+        cr.MPSPrefixBatch._goto, cr.MPSPrefixBatch._costs = goto, costs
     t1 = time.perf_counter()
     res = comp.compile()
-    cr.MPSPrefixBatch._goto, cr.MPSPrefixBatch._costs = orig_goto, orig_costs
+    if record:
+        cr.MPSPrefixBatch._goto, cr.MPSPrefixBatch._costs = orig_goto, orig_costs
     total = time.perf_counter() - t1
     comp._profile_snapshot = snap
     return comp, layers, {"setup_s": setup_s, "compile_s": total, "overlap": float(res.overlap),
@@ -295,7 +300,9 @@ def main():
             t0 = time.perf_counter()
             ogr.general_grad_of_pairs_env(psi, bench.N_QUBITS, inv0, og, od, cmap)
             sweep_env_s = time.perf_counter() - t0
-        calls = comp._profile_snapshot.get("calls", {})
+        print(json.dumps({"note": "second compile, recording the cached evaluator's calls (untimed)"}), flush=True)
+        comp_rec, _, _ = gpu_layers(args, record=True)
+        calls = comp_rec._profile_snapshot.get("calls", {})
         med = sorted(typical, key=lambda r: r["wall_ms"])[len(typical) // 2]
         roto = cpu_cached_replay(calls.get(med["layer"], []), args.threshold, args.max_chi or None, args.cpu_budget)
         layer_s = sweep_env_s + roto["s_estimate"]
