@@ -1294,36 +1294,59 @@ __global__ __launch_bounds__(kT) void k_overlap_zero(const MeasJob* __restrict__
 }
 
 // Zero chains: vec[b] (left, bond b) = <0..0| A_0..A_{b-1};  vec[(n+1)+b] (right) = A_b..A_{n-1}|0..0>.
-// blockIdx.y = 0 -> left chain, 1 -> right chain.
+// blockIdx.y = 0 -> left chain, 1 -> right chain.  The running vector in the LDS; the left chain as
+// k_overlap_zero (lanes along r, the four waves splitting l), the right one with lanes along r too
+// (coalesced rows of A) and one wave sum per output row.  (Round 6: one thread per output entry
+// with the whole dot product and the vector in global memory, columns of A read with a cap stride,
+// made the softened-cost batch's HW-1 amplitudes ~2 ms a call.)
 __global__ __launch_bounds__(kT) void k_zero_chains(const MeasJob* __restrict__ jobs) {
   const MeasJob& j = jobs[blockIdx.x];
-  const int tid = fresh_tid();
+  const int tid = fresh_tid(), q = tid >> 6, lane = tid & 63;
   const int cap = j.cap, n = j.n;
   cplx* L = j.vec;
   cplx* R = j.vec + (size_t)(n + 1) * cap;
+  __shared__ cplx v[2][kMaxCap];
+  __shared__ cplx part[4][64];
+  if (tid == 0) v[0][0] = aqc::cmk(1.0, 0.0);
+  int cur = 0;
   if (blockIdx.y == 0) {
     if (tid == 0) L[0] = aqc::cmk(1.0, 0.0);
     __syncthreads();
     for (int i = 0; i < n; ++i) {
       const int cl = j.dims[i], cr = j.dims[i + 1];
-      for (int r = tid; r < cr; r += kT) {
+      for (int r0 = 0; r0 < cr; r0 += 64) {
+        const int r = r0 + lane;
         cplx acc = aqc::cmk(0, 0);
-        for (int l = 0; l < cl; ++l) acc = aqc::cfma(L[(size_t)i * cap + l], site_a(j.gam, j.lam, cap, i, 0, l, r), acc);
-        L[(size_t)(i + 1) * cap + r] = acc;
+        if (r < cr)
+          for (int l = q; l < cl; l += 4) acc = aqc::cfma(v[cur][l], site_a(j.gam, j.lam, cap, i, 0, l, r), acc);
+        part[q][lane] = acc;
+        __syncthreads();
+        if (q == 0 && r < cr) {
+          const cplx s = aqc::cadd(aqc::cadd(part[0][lane], part[1][lane]), aqc::cadd(part[2][lane], part[3][lane]));
+          v[cur ^ 1][r] = s;
+          L[(size_t)(i + 1) * cap + r] = s;
+        }
+        __syncthreads();
       }
-      __syncthreads();
+      cur ^= 1;
     }
   } else {
     if (tid == 0) R[(size_t)n * cap] = aqc::cmk(1.0, 0.0);
     __syncthreads();
     for (int i = n - 1; i >= 0; --i) {
       const int cl = j.dims[i], cr = j.dims[i + 1];
-      for (int l = tid; l < cl; l += kT) {
+      for (int l = q; l < cl; l += 4) {  // (uniform per wave)
         cplx acc = aqc::cmk(0, 0);
-        for (int r = 0; r < cr; ++r) acc = aqc::cfma(site_a(j.gam, j.lam, cap, i, 0, l, r), R[(size_t)(i + 1) * cap + r], acc);
-        R[(size_t)i * cap + l] = acc;
+        for (int r = lane; r < cr; r += 64) acc = aqc::cfma(site_a(j.gam, j.lam, cap, i, 0, l, r), v[cur][r], acc);
+        acc.x = wave_sum_d(acc.x);
+        acc.y = wave_sum_d(acc.y);
+        if (lane == 0) {
+          v[cur ^ 1][l] = acc;
+          R[(size_t)i * cap + l] = acc;
+        }
       }
       __syncthreads();
+      cur ^= 1;
     }
   }
 }
