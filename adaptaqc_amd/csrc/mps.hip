@@ -1003,15 +1003,16 @@ __device__ unsigned long long g_chain_ticks[5];
 // thread (ty, tx) = (lt / 16, lt % 16) rows l0 + tx + 16 i, columns r0 + ty + 16 jj (i, jj < 2):
 // 16 complex accumulators, 8 LDS reads per 64 FMAs (one output per thread read 4 per 16 and was
 // LDS-bound), then the gate mix in registers and coalesced theta writes (lanes along l).  Every
-// sub-group runs the same m steps, so the barriers pair up.  (An MFMA form needs more than the
-// chain's 128 VGPRs per lane: four P's of a quadrant are 16 accumulator tiles.)
+// sub-group runs the same m steps, so the barriers pair up.  Kept as the A/B form of the MFMA
+// theta below (-DAQC_THETA_MFMA=0): per k_chain workgroup 6.48 M against 5.18 M ticks of theta
+// over 49 updates, bench 7.83 against 8.06 M evals/s (round 6).
 // m is staged 8 at a time (16, with A's rows XOR-swizzled instead of padded -- half the barriers,
 // twice the loads in flight per step -- measured slower: 41.9 against 39.3 ms per k_chain launch)
 constexpr int kThetaCh = 8;
 constexpr int kThetaAPitch = 9;
 constexpr int kThetaLds = 2 * 32 * kThetaAPitch + 2 * kThetaCh * 33;  // complex per sub-group
 static_assert(4 * kThetaLds * 16 <= kChainLdsBytes, "theta staging exceeds the chain's LDS");
-__device__ __forceinline__ void chain_theta(const TwoSiteJob& j) {
+[[maybe_unused]] __device__ __forceinline__ void chain_theta(const TwoSiteJob& j) {
   extern __shared__ double2 xbuf[];
   const int tid = fresh_tid(), sg = tid >> 8, lt = tid & 255;
   constexpr int KCH = kThetaCh;
@@ -1106,6 +1107,117 @@ __device__ __forceinline__ void chain_theta(const TwoSiteJob& j) {
       }
   }
 }
+#ifndef AQC_THETA_MFMA
+#define AQC_THETA_MFMA 1
+#endif
+// theta in the chain on the FP64 matrix cores (round 6): wave w owns the 16 x 16 output tile
+// (r0, l0) = 16 (w >> 2, w & 3) of all four P_{s1 s2}, computed transposed -- P^T[r][l] = sum_m
+// B_{s2}[m][r] A_{s1}[l][m] (A operand: B_{s2} from the LDS, lane l: row r0 + l % 16, k = l / 16;
+// B operand: A_{s1}) -- so the accumulator rows run along r and its columns along l, and the theta
+// stores (column-major, l fastest) go out as 256-byte runs.  A complex product is four real MFMAs
+// into two accumulators (4 P's: 64 VGPRs of accumulators, the VALU form's 16 complex).  m is staged
+// 8 at a time for the whole workgroup (A: 2 x 64 x 8, B: 2 x 8 x 64 complex, double-buffered, one
+// barrier per chunk), the next chunk's global loads in flight during the current chunk's MFMAs.
+constexpr int kThetaMfmaAP = 9;   // As row pitch (complex): [s1][l][m]
+constexpr int kThetaMfmaBP = 65;  // Bs row pitch: [s2][m][r]
+constexpr int kThetaMfmaBuf = 2 * 64 * kThetaMfmaAP + 2 * 8 * kThetaMfmaBP;  // complex per buffer
+static_assert(2 * kThetaMfmaBuf * 16 <= kChainLdsBytes, "theta staging exceeds the chain's LDS");
+__device__ __forceinline__ void chain_theta_mfma(const TwoSiteJob& j) {
+  extern __shared__ double2 xbuf[];
+  const int tid = fresh_tid(), wave = tid >> 6, lane = tid & 63, li = lane & 15, lk = lane >> 4;
+  const int chl = j.dims[0], chm = j.dims[1], chr = j.dims[2];
+  const int cap = j.cap;
+  const size_t half = (size_t)cap * cap;
+  const int M = 2 * chl;
+  const int r0 = 16 * (wave >> 2), l0 = 16 * (wave & 3);
+  const bool active = r0 < chr && l0 < chl;  // (uniform per wave)
+  const cplx* gp = j.gp;
+  const cplx* gq = j.gq;
+  const double* llp = j.ll;
+  const double* lmp = j.lm;
+  const double* lrp = j.lr;
+  asm volatile("" : "+s"(gp), "+s"(gq), "+s"(llp), "+s"(lmp), "+s"(lrp));
+  __shared__ cplx sG[16];
+  if (tid < 16) sG[tid] = aqc::ldg(j.G + tid);
+  // this thread's staging element: A[s1 = e >> 9][l = (e >> 3) & 63][m = e & 7],
+  // B[s2 = e >> 9][m = (e >> 6) & 7][r = e & 63]
+  const int as1 = tid >> 9, al = (tid >> 3) & 63, am = tid & 7;
+  const int bs2 = tid >> 9, bm = (tid >> 6) & 7, br = tid & 63;
+  auto fetch = [&](int m0, cplx& a, cplx& b) {
+    const int ma = m0 + am, mb = m0 + bm;
+    a = (al < chl && ma < chm) ? aqc::cscale(aqc::ldg(gp + as1 * half + (size_t)al * cap + ma), aqc::ldg(llp + al) * aqc::ldg(lmp + ma))
+                               : aqc::cmk(0, 0);
+    b = (mb < chm && br < chr) ? aqc::cscale(aqc::ldg(gq + bs2 * half + (size_t)mb * cap + br), aqc::ldg(lrp + br)) : aqc::cmk(0, 0);
+  };
+  auto stash = [&](int buf, cplx a, cplx b) {
+    cplx* base = xbuf + buf * kThetaMfmaBuf;
+    base[(as1 * 64 + al) * kThetaMfmaAP + am] = a;
+    base[2 * 64 * kThetaMfmaAP + (bs2 * 8 + bm) * kThetaMfmaBP + br] = b;
+  };
+  aqc::d4_t cr[2][2], ci[2][2];
+#pragma unroll
+  for (int s1 = 0; s1 < 2; ++s1)
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) cr[s1][s2] = aqc::d4_t{0, 0, 0, 0}, ci[s1][s2] = aqc::d4_t{0, 0, 0, 0};
+  const int nch = (chm + 7) >> 3;
+  {
+    cplx a, b;
+    fetch(0, a, b);
+    stash(0, a, b);
+  }
+  __syncthreads();
+  for (int c = 0; c < nch; ++c) {
+    const bool more = c + 1 < nch;
+    cplx na = aqc::cmk(0, 0), nb = aqc::cmk(0, 0);
+    if (more) fetch(8 * (c + 1), na, nb);
+    if (active) {
+      const cplx* base = xbuf + (c & 1) * kThetaMfmaBuf;
+      const cplx* As = base;
+      const cplx* Bs = base + 2 * 64 * kThetaMfmaAP;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int mm = 4 * ks + lk;
+        cplx x[2], y[2];
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          x[s] = Bs[(s * 8 + mm) * kThetaMfmaBP + r0 + li];     // B_{s2}[m][r0 + li]
+          y[s] = As[(s * 64 + l0 + li) * kThetaMfmaAP + mm];    // A_{s1}[l0 + li][m]
+        }
+#pragma unroll
+        for (int s1 = 0; s1 < 2; ++s1)
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2) {
+            cr[s1][s2] = __builtin_amdgcn_mfma_f64_16x16x4f64(x[s2].x, y[s1].x, cr[s1][s2], 0, 0, 0);
+            cr[s1][s2] = __builtin_amdgcn_mfma_f64_16x16x4f64(-x[s2].y, y[s1].y, cr[s1][s2], 0, 0, 0);
+            ci[s1][s2] = __builtin_amdgcn_mfma_f64_16x16x4f64(x[s2].x, y[s1].y, ci[s1][s2], 0, 0, 0);
+            ci[s1][s2] = __builtin_amdgcn_mfma_f64_16x16x4f64(x[s2].y, y[s1].x, ci[s1][s2], 0, 0, 0);
+          }
+      }
+    }
+    if (more) stash((c + 1) & 1, na, nb);
+    __syncthreads();
+  }
+  if (active) {
+    const int l = l0 + li;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int r = r0 + lk + 4 * q;
+      if (l < chl && r < chr) {
+        const cplx p0 = aqc::cmk(cr[0][0][q], ci[0][0][q]), p1 = aqc::cmk(cr[0][1][q], ci[0][1][q]);
+        const cplx p2 = aqc::cmk(cr[1][0][q], ci[1][0][q]), p3 = aqc::cmk(cr[1][1][q], ci[1][1][q]);
+#pragma unroll
+        for (int o = 0; o < 4; ++o) {
+          cplx v = aqc::cmul(sG[o * 4 + 0], p0);
+          v = aqc::cfma(sG[o * 4 + 1], p1, v);
+          v = aqc::cfma(sG[o * 4 + 2], p2, v);
+          v = aqc::cfma(sG[o * 4 + 3], p3, v);
+          aqc::stg(j.theta + (size_t)((o & 1) * chr + r) * M + (o >> 1) * chl + l, v);  // GLOBAL, not FLAT
+        }
+      }
+    }
+  }
+}
+
 // the register Jacobi is the chain's fallback (Gram path off or refused): a real call, so that
 // its register allocation stays out of k_chain's
 __device__ __noinline__ void chain_jacobi_fallback(const TwoSiteJob& j) { jacobi_reg_body<128, 8, 16>(j); }
@@ -1227,7 +1339,11 @@ __global__ __launch_bounds__(1024) void k_chain(const ChainJob* __restrict__ cha
       continue;
     }
     const TwoSiteJob& j = two[code];
+#if AQC_THETA_MFMA
+    chain_theta_mfma(j);
+#else
     chain_theta(j);
+#endif
     __syncthreads();
     tick(0);
     chain_jacobi(j);
