@@ -511,6 +511,153 @@ __global__ __launch_bounds__(256) void k_env64(const RdmJob* __restrict__ jobs, 
   }
 }
 
+// ---- the sum of every <Z_i> through a window (the local cost's candidates, round 6) -----------
+// The local cost (aer_mps_backend.py:72-74, 80-86) needs only sum_i <Z_i>.  That sum is the
+// expectation of the bond-2 operator sum_i Z_i, whose environments are pairs: from the left
+//   L_{i+1} = sum_s A_s^dag L_i A_s,   LZ_{i+1} = sum_s A_s^dag (LZ_i + z_s L_i) A_s    (z = +1, -1)
+// (LZ_b: one Z somewhere left of bond b), from the right likewise, and sum_i <Z_i> = Tr(LZ_b R_b) +
+// Tr(L_b RZ_b) at any bond b.  A Rotoselect candidate is a copy of the prefix state rewritten only
+// on sites lo..hi (its gate, the suffix and the final sort: the handle's reload bookkeeping), so its
+// sum needs the prefix's pairs at bonds lo and hi + 1 (cached on the prefix handle and extended as
+// it changes) and its own left chain through lo..hi only -- instead of both full chains per
+// candidate.  A step is k_env_split's with the environment rows doubled: GEMM 1 takes [E; EZ]
+// (2 ke rows) against the site's columns, GEMM 2 writes E' to output columns [0, cw) and EZ' to
+// [cw, 2 cw), reading T_E for the first and T_EZ + z_t T_E for the second.
+struct ZJob {
+  const cplx* gam;
+  const double* lam;
+  const int* dims;
+  int cap;
+  int dir;          // 0: left, sites first, first + 1, ...; 1: right, sites first, first - 1, ...
+  int first;
+  int nsteps;
+  const cplx* ein;  // the pair (E, EZ) at the starting bond (2 cap^2)
+  cplx* eout;       // step s's pair at eout + (dir ? -s : s) 2 cap^2
+  cplx* tmp;        // NW x 2 cap x 2 cw
+};
+
+// grid (chains, NW), kT threads; cw = cap / NW output columns of each environment per workgroup.
+// Counters and the bounded hand-off as k_env_split's.
+template <int NB, int NW>
+__global__ __launch_bounds__(kT) void k_zenv(const ZJob* __restrict__ jobs, unsigned* __restrict__ cnt,
+                                             int* __restrict__ err, unsigned long long spin, int nchains, int cw) {
+  const int chain = blockIdx.x, w = blockIdx.y, tid = threadIdx.x;
+  if (chain >= nchains) return;
+  const ZJob& j = jobs[chain];
+  unsigned* ctr = cnt + 32 * chain;
+  __shared__ NarrowLds lds;
+  __shared__ int s_abort;
+  const int cap = j.cap, dir = j.dir;
+  const size_t cc = (size_t)cap * cap;
+  const int c0 = w * cw, ldt = 2 * cw;
+  cplx* Tw = j.tmp + (size_t)w * 2 * cap * ldt;
+  if (tid == 0) s_abort = 0;
+  for (int s = 0; s < j.nsteps; ++s) {
+    const int i = dir == 0 ? j.first + s : j.first - s;
+    const cplx* E = s == 0 ? j.ein : j.eout + (ptrdiff_t)(dir ? 1 - s : s - 1) * 2 * (ptrdiff_t)cc;
+    cplx* O = j.eout + (ptrdiff_t)(dir ? -s : s) * 2 * (ptrdiff_t)cc;
+    const int ke = dir == 0 ? j.dims[i] : j.dims[i + 1];
+    const int m2 = dir == 0 ? j.dims[i + 1] : j.dims[i];
+    const cplx* g = j.gam + (size_t)i * 2 * cc;
+    const double* lam = j.lam + (size_t)(i + 1) * cap;
+    auto site = [&](int t, int l, int r) {  // A_t[l][r] = Gamma_t[l][r] lambda_{i+1}[r]
+      return aqc::cscale(g[t * cc + (size_t)l * cap + r], lam[r]);
+    };
+    auto ea = [&](int l, int k) { return env_ld(E + (l < ke ? 0 : cc) + (size_t)(l < ke ? l : l - ke) * cap + k); };
+    auto ts = [&](int l, int c2, cplx v) { Tw[(size_t)l * ldt + c2] = v; };
+    if (dir == 0)  // T[l][t cw + c] = sum_k [E; EZ][l][k] A_t[k][c0 + c]
+      narrow_cgemm<NB, true, false>(
+          2 * ke, ldt, ke, ea,
+          [&](int k, int c2) { const int t = c2 / cw, c = c0 + c2 % cw; return c < m2 ? site(t, k, c) : aqc::cmk(0, 0); }, ts,
+          lds);
+    else  // T[k][t cw + c] = sum_k' [R; RZ][k][k'] conj(A_t[c0 + c][k'])
+      narrow_cgemm<NB, true, true>(
+          2 * ke, ldt, ke, ea,
+          [&](int k2, int c2) {
+            const int t = c2 / cw, c = c0 + c2 % cw;
+            return c < m2 ? aqc::cconj(site(t, c, k2)) : aqc::cmk(0, 0);
+          },
+          ts, lds);
+    __syncthreads();
+    // GEMM 2 over 2 cw output columns: [0, cw) the environment, [cw, 2 cw) its Z partner
+    auto tb = [&](int kk, int c2) {
+      const int t = kk / ke, k = kk % ke, zc = c2 < cw ? c2 : c2 - cw, col = t * cw + zc;
+      if (c0 + zc >= m2) return aqc::cmk(0, 0);
+      const cplx te = Tw[(size_t)k * ldt + col];
+      if (c2 < cw) return te;
+      const cplx tz = Tw[(size_t)(ke + k) * ldt + col];
+      return t == 0 ? aqc::cadd(tz, te) : aqc::csub(tz, te);
+    };
+    auto os = [&](int r, int c2, cplx v) {
+      const int zc = c2 < cw ? c2 : c2 - cw;
+      if (c0 + zc < m2) env_st(O + (c2 < cw ? 0 : cc) + (size_t)r * cap + c0 + zc, v);
+    };
+    if (dir == 0)  // L'[r][c0 + c] = sum_{t, k} conj(A_t[k][r]) T[k][t cw + c]
+      narrow_cgemm<NB, false, false>(
+          m2, ldt, 2 * ke, [&](int r, int kk) { return aqc::cconj(site(kk / ke, kk % ke, r)); }, tb, os, lds);
+    else  // R'[l][c0 + c] = sum_{t, k} A_t[l][k] T[k][t cw + c]
+      narrow_cgemm<NB, true, false>(
+          m2, ldt, 2 * ke, [&](int l, int kk) { return site(kk / ke, l, kk % ke); }, tb, os, lds);
+    // hand-off (k_env_split's)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned target = (unsigned)NW * (unsigned)(s + 1);
+      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+      while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+        __builtin_amdgcn_s_sleep(1);
+        if (__builtin_amdgcn_s_memrealtime() - t0 > spin) {
+          s_abort = 1;
+          atomicOr(err, 1);
+          break;
+        }
+      }
+    }
+    __syncthreads();
+    if (s_abort) return;
+  }
+}
+
+// out[s] = Re Tr(LZ R) + Re Tr(L RZ) for the pairs (L, LZ) at lp and (R, RZ) at rp, of bond
+// dimension dims[bond]; L[b][k] is bra x ket, R[k][b] ket x bra.  grid (states), kT threads.
+struct ZSumJob {
+  const cplx* lp;
+  const cplx* rp;
+  const int* dims;
+  int bond;
+  int cap;
+};
+__global__ __launch_bounds__(kT) void k_zsum(const ZSumJob* __restrict__ jobs, double* __restrict__ out) {
+  const ZSumJob& j = jobs[blockIdx.x];
+  const int d = j.dims[j.bond], cap = j.cap;
+  const size_t cc = (size_t)cap * cap;
+  double acc = 0.0;
+  for (int e = threadIdx.x; e < d * d; e += kT) {
+    const int b = e / d, k = e % d;  // L[b][k] R[k][b]
+    const cplx l = aqc::ldg(j.lp + (size_t)b * cap + k), lz = aqc::ldg(j.lp + cc + (size_t)b * cap + k);
+    const cplx r = aqc::ldg(j.rp + (size_t)k * cap + b), rz = aqc::ldg(j.rp + cc + (size_t)k * cap + b);
+    acc = fma(lz.x, r.x, fma(-lz.y, r.y, acc));
+    acc = fma(l.x, rz.x, fma(-l.y, rz.y, acc));
+  }
+  __shared__ double red[kT];
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int k = kT / 2; k > 0; k >>= 1) {
+    if ((int)threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[blockIdx.x] = red[0];
+}
+
+// the boundary pairs of a fresh cache: L_0 = [[1]], R_n = [[1]] (LZ_0 = RZ_n = 0 from the memset)
+__global__ void k_zenv_init(cplx* l0, cplx* rn) {
+  if (threadIdx.x == 0) {
+    l0[0] = aqc::cmk(1, 0);
+    rn[0] = aqc::cmk(1, 0);
+  }
+}
+
 // P_b[s][sb] = A_b^s R_{b+1} A_b^{sb dag}, stored transposed (j.P holds P^T: the traces against it,
 // Tr(E P) in the pair chains and Tr(L P) in k_rdm_ztrace, then read both operands along rows);
 // m = 0: (0,0), 1: (0,1), 2: (1,1).  grid (n, 3 or 2, states);
@@ -911,6 +1058,28 @@ int env_timed_out(void* sync, int ns, int cap, bool& timed_out) {
   return AQC_OK;
 }
 
+// The Z-sum chains (k_zenv): the split of launch_envs (env_split_cols / env_split_nw), or one
+// workgroup per chain (single, or a capacity without a split); rounds of <= 224 workgroups so that
+// a chain's workgroups are resident together.  cnt: 32 words per chain, zeroed by the caller.
+int launch_zenv(const ZJob* dj, int nch, int cap, hipStream_t st, unsigned* cnt, int* err, bool single) {
+  const bool one = single || g_env_single || env_split_cols(cap) == 0;
+  const int nw = one ? 1 : env_split_nw(cap), cw = cap / nw;
+  const int kRound = std::max(1, 224 / nw);
+  const unsigned long long spin = g_env_spin;
+  for (int c0 = 0; c0 < nch; c0 += kRound) {
+    const int m = std::min(kRound, nch - c0);
+    const dim3 g((m + 7) / 8 * 8, nw);  // (a chain's workgroups on one XCD, as launch_envs)
+    const ZJob* jb = dj + c0;
+    unsigned* cb = cnt + (size_t)c0 * 32;
+    if (nw == 1) hipLaunchKernelGGL((k_zenv<64, 1>), g, dim3(kT), 0, st, jb, cb, err, spin, m, cw);
+    else if (nw == 16) hipLaunchKernelGGL((k_zenv<64, 16>), g, dim3(kT), 0, st, jb, cb, err, spin, m, cw);
+    else if (cw == 16) hipLaunchKernelGGL((k_zenv<32, kEnvNW>), g, dim3(kT), 0, st, jb, cb, err, spin, m, cw);
+    else hipLaunchKernelGGL((k_zenv<64, kEnvNW>), g, dim3(kT), 0, st, jb, cb, err, spin, m, cw);
+    AQC_CHECK_LAUNCH();
+  }
+  return AQC_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1075,6 +1244,148 @@ int aqc_mps_z_all_batch(aqc_mps_t* hs, int ns, double* out) {
     }
     if (!again) return AQC_OK;
   }
+}
+
+/* sum_i <Z_i> of every state hs[s] (sorted first, as aqc_mps_z_all_batch does): a state copied
+   from `base` (aqc_mps_copy / aqc_mps_copy_batch) while base has not changed since takes base's
+   cached environment pairs outside the sites it has rewritten and runs its own chain through those
+   only; any other state runs aqc_mps_z_all_batch and sums.  base is not modified (its cache is
+   extended). */
+int aqc_mps_z_sum_batch(aqc_mps_t base, aqc_mps_t* hs, int ns, double* out) {
+  AQC_REQUIRE(base && hs && ns >= 0 && (out || ns == 0), "aqc_mps_z_sum_batch: bad arguments");
+  if (ns == 0) return AQC_OK;
+  const int n = base->d.n, cap = base->d.cap;
+  for (int s = 0; s < ns; ++s)
+    AQC_REQUIRE(hs[s] && hs[s] != base && hs[s]->d.n == n && hs[s]->d.cap == cap,
+                "aqc_mps_z_sum_batch: every state needs base's n and capacity (and is not base)");
+  int rc = aqc_mps_sort_batch(hs, ns);
+  if (rc != AQC_OK) return rc;
+  // windows: the sites each state rewrote since its copy from base (empty: site 0, any bond works)
+  std::vector<int> win, lo(ns, -1), hi(ns, -1), fb;
+  int need_l = 0, need_r = n;
+  for (int s = 0; s < ns; ++s) {
+    const aqc_mps_s* h = hs[s];
+    if (h->synced_src != base->uid || h->synced_ver != base->version) {
+      fb.push_back(s);
+      continue;
+    }
+    lo[s] = h->dirty_hi >= h->dirty_lo ? h->dirty_lo : 0;
+    hi[s] = h->dirty_hi >= h->dirty_lo ? h->dirty_hi : 0;
+    need_l = std::max(need_l, lo[s]);
+    need_r = std::min(need_r, hi[s] + 1);
+    win.push_back(s);
+  }
+  const size_t cc = (size_t)cap * cap, pair = 2 * cc;
+  hipStream_t st = aqc::mps_stream();
+  if (!win.empty()) {
+    if (!base->zenv) {
+      base->zenv = (cplx*)aqc::dev_alloc(2 * (size_t)(n + 1) * pair * sizeof(cplx));
+      AQC_REQUIRE(base->zenv, "aqc_mps_z_sum_batch: out of device memory");
+      AQC_HIP_CHECK(hipMemsetAsync(base->zenv, 0, 2 * (size_t)(n + 1) * pair * sizeof(cplx), st));
+      hipLaunchKernelGGL(k_zenv_init, dim3(1), dim3(64), 0, st, base->zenv, base->zenv + (size_t)(n + 1) * pair + (size_t)n * pair);
+      AQC_CHECK_LAUNCH();
+      base->zenv_stale();
+    }
+    cplx* ZL = base->zenv;
+    cplx* ZR = base->zenv + (size_t)(n + 1) * pair;
+    std::vector<ZJob> jobs;
+    auto job = [&](aqc_mps_t h, int dir, int first, int nsteps, const cplx* ein, cplx* eout) {
+      ZJob j;
+      j.gam = h->d.gam;
+      j.lam = h->d.lam;
+      j.dims = h->d.dims;
+      j.cap = cap;
+      j.dir = dir;
+      j.first = first;
+      j.nsteps = nsteps;
+      j.ein = ein;
+      j.eout = eout;
+      j.tmp = nullptr;
+      jobs.push_back(j);
+    };
+    // launch 1: extend base's cache (left pairs to bond need_l, right pairs down to need_r)
+    const int zl = base->zl, zr = base->zr;
+    if (need_l > zl) job(base, 0, zl, need_l - zl, ZL + (size_t)zl * pair, ZL + (size_t)(zl + 1) * pair);
+    if (need_r < zr) job(base, 1, zr - 1, zr - need_r, ZR + (size_t)zr * pair, ZR + (size_t)(zr - 1) * pair);
+    const int nbase = (int)jobs.size();
+    // launch 2: each state's left chain through its window, from base's pair at bond lo
+    size_t wsteps = 0;
+    for (int s : win) wsteps += (size_t)(hi[s] - lo[s] + 1);
+    const int nch = nbase + (int)win.size();
+    const size_t jb = ((nch * sizeof(ZJob) + 255) / 256) * 256;
+    const size_t zb = ((win.size() * sizeof(ZSumJob) + 255) / 256) * 256;
+    const size_t ob = ((win.size() * sizeof(double) + 255) / 256) * 256;
+    const size_t sb = ((((size_t)nch * 32 + 32) * sizeof(unsigned) + 255) / 256) * 256;
+    const size_t tb = (size_t)nch * 4 * cc * sizeof(cplx);
+    const size_t wb = wsteps * pair * sizeof(cplx);
+    RdmBuffers& rb = rbuf();
+    AQC_HIP_CHECK(hipStreamSynchronize(st));
+    rc = ensure(rb, jb + zb + ob + sb + tb + wb + 1024);
+    if (rc != AQC_OK) return rc;
+    char* b = (char*)rb.dev;
+    ZJob* dj = (ZJob*)b;
+    ZSumJob* dz = (ZSumJob*)(b + jb);
+    double* dout = (double*)(b + jb + zb);
+    unsigned* cnt = (unsigned*)(b + jb + zb + ob);
+    int* err = (int*)(cnt + (size_t)nch * 32);
+    cplx* tmp = (cplx*)(b + jb + zb + ob + sb);
+    cplx* wbuf = tmp + (size_t)nch * 4 * cc;
+    std::vector<ZSumJob> sums;
+    size_t woff = 0;
+    for (int s : win) {
+      const int steps = hi[s] - lo[s] + 1;
+      cplx* eo = wbuf + woff * pair;
+      job(hs[s], 0, lo[s], steps, ZL + (size_t)lo[s] * pair, eo);
+      woff += (size_t)steps;
+      ZSumJob z;
+      z.lp = eo + (size_t)(steps - 1) * pair;
+      z.rp = ZR + (size_t)(hi[s] + 1) * pair;
+      z.dims = hs[s]->d.dims;
+      z.bond = hi[s] + 1;
+      z.cap = cap;
+      sums.push_back(z);
+    }
+    for (int c = 0; c < nch; ++c) jobs[c].tmp = tmp + (size_t)c * 4 * cc;
+    AQC_HIP_CHECK(hipMemcpyAsync(dj, jobs.data(), nch * sizeof(ZJob), hipMemcpyHostToDevice, st));
+    AQC_HIP_CHECK(hipMemcpyAsync(dz, sums.data(), sums.size() * sizeof(ZSumJob), hipMemcpyHostToDevice, st));
+    std::vector<double> res(win.size());
+    for (int attempt = 0;; ++attempt) {  // attempt 1: a hand-off timed out, single-workgroup chains
+      AQC_HIP_CHECK(hipMemsetAsync(cnt, 0, sb, st));
+      aqc::KernelTimer::begin(st, "mps_zsum", 0.0, (double)(wsteps + (size_t)(need_l > zl ? need_l - zl : 0) + (size_t)(need_r < zr ? zr - need_r : 0)) * 2.0 * 8.0 * 4.0 * (double)cc * cap);
+      if (nbase) {
+        rc = launch_zenv(dj, nbase, cap, st, cnt, err, attempt > 0);
+        if (rc != AQC_OK) return rc;
+      }
+      rc = launch_zenv(dj + nbase, (int)win.size(), cap, st, cnt + (size_t)nbase * 32, err, attempt > 0);
+      if (rc != AQC_OK) return rc;
+      hipLaunchKernelGGL(k_zsum, dim3((unsigned)win.size()), dim3(kT), 0, st, dz, dout);
+      aqc::KernelTimer::end(st);
+      AQC_CHECK_LAUNCH();
+      AQC_HIP_CHECK(hipMemcpyAsync(res.data(), dout, res.size() * sizeof(double), hipMemcpyDeviceToHost, st));
+      AQC_HIP_CHECK(hipStreamSynchronize(st));
+      int e = 0;
+      AQC_HIP_CHECK(hipMemcpy(&e, err, sizeof(int), hipMemcpyDeviceToHost));
+      if (e == 0) break;
+      AQC_REQUIRE(attempt == 0, "aqc_mps_z_sum_batch: single-workgroup chains timed out");
+      ++g_env_fallbacks;
+    }
+    base->zl = std::max(zl, need_l);
+    base->zr = std::min(zr, need_r);
+    for (size_t k = 0; k < win.size(); ++k) out[win[k]] = res[k];
+  }
+  if (!fb.empty()) {  // states not copied from base (or base changed since): the full chains
+    std::vector<aqc_mps_t> fh;
+    for (int s : fb) fh.push_back(hs[s]);
+    std::vector<double> z((size_t)fb.size() * n);
+    rc = aqc_mps_z_all_batch(fh.data(), (int)fh.size(), z.data());
+    if (rc != AQC_OK) return rc;
+    for (size_t k = 0; k < fb.size(); ++k) {
+      double t = 0.0;
+      for (int q = 0; q < n; ++q) t += z[k * n + q];
+      out[fb[k]] = t;
+    }
+  }
+  return AQC_OK;
 }
 
 /* Environment launches whose split chains timed out on a hand-off and were re-run with

@@ -2325,6 +2325,7 @@ int aqc_mps_create(int n, int chi_cap, double threshold, int max_chi, aqc_mps_t*
   AQC_HIP_CHECK(hipGetDevice(&h->dev));
   h->d.n = n;
   h->d.cap = chi_cap;
+  h->zr = n;
   h->thr = threshold;
   h->max_chi = max_chi;
   h->order.resize(n);
@@ -2390,6 +2391,7 @@ int aqc_mps_destroy(aqc_mps_t h) {
   aqc::dev_free(h->base);
   aqc::dev_free(h->d.env);
   aqc::dev_free(h->gw);
+  aqc::dev_free(h->zenv);
   for (auto& sl : h->slots) {
     aqc::dev_free(sl.theta);
     aqc::dev_free(sl.work);
@@ -2687,6 +2689,7 @@ int aqc_mps_copy_batch(aqc_mps_t* dst, const aqc_mps_t* src, int ns) {
     d->dirty_lo = 1 << 30;
     d->dirty_hi = -1;
     ++d->version;
+    d->zenv_stale();
   }
   hipStream_t st = aqc::mps_stream();
   StagingLease lease(st);  // (the ring: no wait for the stream's earlier work)
@@ -2757,6 +2760,7 @@ int aqc_mps_copy(aqc_mps_t dst, const aqc_mps_t src) {
   dst->ub = src->ub;
   dst->loc = src->loc;
   if (dst != src) {
+    dst->zenv_stale();
     dst->synced_src = src->uid;
     dst->synced_ver = src->version;
     dst->dirty_lo = 1 << 30;

@@ -265,14 +265,27 @@ struct aqc_mps_s {
   unsigned long long synced_src = 0;
   unsigned long long synced_ver = 0;
   int dirty_lo = 1 << 30, dirty_hi = -1;
+  // Cached Z-sum environments (ent.hip, aqc_mps_z_sum_batch): zenv holds, per bond b, the left pair
+  // (L_b, LZ_b) and the right pair (R_b, RZ_b); left pairs are current for bonds <= zl, right pairs
+  // for bonds >= zr.  A rewrite of Gamma sites lo..hi (and the lambdas between them) leaves the left
+  // environments up to bond lo and the right ones from bond hi + 1 as they were.
+  aqc::cplx* zenv = nullptr;
+  int zl = 0, zr = 1 << 30;
   void changed(int lo, int hi) {  // Gamma sites lo..hi rewritten
     ++version;
     dirty_lo = lo < dirty_lo ? lo : dirty_lo;
     dirty_hi = hi > dirty_hi ? hi : dirty_hi;
+    zl = lo < zl ? lo : zl;
+    zr = hi + 1 > zr ? hi + 1 : zr;
   }
   void changed_all() {
     ++version;
     synced_src = 0;
+    zenv_stale();
+  }
+  void zenv_stale() {  // every cached environment past the boundaries
+    zl = 0;
+    zr = d.n;
   }
   // the one device block the handle's fixed buffers are carved from (aqc::dev_alloc)
   void* base = nullptr;

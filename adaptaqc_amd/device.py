@@ -294,6 +294,15 @@ def z_all_batch(states):
     return out.reshape(len(states), n)
 
 
+def z_sum_batch(base, states):
+    """sum_i <Z_i> of every state (aqc_mps_z_sum_batch): states copied from ``base`` (unchanged
+    since) contract only the sites they rewrote, against environments cached on ``base``."""
+    out = np.zeros(len(states))
+    if states:
+        _lib.check(_lib.lib().aqc_mps_z_sum_batch(base.h, _handles(states), len(states), _lib.ptr(out)))
+    return out
+
+
 def amps_hw1_batch(states):
     """Amplitudes <e_i|psi> of every state (rows, complex), one set of launches
     (aqc_mps_amps_hw1_batch)."""

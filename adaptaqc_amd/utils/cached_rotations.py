@@ -30,7 +30,9 @@ candidates differ in one single-qubit gate, so:
   in lock-step batched launches (aqc_mps_copy_batch / apply_batch / overlap_zero_batch).
 * MPS, local cost (0.5 (1 - mean <Z_i>), aer_mps_backend.py:72-74, 80-86) or softened global cost
   (1 - |<0|psi>|^2 - alpha sum_i |<e_i|psi>|^2, :49-70): the same prefix batch, then every
-  candidate's <Z_i> (aqc_mps_z_all_batch) or HW-1 amplitudes (aqc_mps_amps_hw1_batch) in one set of
+  candidate's sum of <Z_i> (aqc_mps_z_sum_batch: a candidate differs from the prefix only on the
+  sites its gate, the suffix and the sort rewrote, so it contracts those against environments of
+  sum_i Z_i cached on the prefix) or HW-1 amplitudes (aqc_mps_amps_hw1_batch) in one set of
   launches.
 * Statevector, local cost (aer_sv_backend.py:32-35, 49-59): no transition shortcut (every <Z_i> of
   every candidate); the prefix state is cached and the candidates replay the suffix from it.
@@ -44,7 +46,7 @@ import numpy as np
 from .. import gates as G
 from .._lib import OP_DTYPE, ops_array
 from ..circuit import device_ops, device_ops_rows
-from ..device import DeviceSV, amps_hw1_batch, apply_batch, copy_batch, overlap_zero_batch, z_all_batch
+from ..device import DeviceSV, amps_hw1_batch, apply_batch, copy_batch, overlap_zero_batch, z_sum_batch
 
 
 class _View:
@@ -190,8 +192,10 @@ class MPSPrefixBatch(_SweepBase):
         lists = [np.frombuffer(cand[i * size:(i + 1) * size] + suffix, dtype=OP_DTYPE) for i in range(len(mats))]
         apply_batch(states, lists, sort=True)
         if self.kind == "local":
-            z = z_all_batch(states)
-            return [float(0.5 * (1 - np.mean(row))) for row in z]
+            # only sum_i <Z_i> enters the cost: each candidate contracts the sites it rewrote
+            # against the prefix's cached environments (aqc_mps_z_sum_batch)
+            n = circ.num_qubits
+            return [float(0.5 * (1 - t / n)) for t in z_sum_batch(self.phi, states)]
         ov = overlap_zero_batch(states)
         costs = [float(1.0 - abs(v) ** 2) for v in ov]
         if self.kind == "soft":

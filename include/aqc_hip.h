@@ -153,6 +153,13 @@ int aqc_mps_amps_hw1(aqc_mps_t h, double* out);
    chains; both are full contractions (no canonical form assumed). */
 int aqc_mps_z_all_batch(aqc_mps_t* hs, int nstates, double* out);
 int aqc_mps_amps_hw1_batch(aqc_mps_t* hs, int nstates, double* out);
+/* out[s] = sum_i <Z_i> of hs[s] (sorted first, as z_all_batch) -- the local cost
+   0.5 (1 - mean <Z_i>) (aer_mps_backend.py:72-74, 80-86) needs only the sum.  A state copied from
+   `base` (aqc_mps_copy / aqc_mps_copy_batch) while base has not changed since contracts only the
+   sites it rewrote, against environment pairs of the operator sum_i Z_i cached on base (extended
+   as base changes: the Rotoselect prefix of cost_minimiser.py:318-368); any other state takes the
+   full chains of z_all_batch.  base itself is not modified and must not be among hs. */
+int aqc_mps_z_sum_batch(aqc_mps_t base, aqc_mps_t* hs, int nstates, double* out);
 
 /* ---- candidate sweep: replaces gradients.py:23-124 ------------------------------ */
 /* For every pair (pairs[2p], pairs[2p+1]) = (control, target):

@@ -1,0 +1,138 @@
+"""sum_i <Z_i> through a window (aqc_mps_z_sum_batch): the local cost's candidates contract only the
+sites they rewrote since their copy from the prefix state, against environment pairs of the operator
+sum_i Z_i cached on the prefix (ent.hip k_zenv / k_zsum).  Checked against the full chains
+(aqc_mps_z_all_batch, itself pinned to the oracle's full contraction) and, for a few states, against
+the oracle directly; the cache is checked as the prefix changes (its pairs stay current only outside
+the rewritten sites)."""
+
+import numpy as np
+import pytest
+
+from conftest import to_circuit
+from oracle import mps as M
+
+pytestmark = pytest.mark.gpu
+
+
+def _dops(n, ops):
+    from adaptaqc_amd.circuit import device_ops
+
+    return device_ops(to_circuit(n, ops))
+
+
+def _layer(rng, qubits):
+    ops = []
+    for q in qubits:
+        ops.append(("ry", (q,), (float(rng.uniform(-np.pi, np.pi)),)))
+        ops.append(("rz", (q,), (float(rng.uniform(-np.pi, np.pi)),)))
+    return ops
+
+
+def _windows(n, rng):
+    """candidate op lists: one-qubit, adjacent, routed (non-adjacent), both edges, none"""
+    c = []
+    c.append(_layer(rng, [5]))
+    c.append(_layer(rng, [6, 7]) + [("cx", (6, 7), ())] + _layer(rng, [6, 7]))
+    c.append(_layer(rng, [2, 9]) + [("cx", (9, 2), ())])
+    c.append([("cx", (0, 1), ())] + _layer(rng, [0]) + [("cx", (n - 2, n - 1), ())])
+    c.append([])
+    c.append(_layer(rng, [n - 1]) + [("cx", (n - 1, 0), ())])
+    return c
+
+
+@pytest.mark.parametrize("cap", [16, 64, 100, 128, 256])
+def test_z_sum_windows_vs_full_chains(cap):
+    """Six candidates of a random 14-qubit prefix (one-qubit, adjacent, routed and edge windows, an
+    empty one, a routed gate spanning the whole chain) plus a state not copied from the prefix (the
+    full-chain fallback): every sum against z_all_batch's row sum at 1e-11, over capacities with the
+    four-workgroup split (16 columns at 64, 32 at 128, 64 at 256) and without it (16, 100).  Then the
+    prefix changes three times -- a gate inside, one at the far right, a reload -- and the sums of
+    fresh candidates are checked again (the cached pairs extended, not reused stale)."""
+    import bench
+    from adaptaqc_amd.device import DeviceMPS, copy_batch, z_all_batch, z_sum_batch
+
+    n = 14
+    rng = np.random.default_rng(cap)
+    bond = min(cap, 48)
+    base = DeviceMPS(n, cap, 1e-16, cap)
+    base.load_aer(bench.random_vidal_mps(n, bond, 900 + cap))
+    other = DeviceMPS(n, cap, 1e-16, cap)
+    other.load_aer(bench.random_vidal_mps(n, bond, 950 + cap))
+    cands = [DeviceMPS(n, cap, 1e-16, cap) for _ in range(6)]
+
+    def check(tag):
+        lists = _windows(n, rng)
+        copy_batch(cands, [base] * len(cands))
+        for d, ops in zip(cands, lists):
+            d.apply(_dops(n, ops))
+        states = cands + [other]
+        got = z_sum_batch(base, states)
+        want = z_all_batch(states).sum(axis=1)
+        np.testing.assert_allclose(got, want, atol=1e-11, err_msg=tag)
+        return got
+
+    check("fresh cache")
+    base.apply(_dops(n, _layer(rng, [4, 5]) + [("cx", (4, 5), ())]))
+    check("prefix changed on sites 4-5")
+    base.apply(_dops(n, [("cx", (n - 2, n - 1), ())] + _layer(rng, [n - 1])))
+    check("prefix changed at the right edge")
+    base.load_aer(bench.random_vidal_mps(n, bond, 990 + cap))
+    got = check("prefix reloaded")
+    # one candidate straight against the oracle
+    pre = cands[1].preprocessed()
+    assert abs(got[1] - sum(M.mps_expectation_z(pre, i) for i in range(n))) < 1e-11
+
+
+def test_z_sum_truncating_candidates_vs_oracle():
+    """Candidates whose gates truncate (max_chi 8 on a bond-8 prefix, capacity 64): the window's
+    chain runs on the truncated tensors and the prefix's cached pairs outside it -- the oracle's full
+    contraction of each candidate's read-back state, at 1e-11."""
+    import bench
+    from adaptaqc_amd.device import DeviceMPS, copy_batch, z_sum_batch
+
+    n, chi = 12, 8
+    rng = np.random.default_rng(3)
+    base = DeviceMPS(n, 64, 1e-16, chi)
+    base.load_aer(bench.random_vidal_mps(n, chi, 77))
+    cands = [DeviceMPS(n, 64, 1e-16, chi) for _ in range(4)]
+    copy_batch(cands, [base] * 4)
+    for k, d in enumerate(cands):
+        a = 2 + 2 * k
+        d.apply(_dops(n, _layer(rng, [a, a + 1]) + [("cx", (a, a + 1), ())] + _layer(rng, [a + 1]) + [("cx", (a + 1, a), ())]))
+    got = z_sum_batch(base, cands)
+    for k, d in enumerate(cands):
+        pre = d.preprocessed()
+        assert max(d.dims()) <= chi
+        assert abs(got[k] - sum(M.mps_expectation_z(pre, i) for i in range(n))) < 1e-11
+
+
+def test_z_sum_timeout_reruns_single_workgroup():
+    """Hand-off spin limit 0: the split Z-sum chains time out and the call re-runs them on one
+    workgroup each (counted by aqc_env_fallbacks), with the same sums."""
+    import ctypes
+
+    import bench
+    from adaptaqc_amd import _lib
+    from adaptaqc_amd.device import DeviceMPS, copy_batch, z_sum_batch
+
+    n, cap = 12, 64
+    lib = _lib.load()
+    cnt = ctypes.c_longlong(0)
+    _lib.check(lib.aqc_env_fallbacks(ctypes.byref(cnt)))
+    sums = []
+    for limit in (-1.0, 0.0):
+        base = DeviceMPS(n, cap, 1e-16, cap)
+        base.load_aer(bench.random_vidal_mps(n, 40, 31))
+        cands = [DeviceMPS(n, cap, 1e-16, cap) for _ in range(3)]
+        copy_batch(cands, [base] * 3)
+        r = np.random.default_rng(11)
+        for k, d in enumerate(cands):
+            d.apply(_dops(n, _layer(r, [3 + k, 4 + k]) + [("cx", (3 + k, 4 + k), ())]))
+        _lib.check(lib.aqc_env_set_spin_limit(limit))
+        try:
+            sums.append(z_sum_batch(base, cands))
+        finally:
+            _lib.check(lib.aqc_env_set_spin_limit(-1.0))
+    _lib.check(lib.aqc_env_fallbacks(ctypes.byref(cnt)))
+    assert cnt.value >= 1
+    np.testing.assert_allclose(sums[1], sums[0], atol=1e-12)
