@@ -29,7 +29,7 @@ EXPORTS = (
     "aqc_mps_create", "aqc_mps_destroy", "aqc_mps_set_truncation", "aqc_mps_set_vidal",
     "aqc_mps_get_vidal", "aqc_mps_get_dims", "aqc_mps_copy", "aqc_mps_copy_batch", "aqc_mps_apply",
     "aqc_mps_apply_batch", "aqc_mps_apply_sort_batch", "aqc_mps_apply_sort_batch_async", "aqc_mps_check_batch", "aqc_mps_sort", "aqc_mps_sort_batch", "aqc_mps_overlap_zero",
-    "aqc_mps_overlap_zero_batch", "aqc_mps_dot", "aqc_mps_z_all", "aqc_mps_amps_hw1", "aqc_mps_z_all_batch", "aqc_mps_z_sum_batch",
+    "aqc_mps_overlap_zero_batch", "aqc_mps_dot", "aqc_mps_z_all", "aqc_mps_amps_hw1", "aqc_mps_z_all_batch", "aqc_mps_z_sum_batch", "aqc_mps_zero_hw1_batch",
     "aqc_mps_amps_hw1_batch",
     "aqc_pair_grads", "aqc_pair_grads_batch", "aqc_argmax_scaled", "aqc_argmax_scaled_batch", "aqc_mps_jacobi_stats",
     "aqc_mps_set_jacobi_tol", "aqc_mps_set_jacobi_stop", "aqc_mps_set_fused_chain", "aqc_mps_chain_ticks", "aqc_svd_debug",
@@ -97,6 +97,7 @@ _SIGS = {
     "aqc_mps_amps_hw1": ([_P, _P], _I),
     "aqc_mps_z_all_batch": ([_P, _I, _P], _I),
     "aqc_mps_z_sum_batch": ([_P, _P, _I, _P], _I),
+    "aqc_mps_zero_hw1_batch": ([_P, _P, _I, _P, _P], _I),
     "aqc_mps_amps_hw1_batch": ([_P, _I, _P], _I),
     "aqc_pair_grads": ([_P, _P, _P, _I, _P, _P, _P, _I, _P, _I], _I),
     "aqc_pair_grads_batch": ([_P, _I, _P, _P, _I, _P, _P, _P, _I, _P, _I], _I),

@@ -1284,7 +1284,8 @@ int aqc_mps_z_sum_batch(aqc_mps_t base, aqc_mps_t* hs, int ns, double* out) {
       AQC_HIP_CHECK(hipMemsetAsync(base->zenv, 0, 2 * (size_t)(n + 1) * pair * sizeof(cplx), st));
       hipLaunchKernelGGL(k_zenv_init, dim3(1), dim3(64), 0, st, base->zenv, base->zenv + (size_t)(n + 1) * pair + (size_t)n * pair);
       AQC_CHECK_LAUNCH();
-      base->zenv_stale();
+      base->zl = 0;
+      base->zr = n;
     }
     cplx* ZL = base->zenv;
     cplx* ZR = base->zenv + (size_t)(n + 1) * pair;

@@ -1495,6 +1495,161 @@ __global__ __launch_bounds__(kT) void k_hw1(const MeasJob* __restrict__ jobs) {
   if (threadIdx.x == 0) j.out[i] = aqc::cmk(red[0][0], red[1][0]);
 }
 
+// ---- zero and Hamming-weight-1 amplitudes through a window (round 6) --------------------------
+// The global cost's <0|psi> and the softened cost's <e_i|psi> (aer_mps_backend.py:49-70, 88-93)
+// are linear in every site tensor.  Rows from the left, per bond b: row 0 = <0..0| A_0 .. A_{b-1}
+// (all sites on 0), row 1 + k = the same with site k < b on 1; from the right: row 0 =
+// A_b .. A_{n-1} |0..0>, row 1 + k = with site k >= b on 1.  A Rotoselect candidate differs from
+// the prefix only on the sites lo..hi it rewrote, so with the prefix's left rows at bond lo (Ml) and
+// right rows at bond hi + 1 (Nr), cached on the prefix handle:
+//   u   = Ml[0] W (W: the window's A[0] product; rows for the window's own flips alongside),
+//   y   = W Nr[0]  (the window from the right),
+//   <0|psi> = u . Nr[0];  amp_k = Ml[1 + k] . y (k < lo), Wrow[1 + k] . Nr[0] (lo <= k <= hi),
+//   u . Nr[1 + k] (k > hi)
+// -- a window of w sites costs w small vector steps instead of two n-step chains.
+struct HwRowsJob {
+  const cplx* gam;
+  const double* lam;
+  const int* dims;
+  int n, cap;
+  int dir, first, nsteps;  // left: sites first .. first + nsteps - 1; right: first down
+  int full;                // every row, or row 0 only
+  cplx* rows;              // bond b's (n + 1) x cap block at rows + b (n + 1) cap
+};
+
+// The prefix's rows.  grid (directions, G): with `full`, workgroup g owns the flip rows 1 + k with
+// k % G == g (each an independent chain once created) and every workgroup carries row 0 itself
+// (in its LDS; workgroup 0 stores it), so the workgroups never wait on each other -- a step's rows
+// of a 50-site chain on one CU's FP64 rate were ~5 us.  Every bond has its own block, written once
+// per launch and read by the next step only (no stale L1 line).  Waves over output rows, lanes
+// over the output's bond index.
+constexpr int kHwRowsG = 8;
+__global__ __launch_bounds__(kT) void k_hw_rows(const HwRowsJob* __restrict__ jobs) {
+  const HwRowsJob& j = jobs[blockIdx.x];
+  const int n = j.n, cap = j.cap, g = blockIdx.y, G = gridDim.y;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const size_t blk = (size_t)(n + 1) * cap;
+  __shared__ cplx v0[2][kMaxCap];  // row 0, this workgroup's copy
+  {
+    const int b = j.dir == 0 ? j.first : j.first + 1, d = j.dims[b];
+    for (int e = threadIdx.x; e < d; e += kT) v0[0][e] = j.rows[(size_t)b * blk + e];
+  }
+  __syncthreads();
+  for (int s = 0; s < j.nsteps; ++s) {
+    const int i = j.dir == 0 ? j.first + s : j.first - s;
+    const int ke = j.dir == 0 ? j.dims[i] : j.dims[i + 1], m2 = j.dir == 0 ? j.dims[i + 1] : j.dims[i];
+    const cplx* M = j.rows + (size_t)(j.dir == 0 ? i : i + 1) * blk;
+    cplx* O = j.rows + (size_t)(j.dir == 0 ? i + 1 : i) * blk;
+    const cplx* v = v0[s & 1];
+    cplx* vn = v0[(s + 1) & 1];
+    // this workgroup's rows: ridx 0 = row 0; then the old flip rows k (left: k < i, right: k > i)
+    // with k % G == g; then the new row 1 + i if i % G == g
+    int k0, nold;
+    if (!j.full) k0 = 0, nold = 0;
+    else if (j.dir == 0) k0 = g, nold = i > g ? (i - g + G - 1) / G : 0;
+    else {
+      k0 = i + 1 + ((g - (i + 1) % G) % G + G) % G;
+      nold = k0 < n ? (n - 1 - k0) / G + 1 : 0;
+    }
+    const int nnew = j.full && i % G == g ? 1 : 0, nr = 1 + nold + nnew;
+    for (int ridx = wave; ridx < nr; ridx += kT / 64) {  // (uniform per wave)
+      int row, t;
+      const cplx* src;
+      if (ridx == 0) row = 0, t = 0, src = v;
+      else if (ridx <= nold) row = 1 + k0 + G * (ridx - 1), t = 0, src = M + (size_t)row * cap;
+      else row = 1 + i, t = 1, src = v;
+      for (int c0 = 0; c0 < m2; c0 += 64) {
+        const int c = c0 + lane;
+        if (c >= m2) continue;
+        cplx acc = aqc::cmk(0, 0);
+        if (j.dir == 0)  // O[row][c] = sum_l src[l] A_t[l][c]
+          for (int l = 0; l < ke; ++l) acc = aqc::cfma(src[l], site_a(j.gam, j.lam, cap, i, t, l, c), acc);
+        else  // O[row][c] = sum_r A_t[c][r] src[r]
+          for (int r = 0; r < ke; ++r) acc = aqc::cfma(site_a(j.gam, j.lam, cap, i, t, c, r), src[r], acc);
+        if (ridx == 0) vn[c] = acc;
+        if (ridx != 0 || g == 0) O[(size_t)row * cap + c] = acc;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+struct HwWinJob {
+  const cplx* gam;
+  const double* lam;
+  const int* dims;
+  int n, cap, lo, hi;
+  const cplx* ml;  // prefix's left rows at bond lo
+  const cplx* nr;  // prefix's right rows at bond hi + 1
+  cplx* ov;        // <0..0|psi> (the amplitude; the host conjugates for mps_dot(psi, zero))
+  cplx* amps;      // n amplitudes, or nullptr
+};
+
+// one workgroup per state; dynamic LDS: W rows (ping-pong, 2 (w + 1) cap) and y (2 cap)
+__global__ __launch_bounds__(kT) void k_hw_win(const HwWinJob* __restrict__ jobs) {
+  const HwWinJob& j = jobs[blockIdx.x];
+  extern __shared__ cplx hw_lds[];
+  const int cap = j.cap, n = j.n, lo = j.lo, hi = j.hi, w = hi - lo + 1;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  cplx* Wb[2] = {hw_lds, hw_lds + (size_t)(w + 1) * cap};
+  cplx* yb[2] = {hw_lds + 2 * (size_t)(w + 1) * cap, hw_lds + 2 * (size_t)(w + 1) * cap + cap};
+  {
+    const int dl = j.dims[lo], dr = j.dims[hi + 1];
+    for (int e = tid; e < dl; e += kT) Wb[0][e] = j.ml[e];
+    for (int e = tid; e < dr; e += kT) yb[0][e] = j.nr[e];
+  }
+  __syncthreads();
+  for (int s = 0; s < w; ++s) {
+    const cplx* W = Wb[s & 1];
+    cplx* Wn = Wb[(s + 1) & 1];
+    const cplx* y = yb[s & 1];
+    cplx* yn = yb[(s + 1) & 1];
+    {  // left: site lo + s, rows 0 .. s + 1 (row s + 1 new: row 0 with the site on 1)
+      const int i = lo + s, ke = j.dims[i], m2 = j.dims[i + 1];
+      for (int e = tid; e < (s + 2) * m2; e += kT) {
+        const int r = e / m2, c = e % m2, src = r == s + 1 ? 0 : r, t = r == s + 1 ? 1 : 0;
+        cplx acc = aqc::cmk(0, 0);
+        for (int l = 0; l < ke; ++l) acc = aqc::cfma(W[(size_t)src * cap + l], site_a(j.gam, j.lam, cap, i, t, l, c), acc);
+        Wn[(size_t)r * cap + c] = acc;
+      }
+    }
+    {  // right: site hi - s, y' = A[0] y
+      const int i = hi - s, ke = j.dims[i + 1], m2 = j.dims[i];
+      for (int l = wave; l < m2; l += kT / 64) {  // (uniform per wave)
+        cplx acc = aqc::cmk(0, 0);
+        for (int c = lane; c < ke; c += 64) acc = aqc::cfma(site_a(j.gam, j.lam, cap, i, 0, l, c), y[c], acc);
+        acc.x = wave_sum_d(acc.x);
+        acc.y = wave_sum_d(acc.y);
+        if (lane == 0) yn[l] = acc;
+      }
+    }
+    __syncthreads();
+  }
+  const cplx* W = Wb[w & 1];  // rows at bond hi + 1: 0 = u, 1 + (k - lo) = window flips
+  const cplx* y = yb[w & 1];  // at bond lo
+  const int dl = j.dims[lo], dr = j.dims[hi + 1];
+  // dot products: wave per output, lanes along the bond; output 0 = <0|psi>, 1 + k = amp_k
+  const int nout = j.amps ? n + 1 : 1;
+  for (int o = wave; o < nout; o += kT / 64) {  // (uniform per wave)
+    const int k = o - 1;
+    const cplx* a;
+    const cplx* b;
+    int d;
+    if (o == 0) a = W, b = j.nr, d = dr;
+    else if (k < lo) a = j.ml + (size_t)(1 + k) * cap, b = y, d = dl;
+    else if (k <= hi) a = W + (size_t)(1 + k - lo) * cap, b = j.nr, d = dr;
+    else a = W, b = j.nr + (size_t)(1 + k) * cap, d = dr;
+    cplx acc = aqc::cmk(0, 0);
+    for (int c = lane; c < d; c += 64) acc = aqc::cfma(a[c], b[c], acc);
+    acc.x = wave_sum_d(acc.x);
+    acc.y = wave_sum_d(acc.y);
+    if (lane == 0) {
+      if (o == 0) j.ov[0] = acc;
+      else j.amps[k] = acc;
+    }
+  }
+}
+
 // Transfer-matrix environments of <a|b> (one workgroup per chain):
 //   left : E_{i+1}[ra][rb] = sum_s sum_{la,lb} conj(A_i[s][la][ra]) E_i[la][lb] B_i[s][lb][rb]
 //   right: E_i[la][lb]     = sum_s sum_{ra,rb} conj(A_i[s][la][ra]) B_i[s][lb][rb] E_{i+1}[ra][rb]
@@ -2325,7 +2480,7 @@ int aqc_mps_create(int n, int chi_cap, double threshold, int max_chi, aqc_mps_t*
   AQC_HIP_CHECK(hipGetDevice(&h->dev));
   h->d.n = n;
   h->d.cap = chi_cap;
-  h->zr = n;
+  h->zr = h->hr = h->h0r = n;
   h->thr = threshold;
   h->max_chi = max_chi;
   h->order.resize(n);
@@ -2392,6 +2547,7 @@ int aqc_mps_destroy(aqc_mps_t h) {
   aqc::dev_free(h->d.env);
   aqc::dev_free(h->gw);
   aqc::dev_free(h->zenv);
+  aqc::dev_free(h->hwenv);
   for (auto& sl : h->slots) {
     aqc::dev_free(sl.theta);
     aqc::dev_free(sl.work);
@@ -2915,6 +3071,156 @@ int aqc_mps_amps_hw1_batch(aqc_mps_t* hs, int ns, double* out) {
   AQC_CHECK_LAUNCH();
   AQC_HIP_CHECK(hipMemcpyAsync(out, dres[dev], need * sizeof(cplx), hipMemcpyDeviceToHost, st));
   AQC_HIP_CHECK(hipStreamSynchronize(st));
+  return AQC_OK;
+}
+
+/* <psi|0..0> (out_ov, 2 doubles per state, as aqc_mps_overlap_zero_batch) and, when out_amps is
+   not null, the amplitudes <e_i|psi> (2 n doubles per state, as aqc_mps_amps_hw1_batch) of every
+   state (sorted first): a state copied from `base` while base has not changed since contracts only
+   the sites it rewrote against rows cached on base; any other state (or a window too wide for the
+   LDS) takes the full chains. */
+int aqc_mps_zero_hw1_batch(aqc_mps_t base, aqc_mps_t* hs, int ns, double* out_ov, double* out_amps) {
+  AQC_REQUIRE(base && hs && ns >= 0 && (out_ov || ns == 0), "aqc_mps_zero_hw1_batch: bad arguments");
+  if (ns == 0) return AQC_OK;
+  const int n = base->d.n, cap = base->d.cap;
+  for (int s = 0; s < ns; ++s)
+    AQC_REQUIRE(hs[s] && hs[s] != base && hs[s]->d.n == n && hs[s]->d.cap == cap,
+                "aqc_mps_zero_hw1_batch: every state needs base's n and capacity (and is not base)");
+  int rc = aqc_mps_sort_batch(hs, ns);
+  if (rc != AQC_OK) return rc;
+  constexpr size_t kWinLds = 128 * 1024;
+  std::vector<int> win, lo(ns), hi(ns), fb;
+  int need_l = 0, need_r = n;
+  for (int s = 0; s < ns; ++s) {
+    const aqc_mps_s* h = hs[s];
+    const bool ok = h->synced_src == base->uid && h->synced_ver == base->version;
+    lo[s] = h->dirty_hi >= h->dirty_lo ? h->dirty_lo : 0;
+    hi[s] = h->dirty_hi >= h->dirty_lo ? h->dirty_hi : 0;
+    const size_t lds = (2 * (size_t)(hi[s] - lo[s] + 2) + 2) * cap * sizeof(cplx);
+    if (!ok || lds > kWinLds) {
+      fb.push_back(s);
+      continue;
+    }
+    need_l = std::max(need_l, lo[s]);
+    need_r = std::min(need_r, hi[s] + 1);
+    win.push_back(s);
+  }
+  hipStream_t st = aqc::mps_stream();
+  const size_t blk = (size_t)(n + 1) * cap;
+  if (!win.empty()) {
+    if (!base->hwenv) {
+      base->hwenv = (cplx*)aqc::dev_alloc(2 * (size_t)(n + 1) * blk * sizeof(cplx));
+      AQC_REQUIRE(base->hwenv, "aqc_mps_zero_hw1_batch: out of device memory");
+      AQC_HIP_CHECK(hipMemsetAsync(base->hwenv, 0, 2 * (size_t)(n + 1) * blk * sizeof(cplx), st));
+      const double one = 1.0;
+      AQC_HIP_CHECK(hipMemcpyAsync(base->hwenv, &one, sizeof(double), hipMemcpyHostToDevice, st));
+      AQC_HIP_CHECK(hipMemcpyAsync(base->hwenv + (size_t)(n + 1) * blk + (size_t)n * blk, &one, sizeof(double),
+                                   hipMemcpyHostToDevice, st));
+      AQC_HIP_CHECK(hipStreamSynchronize(st));  // (the host constant's copies)
+      base->hl = base->h0l = 0;
+      base->hr = base->h0r = n;
+    }
+    cplx* HL = base->hwenv;
+    cplx* HR = base->hwenv + (size_t)(n + 1) * blk;
+    std::vector<HwRowsJob> rj;
+    const int full = out_amps ? 1 : 0;
+    auto rows_job = [&](int dir, int first, int nsteps, cplx* rows) {
+      HwRowsJob j;
+      j.gam = base->d.gam;
+      j.lam = base->d.lam;
+      j.dims = base->d.dims;
+      j.n = n;
+      j.cap = cap;
+      j.dir = dir;
+      j.first = first;
+      j.nsteps = nsteps;
+      j.full = full;
+      j.rows = rows;
+      rj.push_back(j);
+    };
+    // (the amplitudes need every row; the overlap alone row 0)
+    const int hl = full ? base->hl : base->h0l, hr = full ? base->hr : base->h0r;
+    if (need_l > hl) rows_job(0, hl, need_l - hl, HL);
+    if (need_r < hr) rows_job(1, hr - 1, hr - need_r, HR);
+    std::vector<HwWinJob> wj;
+    const size_t jb = ((rj.size() * sizeof(HwRowsJob) + 255) / 256) * 256;
+    const size_t wb = ((win.size() * sizeof(HwWinJob) + 255) / 256) * 256;
+    const size_t rb = (size_t)win.size() * (n + 1) * sizeof(cplx);
+    char* d = (char*)aqc::dev_alloc(jb + wb + rb + 256);
+    AQC_REQUIRE(d, "aqc_mps_zero_hw1_batch: out of device memory");
+    cplx* res = (cplx*)(d + jb + wb);
+    size_t lds_max = 0;
+    for (size_t k = 0; k < win.size(); ++k) {
+      const int s = win[k];
+      HwWinJob j;
+      j.gam = hs[s]->d.gam;
+      j.lam = hs[s]->d.lam;
+      j.dims = hs[s]->d.dims;
+      j.n = n;
+      j.cap = cap;
+      j.lo = lo[s];
+      j.hi = hi[s];
+      j.ml = HL + (size_t)lo[s] * blk;
+      j.nr = HR + (size_t)(hi[s] + 1) * blk;
+      j.ov = res + k * (n + 1);
+      j.amps = out_amps ? res + k * (n + 1) + 1 : nullptr;
+      wj.push_back(j);
+      lds_max = std::max(lds_max, (2 * (size_t)(hi[s] - lo[s] + 2) + 2) * cap * sizeof(cplx));
+    }
+    if (!rj.empty()) AQC_HIP_CHECK(hipMemcpyAsync(d, rj.data(), rj.size() * sizeof(HwRowsJob), hipMemcpyHostToDevice, st));
+    AQC_HIP_CHECK(hipMemcpyAsync(d + jb, wj.data(), wj.size() * sizeof(HwWinJob), hipMemcpyHostToDevice, st));
+    if (!rj.empty()) {
+      hipLaunchKernelGGL(k_hw_rows, dim3((unsigned)rj.size(), full ? kHwRowsG : 1), dim3(kT), 0, st, (const HwRowsJob*)d);
+      AQC_CHECK_LAUNCH();
+    }
+    static bool attr = false;
+    if (!attr) {
+      AQC_HIP_CHECK(hipFuncSetAttribute((const void*)k_hw_win, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kWinLds));
+      attr = true;
+    }
+    aqc::KernelTimer::begin(st, "mps_zero_hw1", 0.0, 0.0);
+    hipLaunchKernelGGL(k_hw_win, dim3((unsigned)win.size()), dim3(kT), lds_max, st, (const HwWinJob*)(d + jb));
+    aqc::KernelTimer::end(st);
+    AQC_CHECK_LAUNCH();
+    std::vector<cplx> h(win.size() * (n + 1));
+    AQC_HIP_CHECK(hipMemcpyAsync(h.data(), res, h.size() * sizeof(cplx), hipMemcpyDeviceToHost, st));
+    AQC_HIP_CHECK(hipStreamSynchronize(st));
+    aqc::dev_free(d);
+    base->h0l = std::max(base->h0l, need_l);
+    base->h0r = std::min(base->h0r, need_r);
+    if (full) {
+      base->hl = std::max(hl, need_l);
+      base->hr = std::min(hr, need_r);
+    }
+    for (size_t k = 0; k < win.size(); ++k) {
+      const int s = win[k];
+      const cplx* v = h.data() + k * (n + 1);
+      out_ov[2 * s] = v[0].x;  // mps_dot(psi, zero) = conj(amplitude of |0..0>)
+      out_ov[2 * s + 1] = -v[0].y;
+      if (out_amps)
+        for (int q = 0; q < n; ++q) {
+          out_amps[((size_t)s * n + q) * 2] = v[1 + q].x;
+          out_amps[((size_t)s * n + q) * 2 + 1] = v[1 + q].y;
+        }
+    }
+  }
+  if (!fb.empty()) {  // the full chains
+    std::vector<aqc_mps_t> fh;
+    for (int s : fb) fh.push_back(hs[s]);
+    std::vector<double> o(2 * fb.size()), a(out_amps ? 2 * fb.size() * n : 0);
+    rc = aqc_mps_overlap_zero_batch(fh.data(), (int)fh.size(), o.data());
+    if (rc != AQC_OK) return rc;
+    if (out_amps) {
+      rc = aqc_mps_amps_hw1_batch(fh.data(), (int)fh.size(), a.data());
+      if (rc != AQC_OK) return rc;
+    }
+    for (size_t k = 0; k < fb.size(); ++k) {
+      const int s = fb[k];
+      out_ov[2 * s] = o[2 * k];
+      out_ov[2 * s + 1] = o[2 * k + 1];
+      if (out_amps) std::memcpy(out_amps + (size_t)s * 2 * n, a.data() + k * 2 * n, 2 * n * sizeof(double));
+    }
+  }
   return AQC_OK;
 }
 

@@ -271,21 +271,31 @@ struct aqc_mps_s {
   // environments up to bond lo and the right ones from bond hi + 1 as they were.
   aqc::cplx* zenv = nullptr;
   int zl = 0, zr = 1 << 30;
+  // Cached zero / Hamming-weight-1 rows (mps.hip, aqc_mps_zero_hw1_batch), per bond b: from the
+  // left <0..0| A_0 .. A_{b-1} (row 0) and the same with site k < b flipped (row 1 + k); from the
+  // right A_b .. A_{n-1} |0..0> (row 0) and with site k >= b flipped (row 1 + k).  Every row is
+  // current for bonds <= hl (left) and >= hr (right), row 0 for bonds <= h0l / >= h0r.
+  aqc::cplx* hwenv = nullptr;
+  int hl = 0, hr = 1 << 30, h0l = 0, h0r = 1 << 30;
   void changed(int lo, int hi) {  // Gamma sites lo..hi rewritten
     ++version;
     dirty_lo = lo < dirty_lo ? lo : dirty_lo;
     dirty_hi = hi > dirty_hi ? hi : dirty_hi;
     zl = lo < zl ? lo : zl;
     zr = hi + 1 > zr ? hi + 1 : zr;
+    hl = lo < hl ? lo : hl;
+    hr = hi + 1 > hr ? hi + 1 : hr;
+    h0l = lo < h0l ? lo : h0l;
+    h0r = hi + 1 > h0r ? hi + 1 : h0r;
   }
   void changed_all() {
     ++version;
     synced_src = 0;
     zenv_stale();
   }
-  void zenv_stale() {  // every cached environment past the boundaries
-    zl = 0;
-    zr = d.n;
+  void zenv_stale() {  // every cached environment and row past the boundaries
+    zl = hl = h0l = 0;
+    zr = hr = h0r = d.n;
   }
   // the one device block the handle's fixed buffers are carved from (aqc::dev_alloc)
   void* base = nullptr;

@@ -303,6 +303,22 @@ def z_sum_batch(base, states):
     return out
 
 
+def zero_hw1_batch(base, states, amps=False):
+    """(<psi|0..0> per state, and with ``amps`` the amplitudes <e_i|psi> as rows) through
+    aqc_mps_zero_hw1_batch: states copied from ``base`` (unchanged since) contract only the sites
+    they rewrote, against rows cached on ``base``."""
+    ns = len(states)
+    ov = np.zeros(2 * ns)
+    a = np.zeros(2 * ns * (states[0].n if ns else 0)) if amps else None
+    if ns:
+        _lib.check(_lib.lib().aqc_mps_zero_hw1_batch(base.h, _handles(states), ns, _lib.ptr(ov),
+                                                     _lib.ptr(a) if amps else None))
+    ovc = ov[0::2] + 1j * ov[1::2]
+    if not amps:
+        return ovc, None
+    return ovc, (a[0::2] + 1j * a[1::2]).reshape(ns, -1)
+
+
 def amps_hw1_batch(states):
     """Amplitudes <e_i|psi> of every state (rows, complex), one set of launches
     (aqc_mps_amps_hw1_batch)."""

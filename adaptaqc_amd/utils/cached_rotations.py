@@ -27,13 +27,14 @@ candidates differ in one single-qubit gate, so:
 * MPS, global cost: truncation makes chi = S^dag|0> differ from the forward replay the
   reference does, so only the prefix is cached (the MPS after the gates before the varied
   one, which is what every replay computes first) and the candidates replay the suffix together
-  in lock-step batched launches (aqc_mps_copy_batch / apply_batch / overlap_zero_batch).
+  in lock-step batched launches (aqc_mps_copy_batch / apply_batch), then <0|psi> of each through
+  the sites it rewrote against rows cached on the prefix (aqc_mps_zero_hw1_batch).
 * MPS, local cost (0.5 (1 - mean <Z_i>), aer_mps_backend.py:72-74, 80-86) or softened global cost
   (1 - |<0|psi>|^2 - alpha sum_i |<e_i|psi>|^2, :49-70): the same prefix batch, then every
   candidate's sum of <Z_i> (aqc_mps_z_sum_batch: a candidate differs from the prefix only on the
   sites its gate, the suffix and the sort rewrote, so it contracts those against environments of
-  sum_i Z_i cached on the prefix) or HW-1 amplitudes (aqc_mps_amps_hw1_batch) in one set of
-  launches.
+  sum_i Z_i cached on the prefix) or HW-1 amplitudes (aqc_mps_zero_hw1_batch, the same window
+  against the prefix's Hamming-weight-1 rows) in one set of launches.
 * Statevector, local cost (aer_sv_backend.py:32-35, 49-59): no transition shortcut (every <Z_i> of
   every candidate); the prefix state is cached and the candidates replay the suffix from it.
   The softened cost raises on the statevector backend, as in the reference (generic path).
@@ -46,7 +47,7 @@ import numpy as np
 from .. import gates as G
 from .._lib import OP_DTYPE, ops_array
 from ..circuit import device_ops, device_ops_rows
-from ..device import DeviceSV, amps_hw1_batch, apply_batch, copy_batch, overlap_zero_batch, z_sum_batch
+from ..device import DeviceSV, apply_batch, copy_batch, z_sum_batch, zero_hw1_batch
 
 
 class _View:
@@ -196,11 +197,12 @@ class MPSPrefixBatch(_SweepBase):
             # against the prefix's cached environments (aqc_mps_z_sum_batch)
             n = circ.num_qubits
             return [float(0.5 * (1 - t / n)) for t in z_sum_batch(self.phi, states)]
-        ov = overlap_zero_batch(states)
+        # <0|psi> (and the softened cost's <e_i|psi>) likewise through the rewritten sites against
+        # rows cached on the prefix (aqc_mps_zero_hw1_batch)
+        ov, amps = zero_hw1_batch(self.phi, states, amps=self.kind == "soft")
         costs = [float(1.0 - abs(v) ** 2) for v in ov]
         if self.kind == "soft":
             alpha = _soften_alpha(self.compiler)
-            amps = amps_hw1_batch(states)
             costs = [c - alpha * float(np.sum(np.abs(a) ** 2)) for c, a in zip(costs, amps)]
         return costs
 

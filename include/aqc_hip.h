@@ -160,6 +160,13 @@ int aqc_mps_amps_hw1_batch(aqc_mps_t* hs, int nstates, double* out);
    as base changes: the Rotoselect prefix of cost_minimiser.py:318-368); any other state takes the
    full chains of z_all_batch.  base itself is not modified and must not be among hs. */
 int aqc_mps_z_sum_batch(aqc_mps_t base, aqc_mps_t* hs, int nstates, double* out);
+/* <psi|0..0> (out_ov: 2 doubles per state, as aqc_mps_overlap_zero_batch) and, when out_amps is not
+   null, <e_i|psi> (2 n doubles per state, as aqc_mps_amps_hw1_batch) -- the global and softened
+   costs (aer_mps_backend.py:49-70, 88-93) of a Rotoselect gate's candidates: a state copied from
+   `base` while base has not changed since contracts only the sites it rewrote, against zero and
+   Hamming-weight-1 rows cached on base; any other state takes the full chains.  base is not
+   modified and must not be among hs. */
+int aqc_mps_zero_hw1_batch(aqc_mps_t base, aqc_mps_t* hs, int nstates, double* out_ov, double* out_amps);
 
 /* ---- candidate sweep: replaces gradients.py:23-124 ------------------------------ */
 /* For every pair (pairs[2p], pairs[2p+1]) = (control, target):

@@ -317,8 +317,11 @@ def test_reference_rotoselect_batched_mps(rotoselect):
             assert ins.operation.name == w[0], (k, ins.operation.name, w[0])
             if ins.operation.params:  # (angles compared modulo 2 pi: +-pi is one rotation up to phase)
                 qp = runs["per_candidate"][0].data[1 + k].operation
-                assert _angle_gap(float(ins.operation.params[0]), float(qp.params[0])) < 1e-9
-                if amps[r] > 1e-7:  # (an angle the cost does not depend on is rounding noise)
+                # (an angle the cost does not depend on is rounding noise: the batched costs are
+                # contracted through the rewritten window, the per-candidate ones over every site,
+                # so their last bits differ)
+                if amps[r] > 1e-7:
+                    assert _angle_gap(float(ins.operation.params[0]), float(qp.params[0])) < 1e-9, (k, amps[r])
                     assert _angle_gap(float(ins.operation.params[0]), w[2][0]) < 1e-6 / amps[r] + 1e-6
                 r += 1
     print(f"\nper gate: reference CostMinimiser batched {1e3 * t_b / n_rot:.2f} ms, per-candidate "
@@ -423,8 +426,8 @@ def test_reference_rotoselect_batched_mps_local_and_softened(kind):
             assert ins.operation.name == w[0], (k, ins.operation.name, w[0])
             if ins.operation.params:
                 qp = runs["per_candidate"][0].data[1 + k].operation
-                assert _angle_gap(float(ins.operation.params[0]), float(qp.params[0])) < 1e-9
-                if amps[r] > 1e-7:
+                if amps[r] > 1e-7:  # (as above: a cost-independent angle is rounding noise)
+                    assert _angle_gap(float(ins.operation.params[0]), float(qp.params[0])) < 1e-9, (k, amps[r])
                     assert _angle_gap(float(ins.operation.params[0]), w[2][0]) < 1e-6 / amps[r] + 1e-6
                 r += 1
     t_g = runs["global"][3]

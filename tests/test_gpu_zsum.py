@@ -3,7 +3,8 @@ sites they rewrote since their copy from the prefix state, against environment p
 sum_i Z_i cached on the prefix (ent.hip k_zenv / k_zsum).  Checked against the full chains
 (aqc_mps_z_all_batch, itself pinned to the oracle's full contraction) and, for a few states, against
 the oracle directly; the cache is checked as the prefix changes (its pairs stay current only outside
-the rewritten sites)."""
+the rewritten sites).  The same for <psi|0> and <e_i|psi> through a window (aqc_mps_zero_hw1_batch,
+mps.hip k_hw_rows / k_hw_win) against the full chains and the oracle."""
 
 import numpy as np
 import pytest
@@ -136,3 +137,67 @@ def test_z_sum_timeout_reruns_single_workgroup():
     _lib.check(lib.aqc_env_fallbacks(ctypes.byref(cnt)))
     assert cnt.value >= 1
     np.testing.assert_allclose(sums[1], sums[0], atol=1e-12)
+
+
+@pytest.mark.parametrize("cap", [16, 64, 100, 256])
+def test_zero_hw1_windows_vs_full_chains(cap):
+    """aqc_mps_zero_hw1_batch: <psi|0> and every <e_i|psi> of the same candidate set as the Z-sum
+    test (one-qubit, adjacent, routed, edge, empty and whole-chain windows, a state not copied from
+    the prefix) against the full chains (overlap_zero_batch / amps_hw1_batch) at 1e-12, while the
+    prefix changes (a gate inside, one at the right edge, a reload); the overlap alone (amps=False)
+    the same."""
+    import bench
+    from adaptaqc_amd.device import DeviceMPS, amps_hw1_batch, copy_batch, overlap_zero_batch, zero_hw1_batch
+
+    n = 14
+    rng = np.random.default_rng(100 + cap)
+    bond = min(cap, 48)
+    base = DeviceMPS(n, cap, 1e-16, cap)
+    base.load_aer(bench.random_vidal_mps(n, bond, 700 + cap))
+    other = DeviceMPS(n, cap, 1e-16, cap)
+    other.load_aer(bench.random_vidal_mps(n, bond, 750 + cap))
+    cands = [DeviceMPS(n, cap, 1e-16, cap) for _ in range(6)]
+
+    def check(tag):
+        lists = _windows(n, rng)
+        copy_batch(cands, [base] * len(cands))
+        for d, ops in zip(cands, lists):
+            d.apply(_dops(n, ops))
+        states = cands + [other]
+        ov2, none = zero_hw1_batch(base, states)  # (row 0 first: the full rows then start behind it)
+        assert none is None
+        ov, amps = zero_hw1_batch(base, states, amps=True)
+        np.testing.assert_allclose(ov, overlap_zero_batch(states), atol=1e-12, err_msg=tag)
+        np.testing.assert_allclose(ov2, ov, atol=1e-14, err_msg=tag)
+        np.testing.assert_allclose(amps, amps_hw1_batch(states), atol=1e-12, err_msg=tag)
+
+    check("fresh cache")
+    base.apply(_dops(n, _layer(rng, [4, 5]) + [("cx", (4, 5), ())]))
+    check("prefix changed on sites 4-5")
+    base.apply(_dops(n, [("cx", (n - 2, n - 1), ())] + _layer(rng, [n - 1])))
+    check("prefix changed at the right edge")
+    base.load_aer(bench.random_vidal_mps(n, bond, 790 + cap))
+    check("prefix reloaded")
+
+
+def test_zero_hw1_truncating_candidates_vs_oracle():
+    """Truncating candidates (max_chi 8): <psi|0> and <e_i|psi> against the oracle's contractions of
+    each candidate's read-back state at 1e-12."""
+    import bench
+    from adaptaqc_amd.device import DeviceMPS, copy_batch, zero_hw1_batch
+
+    n, chi = 12, 8
+    rng = np.random.default_rng(5)
+    base = DeviceMPS(n, 64, 1e-16, chi)
+    base.load_aer(bench.random_vidal_mps(n, chi, 79))
+    cands = [DeviceMPS(n, 64, 1e-16, chi) for _ in range(4)]
+    copy_batch(cands, [base] * 4)
+    for k, d in enumerate(cands):
+        a = 1 + 2 * k
+        d.apply(_dops(n, _layer(rng, [a, a + 1]) + [("cx", (a, a + 1), ())] + _layer(rng, [a]) + [("cx", (a + 1, a), ())]))
+    ov, amps = zero_hw1_batch(base, cands, amps=True)
+    for k, d in enumerate(cands):
+        pre = d.preprocessed()
+        assert abs(ov[k] - M.mps_dot(pre, M.zero_mps(n))) < 1e-12
+        want = [M.extract_amplitude(pre, 2 ** i) for i in range(n)]
+        np.testing.assert_allclose(amps[k], want, atol=1e-12)
