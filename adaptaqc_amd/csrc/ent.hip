@@ -519,7 +519,8 @@ __global__ __launch_bounds__(256) void k_env64(const RdmJob* __restrict__ jobs, 
 // Tr(L_b RZ_b) at any bond b.  A Rotoselect candidate is a copy of the prefix state rewritten only
 // on sites lo..hi (its gate, the suffix and the final sort: the handle's reload bookkeeping), so its
 // sum needs the prefix's pairs at bonds lo and hi + 1 (cached on the prefix handle and extended as
-// it changes) and its own left chain through lo..hi only -- instead of both full chains per
+// it changes) and its own chains through lo..hi only (from both ends, meeting in the middle:
+// Tr(LZ R) + Tr(L RZ) holds at any bond) -- instead of both full chains per
 // candidate.  A step is k_env_split's with the environment rows doubled: GEMM 1 takes [E; EZ]
 // (2 ke rows) against the site's columns, GEMM 2 writes E' to output columns [0, cw) and EZ' to
 // [cw, 2 cw), reading T_E for the first and T_EZ + z_t T_E for the second.
@@ -1309,10 +1310,17 @@ int aqc_mps_z_sum_batch(aqc_mps_t base, aqc_mps_t* hs, int ns, double* out) {
     if (need_l > zl) job(base, 0, zl, need_l - zl, ZL + (size_t)zl * pair, ZL + (size_t)(zl + 1) * pair);
     if (need_r < zr) job(base, 1, zr - 1, zr - need_r, ZR + (size_t)zr * pair, ZR + (size_t)(zr - 1) * pair);
     const int nbase = (int)jobs.size();
-    // launch 2: each state's left chain through its window, from base's pair at bond lo
+    // launch 2: each state's window from both ends -- a left chain from base's pair at bond lo
+    // through the first half, a right chain from base's pair at bond hi + 1 through the rest --
+    // meeting at bond lo + nl
     size_t wsteps = 0;
-    for (int s : win) wsteps += (size_t)(hi[s] - lo[s] + 1);
-    const int nch = nbase + (int)win.size();
+    int nwin_ch = 0;
+    for (int s : win) {
+      const int w = hi[s] - lo[s] + 1, nl = (w + 1) / 2;
+      wsteps += (size_t)w;
+      nwin_ch += 1 + (w > nl ? 1 : 0);
+    }
+    const int nch = nbase + nwin_ch;
     const size_t jb = ((nch * sizeof(ZJob) + 255) / 256) * 256;
     const size_t zb = ((win.size() * sizeof(ZSumJob) + 255) / 256) * 256;
     const size_t ob = ((win.size() * sizeof(double) + 255) / 256) * 256;
@@ -1334,15 +1342,21 @@ int aqc_mps_z_sum_batch(aqc_mps_t base, aqc_mps_t* hs, int ns, double* out) {
     std::vector<ZSumJob> sums;
     size_t woff = 0;
     for (int s : win) {
-      const int steps = hi[s] - lo[s] + 1;
-      cplx* eo = wbuf + woff * pair;
-      job(hs[s], 0, lo[s], steps, ZL + (size_t)lo[s] * pair, eo);
-      woff += (size_t)steps;
+      const int w = hi[s] - lo[s] + 1, nl = (w + 1) / 2, ny = w - nl;
+      cplx* el = wbuf + woff * pair;
+      job(hs[s], 0, lo[s], nl, ZL + (size_t)lo[s] * pair, el);
+      woff += (size_t)nl;
       ZSumJob z;
-      z.lp = eo + (size_t)(steps - 1) * pair;
+      z.lp = el + (size_t)(nl - 1) * pair;
       z.rp = ZR + (size_t)(hi[s] + 1) * pair;
+      if (ny > 0) {  // (right chains store downwards: step k at er + (ny - 1 - k) pair)
+        cplx* er = wbuf + woff * pair;
+        job(hs[s], 1, hi[s], ny, ZR + (size_t)(hi[s] + 1) * pair, er + (size_t)(ny - 1) * pair);
+        woff += (size_t)ny;
+        z.rp = er;
+      }
       z.dims = hs[s]->d.dims;
-      z.bond = hi[s] + 1;
+      z.bond = lo[s] + nl;
       z.cap = cap;
       sums.push_back(z);
     }
@@ -1357,7 +1371,7 @@ int aqc_mps_z_sum_batch(aqc_mps_t base, aqc_mps_t* hs, int ns, double* out) {
         rc = launch_zenv(dj, nbase, cap, st, cnt, err, attempt > 0);
         if (rc != AQC_OK) return rc;
       }
-      rc = launch_zenv(dj + nbase, (int)win.size(), cap, st, cnt + (size_t)nbase * 32, err, attempt > 0);
+      rc = launch_zenv(dj + nbase, nwin_ch, cap, st, cnt + (size_t)nbase * 32, err, attempt > 0);
       if (rc != AQC_OK) return rc;
       hipLaunchKernelGGL(k_zsum, dim3((unsigned)win.size()), dim3(kT), 0, st, dz, dout);
       aqc::KernelTimer::end(st);

@@ -1501,12 +1501,55 @@ __global__ __launch_bounds__(kT) void k_hw1(const MeasJob* __restrict__ jobs) {
 // (all sites on 0), row 1 + k = the same with site k < b on 1; from the right: row 0 =
 // A_b .. A_{n-1} |0..0>, row 1 + k = with site k >= b on 1.  A Rotoselect candidate differs from
 // the prefix only on the sites lo..hi it rewrote, so with the prefix's left rows at bond lo (Ml) and
-// right rows at bond hi + 1 (Nr), cached on the prefix handle:
-//   u   = Ml[0] W (W: the window's A[0] product; rows for the window's own flips alongside),
-//   y   = W Nr[0]  (the window from the right),
-//   <0|psi> = u . Nr[0];  amp_k = Ml[1 + k] . y (k < lo), Wrow[1 + k] . Nr[0] (lo <= k <= hi),
-//   u . Nr[1 + k] (k > hi)
-// -- a window of w sites costs w small vector steps instead of two n-step chains.
+// right rows at bond hi + 1 (Nr), cached on the prefix handle, and the candidate's own row-0
+// vectors through the window, u_b (from Ml[0], bonds lo .. hi + 1) and y_b (from Nr[0], bonds
+// hi + 1 .. lo):
+//   <0|psi> = u_b . y_b (any window bond: the two chains meet in the middle when only it is asked)
+//   amp_k   = Ml[1 + k] . y_lo (k < lo),  u_k A_k[1] y_{k+1} (lo <= k <= hi),  u_{hi+1} . Nr[1 + k] (k > hi)
+// -- w small vector steps per candidate instead of two n-step chains and n closings.
+//
+// One vector step for up to kHwR vectors at once (the same site): left out_r[c] = sum_l v_r[l] A_t[l][c],
+// right out_r[l] = sum_c A_t[l][c] v_r[c].  The four waves split the contraction, lanes run over
+// 64 outputs, partial sums meet in the LDS (two barriers per 64 outputs); t = 1 for the rows
+// flagged in newmask (the flipped site), A_0 otherwise.  src(r, k), dst(r, x, value).
+constexpr int kHwR = 8;
+template <typename FS, typename FD>
+__device__ __forceinline__ void hw_step(const cplx* gam, const double* lam, int cap, int i, bool right, int nrows,
+                                        unsigned newmask, int ke, int m2, FS src, FD dst, cplx (*part)[kHwR][64]) {
+  const int q = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const size_t cc = (size_t)cap * cap;
+  const cplx* g = gam + (size_t)i * 2 * cc;
+  const double* lm = lam + (size_t)(i + 1) * cap;
+  for (int x0 = 0; x0 < m2; x0 += 64) {
+    const int x = x0 + lane;
+    cplx acc[kHwR];
+#pragma unroll
+    for (int r = 0; r < kHwR; ++r) acc[r] = aqc::cmk(0, 0);
+    if (x < m2) {
+      for (int k = q; k < ke; k += 4) {
+        // A_t[l][c] = Gamma_t[l][c] lambda_{i+1}[c]: left (l, c) = (k, x), right (x, k)
+        const size_t o = right ? (size_t)x * cap + k : (size_t)k * cap + x;
+        const double lv = lm[right ? k : x];
+        const cplx a0 = aqc::cscale(g[o], lv);
+        const cplx a1 = newmask ? aqc::cscale(g[cc + o], lv) : a0;
+#pragma unroll
+        for (int r = 0; r < kHwR; ++r)
+          if (r < nrows) acc[r] = aqc::cfma(src(r, k), (newmask >> r) & 1 ? a1 : a0, acc[r]);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < kHwR; ++r)
+      if (r < nrows) part[q][r][lane] = acc[r];
+    __syncthreads();
+    for (int e = threadIdx.x; e < nrows * 64; e += kT) {
+      const int r = e >> 6, ln = e & 63;
+      if (x0 + ln < m2)
+        dst(r, x0 + ln, aqc::cadd(aqc::cadd(part[0][r][ln], part[1][r][ln]), aqc::cadd(part[2][r][ln], part[3][r][ln])));
+    }
+    __syncthreads();
+  }
+}
+
 struct HwRowsJob {
   const cplx* gam;
   const double* lam;
@@ -1519,17 +1562,17 @@ struct HwRowsJob {
 
 // The prefix's rows.  grid (directions, G): with `full`, workgroup g owns the flip rows 1 + k with
 // k % G == g (each an independent chain once created) and every workgroup carries row 0 itself
-// (in its LDS; workgroup 0 stores it), so the workgroups never wait on each other -- a step's rows
-// of a 50-site chain on one CU's FP64 rate were ~5 us.  Every bond has its own block, written once
-// per launch and read by the next step only (no stale L1 line).  Waves over output rows, lanes
-// over the output's bond index.
+// (workgroup 0 stores it), so the workgroups never wait on each other.  Every bond has its own
+// block, written once per launch and read by the next step only (no stale L1 line); row 0 is also
+// kept in the LDS.
 constexpr int kHwRowsG = 8;
 __global__ __launch_bounds__(kT) void k_hw_rows(const HwRowsJob* __restrict__ jobs) {
   const HwRowsJob& j = jobs[blockIdx.x];
   const int n = j.n, cap = j.cap, g = blockIdx.y, G = gridDim.y;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const size_t blk = (size_t)(n + 1) * cap;
-  __shared__ cplx v0[2][kMaxCap];  // row 0, this workgroup's copy
+  extern __shared__ cplx hw_lds[];
+  cplx* v0[2] = {hw_lds, hw_lds + cap};  // row 0, this workgroup's copy
+  cplx (*part)[kHwR][64] = reinterpret_cast<cplx (*)[kHwR][64]>(hw_lds + 2 * cap);
   {
     const int b = j.dir == 0 ? j.first : j.first + 1, d = j.dims[b];
     for (int e = threadIdx.x; e < d; e += kT) v0[0][e] = j.rows[(size_t)b * blk + e];
@@ -1537,40 +1580,41 @@ __global__ __launch_bounds__(kT) void k_hw_rows(const HwRowsJob* __restrict__ jo
   __syncthreads();
   for (int s = 0; s < j.nsteps; ++s) {
     const int i = j.dir == 0 ? j.first + s : j.first - s;
-    const int ke = j.dir == 0 ? j.dims[i] : j.dims[i + 1], m2 = j.dir == 0 ? j.dims[i + 1] : j.dims[i];
-    const cplx* M = j.rows + (size_t)(j.dir == 0 ? i : i + 1) * blk;
-    cplx* O = j.rows + (size_t)(j.dir == 0 ? i + 1 : i) * blk;
+    const bool right = j.dir != 0;
+    const int ke = right ? j.dims[i + 1] : j.dims[i], m2 = right ? j.dims[i] : j.dims[i + 1];
+    const cplx* M = j.rows + (size_t)(right ? i + 1 : i) * blk;
+    cplx* O = j.rows + (size_t)(right ? i : i + 1) * blk;
     const cplx* v = v0[s & 1];
     cplx* vn = v0[(s + 1) & 1];
-    // this workgroup's rows: ridx 0 = row 0; then the old flip rows k (left: k < i, right: k > i)
-    // with k % G == g; then the new row 1 + i if i % G == g
-    int k0, nold;
-    if (!j.full) k0 = 0, nold = 0;
-    else if (j.dir == 0) k0 = g, nold = i > g ? (i - g + G - 1) / G : 0;
-    else {
-      k0 = i + 1 + ((g - (i + 1) % G) % G + G) % G;
-      nold = k0 < n ? (n - 1 - k0) / G + 1 : 0;
-    }
-    const int nnew = j.full && i % G == g ? 1 : 0, nr = 1 + nold + nnew;
-    for (int ridx = wave; ridx < nr; ridx += kT / 64) {  // (uniform per wave)
-      int row, t;
-      const cplx* src;
-      if (ridx == 0) row = 0, t = 0, src = v;
-      else if (ridx <= nold) row = 1 + k0 + G * (ridx - 1), t = 0, src = M + (size_t)row * cap;
-      else row = 1 + i, t = 1, src = v;
-      for (int c0 = 0; c0 < m2; c0 += 64) {
-        const int c = c0 + lane;
-        if (c >= m2) continue;
-        cplx acc = aqc::cmk(0, 0);
-        if (j.dir == 0)  // O[row][c] = sum_l src[l] A_t[l][c]
-          for (int l = 0; l < ke; ++l) acc = aqc::cfma(src[l], site_a(j.gam, j.lam, cap, i, t, l, c), acc);
-        else  // O[row][c] = sum_r A_t[c][r] src[r]
-          for (int r = 0; r < ke; ++r) acc = aqc::cfma(site_a(j.gam, j.lam, cap, i, t, c, r), src[r], acc);
-        if (ridx == 0) vn[c] = acc;
-        if (ridx != 0 || g == 0) O[(size_t)row * cap + c] = acc;
+    // this workgroup's rows: 0; the old flip rows k (left: k < i, right: k > i) with k % G == g;
+    // the new row 1 + i (from row 0 with the site on 1) when i % G == g
+    int k0 = 0, nold = 0;
+    if (j.full) {
+      if (!right) nold = i > g ? (i - g + G - 1) / G : 0, k0 = g;
+      else {
+        k0 = i + 1 + ((g - (i + 1) % G) % G + G) % G;
+        nold = k0 < n ? (n - 1 - k0) / G + 1 : 0;
       }
     }
-    __syncthreads();
+    const int nnew = j.full && i % G == g ? 1 : 0, nr = 1 + nold + nnew;
+    // row list position p: 0 = row 0, 1 .. nold = old rows, nold + 1 = the new row
+    auto row_of = [&](int p) { return p == 0 ? 0 : (p <= nold ? 1 + k0 + G * (p - 1) : 1 + i); };
+    for (int p0 = 0; p0 < nr; p0 += kHwR) {
+      const int cnt = min(kHwR, nr - p0);
+      const unsigned nm = (nnew && nr - 1 >= p0 && nr - 1 < p0 + cnt) ? 1u << (nr - 1 - p0) : 0u;
+      hw_step(
+          j.gam, j.lam, cap, i, right, cnt, nm, ke, m2,
+          [&](int r, int k) {
+            const int p = p0 + r;
+            return (p == 0 || p == nold + 1) ? v[k] : M[(size_t)row_of(p) * cap + k];
+          },
+          [&](int r, int x, cplx val) {
+            const int p = p0 + r;
+            if (p == 0) vn[x] = val;
+            if (p != 0 || g == 0) O[(size_t)row_of(p) * cap + x] = val;
+          },
+          part);
+    }
   }
 }
 
@@ -1583,64 +1627,89 @@ struct HwWinJob {
   const cplx* nr;  // prefix's right rows at bond hi + 1
   cplx* ov;        // <0..0|psi> (the amplitude; the host conjugates for mps_dot(psi, zero))
   cplx* amps;      // n amplitudes, or nullptr
+  cplx* uy;        // with amps: u_b at uy + (b - lo) cap, y_b at uy + (w + 1 + b - lo) cap
 };
 
-// one workgroup per state; dynamic LDS: W rows (ping-pong, 2 (w + 1) cap) and y (2 cap)
+// One workgroup per state.  Dynamic LDS: u and y (2 x 2 cap) and the step partials.  With amps
+// the vectors of every window bond go to the global scratch (each written once, read after the
+// chain: no stale L1 line).
 __global__ __launch_bounds__(kT) void k_hw_win(const HwWinJob* __restrict__ jobs) {
   const HwWinJob& j = jobs[blockIdx.x];
   extern __shared__ cplx hw_lds[];
   const int cap = j.cap, n = j.n, lo = j.lo, hi = j.hi, w = hi - lo + 1;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  cplx* Wb[2] = {hw_lds, hw_lds + (size_t)(w + 1) * cap};
-  cplx* yb[2] = {hw_lds + 2 * (size_t)(w + 1) * cap, hw_lds + 2 * (size_t)(w + 1) * cap + cap};
+  cplx* ub[2] = {hw_lds, hw_lds + cap};
+  cplx* yb[2] = {hw_lds + 2 * cap, hw_lds + 3 * cap};
+  cplx (*part)[kHwR][64] = reinterpret_cast<cplx (*)[kHwR][64]>(hw_lds + 4 * cap);
+  const bool amps = j.amps != nullptr;
+  // u through sites lo .. lo + nl - 1 (bond lo -> lo + nl), y through hi .. hi - ny + 1 (bond
+  // hi + 1 -> hi + 1 - ny); without amplitudes they meet at bond lo + nl
+  const int nl = amps ? w : (w + 1) / 2, ny = amps ? w : w - nl;
+  cplx* U = j.uy;
+  cplx* Y = j.uy + (size_t)(w + 1) * cap;
   {
     const int dl = j.dims[lo], dr = j.dims[hi + 1];
-    for (int e = tid; e < dl; e += kT) Wb[0][e] = j.ml[e];
-    for (int e = tid; e < dr; e += kT) yb[0][e] = j.nr[e];
+    for (int e = tid; e < dl; e += kT) {
+      ub[0][e] = j.ml[e];
+      if (amps) U[e] = j.ml[e];
+    }
+    for (int e = tid; e < dr; e += kT) {
+      yb[0][e] = j.nr[e];
+      if (amps) Y[(size_t)w * cap + e] = j.nr[e];
+    }
   }
   __syncthreads();
-  for (int s = 0; s < w; ++s) {
-    const cplx* W = Wb[s & 1];
-    cplx* Wn = Wb[(s + 1) & 1];
-    const cplx* y = yb[s & 1];
-    cplx* yn = yb[(s + 1) & 1];
-    {  // left: site lo + s, rows 0 .. s + 1 (row s + 1 new: row 0 with the site on 1)
-      const int i = lo + s, ke = j.dims[i], m2 = j.dims[i + 1];
-      for (int e = tid; e < (s + 2) * m2; e += kT) {
-        const int r = e / m2, c = e % m2, src = r == s + 1 ? 0 : r, t = r == s + 1 ? 1 : 0;
-        cplx acc = aqc::cmk(0, 0);
-        for (int l = 0; l < ke; ++l) acc = aqc::cfma(W[(size_t)src * cap + l], site_a(j.gam, j.lam, cap, i, t, l, c), acc);
-        Wn[(size_t)r * cap + c] = acc;
-      }
+  for (int s = 0; s < max(nl, ny); ++s) {
+    if (s < nl) {
+      const int i = lo + s;
+      const cplx* u = ub[s & 1];
+      cplx* un = ub[(s + 1) & 1];
+      hw_step(j.gam, j.lam, cap, i, false, 1, 0u, j.dims[i], j.dims[i + 1], [&](int, int k) { return u[k]; },
+              [&](int, int x, cplx v) {
+                un[x] = v;
+                if (amps) U[(size_t)(s + 1) * cap + x] = v;
+              },
+              part);
     }
-    {  // right: site hi - s, y' = A[0] y
-      const int i = hi - s, ke = j.dims[i + 1], m2 = j.dims[i];
-      for (int l = wave; l < m2; l += kT / 64) {  // (uniform per wave)
-        cplx acc = aqc::cmk(0, 0);
-        for (int c = lane; c < ke; c += 64) acc = aqc::cfma(site_a(j.gam, j.lam, cap, i, 0, l, c), y[c], acc);
-        acc.x = wave_sum_d(acc.x);
-        acc.y = wave_sum_d(acc.y);
-        if (lane == 0) yn[l] = acc;
-      }
+    if (s < ny) {
+      const int i = hi - s;
+      const cplx* y = yb[s & 1];
+      cplx* yn = yb[(s + 1) & 1];
+      hw_step(j.gam, j.lam, cap, i, true, 1, 0u, j.dims[i + 1], j.dims[i], [&](int, int k) { return y[k]; },
+              [&](int, int x, cplx v) {
+                yn[x] = v;
+                if (amps) Y[(size_t)(i - lo) * cap + x] = v;
+              },
+              part);
     }
-    __syncthreads();
   }
-  const cplx* W = Wb[w & 1];  // rows at bond hi + 1: 0 = u, 1 + (k - lo) = window flips
-  const cplx* y = yb[w & 1];  // at bond lo
+  const cplx* u = ub[nl & 1];  // at bond lo + nl
+  const cplx* y = yb[ny & 1];  // at bond hi + 1 - ny
   const int dl = j.dims[lo], dr = j.dims[hi + 1];
-  // dot products: wave per output, lanes along the bond; output 0 = <0|psi>, 1 + k = amp_k
-  const int nout = j.amps ? n + 1 : 1;
+  // closings, a wave per output, lanes along the bond: output 0 = <0|psi>, 1 + k = amp_k (with
+  // amps; window sites as u_k A_k[1] y_{k+1}: lanes along the right index, a loop over the left)
+  const int nout = amps ? n + 1 : 1;
   for (int o = wave; o < nout; o += kT / 64) {  // (uniform per wave)
     const int k = o - 1;
-    const cplx* a;
-    const cplx* b;
-    int d;
-    if (o == 0) a = W, b = j.nr, d = dr;
-    else if (k < lo) a = j.ml + (size_t)(1 + k) * cap, b = y, d = dl;
-    else if (k <= hi) a = W + (size_t)(1 + k - lo) * cap, b = j.nr, d = dr;
-    else a = W, b = j.nr + (size_t)(1 + k) * cap, d = dr;
     cplx acc = aqc::cmk(0, 0);
-    for (int c = lane; c < d; c += 64) acc = aqc::cfma(a[c], b[c], acc);
+    if (o == 0) {  // (with amps u is at bond hi + 1: against Nr[0]; else the chains' meeting bond)
+      const cplx* yy = amps ? j.nr : y;
+      const int d = j.dims[lo + nl];
+      for (int c = lane; c < d; c += 64) acc = aqc::cfma(u[c], yy[c], acc);
+    } else if (k < lo) {
+      for (int c = lane; c < dl; c += 64) acc = aqc::cfma(j.ml[(size_t)(1 + k) * cap + c], y[c], acc);
+    } else if (k > hi) {
+      for (int c = lane; c < dr; c += 64) acc = aqc::cfma(u[c], j.nr[(size_t)(1 + k) * cap + c], acc);
+    } else {
+      const cplx* uk = U + (size_t)(k - lo) * cap;
+      const cplx* yk = Y + (size_t)(k + 1 - lo) * cap;
+      const int kl = j.dims[k], kr = j.dims[k + 1];
+      for (int r = lane; r < kr; r += 64) {
+        cplx t = aqc::cmk(0, 0);
+        for (int l = 0; l < kl; ++l) t = aqc::cfma(uk[l], site_a(j.gam, j.lam, cap, k, 1, l, r), t);
+        acc = aqc::cfma(t, yk[r], acc);
+      }
+    }
     acc.x = wave_sum_d(acc.x);
     acc.y = wave_sum_d(acc.y);
     if (lane == 0) {
@@ -3088,7 +3157,6 @@ int aqc_mps_zero_hw1_batch(aqc_mps_t base, aqc_mps_t* hs, int ns, double* out_ov
                 "aqc_mps_zero_hw1_batch: every state needs base's n and capacity (and is not base)");
   int rc = aqc_mps_sort_batch(hs, ns);
   if (rc != AQC_OK) return rc;
-  constexpr size_t kWinLds = 128 * 1024;
   std::vector<int> win, lo(ns), hi(ns), fb;
   int need_l = 0, need_r = n;
   for (int s = 0; s < ns; ++s) {
@@ -3096,8 +3164,7 @@ int aqc_mps_zero_hw1_batch(aqc_mps_t base, aqc_mps_t* hs, int ns, double* out_ov
     const bool ok = h->synced_src == base->uid && h->synced_ver == base->version;
     lo[s] = h->dirty_hi >= h->dirty_lo ? h->dirty_lo : 0;
     hi[s] = h->dirty_hi >= h->dirty_lo ? h->dirty_hi : 0;
-    const size_t lds = (2 * (size_t)(hi[s] - lo[s] + 2) + 2) * cap * sizeof(cplx);
-    if (!ok || lds > kWinLds) {
+    if (!ok) {
       fb.push_back(s);
       continue;
     }
@@ -3145,11 +3212,14 @@ int aqc_mps_zero_hw1_batch(aqc_mps_t base, aqc_mps_t* hs, int ns, double* out_ov
     std::vector<HwWinJob> wj;
     const size_t jb = ((rj.size() * sizeof(HwRowsJob) + 255) / 256) * 256;
     const size_t wb = ((win.size() * sizeof(HwWinJob) + 255) / 256) * 256;
-    const size_t rb = (size_t)win.size() * (n + 1) * sizeof(cplx);
-    char* d = (char*)aqc::dev_alloc(jb + wb + rb + 256);
+    const size_t rb = (((size_t)win.size() * (n + 1) * sizeof(cplx)) + 255) / 256 * 256;
+    size_t uyb = 0;  // with amps: each state's window vectors (2 (w + 1) cap)
+    if (out_amps)
+      for (int s : win) uyb += 2 * (size_t)(hi[s] - lo[s] + 2) * cap * sizeof(cplx);
+    char* d = (char*)aqc::dev_alloc(jb + wb + rb + uyb + 256);
     AQC_REQUIRE(d, "aqc_mps_zero_hw1_batch: out of device memory");
     cplx* res = (cplx*)(d + jb + wb);
-    size_t lds_max = 0;
+    cplx* uy = (cplx*)(d + jb + wb + rb);
     for (size_t k = 0; k < win.size(); ++k) {
       const int s = win[k];
       HwWinJob j;
@@ -3164,22 +3234,27 @@ int aqc_mps_zero_hw1_batch(aqc_mps_t base, aqc_mps_t* hs, int ns, double* out_ov
       j.nr = HR + (size_t)(hi[s] + 1) * blk;
       j.ov = res + k * (n + 1);
       j.amps = out_amps ? res + k * (n + 1) + 1 : nullptr;
+      j.uy = out_amps ? uy : nullptr;
+      if (out_amps) uy += 2 * (size_t)(hi[s] - lo[s] + 2) * cap;
       wj.push_back(j);
-      lds_max = std::max(lds_max, (2 * (size_t)(hi[s] - lo[s] + 2) + 2) * cap * sizeof(cplx));
     }
+    const size_t lds_win = (4 * (size_t)cap + 4 * kHwR * 64) * sizeof(cplx);
+    const size_t lds_rows = (2 * (size_t)cap + 4 * kHwR * 64) * sizeof(cplx);
     if (!rj.empty()) AQC_HIP_CHECK(hipMemcpyAsync(d, rj.data(), rj.size() * sizeof(HwRowsJob), hipMemcpyHostToDevice, st));
     AQC_HIP_CHECK(hipMemcpyAsync(d + jb, wj.data(), wj.size() * sizeof(HwWinJob), hipMemcpyHostToDevice, st));
-    if (!rj.empty()) {
-      hipLaunchKernelGGL(k_hw_rows, dim3((unsigned)rj.size(), full ? kHwRowsG : 1), dim3(kT), 0, st, (const HwRowsJob*)d);
-      AQC_CHECK_LAUNCH();
-    }
     static bool attr = false;
-    if (!attr) {
-      AQC_HIP_CHECK(hipFuncSetAttribute((const void*)k_hw_win, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kWinLds));
+    if (!attr) {  // (up to 98 KB at capacity 1024)
+      AQC_HIP_CHECK(hipFuncSetAttribute((const void*)k_hw_win, hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024));
+      AQC_HIP_CHECK(hipFuncSetAttribute((const void*)k_hw_rows, hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024));
       attr = true;
     }
+    if (!rj.empty()) {
+      hipLaunchKernelGGL(k_hw_rows, dim3((unsigned)rj.size(), full ? kHwRowsG : 1), dim3(kT), lds_rows, st,
+                         (const HwRowsJob*)d);
+      AQC_CHECK_LAUNCH();
+    }
     aqc::KernelTimer::begin(st, "mps_zero_hw1", 0.0, 0.0);
-    hipLaunchKernelGGL(k_hw_win, dim3((unsigned)win.size()), dim3(kT), lds_max, st, (const HwWinJob*)(d + jb));
+    hipLaunchKernelGGL(k_hw_win, dim3((unsigned)win.size()), dim3(kT), lds_win, st, (const HwWinJob*)(d + jb));
     aqc::KernelTimer::end(st);
     AQC_CHECK_LAUNCH();
     std::vector<cplx> h(win.size() * (n + 1));
