@@ -1382,12 +1382,16 @@ __device__ __forceinline__ cplx site_a(const cplx* gam, const double* lam, int c
 }
 
 // <0...0|psi>: v <- v A_i[0] from the left.  One workgroup per state.
-__global__ __launch_bounds__(kT) void k_overlap_zero(const MeasJob* __restrict__ jobs) {
+// The running vectors in dynamic LDS sized by the batch's largest capacity (vc complex each): at
+// capacity-1024 static arrays (48 KB) three of the bench's four workgroups per CU fit and its 1024
+// states ran in two rounds (483 -> 761 us a launch).
+__global__ __launch_bounds__(kT) void k_overlap_zero(const MeasJob* __restrict__ jobs, int vc) {
   const MeasJob& j = jobs[blockIdx.x];
-  __shared__ cplx v[2][kMaxCap];
+  extern __shared__ cplx ovz_lds[];
+  
   __shared__ cplx part[4][256];
   const int tid = fresh_tid();
-  if (tid == 0) v[0][0] = aqc::cmk(1.0, 0.0);
+  if (tid == 0) ovz_lds[0] = aqc::cmk(1.0, 0.0);
   __syncthreads();
   int cur = 0;
   const int q = tid >> 6, lane = tid & 63;
@@ -1397,16 +1401,16 @@ __global__ __launch_bounds__(kT) void k_overlap_zero(const MeasJob* __restrict__
       const int r = r0 + lane;
       cplx acc = aqc::cmk(0, 0);
       if (r < cr)
-        for (int l = q; l < cl; l += 4) acc = aqc::cfma(v[cur][l], site_a(j.gam, j.lam, j.cap, i, 0, l, r), acc);
+        for (int l = q; l < cl; l += 4) acc = aqc::cfma(ovz_lds[cur * vc + l], site_a(j.gam, j.lam, j.cap, i, 0, l, r), acc);
       part[q][lane + 0] = acc;
       __syncthreads();
       if (q == 0 && r < cr)
-        v[cur ^ 1][r] = aqc::cadd(aqc::cadd(part[0][lane], part[1][lane]), aqc::cadd(part[2][lane], part[3][lane]));
+        ovz_lds[(cur ^ 1) * vc + r] = aqc::cadd(aqc::cadd(part[0][lane], part[1][lane]), aqc::cadd(part[2][lane], part[3][lane]));
       __syncthreads();
     }
     cur ^= 1;
   }
-  if (tid == 0) j.out[0] = v[cur][0];
+  if (tid == 0) j.out[0] = ovz_lds[cur * vc];
 }
 
 // Zero chains: vec[b] (left, bond b) = <0..0| A_0..A_{b-1};  vec[(n+1)+b] (right) = A_b..A_{n-1}|0..0>.
@@ -1415,15 +1419,16 @@ __global__ __launch_bounds__(kT) void k_overlap_zero(const MeasJob* __restrict__
 // (coalesced rows of A) and one wave sum per output row.  (Round 6: one thread per output entry
 // with the whole dot product and the vector in global memory, columns of A read with a cap stride,
 // made the softened-cost batch's HW-1 amplitudes ~2 ms a call.)
-__global__ __launch_bounds__(kT) void k_zero_chains(const MeasJob* __restrict__ jobs) {
+__global__ __launch_bounds__(kT) void k_zero_chains(const MeasJob* __restrict__ jobs, int vc) {
   const MeasJob& j = jobs[blockIdx.x];
   const int tid = fresh_tid(), q = tid >> 6, lane = tid & 63;
   const int cap = j.cap, n = j.n;
   cplx* L = j.vec;
   cplx* R = j.vec + (size_t)(n + 1) * cap;
-  __shared__ cplx v[2][kMaxCap];
+  extern __shared__ cplx ovz_lds[];  // (as k_overlap_zero)
+  
   __shared__ cplx part[4][64];
-  if (tid == 0) v[0][0] = aqc::cmk(1.0, 0.0);
+  if (tid == 0) ovz_lds[0] = aqc::cmk(1.0, 0.0);
   int cur = 0;
   if (blockIdx.y == 0) {
     if (tid == 0) L[0] = aqc::cmk(1.0, 0.0);
@@ -1434,12 +1439,12 @@ __global__ __launch_bounds__(kT) void k_zero_chains(const MeasJob* __restrict__ 
         const int r = r0 + lane;
         cplx acc = aqc::cmk(0, 0);
         if (r < cr)
-          for (int l = q; l < cl; l += 4) acc = aqc::cfma(v[cur][l], site_a(j.gam, j.lam, cap, i, 0, l, r), acc);
+          for (int l = q; l < cl; l += 4) acc = aqc::cfma(ovz_lds[cur * vc + l], site_a(j.gam, j.lam, cap, i, 0, l, r), acc);
         part[q][lane] = acc;
         __syncthreads();
         if (q == 0 && r < cr) {
           const cplx s = aqc::cadd(aqc::cadd(part[0][lane], part[1][lane]), aqc::cadd(part[2][lane], part[3][lane]));
-          v[cur ^ 1][r] = s;
+          ovz_lds[(cur ^ 1) * vc + r] = s;
           L[(size_t)(i + 1) * cap + r] = s;
         }
         __syncthreads();
@@ -1453,11 +1458,11 @@ __global__ __launch_bounds__(kT) void k_zero_chains(const MeasJob* __restrict__ 
       const int cl = j.dims[i], cr = j.dims[i + 1];
       for (int l = q; l < cl; l += 4) {  // (uniform per wave)
         cplx acc = aqc::cmk(0, 0);
-        for (int r = lane; r < cr; r += 64) acc = aqc::cfma(site_a(j.gam, j.lam, cap, i, 0, l, r), v[cur][r], acc);
+        for (int r = lane; r < cr; r += 64) acc = aqc::cfma(site_a(j.gam, j.lam, cap, i, 0, l, r), ovz_lds[cur * vc + r], acc);
         acc.x = wave_sum_d(acc.x);
         acc.y = wave_sum_d(acc.y);
         if (lane == 0) {
-          v[cur ^ 1][l] = acc;
+          ovz_lds[(cur ^ 1) * vc + l] = acc;
           R[(size_t)i * cap + l] = acc;
         }
       }
@@ -3082,7 +3087,9 @@ int aqc_mps_overlap_zero_batch(aqc_mps_t* hs, int ns, double* out) {
   double bytes = 0;
   for (int s = 0; s < ns; ++s) bytes += (double)hs[s]->d.n * hs[s]->d.cap * hs[s]->d.cap * 16.0;
   aqc::KernelTimer::begin(st, "mps_overlap0", bytes, bytes / 2.0);
-  hipLaunchKernelGGL(k_overlap_zero, dim3(ns), dim3(kT), 0, st, dj);
+  int vc = 1;
+  for (int s = 0; s < ns; ++s) vc = std::max(vc, hs[s]->d.cap);
+  hipLaunchKernelGGL(k_overlap_zero, dim3(ns), dim3(kT), 2 * vc * sizeof(cplx), st, dj, vc);
   aqc::KernelTimer::end(st);
   AQC_CHECK_LAUNCH();
   std::vector<cplx> v(ns);
@@ -3134,7 +3141,9 @@ int aqc_mps_amps_hw1_batch(aqc_mps_t* hs, int ns, double* out) {
   const MeasJob* dj = nullptr;
   rc = upload_jobs(jobs, &dj);
   if (rc != AQC_OK) return rc;
-  hipLaunchKernelGGL(k_zero_chains, dim3(ns, 2), dim3(kT), 0, st, dj);
+  int vc = 1;
+  for (int s = 0; s < ns; ++s) vc = std::max(vc, hs[s]->d.cap);
+  hipLaunchKernelGGL(k_zero_chains, dim3(ns, 2), dim3(kT), 2 * vc * sizeof(cplx), st, dj, vc);
   AQC_CHECK_LAUNCH();
   hipLaunchKernelGGL(k_hw1, dim3(n, ns), dim3(kT), 0, st, dj);
   AQC_CHECK_LAUNCH();
@@ -3308,7 +3317,7 @@ int aqc_mps_amps_hw1(aqc_mps_t h, double* out) {
   rc = upload_jobs(jobs, &dj);
   if (rc != AQC_OK) return rc;
   hipStream_t st = aqc::mps_stream();
-  hipLaunchKernelGGL(k_zero_chains, dim3(1, 2), dim3(kT), 0, st, dj);
+  hipLaunchKernelGGL(k_zero_chains, dim3(1, 2), dim3(kT), 2 * h->d.cap * sizeof(cplx), st, dj, h->d.cap);
   AQC_CHECK_LAUNCH();
   hipLaunchKernelGGL(k_hw1, dim3(h->d.n, 1), dim3(kT), 0, st, dj);
   AQC_CHECK_LAUNCH();

@@ -462,11 +462,15 @@ def main():
         if world > 1:
             dist.barrier()
 
+    step_marks = []  # host clock after each timed step (each step ends on the cost read-back)
+
     def timed(fn, k):
         barrier()
         t0 = time.perf_counter()
+        step_marks.clear()
         for _ in range(k):
             r = fn()
+            step_marks.append(time.perf_counter() - t0)
         barrier()
         el = time.perf_counter() - t0
         if world > 1:
@@ -631,6 +635,7 @@ def main():
                                 else f"pairs sharded x{world}"),
             },
             "breakdown_ms": {f: round(v["ms"] / args.steps, 3) for f, v in fams.items()},
+            "step_ms": [round(1e3 * (b - a), 3) for a, b in zip([0.0] + step_marks[:-1], step_marks)],
             "by_kind": {
                 "gradient_evals_per_s": grad_rate, "overlap_evals_per_s": ov_rate,
                 "reference_mix_evals_per_s": ref_mix,

@@ -1,0 +1,9 @@
+#!/bin/bash
+# round 6 (resumed): GPU suite at HEAD, kernel-trace stats of the bench, the full bench line
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out
+timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/r6c22_tests.log 2>&1 || exit $?
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r6c22_kt -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-parity --no-latency > gpurun_out/r6c22_ktrace_bench.json 2> gpurun_out/r6c22_ktrace.err || exit $?
+python3 tools/rocpd_stats.py gpurun_out/r6c22_kt/run_results.db > gpurun_out/r6c22_kernel_stats.csv; rm -rf gpurun_out/r6c22_kt
+timeout -k 10 400 python3 bench.py > gpurun_out/r6c22_bench.json 2> gpurun_out/r6c22_bench.err || exit $?
