@@ -328,6 +328,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=4.0, help="seconds per CPU-baseline leg")
     ap.add_argument("--cpu-workers", type=int, default=0, help="0: min(16, OMP_NUM_THREADS or cores)")
+    ap.add_argument("--cpu-settle", type=float, default=0.0, help="seconds of idle after the CPU-baseline leg")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--no-latency", action="store_true")
     ap.add_argument("--no-pipeline", action="store_true",
@@ -357,6 +358,8 @@ def main():
         cpu = cpu_baselines(args.cpu_budget, workers)
         cpu["workers"] = workers
         cpu["host"] = host_description(workers)
+        if args.cpu_settle > 0:  # let the host's clocks recover before the GPU leg's host-side work
+            time.sleep(args.cpu_settle)
 
     import torch
     import torch.distributed as dist
@@ -486,6 +489,7 @@ def main():
     _lib.timing_enable(True)
     _lib.gram_stats()  # reset the Gram-path counters
     elapsed, (full, best, costs) = timed(step, args.steps)
+    main_step_s = list(step_marks)
     _lib.timing_enable(False)
     gram = _lib.gram_stats()
     if world > 1:
@@ -635,7 +639,7 @@ def main():
                                 else f"pairs sharded x{world}"),
             },
             "breakdown_ms": {f: round(v["ms"] / args.steps, 3) for f, v in fams.items()},
-            "step_ms": [round(1e3 * (b - a), 3) for a, b in zip([0.0] + step_marks[:-1], step_marks)],
+            "step_ms": [round(1e3 * (b - a), 3) for a, b in zip([0.0] + main_step_s[:-1], main_step_s)],
             "by_kind": {
                 "gradient_evals_per_s": grad_rate, "overlap_evals_per_s": ov_rate,
                 "reference_mix_evals_per_s": ref_mix,
