@@ -28,7 +28,7 @@ EXPORTS = (
     "aqc_sv_amp0", "aqc_sv_z_all", "aqc_sv_get", "aqc_sv_set",
     "aqc_mps_create", "aqc_mps_destroy", "aqc_mps_set_truncation", "aqc_mps_set_vidal",
     "aqc_mps_get_vidal", "aqc_mps_get_dims", "aqc_mps_copy", "aqc_mps_copy_batch", "aqc_mps_apply",
-    "aqc_mps_apply_batch", "aqc_mps_apply_sort_batch", "aqc_mps_apply_sort_batch_async", "aqc_mps_check_batch", "aqc_mps_sort", "aqc_mps_sort_batch", "aqc_mps_overlap_zero",
+    "aqc_mps_apply_batch", "aqc_mps_apply_sort_batch", "aqc_mps_apply_sort_batch_async", "aqc_mps_apply_batch_async", "aqc_mps_check_batch", "aqc_mps_sort", "aqc_mps_sort_batch", "aqc_mps_overlap_zero",
     "aqc_mps_overlap_zero_batch", "aqc_mps_dot", "aqc_mps_z_all", "aqc_mps_amps_hw1", "aqc_mps_z_all_batch", "aqc_mps_z_sum_batch", "aqc_mps_zero_hw1_batch",
     "aqc_mps_amps_hw1_batch",
     "aqc_pair_grads", "aqc_pair_grads_batch", "aqc_argmax_scaled", "aqc_argmax_scaled_batch", "aqc_mps_jacobi_stats",
@@ -87,6 +87,7 @@ _SIGS = {
     "aqc_mps_apply_batch": ([_P, _I, _P, _P], _I),
     "aqc_mps_apply_sort_batch": ([_P, _I, _P, _P], _I),
     "aqc_mps_apply_sort_batch_async": ([_P, _I, _P, _P], _I),
+    "aqc_mps_apply_batch_async": ([_P, _I, _P, _P], _I),
     "aqc_mps_check_batch": ([_P, _I], _I),
     "aqc_mps_sort": ([_P], _I),
     "aqc_mps_sort_batch": ([_P, _I], _I),

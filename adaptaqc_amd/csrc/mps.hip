@@ -3049,6 +3049,10 @@ int aqc_mps_apply_sort_batch_async(aqc_mps_t* hs, int ns, const aqc_op_t* const*
   return apply_batch_impl(hs, ns, ops, nops, true, false);
 }
 
+int aqc_mps_apply_batch_async(aqc_mps_t* hs, int ns, const aqc_op_t* const* ops, const int* nops) {
+  return apply_batch_impl(hs, ns, ops, nops, false, false);
+}
+
 int aqc_mps_check_batch(aqc_mps_t* hs, int ns) {
   AQC_REQUIRE(hs && ns >= 0, "aqc_mps_check_batch: null argument");
   for (int s = 0; s < ns; ++s) AQC_REQUIRE(hs[s], "aqc_mps_check_batch: null handle");
@@ -3249,8 +3253,26 @@ int aqc_mps_zero_hw1_batch(aqc_mps_t base, aqc_mps_t* hs, int ns, double* out_ov
     }
     const size_t lds_win = (4 * (size_t)cap + 4 * kHwR * 64) * sizeof(cplx);
     const size_t lds_rows = (2 * (size_t)cap + 4 * kHwR * 64) * sizeof(cplx);
-    if (!rj.empty()) AQC_HIP_CHECK(hipMemcpyAsync(d, rj.data(), rj.size() * sizeof(HwRowsJob), hipMemcpyHostToDevice, st));
-    AQC_HIP_CHECK(hipMemcpyAsync(d + jb, wj.data(), wj.size() * sizeof(HwWinJob), hipMemcpyHostToDevice, st));
+    // the job arrays through a pinned staging set of the ring (pageable copies were a host round
+    // trip each, between the candidates' replay and these kernels)
+    StagingLease lease(st);
+    if (lease.rc() != AQC_OK) {
+      aqc::dev_free(d);
+      return lease.rc();
+    }
+    rc = ensure_staging(lease.buf(), jb + wb);
+    if (rc != AQC_OK) {
+      aqc::dev_free(d);
+      return rc;
+    }
+    char* hj = (char*)lease.buf().host;
+    char* dj = (char*)lease.buf().dev;
+    if (!rj.empty()) std::memcpy(hj, rj.data(), rj.size() * sizeof(HwRowsJob));
+    std::memcpy(hj + jb, wj.data(), wj.size() * sizeof(HwWinJob));
+    if (int e = aqc::upload_async(dj, hj, jb + wb, st)) {
+      aqc::dev_free(d);
+      return e;
+    }
     static bool attr = false;
     if (!attr) {  // (up to 98 KB at capacity 1024)
       AQC_HIP_CHECK(hipFuncSetAttribute((const void*)k_hw_win, hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024));
@@ -3259,11 +3281,11 @@ int aqc_mps_zero_hw1_batch(aqc_mps_t base, aqc_mps_t* hs, int ns, double* out_ov
     }
     if (!rj.empty()) {
       hipLaunchKernelGGL(k_hw_rows, dim3((unsigned)rj.size(), full ? kHwRowsG : 1), dim3(kT), lds_rows, st,
-                         (const HwRowsJob*)d);
+                         (const HwRowsJob*)dj);
       AQC_CHECK_LAUNCH();
     }
     aqc::KernelTimer::begin(st, "mps_zero_hw1", 0.0, 0.0);
-    hipLaunchKernelGGL(k_hw_win, dim3((unsigned)win.size()), dim3(kT), lds_win, st, (const HwWinJob*)(d + jb));
+    hipLaunchKernelGGL(k_hw_win, dim3((unsigned)win.size()), dim3(kT), lds_win, st, (const HwWinJob*)(dj + jb));
     aqc::KernelTimer::end(st);
     AQC_CHECK_LAUNCH();
     std::vector<cplx> h(win.size() * (n + 1));

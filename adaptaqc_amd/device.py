@@ -232,19 +232,17 @@ def apply_batch(states, ops_lists, sort=False, wait=True):
     """Apply per-state op lists (one batched launch sequence, or one fused chain per state); with
     sort=True every state also returns to sorted qubit order in the same schedule (an evaluation's
     replay + save).  ops_lists: a list of op lists / ops arrays, or an OpsBatch.  wait=False
-    (sort=True only) returns once the work is queued; call check_batch(states) before using the
-    states."""
+    returns once the work is queued; call check_batch(states) before trusting the states (their
+    error flags are read there)."""
     if not states:
         return
     l = _lib.lib()
     batch = ops_lists if isinstance(ops_lists, OpsBatch) else OpsBatch(ops_lists)
     if len(batch) != len(states):
         raise ValueError("apply_batch: one op list per state")
-    if not wait and not sort:
-        raise ValueError("apply_batch: wait=False needs sort=True")
     fn = l.aqc_mps_apply_sort_batch if sort else l.aqc_mps_apply_batch
     if not wait:
-        fn = l.aqc_mps_apply_sort_batch_async
+        fn = l.aqc_mps_apply_sort_batch_async if sort else l.aqc_mps_apply_batch_async
     _lib.check(fn(_handles(states), len(states), batch.ptrs, _lib.ptr(batch.counts)))
 
 

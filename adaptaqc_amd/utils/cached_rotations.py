@@ -47,7 +47,7 @@ import numpy as np
 from .. import gates as G
 from .._lib import OP_DTYPE, ops_array
 from ..circuit import device_ops, device_ops_rows
-from ..device import DeviceSV, apply_batch, copy_batch, z_sum_batch, zero_hw1_batch
+from ..device import DeviceSV, apply_batch, check_batch, copy_batch, z_sum_batch, zero_hw1_batch
 
 
 class _View:
@@ -172,12 +172,19 @@ class MPSPrefixBatch(_SweepBase):
         base, start = self.backend.ensure_base(circ)
         if self.phi is None or self.phi.chi_cap != base.chi_cap:
             self.phi, self.pos = self.backend.new_state(), None
+        # the prefix's advance is queued (aqc_mps_apply_batch_async); its error flags are read with
+        # the candidates' after their costs (costs() always follows goto()), so a gate costs one
+        # host wait instead of three
         if self.pos is None or index < self.pos:
             self.phi.copy_from(base)
-            self.phi.apply(device_ops_rows(circ, start, index))
+            self._advance(device_ops_rows(circ, start, index))
         elif index > self.pos:
-            self.phi.apply(device_ops_rows(circ, self.pos, index))
+            self._advance(device_ops_rows(circ, self.pos, index))
         self.pos = index
+
+    def _advance(self, rows):
+        if len(rows):
+            apply_batch([self.phi], [rows], wait=False)
 
     def _costs(self, index, mats):
         circ = self.compiler.full_circuit
@@ -191,15 +198,19 @@ class MPSPrefixBatch(_SweepBase):
         states = self.backend.scratch_states(len(mats))
         copy_batch(states, [self.phi] * len(mats))
         lists = [np.frombuffer(cand[i * size:(i + 1) * size] + suffix, dtype=OP_DTYPE) for i in range(len(mats))]
-        apply_batch(states, lists, sort=True)
+        # queued; the prefix's and the candidates' error flags are read after the costs' read-back
+        apply_batch(states, lists, sort=True, wait=False)
         if self.kind == "local":
             # only sum_i <Z_i> enters the cost: each candidate contracts the sites it rewrote
             # against the prefix's cached environments (aqc_mps_z_sum_batch)
             n = circ.num_qubits
-            return [float(0.5 * (1 - t / n)) for t in z_sum_batch(self.phi, states)]
+            zs = z_sum_batch(self.phi, states)
+            check_batch([self.phi] + states)
+            return [float(0.5 * (1 - t / n)) for t in zs]
         # <0|psi> (and the softened cost's <e_i|psi>) likewise through the rewritten sites against
         # rows cached on the prefix (aqc_mps_zero_hw1_batch)
         ov, amps = zero_hw1_batch(self.phi, states, amps=self.kind == "soft")
+        check_batch([self.phi] + states)
         costs = [float(1.0 - abs(v) ** 2) for v in ov]
         if self.kind == "soft":
             alpha = _soften_alpha(self.compiler)

@@ -112,6 +112,9 @@ int aqc_mps_apply_sort_batch(aqc_mps_t* hs, int nstates, const aqc_op_t* const* 
    (capacity, Jacobi sweep limit) are not read back -- call aqc_mps_check_batch before using the
    results.  Lets the host prepare further work (the candidate sweep) while the chain runs. */
 int aqc_mps_apply_sort_batch_async(aqc_mps_t* hs, int nstates, const aqc_op_t* const* ops, const int* nops);
+/* As aqc_mps_apply_batch (no sort), returning once the work is queued; flags as above.  The
+   cached Rotoselect evaluator advances its prefix with it (one host wait per gate instead of three). */
+int aqc_mps_apply_batch_async(aqc_mps_t* hs, int nstates, const aqc_op_t* const* ops, const int* nops);
 /* Wait for the states' queued work and report their error flags (AQC_ERR_STATE etc.). */
 int aqc_mps_check_batch(aqc_mps_t* hs, int nstates);
 /* ---- ISL entanglement sweep (adapt_compiler.py:955-976 -> entanglement_measures.py:39-98) ----
