@@ -1633,63 +1633,211 @@ struct HwWinJob {
   cplx* ov;        // <0..0|psi> (the amplitude; the host conjugates for mps_dot(psi, zero))
   cplx* amps;      // n amplitudes, or nullptr
   cplx* uy;        // with amps: u_b at uy + (b - lo) cap, y_b at uy + (w + 1 + b - lo) cap
+  cplx* fin;       // the two chains' last vectors (2 cap): u at fin, y at fin + cap
+  int* cnt;        // the job's hand-off counter (0 at launch)
+  int pad;
 };
 
-// One workgroup per state.  Dynamic LDS: u and y (2 x 2 cap) and the step partials.  With amps
-// the vectors of every window bond go to the global scratch (each written once, read after the
-// chain: no stale L1 line).
+// Vectors handed between the two chains' workgroups (possibly on different XCDs): agent-scope
+// stores and loads, as the environment chains' hand-offs (ent.hip)
+typedef __attribute__((address_space(1))) double win_gdbl;
+__device__ __forceinline__ void win_st(cplx* p, cplx v) {
+  win_gdbl* q = (win_gdbl*)(double*)p;
+  __hip_atomic_store(q, v.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(q + 1, v.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ cplx win_ld(const cplx* p) {
+  win_gdbl* q = (win_gdbl*)(double*)p;
+  return aqc::cmk(__hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                  __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
+// One window step with the running vector v in the LDS (out in the LDS too, and to `store` when
+// not null).  Left (site i, bond i -> i + 1): out[x] = sum_k v[k] A_i[0][k][x] -- lanes along x
+// (coalesced rows of Gamma), the four waves splitting k, partial sums through the LDS.  Right (bond
+// i + 1 -> i): out[x] = sum_k A_i[0][x][k] v[k] -- lanes along k (coalesced rows again), four
+// outputs per wave in flight, wave sums.  A = Gamma lambda_{i+1}.
+__device__ __forceinline__ void win_step(const cplx* __restrict__ gam, const double* __restrict__ lam, int cap, int i,
+                                         bool right, int ke, int m2, const cplx* v, cplx* out, cplx* store,
+                                         cplx (*part)[64]) {
+  const int q = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const cplx* g = gam + (size_t)i * 2 * cap * cap;
+  const double* lm = lam + (size_t)(i + 1) * cap;
+  if (!right) {
+    for (int x0 = 0; x0 < m2; x0 += 64) {
+      const int x = x0 + lane;
+      cplx acc = aqc::cmk(0, 0);
+      if (x < m2) {
+        int k = q;
+        for (; k + 12 < ke; k += 16) {  // four rows' loads issued together
+          cplx a[4];
+#pragma unroll
+          for (int t = 0; t < 4; ++t) a[t] = g[(size_t)(k + 4 * t) * cap + x];
+#pragma unroll
+          for (int t = 0; t < 4; ++t) acc = aqc::cfma(v[k + 4 * t], a[t], acc);
+        }
+        for (; k < ke; k += 4) acc = aqc::cfma(v[k], g[(size_t)k * cap + x], acc);
+        acc = aqc::cscale(acc, lm[x]);
+      }
+      part[q][lane] = acc;
+      __syncthreads();
+      if (q == 0 && x < m2) {
+        const cplx r = aqc::cadd(aqc::cadd(part[0][lane], part[1][lane]), aqc::cadd(part[2][lane], part[3][lane]));
+        out[x] = r;
+        if (store) win_st(store + x, r);
+      }
+      __syncthreads();
+    }
+  } else {
+    for (int x0 = 4 * q; x0 < m2; x0 += 16) {  // (uniform per wave)
+      cplx acc[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc[t] = aqc::cmk(0, 0);
+      for (int k = lane; k < ke; k += 64) {
+        const cplx vk = aqc::cscale(v[k], lm[k]);
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+          if (x0 + t < m2) acc[t] = aqc::cfma(g[(size_t)(x0 + t) * cap + k], vk, acc[t]);
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        acc[t].x = wave_sum_d(acc[t].x);
+        acc[t].y = wave_sum_d(acc[t].y);
+      }
+      if (lane < 4 && x0 + lane < m2) {
+        const cplx r = lane == 0 ? acc[0] : lane == 1 ? acc[1] : lane == 2 ? acc[2] : acc[3];
+        out[x0 + lane] = r;
+        if (store) win_st(store + x0 + lane, r);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// Two workgroups per state (blockIdx.y): the left chain u through sites lo .. lo + nl - 1 (bond lo
+// -> lo + nl) and the right chain y through hi .. hi - ny + 1 (bond hi + 1 -> hi + 1 - ny) run side
+// by side; without amplitudes they meet at bond lo + nl, with them both run the whole window.
+// Each writes its last vector to fin; the second to finish (the job's counter) closes: <0|psi> =
+// u . y and, with amps, the window's amplitudes from the bond vectors in uy (every vector written
+// once to global memory before the hand-off, read after it).  Dynamic LDS: two vectors (2 cap)
+// and the step partials.  (One workgroup running the two chains one step after the other: ~190 us
+// a launch in the paper-setting layer, lanes strided by cap on the right chain's rows.)
 __global__ __launch_bounds__(kT) void k_hw_win(const HwWinJob* __restrict__ jobs) {
   const HwWinJob& j = jobs[blockIdx.x];
+  const int side = blockIdx.y;
   extern __shared__ cplx hw_lds[];
   const int cap = j.cap, n = j.n, lo = j.lo, hi = j.hi, w = hi - lo + 1;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  cplx* ub[2] = {hw_lds, hw_lds + cap};
-  cplx* yb[2] = {hw_lds + 2 * cap, hw_lds + 3 * cap};
-  cplx (*part)[kHwR][64] = reinterpret_cast<cplx (*)[kHwR][64]>(hw_lds + 4 * cap);
+  cplx* vb[2] = {hw_lds, hw_lds + cap};
+  cplx (*part)[64] = reinterpret_cast<cplx (*)[64]>(hw_lds + 2 * cap);
   const bool amps = j.amps != nullptr;
-  // u through sites lo .. lo + nl - 1 (bond lo -> lo + nl), y through hi .. hi - ny + 1 (bond
-  // hi + 1 -> hi + 1 - ny); without amplitudes they meet at bond lo + nl
   const int nl = amps ? w : (w + 1) / 2, ny = amps ? w : w - nl;
   cplx* U = j.uy;
   cplx* Y = j.uy + (size_t)(w + 1) * cap;
+  const int steps = side == 0 ? nl : ny;
   {
-    const int dl = j.dims[lo], dr = j.dims[hi + 1];
-    for (int e = tid; e < dl; e += kT) {
-      ub[0][e] = j.ml[e];
-      if (amps) U[e] = j.ml[e];
-    }
-    for (int e = tid; e < dr; e += kT) {
-      yb[0][e] = j.nr[e];
-      if (amps) Y[(size_t)w * cap + e] = j.nr[e];
+    const int d0 = side == 0 ? j.dims[lo] : j.dims[hi + 1];
+    const cplx* src = side == 0 ? j.ml : j.nr;
+    cplx* st0 = amps ? (side == 0 ? U : Y + (size_t)w * cap) : nullptr;
+    for (int e = tid; e < d0; e += kT) {
+      vb[0][e] = src[e];
+      if (st0) win_st(st0 + e, src[e]);
     }
   }
   __syncthreads();
-  for (int s = 0; s < max(nl, ny); ++s) {
-    if (s < nl) {
-      const int i = lo + s;
-      const cplx* u = ub[s & 1];
-      cplx* un = ub[(s + 1) & 1];
-      hw_step(j.gam, j.lam, cap, i, false, 1, 0u, j.dims[i], j.dims[i + 1], [&](int, int k) { return u[k]; },
-              [&](int, int x, cplx v) {
-                un[x] = v;
-                if (amps) U[(size_t)(s + 1) * cap + x] = v;
-              },
-              part);
+  if (cap <= 64) {
+    // capacity <= 64: a step's whole 64 x 64 tile is 16 entries per thread, all loaded at once --
+    // and the next step's issued before this step's products (the tiles do not depend on the
+    // running vector), so a step waits on no global load.  Left: thread (q, x) holds A[q + 4t][x];
+    // right: thread (q, k) holds A[q + 4t][k] (rows along the lanes either way: coalesced), its 16
+    // products reduced over k through the LDS (red, 64 x 65).
+    cplx (*red)[65] = reinterpret_cast<cplx (*)[65]>(hw_lds + 2 * cap + 4 * 64);
+    auto site_of = [&](int s) { return side == 0 ? lo + s : hi - s; };
+    auto fetch = [&](int s, cplx (&a)[16]) {
+      const int i = site_of(s);
+      const int rows = side == 0 ? j.dims[i] : j.dims[i];      // A's row count (left: k; right: x)
+      const int cols = side == 0 ? j.dims[i + 1] : j.dims[i + 1];
+      const cplx* g = j.gam + (size_t)i * 2 * cap * cap;
+#pragma unroll
+      for (int t = 0; t < 16; ++t) {
+        const int r = wave + 4 * t;
+        a[t] = (r < rows && lane < cols) ? g[(size_t)r * cap + lane] : aqc::cmk(0, 0);
+      }
+    };
+    cplx a[16], an[16];
+    if (steps > 0) fetch(0, a);
+    for (int s = 0; s < steps; ++s) {
+      if (s + 1 < steps) fetch(s + 1, an);
+      const int i = site_of(s);
+      const cplx* v = vb[s & 1];
+      cplx* vn = vb[(s + 1) & 1];
+      const double* lm = j.lam + (size_t)(i + 1) * cap;
+      if (side == 0) {  // out[x] = lambda[x] sum_k v[k] A[k][x], x = lane
+        const int ke = j.dims[i], m2 = j.dims[i + 1];
+        cplx acc = aqc::cmk(0, 0);
+#pragma unroll
+        for (int t = 0; t < 16; ++t)
+          if (wave + 4 * t < ke) acc = aqc::cfma(v[wave + 4 * t], a[t], acc);
+        part[wave][lane] = acc;
+        __syncthreads();
+        if (wave == 0 && lane < m2) {
+          const cplx r = aqc::cscale(aqc::cadd(aqc::cadd(part[0][lane], part[1][lane]), aqc::cadd(part[2][lane], part[3][lane])),
+                                     lm[lane]);
+          vn[lane] = r;
+          if (amps) win_st(U + (size_t)(s + 1) * cap + lane, r);
+        }
+      } else {  // out[x] = sum_k A[x][k] lambda[k] v[k], k = lane
+        const int ke = j.dims[i + 1], m2 = j.dims[i];
+        const cplx vk = lane < ke ? aqc::cscale(v[lane], lm[lane]) : aqc::cmk(0, 0);
+#pragma unroll
+        for (int t = 0; t < 16; ++t) red[wave + 4 * t][lane] = aqc::cmul(a[t], vk);
+        __syncthreads();
+        {  // thread (x = tid / 4, quarter p = tid % 4): 16 k's, then the four quarters by shuffles
+          const int x = tid >> 2, p = tid & 3;
+          cplx acc = aqc::cmk(0, 0);
+#pragma unroll
+          for (int c = 0; c < 16; ++c) acc = aqc::cadd(acc, red[x][16 * p + c]);
+          acc.x += __shfl_xor(acc.x, 1);
+          acc.y += __shfl_xor(acc.y, 1);
+          acc.x += __shfl_xor(acc.x, 2);
+          acc.y += __shfl_xor(acc.y, 2);
+          if (p == 0 && x < m2) {
+            vn[x] = acc;
+            if (amps) win_st(Y + (size_t)(i - lo) * cap + x, acc);
+          }
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int t = 0; t < 16; ++t) a[t] = an[t];
     }
-    if (s < ny) {
+  } else
+  for (int s = 0; s < steps; ++s) {
+    const cplx* v = vb[s & 1];
+    cplx* vn = vb[(s + 1) & 1];
+    if (side == 0) {
+      const int i = lo + s;
+      win_step(j.gam, j.lam, cap, i, false, j.dims[i], j.dims[i + 1], v, vn, amps ? U + (size_t)(s + 1) * cap : nullptr,
+               part);
+    } else {
       const int i = hi - s;
-      const cplx* y = yb[s & 1];
-      cplx* yn = yb[(s + 1) & 1];
-      hw_step(j.gam, j.lam, cap, i, true, 1, 0u, j.dims[i + 1], j.dims[i], [&](int, int k) { return y[k]; },
-              [&](int, int x, cplx v) {
-                yn[x] = v;
-                if (amps) Y[(size_t)(i - lo) * cap + x] = v;
-              },
-              part);
+      win_step(j.gam, j.lam, cap, i, true, j.dims[i + 1], j.dims[i], v, vn, amps ? Y + (size_t)(i - lo) * cap : nullptr,
+               part);
     }
   }
-  const cplx* u = ub[nl & 1];  // at bond lo + nl
-  const cplx* y = yb[ny & 1];  // at bond hi + 1 - ny
+  {
+    const cplx* v = vb[steps & 1];
+    const int d = side == 0 ? j.dims[lo + nl] : j.dims[hi + 1 - ny];
+    for (int e = tid; e < d; e += kT) win_st(j.fin + (size_t)side * cap + e, v[e]);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  __shared__ int last;
+  if (tid == 0) last = __hip_atomic_fetch_add(j.cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 1;
+  __syncthreads();
+  if (!last) return;
+  const cplx* u = j.fin;        // at bond lo + nl
+  const cplx* y = j.fin + cap;  // at bond hi + 1 - ny
   const int dl = j.dims[lo], dr = j.dims[hi + 1];
   // closings, a wave per output, lanes along the bond: output 0 = <0|psi>, 1 + k = amp_k (with
   // amps; window sites as u_k A_k[1] y_{k+1}: lanes along the right index, a loop over the left)
@@ -1700,19 +1848,19 @@ __global__ __launch_bounds__(kT) void k_hw_win(const HwWinJob* __restrict__ jobs
     if (o == 0) {  // (with amps u is at bond hi + 1: against Nr[0]; else the chains' meeting bond)
       const cplx* yy = amps ? j.nr : y;
       const int d = j.dims[lo + nl];
-      for (int c = lane; c < d; c += 64) acc = aqc::cfma(u[c], yy[c], acc);
+      for (int c = lane; c < d; c += 64) acc = aqc::cfma(win_ld(u + c), amps ? yy[c] : win_ld(yy + c), acc);
     } else if (k < lo) {
-      for (int c = lane; c < dl; c += 64) acc = aqc::cfma(j.ml[(size_t)(1 + k) * cap + c], y[c], acc);
+      for (int c = lane; c < dl; c += 64) acc = aqc::cfma(j.ml[(size_t)(1 + k) * cap + c], win_ld(y + c), acc);
     } else if (k > hi) {
-      for (int c = lane; c < dr; c += 64) acc = aqc::cfma(u[c], j.nr[(size_t)(1 + k) * cap + c], acc);
+      for (int c = lane; c < dr; c += 64) acc = aqc::cfma(win_ld(u + c), j.nr[(size_t)(1 + k) * cap + c], acc);
     } else {
       const cplx* uk = U + (size_t)(k - lo) * cap;
       const cplx* yk = Y + (size_t)(k + 1 - lo) * cap;
       const int kl = j.dims[k], kr = j.dims[k + 1];
       for (int r = lane; r < kr; r += 64) {
         cplx t = aqc::cmk(0, 0);
-        for (int l = 0; l < kl; ++l) t = aqc::cfma(uk[l], site_a(j.gam, j.lam, cap, k, 1, l, r), t);
-        acc = aqc::cfma(t, yk[r], acc);
+        for (int l = 0; l < kl; ++l) t = aqc::cfma(win_ld(uk + l), site_a(j.gam, j.lam, cap, k, 1, l, r), t);
+        acc = aqc::cfma(t, win_ld(yk + r), acc);
       }
     }
     acc.x = wave_sum_d(acc.x);
@@ -3226,13 +3374,16 @@ int aqc_mps_zero_hw1_batch(aqc_mps_t base, aqc_mps_t* hs, int ns, double* out_ov
     const size_t jb = ((rj.size() * sizeof(HwRowsJob) + 255) / 256) * 256;
     const size_t wb = ((win.size() * sizeof(HwWinJob) + 255) / 256) * 256;
     const size_t rb = (((size_t)win.size() * (n + 1) * sizeof(cplx)) + 255) / 256 * 256;
+    const size_t fnb = (size_t)win.size() * 2 * cap * sizeof(cplx);  // the chains' last vectors
+    const size_t cb = ((win.size() * sizeof(int) + 255) / 256) * 256;  // hand-off counters
     size_t uyb = 0;  // with amps: each state's window vectors (2 (w + 1) cap)
     if (out_amps)
       for (int s : win) uyb += 2 * (size_t)(hi[s] - lo[s] + 2) * cap * sizeof(cplx);
-    char* d = (char*)aqc::dev_alloc(jb + wb + rb + uyb + 256);
+    char* d = (char*)aqc::dev_alloc(rb + fnb + uyb + 256);
     AQC_REQUIRE(d, "aqc_mps_zero_hw1_batch: out of device memory");
-    cplx* res = (cplx*)(d + jb + wb);
-    cplx* uy = (cplx*)(d + jb + wb + rb);
+    cplx* res = (cplx*)d;
+    cplx* fin = (cplx*)(d + rb);
+    cplx* uy = (cplx*)(d + rb + fnb);
     for (size_t k = 0; k < win.size(); ++k) {
       const int s = win[k];
       HwWinJob j;
@@ -3249,9 +3400,13 @@ int aqc_mps_zero_hw1_batch(aqc_mps_t base, aqc_mps_t* hs, int ns, double* out_ov
       j.amps = out_amps ? res + k * (n + 1) + 1 : nullptr;
       j.uy = out_amps ? uy : nullptr;
       if (out_amps) uy += 2 * (size_t)(hi[s] - lo[s] + 2) * cap;
+      j.fin = fin + k * 2 * (size_t)cap;
+      j.cnt = nullptr;  // (set below: in the staging buffer)
+      j.pad = 0;
       wj.push_back(j);
     }
-    const size_t lds_win = (4 * (size_t)cap + 4 * kHwR * 64) * sizeof(cplx);
+    // (capacity <= 64: plus the right steps' 64 x 65 reduction tile)
+    const size_t lds_win = (2 * (size_t)cap + 4 * 64 + (cap <= 64 ? 64 * 65 : 0)) * sizeof(cplx);
     const size_t lds_rows = (2 * (size_t)cap + 4 * kHwR * 64) * sizeof(cplx);
     // the job arrays through a pinned staging set of the ring (pageable copies were a host round
     // trip each, between the candidates' replay and these kernels)
@@ -3260,16 +3415,18 @@ int aqc_mps_zero_hw1_batch(aqc_mps_t base, aqc_mps_t* hs, int ns, double* out_ov
       aqc::dev_free(d);
       return lease.rc();
     }
-    rc = ensure_staging(lease.buf(), jb + wb);
+    rc = ensure_staging(lease.buf(), jb + wb + cb);
     if (rc != AQC_OK) {
       aqc::dev_free(d);
       return rc;
     }
     char* hj = (char*)lease.buf().host;
     char* dj = (char*)lease.buf().dev;
+    for (size_t k = 0; k < wj.size(); ++k) wj[k].cnt = (int*)(dj + jb + wb) + k;
     if (!rj.empty()) std::memcpy(hj, rj.data(), rj.size() * sizeof(HwRowsJob));
     std::memcpy(hj + jb, wj.data(), wj.size() * sizeof(HwWinJob));
-    if (int e = aqc::upload_async(dj, hj, jb + wb, st)) {
+    std::memset(hj + jb + wb, 0, cb);
+    if (int e = aqc::upload_async(dj, hj, jb + wb + cb, st)) {
       aqc::dev_free(d);
       return e;
     }
@@ -3285,7 +3442,7 @@ int aqc_mps_zero_hw1_batch(aqc_mps_t base, aqc_mps_t* hs, int ns, double* out_ov
       AQC_CHECK_LAUNCH();
     }
     aqc::KernelTimer::begin(st, "mps_zero_hw1", 0.0, 0.0);
-    hipLaunchKernelGGL(k_hw_win, dim3((unsigned)win.size()), dim3(kT), lds_win, st, (const HwWinJob*)(dj + jb));
+    hipLaunchKernelGGL(k_hw_win, dim3((unsigned)win.size(), 2), dim3(kT), lds_win, st, (const HwWinJob*)(dj + jb));
     aqc::KernelTimer::end(st);
     AQC_CHECK_LAUNCH();
     std::vector<cplx> h(win.size() * (n + 1));
