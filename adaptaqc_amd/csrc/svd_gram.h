@@ -670,7 +670,17 @@ __device__ __noinline__ double gram_cert128(const TwoSiteJob& j, int C, int K, c
 // (>= 4 GemmLds).  Returns false (work untouched beyond scratch, caller runs the Jacobi) when the
 // fast path does not apply.  Uniform in the workgroup.
 // Returns 0: declined (the caller runs the register Jacobi), 1: done, 2: done if gram_certified.
-__device__ __noinline__ int gram_svd_body(const TwoSiteJob& j) {
+// AQC_GRAM_INLINE=1: the body inlined into its callers (no call frame: the callee-saved VGPR saves
+// of a real call go to scratch on every update)
+#ifndef AQC_GRAM_INLINE
+#define AQC_GRAM_INLINE 0
+#endif
+#if AQC_GRAM_INLINE
+__device__ __forceinline__
+#else
+__device__ __noinline__
+#endif
+int gram_svd_body(const TwoSiteJob& j) {
   extern __shared__ double2 xbuf[];
   __shared__ double s_d[128], s_e[128], s_e2[128], s_lam[128], s_err[128], s_sig2[kGramMaxK], s_tail;
   __shared__ int s_K, s_cert;
