@@ -154,6 +154,15 @@ def load(path=LIB_PATH):
             raise AqcError(
                 f"HIP library not found at {path}; build it with `python -c 'import __graft_entry__ as g; g.build()'`"
             )
+        # PyTorch first when it is installed: libaqchip and torch both need a libamdhip64.so.7 (the
+        # ROCm under /opt/rocm, and torch's bundled one); the first loaded serves the process.  With
+        # libaqchip first, torch then ran on the other runtime and found no GPU ("No HIP GPUs are
+        # available"); with torch first both share torch's -- the configuration the bench and the
+        # GPU suite always ran (they import torch before any library call).
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         lib = ctypes.CDLL(path)
         missing = []
         for name, (args, res) in _SIGS.items():

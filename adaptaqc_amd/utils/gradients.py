@@ -106,7 +106,11 @@ def general_grad_of_pairs(
 
     if backend is None:
         from ..backends.python_default_backends import MPS_SIM as backend
-    psi = device_mps_from_circuit(circuit.copy(), sim=backend.simulator)
+    # the device MPS backend replays from its cached device copy of the target payload (the same
+    # data load_aer would upload again: ~3.5 ms of host marshalling and copy per layer at 50 qubits,
+    # chi = 64), into its work state; other backends build a fresh state
+    replay = getattr(backend, "device_state", None)
+    psi = replay(circuit) if replay is not None else device_mps_from_circuit(circuit.copy(), sim=backend.simulator)
     n = circuit.num_qubits
     return sharded_pair_scores(
         lambda pairs: grads_for_state(psi, n, inverse_zero_ansatz, generators, degeneracies, pairs,
