@@ -972,9 +972,17 @@ __global__ __launch_bounds__(64) void k_gb_inv(const TwoSiteJob* __restrict__ jo
 
 // ---- Gram-Schmidt inside clusters (eigenvalue gaps below 1e-7 ||T||; the vectors of separated
 // eigenvalues come out orthogonal to ~1e-14 from three inverse-iteration steps), then the cluster
-// members' sigma^2 again: grid (nj), one wave ----
+// members' sigma^2 again: grid (nj), 256 threads ----
+// Member i of a cluster starting at `start` against members start .. i - 1 (already orthonormal) in
+// block form, twice (classical Gram-Schmidt with re-orthogonalisation): all m = i - start dot
+// products at once -- lanes along the members (coalesced 512-byte row pieces of the row-major
+// scratch), the four waves splitting the rows, partials through the LDS -- then each row's update
+// by its own thread.  (Round 5: one wave, sequential Gram-Schmidt with every dot product a column
+// read strided by CT: 403 us a call at CT = 256 when the kept spectrum's tiny values form one wide
+// cluster -- the absolute gap test puts every sigma^2 below 1e-7 ||T|| in it -- 23% of a C = 256
+// update in the unbounded compile's Rotosolve layer.)
 template <int CT>
-__global__ __launch_bounds__(64) void k_gb_gs(const TwoSiteJob* __restrict__ jobs, GBArgs a, int job0) {
+__global__ __launch_bounds__(256) void k_gb_gs(const TwoSiteJob* __restrict__ jobs, GBArgs a, int job0) {
   const int jb = job0 + (int)blockIdx.x;
   if (*(const gi32*)(a.status + jb) != 0) return;
   const TwoSiteJob& j = jobs[jb];
@@ -982,40 +990,80 @@ __global__ __launch_bounds__(64) void k_gb_gs(const TwoSiteJob* __restrict__ job
   bool tr;
   job_dims(j, M, L, C, tr, K);
   K = kept_count(a, jb);
-  const int lane = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const double* lam = a.lam + (size_t)jb * CT;
   const double ortol = 1e-7 * ldg(a.tn + jb);
   double* zb = a.z + (size_t)jb * CT * CT;
   const double* dd = a.d + (size_t)jb * CT;
   const double* ee = a.e + (size_t)jb * CT;
+  __shared__ double part[4][64];
+  __shared__ double dp[CT];
+  __shared__ double red[2][4];
+  auto block_sum2 = [&](double x, double y, double& sx, double& sy) {
+    x = wave_sum_b(x);
+    y = wave_sum_b(y);
+    if (lane == 0) red[0][wave] = x, red[1][wave] = y;
+    __syncthreads();
+    sx = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
+    sy = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
+    __syncthreads();
+  };
   int start = 0;
   for (int i = 1; i < K; ++i) {
-    if (ldg(lam + i - 1) - ldg(lam + i) >= ortol) {
+    if (ldg(lam + i - 1) - ldg(lam + i) >= ortol) {  // (uniform)
       start = i;
       continue;
     }
-    for (int jj = start; jj < i; ++jj) {
-      double dp = 0.0;
-      for (int row = lane; row < CT; row += 64) dp = fma(zb[(size_t)row * CT + i], zb[(size_t)row * CT + jj], dp);
-      dp = wave_sum_b(dp);
-      for (int row = lane; row < CT; row += 64)
-        zb[(size_t)row * CT + i] = fma(-dp, zb[(size_t)row * CT + jj], zb[(size_t)row * CT + i]);
+    const int m = i - start;
+    // ||z_i||^2 before the projection (the "twice is enough" test below)
+    double nb = 0.0, unused = 0.0;
+    for (int r = tid; r < CT; r += 256) {
+      const double z = zb[(size_t)r * CT + i];
+      nb = fma(z, z, nb);
     }
+    block_sum2(nb, 0.0, nb, unused);
     double n2 = 0.0;
-    for (int row = lane; row < CT; row += 64) n2 = fma(zb[(size_t)row * CT + i], zb[(size_t)row * CT + i], n2);
-    n2 = wave_sum_b(n2);
-    const double sc = 1.0 / sqrt(n2);
-    double s2 = 0.0;
-    for (int row = lane; row < CT; row += 64) {
-      const double z = zb[(size_t)row * CT + i] * sc;
-      zb[(size_t)row * CT + i] = z;
-      s2 = fma(ldg(dd + row) * z, z, s2);
+    for (int pass = 0; pass < 2; ++pass) {
+      for (int c0 = 0; c0 < m; c0 += 64) {
+        const int c = c0 + lane;
+        double acc = 0.0;
+        if (c < m) {
+          const double* col = zb + start + c;
+#pragma unroll 8
+          for (int r = wave; r < CT; r += 4) acc = fma(zb[(size_t)r * CT + i], col[(size_t)r * CT], acc);
+        }
+        part[wave][lane] = acc;
+        __syncthreads();
+        if (wave == 0 && c < m) dp[c] = (part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]);
+        __syncthreads();
+      }
+      n2 = 0.0;
+      for (int r = tid; r < CT; r += 256) {
+        const double* row = zb + (size_t)r * CT + start;
+        double z = zb[(size_t)r * CT + i];
+        for (int t = 0; t < m; ++t) z = fma(-dp[t], row[t], z);
+        zb[(size_t)r * CT + i] = z;
+        n2 = fma(z, z, n2);
+      }
+      // (its barriers also order the rows' updates before any later read.)  Kahan / Parlett: when
+      // the projection kept more than half of ||z||^2 the vector was not nearly in the span, one
+      // pass is orthogonal to rounding and the second is skipped
+      block_sum2(n2, 0.0, n2, unused);
+      if (n2 > 0.5 * nb) break;  // (uniform)
+      nb = n2;
     }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-    for (int row = lane; row < CT - 1; row += 64)
-      s2 = fma(2.0 * ldg(ee + row) * zb[(size_t)row * CT + i], zb[(size_t)(row + 1) * CT + i], s2);
-    s2 = wave_sum_b(s2);
-    if (lane == 0) stg(a.sig2 + (size_t)jb * CT + i, s2 > 0.0 ? s2 : 0.0);
+    const double sc = 1.0 / sqrt(n2);
+    for (int r = tid; r < CT; r += 256) zb[(size_t)r * CT + i] *= sc;
+    __syncthreads();
+    double s2a = 0.0, s2b = 0.0;
+    for (int r = tid; r < CT; r += 256) {
+      const double z = zb[(size_t)r * CT + i];
+      s2a = fma(ldg(dd + r) * z, z, s2a);
+      if (r < CT - 1) s2b = fma(2.0 * ldg(ee + r) * z, zb[(size_t)(r + 1) * CT + i], s2b);
+    }
+    block_sum2(s2a, s2b, s2a, s2b);
+    const double s2 = s2a + s2b;
+    if (tid == 0) stg(a.sig2 + (size_t)jb * CT + i, s2 > 0.0 ? s2 : 0.0);
   }
 }
 
@@ -1447,7 +1495,7 @@ int run_gram_big(const TwoSiteJob* hjobs, const TwoSiteJob* jobs, int nj, int ca
     AQC_CHECK_LAUNCH();
     hipLaunchKernelGGL((k_gb_inv<CT>), dim3(CT / 64, nr), dim3(64), 0, ps, jobs, a, j0);
     AQC_CHECK_LAUNCH();
-    hipLaunchKernelGGL((k_gb_gs<CT>), dim3(nr), dim3(64), 0, ps, jobs, a, j0);
+    hipLaunchKernelGGL((k_gb_gs<CT>), dim3(nr), dim3(256), 0, ps, jobs, a, j0);
     AQC_CHECK_LAUNCH();
     if (s3 != ps) {
       hipEvent_t e1 = gb_event(evi++);
