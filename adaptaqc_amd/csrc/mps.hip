@@ -1690,22 +1690,26 @@ __device__ __forceinline__ void win_step(const cplx* __restrict__ gam, const dou
     }
   } else {
     for (int x0 = 4 * q; x0 < m2; x0 += 16) {  // (uniform per wave)
-      cplx acc[4];
-#pragma unroll
-      for (int t = 0; t < 4; ++t) acc[t] = aqc::cmk(0, 0);
+      // (four named sums: as an array the compiler kept them in scratch)
+      cplx c0 = aqc::cmk(0, 0), c1 = c0, c2 = c0, c3 = c0;
+      const bool h1 = x0 + 1 < m2, h2 = x0 + 2 < m2, h3 = x0 + 3 < m2;
       for (int k = lane; k < ke; k += 64) {
         const cplx vk = aqc::cscale(v[k], lm[k]);
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-          if (x0 + t < m2) acc[t] = aqc::cfma(g[(size_t)(x0 + t) * cap + k], vk, acc[t]);
+        const cplx* gk = g + (size_t)x0 * cap + k;
+        c0 = aqc::cfma(gk[0], vk, c0);
+        if (h1) c1 = aqc::cfma(gk[cap], vk, c1);
+        if (h2) c2 = aqc::cfma(gk[2 * (size_t)cap], vk, c2);
+        if (h3) c3 = aqc::cfma(gk[3 * (size_t)cap], vk, c3);
       }
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        acc[t].x = wave_sum_d(acc[t].x);
-        acc[t].y = wave_sum_d(acc[t].y);
-      }
+      c0.x = wave_sum_d(c0.x), c0.y = wave_sum_d(c0.y);
+      c1.x = wave_sum_d(c1.x), c1.y = wave_sum_d(c1.y);
+      c2.x = wave_sum_d(c2.x), c2.y = wave_sum_d(c2.y);
+      c3.x = wave_sum_d(c3.x), c3.y = wave_sum_d(c3.y);
       if (lane < 4 && x0 + lane < m2) {
-        const cplx r = lane == 0 ? acc[0] : lane == 1 ? acc[1] : lane == 2 ? acc[2] : acc[3];
+        cplx r = c0;
+        if (lane == 1) r = c1;
+        if (lane == 2) r = c2;
+        if (lane == 3) r = c3;
         out[x0 + lane] = r;
         if (store) win_st(store + x0 + lane, r);
       }
@@ -1728,7 +1732,6 @@ __global__ __launch_bounds__(kT) void k_hw_win(const HwWinJob* __restrict__ jobs
   extern __shared__ cplx hw_lds[];
   const int cap = j.cap, n = j.n, lo = j.lo, hi = j.hi, w = hi - lo + 1;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  cplx* vb[2] = {hw_lds, hw_lds + cap};
   cplx (*part)[64] = reinterpret_cast<cplx (*)[64]>(hw_lds + 2 * cap);
   const bool amps = j.amps != nullptr;
   const int nl = amps ? w : (w + 1) / 2, ny = amps ? w : w - nl;
@@ -1740,7 +1743,7 @@ __global__ __launch_bounds__(kT) void k_hw_win(const HwWinJob* __restrict__ jobs
     const cplx* src = side == 0 ? j.ml : j.nr;
     cplx* st0 = amps ? (side == 0 ? U : Y + (size_t)w * cap) : nullptr;
     for (int e = tid; e < d0; e += kT) {
-      vb[0][e] = src[e];
+      hw_lds[e] = src[e];
       if (st0) win_st(st0 + e, src[e]);
     }
   }
@@ -1769,8 +1772,8 @@ __global__ __launch_bounds__(kT) void k_hw_win(const HwWinJob* __restrict__ jobs
     for (int s = 0; s < steps; ++s) {
       if (s + 1 < steps) fetch(s + 1, an);
       const int i = site_of(s);
-      const cplx* v = vb[s & 1];
-      cplx* vn = vb[(s + 1) & 1];
+      const cplx* v = hw_lds + (s & 1) * cap;
+      cplx* vn = hw_lds + ((s + 1) & 1) * cap;
       const double* lm = j.lam + (size_t)(i + 1) * cap;
       if (side == 0) {  // out[x] = lambda[x] sum_k v[k] A[k][x], x = lane
         const int ke = j.dims[i], m2 = j.dims[i + 1];
@@ -1813,8 +1816,8 @@ __global__ __launch_bounds__(kT) void k_hw_win(const HwWinJob* __restrict__ jobs
     }
   } else
   for (int s = 0; s < steps; ++s) {
-    const cplx* v = vb[s & 1];
-    cplx* vn = vb[(s + 1) & 1];
+    const cplx* v = hw_lds + (s & 1) * cap;
+    cplx* vn = hw_lds + ((s + 1) & 1) * cap;
     if (side == 0) {
       const int i = lo + s;
       win_step(j.gam, j.lam, cap, i, false, j.dims[i], j.dims[i + 1], v, vn, amps ? U + (size_t)(s + 1) * cap : nullptr,
@@ -1826,7 +1829,7 @@ __global__ __launch_bounds__(kT) void k_hw_win(const HwWinJob* __restrict__ jobs
     }
   }
   {
-    const cplx* v = vb[steps & 1];
+    const cplx* v = hw_lds + (steps & 1) * cap;
     const int d = side == 0 ? j.dims[lo + nl] : j.dims[hi + 1 - ny];
     for (int e = tid; e < d; e += kT) win_st(j.fin + (size_t)side * cap + e, v[e]);
   }
