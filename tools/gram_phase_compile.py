@@ -15,7 +15,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 
-NAMES = ["S1", "S2+S3", "S4", "S5", "S6", "output", "S3_columns", "S5_inverse_iteration", "S3_phaseA"]
+NAMES = ["S1", "S2+S3", "S4", "S5", "S6", "output", "S3_columns", "S5_inverse_iteration", "S3_phaseA",
+         "S3_cols_32_63", "S3_cols_64_95", "S3_cols_96_on"]
 
 
 def read(L):
