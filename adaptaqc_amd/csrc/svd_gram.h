@@ -670,6 +670,133 @@ __device__ __noinline__ double gram_cert128(const TwoSiteJob& j, int C, int K, c
 // (>= 4 GemmLds).  Returns false (work untouched beyond scratch, caller runs the Jacobi) when the
 // fast path does not apply.  Uniform in the workgroup.
 // Returns 0: declined (the caller runs the register Jacobi), 1: done, 2: done if gram_certified.
+// Off by default (measured slower, profiles/r6_s3_tail_ab.json: k_chain 35.6 -> 37.75 ms -- one
+// wave issuing the whole 32 x 32 block's 12 FMAs per element, four wave reductions and three LDS
+// round trips per column costs more than the main loop's late columns with their two barriers);
+// -DAQC_S3_TAIL=1 builds it (parity green: test_gpu_svd / headline / mps / threshold).
+#ifndef AQC_S3_TAIL
+#define AQC_S3_TAIL 0
+#endif
+constexpr int kS3Tail = 32;
+#if defined(__HIP_DEVICE_COMPILE__)
+using s3_lcplx = __attribute__((address_space(3))) cplx;
+using s3_ldbl = __attribute__((address_space(3))) double;
+#else
+using s3_lcplx = cplx;
+using s3_ldbl = double;
+#endif
+// S3's last kS3Tail = 32 columns (columns T0 = C - 32 .. C - 2) in wave 0 alone.  On entry every
+// thread holds G^(T0 - 1) in the main layout (row r, columns q + 8 i) and the LDS reflector T0 - 1
+// (p, v at buffer (T0 - 1) & 1, a2): the trailing block gets that reflector's rank-2 update and goes
+// through the LDS to wave 0, lane l holding row l >> 1, columns (l & 1) + 2 i (i < 16) of it.  Then
+// per column k' = 0 .. 30 (global K = T0 + k') the lower zhetd2 step with the main loop's zlarfg
+// formulas -- column k' below the diagonal from its lane pairs, p = tau A v from the lanes' 16
+// columns (v, p through a wave-private LDS vector), a2 = -tau (p^H v) / 2, A -= v p^H + (p + 2
+// Re(a2) v) v^H -- with only wave-level reductions: no workgroup barrier per column (the main
+// loop's two barriers and phase B hand-off cost ~3 K ticks a column at its end).  Writes d, e, tau
+// and the reflectors exactly where the main loop does.
+__device__ __forceinline__ void s3_tail(cplx (&g)[16], int C, int r0, int q0, int tid, int lane, int wave,
+                                        s3_lcplx* lb, cplx* hh) {
+  const int T0 = C - kS3Tail;
+  s3_lcplx* pvb = lb;
+  s3_lcplx* vbb = lb + 256;
+  s3_lcplx* tauS = lb + 1921;
+  s3_ldbl* eS = (s3_ldbl*)(lb + 2050);
+  s3_ldbl* dS = (s3_ldbl*)(lb + 2114);
+  s3_lcplx* a2b = lb + 2178;
+  s3_lcplx* tile = lb + 2304;  // [32][33]
+  s3_lcplx* vt = lb + 2304 + 32 * 33;
+  s3_lcplx* pt = vt + 32;
+  {  // reflector T0 - 1's update of the trailing block, which goes to the LDS
+    const int bp = (T0 - 1) & 1;
+    const int r = r0, q = q0;
+    if (r >= T0 && r < C) {
+      const cplx vr = vbb[bp * 128 + r], pr = pvb[bp * 128 + r];
+      const double a2r2 = 2.0 * a2b[bp].x;
+      const cplx wr = aqc::cmk(fma(a2r2, vr.x, pr.x), fma(a2r2, vr.y, pr.y));
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int c = q + 8 * i;
+        if (c >= T0 && c < C) {
+          const cplx vc = vbb[bp * 128 + c], pc = pvb[bp * 128 + c];
+          cplx x = g[i];
+          x.x = fma(-vr.x, pc.x, fma(-vr.y, pc.y, fma(-wr.x, vc.x, fma(-wr.y, vc.y, x.x))));
+          x.y = fma(-vr.y, pc.x, fma(vr.x, pc.y, fma(-wr.y, vc.x, fma(wr.x, vc.y, x.y))));
+          tile[(r - T0) * 33 + (c - T0)] = x;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  if (wave == 0) {
+    const int rr = lane >> 1, h = lane & 1;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) g[i] = tile[rr * 33 + 2 * i + h];
+    for (int kk = 0; kk < kS3Tail - 1; ++kk) {
+      const int K = T0 + kk;
+      // column kk below the diagonal, on both lanes of each row
+      cplx x = h == (kk & 1) ? pick16(g, kk >> 1) : aqc::cmk(0, 0);
+      x.x += __shfl_xor(x.x, 1);
+      x.y += __shfl_xor(x.y, 1);
+      const double xn2 = wave_sum_dpp(h == 0 && rr > kk + 1 ? aqc::cnorm2(x) : 0.0);
+      const double dkk = bcast_d(x.x, 2 * kk);  // (the diagonal: row kk, column kk)
+      const cplx alpha = aqc::cmk(bcast_d(x.x, 2 * (kk + 1)), bcast_d(x.y, 2 * (kk + 1)));
+      // zlarfg, as the main loop's wave 0
+      const double x2 = fma(alpha.x, alpha.x, fma(alpha.y, alpha.y, xn2));
+      double rs = __builtin_amdgcn_rsq(x2);
+      rs = rs * fma(-0.5 * x2 * rs, rs, 1.5);
+      rs = rs * fma(-0.5 * x2 * rs, rs, 1.5);
+      const double nn = x2 * rs;
+      const bool triv = xn2 == 0.0 && alpha.y == 0.0;
+      const double beta = triv ? alpha.x : (alpha.x >= 0.0 ? -nn : nn);
+      const double ib = alpha.x >= 0.0 ? -rs : rs;
+      const double dr = alpha.x - beta, di = alpha.y, id2 = rcp_nr(fma(dr, dr, di * di));
+      const cplx tau = triv ? aqc::cmk(0, 0) : aqc::cmk((beta - alpha.x) * ib, -alpha.y * ib);
+      const cplx scl = triv ? aqc::cmk(0, 0) : aqc::cmk(dr * id2, -di * id2);
+      // v: 1 at kk + 1, scl x below, 0 above
+      cplx v = rr > kk + 1 ? aqc::cmul(x, scl) : aqc::cmk(rr == kk + 1 ? 1.0 : 0.0, 0.0);
+      if (lane == 0) {
+        tauS[K] = tau;
+        eS[K] = beta;
+        dS[K] = dkk;
+      }
+      if (h == 0) {
+        vt[rr] = v;
+        if (rr > kk) aqc::stg(hh + (size_t)K * (2 * C - K - 1) / 2 + (T0 + rr - K - 1), v);  // GLOBAL, not FLAT
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      // p = tau A v (v_c = 0 at and above kk: no masks; v_c read where used, so that no 16 of
+      // them stay live beside the block)
+      cplx acc = aqc::cmk(0, 0);
+#pragma unroll
+      for (int i = 0; i < 16; ++i)
+        if (2 * i + 1 > kk) acc = aqc::cfma(g[i], vt[2 * i + h], acc);  // (uniform skip)
+      acc.x += __shfl_xor(acc.x, 1);
+      acc.y += __shfl_xor(acc.y, 1);
+      const cplx p = rr > kk ? aqc::cmul(tau, acc) : aqc::cmk(0, 0);
+      const double ktx = wave_sum_dpp(h == 0 ? fma(p.x, v.x, p.y * v.y) : 0.0);
+      const double kty = wave_sum_dpp(h == 0 ? fma(p.x, v.y, -p.y * v.x) : 0.0);
+      const cplx a2 = aqc::cscale(aqc::cmul(tau, aqc::cmk(ktx, kty)), -0.5);
+      if (h == 0) pt[rr] = p;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      const double a2r2 = 2.0 * a2.x;
+      const cplx w = aqc::cmk(fma(a2r2, v.x, p.x), fma(a2r2, v.y, p.y));
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        if (2 * i + 1 > kk) {  // (uniform)
+          const cplx pc = pt[2 * i + h], vci = vt[2 * i + h];
+          g[i].x = fma(-v.x, pc.x, fma(-v.y, pc.y, fma(-w.x, vci.x, fma(-w.y, vci.y, g[i].x))));
+          g[i].y = fma(-v.y, pc.x, fma(v.x, pc.y, fma(-w.y, vci.x, fma(w.x, vci.y, g[i].y))));
+        }
+      }
+    }
+    // d_{C-1}: the last diagonal entry after reflector C - 2's update
+    const cplx glast = pick16(g, (kS3Tail - 1) >> 1);
+    const double dl = bcast_d(glast.x, 2 * (kS3Tail - 1) + ((kS3Tail - 1) & 1));
+    if (lane == 0) dS[C - 1] = dl;
+  }
+}
+
 // AQC_GRAM_INLINE=1: the body inlined into its callers (no call frame: the callee-saved VGPR saves
 // of a real call go to scratch on every update)
 #ifndef AQC_GRAM_INLINE
@@ -912,7 +1039,10 @@ int gram_svd_body(const TwoSiteJob& j) {
     xvb[128 + r] = (r > 0 && r < C) ? g[0] : aqc::cmk(0, 0);
   }
   __syncthreads();
-  for (int k = 0; k < C - 1; ++k) {
+  // the last kS3Tail columns in wave 0 alone (AQC_S3_TAIL): no workgroup barrier per column
+  const bool s3tail = AQC_S3_TAIL && C >= 64;
+  const int kEnd = s3tail ? C - kS3Tail : C - 1;
+  for (int k = 0; k < kEnd; ++k) {
     const int b = k & 1, bp = b ^ 1;
     // q and r laundered through an empty asm each step: otherwise the compiler hoists the 16
     // columns' loop-invariant index / address values out of the k loop and spills them
@@ -1072,6 +1202,9 @@ int gram_svd_body(const TwoSiteJob& j) {
     __syncthreads();
     tick_step(t_a);
   }
+  if (s3tail) {
+    s3_tail(g, C, r0, q0, tid, lane, wave, lb, hh);
+  } else
   // d_{C-1}: reflector C - 2's update of the last diagonal entry
   if (wave == (C - 1) >> 3) {
     const int bp = (C - 2) & 1;
