@@ -3382,11 +3382,15 @@ int aqc_mps_zero_hw1_batch(aqc_mps_t base, aqc_mps_t* hs, int ns, double* out_ov
     size_t uyb = 0;  // with amps: each state's window vectors (2 (w + 1) cap)
     if (out_amps)
       for (int s : win) uyb += 2 * (size_t)(hi[s] - lo[s] + 2) * cap * sizeof(cplx);
-    char* d = (char*)aqc::dev_alloc(rb + fnb + uyb + 256);
+    // the states' and base's error flags are gathered beside the results (one read-back: the
+    // caller needs no separate aqc_mps_check_batch round trip)
+    const size_t flb = (((size_t)ns + 1) * sizeof(int) + 255) / 256 * 256;
+    char* d = (char*)aqc::dev_alloc(rb + flb + fnb + uyb + 256);
     AQC_REQUIRE(d, "aqc_mps_zero_hw1_batch: out of device memory");
     cplx* res = (cplx*)d;
-    cplx* fin = (cplx*)(d + rb);
-    cplx* uy = (cplx*)(d + rb + fnb);
+    int* dflags = (int*)(d + rb);
+    cplx* fin = (cplx*)(d + rb + flb);
+    cplx* uy = (cplx*)(d + rb + flb + fnb);
     for (size_t k = 0; k < win.size(); ++k) {
       const int s = win[k];
       HwWinJob j;
@@ -3418,7 +3422,8 @@ int aqc_mps_zero_hw1_batch(aqc_mps_t base, aqc_mps_t* hs, int ns, double* out_ov
       aqc::dev_free(d);
       return lease.rc();
     }
-    rc = ensure_staging(lease.buf(), jb + wb + cb);
+    const size_t fpb = ((size_t)ns + 1) * sizeof(int*);
+    rc = ensure_staging(lease.buf(), jb + wb + cb + fpb);
     if (rc != AQC_OK) {
       aqc::dev_free(d);
       return rc;
@@ -3429,7 +3434,10 @@ int aqc_mps_zero_hw1_batch(aqc_mps_t base, aqc_mps_t* hs, int ns, double* out_ov
     if (!rj.empty()) std::memcpy(hj, rj.data(), rj.size() * sizeof(HwRowsJob));
     std::memcpy(hj + jb, wj.data(), wj.size() * sizeof(HwWinJob));
     std::memset(hj + jb + wb, 0, cb);
-    if (int e = aqc::upload_async(dj, hj, jb + wb + cb, st)) {
+    int** hfp = (int**)(hj + jb + wb + cb);
+    for (int s = 0; s < ns; ++s) hfp[s] = hs[s]->d.flags;
+    hfp[ns] = base->d.flags;
+    if (int e = aqc::upload_async(dj, hj, jb + wb + cb + fpb, st)) {
       aqc::dev_free(d);
       return e;
     }
@@ -3448,10 +3456,20 @@ int aqc_mps_zero_hw1_batch(aqc_mps_t base, aqc_mps_t* hs, int ns, double* out_ov
     hipLaunchKernelGGL(k_hw_win, dim3((unsigned)win.size(), 2), dim3(kT), lds_win, st, (const HwWinJob*)(dj + jb));
     aqc::KernelTimer::end(st);
     AQC_CHECK_LAUNCH();
-    std::vector<cplx> h(win.size() * (n + 1));
-    AQC_HIP_CHECK(hipMemcpyAsync(h.data(), res, h.size() * sizeof(cplx), hipMemcpyDeviceToHost, st));
+    hipLaunchKernelGGL(k_gather_flags, dim3(1), dim3(256), 0, st, (int* const*)(dj + jb + wb + cb), ns + 1, dflags);
+    AQC_CHECK_LAUNCH();
+    std::vector<cplx> h(rb / sizeof(cplx) + flb / sizeof(cplx));
+    AQC_HIP_CHECK(hipMemcpyAsync(h.data(), res, rb + flb, hipMemcpyDeviceToHost, st));
     AQC_HIP_CHECK(hipStreamSynchronize(st));
     aqc::dev_free(d);
+    {
+      const int* hf = (const int*)((const char*)h.data() + rb);
+      for (int s = 0; s <= ns; ++s)
+        if (hf[s]) {
+          const int frc = check_flags(s < ns ? hs[s] : base);
+          if (frc != AQC_OK) return frc;
+        }
+    }
     base->h0l = std::max(base->h0l, need_l);
     base->h0r = std::min(base->h0r, need_r);
     if (full) {
@@ -3480,6 +3498,9 @@ int aqc_mps_zero_hw1_batch(aqc_mps_t base, aqc_mps_t* hs, int ns, double* out_ov
       rc = aqc_mps_amps_hw1_batch(fh.data(), (int)fh.size(), a.data());
       if (rc != AQC_OK) return rc;
     }
+    fh.push_back(base);  // (their error flags and base's, as on the window path)
+    rc = check_flags_batch(fh.data(), (int)fh.size());
+    if (rc != AQC_OK) return rc;
     for (size_t k = 0; k < fb.size(); ++k) {
       const int s = fb[k];
       out_ov[2 * s] = o[2 * k];

@@ -209,8 +209,8 @@ class MPSPrefixBatch(_SweepBase):
             return [float(0.5 * (1 - t / n)) for t in zs]
         # <0|psi> (and the softened cost's <e_i|psi>) likewise through the rewritten sites against
         # rows cached on the prefix (aqc_mps_zero_hw1_batch)
+        # (its read-back also carries the prefix's and the candidates' error flags)
         ov, amps = zero_hw1_batch(self.phi, states, amps=self.kind == "soft")
-        check_batch([self.phi] + states)
         costs = [float(1.0 - abs(v) ** 2) for v in ov]
         if self.kind == "soft":
             alpha = _soften_alpha(self.compiler)

@@ -168,7 +168,8 @@ int aqc_mps_z_sum_batch(aqc_mps_t base, aqc_mps_t* hs, int nstates, double* out)
    costs (aer_mps_backend.py:49-70, 88-93) of a Rotoselect gate's candidates: a state copied from
    `base` while base has not changed since contracts only the sites it rewrote, against zero and
    Hamming-weight-1 rows cached on base; any other state takes the full chains.  base is not
-   modified and must not be among hs. */
+   modified and must not be among hs.  The states' and base's error flags are read with the
+   results (as aqc_mps_check_batch would: AQC_ERR_STATE on a capacity overflow of queued work). */
 int aqc_mps_zero_hw1_batch(aqc_mps_t base, aqc_mps_t* hs, int nstates, double* out_ov, double* out_amps);
 
 /* ---- candidate sweep: replaces gradients.py:23-124 ------------------------------ */
