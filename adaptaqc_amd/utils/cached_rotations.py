@@ -141,6 +141,57 @@ class MPSPrefixBatch(_SweepBase):
         self.backend = compiler.backend
         self.phi = None
         self.kind = kind
+        # (instruction ids, rows of the whole circuit, row offsets, first row, the instructions --
+        # held so that no id in the key can be reused by a new instruction while it is cached)
+        self._conv = None
+
+    def _rows(self, circ, lo, hi):
+        """device_ops_rows(circ, lo, hi) from one conversion per circuit state: a gate's visit asks
+        for the prefix advance (goto) and the suffix (costs) of the same circuit, and each call of
+        the memoised conversion still walks every instruction in Python (~0.15 ms at 150 gates).
+        The conversion is reused while no instruction object was replaced (replace_1q_gate swaps
+        the instruction; an in-place parameter change would go unnoticed, which no caller of the
+        cached evaluator makes between a goto and its costs)."""
+        data = circ.data
+        ids = tuple(map(id, data))
+        if self._conv is not None and self._conv[0] != ids and len(self._conv[0]) == len(ids):
+            self._patch(circ, ids)
+        if self._conv is None or self._conv[0] != ids:
+            start = 1 if len(data) and data[0].operation.name == "set_matrix_product_state" else 0
+            full = device_ops_rows(circ, start, len(data))
+            from ..circuit import _memo_get
+
+            prev = _memo_get(circ)
+            if prev is None or prev[0] != start:
+                return device_ops_rows(circ, lo, hi)
+            size = OP_DTYPE.itemsize
+            off = np.cumsum([0] + [len(e[3]) // size for e in prev[1]])
+            self._conv = (ids, full, off, start, tuple(data))
+        _, full, off, start, _ = self._conv
+        lo, hi = max(lo, start), min(hi, len(data))
+        if hi <= lo:
+            return full[:0]
+        return full[off[lo - start]:off[hi - start]]
+
+    def _patch(self, circ, ids):
+        """The sweep replaced a few instructions since the last conversion (the visited gate):
+        re-convert just those into the cached rows when each keeps its row count, else drop the
+        cache (the next _rows converts the circuit again)."""
+        from ..circuit import _Range
+
+        old_ids, full, off, start, _ = self._conv
+        changed = [i for i, (a, b) in enumerate(zip(ids, old_ids)) if a != b]
+        if not changed or len(changed) > 4 or changed[0] < start:
+            self._conv = None
+            return
+        for i in changed:
+            rows = ops_array(device_ops(_Range(circ, i, i + 1)))
+            a, b = off[i - start], off[i - start + 1]
+            if len(rows) != b - a:
+                self._conv = None
+                return
+            full[a:b] = rows
+        self._conv = (ids, full, off, start, tuple(circ.data))
 
     def _grown(self, e):
         """A capacity overflow of an unbounded run: the backend grew its capacity, so the prefix
@@ -177,9 +228,9 @@ class MPSPrefixBatch(_SweepBase):
         # host wait instead of three
         if self.pos is None or index < self.pos:
             self.phi.copy_from(base)
-            self._advance(device_ops_rows(circ, start, index))
+            self._advance(self._rows(circ, start, index))
         elif index > self.pos:
-            self._advance(device_ops_rows(circ, self.pos, index))
+            self._advance(self._rows(circ, self.pos, index))
         self.pos = index
 
     def _advance(self, rows):
@@ -192,7 +243,7 @@ class MPSPrefixBatch(_SweepBase):
         # the suffix's rows from the circuit's memoised conversion (device_ops_rows), the candidates'
         # gates in one conversion, each list joined as bytes (a structured-array concatenate costs
         # ~16 us)
-        suffix = device_ops_rows(circ, index + 1, len(circ.data)).tobytes()
+        suffix = self._rows(circ, index + 1, len(circ.data)).tobytes()
         cand = ops_array([(m, (q,)) for m in mats]).tobytes()
         size = len(cand) // len(mats)
         states = self.backend.scratch_states(len(mats))
