@@ -485,11 +485,21 @@ def main():
     for _ in range(args.warmup):
         step()
     barrier()
+    # no Python garbage-collection pass inside the timed steps (measurement hygiene: a collection
+    # holds the host while the GPU waits for the next launches).  On a quiet box it changes nothing
+    # (profiles/r6_bench_gc_ab.json); two full lines run right after the whole GPU suite in the same
+    # call showed 40.8-45.5 ms steps against 38.7-39.0 ms, with no cause pinned.
+    import gc
+
+    gc.collect()
+    if os.environ.get("AQC_BENCH_GC", "0") != "1":  # (AQC_BENCH_GC=1: collections on, for A/B)
+        gc.disable()
     _lib.timing_reset()
     _lib.timing_enable(True)
     _lib.gram_stats()  # reset the Gram-path counters
     elapsed, (full, best, costs) = timed(step, args.steps)
     main_step_s = list(step_marks)
+    gc.enable()
     _lib.timing_enable(False)
     gram = _lib.gram_stats()
     if world > 1:
