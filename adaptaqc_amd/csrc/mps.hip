@@ -2632,13 +2632,14 @@ int check_flags_batch(aqc_mps_t* hs, int ns) {
   int* hout = (int*)((char*)fs.host + (size_t)ns * sizeof(int*));
   AQC_HIP_CHECK(hipMemcpyAsync(hout, dout, (size_t)ns * sizeof(int), hipMemcpyDeviceToHost, st));
   AQC_HIP_CHECK(hipStreamSynchronize(st));
+  int first = AQC_OK;  // every raised flag is read and reset; the first error is reported
   for (int s = 0; s < ns; ++s) {
     if (hout[s]) {
-      int rc = check_flags(hs[s]);
-      if (rc != AQC_OK) return rc;
+      const int rc = check_flags(hs[s]);
+      if (first == AQC_OK) first = rc;
     }
   }
-  return AQC_OK;
+  return first;
 }
 
 bool is_sorted_order(aqc_mps_t h) {
@@ -3219,8 +3220,10 @@ int aqc_mps_overlap_zero_batch(aqc_mps_t* hs, int ns, double* out) {
   if (ns == 0) return AQC_OK;
   int rc = aqc_mps_sort_batch(hs, ns);
   if (rc != AQC_OK) return rc;
-  static cplx* dres[64] = {nullptr};
-  static int dres_n[64] = {0};
+  // results (ns complex) and the states' gathered error flags (ns ints) in one device buffer: one
+  // read-back for both (the caller needs no aqc_mps_check_batch round trip after it)
+  static char* dres[64] = {nullptr};
+  static size_t dres_n[64] = {0};
   static void (*release)() = [] {
     for (int d = 0; d < 64; ++d)
       if (dres[d]) (void)hipFree(dres[d]), dres[d] = nullptr, dres_n[d] = 0;
@@ -3228,28 +3231,54 @@ int aqc_mps_overlap_zero_batch(aqc_mps_t* hs, int ns, double* out) {
   aqc::on_finalize(release);
   int dev = 0;
   hipGetDevice(&dev);
-  if (dres_n[dev] < ns) {
-    if (dres[dev]) hipFree(dres[dev]);
-    dres_n[dev] = std::max(ns, 2 * dres_n[dev]);
-    AQC_HIP_CHECK(hipMalloc(&dres[dev], (size_t)dres_n[dev] * sizeof(cplx)));
-  }
-  std::vector<MeasJob> jobs(ns);
-  for (int s = 0; s < ns; ++s) jobs[s] = make_meas(hs[s], dres[dev] + s);  // one contiguous result array
-  const MeasJob* dj = nullptr;
-  rc = upload_jobs(jobs, &dj);
-  if (rc != AQC_OK) return rc;
   hipStream_t st = aqc::mps_stream();
+  const size_t rbytes = (size_t)ns * sizeof(cplx), need = rbytes + (size_t)ns * sizeof(int);
+  if (dres_n[dev] < need) {
+    AQC_HIP_CHECK(hipStreamSynchronize(st));
+    if (dres[dev]) hipFree(dres[dev]);
+    dres_n[dev] = std::max(need, 2 * dres_n[dev]);
+    AQC_HIP_CHECK(hipMalloc(&dres[dev], dres_n[dev]));
+  }
+  cplx* dr = (cplx*)dres[dev];
+  int* dflags = (int*)(dres[dev] + rbytes);
+  // the jobs and flag pointers through a pinned staging set of the ring: no wait for the stream's
+  // earlier work (the chain that wrote the states) before these launches are queued
+  StagingLease lease(st);
+  if (lease.rc() != AQC_OK) return lease.rc();
+  const size_t jb = ((ns * sizeof(MeasJob) + 255) / 256) * 256, fpb = (size_t)ns * sizeof(int*);
+  rc = ensure_staging(lease.buf(), jb + fpb);
+  if (rc != AQC_OK) return rc;
+  char* hj = (char*)lease.buf().host;
+  char* dj = (char*)lease.buf().dev;
+  MeasJob* hjobs = (MeasJob*)hj;
+  int** hfp = (int**)(hj + jb);
+  for (int s = 0; s < ns; ++s) {
+    hjobs[s] = make_meas(hs[s], dr + s);  // one contiguous result array
+    hfp[s] = hs[s]->d.flags;
+  }
+  if (int e = aqc::upload_async(dj, hj, jb + fpb, st)) return e;
   double bytes = 0;
   for (int s = 0; s < ns; ++s) bytes += (double)hs[s]->d.n * hs[s]->d.cap * hs[s]->d.cap * 16.0;
   aqc::KernelTimer::begin(st, "mps_overlap0", bytes, bytes / 2.0);
   int vc = 1;
   for (int s = 0; s < ns; ++s) vc = std::max(vc, hs[s]->d.cap);
-  hipLaunchKernelGGL(k_overlap_zero, dim3(ns), dim3(kT), 2 * vc * sizeof(cplx), st, dj, vc);
+  hipLaunchKernelGGL(k_overlap_zero, dim3(ns), dim3(kT), 2 * vc * sizeof(cplx), st, (const MeasJob*)dj, vc);
   aqc::KernelTimer::end(st);
   AQC_CHECK_LAUNCH();
-  std::vector<cplx> v(ns);
-  AQC_HIP_CHECK(hipMemcpyAsync(v.data(), dres[dev], (size_t)ns * sizeof(cplx), hipMemcpyDeviceToHost, st));
+  hipLaunchKernelGGL(k_gather_flags, dim3((ns + 255) / 256), dim3(256), 0, st, (int* const*)(dj + jb), ns, dflags);
+  AQC_CHECK_LAUNCH();
+  std::vector<char> hv(need);
+  AQC_HIP_CHECK(hipMemcpyAsync(hv.data(), dres[dev], need, hipMemcpyDeviceToHost, st));
   AQC_HIP_CHECK(hipStreamSynchronize(st));
+  const cplx* v = (const cplx*)hv.data();
+  const int* hf = (const int*)(hv.data() + rbytes);
+  int first = AQC_OK;  // (every raised flag reset; the first error reported)
+  for (int s = 0; s < ns; ++s)
+    if (hf[s]) {
+      const int frc = check_flags(hs[s]);
+      if (first == AQC_OK) first = frc;
+    }
+  if (first != AQC_OK) return first;
   for (int s = 0; s < ns; ++s) {
     // mps_dot(psi, zero) = <psi|0..0> = conj(amplitude of |0..0>)
     out[2 * s] = v[s].x;
@@ -3464,11 +3493,13 @@ int aqc_mps_zero_hw1_batch(aqc_mps_t base, aqc_mps_t* hs, int ns, double* out_ov
     aqc::dev_free(d);
     {
       const int* hf = (const int*)((const char*)h.data() + rb);
+      int first = AQC_OK;  // (every raised flag reset; the first error reported)
       for (int s = 0; s <= ns; ++s)
         if (hf[s]) {
           const int frc = check_flags(s < ns ? hs[s] : base);
-          if (frc != AQC_OK) return frc;
+          if (first == AQC_OK) first = frc;
         }
+      if (first != AQC_OK) return first;
     }
     base->h0l = std::max(base->h0l, need_l);
     base->h0r = std::min(base->h0r, need_r);

@@ -139,7 +139,8 @@ int aqc_entanglement_measures(const double* rdms, int count, int method, double*
 /* move_all_qubits_to_sorted_ordering (done implicitly by every measurement below). */
 int aqc_mps_sort(aqc_mps_t h);
 int aqc_mps_sort_batch(aqc_mps_t* hs, int nstates);
-/* mps_dot(psi, zero_mps) = <psi|0...0> (aer_mps_backend.py:49-57). */
+/* mps_dot(psi, zero_mps) = <psi|0...0> (aer_mps_backend.py:49-57).  The states' error flags are
+   read with the result (AQC_ERR_STATE as aqc_mps_check_batch: work queued by the async applies). */
 int aqc_mps_overlap_zero(aqc_mps_t h, double* re, double* im);
 int aqc_mps_overlap_zero_batch(aqc_mps_t* hs, int nstates, double* out /* 2*nstates */);
 /* mps_dot(a, b) = <a|b>, conjugating a. */
