@@ -482,18 +482,20 @@ def main():
             el = float(t.item())
         return el, r
 
-    for _ in range(args.warmup):
-        step()
-    barrier()
     # no Python garbage-collection pass inside the timed steps (measurement hygiene: a collection
     # holds the host while the GPU waits for the next launches).  On a quiet box it changes nothing
     # (profiles/r6_bench_gc_ab.json); two full lines run right after the whole GPU suite in the same
-    # call showed 40.8-45.5 ms steps against 38.7-39.0 ms, with no cause pinned.
+    # call showed 40.8-45.5 ms steps against 38.7-39.0 ms, with no cause pinned.  The collection
+    # runs before the warm-up steps: between them and the timed ones it left the GPU idle long
+    # enough that the first timed step ran ~1 ms slow.
     import gc
 
     gc.collect()
     if os.environ.get("AQC_BENCH_GC", "0") != "1":  # (AQC_BENCH_GC=1: collections on, for A/B)
         gc.disable()
+    for _ in range(args.warmup):
+        step()
+    barrier()
     _lib.timing_reset()
     _lib.timing_enable(True)
     _lib.gram_stats()  # reset the Gram-path counters
