@@ -2229,6 +2229,26 @@ class StagingLease {
   Staging& buf() { return ss_->buf; }
   int rc() const { return rc_; }
 
+  // Sizes the leased set for `bytes`.  A set that must grow brings the whole ring to the new size
+  // at once (waiting for the other sets' last uses): grown one set at a time, a workload whose
+  // calls per step are not a multiple of the ring's length met a fresh (smaller) set in each of
+  // its first four steps, and each growth's hipFree drained the device mid-step.
+  int ensure(size_t bytes) {
+    Staging& mine = ss_->buf;
+    if (bytes <= mine.cap && bytes <= mine.hcap) return AQC_OK;
+    const size_t want = std::max({bytes, mine.cap * 2, mine.hcap * 2});
+    StagingSet* ring = g_stage_sets[device()];
+    for (int i = 0; i < kStagingRing; ++i) {
+      StagingSet& s = ring[i];
+      if (&s != ss_ && s.pending) {
+        AQC_HIP_CHECK(hipEventSynchronize(s.done));
+        s.pending = false;
+      }
+      if (int rc = ensure_staging(s.buf, want)) return rc;
+    }
+    return AQC_OK;
+  }
+
  private:
   static int device() {
     int dev = 0;
@@ -2361,7 +2381,7 @@ int run_chains(aqc_mps_t* hs, int ns, std::vector<std::vector<DevOp>>& lists, in
   StagingLease lease(st);
   if (lease.rc() != AQC_OK) return lease.rc();
   Staging& sg = lease.buf();
-  int rc = ensure_staging(sg, total);
+  int rc = lease.ensure(total);
   if (rc != AQC_OK) return rc;
   char* hb = (char*)sg.host;
   char* db = (char*)sg.dev;
@@ -2500,7 +2520,7 @@ int run_waves(aqc_mps_t* hs, int ns, std::vector<std::vector<DevOp>>& lists) {
   StagingLease lease(st);
   if (lease.rc() != AQC_OK) return lease.rc();
   Staging& sg = lease.buf();
-  int rc = ensure_staging(sg, tb + ob + 256);
+  int rc = lease.ensure(tb + ob + 256);
   if (rc != AQC_OK) return rc;
   std::memcpy(sg.host, two.data(), tb);
   std::memcpy((char*)sg.host + tb, one.data(), ob);
@@ -3078,7 +3098,7 @@ int aqc_mps_copy_batch(aqc_mps_t* dst, const aqc_mps_t* src, int ns) {
   if (lease.rc() != AQC_OK) return lease.rc();
   Staging& sg = lease.buf();
   const size_t bytes = jobs.size() * sizeof(CopyJob);
-  int rc = ensure_staging(sg, bytes);
+  int rc = lease.ensure(bytes);
   if (rc != AQC_OK) return rc;
   std::memcpy(sg.host, jobs.data(), bytes);
   if (int e = aqc::upload_async(sg.dev, sg.host, bytes, st)) return e;
@@ -3246,7 +3266,7 @@ int aqc_mps_overlap_zero_batch(aqc_mps_t* hs, int ns, double* out) {
   StagingLease lease(st);
   if (lease.rc() != AQC_OK) return lease.rc();
   const size_t jb = ((ns * sizeof(MeasJob) + 255) / 256) * 256, fpb = (size_t)ns * sizeof(int*);
-  rc = ensure_staging(lease.buf(), jb + fpb);
+  rc = lease.ensure(jb + fpb);
   if (rc != AQC_OK) return rc;
   char* hj = (char*)lease.buf().host;
   char* dj = (char*)lease.buf().dev;
@@ -3452,7 +3472,7 @@ int aqc_mps_zero_hw1_batch(aqc_mps_t base, aqc_mps_t* hs, int ns, double* out_ov
       return lease.rc();
     }
     const size_t fpb = ((size_t)ns + 1) * sizeof(int*);
-    rc = ensure_staging(lease.buf(), jb + wb + cb + fpb);
+    rc = lease.ensure(jb + wb + cb + fpb);
     if (rc != AQC_OK) {
       aqc::dev_free(d);
       return rc;
