@@ -1,0 +1,10 @@
+#!/bin/bash
+# round 6: k_gb_keep stages the eigenvalues through the LDS -- gram_big tests, the 11-layer
+# compile (costs must be unchanged), and its kernel stats
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out
+timeout -k 10 600 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread -p no:cacheprovider \
+  tests/test_gpu_gram_big.py tests/test_gpu_bigchi.py > gpurun_out/r6c53_tests.log 2>&1 || exit $?
+timeout -k 10 600 python3 -u tools/layer_profile.py --target graded --cpu-pairs 0 > gpurun_out/r6c53_layers.json 2> gpurun_out/r6c53_layers.err || exit $?
+timeout -k 10 500 rocprofv3 --kernel-trace --stats -d gpurun_out/r6c53_kt -o run -- python3 tools/layer_profile.py --target graded --cpu-pairs 0 > gpurun_out/r6c53_layers_kt.json 2> gpurun_out/r6c53_layers_kt.err || exit $?
